@@ -1,0 +1,30 @@
+# libpnr.so: the MI355X (gfx950) Point-NeRF hot path behind include/pnr.h.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+SRC_DIR := pointnerf_amd/csrc
+SRCS := $(wildcard $(SRC_DIR)/*.hip)
+OBJS := $(patsubst $(SRC_DIR)/%.hip,build/%.o,$(SRCS))
+LIB := pointnerf_amd/libpnr.so
+HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -Wno-unused-result \
+            -munsafe-fp-atomics -Iinclude
+
+all: $(LIB) oracle
+
+build/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pnr_common.h include/pnr.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# The query kernels must round exactly like the reference's fp32 ops: no FMA contraction.
+build/query.o build/grid.o: HIPFLAGS += -ffp-contract=off
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

@@ -1,0 +1,16 @@
+"""pointnerf_amd -- MI355X-native Point-NeRF hot path.
+
+The world-coordinate neural-point query, K-neighbour gather + aggregation MLP
+and ray-march composite of yjcaimeow/pointnerf, as hand-written HIP kernels for
+gfx950 behind the C ABI in include/pnr.h (libpnr.so), with Python drop-ins for
+the reference's querier / PointAggregator / ray_march / NeuralPointsRayMarching
+seams.  See DESIGN.md.
+"""
+from . import _lib  # noqa: F401  (loads torch before libpnr.so)
+from .aggregator import PointAggregator, frag_pack, frag_unpack  # noqa: F401
+from .options import lego_opt  # noqa: F401
+from .querier import lighting_fast_querier, ray_mid_t, hyperparameters_from_bbox  # noqa: F401
+from .ray_march import ray_march, radiance_render, alpha_blend, no_tone_map  # noqa: F401
+from .renderer import NeuralPoints, NeuralPointsRayMarching  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,150 @@
+"""ctypes binding of libpnr.so (include/pnr.h).
+
+The library is the only compute path of this package: if it is missing, or no
+GPU is visible, every op raises -- there is no CPU fallback.  ``torch`` is
+imported first so that libpnr.so binds to the HIP runtime torch already loaded
+(both have soname libamdhip64.so.7): one runtime, shared streams and pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before libpnr.so, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
+
+c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
+c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
+ABI_VERSION = 1
+
+
+class PnrError(RuntimeError):
+    pass
+
+
+class GridParams(ctypes.Structure):
+    _fields_ = [("shift", c_float * 3), ("vsize", c_float * 3), ("dims", c_int32 * 3),
+                ("query_size", c_int32 * 3), ("max_o", c_int32), ("P", c_int32),
+                ("slot0_drop", c_int32)]
+
+
+class GridStats(ctypes.Structure):
+    _fields_ = [("n_points_in_grid", c_int64), ("n_voxels", c_int64), ("n_voxels_kept", c_int64),
+                ("n_points_dropped", c_int64), ("max_points_per_voxel", c_int32),
+                ("dims", c_int32 * 3)]
+
+
+class Rays(ctypes.Structure):
+    _fields_ = [("campos_dev", c_void_p), ("camrot_dev", c_void_p), ("raydir_dev", c_void_p),
+                ("tvals_dev", c_void_p), ("R", c_int64), ("D", c_int32), ("tvals_per_ray", c_int32)]
+
+
+class QueryParams(ctypes.Structure):
+    _fields_ = [("SR", c_int32), ("K", c_int32), ("kernel_size", c_int32 * 3),
+                ("radius_limit2", c_float)]
+
+
+class QueryBufs(ctypes.Structure):
+    _fields_ = [("n_filled", c_void_p), ("slot_d", c_void_p), ("ray_off", c_void_p),
+                ("fill_rs", c_void_p), ("pidx", c_void_p), ("valid_off", c_void_p),
+                ("valid_list", c_void_p), ("vflag", c_void_p), ("ray_vcnt", c_void_p),
+                ("ray_row", c_void_p), ("sample_w", c_void_p), ("sample_p", c_void_p),
+                ("counts", c_void_p), ("scratch", c_void_p), ("scratch_bytes", c_size_t)]
+
+
+class Mlp(ctypes.Structure):
+    _fields_ = [("w1f", c_void_p), ("b1", c_void_p), ("w2f", c_void_p), ("b2", c_void_p),
+                ("w3f", c_void_p), ("b3", c_void_p), ("w4f", c_void_p), ("b4", c_void_p),
+                ("wa", c_void_p), ("ba", c_void_p), ("wc1t", c_void_p), ("bc1", c_void_p),
+                ("wc2t", c_void_p), ("bc2", c_void_p), ("wc3t", c_void_p), ("bc3", c_void_p),
+                ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32)]
+
+
+class Points(ctypes.Structure):
+    _fields_ = [("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
+                ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p)]
+
+
+class Samples(ctypes.Structure):
+    _fields_ = [("samp_list", c_void_p), ("n_dev", c_void_p), ("n_max", c_int64), ("pidx", c_void_p),
+                ("sample_w", c_void_p), ("sample_p", c_void_p), ("dirs", c_void_p),
+                ("dir_map", c_void_p), ("dir_div", c_int32), ("K", c_int32)]
+
+
+class CompositeParams(ctypes.Structure):
+    _fields_ = [("vsize_z", c_float), ("raydist_mode_unit", c_int32), ("C", c_int32),
+                ("bg_color", c_void_p)]
+
+
+P = ctypes.POINTER
+# name -> (restype, argtypes); exactly the functions include/pnr.h declares.
+SIGNATURES = {
+    "pnr_abi_version": (c_int, []),
+    "pnr_last_error": (ctypes.c_char_p, []),
+    "pnr_create": (c_int, [c_int, P(c_void_p)]),
+    "pnr_destroy": (c_int, [c_void_p]),
+    "pnr_points_bbox": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "pnr_grid_build": (c_int, [c_void_p, c_void_p, c_int64, P(GridParams), c_void_p]),
+    "pnr_grid_stats_get": (c_int, [c_void_p, P(GridStats)]),
+    "pnr_grid_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_query_scratch_bytes": (c_int, [c_int64, c_int32, P(c_size_t)]),
+    "pnr_query": (c_int, [c_void_p, P(Rays), P(QueryParams), P(QueryBufs), c_void_p]),
+    "pnr_query_compact": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), c_int64, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_aggregate_fwd": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
+    "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p]),
+    "pnr_composite_fwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams),
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_ray_march_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_scan_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
+    "pnr_exclusive_scan_i32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_size_t, c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libpnr.so once; raise loudly when it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PnrError(f"libpnr.so not found at {LIB_PATH}: build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` or `make`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.pnr_abi_version() != ABI_VERSION:
+            raise PnrError(f"libpnr ABI {L.pnr_abi_version()} != expected {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != PNR_OK:
+        msg = lib().pnr_last_error().decode(errors="replace")
+        raise PnrError(f"{what} failed (status {rc}): {msg}")
+
+
+def require_gpu(t: torch.Tensor | None = None):
+    if not torch.cuda.is_available():
+        raise PnrError("pointnerf_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                       "there is no CPU fallback")
+    if t is not None and not t.is_cuda:
+        raise PnrError("pointnerf_amd ops take device tensors; got a CPU tensor")
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)

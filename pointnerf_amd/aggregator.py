@@ -1,0 +1,187 @@
+"""PointAggregator drop-in on libpnr.so.
+
+Same module tree and ``state_dict`` names as
+models/aggregators/point_aggregators.py:12-348 for the lego configuration
+(viewmlp, agg_intrp_order 2, linear kernel, agg_dist_pers 20): ``block1.{0,2}``,
+``block3.{0,2}``, ``alpha_branch.0``, ``color_branch.{0,2,4}``, so reference
+checkpoints load with ``load_state_dict(strict=False)`` as in
+mvs_points_volumetric_model.py:320-335.  ``forward`` keeps the 13-argument
+signature of point_aggregators.py:729 and runs the fused HIP kernel; the
+renderer uses ``packed()`` + ``pnr_aggregate_fwd`` directly on query buffers.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+
+SUPPORTED = dict(which_agg_model="viewmlp", agg_intrp_order=2, agg_distance_kernel="linear",
+                 agg_dist_pers=20, point_features_dim=32, num_feat_freqs=3, dist_xyz_freq=5,
+                 num_viewdir_freqs=4, shading_feature_num=256, shading_feature_mlp_layer1=2,
+                 shading_feature_mlp_layer2=0, shading_feature_mlp_layer3=2,
+                 shading_alpha_mlp_layer=1, shading_color_mlp_layer=4,
+                 shading_color_channel_num=128, apply_pnt_mask=1, agg_weight_norm=1)
+
+
+def check_supported(opt):
+    bad = {k: (getattr(opt, k, v), v) for k, v in SUPPORTED.items() if getattr(opt, k, v) != v}
+    if getattr(opt, "dist_xyz_deno", 0.0) != 0.0:
+        bad["dist_xyz_deno"] = (opt.dist_xyz_deno, 0.0)
+    for k in ("agg_feat_xyz_mode", "agg_alpha_xyz_mode", "agg_color_xyz_mode"):
+        if getattr(opt, k, "None") != "None":
+            bad[k] = (getattr(opt, k), "None")
+    if bad:
+        raise L.PnrError(f"aggregator configuration not implemented by libpnr: {bad}")
+
+
+def _xavier_(lin: nn.Linear, gain: float):
+    # models/helpers/networks.py:71-122: uniform(+-gain*sqrt(2/(in+out))*sqrt(3)), bias 0
+    std = gain * math.sqrt(2.0 / (lin.in_features + lin.out_features))
+    with torch.no_grad():
+        lin.weight.uniform_(-std * math.sqrt(3.0), std * math.sqrt(3.0))
+        lin.bias.zero_()
+
+
+def _init_seq(seq: nn.Sequential):
+    # networks.py:163-172 init_seq
+    mods = list(seq)
+    for a, b in zip(mods[:-1], mods[1:]):
+        if isinstance(a, nn.Linear):
+            if isinstance(b, nn.LeakyReLU):
+                _xavier_(a, nn.init.calculate_gain("leaky_relu", b.negative_slope))
+            elif isinstance(b, nn.ReLU):
+                _xavier_(a, nn.init.calculate_gain("relu"))
+            else:
+                _xavier_(a, 1.0)
+    if isinstance(mods[-1], nn.Linear):
+        _xavier_(mods[-1], 1.0)
+
+
+def frag_pack(W: torch.Tensor, nsteps: int) -> torch.Tensor:
+    """[256, Kin] nn.Linear weight -> MFMA A-operand fragments
+    F[t][T][lane] = W[32T + (lane & 31)][2t + (lane >> 5)] (zero padded)."""
+    out_f, kin = W.shape
+    assert out_f == 256 and kin <= 2 * nsteps
+    Wp = torch.zeros((256, 2 * nsteps), dtype=torch.float32, device=W.device)
+    Wp[:, :kin] = W.float()
+    return Wp.view(8, 32, nsteps, 2).permute(2, 0, 3, 1).contiguous().view(-1)
+
+
+def frag_unpack(F: torch.Tensor, nsteps: int, kin: int) -> torch.Tensor:
+    return F.view(nsteps, 8, 2, 32).permute(1, 3, 0, 2).reshape(256, 2 * nsteps)[:, :kin]
+
+
+class PointAggregator(nn.Module):
+    """point_aggregators.PointAggregator (viewmlp, order 2) on libpnr.so."""
+
+    def __init__(self, opt):
+        super().__init__()
+        check_supported(opt)
+        self.opt = opt
+        act = opt.act_type
+        if act == "LeakyReLU":
+            mk, self.neg_slope = (lambda: nn.LeakyReLU(inplace=True)), 0.01
+        elif act == "ReLU":
+            mk, self.neg_slope = (lambda: nn.ReLU(inplace=True)), 0.0
+        else:
+            raise L.PnrError(f"act_type {act} not implemented by libpnr")
+        self.act_super = int(getattr(opt, "act_super", 1))
+        # shapes of point_aggregators.py:276-348 for the lego flag set
+        self.block1 = nn.Sequential(nn.Linear(284, 256), mk(), nn.Linear(256, 256), mk())
+        self.block3 = nn.Sequential(nn.Linear(263, 256), mk(), nn.Linear(256, 256), mk())
+        self.alpha_branch = nn.Sequential(nn.Linear(256, 1))
+        self.color_branch = nn.Sequential(nn.Linear(280, 128), mk(), nn.Linear(128, 128), mk(),
+                                          nn.Linear(128, 128), mk())
+        for s in (self.block1, self.block3, self.alpha_branch, self.color_branch):
+            _init_seq(s)
+        self._packed = None
+        self._packed_key = None
+        self.register_buffer("rw2c", torch.eye(3), persistent=False)
+
+    # ---------------------------------------------------------------- weights
+    def packed(self) -> tuple[L.Mlp, dict]:
+        """Fragment-packed weights on the module's device, rebuilt only when a
+        parameter changed (version counters)."""
+        ps = list(self.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in ps) + ((self.rw2c.data_ptr(), self.rw2c._version),)
+        if self._packed is not None and key == self._packed_key:
+            return self._packed
+        with torch.no_grad():
+            b1, b3 = self.block1, self.block3
+            t = dict(
+                w1f=frag_pack(b1[0].weight, 142), b1=b1[0].bias.float().contiguous(),
+                w2f=frag_pack(b1[2].weight, 128), b2=b1[2].bias.float().contiguous(),
+                w3f=frag_pack(b3[0].weight, 132), b3=b3[0].bias.float().contiguous(),
+                w4f=frag_pack(b3[2].weight, 128), b4=b3[2].bias.float().contiguous(),
+                wa=self.alpha_branch[0].weight.float().reshape(-1).contiguous(),
+                ba=self.alpha_branch[0].bias.float().contiguous(),
+                wc1t=self.color_branch[0].weight.float().t().contiguous(),
+                bc1=self.color_branch[0].bias.float().contiguous(),
+                wc2t=self.color_branch[2].weight.float().t().contiguous(),
+                bc2=self.color_branch[2].bias.float().contiguous(),
+                wc3t=self.color_branch[4].weight.float().t().contiguous(),
+                bc3=self.color_branch[4].bias.float().contiguous(),
+                rw2c=self.rw2c.float().contiguous())
+        m = L.Mlp()
+        for k, v in t.items():
+            setattr(m, k, v.data_ptr())
+        m.neg_slope = float(self.neg_slope)
+        m.act_super = self.act_super
+        self._packed, self._packed_key = (m, t), key
+        return self._packed
+
+    def set_rw2c(self, rw2c: torch.Tensor | None):
+        """Uniform Rw2c of the point cloud (neural_points.py:289; eye by default)."""
+        with torch.no_grad():
+            self.rw2c.copy_(torch.eye(3) if rw2c is None else rw2c.reshape(3, 3))
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, sampled_color, sampled_Rw2c, sampled_dir, sampled_conf, sampled_embedding,
+                sampled_xyz_pers, sampled_xyz, sample_pnt_mask, sample_loc, sample_loc_w,
+                sample_ray_dirs, vsize, grid_vox_sz):
+        """point_aggregators.py:729-816 -> (features [B,R,SR,C+1], ray_valid
+        [B,R,SR], weight, conf_coefficient)."""
+        L.require_gpu(sample_loc_w)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) and self.training:
+            raise L.PnrError("libpnr PointAggregator backward is not implemented yet (forward/eval only)")
+        if sampled_Rw2c is not None and sampled_Rw2c.dim() != 2:
+            raise L.PnrError("per-point Rw2c is not implemented by libpnr (uniform Rw2c only)")
+        if sampled_Rw2c is not None:
+            self.set_rw2c(sampled_Rw2c.to(self.rw2c.device))
+        B, R, SR, K = sample_pnt_mask.shape
+        rows = B * R * SR
+        dev = sample_loc_w.device
+        C = 128
+        ray_valid = torch.any(sample_pnt_mask, dim=-1)
+        out = torch.zeros((rows, C + 1), dtype=torch.float32, device=dev)
+        weight = torch.empty((rows, K), dtype=torch.float32, device=dev)
+        conf = torch.empty((rows, K), dtype=torch.float32, device=dev)
+        if rows == 0:
+            return out.view(B, R, SR, C + 1), ray_valid, weight.view(B, R, SR, K), conf.view(B, R, SR, K)
+
+        def flat(t, c):
+            return None if t is None else t.reshape(-1, c).float().contiguous()
+
+        keep = dict(xyz=flat(sampled_xyz, 3), pers=flat(sampled_xyz_pers, 3),
+                    emb=flat(sampled_embedding, 32), color=flat(sampled_color, 3),
+                    dir=flat(sampled_dir, 3), conf=flat(sampled_conf, 1),
+                    sw=flat(sample_loc_w, 3), sp=flat(sample_loc, 3), sd=flat(sample_ray_dirs, 3),
+                    mask=sample_pnt_mask.reshape(-1).contiguous().view(torch.uint8))
+        pts = L.Points(keep["xyz"].data_ptr(), keep["pers"].data_ptr(), keep["emb"].data_ptr(),
+                       L.ptr(keep["color"]), L.ptr(keep["dir"]), L.ptr(keep["conf"]), None, None)
+        s = L.Samples(None, None, rows, None, keep["sw"].data_ptr(), keep["sp"].data_ptr(),
+                      keep["sd"].data_ptr(), None, 1, K)
+        mlp, _ = self.packed()
+        L.check(L.lib().pnr_aggregate_fwd_masked(L.ctypes.byref(pts), L.ctypes.byref(s),
+                                                 L.ctypes.byref(mlp), L.ptr(keep["mask"]), L.ptr(out),
+                                                 L.ptr(weight), L.ptr(conf), L.stream_ptr(dev)),
+                "pnr_aggregate_fwd_masked")
+        weight, conf = weight.view(B, R, SR, K), conf.view(B, R, SR, K)
+        o = self.opt
+        if (getattr(o, "sparse_loss_weight", 0) <= 0 and "conf_coefficient" not in getattr(o, "zero_one_loss_items", [])
+                and getattr(o, "prob", 0) == 0):
+            weight, conf = None, None
+        return out.view(B, R, SR, C + 1), ray_valid, weight, conf

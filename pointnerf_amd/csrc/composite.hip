@@ -1,0 +1,289 @@
+// Ray-march alpha composite.
+//
+// k_composite fuses, for every ray of the batch:
+//   ray_dist = cummax(sample_loc z) differences, unit-voxel clamp, x ray_valid
+//                                   neural_points_volumetric_model.py:293-301
+//   ray_march + radiance_render + alpha_blend + tone_map 'off'
+//                                   diff_ray_marching.py:509-555, diff_render_func.py:36-63
+//   fill_invalid (background rays)  neural_points_volumetric_model.py:354-389
+// One wave per ray: lane s owns shading slots s and s+64 for the per-slot
+// scalars (z, sigma, opacity) and the cummax / exclusive cumprod run as
+// wave scans; then lane c owns colour channels c and c+64 and the wave walks
+// the valid slots once, reading each sample's 129-float feature row with two
+// coalesced 256-B loads.  Empty and invalid slots cost no feature traffic.
+#include "pnr_common.h"
+
+namespace pnr {
+
+constexpr int kCBlock = 256;
+
+__device__ __forceinline__ float wave_max_scan_incl(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    float t = __shfl_up(v, o);
+    if (lane >= o) v = fmaxf(v, t);
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_prod_scan_incl(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    float t = __shfl_up(v, o);
+    if (lane >= o) v = v * t;
+  }
+  return v;
+}
+
+// Per-slot scalars -> opacity, exclusive transmittance, blend weight, bg T.
+// Inputs per lane for slots s0 = lane, s1 = lane + 64 (SR <= 128).
+struct SlotOut {
+  float op0, op1, T0, T1, bgT;
+};
+
+__device__ __forceinline__ SlotOut march_slots(float sig0, float dist0, float sig1, float dist1, int SR) {
+  const int lane = threadIdx.x & 63;
+  // sigma = features[...,0] * ray_valid; opacity = 1 - exp(-sigma * dist)
+  const float op0 = 1.f - expf(-sig0 * dist0);
+  const float op1 = 1.f - expf(-sig1 * dist1);
+  // cumprod(1 - opacity + 1e-10), made exclusive (diff_ray_marching.py:534-539)
+  float f0 = (lane < SR) ? (1.f - op0 + 1e-10f) : 1.f;
+  float f1 = (lane + 64 < SR) ? (1.f - op1 + 1e-10f) : 1.f;
+  float i0 = wave_prod_scan_incl(f0);
+  float tot0 = __shfl(i0, 63);
+  float i1 = wave_prod_scan_incl(f1) * tot0;
+  float e0 = __shfl_up(i0, 1);
+  float e1 = __shfl_up(i1, 1);
+  if (lane == 0) {
+    e0 = 1.f;
+    e1 = tot0;
+  }
+  SlotOut o;
+  o.op0 = op0;
+  o.op1 = op1;
+  o.T0 = e0;
+  o.T1 = e1;
+  // background transmission = inclusive product at slot SR-1
+  const int last = SR - 1;
+  o.bgT = last < 64 ? __shfl(i0, last) : __shfl(i1, last - 64);
+  return o;
+}
+
+struct CompArgs {
+  const float* campos;
+  const float* camrot;
+  int64_t R;
+  int SR;
+  const int32_t* n_filled;
+  const int32_t* ray_off;
+  const int32_t* ray_vcnt;
+  const int32_t* vflag;
+  const int32_t* valid_off;
+  const float* sample_p;
+  const float* feat;
+  float vsize_z;
+  int unit;
+  int C;
+  const float* bg;
+  float* ray_color;
+  float* opacity;
+  float* is_bg;
+  int8_t* ray_mask;
+};
+
+__global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int SR = a.SR, C = a.C, CF = C + 1;
+  // depth of the world origin: the z of every unfilled slot (sample_loc_w = 0)
+  float zo;
+  {
+    const float c[3] = {a.campos[0], a.campos[1], a.campos[2]};
+    float Rm[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rm[i] = a.camrot[i];
+    const float zero[3] = {0.f, 0.f, 0.f};
+    float pc[3];
+    world_to_cam(zero, c, Rm, pc);
+    zo = pc[2];
+  }
+  const float vz = a.vsize_z, two_vz = 2.f * a.vsize_z;
+  for (int64_t r = wave0; r < a.R; r += nwaves) {
+    const bool mask = a.ray_vcnt[r] > 0;
+    if (!mask) {  // fill_invalid: background ray
+      for (int c = lane; c < C; c += 64) a.ray_color[r * C + c] = a.bg ? a.bg[c] : 0.f;
+      for (int s = lane; s < SR; s += 64) a.opacity[r * SR + s] = 0.f;
+      if (lane == 0) {
+        a.is_bg[r] = 1.f;
+        a.ray_mask[r] = 0;
+      }
+      continue;
+    }
+    const int n = a.n_filled[r], off = a.ray_off[r];
+    float z[2], sig[2];
+    int vrow[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      const bool filled = s < n;
+      const int64_t i = off + s;
+      z[q] = filled ? a.sample_p[i * 3 + 2] : (s < SR ? zo : -INFINITY);
+      const bool val = filled && a.vflag[i];
+      vrow[q] = val ? a.valid_off[i] : -1;
+      sig[q] = val ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
+    }
+    // cummax over slots (neural_points_volumetric_model.py:293)
+    float cm0 = wave_max_scan_incl(z[0]);
+    float cm1 = fmaxf(wave_max_scan_incl(z[1]), __shfl(cm0, 63));
+    // next slot's cummax
+    float nx0 = __shfl_down(cm0, 1), nx1 = __shfl_down(cm1, 1);
+    const float cm1_first = __shfl(cm1, 0);
+    if (lane == 63) nx0 = cm1_first;
+    float dist[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      const float cm = q ? cm1 : cm0, nx = q ? nx1 : nx0;
+      float d = (s < SR - 1) ? (nx - cm) : vz;
+      const bool msk = (d < 1e-8f) || (a.unit && d > two_vz);
+      d = msk ? vz : d;
+      dist[q] = vrow[q] >= 0 ? d : 0.f;  // ray_dist *= ray_valid
+    }
+    const SlotOut so = march_slots(sig[0], dist[0], sig[1], dist[1], SR);
+    if (lane < SR) a.opacity[r * SR + lane] = so.op0;
+    if (lane + 64 < SR) a.opacity[r * SR + lane + 64] = so.op1;
+    const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
+    // colour = sum_s w_s * features[s, 1:] + bg * T_bg  (lane = channel)
+    float col0 = 0.f, col1 = 0.f;
+    const int smax = n < SR ? n : SR;
+    for (int s = 0; s < smax; ++s) {
+      const int q = s >> 6, src = s & 63;
+      const int vr = __shfl(q ? vrow[1] : vrow[0], src);
+      if (vr < 0) continue;
+      const float w = __shfl(q ? w1 : w0, src);
+      const float* f = a.feat + (int64_t)vr * CF + 1;
+      if (lane < C) col0 += w * f[lane];
+      if (lane + 64 < C) col1 += w * f[lane + 64];
+    }
+    for (int c = lane, q = 0; c < C; c += 64, ++q) {
+      float v = q == 0 ? col0 : (q == 1 ? col1 : 0.f);
+      if (a.bg) v += a.bg[c] * so.bgT;
+      a.ray_color[r * C + c] = v;
+    }
+    if (lane == 0) {
+      a.is_bg[r] = so.bgT;
+      a.ray_mask[r] = 1;
+    }
+  }
+}
+
+// ray_march on dense [NR, SR, C+1] features (mirror path).
+__global__ void __launch_bounds__(kCBlock) k_ray_march_dense(const float* __restrict__ ray_dist,
+                                                             const uint8_t* __restrict__ ray_valid,
+                                                             const float* __restrict__ feat,
+                                                             const float* __restrict__ bg, int64_t NR,
+                                                             int SR, int C, float* ray_color,
+                                                             float* opacity, float* acc_T,
+                                                             float* blend_w, float* bg_T) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int CF = C + 1;
+  for (int64_t r = wave0; r < NR; r += nwaves) {
+    float sig[2], dist[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      const bool in = s < SR;
+      const int64_t e = r * SR + s;
+      const float v = (in && ray_valid[e]) ? 1.f : 0.f;
+      sig[q] = in ? feat[e * CF] * v : 0.f;
+      dist[q] = in ? ray_dist[e] : 0.f;
+    }
+    const SlotOut so = march_slots(sig[0], dist[0], sig[1], dist[1], SR);
+    const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
+    if (lane < SR) {
+      opacity[r * SR + lane] = so.op0;
+      acc_T[r * SR + lane] = so.T0;
+      blend_w[r * SR + lane] = w0;
+    }
+    if (lane + 64 < SR) {
+      opacity[r * SR + lane + 64] = so.op1;
+      acc_T[r * SR + lane + 64] = so.T1;
+      blend_w[r * SR + lane + 64] = w1;
+    }
+    for (int c0 = 0; c0 < C; c0 += 64) {
+      const int c = c0 + lane;
+      float v = 0.f;
+      for (int s = 0; s < SR; ++s) {
+        const int q = s >> 6, src = s & 63;
+        const float w = __shfl(q ? w1 : w0, src);
+        if (c < C) v += w * feat[(r * SR + s) * CF + 1 + c];
+      }
+      if (c < C) {
+        if (bg) v += bg[c] * so.bgT;
+        ray_color[r * C + c] = v;
+      }
+    }
+    if (lane == 0) bg_T[r] = so.bgT;
+  }
+}
+
+}  // namespace pnr
+
+using namespace pnr;
+
+extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q,
+                                 const pnr_query_bufs* b, const pnr_composite_params* c,
+                                 const float* feat, float* ray_color, float* opacity, float* is_bg,
+                                 int8_t* ray_mask, void* stream) {
+  PNR_CHECK_ARG(rays && q && b && c && ray_color && opacity && is_bg && ray_mask,
+                "composite: null pointer");
+  PNR_CHECK_ARG(rays->campos_dev && rays->camrot_dev, "composite: camera required");
+  PNR_CHECK_ARG(q->SR >= 1 && q->SR <= 128, "composite: SR=%d unsupported (1..128)", q->SR);
+  PNR_CHECK_ARG(c->C >= 1 && c->C <= 128, "composite: C=%d unsupported (1..128)", c->C);
+  if (rays->R == 0) return PNR_OK;
+  CompArgs a;
+  a.campos = rays->campos_dev;
+  a.camrot = rays->camrot_dev;
+  a.R = rays->R;
+  a.SR = q->SR;
+  a.n_filled = b->n_filled;
+  a.ray_off = b->ray_off;
+  a.ray_vcnt = b->ray_vcnt;
+  a.vflag = b->vflag;
+  a.valid_off = b->valid_off;
+  a.sample_p = b->sample_p;
+  a.feat = feat;
+  a.vsize_z = c->vsize_z;
+  a.unit = c->raydist_mode_unit;
+  a.C = c->C;
+  a.bg = c->bg_color;
+  a.ray_color = ray_color;
+  a.opacity = opacity;
+  a.is_bg = is_bg;
+  a.ray_mask = ray_mask;
+  const unsigned grid = grid_for(rays->R * 64, kCBlock, 256 * 16);
+  hipLaunchKernelGGL(k_composite, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_ray_march_fwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
+                                 const float* bg, int64_t NR, int32_t SR, int32_t C, float* ray_color,
+                                 float* opacity, float* acc_T, float* blend_w, float* bg_T,
+                                 void* stream) {
+  PNR_CHECK_ARG(ray_dist && ray_valid && feat && ray_color && opacity && acc_T && blend_w && bg_T,
+                "ray_march: null pointer");
+  PNR_CHECK_ARG(SR >= 1 && SR <= 128, "ray_march: SR=%d unsupported (1..128)", SR);
+  PNR_CHECK_ARG(C >= 1, "ray_march: C must be >= 1");
+  if (NR == 0) return PNR_OK;
+  const unsigned grid = grid_for(NR * 64, kCBlock, 256 * 16);
+  hipLaunchKernelGGL(k_ray_march_dense, dim3(grid), dim3(kCBlock), 0, as_stream(stream), ray_dist,
+                     ray_valid, feat, bg, NR, SR, C, ray_color, opacity, acc_T, blend_w, bg_T);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}

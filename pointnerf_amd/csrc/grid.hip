@@ -1,0 +1,374 @@
+// Persistent sparse voxel grid of the neural points.
+//
+// Replaces build_occ_vox (query_point_indices_worldcoords.py:546-611) and its
+// three atomics-ordered kernels claim_occ / map_coor2occ / fill_occ2pnts
+// (qpiw.py:243-387).  The reference rebuilds this for every 2304-ray chunk and
+// its slot order depends on atomic arrival; here it is built once per point
+// cloud version, deterministically, in the serial order of the reference
+// kernels (slot = rank of the first point index that lands in the voxel,
+// points inside a voxel in ascending index order), which is what the serial
+// execution of claim_occ/fill_occ2pnts produces when nothing overflows.
+//
+// HBM layout (MI355X, 288 GB): one dense int32 cell->slot grid (lego 162x290x189
+// = 35.5 MB), one dilated-occupancy BITMAP (1 bit per cell: 1.1 MB, stays in
+// every XCD's L2 for the ray march), and a slot-major float4 table
+// {x, y, z, point id} of P entries per slot so the KNN loop reads one 16-B
+// record per candidate instead of an index plus a 12-B xyz gather.
+#include "pnr_common.h"
+
+namespace pnr {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------- bbox
+__device__ __forceinline__ unsigned f2ord(float f) {
+  unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ void k_bbox_init(unsigned* acc) {
+  if (threadIdx.x < 3) acc[threadIdx.x] = 0xffffffffu;
+  else if (threadIdx.x < 6) acc[threadIdx.x] = 0u;
+}
+
+__global__ void __launch_bounds__(kBlock) k_bbox(const float* __restrict__ xyz, int64_t n, unsigned* acc) {
+  unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      unsigned o = f2ord(xyz[i * 3 + c]);
+      mn[c] = min(mn[c], o);
+      mx[c] = max(mx[c], o);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[c] = min(mn[c], (unsigned)__shfl_xor((int)mn[c], o));
+      mx[c] = max(mx[c], (unsigned)__shfl_xor((int)mx[c], o));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      atomicMin(acc + c, mn[c]);
+      atomicMax(acc + 3 + c, mx[c]);
+    }
+  }
+}
+
+__global__ void k_bbox_fin(unsigned* acc) {
+  if (threadIdx.x < 6) {
+    float f = ord2f(acc[threadIdx.x]);
+    reinterpret_cast<float*>(acc)[threadIdx.x] = f;
+  }
+}
+
+// ---------------------------------------------------------------- build
+struct GridDev {
+  float shift[3], vs[3];
+  int dims[3], qs[3];
+  int max_o, P, slot0_drop;
+};
+
+__device__ __forceinline__ int cell_of(const float* p, const GridDev& g, int c[3]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) c[a] = vox_coord(p[a], g.shift[a], g.vs[a]);
+  if (c[0] < 0 || c[0] >= g.dims[0] || c[1] < 0 || c[1] >= g.dims[1] || c[2] < 0 ||
+      c[2] >= g.dims[2])
+    return -1;
+  return (c[0] * g.dims[1] + c[1]) * g.dims[2] + c[2];
+}
+
+// claim_occ's voxel coordinate + first-claimer (qpiw.py:262-283), made
+// order-free: the claimer is the smallest point index of the voxel.
+__global__ void __launch_bounds__(kBlock) k_cells(const float* __restrict__ xyz, int64_t n, GridDev g,
+                                                  int32_t* __restrict__ pt_cell,
+                                                  int32_t* __restrict__ first_pt, int32_t* counters) {
+  int in_grid = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
+    int c[3];
+    int cell = cell_of(p, g, c);
+    pt_cell[i] = cell;
+    if (cell >= 0) {
+      atomicMin(first_pt + cell, (int)i);
+      ++in_grid;
+    }
+  }
+  in_grid = wave_sum_i32(in_grid);
+  if ((threadIdx.x & 63) == 0 && in_grid) atomicAdd(counters + 1, in_grid);
+}
+
+__global__ void __launch_bounds__(kBlock) k_first_flags(int64_t n, const int32_t* __restrict__ pt_cell,
+                                                        const int32_t* __restrict__ first_pt,
+                                                        int32_t* __restrict__ flag) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int cell = pt_cell[i];
+    flag[i] = (cell >= 0 && first_pt[cell] == (int)i) ? 1 : 0;
+  }
+}
+
+// map_coor2occ (qpiw.py:305-340): slot -> coor_2_occ, dilation of the
+// occupancy by query_size (bitmap, atomicOr).
+__global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz, int64_t n, GridDev g,
+                                                  const int32_t* __restrict__ pt_cell,
+                                                  const int32_t* __restrict__ flag,
+                                                  const int32_t* __restrict__ pt_slot,
+                                                  int32_t* __restrict__ coor_2_occ,
+                                                  int32_t* __restrict__ occ_2_coor,
+                                                  uint32_t* __restrict__ occ_bits) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (!flag[i]) continue;
+    int slot = pt_slot[i];
+    if (slot >= g.max_o) continue;  // deterministic truncation (reference: reservoir)
+    int cell = pt_cell[i];
+    int c[3];
+    c[2] = cell % g.dims[2];
+    c[1] = (cell / g.dims[2]) % g.dims[1];
+    c[0] = cell / (g.dims[2] * g.dims[1]);
+    coor_2_occ[cell] = slot;
+    occ_2_coor[slot * 3 + 0] = c[0];
+    occ_2_coor[slot * 3 + 1] = c[1];
+    occ_2_coor[slot * 3 + 2] = c[2];
+    const int x0 = max(0, c[0] - g.qs[0] / 2), x1 = min(g.dims[0], c[0] + (g.qs[0] + 1) / 2);
+    const int y0 = max(0, c[1] - g.qs[1] / 2), y1 = min(g.dims[1], c[1] + (g.qs[1] + 1) / 2);
+    const int z0 = max(0, c[2] - g.qs[2] / 2), z1 = min(g.dims[2], c[2] + (g.qs[2] + 1) / 2);
+    for (int x = x0; x < x1; ++x)
+      for (int y = y0; y < y1; ++y)
+        for (int z = z0; z < z1; ++z) {
+          int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
+          atomicOr(occ_bits + (id >> 5), 1u << (id & 31));
+        }
+  }
+}
+
+// fill_occ2pnts (qpiw.py:342-387) part 1: per-voxel counts.  `voxel_idx > 0`
+// (qpiw.py:372) when slot0_drop: the voxel holding slot 0 gets no points.
+__global__ void __launch_bounds__(kBlock) k_count(int64_t n, GridDev g, const int32_t* __restrict__ pt_cell,
+                                                  const int32_t* __restrict__ coor_2_occ,
+                                                  int32_t* __restrict__ occ_numpnts) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int cell = pt_cell[i];
+    if (cell < 0) continue;
+    int slot = coor_2_occ[cell];
+    if (slot < 0 || (g.slot0_drop && slot == 0)) continue;
+    atomicAdd(occ_numpnts + slot, 1);
+  }
+}
+
+// part 2: bucket every point of a kept voxel (arrival order arbitrary).
+__global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, GridDev g, const int32_t* __restrict__ pt_cell,
+                                                    const int32_t* __restrict__ coor_2_occ,
+                                                    const int32_t* __restrict__ slot_off,
+                                                    int32_t* __restrict__ cursor,
+                                                    int32_t* __restrict__ bucket) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int cell = pt_cell[i];
+    if (cell < 0) continue;
+    int slot = coor_2_occ[cell];
+    if (slot < 0 || (g.slot0_drop && slot == 0)) continue;
+    int pos = atomicAdd(cursor + slot, 1);
+    bucket[slot_off[slot] + pos] = (int)i;
+  }
+}
+
+// part 3: per slot keep the P smallest point ids in ascending order (the
+// serial arrival order), write {xyz, id} records.
+__global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const float* __restrict__ xyz,
+                                                   const int32_t* __restrict__ occ_numpnts,
+                                                   const int32_t* __restrict__ slot_off,
+                                                   const int32_t* __restrict__ bucket,
+                                                   float4* __restrict__ occ_pts, int32_t* counters) {
+  int dropped = 0, mx = 0;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
+    const int cnt = occ_numpnts[s];
+    if (cnt == 0) continue;
+    const int off = slot_off[s];
+    const int keep = min(cnt, g.P);
+    int prev = -1;
+    for (int q = 0; q < keep; ++q) {
+      int best = 0x7fffffff;
+      for (int j = 0; j < cnt; ++j) {
+        int v = bucket[off + j];
+        best = (v > prev && v < best) ? v : best;
+      }
+      prev = best;
+      occ_pts[(int64_t)s * g.P + q] =
+          make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
+                      __int_as_float(best));
+    }
+    dropped += cnt - keep;
+    mx = max(mx, cnt);
+  }
+  dropped = wave_sum_i32(dropped);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) {
+    if (dropped) atomicAdd(counters + 2, dropped);
+    atomicMax(counters + 3, mx);
+  }
+}
+
+}  // namespace pnr
+
+using namespace pnr;
+
+extern "C" int pnr_points_bbox(const float* xyz_dev, int64_t n, float* out6_dev, void* stream) {
+  PNR_CHECK_ARG(xyz_dev && out6_dev, "bbox: null pointer");
+  PNR_CHECK_ARG(n > 0, "bbox: empty point set");
+  hipStream_t st = as_stream(stream);
+  unsigned* acc = reinterpret_cast<unsigned*>(out6_dev);
+  hipLaunchKernelGGL(k_bbox_init, dim3(1), dim3(64), 0, st, acc);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bbox, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, xyz_dev, n, acc);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bbox_fin, dim3(1), dim3(64), 0, st, acc);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
+                              const pnr_grid_params* p, void* stream) {
+  PNR_CHECK_ARG(h && xyz_dev && p, "grid_build: null pointer");
+  PNR_CHECK_ARG(n > 0 && n < (int64_t)1 << 31, "grid_build: point count %lld out of range", (long long)n);
+  PNR_CHECK_ARG(p->dims[0] > 0 && p->dims[1] > 0 && p->dims[2] > 0, "grid_build: empty grid dims");
+  PNR_CHECK_ARG(p->max_o > 0 && p->P > 0, "grid_build: max_o and P must be > 0");
+  PNR_CHECK_ARG(p->vsize[0] > 0 && p->vsize[1] > 0 && p->vsize[2] > 0, "grid_build: vsize <= 0");
+  const int64_t gvol = (int64_t)p->dims[0] * p->dims[1] * p->dims[2];
+  PNR_CHECK_ARG(gvol < (int64_t)1 << 31, "grid_build: grid of %lld cells exceeds int32 indexing",
+                (long long)gvol);
+  PNR_HIP(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  int rc;
+  const int64_t words = cdiv(gvol, 32);
+  const int64_t cap_o = p->max_o;
+  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->first_pt.ensure(gvol * 4)) ||
+      (rc = h->occ_bits.ensure(words * 4)) || (rc = h->occ_numpnts.ensure(cap_o * 4)) ||
+      (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
+      (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->slot_cursor.ensure(cap_o * 4)) ||
+      (rc = h->slot_off.ensure((cap_o + 1) * 4)) || (rc = h->pt_cell.ensure(n * 4)) ||
+      (rc = h->pt_flag.ensure(n * 4)) || (rc = h->pt_slot.ensure((n + 1) * 4)) ||
+      (rc = h->bucket.ensure(n * 4)) || (rc = h->counters.ensure(8 * 4)) ||
+      (rc = h->scan_tmp.ensure(scan_scratch_bytes(n > cap_o ? n : cap_o))))
+    return rc;
+  int32_t* coor_2_occ = h->coor_2_occ.as<int32_t>();
+  int32_t* first_pt = h->first_pt.as<int32_t>();
+  uint32_t* occ_bits = h->occ_bits.as<uint32_t>();
+  int32_t* occ_numpnts = h->occ_numpnts.as<int32_t>();
+  float4* occ_pts = h->occ_pts.as<float4>();
+  int32_t* occ_2_coor = h->occ_2_coor.as<int32_t>();
+  int32_t* slot_cursor = h->slot_cursor.as<int32_t>();
+  int32_t* slot_off = h->slot_off.as<int32_t>();
+  int32_t* pt_cell = h->pt_cell.as<int32_t>();
+  int32_t* pt_flag = h->pt_flag.as<int32_t>();
+  int32_t* pt_slot = h->pt_slot.as<int32_t>();
+  int32_t* bucket = h->bucket.as<int32_t>();
+  int32_t* counters = h->counters.as<int32_t>();
+
+  GridDev g;
+  for (int a = 0; a < 3; ++a) {
+    g.shift[a] = p->shift[a];
+    g.vs[a] = p->vsize[a];
+    g.dims[a] = p->dims[a];
+    g.qs[a] = p->query_size[a];
+  }
+  g.max_o = p->max_o;
+  g.P = p->P;
+  g.slot0_drop = p->slot0_drop;
+
+  PNR_HIP(hipMemsetAsync(first_pt, 0x7f, (size_t)gvol * 4, st));
+  PNR_HIP(hipMemsetAsync(coor_2_occ, 0xff, (size_t)gvol * 4, st));
+  PNR_HIP(hipMemsetAsync(occ_bits, 0, (size_t)words * 4, st));
+  PNR_HIP(hipMemsetAsync(occ_numpnts, 0, (size_t)cap_o * 4, st));
+  PNR_HIP(hipMemsetAsync(slot_cursor, 0, (size_t)cap_o * 4, st));
+  PNR_HIP(hipMemsetAsync(occ_2_coor, 0xff, (size_t)cap_o * 12, st));
+  PNR_HIP(hipMemsetAsync(counters, 0, 8 * 4, st));
+
+  const unsigned gp = grid_for(n, kBlock);
+  hipLaunchKernelGGL(k_cells, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, pt_cell, first_pt,
+                     counters);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_first_flags, dim3(gp), dim3(kBlock), 0, st, n, pt_cell, first_pt, pt_flag);
+  PNR_LAUNCH_CHECK();
+  if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p,
+                           h->scan_tmp.bytes, st)))
+    return rc;
+  hipLaunchKernelGGL(k_claim, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, pt_cell, pt_flag,
+                     pt_slot, coor_2_occ, occ_2_coor, occ_bits);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_count, dim3(gp), dim3(kBlock), 0, st, n, g, pt_cell, coor_2_occ,
+                     occ_numpnts);
+  PNR_LAUNCH_CHECK();
+  if ((rc = exclusive_scan(occ_numpnts, cap_o, nullptr, slot_off, nullptr, h->scan_tmp.p,
+                           h->scan_tmp.bytes, st)))
+    return rc;
+  hipLaunchKernelGGL(k_scatter, dim3(gp), dim3(kBlock), 0, st, n, g, pt_cell, coor_2_occ,
+                     slot_off, slot_cursor, bucket);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_select, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
+                     xyz_dev, occ_numpnts, slot_off, bucket, occ_pts, counters);
+  PNR_LAUNCH_CHECK();
+
+  int32_t cnt[8];
+  PNR_HIP(hipMemcpyAsync(cnt, counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
+  PNR_HIP(hipStreamSynchronize(st));
+  h->gp = *p;
+  h->gvol = gvol;
+  h->n_points = n;
+  h->stats.n_voxels = cnt[0];
+  h->stats.n_voxels_kept = cnt[0] < p->max_o ? cnt[0] : p->max_o;
+  h->stats.n_points_in_grid = cnt[1];
+  h->stats.n_points_dropped = cnt[2];
+  h->stats.max_points_per_voxel = cnt[3];
+  for (int a = 0; a < 3; ++a) h->stats.dims[a] = p->dims[a];
+  h->built = true;
+  return PNR_OK;
+}
+
+__global__ void k_export_ids(int n_slots, int P, const int32_t* __restrict__ occ_numpnts,
+                             const float4* __restrict__ occ_pts, int32_t* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)n_slots * P;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = e / P;
+    const int g = (int)(e - s * P);
+    out[e] = g < occ_numpnts[s] ? __float_as_int(occ_pts[e].w) : -1;
+  }
+}
+
+extern "C" int pnr_grid_export(pnr_handle* h, int32_t* coor_2_occ, uint32_t* occ_bits,
+                               int32_t* occ_numpnts, int32_t* occ_2_pnts, void* stream) {
+  PNR_CHECK_ARG(h && h->built, "grid_export: grid not built");
+  hipStream_t st = as_stream(stream);
+  const int64_t words = cdiv(h->gvol, 32);
+  const int64_t cap_o = h->gp.max_o;
+  if (coor_2_occ)
+    PNR_HIP(hipMemcpyAsync(coor_2_occ, h->coor_2_occ.p, h->gvol * 4, hipMemcpyDeviceToDevice, st));
+  if (occ_bits) PNR_HIP(hipMemcpyAsync(occ_bits, h->occ_bits.p, words * 4, hipMemcpyDeviceToDevice, st));
+  if (occ_numpnts)
+    PNR_HIP(hipMemcpyAsync(occ_numpnts, h->occ_numpnts.p, cap_o * 4, hipMemcpyDeviceToDevice, st));
+  if (occ_2_pnts) {
+    hipLaunchKernelGGL(k_export_ids, dim3(grid_for(cap_o * h->gp.P, kBlock)), dim3(kBlock), 0, st,
+                       (int)cap_o, h->gp.P, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(),
+                       occ_2_pnts);
+    PNR_LAUNCH_CHECK();
+  }
+  return PNR_OK;
+}
+
+extern "C" int pnr_grid_stats_get(pnr_handle* h, pnr_grid_stats* out) {
+  PNR_CHECK_ARG(h && out, "grid_stats: null pointer");
+  PNR_CHECK_ARG(h->built, "grid_stats: grid not built");
+  *out = h->stats;
+  return PNR_OK;
+}

@@ -1,0 +1,156 @@
+// Shared host/device helpers for libpnr.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/pnr.h"
+
+namespace pnr {
+
+// ------------------------------------------------------------ error plumbing
+void set_error(const char* fmt, ...);
+
+#define PNR_CHECK_ARG(cond, ...)          \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::pnr::set_error(__VA_ARGS__);      \
+      return PNR_EINVAL;                  \
+    }                                     \
+  } while (0)
+
+#define PNR_HIP(call)                                                         \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      ::pnr::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call,           \
+                       hipGetErrorString(e_));                                \
+      return PNR_EHIP;                                                        \
+    }                                                                         \
+  } while (0)
+
+#define PNR_LAUNCH_CHECK() PNR_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Persistent-grid launch size for grid-stride kernels: enough workgroups to
+// fill 256 CUs several times over, never more than the work needs.
+inline unsigned grid_for(int64_t items, int block, int max_blocks = 256 * 8) {
+  int64_t g = cdiv(items, block);
+  if (g < 1) g = 1;
+  if (g > max_blocks) g = max_blocks;
+  return (unsigned)g;
+}
+
+// Device-wide exclusive scan (scan.hip).
+int64_t scan_blocks(int64_t n);
+size_t scan_scratch_bytes(int64_t n);
+int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
+                   int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
+                   int as_flag = 0);  // as_flag: scan (in[i] != 0) instead of in[i]
+
+// --------------------------------------------------------- device helpers
+// floor((p - shift) / vs) exactly as the reference kernels compute it in fp32
+// (qpiw.py:265-267, 406-408, 471-473): one rounded subtraction, one correctly
+// rounded division, floor, truncating cast.
+__device__ __forceinline__ int vox_coord(float p, float shift, float vs) {
+  return (int)floorf(__fdiv_rn(__fsub_rn(p, shift), vs));
+}
+
+// raypos = campos + raydir * t  (diff_ray_marching.py:387: mul, then add).
+__device__ __forceinline__ float ray_at(float c, float d, float t) {
+  return __fadd_rn(c, __fmul_rn(d, t));
+}
+
+// Camera-space coordinates, xyz_c_j = sum_i (p_i - c_i) * R[i][j] with the
+// reference's summation order (qpiw.py:104-105, neural_points.py:687-693).
+__device__ __forceinline__ void world_to_cam(const float p[3], const float c[3],
+                                             const float R[9], float out[3]) {
+  float s0 = __fsub_rn(p[0], c[0]);
+  float s1 = __fsub_rn(p[1], c[1]);
+  float s2 = __fsub_rn(p[2], c[2]);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float a = __fmul_rn(s0, R[0 * 3 + j]);
+    float b = __fmul_rn(s1, R[1 * 3 + j]);
+    float d = __fmul_rn(s2, R[2 * 3 + j]);
+    out[j] = __fadd_rn(__fadd_rn(a, b), d);
+  }
+}
+
+// (x/z, y/z, z)
+__device__ __forceinline__ void world_to_pers(const float p[3], const float c[3],
+                                              const float R[9], float out[3]) {
+  float xc[3];
+  world_to_cam(p, c, R, xc);
+  out[0] = __fdiv_rn(xc[0], xc[2]);
+  out[1] = __fdiv_rn(xc[1], xc[2]);
+  out[2] = xc[2];
+}
+
+// Sum over the 64 lanes of a wave.
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+}  // namespace pnr
+
+// A device allocation that only grows.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want) {
+    if (p && bytes >= want) return PNR_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, want ? want : 16) != hipSuccess) {
+      ::pnr::set_error("hipMalloc of %zu bytes failed", want);
+      return PNR_ENOMEM;
+    }
+    bytes = want;
+    return PNR_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// Persistent grid tables owned by a handle (built by pnr_grid_build).
+struct pnr_handle {
+  int device = 0;
+  pnr_grid_params gp{};
+  int64_t gvol = 0;       // dims[0]*dims[1]*dims[2]
+  DevBuf coor_2_occ;      // int32 [gvol]   cell -> slot, -1 = empty
+  DevBuf occ_bits;        // uint32 [gvol/32] dilated occupancy bitmap
+  DevBuf first_pt;        // int32 [gvol]   smallest point id per cell
+  DevBuf occ_numpnts;     // int32 [max_o]  points that fell in the voxel
+  DevBuf occ_pts;         // float4 [max_o*P] {x, y, z, bitcast(point id)}
+  DevBuf occ_2_coor;      // int32 [max_o*3]
+  DevBuf slot_cursor;     // int32 [max_o]
+  DevBuf slot_off;        // int32 [max_o+1]
+  DevBuf pt_cell;         // int32 [N]
+  DevBuf pt_flag;         // int32 [N]
+  DevBuf pt_slot;         // int32 [N+1]
+  DevBuf bucket;          // int32 [N]
+  DevBuf counters;        // int32 [8]
+  DevBuf scan_tmp;
+  int64_t n_points = 0;
+  pnr_grid_stats stats{};
+  bool built = false;
+  void release_all() {
+    DevBuf* all[] = {&coor_2_occ, &occ_bits, &first_pt, &occ_numpnts, &occ_pts, &occ_2_coor,
+                     &slot_cursor, &slot_off, &pt_cell, &pt_flag, &pt_slot, &bucket,
+                     &counters, &scan_tmp};
+    for (DevBuf* b : all) b->release();
+  }
+};

@@ -1,0 +1,171 @@
+// Device-wide exclusive scan of int32 (three-pass: tile reduce, scan of tile
+// sums, tile scan + offset).  Used for every data-dependent compaction of the
+// query (R -> R' -> R'' and the SR pick of qpiw.py:655-719), so none of them
+// needs a host round trip.
+#include "pnr_common.h"
+
+namespace pnr {
+
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanBlock * kScanItems;  // 2048
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan of one value per thread over a 256-thread block; returns the
+// block total through *total.
+__device__ __forceinline__ int block_excl_scan(int v, int* lds4, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int inc = wave_incl_scan(v);
+  if (lane == 63) lds4[w] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kScanBlock / 64; ++i) {
+    int x = lds4[i];
+    base += (i < w) ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
+__device__ __forceinline__ int64_t eff_len(int64_t n, const int32_t* n_dev) {
+  if (!n_dev) return n;
+  int64_t m = *n_dev;
+  return m < n ? (m < 0 ? 0 : m) : n;
+}
+
+__device__ __forceinline__ int load_item(const int32_t* in, int64_t i, int64_t ne, int as_flag) {
+  if (i >= ne) return 0;
+  int v = in[i];
+  return as_flag ? (v != 0) : v;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_reduce(const int32_t* __restrict__ in, int64_t n,
+                                                            const int32_t* n_dev, int as_flag,
+                                                            int32_t* __restrict__ sums) {
+  __shared__ int lds4[4];
+  const int64_t ne = eff_len(n, n_dev);
+  const int64_t start = (int64_t)blockIdx.x * kScanTile;
+  if (start >= ne) {
+    if (threadIdx.x == 0) sums[blockIdx.x] = 0;
+    return;
+  }
+  int acc = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = start + j * kScanBlock + threadIdx.x;
+    acc += load_item(in, i, ne, as_flag);
+  }
+  int tot;
+  block_excl_scan(acc, lds4, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// One block scans all tile sums in place (exclusive); writes the grand total
+// to out[n_eff] and total_dev.
+__global__ void __launch_bounds__(kScanBlock) k_scan_sums(int32_t* sums, int64_t nb, int64_t n,
+                                                          const int32_t* n_dev, int32_t* out,
+                                                          int32_t* total_dev) {
+  __shared__ int lds4[4];
+  const int64_t per = cdiv(nb, kScanBlock);
+  const int64_t b0 = threadIdx.x * per;
+  int acc = 0;
+  for (int64_t i = b0; i < b0 + per && i < nb; ++i) acc += sums[i];
+  int tot;
+  int base = block_excl_scan(acc, lds4, &tot);
+  for (int64_t i = b0; i < b0 + per && i < nb; ++i) {
+    int x = sums[i];
+    sums[i] = base;
+    base += x;
+  }
+  if (threadIdx.x == 0) {
+    out[eff_len(n, n_dev)] = tot;
+    if (total_dev) *total_dev = tot;
+  }
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_final(const int32_t* __restrict__ in, int64_t n,
+                                                           const int32_t* n_dev, int as_flag,
+                                                           const int32_t* __restrict__ sums,
+                                                           int32_t* __restrict__ out) {
+  __shared__ int tile[kScanTile];
+  __shared__ int lds4[4];
+  const int64_t ne = eff_len(n, n_dev);
+  const int64_t start = (int64_t)blockIdx.x * kScanTile;
+  if (start >= ne) return;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = start + j * kScanBlock + threadIdx.x;
+    tile[j * kScanBlock + threadIdx.x] = load_item(in, i, ne, as_flag);
+  }
+  __syncthreads();
+  int v[kScanItems];
+  int acc = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    v[j] = tile[threadIdx.x * kScanItems + j];
+    acc += v[j];
+  }
+  int tot;
+  int base = block_excl_scan(acc, lds4, &tot) + sums[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    tile[threadIdx.x * kScanItems + j] = base;
+    base += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = start + j * kScanBlock + threadIdx.x;
+    if (i < ne) out[i] = tile[j * kScanBlock + threadIdx.x];
+  }
+}
+
+int64_t scan_blocks(int64_t n) { return cdiv(n > 0 ? n : 1, kScanTile); }
+
+size_t scan_scratch_bytes(int64_t n) { return (size_t)(scan_blocks(n) + 1) * sizeof(int32_t); }
+
+int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
+                   int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
+                   int as_flag) {
+  PNR_CHECK_ARG(in && out && scratch, "scan: null pointer");
+  PNR_CHECK_ARG(n >= 0, "scan: negative length");
+  const int64_t nb = scan_blocks(n);
+  PNR_CHECK_ARG(scratch_bytes >= scan_scratch_bytes(n), "scan: scratch too small (%zu < %zu)",
+                scratch_bytes, scan_scratch_bytes(n));
+  PNR_CHECK_ARG(nb < (int64_t)1 << 31, "scan: too many tiles");
+  int32_t* sums = static_cast<int32_t*>(scratch);
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanBlock), 0, st, sums, nb, n, n_dev, out, total_dev);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, out);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+}  // namespace pnr
+
+extern "C" int pnr_scan_scratch_bytes(int64_t n, size_t* out) {
+  PNR_CHECK_ARG(out, "null out");
+  *out = pnr::scan_scratch_bytes(n);
+  return PNR_OK;
+}
+
+extern "C" int pnr_exclusive_scan_i32(const int32_t* in, int64_t n, const int32_t* n_dev,
+                                      int32_t* out, int32_t* total_dev, void* scratch,
+                                      size_t scratch_bytes, void* stream) {
+  return pnr::exclusive_scan(in, n, n_dev, out, total_dev, scratch, scratch_bytes,
+                             pnr::as_stream(stream), 0);
+}

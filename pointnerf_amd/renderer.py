@@ -1,0 +1,187 @@
+"""Neural point cloud + the fused render module (the north-star hot path).
+
+``NeuralPoints`` mirrors the parameter table of
+models/neural_points/neural_points.py:11-331 (same parameter names, so the
+``neural_points.*`` keys of a reference checkpoint load into it) and its
+14-tuple ``forward`` (neural_points.py:782-812) for API compatibility.
+
+``NeuralPointsRayMarching`` mirrors
+models/neural_points_volumetric_model.py:230-389 (forward(**input) -> dict with
+coarse_raycolor / coarse_point_opacity / coarse_is_background / coarse_mask /
+queried_shading / ray_mask).  Its forward is the fused MI355X path:
+    pnr_query  (grid-resident march + layered KNN, device-side compaction)
+ -> pnr_aggregate_fwd (gather + weights + PE + MFMA MLP + K-sum + colour MLP)
+ -> pnr_composite_fwd (ray_dist + alpha composite + fill_invalid)
+with one small device->host read of the sample counts per ray batch (to size
+the feature buffer) and no ``raypos[R,400,3]`` / ``[R,SR,K,38]`` intermediates.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .aggregator import PointAggregator
+from .querier import QueryBuffers, lighting_fast_querier
+
+
+class NeuralPoints(nn.Module):
+    """Point table of neural_points.NeuralPoints (world-coordinate querier)."""
+
+    def __init__(self, opt, device, xyz=None, embedding=None, color=None, dirs=None, conf=None,
+                 Rw2c=None):
+        super().__init__()
+        self.opt = opt
+        self.device = torch.device(device)
+        self.xyz = nn.Parameter(torch.zeros((0, 3), device=self.device), requires_grad=False)
+        self.points_embeding = nn.Parameter(torch.zeros((1, 0, 32), device=self.device))
+        self.points_conf = None
+        self.points_dir = None
+        self.points_color = None
+        self.Rw2c = torch.eye(3, device=self.device)
+        if xyz is not None:
+            self.set_points(xyz, embedding, color, dirs, conf, Rw2c)
+        self.querier = lighting_fast_querier(self.device, opt)
+
+    def set_points(self, xyz, embedding, color=None, dirs=None, conf=None, Rw2c=None):
+        """set_points (neural_points.py:480-546) with point_*_mode '1'."""
+        dev = self.device
+        self.xyz = nn.Parameter(xyz.to(dev).float().reshape(-1, 3).contiguous(),
+                                requires_grad=getattr(self.opt, "xyz_grad", 0) > 0)
+        self.points_embeding = nn.Parameter(embedding.to(dev).float().reshape(1, -1, 32).contiguous())
+        self.points_color = None if color is None else nn.Parameter(color.to(dev).float().reshape(1, -1, 3).contiguous())
+        self.points_dir = None if dirs is None else nn.Parameter(dirs.to(dev).float().reshape(1, -1, 3).contiguous())
+        self.points_conf = None if conf is None else nn.Parameter(conf.to(dev).float().reshape(1, -1, 1).contiguous())
+        self.Rw2c = torch.eye(3, device=dev) if Rw2c is None else Rw2c.to(dev).float()
+
+    def tables(self, campos=None, camrot=None) -> tuple[L.Points, tuple]:
+        keep = (self.xyz.detach().contiguous(), self.points_embeding.detach().reshape(-1, 32).contiguous(),
+                None if self.points_color is None else self.points_color.detach().reshape(-1, 3).contiguous(),
+                None if self.points_dir is None else self.points_dir.detach().reshape(-1, 3).contiguous(),
+                None if self.points_conf is None else self.points_conf.detach().reshape(-1).contiguous())
+        p = L.Points(keep[0].data_ptr(), None, keep[1].data_ptr(), L.ptr(keep[2]), L.ptr(keep[3]),
+                     L.ptr(keep[4]), L.ptr(campos), L.ptr(camrot))
+        return p, keep
+
+    def w2pers(self, point_xyz, camrotc2w, campos):
+        """neural_points.py:687-693."""
+        point_xyz_shift = point_xyz[None, ...] - campos[:, None, :]
+        xyz = torch.sum(camrotc2w[:, None, :, :] * point_xyz_shift[:, :, :, None], dim=-2)
+        return torch.stack([xyz[:, :, 0] / xyz[:, :, 2], xyz[:, :, 1] / xyz[:, :, 2], xyz[:, :, 2]], dim=-1)
+
+    def forward(self, inputs):
+        """neural_points.py:782-812: query + gather, returns the 14-tuple the
+        reference PointAggregator consumes (API path; the fused renderer does
+        the gather inside pnr_aggregate_fwd instead)."""
+        camrotc2w, campos = inputs["camrotc2w"], inputs["campos"]
+        near, far = inputs["near"], inputs["far"]
+        pers = self.w2pers(self.xyz, camrotc2w, campos)
+        (sample_pidx, sample_loc, sample_loc_w, sample_ray_dirs, ray_mask, vsize, ranges) = \
+            self.querier.query_points(inputs.get("pixel_idx"), pers, self.xyz[None, ...], None,
+                                      inputs.get("h"), inputs.get("w"), inputs.get("intrinsic"),
+                                      torch.min(near).item(), torch.max(far).item(), inputs["raydir"],
+                                      campos, camrotc2w)
+        mask = sample_pidx >= 0
+        B, R, SR, K = sample_pidx.shape
+        idx = torch.clamp(sample_pidx, min=0).view(-1).long()
+        cat = torch.cat([self.xyz[None, ...], pers, self.points_embeding], dim=-1)
+        g = torch.index_select(cat, 1, idx).view(B, R, SR, K, cat.shape[-1])
+
+        def sel(t, c):
+            return None if t is None else torch.index_select(t, 1, idx).view(B, R, SR, K, c)
+
+        return (sel(self.points_color, 3), self.Rw2c, sel(self.points_dir, 3), sel(self.points_conf, 1),
+                g[..., 6:], g[..., 3:6], g[..., :3], mask, sample_loc, sample_loc_w, sample_ray_dirs,
+                ray_mask, vsize, 0)
+
+
+class NeuralPointsRayMarching(nn.Module):
+    """neural_points_volumetric_model.NeuralPointsRayMarching, fused HIP path."""
+
+    def __init__(self, opt, neural_points: NeuralPoints, aggregator: PointAggregator | None = None,
+                 chunk_rays: int | None = None):
+        super().__init__()
+        self.opt = opt
+        self.neural_points = neural_points
+        self.aggregator = aggregator if aggregator is not None else PointAggregator(opt).to(neural_points.device)
+        self.chunk_rays = chunk_rays
+        self._bufs = None
+        self.last_counts = None
+        if getattr(opt, "which_render_func", "radiance") != "radiance" or \
+                getattr(opt, "which_blend_func", "alpha") != "alpha" or \
+                getattr(opt, "which_tonemap_func", "off") != "off":
+            raise L.PnrError("libpnr implements radiance render, alpha blend and tone map 'off'")
+
+    @torch.no_grad()
+    def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False):
+        """Fused query -> aggregate -> composite for one ray batch [R,3].
+        Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8)."""
+        opt = self.opt
+        dev = raydir.device
+        L.require_gpu(raydir)
+        np_ = self.neural_points
+        q = np_.querier
+        if force_grid:
+            q.grid.key = None
+        R = raydir.shape[0]
+        SR, K, C = opt.SR, opt.K, 128
+        f32 = dict(dtype=torch.float32, device=dev)
+        ray_color = torch.empty((R, C), **f32)
+        opacity = torch.empty((R, SR), **f32)
+        is_bg = torch.empty((R,), **f32)
+        ray_mask = torch.empty((R,), dtype=torch.int8, device=dev)
+        bg = bg_color.to(dev).float().reshape(-1).contiguous() if bg_color is not None else None
+        if bg is not None and bg.numel() != C:
+            bg = bg.expand(C).contiguous() if bg.numel() == 1 else None
+            if bg is None:
+                raise L.PnrError("bg_color must have 1 or 128 channels")
+        campos = campos.reshape(3).float().contiguous()
+        camrot = camrot.reshape(3, 3).float().contiguous()
+        mlp, _keepw = self.aggregator.packed()
+        pts, _keepp = np_.tables(campos, camrot)
+        totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0)
+        chunk = self.chunk_rays or R
+        for r0 in range(0, R, chunk):
+            r1 = min(R, r0 + chunk)
+            rd = raydir[r0:r1].contiguous()
+            bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=self._bufs)
+            self._bufs = bufs
+            cnt = bufs.read_counts()
+            for k in totals:
+                totals[k] += cnt[k]
+            Sv = cnt["S_valid"]
+            feat = torch.empty((max(Sv, 1), C + 1), **f32)
+            s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
+                          bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
+                          bufs.fill_rs.data_ptr(), SR, K)
+            L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
+                                              L.ptr(feat), None, None, L.stream_ptr(dev)),
+                    "pnr_aggregate_fwd")
+            cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
+            L.check(L.lib().pnr_composite_fwd(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),
+                                              L.ctypes.byref(cp), L.ptr(feat), L.ptr(ray_color[r0:r1]),
+                                              L.ptr(opacity[r0:r1]), L.ptr(is_bg[r0:r1]),
+                                              L.ptr(ray_mask[r0:r1]), L.stream_ptr(dev)),
+                    "pnr_composite_fwd")
+        self.last_counts = totals
+        return ray_color, opacity, is_bg, ray_mask
+
+    def forward(self, campos, raydir, gt_image=None, bg_color=None, camrotc2w=None, pixel_idx=None,
+                near=None, far=None, focal=None, h=None, w=None, intrinsic=None, **kargs):
+        """neural_points_volumetric_model.py:272-352 (+ fill_invalid :354-389);
+        B = 1; the 2-D neural_render decoder of the fork is out of scope."""
+        if raydir.dim() == 3 and raydir.shape[0] != 1:
+            raise L.PnrError("batch size B > 1 is not supported (the reference uses B = 1)")
+        near_v = float(torch.min(near).item()) if torch.is_tensor(near) else float(near)
+        far_v = float(torch.max(far).item()) if torch.is_tensor(far) else float(far)
+        if "bg_ray" in kargs:
+            bg_color = None
+        color, opacity, is_bg, ray_mask = self.render_rays(campos, camrotc2w, raydir.reshape(-1, 3),
+                                                           near_v, far_v, bg_color)
+        R = color.shape[0]
+        mask_f = ray_mask.float().view(1, R, 1)
+        out = dict(coarse_raycolor=color.view(1, R, -1), coarse_point_opacity=opacity.view(1, R, -1),
+                   coarse_is_background=is_bg.view(1, R, 1), ray_mask=ray_mask.view(1, R))
+        out["coarse_mask"] = 1 - out["coarse_is_background"]
+        out["queried_shading"] = (1 - mask_f).repeat(1, 1, 3)
+        return out

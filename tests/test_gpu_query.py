@@ -1,0 +1,131 @@
+"""libpnr query kernels vs the CPU oracle (bit-exact integer/index results)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from scenes import scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(sc, cuda):
+    from pointnerf_amd.querier import lighting_fast_querier
+    return lighting_fast_querier(cuda, sc["opt"])
+
+
+def _run(sc, cuda, q=None):
+    q = q or _engine(sc, cuda)
+    xyz = torch.from_numpy(sc["xyz"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    cp = torch.from_numpy(sc["campos"]).to(cuda)
+    cr = torch.from_numpy(sc["camrot"]).to(cuda)
+    out = q.query_points(None, None, xyz[None], None, 800, 800, None, 2.0, 6.0, rd[None], cp[None], cr[None])
+    return q, out
+
+
+@pytest.mark.parametrize("slot0_drop", [1, 0])
+def test_grid_tables_bit_exact(cuda, slot0_drop):
+    sc = scene(20000, slot0_drop=slot0_drop)
+    q = _engine(sc, cuda)
+    xyz = torch.from_numpy(sc["xyz"]).to(cuda)
+    hp = q.grid.build(sc["opt"], xyz)
+    g = O.grid_build(sc["opt"], sc["xyz"])
+    assert np.array_equal(hp["shift"], g["hp"]["shift"]) and np.array_equal(hp["dims"], g["hp"]["dims"])
+    assert np.array_equal(hp["vsize_s"], g["hp"]["vsize_s"])
+    t = q.grid.export()
+    assert np.array_equal(t["coor_2_occ"].cpu().numpy(), g["coor_2_occ"])
+    bits = t["occ_bits"].cpu().numpy().view(np.uint32)
+    occ = ((bits[:, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(-1)[: g["coor_occ"].size]
+    assert np.array_equal(occ.astype(np.uint8), g["coor_occ"])
+    assert np.array_equal(t["occ_numpnts"].cpu().numpy(), g["occ_numpnts"])
+    assert np.array_equal(t["occ_2_pnts"].cpu().numpy(), g["occ_2_pnts"])
+    st = q.grid.stats()
+    assert st["n_voxels"] == g["n_occ"] and st["n_points_dropped"] == 0
+    if slot0_drop:
+        assert g["occ_numpnts"][0] == 0  # the fill_occ2pnts `voxel_idx > 0` quirk (qpiw.py:372)
+
+
+@pytest.mark.parametrize("K,theta", [(8, 30.0), (4, 130.0)])
+def test_query_points_bit_exact(cuda, K, theta):
+    sc = scene(20000, H=48, W=40, theta=theta, K=K)
+    _, out = _run(sc, cuda)
+    ref = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
+    pidx, loc, loc_w, dirs, ray_mask = [t.cpu().numpy() for t in out[:5]]
+    assert np.array_equal(ray_mask[0], ref["ray_mask"])
+    assert ref["ray_mask"].sum() > 100, "scene must exercise the query"
+    assert pidx.shape == (1,) + ref["sample_pidx"].shape
+    assert np.array_equal(pidx[0], ref["sample_pidx"])          # same neighbours, same order
+    assert np.array_equal(loc_w[0], ref["sample_loc_w"])
+    assert np.array_equal(loc[0], ref["sample_loc"])
+    assert np.array_equal(dirs[0], ref["sample_ray_dirs"])
+    np.testing.assert_array_equal(out[6], ref["ranges"])
+
+
+def test_query_internal_buffers(cuda):
+    sc = scene(20000, H=32, W=32)
+    q = _engine(sc, cuda)
+    xyz = torch.from_numpy(sc["xyz"]).to(cuda)
+    bufs, hp, rays, qp = q.run(xyz, torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["campos"]).to(cuda),
+                               torch.from_numpy(sc["camrot"]).to(cuda), 2.0, 6.0)
+    c = bufs.read_counts()
+    ref = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
+    R, SR = sc["raydir"].shape[0], sc["opt"].SR
+    nf = bufs.n_filled[:R].cpu().numpy()
+    assert np.array_equal(nf, ref["n_filled"])
+    sd = bufs.slot_d[: R * SR].cpu().numpy().astype(np.int32).reshape(R, SR)
+    for r in range(R):
+        assert np.array_equal(sd[r, : nf[r]], ref["slot_d"][r, : nf[r]])
+    assert c["S_filled"] == nf.sum() and c["R_hit"] == (nf > 0).sum()
+    assert c["R_valid"] == ref["ray_mask"].sum()
+    assert c["n_pairs"] == (ref["pidx_dense"] >= 0).sum()
+    assert c["S_valid"] == (ref["pidx_dense"] >= 0).any(-1).sum()
+
+
+def test_jittered_rays_per_ray_table(cuda):
+    # training mode: per-ray jittered depths (diff_ray_marching.py:373-375)
+    sc = scene(20000, H=24, W=24, is_train=1)
+    q = _engine(sc, cuda)
+    torch.manual_seed(3)
+    _, out = _run(sc, cuda, q)
+    torch.manual_seed(3)
+    from pointnerf_amd.querier import ray_mid_t
+    tv = ray_mid_t(2.0, 6.0, 400, R=sc["raydir"].shape[0], jitter=0.3, device=cuda).cpu().numpy()
+    ref = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], mid_t=tv)
+    assert np.array_equal(out[4].cpu().numpy()[0], ref["ray_mask"])
+    assert np.array_equal(out[0].cpu().numpy()[0], ref["sample_pidx"])
+
+
+def test_rays_missing_everything(cuda):
+    # rays pointing away from the scene: R'' = 0, empty outputs, ray_mask all 0
+    sc = scene(5000, H=8, W=8)
+    sc["raydir"] = -sc["raydir"]
+    _, out = _run(sc, cuda)
+    assert out[0].shape == (1, 0, sc["opt"].SR, sc["opt"].K)
+    assert int(out[4].sum()) == 0
+
+
+def test_deterministic_and_repeatable(cuda):
+    sc = scene(20000, H=32, W=32)
+    q, a = _run(sc, cuda)
+    q.grid.key = None  # force a rebuild
+    _, b = _run(sc, cuda, q)
+    for x, y in zip(a[:5], b[:5]):
+        assert torch.equal(x, y)
+
+
+def test_scan_matches_cumsum(cuda):
+    from pointnerf_amd import _lib as L
+    rng = np.random.default_rng(0)
+    for n in (1, 7, 2048, 2049, 100000, 1 << 20):
+        x = torch.from_numpy(rng.integers(0, 5, size=n).astype(np.int32)).to(cuda)
+        out = torch.empty(n + 1, dtype=torch.int32, device=cuda)
+        tot = torch.empty(1, dtype=torch.int32, device=cuda)
+        nb = L.c_size_t(0)
+        L.lib().pnr_scan_scratch_bytes(n, L.ctypes.byref(nb))
+        scratch = torch.empty(nb.value, dtype=torch.uint8, device=cuda)
+        L.check(L.lib().pnr_exclusive_scan_i32(L.ptr(x), n, None, L.ptr(out), L.ptr(tot), L.ptr(scratch),
+                                               nb.value, L.stream_ptr()), "scan")
+        ref = np.concatenate([[0], np.cumsum(x.cpu().numpy())])
+        assert np.array_equal(out.cpu().numpy(), ref)
+        assert int(tot.item()) == ref[-1]
