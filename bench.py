@@ -1,0 +1,275 @@
+"""Point-NeRF hot-path benchmark on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json metric "Mray-samples/sec at 800x800, K=8, 2M neural
+points"): lego flag set (dev_scripts/w_n360/lego.sh), a seeded synthetic
+2,000,000-point lego-like cloud, 800x800 NeRF-synthetic cameras, forward
+render.  One step = every GPU renders one full frame's worth of rays through
+the whole hot path: voxel-grid build, query, fused gather+MLP aggregation,
+composite+fill_invalid; with N > 1 the step's N frames are split across ranks
+in interleaved 16x16 pixel tiles and the rendered tiles are all-gathered over
+RCCL (weak scaling: per-GPU work is fixed).  A ray-sample is one (ray,
+shading-slot) entry of the dense H*W*SR grid the reference materialises
+(SURVEY 8(d)); value = all ranks' ray-samples / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FLOP_PER_PAIR = 542_720     # GEMM FLOPs per valid (sample, neighbour) pair
+FLOP_PER_SAMPLE = 137_216   # colour-branch GEMM FLOPs per valid sample
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector peak
+HBM_PEAK_GBS = 8000.0
+TILE = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--points", type=int, default=2_000_000)
+    ap.add_argument("--hw", type=int, default=800)
+    ap.add_argument("--no-grid-rebuild", action="store_true",
+                    help="reuse the voxel grid across steps (default: rebuild every step)")
+    ap.add_argument("--no-gather", action="store_true", help="skip the tile all-gather (N > 1)")
+    ap.add_argument("--cpu-rays", type=int, default=1500, help="rays in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
+    return ap.parse_args()
+
+
+def tile_owner(H, W, world, frame):
+    """rank owning each pixel: interleaved 16x16 tiles, round robin, rotated per frame."""
+    ty, tx = np.meshgrid(np.arange(H) // TILE, np.arange(W) // TILE, indexing="ij")
+    tiles_x = (W + TILE - 1) // TILE
+    return ((ty * tiles_x + tx + frame) % world).reshape(-1)
+
+
+def build_scene(args, device):
+    from pointnerf_amd import synthetic as S
+    from pointnerf_amd.aggregator import PointAggregator
+    from pointnerf_amd.options import lego_opt
+    from pointnerf_amd.renderer import NeuralPoints, NeuralPointsRayMarching
+    opt = lego_opt()
+    pts = S.lego_like_points(args.points, seed=0)
+    emb, color, dirs, conf = S.point_features(args.points, seed=0, default_conf=opt.default_conf)
+    torch.manual_seed(0)
+    agg = PointAggregator(opt).to(device).eval()   # random-init weights (xavier, networks.py:163-172)
+    np_ = NeuralPoints(opt, device, torch.from_numpy(pts), emb, color, dirs, conf)
+    model = NeuralPointsRayMarching(opt, np_, agg)
+    return opt, pts, (emb, color, dirs, conf), agg, model
+
+
+def cameras(n_frames, H, W):
+    from pointnerf_amd import synthetic as S
+    f = S.lego_focal(H)
+    cams = []
+    for i in range(n_frames):
+        theta = -180.0 + 360.0 * i / max(n_frames, 1)
+        campos, camrot = S.camera(theta, -30.0, 4.0)
+        cams.append((campos, camrot, S.pixel_rays(H, W, f, camrot)))
+    return cams
+
+
+def cpu_baseline(args, opt, pts, feats, agg, cam, H, W):
+    """The oracle (CPU port of the reference path) on a bounded sample of the
+    same workload: grid build once + query/aggregate/composite of a random
+    subset of one frame's rays, extrapolated to the frame."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    from oracle import oracle as O
+    threads = 16
+    ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+    torch.set_num_threads(threads)
+    emb, color, dirs, conf = feats
+    points = dict(xyz=pts, emb=emb.numpy(), color=color.numpy(), dir=dirs.numpy(), conf=conf.numpy())
+    params = {k: v.detach().cpu().numpy() for k, v in agg.state_dict().items()}
+    campos, camrot, rd = cam
+    rng = np.random.default_rng(0)
+    sel = rng.choice(rd.shape[0], size=min(args.cpu_rays, rd.shape[0]), replace=False)
+    bg = np.random.default_rng(1).uniform(size=128).astype(np.float32)
+    t0 = time.perf_counter()
+    grid = O.grid_build(opt, pts)
+    t1 = time.perf_counter()
+    q = O.query_points(opt, pts, campos, camrot, rd[sel], near=opt.near_plane, far=opt.far_plane, grid=grid)
+    O.render(opt, points, params, campos, camrot, rd[sel], bg, q=q)
+    t2 = time.perf_counter()
+    if ctx is not None:
+        ctx.__exit__(None, None, None)
+    R = H * W
+    t_frame = (t1 - t0) + (t2 - t1) * R / len(sel)
+    return {"value": round(R * opt.SR / t_frame / 1e6, 4), "unit": "Mray-samples/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle/ (C query, 1 thread; NumPy fp32 aggregate/composite, BLAS {threads} threads) "
+                       f"on {len(sel)} random rays of one {H}x{W} frame, {args.points} points: grid build "
+                       f"{t1 - t0:.2f}s + sample {t2 - t1:.2f}s, extrapolated to the frame "
+                       f"({t_frame:.1f}s/frame)")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+    from pointnerf_amd import _lib as L
+
+    H = W = args.hw
+    opt, pts, feats, agg, model = build_scene(args, device)
+    cams = cameras(8, H, W)
+    SR = opt.SR
+    # per-(frame, rank) pixel lists: step s renders frames s*world .. s*world+world-1
+    dev_cams = []
+    for campos, camrot, rd in cams:
+        dev_cams.append((torch.from_numpy(campos).to(device), torch.from_numpy(camrot).to(device),
+                         torch.from_numpy(rd).to(device)))
+    bg = torch.from_numpy(np.random.default_rng(1).uniform(size=128).astype(np.float32)).to(device)
+
+    owners = {}
+
+    def my_rays(frame):
+        ci = frame % len(cams)
+        if world == 1:
+            return ci, dev_cams[ci][2], None
+        key = (frame % world, ci)
+        if key not in owners:
+            own = tile_owner(H, W, world, frame)
+            idx = torch.from_numpy(np.nonzero(own == rank)[0]).to(device)
+            owners[key] = idx
+        idx = owners[key]
+        return ci, dev_cams[ci][2].index_select(0, idx).contiguous(), idx
+
+    stage = {"agg_ms": 0.0, "agg_calls": 0, "flops": 0.0, "pairs": 0, "valid": 0, "filled": 0}
+
+    def step(s, timed):
+        gathered = []
+        for f in range(world):
+            frame = s * world + f
+            ci, rd, idx = my_rays(frame)
+            campos, camrot, _ = dev_cams[ci]
+            ev = [] if timed else None
+            color, opac, is_bg, mask = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
+                                                         force_grid=not args.no_grid_rebuild, events=ev)
+            if timed:
+                c = model.last_counts
+                stage["pairs"] += c["n_pairs"]
+                stage["valid"] += c["S_valid"]
+                stage["filled"] += c["S_filled"]
+                stage["flops"] += c["n_pairs"] * FLOP_PER_PAIR + c["S_valid"] * FLOP_PER_SAMPLE
+                stage["_ev"] = stage.get("_ev", []) + ev
+            gathered.append(color)
+        if world > 1 and not args.no_gather:
+            # all-gather every rank's rendered tiles, each frame's share padded to the
+            # largest per-rank share (2500 tiles do not split evenly over 8 ranks)
+            parts = []
+            for f, g in enumerate(gathered):
+                mx = maxc[(s * world + f) % world]
+                if g.shape[0] < mx:
+                    g = torch.cat([g, g.new_zeros((mx - g.shape[0], g.shape[1]))])
+                parts.append(g.reshape(-1))
+            local_buf = torch.cat(parts)
+            full = torch.empty(world * local_buf.numel(), dtype=local_buf.dtype, device=device)
+            dist.all_gather_into_tensor(full, local_buf)
+            return full
+        return gathered
+
+    # largest per-rank ray share of each frame phase (all_gather_into_tensor needs equal sizes)
+    maxc = {fr: int(np.bincount(tile_owner(H, W, world, fr), minlength=world).max()) for fr in range(world)}
+
+    for s in range(args.warmup):
+        step(s, False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s, True)
+    torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        tt = torch.tensor([t_local], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    else:
+        t_max = t_local
+    torch.cuda.synchronize()
+    # per-stage times from HIP events recorded on the launch stream
+    per = {}
+    for name, a, b in stage.get("_ev", []):
+        per.setdefault(name, []).append(a.elapsed_time(b))
+    agg_ms = per.get("aggregate", [0.0])
+    avg_agg_s = float(np.mean(agg_ms)) / 1e3
+    launches = len(agg_ms)
+    flops_per_launch = stage["flops"] / max(launches, 1)
+
+    total_samples = H * W * SR * world * args.steps      # every rank renders one frame's worth
+    value = total_samples / t_max / 1e6
+    if rank == 0:
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "r01_pmc_aggregate.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        achieved = flops_per_launch / avg_agg_s / 1e12 if avg_agg_s > 0 else 0.0
+        out = {
+            "metric": "Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref",
+            "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded lego-like 2M-point cloud, random-init lego viewmlp weights)",
+            "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
+                       "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
+                       "grid_rebuild_per_frame": not args.no_grid_rebuild,
+                       "parallelism": f"dp{world} (16x16 ray tiles, RCCL all_gather of tiles)" if world > 1
+                       else "single GPU"},
+            "roofline": {"bound": "mfma", "kernel": "k_aggregate (fused gather+MLP, v_mfma_f32_32x32x2_f32)",
+                         "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},
+            "stages_ms": {k: round(float(np.mean(v)), 3) for k, v in per.items()},
+            "counts_per_frame": {"valid_pairs": stage["pairs"] // max(launches, 1),
+                                 "valid_samples": stage["valid"] // max(launches, 1),
+                                 "filled_samples": stage["filled"] // max(launches, 1)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args, opt, pts, feats, agg, cams[0], H, W)
+            except Exception as e:  # the baseline must never hide the GPU number
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

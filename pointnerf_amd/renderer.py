@@ -113,9 +113,11 @@ class NeuralPointsRayMarching(nn.Module):
             raise L.PnrError("libpnr implements radiance render, alpha blend and tone map 'off'")
 
     @torch.no_grad()
-    def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False):
+    def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None):
         """Fused query -> aggregate -> composite for one ray batch [R,3].
-        Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8)."""
+        Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8).
+        ``events``: optional list that receives (stage, start, end) HIP events
+        recorded on the launch stream around each stage."""
         opt = self.opt
         dev = raydir.device
         L.require_gpu(raydir)
@@ -141,10 +143,19 @@ class NeuralPointsRayMarching(nn.Module):
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0)
         chunk = self.chunk_rays or R
+        def mark():
+            if events is None:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+
         for r0 in range(0, R, chunk):
             r1 = min(R, r0 + chunk)
             rd = raydir[r0:r1].contiguous()
+            e0 = mark()
             bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=self._bufs)
+            e1 = mark()
             self._bufs = bufs
             cnt = bufs.read_counts()
             for k in totals:
@@ -154,15 +165,20 @@ class NeuralPointsRayMarching(nn.Module):
             s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
+            e2 = mark()
             L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                               L.ptr(feat), None, None, L.stream_ptr(dev)),
                     "pnr_aggregate_fwd")
+            e3 = mark()
             cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
             L.check(L.lib().pnr_composite_fwd(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),
                                               L.ctypes.byref(cp), L.ptr(feat), L.ptr(ray_color[r0:r1]),
                                               L.ptr(opacity[r0:r1]), L.ptr(is_bg[r0:r1]),
                                               L.ptr(ray_mask[r0:r1]), L.stream_ptr(dev)),
                     "pnr_composite_fwd")
+            if events is not None:
+                e4 = mark()
+                events += [("query", e0, e1), ("aggregate", e2, e3), ("composite", e3, e4)]
         self.last_counts = totals
         return ray_color, opacity, is_bg, ray_mask
 
