@@ -33,7 +33,6 @@ FLOP_PER_PAIR = 542_720     # GEMM FLOPs per valid (sample, neighbour) pair (SUR
 FLOP_PER_SAMPLE = 137_216   # colour-branch GEMM FLOPs per valid sample
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector peak
 HBM_PEAK_GBS = 8000.0
-TILE = 16
 
 
 def parse():
@@ -50,13 +49,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     return ap.parse_args()
-
-
-def tile_owner(H, W, world, frame):
-    """rank owning each pixel: interleaved 16x16 tiles, round robin, rotated per frame."""
-    ty, tx = np.meshgrid(np.arange(H) // TILE, np.arange(W) // TILE, indexing="ij")
-    tiles_x = (W + TILE - 1) // TILE
-    return ((ty * tiles_x + tx + frame) % world).reshape(-1)
 
 
 def build_scene(args, device):
@@ -150,27 +142,27 @@ def main():
                          torch.from_numpy(rd).to(device)))
     bg = torch.from_numpy(np.random.default_rng(1).uniform(size=128).astype(np.float32)).to(device)
 
-    owners = {}
+    from pointnerf_amd.parallel import TileShard
+    shards = {}
 
     def my_rays(frame):
         ci = frame % len(cams)
         if world == 1:
             return ci, dev_cams[ci][2], None
         key = (frame % world, ci)
-        if key not in owners:
-            own = tile_owner(H, W, world, frame)
-            idx = torch.from_numpy(np.nonzero(own == rank)[0]).to(device)
-            owners[key] = idx
-        idx = owners[key]
-        return ci, dev_cams[ci][2].index_select(0, idx).contiguous(), idx
+        if key not in shards:
+            sh = TileShard(H, W, rank, world, frame % world, device)
+            shards[key] = (sh, sh.select(dev_cams[ci][2]))
+        sh, rd = shards[key]
+        return ci, rd, sh
 
-    stage = {"agg_ms": 0.0, "agg_calls": 0, "flops": 0.0, "pairs": 0, "valid": 0, "filled": 0}
+    stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0}
 
     def step(s, timed):
-        gathered = []
+        frames = []
         for f in range(world):
             frame = s * world + f
-            ci, rd, idx = my_rays(frame)
+            ci, rd, sh = my_rays(frame)
             campos, camrot, _ = dev_cams[ci]
             ev = [] if timed else None
             color, opac, is_bg, mask = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
@@ -182,24 +174,12 @@ def main():
                 stage["filled"] += c["S_filled"]
                 stage["flops"] += c["n_pairs"] * FLOP_PER_PAIR + c["S_valid"] * FLOP_PER_SAMPLE
                 stage["_ev"] = stage.get("_ev", []) + ev
-            gathered.append(color)
-        if world > 1 and not args.no_gather:
-            # all-gather every rank's rendered tiles, each frame's share padded to the
-            # largest per-rank share (2500 tiles do not split evenly over 8 ranks)
-            parts = []
-            for f, g in enumerate(gathered):
-                mx = maxc[(s * world + f) % world]
-                if g.shape[0] < mx:
-                    g = torch.cat([g, g.new_zeros((mx - g.shape[0], g.shape[1]))])
-                parts.append(g.reshape(-1))
-            local_buf = torch.cat(parts)
-            full = torch.empty(world * local_buf.numel(), dtype=local_buf.dtype, device=device)
-            dist.all_gather_into_tensor(full, local_buf)
-            return full
-        return gathered
-
-    # largest per-rank ray share of each frame phase (all_gather_into_tensor needs equal sizes)
-    maxc = {fr: int(np.bincount(tile_owner(H, W, world, fr), minlength=world).max()) for fr in range(world)}
+            if world > 1 and not args.no_gather:
+                # RCCL all-gather of the rendered 16x16 tiles: every rank holds the frame
+                frames.append(sh.assemble(color))
+            else:
+                frames.append(color)
+        return frames
 
     for s in range(args.warmup):
         step(s, False)

@@ -1,0 +1,76 @@
+"""Host-side logic: weight packing, hyperparameters, flag set, synthetic data."""
+import numpy as np
+import torch
+
+from oracle import oracle as O
+
+
+def test_frag_pack_roundtrip_and_layout():
+    from pointnerf_amd.aggregator import frag_pack, frag_unpack
+    W = torch.randn(256, 263)
+    F = frag_pack(W, 132)
+    assert F.numel() == 132 * 8 * 64
+    assert torch.equal(frag_unpack(F, 132, 263), W)
+    # F[t][T][lane] = W[32T + (lane & 31)][2t + (lane >> 5)]
+    Fv = F.view(132, 8, 64)
+    for t, T, lane in [(0, 0, 0), (5, 3, 17), (131, 7, 40), (77, 2, 63)]:
+        k = 2 * t + (lane >> 5)
+        want = W[32 * T + (lane & 31), k] if k < 263 else 0.0
+        assert float(Fv[t, T, lane]) == float(want)
+
+
+def test_hyperparameters_match_oracle():
+    from pointnerf_amd.options import lego_opt
+    from pointnerf_amd.querier import hyperparameters_from_bbox
+    from pointnerf_amd import synthetic as S
+    opt = lego_opt()
+    for n, seed in [(5000, 0), (30000, 1)]:
+        pts = S.lego_like_points(n, seed=seed)
+        a = hyperparameters_from_bbox(opt, pts.min(0), pts.max(0))
+        b = O.get_hyperparameters(O.lego_opt(), pts)
+        for k in ("ranges", "shift", "vsize_s", "dims", "radius_limit2"):
+            assert np.array_equal(a[k], b[k]), k
+    # no ranges (ranges[0] >= ranges[3] disables clipping, qpiw.py:61-62)
+    pts = np.random.default_rng(0).uniform(-0.3, 0.3, size=(1000, 3)).astype(np.float32)
+    a = hyperparameters_from_bbox(lego_opt(ranges=[1, 1, 1, 0, 0, 0]), pts.min(0), pts.max(0))
+    b = O.get_hyperparameters(O.lego_opt(ranges=[1, 1, 1, 0, 0, 0]), pts)
+    assert np.array_equal(a["dims"], b["dims"]) and np.array_equal(a["shift"], b["shift"])
+
+
+def test_lego_flags():
+    from pointnerf_amd.options import lego_opt
+    o = lego_opt()
+    assert (o.SR, o.K, o.P, o.max_o, o.z_depth_dim) == (80, 8, 9, 830000, 400)
+    assert o.vsize == [0.004] * 3 and o.vscale == [2, 2, 2] and o.kernel_size == [3, 3, 3]
+    assert lego_opt(query_size=[0, 0, 0]).query_size == [3, 3, 3]   # neural_points.py:329
+
+
+def test_tvals_mirror_equals_oracle():
+    from pointnerf_amd.querier import ray_mid_t
+    assert np.array_equal(ray_mid_t(2.0, 6.0, 400)[0].numpy(), O.ray_mid_t(2.0, 6.0, 400)[0])
+
+
+def test_synthetic_points_respect_voxel_capacity():
+    from pointnerf_amd import synthetic as S
+    pts = S.lego_like_points(50000, seed=2)
+    g = O.grid_build(O.lego_opt(), pts)
+    assert g["occ_numpnts"].max() <= 8 < O.lego_opt().P
+    assert g["n_occ"] < O.lego_opt().max_o
+    campos, camrot = S.camera(0.0, -30.0, 4.0)
+    # camera looks at the origin: the centre pixel ray passes near it
+    d = S.pixel_rays(2, 2, 1000.0, camrot)[0]
+    t = -np.dot(campos, d) / np.dot(d, d)
+    assert np.linalg.norm(campos + t * d) < 0.05
+
+
+def test_product_fails_loudly_without_gpu():
+    import pytest
+    from pointnerf_amd import _lib as L
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(L.PnrError):
+        L.require_gpu()
+    from pointnerf_amd.querier import lighting_fast_querier
+    from pointnerf_amd.options import lego_opt
+    with pytest.raises(L.PnrError):
+        lighting_fast_querier(torch.device("cpu"), lego_opt())
