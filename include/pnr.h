@@ -172,18 +172,19 @@ int pnr_query_compact(const pnr_rays* rays, const pnr_query_params* q,
  * viewmlp with agg_intrp_order 2, agg_distance_kernel linear, agg_dist_pers 20,
  * point_features_dim 32, num_feat_freqs 3, dist_xyz_freq 5, num_viewdir_freqs 4,
  * shading_feature_num 256, block1 x2, block3 x2, alpha x1, colour x3 (C=128).
- * Weights are device fp32 arrays in the "fragment" layouts produced by
- * pointnerf_amd.aggregator.pack_weights() from the reference nn.Linear
- * [out,in] layout. */
+ * Weights are device fp32 arrays in the MFMA A-operand "fragment" layout
+ * produced by pointnerf_amd.aggregator.frag_pack() from the reference
+ * nn.Linear [out,in] weight W:  W_f[t][T][lane] = W[32T + (lane&31)][2t + (lane>>5)]
+ * for t < ceil(in/2) + 4 (4 trailing zero k-steps: prefetch padding), T < out/32. */
 typedef struct {
   const float* w1f; const float* b1;   /* block1.0  [256,284] fragment-packed */
   const float* w2f; const float* b2;   /* block1.2  [256,256]                  */
   const float* w3f; const float* b3;   /* block3.0  [256,263]                  */
   const float* w4f; const float* b4;   /* block3.2  [256,256]                  */
   const float* wa;  const float* ba;   /* alpha_branch.0 [1,256]               */
-  const float* wc1t; const float* bc1; /* color_branch.0 [128,280] transposed  */
-  const float* wc2t; const float* bc2; /* color_branch.2 [128,128] transposed  */
-  const float* wc3t; const float* bc3; /* color_branch.4 [128,128] transposed  */
+  const float* wc1f; const float* bc1; /* color_branch.0 [128,280]             */
+  const float* wc2f; const float* bc2; /* color_branch.2 [128,128]             */
+  const float* wc3f; const float* bc3; /* color_branch.4 [128,128]             */
   const float* rw2c;                   /* [3,3] uniform Rw2c (identity default) */
   float neg_slope;                     /* LeakyReLU slope (0 = ReLU)           */
   int32_t act_super;                   /* 1: softplus(x-1), 0: relu(x)         */
@@ -218,16 +219,19 @@ typedef struct {
  * row = v when samp_list is NULL) that has >= 1 valid neighbour:
  * out_feat[v, 0] = alpha, out_feat[v, 1..128] = colour features (rows of
  * samples without neighbours are left untouched).  Optional (may be NULL):
- * out_weight[row,K] normalised weights, out_conf[row,K] clamped confidence. */
+ * out_weight[row,K] normalised weights, out_conf[row,K] clamped confidence.
+ * scratch: 16-B aligned device buffer of pnr_aggregate_scratch_bytes(n_max). */
+int pnr_aggregate_scratch_bytes(int64_t n_max, size_t* out);
 int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
-                      float* out_feat, float* out_weight, float* out_conf, void* stream);
+                      float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                      size_t scratch_bytes, void* stream);
 
 /* PointAggregator.forward signature (pre-gathered tensors): pts tables are the
  * gathered [rows*K, C] tensors, s->pidx must be NULL (pair row = row*K + k),
  * pts->pers required, validity from pair_mask[rows*K] (sample_pnt_mask). */
 int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                              const uint8_t* pair_mask, float* out_feat, float* out_weight,
-                             float* out_conf, void* stream);
+                             float* out_conf, void* scratch, size_t scratch_bytes, void* stream);
 
 /* -------------------------------------------------------------- composite
  * Fused ray_dist (cummax), alpha composite and fill_invalid for the full ray

@@ -58,8 +58,8 @@ class QueryBufs(ctypes.Structure):
 class Mlp(ctypes.Structure):
     _fields_ = [("w1f", c_void_p), ("b1", c_void_p), ("w2f", c_void_p), ("b2", c_void_p),
                 ("w3f", c_void_p), ("b3", c_void_p), ("w4f", c_void_p), ("b4", c_void_p),
-                ("wa", c_void_p), ("ba", c_void_p), ("wc1t", c_void_p), ("bc1", c_void_p),
-                ("wc2t", c_void_p), ("bc2", c_void_p), ("wc3t", c_void_p), ("bc3", c_void_p),
+                ("wa", c_void_p), ("ba", c_void_p), ("wc1f", c_void_p), ("bc1", c_void_p),
+                ("wc2f", c_void_p), ("bc2", c_void_p), ("wc3f", c_void_p), ("bc3", c_void_p),
                 ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32)]
 
 
@@ -94,10 +94,11 @@ SIGNATURES = {
     "pnr_query": (c_int, [c_void_p, P(Rays), P(QueryParams), P(QueryBufs), c_void_p]),
     "pnr_query_compact": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), c_int64, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_aggregate_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
     "pnr_aggregate_fwd": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p, c_void_p,
-                                  c_void_p]),
+                                  c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
-                                         c_void_p, c_void_p, c_void_p]),
+                                         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_composite_fwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams),
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_ray_march_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
@@ -144,6 +145,13 @@ def require_gpu(t: torch.Tensor | None = None):
 
 def ptr(t: torch.Tensor | None):
     return None if t is None else c_void_p(t.data_ptr())
+
+
+def aggregate_scratch(n_max: int, device) -> torch.Tensor:
+    """Device scratch for pnr_aggregate_fwd(_masked) (K-summed features + masks)."""
+    nb = c_size_t(0)
+    check(lib().pnr_aggregate_scratch_bytes(int(n_max), ctypes.byref(nb)), "pnr_aggregate_scratch_bytes")
+    return torch.empty((int(nb.value) + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
 def stream_ptr(device=None):

@@ -60,18 +60,32 @@ def _init_seq(seq: nn.Sequential):
         _xavier_(mods[-1], 1.0)
 
 
-def frag_pack(W: torch.Tensor, nsteps: int) -> torch.Tensor:
-    """[256, Kin] nn.Linear weight -> MFMA A-operand fragments
-    F[t][T][lane] = W[32T + (lane & 31)][2t + (lane >> 5)] (zero padded)."""
+PREFETCH_PAD = 4   # kPD in aggregate.hip: zero k-steps appended for the weight prefetch
+
+
+def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """[out, Kin] nn.Linear weight (out a multiple of 32) and bias -> MFMA
+    A-operand fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)]
+    of W' = [W | bias | 0]: the bias rides in the GEMM as input column Kin
+    (the kernel sets X^T row Kin to 1).  ceil((Kin+1)/2) k-steps plus
+    PREFETCH_PAD zero ones."""
     out_f, kin = W.shape
-    assert out_f == 256 and kin <= 2 * nsteps
-    Wp = torch.zeros((256, 2 * nsteps), dtype=torch.float32, device=W.device)
+    assert out_f % 32 == 0
+    cols = kin + (1 if bias is not None else 0)
+    nsteps = (cols + 1) // 2
+    NT = out_f // 32
+    tot = nsteps + PREFETCH_PAD
+    Wp = torch.zeros((out_f, 2 * tot), dtype=torch.float32, device=W.device)
     Wp[:, :kin] = W.float()
-    return Wp.view(8, 32, nsteps, 2).permute(2, 0, 3, 1).contiguous().view(-1)
+    if bias is not None:
+        Wp[:, kin] = bias.float()
+    return Wp.view(NT, 32, tot, 2).permute(2, 0, 3, 1).contiguous().view(-1)
 
 
-def frag_unpack(F: torch.Tensor, nsteps: int, kin: int) -> torch.Tensor:
-    return F.view(nsteps, 8, 2, 32).permute(1, 3, 0, 2).reshape(256, 2 * nsteps)[:, :kin]
+def frag_unpack(F: torch.Tensor, kin: int, out_f: int = 256) -> torch.Tensor:
+    NT = out_f // 32
+    tot = F.numel() // (NT * 64)
+    return F.view(tot, NT, 2, 32).permute(1, 3, 0, 2).reshape(out_f, 2 * tot)[:, :kin]
 
 
 class PointAggregator(nn.Module):
@@ -112,17 +126,17 @@ class PointAggregator(nn.Module):
         with torch.no_grad():
             b1, b3 = self.block1, self.block3
             t = dict(
-                w1f=frag_pack(b1[0].weight, 142), b1=b1[0].bias.float().contiguous(),
-                w2f=frag_pack(b1[2].weight, 128), b2=b1[2].bias.float().contiguous(),
-                w3f=frag_pack(b3[0].weight, 132), b3=b3[0].bias.float().contiguous(),
-                w4f=frag_pack(b3[2].weight, 128), b4=b3[2].bias.float().contiguous(),
+                w1f=frag_pack(b1[0].weight, b1[0].bias), b1=b1[0].bias.float().contiguous(),
+                w2f=frag_pack(b1[2].weight, b1[2].bias), b2=b1[2].bias.float().contiguous(),
+                w3f=frag_pack(b3[0].weight, b3[0].bias), b3=b3[0].bias.float().contiguous(),
+                w4f=frag_pack(b3[2].weight, b3[2].bias), b4=b3[2].bias.float().contiguous(),
                 wa=self.alpha_branch[0].weight.float().reshape(-1).contiguous(),
                 ba=self.alpha_branch[0].bias.float().contiguous(),
-                wc1t=self.color_branch[0].weight.float().t().contiguous(),
+                wc1f=frag_pack(self.color_branch[0].weight, self.color_branch[0].bias),
                 bc1=self.color_branch[0].bias.float().contiguous(),
-                wc2t=self.color_branch[2].weight.float().t().contiguous(),
+                wc2f=frag_pack(self.color_branch[2].weight, self.color_branch[2].bias),
                 bc2=self.color_branch[2].bias.float().contiguous(),
-                wc3t=self.color_branch[4].weight.float().t().contiguous(),
+                wc3f=frag_pack(self.color_branch[4].weight, self.color_branch[4].bias),
                 bc3=self.color_branch[4].bias.float().contiguous(),
                 rw2c=self.rw2c.float().contiguous())
         m = L.Mlp()
@@ -175,9 +189,11 @@ class PointAggregator(nn.Module):
         s = L.Samples(None, None, rows, None, keep["sw"].data_ptr(), keep["sp"].data_ptr(),
                       keep["sd"].data_ptr(), None, 1, K)
         mlp, _ = self.packed()
+        scratch = L.aggregate_scratch(rows, dev)
         L.check(L.lib().pnr_aggregate_fwd_masked(L.ctypes.byref(pts), L.ctypes.byref(s),
                                                  L.ctypes.byref(mlp), L.ptr(keep["mask"]), L.ptr(out),
-                                                 L.ptr(weight), L.ptr(conf), L.stream_ptr(dev)),
+                                                 L.ptr(weight), L.ptr(conf), L.ptr(scratch),
+                                                 scratch.numel() * 4, L.stream_ptr(dev)),
                 "pnr_aggregate_fwd_masked")
         weight, conf = weight.view(B, R, SR, K), conf.view(B, R, SR, K)
         o = self.opt

@@ -1,5 +1,5 @@
 // Fused K-neighbour gather + inverse-distance weights + positional encodings +
-// per-(sample, neighbour) MLP + K-weighted sums + per-sample colour MLP.
+// per-(sample, neighbour) MLP + K-weighted sums, then the per-sample colour MLP.
 //
 // Replaces, for agg_intrp_order 2 / agg_distance_kernel "linear" /
 // agg_dist_pers 20 (the lego configuration, dev_scripts/w_n360/lego.sh):
@@ -10,42 +10,53 @@
 //   viewmlp (order 2)                       point_aggregators.py:488-646
 //   positional_encoding                     models/helpers/networks.py:175-190
 //
-// CDNA4 mapping.  One wave owns 32 (sample, neighbour) pairs = 4 samples x K=8
-// and carries them through all four 256-wide layers:
-//   Y^T[256 x 32] = W[256 x Kin] . X^T[Kin x 32]  with v_mfma_f32_32x32x2_f32
+// CDNA4 mapping.
+// k_pairs: one wave owns 32 (sample, neighbour) pairs = 4 samples x K=8 and
+// carries them through the four 256-wide layers as
+//   Y^T[256 x 32] = W[256 x Kin] . X^T[Kin x 32]  on v_mfma_f32_32x32x2_f32
 // (exact fp32 fmaf chains; gfx950 has no TF32).  The pair is the MFMA column
-// (lane & 31): the 8 accumulator tiles (128 AGPRs) hold the layer output with
-// the neuron on the register and the pair on the lane.  Each layer's input
-// X^T lives in a per-wave k-major LDS slice [k][32] (36 KB; 4 waves = 144 KB
-// of the CU's 160 KB), read with one conflict-free ds_read_b32 per k-step and
-// shared by the 8 MFMAs of the step; the activated accumulator is written
-// back in natural neuron order, so every weight matrix uses one "fragment"
-// layout W_f[t][T][lane] = W[32T + (lane&31)][2t + (lane>>5)] and every
-// A-operand load is a coalesced 256-B wave load from L2.  Layer-1 inputs
-// (embedding, 3-band PE of the embedding, 5-band PE of the 6-d distance) are
-// produced straight into the LDS slice by the lane that owns the pair.  No
-// workgroup barriers: waves run independent persistent loops.  The
-// 280->128->128->128 colour branch (3 % of the FLOPs) runs on the VALU from
-// the same (then dead) LDS slice.
+// (lane & 31): 8 accumulator tiles (128 AGPRs) hold a layer's output with the
+// neuron on the register and the pair on the lane.  Each layer's input X^T
+// lives in a per-wave k-major LDS slice [k][33] (37 KB; 4 waves = 148 KB of
+// the CU's 160 KB), one conflict-free ds_read_b32 per k-step shared by 8
+// MFMAs; activations are written back in natural neuron order, so every
+// weight matrix uses one "fragment" layout W_f[t][T][lane] =
+// W[32T + (lane&31)][2t + (lane>>5)] and every A-operand load is a coalesced
+// 256-B wave load from L2, software-pipelined kPD k-steps ahead.  Layer-1
+// inputs (embedding, 3-band PE of the embedding via sincos + angle doubling,
+// 5-band PE of the 6-d distance) are produced straight into the LDS slice by
+// the lane that owns the pair.  The K-sums run as wave shuffles; per valid
+// sample only alpha (-> out_feat[:,0]) and the 256-d feature leave the kernel.
+// k_color: one wave owns 32 samples and runs 280->128->128->128 with the same
+// machinery (4 accumulator tiles), so the colour branch (3 % of the FLOPs) also
+// runs on full-width MFMA instead of 4-sample VALU loops.
 #include "pnr_common.h"
 
 namespace pnr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kAggBlock = 256;     // 4 waves
+constexpr int kAggBlock = 256;     // 4 waves, each independent
 constexpr int kSampPerWave = 4;    // 4 samples x 8 neighbours = 32 MFMA columns
 constexpr int kKN = 8;
 constexpr int kHid = 256;
 constexpr int kEmb = 32;
 constexpr int kC = 128;
 constexpr int kCin = 280;          // 256 + 24 view PE
-constexpr int kFPitch = 288;       // LDS row pitch of the colour-branch input
+constexpr int kPitch = 33;         // LDS row pitch (floats) of X^T[k][32 + 1]
+constexpr int kXRows = 288;        // >= 284 layer-1 inputs
+constexpr int kWaveLds = kXRows * kPitch;  // floats per wave slice
+constexpr size_t kAggLdsBytes = (size_t)4 * kWaveLds * sizeof(float);
+constexpr int kWtRow = 286;        // X^T row holding the per-pair blend weight after layer 4
+constexpr int kPD = 4;             // weight prefetch depth in k-steps (packed weights are
+                                   // padded with kPD zero k-steps so prefetch never overruns)
 
 struct AggArgs {
   pnr_points pts;
   pnr_samples s;
   pnr_mlp w;
+  float* hid;                 // [n_max, 256] K-summed features (k_pairs -> k_color)
+  int32_t* vmask;             // [n_max] sample has >= 1 valid neighbour (k_pairs -> k_color)
   float* out_feat;
   float* out_weight;
   float* out_conf;
@@ -61,44 +72,74 @@ __device__ __forceinline__ float softplus(float x) {  // torch.nn.Softplus(beta=
 // Row of the accumulator register `r` for lane half `h` (32x32 C/D layout).
 __device__ __forceinline__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-__device__ __forceinline__ void bias_init(f32x16 (&acc)[8], const float* __restrict__ b, int h) {
+template <int NT>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[NT]) {
 #pragma unroll
-  for (int T = 0; T < 8; ++T)
+  for (int T = 0; T < NT; ++T) acc[T] = (f32x16){0.f};
+}
+
+// The bias rides in the MFMA: the packed weights carry it as input column
+// `kin` (frag_pack), so X^T row kin holds 1 and row kin+1 (if the k-step is
+// shared) holds 0.
+__device__ __forceinline__ void bias_rows(float* X, int kin, int lane) {
+  const int m = lane & 31, h = lane >> 5;
+  if ((kin & 1) == 0) X[(kin + h) * kPitch + m] = h ? 0.f : 1.f;
+  else if (h == 0) X[kin * kPitch + m] = 1.f;
+}
+
+template <int NT>
+__device__ __forceinline__ void load_w(float (&a)[NT], const float* __restrict__ p, int t) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[T][r] = b[32 * T + acc_row(r, h)];
+  for (int T = 0; T < NT; ++T) a[T] = p[(t * NT + T) * 64];
+}
+
+template <int NT>
+__device__ __forceinline__ void mfma_step(f32x16 (&acc)[NT], const float (&a)[NT], float x) {
+#pragma unroll
+  for (int T = 0; T < NT; ++T) acc[T] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[T], x, acc[T], 0, 0, 0);
 }
 
 // Y^T += W . X^T over nsteps k-steps (2 k-values each); X^T from the wave's
-// LDS slice, W in fragment layout.  8 MFMAs share each B operand.
-__device__ __forceinline__ void mlp_layer(f32x16 (&acc)[8], const float* __restrict__ wf,
+// LDS slice, W in fragment layout, weight loads issued kPD steps ahead.
+template <int NT>
+__device__ __forceinline__ void mlp_layer(f32x16 (&acc)[NT], const float* __restrict__ wf,
                                           const float* X, int nsteps, int lane) {
   const int m = lane & 31, h = lane >> 5;
   const float* p = wf + lane;
-#pragma unroll 2
-  for (int t = 0; t < nsteps; ++t) {
-    const float x = X[(2 * t + h) * 32 + m];
-    float a[8];
-#pragma unroll
-    for (int T = 0; T < 8; ++T) a[T] = p[(t * 8 + T) * 64];
-#pragma unroll
-    for (int T = 0; T < 8; ++T) acc[T] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[T], x, acc[T], 0, 0, 0);
+  const float* xr = X + h * kPitch + m;
+  float a0[NT], a1[NT], a2[NT], a3[NT];
+  load_w<NT>(a0, p, 0);
+  load_w<NT>(a1, p, 1);
+  load_w<NT>(a2, p, 2);
+  load_w<NT>(a3, p, 3);
+  int t = 0;
+#pragma unroll 1
+  for (; t + kPD <= nsteps; t += kPD) {
+    float x0 = xr[(2 * t + 0) * kPitch], x1 = xr[(2 * t + 2) * kPitch];
+    float x2 = xr[(2 * t + 4) * kPitch], x3 = xr[(2 * t + 6) * kPitch];
+    mfma_step<NT>(acc, a0, x0);
+    load_w<NT>(a0, p, t + 4);
+    mfma_step<NT>(acc, a1, x1);
+    load_w<NT>(a1, p, t + 5);
+    mfma_step<NT>(acc, a2, x2);
+    load_w<NT>(a2, p, t + 6);
+    mfma_step<NT>(acc, a3, x3);
+    load_w<NT>(a3, p, t + 7);
   }
+  const int rem = nsteps - t;  // 0..3
+  if (rem > 0) mfma_step<NT>(acc, a0, xr[(2 * t + 0) * kPitch]);
+  if (rem > 1) mfma_step<NT>(acc, a1, xr[(2 * t + 2) * kPitch]);
+  if (rem > 2) mfma_step<NT>(acc, a2, xr[(2 * t + 4) * kPitch]);
 }
 
 // Activated accumulator -> X^T rows in natural neuron order.
-__device__ __forceinline__ void store_act(const f32x16 (&acc)[8], float* X, float s, int lane) {
+template <int NT>
+__device__ __forceinline__ void store_act(const f32x16 (&acc)[NT], float* X, float s, int lane) {
   const int m = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int T = 0; T < 8; ++T)
+  for (int T = 0; T < NT; ++T)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) X[(32 * T + acc_row(r, h)) * 32 + m] = lrelu(acc[T][r], s);
-}
-
-__device__ __forceinline__ void activate(f32x16 (&acc)[8], float s) {  // in place
-#pragma unroll
-  for (int T = 0; T < 8; ++T)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[T][r] = lrelu(acc[T][r], s);
+    for (int r = 0; r < 16; ++r) X[(32 * T + acc_row(r, h)) * kPitch + m] = lrelu(acc[T][r], s);
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -120,22 +161,30 @@ __device__ __forceinline__ void mat3(const float* R, const float v[3], float o[3
   for (int j = 0; j < 3; ++j) o[j] = v[0] * R[j * 3 + 0] + v[1] * R[j * 3 + 1] + v[2] * R[j * 3 + 2];
 }
 
-constexpr int kXRows = 288;                 // >= 284 (layer-1 inputs), multiple of 32
-constexpr int kWaveLds = kXRows * 32;       // floats per wave slice (36 KB)
+__device__ __forceinline__ int64_t sample_row(const pnr_samples& s, int64_t v) {
+  return s.samp_list ? (int64_t)s.samp_list[v] : v;
+}
 
-__global__ void __launch_bounds__(kAggBlock, 1) k_aggregate(AggArgs A) {
-  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* X = lds_dyn + wid * kWaveLds;          // [kXRows][32] layer input X^T
-  float* F = X;                                 // [4][kFPitch] colour input (aliases X)
-  float* G = X + kSampPerWave * kFPitch;        // [4][kC] colour hidden (aliases X)
-  const int m = lane & 31, h = lane >> 5, j = m >> 3, k = m & 7;
-  const int K = A.s.K;
-  int64_t n = A.s.n_max;
-  if (A.s.n_dev) {
-    int64_t nd = *A.s.n_dev;
+__device__ __forceinline__ int64_t dir_row(const pnr_samples& s, int64_t row) {
+  return (s.dir_map ? (int64_t)s.dir_map[row] : row) / s.dir_div;
+}
+
+__device__ __forceinline__ int64_t eff_n(const pnr_samples& s) {
+  int64_t n = s.n_max;
+  if (s.n_dev) {
+    int64_t nd = *s.n_dev;
     n = nd < n ? nd : n;
   }
+  return n;
+}
+
+__global__ void __launch_bounds__(kAggBlock, 1) k_pairs(AggArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* X = lds_dyn + wid * kWaveLds;          // [kXRows][kPitch] layer input X^T
+  const int m = lane & 31, h = lane >> 5, j = m >> 3, k = m & 7;
+  const int K = A.s.K;
+  const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kSampPerWave);
   const float neg = A.w.neg_slope;
   float Rw[9];
@@ -153,7 +202,7 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_aggregate(AggArgs A) {
     // ------------------------------------------------------------ gather (neural_points.py:788-799)
     const int64_t v = tile * kSampPerWave + j;
     const bool active = v < n;
-    const int64_t row = active ? (A.s.samp_list ? (int64_t)A.s.samp_list[v] : v) : 0;
+    const int64_t row = active ? sample_row(A.s, v) : 0;
     int64_t prow = -1;  // point row
     bool valid = false;
     if (active && k < K) {
@@ -168,7 +217,7 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_aggregate(AggArgs A) {
     }
     float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
     if (active) {
-      const int64_t drow = (A.s.dir_map ? (int64_t)A.s.dir_map[row] : row) / A.s.dir_div;
+      const int64_t drow = dir_row(A.s, row);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         sw[a] = A.s.sample_w[row * 3 + a];
@@ -194,12 +243,6 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_aggregate(AggArgs A) {
       }
     }
     if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
-    // embedding -> X rows 0..31 (lane half h writes the odd/even rows)
-    {
-      const float* e = A.pts.emb + (valid ? prow : 0) * kEmb;
-#pragma unroll
-      for (int q = 0; q < kEmb / 2; ++q) X[(2 * q + h) * 32 + m] = valid ? e[2 * q + h] : 0.f;
-    }
     // dists, agg_dist_pers == 20 (point_aggregators.py:775-783)
     float d6[6];
     d6[0] = pw[0] - sw[0];
@@ -229,238 +272,287 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_aggregate(AggArgs A) {
     float vrot[3], drot[3];
     mat3(Rw, vd, vrot);
     mat3(Rw, pdir, drot);
-    wave_sync();
-    // PE_3(embedding) -> X rows 32..223: row 32 + 2(3c+f) + {sin, cos}
-    for (int i = 16; i < 112; ++i) {
-      const int p = i - 16, c = p / 3, f = p - 3 * c;
-      const float arg = X[c * 32 + m] * (float)(1 << f);
-      X[(2 * i + h) * 32 + m] = h ? cosf(arg) : sinf(arg);
-    }
-    // PE_5(rotated dists) -> X rows 224..283
-    for (int i = 112; i < 142; ++i) {
-      const int p = i - 112, c = p / 5, f = p - 5 * c;
-      float dc = dr6[0];
-      dc = c == 1 ? dr6[1] : dc;
-      dc = c == 2 ? dr6[2] : dc;
-      dc = c == 3 ? dr6[3] : dc;
-      dc = c == 4 ? dr6[4] : dc;
-      dc = c == 5 ? dr6[5] : dc;
-      const float arg = dc * (float)(1 << f);
-      X[(2 * i + h) * 32 + m] = h ? cosf(arg) : sinf(arg);
+
+    // ---------------------------------------------------- layer-1 inputs -> X^T
+    // lane half h owns embedding channels [16h, 16h+16): the channel itself
+    // (row c) and its 3-band PE (rows 32 + 2(3c+f) + {0: sin, 1: cos}); angle
+    // doubling from one sincos: sin 2x = 2 sin x cos x, cos 2x = (c - s)(c + s).
+    {
+      const float* e = A.pts.emb + (valid ? prow : 0) * kEmb + 16 * h;
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        float4 e4 = valid ? reinterpret_cast<const float4*>(e)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = 16 * h + 4 * q + u;
+          X[c * kPitch + m] = ev[u];
+          float s0, c0;
+          sincosf(ev[u], &s0, &c0);
+          const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
+          const float s2 = 2.f * s1 * c1, c2 = (c1 - s1) * (c1 + s1);
+          const int r0 = kEmb + 6 * c;
+          X[(r0 + 0) * kPitch + m] = s0;
+          X[(r0 + 1) * kPitch + m] = c0;
+          X[(r0 + 2) * kPitch + m] = s1;
+          X[(r0 + 3) * kPitch + m] = c1;
+          X[(r0 + 4) * kPitch + m] = s2;
+          X[(r0 + 5) * kPitch + m] = c2;
+        }
+      }
+      // 5-band PE of the 6-d rotated distance: rows 224 + 2(5c+f) + {sin, cos};
+      // half h owns channels 3h..3h+2 (direct sincos per band: |arg| grows to 16x)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        const int c = 3 * h + cc;
+        const float dc = h ? dr6[3 + cc] : dr6[cc];
+#pragma unroll 1
+        for (int f = 0; f < 5; ++f) {
+          float s, co;
+          sincosf(dc * (float)(1 << f), &s, &co);
+          const int r = kEmb + 6 * kEmb + 2 * (5 * c + f);
+          X[r * kPitch + m] = s;
+          X[(r + 1) * kPitch + m] = co;
+        }
+      }
+      bias_rows(X, 284, lane);
     }
     wave_sync();
 
     f32x16 acc[8];
     // ------------------------------------------------------------ block1: 284 -> 256 -> 256
-    bias_init(acc, A.w.b1, h);
-    mlp_layer(acc, A.w.w1f, X, 142, lane);
+    zero_acc<8>(acc);
+    mlp_layer<8>(acc, A.w.w1f, X, 143, lane);       // 284 inputs + bias column
     wave_sync();
-    store_act(acc, X, neg, lane);
+    store_act<8>(acc, X, neg, lane);
+    bias_rows(X, 256, lane);
     wave_sync();
-    bias_init(acc, A.w.b2, h);
-    mlp_layer(acc, A.w.w2f, X, 128, lane);
+    zero_acc<8>(acc);
+    mlp_layer<8>(acc, A.w.w2f, X, 129, lane);
     wave_sync();
-    store_act(acc, X, neg, lane);
-    // block3 extra inputs, rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), 0
+    store_act<8>(acc, X, neg, lane);
+    // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
     {
       const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
       const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0],
-                           drot[1] - vrot[1], drot[2] - vrot[2], dot, 0.f};
+                           drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) X[(256 + 2 * e + h) * 32 + m] = h ? ex[2 * e + 1] : ex[2 * e];
+      for (int e = 0; e < 4; ++e) X[(256 + 2 * e + h) * kPitch + m] = h ? ex[2 * e + 1] : ex[2 * e];
     }
     wave_sync();
     // ------------------------------------------------------------ block3: 263 -> 256 -> 256
-    bias_init(acc, A.w.b3, h);
-    mlp_layer(acc, A.w.w3f, X, 132, lane);
+    zero_acc<8>(acc);
+    mlp_layer<8>(acc, A.w.w3f, X, 132, lane);
     wave_sync();
-    store_act(acc, X, neg, lane);
+    store_act<8>(acc, X, neg, lane);
+    bias_rows(X, 256, lane);
     wave_sync();
-    bias_init(acc, A.w.b4, h);
-    mlp_layer(acc, A.w.w4f, X, 128, lane);
-    activate(acc, neg);
-    wave_sync();  // X is dead from here on: F/G alias it
+    zero_acc<8>(acc);
+    mlp_layer<8>(acc, A.w.w4f, X, 129, lane);
+    wave_sync();
+    store_act<8>(acc, X, neg, lane);                // h4 -> X^T rows 0..255
+    if (h == 0) X[kWtRow * kPitch + m] = wt;        // per-pair blend weight
+    wave_sync();
     // ------------------------------------------------------------ alpha branch + K sums
-    float pa = 0.f;
-#pragma unroll
-    for (int T = 0; T < 8; ++T)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) pa += acc[T][r] * A.w.wa[32 * T + acc_row(r, h)];
-    pa += __shfl_xor(pa, 32);
-    pa += A.w.ba[0];
+    // alpha_k = softplus(W_a . h4 + b_a - 1) per pair (both lane halves compute it;
+    // W_a[n] is wave-uniform -> scalar loads)
+    float pa = A.w.ba[0];
+    const float* xc = X + m;
+#pragma unroll 8
+    for (int nn = 0; nn < kHid; ++nn) pa += A.w.wa[nn] * xc[nn * kPitch];
     const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
     const float alpha_s = xor8_sum(wt * alpha_k);   // point_aggregators.py:608-614
-    // feature K-sum (point_aggregators.py:622-628) -> F[j][n]
+    // feature K-sum (point_aggregators.py:622-628): lane owns neurons lane + 64i,
+    // written straight to hid[v] (256-B coalesced rows)
+    float wk[kKN];
 #pragma unroll
-    for (int T = 0; T < 8; ++T)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float s = xor8_sum(acc[T][r] * wt);
-        if (k == 0) F[j * kFPitch + 32 * T + acc_row(r, h)] = s;
-      }
-    // view-direction PE, ori dropped (point_aggregators.py:507-512): sin block then cos block
-    {
-      const int qd = k * 2 + h;  // 0..15 per sample
-#pragma unroll
-      for (int rep = 0; rep < 2; ++rep) {
-        const int q = qd + 16 * rep;
-        if (q < 24) {
-          const int blk = q / 12, c = (q % 12) / 4, f = q % 4;
-          const float vc = c == 0 ? vrot[0] : (c == 1 ? vrot[1] : vrot[2]);
-          const float arg = vc * (float)(1 << f);
-          F[j * kFPitch + kHid + q] = blk ? cosf(arg) : sinf(arg);
-        }
-      }
-    }
-    wave_sync();
-    // ------------------------------------------------------------ colour branch 280->128->128->128
-    float c0[kSampPerWave], c1[kSampPerWave];
-#pragma unroll
-    for (int s = 0; s < kSampPerWave; ++s) {
-      c0[s] = A.w.bc1[lane];
-      c1[s] = A.w.bc1[lane + 64];
-    }
-#pragma unroll 4
-    for (int kk = 0; kk < kCin; ++kk) {
-      const float w0 = A.w.wc1t[kk * kC + lane], w1 = A.w.wc1t[kk * kC + 64 + lane];
-#pragma unroll
-      for (int s = 0; s < kSampPerWave; ++s) {
-        const float x = F[s * kFPitch + kk];
-        c0[s] += w0 * x;
-        c1[s] += w1 * x;
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < kSampPerWave; ++s) {
-      G[s * kC + lane] = lrelu(c0[s], neg);
-      G[s * kC + 64 + lane] = lrelu(c1[s], neg);
-    }
-    wave_sync();
-#pragma unroll
-    for (int s = 0; s < kSampPerWave; ++s) {
-      c0[s] = A.w.bc2[lane];
-      c1[s] = A.w.bc2[lane + 64];
-    }
-#pragma unroll 4
-    for (int kk = 0; kk < kC; ++kk) {
-      const float w0 = A.w.wc2t[kk * kC + lane], w1 = A.w.wc2t[kk * kC + 64 + lane];
-#pragma unroll
-      for (int s = 0; s < kSampPerWave; ++s) {
-        const float x = G[s * kC + kk];
-        c0[s] += w0 * x;
-        c1[s] += w1 * x;
-      }
-    }
-    wave_sync();
-#pragma unroll
-    for (int s = 0; s < kSampPerWave; ++s) {
-      F[s * kFPitch + lane] = lrelu(c0[s], neg);
-      F[s * kFPitch + 64 + lane] = lrelu(c1[s], neg);
-    }
-    wave_sync();
-#pragma unroll
-    for (int s = 0; s < kSampPerWave; ++s) {
-      c0[s] = A.w.bc3[lane];
-      c1[s] = A.w.bc3[lane + 64];
-    }
-#pragma unroll 4
-    for (int kk = 0; kk < kC; ++kk) {
-      const float w0 = A.w.wc3t[kk * kC + lane], w1 = A.w.wc3t[kk * kC + 64 + lane];
-#pragma unroll
-      for (int s = 0; s < kSampPerWave; ++s) {
-        const float x = F[s * kFPitch + kk];
-        c0[s] += w0 * x;
-        c1[s] += w1 * x;
-      }
-    }
-    // ------------------------------------------------------------ write [alpha, c_1..c_128]
-    // each sample's (row, valid, alpha) comes from the lane owning its neighbour 0
+    for (int q = 0; q < kKN; ++q) wk[q] = 0.f;
 #pragma unroll
     for (int s = 0; s < kSampPerWave; ++s) {
       const int src = s * 8;
       const bool act_s = __shfl((int)(active && samp_valid), src) != 0;
       const float al_s = __shfl(alpha_s, src);
-      if (act_s) {
-        // output row = position in the sample list (compact valid-sample index)
-        float* o = A.out_feat + (tile * kSampPerWave + s) * (kC + 1);
-        if (lane == 0) o[0] = al_s;
-        o[1 + lane] = lrelu(c0[s], neg);
-        o[1 + 64 + lane] = lrelu(c1[s], neg);
+      const int64_t vo = tile * kSampPerWave + s;   // sample-list index
+      if (vo < n && lane == 0) A.vmask[vo] = act_s;
+      if (!act_s) continue;
+#pragma unroll
+      for (int q = 0; q < kKN; ++q) wk[q] = X[kWtRow * kPitch + s * 8 + q];
+      if (lane == 0) A.out_feat[vo * (kC + 1)] = al_s;
+#pragma unroll
+      for (int i = 0; i < kHid / 64; ++i) {
+        const float* xr = X + (lane + 64 * i) * kPitch + s * 8;
+        float f = 0.f;
+#pragma unroll
+        for (int q = 0; q < kKN; ++q) f += wk[q] * xr[q];
+        A.hid[vo * kHid + lane + 64 * i] = f;
       }
     }
     wave_sync();
   }
 }
 
-constexpr size_t kAggLdsBytes = (size_t)4 * kWaveLds * sizeof(float);
+// colour branch (point_aggregators.py:630-641): [f(256), PE_4(R.v)(24)] -> 128 x3.
+__global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* X = lds_dyn + wid * kWaveLds;   // [kXRows][kPitch]
+  const int m = lane & 31, h = lane >> 5;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, 32);
+  const float neg = A.w.neg_slope;
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t v0 = tile * 32;
+    const int nv = (int)((n - v0) < 32 ? (n - v0) : 32);
+    const int my_valid = (m < nv) ? A.vmask[v0 + m] : 0;
+    const unsigned long long vbits = __ballot(my_valid != 0);   // bit q (and q+32): sample q valid
+    // hid rows (one 1-KB row per wave instruction) -> X^T rows 0..255 (transpose)
+#pragma unroll 4
+    for (int q = 0; q < 32; ++q) {
+      float4 f4 = ((vbits >> q) & 1ull) ? reinterpret_cast<const float4*>(A.hid + (v0 + q) * kHid)[lane]
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      X[(4 * lane + 0) * kPitch + q] = f4.x;
+      X[(4 * lane + 1) * kPitch + q] = f4.y;
+      X[(4 * lane + 2) * kPitch + q] = f4.z;
+      X[(4 * lane + 3) * kPitch + q] = f4.w;
+    }
+    // view-direction PE, ori dropped (point_aggregators.py:506-512): rows 256..279 =
+    // sin block (c*4+f) then cos block; lane half h writes block h
+    {
+      float vrot[3] = {0.f, 0.f, 0.f};
+      if (m < nv) {
+        const int64_t row = sample_row(A.s, v0 + m);
+        const int64_t drow = dir_row(A.s, row);
+        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+        mat3(Rw, vd, vrot);
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          float s, co;
+          sincosf(vrot[c] * (float)(1 << f), &s, &co);
+          X[(kHid + 12 * h + 4 * c + f) * kPitch + m] = h ? co : s;
+        }
+    }
+    bias_rows(X, kCin, lane);
+    wave_sync();
+    f32x16 acc[4];
+    zero_acc<4>(acc);
+    mlp_layer<4>(acc, A.w.wc1f, X, 141, lane);      // 280 inputs + bias column
+    wave_sync();
+    store_act<4>(acc, X, neg, lane);
+    bias_rows(X, kC, lane);
+    wave_sync();
+    zero_acc<4>(acc);
+    mlp_layer<4>(acc, A.w.wc2f, X, 65, lane);
+    wave_sync();
+    store_act<4>(acc, X, neg, lane);
+    bias_rows(X, kC, lane);
+    wave_sync();
+    zero_acc<4>(acc);
+    mlp_layer<4>(acc, A.w.wc3f, X, 65, lane);
+    wave_sync();
+    store_act<4>(acc, X, neg, lane);   // X^T rows 0..127 = colour features
+    wave_sync();
+    // write out_feat[v, 1..128]: lane = channel pair, loop over the 32 samples
+    for (int q = 0; q < nv; ++q) {
+      if (!((vbits >> q) & 1ull)) continue;   // samples without neighbours keep zeros
+      float* o = A.out_feat + (v0 + q) * (kC + 1) + 1;
+      o[lane] = X[lane * kPitch + q];
+      o[64 + lane] = X[(64 + lane) * kPitch + q];
+    }
+    wave_sync();
+  }
+}
+
+int launch(const AggArgs& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
+    attr = true;
+  }
+  const int64_t tiles = cdiv(a.s.n_max, kSampPerWave);
+  hipLaunchKernelGGL(k_pairs, dim3(grid_for(tiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
+  PNR_LAUNCH_CHECK();
+  const int64_t ctiles = cdiv(a.s.n_max, 32);
+  hipLaunchKernelGGL(k_color, dim3(grid_for(ctiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, float* out_feat,
+                 float* scratch, size_t scratch_bytes) {
+  PNR_CHECK_ARG(pts && s && w && out_feat, "aggregate: null pointer");
+  PNR_CHECK_ARG(pts->xyz && pts->emb, "aggregate: point xyz/emb required");
+  PNR_CHECK_ARG(s->sample_w && s->sample_p && s->dirs, "aggregate: sample arrays required");
+  PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate: K=%d unsupported (1..8)", s->K);
+  PNR_CHECK_ARG(s->dir_div >= 1, "aggregate: dir_div must be >= 1");
+  PNR_CHECK_ARG(w->w1f && w->b1 && w->w2f && w->b2 && w->w3f && w->b3 && w->w4f && w->b4 && w->wa &&
+                    w->ba && w->wc1f && w->bc1 && w->wc2f && w->bc2 && w->wc3f && w->bc3,
+                "aggregate: null weight");
+  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0, "aggregate: emb must be 16-B aligned");
+  PNR_CHECK_ARG(scratch && ((uintptr_t)scratch & 15) == 0, "aggregate: 16-B aligned scratch required");
+  PNR_CHECK_ARG(scratch_bytes >= (size_t)(s->n_max > 0 ? s->n_max : 0) * (kHid + 1) * sizeof(float),
+                "aggregate: scratch too small (%zu bytes for %lld samples)", scratch_bytes,
+                (long long)s->n_max);
+  return PNR_OK;
+}
 
 }  // namespace pnr
 
 using namespace pnr;
 
-static void set_lds_attr() {
-  static bool done = false;
-  if (!done) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&k_aggregate),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes);
-    done = true;
-  }
+extern "C" int pnr_aggregate_scratch_bytes(int64_t n_max, size_t* out) {
+  PNR_CHECK_ARG(out && n_max >= 0, "aggregate_scratch_bytes: bad args");
+  *out = (size_t)(n_max > 0 ? n_max : 1) * (kHid + 1) * sizeof(float);
+  return PNR_OK;
 }
 
 extern "C" int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
-                                 float* out_feat, float* out_weight, float* out_conf, void* stream) {
-  PNR_CHECK_ARG(pts && s && w && out_feat, "aggregate: null pointer");
-  PNR_CHECK_ARG(pts->xyz && pts->emb, "aggregate: point xyz/emb required");
+                                 float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                                 size_t scratch_bytes, void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
   PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate: need pers or camera");
-  PNR_CHECK_ARG(s->sample_w && s->sample_p && s->dirs, "aggregate: sample arrays required");
-  PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate: K=%d unsupported (1..8)", s->K);
-  PNR_CHECK_ARG(s->dir_div >= 1, "aggregate: dir_div must be >= 1");
-  PNR_CHECK_ARG(w->w1f && w->b1 && w->w2f && w->b2 && w->w3f && w->b3 && w->w4f && w->b4 && w->wa &&
-                    w->ba && w->wc1t && w->bc1 && w->wc2t && w->bc2 && w->wc3t && w->bc3,
-                "aggregate: null weight");
-  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0, "aggregate: emb must be 16-B aligned");
   if (s->n_max <= 0) return PNR_OK;
   AggArgs a;
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
+  a.hid = static_cast<float*>(scratch);
+  a.vmask = reinterpret_cast<int32_t*>(a.hid + (s->n_max > 0 ? s->n_max : 1) * kHid);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.pair_mask = nullptr;
-  const int64_t tiles = cdiv(s->n_max, kSampPerWave);
-  const unsigned grid = grid_for(tiles, 4, 256);
-  set_lds_attr();
-  hipLaunchKernelGGL(k_aggregate, dim3(grid), dim3(kAggBlock), kAggLdsBytes, as_stream(stream), a);
-  PNR_LAUNCH_CHECK();
-  return PNR_OK;
+  return launch(a, as_stream(stream));
 }
 
-// Mirror-path entry: pre-gathered [rows,K,C] tensors (PointAggregator.forward
-// signature), validity from sample_pnt_mask.  Not in the public header's hot
-// path; used by pointnerf_amd.aggregator.PointAggregator.
 extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                         const uint8_t* pair_mask, float* out_feat, float* out_weight,
-                                        float* out_conf, void* stream) {
-  PNR_CHECK_ARG(pts && s && w && out_feat && pair_mask, "aggregate_masked: null pointer");
-  PNR_CHECK_ARG(pts->xyz && pts->emb && pts->pers, "aggregate_masked: xyz/emb/pers required");
+                                        float* out_conf, void* scratch, size_t scratch_bytes,
+                                        void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
+  PNR_CHECK_ARG(pair_mask, "aggregate_masked: null pair_mask");
+  PNR_CHECK_ARG(pts->pers, "aggregate_masked: pers required");
   PNR_CHECK_ARG(s->pidx == nullptr, "aggregate_masked: pidx must be NULL (identity rows)");
-  PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate_masked: K=%d unsupported (1..8)", s->K);
-  PNR_CHECK_ARG(s->dir_div >= 1, "aggregate_masked: dir_div must be >= 1");
-  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0, "aggregate_masked: emb must be 16-B aligned");
   if (s->n_max <= 0) return PNR_OK;
   AggArgs a;
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
+  a.hid = static_cast<float*>(scratch);
+  a.vmask = reinterpret_cast<int32_t*>(a.hid + (s->n_max > 0 ? s->n_max : 1) * kHid);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.pair_mask = pair_mask;
-  const int64_t tiles = cdiv(s->n_max, kSampPerWave);
-  const unsigned grid = grid_for(tiles, 4, 256);
-  set_lds_attr();
-  hipLaunchKernelGGL(k_aggregate, dim3(grid), dim3(kAggBlock), kAggLdsBytes, as_stream(stream), a);
-  PNR_LAUNCH_CHECK();
-  return PNR_OK;
+  return launch(a, as_stream(stream));
 }

@@ -166,8 +166,10 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
             e2 = mark()
+            scratch = L.aggregate_scratch(max(Sv, 1), dev)
             L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
-                                              L.ptr(feat), None, None, L.stream_ptr(dev)),
+                                              L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
+                                              L.stream_ptr(dev)),
                     "pnr_aggregate_fwd")
             e3 = mark()
             cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))

@@ -48,7 +48,7 @@ def test_ctypes_binding_covers_header_and_loads(built):
     assert b"null" in lib.pnr_last_error()
     assert lib.pnr_grid_build(None, None, 0, None, None) == L.PNR_EINVAL
     assert lib.pnr_query(None, None, None, None, None) == L.PNR_EINVAL
-    assert lib.pnr_aggregate_fwd(None, None, None, None, None, None, None) == L.PNR_EINVAL
+    assert lib.pnr_aggregate_fwd(None, None, None, None, None, None, None, 0, None) == L.PNR_EINVAL
     assert lib.pnr_destroy(None) == L.PNR_OK
 
 

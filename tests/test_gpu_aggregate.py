@@ -98,8 +98,10 @@ def test_fused_gather_aggregate_vs_oracle(cuda):
     pts, _p = np_.tables(cp, cr)
     s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                   bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(), bufs.fill_rs.data_ptr(), SR, K)
+    scratch = L.aggregate_scratch(Sv, cuda)
     L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), L.ptr(feat),
-                                      None, None, L.stream_ptr()), "aggregate")
+                                      None, None, L.ptr(scratch), scratch.numel() * 4, L.stream_ptr()),
+            "aggregate")
     # oracle: reference query -> gather -> aggregate, then pick the valid samples in the same order
     q = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
     gth = O.gather(oracle_points(sc), q["sample_pidx"], sc["campos"], sc["camrot"])

@@ -1,0 +1,45 @@
+"""Dev tool: time the stages of one 800x800 frame render (2M points) with the
+libpnr.so named by $PNR_LIB; prints one JSON line."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=2_000_000)
+    ap.add_argument("--hw", type=int, default=800)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import bench
+    dev = torch.device("cuda:0")
+    ns = argparse.Namespace(points=a.points)
+    opt, pts, feats, agg, model = bench.build_scene(ns, dev)
+    campos, camrot, rd = bench.cameras(1, a.hw, a.hw)[0]
+    cp, cr, rd = [torch.from_numpy(x).to(dev) for x in (campos, camrot, rd)]
+    bg = torch.rand(128, device=dev)
+    model.render_rays(cp, cr, rd, 2.0, 6.0, bg)
+    per = {}
+    for _ in range(a.reps):
+        ev = []
+        out = model.render_rays(cp, cr, rd, 2.0, 6.0, bg, events=ev)
+        torch.cuda.synchronize()
+        for n, s, e in ev:
+            per.setdefault(n, []).append(s.elapsed_time(e))
+    c = model.last_counts
+    flops = c["n_pairs"] * 542720 + c["S_valid"] * 137216
+    agg_ms = float(np.median(per["aggregate"]))
+    print(json.dumps({"lib": os.environ.get("PNR_LIB", "default"),
+                      "stages_ms": {k: round(float(np.median(v)), 3) for k, v in per.items()},
+                      "agg_tflops": round(flops / agg_ms / 1e9, 2), "counts": c,
+                      "checksum": float(out[0].double().sum().item())}))
+
+
+if __name__ == "__main__":
+    main()
