@@ -177,7 +177,9 @@ int pnr_query_compact(const pnr_rays* rays, const pnr_query_params* q,
  * nn.Linear [out,in] weight W:  W_f[t][T][lane] = W[32T + (lane&31)][2t + (lane>>5)]
  * for t < ceil(in/2) + 4 (4 trailing zero k-steps: prefetch padding), T < out/32. */
 typedef struct {
-  const float* w1f; const float* b1;   /* block1.0  [256,284] fragment-packed */
+  const float* w1af;                   /* block1.0 columns 0..223 (embedding + its PE) + bias:
+                                          evaluated once per point (pnr_aggregate_fwd step 1) */
+  const float* w1bf;                   /* block1.0 columns 224..283 (PE of the 6-d distance)  */
   const float* w2f; const float* b2;   /* block1.2  [256,256]                  */
   const float* w3f; const float* b3;   /* block3.0  [256,263]                  */
   const float* w4f; const float* b4;   /* block3.2  [256,256]                  */
@@ -191,6 +193,7 @@ typedef struct {
 } pnr_mlp;
 
 typedef struct {
+  int64_t n;            /* N: rows of every point table                             */
   const float* xyz;     /* [N,3] world xyz (index space of pidx)                   */
   const float* pers;    /* [N,3] perspective xyz, or NULL = w2pers(xyz) on the fly */
   const float* emb;     /* [N,32]                                                   */
@@ -220,8 +223,11 @@ typedef struct {
  * out_feat[v, 0] = alpha, out_feat[v, 1..128] = colour features (rows of
  * samples without neighbours are left untouched).  Optional (may be NULL):
  * out_weight[row,K] normalised weights, out_conf[row,K] clamped confidence.
- * scratch: 16-B aligned device buffer of pnr_aggregate_scratch_bytes(n_max). */
-int pnr_aggregate_scratch_bytes(int64_t n_max, size_t* out);
+ * scratch: 16-B aligned device buffer of pnr_aggregate_scratch_bytes(n_max, N).
+ * Block1.0 is split exactly: W1[:, :224].[emb, PE(emb)] + b1 depends only on
+ * the point, so it is computed once per point (N x 256) and gathered per
+ * pair; only the 60 distance-PE columns run per (sample, neighbour) pair. */
+int pnr_aggregate_scratch_bytes(int64_t n_max, int64_t n_points, size_t* out);
 int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                       float* out_feat, float* out_weight, float* out_conf, void* scratch,
                       size_t scratch_bytes, void* stream);

@@ -56,7 +56,7 @@ class QueryBufs(ctypes.Structure):
 
 
 class Mlp(ctypes.Structure):
-    _fields_ = [("w1f", c_void_p), ("b1", c_void_p), ("w2f", c_void_p), ("b2", c_void_p),
+    _fields_ = [("w1af", c_void_p), ("w1bf", c_void_p), ("w2f", c_void_p), ("b2", c_void_p),
                 ("w3f", c_void_p), ("b3", c_void_p), ("w4f", c_void_p), ("b4", c_void_p),
                 ("wa", c_void_p), ("ba", c_void_p), ("wc1f", c_void_p), ("bc1", c_void_p),
                 ("wc2f", c_void_p), ("bc2", c_void_p), ("wc3f", c_void_p), ("bc3", c_void_p),
@@ -64,7 +64,7 @@ class Mlp(ctypes.Structure):
 
 
 class Points(ctypes.Structure):
-    _fields_ = [("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
+    _fields_ = [("n", c_int64), ("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
                 ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p)]
 
 
@@ -94,7 +94,7 @@ SIGNATURES = {
     "pnr_query": (c_int, [c_void_p, P(Rays), P(QueryParams), P(QueryBufs), c_void_p]),
     "pnr_query_compact": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), c_int64, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
-    "pnr_aggregate_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
+    "pnr_aggregate_scratch_bytes": (c_int, [c_int64, c_int64, P(c_size_t)]),
     "pnr_aggregate_fwd": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
@@ -147,10 +147,12 @@ def ptr(t: torch.Tensor | None):
     return None if t is None else c_void_p(t.data_ptr())
 
 
-def aggregate_scratch(n_max: int, device) -> torch.Tensor:
-    """Device scratch for pnr_aggregate_fwd(_masked) (K-summed features + masks)."""
+def aggregate_scratch(n_max: int, n_points: int, device) -> torch.Tensor:
+    """Device scratch for pnr_aggregate_fwd(_masked): per-point block1 partial
+    products, K-summed features, masks."""
     nb = c_size_t(0)
-    check(lib().pnr_aggregate_scratch_bytes(int(n_max), ctypes.byref(nb)), "pnr_aggregate_scratch_bytes")
+    check(lib().pnr_aggregate_scratch_bytes(int(n_max), int(n_points), ctypes.byref(nb)),
+          "pnr_aggregate_scratch_bytes")
     return torch.empty((int(nb.value) + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 

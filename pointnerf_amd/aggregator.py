@@ -126,7 +126,8 @@ class PointAggregator(nn.Module):
         with torch.no_grad():
             b1, b3 = self.block1, self.block3
             t = dict(
-                w1f=frag_pack(b1[0].weight, b1[0].bias), b1=b1[0].bias.float().contiguous(),
+                w1af=frag_pack(b1[0].weight[:, :224], b1[0].bias),
+                w1bf=frag_pack(b1[0].weight[:, 224:]),
                 w2f=frag_pack(b1[2].weight, b1[2].bias), b2=b1[2].bias.float().contiguous(),
                 w3f=frag_pack(b3[0].weight, b3[0].bias), b3=b3[0].bias.float().contiguous(),
                 w4f=frag_pack(b3[2].weight, b3[2].bias), b4=b3[2].bias.float().contiguous(),
@@ -184,12 +185,12 @@ class PointAggregator(nn.Module):
                     dir=flat(sampled_dir, 3), conf=flat(sampled_conf, 1),
                     sw=flat(sample_loc_w, 3), sp=flat(sample_loc, 3), sd=flat(sample_ray_dirs, 3),
                     mask=sample_pnt_mask.reshape(-1).contiguous().view(torch.uint8))
-        pts = L.Points(keep["xyz"].data_ptr(), keep["pers"].data_ptr(), keep["emb"].data_ptr(),
+        pts = L.Points(rows * K, keep["xyz"].data_ptr(), keep["pers"].data_ptr(), keep["emb"].data_ptr(),
                        L.ptr(keep["color"]), L.ptr(keep["dir"]), L.ptr(keep["conf"]), None, None)
         s = L.Samples(None, None, rows, None, keep["sw"].data_ptr(), keep["sp"].data_ptr(),
                       keep["sd"].data_ptr(), None, 1, K)
         mlp, _ = self.packed()
-        scratch = L.aggregate_scratch(rows, dev)
+        scratch = L.aggregate_scratch(rows, rows * K, dev)
         L.check(L.lib().pnr_aggregate_fwd_masked(L.ctypes.byref(pts), L.ctypes.byref(s),
                                                  L.ctypes.byref(mlp), L.ptr(keep["mask"]), L.ptr(out),
                                                  L.ptr(weight), L.ptr(conf), L.ptr(scratch),

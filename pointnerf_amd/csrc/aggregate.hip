@@ -17,7 +17,7 @@
 // (exact fp32 fmaf chains; gfx950 has no TF32).  The pair is the MFMA column
 // (lane & 31): 8 accumulator tiles (128 AGPRs) hold a layer's output with the
 // neuron on the register and the pair on the lane.  Each layer's input X^T
-// lives in a per-wave k-major LDS slice [k][33] (37 KB; 4 waves = 148 KB of
+// lives in a per-wave k-major LDS slice [k][33] (38 KB; 4 waves = 153 KB of
 // the CU's 160 KB), one conflict-free ds_read_b32 per k-step shared by 8
 // MFMAs; activations are written back in natural neuron order, so every
 // weight matrix uses one "fragment" layout W_f[t][T][lane] =
@@ -44,7 +44,7 @@ constexpr int kEmb = 32;
 constexpr int kC = 128;
 constexpr int kCin = 280;          // 256 + 24 view PE
 constexpr int kPitch = 33;         // LDS row pitch (floats) of X^T[k][32 + 1]
-constexpr int kXRows = 288;        // >= 284 layer-1 inputs
+constexpr int kXRows = 296;        // >= 286 layer-1 inputs + bias, + x prefetch overrun
 constexpr int kWaveLds = kXRows * kPitch;  // floats per wave slice
 constexpr size_t kAggLdsBytes = (size_t)4 * kWaveLds * sizeof(float);
 constexpr int kWtRow = 286;        // X^T row holding the per-pair blend weight after layer 4
@@ -55,6 +55,7 @@ struct AggArgs {
   pnr_points pts;
   pnr_samples s;
   pnr_mlp w;
+  float* p1;                  // [N, 256] per-point block1.0 partial (k_point_pre -> k_pairs)
   float* hid;                 // [n_max, 256] K-summed features (k_pairs -> k_color)
   int32_t* vmask;             // [n_max] sample has >= 1 valid neighbour (k_pairs -> k_color)
   float* out_feat;
@@ -112,24 +113,37 @@ __device__ __forceinline__ void mlp_layer(f32x16 (&acc)[NT], const float* __rest
   load_w<NT>(a1, p, 1);
   load_w<NT>(a2, p, 2);
   load_w<NT>(a3, p, 3);
+  // B operands of the current 4 k-steps; the next 4 are read from LDS one
+  // iteration ahead (rows past the layer's inputs are read but never used)
+  float x0 = xr[0], x1 = xr[2 * kPitch], x2 = xr[4 * kPitch], x3 = xr[6 * kPitch];
   int t = 0;
 #pragma unroll 1
   for (; t + kPD <= nsteps; t += kPD) {
-    float x0 = xr[(2 * t + 0) * kPitch], x1 = xr[(2 * t + 2) * kPitch];
-    float x2 = xr[(2 * t + 4) * kPitch], x3 = xr[(2 * t + 6) * kPitch];
+    const float* xn = xr + 2 * (t + kPD) * kPitch;
+    // sched_barrier(0) pins the software pipeline: hipcc otherwise sinks the
+    // next iteration's LDS reads next to their use (exposed LDS latency)
     mfma_step<NT>(acc, a0, x0);
+    const float y0 = xn[0], y1 = xn[2 * kPitch], y2 = xn[4 * kPitch], y3 = xn[6 * kPitch];
     load_w<NT>(a0, p, t + 4);
+    __builtin_amdgcn_sched_barrier(0);
     mfma_step<NT>(acc, a1, x1);
     load_w<NT>(a1, p, t + 5);
+    __builtin_amdgcn_sched_barrier(0);
     mfma_step<NT>(acc, a2, x2);
     load_w<NT>(a2, p, t + 6);
+    __builtin_amdgcn_sched_barrier(0);
     mfma_step<NT>(acc, a3, x3);
     load_w<NT>(a3, p, t + 7);
+    __builtin_amdgcn_sched_barrier(0);
+    x0 = y0;
+    x1 = y1;
+    x2 = y2;
+    x3 = y3;
   }
   const int rem = nsteps - t;  // 0..3
-  if (rem > 0) mfma_step<NT>(acc, a0, xr[(2 * t + 0) * kPitch]);
-  if (rem > 1) mfma_step<NT>(acc, a1, xr[(2 * t + 2) * kPitch]);
-  if (rem > 2) mfma_step<NT>(acc, a2, xr[(2 * t + 4) * kPitch]);
+  if (rem > 0) mfma_step<NT>(acc, a0, x0);
+  if (rem > 1) mfma_step<NT>(acc, a1, x1);
+  if (rem > 2) mfma_step<NT>(acc, a2, x2);
 }
 
 // Activated accumulator -> X^T rows in natural neuron order.
@@ -176,6 +190,63 @@ __device__ __forceinline__ int64_t eff_n(const pnr_samples& s) {
     n = nd < n ? nd : n;
   }
   return n;
+}
+
+// Per-point half of block1.0 (exact split of the 284-input Linear): the
+// embedding and its 3-band PE depend only on the point, so
+// P1[p] = W1[:, :224] . [emb_p, PE_3(emb_p)] + b1 is evaluated once per point
+// and gathered per pair instead of being recomputed for every (sample,
+// neighbour) pair that references the point (~22x reuse at 2 M points).
+__global__ void __launch_bounds__(kAggBlock, 1) k_point_pre(AggArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* X = lds_dyn + wid * kWaveLds;
+  const int m = lane & 31, h = lane >> 5;
+  const int64_t np = A.pts.n;
+  const int64_t ntiles = cdiv(np, 32);
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t pt = tile * 32 + m;
+    const bool act = pt < np;
+    // lane half h owns embedding channels [16h, 16h+16): the channel itself (row c)
+    // and its 3-band PE (rows 32 + 2(3c+f) + {0: sin, 1: cos}); angle doubling
+    // from one sincos: sin 2x = 2 sin x cos x, cos 2x = (c - s)(c + s).
+    const float* e = A.pts.emb + (act ? pt : 0) * kEmb + 16 * h;
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+      float4 e4 = act ? reinterpret_cast<const float4*>(e)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = 16 * h + 4 * q + u;
+        X[c * kPitch + m] = ev[u];
+        float s0, c0;
+        sincosf(ev[u], &s0, &c0);
+        const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
+        const float s2 = 2.f * s1 * c1, c2 = (c1 - s1) * (c1 + s1);
+        const int r0 = kEmb + 6 * c;
+        X[(r0 + 0) * kPitch + m] = s0;
+        X[(r0 + 1) * kPitch + m] = c0;
+        X[(r0 + 2) * kPitch + m] = s1;
+        X[(r0 + 3) * kPitch + m] = c1;
+        X[(r0 + 4) * kPitch + m] = s2;
+        X[(r0 + 5) * kPitch + m] = c2;
+      }
+    }
+    bias_rows(X, kEmb * 7, lane);   // row 224 = 1 (bias column), 225 = 0
+    wave_sync();
+    f32x16 acc[8];
+    zero_acc<8>(acc);
+    mlp_layer<8>(acc, A.w.w1af, X, 113, lane);
+    if (act) {
+      float4* o = reinterpret_cast<float4*>(A.p1 + pt * kHid);
+#pragma unroll
+      for (int T = 0; T < 8; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[8 * T + 2 * q + h] = make_float4(acc[T][4 * q], acc[T][4 * q + 1], acc[T][4 * q + 2], acc[T][4 * q + 3]);
+    }
+    wave_sync();
+  }
 }
 
 __global__ void __launch_bounds__(kAggBlock, 1) k_pairs(AggArgs A) {
@@ -274,55 +345,42 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_pairs(AggArgs A) {
     mat3(Rw, pdir, drot);
 
     // ---------------------------------------------------- layer-1 inputs -> X^T
-    // lane half h owns embedding channels [16h, 16h+16): the channel itself
-    // (row c) and its 3-band PE (rows 32 + 2(3c+f) + {0: sin, 1: cos}); angle
-    // doubling from one sincos: sin 2x = 2 sin x cos x, cos 2x = (c - s)(c + s).
-    {
-      const float* e = A.pts.emb + (valid ? prow : 0) * kEmb + 16 * h;
-#pragma unroll 1
-      for (int q = 0; q < 4; ++q) {
-        float4 e4 = valid ? reinterpret_cast<const float4*>(e)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+    // 5-band PE of the 6-d rotated distance: rows 2(5c+f) + {sin, cos} (block1.0
+    // columns 224..283); half h owns channels 3h..3h+2
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int c = 16 * h + 4 * q + u;
-          X[c * kPitch + m] = ev[u];
-          float s0, c0;
-          sincosf(ev[u], &s0, &c0);
-          const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
-          const float s2 = 2.f * s1 * c1, c2 = (c1 - s1) * (c1 + s1);
-          const int r0 = kEmb + 6 * c;
-          X[(r0 + 0) * kPitch + m] = s0;
-          X[(r0 + 1) * kPitch + m] = c0;
-          X[(r0 + 2) * kPitch + m] = s1;
-          X[(r0 + 3) * kPitch + m] = c1;
-          X[(r0 + 4) * kPitch + m] = s2;
-          X[(r0 + 5) * kPitch + m] = c2;
-        }
-      }
-      // 5-band PE of the 6-d rotated distance: rows 224 + 2(5c+f) + {sin, cos};
-      // half h owns channels 3h..3h+2 (direct sincos per band: |arg| grows to 16x)
-#pragma unroll
-      for (int cc = 0; cc < 3; ++cc) {
-        const int c = 3 * h + cc;
-        const float dc = h ? dr6[3 + cc] : dr6[cc];
+    for (int cc = 0; cc < 3; ++cc) {
+      const int c = 3 * h + cc;
+      const float dc = h ? dr6[3 + cc] : dr6[cc];
 #pragma unroll 1
-        for (int f = 0; f < 5; ++f) {
-          float s, co;
-          sincosf(dc * (float)(1 << f), &s, &co);
-          const int r = kEmb + 6 * kEmb + 2 * (5 * c + f);
-          X[r * kPitch + m] = s;
-          X[(r + 1) * kPitch + m] = co;
-        }
+      for (int f = 0; f < 5; ++f) {
+        float s, co;
+        sincosf(dc * (float)(1 << f), &s, &co);
+        const int r = 2 * (5 * c + f);
+        X[r * kPitch + m] = s;
+        X[(r + 1) * kPitch + m] = co;
       }
-      bias_rows(X, 284, lane);
     }
     wave_sync();
 
     f32x16 acc[8];
     // ------------------------------------------------------------ block1: 284 -> 256 -> 256
-    zero_acc<8>(acc);
-    mlp_layer<8>(acc, A.w.w1f, X, 143, lane);       // 284 inputs + bias column
+    // accumulator starts at the gathered per-point partial P1[p] (bias included)
+    if (valid) {
+      const float4* pr = reinterpret_cast<const float4*>(A.p1 + prow * kHid);
+#pragma unroll
+      for (int T = 0; T < 8; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = pr[8 * T + 2 * q + h];
+          acc[T][4 * q] = v4.x;
+          acc[T][4 * q + 1] = v4.y;
+          acc[T][4 * q + 2] = v4.z;
+          acc[T][4 * q + 3] = v4.w;
+        }
+    } else {
+      zero_acc<8>(acc);
+    }
+    mlp_layer<8>(acc, A.w.w1bf, X, 30, lane);       // + W1[:, 224:284] . PE_5(dist)
     wave_sync();
     store_act<8>(acc, X, neg, lane);
     bias_rows(X, 256, lane);
@@ -473,10 +531,15 @@ int launch(const AggArgs& a, hipStream_t st) {
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     attr = true;
   }
+  hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.n, 32), 4, 256)), dim3(kAggBlock), kAggLdsBytes,
+                     st, a);
+  PNR_LAUNCH_CHECK();
   const int64_t tiles = cdiv(a.s.n_max, kSampPerWave);
   hipLaunchKernelGGL(k_pairs, dim3(grid_for(tiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
   PNR_LAUNCH_CHECK();
@@ -486,6 +549,19 @@ int launch(const AggArgs& a, hipStream_t st) {
   return PNR_OK;
 }
 
+static size_t scratch_need(int64_t n_max, int64_t n_points) {
+  const int64_t nm = n_max > 0 ? n_max : 1;
+  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
+         sizeof(float);
+}
+
+static void carve(AggArgs& a, void* scratch, int64_t n_max) {
+  const int64_t nm = n_max > 0 ? n_max : 1;
+  a.hid = static_cast<float*>(scratch);
+  a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
+  a.p1 = reinterpret_cast<float*>(a.vmask) + cdiv(nm, 4) * 4;
+}
+
 int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, float* out_feat,
                  float* scratch, size_t scratch_bytes) {
   PNR_CHECK_ARG(pts && s && w && out_feat, "aggregate: null pointer");
@@ -493,14 +569,15 @@ int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, 
   PNR_CHECK_ARG(s->sample_w && s->sample_p && s->dirs, "aggregate: sample arrays required");
   PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate: K=%d unsupported (1..8)", s->K);
   PNR_CHECK_ARG(s->dir_div >= 1, "aggregate: dir_div must be >= 1");
-  PNR_CHECK_ARG(w->w1f && w->b1 && w->w2f && w->b2 && w->w3f && w->b3 && w->w4f && w->b4 && w->wa &&
+  PNR_CHECK_ARG(w->w1af && w->w1bf && w->w2f && w->b2 && w->w3f && w->b3 && w->w4f && w->b4 && w->wa &&
                     w->ba && w->wc1f && w->bc1 && w->wc2f && w->bc2 && w->wc3f && w->bc3,
                 "aggregate: null weight");
   PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0, "aggregate: emb must be 16-B aligned");
   PNR_CHECK_ARG(scratch && ((uintptr_t)scratch & 15) == 0, "aggregate: 16-B aligned scratch required");
-  PNR_CHECK_ARG(scratch_bytes >= (size_t)(s->n_max > 0 ? s->n_max : 0) * (kHid + 1) * sizeof(float),
-                "aggregate: scratch too small (%zu bytes for %lld samples)", scratch_bytes,
-                (long long)s->n_max);
+  PNR_CHECK_ARG(pts->n > 0, "aggregate: empty point table");
+  PNR_CHECK_ARG(scratch_bytes >= scratch_need(s->n_max, pts->n),
+                "aggregate: scratch too small (%zu bytes for %lld samples, %lld points)", scratch_bytes,
+                (long long)s->n_max, (long long)pts->n);
   return PNR_OK;
 }
 
@@ -508,9 +585,9 @@ int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, 
 
 using namespace pnr;
 
-extern "C" int pnr_aggregate_scratch_bytes(int64_t n_max, size_t* out) {
-  PNR_CHECK_ARG(out && n_max >= 0, "aggregate_scratch_bytes: bad args");
-  *out = (size_t)(n_max > 0 ? n_max : 1) * (kHid + 1) * sizeof(float);
+extern "C" int pnr_aggregate_scratch_bytes(int64_t n_max, int64_t n_points, size_t* out) {
+  PNR_CHECK_ARG(out && n_max >= 0 && n_points >= 0, "aggregate_scratch_bytes: bad args");
+  *out = scratch_need(n_max, n_points);
   return PNR_OK;
 }
 
@@ -525,8 +602,7 @@ extern "C" int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, co
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  a.hid = static_cast<float*>(scratch);
-  a.vmask = reinterpret_cast<int32_t*>(a.hid + (s->n_max > 0 ? s->n_max : 1) * kHid);
+  carve(a, scratch, s->n_max);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
@@ -548,8 +624,7 @@ extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  a.hid = static_cast<float*>(scratch);
-  a.vmask = reinterpret_cast<int32_t*>(a.hid + (s->n_max > 0 ? s->n_max : 1) * kHid);
+  carve(a, scratch, s->n_max);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;

@@ -59,7 +59,7 @@ class NeuralPoints(nn.Module):
                 None if self.points_color is None else self.points_color.detach().reshape(-1, 3).contiguous(),
                 None if self.points_dir is None else self.points_dir.detach().reshape(-1, 3).contiguous(),
                 None if self.points_conf is None else self.points_conf.detach().reshape(-1).contiguous())
-        p = L.Points(keep[0].data_ptr(), None, keep[1].data_ptr(), L.ptr(keep[2]), L.ptr(keep[3]),
+        p = L.Points(keep[0].shape[0], keep[0].data_ptr(), None, keep[1].data_ptr(), L.ptr(keep[2]), L.ptr(keep[3]),
                      L.ptr(keep[4]), L.ptr(campos), L.ptr(camrot))
         return p, keep
 
@@ -166,7 +166,7 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
             e2 = mark()
-            scratch = L.aggregate_scratch(max(Sv, 1), dev)
+            scratch = L.aggregate_scratch(max(Sv, 1), pts.n, dev)
             L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                               L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
                                               L.stream_ptr(dev)),

@@ -98,7 +98,7 @@ def test_fused_gather_aggregate_vs_oracle(cuda):
     pts, _p = np_.tables(cp, cr)
     s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                   bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(), bufs.fill_rs.data_ptr(), SR, K)
-    scratch = L.aggregate_scratch(Sv, cuda)
+    scratch = L.aggregate_scratch(Sv, pts.n, cuda)
     L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), L.ptr(feat),
                                       None, None, L.ptr(scratch), scratch.numel() * 4, L.stream_ptr()),
             "aggregate")
