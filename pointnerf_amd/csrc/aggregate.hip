@@ -32,6 +32,10 @@
 // runs on full-width MFMA instead of 4-sample VALU loops.
 #include "pnr_common.h"
 
+#ifndef PNR_ABLATE
+#define PNR_ABLATE 0  // dev-only timing ablations (tools/build_ablations.sh)
+#endif
+
 namespace pnr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -88,10 +92,12 @@ __device__ __forceinline__ void bias_rows(float* X, int kin, int lane) {
   else if (h == 0) X[kin * kPitch + m] = 1.f;
 }
 
-template <int NT>
+// NT tiles of this wave out of NTOT tiles per k-step in the packed layout
+// (p already points at this wave's first tile).
+template <int NT, int NTOT = NT>
 __device__ __forceinline__ void load_w(float (&a)[NT], const float* __restrict__ p, int t) {
 #pragma unroll
-  for (int T = 0; T < NT; ++T) a[T] = p[(t * NT + T) * 64];
+  for (int T = 0; T < NT; ++T) a[T] = p[(((PNR_ABLATE & 8) ? (t & 3) : t) * NTOT + T) * 64];
 }
 
 template <int NT>
@@ -102,17 +108,17 @@ __device__ __forceinline__ void mfma_step(f32x16 (&acc)[NT], const float (&a)[NT
 
 // Y^T += W . X^T over nsteps k-steps (2 k-values each); X^T from the wave's
 // LDS slice, W in fragment layout, weight loads issued kPD steps ahead.
-template <int NT>
+template <int NT, int NTOT = NT>
 __device__ __forceinline__ void mlp_layer(f32x16 (&acc)[NT], const float* __restrict__ wf,
                                           const float* X, int nsteps, int lane) {
   const int m = lane & 31, h = lane >> 5;
   const float* p = wf + lane;
   const float* xr = X + h * kPitch + m;
   float a0[NT], a1[NT], a2[NT], a3[NT];
-  load_w<NT>(a0, p, 0);
-  load_w<NT>(a1, p, 1);
-  load_w<NT>(a2, p, 2);
-  load_w<NT>(a3, p, 3);
+  load_w<NT, NTOT>(a0, p, 0);
+  load_w<NT, NTOT>(a1, p, 1);
+  load_w<NT, NTOT>(a2, p, 2);
+  load_w<NT, NTOT>(a3, p, 3);
   // B operands of the current 4 k-steps; the next 4 are read from LDS one
   // iteration ahead (rows past the layer's inputs are read but never used)
   float x0 = xr[0], x1 = xr[2 * kPitch], x2 = xr[4 * kPitch], x3 = xr[6 * kPitch];
@@ -124,16 +130,16 @@ __device__ __forceinline__ void mlp_layer(f32x16 (&acc)[NT], const float* __rest
     // next iteration's LDS reads next to their use (exposed LDS latency)
     mfma_step<NT>(acc, a0, x0);
     const float y0 = xn[0], y1 = xn[2 * kPitch], y2 = xn[4 * kPitch], y3 = xn[6 * kPitch];
-    load_w<NT>(a0, p, t + 4);
+    load_w<NT, NTOT>(a0, p, t + 4);
     __builtin_amdgcn_sched_barrier(0);
     mfma_step<NT>(acc, a1, x1);
-    load_w<NT>(a1, p, t + 5);
+    load_w<NT, NTOT>(a1, p, t + 5);
     __builtin_amdgcn_sched_barrier(0);
     mfma_step<NT>(acc, a2, x2);
-    load_w<NT>(a2, p, t + 6);
+    load_w<NT, NTOT>(a2, p, t + 6);
     __builtin_amdgcn_sched_barrier(0);
     mfma_step<NT>(acc, a3, x3);
-    load_w<NT>(a3, p, t + 7);
+    load_w<NT, NTOT>(a3, p, t + 7);
     __builtin_amdgcn_sched_barrier(0);
     x0 = y0;
     x1 = y1;
@@ -148,12 +154,12 @@ __device__ __forceinline__ void mlp_layer(f32x16 (&acc)[NT], const float* __rest
 
 // Activated accumulator -> X^T rows in natural neuron order.
 template <int NT>
-__device__ __forceinline__ void store_act(const f32x16 (&acc)[NT], float* X, float s, int lane) {
+__device__ __forceinline__ void store_act(const f32x16 (&acc)[NT], float* X, float s, int lane, int T0 = 0) {
   const int m = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int T = 0; T < NT; ++T)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) X[(32 * T + acc_row(r, h)) * kPitch + m] = lrelu(acc[T][r], s);
+    for (int r = 0; r < 16; ++r) X[(32 * (T0 + T) + acc_row(r, h)) * kPitch + m] = lrelu(acc[T][r], s);
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -249,207 +255,6 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_point_pre(AggArgs A) {
   }
 }
 
-__global__ void __launch_bounds__(kAggBlock, 1) k_pairs(AggArgs A) {
-  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* X = lds_dyn + wid * kWaveLds;          // [kXRows][kPitch] layer input X^T
-  const int m = lane & 31, h = lane >> 5, j = m >> 3, k = m & 7;
-  const int K = A.s.K;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, kSampPerWave);
-  const float neg = A.w.neg_slope;
-  float Rw[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
-  float cam_c[3] = {0.f, 0.f, 0.f}, cam_R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
-  if (!A.pts.pers) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) cam_c[i] = A.pts.campos[i];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) cam_R[i] = A.pts.camrot[i];
-  }
-
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    // ------------------------------------------------------------ gather (neural_points.py:788-799)
-    const int64_t v = tile * kSampPerWave + j;
-    const bool active = v < n;
-    const int64_t row = active ? sample_row(A.s, v) : 0;
-    int64_t prow = -1;  // point row
-    bool valid = false;
-    if (active && k < K) {
-      if (A.s.pidx) {
-        const int pid = A.s.pidx[row * K + k];
-        valid = pid >= 0;
-        prow = valid ? pid : 0;  // torch.clamp(sample_pidx, min=0)
-      } else {
-        prow = row * K + k;
-        valid = A.pair_mask[prow] != 0;
-      }
-    }
-    float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
-    if (active) {
-      const int64_t drow = dir_row(A.s, row);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        sw[a] = A.s.sample_w[row * 3 + a];
-        sp[a] = A.s.sample_p[row * 3 + a];
-        vd[a] = A.s.dirs[drow * 3 + a];
-      }
-    }
-    float pw[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, col[3] = {0.f, 0.f, 0.f},
-          pdir[3] = {0.f, 0.f, 0.f};
-    float cf = 1.f;
-    if (valid) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        pw[a] = A.pts.xyz[prow * 3 + a];
-        col[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
-        pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
-      }
-      if (A.pts.pers) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
-      } else {
-        world_to_pers(pw, cam_c, cam_R, pp);
-      }
-    }
-    if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
-    // dists, agg_dist_pers == 20 (point_aggregators.py:775-783)
-    float d6[6];
-    d6[0] = pw[0] - sw[0];
-    d6[1] = pw[1] - sw[1];
-    d6[2] = pw[2] - sw[2];
-    d6[3] = pp[0] * pp[2] - sp[0] * sp[2];
-    d6[4] = pp[1] * pp[2] - sp[1] * sp[2];
-    d6[5] = pp[2] - sp[2];
-    // linear kernel (point_aggregators.py:421-429) and normalisation (:803-804)
-    const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
-    const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
-    const float wsum = xor8_sum(wl);
-    const float wn = wl / fmaxf(wsum, 1e-8f);
-    const float confc = fminf(fmaxf(cf, 1e-4f), 1.f);
-    const float wt = wn * confc;
-    const bool samp_valid = xor8_sum(valid ? 1.f : 0.f) > 0.f;
-    if (h == 0 && active && k < K) {
-      if (A.out_weight) A.out_weight[row * K + k] = wn;
-      if (A.out_conf) A.out_conf[row * K + k] = confc;
-    }
-    // rotated distance / direction inputs (point_aggregators.py:506, 526, 566-570)
-    float dr6[6];
-    mat3(Rw, d6, dr6);
-    dr6[3] = d6[3];
-    dr6[4] = d6[4];
-    dr6[5] = d6[5];
-    float vrot[3], drot[3];
-    mat3(Rw, vd, vrot);
-    mat3(Rw, pdir, drot);
-
-    // ---------------------------------------------------- layer-1 inputs -> X^T
-    // 5-band PE of the 6-d rotated distance: rows 2(5c+f) + {sin, cos} (block1.0
-    // columns 224..283); half h owns channels 3h..3h+2
-#pragma unroll
-    for (int cc = 0; cc < 3; ++cc) {
-      const int c = 3 * h + cc;
-      const float dc = h ? dr6[3 + cc] : dr6[cc];
-#pragma unroll 1
-      for (int f = 0; f < 5; ++f) {
-        float s, co;
-        sincosf(dc * (float)(1 << f), &s, &co);
-        const int r = 2 * (5 * c + f);
-        X[r * kPitch + m] = s;
-        X[(r + 1) * kPitch + m] = co;
-      }
-    }
-    wave_sync();
-
-    f32x16 acc[8];
-    // ------------------------------------------------------------ block1: 284 -> 256 -> 256
-    // accumulator starts at the gathered per-point partial P1[p] (bias included)
-    if (valid) {
-      const float4* pr = reinterpret_cast<const float4*>(A.p1 + prow * kHid);
-#pragma unroll
-      for (int T = 0; T < 8; ++T)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v4 = pr[8 * T + 2 * q + h];
-          acc[T][4 * q] = v4.x;
-          acc[T][4 * q + 1] = v4.y;
-          acc[T][4 * q + 2] = v4.z;
-          acc[T][4 * q + 3] = v4.w;
-        }
-    } else {
-      zero_acc<8>(acc);
-    }
-    mlp_layer<8>(acc, A.w.w1bf, X, 30, lane);       // + W1[:, 224:284] . PE_5(dist)
-    wave_sync();
-    store_act<8>(acc, X, neg, lane);
-    bias_rows(X, 256, lane);
-    wave_sync();
-    zero_acc<8>(acc);
-    mlp_layer<8>(acc, A.w.w2f, X, 129, lane);
-    wave_sync();
-    store_act<8>(acc, X, neg, lane);
-    // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
-    {
-      const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
-      const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0],
-                           drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) X[(256 + 2 * e + h) * kPitch + m] = h ? ex[2 * e + 1] : ex[2 * e];
-    }
-    wave_sync();
-    // ------------------------------------------------------------ block3: 263 -> 256 -> 256
-    zero_acc<8>(acc);
-    mlp_layer<8>(acc, A.w.w3f, X, 132, lane);
-    wave_sync();
-    store_act<8>(acc, X, neg, lane);
-    bias_rows(X, 256, lane);
-    wave_sync();
-    zero_acc<8>(acc);
-    mlp_layer<8>(acc, A.w.w4f, X, 129, lane);
-    wave_sync();
-    store_act<8>(acc, X, neg, lane);                // h4 -> X^T rows 0..255
-    if (h == 0) X[kWtRow * kPitch + m] = wt;        // per-pair blend weight
-    wave_sync();
-    // ------------------------------------------------------------ alpha branch + K sums
-    // alpha_k = softplus(W_a . h4 + b_a - 1) per pair (both lane halves compute it;
-    // W_a[n] is wave-uniform -> scalar loads)
-    float pa = A.w.ba[0];
-    const float* xc = X + m;
-#pragma unroll 8
-    for (int nn = 0; nn < kHid; ++nn) pa += A.w.wa[nn] * xc[nn * kPitch];
-    const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
-    const float alpha_s = xor8_sum(wt * alpha_k);   // point_aggregators.py:608-614
-    // feature K-sum (point_aggregators.py:622-628): lane owns neurons lane + 64i,
-    // written straight to hid[v] (256-B coalesced rows)
-    float wk[kKN];
-#pragma unroll
-    for (int q = 0; q < kKN; ++q) wk[q] = 0.f;
-#pragma unroll
-    for (int s = 0; s < kSampPerWave; ++s) {
-      const int src = s * 8;
-      const bool act_s = __shfl((int)(active && samp_valid), src) != 0;
-      const float al_s = __shfl(alpha_s, src);
-      const int64_t vo = tile * kSampPerWave + s;   // sample-list index
-      if (vo < n && lane == 0) A.vmask[vo] = act_s;
-      if (!act_s) continue;
-#pragma unroll
-      for (int q = 0; q < kKN; ++q) wk[q] = X[kWtRow * kPitch + s * 8 + q];
-      if (lane == 0) A.out_feat[vo * (kC + 1)] = al_s;
-#pragma unroll
-      for (int i = 0; i < kHid / 64; ++i) {
-        const float* xr = X + (lane + 64 * i) * kPitch + s * 8;
-        float f = 0.f;
-#pragma unroll
-        for (int q = 0; q < kKN; ++q) f += wk[q] * xr[q];
-        A.hid[vo * kHid + lane + 64 * i] = f;
-      }
-    }
-    wave_sync();
-  }
-}
-
-// colour branch (point_aggregators.py:630-641): [f(256), PE_4(R.v)(24)] -> 128 x3.
 __global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -526,11 +331,364 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_pairs: one workgroup (4 waves) owns a tile of 64 pairs = 8 samples x K=8.
+// Wave w computes neuron tiles {2w, 2w+1} for both 32-pair halves of the tile
+// (4 accumulator tiles, 64 VGPRs), so every 256-B weight fragment fetched
+// from L2 feeds two MFMAs and every LDS B-operand read feeds two.  Two
+// workgroups per CU (2 waves per SIMD) overlap one tile's gather / PE / tail
+// with the other's MFMA stream.
+//
+// LDS layout of the tile's layer input X^T (quad rows): neuron / input row n
+// of pair column c lives at (n >> 2) * kQP + 4c + perm(n & 3) with
+// perm = {0, 2, 1, 3}.  Then
+//   * the MFMA B operand of k-steps t, t+1 (rows 2t+h, 2t+2+h for lane half
+//     h) is ONE ds_read_b64 at (t >> 1) * kQP + 4c + 2h (t even), and
+//   * an accumulator quad (rows 8q + 4h + 0..3 of a tile) is ONE
+//     ds_write_b128,
+// both conflict-free; kQP = 260 keeps the tail's row-strided b128 reads
+// conflict-free too.
+constexpr int kTP = 64;                 // pairs per tile
+constexpr int kTS = kTP / kKN;          // samples per tile
+constexpr int kQP = 4 * kTP + 4;        // floats per quad row
+constexpr int kQRows = 68;              // 272 input rows: 264 (layer 3) + x prefetch overrun
+constexpr int kPairsLdsFloats = kQRows * kQP + kTP /*wt*/ + 4 * kTP /*alpha parts*/ + kTS /*flags*/;
+constexpr size_t kPairsLdsBytes = (size_t)kPairsLdsFloats * sizeof(float);
+
+__device__ __forceinline__ constexpr int qperm(int i) { return ((i & 1) << 1) | (i >> 1); }
+__device__ __forceinline__ constexpr int qaddr(int n, int c) { return (n >> 2) * kQP + 4 * c + qperm(n & 3); }
+
+// Y^T += W . X^T for NT neuron tiles x PT 32-pair halves over nsteps k-steps.
+// Weight fragments kPD steps ahead in a register ring; the next 4 steps' B
+// operands read from LDS one iteration ahead (2 x b64 per half).
+template <int NT, int PT>
+__device__ __forceinline__ void mlp_layer_q(f32x16 (&acc)[PT * NT], const float* __restrict__ wf,
+                                            const float* X, int nsteps, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const float* p = wf + lane;
+  const float* xr = X + 4 * c + 2 * h;
+  float a0[NT], a1[NT], a2[NT], a3[NT];
+  load_w<NT, 8>(a0, p, 0);
+  load_w<NT, 8>(a1, p, 1);
+  load_w<NT, 8>(a2, p, 2);
+  load_w<NT, 8>(a3, p, 3);
+  float2 x01[PT], x23[PT];
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    x01[pt] = *reinterpret_cast<const float2*>(xr + 128 * pt);
+    x23[pt] = *reinterpret_cast<const float2*>(xr + 128 * pt + kQP);
+  }
+  auto step = [&](const float (&a)[NT], const float2 (&x)[PT], bool hi) {
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+        acc[pt * NT + T] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[T], hi ? x[pt].y : x[pt].x,
+                                                                acc[pt * NT + T], 0, 0, 0);
+  };
+  int t = 0;
+#pragma unroll 1
+  for (; t + kPD <= nsteps; t += kPD) {
+    const float* xn = xr + ((t + kPD) >> 1) * kQP;
+    float2 y01[PT], y23[PT];
+    step(a0, x01, false);
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+      y01[pt] = *reinterpret_cast<const float2*>(xn + 128 * pt);
+      y23[pt] = *reinterpret_cast<const float2*>(xn + 128 * pt + kQP);
+    }
+    load_w<NT, 8>(a0, p, t + 4);
+    __builtin_amdgcn_sched_barrier(0);
+    step(a1, x01, true);
+    load_w<NT, 8>(a1, p, t + 5);
+    __builtin_amdgcn_sched_barrier(0);
+    step(a2, x23, false);
+    load_w<NT, 8>(a2, p, t + 6);
+    __builtin_amdgcn_sched_barrier(0);
+    step(a3, x23, true);
+    load_w<NT, 8>(a3, p, t + 7);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+      x01[pt] = y01[pt];
+      x23[pt] = y23[pt];
+    }
+  }
+  const int rem = nsteps - t;  // 0..3
+  if (rem > 0) step(a0, x01, false);
+  if (rem > 1) step(a1, x01, true);
+  if (rem > 2) step(a2, x23, false);
+}
+
+// Activated accumulators -> quad rows (one b128 per accumulator quad).
+template <int NT, int PT>
+__device__ __forceinline__ void store_act_q(const f32x16 (&acc)[PT * NT], float* X, float s, int lane,
+                                            int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16& v = acc[pt * NT + T];
+        *reinterpret_cast<float4*>(X + (8 * (T0 + T) + 2 * q + h) * kQP + 4 * (32 * pt + c)) =
+            make_float4(lrelu(v[4 * q], s), lrelu(v[4 * q + 2], s), lrelu(v[4 * q + 1], s),
+                        lrelu(v[4 * q + 3], s));
+      }
+}
+
+// X^T row kin = 1 (bias column of the packed weights), row kin + 1 = 0 when
+// the k-step is shared; one wave, lane = pair column.
+__device__ __forceinline__ void bias_rows_q(float* X, int kin, int lane) {
+  X[qaddr(kin, lane)] = 1.f;
+  if ((kin & 1) == 0) X[qaddr(kin + 1, lane)] = 0.f;
+}
+
+constexpr int kPairWaves = 4;
+constexpr int kNTW = 8 / kPairWaves;   // neuron tiles per wave
+constexpr int kPTW = kTP / 32;         // 32-pair halves per tile
+
+__global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  float* X = lds_dyn;                          // quad rows [kQRows][kQP]
+  float* wtL = X + kQRows * kQP;               // [64] per-pair blend weight w_k * conf_k
+  float* apart = wtL + kTP;                    // [4][64] alpha partial dots
+  int* sflag = reinterpret_cast<int*>(apart + 4 * kTP);  // [8] sample has a valid neighbour
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int j = lane >> 3, k = lane & 7;       // gather layout: lane = pair column
+  const int T0 = wid * kNTW;
+  const int K = A.s.K;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kTS);
+  const float neg = A.w.neg_slope;
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  float cam_c[3] = {0.f, 0.f, 0.f}, cam_R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+  if (!A.pts.pers) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cam_c[i] = A.pts.campos[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cam_R[i] = A.pts.camrot[i];
+  }
+  const float* w1b = A.w.w1bf + T0 * 64;
+  const float* w2 = A.w.w2f + T0 * 64;
+  const float* w3 = A.w.w3f + T0 * 64;
+  const float* w4 = A.w.w4f + T0 * 64;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // ------------------------------------------------------------ gather (neural_points.py:788-799)
+    const int64_t v = tile * kTS + j;
+    const bool active = v < n;
+    const int64_t row = active ? sample_row(A.s, v) : 0;
+    int64_t prow = -1;  // point row
+    bool valid = false;
+    if (active && k < K) {
+      if (A.s.pidx) {
+        const int pid = A.s.pidx[row * K + k];
+        valid = pid >= 0;
+        prow = valid ? pid : 0;  // torch.clamp(sample_pidx, min=0)
+      } else {
+        prow = row * K + k;
+        valid = A.pair_mask[prow] != 0;
+      }
+    }
+    // this wave's neuron tiles of the gathered per-point block1.0 partial P1
+    // (bias included) for the pairs of both halves (MFMA layout: column c)
+    f32x16 acc[kPTW * kNTW];
+#pragma unroll
+    for (int pt = 0; pt < kPTW; ++pt) {
+      const int64_t pr_pt = __shfl(prow, 32 * pt + c);
+      const bool v_pt = __shfl((int)valid, 32 * pt + c) != 0;
+      if (v_pt && !(PNR_ABLATE & 1)) {
+        const float4* pr = reinterpret_cast<const float4*>(A.p1 + pr_pt * kHid);
+#pragma unroll
+        for (int T = 0; T < kNTW; ++T)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v4 = pr[8 * (T0 + T) + 2 * q + h];
+            acc[pt * kNTW + T][4 * q] = v4.x;
+            acc[pt * kNTW + T][4 * q + 1] = v4.y;
+            acc[pt * kNTW + T][4 * q + 2] = v4.z;
+            acc[pt * kNTW + T][4 * q + 3] = v4.w;
+          }
+      } else {
+#pragma unroll
+        for (int T = 0; T < kNTW; ++T) acc[pt * kNTW + T] = (f32x16){0.f};
+      }
+    }
+    float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
+    if (active) {
+      const int64_t drow = dir_row(A.s, row);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        sw[a] = A.s.sample_w[row * 3 + a];
+        sp[a] = A.s.sample_p[row * 3 + a];
+        vd[a] = A.s.dirs[drow * 3 + a];
+      }
+    }
+    float pw[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, col[3] = {0.f, 0.f, 0.f},
+          pdir[3] = {0.f, 0.f, 0.f};
+    float cf = 1.f;
+    if (valid) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        pw[a] = A.pts.xyz[prow * 3 + a];
+        col[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
+        pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
+      }
+      if (A.pts.pers) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
+      } else {
+        world_to_pers(pw, cam_c, cam_R, pp);
+      }
+    }
+    if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
+    // dists, agg_dist_pers == 20 (point_aggregators.py:775-783)
+    float d6[6];
+    d6[0] = pw[0] - sw[0];
+    d6[1] = pw[1] - sw[1];
+    d6[2] = pw[2] - sw[2];
+    d6[3] = pp[0] * pp[2] - sp[0] * sp[2];
+    d6[4] = pp[1] * pp[2] - sp[1] * sp[2];
+    d6[5] = pp[2] - sp[2];
+    // linear kernel (point_aggregators.py:421-429) and normalisation (:803-804)
+    const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
+    const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
+    const float wsum = xor8_sum(wl);
+    const float wn = wl / fmaxf(wsum, 1e-8f);
+    const float confc = fminf(fmaxf(cf, 1e-4f), 1.f);
+    const float wt = wn * confc;
+    const bool samp_valid = xor8_sum(valid ? 1.f : 0.f) > 0.f;
+    // rotated distance / direction inputs (point_aggregators.py:506, 526, 566-570)
+    float dr6[6];
+    mat3(Rw, d6, dr6);
+    dr6[3] = d6[3];
+    dr6[4] = d6[4];
+    dr6[5] = d6[5];
+    float vrot[3], drot[3];
+    mat3(Rw, vd, vrot);
+    mat3(Rw, pdir, drot);
+    if (wid == 0) {
+      if (active && k < K) {
+        if (A.out_weight) A.out_weight[row * K + k] = wn;
+        if (A.out_conf) A.out_conf[row * K + k] = confc;
+      }
+      wtL[lane] = wt;
+      if (k == 0) sflag[j] = active && samp_valid;
+    }
+    // 5-band PE of the 6-d rotated distance -> rows 2e + {0: sin, 1: cos},
+    // e = 5 ch + f (block1.0 columns 224..283); wave w owns e = w (mod 4)
+    if (!(PNR_ABLATE & 2)) {
+#pragma unroll 1
+      for (int e = wid; e < 30; e += kPairWaves) {
+        const int ch = e / 5, f = e - 5 * ch;
+        float dc = dr6[0];
+        dc = ch == 1 ? dr6[1] : dc;
+        dc = ch == 2 ? dr6[2] : dc;
+        dc = ch == 3 ? dr6[3] : dc;
+        dc = ch == 4 ? dr6[4] : dc;
+        dc = ch == 5 ? dr6[5] : dc;
+        float sn, cs;
+        sincosf(dc * (float)(1 << f), &sn, &cs);
+        X[qaddr(2 * e, lane)] = sn;
+        X[qaddr(2 * e + 1, lane)] = cs;
+      }
+    }
+    __syncthreads();
+    // ------------------------------------------------------------ block1: 284 -> 256 -> 256
+    mlp_layer_q<kNTW, kPTW>(acc, w1b, X, 30, lane);   // + W1[:, 224:284] . PE_5(dist)
+    __syncthreads();
+    store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
+    if (wid == 0) bias_rows_q(X, 256, lane);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_q<kNTW, kPTW>(acc, w2, X, 129, lane);
+    __syncthreads();
+    store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
+    // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
+    if (wid == 0) {
+      const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
+      const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0],
+                           drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) X[qaddr(256 + e, lane)] = ex[e];
+    }
+    __syncthreads();
+    // ------------------------------------------------------------ block3: 263 -> 256 -> 256
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_q<kNTW, kPTW>(acc, w3, X, 132, lane);
+    __syncthreads();
+    store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
+    if (wid == 0) bias_rows_q(X, 256, lane);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_q<kNTW, kPTW>(acc, w4, X, 129, lane);
+    __syncthreads();
+    store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);   // h4 -> rows 0..255
+    __syncthreads();
+    if (!(PNR_ABLATE & 4)) {
+      // ---------------------------------------------------------- alpha branch
+      // wave w: partial dot of every pair (lane) over neurons [64w, 64w + 64)
+      {
+        float pa = 0.f;
+#pragma unroll 4
+        for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
+          const float4 x4 = *reinterpret_cast<const float4*>(X + u * kQP + 4 * lane);
+          pa += A.w.wa[4 * u] * x4.x + A.w.wa[4 * u + 2] * x4.y + A.w.wa[4 * u + 1] * x4.z +
+                A.w.wa[4 * u + 3] * x4.w;
+        }
+        apart[wid * kTP + lane] = pa;
+      }
+      __syncthreads();
+      if (wid == 0) {
+        const float pa = apart[lane] + apart[kTP + lane] + apart[2 * kTP + lane] + apart[3 * kTP + lane] +
+                         A.w.ba[0];
+        const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
+        const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
+        const int64_t vo = tile * kTS + j;
+        if (k == 0 && vo < n) {
+          A.vmask[vo] = sflag[j];
+          if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
+        }
+      }
+      // ---------------------------------------------------------- K sums
+      // thread (wave w, lane = quad u): samples 2w, 2w+1, neurons 4u..4u+3
+      // (point_aggregators.py:622-628), one 1-KB coalesced row per sample
+#pragma unroll
+      for (int si = 0; si < kTS / kPairWaves; ++si) {
+        const int sj = si * kPairWaves + wid;
+        const int64_t vo = tile * kTS + sj;
+        if (vo >= n || !sflag[sj]) continue;
+        float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < kKN; ++q) {
+          const float wk = wtL[8 * sj + q];
+          const float4 x4 = *reinterpret_cast<const float4*>(X + lane * kQP + 4 * (8 * sj + q));
+          f.x += wk * x4.x;
+          f.y += wk * x4.y;
+          f.z += wk * x4.z;
+          f.w += wk * x4.w;
+        }
+        reinterpret_cast<float4*>(A.hid + vo * kHid)[lane] = make_float4(f.x, f.z, f.y, f.w);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 int launch(const AggArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsLdsBytes));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color),
@@ -540,8 +698,8 @@ int launch(const AggArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.n, 32), 4, 256)), dim3(kAggBlock), kAggLdsBytes,
                      st, a);
   PNR_LAUNCH_CHECK();
-  const int64_t tiles = cdiv(a.s.n_max, kSampPerWave);
-  hipLaunchKernelGGL(k_pairs, dim3(grid_for(tiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
+  const int64_t tiles = cdiv(a.s.n_max, kTS);
+  hipLaunchKernelGGL(k_pairs, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kPairsLdsBytes, st, a);
   PNR_LAUNCH_CHECK();
   const int64_t ctiles = cdiv(a.s.n_max, 32);
   hipLaunchKernelGGL(k_color, dim3(grid_for(ctiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
