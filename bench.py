@@ -231,7 +231,7 @@ def main():
                        "grid_rebuild_per_frame": not args.no_grid_rebuild,
                        "parallelism": f"dp{world} (16x16 ray tiles, RCCL all_gather of tiles)" if world > 1
                        else "single GPU"},
-            "roofline": {"bound": "mfma", "kernel": "k_aggregate (fused gather+MLP, v_mfma_f32_32x32x2_f32)",
+            "roofline": {"bound": "mfma", "kernel": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
                          "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                          "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},

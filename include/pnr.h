@@ -175,7 +175,7 @@ int pnr_query_compact(const pnr_rays* rays, const pnr_query_params* q,
  * Weights are device fp32 arrays in the MFMA A-operand "fragment" layout
  * produced by pointnerf_amd.aggregator.frag_pack() from the reference
  * nn.Linear [out,in] weight W:  W_f[t][T][lane] = W[32T + (lane&31)][2t + (lane>>5)]
- * for t < ceil(in/2) + 4 (4 trailing zero k-steps: prefetch padding), T < out/32. */
+ * for t < ceil(in/2) + 8 (8 trailing zero k-steps: prefetch padding), T < out/32. */
 typedef struct {
   const float* w1af;                   /* block1.0 columns 0..223 (embedding + its PE) + bias:
                                           evaluated once per point (pnr_aggregate_fwd step 1) */

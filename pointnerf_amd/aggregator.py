@@ -60,7 +60,7 @@ def _init_seq(seq: nn.Sequential):
         _xavier_(mods[-1], 1.0)
 
 
-PREFETCH_PAD = 4   # kPD in aggregate.hip: zero k-steps appended for the weight prefetch
+PREFETCH_PAD = 8   # kPackPad in aggregate.hip: zero k-steps appended for the weight prefetch
 
 
 def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:

@@ -52,8 +52,9 @@ constexpr int kXRows = 296;        // >= 286 layer-1 inputs + bias, + x prefetch
 constexpr int kWaveLds = kXRows * kPitch;  // floats per wave slice
 constexpr size_t kAggLdsBytes = (size_t)4 * kWaveLds * sizeof(float);
 constexpr int kWtRow = 286;        // X^T row holding the per-pair blend weight after layer 4
-constexpr int kPD = 4;             // weight prefetch depth in k-steps (packed weights are
-                                   // padded with kPD zero k-steps so prefetch never overruns)
+constexpr int kPD = 4;             // weight prefetch depth in k-steps of mlp_layer
+constexpr int kPackPad = 8;        // zero k-steps padded onto every packed weight matrix
+                                   // (>= every prefetch depth, so prefetch never overruns)
 
 struct AggArgs {
   pnr_points pts;
@@ -352,73 +353,67 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
 constexpr int kTP = 64;                 // pairs per tile
 constexpr int kTS = kTP / kKN;          // samples per tile
 constexpr int kQP = 4 * kTP + 4;        // floats per quad row
-constexpr int kQRows = 68;              // 272 input rows: 264 (layer 3) + x prefetch overrun
+constexpr int kQD = 4;                  // k_pairs weight prefetch depth (k-steps)
+constexpr int kQRows = (264 + 2 * kQD + 3) / 4;  // layer-3 input rows + x prefetch overrun
 constexpr int kPairsLdsFloats = kQRows * kQP + kTP /*wt*/ + 4 * kTP /*alpha parts*/ + kTS /*flags*/;
+static_assert(kQD <= kPackPad && kPD <= kPackPad, "prefetch deeper than the packed padding");
 constexpr size_t kPairsLdsBytes = (size_t)kPairsLdsFloats * sizeof(float);
 
 __device__ __forceinline__ constexpr int qperm(int i) { return ((i & 1) << 1) | (i >> 1); }
 __device__ __forceinline__ constexpr int qaddr(int n, int c) { return (n >> 2) * kQP + 4 * c + qperm(n & 3); }
 
 // Y^T += W . X^T for NT neuron tiles x PT 32-pair halves over nsteps k-steps.
-// Weight fragments kPD steps ahead in a register ring; the next 4 steps' B
-// operands read from LDS one iteration ahead (2 x b64 per half).
+// Weight fragments kQD steps ahead in a register ring; the next kQD steps' B
+// operands read from LDS one iteration ahead (kQD/2 b64 per half).
 template <int NT, int PT>
 __device__ __forceinline__ void mlp_layer_q(f32x16 (&acc)[PT * NT], const float* __restrict__ wf,
                                             const float* X, int nsteps, int lane) {
+  constexpr int D = kQD;
   const int c = lane & 31, h = lane >> 5;
   const float* p = wf + lane;
   const float* xr = X + 4 * c + 2 * h;
-  float a0[NT], a1[NT], a2[NT], a3[NT];
-  load_w<NT, 8>(a0, p, 0);
-  load_w<NT, 8>(a1, p, 1);
-  load_w<NT, 8>(a2, p, 2);
-  load_w<NT, 8>(a3, p, 3);
-  float2 x01[PT], x23[PT];
+  float a[D][NT];
 #pragma unroll
-  for (int pt = 0; pt < PT; ++pt) {
-    x01[pt] = *reinterpret_cast<const float2*>(xr + 128 * pt);
-    x23[pt] = *reinterpret_cast<const float2*>(xr + 128 * pt + kQP);
-  }
-  auto step = [&](const float (&a)[NT], const float2 (&x)[PT], bool hi) {
+  for (int d = 0; d < D; ++d) load_w<NT, 8>(a[d], p, d);
+  float2 x[D / 2][PT];
+#pragma unroll
+  for (int i = 0; i < D / 2; ++i)
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) x[i][pt] = *reinterpret_cast<const float2*>(xr + 128 * pt + i * kQP);
+  auto step = [&](const float (&w)[NT], const float2 (&xx)[PT], bool hi) {
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
       for (int T = 0; T < NT; ++T)
-        acc[pt * NT + T] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[T], hi ? x[pt].y : x[pt].x,
+        acc[pt * NT + T] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[T], hi ? xx[pt].y : xx[pt].x,
                                                                 acc[pt * NT + T], 0, 0, 0);
   };
   int t = 0;
 #pragma unroll 1
-  for (; t + kPD <= nsteps; t += kPD) {
-    const float* xn = xr + ((t + kPD) >> 1) * kQP;
-    float2 y01[PT], y23[PT];
-    step(a0, x01, false);
+  for (; t + D <= nsteps; t += D) {
+    const float* xn = xr + ((t + D) >> 1) * kQP;
+    float2 y[D / 2][PT];
 #pragma unroll
-    for (int pt = 0; pt < PT; ++pt) {
-      y01[pt] = *reinterpret_cast<const float2*>(xn + 128 * pt);
-      y23[pt] = *reinterpret_cast<const float2*>(xn + 128 * pt + kQP);
-    }
-    load_w<NT, 8>(a0, p, t + 4);
-    __builtin_amdgcn_sched_barrier(0);
-    step(a1, x01, true);
-    load_w<NT, 8>(a1, p, t + 5);
-    __builtin_amdgcn_sched_barrier(0);
-    step(a2, x23, false);
-    load_w<NT, 8>(a2, p, t + 6);
-    __builtin_amdgcn_sched_barrier(0);
-    step(a3, x23, true);
-    load_w<NT, 8>(a3, p, t + 7);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int d = 0; d < D; ++d) {
+      step(a[d], x[d >> 1], d & 1);
+      if (d == 0) {
 #pragma unroll
-    for (int pt = 0; pt < PT; ++pt) {
-      x01[pt] = y01[pt];
-      x23[pt] = y23[pt];
+        for (int i = 0; i < D / 2; ++i)
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt) y[i][pt] = *reinterpret_cast<const float2*>(xn + 128 * pt + i * kQP);
+      }
+      load_w<NT, 8>(a[d], p, t + D + d);
+      __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i)
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) x[i][pt] = y[i][pt];
   }
-  const int rem = nsteps - t;  // 0..3
-  if (rem > 0) step(a0, x01, false);
-  if (rem > 1) step(a1, x01, true);
-  if (rem > 2) step(a2, x23, false);
+  const int rem = nsteps - t;  // 0..D-1
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d)
+    if (rem > d) step(a[d], x[d >> 1], d & 1);
 }
 
 // Activated accumulators -> quad rows (one b128 per accumulator quad).

@@ -9,13 +9,13 @@ def test_frag_pack_roundtrip_and_layout():
     from pointnerf_amd.aggregator import frag_pack, frag_unpack
     W, b = torch.randn(256, 263), torch.randn(256)
     F = frag_pack(W, b)
-    assert F.numel() == (132 + 4) * 8 * 64          # 263 + bias = 132 k-steps, +4 prefetch padding
+    assert F.numel() == (132 + 8) * 8 * 64          # 263 + bias = 132 k-steps, +8 prefetch padding
     assert torch.equal(frag_unpack(F, 264), torch.cat([W, b[:, None]], 1))
     Wc, bc = torch.randn(128, 280), torch.randn(128)
     assert torch.equal(frag_unpack(frag_pack(Wc, bc), 281, 128), torch.cat([Wc, bc[:, None]], 1))
-    assert frag_pack(torch.randn(256, 284), torch.randn(256)).numel() == (143 + 4) * 8 * 64
+    assert frag_pack(torch.randn(256, 284), torch.randn(256)).numel() == (143 + 8) * 8 * 64
     # F[t][T][lane] = W[32T + (lane & 31)][2t + (lane >> 5)]
-    Fv = F.view(136, 8, 64)
+    Fv = F.view(140, 8, 64)
     assert torch.all(Fv[132:] == 0)
     for t, T, lane in [(0, 0, 0), (5, 3, 17), (131, 7, 40), (77, 2, 63)]:
         k = 2 * t + (lane >> 5)

@@ -1,0 +1,71 @@
+"""Dev tool: fold a tools/prof_bench.sh run (gpurun_out/<dir>) into profiles/.
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats),
+profiles/<tag>_bench.json (the bench line) and profiles/<tag>_pmc_aggregate.json:
+per aggregate launch (k_point_pre + k_pairs + k_color, one launch per frame)
+the FETCH_SIZE / WRITE_SIZE bytes with the gfx950 correction of
+MI355X_MICROARCH.md "HBM" (FETCH_SIZE counts 128-B reads at 64 B: x2),
+MFMA busy fraction and effective clock.  bench.py reads hbm_bytes_per_launch.
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+AGG = ("k_point_pre", "k_pairs", "k_color")
+
+
+def short(name):
+    return name.split("(")[0].replace("pnr::", "").replace("void ", "")
+
+
+def per_kernel(path, counters):
+    sums = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        if k in AGG and r["Counter_Name"] in counters:
+            sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    return {k: {c: v / len(disp[k]) for c, v in d.items()} for k, d in sums.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    json.dump(bench, open(os.path.join(prof, f"{tag}_bench.json"), "w"), indent=1)
+    stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv")))}
+    fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), {"FETCH_SIZE"})
+    write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), {"WRITE_SIZE"})
+    mfma = per_kernel(os.path.join(src, "mfma", "run_counter_collection.csv"),
+                      {"SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU_MFMA_MOPS_F32"})
+    out = {"source": "tools/prof_bench.sh -> tools/profile_summary.py", "kernels": {}}
+    tot_bytes, tot_ns = 0.0, 0.0
+    for k in AGG:
+        avg_ns = float(stats[k]["AverageNs"])
+        fb = fetch[k]["FETCH_SIZE"] * 1024 * 2      # KB -> B, gfx950 x2 correction
+        wb = write[k]["WRITE_SIZE"] * 1024
+        m = mfma.get(k, {})
+        gui = m.get("GRBM_GUI_ACTIVE", 0.0) / 8         # summed over 8 XCDs
+        busy = m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / 1024   # per SIMD (256 CUs x 4)
+        out["kernels"][k] = {"calls": int(stats[k]["Calls"]), "avg_ms": avg_ns / 1e6,
+                             "fetch_bytes": fb, "write_bytes": wb,
+                             "mfma_busy_frac": busy / gui if gui else None,
+                             "eff_clock_ghz_profiled": gui / avg_ns if gui else None}
+        tot_bytes += fb + wb
+        tot_ns += avg_ns
+    out["hbm_bytes_per_launch"] = tot_bytes
+    out["avg_launch_ms_rocprof"] = tot_ns / 1e6
+    out["avg_launch_ms_bench_events"] = bench["roofline"]["avg_launch_ms"]
+    json.dump(out, open(os.path.join(prof, f"{tag}_pmc_aggregate.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
