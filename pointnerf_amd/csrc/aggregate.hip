@@ -10,26 +10,21 @@
 //   viewmlp (order 2)                       point_aggregators.py:488-646
 //   positional_encoding                     models/helpers/networks.py:175-190
 //
-// CDNA4 mapping.
-// k_pairs: one wave owns 32 (sample, neighbour) pairs = 4 samples x K=8 and
-// carries them through the four 256-wide layers as
-//   Y^T[256 x 32] = W[256 x Kin] . X^T[Kin x 32]  on v_mfma_f32_32x32x2_f32
-// (exact fp32 fmaf chains; gfx950 has no TF32).  The pair is the MFMA column
-// (lane & 31): 8 accumulator tiles (128 AGPRs) hold a layer's output with the
-// neuron on the register and the pair on the lane.  Each layer's input X^T
-// lives in a per-wave k-major LDS slice [k][33] (38 KB; 4 waves = 153 KB of
-// the CU's 160 KB), one conflict-free ds_read_b32 per k-step shared by 8
-// MFMAs; activations are written back in natural neuron order, so every
-// weight matrix uses one "fragment" layout W_f[t][T][lane] =
-// W[32T + (lane&31)][2t + (lane>>5)] and every A-operand load is a coalesced
-// 256-B wave load from L2, software-pipelined kPD k-steps ahead.  Layer-1
-// inputs (embedding, 3-band PE of the embedding via sincos + angle doubling,
-// 5-band PE of the 6-d distance) are produced straight into the LDS slice by
-// the lane that owns the pair.  The K-sums run as wave shuffles; per valid
-// sample only alpha (-> out_feat[:,0]) and the 256-d feature leave the kernel.
-// k_color: one wave owns 32 samples and runs 280->128->128->128 with the same
-// machinery (4 accumulator tiles), so the colour branch (3 % of the FLOPs) also
-// runs on full-width MFMA instead of 4-sample VALU loops.
+// CDNA4 mapping (three launches):
+// k_point_pre: P1[p] = W1[:, :224] . [emb_p, PE_3(emb_p)] + b1 once per point
+//   (the point-only half of block1.0; 32 points per wave, 8 accumulator tiles).
+// k_pairs: a 4-wave workgroup owns 64 (sample, neighbour) pairs = 8 samples x
+//   K=8 and runs the rest of block1 and block3 as Y^T[256 x 64] = W . X^T on
+//   v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains; gfx950 has no TF32); wave w
+//   owns neuron tiles {2w, 2w+1} for both 32-pair halves, the tile's X^T sits in
+//   a quad-row LDS layout (b64 operand reads, b128 activation stores); gather,
+//   weights, PE, alpha and the K-sums are fused around the GEMMs.
+// k_color: one wave owns 32 valid samples and runs 280->128->128->128 on the
+//   same MFMA machinery (4 accumulator tiles).
+// Every weight matrix uses one A-operand "fragment" layout
+// W_f[t][T][lane] = W[32T + (lane&31)][2t + (lane>>5)] (bias as an extra input
+// column), so every weight load is a coalesced 256-B wave load from L2,
+// software-pipelined a few k-steps ahead.
 #include "pnr_common.h"
 
 #ifndef PNR_ABLATE
