@@ -114,6 +114,37 @@ def cpu_baseline(args, opt, pts, feats, agg, cam, H, W):
                        f"({t_frame:.1f}s/frame)")}
 
 
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def stage_rooflines(args, opt, model, stage, per, launches):
+    """SURVEY 8(d) compulsory-byte formulas for the memory/latency-bound stages,
+    per frame, against HBM peak (informational; the headline roofline is the
+    aggregate's).  query = grid build + march + KNN + compactions (the bench
+    rebuilds the grid every frame)."""
+    n = max(launches, 1)
+    dims = model.neural_points.querier.grid.hp["dims"]
+    cells = int(np.prod(np.asarray(dims, dtype=np.int64)))
+    R = stage["rays"] / n
+    S = stage["filled"] / n
+    V = stage["valid"] / n
+    cand = stage["cand"] / n
+    D, C, SR = int(opt.z_depth_dim), 128, int(opt.SR)
+    grid_b = args.points * 12 + cells * 4 * 2 + int(opt.max_o) * (int(opt.P) + 4) * 4
+    march_b = R * D * 4 + R * 16
+    knn_b = S * 27 * 8 + cand * 16
+    comp_b = V * (C + 1) * 4 + R * (C + 1 + SR) * 4
+    res = {}
+    for name, b in (("query", grid_b + march_b + knn_b), ("composite", comp_b)):
+        ms = float(np.mean(per.get(name, [0.0])))
+        gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        res[name] = {"bytes": int(b), "ms": round(ms, 3), "achieved_GBs": round(gbs, 1),
+                     "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+    res["query"]["parts_bytes"] = {"grid_build": int(grid_b), "march": int(march_b), "knn": int(knn_b)}
+    res["query"]["knn_candidates"] = int(cand)
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,7 +187,7 @@ def main():
         sh, rd = shards[key]
         return ci, rd, sh
 
-    stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0}
+    stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0, "cand": 0, "rays": 0}
 
     def step(s, timed):
         frames = []
@@ -172,6 +203,8 @@ def main():
                 stage["pairs"] += c["n_pairs"]
                 stage["valid"] += c["S_valid"]
                 stage["filled"] += c["S_filled"]
+                stage["cand"] += c["n_cand"]
+                stage["rays"] += rd.shape[0]
                 stage["flops"] += c["n_pairs"] * FLOP_PER_PAIR + c["S_valid"] * FLOP_PER_SAMPLE
                 stage["_ev"] = stage.get("_ev", []) + ev
             if world > 1 and not args.no_gather:
@@ -240,6 +273,7 @@ def main():
                                  "valid_samples": stage["valid"] // max(launches, 1),
                                  "filled_samples": stage["filled"] // max(launches, 1)},
         }
+        out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per, launches)
         if not args.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(args, opt, pts, feats, agg, cams[0], H, W)

@@ -146,7 +146,9 @@ typedef struct {
   int32_t* ray_row;     /* [R+1]    exclusive scan of ray_mask: compacted row of ray  */
   float* sample_w;      /* [R*SR*3] world position of each filled sample              */
   float* sample_p;      /* [R*SR*3] camera-perspective (x/z, y/z, z) of each sample   */
-  int32_t* counts;      /* [8] {S_filled, S_valid, R_hit(R'), R_valid(R''), n_pairs}  */
+  int32_t* counts;      /* [8] {S_filled, S_valid, R_hit(R'), R_valid(R''), n_pairs, 0,
+                           n_cand (int64 in [6..7]: KNN candidate records read)};
+                           8-byte aligned */
   void* scratch;        /* scan scratch, scratch_bytes from pnr_query_sizes()         */
   size_t scratch_bytes;
 } pnr_query_bufs;

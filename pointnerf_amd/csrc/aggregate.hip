@@ -357,19 +357,27 @@ constexpr size_t kPairsLdsBytes = (size_t)kPairsLdsFloats * sizeof(float);
 __device__ __forceinline__ constexpr int qperm(int i) { return ((i & 1) << 1) | (i >> 1); }
 __device__ __forceinline__ constexpr int qaddr(int n, int c) { return (n >> 2) * kQP + 4 * c + qperm(n & 3); }
 
+// Issue the first kQD k-steps of a layer's weight fragments into the ring.
+// Called as soon as the previous layer's last MFMA is issued (or before the
+// gather for layer 1), so the L2 latency hides behind the layer boundary.
+template <int NT>
+__device__ __forceinline__ void prime_q(float (&a)[kQD][NT], const float* __restrict__ wf, int lane) {
+#pragma unroll
+  for (int d = 0; d < kQD; ++d) load_w<NT, 8>(a[d], wf + lane, d);
+}
+
 // Y^T += W . X^T for NT neuron tiles x PT 32-pair halves over nsteps k-steps.
-// Weight fragments kQD steps ahead in a register ring; the next kQD steps' B
-// operands read from LDS one iteration ahead (kQD/2 b64 per half).
+// Weight fragments kQD steps ahead in a register ring (primed by prime_q);
+// the next kQD steps' B operands read from LDS one iteration ahead (kQD/2 b64
+// per half).
 template <int NT, int PT>
-__device__ __forceinline__ void mlp_layer_q(f32x16 (&acc)[PT * NT], const float* __restrict__ wf,
-                                            const float* X, int nsteps, int lane) {
+__device__ __forceinline__ void mlp_layer_q(f32x16 (&acc)[PT * NT], float (&a)[kQD][NT],
+                                            const float* __restrict__ wf, const float* X, int nsteps,
+                                            int lane) {
   constexpr int D = kQD;
   const int c = lane & 31, h = lane >> 5;
   const float* p = wf + lane;
   const float* xr = X + 4 * c + 2 * h;
-  float a[D][NT];
-#pragma unroll
-  for (int d = 0; d < D; ++d) load_w<NT, 8>(a[d], p, d);
   float2 x[D / 2][PT];
 #pragma unroll
   for (int i = 0; i < D / 2; ++i)
@@ -468,6 +476,8 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
   const float* w2 = A.w.w2f + T0 * 64;
   const float* w3 = A.w.w3f + T0 * 64;
   const float* w4 = A.w.w4f + T0 * 64;
+  float ring[kQD][kNTW];
+  prime_q<kNTW>(ring, w1b, lane);
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // ------------------------------------------------------------ gather (neural_points.py:788-799)
@@ -591,14 +601,16 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     }
     __syncthreads();
     // ------------------------------------------------------------ block1: 284 -> 256 -> 256
-    mlp_layer_q<kNTW, kPTW>(acc, w1b, X, 30, lane);   // + W1[:, 224:284] . PE_5(dist)
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w1b, X, 30, lane);   // + W1[:, 224:284] . PE_5(dist)
+    prime_q<kNTW>(ring, w2, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_q<kNTW, kPTW>(acc, w2, X, 129, lane);
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w2, X, 129, lane);
+    prime_q<kNTW>(ring, w3, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
@@ -613,14 +625,16 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     // ------------------------------------------------------------ block3: 263 -> 256 -> 256
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_q<kNTW, kPTW>(acc, w3, X, 132, lane);
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w3, X, 132, lane);
+    prime_q<kNTW>(ring, w4, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_q<kNTW, kPTW>(acc, w4, X, 129, lane);
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w4, X, 129, lane);
+    prime_q<kNTW>(ring, w1b, lane);                   // the next tile's layer 1
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);   // h4 -> rows 0..255
     __syncthreads();

@@ -92,7 +92,8 @@ template <int KMAX>
 __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, int layers, float r2,
                                        const int32_t* __restrict__ coor_2_occ,
                                        const int32_t* __restrict__ occ_numpnts,
-                                       const float4* __restrict__ occ_pts, int32_t out[KMAX]) {
+                                       const float4* __restrict__ occ_pts, int32_t out[KMAX],
+                                       int& n_cand) {
   const int fx = vox_coord(p[0], g.shift[0], g.vs[0]);
   const int fy = vox_coord(p[1], g.shift[1], g.vs[1]);
   const int fz = vox_coord(p[2], g.shift[2], g.vs[2]);
@@ -116,6 +117,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
           const int slot = coor_2_occ[cell];
           if (slot < 0) continue;
           const int cnt = min(g.P, occ_numpnts[slot]);
+          n_cand += cnt;
           const float4* rec = occ_pts + (int64_t)slot * g.P;
           for (int gi = 0; gi < cnt; ++gi) {
             const float4 v = rec[gi];
@@ -186,7 +188,7 @@ __global__ void __launch_bounds__(kQBlock) k_knn(QRays q, QGrid g, int SR, int K
   float Rm[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Rm[i] = q.camrot[i];
-  int pairs = 0;
+  int pairs = 0, n_cand = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < S;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int rs = fill_rs[i];
@@ -202,7 +204,7 @@ __global__ void __launch_bounds__(kQBlock) k_knn(QRays q, QGrid g, int SR, int K
       sample_p[i * 3 + a] = pp[a];
     }
     int32_t out[KMAX];
-    const int nk = knn_one<KMAX>(p, g, K, layers, r2, coor_2_occ, occ_numpnts, occ_pts, out);
+    const int nk = knn_one<KMAX>(p, g, K, layers, r2, coor_2_occ, occ_numpnts, occ_pts, out, n_cand);
     for (int k = 0; k < K; ++k) {
 #pragma unroll
       for (int j = 0; j < KMAX; ++j)
@@ -213,7 +215,11 @@ __global__ void __launch_bounds__(kQBlock) k_knn(QRays q, QGrid g, int SR, int K
     pairs += nk;
   }
   pairs = wave_sum_i32(pairs);
+  n_cand = wave_sum_i32(n_cand);
   if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(counts + 4, pairs);
+  // candidate records read (measurement only): int64 in counts[6..7]
+  if ((threadIdx.x & 63) == 0 && n_cand)
+    atomicAdd(reinterpret_cast<unsigned long long*>(counts + 6), (unsigned long long)n_cand);
 }
 
 __global__ void __launch_bounds__(kQBlock) k_valid_list(const int32_t* __restrict__ vflag,

@@ -98,9 +98,11 @@ class QueryBuffers:
         return self.R == R and self.SR == SR and self.K == K
 
     def read_counts(self):
-        """{S_filled, S_valid, R_hit, R_valid, n_pairs} (one D2H copy, syncs)."""
-        c = self.counts.cpu().tolist()
-        return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4])
+        """{S_filled, S_valid, R_hit, R_valid, n_pairs, n_cand} (one D2H copy, syncs)."""
+        c = self.counts.cpu()
+        n_cand = int(c[6:8].view(torch.int64).item())
+        c = c.tolist()
+        return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand)
 
 
 class GridHandle:
