@@ -115,6 +115,24 @@ def main():
                         ray_valid=ray_valid.numpy(), weight=weight.numpy(), conf_coefficient=conf.numpy(),
                         **{k: np.ascontiguousarray(v) for k, v in inputs.items()})
 
+    # 3b. PointAggregator backward (autograd of the same forward): upstream gradient
+    #     g_feat on the output, grads of the gathered inputs and of every parameter
+    tg = {k: v.clone().requires_grad_(k in ("sampled_color", "sampled_dir", "sampled_conf",
+                                             "sampled_embedding"))
+          for k, v in t.items()}
+    agg.zero_grad()
+    feats_g, _, _, _ = agg(tg["sampled_color"], torch.eye(3), tg["sampled_dir"], tg["sampled_conf"],
+                           tg["sampled_embedding"], tg["sampled_xyz_pers"], tg["sampled_xyz"],
+                           tg["sample_pnt_mask"], tg["sample_loc"], tg["sample_loc_w"],
+                           tg["sample_ray_dirs"], [0.004, 0.004, 0.004], 0)
+    g_feat = torch.tensor(rng.normal(size=tuple(feats_g.shape)), dtype=torch.float32)
+    (feats_g * g_feat).sum().backward()
+    grads = {"g_" + k: tg[k].grad.numpy() for k in ("sampled_color", "sampled_dir", "sampled_conf",
+                                                   "sampled_embedding")}
+    grads.update({"gp_" + k.replace(".", "_"): p.grad.numpy() for k, p in agg.named_parameters()})
+    np.savez_compressed(os.path.join(HERE, "aggregator_bwd.npz"), g_feat=g_feat.numpy(),
+                        features=feats_g.detach().numpy(), **grads)
+
     # 4. ray_march + radiance_render + alpha_blend (diff_ray_marching.py:509-555)
     NR, SRm, C = 12, 24, 128
     rd = torch.tensor(rng.uniform(0.0, 0.01, size=(1, NR, SRm)), dtype=torch.float32)
@@ -128,6 +146,13 @@ def main():
     np.savez_compressed(os.path.join(HERE, "raymarch.npz"), ray_dist=rd.numpy(), ray_valid=rv.numpy(),
                         ray_features=rf.numpy(), bg_color=bg.numpy(),
                         **{n: (o.numpy() if torch.is_tensor(o) else np.asarray(o)) for n, o in zip(names, out)})
+    # 4b. ray_march backward: upstream gradient on ray_color -> d ray_features
+    rfg = rf.clone().requires_grad_(True)
+    outg = ray_march(rd, rv, rfg, radiance_render, alpha_blend, bg)
+    g_color = torch.tensor(rng.normal(size=tuple(outg[0].shape)), dtype=torch.float32)
+    (outg[0] * g_color).sum().backward()
+    np.savez_compressed(os.path.join(HERE, "raymarch_bwd.npz"), g_color=g_color.numpy(),
+                        g_features=rfg.grad.numpy())
     print("golden vectors written to", HERE)
 
 

@@ -53,7 +53,8 @@ def test_ray_march(golden_dir):
     g = load(golden_dir, "raymarch.npz")
     c, pc, op, T, bw, bgT = O.ray_march(g["ray_dist"][0], g["ray_valid"][0], g["ray_features"][0], g["bg_color"])
     np.testing.assert_allclose(c, g["ray_color"][0], atol=2e-6, rtol=1e-5)
-    np.testing.assert_allclose(op, g["opacity"][0], atol=1e-7, rtol=0)
+    # 1 - exp(-x): numpy and torch exp may differ by 1 ulp
+    np.testing.assert_allclose(op, g["opacity"][0], atol=2.5e-7, rtol=0)
     np.testing.assert_allclose(T, g["acc_transmission"][0], atol=2e-7, rtol=1e-6)
     np.testing.assert_allclose(bw, g["blend_weight"][0], atol=2e-7, rtol=1e-6)
     np.testing.assert_allclose(bgT, g["background_transmission"][0], atol=2e-7, rtol=1e-6)
