@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 1
+#define PNR_ABI_VERSION 2
 
 enum {
   PNR_OK = 0,
@@ -241,6 +241,61 @@ int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const 
                              const uint8_t* pair_mask, float* out_feat, float* out_weight,
                              float* out_conf, void* scratch, size_t scratch_bytes, void* stream);
 
+/* ------------------------------------------------------- aggregate backward
+ * Training path (autograd of point_aggregators.py:729-816 /
+ * 488-646 and the gather neural_points.py:788-799).  pnr_aggregate_fwd_train
+ * runs the forward and keeps the activations the backward needs; all saved
+ * arrays are indexed by sample-list entry v (< n_max) and pair row v*8 + k. */
+typedef struct {
+  float* h1; float* h2; float* h3; float* h4;  /* [n_max*8,256] post-activation outputs of
+                                                  block1.0, block1.2, block3.0, block3.2 */
+  float* pe5;      /* [n_max*8,60] PE_5 of the rotated 6-d distance (block1.0 cols 224..283) */
+  float* x3e;      /* [n_max*8,8]  block3.0 inputs 256..262 (colour, R.dir - R.v, <R.dir,R.v>), 1 */
+  float* pa;       /* [n_max*8]    alpha_branch.0 output (before softplus(x - 1))              */
+  float* wt;       /* [n_max*8]    w_k * clamp(conf_k); 0 for empty pairs                      */
+  float* wn;       /* [n_max*8]    normalised distance weight w_k                              */
+  int32_t* prow;   /* [n_max*8]    point row of the pair, -1 = empty                           */
+  float* hid;      /* [n_max,256]  K-summed features (colour-branch input 0..255)              */
+  float* vpe;      /* [n_max,24]   view-direction PE (colour-branch input 256..279)            */
+  float* hc1; float* hc2; float* hc3;  /* [n_max,128] colour-branch activations              */
+  int32_t* vmask;  /* [n_max]      sample has >= 1 valid neighbour                             */
+} pnr_agg_saved;
+
+/* Transposed weights for the backward GEMMs, fragment-packed like pnr_mlp
+ * (frag_pack(W.T)): w4t = block3.2^T, w3t = block3.0[:, :256]^T, w2t = block1.2^T,
+ * w3e = block3.0[:, 256:263] row-major [256,7]. */
+typedef struct {
+  const float* w4t; const float* w3t; const float* w2t; const float* w3e;
+} pnr_mlp_bwd;
+
+int pnr_aggregate_fwd_train(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                            const pnr_agg_saved* saved, float* out_feat, float* out_weight,
+                            float* out_conf, void* scratch, size_t scratch_bytes, void* stream);
+/* Same, for the PointAggregator.forward mirror (pre-gathered tables, pair_mask). */
+int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                   const uint8_t* pair_mask, const pnr_agg_saved* saved,
+                                   float* out_feat, float* out_weight, float* out_conf,
+                                   void* scratch, size_t scratch_bytes, void* stream);
+
+/* Per-pair backward of block3.2 .. block1.0's pair half, alpha branch, K-sums,
+ * weights and gather, given d_feat[n,129] (column 0: d alpha) and
+ * d_hid[n,256] (gradient of the K-summed features from the colour branch).
+ * Writes dz1..dz4[n_max*8,256] (gradients of the four pre-activations; rows
+ * of empty pairs are 0) and dpa[n_max*8]; accumulates (atomically, so the
+ * caller zeroes them) d_p1[N,256] += dz1 per point (block1.0 point half),
+ * d_color[N,3], d_dir[N,3], d_conf[N] (straight-through clamp gradient).
+ * Any of d_color / d_dir / d_conf may be NULL. */
+int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                            const pnr_mlp_bwd* wb, const pnr_agg_saved* saved,
+                            const float* d_feat, const float* d_hid, float* dz1, float* dz2,
+                            float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
+                            float* d_dir, float* d_conf, void* stream);
+
+/* X1[p] = [emb_p, PE_3(emb_p)] (block1.0 columns 0..223) for p < n, and the
+ * matching backward d_emb[p] += dX1[p] . dX1/d emb (networks.py:175-190). */
+int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* stream);
+int pnr_point_pe3_bwd(const float* emb, const float* d_x1, int64_t n, float* d_emb, void* stream);
+
 /* -------------------------------------------------------------- composite
  * Fused ray_dist (cummax), alpha composite and fill_invalid for the full ray
  * batch R, straight from the query buffers and the decoded features
@@ -266,6 +321,18 @@ int pnr_ray_march_fwd(const float* ray_dist, const uint8_t* ray_valid, const flo
                       const float* bg, int64_t NR, int32_t SR, int32_t C,
                       float* ray_color, float* opacity, float* acc_T, float* blend_w,
                       float* bg_T, void* stream);
+
+/* Backward of pnr_composite_fwd with respect to feat (diff_ray_marching.py:509-555
+ * autograd): d_feat[S_valid, C+1] from d_ray_color[R,C] (every valid row is
+ * written; opacity / is_bg gradients are not propagated). */
+int pnr_composite_bwd(const pnr_rays* rays, const pnr_query_params* q,
+                      const pnr_query_bufs* b, const pnr_composite_params* c,
+                      const float* feat, const float* d_ray_color, float* d_feat, void* stream);
+
+/* Backward of pnr_ray_march_fwd with respect to feat: d_feat[NR,SR,C+1]. */
+int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
+                      const float* bg, int64_t NR, int32_t SR, int32_t C,
+                      const float* d_ray_color, float* d_feat, void* stream);
 
 /* ------------------------------------------------------------- utilities */
 /* Exclusive scan of n int32 values (n_dev: optional device-side length <= n,

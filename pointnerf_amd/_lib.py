@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class PnrError(RuntimeError):
@@ -79,6 +79,15 @@ class CompositeParams(ctypes.Structure):
                 ("bg_color", c_void_p)]
 
 
+class AggSaved(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("h1", "h2", "h3", "h4", "pe5", "x3e", "pa", "wt", "wn", "prow", "hid",
+                                        "vpe", "hc1", "hc2", "hc3", "vmask")]
+
+
+class MlpBwd(ctypes.Structure):
+    _fields_ = [("w4t", c_void_p), ("w3t", c_void_p), ("w2t", c_void_p), ("w3e", c_void_p)]
+
+
 P = ctypes.POINTER
 # name -> (restype, argtypes); exactly the functions include/pnr.h declares.
 SIGNATURES = {
@@ -99,6 +108,19 @@ SIGNATURES = {
                                   c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_train": (c_int, [P(Points), P(Samples), P(Mlp), P(AggSaved), c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_train_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, P(AggSaved), c_void_p,
+                                               c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_bwd_pairs": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(AggSaved), c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_point_pe3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "pnr_point_pe3_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pnr_composite_bwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams), c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
+    "pnr_ray_march_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                  c_void_p, c_void_p, c_void_p]),
     "pnr_composite_fwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams),
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_ray_march_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,

@@ -160,8 +160,6 @@ class PointAggregator(nn.Module):
         """point_aggregators.py:729-816 -> (features [B,R,SR,C+1], ray_valid
         [B,R,SR], weight, conf_coefficient)."""
         L.require_gpu(sample_loc_w)
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) and self.training:
-            raise L.PnrError("libpnr PointAggregator backward is not implemented yet (forward/eval only)")
         if sampled_Rw2c is not None and sampled_Rw2c.dim() != 2:
             raise L.PnrError("per-point Rw2c is not implemented by libpnr (uniform Rw2c only)")
         if sampled_Rw2c is not None:
@@ -171,31 +169,59 @@ class PointAggregator(nn.Module):
         dev = sample_loc_w.device
         C = 128
         ray_valid = torch.any(sample_pnt_mask, dim=-1)
-        out = torch.zeros((rows, C + 1), dtype=torch.float32, device=dev)
         weight = torch.empty((rows, K), dtype=torch.float32, device=dev)
         conf = torch.empty((rows, K), dtype=torch.float32, device=dev)
         if rows == 0:
+            out = torch.zeros((rows, C + 1), dtype=torch.float32, device=dev)
             return out.view(B, R, SR, C + 1), ray_valid, weight.view(B, R, SR, K), conf.view(B, R, SR, K)
 
         def flat(t, c):
             return None if t is None else t.reshape(-1, c).float().contiguous()
 
         keep = dict(xyz=flat(sampled_xyz, 3), pers=flat(sampled_xyz_pers, 3),
-                    emb=flat(sampled_embedding, 32), color=flat(sampled_color, 3),
-                    dir=flat(sampled_dir, 3), conf=flat(sampled_conf, 1),
                     sw=flat(sample_loc_w, 3), sp=flat(sample_loc, 3), sd=flat(sample_ray_dirs, 3),
                     mask=sample_pnt_mask.reshape(-1).contiguous().view(torch.uint8))
-        pts = L.Points(rows * K, keep["xyz"].data_ptr(), keep["pers"].data_ptr(), keep["emb"].data_ptr(),
-                       L.ptr(keep["color"]), L.ptr(keep["dir"]), L.ptr(keep["conf"]), None, None)
         s = L.Samples(None, None, rows, None, keep["sw"].data_ptr(), keep["sp"].data_ptr(),
                       keep["sd"].data_ptr(), None, 1, K)
-        mlp, _ = self.packed()
-        scratch = L.aggregate_scratch(rows, rows * K, dev)
-        L.check(L.lib().pnr_aggregate_fwd_masked(L.ctypes.byref(pts), L.ctypes.byref(s),
-                                                 L.ctypes.byref(mlp), L.ptr(keep["mask"]), L.ptr(out),
-                                                 L.ptr(weight), L.ptr(conf), L.ptr(scratch),
-                                                 scratch.numel() * 4, L.stream_ptr(dev)),
-                "pnr_aggregate_fwd_masked")
+        diff = [t for t in (sampled_embedding, sampled_color, sampled_dir, sampled_conf) if t is not None]
+        if torch.is_grad_enabled() and (any(t.requires_grad for t in diff) or
+                                        any(p.requires_grad for p in self.parameters())):
+            # training path: autograd through pnr_aggregate_fwd_train / _bwd_pairs (train.py)
+            from .train import AggSpec, AggregateFn, agg_params
+            spec = AggSpec(self, s, rows, dict(xyz=keep["xyz"], pers=keep["pers"]), pair_mask=keep["mask"],
+                           keep=(keep,))
+            out = AggregateFn.apply(spec, sampled_embedding.reshape(-1, 32).float(),
+                                    None if sampled_color is None else sampled_color.reshape(-1, 3).float(),
+                                    None if sampled_dir is None else sampled_dir.reshape(-1, 3).float(),
+                                    None if sampled_conf is None else sampled_conf.reshape(-1, 1).float(),
+                                    *agg_params(self))
+            out = out[:rows]
+        else:
+            out = torch.zeros((rows, C + 1), dtype=torch.float32, device=dev)
+            keep.update(emb=flat(sampled_embedding, 32), color=flat(sampled_color, 3), dir=flat(sampled_dir, 3),
+                        conf=flat(sampled_conf, 1))
+            pts = L.Points(rows * K, keep["xyz"].data_ptr(), keep["pers"].data_ptr(), keep["emb"].data_ptr(),
+                           L.ptr(keep["color"]), L.ptr(keep["dir"]), L.ptr(keep["conf"]), None, None)
+            mlp, _ = self.packed()
+            scratch = L.aggregate_scratch(rows, rows * K, dev)
+            L.check(L.lib().pnr_aggregate_fwd_masked(L.ctypes.byref(pts), L.ctypes.byref(s),
+                                                     L.ctypes.byref(mlp), L.ptr(keep["mask"]), L.ptr(out),
+                                                     L.ptr(weight), L.ptr(conf), L.ptr(scratch),
+                                                     scratch.numel() * 4, L.stream_ptr(dev)),
+                    "pnr_aggregate_fwd_masked")
+        if out.requires_grad:
+            # weight / conf_coefficient as the reference returns them (conf with the
+            # straight-through clamp gradient, point_aggregators.py:724-726, 803-804)
+            with torch.no_grad():
+                m = sample_pnt_mask.reshape(rows, K).float()
+                xyz3 = keep["xyz"].view(rows, K, 3) - keep["sw"].view(rows, 1, 3)
+                w = m / torch.clamp(torch.linalg.norm(xyz3, dim=-1), min=1e-6)
+                weight = w / torch.clamp(w.sum(-1, keepdim=True), min=1e-8)
+            if sampled_conf is not None:
+                cf = sampled_conf.reshape(rows, K).float()
+                conf = cf - (cf - torch.clamp(cf, 1e-4, 1.0)).detach()
+            else:
+                conf = torch.ones((rows, K), dtype=torch.float32, device=dev)
         weight, conf = weight.view(B, R, SR, K), conf.view(B, R, SR, K)
         o = self.opt
         if (getattr(o, "sparse_loss_weight", 0) <= 0 and "conf_coefficient" not in getattr(o, "zero_one_loss_items", [])

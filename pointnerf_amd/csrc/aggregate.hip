@@ -36,7 +36,6 @@ namespace pnr {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kAggBlock = 256;     // 4 waves, each independent
-constexpr int kSampPerWave = 4;    // 4 samples x 8 neighbours = 32 MFMA columns
 constexpr int kKN = 8;
 constexpr int kHid = 256;
 constexpr int kEmb = 32;
@@ -46,7 +45,6 @@ constexpr int kPitch = 33;         // LDS row pitch (floats) of X^T[k][32 + 1]
 constexpr int kXRows = 296;        // >= 286 layer-1 inputs + bias, + x prefetch overrun
 constexpr int kWaveLds = kXRows * kPitch;  // floats per wave slice
 constexpr size_t kAggLdsBytes = (size_t)4 * kWaveLds * sizeof(float);
-constexpr int kWtRow = 286;        // X^T row holding the per-pair blend weight after layer 4
 constexpr int kPD = 4;             // weight prefetch depth in k-steps of mlp_layer
 constexpr int kPackPad = 8;        // zero k-steps padded onto every packed weight matrix
                                    // (>= every prefetch depth, so prefetch never overruns)
@@ -62,6 +60,7 @@ struct AggArgs {
   float* out_weight;
   float* out_conf;
   const uint8_t* pair_mask;   // mirror path: validity per (row, k); pidx == NULL
+  pnr_agg_saved sv;           // training forward: activations kept for the backward
 };
 
 __device__ __forceinline__ float lrelu(float x, float s) { return x > 0.f ? x : x * s; }
@@ -251,6 +250,22 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_point_pre(AggArgs A) {
   }
 }
 
+// Post-activation accumulator tiles -> [row][ld] global rows (training saves);
+// lane column m = row offset, rows of tile T at columns 32T + 8q + 4h.
+template <int NT>
+__device__ __forceinline__ void save_rows(const f32x16 (&acc)[NT], float* dst, int64_t row, int ld, float s,
+                                          int lane, int T0 = 0) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int T = 0; T < NT; ++T)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(dst + row * ld + 32 * (T0 + T) + 8 * q + 4 * h) =
+          make_float4(lrelu(acc[T][4 * q], s), lrelu(acc[T][4 * q + 1], s), lrelu(acc[T][4 * q + 2], s),
+                      lrelu(acc[T][4 * q + 3], s));
+}
+
+template <bool TRAIN>
 __global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -294,6 +309,7 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
           float s, co;
           sincosf(vrot[c] * (float)(1 << f), &s, &co);
           X[(kHid + 12 * h + 4 * c + f) * kPitch + m] = h ? co : s;
+          if (TRAIN && m < nv) A.sv.vpe[(v0 + m) * 24 + 12 * h + 4 * c + f] = h ? co : s;
         }
     }
     bias_rows(X, kCin, lane);
@@ -303,18 +319,21 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
     mlp_layer<4>(acc, A.w.wc1f, X, 141, lane);      // 280 inputs + bias column
     wave_sync();
     store_act<4>(acc, X, neg, lane);
+    if (TRAIN && m < nv) save_rows<4>(acc, A.sv.hc1, v0 + m, kC, neg, lane);
     bias_rows(X, kC, lane);
     wave_sync();
     zero_acc<4>(acc);
     mlp_layer<4>(acc, A.w.wc2f, X, 65, lane);
     wave_sync();
     store_act<4>(acc, X, neg, lane);
+    if (TRAIN && m < nv) save_rows<4>(acc, A.sv.hc2, v0 + m, kC, neg, lane);
     bias_rows(X, kC, lane);
     wave_sync();
     zero_acc<4>(acc);
     mlp_layer<4>(acc, A.w.wc3f, X, 65, lane);
     wave_sync();
     store_act<4>(acc, X, neg, lane);   // X^T rows 0..127 = colour features
+    if (TRAIN && m < nv) save_rows<4>(acc, A.sv.hc3, v0 + m, kC, neg, lane);
     wave_sync();
     // write out_feat[v, 1..128]: lane = channel pair, loop over the 32 samples
     for (int q = 0; q < nv; ++q) {
@@ -448,6 +467,23 @@ constexpr int kPairWaves = 4;
 constexpr int kNTW = 8 / kPairWaves;   // neuron tiles per wave
 constexpr int kPTW = kTP / 32;         // 32-pair halves per tile
 
+// Training save of a tile's post-activation quad (both halves) -> dst[pair][256].
+template <int NT, int PT>
+__device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float* dst, int64_t tile,
+                                             int64_t n, float s, int lane, int T0) {
+  const int c = lane & 31;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    const int col = 32 * pt + c;
+    if (tile * kTS + (col >> 3) >= n) continue;
+    f32x16 one[NT];
+#pragma unroll
+    for (int T = 0; T < NT; ++T) one[T] = acc[pt * NT + T];
+    save_rows<NT>(one, dst, tile * kTP + col, kHid, s, lane, T0);
+  }
+}
+
+template <bool TRAIN>
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   float* X = lds_dyn;                          // quad rows [kQRows][kQP]
@@ -580,6 +616,12 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
       }
       wtL[lane] = wt;
       if (k == 0) sflag[j] = active && samp_valid;
+      if (TRAIN && active) {
+        const int64_t pr = tile * kTP + lane;
+        A.sv.wt[pr] = wt;
+        A.sv.wn[pr] = wn;
+        A.sv.prow[pr] = valid ? (int32_t)prow : -1;
+      }
     }
     // 5-band PE of the 6-d rotated distance -> rows 2e + {0: sin, 1: cos},
     // e = 5 ch + f (block1.0 columns 224..283); wave w owns e = w (mod 4)
@@ -597,6 +639,11 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
         sincosf(dc * (float)(1 << f), &sn, &cs);
         X[qaddr(2 * e, lane)] = sn;
         X[qaddr(2 * e + 1, lane)] = cs;
+        if (TRAIN && active) {
+          float* pe = A.sv.pe5 + (tile * kTP + lane) * 60 + 2 * e;
+          pe[0] = sn;
+          pe[1] = cs;
+        }
       }
     }
     __syncthreads();
@@ -605,6 +652,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w2, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h1, tile, n, neg, lane, T0);
     if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
@@ -613,6 +661,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w3, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h2, tile, n, neg, lane, T0);
     // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
     if (wid == 0) {
       const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
@@ -620,6 +669,10 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
                            drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
 #pragma unroll
       for (int e = 0; e < 8; ++e) X[qaddr(256 + e, lane)] = ex[e];
+      if (TRAIN && active) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) A.sv.x3e[(tile * kTP + lane) * 8 + e] = ex[e];
+      }
     }
     __syncthreads();
     // ------------------------------------------------------------ block3: 263 -> 256 -> 256
@@ -629,6 +682,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w4, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h3, tile, n, neg, lane, T0);
     if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
@@ -637,6 +691,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w1b, lane);                   // the next tile's layer 1
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);   // h4 -> rows 0..255
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h4, tile, n, neg, lane, T0);
     __syncthreads();
     if (!(PNR_ABLATE & 4)) {
       // ---------------------------------------------------------- alpha branch
@@ -658,6 +713,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
         const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
         const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
         const int64_t vo = tile * kTS + j;
+        if (TRAIN && vo < n) A.sv.pa[tile * kTP + lane] = pa;
         if (k == 0 && vo < n) {
           A.vmask[vo] = sflag[j];
           if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
@@ -688,14 +744,15 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
   }
 }
 
-int launch(const AggArgs& a, hipStream_t st) {
+template <bool TRAIN>
+int launch_t(const AggArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs<TRAIN>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsLdsBytes));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color<TRAIN>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     attr = true;
   }
@@ -703,12 +760,306 @@ int launch(const AggArgs& a, hipStream_t st) {
                      st, a);
   PNR_LAUNCH_CHECK();
   const int64_t tiles = cdiv(a.s.n_max, kTS);
-  hipLaunchKernelGGL(k_pairs, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kPairsLdsBytes, st, a);
+  hipLaunchKernelGGL(k_pairs<TRAIN>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kPairsLdsBytes,
+                     st, a);
   PNR_LAUNCH_CHECK();
   const int64_t ctiles = cdiv(a.s.n_max, 32);
-  hipLaunchKernelGGL(k_color, dim3(grid_for(ctiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
+  hipLaunchKernelGGL(k_color<TRAIN>, dim3(grid_for(ctiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
+}
+
+int launch(const AggArgs& a, hipStream_t st, bool train) {
+  return train ? launch_t<true>(a, st) : launch_t<false>(a, st);
+}
+
+// ===========================================================================
+// Backward.  k_pairs_bwd mirrors k_pairs: a 4-wave workgroup
+// owns 64 pairs, wave w owns neuron tiles {2w, 2w+1} of both halves, and the
+// three dX GEMMs (block3.2^T, block3.0[:, :256]^T, block1.2^T) run on the same
+// quad-row LDS pipeline with transposed, fragment-packed weights.  The dW
+// GEMMs (sum over pairs) are plain GEMMs and left to the caller (hipBLASLt).
+struct BwdArgs {
+  pnr_points pts;
+  pnr_samples s;
+  pnr_mlp w;
+  pnr_mlp_bwd wb;
+  pnr_agg_saved sv;
+  const float* d_feat;   // [n,129]
+  const float* d_hid;    // [n,256]
+  float* dz[4];          // dz1..dz4 [n*8,256]
+  float* dpa;            // [n*8]
+  float* d_p1;           // [N,256] (+=)
+  float* d_color;        // [N,3] (+=) or null
+  float* d_dir;          // [N,3] (+=) or null
+  float* d_conf;         // [N]   (+=) or null
+};
+
+constexpr int kBwdLdsFloats = 66 * kQP + 4 * kTP /*dot parts*/ + 4 * 7 * kTP /*extras parts*/;
+constexpr size_t kBwdLdsBytes = (size_t)kBwdLdsFloats * sizeof(float);
+
+// acc-layout float4 of a [pair][256] array for (half pt, tile T, quad q)
+__device__ __forceinline__ float4 ld_q(const float* base, int64_t pair, int T, int q, int h) {
+  return *reinterpret_cast<const float4*>(base + pair * kHid + 32 * T + 8 * q + 4 * h);
+}
+
+// Raw (no activation) accumulator quads -> quad rows.
+template <int NT, int PT>
+__device__ __forceinline__ void store_q(const f32x16 (&acc)[PT * NT], float* X, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16& v = acc[pt * NT + T];
+        *reinterpret_cast<float4*>(X + (8 * (T0 + T) + 2 * q + h) * kQP + 4 * (32 * pt + c)) =
+            make_float4(v[4 * q], v[4 * q + 2], v[4 * q + 1], v[4 * q + 3]);
+      }
+}
+
+// dz = dh * lrelu'(h) with h the saved post-activation (h > 0 <=> z > 0 for
+// slope >= 0); writes dz back into acc and to dst rows of active pairs.
+template <int NT, int PT>
+__device__ __forceinline__ void lrelu_bwd_q(f32x16 (&acc)[PT * NT], const float* h_saved, float* dst,
+                                            int64_t tile, int64_t n, float slope, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    const int col = 32 * pt + c;
+    const bool act = tile * kTS + (col >> 3) < n;
+    const int64_t pair = tile * kTP + col;
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x16& v = acc[pt * NT + T];
+        float4 hv = act ? ld_q(h_saved, pair, T0 + T, q, h) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[4 * q + 0] = hv.x > 0.f ? v[4 * q + 0] : v[4 * q + 0] * slope;
+        v[4 * q + 1] = hv.y > 0.f ? v[4 * q + 1] : v[4 * q + 1] * slope;
+        v[4 * q + 2] = hv.z > 0.f ? v[4 * q + 2] : v[4 * q + 2] * slope;
+        v[4 * q + 3] = hv.w > 0.f ? v[4 * q + 3] : v[4 * q + 3] * slope;
+        if (!act) v[4 * q] = v[4 * q + 1] = v[4 * q + 2] = v[4 * q + 3] = 0.f;
+        if (act)
+          *reinterpret_cast<float4*>(dst + pair * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
+              make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      }
+  }
+}
+
+__global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  float* X = lds_dyn;                   // quad rows [66][kQP]
+  float* dotp = X + 66 * kQP;           // [4][64] partial <d_hid, h4> per wave
+  float* exP = dotp + 4 * kTP;          // [4][7][64] partial block3.0 extras gradients
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int j = lane >> 3;
+  const int T0 = wid * kNTW;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kTS);
+  const float slope = A.w.neg_slope;
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  const float* w4t = A.wb.w4t + T0 * 64;
+  const float* w3t = A.wb.w3t + T0 * 64;
+  const float* w2t = A.wb.w2t + T0 * 64;
+  float ring[kQD][kNTW];
+  prime_q<kNTW>(ring, w4t, lane);
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // ---------------------------------------------------------- per-pair scalars (lane = pair)
+    const int64_t v = tile * kTS + j;
+    const bool active = v < n;
+    const int64_t pair = tile * kTP + lane;
+    const bool svalid = active && A.sv.vmask[v] != 0;
+    const float wt = active ? A.sv.wt[pair] : 0.f;
+    const float pa = active ? A.sv.pa[pair] : 0.f;
+    const float dalpha = svalid ? A.d_feat[v * (kC + 1)] : 0.f;
+    // alpha_k = softplus(pa - 1) (threshold 20) or relu(pa) (point_aggregators.py:262-267)
+    float a_k, sig;
+    if (A.w.act_super) {
+      const float x = pa - 1.f;
+      a_k = softplus(x);
+      sig = x > 20.f ? 1.f : 1.f / (1.f + expf(-x));
+    } else {
+      a_k = fmaxf(pa, 0.f);
+      sig = pa > 0.f ? 1.f : 0.f;
+    }
+    const float dpa = dalpha * wt * sig;   // d alpha_s / d pa_k
+    if (wid == 0 && active) A.dpa[pair] = dpa;
+    // ---------------------------------------------------------- d h4 -> dz4 (acc layout)
+    f32x16 acc[kPTW * kNTW];
+    float dot[kPTW];
+#pragma unroll
+    for (int pt = 0; pt < kPTW; ++pt) {
+      const int col = 32 * pt + c;
+      const int64_t pp = tile * kTP + col;
+      const int64_t vv = tile * kTS + (col >> 3);
+      const bool act = vv < n;
+      const float wt_p = __shfl(wt, col), dpa_p = __shfl(dpa, col);
+      const bool sv_p = __shfl((int)svalid, col) != 0;
+      dot[pt] = 0.f;
+#pragma unroll
+      for (int T = 0; T < kNTW; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 h4 = act ? ld_q(A.sv.h4, pp, T0 + T, q, h) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 df = sv_p ? ld_q(A.d_hid, vv, T0 + T, q, h) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 wa = *reinterpret_cast<const float4*>(A.w.wa + 32 * (T0 + T) + 8 * q + 4 * h);
+          dot[pt] += df.x * h4.x + df.y * h4.y + df.z * h4.z + df.w * h4.w;
+          // f_s = sum_k wt_k h4_k ; alpha_s = sum_k wt_k softplus(wa.h4_k + ba - 1)
+          acc[pt * kNTW + T][4 * q + 0] = wt_p * df.x + dpa_p * wa.x;
+          acc[pt * kNTW + T][4 * q + 1] = wt_p * df.y + dpa_p * wa.y;
+          acc[pt * kNTW + T][4 * q + 2] = wt_p * df.z + dpa_p * wa.z;
+          acc[pt * kNTW + T][4 * q + 3] = wt_p * df.w + dpa_p * wa.w;
+        }
+      dot[pt] += __shfl_xor(dot[pt], 32);
+    }
+    if (h == 0) {
+      dotp[wid * kTP + c] = dot[0];
+      dotp[wid * kTP + 32 + c] = dot[1];
+    }
+    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h4, A.dz[3], tile, n, slope, lane, T0);
+    store_q<kNTW, kPTW>(acc, X, lane, T0);
+    __syncthreads();
+    // d wt_k = d alpha_s a_k + <d f_s, h4_k>  ->  d conf_k (straight-through clamp, :724-726)
+    if (wid == 0 && active && A.d_conf) {
+      const int32_t pr = A.sv.prow[pair];
+      if (pr >= 0) {
+        const float dwt = dalpha * a_k + dotp[lane] + dotp[kTP + lane] + dotp[2 * kTP + lane] +
+                          dotp[3 * kTP + lane];
+        atomicAdd(A.d_conf + pr, dwt * A.sv.wn[pair]);
+      }
+    }
+    // ---------------------------------------------------------- block3.2^T: dh3 = W4^T dz4
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w4t, X, 128, lane);
+    prime_q<kNTW>(ring, w3t, lane);
+    __syncthreads();
+    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h3, A.dz[2], tile, n, slope, lane, T0);
+    store_q<kNTW, kPTW>(acc, X, lane, T0);
+    // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
+    // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
+    wave_sync();
+    {
+      float ex[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
+        const float4 x4 = *reinterpret_cast<const float4*>(X + u * kQP + 4 * lane);
+        const float xv[4] = {x4.x, x4.z, x4.y, x4.w};   // neurons 4u + 0..3 (quad perm)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float* we = A.wb.w3e + (4 * u + i) * 7;
+#pragma unroll
+          for (int e = 0; e < 7; ++e) ex[e] += we[e] * xv[i];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 7; ++e) exP[(wid * 7 + e) * kTP + lane] = ex[e];
+    }
+    __syncthreads();
+    // ---------------------------------------------------------- block3.0^T: dh2 = W3[:, :256]^T dz3
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
+    prime_q<kNTW>(ring, w2t, lane);
+    // colour / dir gradients of the pair (wave 0, lane = pair; exP is not
+    // overwritten before the next tile's barrier)
+    if (wid == 0 && active) {
+      const int32_t pr = A.sv.prow[pair];
+      if (pr >= 0) {
+        float g[7];
+#pragma unroll
+        for (int e = 0; e < 7; ++e)
+          g[e] = exP[(0 * 7 + e) * kTP + lane] + exP[(1 * 7 + e) * kTP + lane] + exP[(2 * 7 + e) * kTP + lane] +
+                 exP[(3 * 7 + e) * kTP + lane];
+        if (A.d_color) {
+#pragma unroll
+          for (int a = 0; a < 3; ++a) atomicAdd(A.d_color + (int64_t)pr * 3 + a, g[a]);
+        }
+        if (A.d_dir) {
+          // inputs: R.dir - R.v (3), <R.dir, R.v> (1) with R.dir = dir @ Rw^T
+          const int64_t row = sample_row(A.s, v);
+          const int64_t drow = dir_row(A.s, row);
+          const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+          float vrot[3];
+          mat3(Rw, vd, vrot);
+          const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
+          // drot_j = sum_i Rw[j][i] dir_i  ->  d dir_i = sum_j Rw[j][i] d drot_j
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            atomicAdd(A.d_dir + (int64_t)pr * 3 + i, Rw[i] * gd[0] + Rw[3 + i] * gd[1] + Rw[6 + i] * gd[2]);
+        }
+      }
+    }
+    __syncthreads();
+    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h2, A.dz[1], tile, n, slope, lane, T0);
+    store_q<kNTW, kPTW>(acc, X, lane, T0);
+    __syncthreads();
+    // ---------------------------------------------------------- block1.2^T: dh1 = W2^T dz2
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
+    prime_q<kNTW>(ring, w4t, lane);   // the next tile
+    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h1, A.dz[0], tile, n, slope, lane, T0);
+    // block1.0 point half: d P1[p] += dz1 (the P1 gather's backward)
+#pragma unroll
+    for (int pt = 0; pt < kPTW; ++pt) {
+      const int col = 32 * pt + c;
+      const bool act = tile * kTS + (col >> 3) < n;
+      const int32_t pr = act ? A.sv.prow[tile * kTP + col] : -1;
+      if (pr < 0) continue;
+      float* dst = A.d_p1 + (int64_t)pr * kHid;
+#pragma unroll
+      for (int T = 0; T < kNTW; ++T)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) atomicAdd(dst + 32 * (T0 + T) + acc_row(r, h), acc[pt * kNTW + T][r]);
+    }
+    __syncthreads();
+  }
+}
+
+// X1[p] = [emb, PE_3(emb)] (networks.py:175-190: channel d, band f -> 32 + 2(3d+f) + {sin, cos})
+__global__ void k_point_pe3(const float* __restrict__ emb, int64_t n, float* __restrict__ x1) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kEmb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / kEmb;
+    const int d = (int)(i - p * kEmb);
+    const float e = emb[i];
+    float* o = x1 + p * 224;
+    o[d] = e;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      float sn, cs;
+      sincosf(e * (float)(1 << f), &sn, &cs);
+      o[kEmb + 2 * (3 * d + f)] = sn;
+      o[kEmb + 2 * (3 * d + f) + 1] = cs;
+    }
+  }
+}
+
+__global__ void k_point_pe3_bwd(const float* __restrict__ emb, const float* __restrict__ dx1, int64_t n,
+                                float* __restrict__ d_emb) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kEmb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / kEmb;
+    const int d = (int)(i - p * kEmb);
+    const float e = emb[i];
+    const float* g = dx1 + p * 224;
+    float acc = g[d];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const float b = (float)(1 << f);
+      float sn, cs;
+      sincosf(e * b, &sn, &cs);
+      acc += b * (cs * g[kEmb + 2 * (3 * d + f)] - sn * g[kEmb + 2 * (3 * d + f) + 1]);
+    }
+    d_emb[i] += acc;
+  }
 }
 
 static size_t scratch_need(int64_t n_max, int64_t n_points) {
@@ -769,7 +1120,7 @@ extern "C" int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, co
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.pair_mask = nullptr;
-  return launch(a, as_stream(stream));
+  return launch(a, as_stream(stream), false);
 }
 
 extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
@@ -791,5 +1142,127 @@ extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.pair_mask = pair_mask;
-  return launch(a, as_stream(stream));
+  return launch(a, as_stream(stream), false);
+}
+
+static int check_saved(const pnr_agg_saved* sv) {
+  PNR_CHECK_ARG(sv, "aggregate train: null saved struct");
+  PNR_CHECK_ARG(sv->h1 && sv->h2 && sv->h3 && sv->h4 && sv->pe5 && sv->x3e && sv->pa && sv->wt && sv->wn &&
+                    sv->prow && sv->hid && sv->vpe && sv->hc1 && sv->hc2 && sv->hc3 && sv->vmask,
+                "aggregate train: null saved array");
+  PNR_CHECK_ARG((((uintptr_t)sv->h1 | (uintptr_t)sv->h2 | (uintptr_t)sv->h3 | (uintptr_t)sv->h4 |
+                  (uintptr_t)sv->hid | (uintptr_t)sv->hc1 | (uintptr_t)sv->hc2 | (uintptr_t)sv->hc3) & 15) == 0,
+                "aggregate train: saved activations must be 16-B aligned");
+  return PNR_OK;
+}
+
+extern "C" int pnr_aggregate_fwd_train(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                       const pnr_agg_saved* saved, float* out_feat, float* out_weight,
+                                       float* out_conf, void* scratch, size_t scratch_bytes, void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
+  if ((rc = check_saved(saved))) return rc;
+  PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate: need pers or camera");
+  if (s->n_max <= 0) return PNR_OK;
+  AggArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  carve(a, scratch, s->n_max);
+  a.sv = *saved;
+  a.hid = saved->hid;
+  a.vmask = saved->vmask;
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  a.pair_mask = nullptr;
+  return launch(a, as_stream(stream), true);
+}
+
+extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                              const uint8_t* pair_mask, const pnr_agg_saved* saved,
+                                              float* out_feat, float* out_weight, float* out_conf,
+                                              void* scratch, size_t scratch_bytes, void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
+  if ((rc = check_saved(saved))) return rc;
+  PNR_CHECK_ARG(pair_mask, "aggregate_masked: null pair_mask");
+  PNR_CHECK_ARG(pts->pers, "aggregate_masked: pers required");
+  PNR_CHECK_ARG(s->pidx == nullptr, "aggregate_masked: pidx must be NULL (identity rows)");
+  if (s->n_max <= 0) return PNR_OK;
+  AggArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  carve(a, scratch, s->n_max);
+  a.sv = *saved;
+  a.hid = saved->hid;
+  a.vmask = saved->vmask;
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  a.pair_mask = pair_mask;
+  return launch(a, as_stream(stream), true);
+}
+
+extern "C" int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                       const pnr_mlp_bwd* wb, const pnr_agg_saved* saved,
+                                       const float* d_feat, const float* d_hid, float* dz1, float* dz2,
+                                       float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
+                                       float* d_dir, float* d_conf, void* stream) {
+  int rc;
+  PNR_CHECK_ARG(pts && s && w && wb, "aggregate_bwd: null pointer");
+  if ((rc = check_saved(saved))) return rc;
+  PNR_CHECK_ARG(wb->w4t && wb->w3t && wb->w2t && wb->w3e && w->wa, "aggregate_bwd: null weight");
+  PNR_CHECK_ARG(d_feat && d_hid && dz1 && dz2 && dz3 && dz4 && dpa && d_p1, "aggregate_bwd: null buffer");
+  PNR_CHECK_ARG((((uintptr_t)d_hid | (uintptr_t)dz1 | (uintptr_t)dz2 | (uintptr_t)dz3 | (uintptr_t)dz4) & 15) == 0,
+                "aggregate_bwd: gradient buffers must be 16-B aligned");
+  PNR_CHECK_ARG(s->dirs && s->dir_div >= 1, "aggregate_bwd: sample dirs required");
+  PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate_bwd: K=%d unsupported (1..8)", s->K);
+  if (s->n_max <= 0) return PNR_OK;
+  hipStream_t st = as_stream(stream);
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBwdLdsBytes));
+    attr = true;
+  }
+  BwdArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  a.wb = *wb;
+  a.sv = *saved;
+  a.d_feat = d_feat;
+  a.d_hid = d_hid;
+  a.dz[0] = dz1;
+  a.dz[1] = dz2;
+  a.dz[2] = dz3;
+  a.dz[3] = dz4;
+  a.dpa = dpa;
+  a.d_p1 = d_p1;
+  a.d_color = d_color;
+  a.d_dir = d_dir;
+  a.d_conf = d_conf;
+  const int64_t tiles = cdiv(s->n_max, kTS);
+  hipLaunchKernelGGL(k_pairs_bwd, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* stream) {
+  PNR_CHECK_ARG(emb && x1 && n >= 0, "point_pe3: bad args");
+  if (n == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_point_pe3, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, n, x1);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_point_pe3_bwd(const float* emb, const float* d_x1, int64_t n, float* d_emb, void* stream) {
+  PNR_CHECK_ARG(emb && d_x1 && d_emb && n >= 0, "point_pe3_bwd: bad args");
+  if (n == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_point_pe3_bwd, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, d_x1,
+                     n, d_emb);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
 }

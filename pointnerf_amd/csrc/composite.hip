@@ -232,6 +232,208 @@ __global__ void __launch_bounds__(kCBlock) k_ray_march_dense(const float* __rest
   }
 }
 
+// ---------------------------------------------------------------- backward
+// Reverse-mode of march_slots + the colour sum (autograd of
+// diff_ray_marching.py:530-555): gw = <d colour, c_s> per slot, dbgT =
+// <d colour, bg>.  With f_s = 1 - o_s + 1e-10, P = cumprod(f) (inclusive),
+// T_s = P_{s-1} (exclusive), w_s = o_s T_s, bgT = P_{SR-1}:
+//   dP_i = dT_{i+1} (i < SR-1), dP_{SR-1} = dbgT          (made-exclusive shift)
+//   df_j = sum_{i >= j} dP_i P_i / f_j                   (torch cumprod backward)
+//   do_j = gw_j T_j - df_j,  dsigma_j = do_j exp(-sigma_j d_j) d_j.
+__device__ __forceinline__ float wave_sum_suffix_incl(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    float t = __shfl_down(v, o);
+    if (lane + o < 64) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void march_slots_bwd(const float sig[2], const float dist[2], const float gw[2], float dbgT,
+                                                int SR, float dsig[2]) {
+  const int lane = threadIdx.x & 63;
+  const float op0 = 1.f - expf(-sig[0] * dist[0]);
+  const float op1 = 1.f - expf(-sig[1] * dist[1]);
+  const float f0 = (lane < SR) ? (1.f - op0 + 1e-10f) : 1.f;
+  const float f1 = (lane + 64 < SR) ? (1.f - op1 + 1e-10f) : 1.f;
+  const float i0 = wave_prod_scan_incl(f0);
+  const float tot0 = __shfl(i0, 63);
+  const float i1 = wave_prod_scan_incl(f1) * tot0;
+  float e0 = __shfl_up(i0, 1), e1 = __shfl_up(i1, 1);
+  if (lane == 0) {
+    e0 = 1.f;
+    e1 = tot0;
+  }
+  // dT (exclusive) per slot, then dP_i = dT_{i+1}
+  const float dT0 = gw[0] * op0, dT1 = gw[1] * op1;
+  float dP0 = __shfl_down(dT0, 1), dP1 = __shfl_down(dT1, 1);
+  const float dT1_first = __shfl(dT1, 0);
+  if (lane == 63) {
+    dP0 = dT1_first;
+    dP1 = 0.f;
+  }
+  const int last = SR - 1;
+  if (lane == last) dP0 = dbgT;
+  if (lane + 64 == last) dP1 = dbgT;
+  if (lane > last) dP0 = 0.f;
+  if (lane + 64 > last) dP1 = 0.f;
+  // suffix sums of dP_i P_i (slots 64.. first, then 0..63 plus the upper total)
+  const float s1 = wave_sum_suffix_incl(dP1 * i1);
+  const float tot1 = __shfl(s1, 0);
+  const float s0 = wave_sum_suffix_incl(dP0 * i0) + tot1;
+  const float df0 = (lane < SR) ? s0 / f0 : 0.f;
+  const float df1 = (lane + 64 < SR) ? s1 / f1 : 0.f;
+  const float do0 = gw[0] * e0 - df0, do1 = gw[1] * e1 - df1;
+  dsig[0] = do0 * expf(-sig[0] * dist[0]) * dist[0];
+  dsig[1] = do1 * expf(-sig[1] * dist[1]) * dist[1];
+}
+
+struct CompBwdArgs {
+  CompArgs f;
+  const float* d_color;   // [R,C]
+  float* d_feat;          // [S_valid,C+1]
+};
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ void __launch_bounds__(kCBlock) k_composite_bwd(CompBwdArgs A) {
+  const CompArgs& a = A.f;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int SR = a.SR, C = a.C, CF = C + 1;
+  float zo;
+  {
+    const float c[3] = {a.campos[0], a.campos[1], a.campos[2]};
+    float Rm[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rm[i] = a.camrot[i];
+    const float zero[3] = {0.f, 0.f, 0.f};
+    float pc[3];
+    world_to_cam(zero, c, Rm, pc);
+    zo = pc[2];
+  }
+  const float vz = a.vsize_z, two_vz = 2.f * a.vsize_z;
+  for (int64_t r = wave0; r < a.R; r += nwaves) {
+    if (a.ray_vcnt[r] <= 0) continue;   // background ray: no feature gradient
+    // forward recompute (same as k_composite)
+    const int n = a.n_filled[r], off = a.ray_off[r];
+    float z[2], sig[2];
+    int vrow[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      const bool filled = s < n;
+      const int64_t i = off + s;
+      z[q] = filled ? a.sample_p[i * 3 + 2] : (s < SR ? zo : -INFINITY);
+      const bool val = filled && a.vflag[i];
+      vrow[q] = val ? a.valid_off[i] : -1;
+      sig[q] = val ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
+    }
+    float cm0 = wave_max_scan_incl(z[0]);
+    float cm1 = fmaxf(wave_max_scan_incl(z[1]), __shfl(cm0, 63));
+    float nx0 = __shfl_down(cm0, 1), nx1 = __shfl_down(cm1, 1);
+    const float cm1_first = __shfl(cm1, 0);
+    if (lane == 63) nx0 = cm1_first;
+    float dist[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      const float cm = q ? cm1 : cm0, nx = q ? nx1 : nx0;
+      float d = (s < SR - 1) ? (nx - cm) : vz;
+      const bool msk = (d < 1e-8f) || (a.unit && d > two_vz);
+      d = msk ? vz : d;
+      dist[q] = vrow[q] >= 0 ? d : 0.f;
+    }
+    const SlotOut so = march_slots(sig[0], dist[0], sig[1], dist[1], SR);
+    const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
+    // colour part: lane = channel
+    const float* dc = A.d_color + r * C;
+    const float dc0 = lane < C ? dc[lane] : 0.f, dc1 = lane + 64 < C ? dc[lane + 64] : 0.f;
+    float dbgT = 0.f;
+    if (a.bg) dbgT = wave_sum_f32((lane < C ? dc0 * a.bg[lane] : 0.f) + (lane + 64 < C ? dc1 * a.bg[lane + 64] : 0.f));
+    float gw[2] = {0.f, 0.f};
+    const int smax = n < SR ? n : SR;
+    for (int s = 0; s < smax; ++s) {
+      const int q = s >> 6, src = s & 63;
+      const int vr = __shfl(q ? vrow[1] : vrow[0], src);
+      if (vr < 0) continue;
+      const float w = __shfl(q ? w1 : w0, src);
+      const float* f = a.feat + (int64_t)vr * CF + 1;
+      float* g = A.d_feat + (int64_t)vr * CF + 1;
+      float part = 0.f;
+      if (lane < C) {
+        part += dc0 * f[lane];
+        g[lane] = w * dc0;
+      }
+      if (lane + 64 < C) {
+        part += dc1 * f[lane + 64];
+        g[lane + 64] = w * dc1;
+      }
+      const float gws = wave_sum_f32(part);
+      if (lane == src) gw[q] = gws;
+    }
+    float dsig[2];
+    march_slots_bwd(sig, dist, gw, dbgT, SR, dsig);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (vrow[q] >= 0) A.d_feat[(int64_t)vrow[q] * CF] = dsig[q];
+  }
+}
+
+__global__ void __launch_bounds__(kCBlock) k_ray_march_dense_bwd(const float* __restrict__ ray_dist,
+                                                                 const uint8_t* __restrict__ ray_valid,
+                                                                 const float* __restrict__ feat,
+                                                                 const float* __restrict__ bg, int64_t NR, int SR,
+                                                                 int C, const float* __restrict__ d_color,
+                                                                 float* __restrict__ d_feat) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int CF = C + 1;
+  for (int64_t r = wave0; r < NR; r += nwaves) {
+    float sig[2], dist[2], vv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      const bool in = s < SR;
+      const int64_t e = r * SR + s;
+      vv[q] = (in && ray_valid[e]) ? 1.f : 0.f;
+      sig[q] = in ? feat[e * CF] * vv[q] : 0.f;
+      dist[q] = in ? ray_dist[e] : 0.f;
+    }
+    const SlotOut so = march_slots(sig[0], dist[0], sig[1], dist[1], SR);
+    const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
+    float gw[2] = {0.f, 0.f};
+    float dbgT = 0.f;
+    for (int c0 = 0; c0 < C; c0 += 64) {
+      const int c = c0 + lane;
+      const float dcv = c < C ? d_color[r * C + c] : 0.f;
+      if (bg) dbgT += wave_sum_f32(c < C ? dcv * bg[c] : 0.f);
+      for (int s = 0; s < SR; ++s) {
+        const int q = s >> 6, src = s & 63;
+        const float w = __shfl(q ? w1 : w0, src);
+        const int64_t e = (r * SR + s) * CF + 1 + c;
+        const float gws = wave_sum_f32(c < C ? dcv * feat[e] : 0.f);
+        if (lane == src) gw[q] += gws;
+        if (c < C) d_feat[e] = w * dcv;
+      }
+    }
+    float dsig[2];
+    march_slots_bwd(sig, dist, gw, dbgT, SR, dsig);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s = lane + 64 * q;
+      if (s < SR) d_feat[(r * SR + s) * CF] = dsig[q] * vv[q];
+    }
+  }
+}
+
 }  // namespace pnr
 
 using namespace pnr;
@@ -284,6 +486,56 @@ extern "C" int pnr_ray_march_fwd(const float* ray_dist, const uint8_t* ray_valid
   const unsigned grid = grid_for(NR * 64, kCBlock, 256 * 16);
   hipLaunchKernelGGL(k_ray_march_dense, dim3(grid), dim3(kCBlock), 0, as_stream(stream), ray_dist,
                      ray_valid, feat, bg, NR, SR, C, ray_color, opacity, acc_T, blend_w, bg_T);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_composite_bwd(const pnr_rays* rays, const pnr_query_params* q, const pnr_query_bufs* b,
+                                 const pnr_composite_params* c, const float* feat, const float* d_ray_color,
+                                 float* d_feat, void* stream) {
+  PNR_CHECK_ARG(rays && q && b && c && feat && d_ray_color && d_feat, "composite_bwd: null pointer");
+  PNR_CHECK_ARG(rays->campos_dev && rays->camrot_dev, "composite_bwd: camera required");
+  PNR_CHECK_ARG(q->SR >= 1 && q->SR <= 128, "composite_bwd: SR=%d unsupported (1..128)", q->SR);
+  PNR_CHECK_ARG(c->C >= 1 && c->C <= 128, "composite_bwd: C=%d unsupported (1..128)", c->C);
+  if (rays->R == 0) return PNR_OK;
+  CompBwdArgs a;
+  a.f.campos = rays->campos_dev;
+  a.f.camrot = rays->camrot_dev;
+  a.f.R = rays->R;
+  a.f.SR = q->SR;
+  a.f.n_filled = b->n_filled;
+  a.f.ray_off = b->ray_off;
+  a.f.ray_vcnt = b->ray_vcnt;
+  a.f.vflag = b->vflag;
+  a.f.valid_off = b->valid_off;
+  a.f.sample_p = b->sample_p;
+  a.f.feat = feat;
+  a.f.vsize_z = c->vsize_z;
+  a.f.unit = c->raydist_mode_unit;
+  a.f.C = c->C;
+  a.f.bg = c->bg_color;
+  a.f.ray_color = nullptr;
+  a.f.opacity = nullptr;
+  a.f.is_bg = nullptr;
+  a.f.ray_mask = nullptr;
+  a.d_color = d_ray_color;
+  a.d_feat = d_feat;
+  const unsigned grid = grid_for(rays->R * 64, kCBlock, 256 * 16);
+  hipLaunchKernelGGL(k_composite_bwd, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
+                                 const float* bg, int64_t NR, int32_t SR, int32_t C, const float* d_ray_color,
+                                 float* d_feat, void* stream) {
+  PNR_CHECK_ARG(ray_dist && ray_valid && feat && d_ray_color && d_feat, "ray_march_bwd: null pointer");
+  PNR_CHECK_ARG(SR >= 1 && SR <= 128, "ray_march_bwd: SR=%d unsupported (1..128)", SR);
+  PNR_CHECK_ARG(C >= 1, "ray_march_bwd: C must be >= 1");
+  if (NR == 0) return PNR_OK;
+  const unsigned grid = grid_for(NR * 64, kCBlock, 256 * 16);
+  hipLaunchKernelGGL(k_ray_march_dense_bwd, dim3(grid), dim3(kCBlock), 0, as_stream(stream), ray_dist, ray_valid,
+                     feat, bg, NR, SR, C, d_ray_color, d_feat);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

@@ -184,6 +184,47 @@ class NeuralPointsRayMarching(nn.Module):
         self.last_counts = totals
         return ray_color, opacity, is_bg, ray_mask
 
+    def render_rays_train(self, campos, camrot, raydir, near, far, bg_color):
+        """Differentiable render of one training ray batch [R,3] (SURVEY 8(a)
+        a17): same query / aggregate / composite as render_rays, with autograd
+        through pnr_aggregate_fwd_train -> pnr_aggregate_bwd_pairs and
+        pnr_composite_fwd -> pnr_composite_bwd (train.py).  Returns ray_color
+        [R,C] (requires grad w.r.t. points_embeding / color / dir / conf and the
+        aggregator parameters), opacity [R,SR], is_bg [R], ray_mask [R]."""
+        from .train import AggregateFn, AggSpec, CompositeFn, CompositeSpec, agg_params
+        opt = self.opt
+        dev = raydir.device
+        L.require_gpu(raydir)
+        np_ = self.neural_points
+        q = np_.querier
+        R = raydir.shape[0]
+        SR, K, C = opt.SR, opt.K, 128
+        bg = bg_color.to(dev).float().reshape(-1).contiguous() if bg_color is not None else None
+        if bg is not None and bg.numel() == 1:
+            bg = bg.expand(C).contiguous()
+        campos = campos.reshape(3).float().contiguous()
+        camrot = camrot.reshape(3, 3).float().contiguous()
+        rd = raydir.float().contiguous()
+        xyz = np_.xyz.detach().contiguous()
+        bufs, hp, rays, qp = q.run(xyz, rd, campos, camrot, near, far, bufs=None)
+        cnt = bufs.read_counts()
+        self.last_counts = cnt
+        Sv = cnt["S_valid"]
+        s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
+                      bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
+                      bufs.fill_rs.data_ptr(), SR, K)
+        n = xyz.shape[0]
+
+        def tab(t, c):
+            return None if t is None else t.reshape(n, c)
+
+        spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd))
+        feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
+                                 tab(np_.points_dir, 3), tab(np_.points_conf, 1), *agg_params(self.aggregator))
+        cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
+        cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(bg, campos, camrot, rd, hp))
+        return CompositeFn.apply(cspec, feat)
+
     def forward(self, campos, raydir, gt_image=None, bg_color=None, camrotc2w=None, pixel_idx=None,
                 near=None, far=None, focal=None, h=None, w=None, intrinsic=None, **kargs):
         """neural_points_volumetric_model.py:272-352 (+ fill_invalid :354-389);

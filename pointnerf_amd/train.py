@@ -1,0 +1,247 @@
+"""Autograd through the HIP path (the per-scene finetune step).
+
+``AggregateFn`` and ``CompositeFn`` are torch.autograd.Functions whose forward
+runs ``pnr_aggregate_fwd_train`` / ``pnr_composite_fwd`` and whose backward runs
+
+  colour branch backward      3 small GEMMs per layer on hipBLASLt (torch.matmul)
+  pnr_aggregate_bwd_pairs     fused per-pair dX chain on MFMA (k_pairs_bwd): alpha
+                              branch + K-sum backward, block3.2^T / block3.0^T /
+                              block1.2^T, LeakyReLU masks, weight / conf / colour /
+                              dir gradients, scatter-add of dz1 into the per-point
+                              block1.0 partial (the gather's index_add)
+  weight gradients            dW = dZ^T X over all pairs: plain GEMMs (hipBLASLt)
+  pnr_point_pe3(_bwd)         block1.0's point half: dW1[:, :224] = dP1^T X1,
+                              d emb = PE_3 backward of dP1 W1[:, :224]
+  pnr_composite_bwd           reverse scans of the alpha composite
+
+matching the autograd of point_aggregators.py:729-816 / 488-646,
+gradiant_clamp (:724-726), the gather (neural_points.py:788-799) and
+ray_march (diff_ray_marching.py:509-555).  Gradients are produced for
+points_embeding, points_color, points_dir, points_conf and every aggregator
+parameter; xyz gradients (xyz_grad) are not implemented.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+from .aggregator import frag_pack
+
+_PARAM_NAMES = ("block1.0.weight", "block1.0.bias", "block1.2.weight", "block1.2.bias",
+                "block3.0.weight", "block3.0.bias", "block3.2.weight", "block3.2.bias",
+                "alpha_branch.0.weight", "alpha_branch.0.bias",
+                "color_branch.0.weight", "color_branch.0.bias", "color_branch.2.weight",
+                "color_branch.2.bias", "color_branch.4.weight", "color_branch.4.bias")
+
+
+def agg_params(agg) -> list:
+    d = dict(agg.named_parameters())
+    return [d[n] for n in _PARAM_NAMES]
+
+
+def packed_bwd(agg):
+    """Transposed fragment packs for the backward GEMMs (pnr_mlp_bwd)."""
+    with torch.no_grad():
+        W3 = agg.block3[0].weight
+        t = dict(w4t=frag_pack(agg.block3[2].weight.t()), w3t=frag_pack(W3[:, :256].t()),
+                 w2t=frag_pack(agg.block1[2].weight.t()), w3e=W3[:, 256:263].float().contiguous())
+    m = L.MlpBwd(*(t[k].data_ptr() for k in ("w4t", "w3t", "w2t", "w3e")))
+    return m, t
+
+
+class Saved:
+    """Device activations kept by pnr_aggregate_fwd_train (pnr_agg_saved)."""
+
+    def __init__(self, n_max: int, device):
+        n = max(int(n_max), 1)
+        f = dict(dtype=torch.float32, device=device)
+        P = n * 8
+        self.t = dict(h1=torch.empty((P, 256), **f), h2=torch.empty((P, 256), **f),
+                      h3=torch.empty((P, 256), **f), h4=torch.empty((P, 256), **f),
+                      pe5=torch.empty((P, 60), **f), x3e=torch.empty((P, 8), **f), pa=torch.empty(P, **f),
+                      wt=torch.empty(P, **f), wn=torch.empty(P, **f),
+                      prow=torch.empty(P, dtype=torch.int32, device=device),
+                      hid=torch.zeros((n, 256), **f), vpe=torch.empty((n, 24), **f),
+                      hc1=torch.empty((n, 128), **f), hc2=torch.empty((n, 128), **f),
+                      hc3=torch.empty((n, 128), **f), vmask=torch.empty(n, dtype=torch.int32, device=device))
+        self.c = L.AggSaved(*(self.t[k].data_ptr() for k, _ in L.AggSaved._fields_))
+
+    def __getitem__(self, k):
+        return self.t[k]
+
+
+def _lrelu_grad(dy, h, slope):
+    return torch.where(h > 0, dy, dy * slope)
+
+
+class AggSpec:
+    """Non-tensor description of one aggregate call (structs + keep-alive)."""
+
+    def __init__(self, agg, samples: L.Samples, n: int, pts_extra: dict, pair_mask=None, keep=()):
+        self.agg, self.samples, self.n = agg, samples, int(n)
+        self.pts_extra = pts_extra      # xyz / pers / campos / camrot pointers (no grad)
+        self.pair_mask = pair_mask
+        self.keep = keep
+
+
+class AggregateFn(torch.autograd.Function):
+    """feat[n_max, 129] = aggregate(point tables, MLP); differentiable in emb,
+    color, dir, conf and the 16 aggregator parameters."""
+
+    @staticmethod
+    def forward(ctx, spec: AggSpec, emb, color, dirs, conf, *params):
+        dev = emb.device
+        agg = spec.agg
+        s = spec.samples
+        n_max = int(s.n_max)
+        N = emb.shape[0]
+        tabs = [emb.detach().contiguous(), None if color is None else color.detach().contiguous(),
+                None if dirs is None else dirs.detach().contiguous(),
+                None if conf is None else conf.detach().reshape(-1).contiguous()]
+        pe = spec.pts_extra
+        pts = L.Points(N, pe["xyz"].data_ptr(), L.ptr(pe.get("pers")), tabs[0].data_ptr(), L.ptr(tabs[1]),
+                       L.ptr(tabs[2]), L.ptr(tabs[3]), L.ptr(pe.get("campos")), L.ptr(pe.get("camrot")))
+        mlp, keepw = agg.packed()
+        sv = Saved(n_max, dev)
+        feat = torch.zeros((max(n_max, 1), 129), dtype=torch.float32, device=dev)
+        scratch = L.aggregate_scratch(max(n_max, 1), N, dev)
+        if spec.pair_mask is None:
+            L.check(L.lib().pnr_aggregate_fwd_train(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
+                                                    ctypes.byref(sv.c), L.ptr(feat), None, None, L.ptr(scratch),
+                                                    scratch.numel() * 4, L.stream_ptr(dev)),
+                    "pnr_aggregate_fwd_train")
+        else:
+            L.check(L.lib().pnr_aggregate_fwd_train_masked(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
+                                                           L.ptr(spec.pair_mask), ctypes.byref(sv.c), L.ptr(feat),
+                                                           None, None, L.ptr(scratch), scratch.numel() * 4,
+                                                           L.stream_ptr(dev)),
+                    "pnr_aggregate_fwd_train_masked")
+        ctx.spec, ctx.sv, ctx.pts, ctx.tabs, ctx.mlp, ctx.keepw = spec, sv, pts, tabs, mlp, keepw
+        ctx.has = (color is not None, dirs is not None, conf is not None)
+        ctx.shapes = (emb.shape, None if conf is None else conf.shape)
+        ctx.save_for_backward(*params)
+        return feat
+
+    @staticmethod
+    def backward(ctx, d_feat):
+        spec, sv = ctx.spec, ctx.sv
+        agg = spec.agg
+        params = ctx.saved_tensors
+        P = dict(zip(_PARAM_NAMES, params))
+        dev = d_feat.device
+        n = spec.n
+        n_max = int(spec.samples.n_max)
+        N = ctx.tabs[0].shape[0]
+        slope = float(agg.neg_slope)
+        d_feat = d_feat.contiguous()
+        f32 = dict(dtype=torch.float32, device=dev)
+        grads = {}
+        # ---- colour branch (color_branch.{0,2,4}: 280 -> 128 -> 128 -> 128, LeakyReLU each)
+        vm = (sv["vmask"][:n] != 0).float()[:, None]
+        dc = d_feat[:n, 1:] * vm
+        hc1, hc2, hc3 = sv["hc1"][:n], sv["hc2"][:n], sv["hc3"][:n]
+        y0 = torch.cat([sv["hid"][:n], sv["vpe"][:n]], 1)
+        dz = _lrelu_grad(dc, hc3, slope)
+        grads["color_branch.4.weight"], grads["color_branch.4.bias"] = dz.t() @ hc2, dz.sum(0)
+        dz = _lrelu_grad(dz @ P["color_branch.4.weight"], hc2, slope)
+        grads["color_branch.2.weight"], grads["color_branch.2.bias"] = dz.t() @ hc1, dz.sum(0)
+        dz = _lrelu_grad(dz @ P["color_branch.2.weight"], hc1, slope)
+        grads["color_branch.0.weight"], grads["color_branch.0.bias"] = dz.t() @ y0, dz.sum(0)
+        d_hid = torch.zeros((max(n_max, 1), 256), **f32)
+        d_hid[:n] = dz @ P["color_branch.0.weight"][:, :256]
+        # ---- per-pair chain on MFMA
+        Pn = max(n_max, 1) * 8
+        dz1, dz2, dz3, dz4 = (torch.empty((Pn, 256), **f32) for _ in range(4))
+        dpa = torch.empty(Pn, **f32)
+        d_p1 = torch.zeros((N, 256), **f32)
+        has_c, has_d, has_f = ctx.has
+        d_color = torch.zeros((N, 3), **f32) if has_c else None
+        d_dir = torch.zeros((N, 3), **f32) if has_d else None
+        d_conf = torch.zeros(N, **f32) if has_f else None
+        wb, _keepb = packed_bwd(agg)
+        L.check(L.lib().pnr_aggregate_bwd_pairs(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(sv.c),
+                                                L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3),
+                                                L.ptr(dz4), L.ptr(dpa), L.ptr(d_p1), L.ptr(d_color), L.ptr(d_dir),
+                                                L.ptr(d_conf), L.stream_ptr(dev)),
+                "pnr_aggregate_bwd_pairs")
+        m = n * 8
+        dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
+        h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
+        grads["block3.2.weight"], grads["block3.2.bias"] = dz4.t() @ h3, dz4.sum(0)
+        x3 = torch.cat([h2, sv["x3e"][:m, :7]], 1)
+        grads["block3.0.weight"], grads["block3.0.bias"] = dz3.t() @ x3, dz3.sum(0)
+        grads["block1.2.weight"], grads["block1.2.bias"] = dz2.t() @ h1, dz2.sum(0)
+        grads["alpha_branch.0.weight"], grads["alpha_branch.0.bias"] = (dpa[None, :] @ h4), dpa.sum(0, keepdim=True)
+        # ---- block1.0: pair half from dz1 / PE_5, point half from dP1 / X1
+        emb = ctx.tabs[0]
+        x1 = torch.empty((N, 224), **f32)
+        L.check(L.lib().pnr_point_pe3(L.ptr(emb), N, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
+        gW1 = torch.empty((256, 284), **f32)
+        gW1[:, :224] = d_p1.t() @ x1
+        gW1[:, 224:] = dz1.t() @ sv["pe5"][:m]
+        grads["block1.0.weight"], grads["block1.0.bias"] = gW1, dz1.sum(0)
+        dx1 = (d_p1 @ P["block1.0.weight"][:, :224]).contiguous()
+        d_emb = torch.zeros((N, 32), **f32)
+        L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), N, L.ptr(d_emb), L.stream_ptr(dev)),
+                "pnr_point_pe3_bwd")
+        emb_shape, conf_shape = ctx.shapes
+        out = [None, d_emb.view(emb_shape), d_color, d_dir, None if d_conf is None else d_conf.view(conf_shape)]
+        out += [grads[k] for k in _PARAM_NAMES]
+        return tuple(out)
+
+
+class CompositeSpec:
+    def __init__(self, rays, qp, bufs, cp, R, SR, C, keep=()):
+        self.rays, self.qp, self.bufs, self.cp = rays, qp, bufs, cp
+        self.R, self.SR, self.C = R, SR, C
+        self.keep = keep
+
+
+class CompositeFn(torch.autograd.Function):
+    """ray_color[R, C] = composite(feat[S_valid, C+1]); opacity / is_bg / mask
+    are returned as non-differentiable outputs."""
+
+    @staticmethod
+    def forward(ctx, spec: CompositeSpec, feat):
+        dev = feat.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        R, SR, C = spec.R, spec.SR, spec.C
+        ray_color = torch.empty((R, C), **f32)
+        opacity = torch.empty((R, SR), **f32)
+        is_bg = torch.empty((R,), **f32)
+        ray_mask = torch.empty((R,), dtype=torch.int8, device=dev)
+        feat_c = feat.detach().contiguous()
+        L.check(L.lib().pnr_composite_fwd(ctypes.byref(spec.rays), ctypes.byref(spec.qp), ctypes.byref(spec.bufs.c),
+                                          ctypes.byref(spec.cp), L.ptr(feat_c), L.ptr(ray_color), L.ptr(opacity),
+                                          L.ptr(is_bg), L.ptr(ray_mask), L.stream_ptr(dev)),
+                "pnr_composite_fwd")
+        ctx.spec, ctx.feat = spec, feat_c
+        ctx.mark_non_differentiable(opacity, is_bg, ray_mask)
+        return ray_color, opacity, is_bg, ray_mask
+
+    @staticmethod
+    def backward(ctx, d_color, _d_op, _d_bg, _d_mask):
+        spec = ctx.spec
+        dev = ctx.feat.device
+        d_feat = torch.zeros_like(ctx.feat)
+        if d_color is None:
+            return None, d_feat
+        d_color = d_color.contiguous()
+        L.check(L.lib().pnr_composite_bwd(ctypes.byref(spec.rays), ctypes.byref(spec.qp), ctypes.byref(spec.bufs.c),
+                                          ctypes.byref(spec.cp), L.ptr(ctx.feat), L.ptr(d_color), L.ptr(d_feat),
+                                          L.stream_ptr(dev)),
+                "pnr_composite_bwd")
+        return None, d_feat
+
+
+def ray_march_bwd(ray_dist, ray_valid, feat, bg, d_color):
+    """d feat of pnr_ray_march_fwd (dense mirror) for a given d ray_color."""
+    NR, SR, CF = feat.shape
+    d_feat = torch.zeros_like(feat)
+    L.check(L.lib().pnr_ray_march_bwd(L.ptr(ray_dist), L.ptr(ray_valid), L.ptr(feat), L.ptr(bg), NR, SR, CF - 1,
+                                      L.ptr(d_color.contiguous()), L.ptr(d_feat), L.stream_ptr(feat.device)),
+            "pnr_ray_march_bwd")
+    return d_feat

@@ -1,0 +1,158 @@
+"""Backward pass of the HIP path against the reference's own
+autograd gradients (golden) and the differentiable CPU oracle.
+
+Tolerance (fp32 throughout): |d| <= s * max|ref| + 1e-4 * |ref| per tensor
+with s = 1e-5 for the golden cases; end to end s = 5e-5 for the point
+tables (one point's gradient sums up to ~100 (sample, neighbour) pairs with
+cancellation) and 3e-4 for the MLP weights (sums over ~1e5 pairs through three
+backpropagated layers, plus LeakyReLU kinks where a pre-activation within
+fp32 noise of 0 takes the other slope) -- the backward reorders those fp32 sums (atomics into
+point rows, GEMM blocking), so it is not bitwise."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from formula import formula_params
+from oracle import oracle as O
+from oracle import oracle_grad as OG
+from scenes import scene
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, ref, name, rel=1e-4, scale=1e-5):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    ref = ref.detach().cpu().numpy() if torch.is_tensor(ref) else np.asarray(ref)
+    tol = scale * max(float(np.abs(ref).max()), 1e-30) + rel * np.abs(ref)
+    bad = np.abs(a - ref) > tol
+    assert not bad.any(), (f"{name}: {bad.sum()} / {bad.size} outside tol, max |d| {np.abs(a - ref).max():.3e}, "
+                           f"max |ref| {np.abs(ref).max():.3e}")
+
+
+def test_ray_march_bwd_vs_reference_golden(golden_dir, cuda):
+    from pointnerf_amd.train import ray_march_bwd
+    g = np.load(os.path.join(golden_dir, "raymarch.npz"), allow_pickle=False)
+    gb = np.load(os.path.join(golden_dir, "raymarch_bwd.npz"), allow_pickle=False)
+    rd = torch.from_numpy(g["ray_dist"][0]).to(cuda).contiguous()
+    rv = torch.from_numpy(g["ray_valid"][0]).to(cuda).to(torch.uint8).contiguous()
+    rf = torch.from_numpy(g["ray_features"][0]).to(cuda).contiguous()
+    bg = torch.from_numpy(g["bg_color"]).to(cuda)
+    d = ray_march_bwd(rd, rv, rf, bg, torch.from_numpy(gb["g_color"][0]).to(cuda))
+    close(d, gb["g_features"][0], "d ray_features")
+
+
+def test_aggregator_bwd_vs_reference_golden(golden_dir, cuda):
+    from pointnerf_amd.aggregator import PointAggregator
+    from pointnerf_amd.options import lego_opt
+    g = np.load(os.path.join(golden_dir, "aggregator.npz"), allow_pickle=False)
+    gb = np.load(os.path.join(golden_dir, "aggregator_bwd.npz"), allow_pickle=False)
+    agg = PointAggregator(lego_opt()).to(cuda)
+    agg.load_state_dict({k: torch.from_numpy(v) for k, v in formula_params().items()})
+    agg.train()
+    t = {k: torch.from_numpy(np.ascontiguousarray(g[k])).to(cuda) for k in
+         ("sampled_color", "sampled_dir", "sampled_conf", "sampled_embedding", "sampled_xyz_pers",
+          "sampled_xyz", "sample_pnt_mask", "sample_loc", "sample_loc_w", "sample_ray_dirs")}
+    leaves = ("sampled_color", "sampled_dir", "sampled_conf", "sampled_embedding")
+    for k in leaves:
+        t[k].requires_grad_(True)
+    out, _, _, _ = agg(t["sampled_color"], torch.eye(3, device=cuda), t["sampled_dir"], t["sampled_conf"],
+                       t["sampled_embedding"], t["sampled_xyz_pers"], t["sampled_xyz"], t["sample_pnt_mask"],
+                       t["sample_loc"], t["sample_loc_w"], t["sample_ray_dirs"], [0.004] * 3, 0)
+    close(out, gb["features"], "features", rel=1e-4, scale=1e-5)
+    (out * torch.from_numpy(gb["g_feat"]).to(cuda)).sum().backward()
+    for k in leaves:
+        close(t[k].grad, gb["g_" + k], "d " + k)
+    for k, p in agg.named_parameters():
+        close(p.grad, gb["gp_" + k.replace(".", "_")], "d " + k)
+
+
+def _train_model(sc, cuda, params):
+    from pointnerf_amd.aggregator import PointAggregator
+    from pointnerf_amd.renderer import NeuralPoints, NeuralPointsRayMarching
+    agg = PointAggregator(sc["opt"]).to(cuda)
+    agg.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
+                       torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]))
+    return NeuralPointsRayMarching(sc["opt"], np_, agg.train())
+
+
+def test_render_train_grads_vs_oracle(cuda):
+    """End to end: loss = <G, ray_color> through query -> aggregate -> composite;
+    every point-table and MLP gradient vs torch autograd of the CPU oracle."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    params = formula_params(salt=0.3)
+    m = _train_model(sc, cuda, params)
+    campos = torch.from_numpy(sc["campos"]).to(cuda)
+    camrot = torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    color, opacity, is_bg, ray_mask = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)
+    G = torch.randn(color.shape, generator=torch.Generator().manual_seed(5)).to(cuda)
+    (color * G).sum().backward()
+    # oracle: same neighbours (the query is bit-exact vs oracle, test_gpu_query), torch autograd
+    opt = sc["opt"]
+    q = O.query_points(opt, sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
+    assert np.array_equal(ray_mask.cpu().numpy(), q["ray_mask"])
+    tp = {k: torch.from_numpy(np.ascontiguousarray(sc[k])).requires_grad_(True) for k in ("emb", "color", "dir", "conf")}
+    pp = {k: torch.from_numpy(v).requires_grad_(True) for k, v in params.items()}
+    pidx = torch.from_numpy(q["sample_pidx"]).long()
+    mask = pidx >= 0
+    idx = pidx.clamp(min=0).reshape(-1)
+    shp = tuple(pidx.shape)
+    xyz = torch.from_numpy(sc["xyz"])
+    pers = torch.from_numpy(O.w2pers(sc["xyz"], sc["campos"], sc["camrot"]))
+    gsel = lambda a, c: a.reshape(-1, c)[idx].reshape(shp + (c,))  # noqa: E731
+    feats, rv, _, _ = OG.aggregate(pp, gsel(tp["color"], 3), gsel(tp["dir"], 3), gsel(tp["conf"], 1),
+                                   gsel(tp["emb"], 32), gsel(pers, 3), gsel(xyz, 3), mask,
+                                   torch.from_numpy(q["sample_loc"]), torch.from_numpy(q["sample_loc_w"]),
+                                   torch.from_numpy(q["sample_ray_dirs"]))
+    rdist = torch.from_numpy(O.ray_dist(q["sample_loc"], rv.numpy(), opt.vsize[2], opt.raydist_mode_unit))
+    c_ref = OG.ray_march(rdist, rv, feats, torch.from_numpy(sc["bg"]))
+    mk = torch.from_numpy(q["ray_mask"] > 0)
+    Gc = G.cpu()[mk]
+    close(color[mk.to(cuda)], c_ref, "ray_color", rel=1e-4, scale=2e-5)
+    (c_ref * Gc).sum().backward()
+    npts = m.neural_points
+    errs = []
+
+    def check(a, ref, name, scale=5e-5):
+        try:
+            close(a, ref, name, scale=scale)
+        except AssertionError as e:
+            errs.append(str(e).splitlines()[0])
+
+    check(npts.points_embeding.grad.reshape(-1, 32), tp["emb"].grad, "d points_embeding")
+    check(npts.points_color.grad.reshape(-1, 3), tp["color"].grad, "d points_color")
+    check(npts.points_dir.grad.reshape(-1, 3), tp["dir"].grad, "d points_dir")
+    check(npts.points_conf.grad.reshape(-1, 1), tp["conf"].grad, "d points_conf")
+    for k, p in m.aggregator.named_parameters():
+        # weight gradients sum over every pair of the batch (~1e5 terms), and a
+        # pre-activation within fp32 noise of 0 may take the other LeakyReLU
+        # slope than on the CPU (forward sums differ in order)
+        check(p.grad, pp[k].grad, "d " + k, scale=3e-4)
+    assert not errs, errs
+
+
+def test_train_step_reduces_loss(cuda):
+    """A few Adam steps on the point features + MLP lower a colour loss."""
+    sc = scene(8000, H=24, W=24, theta=10.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.7))
+    campos = torch.from_numpy(sc["campos"]).to(cuda)
+    camrot = torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    target = torch.rand((rd.shape[0], 3), generator=torch.Generator().manual_seed(3)).to(cuda)
+    ps = [p for p in m.parameters() if p.requires_grad]
+    optim = torch.optim.Adam(ps, lr=1e-3)
+    losses = []
+    for _ in range(6):
+        optim.zero_grad()
+        color, _, _, _ = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)
+        loss = torch.mean((color[:, :3] - target) ** 2)
+        loss.backward()
+        optim.step()
+        losses.append(float(loss))
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0]
