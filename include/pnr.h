@@ -204,6 +204,12 @@ typedef struct {
   const float* conf;    /* [N] or NULL (conf = 1)                                   */
   const float* campos;  /* [3] needed when pers == NULL                             */
   const float* camrot;  /* [3,3] needed when pers == NULL                           */
+  const int32_t* used;  /* optional [n_used] point rows the samples reference (NULL = all
+                           n rows): block1.0's point half (scratch P1) is then computed
+                           for these rows only -- the training-batch case            */
+  int64_t n_used;
+  const int32_t* used_map; /* [n] row -> index into used (-1 = unreferenced); required
+                              with used                                              */
 } pnr_points;
 
 typedef struct {
@@ -225,7 +231,8 @@ typedef struct {
  * out_feat[v, 0] = alpha, out_feat[v, 1..128] = colour features (rows of
  * samples without neighbours are left untouched).  Optional (may be NULL):
  * out_weight[row,K] normalised weights, out_conf[row,K] clamped confidence.
- * scratch: 16-B aligned device buffer of pnr_aggregate_scratch_bytes(n_max, N).
+ * scratch: 16-B aligned device buffer of pnr_aggregate_scratch_bytes(n_max, N)
+ * (N = pts->n_used when pts->used is set).
  * Block1.0 is split exactly: W1[:, :224].[emb, PE(emb)] + b1 depends only on
  * the point, so it is computed once per point (N x 256) and gathered per
  * pair; only the 60 distance-PE columns run per (sample, neighbour) pair. */
@@ -282,7 +289,8 @@ int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, 
  * d_hid[n,256] (gradient of the K-summed features from the colour branch).
  * Writes dz1..dz4[n_max*8,256] (gradients of the four pre-activations; rows
  * of empty pairs are 0) and dpa[n_max*8]; accumulates (atomically, so the
- * caller zeroes them) d_p1[N,256] += dz1 per point (block1.0 point half),
+ * caller zeroes them) d_p1[N,256] += dz1 per point (block1.0 point half; rows
+ * are used_map[point] when pts->used is set, i.e. d_p1 is [n_used,256]),
  * d_color[N,3], d_dir[N,3], d_conf[N] (straight-through clamp gradient).
  * Any of d_color / d_dir / d_conf may be NULL. */
 int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,

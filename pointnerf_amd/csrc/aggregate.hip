@@ -203,15 +203,16 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_point_pre(AggArgs A) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* X = lds_dyn + wid * kWaveLds;
   const int m = lane & 31, h = lane >> 5;
-  const int64_t np = A.pts.n;
+  const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;   // P1 rows
   const int64_t ntiles = cdiv(np, 32);
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t pt = tile * 32 + m;
+    const int64_t pt = tile * 32 + m;                         // P1 row
     const bool act = pt < np;
+    const int64_t prow = act ? (A.pts.used ? (int64_t)A.pts.used[pt] : pt) : 0;   // point row
     // lane half h owns embedding channels [16h, 16h+16): the channel itself (row c)
     // and its 3-band PE (rows 32 + 2(3c+f) + {0: sin, 1: cos}); angle doubling
     // from one sincos: sin 2x = 2 sin x cos x, cos 2x = (c - s)(c + s).
-    const float* e = A.pts.emb + (act ? pt : 0) * kEmb + 16 * h;
+    const float* e = A.pts.emb + prow * kEmb + 16 * h;
 #pragma unroll 1
     for (int q = 0; q < 4; ++q) {
       float4 e4 = act ? reinterpret_cast<const float4*>(e)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -540,7 +541,8 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
       const int64_t pr_pt = __shfl(prow, 32 * pt + c);
       const bool v_pt = __shfl((int)valid, 32 * pt + c) != 0;
       if (v_pt && !(PNR_ABLATE & 1)) {
-        const float4* pr = reinterpret_cast<const float4*>(A.p1 + pr_pt * kHid);
+        const int64_t p1r = A.pts.used_map ? (int64_t)A.pts.used_map[pr_pt] : pr_pt;
+        const float4* pr = reinterpret_cast<const float4*>(A.p1 + p1r * kHid);
 #pragma unroll
         for (int T = 0; T < kNTW; ++T)
 #pragma unroll
@@ -756,7 +758,8 @@ int launch_t(const AggArgs& a, hipStream_t st) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     attr = true;
   }
-  hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.n, 32), 4, 256)), dim3(kAggBlock), kAggLdsBytes,
+  hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.used ? a.pts.n_used : a.pts.n, 32), 4, 256)),
+                     dim3(kAggBlock), kAggLdsBytes,
                      st, a);
   PNR_LAUNCH_CHECK();
   const int64_t tiles = cdiv(a.s.n_max, kTS);
@@ -1013,7 +1016,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       const bool act = tile * kTS + (col >> 3) < n;
       const int32_t pr = act ? A.sv.prow[tile * kTP + col] : -1;
       if (pr < 0) continue;
-      float* dst = A.d_p1 + (int64_t)pr * kHid;
+      float* dst = A.d_p1 + (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr) * kHid;
 #pragma unroll
       for (int T = 0; T < kNTW; ++T)
 #pragma unroll
@@ -1088,7 +1091,9 @@ int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, 
   PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0, "aggregate: emb must be 16-B aligned");
   PNR_CHECK_ARG(scratch && ((uintptr_t)scratch & 15) == 0, "aggregate: 16-B aligned scratch required");
   PNR_CHECK_ARG(pts->n > 0, "aggregate: empty point table");
-  PNR_CHECK_ARG(scratch_bytes >= scratch_need(s->n_max, pts->n),
+  PNR_CHECK_ARG(!pts->used || (pts->used_map && pts->n_used >= 0 && pts->n_used <= pts->n),
+                "aggregate: used list needs used_map and 0 <= n_used <= n");
+  PNR_CHECK_ARG(scratch_bytes >= scratch_need(s->n_max, pts->used ? pts->n_used : pts->n),
                 "aggregate: scratch too small (%zu bytes for %lld samples, %lld points)", scratch_bytes,
                 (long long)s->n_max, (long long)pts->n);
   return PNR_OK;

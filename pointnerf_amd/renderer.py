@@ -218,7 +218,11 @@ class NeuralPointsRayMarching(nn.Module):
         def tab(t, c):
             return None if t is None else t.reshape(n, c)
 
-        spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd))
+        # block1.0's point half only for the points this batch references
+        from .train import used_points
+        used = used_points(bufs.pidx[:cnt["S_filled"] * K], n)
+        spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd),
+                       used=used)
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
                                  tab(np_.points_dir, 3), tab(np_.points_conf, 1), *agg_params(self.aggregator))
         cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))

@@ -72,6 +72,16 @@ class Saved:
         return self.t[k]
 
 
+def used_points(pidx: torch.Tensor, n_points: int):
+    """(used, used_map): sorted point rows referenced by a query's sample_pidx
+    and the inverse map (-1 = unreferenced) -- pnr_points.used / used_map."""
+    ids = pidx[pidx >= 0]
+    used = torch.unique(ids).to(torch.int32)
+    used_map = torch.full((n_points,), -1, dtype=torch.int32, device=pidx.device)
+    used_map[used.long()] = torch.arange(used.numel(), dtype=torch.int32, device=pidx.device)
+    return used, used_map
+
+
 def _lrelu_grad(dy, h, slope):
     return torch.where(h > 0, dy, dy * slope)
 
@@ -79,8 +89,9 @@ def _lrelu_grad(dy, h, slope):
 class AggSpec:
     """Non-tensor description of one aggregate call (structs + keep-alive)."""
 
-    def __init__(self, agg, samples: L.Samples, n: int, pts_extra: dict, pair_mask=None, keep=()):
+    def __init__(self, agg, samples: L.Samples, n: int, pts_extra: dict, pair_mask=None, keep=(), used=None):
         self.agg, self.samples, self.n = agg, samples, int(n)
+        self.used = used                # optional (used[int32], used_map[int32]) point subset
         self.pts_extra = pts_extra      # xyz / pers / campos / camrot pointers (no grad)
         self.pair_mask = pair_mask
         self.keep = keep
@@ -103,10 +114,15 @@ class AggregateFn(torch.autograd.Function):
         pe = spec.pts_extra
         pts = L.Points(N, pe["xyz"].data_ptr(), L.ptr(pe.get("pers")), tabs[0].data_ptr(), L.ptr(tabs[1]),
                        L.ptr(tabs[2]), L.ptr(tabs[3]), L.ptr(pe.get("campos")), L.ptr(pe.get("camrot")))
+        n_p1 = N
+        if spec.used is not None:
+            used, used_map = spec.used
+            pts.used, pts.n_used, pts.used_map = used.data_ptr(), used.numel(), used_map.data_ptr()
+            n_p1 = used.numel()
         mlp, keepw = agg.packed()
         sv = Saved(n_max, dev)
         feat = torch.zeros((max(n_max, 1), 129), dtype=torch.float32, device=dev)
-        scratch = L.aggregate_scratch(max(n_max, 1), N, dev)
+        scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
         if spec.pair_mask is None:
             L.check(L.lib().pnr_aggregate_fwd_train(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
                                                     ctypes.byref(sv.c), L.ptr(feat), None, None, L.ptr(scratch),
@@ -155,7 +171,9 @@ class AggregateFn(torch.autograd.Function):
         Pn = max(n_max, 1) * 8
         dz1, dz2, dz3, dz4 = (torch.empty((Pn, 256), **f32) for _ in range(4))
         dpa = torch.empty(Pn, **f32)
-        d_p1 = torch.zeros((N, 256), **f32)
+        used = None if spec.used is None else spec.used[0]
+        n_p1 = N if used is None else used.numel()
+        d_p1 = torch.zeros((max(n_p1, 1), 256), **f32)
         has_c, has_d, has_f = ctx.has
         d_color = torch.zeros((N, 3), **f32) if has_c else None
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
@@ -176,17 +194,22 @@ class AggregateFn(torch.autograd.Function):
         grads["block1.2.weight"], grads["block1.2.bias"] = dz2.t() @ h1, dz2.sum(0)
         grads["alpha_branch.0.weight"], grads["alpha_branch.0.bias"] = (dpa[None, :] @ h4), dpa.sum(0, keepdim=True)
         # ---- block1.0: pair half from dz1 / PE_5, point half from dP1 / X1
-        emb = ctx.tabs[0]
-        x1 = torch.empty((N, 224), **f32)
-        L.check(L.lib().pnr_point_pe3(L.ptr(emb), N, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
+        emb = ctx.tabs[0] if used is None else ctx.tabs[0].index_select(0, used.long()).contiguous()
+        d_p1 = d_p1[:n_p1]
+        x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
+        L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
         gW1 = torch.empty((256, 284), **f32)
         gW1[:, :224] = d_p1.t() @ x1
         gW1[:, 224:] = dz1.t() @ sv["pe5"][:m]
         grads["block1.0.weight"], grads["block1.0.bias"] = gW1, dz1.sum(0)
         dx1 = (d_p1 @ P["block1.0.weight"][:, :224]).contiguous()
-        d_emb = torch.zeros((N, 32), **f32)
-        L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), N, L.ptr(d_emb), L.stream_ptr(dev)),
+        d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
+        L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb_u), L.stream_ptr(dev)),
                 "pnr_point_pe3_bwd")
+        if used is None:
+            d_emb = d_emb_u
+        else:
+            d_emb = torch.zeros((N, 32), **f32).index_copy_(0, used.long(), d_emb_u[:n_p1])
         emb_shape, conf_shape = ctx.shapes
         out = [None, d_emb.view(emb_shape), d_color, d_dir, None if d_conf is None else d_conf.view(conf_shape)]
         out += [grads[k] for k in _PARAM_NAMES]

@@ -153,6 +153,6 @@ def test_train_step_reduces_loss(cuda):
         loss = torch.mean((color[:, :3] - target) ** 2)
         loss.backward()
         optim.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
