@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=1500, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--mode", choices=("render", "train"), default="render",
+                    help="render: the headline forward frame render; train: the per-scene finetune "
+                         "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
+    ap.add_argument("--train-rays", type=int, default=3600, help="rays per train step (random_sample_size 60^2)")
     return ap.parse_args()
 
 
@@ -145,8 +149,65 @@ def stage_rooflines(args, opt, model, stage, per, launches):
     return res
 
 
+def run_train(args, device):
+    """Finetune step: random batch of pixels of one of
+    8 cameras -> query -> aggregate (training forward) -> composite -> MSE on
+    the first 3 colour channels vs a synthetic target -> backward through the
+    HIP kernels -> Adam on points_embeding/color/dir/conf and the aggregator."""
+    opt, pts, feats, agg, model = build_scene(args, device)
+    agg.train()
+    H = W = args.hw
+    cams = cameras(8, H, W)
+    dev_cams = [tuple(torch.from_numpy(x).to(device) for x in c) for c in cams]
+    bg = torch.from_numpy(np.random.default_rng(1).uniform(size=128).astype(np.float32)).to(device)
+    target = torch.rand((H * W, 3), generator=torch.Generator().manual_seed(2)).to(device)
+    params = [p for p in model.parameters() if p.requires_grad]
+    optim = torch.optim.Adam(params, lr=5e-4, fused=True)
+    gen = torch.Generator(device=device).manual_seed(0)
+    stats = {"pairs": 0, "valid": 0, "filled": 0}
+
+    def step(i, timed):
+        campos, camrot, rd = dev_cams[i % len(dev_cams)]
+        sel = torch.randint(0, H * W, (args.train_rays,), generator=gen, device=device)
+        optim.zero_grad(set_to_none=True)
+        color, _, _, _ = model.render_rays_train(campos, camrot, rd[sel], opt.near_plane, opt.far_plane, bg)
+        loss = torch.mean((color[:, :3] - target[sel]) ** 2)
+        loss.backward()
+        optim.step()
+        if timed:
+            c = model.last_counts
+            stats["pairs"] += c["n_pairs"]
+            stats["valid"] += c["S_valid"]
+            stats["filled"] += c["S_filled"]
+
+    for i in range(args.warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, True)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    k = max(args.steps, 1)
+    flops = 3.0 * (stats["pairs"] * FLOP_PER_PAIR + stats["valid"] * FLOP_PER_SAMPLE) / k  # fwd + 2x bwd GEMMs
+    ms = t / k * 1e3
+    print(json.dumps({
+        "metric": "train steps/s (fwd+bwd+Adam, 3600-ray batches), 2M neural points",
+        "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic (seeded lego-like point cloud, random target colours)",
+        "config": {"workload": f"finetune step, {args.train_rays} random rays of {H}x{W} frames, {args.points} points",
+                   "K": opt.K, "SR": opt.SR},
+        "ray_samples_per_s_M": round(args.train_rays * opt.SR / (ms * 1e-3) / 1e6, 3),
+        "gemm_tflops_per_s": round(flops / (ms * 1e-3) / 1e12, 3),
+        "counts_per_step": {k2: v // k for k2, v in stats.items()}}), flush=True)
+
+
 def main():
     args = parse()
+    if args.mode == "train":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        return run_train(args, torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

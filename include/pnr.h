@@ -256,8 +256,10 @@ int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const 
 typedef struct {
   float* h1; float* h2; float* h3; float* h4;  /* [n_max*8,256] post-activation outputs of
                                                   block1.0, block1.2, block3.0, block3.2 */
-  float* pe5;      /* [n_max*8,60] PE_5 of the rotated 6-d distance (block1.0 cols 224..283) */
-  float* x3e;      /* [n_max*8,8]  block3.0 inputs 256..262 (colour, R.dir - R.v, <R.dir,R.v>), 1 */
+  float* pe5;      /* [n_max*8,64] PE_5 of the rotated 6-d distance (block1.0 cols 224..283),
+                      columns 60..63 zero (GEMM padding)                                        */
+  float* x3e;      /* [n_max*8,32] block3.0 inputs 256..262 (colour, R.dir - R.v, <R.dir,R.v>),
+                      1, then zeros (GEMM padding)                                              */
   float* pa;       /* [n_max*8]    alpha_branch.0 output (before softplus(x - 1))              */
   float* wt;       /* [n_max*8]    w_k * clamp(conf_k); 0 for empty pairs                      */
   float* wn;       /* [n_max*8]    normalised distance weight w_k                              */
@@ -266,6 +268,9 @@ typedef struct {
   float* vpe;      /* [n_max,24]   view-direction PE (colour-branch input 256..279)            */
   float* hc1; float* hc2; float* hc3;  /* [n_max,128] colour-branch activations              */
   int32_t* vmask;  /* [n_max]      sample has >= 1 valid neighbour                             */
+  uint16_t* mask;  /* [n_max*8,64] LeakyReLU derivative bits of the four 256-wide layers
+                      (layer l, tile T, lane half h: word 16l + 2T + h; bit r = pre-activation
+                      of MFMA accumulator register r > 0), read by the backward            */
 } pnr_agg_saved;
 
 /* Transposed weights for the backward GEMMs, fragment-packed like pnr_mlp
@@ -298,6 +303,14 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             const float* d_feat, const float* d_hid, float* dz1, float* dz2,
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
+
+/* Weight-gradient GEMM: C[M,N] = A^T B over K rows (A[K,M], B[K,N] row-major,
+ * leading dimensions lda/ldb), colsum_a[M] = column sums of A (bias gradient,
+ * may be NULL).  M, N multiples of 32.  Split-K on MFMA with a deterministic
+ * ordered reduction; scratch of pnr_gemm_tn_scratch_bytes(K, M, N). */
+int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t* out);
+int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
+                float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream);
 
 /* X1[p] = [emb_p, PE_3(emb_p)] (block1.0 columns 0..223) for p < n, and the
  * matching backward d_emb[p] += dX1[p] . dX1/d emb (networks.py:175-190). */

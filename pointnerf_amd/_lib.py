@@ -82,7 +82,7 @@ class CompositeParams(ctypes.Structure):
 
 class AggSaved(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("h1", "h2", "h3", "h4", "pe5", "x3e", "pa", "wt", "wn", "prow", "hid",
-                                        "vpe", "hc1", "hc2", "hc3", "vmask")]
+                                        "vpe", "hc1", "hc2", "hc3", "vmask", "mask")]
 
 
 class MlpBwd(ctypes.Structure):
@@ -116,6 +116,9 @@ SIGNATURES = {
     "pnr_aggregate_bwd_pairs": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(AggSaved), c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_gemm_tn_scratch_bytes": (c_int, [c_int64, c_int32, c_int32, P(c_size_t)]),
+    "pnr_gemm_tn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                            c_void_p, c_size_t, c_void_p]),
     "pnr_point_pe3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_point_pe3_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_composite_bwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams), c_void_p,
@@ -177,6 +180,22 @@ def aggregate_scratch(n_max: int, n_points: int, device) -> torch.Tensor:
     check(lib().pnr_aggregate_scratch_bytes(int(n_max), int(n_points), ctypes.byref(nb)),
           "pnr_aggregate_scratch_bytes")
     return torch.empty((int(nb.value) + 15) // 16 * 4, dtype=torch.float32, device=device)
+
+
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False):
+    """C = A^T B (A [K,M], B [K,N], fp32 row-major with unit column stride) on
+    pnr_gemm_tn; returns C [M,N] (and A's column sums when colsum)."""
+    K, M = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == K and A.stride(1) == 1 and B.stride(1) == 1
+    nb = c_size_t(0)
+    check(lib().pnr_gemm_tn_scratch_bytes(K, M, N, ctypes.byref(nb)), "pnr_gemm_tn_scratch_bytes")
+    scratch = torch.empty(max(int(nb.value) // 4, 1), dtype=torch.float32, device=A.device)
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    cs = torch.empty(M, dtype=torch.float32, device=A.device) if colsum else None
+    check(lib().pnr_gemm_tn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
+                            scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")
+    return (C, cs) if colsum else C
 
 
 def stream_ptr(device=None):

@@ -469,10 +469,12 @@ constexpr int kNTW = 8 / kPairWaves;   // neuron tiles per wave
 constexpr int kPTW = kTP / 32;         // 32-pair halves per tile
 
 // Training save of a tile's post-activation quad (both halves) -> dst[pair][256].
+// Also keeps the LeakyReLU derivative as bits: mask[pair][16 * layer + 2T + h]
+// bit r = (pre-activation of accumulator register r of tile T, lane half h > 0).
 template <int NT, int PT>
-__device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float* dst, int64_t tile,
-                                             int64_t n, float s, int lane, int T0) {
-  const int c = lane & 31;
+__device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float* dst, uint16_t* mask,
+                                             int layer, int64_t tile, int64_t n, float s, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int pt = 0; pt < PT; ++pt) {
     const int col = 32 * pt + c;
@@ -481,6 +483,13 @@ __device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float
 #pragma unroll
     for (int T = 0; T < NT; ++T) one[T] = acc[pt * NT + T];
     save_rows<NT>(one, dst, tile * kTP + col, kHid, s, lane, T0);
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bits |= (one[T][r] > 0.f ? 1u : 0u) << r;
+      mask[(tile * kTP + col) * 64 + 16 * layer + 2 * (T0 + T) + h] = (uint16_t)bits;
+    }
   }
 }
 
@@ -642,19 +651,21 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
         X[qaddr(2 * e, lane)] = sn;
         X[qaddr(2 * e + 1, lane)] = cs;
         if (TRAIN && active) {
-          float* pe = A.sv.pe5 + (tile * kTP + lane) * 60 + 2 * e;
+          float* pe = A.sv.pe5 + (tile * kTP + lane) * 64 + 2 * e;
           pe[0] = sn;
           pe[1] = cs;
         }
       }
     }
+    if (TRAIN && active && wid == kPairWaves - 1)   // pe5 rows are padded to 64 for the dW GEMM
+      *reinterpret_cast<float4*>(A.sv.pe5 + (tile * kTP + lane) * 64 + 60) = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
     // ------------------------------------------------------------ block1: 284 -> 256 -> 256
     mlp_layer_q<kNTW, kPTW>(acc, ring, w1b, X, 30, lane);   // + W1[:, 224:284] . PE_5(dist)
     prime_q<kNTW>(ring, w2, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
-    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h1, tile, n, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h1, A.sv.mask, 0, tile, n, neg, lane, T0);
     if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
@@ -663,7 +674,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w3, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
-    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h2, tile, n, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h2, A.sv.mask, 1, tile, n, neg, lane, T0);
     // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
     if (wid == 0) {
       const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
@@ -673,7 +684,10 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
       for (int e = 0; e < 8; ++e) X[qaddr(256 + e, lane)] = ex[e];
       if (TRAIN && active) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) A.sv.x3e[(tile * kTP + lane) * 8 + e] = ex[e];
+        for (int e = 0; e < 8; ++e) A.sv.x3e[(tile * kTP + lane) * 32 + e] = ex[e];
+        float4* z = reinterpret_cast<float4*>(A.sv.x3e + (tile * kTP + lane) * 32 + 8);
+#pragma unroll
+        for (int e = 0; e < 6; ++e) z[e] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     __syncthreads();
@@ -684,7 +698,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w4, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
-    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h3, tile, n, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h3, A.sv.mask, 2, tile, n, neg, lane, T0);
     if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
@@ -693,7 +707,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     prime_q<kNTW>(ring, w1b, lane);                   // the next tile's layer 1
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);   // h4 -> rows 0..255
-    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h4, tile, n, neg, lane, T0);
+    if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h4, A.sv.mask, 3, tile, n, neg, lane, T0);
     __syncthreads();
     if (!(PNR_ABLATE & 4)) {
       // ---------------------------------------------------------- alpha branch
@@ -851,6 +865,47 @@ __device__ __forceinline__ void lrelu_bwd_q(f32x16 (&acc)[PT * NT], const float*
   }
 }
 
+// dz = dh * lrelu'(z) from the saved derivative bits (words prefetched by
+// load_masks before the layer's GEMM, so the mask latency hides behind it).
+template <int NT, int PT>
+__device__ __forceinline__ void load_masks(unsigned (&mk)[PT * NT], const uint16_t* mask, int layer, int64_t tile,
+                                           int64_t n, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    const int col = 32 * pt + c;
+    const bool act = tile * kTS + (col >> 3) < n;
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+      mk[pt * NT + T] = act ? mask[(tile * kTP + col) * 64 + 16 * layer + 2 * (T0 + T) + h] : 0u;
+  }
+}
+
+template <int NT, int PT>
+__device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsigned (&mk)[PT * NT], float* dst,
+                                            int64_t tile, int64_t n, float slope, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    const int col = 32 * pt + c;
+    const bool act = tile * kTS + (col >> 3) < n;
+    const int64_t pair = tile * kTP + col;
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      f32x16& v = acc[pt * NT + T];
+      const unsigned b = mk[pt * NT + T];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = act ? (((b >> r) & 1u) ? v[r] : v[r] * slope) : 0.f;
+      if (act) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<float4*>(dst + pair * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
+              make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   float* X = lds_dyn;                   // quad rows [66][kQP]
@@ -940,10 +995,12 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // ---------------------------------------------------------- block3.2^T: dh3 = W4^T dz4
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    unsigned mk[kPTW * kNTW];
+    load_masks<kNTW, kPTW>(mk, A.sv.mask, 2, tile, n, lane, T0);
     mlp_layer_q<kNTW, kPTW>(acc, ring, w4t, X, 128, lane);
     prime_q<kNTW>(ring, w3t, lane);
     __syncthreads();
-    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h3, A.dz[2], tile, n, slope, lane, T0);
+    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[2], tile, n, slope, lane, T0);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
     // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
@@ -968,6 +1025,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // ---------------------------------------------------------- block3.0^T: dh2 = W3[:, :256]^T dz3
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    load_masks<kNTW, kPTW>(mk, A.sv.mask, 1, tile, n, lane, T0);
     mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
     prime_q<kNTW>(ring, w2t, lane);
     // colour / dir gradients of the pair (wave 0, lane = pair; exP is not
@@ -1000,27 +1058,33 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       }
     }
     __syncthreads();
-    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h2, A.dz[1], tile, n, slope, lane, T0);
+    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[1], tile, n, slope, lane, T0);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     __syncthreads();
     // ---------------------------------------------------------- block1.2^T: dh1 = W2^T dz2
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    load_masks<kNTW, kPTW>(mk, A.sv.mask, 0, tile, n, lane, T0);
     mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
     prime_q<kNTW>(ring, w4t, lane);   // the next tile
-    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h1, A.dz[0], tile, n, slope, lane, T0);
-    // block1.0 point half: d P1[p] += dz1 (the P1 gather's backward)
-#pragma unroll
-    for (int pt = 0; pt < kPTW; ++pt) {
-      const int col = 32 * pt + c;
-      const bool act = tile * kTS + (col >> 3) < n;
-      const int32_t pr = act ? A.sv.prow[tile * kTP + col] : -1;
+    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[0], tile, n, slope, lane, T0);
+    // block1.0 point half: d P1[p] += dz1 (the P1 gather's backward).  dz1 goes
+    // through LDS so each pair's 1-KB row is added with 4 coalesced 256-B
+    // atomic wave instructions (wave w: pairs 16w..16w+15, lane = neuron).
+    __syncthreads();                 // every wave is done reading X (W2^T GEMM)
+    store_q<kNTW, kPTW>(acc, X, lane, T0);
+    __syncthreads();
+    for (int i = 0; i < kTP / kPairWaves; ++i) {
+      const int col = wid * (kTP / kPairWaves) + i;
+      if (tile * kTS + (col >> 3) >= n) break;
+      const int32_t pr = A.sv.prow[tile * kTP + col];
       if (pr < 0) continue;
       float* dst = A.d_p1 + (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr) * kHid;
 #pragma unroll
-      for (int T = 0; T < kNTW; ++T)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) atomicAdd(dst + 32 * (T0 + T) + acc_row(r, h), acc[pt * kNTW + T][r]);
+      for (int q = 0; q < 4; ++q) {
+        const int nn = lane + 64 * q;
+        atomicAdd(dst + nn, X[qaddr(nn, col)]);
+      }
     }
     __syncthreads();
   }
@@ -1153,7 +1217,7 @@ extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples
 static int check_saved(const pnr_agg_saved* sv) {
   PNR_CHECK_ARG(sv, "aggregate train: null saved struct");
   PNR_CHECK_ARG(sv->h1 && sv->h2 && sv->h3 && sv->h4 && sv->pe5 && sv->x3e && sv->pa && sv->wt && sv->wn &&
-                    sv->prow && sv->hid && sv->vpe && sv->hc1 && sv->hc2 && sv->hc3 && sv->vmask,
+                    sv->prow && sv->hid && sv->vpe && sv->hc1 && sv->hc2 && sv->hc3 && sv->vmask && sv->mask,
                 "aggregate train: null saved array");
   PNR_CHECK_ARG((((uintptr_t)sv->h1 | (uintptr_t)sv->h2 | (uintptr_t)sv->h3 | (uintptr_t)sv->h4 |
                   (uintptr_t)sv->hid | (uintptr_t)sv->hc1 | (uintptr_t)sv->hc2 | (uintptr_t)sv->hc3) & 15) == 0,

@@ -1,0 +1,229 @@
+// Weight-gradient GEMM of the backward pass: C[M,N] = A^T B summed over a long
+// K (every (sample, neighbour) pair of the batch), A[K,M] / B[K,N] row-major
+// -- dW = dZ^T X for block3.2, block3.0, block1.2 and block1.0's point half
+// (the reference gets these from autograd of nn.Linear).
+//
+// CDNA4 mapping: v_mfma_f32_32x32x2_f32 consumes two K rows per step and both
+// operands come straight from global memory in MFMA lane order (lane l reads
+// A[k0 + (l>>5)][m0 + (l&31)] and B[k0 + (l>>5)][n0 + (l&31)]: two 128-B
+// row segments per half-wave, no LDS and no transpose).  A workgroup of 8
+// waves owns the whole C (M <= 256 rows, N <= 256 columns; wave w: rows
+// 32w..32w+31 x every column tile, up to 128 accumulator VGPRs) for one K
+// split, so A and B are read from HBM exactly once; the 8 waves read the same
+// B rows (L1 hits).  K is split over ~256 workgroups (one per CU, 2 waves per
+// SIMD); every split writes its own partial C, summed in a fixed order by a
+// two-level reduction: deterministic, no float atomics.  Column sums of A
+// (the bias gradients) ride along as an extra partial row.
+#include "pnr_common.h"
+
+namespace pnr {
+
+typedef float f32x16g __attribute__((ext_vector_type(16)));
+
+constexpr int kGWaves = 8;   // waves per workgroup = 32-row tiles of C (M <= 256)
+constexpr int kGMaxNT = 8;   // 32-column tiles of C (N <= 256)
+constexpr int kGUnroll = 4;  // k-steps per software-pipeline stage
+constexpr int kGGroup = 16;  // splits summed per first-level reduction thread
+
+struct GemmArgs {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  int64_t K;
+  int M, N;
+  int64_t kchunk;      // rows of K per split (multiple of 2 * kGUnroll)
+  float* part;         // [nsplit][M*N + M]  (C partial, then colsum partial)
+  int colsum;
+};
+
+template <int NT>
+__device__ __forceinline__ void gemm_body(const GemmArgs& g, int m0, int64_t k_begin, int64_t k_end, float* out,
+                                          float* cs_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31, h = lane >> 5;
+  f32x16g acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = (f32x16g){0.f};
+  float csum = 0.f;
+  const float* pa = g.A + m0 + c;
+  const float* pb = g.B + c;
+  int64_t k = k_begin;
+  // software pipeline: the next stage's operands are loaded while this
+  // stage's MFMAs run (double-buffered registers)
+  if (k + 2 * kGUnroll <= k_end) {
+    float a[kGUnroll], b[kGUnroll][NT];
+#pragma unroll
+    for (int u = 0; u < kGUnroll; ++u) {
+      const int64_t r = k + 2 * u + h;
+      a[u] = pa[r * g.lda];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[u][t] = pb[r * g.ldb + 32 * t];
+    }
+    for (;;) {
+      const int64_t kn = k + 2 * kGUnroll;
+      const bool more = kn + 2 * kGUnroll <= k_end;
+      float an[kGUnroll], bn[kGUnroll][NT];
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < kGUnroll; ++u) {
+          const int64_t r = kn + 2 * u + h;
+          an[u] = pa[r * g.lda];
+#pragma unroll
+          for (int t = 0; t < NT; ++t) bn[u][t] = pb[r * g.ldb + 32 * t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGUnroll; ++u) {
+        csum += a[u];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u][t], acc[t], 0, 0, 0);
+      }
+      k = kn;
+      if (!more) break;
+#pragma unroll
+      for (int u = 0; u < kGUnroll; ++u) {
+        a[u] = an[u];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b[u][t] = bn[u][t];
+      }
+    }
+  }
+  for (; k < k_end; k += 2) {
+    const int64_t r = k + h;
+    const bool ok = r < k_end;
+    const float a = ok ? pa[r * g.lda] : 0.f;
+    csum += a;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float b = ok ? pb[r * g.ldb + 32 * t] : 0.f;
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+    }
+  }
+  // C/D layout: row = (r&3) + 8(r>>2) + 4h, col = c
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[(int64_t)(m0 + (r & 3) + 8 * (r >> 2) + 4 * h) * g.N + 32 * t + c] = acc[t][r];
+  if (cs_out) {
+    csum += __shfl_xor(csum, 32);
+    if (h == 0) cs_out[m0 + c] = csum;
+  }
+}
+
+__global__ void __launch_bounds__(64 * kGWaves, 1) k_gemm_tn_part(GemmArgs g) {
+  const int wid = threadIdx.x >> 6;
+  const int m0 = 32 * wid;
+  if (m0 >= g.M) return;
+  const int split = blockIdx.x;
+  const int64_t k_begin = (int64_t)split * g.kchunk;
+  int64_t k_end = k_begin + g.kchunk;
+  if (k_end > g.K) k_end = g.K;
+  const int64_t stride = (int64_t)g.M * g.N + g.M;
+  float* out = g.part + (int64_t)split * stride;
+  float* cs = g.colsum ? out + (int64_t)g.M * g.N : nullptr;
+  switch (g.N / 32) {   // column tiles (N % 32 == 0, N <= 256)
+    case 1: gemm_body<1>(g, m0, k_begin, k_end, out, cs); break;
+    case 2: gemm_body<2>(g, m0, k_begin, k_end, out, cs); break;
+    case 3: gemm_body<3>(g, m0, k_begin, k_end, out, cs); break;
+    case 4: gemm_body<4>(g, m0, k_begin, k_end, out, cs); break;
+    case 5: gemm_body<5>(g, m0, k_begin, k_end, out, cs); break;
+    case 6: gemm_body<6>(g, m0, k_begin, k_end, out, cs); break;
+    case 7: gemm_body<7>(g, m0, k_begin, k_end, out, cs); break;
+    default: gemm_body<8>(g, m0, k_begin, k_end, out, cs); break;
+  }
+}
+
+// out[grp][i] = sum_{s in group grp} part[s][i] in split order (float4 lanes).
+__global__ void k_reduce_splits(const float* __restrict__ part, int64_t n4, int nsplit, int group,
+                                float* __restrict__ out) {
+  const int grp = blockIdx.y;
+  const int s0 = grp * group, s1 = min(nsplit, s0 + group);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = s0; q < s1; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(part)[(int64_t)q * n4 + i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[(int64_t)grp * n4 + i] = acc;
+  }
+}
+
+static void gemm_plan(int64_t K, int* nsplit, int64_t* kchunk) {
+  int64_t s = 256;                                   // one 8-wave workgroup per CU
+  const int64_t maxs = K / 128 > 0 ? K / 128 : 1;    // >= 128 k-rows per split
+  if (s > maxs) s = maxs;
+  int64_t kc = cdiv(K > 0 ? K : 1, s);
+  kc = cdiv(kc, 2 * kGUnroll) * (2 * kGUnroll);
+  *kchunk = kc;
+  *nsplit = (int)(K > 0 ? cdiv(K, kc) : 1);
+}
+
+static size_t gemm_scratch(int64_t K, int M, int N) {
+  int ns;
+  int64_t kc;
+  gemm_plan(K, &ns, &kc);
+  const size_t stride = (size_t)M * N + M;
+  return (stride * ns + stride * cdiv(ns, kGGroup)) * sizeof(float);
+}
+
+}  // namespace pnr
+
+using namespace pnr;
+
+extern "C" int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t* out) {
+  PNR_CHECK_ARG(out && K >= 0 && M > 0 && N > 0, "gemm_tn_scratch_bytes: bad args");
+  *out = gemm_scratch(K, M, N);
+  return PNR_OK;
+}
+
+extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
+                           int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
+                           void* stream) {
+  PNR_CHECK_ARG(C && scratch && (K == 0 || (A && B)), "gemm_tn: null pointer");
+  PNR_CHECK_ARG(M > 0 && N > 0 && M % 32 == 0 && N % 32 == 0 && M <= 32 * kGWaves && N <= 32 * kGMaxNT,
+                "gemm_tn: M, N must be multiples of 32 in [32, 256]");
+  PNR_CHECK_ARG(lda >= M && ldb >= N && K >= 0, "gemm_tn: bad leading dimensions");
+  PNR_CHECK_ARG(((uintptr_t)scratch & 15) == 0, "gemm_tn: 16-B aligned scratch required");
+  PNR_CHECK_ARG(scratch_bytes >= gemm_scratch(K, M, N), "gemm_tn: scratch too small");
+  hipStream_t st = as_stream(stream);
+  if (K == 0) {
+    PNR_HIP(hipMemsetAsync(C, 0, (size_t)M * N * sizeof(float), st));
+    if (colsum_a) PNR_HIP(hipMemsetAsync(colsum_a, 0, (size_t)M * sizeof(float), st));
+    return PNR_OK;
+  }
+  int ns;
+  int64_t kc;
+  gemm_plan(K, &ns, &kc);
+  GemmArgs g;
+  g.A = A;
+  g.lda = lda;
+  g.B = B;
+  g.ldb = ldb;
+  g.K = K;
+  g.M = M;
+  g.N = N;
+  g.kchunk = kc;
+  g.part = static_cast<float*>(scratch);
+  g.colsum = colsum_a != nullptr;
+  hipLaunchKernelGGL(k_gemm_tn_part, dim3(ns), dim3(64 * kGWaves), 0, st, g);
+  PNR_LAUNCH_CHECK();
+  // two-level ordered reduction: groups of kGGroup splits, then the groups
+  const int64_t stride = (int64_t)M * N + M;   // multiple of 4 (M % 32 == 0)
+  const int64_t n4 = stride / 4;
+  const int ngrp = (int)cdiv(ns, kGGroup);
+  float* lvl1 = g.part + (size_t)ns * stride;
+  hipLaunchKernelGGL(k_reduce_splits, dim3(grid_for(n4, 256, 256), ngrp), dim3(256), 0, st, g.part, n4, ns, kGGroup,
+                     lvl1);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_reduce_splits, dim3(grid_for(n4, 256, 256), 1), dim3(256), 0, st, lvl1, n4, ngrp, ngrp,
+                     g.part);
+  PNR_LAUNCH_CHECK();
+  PNR_HIP(hipMemcpyAsync(C, g.part, (size_t)M * N * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (colsum_a)
+    PNR_HIP(hipMemcpyAsync(colsum_a, g.part + (size_t)M * N, (size_t)M * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return PNR_OK;
+}

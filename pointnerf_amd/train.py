@@ -60,12 +60,13 @@ class Saved:
         P = n * 8
         self.t = dict(h1=torch.empty((P, 256), **f), h2=torch.empty((P, 256), **f),
                       h3=torch.empty((P, 256), **f), h4=torch.empty((P, 256), **f),
-                      pe5=torch.empty((P, 60), **f), x3e=torch.empty((P, 8), **f), pa=torch.empty(P, **f),
+                      pe5=torch.empty((P, 64), **f), x3e=torch.empty((P, 32), **f), pa=torch.empty(P, **f),
                       wt=torch.empty(P, **f), wn=torch.empty(P, **f),
                       prow=torch.empty(P, dtype=torch.int32, device=device),
                       hid=torch.zeros((n, 256), **f), vpe=torch.empty((n, 24), **f),
                       hc1=torch.empty((n, 128), **f), hc2=torch.empty((n, 128), **f),
-                      hc3=torch.empty((n, 128), **f), vmask=torch.empty(n, dtype=torch.int32, device=device))
+                      hc3=torch.empty((n, 128), **f), vmask=torch.empty(n, dtype=torch.int32, device=device),
+                      mask=torch.empty((P, 64), dtype=torch.int16, device=device))
         self.c = L.AggSaved(*(self.t[k].data_ptr() for k, _ in L.AggSaved._fields_))
 
     def __getitem__(self, k):
@@ -188,20 +189,26 @@ class AggregateFn(torch.autograd.Function):
         m = n * 8
         dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
         h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
-        grads["block3.2.weight"], grads["block3.2.bias"] = dz4.t() @ h3, dz4.sum(0)
-        x3 = torch.cat([h2, sv["x3e"][:m, :7]], 1)
-        grads["block3.0.weight"], grads["block3.0.bias"] = dz3.t() @ x3, dz3.sum(0)
-        grads["block1.2.weight"], grads["block1.2.bias"] = dz2.t() @ h1, dz2.sum(0)
-        grads["alpha_branch.0.weight"], grads["alpha_branch.0.bias"] = (dpa[None, :] @ h4), dpa.sum(0, keepdim=True)
+        # dW = dZ^T X over all pairs: split-K MFMA GEMM (pnr_gemm_tn), bias = column sums
+        grads["block3.2.weight"], grads["block3.2.bias"] = L.gemm_tn(dz4, h3, colsum=True)
+        gW3 = torch.empty((256, 263), **f32)
+        gW3[:, :256], grads["block3.0.bias"] = L.gemm_tn(dz3, h2, colsum=True)
+        gW3[:, 256:] = L.gemm_tn(dz3, sv["x3e"][:m])[:, :7]
+        grads["block3.0.weight"] = gW3
+        grads["block1.2.weight"], grads["block1.2.bias"] = L.gemm_tn(dz2, h1, colsum=True)
+        dpa32 = torch.zeros((m, 32), **f32)      # M padded to one 32-row MFMA tile
+        dpa32[:, 0] = dpa
+        grads["alpha_branch.0.weight"] = L.gemm_tn(dpa32, h4)[:1]
+        grads["alpha_branch.0.bias"] = dpa.sum(0, keepdim=True)
         # ---- block1.0: pair half from dz1 / PE_5, point half from dP1 / X1
         emb = ctx.tabs[0] if used is None else ctx.tabs[0].index_select(0, used.long()).contiguous()
         d_p1 = d_p1[:n_p1]
         x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
         L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
         gW1 = torch.empty((256, 284), **f32)
-        gW1[:, :224] = d_p1.t() @ x1
-        gW1[:, 224:] = dz1.t() @ sv["pe5"][:m]
-        grads["block1.0.weight"], grads["block1.0.bias"] = gW1, dz1.sum(0)
+        gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True)   # sum_p dP1 = sum_pairs dz1
+        gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m])[:, :60]
+        grads["block1.0.weight"] = gW1
         dx1 = (d_p1 @ P["block1.0.weight"][:, :224]).contiguous()
         d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
         L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb_u), L.stream_ptr(dev)),

@@ -156,3 +156,17 @@ def test_train_step_reduces_loss(cuda):
         losses.append(float(loss.detach()))
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("K,M,N", [(235001, 256, 256), (4097, 256, 224), (37, 256, 32), (0, 128, 64)])
+def test_gemm_tn_vs_torch(cuda, K, M, N):
+    from pointnerf_amd import _lib as L
+    g = torch.Generator(device=cuda).manual_seed(K + N)
+    A = torch.randn((K, M), device=cuda, generator=g)
+    B = torch.randn((K, N + 8), device=cuda, generator=g)[:, :N]        # ldb > N
+    C, cs = L.gemm_tn(A, B, colsum=True)
+    ref = (A.double().t() @ B.double()).float()
+    close(C, ref, "C", rel=1e-4, scale=2e-6)
+    close(cs, A.double().sum(0).float(), "colsum", rel=1e-4, scale=2e-6)
+    C2 = L.gemm_tn(A, B)
+    assert torch.equal(C, C2)          # deterministic split-K reduction
