@@ -266,86 +266,6 @@ __device__ __forceinline__ void save_rows(const f32x16 (&acc)[NT], float* dst, i
                       lrelu(acc[T][4 * q + 3], s));
 }
 
-template <bool TRAIN>
-__global__ void __launch_bounds__(kAggBlock, 1) k_color(AggArgs A) {
-  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* X = lds_dyn + wid * kWaveLds;   // [kXRows][kPitch]
-  const int m = lane & 31, h = lane >> 5;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, 32);
-  const float neg = A.w.neg_slope;
-  float Rw[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t v0 = tile * 32;
-    const int nv = (int)((n - v0) < 32 ? (n - v0) : 32);
-    const int my_valid = (m < nv) ? A.vmask[v0 + m] : 0;
-    const unsigned long long vbits = __ballot(my_valid != 0);   // bit q (and q+32): sample q valid
-    // hid rows (one 1-KB row per wave instruction) -> X^T rows 0..255 (transpose)
-#pragma unroll 4
-    for (int q = 0; q < 32; ++q) {
-      float4 f4 = ((vbits >> q) & 1ull) ? reinterpret_cast<const float4*>(A.hid + (v0 + q) * kHid)[lane]
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-      X[(4 * lane + 0) * kPitch + q] = f4.x;
-      X[(4 * lane + 1) * kPitch + q] = f4.y;
-      X[(4 * lane + 2) * kPitch + q] = f4.z;
-      X[(4 * lane + 3) * kPitch + q] = f4.w;
-    }
-    // view-direction PE, ori dropped (point_aggregators.py:506-512): rows 256..279 =
-    // sin block (c*4+f) then cos block; lane half h writes block h
-    {
-      float vrot[3] = {0.f, 0.f, 0.f};
-      if (m < nv) {
-        const int64_t row = sample_row(A.s, v0 + m);
-        const int64_t drow = dir_row(A.s, row);
-        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
-        mat3(Rw, vd, vrot);
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          float s, co;
-          sincosf(vrot[c] * (float)(1 << f), &s, &co);
-          X[(kHid + 12 * h + 4 * c + f) * kPitch + m] = h ? co : s;
-          if (TRAIN && m < nv) A.sv.vpe[(v0 + m) * 24 + 12 * h + 4 * c + f] = h ? co : s;
-        }
-    }
-    bias_rows(X, kCin, lane);
-    wave_sync();
-    f32x16 acc[4];
-    zero_acc<4>(acc);
-    mlp_layer<4>(acc, A.w.wc1f, X, 141, lane);      // 280 inputs + bias column
-    wave_sync();
-    store_act<4>(acc, X, neg, lane);
-    if (TRAIN && m < nv) save_rows<4>(acc, A.sv.hc1, v0 + m, kC, neg, lane);
-    bias_rows(X, kC, lane);
-    wave_sync();
-    zero_acc<4>(acc);
-    mlp_layer<4>(acc, A.w.wc2f, X, 65, lane);
-    wave_sync();
-    store_act<4>(acc, X, neg, lane);
-    if (TRAIN && m < nv) save_rows<4>(acc, A.sv.hc2, v0 + m, kC, neg, lane);
-    bias_rows(X, kC, lane);
-    wave_sync();
-    zero_acc<4>(acc);
-    mlp_layer<4>(acc, A.w.wc3f, X, 65, lane);
-    wave_sync();
-    store_act<4>(acc, X, neg, lane);   // X^T rows 0..127 = colour features
-    if (TRAIN && m < nv) save_rows<4>(acc, A.sv.hc3, v0 + m, kC, neg, lane);
-    wave_sync();
-    // write out_feat[v, 1..128]: lane = channel pair, loop over the 32 samples
-    for (int q = 0; q < nv; ++q) {
-      if (!((vbits >> q) & 1ull)) continue;   // samples without neighbours keep zeros
-      float* o = A.out_feat + (v0 + q) * (kC + 1) + 1;
-      o[lane] = X[lane * kPitch + q];
-      o[64 + lane] = X[(64 + lane) * kPitch + q];
-    }
-    wave_sync();
-  }
-}
 
 
 // ---------------------------------------------------------------------------
@@ -370,7 +290,8 @@ constexpr int kTS = kTP / kKN;          // samples per tile
 constexpr int kQP = 4 * kTP + 4;        // floats per quad row
 constexpr int kQD = 4;                  // k_pairs weight prefetch depth (k-steps)
 constexpr int kQRows = (264 + 2 * kQD + 3) / 4;  // layer-3 input rows + x prefetch overrun
-constexpr int kPairsLdsFloats = kQRows * kQP + kTP /*wt*/ + 4 * kTP /*alpha parts*/ + kTS /*flags*/;
+constexpr int kPairsLdsFloats = kQRows * kQP + kTP /*wt*/ + 4 * kTP /*alpha parts*/ + kTS /*flags*/ +
+                                8 * kTP /*block3 extras*/;
 static_assert(kQD <= kPackPad && kPD <= kPackPad, "prefetch deeper than the packed padding");
 constexpr size_t kPairsLdsBytes = (size_t)kPairsLdsFloats * sizeof(float);
 
@@ -380,17 +301,17 @@ __device__ __forceinline__ constexpr int qaddr(int n, int c) { return (n >> 2) *
 // Issue the first kQD k-steps of a layer's weight fragments into the ring.
 // Called as soon as the previous layer's last MFMA is issued (or before the
 // gather for layer 1), so the L2 latency hides behind the layer boundary.
-template <int NT>
+template <int NT, int NTOT = 8>
 __device__ __forceinline__ void prime_q(float (&a)[kQD][NT], const float* __restrict__ wf, int lane) {
 #pragma unroll
-  for (int d = 0; d < kQD; ++d) load_w<NT, 8>(a[d], wf + lane, d);
+  for (int d = 0; d < kQD; ++d) load_w<NT, NTOT>(a[d], wf + lane, d);
 }
 
 // Y^T += W . X^T for NT neuron tiles x PT 32-pair halves over nsteps k-steps.
 // Weight fragments kQD steps ahead in a register ring (primed by prime_q);
 // the next kQD steps' B operands read from LDS one iteration ahead (kQD/2 b64
 // per half).
-template <int NT, int PT>
+template <int NT, int PT, int NTOT = 8>
 __device__ __forceinline__ void mlp_layer_q(f32x16 (&acc)[PT * NT], float (&a)[kQD][NT],
                                             const float* __restrict__ wf, const float* X, int nsteps,
                                             int lane) {
@@ -425,7 +346,7 @@ __device__ __forceinline__ void mlp_layer_q(f32x16 (&acc)[PT * NT], float (&a)[k
 #pragma unroll
           for (int pt = 0; pt < PT; ++pt) y[i][pt] = *reinterpret_cast<const float2*>(xn + 128 * pt + i * kQP);
       }
-      load_w<NT, 8>(a[d], p, t + D + d);
+      load_w<NT, NTOT>(a[d], p, t + D + d);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -468,6 +389,20 @@ constexpr int kPairWaves = 4;
 constexpr int kNTW = 8 / kPairWaves;   // neuron tiles per wave
 constexpr int kPTW = kTP / 32;         // 32-pair halves per tile
 
+// Training save of a colour-branch tile (output tile T0, PT sample halves) -> dst[v][128].
+template <int PT>
+__device__ __forceinline__ void save_cols(const f32x16 (&acc)[PT], float* dst, int64_t v0, int64_t n, float s,
+                                          int lane, int T0) {
+  const int c = lane & 31;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    const int64_t v = v0 + 32 * pt + c;
+    if (v >= n) continue;
+    f32x16 one[1] = {acc[pt]};
+    save_rows<1>(one, dst, v, kC, s, lane, T0);
+  }
+}
+
 // Training save of a tile's post-activation quad (both halves) -> dst[pair][256].
 // Also keeps the LeakyReLU derivative as bits: mask[pair][16 * layer + 2T + h]
 // bit r = (pre-activation of accumulator register r of tile T, lane half h > 0).
@@ -500,6 +435,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
   float* wtL = X + kQRows * kQP;               // [64] per-pair blend weight w_k * conf_k
   float* apart = wtL + kTP;                    // [4][64] alpha partial dots
   int* sflag = reinterpret_cast<int*>(apart + 4 * kTP);  // [8] sample has a valid neighbour
+  float* exL = apart + 4 * kTP + kTS;          // [8][64] block3.0 extra inputs, parked from the gather
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int j = lane >> 3, k = lane & 7;       // gather layout: lane = pair column
@@ -621,6 +557,19 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     mat3(Rw, vd, vrot);
     mat3(Rw, pdir, drot);
     if (wid == 0) {
+      // block3 inputs 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
+      const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
+      const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0],
+                           drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) exL[e * kTP + lane] = ex[e];
+      if (TRAIN && active) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) A.sv.x3e[(tile * kTP + lane) * 32 + e] = ex[e];
+        float4* z = reinterpret_cast<float4*>(A.sv.x3e + (tile * kTP + lane) * 32 + 8);
+#pragma unroll
+        for (int e = 0; e < 6; ++e) z[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       if (active && k < K) {
         if (A.out_weight) A.out_weight[row * K + k] = wn;
         if (A.out_conf) A.out_conf[row * K + k] = confc;
@@ -675,20 +624,10 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h2, A.sv.mask, 1, tile, n, neg, lane, T0);
-    // block3 inputs rows 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
+    // block3 inputs rows 256..263 (parked in exL by the gather)
     if (wid == 0) {
-      const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
-      const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0],
-                           drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) X[qaddr(256 + e, lane)] = ex[e];
-      if (TRAIN && active) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) A.sv.x3e[(tile * kTP + lane) * 32 + e] = ex[e];
-        float4* z = reinterpret_cast<float4*>(A.sv.x3e + (tile * kTP + lane) * 32 + 8);
-#pragma unroll
-        for (int e = 0; e < 6; ++e) z[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      for (int e = 0; e < 8; ++e) X[qaddr(256 + e, lane)] = exL[e * kTP + lane];
     }
     __syncthreads();
     // ------------------------------------------------------------ block3: 263 -> 256 -> 256
@@ -705,22 +644,65 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     mlp_layer_q<kNTW, kPTW>(acc, ring, w4, X, 129, lane);
     prime_q<kNTW>(ring, w1b, lane);                   // the next tile's layer 1
-    __syncthreads();
-    store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);   // h4 -> rows 0..255
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h4, A.sv.mask, 3, tile, n, neg, lane, T0);
-    __syncthreads();
     if (!(PNR_ABLATE & 4)) {
-      // ---------------------------------------------------------- alpha branch
-      // wave w: partial dot of every pair (lane) over neurons [64w, 64w + 64)
-      {
-        float pa = 0.f;
-#pragma unroll 4
-        for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
-          const float4 x4 = *reinterpret_cast<const float4*>(X + u * kQP + 4 * lane);
-          pa += A.w.wa[4 * u] * x4.x + A.w.wa[4 * u + 2] * x4.y + A.w.wa[4 * u + 1] * x4.z +
-                A.w.wa[4 * u + 3] * x4.w;
+      // ---------------------------------------------------------- alpha + K sums from registers
+      // h4 = lrelu(acc) never goes to LDS.  alpha: each lane dots its 32 rows of
+      // the wave's 64 neurons with W_a, the two lane halves and the 4 waves are
+      // summed through LDS.  K sums (point_aggregators.py:622-628): the 8 pairs
+      // of a sample are 8 adjacent lanes; a 3-round DPP reduce-scatter (row
+      // half-mirror, quad xor 2, quad xor 1) leaves lane i of the 8 with the
+      // sums of accumulator registers 2i, 2i+1 = two adjacent neurons.
+      float pa_part[kPTW] = {0.f, 0.f};
+#pragma unroll
+      for (int pt = 0; pt < kPTW; ++pt) {
+        const float wtp = wtL[32 * pt + c];
+        const int sj = (32 * pt + c) >> 3;
+        const int64_t vo = tile * kTS + sj;
+        const bool wr = vo < n && sflag[sj];
+        const int i8 = c & 7;
+#pragma unroll
+        for (int T = 0; T < kNTW; ++T) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float hv = lrelu(acc[pt * kNTW + T][r], neg);
+            pa_part[pt] += A.w.wa[32 * (T0 + T) + acc_row(r, h)] * hv;
+            v[r] = wtp * hv;
+          }
+          float w8[8], w4[4], w2[2];
+          const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float send = b2 ? v[q] : v[q + 8];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send),
+                                                                                  0x141, 0xf, 0xf, false));
+            w8[q] = (b2 ? v[q + 8] : v[q]) + recv;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float send = b1 ? w8[q] : w8[q + 4];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send),
+                                                                                  0x4E, 0xf, 0xf, false));
+            w4[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float send = b0 ? w4[q] : w4[q + 2];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send),
+                                                                                  0xB1, 0xf, 0xf, false));
+            w2[q] = (b0 ? w4[q + 2] : w4[q]) + recv;
+          }
+          // registers 2 i8, 2 i8 + 1 -> rows (2 i8 & 3) + 8 (i8 >> 1) + 4h (+1)
+          if (wr)
+            *reinterpret_cast<float2*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h) =
+                make_float2(w2[0], w2[1]);
         }
-        apart[wid * kTP + lane] = pa;
+        pa_part[pt] += __shfl_xor(pa_part[pt], 32);
+      }
+      if (h == 0) {
+        apart[wid * kTP + c] = pa_part[0];
+        apart[wid * kTP + 32 + c] = pa_part[1];
       }
       __syncthreads();
       if (wid == 0) {
@@ -735,26 +717,111 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
           if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
         }
       }
-      // ---------------------------------------------------------- K sums
-      // thread (wave w, lane = quad u): samples 2w, 2w+1, neurons 4u..4u+3
-      // (point_aggregators.py:622-628), one 1-KB coalesced row per sample
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_color: the colour branch 280 -> 128 -> 128 -> 128 (LeakyReLU each,
+// point_aggregators.py:630-638) for 64 valid samples per 4-wave workgroup, on
+// the same quad-row LDS pipeline as k_pairs: wave w owns output tile w for
+// both 32-sample halves (2 MFMAs per weight fragment).  Input rows: the
+// K-summed features hid (transposed from [sample][256] rows with one float4
+// per lane), the 4-band view-direction PE (sin block, cos block, :506-512)
+// and the bias row.
+constexpr int kColWaves = 4;
+constexpr int kColQRows = (282 + 2 * kQD + 3) / 4;
+constexpr size_t kColLdsBytes = (size_t)kColQRows * kQP * sizeof(float);
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(64 * kColWaves, 2) k_color(AggArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  float* X = lds_dyn;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kTP);
+  const float neg = A.w.neg_slope;
+  float Rw[9];
 #pragma unroll
-      for (int si = 0; si < kTS / kPairWaves; ++si) {
-        const int sj = si * kPairWaves + wid;
-        const int64_t vo = tile * kTS + sj;
-        if (vo >= n || !sflag[sj]) continue;
-        float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < kKN; ++q) {
-          const float wk = wtL[8 * sj + q];
-          const float4 x4 = *reinterpret_cast<const float4*>(X + lane * kQP + 4 * (8 * sj + q));
-          f.x += wk * x4.x;
-          f.y += wk * x4.y;
-          f.z += wk * x4.z;
-          f.w += wk * x4.w;
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  const float* w1 = A.w.wc1f + wid * 64;
+  const float* w2 = A.w.wc2f + wid * 64;
+  const float* w3 = A.w.wc3f + wid * 64;
+  float ring[kQD][1];
+  prime_q<1, 4>(ring, w1, lane);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t v0 = tile * kTP;
+    // hid rows -> X^T rows 0..255 (wave w: samples 16w..16w+15, lane = neuron quad)
+    for (int i = 0; i < kTP / kColWaves; ++i) {
+      const int col = wid * (kTP / kColWaves) + i;
+      const int64_t v = v0 + col;
+      const bool ok = v < n && A.vmask[v] != 0;
+      const float4 f4 = ok ? reinterpret_cast<const float4*>(A.hid + v * kHid)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(X + lane * kQP + 4 * col) = make_float4(f4.x, f4.z, f4.y, f4.w);
+    }
+    // view-direction PE (ori dropped): rows 256 + 4ch + f = sin, 268 + 4ch + f = cos;
+    // wave ch < 3 owns channel ch, wave 3 the bias rows 280 (1) / 281 (0); lane = sample
+    {
+      const int64_t v = v0 + lane;
+      if (wid < 3) {
+        float vrot[3] = {0.f, 0.f, 0.f};
+        if (v < n) {
+          const int64_t row = sample_row(A.s, v);
+          const int64_t drow = dir_row(A.s, row);
+          const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+          mat3(Rw, vd, vrot);
         }
-        reinterpret_cast<float4*>(A.hid + vo * kHid)[lane] = make_float4(f.x, f.z, f.y, f.w);
+        const float x = wid == 0 ? vrot[0] : (wid == 1 ? vrot[1] : vrot[2]);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          float sn, cs;
+          sincosf(x * (float)(1 << f), &sn, &cs);
+          X[qaddr(kHid + 4 * wid + f, lane)] = sn;
+          X[qaddr(kHid + 12 + 4 * wid + f, lane)] = cs;
+          if (TRAIN && v < n) {
+            A.sv.vpe[v * 24 + 4 * wid + f] = sn;
+            A.sv.vpe[v * 24 + 12 + 4 * wid + f] = cs;
+          }
+        }
+      } else {
+        X[qaddr(kCin, lane)] = 1.f;
+        X[qaddr(kCin + 1, lane)] = 0.f;
       }
+    }
+    __syncthreads();
+    f32x16 acc[2];
+    acc[0] = acc[1] = (f32x16){0.f};
+    mlp_layer_q<1, 2, 4>(acc, ring, w1, X, 141, lane);   // 280 inputs + bias column
+    prime_q<1, 4>(ring, w2, lane);
+    __syncthreads();
+    store_act_q<1, 2>(acc, X, neg, lane, wid);
+    if (wid == 0) bias_rows_q(X, kC, lane);
+    if (TRAIN) save_cols<2>(acc, A.sv.hc1, v0, n, neg, lane, wid);
+    __syncthreads();
+    acc[0] = acc[1] = (f32x16){0.f};
+    mlp_layer_q<1, 2, 4>(acc, ring, w2, X, 65, lane);
+    prime_q<1, 4>(ring, w3, lane);
+    __syncthreads();
+    store_act_q<1, 2>(acc, X, neg, lane, wid);
+    if (wid == 0) bias_rows_q(X, kC, lane);
+    if (TRAIN) save_cols<2>(acc, A.sv.hc2, v0, n, neg, lane, wid);
+    __syncthreads();
+    acc[0] = acc[1] = (f32x16){0.f};
+    mlp_layer_q<1, 2, 4>(acc, ring, w3, X, 65, lane);
+    prime_q<1, 4>(ring, w1, lane);   // the next tile
+    if (TRAIN) save_cols<2>(acc, A.sv.hc3, v0, n, neg, lane, wid);
+    // out_feat[v, 1 + n] (valid samples only; the others keep their zeros)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int64_t v = v0 + 32 * pt + c;
+      if (v >= n || A.vmask[v] == 0) continue;
+      float* o = A.out_feat + v * (kC + 1) + 1 + 32 * wid + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
     }
     __syncthreads();
   }
@@ -769,7 +836,7 @@ int launch_t(const AggArgs& a, hipStream_t st) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color<TRAIN>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kColLdsBytes));
     attr = true;
   }
   hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.used ? a.pts.n_used : a.pts.n, 32), 4, 256)),
@@ -780,8 +847,8 @@ int launch_t(const AggArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_pairs<TRAIN>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kPairsLdsBytes,
                      st, a);
   PNR_LAUNCH_CHECK();
-  const int64_t ctiles = cdiv(a.s.n_max, 32);
-  hipLaunchKernelGGL(k_color<TRAIN>, dim3(grid_for(ctiles, 4, 256)), dim3(kAggBlock), kAggLdsBytes, st, a);
+  const int64_t ctiles = cdiv(a.s.n_max, kTP);
+  hipLaunchKernelGGL(k_color<TRAIN>, dim3(grid_for(ctiles, 1, 256 * 2)), dim3(64 * kColWaves), kColLdsBytes, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
