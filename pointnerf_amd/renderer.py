@@ -142,7 +142,7 @@ class NeuralPointsRayMarching(nn.Module):
         mlp, _keepw = self.aggregator.packed()
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
-        chunk = self.chunk_rays or R
+        chunk = max(1, self.chunk_rays or R)
         def mark():
             if events is None:
                 return None
