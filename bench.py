@@ -258,7 +258,7 @@ def main():
             campos, camrot, _ = dev_cams[ci]
             ev = [] if timed else None
             color, opac, is_bg, mask = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
-                                                         force_grid=not args.no_grid_rebuild, events=ev)
+                                                         force_grid=(f == 0 and not args.no_grid_rebuild), events=ev)
             if timed:
                 c = model.last_counts
                 stage["pairs"] += c["n_pairs"]
@@ -322,7 +322,7 @@ def main():
             "data": "synthetic (seeded lego-like 2M-point cloud, random-init lego viewmlp weights)",
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
-                       "grid_rebuild_per_frame": not args.no_grid_rebuild,
+                       "grid_rebuild_per_step": not args.no_grid_rebuild,
                        "parallelism": f"dp{world} (16x16 ray tiles, RCCL all_gather of tiles)" if world > 1
                        else "single GPU"},
             "roofline": {"bound": "mfma", "kernel": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
@@ -330,6 +330,8 @@ def main():
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                          "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},
             "stages_ms": {k: round(float(np.mean(v)), 3) for k, v in per.items()},
+            "frames_per_s": round(world * args.steps / t_max, 3),
+            "rays_per_s_M": round(H * W * world * args.steps / t_max / 1e6, 3),
             "counts_per_frame": {"valid_pairs": stage["pairs"] // max(launches, 1),
                                  "valid_samples": stage["valid"] // max(launches, 1),
                                  "filled_samples": stage["filled"] // max(launches, 1)},

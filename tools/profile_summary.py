@@ -18,7 +18,8 @@ AGG = ("k_point_pre", "k_pairs", "k_color")
 
 
 def short(name):
-    return name.split("(")[0].replace("pnr::", "").replace("void ", "")
+    n = name.split("(")[0].replace("pnr::", "").replace("void ", "")
+    return n.split("<")[0]
 
 
 def per_kernel(path, counters):
