@@ -10,7 +10,7 @@ HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -Wno-unused-result
 
 all: $(LIB) oracle
 
-build/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pnr_common.h include/pnr.h
+build/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pnr_common.h $(SRC_DIR)/agg_common.h include/pnr.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

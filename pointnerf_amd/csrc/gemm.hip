@@ -81,10 +81,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, int m0, int64_t k_b
       }
       k = kn;
       if (!more) break;
-#pragma unroll
       for (int u = 0; u < kGUnroll; ++u) {
         a[u] = an[u];
-#pragma unroll
         for (int t = 0; t < NT; ++t) b[u][t] = bn[u][t];
       }
     }
