@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 FLOP_PER_PAIR = 542_720     # GEMM FLOPs per valid (sample, neighbour) pair
 FLOP_PER_SAMPLE = 137_216   # colour-branch GEMM FLOPs per valid sample
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -52,6 +53,9 @@ def parse():
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
     ap.add_argument("--train-rays", type=int, default=3600, help="rays per train step (random_sample_size 60^2)")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="MLP compute precision: fp32 = the reference's (headline); bf16 = v_mfma_f32_32x32x16_bf16 "
+                         "operands with fp32 accumulation (SURVEY config c5)")
     return ap.parse_args()
 
 
@@ -225,6 +229,7 @@ def main():
 
     H = W = args.hw
     opt, pts, feats, agg, model = build_scene(args, device)
+    model.precision = args.dtype
     cams = cameras(8, H, W)
     SR = opt.SR
     # per-(frame, rank) pixel lists: step s renders frames s*world .. s*world+world-1
@@ -314,20 +319,26 @@ def main():
             except Exception:
                 traffic = None
         achieved = flops_per_launch / avg_agg_s / 1e12 if avg_agg_s > 0 else 0.0
+        peak = FP32_MFMA_PEAK_TFLOPS if args.dtype == "fp32" else BF16_MFMA_PEAK_TFLOPS
+        if args.dtype != "fp32":
+            traffic = None   # the committed PMC summary is for the fp32 kernels
         out = {
             "metric": "Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref",
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded lego-like 2M-point cloud, random-init lego viewmlp weights)",
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "grid_rebuild_per_step": not args.no_grid_rebuild,
                        "parallelism": f"dp{world} (16x16 ray tiles, RCCL all_gather of tiles)" if world > 1
                        else "single GPU"},
-            "roofline": {"bound": "mfma", "kernel": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
-                         "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+            "roofline": {"bound": "mfma", "kernel": (
+                             "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)"
+                             if args.dtype == "fp32" else
+                             "pnr_aggregate_fwd_bf16 = k_point_pre_b + k_pairs_b + k_color_b (v_mfma_f32_32x32x16_bf16)"),
+                         "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
                          "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},
             "stages_ms": {k: round(float(np.mean(v)), 3) for k, v in per.items()},
             "frames_per_s": round(world * args.steps / t_max, 3),

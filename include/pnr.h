@@ -241,6 +241,30 @@ int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, const pnr_mlp
                       float* out_feat, float* out_weight, float* out_conf, void* scratch,
                       size_t scratch_bytes, void* stream);
 
+/* bf16-MFMA variant (SURVEY config c5: bf16 MLP on v_mfma_f32_32x32x16_bf16,
+ * fp32 accumulation; NOT the reference's precision).  Weights are bf16
+ * fragment packs from pointnerf_amd.aggregator.frag_pack_bf16():
+ * W_f[t][T][lane][j] = W'[32T + (lane&31)][16t + 8(lane>>5) + j], W' = [W | bias | 0]
+ * for t < ceil((in+1)/16) + 2.  Same inputs / outputs as pnr_aggregate_fwd
+ * (pidx required); scratch of pnr_aggregate_scratch_bytes_bf16(n_max, N). */
+typedef struct {
+  const uint16_t* w1af;  /* block1.0 columns 0..223 + bias (per point)   */
+  const uint16_t* w1bf;  /* block1.0 columns 224..283 (no bias)         */
+  const uint16_t* w2f;   /* block1.2 + bias                             */
+  const uint16_t* w3f;   /* block3.0 + bias                             */
+  const uint16_t* w4f;   /* block3.2 + bias                             */
+  const float* wa; const float* ba;   /* alpha_branch.0 (fp32)          */
+  const uint16_t* wc1f; const uint16_t* wc2f; const uint16_t* wc3f;  /* color_branch.{0,2,4} + bias */
+  const float* rw2c;
+  float neg_slope;
+  int32_t act_super;
+} pnr_mlp_bf16;
+
+int pnr_aggregate_scratch_bytes_bf16(int64_t n_max, int64_t n_points, size_t* out);
+int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
+                           float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                           size_t scratch_bytes, void* stream);
+
 /* PointAggregator.forward signature (pre-gathered tensors): pts tables are the
  * gathered [rows*K, C] tensors, s->pidx must be NULL (pair row = row*K + k),
  * pts->pers required, validity from pair_mask[rows*K] (sample_pnt_mask). */

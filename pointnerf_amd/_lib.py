@@ -63,6 +63,12 @@ class Mlp(ctypes.Structure):
                 ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32)]
 
 
+class MlpBf16(ctypes.Structure):
+    _fields_ = [("w1af", c_void_p), ("w1bf", c_void_p), ("w2f", c_void_p), ("w3f", c_void_p), ("w4f", c_void_p),
+                ("wa", c_void_p), ("ba", c_void_p), ("wc1f", c_void_p), ("wc2f", c_void_p), ("wc3f", c_void_p),
+                ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32)]
+
+
 class Points(ctypes.Structure):
     _fields_ = [("n", c_int64), ("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
                 ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p),
@@ -109,6 +115,9 @@ SIGNATURES = {
                                   c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_scratch_bytes_bf16": (c_int, [c_int64, c_int64, P(c_size_t)]),
+    "pnr_aggregate_fwd_bf16": (c_int, [P(Points), P(Samples), P(MlpBf16), c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train": (c_int, [P(Points), P(Samples), P(Mlp), P(AggSaved), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, P(AggSaved), c_void_p,
@@ -196,6 +205,13 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False):
     check(lib().pnr_gemm_tn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
                             scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")
     return (C, cs) if colsum else C
+
+
+def aggregate_scratch_bf16(n_max: int, n_points: int, device) -> torch.Tensor:
+    nb = c_size_t(0)
+    check(lib().pnr_aggregate_scratch_bytes_bf16(int(n_max), int(n_points), ctypes.byref(nb)),
+          "pnr_aggregate_scratch_bytes_bf16")
+    return torch.empty((int(nb.value) + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
 def stream_ptr(device=None):

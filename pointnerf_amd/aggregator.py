@@ -82,6 +82,27 @@ def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor
     return Wp.view(NT, 32, tot, 2).permute(2, 0, 3, 1).contiguous().view(-1)
 
 
+BF16_PAD = 2   # kBPad in aggregate_bf16.hip
+
+
+def frag_pack_bf16(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 A-operand fragments of v_mfma_f32_32x32x16_bf16:
+    F[t][T][lane][j] = W'[32T + (lane & 31)][16t + 8(lane >> 5) + j] of
+    W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus BF16_PAD zero ones
+    (round-to-nearest-even conversion)."""
+    out_f, kin = W.shape
+    assert out_f % 32 == 0
+    cols = kin + (1 if bias is not None else 0)
+    tot = (cols + 15) // 16 + BF16_PAD
+    NT = out_f // 32
+    Wp = torch.zeros((out_f, 16 * tot), dtype=torch.float32, device=W.device)
+    Wp[:, :kin] = W.float()
+    if bias is not None:
+        Wp[:, kin] = bias.float()
+    F = Wp.view(NT, 32, tot, 2, 8).permute(2, 0, 3, 1, 4).contiguous()   # [t][T][h][r][j]
+    return F.view(-1).to(torch.bfloat16)
+
+
 def frag_unpack(F: torch.Tensor, kin: int, out_f: int = 256) -> torch.Tensor:
     NT = out_f // 32
     tot = F.numel() // (NT * 64)
@@ -147,6 +168,30 @@ class PointAggregator(nn.Module):
         m.act_super = self.act_super
         self._packed, self._packed_key = (m, t), key
         return self._packed
+
+    def packed_bf16(self) -> tuple[L.MlpBf16, dict]:
+        """bf16 fragment packs for pnr_aggregate_fwd_bf16 (cached like packed())."""
+        ps = list(self.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in ps) + ((self.rw2c.data_ptr(), self.rw2c._version),)
+        if getattr(self, "_packed16", None) is not None and key == self._packed16_key:
+            return self._packed16
+        with torch.no_grad():
+            b1, b3, cb = self.block1, self.block3, self.color_branch
+            t = dict(w1af=frag_pack_bf16(b1[0].weight[:, :224], b1[0].bias),
+                     w1bf=frag_pack_bf16(b1[0].weight[:, 224:]),
+                     w2f=frag_pack_bf16(b1[2].weight, b1[2].bias), w3f=frag_pack_bf16(b3[0].weight, b3[0].bias),
+                     w4f=frag_pack_bf16(b3[2].weight, b3[2].bias),
+                     wa=self.alpha_branch[0].weight.float().reshape(-1).contiguous(),
+                     ba=self.alpha_branch[0].bias.float().contiguous(),
+                     wc1f=frag_pack_bf16(cb[0].weight, cb[0].bias), wc2f=frag_pack_bf16(cb[2].weight, cb[2].bias),
+                     wc3f=frag_pack_bf16(cb[4].weight, cb[4].bias), rw2c=self.rw2c.float().contiguous())
+        m = L.MlpBf16()
+        for k, v in t.items():
+            setattr(m, k, v.data_ptr())
+        m.neg_slope = float(self.neg_slope)
+        m.act_super = self.act_super
+        self._packed16, self._packed16_key = (m, t), key
+        return self._packed16
 
     def set_rw2c(self, rw2c: torch.Tensor | None):
         """Uniform Rw2c of the point cloud (neural_points.py:289; eye by default)."""

@@ -1,0 +1,617 @@
+// bf16-MFMA variant of the fused aggregation (SURVEY config c5: "bf16 point
+// features + MFMA MLP"): same algorithm and data flow as aggregate.hip, with
+// every GEMM on v_mfma_f32_32x32x16_bf16 (bf16 operands, fp32 accumulation,
+// 16x the fp32 MFMA rate).  Not the headline path (the reference computes in
+// fp32); selected explicitly by the caller.
+//
+// Layout.  A layer input X is kept in LDS pair-major in bf16, Xb[pair][k]
+// (pitch kPB, 16-B aligned rows): the B fragment of k-step t for lane
+// (c, h) -- B[k = 16t + 8h + j][col c], j = 0..7 -- is ONE ds_read_b128 at
+// Xb[pair c][16t + 8h] (row pitch 560 B spreads 16 lanes over all 64 banks),
+// and an accumulator quad (4 consecutive neurons of one pair) is one 8-B
+// store.  Weights are fragment-packed (aggregator.frag_pack_bf16):
+// W_f[t][T][lane][j] = W'[32T + (lane&31)][16t + 8(lane>>5) + j], one 16-B
+// load per lane per (k-step, tile).
+//
+// Tiles.  A 4-wave workgroup owns 128 (sample, neighbour) pairs = 16 samples
+// x K 8 (k_pairs_b) or 128 samples (k_color_b) or 128 points (k_point_pre_b);
+// wave w owns output tiles {2w, 2w+1} (256-wide layers) or {w} (128-wide)
+// for all four 32-column quarters, so each 1-KB weight fragment feeds 4
+// MFMAs.  ~78 KB of LDS per workgroup -> 2 per CU (2 waves per SIMD).
+#include "agg_common.h"
+
+namespace pnr {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kBT = 128;                 // columns (pairs / samples / points) per tile
+constexpr int kBPT = kBT / 32;           // 32-column quarters per tile
+constexpr int kBWaves = 4;
+constexpr int kPB = 280;                 // Xb pitch (bf16) for <= 272 input rows (k_pairs_b, k_point_pre_b)
+constexpr int kPBc = 296;                // Xb pitch for the colour branch (288 input rows)
+constexpr int kBPad = 2;                 // zero k-steps padded onto bf16 weight packs (prefetch)
+static_assert(kBPad >= 2, "mlp_layer_b loads weights two k-steps ahead");
+
+struct AggArgsB {
+  pnr_points pts;
+  pnr_samples s;
+  pnr_mlp_bf16 w;
+  uint16_t* p1;      // [n_p1, 256] bf16 per-point block1.0 partial
+  uint16_t* hid;     // [n_max, 256] bf16 K-summed features
+  int32_t* vmask;    // [n_max]
+  float* out_feat;
+  float* out_weight;
+  float* out_conf;
+};
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  bf16x2 p = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, p);
+}
+__device__ __forceinline__ float bf16_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+__device__ __forceinline__ uint16_t to_bf16(float a) { return __builtin_bit_cast(uint16_t, (__bf16)a); }
+
+// Y^T += W . X^T on bf16 MFMA: NT output tiles x PT 32-column quarters over
+// nsteps k-steps of 16.  Weight fragments 2 steps ahead, B fragments 1 step.
+template <int NT, int PT, int NTOT, int PITCH>
+__device__ __forceinline__ void mlp_layer_b(f32x16 (&acc)[PT * NT], const uint4* __restrict__ wf,
+                                            const uint16_t* Xb, int nsteps, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const uint4* p = wf + lane;
+  uint4 a0[NT], a1[NT];
+#pragma unroll
+  for (int T = 0; T < NT; ++T) {
+    a0[T] = p[(0 * NTOT + T) * 64];
+    a1[T] = p[(1 * NTOT + T) * 64];
+  }
+  const uint16_t* xr = Xb + c * PITCH + 8 * h;
+  uint4 x[PT];
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) x[pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH);
+#pragma unroll 1
+  for (int t = 0; t < nsteps; ++t) {
+    uint4 y[PT];
+    const int tn = t + 1 < nsteps ? t + 1 : t;
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) y[pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH + 16 * tn);
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+        acc[pt * NT + T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            __builtin_bit_cast(bf16x8, a0[T]), __builtin_bit_cast(bf16x8, x[pt]), acc[pt * NT + T], 0, 0, 0);
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      a0[T] = a1[T];
+      a1[T] = p[((t + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
+    }
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) x[pt] = y[pt];
+  }
+}
+
+// Activated accumulators (rows 32(T0+T) + 8q + 4h + i) -> Xb[col][row] bf16.
+template <int NT, int PT, int PITCH>
+__device__ __forceinline__ void store_act_b(const f32x16 (&acc)[PT * NT], uint16_t* Xb, float s, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16& v = acc[pt * NT + T];
+        uint2 u;
+        u.x = pack_bf16x2(lrelu(v[4 * q], s), lrelu(v[4 * q + 1], s));
+        u.y = pack_bf16x2(lrelu(v[4 * q + 2], s), lrelu(v[4 * q + 3], s));
+        *reinterpret_cast<uint2*>(Xb + (32 * pt + c) * PITCH + 32 * (T0 + T) + 8 * q + 4 * h) = u;
+      }
+}
+
+// Rows [r0, r0 + 16) of one column: first `nval` from vals, then 1 (bias) if
+// bias, then zeros -- the inputs past a layer's last real row.
+__device__ __forceinline__ void tail_rows_b(uint16_t* Xb, int pitch, int col, int r0, const float* vals, int nval) {
+  unsigned w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float lo = 2 * i < nval ? vals[2 * i] : 0.f;
+    const float hi = 2 * i + 1 < nval ? vals[2 * i + 1] : 0.f;
+    w[i] = pack_bf16x2(lo, hi);
+  }
+  uint4* d = reinterpret_cast<uint4*>(Xb + col * pitch + r0);
+  d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// ---------------------------------------------------------------------------
+// k_point_pre_b: P1[p] = W1[:, :224] . [emb, PE_3(emb)] + b1 (bf16 result).
+__global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xb_dyn[];
+  uint16_t* Xb = xb_dyn;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;
+  const int64_t ntiles = cdiv(np, kBT);
+  const uint4* wf = reinterpret_cast<const uint4*>(A.w.w1af) + 2 * wid * 64;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // inputs: thread = (point col = tid & 127, half = tid >> 7): channels [16 half, 16 half + 16)
+    {
+      const int col = threadIdx.x & (kBT - 1), half = threadIdx.x >> 7;
+      const int64_t pt = tile * kBT + col;
+      const bool act = pt < np;
+      const int64_t prow = act ? (A.pts.used ? (int64_t)A.pts.used[pt] : pt) : 0;
+      const float* e = A.pts.emb + prow * kEmb + 16 * half;
+      uint16_t* xc = Xb + col * kPB;
+#pragma unroll 2
+      for (int q = 0; q < 4; ++q) {
+        const float4 e4 = act ? reinterpret_cast<const float4*>(e)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ch = 16 * half + 4 * q + u;
+          xc[ch] = to_bf16(ev[u]);
+          float s0, c0;
+          sincosf(ev[u], &s0, &c0);
+          const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
+          const float s2 = 2.f * s1 * c1, c2 = (c1 - s1) * (c1 + s1);
+          const int r0 = kEmb + 6 * ch;
+          *reinterpret_cast<unsigned*>(xc + r0) = pack_bf16x2(s0, c0);
+          *reinterpret_cast<unsigned*>(xc + r0 + 2) = pack_bf16x2(s1, c1);
+          *reinterpret_cast<unsigned*>(xc + r0 + 4) = pack_bf16x2(s2, c2);
+        }
+      }
+      if (half == 0) {
+        const float one = 1.f;
+        tail_rows_b(Xb, kPB, col, 224, &one, 1);   // bias row 224, zeros to 239
+      }
+    }
+    __syncthreads();
+    f32x16 acc[kBPT * 2];
+#pragma unroll
+    for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<2, kBPT, 8, kPB>(acc, wf, Xb, 15, lane);
+#pragma unroll
+    for (int pt = 0; pt < kBPT; ++pt) {
+      const int64_t row = tile * kBT + 32 * pt + c;
+      if (row >= np) continue;
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x16& v = acc[pt * 2 + T];
+          uint2 u;
+          u.x = pack_bf16x2(v[4 * q], v[4 * q + 1]);
+          u.y = pack_bf16x2(v[4 * q + 2], v[4 * q + 3]);
+          *reinterpret_cast<uint2*>(A.p1 + row * kHid + 32 * (2 * wid + T) + 8 * q + 4 * h) = u;
+        }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_pairs_b: gather + weights + PE_5 + the rest of block1, block3, alpha and
+// K-sums for 128 pairs per workgroup.
+constexpr int kBTS = kBT / kKN;   // samples per tile
+constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTS + 8 * kBT + kBT) * 4;
+
+__global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xb_dyn[];
+  uint16_t* Xb = xb_dyn;                                   // [128][kPB]
+  float* wtL = reinterpret_cast<float*>(Xb + kBT * kPB);   // [128]
+  float* apart = wtL + kBT;                                // [4][128]
+  int* sflag = reinterpret_cast<int*>(apart + 4 * kBT);    // [16]
+  float* exL = reinterpret_cast<float*>(sflag + kBTS);     // [8][128]
+  int* prowL = reinterpret_cast<int*>(exL + 8 * kBT);      // [128]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int K = A.s.K;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kBTS);
+  const float neg = A.w.neg_slope;
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  float cam_c[3] = {0.f, 0.f, 0.f}, cam_R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+  if (!A.pts.pers) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cam_c[i] = A.pts.campos[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cam_R[i] = A.pts.camrot[i];
+  }
+  const int T0 = 2 * wid;
+  const uint4* w1b = reinterpret_cast<const uint4*>(A.w.w1bf) + T0 * 64;
+  const uint4* w2 = reinterpret_cast<const uint4*>(A.w.w2f) + T0 * 64;
+  const uint4* w3 = reinterpret_cast<const uint4*>(A.w.w3f) + T0 * 64;
+  const uint4* w4 = reinterpret_cast<const uint4*>(A.w.w4f) + T0 * 64;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
+    {
+      const int col = threadIdx.x & (kBT - 1), role = threadIdx.x >> 7;
+      const int j = col >> 3, k = col & 7;
+      const int64_t v = tile * kBTS + j;
+      const bool active = v < n;
+      const int64_t row = active ? sample_row(A.s, v) : 0;
+      int64_t prow = -1;
+      bool valid = false;
+      if (active && k < K) {
+        const int pid = A.s.pidx[row * K + k];
+        valid = pid >= 0;
+        prow = valid ? pid : 0;
+      }
+      float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
+      if (active) {
+        const int64_t drow = dir_row(A.s, row);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          sw[a] = A.s.sample_w[row * 3 + a];
+          sp[a] = A.s.sample_p[row * 3 + a];
+          vd[a] = A.s.dirs[drow * 3 + a];
+        }
+      }
+      float pw[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, colr[3] = {0.f, 0.f, 0.f},
+            pdir[3] = {0.f, 0.f, 0.f};
+      float cf = 1.f;
+      if (valid) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          pw[a] = A.pts.xyz[prow * 3 + a];
+          colr[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
+          pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
+        }
+        if (A.pts.pers) {
+#pragma unroll
+          for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
+        } else {
+          world_to_pers(pw, cam_c, cam_R, pp);
+        }
+      }
+      if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
+      float d6[6];
+      d6[0] = pw[0] - sw[0];
+      d6[1] = pw[1] - sw[1];
+      d6[2] = pw[2] - sw[2];
+      d6[3] = pp[0] * pp[2] - sp[0] * sp[2];
+      d6[4] = pp[1] * pp[2] - sp[1] * sp[2];
+      d6[5] = pp[2] - sp[2];
+      const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
+      const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
+      const float wsum = xor8_sum(wl);
+      const float wn = wl / fmaxf(wsum, 1e-8f);
+      const float confc = fminf(fmaxf(cf, 1e-4f), 1.f);
+      const bool samp_valid = xor8_sum(valid ? 1.f : 0.f) > 0.f;
+      float dr6[6];
+      mat3(Rw, d6, dr6);
+      dr6[3] = d6[3];
+      dr6[4] = d6[4];
+      dr6[5] = d6[5];
+      if (role == 0) {
+        float vrot[3], drot[3];
+        mat3(Rw, vd, vrot);
+        mat3(Rw, pdir, drot);
+        const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
+        const float ex[8] = {colr[0], colr[1], colr[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2],
+                             dot, 1.f};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) exL[e * kBT + col] = ex[e];
+        wtL[col] = wn * confc;
+        prowL[col] = valid ? (int)prow : -1;
+        if (k == 0) sflag[j] = active && samp_valid;
+        if (active && k < K) {
+          if (A.out_weight) A.out_weight[row * K + k] = wn;
+          if (A.out_conf) A.out_conf[row * K + k] = confc;
+        }
+        *reinterpret_cast<uint2*>(Xb + col * kPB + 60) = make_uint2(0u, 0u);   // rows 60..63: k padding
+      }
+      // 5-band PE of the rotated distance -> rows 2e, 2e+1 (e = 5 ch + f); role r: e = r (mod 2)
+      uint16_t* xc = Xb + col * kPB;
+#pragma unroll 1
+      for (int e = role; e < 30; e += 2) {
+        const int ch = e / 5, f = e - 5 * ch;
+        float dc = dr6[0];
+        dc = ch == 1 ? dr6[1] : dc;
+        dc = ch == 2 ? dr6[2] : dc;
+        dc = ch == 3 ? dr6[3] : dc;
+        dc = ch == 4 ? dr6[4] : dc;
+        dc = ch == 5 ? dr6[5] : dc;
+        float sn, cs;
+        sincosf(dc * (float)(1 << f), &sn, &cs);
+        *reinterpret_cast<unsigned*>(xc + 2 * e) = pack_bf16x2(sn, cs);
+      }
+    }
+    __syncthreads();
+    // -------------------------------------------- P1 gather into the accumulators
+    f32x16 acc[kBPT * 2];
+#pragma unroll
+    for (int pt = 0; pt < kBPT; ++pt) {
+      const int pr = prowL[32 * pt + c];
+      const int64_t p1r = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        if (p1r >= 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint2 u = *reinterpret_cast<const uint2*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 8 * q + 4 * h);
+            acc[pt * 2 + T][4 * q + 0] = bf16_lo(u.x);
+            acc[pt * 2 + T][4 * q + 1] = bf16_hi(u.x);
+            acc[pt * 2 + T][4 * q + 2] = bf16_lo(u.y);
+            acc[pt * 2 + T][4 * q + 3] = bf16_hi(u.y);
+          }
+        } else {
+          acc[pt * 2 + T] = (f32x16){0.f};
+        }
+      }
+    }
+    // -------------------------------------------- block1: + W1[:, 224:284] . PE_5 (4 steps), block1.2
+    mlp_layer_b<2, kBPT, 8, kPB>(acc, w1b, Xb, 4, lane);
+    __syncthreads();
+    store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
+    if (wid == 0) {
+      const float one = 1.f;
+      tail_rows_b(Xb, kPB, lane, 256, &one, 1);
+      tail_rows_b(Xb, kPB, lane + 64, 256, &one, 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<2, kBPT, 8, kPB>(acc, w2, Xb, 17, lane);
+    __syncthreads();
+    store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
+    if (wid == 0) {   // block3.0 inputs 256..263 (+ zeros to 271)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int col = lane + 64 * half;
+        float ex[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ex[e] = exL[e * kBT + col];
+        tail_rows_b(Xb, kPB, col, 256, ex, 8);
+      }
+    }
+    __syncthreads();
+    // -------------------------------------------- block3
+#pragma unroll
+    for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<2, kBPT, 8, kPB>(acc, w3, Xb, 17, lane);
+    __syncthreads();
+    store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
+    if (wid == 0) {
+      const float one = 1.f;
+      tail_rows_b(Xb, kPB, lane, 256, &one, 1);
+      tail_rows_b(Xb, kPB, lane + 64, 256, &one, 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<2, kBPT, 8, kPB>(acc, w4, Xb, 17, lane);
+    // -------------------------------------------- alpha + K sums from the fp32 accumulators
+    float pa_part[kBPT];
+#pragma unroll
+    for (int pt = 0; pt < kBPT; ++pt) {
+      pa_part[pt] = 0.f;
+      const int col = 32 * pt + c;
+      const float wtp = wtL[col];
+      const int sj = col >> 3;
+      const int64_t vo = tile * kBTS + sj;
+      const bool wr = vo < n && sflag[sj];
+      const int i8 = c & 7;
+      const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        float vv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float hv = lrelu(acc[pt * 2 + T][r], neg);
+          pa_part[pt] += A.w.wa[32 * (T0 + T) + acc_row(r, h)] * hv;
+          vv[r] = wtp * hv;
+        }
+        float w8[8], w4v[4], w2[2];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float send = b2 ? vv[q] : vv[q + 8];
+          const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x141,
+                                                                                0xf, 0xf, false));
+          w8[q] = (b2 ? vv[q + 8] : vv[q]) + recv;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float send = b1 ? w8[q] : w8[q + 4];
+          const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E,
+                                                                                0xf, 0xf, false));
+          w4v[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float send = b0 ? w4v[q] : w4v[q + 2];
+          const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
+                                                                                0xf, 0xf, false));
+          w2[q] = (b0 ? w4v[q + 2] : w4v[q]) + recv;
+        }
+        if (wr)
+          *reinterpret_cast<unsigned*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h) =
+              pack_bf16x2(w2[0], w2[1]);
+      }
+      pa_part[pt] += __shfl_xor(pa_part[pt], 32);
+    }
+    if (h == 0) {
+#pragma unroll
+      for (int pt = 0; pt < kBPT; ++pt) apart[wid * kBT + 32 * pt + c] = pa_part[pt];
+    }
+    __syncthreads();
+    if (wid < 2) {
+      const int col = 64 * wid + lane;
+      const int j = col >> 3, k = col & 7;
+      const float pa = apart[col] + apart[kBT + col] + apart[2 * kBT + col] + apart[3 * kBT + col] + A.w.ba[0];
+      const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
+      const float alpha_s = xor8_sum(wtL[col] * alpha_k);
+      const int64_t vo = tile * kBTS + j;
+      if (k == 0 && vo < n) {
+        A.vmask[vo] = sflag[j];
+        if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_color_b: [hid, PE_4(view dir)] -> 128 -> 128 -> 128 for 128 samples.
+constexpr size_t kColorBLds = (size_t)kBT * kPBc * 2;
+
+__global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xb_dyn[];
+  uint16_t* Xb = xb_dyn;   // [128][kPBc]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kBT);
+  const float neg = A.w.neg_slope;
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  const uint4* w1 = reinterpret_cast<const uint4*>(A.w.wc1f) + wid * 64;
+  const uint4* w2 = reinterpret_cast<const uint4*>(A.w.wc2f) + wid * 64;
+  const uint4* w3 = reinterpret_cast<const uint4*>(A.w.wc3f) + wid * 64;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t v0 = tile * kBT;
+    // hid rows (512 B each) -> Xb rows 0..255: 16 x 16-B chunks per thread
+    for (int i = threadIdx.x; i < kBT * 32; i += 64 * kBWaves) {
+      const int col = i >> 5, q = i & 31;
+      const int64_t v = v0 + col;
+      const bool ok = v < n && A.vmask[v] != 0;
+      const uint4 u = ok ? reinterpret_cast<const uint4*>(A.hid + v * kHid)[q] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(Xb + col * kPBc + 8 * q) = u;
+    }
+    // view PE (ori dropped): rows 256 + 4ch + f = sin, 268 + 4ch + f = cos, bias 280, zeros to 287
+    if (threadIdx.x < kBT) {
+      const int col = threadIdx.x;
+      const int64_t v = v0 + col;
+      float vrot[3] = {0.f, 0.f, 0.f};
+      if (v < n) {
+        const int64_t row = sample_row(A.s, v);
+        const int64_t drow = dir_row(A.s, row);
+        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+        mat3(Rw, vd, vrot);
+      }
+      float pe[32];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          float sn, cs;
+          sincosf(vrot[ch] * (float)(1 << f), &sn, &cs);
+          pe[4 * ch + f] = sn;
+          pe[12 + 4 * ch + f] = cs;
+        }
+      pe[24] = 1.f;
+#pragma unroll
+      for (int i = 25; i < 32; ++i) pe[i] = 0.f;
+      tail_rows_b(Xb, kPBc, col, 256, pe, 16);
+      tail_rows_b(Xb, kPBc, col, 272, pe + 16, 16);
+    }
+    __syncthreads();
+    f32x16 acc[kBPT];
+#pragma unroll
+    for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<1, kBPT, 4, kPBc>(acc, w1, Xb, 18, lane);
+    __syncthreads();
+    store_act_b<1, kBPT, kPBc>(acc, Xb, neg, lane, wid);
+    if (wid == 0) {
+      const float one = 1.f;
+      tail_rows_b(Xb, kPBc, lane, kC, &one, 1);
+      tail_rows_b(Xb, kPBc, lane + 64, kC, &one, 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<1, kBPT, 4, kPBc>(acc, w2, Xb, 9, lane);
+    __syncthreads();
+    store_act_b<1, kBPT, kPBc>(acc, Xb, neg, lane, wid);
+    if (wid == 0) {
+      const float one = 1.f;
+      tail_rows_b(Xb, kPBc, lane, kC, &one, 1);
+      tail_rows_b(Xb, kPBc, lane + 64, kC, &one, 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
+    mlp_layer_b<1, kBPT, 4, kPBc>(acc, w3, Xb, 9, lane);
+#pragma unroll
+    for (int pt = 0; pt < kBPT; ++pt) {
+      const int64_t v = v0 + 32 * pt + c;
+      if (v >= n || A.vmask[v] == 0) continue;
+      float* o = A.out_feat + v * (kC + 1) + 1 + 32 * wid + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
+    }
+    __syncthreads();
+  }
+}
+
+static size_t scratch_need_b(int64_t n_max, int64_t n_p1) {
+  const int64_t nm = n_max > 0 ? n_max : 1;
+  const int64_t np = n_p1 > 0 ? n_p1 : 1;
+  return (size_t)nm * kHid * 2 + (size_t)cdiv(nm, 4) * 16 + (size_t)np * kHid * 2;
+}
+
+}  // namespace pnr
+
+using namespace pnr;
+
+extern "C" int pnr_aggregate_scratch_bytes_bf16(int64_t n_max, int64_t n_points, size_t* out) {
+  PNR_CHECK_ARG(out && n_max >= 0 && n_points >= 0, "aggregate_scratch_bytes_bf16: bad args");
+  *out = scratch_need_b(n_max, n_points);
+  return PNR_OK;
+}
+
+extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
+                                      float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                                      size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(pts && s && w && out_feat, "aggregate_bf16: null pointer");
+  PNR_CHECK_ARG(pts->xyz && pts->emb && s->pidx, "aggregate_bf16: point xyz/emb and pidx required");
+  PNR_CHECK_ARG(s->sample_w && s->sample_p && s->dirs && s->dir_div >= 1, "aggregate_bf16: sample arrays required");
+  PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate_bf16: K=%d unsupported (1..8)", s->K);
+  PNR_CHECK_ARG(w->w1af && w->w1bf && w->w2f && w->w3f && w->w4f && w->wa && w->ba && w->wc1f && w->wc2f && w->wc3f,
+                "aggregate_bf16: null weight");
+  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+                "aggregate_bf16: emb and scratch must be 16-B aligned");
+  PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_bf16: need pers or camera");
+  PNR_CHECK_ARG(!pts->used || pts->used_map, "aggregate_bf16: used list needs used_map");
+  const int64_t n_p1 = pts->used ? pts->n_used : pts->n;
+  PNR_CHECK_ARG(scratch_bytes >= scratch_need_b(s->n_max, n_p1), "aggregate_bf16: scratch too small");
+  if (s->n_max <= 0) return PNR_OK;
+  hipStream_t st = as_stream(stream);
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre_b),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kBT * kPB * 2)));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_b), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kColorBLds));
+    attr = true;
+  }
+  const int64_t nm = s->n_max;
+  AggArgsB a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  a.hid = static_cast<uint16_t*>(scratch);
+  a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
+  a.p1 = reinterpret_cast<uint16_t*>(a.vmask + cdiv(nm, 4) * 4);
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  hipLaunchKernelGGL(k_point_pre_b, dim3(grid_for(cdiv(n_p1, kBT), 1, 256 * 2)), dim3(64 * kBWaves),
+                     kBT * kPB * 2, st, a);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_pairs_b, dim3(grid_for(cdiv(nm, kBTS), 1, 256 * 2)), dim3(64 * kBWaves), kPairsBLds, st, a);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_color_b, dim3(grid_for(cdiv(nm, kBT), 1, 256 * 2)), dim3(64 * kBWaves), kColorBLds, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}

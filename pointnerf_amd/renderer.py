@@ -99,8 +99,11 @@ class NeuralPointsRayMarching(nn.Module):
     """neural_points_volumetric_model.NeuralPointsRayMarching, fused HIP path."""
 
     def __init__(self, opt, neural_points: NeuralPoints, aggregator: PointAggregator | None = None,
-                 chunk_rays: int | None = None):
+                 chunk_rays: int | None = None, precision: str = "fp32"):
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise L.PnrError(f"precision {precision!r}: fp32 (the reference's) or bf16 (MFMA fast path)")
+        self.precision = precision
         self.opt = opt
         self.neural_points = neural_points
         self.aggregator = aggregator if aggregator is not None else PointAggregator(opt).to(neural_points.device)
@@ -139,7 +142,8 @@ class NeuralPointsRayMarching(nn.Module):
                 raise L.PnrError("bg_color must have 1 or 128 channels")
         campos = campos.reshape(3).float().contiguous()
         camrot = camrot.reshape(3, 3).float().contiguous()
-        mlp, _keepw = self.aggregator.packed()
+        bf16 = self.precision == "bf16"
+        mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
         chunk = max(1, self.chunk_rays or R)
@@ -166,11 +170,18 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
             e2 = mark()
-            scratch = L.aggregate_scratch(max(Sv, 1), pts.n, dev)
-            L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
-                                              L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
-                                              L.stream_ptr(dev)),
-                    "pnr_aggregate_fwd")
+            if bf16:
+                scratch = L.aggregate_scratch_bf16(max(Sv, 1), pts.n, dev)
+                L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
+                                                       L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
+                                                       L.stream_ptr(dev)),
+                        "pnr_aggregate_fwd_bf16")
+            else:
+                scratch = L.aggregate_scratch(max(Sv, 1), pts.n, dev)
+                L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
+                                                  L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
+                                                  L.stream_ptr(dev)),
+                        "pnr_aggregate_fwd")
             e3 = mark()
             cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
             L.check(L.lib().pnr_composite_fwd(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),

@@ -1,0 +1,96 @@
+"""bf16-MFMA aggregation (pnr_aggregate_fwd_bf16, SURVEY config c5) against the
+fp32 path / CPU oracle.
+
+Tolerance (bf16 operands, 8-bit mantissa, fp32 accumulation): decoded
+features within 2 % relative RMS and |d| <= 5 % of the tensor's max; the
+rendered image within 40 dB PSNR of the fp32 oracle.  The query is shared
+with the fp32 path, so ray masks are identical."""
+import numpy as np
+import pytest
+import torch
+
+from formula import formula_params
+from oracle import oracle as O
+from scenes import oracle_points, scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(sc, cuda, params=None):
+    from pointnerf_amd.aggregator import PointAggregator
+    from pointnerf_amd.renderer import NeuralPoints
+    agg = PointAggregator(sc["opt"]).to(cuda)
+    if params is not None:
+        agg.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
+                       torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]))
+    return agg.eval(), np_
+
+
+def _features(agg, np_, sc, cuda, used=False):
+    """Both aggregate paths on one query; returns (fp32 feat, bf16 feat)."""
+    from pointnerf_amd import _lib as L
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda).contiguous()
+    bufs, hp, rays, qp = np_.querier.run(np_.xyz.detach(), rd, cp, cr, 2.0, 6.0)
+    cnt = bufs.read_counts()
+    Sv, K = cnt["S_valid"], sc["opt"].K
+    s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
+                  bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(), bufs.fill_rs.data_ptr(),
+                  sc["opt"].SR, K)
+    pts, keep = np_.tables(cp, cr)
+    n_p1 = pts.n
+    if used:
+        from pointnerf_amd.train import used_points
+        u = used_points(bufs.pidx[:cnt["S_filled"] * K], pts.n)
+        pts.used, pts.n_used, pts.used_map = u[0].data_ptr(), u[0].numel(), u[1].data_ptr()
+        n_p1 = u[0].numel()
+    f32 = torch.zeros((Sv, 129), device=cuda)
+    f16 = torch.zeros((Sv, 129), device=cuda)
+    mlp, _k1 = agg.packed()
+    sc32 = L.aggregate_scratch(Sv, n_p1, cuda)
+    L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), L.ptr(f32),
+                                      None, None, L.ptr(sc32), sc32.numel() * 4, L.stream_ptr(cuda)), "fp32")
+    mlp16, _k2 = agg.packed_bf16()
+    sc16 = L.aggregate_scratch_bf16(Sv, n_p1, cuda)
+    L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp16),
+                                           L.ptr(f16), None, None, L.ptr(sc16), sc16.numel() * 4,
+                                           L.stream_ptr(cuda)), "bf16")
+    torch.cuda.synchronize()
+    return f32.cpu().numpy(), f16.cpu().numpy(), Sv
+
+
+@pytest.mark.parametrize("used", [False, True])
+def test_bf16_features_vs_fp32(cuda, used):
+    sc = scene(30000, H=48, W=48, theta=30.0)
+    torch.manual_seed(0)
+    agg, np_ = _setup(sc, cuda)          # random xavier weights (networks.py:163-172)
+    a, b, Sv = _features(agg, np_, sc, cuda, used=used)
+    assert Sv > 1000
+    for name, sl in (("alpha", slice(0, 1)), ("color", slice(1, 129))):
+        d = np.abs(a[:, sl] - b[:, sl])
+        r = np.abs(a[:, sl])
+        assert np.sqrt((d ** 2).mean() / (r ** 2).mean()) < 0.02, name
+        assert d.max() <= 0.05 * r.max(), name
+
+
+def test_bf16_render_vs_oracle(cuda):
+    from pointnerf_amd.renderer import NeuralPointsRayMarching
+    sc = scene(30000, H=48, W=48, theta=200.0)
+    params = formula_params(salt=0.1)
+    agg, np_ = _setup(sc, cuda, params)
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="bf16")
+    with torch.no_grad():
+        c, op, bg, mask = m.render_rays(torch.from_numpy(sc["campos"]).to(cuda),
+                                        torch.from_numpy(sc["camrot"]).to(cuda),
+                                        torch.from_numpy(sc["raydir"]).to(cuda), 2.0, 6.0,
+                                        torch.from_numpy(sc["bg"]).to(cuda))
+        c2, _, _, _ = m.render_rays(torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda),
+                                    torch.from_numpy(sc["raydir"]).to(cuda), 2.0, 6.0,
+                                    torch.from_numpy(sc["bg"]).to(cuda))
+    assert torch.equal(c, c2)            # deterministic
+    ref = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"])
+    assert np.array_equal(mask.cpu().numpy(), ref["ray_mask"])
+    x, y = c.cpu().numpy(), ref["coarse_raycolor"]
+    psnr = 10 * np.log10(float(np.abs(y).max()) ** 2 / max(float(np.mean((x - y) ** 2)), 1e-30))
+    assert psnr >= 40.0, psnr

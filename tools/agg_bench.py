@@ -16,11 +16,13 @@ def main():
     ap.add_argument("--points", type=int, default=2_000_000)
     ap.add_argument("--hw", type=int, default=800)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--precision", default="fp32")
     a = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
     ns = argparse.Namespace(points=a.points)
     opt, pts, feats, agg, model = bench.build_scene(ns, dev)
+    model.precision = a.precision
     campos, camrot, rd = bench.cameras(1, a.hw, a.hw)[0]
     cp, cr, rd = [torch.from_numpy(x).to(dev) for x in (campos, camrot, rd)]
     bg = torch.rand(128, device=dev)
