@@ -20,6 +20,10 @@
 // MFMAs.  ~78 KB of LDS per workgroup -> 2 per CU (2 waves per SIMD).
 #include "agg_common.h"
 
+#ifndef PNR_ABLATE
+#define PNR_ABLATE 0  // dev-only timing ablations (tools/build_ablations.sh)
+#endif
+
 namespace pnr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -85,7 +89,7 @@ __device__ __forceinline__ void mlp_layer_b(f32x16 (&acc)[PT * NT], const uint4*
 #pragma unroll
     for (int T = 0; T < NT; ++T) {
       a0[T] = a1[T];
-      a1[T] = p[((t + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
+      a1[T] = p[((((PNR_ABLATE & 8) ? 0 : t) + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
     }
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) x[pt] = y[pt];
@@ -309,7 +313,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       // 5-band PE of the rotated distance -> rows 2e, 2e+1 (e = 5 ch + f); role r: e = r (mod 2)
       uint16_t* xc = Xb + col * kPB;
 #pragma unroll 1
-      for (int e = role; e < 30; e += 2) {
+      for (int e = role; e < ((PNR_ABLATE & 2) ? 0 : 30); e += 2) {
         const int ch = e / 5, f = e - 5 * ch;
         float dc = dr6[0];
         dc = ch == 1 ? dr6[1] : dc;
@@ -331,7 +335,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       const int64_t p1r = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        if (p1r >= 0) {
+        if (p1r >= 0 && !(PNR_ABLATE & 1)) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint2 u = *reinterpret_cast<const uint2*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 8 * q + 4 * h);
@@ -387,24 +391,27 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     mlp_layer_b<2, kBPT, 8, kPB>(acc, w4, Xb, 17, lane);
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
-    float pa_part[kBPT];
+    if (!(PNR_ABLATE & 4)) {
+    float pa_part[kBPT] = {0.f, 0.f, 0.f, 0.f};
+    const int i8 = c & 7;
+    const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
 #pragma unroll
-    for (int pt = 0; pt < kBPT; ++pt) {
-      pa_part[pt] = 0.f;
-      const int col = 32 * pt + c;
-      const float wtp = wtL[col];
-      const int sj = col >> 3;
-      const int64_t vo = tile * kBTS + sj;
-      const bool wr = vo < n && sflag[sj];
-      const int i8 = c & 7;
-      const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
+    for (int T = 0; T < 2; ++T) {
+      float wa[16];
 #pragma unroll
-      for (int T = 0; T < 2; ++T) {
+      for (int r = 0; r < 16; ++r) wa[r] = A.w.wa[32 * (T0 + T) + acc_row(r, h)];
+#pragma unroll
+      for (int pt = 0; pt < kBPT; ++pt) {
+        const int col = 32 * pt + c;
+        const float wtp = wtL[col];
+        const int sj = col >> 3;
+        const int64_t vo = tile * kBTS + sj;
+        const bool wr = vo < n && sflag[sj];
         float vv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float hv = lrelu(acc[pt * 2 + T][r], neg);
-          pa_part[pt] += A.w.wa[32 * (T0 + T) + acc_row(r, h)] * hv;
+          pa_part[pt] += wa[r] * hv;
           vv[r] = wtp * hv;
         }
         float w8[8], w4v[4], w2[2];
@@ -433,8 +440,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
           *reinterpret_cast<unsigned*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h) =
               pack_bf16x2(w2[0], w2[1]);
       }
-      pa_part[pt] += __shfl_xor(pa_part[pt], 32);
     }
+#pragma unroll
+    for (int pt = 0; pt < kBPT; ++pt) pa_part[pt] += __shfl_xor(pa_part[pt], 32);
     if (h == 0) {
 #pragma unroll
       for (int pt = 0; pt < kBPT; ++pt) apart[wid * kBT + 32 * pt + c] = pa_part[pt];
@@ -451,6 +459,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
         A.vmask[vo] = sflag[j];
         if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
       }
+    }
     }
     __syncthreads();
   }

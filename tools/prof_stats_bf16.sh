@@ -1,0 +1,8 @@
+#!/bin/bash
+# Dev tool: rocprofv3 kernel-trace stats over tools/agg_bench.py --precision bf16.
+set -e
+export TMPDIR=/tmp
+OUT=${1:-gpurun_out/stats_bf16}
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- python tools/agg_bench.py --reps 2 --precision bf16 > $OUT/run.log 2>&1
+find $OUT -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
