@@ -328,7 +328,10 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
 
-/* Weight-gradient GEMM: C[M,N] = A^T B over K rows (A[K,M], B[K,N] row-major,
+/* Weight-gradient GEMM (replaces the dW = dY^T X of torch's nn.Linear autograd
+ * for block1.0/1.2/3.0/3.2, point_aggregators.py:276-348 trained by
+ * mvs_points_volumetric_model.py:102-123 setup_optimizer):
+ * C[M,N] = A^T B over K rows (A[K,M], B[K,N] row-major,
  * leading dimensions lda/ldb), colsum_a[M] = column sums of A (bias gradient,
  * may be NULL).  M, N multiples of 32.  Split-K on MFMA with a deterministic
  * ordered reduction; scratch of pnr_gemm_tn_scratch_bytes(K, M, N). */
