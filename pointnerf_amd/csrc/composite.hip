@@ -157,16 +157,42 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
     if (lane + 64 < SR) a.opacity[r * SR + lane + 64] = so.op1;
     const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
     // colour = sum_s w_s * features[s, 1:] + bg * T_bg  (lane = channel)
+    // valid slots in slot order, 4 feature rows in flight per iteration
+    // (same accumulation order as a plain slot loop)
     float col0 = 0.f, col1 = 0.f;
-    const int smax = n < SR ? n : SR;
-    for (int s = 0; s < smax; ++s) {
-      const int q = s >> 6, src = s & 63;
-      const int vr = __shfl(q ? vrow[1] : vrow[0], src);
-      if (vr < 0) continue;
-      const float w = __shfl(q ? w1 : w0, src);
-      const float* f = a.feat + (int64_t)vr * CF + 1;
-      if (lane < C) col0 += w * f[lane];
-      if (lane + 64 < C) col1 += w * f[lane + 64];
+    unsigned long long m0 = __ballot(vrow[0] >= 0), m1 = __ballot(vrow[1] >= 0);
+    while (m0 | m1) {
+      int vr[4];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        vr[u] = -1;
+        w[u] = 0.f;
+        if (m0) {
+          const int src = __builtin_ctzll(m0);
+          m0 &= m0 - 1;
+          vr[u] = __shfl(vrow[0], src);
+          w[u] = __shfl(w0, src);
+        } else if (m1) {
+          const int src = __builtin_ctzll(m1);
+          m1 &= m1 - 1;
+          vr[u] = __shfl(vrow[1], src);
+          w[u] = __shfl(w1, src);
+        }
+      }
+      float f0[4], f1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* f = a.feat + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * CF + 1;
+        f0[u] = (vr[u] >= 0 && lane < C) ? f[lane] : 0.f;
+        f1[u] = (vr[u] >= 0 && lane + 64 < C) ? f[lane + 64] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (vr[u] < 0) break;
+        col0 += w[u] * f0[u];
+        col1 += w[u] * f1[u];
+      }
     }
     for (int c = lane, q = 0; c < C; c += 64, ++q) {
       float v = q == 0 ? col0 : (q == 1 ? col1 : 0.f);
