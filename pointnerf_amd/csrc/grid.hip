@@ -53,12 +53,23 @@ __global__ void __launch_bounds__(kBlock) k_bbox(const float* __restrict__ xyz, 
       mx[c] = max(mx[c], (unsigned)__shfl_xor((int)mx[c], o));
     }
   }
+  // one atomic per block and bound (the per-wave atomics on 6 shared words serialised)
+  __shared__ unsigned red[kBlock / 64][6];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      atomicMin(acc + c, mn[c]);
-      atomicMax(acc + 3 + c, mx[c]);
+      red[w][c] = mn[c];
+      red[w][3 + c] = mx[c];
     }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int c = threadIdx.x;
+    unsigned v = red[0][c];
+    for (int i = 1; i < kBlock / 64; ++i) v = c < 3 ? min(v, red[i][c]) : max(v, red[i][c]);
+    if (c < 3) atomicMin(acc + c, v);
+    else atomicMax(acc + c, v);
   }
 }
 
@@ -124,7 +135,7 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
                                                   const int32_t* __restrict__ pt_slot,
                                                   int32_t* __restrict__ coor_2_occ,
                                                   int32_t* __restrict__ occ_2_coor,
-                                                  uint32_t* __restrict__ occ_bits) {
+                                                  uint8_t* __restrict__ occ_bytes) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (!flag[i]) continue;
@@ -145,9 +156,26 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
     for (int x = x0; x < x1; ++x)
       for (int y = y0; y < y1; ++y)
         for (int z = z0; z < z1; ++z) {
-          int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
-          atomicOr(occ_bits + (id >> 5), 1u << (id & 31));
+          // idempotent byte stores (no atomics); packed into bits by k_pack_bits
+          occ_bytes[((int64_t)x * g.dims[1] + y) * g.dims[2] + z] = 1;
         }
+  }
+}
+
+// Dilated occupancy bytes -> bitmap word w (cells 32w .. 32w+31).
+__global__ void __launch_bounds__(kBlock) k_pack_bits(const uint8_t* __restrict__ occ_bytes, int64_t words,
+                                                      uint32_t* __restrict__ occ_bits) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    const uint4* b = reinterpret_cast<const uint4*>(occ_bytes + 32 * w);
+    const uint4 lo = b[0], hi = b[1];
+    const unsigned v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bits |= ((v[q] >> (8 * k)) & 0xffu ? 1u : 0u) << (4 * q + k);
+    occ_bits[w] = bits;
   }
 }
 
@@ -231,7 +259,7 @@ extern "C" int pnr_points_bbox(const float* xyz_dev, int64_t n, float* out6_dev,
   unsigned* acc = reinterpret_cast<unsigned*>(out6_dev);
   hipLaunchKernelGGL(k_bbox_init, dim3(1), dim3(64), 0, st, acc);
   PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bbox, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, st, xyz_dev, n, acc);
+  hipLaunchKernelGGL(k_bbox, dim3(grid_for(n, kBlock, 512)), dim3(kBlock), 0, st, xyz_dev, n, acc);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_bbox_fin, dim3(1), dim3(64), 0, st, acc);
   PNR_LAUNCH_CHECK();
@@ -253,7 +281,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   int rc;
   const int64_t words = cdiv(gvol, 32);
   const int64_t cap_o = p->max_o;
-  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->first_pt.ensure(gvol * 4)) ||
+  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->first_pt.ensure(gvol * 4 > words * 32 ? gvol * 4 : words * 32)) ||
       (rc = h->occ_bits.ensure(words * 4)) || (rc = h->occ_numpnts.ensure(cap_o * 4)) ||
       (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
       (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->slot_cursor.ensure(cap_o * 4)) ||
@@ -289,7 +317,6 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
 
   PNR_HIP(hipMemsetAsync(first_pt, 0x7f, (size_t)gvol * 4, st));
   PNR_HIP(hipMemsetAsync(coor_2_occ, 0xff, (size_t)gvol * 4, st));
-  PNR_HIP(hipMemsetAsync(occ_bits, 0, (size_t)words * 4, st));
   PNR_HIP(hipMemsetAsync(occ_numpnts, 0, (size_t)cap_o * 4, st));
   PNR_HIP(hipMemsetAsync(slot_cursor, 0, (size_t)cap_o * 4, st));
   PNR_HIP(hipMemsetAsync(occ_2_coor, 0xff, (size_t)cap_o * 12, st));
@@ -304,8 +331,14 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p,
                            h->scan_tmp.bytes, st)))
     return rc;
+  // first_pt is dead after k_first_flags: its storage (4 B/cell) holds the
+  // dilated occupancy bytes (32 * words <= 4 * gvol bytes)
+  uint8_t* occ_bytes = reinterpret_cast<uint8_t*>(first_pt);
+  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
   hipLaunchKernelGGL(k_claim, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, pt_cell, pt_flag,
-                     pt_slot, coor_2_occ, occ_2_coor, occ_bits);
+                     pt_slot, coor_2_occ, occ_2_coor, occ_bytes);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, occ_bits);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_count, dim3(gp), dim3(kBlock), 0, st, n, g, pt_cell, coor_2_occ,
                      occ_numpnts);
