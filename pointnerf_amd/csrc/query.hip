@@ -119,8 +119,15 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
           const int cnt = min(g.P, occ_numpnts[slot]);
           n_cand += cnt;
           const float4* rec = occ_pts + (int64_t)slot * g.P;
-          for (int gi = 0; gi < cnt; ++gi) {
-            const float4 v = rec[gi];
+          // records fetched 4 at a time (memory-level parallelism), visited in order
+          for (int g0 = 0; g0 < cnt; g0 += 4) {
+            float4 vb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+            if (g0 + u >= cnt) break;
+            const float4 v = vb[u];
             const float xv = __fsub_rn(v.x, p[0]);
             const float yv = __fsub_rn(v.y, p[1]);
             const float zv = __fsub_rn(v.z, p[2]);
@@ -162,6 +169,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
                   }
                 }
               }
+            }
             }
           }
         }
