@@ -382,6 +382,27 @@ int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const flo
                       const float* bg, int64_t NR, int32_t SR, int32_t C,
                       const float* d_ray_color, float* d_feat, void* stream);
 
+/* -------------------------------------------------------- 2-D neural renderer
+ * NeuralRenderer(input_dim=128) (models/neural_render/neural_renderer.py:24-104,
+ * applied at neural_points_volumetric_model.py:343-344 when neural_render == "cnn")
+ * on the composited feature image x[H,W,128] (row-major pixels = ray order):
+ * out_rgb[H,W,3] = sigmoid(conv_rgb0(x) + conv_rgb1(net0) + conv_rgb2(net1)),
+ * net0 = lrelu_0.2(conv_layers.0(x)), net1 = lrelu_0.2(conv_layers.1(net0)),
+ * all 3x3 / stride 1 / pad 1.  Weights per stage s: the trunk conv's and the
+ * rgb conv's [cout, cin, 3, 3] weights stacked as rows (trunk first, then the 3
+ * rgb rows, zero rows to a multiple of 32), columns k = (ky*3 + kx) * cin + ci,
+ * fragment-packed like pnr_mlp (frag_pack, no bias column); b_s = the stacked biases. */
+typedef struct {
+  const float* wf0; const float* b0;   /* conv_layers.0 (128->64) + conv_rgb.0 (128->3): 96 rows */
+  const float* wf1; const float* b1;   /* conv_layers.1 (64->32)  + conv_rgb.1 (64->3):  64 rows */
+  const float* wf2; const float* b2;   /* conv_rgb.2 (32->3):                            32 rows */
+  float neg_slope;                     /* 0.2 */
+} pnr_neural_render_w;
+
+int pnr_neural_render_scratch_bytes(int32_t H, int32_t W, size_t* out);
+int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const pnr_neural_render_w* w,
+                          float* out_rgb, void* scratch, size_t scratch_bytes, void* stream);
+
 /* ------------------------------------------------------------- utilities */
 /* Exclusive scan of n int32 values (n_dev: optional device-side length <= n,
  * entries past it are treated as 0 and out[] is written up to n_dev+1);

@@ -63,6 +63,11 @@ class Mlp(ctypes.Structure):
                 ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32)]
 
 
+class NeuralRenderW(ctypes.Structure):
+    _fields_ = [("wf0", c_void_p), ("b0", c_void_p), ("wf1", c_void_p), ("b1", c_void_p), ("wf2", c_void_p),
+                ("b2", c_void_p), ("neg_slope", c_float)]
+
+
 class MlpBf16(ctypes.Structure):
     _fields_ = [("w1af", c_void_p), ("w1bf", c_void_p), ("w2f", c_void_p), ("w3f", c_void_p), ("w4f", c_void_p),
                 ("wa", c_void_p), ("ba", c_void_p), ("wc1f", c_void_p), ("wc2f", c_void_p), ("wc3f", c_void_p),
@@ -138,6 +143,9 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_ray_march_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_neural_render_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
+    "pnr_neural_render_fwd": (c_int, [c_void_p, c_int32, c_int32, P(NeuralRenderW), c_void_p, c_void_p, c_size_t,
+                                      c_void_p]),
     "pnr_scan_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
     "pnr_exclusive_scan_i32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),

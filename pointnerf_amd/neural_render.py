@@ -1,0 +1,96 @@
+"""The fork's 2-D neural renderer on libpnr.
+
+``NeuralRenderer`` keeps the module tree and parameter names of
+models/neural_render/neural_renderer.py:7-104 for the configuration the fork
+builds, ``NeuralRenderer(input_dim=128)`` (neural_points_volumetric_model.py:258-260):
+n_feat 128 (conv_in = identity), img_size 64 -> 2 blocks, rgb skips, no norm,
+LeakyReLU(0.2), final sigmoid -- so ``neural_render_2d.*`` checkpoint keys load.
+Forward (no grad) runs ``pnr_neural_render_fwd``: three fused implicit-GEMM 3x3
+convolutions on fp32 MFMA.  With autograd enabled the same module computes with
+torch convolutions (MIOpen) so the finetune step can train it; the HIP kernels
+are inference-only in this round.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+from .aggregator import frag_pack
+
+
+class NeuralRenderer(nn.Module):
+    def __init__(self, n_feat=128, input_dim=128, out_dim=3, final_actvn=True, min_feat=32, img_size=64,
+                 use_rgb_skip=True, upsample_feat="nn", upsample_rgb="bilinear", use_norm=False):
+        super().__init__()
+        n_blocks = int(math.log2(img_size) - 4)
+        if (n_feat, input_dim, out_dim, n_blocks, use_rgb_skip, use_norm, final_actvn) != (128, 128, 3, 2, True,
+                                                                                            False, True):
+            raise L.PnrError("libpnr implements NeuralRenderer(input_dim=128) as built by the fork only")
+        self.final_actvn = final_actvn
+        self.conv_layers = nn.ModuleList([nn.Conv2d(128, 64, 3, 1, 1), nn.Conv2d(64, 32, 3, 1, 1)])
+        self.conv_rgb = nn.ModuleList([nn.Conv2d(128, 3, 3, 1, 1), nn.Conv2d(64, 3, 3, 1, 1),
+                                       nn.Conv2d(32, 3, 3, 1, 1)])
+        self._packed = None
+        self._packed_key = None
+
+    @staticmethod
+    def _stack(trunk, rgb):
+        """[cout, cin, 3, 3] weights of trunk (or None) and rgb conv -> rows x
+        (tap-major k = (ky*3+kx)*cin + ci), zero rows to a multiple of 32."""
+        ws = ([trunk.weight] if trunk is not None else []) + [rgb.weight]
+        bs = ([trunk.bias] if trunk is not None else []) + [rgb.bias]
+        W = torch.cat(ws, 0).float()
+        b = torch.cat(bs, 0).float()
+        rows = (W.shape[0] + 31) // 32 * 32
+        cin = W.shape[1]
+        W2 = torch.zeros((rows, 9 * cin), dtype=torch.float32, device=W.device)
+        W2[: W.shape[0]] = W.permute(0, 2, 3, 1).reshape(W.shape[0], 9 * cin)
+        bias = torch.zeros(rows, dtype=torch.float32, device=W.device)
+        bias[: b.shape[0]] = b
+        return frag_pack(W2), bias
+
+    def packed(self):
+        ps = list(self.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if self._packed is not None and key == self._packed_key:
+            return self._packed
+        with torch.no_grad():
+            wf0, b0 = self._stack(self.conv_layers[0], self.conv_rgb[0])
+            wf1, b1 = self._stack(self.conv_layers[1], self.conv_rgb[1])
+            wf2, b2 = self._stack(None, self.conv_rgb[2])
+        t = dict(wf0=wf0, b0=b0, wf1=wf1, b1=b1, wf2=wf2, b2=b2)
+        w = L.NeuralRenderW(*(t[k].data_ptr() for k in ("wf0", "b0", "wf1", "b1", "wf2", "b2")), 0.2)
+        self._packed, self._packed_key = (w, t), key
+        return self._packed
+
+    def forward_torch(self, x):
+        """neural_renderer.py:81-104 with torch convolutions (autograd path)."""
+        x = x.permute(0, 3, 1, 2)
+        rgb = self.conv_rgb[0](x)
+        net = x
+        for i, layer in enumerate(self.conv_layers):
+            net = F.leaky_relu(layer(net), 0.2)
+            rgb = rgb + self.conv_rgb[i + 1](net)
+        return torch.sigmoid(rgb).permute(0, 2, 3, 1)
+
+    def forward(self, x):
+        """x [1, H, W, 128] -> rgb [1, H, W, 3]."""
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return self.forward_torch(x)
+        L.require_gpu(x)
+        B, H, W, C = x.shape
+        if B != 1 or C != 128:
+            raise L.PnrError("NeuralRenderer expects [1, H, W, 128]")
+        xc = x.reshape(H * W, 128).float().contiguous()
+        out = torch.empty((H * W, 3), dtype=torch.float32, device=x.device)
+        nb = L.c_size_t(0)
+        L.check(L.lib().pnr_neural_render_scratch_bytes(H, W, L.ctypes.byref(nb)), "pnr_neural_render_scratch_bytes")
+        scratch = torch.empty(max(int(nb.value) // 4, 4), dtype=torch.float32, device=x.device)
+        w, _keep = self.packed()
+        L.check(L.lib().pnr_neural_render_fwd(L.ptr(xc), H, W, L.ctypes.byref(w), L.ptr(out), L.ptr(scratch),
+                                              scratch.numel() * 4, L.stream_ptr(x.device)), "pnr_neural_render_fwd")
+        return out.view(1, H, W, 3)

@@ -109,6 +109,11 @@ class NeuralPointsRayMarching(nn.Module):
         self.aggregator = aggregator if aggregator is not None else PointAggregator(opt).to(neural_points.device)
         self.chunk_rays = chunk_rays
         self._bufs = None
+        # fork's 2-D CNN after the composite (neural_points_volumetric_model.py:258-260, 343-344)
+        self.neural_render_2d = None
+        if getattr(opt, "neural_render", "none") == "cnn":
+            from .neural_render import NeuralRenderer
+            self.neural_render_2d = NeuralRenderer(input_dim=128).to(neural_points.device)
         self.last_counts = None
         if getattr(opt, "which_render_func", "radiance") != "radiance" or \
                 getattr(opt, "which_blend_func", "alpha") != "alpha" or \
@@ -243,7 +248,8 @@ class NeuralPointsRayMarching(nn.Module):
     def forward(self, campos, raydir, gt_image=None, bg_color=None, camrotc2w=None, pixel_idx=None,
                 near=None, far=None, focal=None, h=None, w=None, intrinsic=None, **kargs):
         """neural_points_volumetric_model.py:272-352 (+ fill_invalid :354-389);
-        B = 1; the 2-D neural_render decoder of the fork is out of scope."""
+        B = 1.  With opt.neural_render == "cnn" the fork's 2-D decoder
+        (NeuralRenderer, :343-344) adds final_coarse_raycolor (needs h, w)."""
         if raydir.dim() == 3 and raydir.shape[0] != 1:
             raise L.PnrError("batch size B > 1 is not supported (the reference uses B = 1)")
         near_v = float(torch.min(near).item()) if torch.is_tensor(near) else float(near)
@@ -258,4 +264,9 @@ class NeuralPointsRayMarching(nn.Module):
                    coarse_is_background=is_bg.view(1, R, 1), ray_mask=ray_mask.view(1, R))
         out["coarse_mask"] = 1 - out["coarse_is_background"]
         out["queried_shading"] = (1 - mask_f).repeat(1, 1, 3)
+        if self.neural_render_2d is not None:
+            img_h = int(h.item()) if torch.is_tensor(h) else int(h)
+            img_w = int(w.item()) if torch.is_tensor(w) else int(w)
+            out["final_coarse_raycolor"] = self.neural_render_2d(
+                out["coarse_raycolor"].reshape(1, img_h, img_w, -1)).reshape(1, -1, 3)
         return out
