@@ -381,21 +381,28 @@ __device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float
   }
 }
 
+#ifndef PNR_PAIR_SUB
+#define PNR_PAIR_SUB 1   // tiles per workgroup sharing barriers (and weight-fragment fetches)
+#endif
+constexpr int kPairSub = PNR_PAIR_SUB;
+
 template <bool TRAIN>
-__global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
+__global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pairs(AggArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
-  float* X = lds_dyn;                          // quad rows [kQRows][kQP]
+  const int sub = (threadIdx.x >> 6) / kPairWaves;   // which of the workgroup's tiles
+  float* X = lds_dyn + sub * kPairsLdsFloats;  // quad rows [kQRows][kQP]
   float* wtL = X + kQRows * kQP;               // [64] per-pair blend weight w_k * conf_k
   float* apart = wtL + kTP;                    // [4][64] alpha partial dots
   int* sflag = reinterpret_cast<int*>(apart + 4 * kTP);  // [8] sample has a valid neighbour
   float* exL = apart + 4 * kTP + kTS;          // [8][64] block3.0 extra inputs, parked from the gather
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) % kPairWaves;
   const int c = lane & 31, h = lane >> 5;
   const int j = lane >> 3, k = lane & 7;       // gather layout: lane = pair column
   const int T0 = wid * kNTW;
   const int K = A.s.K;
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kTS);
+  const int64_t ngroups = cdiv(ntiles, kPairSub);
   const float neg = A.w.neg_slope;
   float Rw[9];
 #pragma unroll
@@ -414,7 +421,8 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs(AggArgs A) {
   float ring[kQD][kNTW];
   prime_q<kNTW>(ring, w1b, lane);
 
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t tile = grp * kPairSub + sub;   // past ntiles: every pair inactive
     // ------------------------------------------------------------ gather (neural_points.py:788-799)
     const int64_t v = tile * kTS + j;
     const bool active = v < n;
@@ -785,7 +793,7 @@ int launch_t(const AggArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs<TRAIN>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsLdsBytes));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kPairsLdsBytes * kPairSub)));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color<TRAIN>),
@@ -797,8 +805,8 @@ int launch_t(const AggArgs& a, hipStream_t st) {
                      st, a);
   PNR_LAUNCH_CHECK();
   const int64_t tiles = cdiv(a.s.n_max, kTS);
-  hipLaunchKernelGGL(k_pairs<TRAIN>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kPairsLdsBytes,
-                     st, a);
+  hipLaunchKernelGGL(k_pairs<TRAIN>, dim3(grid_for(cdiv(tiles, kPairSub), 1, 256 * 2 / kPairSub)),
+                     dim3(64 * kPairWaves * kPairSub), kPairsLdsBytes * kPairSub, st, a);
   PNR_LAUNCH_CHECK();
   const int64_t ctiles = cdiv(a.s.n_max, kTP);
   hipLaunchKernelGGL(k_color<TRAIN>, dim3(grid_for(ctiles, 1, 256 * 2)), dim3(64 * kColWaves), kColLdsBytes, st, a);

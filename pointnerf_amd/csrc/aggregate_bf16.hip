@@ -41,7 +41,7 @@ struct AggArgsB {
   pnr_points pts;
   pnr_samples s;
   pnr_mlp_bf16 w;
-  uint16_t* p1;      // [n_p1, 256] bf16 per-point block1.0 partial
+  uint16_t* p1;      // [n_p1, 256] bf16 per-point block1.0 partial, accumulator order
   uint16_t* hid;     // [n_max, 256] bf16 K-summed features
   int32_t* vmask;    // [n_max]
   float* out_feat;
@@ -180,16 +180,17 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
     for (int pt = 0; pt < kBPT; ++pt) {
       const int64_t row = tile * kBT + 32 * pt + c;
       if (row >= np) continue;
+      // P1 rows in accumulator order: neuron tile T, lane half h -> 16 contiguous
+      // bf16 (the tile's 16 registers), so k_pairs_b reloads them with 2 x 16-B loads
 #pragma unroll
-      for (int T = 0; T < 2; ++T)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x16& v = acc[pt * 2 + T];
-          uint2 u;
-          u.x = pack_bf16x2(v[4 * q], v[4 * q + 1]);
-          u.y = pack_bf16x2(v[4 * q + 2], v[4 * q + 3]);
-          *reinterpret_cast<uint2*>(A.p1 + row * kHid + 32 * (2 * wid + T) + 8 * q + 4 * h) = u;
-        }
+      for (int T = 0; T < 2; ++T) {
+        const f32x16& v = acc[pt * 2 + T];
+        uint4* d = reinterpret_cast<uint4*>(A.p1 + row * kHid + 32 * (2 * wid + T) + 16 * h);
+        d[0] = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                          pack_bf16x2(v[6], v[7]));
+        d[1] = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
+                          pack_bf16x2(v[14], v[15]));
+      }
     }
     __syncthreads();
   }
@@ -336,13 +337,13 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
         if (p1r >= 0 && !(PNR_ABLATE & 1)) {
+          const uint4* src = reinterpret_cast<const uint4*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 16 * h);
+          const uint4 u0 = src[0], u1 = src[1];
+          const unsigned w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint2 u = *reinterpret_cast<const uint2*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 8 * q + 4 * h);
-            acc[pt * 2 + T][4 * q + 0] = bf16_lo(u.x);
-            acc[pt * 2 + T][4 * q + 1] = bf16_hi(u.x);
-            acc[pt * 2 + T][4 * q + 2] = bf16_lo(u.y);
-            acc[pt * 2 + T][4 * q + 3] = bf16_hi(u.y);
+          for (int q = 0; q < 8; ++q) {
+            acc[pt * 2 + T][2 * q] = bf16_lo(w[q]);
+            acc[pt * 2 + T][2 * q + 1] = bf16_hi(w[q]);
           }
         } else {
           acc[pt * 2 + T] = (f32x16){0.f};
