@@ -243,7 +243,32 @@ class NeuralPointsRayMarching(nn.Module):
                                  tab(np_.points_dir, 3), tab(np_.points_conf, 1), *agg_params(self.aggregator))
         cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
         cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(bg, campos, camrot, rd, hp))
-        return CompositeFn.apply(cspec, feat)
+        out = CompositeFn.apply(cspec, feat)
+        # conf_coefficient [1, R'', SR, K] as the reference returns it for the
+        # zero_one loss (point_aggregators.py:810-816): gradiant_clamp of the
+        # gathered conf, empty slots gather point 0 (torch.clamp(pidx, 0))
+        self.last_train_aux = {}
+        if np_.points_conf is not None:
+            Rv = cnt["R_valid"]
+            f32 = dict(dtype=torch.float32, device=dev)
+            pidx = torch.empty((1, Rv, SR, K), dtype=torch.int32, device=dev)
+            scratch3 = [torch.empty((1, Rv, SR, 3), **f32) for _ in range(3)]
+            rmask = torch.empty((1, R), dtype=torch.int8, device=dev)
+            L.check(L.lib().pnr_query_compact(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c), Rv,
+                                              L.ptr(pidx), L.ptr(scratch3[0]), L.ptr(scratch3[1]),
+                                              L.ptr(scratch3[2]), L.ptr(rmask), L.stream_ptr(dev)),
+                    "pnr_query_compact")
+            cf = np_.points_conf.reshape(-1)[pidx.clamp(min=0).long()]
+            self.last_train_aux["conf_coefficient"] = cf - (cf - torch.clamp(cf, 1e-4, 1.0)).detach()
+            self.last_train_aux["sample_pidx"] = pidx
+        return out
+
+    @staticmethod
+    def zero_one_loss(val, zero_epsilon: float = 1e-3):
+        """base_rendering_model.py:630-641: mean(log(v) + log(1 - v)), v clamped
+        to [eps, 1 - eps]."""
+        v = torch.clamp(val, zero_epsilon, 1 - zero_epsilon)
+        return torch.mean(torch.log(v) + torch.log(1 - v))
 
     def forward(self, campos, raydir, gt_image=None, bg_color=None, camrotc2w=None, pixel_idx=None,
                 near=None, far=None, focal=None, h=None, w=None, intrinsic=None, **kargs):

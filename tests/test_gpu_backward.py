@@ -170,3 +170,25 @@ def test_gemm_tn_vs_torch(cuda, K, M, N):
     close(cs, A.double().sum(0).float(), "colsum", rel=1e-4, scale=2e-6)
     C2 = L.gemm_tn(A, B)
     assert torch.equal(C, C2)          # deterministic split-K reduction
+
+
+def test_conf_coefficient_and_zero_one_loss(cuda):
+    """conf_coefficient [1, R'', SR, K] (empty slots gather point 0, as
+    torch.clamp(pidx, 0) does in the reference) and the zero_one loss gradient
+    into points_conf, vs a torch CPU restatement on the oracle's query."""
+    sc = scene(8000, H=24, W=24, theta=40.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.2))
+    campos, camrot = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)
+    cc = m.last_train_aux["conf_coefficient"]
+    loss = m.zero_one_loss(cc) * 1e-4
+    loss.backward()
+    q = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
+    conf = torch.from_numpy(np.ascontiguousarray(sc["conf"])).reshape(-1).requires_grad_(True)
+    ref_cc = OG.gradiant_clamp(conf[torch.from_numpy(q["sample_pidx"]).long().clamp(min=0)])
+    assert cc.shape[1:] == ref_cc.shape
+    np.testing.assert_array_equal(cc.detach().cpu().numpy()[0], ref_cc.detach().numpy())
+    (torch.mean(torch.log(ref_cc.clamp(1e-3, 1 - 1e-3)) + torch.log(1 - ref_cc.clamp(1e-3, 1 - 1e-3))) * 1e-4).backward()
+    # point 0 sums the terms of every empty slot (thousands): looser scale term
+    close(m.neural_points.points_conf.grad.reshape(-1), conf.grad, "d points_conf (zero_one)", scale=5e-4)
