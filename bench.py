@@ -156,8 +156,9 @@ def stage_rooflines(args, opt, model, stage, per, launches):
 def run_train(args, device):
     """Finetune step: random batch of pixels of one of
     8 cameras -> query -> aggregate (training forward) -> composite -> MSE on
-    the first 3 colour channels vs a synthetic target -> backward through the
-    HIP kernels -> Adam on points_embeding/color/dir/conf and the aggregator."""
+    the first 3 colour channels vs a synthetic target + 1e-4 x the zero_one loss
+    on conf_coefficient (ship.sh) -> backward through the HIP kernels -> Adam on
+    points_embeding/color/dir/conf and the aggregator."""
     opt, pts, feats, agg, model = build_scene(args, device)
     agg.train()
     H = W = args.hw
@@ -176,6 +177,8 @@ def run_train(args, device):
         optim.zero_grad(set_to_none=True)
         color, _, _, _ = model.render_rays_train(campos, camrot, rd[sel], opt.near_plane, opt.far_plane, bg)
         loss = torch.mean((color[:, :3] - target[sel]) ** 2)
+        if "conf_coefficient" in model.last_train_aux:   # ship.sh: zero_one_loss_weights 1e-4
+            loss = loss + 1e-4 * model.zero_one_conf_loss()
         loss.backward()
         optim.step()
         if timed:

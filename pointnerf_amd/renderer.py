@@ -263,6 +263,25 @@ class NeuralPointsRayMarching(nn.Module):
             self.last_train_aux["sample_pidx"] = pidx
         return out
 
+    def zero_one_conf_loss(self, zero_epsilon: float = 1e-3):
+        """zero_one_loss(conf_coefficient) of the last render_rays_train, computed
+        per point: every entry of conf_coefficient is a function of one point's
+        conf, so the mean over the [1, R'', SR, K] entries equals
+        sum_p count_p f(conf_p) / entries (count_p = entries gathering point p,
+        point 0 also collecting the empty slots) -- same value and gradient
+        without the gather's scatter-add backward (point 0 alone receives most
+        of the empty-slot entries)."""
+        pidx = self.last_train_aux["sample_pidx"]
+        conf = self.neural_points.points_conf.reshape(-1)
+        ids = pidx[pidx >= 0].long()
+        counts = torch.bincount(ids, minlength=conf.numel()).float()
+        counts[0] += (pidx < 0).sum()
+        used = counts > 0
+        c = conf[used]
+        cc = c - (c - torch.clamp(c, 1e-4, 1.0)).detach()        # gradiant_clamp
+        v = torch.clamp(cc, zero_epsilon, 1 - zero_epsilon)
+        return torch.sum(counts[used] * (torch.log(v) + torch.log(1 - v))) / pidx.numel()
+
     @staticmethod
     def zero_one_loss(val, zero_epsilon: float = 1e-3):
         """base_rendering_model.py:630-641: mean(log(v) + log(1 - v)), v clamped

@@ -184,6 +184,13 @@ def test_conf_coefficient_and_zero_one_loss(cuda):
     cc = m.last_train_aux["conf_coefficient"]
     loss = m.zero_one_loss(cc) * 1e-4
     loss.backward()
+    g_gather = m.neural_points.points_conf.grad.clone()
+    m.neural_points.points_conf.grad = None
+    loss2 = m.zero_one_conf_loss() * 1e-4          # per-point form: same value and gradient
+    loss2.backward()
+    assert abs(float(loss2.detach()) - float(loss.detach())) <= 1e-6 * abs(float(loss.detach())) + 1e-12
+    close(m.neural_points.points_conf.grad, g_gather, "per-point zero_one gradient", scale=5e-4)
+    m.neural_points.points_conf.grad = g_gather
     q = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
     conf = torch.from_numpy(np.ascontiguousarray(sc["conf"])).reshape(-1).requires_grad_(True)
     ref_cc = OG.gradiant_clamp(conf[torch.from_numpy(q["sample_pidx"]).long().clamp(min=0)])
