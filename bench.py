@@ -222,12 +222,18 @@ def main():
         if world == 1 and args.gpus > 1:
             print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(ndev, 1)          # == local on a node with one GPU per rank
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("PNR_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only for 1-GPU rehearsals
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     from pointnerf_amd import _lib as L
 
     H = W = args.hw
