@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--no-grid-rebuild", action="store_true",
                     help="reuse the voxel grid across steps (default: rebuild every step)")
     ap.add_argument("--no-gather", action="store_true", help="skip the tile all-gather (N > 1)")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="diagnostic (single process): do rank 0's share of an N-rank step (N partial frames of "
+                         "1/N of the rays, no collective) to project per-rank overheads of the N-GPU run")
     ap.add_argument("--cpu-rays", type=int, default=1500, help="rays in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
@@ -242,6 +245,9 @@ def main():
     cams = cameras(8, H, W)
     SR = opt.SR
     # per-(frame, rank) pixel lists: step s renders frames s*world .. s*world+world-1
+    shard_world = world
+    if world == 1 and args.emulate_world > 1:
+        shard_world = args.emulate_world
     dev_cams = []
     for campos, camrot, rd in cams:
         dev_cams.append((torch.from_numpy(campos).to(device), torch.from_numpy(camrot).to(device),
@@ -253,11 +259,11 @@ def main():
 
     def my_rays(frame):
         ci = frame % len(cams)
-        if world == 1:
+        if shard_world == 1:
             return ci, dev_cams[ci][2], None
-        key = (frame % world, ci)
+        key = (frame % shard_world, ci)
         if key not in shards:
-            sh = TileShard(H, W, rank, world, frame % world, device)
+            sh = TileShard(H, W, rank, shard_world, frame % shard_world, device)
             shards[key] = (sh, sh.select(dev_cams[ci][2]))
         sh, rd = shards[key]
         return ci, rd, sh
@@ -266,13 +272,14 @@ def main():
 
     def step(s, timed):
         frames = []
-        for f in range(world):
-            frame = s * world + f
+        for f in range(shard_world):
+            frame = s * shard_world + f
             ci, rd, sh = my_rays(frame)
             campos, camrot, _ = dev_cams[ci]
             ev = [] if timed else None
             color, opac, is_bg, mask = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
-                                                         force_grid=(f == 0 and not args.no_grid_rebuild), events=ev)
+                                                         force_grid=(f == 0 and not args.no_grid_rebuild), events=ev,
+                                                         reuse_p1=f > 0)
             if timed:
                 c = model.last_counts
                 stage["pairs"] += c["n_pairs"]
@@ -284,10 +291,11 @@ def main():
                 stage["_ev"] = stage.get("_ev", []) + ev
             if world > 1 and not args.no_gather:
                 # RCCL all-gather of the rendered 16x16 tiles: every rank holds the frame
-                frames.append(sh.assemble(color))
+                # (async: the tiles travel over xGMI while the next partial frame renders)
+                frames.append(sh.assemble_async(color))
             else:
                 frames.append(color)
-        return frames
+        return [f.wait() if hasattr(f, "wait") else f for f in frames]
 
     for s in range(args.warmup):
         step(s, False)
@@ -340,7 +348,7 @@ def main():
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "grid_rebuild_per_step": not args.no_grid_rebuild,
-                       "parallelism": f"dp{world} (16x16 ray tiles, RCCL all_gather of tiles)" if world > 1
+                       "parallelism": f"dp{world} (16x16 ray tiles, async RCCL all_gather of tiles)" if world > 1
                        else "single GPU"},
             "roofline": {"bound": "mfma", "kernel": (
                              "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)"
@@ -356,6 +364,8 @@ def main():
                                  "valid_samples": stage["valid"] // max(launches, 1),
                                  "filled_samples": stage["filled"] // max(launches, 1)},
         }
+        if shard_world != world:
+            out["config"]["emulated_world"] = shard_world   # diagnostic: rank 0's share of an N-rank step
         out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per, launches)
         if not args.no_cpu_baseline and world == 1:
             try:

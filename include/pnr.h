@@ -210,6 +210,12 @@ typedef struct {
   int64_t n_used;
   const int32_t* used_map; /* [n] row -> index into used (-1 = unreferenced); required
                               with used                                              */
+  int32_t p1_ready;     /* aggregate forward only: 1 = the scratch's first n_p1*256
+                           values already hold block1.0's point half for these same
+                           rows and weights (an earlier call on the same scratch with
+                           the same emb / used rows / block1.0, e.g. the other ray
+                           batches of one step), so the per-point pass is skipped.
+                           Camera-independent.  0 = compute it (always safe).     */
 } pnr_points;
 
 typedef struct {

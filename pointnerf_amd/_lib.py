@@ -77,7 +77,8 @@ class MlpBf16(ctypes.Structure):
 class Points(ctypes.Structure):
     _fields_ = [("n", c_int64), ("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
                 ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p),
-                ("used", c_void_p), ("n_used", c_int64), ("used_map", c_void_p)]
+                ("used", c_void_p), ("n_used", c_int64), ("used_map", c_void_p),
+                ("p1_ready", c_int32)]
 
 
 class Samples(ctypes.Structure):

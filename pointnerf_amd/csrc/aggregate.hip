@@ -800,10 +800,11 @@ int launch_t(const AggArgs& a, hipStream_t st) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kColLdsBytes));
     attr = true;
   }
-  hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.used ? a.pts.n_used : a.pts.n, 32), 4, 256)),
-                     dim3(kAggBlock), kAggLdsBytes,
-                     st, a);
-  PNR_LAUNCH_CHECK();
+  if (!a.pts.p1_ready) {
+    hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.used ? a.pts.n_used : a.pts.n, 32), 4, 256)),
+                       dim3(kAggBlock), kAggLdsBytes, st, a);
+    PNR_LAUNCH_CHECK();
+  }
   const int64_t tiles = cdiv(a.s.n_max, kTS);
   hipLaunchKernelGGL(k_pairs<TRAIN>, dim3(grid_for(cdiv(tiles, kPairSub), 1, 256 * 2 / kPairSub)),
                      dim3(64 * kPairWaves * kPairSub), kPairsLdsBytes * kPairSub, st, a);
@@ -1163,11 +1164,13 @@ static size_t scratch_need(int64_t n_max, int64_t n_points) {
          sizeof(float);
 }
 
-static void carve(AggArgs& a, void* scratch, int64_t n_max) {
+// scratch = P1 [n_p1, 256] | hid [n_max, 256] | vmask: P1 first, so its place
+// does not depend on n_max and a later call may reuse it (pnr_points.p1_ready)
+static void carve(AggArgs& a, void* scratch, int64_t n_max, int64_t n_p1) {
   const int64_t nm = n_max > 0 ? n_max : 1;
-  a.hid = static_cast<float*>(scratch);
+  a.p1 = static_cast<float*>(scratch);
+  a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
   a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
-  a.p1 = reinterpret_cast<float*>(a.vmask) + cdiv(nm, 4) * 4;
 }
 
 int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, float* out_feat,
@@ -1212,7 +1215,7 @@ extern "C" int pnr_aggregate_fwd(const pnr_points* pts, const pnr_samples* s, co
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  carve(a, scratch, s->n_max);
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
@@ -1234,7 +1237,7 @@ extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  carve(a, scratch, s->n_max);
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
@@ -1265,7 +1268,7 @@ extern "C" int pnr_aggregate_fwd_train(const pnr_points* pts, const pnr_samples*
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  carve(a, scratch, s->n_max);
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
   a.sv = *saved;
   a.hid = saved->hid;
   a.vmask = saved->vmask;
@@ -1291,7 +1294,7 @@ extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_s
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  carve(a, scratch, s->n_max);
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
   a.sv = *saved;
   a.hid = saved->hid;
   a.vmask = saved->vmask;

@@ -610,15 +610,18 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  a.hid = static_cast<uint16_t*>(scratch);
+  // P1 [n_p1, 256] first (fixed place, reusable via p1_ready) | hid | vmask
+  a.p1 = static_cast<uint16_t*>(scratch);
+  a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
   a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
-  a.p1 = reinterpret_cast<uint16_t*>(a.vmask + cdiv(nm, 4) * 4);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
-  hipLaunchKernelGGL(k_point_pre_b, dim3(grid_for(cdiv(n_p1, kBT), 1, 256 * 2)), dim3(64 * kBWaves),
-                     kBT * kPB * 2, st, a);
-  PNR_LAUNCH_CHECK();
+  if (!pts->p1_ready) {
+    hipLaunchKernelGGL(k_point_pre_b, dim3(grid_for(cdiv(n_p1, kBT), 1, 256 * 2)), dim3(64 * kBWaves),
+                       kBT * kPB * 2, st, a);
+    PNR_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(k_pairs_b, dim3(grid_for(cdiv(nm, kBTS), 1, 256 * 2)), dim3(64 * kBWaves), kPairsBLds, st, a);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_color_b, dim3(grid_for(cdiv(nm, kBT), 1, 256 * 2)), dim3(64 * kBWaves), kColorBLds, st, a);

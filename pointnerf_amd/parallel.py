@@ -33,8 +33,14 @@ class TileShard:
         self.counts = np.bincount(own, minlength=world)
         self.max_count = int(self.counts.max())
         self.pixels = [np.nonzero(own == r)[0] for r in range(world)]
-        self.idx = torch.from_numpy(self.pixels[rank]).to(device) if device is not None else \
-            torch.from_numpy(self.pixels[rank])
+        # pixel -> row of the gathered [world * max_count] buffer (rank r's j-th pixel)
+        src = np.empty(H * W, dtype=np.int64)
+        for r in range(world):
+            src[self.pixels[r]] = r * self.max_count + np.arange(self.pixels[r].size)
+        self.idx = torch.from_numpy(self.pixels[rank])
+        self.src = torch.from_numpy(src)
+        if device is not None:
+            self.idx, self.src = self.idx.to(device), self.src.to(device)
 
     def select(self, per_pixel: torch.Tensor) -> torch.Tensor:
         """Rows of a [H*W, ...] tensor owned by this rank."""
@@ -42,22 +48,30 @@ class TileShard:
 
     def assemble(self, local: torch.Tensor, group=None) -> torch.Tensor:
         """All-gather every rank's [count_r, C] rows into the full [H*W, C] frame."""
+        return self.assemble_async(local, group).wait()
+
+    def assemble_async(self, local: torch.Tensor, group=None) -> "_Gather":
+        """Start the all-gather and return a handle whose wait() yields the
+        [H*W, C] frame.  On RCCL the collective runs on its own stream, so the
+        caller can render the next ray batch while the tiles travel over xGMI."""
         import torch.distributed as dist
         C = local.shape[1]
-        pad = local
-        if local.shape[0] < self.max_count:
-            pad = torch.cat([local, local.new_zeros((self.max_count - local.shape[0], C))])
-        backend = dist.get_backend(group)
-        if backend == "nccl":
+        pad = local.new_zeros((self.max_count, C))
+        pad[: local.shape[0]] = local
+        if dist.get_backend(group) == "nccl":
             buf = torch.empty((self.world * self.max_count, C), dtype=local.dtype, device=local.device)
-            dist.all_gather_into_tensor(buf, pad.contiguous(), group=group)
-            parts = buf.view(self.world, self.max_count, C)
-        else:
-            lst = [torch.empty_like(pad) for _ in range(self.world)]
-            dist.all_gather(lst, pad.contiguous(), group=group)
-            parts = torch.stack(lst)
-        out = torch.empty((self.H * self.W, C), dtype=local.dtype, device=local.device)
-        for r in range(self.world):
-            n = int(self.counts[r])
-            out[torch.from_numpy(self.pixels[r]).to(local.device)] = parts[r, :n]
-        return out
+            work = dist.all_gather_into_tensor(buf, pad, group=group, async_op=True)
+            return _Gather(self, work, buf, None)
+        lst = [torch.empty_like(pad) for _ in range(self.world)]
+        work = dist.all_gather(lst, pad, group=group, async_op=True)
+        return _Gather(self, work, None, lst)
+
+
+class _Gather:
+    def __init__(self, shard, work, buf, parts):
+        self.shard, self.work, self.buf, self.parts = shard, work, buf, parts
+
+    def wait(self) -> torch.Tensor:
+        self.work.wait()
+        buf = self.buf if self.buf is not None else torch.cat(self.parts)
+        return buf.index_select(0, self.shard.src.to(buf.device))

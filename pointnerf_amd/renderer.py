@@ -121,11 +121,17 @@ class NeuralPointsRayMarching(nn.Module):
             raise L.PnrError("libpnr implements radiance render, alpha blend and tone map 'off'")
 
     @torch.no_grad()
-    def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None):
+    def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None,
+                    reuse_p1=False):
         """Fused query -> aggregate -> composite for one ray batch [R,3].
         Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8).
         ``events``: optional list that receives (stage, start, end) HIP events
-        recorded on the launch stream around each stage."""
+        recorded on the launch stream around each stage.
+        ``reuse_p1``: the caller guarantees points_embeding and block1.0 are
+        unchanged since the previous render_rays call (e.g. the other partial
+        frames of one multi-GPU step), so block1.0's per-point half (P1, which
+        does not depend on the camera) is taken from that call's scratch
+        instead of recomputed.  The ray chunks of one call always share it."""
         opt = self.opt
         dev = raydir.device
         L.require_gpu(raydir)
@@ -175,14 +181,14 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
             e2 = mark()
+            scratch, ready = self._agg_scratch(max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0)
+            pts.p1_ready = int(ready)
             if bf16:
-                scratch = L.aggregate_scratch_bf16(max(Sv, 1), pts.n, dev)
                 L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                                        L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
                                                        L.stream_ptr(dev)),
                         "pnr_aggregate_fwd_bf16")
             else:
-                scratch = L.aggregate_scratch(max(Sv, 1), pts.n, dev)
                 L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                                   L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
                                                   L.stream_ptr(dev)),
@@ -199,6 +205,28 @@ class NeuralPointsRayMarching(nn.Module):
                 events += [("query", e0, e1), ("aggregate", e2, e3), ("composite", e3, e4)]
         self.last_counts = totals
         return ray_color, opacity, is_bg, ray_mask
+
+    def _agg_scratch(self, n_max, n_points, dev, bf16, reuse):
+        """Persistent aggregate scratch (P1 lives at its start, see
+        pnr_points.p1_ready) -> (tensor, P1 already valid).  The P1 is valid
+        when reuse is requested and the embedding storage, block1.0 and the
+        precision match the call that wrote it."""
+        emb = self.neural_points.points_embeding
+        b1 = self.aggregator.block1[0]
+        key = (bf16, n_points, emb.data_ptr(), emb._version, b1.weight.data_ptr(), b1.weight._version,
+               b1.bias.data_ptr(), b1.bias._version)
+        need = (L.aggregate_scratch_bf16 if bf16 else L.aggregate_scratch)
+        nb = L.c_size_t(0)
+        fn = L.lib().pnr_aggregate_scratch_bytes_bf16 if bf16 else L.lib().pnr_aggregate_scratch_bytes
+        L.check(fn(int(n_max), int(n_points), L.ctypes.byref(nb)), "aggregate scratch bytes")
+        buf = getattr(self, "_scratch", None)
+        if buf is None or buf.device != dev or buf.numel() * 4 < int(nb.value):
+            buf = need(int(n_max * 1.25) + 1024, n_points, dev)   # headroom: n_max varies per batch
+            self._scratch = buf
+            self._scratch_key = None
+        ready = reuse and self._scratch_key == key
+        self._scratch_key = key
+        return buf, ready
 
     def render_rays_train(self, campos, camrot, raydir, near, far, bg_color):
         """Differentiable render of one training ray batch [R,3] (SURVEY 8(a)

@@ -82,3 +82,33 @@ def test_all_background(cuda):
     bg = torch.from_numpy(sc["bg"]).to(cuda)
     assert torch.equal(out["coarse_raycolor"][0], bg.expand(64, 128))
     assert torch.all(out["coarse_is_background"] == 1)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_reuse_p1_across_batches(cuda, precision):
+    """render_rays(reuse_p1=True) (the partial frames of one multi-GPU step)
+    equals a fresh computation bitwise, and an in-place change of block1.0 or
+    the embedding invalidates the reused per-point half."""
+    sc = scene(20000, H=40, W=40, theta=30.0)
+    sc2 = scene(20000, H=40, W=40, theta=200.0)
+    params = formula_params(salt=0.3)
+    m = _renderer(sc, cuda, params)
+    m.precision = precision
+    cp, cr, bg = (torch.from_numpy(sc[k]).to(cuda) for k in ("campos", "camrot", "bg"))
+    cp2, cr2 = torch.from_numpy(sc2["campos"]).to(cuda), torch.from_numpy(sc2["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    rd2 = torch.from_numpy(sc2["raydir"]).to(cuda)
+    fresh = m.render_rays(cp2, cr2, rd2[::2].contiguous(), 2.0, 6.0, bg)[0]
+    m.render_rays(cp, cr, rd[1::2].contiguous(), 2.0, 6.0, bg)
+    reused = m.render_rays(cp2, cr2, rd2[::2].contiguous(), 2.0, 6.0, bg, reuse_p1=True)[0]
+    assert torch.equal(fresh, reused)
+    with torch.no_grad():
+        m.aggregator.block1[0].weight.mul_(0.5)
+    stale_check = m.render_rays(cp2, cr2, rd2[::2].contiguous(), 2.0, 6.0, bg, reuse_p1=True)[0]
+    new = m.render_rays(cp2, cr2, rd2[::2].contiguous(), 2.0, 6.0, bg)[0]
+    assert torch.equal(stale_check, new) and not torch.equal(new, fresh)
+    with torch.no_grad():
+        m.neural_points.points_embeding.add_(0.25)
+    stale_check = m.render_rays(cp2, cr2, rd2[::2].contiguous(), 2.0, 6.0, bg, reuse_p1=True)[0]
+    new2 = m.render_rays(cp2, cr2, rd2[::2].contiguous(), 2.0, 6.0, bg)[0]
+    assert torch.equal(stale_check, new2) and not torch.equal(new2, new)
