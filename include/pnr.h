@@ -271,6 +271,24 @@ int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pn
                            float* out_feat, float* out_weight, float* out_conf, void* scratch,
                            size_t scratch_bytes, void* stream);
 
+/* fp32-accurate aggregation on bf16 MFMA (same contract and scratch as
+ * pnr_aggregate_fwd).  Each fp32 GEMM operand is split exactly into three bf16
+ * terms (x = x0 + x1 + x2) and block1.0's distance half, block1.2, block3.0 and
+ * block3.2 run as the six cross products of weight >= 2^-16 on
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation: the dropped terms are
+ * below one fp32 rounding of each product.  The per-point block1.0 half and
+ * the colour branch stay on the fp32 MFMA.  wx: split packs from
+ * pointnerf_amd.aggregator.frag_pack_x3 (uint16 bf16 planes). */
+typedef struct {
+  const void* w1bx;   /* block1.0 columns 224..283 */
+  const void* w2x;    /* block1.2 + bias           */
+  const void* w3x;    /* block3.0 + bias           */
+  const void* w4x;    /* block3.2 + bias           */
+} pnr_mlp_x3;
+int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_x3* wx,
+                         float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                         size_t scratch_bytes, void* stream);
+
 /* PointAggregator.forward signature (pre-gathered tensors): pts tables are the
  * gathered [rows*K, C] tensors, s->pidx must be NULL (pair row = row*K + k),
  * pts->pers required, validity from pair_mask[rows*K] (sample_pnt_mask). */

@@ -97,6 +97,10 @@ class AggSaved(ctypes.Structure):
                                         "vpe", "hc1", "hc2", "hc3", "vmask", "mask")]
 
 
+class MlpX3(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w1bx", "w2x", "w3x", "w4x")]
+
+
 class MlpBwd(ctypes.Structure):
     _fields_ = [("w4t", c_void_p), ("w3t", c_void_p), ("w2t", c_void_p), ("w3e", c_void_p)]
 
@@ -119,6 +123,8 @@ SIGNATURES = {
     "pnr_aggregate_scratch_bytes": (c_int, [c_int64, c_int64, P(c_size_t)]),
     "pnr_aggregate_fwd": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpX3), c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_scratch_bytes_bf16": (c_int, [c_int64, c_int64, P(c_size_t)]),

@@ -103,6 +103,41 @@ def frag_pack_bf16(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.T
     return F.view(-1).to(torch.bfloat16)
 
 
+X3_PAD = 2   # kXPad in aggregate.hip
+X3_SIGMA = (0, 2, 1, 3, 4, 6, 5, 7)   # k order of two quad-row float4 reads (qperm {0,2,1,3})
+
+
+def split3_bf16(W: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """fp32 W -> bf16 (W0, W1, W2) with W == W0 + W1 + W2 exactly (each residual
+    is exact in fp32; round-to-nearest-even at every step, like v_cvt_pk_bf16_f32)."""
+    W = W.float()
+    w0 = W.to(torch.bfloat16)
+    r = W - w0.float()
+    w1 = r.to(torch.bfloat16)
+    w2 = (r - w1.float()).to(torch.bfloat16)
+    return w0, w1, w2
+
+
+def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Split-bf16 A-operand packs for pnr_aggregate_fwd_x3:
+    F[t][T][plane][lane][j] = plane of W'[32T + (lane & 31)][16t + 8(lane >> 5) + sigma(j)],
+    W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus X3_PAD zero ones."""
+    out_f, kin = W.shape
+    assert out_f % 32 == 0
+    cols = kin + (1 if bias is not None else 0)
+    tot = (cols + 15) // 16 + X3_PAD
+    NT = out_f // 32
+    Wp = torch.zeros((out_f, 16 * tot), dtype=torch.float32, device=W.device)
+    Wp[:, :kin] = W.float()
+    if bias is not None:
+        Wp[:, kin] = bias.float()
+    sig = torch.tensor(X3_SIGMA, device=W.device)
+    Wp = Wp.view(out_f, tot, 2, 8)[..., sig]                             # k = 16t + 8h + sigma(j)
+    planes = torch.stack(split3_bf16(Wp), 0)                            # [3][out][t][h][j]
+    F = planes.view(3, NT, 32, tot, 2, 8).permute(3, 1, 0, 4, 2, 5).contiguous()   # [t][T][pl][h][r][j]
+    return F.view(-1)
+
+
 def frag_unpack(F: torch.Tensor, kin: int, out_f: int = 256) -> torch.Tensor:
     NT = out_f // 32
     tot = F.numel() // (NT * 64)
@@ -192,6 +227,21 @@ class PointAggregator(nn.Module):
         m.act_super = self.act_super
         self._packed16, self._packed16_key = (m, t), key
         return self._packed16
+
+    def packed_x3(self) -> tuple[L.MlpX3, dict]:
+        """Split-bf16 packs of block1.0[:, 224:], block1.2, block3.0, block3.2
+        for pnr_aggregate_fwd_x3 (used with packed(); cached like it)."""
+        ps = list(self.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if getattr(self, "_packedx3", None) is not None and key == self._packedx3_key:
+            return self._packedx3
+        with torch.no_grad():
+            b1, b3 = self.block1, self.block3
+            t = dict(w1bx=frag_pack_x3(b1[0].weight[:, 224:]), w2x=frag_pack_x3(b1[2].weight, b1[2].bias),
+                     w3x=frag_pack_x3(b3[0].weight, b3[0].bias), w4x=frag_pack_x3(b3[2].weight, b3[2].bias))
+        m = L.MlpX3(*(t[k].data_ptr() for k in ("w1bx", "w2x", "w3x", "w4x")))
+        self._packedx3, self._packedx3_key = (m, t), key
+        return self._packedx3
 
     def set_rw2c(self, rw2c: torch.Tensor | None):
         """Uniform Rw2c of the point cloud (neural_points.py:289; eye by default)."""

@@ -95,14 +95,20 @@ class NeuralPoints(nn.Module):
                 ray_mask, vsize, 0)
 
 
+# fp32: the reference's arithmetic on v_mfma_f32_32x32x2_f32.  fp32x3: the same
+# fp32 GEMMs as exact 3-way bf16 splits on v_mfma_f32_32x32x16_bf16 (six cross
+# products, fp32-accurate; pnr_aggregate_fwd_x3).  bf16: bf16 operands (config c5).
+PRECISIONS = ("fp32", "fp32x3", "bf16")
+
+
 class NeuralPointsRayMarching(nn.Module):
     """neural_points_volumetric_model.NeuralPointsRayMarching, fused HIP path."""
 
     def __init__(self, opt, neural_points: NeuralPoints, aggregator: PointAggregator | None = None,
                  chunk_rays: int | None = None, precision: str = "fp32"):
         super().__init__()
-        if precision not in ("fp32", "bf16"):
-            raise L.PnrError(f"precision {precision!r}: fp32 (the reference's) or bf16 (MFMA fast path)")
+        if precision not in PRECISIONS:
+            raise L.PnrError(f"precision {precision!r}: one of {PRECISIONS}")
         self.precision = precision
         self.opt = opt
         self.neural_points = neural_points
@@ -155,6 +161,8 @@ class NeuralPointsRayMarching(nn.Module):
         camrot = camrot.reshape(3, 3).float().contiguous()
         bf16 = self.precision == "bf16"
         mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
+        if self.precision == "fp32x3":
+            mlpx, _keepx = self.aggregator.packed_x3()
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
         chunk = max(1, self.chunk_rays or R)
@@ -188,6 +196,11 @@ class NeuralPointsRayMarching(nn.Module):
                                                        L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
                                                        L.stream_ptr(dev)),
                         "pnr_aggregate_fwd_bf16")
+            elif self.precision == "fp32x3":
+                L.check(L.lib().pnr_aggregate_fwd_x3(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
+                                                     L.ctypes.byref(mlpx), L.ptr(feat), None, None, L.ptr(scratch),
+                                                     scratch.numel() * 4, L.stream_ptr(dev)),
+                        "pnr_aggregate_fwd_x3")
             else:
                 L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                                   L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
