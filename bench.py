@@ -56,9 +56,10 @@ def parse():
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
     ap.add_argument("--train-rays", type=int, default=3600, help="rays per train step (random_sample_size 60^2)")
-    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
-                    help="MLP compute precision: fp32 = the reference's (headline); bf16 = v_mfma_f32_32x32x16_bf16 "
-                         "operands with fp32 accumulation (SURVEY config c5)")
+    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "bf16"), default="fp32",
+                    help="MLP arithmetic: fp32 = the reference's on v_mfma_f32_32x32x2_f32; fp32x3 = the same fp32 "
+                         "GEMMs as exact 3-way bf16 splits (6 cross products) on v_mfma_f32_32x32x16_bf16, "
+                         "fp32-accurate; bf16 = bf16 operands (SURVEY config c5)")
     return ap.parse_args()
 
 
@@ -336,25 +337,46 @@ def main():
             except Exception:
                 traffic = None
         achieved = flops_per_launch / avg_agg_s / 1e12 if avg_agg_s > 0 else 0.0
-        peak = FP32_MFMA_PEAK_TFLOPS if args.dtype == "fp32" else BF16_MFMA_PEAK_TFLOPS
-        if args.dtype != "fp32":
-            traffic = None   # the committed PMC summary is for the fp32 kernels
+        # fp32x3: every fp32 MAC costs 6 bf16 MFMA products -> fp32-equivalent ceiling = bf16 dense / 6
+        peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "fp32x3": round(BF16_MFMA_PEAK_TFLOPS / 6, 1),
+                "bf16": BF16_MFMA_PEAK_TFLOPS}[args.dtype]
+        pmc_x3 = os.path.join(ROOT, "profiles", "r01_pmc_aggregate_x3.json")
+        if args.dtype == "fp32x3":
+            traffic = None
+            if os.path.exists(pmc_x3):
+                try:
+                    traffic = json.load(open(pmc_x3)).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+        elif args.dtype != "fp32":
+            traffic = None   # the committed PMC summaries are for the fp32 / fp32x3 kernels
         out = {
             "metric": "Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref",
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32" if args.dtype in ("fp32", "fp32x3") else args.dtype,
+            "arith": {"fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
+                      "fp32x3": "fp32-accurate: exact 3-way bf16 split of each fp32 operand, 6 cross products on "
+                                "v_mfma_f32_32x32x16_bf16, fp32 accumulation (error vs an fp64 oracle = native "
+                                "fp32's, tests/test_gpu_x3.py)",
+                      "bf16": "bf16 operands, fp32 accumulation"}[args.dtype],
             "data": "synthetic (seeded lego-like 2M-point cloud, random-init lego viewmlp weights)",
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "grid_rebuild_per_step": not args.no_grid_rebuild,
                        "parallelism": f"dp{world} (16x16 ray tiles, async RCCL all_gather of tiles)" if world > 1
                        else "single GPU"},
-            "roofline": {"bound": "mfma", "kernel": (
-                             "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)"
-                             if args.dtype == "fp32" else
-                             "pnr_aggregate_fwd_bf16 = k_point_pre_b + k_pairs_b + k_color_b (v_mfma_f32_32x32x16_bf16)"),
+            "roofline": {"bound": "mfma", "kernel": {
+                             "fp32": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
+                             "fp32x3": "pnr_aggregate_fwd_x3 = k_point_pre + k_pairs_x3 (bf16x3 split, "
+                                       "v_mfma_f32_32x32x16_bf16) + k_color",
+                             "bf16": "pnr_aggregate_fwd_bf16 = k_point_pre_b + k_pairs_b + k_color_b "
+                                     "(v_mfma_f32_32x32x16_bf16)"}[args.dtype],
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                         "peak_note": {"fp32": "fp32 MFMA dense peak",
+                                       "fp32x3": "fp32-equivalent: bf16 MFMA dense peak / 6 products per fp32 MAC",
+                                       "bf16": "bf16 MFMA dense peak"}[args.dtype],
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},
             "stages_ms": {k: round(float(np.mean(v)), 3) for k, v in per.items()},

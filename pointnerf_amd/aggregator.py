@@ -103,8 +103,7 @@ def frag_pack_bf16(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.T
     return F.view(-1).to(torch.bfloat16)
 
 
-X3_PAD = 2   # kXPad in aggregate.hip
-X3_SIGMA = (0, 2, 1, 3, 4, 6, 5, 7)   # k order of two quad-row float4 reads (qperm {0,2,1,3})
+X3_PAD = 3   # zero k-steps after each split pack (kWD in aggregate_x3.hip: weights three steps ahead)
 
 
 def split3_bf16(W: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -120,8 +119,9 @@ def split3_bf16(W: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tens
 
 def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """Split-bf16 A-operand packs for pnr_aggregate_fwd_x3:
-    F[t][T][plane][lane][j] = plane of W'[32T + (lane & 31)][16t + 8(lane >> 5) + sigma(j)],
-    W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus X3_PAD zero ones."""
+    F[t][T][plane][lane][j] = plane of W'[32T + (lane & 31)][16t + 8(lane >> 5) + j],
+    W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus X3_PAD zero ones; planes
+    from split3_bf16 (W' == plane0 + plane1 + plane2 exactly)."""
     out_f, kin = W.shape
     assert out_f % 32 == 0
     cols = kin + (1 if bias is not None else 0)
@@ -131,8 +131,7 @@ def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Ten
     Wp[:, :kin] = W.float()
     if bias is not None:
         Wp[:, kin] = bias.float()
-    sig = torch.tensor(X3_SIGMA, device=W.device)
-    Wp = Wp.view(out_f, tot, 2, 8)[..., sig]                             # k = 16t + 8h + sigma(j)
+    Wp = Wp.view(out_f, tot, 2, 8)                                      # k = 16t + 8h + j
     planes = torch.stack(split3_bf16(Wp), 0)                            # [3][out][t][h][j]
     F = planes.view(3, NT, 32, tot, 2, 8).permute(3, 1, 0, 4, 2, 5).contiguous()   # [t][T][pl][h][r][j]
     return F.view(-1)

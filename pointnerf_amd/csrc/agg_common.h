@@ -53,4 +53,44 @@ __device__ __forceinline__ int64_t eff_n(const pnr_samples& s) {
   return n;
 }
 
+// ---------------------------------------------------------------------------
+// Exact 3-way bf16 split of fp32 values for the fp32-accurate bf16-MFMA GEMMs
+// (aggregate_x3.hip): x = x0 + x1 + x2 with x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = bf16(x - x0 - x1), round-to-nearest-even, every residual exact in fp32.
+// W . X then keeps the six cross products of weight >= 2^-16,
+//   W2.X0 + W1.X1 + W0.X2 + W1.X0 + W0.X1 + W0.X0,
+// on v_mfma_f32_32x32x16_bf16 (bf16 products are exact in fp32, fp32
+// accumulation): the dropped terms are <= 2^-24 |w x|, one fp32 rounding.
+__device__ __forceinline__ unsigned cvt_bf16x2(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  bf2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+// low bf16 of a pair as fp32 (v_perm_b32: `u << 16` gets rewritten into a second cvt)
+__device__ __forceinline__ float bf16_lo_f(unsigned u) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_perm(u, 0u, 0x05040c0cu));
+}
+__device__ __forceinline__ float bf16_hi_f(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+
+// (a, b) -> three bf16 pairs (low half = a); 9 VALU
+__device__ __forceinline__ void split2(float a, float b, unsigned& x0, unsigned& x1, unsigned& x2) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  x0 = cvt_bf16x2(a, b);
+  const f2 r = v - (f2){bf16_lo_f(x0), bf16_hi_f(x0)};
+  x1 = cvt_bf16x2(r.x, r.y);
+  const f2 r2 = r - (f2){bf16_lo_f(x1), bf16_hi_f(x1)};
+  x2 = cvt_bf16x2(r2.x, r2.y);
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, const f32x16& c) {
+  typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+}
+
+// aggregate_x3.hip: the pairs stage of pnr_aggregate_fwd_x3
+int launch_pairs_x3(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const pnr_mlp_x3& wx,
+                    const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
+                    float* out_conf, hipStream_t st);
+
 }  // namespace pnr

@@ -53,7 +53,6 @@ struct AggArgs {
   float* out_conf;
   const uint8_t* pair_mask;   // mirror path: validity per (row, k); pidx == NULL
   pnr_agg_saved sv;           // training forward: activations kept for the backward
-  pnr_mlp_x3 wx;              // split-bf16 packs (pnr_aggregate_fwd_x3)
 };
 
 template <int NT>
@@ -332,200 +331,11 @@ __device__ __forceinline__ void store_act_q(const f32x16 (&acc)[PT * NT], float*
       }
 }
 
-// ---------------------------------------------------------------------------
-// fp32 GEMM on bf16 MFMA by a 3-way split (pnr_aggregate_fwd_x3).  Every fp32
-// operand is the exact sum of three bf16 values, x = x0 + x1 + x2 (x0 =
-// bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1); each subtraction is exact
-// in fp32), and W . X keeps the six cross products of weight >= 2^-16:
-//   W2.X0 + W1.X1 + W0.X2 + W1.X0 + W0.X1 + W0.X0   (smallest first)
-// on v_mfma_f32_32x32x16_bf16 (bf16 products are exact in fp32, accumulation
-// in fp32).  The dropped terms are <= 2^-24 of |w x|, the size of one fp32
-// rounding, so the result is an fp32-accurate GEMM at 6 x 32 = 192 MFMA
-// cycles per 16 k instead of 8 x 64 = 512 for v_mfma_f32_32x32x2_f32.
-// Weights are pre-split (aggregator.frag_pack_x3): uint4 Wx[t][T][plane][lane]
-// = bf16 plane of W'[32T + (lane&31)][16t + 8(lane>>5) + sigma(j)], j = 0..7,
-// sigma = {0,2,1,3,4,6,5,7} -- the k order of two quad-row float4 reads, so
-// the B operand of a k-step is two ds_read_b128 of the fp32 quad-row tile,
-// split in registers.
-constexpr int kXPad = 2;   // zero k-steps padded onto the split packs (two-step weight prefetch)
-#ifndef PNR_X3_SCHED
-#define PNR_X3_SCHED 0      // VALU per MFMA in a forced interleave (0: compiler's schedule)
-#endif
-
-__device__ __forceinline__ unsigned cvt_bf16x2(float a, float b) {
-  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-  bf2 v = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(unsigned, v);
-}
-// (v_perm_b32, opaque to instcombine: `u << 16` is rewritten into a second cvt)
-__device__ __forceinline__ float bf_lo(unsigned u) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_perm(u, 0u, 0x05040c0cu));
-}
-__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
-
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-// 9 VALU per pair: 3 v_cvt_pk_bf16_f32, 2 x (shl, and, v_pk_add_f32)
-__device__ __forceinline__ void split_pair(float a, float b, unsigned& x0, unsigned& x1, unsigned& x2) {
-  const f32x2v v = {a, b};
-  x0 = cvt_bf16x2(a, b);
-  const f32x2v r = v - (f32x2v){bf_lo(x0), bf_hi(x0)};
-  x1 = cvt_bf16x2(r.x, r.y);
-  const f32x2v r2 = r - (f32x2v){bf_lo(x1), bf_hi(x1)};
-  x2 = cvt_bf16x2(r2.x, r2.y);
-}
-
-// 8 fp32 (two quad-row float4s) -> three bf16x8 B fragments
-__device__ __forceinline__ void split8(const float4& p, const float4& q, uint4& x0, uint4& x1, uint4& x2) {
-  if (PNR_ABLATE & 16) {   // timing only: no split
-    x0 = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(q.x), __float_as_uint(q.y));
-    x1 = make_uint4(__float_as_uint(p.z), __float_as_uint(p.w), __float_as_uint(q.z), __float_as_uint(q.w));
-    x2 = x0;
-    return;
-  }
-  split_pair(p.x, p.y, x0.x, x1.x, x2.x);
-  split_pair(p.z, p.w, x0.y, x1.y, x2.y);
-  split_pair(q.x, q.y, x0.z, x1.z, x2.z);
-  split_pair(q.z, q.w, x0.w, x1.w, x2.w);
-}
-
-typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ f32x16 mfma_bf(const uint4& a, const uint4& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8v, a), __builtin_bit_cast(bf16x8v, b), c,
-                                                 0, 0, 0);
-}
-
-// Split packs are read with buffer loads: descriptor from the (uniform) pack
-// base, voffset = this lane's 16 B of the wave's first tile, soffset = k-step
-// and tile, immediate = plane -- no 64-bit VGPR address arithmetic per load.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t pack_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-}
-
-// this wave's NT tiles of k-step t, 3 planes each (voff = (T0 * 3 * 64 + lane) * 16)
-template <int NT>
-__device__ __forceinline__ void load_wx(uint4 (&a)[NT][3], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
-#pragma unroll
-  for (int T = 0; T < NT; ++T)
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-      a[T][pl] = bload16(rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * 8 + T) * 3 * 1024);
-}
-
-template <int NT>
-__device__ __forceinline__ void prime_x(uint4 (&a0)[NT][3], uint4 (&a1)[NT][3], __amdgpu_buffer_rsrc_t rs,
-                                        int voff) {
-  load_wx<NT>(a0, rs, voff, 0);
-  load_wx<NT>(a1, rs, voff, 1);
-}
-
-// the 6 cross products of one 32-pair half for NT tiles (smallest first)
-template <int NT>
-__device__ __forceinline__ void x3_products(f32x16* ac, const uint4 (&a)[NT][3], const uint4& b0, const uint4& b1,
-                                            const uint4& b2) {
-  if (PNR_ABLATE & 32) {   // timing only: one product
-#pragma unroll
-    for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][0], b0, ac[T]);
-    return;
-  }
-#pragma unroll
-  for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][2], b0, ac[T]);
-#pragma unroll
-  for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][1], b1, ac[T]);
-#pragma unroll
-  for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][0], b2, ac[T]);
-#pragma unroll
-  for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][1], b0, ac[T]);
-#pragma unroll
-  for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][0], b1, ac[T]);
-#pragma unroll
-  for (int T = 0; T < NT; ++T) ac[T] = mfma_bf(a[T][0], b0, ac[T]);
-}
-
-// Y^T += W . X^T, NT neuron tiles x PT 32-pair halves over nsteps k-steps of
-// 16, X^T from the fp32 quad-row tile (rows past the layer's inputs up to
-// 16 * nsteps must be finite: zero rows / bias rows, see k_pairs).  Weight
-// fragments two steps ahead (primed by prime_x).  Software pipeline: the
-// split of the next operand (the next half, or the next step's first half,
-// read from LDS one step ahead) runs on the VALU between the current half's
-// MFMAs.
-template <int NT, int PT>
-__device__ __forceinline__ void mlp_layer_x(f32x16 (&acc)[PT * NT], uint4 (&a0)[NT][3], uint4 (&a1)[NT][3],
-                                            __amdgpu_buffer_rsrc_t rs, int voff, const float* X, int nsteps,
-                                            int lane) {
-  const int c = lane & 31, h = lane >> 5;
-  const float* xr = X + 2 * h * kQP + 4 * c;
-  auto ldx = [&](int t, int pt, float4& p, float4& q) {
-    p = *reinterpret_cast<const float4*>(xr + 4 * t * kQP + 128 * pt);
-    q = *reinterpret_cast<const float4*>(xr + 4 * t * kQP + 128 * pt + kQP);
-  };
-  float4 xp[PT], xq[PT];   // this step's fp32 operands (halves >= 1) / the next step's
-  uint4 b0, b1, b2;        // the split operand being multiplied
-  {
-    float4 p, q;
-    ldx(0, 0, p, q);
-    split8(p, q, b0, b1, b2);
-#pragma unroll
-    for (int pt = 1; pt < PT; ++pt) ldx(0, pt, xp[pt], xq[pt]);
-  }
-  auto step = [&](uint4 (&a)[NT][3], int t) {
-    const int tn = t + 1 < nsteps ? t + 1 : t;
-    float4 np[PT], nq[PT];
-#pragma unroll
-    for (int pt = 0; pt < PT; ++pt) ldx(tn, pt, np[pt], nq[pt]);
-#pragma unroll
-    for (int pt = 0; pt < PT; ++pt) {
-      uint4 c0, c1, c2;
-      if (pt + 1 < PT) split8(xp[pt + 1], xq[pt + 1], c0, c1, c2);
-      else split8(np[0], nq[0], c0, c1, c2);
-      x3_products<NT>(acc + pt * NT, a, b0, b1, b2);
-#if PNR_X3_SCHED
-      // interleave the next operand's split (~40 VALU) with this half's 12 MFMAs
-#pragma unroll
-      for (int i = 0; i < 6 * NT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, PNR_X3_SCHED, 0);
-      }
-#endif
-      b0 = c0;
-      b1 = c1;
-      b2 = c2;
-    }
-#pragma unroll
-    for (int pt = 1; pt < PT; ++pt) {
-      xp[pt] = np[pt];
-      xq[pt] = nq[pt];
-    }
-    load_wx<NT>(a, rs, voff, t + 2);   // packs carry kXPad zero steps
-  };
-  int t = 0;
-#pragma unroll 1
-  for (; t + 2 <= nsteps; t += 2) {
-    step(a0, t);
-    step(a1, t + 1);
-  }
-  if (t < nsteps) step(a0, t);   // (the ring then holds padding; prime_x refills it)
-}
-
 // X^T row kin = 1 (bias column of the packed weights), row kin + 1 = 0 when
 // the k-step is shared; one wave, lane = pair column.
 __device__ __forceinline__ void bias_rows_q(float* X, int kin, int lane) {
   X[qaddr(kin, lane)] = 1.f;
   if ((kin & 1) == 0) X[qaddr(kin + 1, lane)] = 0.f;
-}
-
-// Bias row 256 = 1 before block1.2 / block3.2; the split path's 16-k steps
-// also read rows 257..263, which must be finite (zero here).
-template <bool EMU>
-__device__ __forceinline__ void emu_bias_rows(float* X, int lane) {
-  if constexpr (EMU) {
-    *reinterpret_cast<float4*>(X + 64 * kQP + 4 * lane) = make_float4(1.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(X + 65 * kQP + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
-  } else {
-    bias_rows_q(X, 256, lane);
-  }
 }
 
 constexpr int kPairWaves = 4;
@@ -576,9 +386,8 @@ __device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float
 #endif
 constexpr int kPairSub = PNR_PAIR_SUB;
 
-template <bool TRAIN, bool EMU = false>
+template <bool TRAIN>
 __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pairs(AggArgs A) {
-  static_assert(!(TRAIN && EMU), "the split-bf16 path is forward-only");
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   const int sub = (threadIdx.x >> 6) / kPairWaves;   // which of the workgroup's tiles
   float* X = lds_dyn + sub * kPairsLdsFloats;  // quad rows [kQRows][kQP]
@@ -610,23 +419,7 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
   const float* w3 = A.w.w3f + T0 * 64;
   const float* w4 = A.w.w4f + T0 * 64;
   float ring[kQD][kNTW];
-  uint4 rx0[kNTW][3], rx1[kNTW][3];
-  __amdgpu_buffer_rsrc_t x1b, x2, x3, x4;
-  const int xvo = (T0 * 3 * 64 + lane) * 16;
-  if constexpr (EMU) {
-    x1b = pack_rsrc(A.wx.w1bx);
-    x2 = pack_rsrc(A.wx.w2x);
-    x3 = pack_rsrc(A.wx.w3x);
-    x4 = pack_rsrc(A.wx.w4x);
-    prime_x<kNTW>(rx0, rx1, x1b, xvo);
-    // rows 264..271 (quads 66, 67): read by the 16-k steps of block3, never written
-    if (wid == 0) {
-      *reinterpret_cast<float4*>(X + 66 * kQP + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(X + 67 * kQP + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  } else {
-    prime_q<kNTW>(ring, w1b, lane);
-  }
+  prime_q<kNTW>(ring, w1b, lane);
 
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t tile = grp * kPairSub + sub;   // past ntiles: every pair inactive
@@ -774,33 +567,21 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
         }
       }
     }
-    if (EMU && wid == 1)   // rows 60..63: the 4th 16-k step of block1.0's distance half
-      *reinterpret_cast<float4*>(X + 15 * kQP + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
     if (TRAIN && active && wid == kPairWaves - 1)   // pe5 rows are padded to 64 for the dW GEMM
       *reinterpret_cast<float4*>(A.sv.pe5 + (tile * kTP + lane) * 64 + 60) = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
     // ------------------------------------------------------------ block1: 284 -> 256 -> 256
-    if constexpr (EMU) {
-      mlp_layer_x<kNTW, kPTW>(acc, rx0, rx1, x1b, xvo, X, 4, lane);
-      prime_x<kNTW>(rx0, rx1, x2, xvo);
-    } else {
-      mlp_layer_q<kNTW, kPTW>(acc, ring, w1b, X, 30, lane);   // + W1[:, 224:284] . PE_5(dist)
-      prime_q<kNTW>(ring, w2, lane);
-    }
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w1b, X, 30, lane);   // + W1[:, 224:284] . PE_5(dist)
+    prime_q<kNTW>(ring, w2, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h1, A.sv.mask, 0, tile, n, neg, lane, T0);
-    if (wid == 0) emu_bias_rows<EMU>(X, lane);
+    if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    if constexpr (EMU) {
-      mlp_layer_x<kNTW, kPTW>(acc, rx0, rx1, x2, xvo, X, 17, lane);
-      prime_x<kNTW>(rx0, rx1, x3, xvo);
-    } else {
-      mlp_layer_q<kNTW, kPTW>(acc, ring, w2, X, 129, lane);
-      prime_q<kNTW>(ring, w3, lane);
-    }
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w2, X, 129, lane);
+    prime_q<kNTW>(ring, w3, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h2, A.sv.mask, 1, tile, n, neg, lane, T0);
@@ -813,27 +594,17 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
     // ------------------------------------------------------------ block3: 263 -> 256 -> 256
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    if constexpr (EMU) {
-      mlp_layer_x<kNTW, kPTW>(acc, rx0, rx1, x3, xvo, X, 17, lane);
-      prime_x<kNTW>(rx0, rx1, x4, xvo);
-    } else {
-      mlp_layer_q<kNTW, kPTW>(acc, ring, w3, X, 132, lane);
-      prime_q<kNTW>(ring, w4, lane);
-    }
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w3, X, 132, lane);
+    prime_q<kNTW>(ring, w4, lane);
     __syncthreads();
     store_act_q<kNTW, kPTW>(acc, X, neg, lane, T0);
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h3, A.sv.mask, 2, tile, n, neg, lane, T0);
-    if (wid == 0) emu_bias_rows<EMU>(X, lane);
+    if (wid == 0) bias_rows_q(X, 256, lane);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    if constexpr (EMU) {
-      mlp_layer_x<kNTW, kPTW>(acc, rx0, rx1, x4, xvo, X, 17, lane);
-      prime_x<kNTW>(rx0, rx1, x1b, xvo);              // the next tile's layer 1
-    } else {
-      mlp_layer_q<kNTW, kPTW>(acc, ring, w4, X, 129, lane);
-      prime_q<kNTW>(ring, w1b, lane);                 // the next tile's layer 1
-    }
+    mlp_layer_q<kNTW, kPTW>(acc, ring, w4, X, 129, lane);
+    prime_q<kNTW>(ring, w1b, lane);                   // the next tile's layer 1
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h4, A.sv.mask, 3, tile, n, neg, lane, T0);
     if (!(PNR_ABLATE & 4)) {
       // ---------------------------------------------------------- alpha + K sums from registers
@@ -1017,11 +788,13 @@ __global__ void __launch_bounds__(64 * kColWaves, 2) k_color(AggArgs A) {
   }
 }
 
-template <bool TRAIN, bool EMU = false>
-int launch_t(const AggArgs& a, hipStream_t st) {
+constexpr int kStagePre = 1, kStagePairs = 2, kStageColor = 4, kStageAll = 7;
+
+template <bool TRAIN>
+int launch_t(const AggArgs& a, hipStream_t st, int stages = kStageAll) {
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs<TRAIN, EMU>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs<TRAIN>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kPairsLdsBytes * kPairSub)));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggLdsBytes));
@@ -1029,18 +802,23 @@ int launch_t(const AggArgs& a, hipStream_t st) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kColLdsBytes));
     attr = true;
   }
-  if (!a.pts.p1_ready) {
+  if ((stages & kStagePre) && !a.pts.p1_ready) {
     hipLaunchKernelGGL(k_point_pre, dim3(grid_for(cdiv(a.pts.used ? a.pts.n_used : a.pts.n, 32), 4, 256)),
                        dim3(kAggBlock), kAggLdsBytes, st, a);
     PNR_LAUNCH_CHECK();
   }
-  const int64_t tiles = cdiv(a.s.n_max, kTS);
-  hipLaunchKernelGGL((k_pairs<TRAIN, EMU>), dim3(grid_for(cdiv(tiles, kPairSub), 1, 256 * 2 / kPairSub)),
-                     dim3(64 * kPairWaves * kPairSub), kPairsLdsBytes * kPairSub, st, a);
-  PNR_LAUNCH_CHECK();
-  const int64_t ctiles = cdiv(a.s.n_max, kTP);
-  hipLaunchKernelGGL(k_color<TRAIN>, dim3(grid_for(ctiles, 1, 256 * 2)), dim3(64 * kColWaves), kColLdsBytes, st, a);
-  PNR_LAUNCH_CHECK();
+  if (stages & kStagePairs) {
+    const int64_t tiles = cdiv(a.s.n_max, kTS);
+    hipLaunchKernelGGL(k_pairs<TRAIN>, dim3(grid_for(cdiv(tiles, kPairSub), 1, 256 * 2 / kPairSub)),
+                       dim3(64 * kPairWaves * kPairSub), kPairsLdsBytes * kPairSub, st, a);
+    PNR_LAUNCH_CHECK();
+  }
+  if (stages & kStageColor) {
+    const int64_t ctiles = cdiv(a.s.n_max, kTP);
+    hipLaunchKernelGGL(k_color<TRAIN>, dim3(grid_for(ctiles, 1, 256 * 2)), dim3(64 * kColWaves), kColLdsBytes, st,
+                       a);
+    PNR_LAUNCH_CHECK();
+  }
   return PNR_OK;
 }
 
@@ -1460,6 +1238,7 @@ extern "C" int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s,
   PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_x3: need pers or camera");
   PNR_CHECK_ARG(s->pidx, "aggregate_x3: pidx required");
   PNR_CHECK_ARG(wx && wx->w1bx && wx->w2x && wx->w3x && wx->w4x, "aggregate_x3: null split weight pack");
+  PNR_CHECK_ARG(w->neg_slope >= 0.f && w->neg_slope <= 1.f, "aggregate_x3: LeakyReLU slope must be in [0, 1]");
   PNR_CHECK_ARG((((uintptr_t)wx->w1bx | (uintptr_t)wx->w2x | (uintptr_t)wx->w3x | (uintptr_t)wx->w4x) & 15) == 0,
                 "aggregate_x3: split packs must be 16-B aligned");
   if (s->n_max <= 0) return PNR_OK;
@@ -1467,13 +1246,17 @@ extern "C" int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s,
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  a.wx = *wx;
   carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.pair_mask = nullptr;
-  return launch_t<false, true>(a, as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  // k_point_pre (fp32 P1) -> k_pairs_x3 (aggregate_x3.hip) -> k_color
+  if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
+  if ((rc = launch_pairs_x3(a.pts, a.s, a.w, *wx, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf, st)))
+    return rc;
+  return launch_t<false>(a, st, kStageColor);
 }
 
 extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,

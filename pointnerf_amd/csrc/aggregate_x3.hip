@@ -1,0 +1,640 @@
+// fp32-accurate k_pairs on bf16 MFMA (pnr_aggregate_fwd_x3): block1.0's
+// distance half, block1.2, block3.0 and block3.2 for 64 (sample, neighbour)
+// pairs per tile, as in aggregate.hip's k_pairs, with every fp32 GEMM done as
+// an exact 3-way bf16 split (see agg_common.h, split2).
+//
+// Producer / consumer workgroup (one 8-wave workgroup per CU):
+//   * consumers (waves 0..3) own neuron tiles {2w, 2w+1} x both 32-pair halves
+//     and run the MFMA stream: 6 products per 16-k step, weights from split
+//     packs three steps ahead (buffer loads), B fragments = three ds_read_b128 of
+//     the bf16 planes of the layer input.  Each activation is split ONCE, by the
+//     wave that produced it, when it is stored (not once per consuming wave).
+//   * producers (waves 4..7) prepare the NEXT tile while the consumers run
+//     block1.2 of the current one: gather (pidx, xyz, w2pers, colour, dir,
+//     conf), 6-d distance, normalised weights, the 5-band PE split into planes,
+//     the block3.0 extras -- so the gather latency and the sincos never stall
+//     the MFMA pipe.  The consumers prefetch the next tile's per-point
+//     block1.0 half (P1) into registers during block3.2.
+// LDS (135 KB): layer-input planes [3][34 row groups][64 pairs][8 bf16]
+// (rows 0..271; row group g, pair c at (g*64 + c)*16 B, so a B fragment is one
+// conflict-free ds_read_b128 and an accumulator quad one ds_write_b64 per
+// plane), next-tile PE planes [3][8][64][8], and double-buffered per-tile
+// extras / weights / point rows / sample flags.
+#include "agg_common.h"
+
+#ifndef PNR_ABLATE
+#define PNR_ABLATE 0  // dev-only timing ablations (tools/build_ablations.sh)
+#endif
+
+namespace pnr {
+namespace {
+
+constexpr int kXT = 64;            // pairs per tile
+constexpr int kXTS = kXT / kKN;    // samples per tile
+constexpr int kXG = 34;            // 8-row groups of a layer input (272 rows)
+constexpr int kPG = 8;             // 8-row groups of the distance PE (64 rows)
+constexpr int kPlaneX = kXG * kXT * 16;
+constexpr int kPlaneP = kPG * kXT * 16;
+constexpr int kOffPE = 3 * kPlaneX;
+constexpr int kOffEx = kOffPE + 3 * kPlaneP;     // float [2][8][64]
+constexpr int kOffWt = kOffEx + 2 * 8 * kXT * 4;  // float [2][64]
+constexpr int kOffPr = kOffWt + 2 * kXT * 4;      // int   [2][64]
+constexpr int kOffSf = kOffPr + 2 * kXT * 4;      // int   [2][8]
+constexpr int kOffAp = kOffSf + 2 * kXTS * 4;     // float [4][64]
+constexpr int kOffWa = kOffAp + 4 * kXT * 4;      // float [256] alpha_branch.0 weights
+constexpr size_t kX3Lds = (size_t)kOffWa + kHid * 4;
+constexpr int kP1Pitch = kHid + 4;                 // floats per parked P1 row (conflict-free b128 reads)
+static_assert(kXT * kP1Pitch * 4 <= 3 * kPlaneX, "parked P1 fits the layer-input area");
+static_assert(kX3Lds <= 160 * 1024, "LDS budget");
+
+#ifndef PNR_TRACE
+#define PNR_TRACE 0   // dev-only: per-phase s_memtime stamps of block 0 (pnr_debug_x3_trace)
+#endif
+#if PNR_TRACE
+__device__ unsigned long long g_x3_trace[2][64][16];
+__device__ unsigned long long g_x3_blk[1024][2];   // per block: loop start, loop end (consumer wave 0)
+#define X3_TR(role, ev)                                                        \
+  do {                                                                         \
+    if (blockIdx.x == 0 && (threadIdx.x & 255) == 0 && it < 64)                \
+      g_x3_trace[role][it][ev] = clock64();                                    \
+  } while (0)
+#else
+#define X3_TR(role, ev) \
+  do {                  \
+  } while (0)
+#endif
+
+typedef float f32x2n __attribute__((ext_vector_type(2)));
+typedef float f32x4n __attribute__((ext_vector_type(4)));
+
+struct X3Args {
+  pnr_points pts;
+  pnr_samples s;
+  pnr_mlp w;
+  pnr_mlp_x3 wx;
+  const float* p1;
+  float* hid;
+  int32_t* vmask;
+  float* out_feat;
+  float* out_weight;
+  float* out_conf;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+// this wave's 2 neuron tiles of k-step t, 3 planes each; voff = (T0 * 3 * 64 + lane) * 16
+__device__ __forceinline__ void load_w(uint4 (&a)[2][3], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
+#pragma unroll
+  for (int T = 0; T < 2; ++T)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      a[T][pl] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * 8 + T) * 3 * 1024, 0));
+}
+
+constexpr int kWD = 3;   // weight ring depth (k-steps in flight); the packs carry kWD zero steps
+
+struct WRing {
+  uint4 a[kWD][2][3];
+};
+
+__device__ __forceinline__ void prime(WRing& w, __amdgpu_buffer_rsrc_t rs, int voff) {
+#pragma unroll
+  for (int d = 0; d < kWD; ++d) load_w(w.a[d], rs, voff, d);
+}
+
+// the six cross products of one 32-pair half, both tiles, smallest first
+__device__ __forceinline__ void products(f32x16* ac, const uint4 (&a)[2][3], const uint4 (&b)[3]) {
+#pragma unroll
+  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][2], b[0], ac[T]);
+#pragma unroll
+  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][1], b[1], ac[T]);
+#pragma unroll
+  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][0], b[2], ac[T]);
+#pragma unroll
+  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][1], b[0], ac[T]);
+#pragma unroll
+  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][0], b[1], ac[T]);
+#pragma unroll
+  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][0], b[0], ac[T]);
+}
+
+// Y^T += W . X^T over nsteps 16-k steps; X^T = the bf16 planes at `planes`
+// (plane stride pstride bytes, 64 pairs per 8-row group).  Weights kWD steps
+// ahead in the ring (slot d: steps = d mod kWD), B one step ahead.
+__device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing& w, __amdgpu_buffer_rsrc_t rs, int voff,
+                                      const char* planes, int pstride, int nsteps, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const char* base = planes + (h * kXT + c) * 16;
+  auto ldb = [&](int t, int pt, uint4 (&bb)[3]) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      bb[pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * t * kXT + 32 * pt) * 16);
+  };
+  uint4 b[2][3];
+  ldb(0, 0, b[0]);
+  ldb(0, 1, b[1]);
+  // each half's next-step B is read right after its products issue (hidden by the other half's)
+  auto step = [&](uint4 (&a)[2][3], int t) {
+    const int tn = t + 1 < nsteps ? t + 1 : t;
+    // sched_barrier(0) pins this order: hipcc otherwise sinks the B reads next
+    // to their MFMAs (exposed LDS latency) and merges the weight waits
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      if (PNR_ABLATE & 32) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_bf16(a[T][0], b[pt][0], acc[2 * pt + T]);
+      } else {
+        products(acc + 2 * pt, a, b[pt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(PNR_ABLATE & 64)) ldb(tn, pt, b[pt]);   // (64: timing only, B fixed)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    load_w(a, rs, voff, t + kWD);   // packs carry kWD zero steps
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int t = 0;
+#pragma unroll 1
+  for (; t + kWD <= nsteps; t += kWD) {
+#pragma unroll
+    for (int d = 0; d < kWD; ++d) step(w.a[d], t + d);
+  }
+#pragma unroll
+  for (int d = 0; d < kWD - 1; ++d)
+    if (t + d < nsteps) step(w.a[d], t + d);   // the ring then holds padding; prime() refills it
+}
+
+// lrelu(acc) -> layer-input planes, rows 32(T0+T) + 8q + 4h + i: one ds_write_b64 per plane and quad
+__device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, float s, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+  if (PNR_ABLATE & 128) {   // timing only: no split (hi plane = bf16(x), other planes untouched)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x16& v = acc[2 * pt + T];
+          char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
+          *reinterpret_cast<uint2*>(d) = make_uint2(cvt_bf16x2(lrelu(v[4 * q], s), lrelu(v[4 * q + 1], s)),
+                                                    cvt_bf16x2(lrelu(v[4 * q + 2], s), lrelu(v[4 * q + 3], s)));
+        }
+    return;
+  }
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16& v = acc[2 * pt + T];
+        unsigned a0, a1, a2, b0, b1, b2;
+        // lrelu(x) = max(x, s x) for 0 <= s <= 1 (same value and sign of zero)
+        split2(fmaxf(v[4 * q], s * v[4 * q]), fmaxf(v[4 * q + 1], s * v[4 * q + 1]), a0, a1, a2);
+        split2(fmaxf(v[4 * q + 2], s * v[4 * q + 2]), fmaxf(v[4 * q + 3], s * v[4 * q + 3]), b0, b1, b2);
+        char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
+        *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
+        *reinterpret_cast<uint2*>(d + kPlaneX) = make_uint2(a1, b1);
+        *reinterpret_cast<uint2*>(d + 2 * kPlaneX) = make_uint2(a2, b2);
+      }
+}
+
+// 8 fp32 rows of one pair -> row group g of the three planes (ds_write_b128 each)
+__device__ __forceinline__ void store_group(char* planes, int pstride, int g, int pair, const float (&v)[8]) {
+  uint4 p0, p1, p2;
+  split2(v[0], v[1], p0.x, p1.x, p2.x);
+  split2(v[2], v[3], p0.y, p1.y, p2.y);
+  split2(v[4], v[5], p0.z, p1.z, p2.z);
+  split2(v[6], v[7], p0.w, p1.w, p2.w);
+  char* d = planes + (g * kXT + pair) * 16;
+  *reinterpret_cast<uint4*>(d) = p0;
+  *reinterpret_cast<uint4*>(d + pstride) = p1;
+  *reinterpret_cast<uint4*>(d + 2 * pstride) = p2;
+}
+
+// producer wave pw (0..3), lane = pair column: gather + weights + PE planes of `tile`
+// into buffer nb (neural_points.py:788-799, point_aggregators.py:421-429, 775-804).
+__device__ __forceinline__ void gather(const X3Args& A, int64_t tile, int nb, char* lds, int pw, int lane,
+                                       float (&dr6)[6]) {
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  float cam_c[3] = {0.f, 0.f, 0.f}, cam_R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+  if (!A.pts.pers) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cam_c[i] = A.pts.campos[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cam_R[i] = A.pts.camrot[i];
+  }
+  const int j = lane >> 3, k = lane & 7;
+  const int K = A.s.K;
+  const int64_t n = eff_n(A.s);
+  const int64_t v = tile * kXTS + j;
+  const bool active = v < n;
+  const int64_t row = active ? sample_row(A.s, v) : 0;
+  int64_t prow = -1;
+  bool valid = false;
+  if (active && k < K) {
+    const int pid = A.s.pidx[row * K + k];
+    valid = pid >= 0;
+    prow = valid ? pid : 0;   // torch.clamp(sample_pidx, min=0)
+  }
+  float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
+  if (active) {
+    const int64_t drow = dir_row(A.s, row);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      sw[a] = A.s.sample_w[row * 3 + a];
+      sp[a] = A.s.sample_p[row * 3 + a];
+      vd[a] = A.s.dirs[drow * 3 + a];
+    }
+  }
+  float pw3[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, col[3] = {0.f, 0.f, 0.f}, pdir[3] = {0.f, 0.f, 0.f};
+  float cf = 1.f;
+  if (valid) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      pw3[a] = A.pts.xyz[prow * 3 + a];
+      col[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
+      pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
+    }
+    if (A.pts.pers) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
+    } else {
+      world_to_pers(pw3, cam_c, cam_R, pp);
+    }
+  }
+  if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
+  float d6[6];
+  d6[0] = pw3[0] - sw[0];
+  d6[1] = pw3[1] - sw[1];
+  d6[2] = pw3[2] - sw[2];
+  d6[3] = pp[0] * pp[2] - sp[0] * sp[2];
+  d6[4] = pp[1] * pp[2] - sp[1] * sp[2];
+  d6[5] = pp[2] - sp[2];
+  mat3(Rw, d6, dr6);
+  dr6[3] = d6[3];
+  dr6[4] = d6[4];
+  dr6[5] = d6[5];
+  if (pw == 0) {
+    const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
+    const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
+    const float wsum = xor8_sum(wl);
+    const float wn = wl / fmaxf(wsum, 1e-8f);
+    const float confc = fminf(fmaxf(cf, 1e-4f), 1.f);
+    const bool samp_valid = xor8_sum(valid ? 1.f : 0.f) > 0.f;
+    float vrot[3], drot[3];
+    mat3(Rw, vd, vrot);
+    mat3(Rw, pdir, drot);
+    const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
+    const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
+    float* exL = reinterpret_cast<float*>(lds + kOffEx) + nb * 8 * kXT;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) exL[e * kXT + lane] = ex[e];
+    reinterpret_cast<float*>(lds + kOffWt)[nb * kXT + lane] = wn * confc;
+    reinterpret_cast<int*>(lds + kOffPr)[nb * kXT + lane] = valid ? (int)prow : -1;
+    if (k == 0) reinterpret_cast<int*>(lds + kOffSf)[nb * kXTS + j] = active && samp_valid;
+    if (active && k < K) {
+      if (A.out_weight) A.out_weight[row * K + k] = wn;
+      if (A.out_conf) A.out_conf[row * K + k] = confc;
+    }
+  }
+}
+
+// 5-band PE of the rotated 6-d distance of this lane's pair -> rows 2e (sin),
+// 2e + 1 (cos), e = 5 ch + f, of the PE planes; producer wave pw takes e = pw (mod 4)
+__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6]) {
+  if (pw == 0) {   // rows 60..63: the 4th 16-k step reads them
+    char* pz = lds + kOffPE + (7 * kXT + lane) * 16 + 8;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
+  }
+  if (!(PNR_ABLATE & 2)) {
+#pragma unroll 1
+    for (int e = pw; e < 30; e += 4) {
+      const int ch = e / 5, f = e - 5 * ch;
+      float dc = dr6[0];
+      dc = ch == 1 ? dr6[1] : dc;
+      dc = ch == 2 ? dr6[2] : dc;
+      dc = ch == 3 ? dr6[3] : dc;
+      dc = ch == 4 ? dr6[4] : dc;
+      dc = ch == 5 ? dr6[5] : dc;
+      float sn, cs;
+      sincosf(dc * (float)(1 << f), &sn, &cs);
+      unsigned x0, x1, x2;
+      split2(sn, cs, x0, x1, x2);
+      const int r = 2 * e;
+      char* d = lds + kOffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
+      *reinterpret_cast<unsigned*>(d) = x0;
+      *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+      *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
+    }
+  }
+}
+
+// Consumer: block1.0 (distance half) .. block3.2, alpha and K sums of one tile
+// per iteration.  Barriers S1..S8 pair with the producer loop's.
+__device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wid, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kXTS);
+  const float neg = A.w.neg_slope;
+  char* XP = lds;
+  const char* PE = lds + kOffPE;
+  const float* P1L = reinterpret_cast<const float*>(lds);   // P1 rows parked in the XP area between tiles
+  float* apart = reinterpret_cast<float*>(lds + kOffAp);
+  const float* waL = reinterpret_cast<const float*>(lds + kOffWa);
+  const int T0 = 2 * wid;
+  const int voff = (T0 * 3 * 64 + lane) * 16;
+  const __amdgpu_buffer_rsrc_t r1 = rsrc(A.wx.w1bx), r2 = rsrc(A.wx.w2x), r3 = rsrc(A.wx.w3x), r4 = rsrc(A.wx.w4x);
+  WRing wr;
+  f32x16 acc[4];
+  prime(wr, r1, voff);
+  __syncthreads();   // S0: the first tile's inputs and P1 are in LDS
+#if PNR_TRACE
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][0] = wall_clock64();
+#endif
+  int it = 0;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+    const int buf = it & 1;
+    X3_TR(0, 0);
+    // acc = P1 (block1.0 point half + bias) from LDS
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = *reinterpret_cast<const float4*>(P1L + (32 * pt + c) * kP1Pitch + 32 * (T0 + T) + 8 * q +
+                                                             4 * h);
+          acc[2 * pt + T][4 * q] = v4.x;
+          acc[2 * pt + T][4 * q + 1] = v4.y;
+          acc[2 * pt + T][4 * q + 2] = v4.z;
+          acc[2 * pt + T][4 * q + 3] = v4.w;
+        }
+    // ------------------------------------------------------------ block1.0, distance half
+    X3_TR(0, 1);
+    layer(acc, wr, r1, voff, PE, kPlaneP, 4, lane);
+    prime(wr, r2, voff);
+    X3_TR(0, 2);
+    __syncthreads();   // S1: PE planes and the parked P1 consumed
+    X3_TR(0, 3);
+    store_act(acc, XP, neg, lane, T0);
+    if (wid == 0) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
+        *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (32 * kXT + lane) * 16) =
+            make_uint4(pl == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (33 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    X3_TR(0, 4);
+    __syncthreads();   // S2
+    X3_TR(0, 5);
+    // ------------------------------------------------------------ block1.2
+    layer(acc, wr, r2, voff, XP, kPlaneX, 17, lane);
+    prime(wr, r3, voff);
+    X3_TR(0, 6);
+    __syncthreads();   // S3
+    X3_TR(0, 7);
+    store_act(acc, XP, neg, lane, T0);
+    if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
+      const float* exL = reinterpret_cast<const float*>(lds + kOffEx) + buf * 8 * kXT;
+      float ex[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ex[e] = exL[e * kXT + lane];
+      store_group(XP, kPlaneX, 32, lane, ex);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    __syncthreads();   // S4
+    X3_TR(0, 8);
+    // ------------------------------------------------------------ block3.0
+    layer(acc, wr, r3, voff, XP, kPlaneX, 17, lane);
+    prime(wr, r4, voff);
+    X3_TR(0, 9);
+    __syncthreads();   // S5
+    X3_TR(0, 10);
+    store_act(acc, XP, neg, lane, T0);
+    if (wid == 0) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (32 * kXT + lane) * 16) =
+            make_uint4(pl == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    __syncthreads();   // S6
+    X3_TR(0, 11);
+    // ------------------------------------------------------------ block3.2, alpha, K sums
+    layer(acc, wr, r4, voff, XP, kPlaneX, 17, lane);
+    prime(wr, r1, voff);   // the next tile's block1.0
+    X3_TR(0, 12);
+    if (!(PNR_ABLATE & 4)) {
+      const float* wtL = reinterpret_cast<const float*>(lds + kOffWt) + buf * kXT;
+      const int* sflag = reinterpret_cast<const int*>(lds + kOffSf) + buf * kXTS;
+      float pa_part[2] = {0.f, 0.f};
+      const int i8 = c & 7;
+      const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        const float wtp = wtL[32 * pt + c];
+        const int sj = (32 * pt + c) >> 3;
+        const int64_t vo = tile * kXTS + sj;
+        const bool wr = vo < n && sflag[sj];
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float hv = lrelu(acc[2 * pt + T][r], neg);
+            pa_part[pt] += waL[32 * (T0 + T) + acc_row(r, h)] * hv;
+            v[r] = wtp * hv;
+          }
+          // K sums (point_aggregators.py:622-628): DPP reduce-scatter over the 8 lanes of a sample
+          float w8[8], w4[4], w2[2];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float send = b2 ? v[q] : v[q + 8];
+            const float recv = __builtin_bit_cast(
+                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x141, 0xf, 0xf, false));
+            w8[q] = (b2 ? v[q + 8] : v[q]) + recv;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float send = b1 ? w8[q] : w8[q + 4];
+            const float recv = __builtin_bit_cast(
+                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E, 0xf, 0xf, false));
+            w4[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float send = b0 ? w4[q] : w4[q + 2];
+            const float recv = __builtin_bit_cast(
+                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xf, 0xf, false));
+            w2[q] = (b0 ? w4[q + 2] : w4[q]) + recv;
+          }
+          if (wr)
+            __builtin_nontemporal_store(
+                (f32x2n){w2[0], w2[1]},
+                reinterpret_cast<f32x2n*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h));
+        }
+        pa_part[pt] += __shfl_xor(pa_part[pt], 32);
+      }
+      if (h == 0) {
+        apart[wid * kXT + c] = pa_part[0];
+        apart[wid * kXT + 32 + c] = pa_part[1];
+      }
+    }
+    X3_TR(0, 13);
+    __syncthreads();   // S7: layer-input planes free (the producers park the next P1 there)
+    X3_TR(0, 14);
+    if (wid == 0 && !(PNR_ABLATE & 4)) {
+      const int j = lane >> 3, k = lane & 7;
+      const float* wtL = reinterpret_cast<const float*>(lds + kOffWt) + buf * kXT;
+      const int* sflag = reinterpret_cast<const int*>(lds + kOffSf) + buf * kXTS;
+      const float pa = apart[lane] + apart[kXT + lane] + apart[2 * kXT + lane] + apart[3 * kXT + lane] + A.w.ba[0];
+      const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
+      const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
+      const int64_t vo = tile * kXTS + j;
+      if (k == 0 && vo < n) {
+        A.vmask[vo] = sflag[j];
+        if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
+      }
+    }
+    __syncthreads();   // S8: next P1 parked
+    X3_TR(0, 15);
+  }
+#if PNR_TRACE
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][1] = wall_clock64();
+#endif
+}
+
+// Producer wave pw: P1 rows 16 pw .. 16 pw + 15 of a tile (1 KB each, one
+// coalesced float4 per lane per row) into registers.
+__device__ __forceinline__ void fetch_p1(float4 (&r)[16], const X3Args& A, const int* prow, int pw, int lane) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int pr = prow[16 * pw + i];
+    const int64_t p1r = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
+    // streamed once: non-temporal, so the rows do not evict the weight packs from L2
+    r[i] = (p1r >= 0 && !(PNR_ABLATE & 1))
+               ? __builtin_bit_cast(float4, __builtin_nontemporal_load(
+                                                reinterpret_cast<const f32x4n*>(A.p1 + p1r * kHid) + lane))
+               : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void park_p1(const float4 (&r)[16], char* lds, int pw, int lane) {
+  float* P1L = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(P1L + (16 * pw + i) * kP1Pitch + 4 * lane) = r[i];
+}
+
+// Producer: while the consumers run tile i, prepare tile i + 1 (gather, PE
+// planes, extras, weights) during block1.2 and fetch its P1 rows during
+// block3.0 / block3.2; park them in LDS once the consumers are done with the
+// layer-input planes.
+__device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw, int lane) {
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kXTS);
+  float4 p1r[16];
+  float dr6[6];
+  gather(A, blockIdx.x, 0, lds, pw, lane, dr6);
+  pe_planes(lds, pw, lane, dr6);
+  __syncthreads();   // (prologue) prow of the first tile visible to all producers
+  fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr), pw, lane);
+  park_p1(p1r, lds, pw, lane);
+  __syncthreads();   // S0
+  int it = 0;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+    const int nbuf = (it & 1) ^ 1;
+    const int64_t next = tile + gridDim.x;
+    X3_TR(1, 0);
+    __syncthreads();   // S1
+    __syncthreads();   // S2
+    // during block1.2: gather (nbuf's arrays are free: their last reader was the previous tile's finalize)
+    if (!(PNR_ABLATE & 256)) gather(A, next, nbuf, lds, pw, lane, dr6);   // (256: timing only, no producer work)
+    X3_TR(1, 1);
+    __syncthreads();   // S3: the next tile's point rows are in LDS
+    if (!(PNR_ABLATE & 256)) fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr) + nbuf * kXT, pw, lane);
+    X3_TR(1, 2);
+    __syncthreads();   // S4
+    if (!(PNR_ABLATE & 256)) pe_planes(lds, pw, lane, dr6);   // during block3.0 (the PE planes were freed at S1)
+    X3_TR(1, 3);
+    __syncthreads();   // S5
+    __syncthreads();   // S6
+    __syncthreads();   // S7
+    X3_TR(1, 4);
+    park_p1(p1r, lds, pw, lane);
+    X3_TR(1, 5);
+    __syncthreads();   // S8
+    X3_TR(1, 6);
+  }
+}
+
+__global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // alpha_branch.0 weights for the consumers' tail
+  if (threadIdx.x < kHid) reinterpret_cast<float*>(lds + kOffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
+  if (wid < 4) {
+    __syncthreads();   // (prologue)
+    consumer_loop(A, lds, wid, lane);
+  } else {
+    producer_loop(A, lds, wid - 4, lane);
+  }
+}
+
+}  // namespace
+
+#if PNR_TRACE
+extern "C" int pnr_debug_x3_trace(unsigned long long* out, int n) {
+  const size_t want = sizeof(g_x3_trace);
+  if (!out || (size_t)n * sizeof(unsigned long long) < want) return PNR_EINVAL;
+  PNR_HIP(hipDeviceSynchronize());
+  PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_trace), want));
+  return PNR_OK;
+}
+extern "C" int pnr_debug_x3_blocks(unsigned long long* out, int n) {
+  if (!out || (size_t)n * sizeof(unsigned long long) < sizeof(g_x3_blk)) return PNR_EINVAL;
+  PNR_HIP(hipDeviceSynchronize());
+  PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_blk), sizeof(g_x3_blk)));
+  return PNR_OK;
+}
+#endif
+
+int launch_pairs_x3(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const pnr_mlp_x3& wx,
+                    const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
+                    float* out_conf, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_x3),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kX3Lds));
+    attr = true;
+  }
+  X3Args a;
+  a.pts = pts;
+  a.s = s;
+  a.w = w;
+  a.wx = wx;
+  a.p1 = p1;
+  a.hid = hid;
+  a.vmask = vmask;
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  const int64_t tiles = cdiv(s.n_max, kXTS);
+  hipLaunchKernelGGL(k_pairs_x3, dim3(grid_for(tiles, 1, 256)), dim3(512), kX3Lds, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+}  // namespace pnr
