@@ -56,10 +56,11 @@ def parse():
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
     ap.add_argument("--train-rays", type=int, default=3600, help="rays per train step (random_sample_size 60^2)")
-    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "bf16"), default="fp32",
-                    help="MLP arithmetic: fp32 = the reference's on v_mfma_f32_32x32x2_f32; fp32x3 = the same fp32 "
-                         "GEMMs as exact 3-way bf16 splits (6 cross products) on v_mfma_f32_32x32x16_bf16, "
-                         "fp32-accurate; bf16 = bf16 operands (SURVEY config c5)")
+    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "bf16"), default="fp32x3",
+                    help="MLP arithmetic: fp32x3 (headline) = the reference's fp32 GEMMs as exact 3-way bf16 splits "
+                         "(6 cross products) on v_mfma_f32_32x32x16_bf16, fp32-accurate (error vs an fp64 oracle "
+                         "equal to native fp32's); fp32 = native v_mfma_f32_32x32x2_f32; bf16 = bf16 operands "
+                         "(SURVEY config c5)")
     return ap.parse_args()
 
 

@@ -47,6 +47,9 @@ constexpr int kP1Pitch = kHid + 4;                 // floats per parked P1 row (
 static_assert(kXT * kP1Pitch * 4 <= 3 * kPlaneX, "parked P1 fits the layer-input area");
 static_assert(kX3Lds <= 160 * 1024, "LDS budget");
 
+#ifndef PNR_X3_PRIO
+#define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
+#endif
 #ifndef PNR_TRACE
 #define PNR_TRACE 0   // dev-only: per-phase s_memtime stamps of block 0 (pnr_debug_x3_trace)
 #endif
@@ -106,22 +109,6 @@ __device__ __forceinline__ void prime(WRing& w, __amdgpu_buffer_rsrc_t rs, int v
   for (int d = 0; d < kWD; ++d) load_w(w.a[d], rs, voff, d);
 }
 
-// the six cross products of one 32-pair half, both tiles, smallest first
-__device__ __forceinline__ void products(f32x16* ac, const uint4 (&a)[2][3], const uint4 (&b)[3]) {
-#pragma unroll
-  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][2], b[0], ac[T]);
-#pragma unroll
-  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][1], b[1], ac[T]);
-#pragma unroll
-  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][0], b[2], ac[T]);
-#pragma unroll
-  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][1], b[0], ac[T]);
-#pragma unroll
-  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][0], b[1], ac[T]);
-#pragma unroll
-  for (int T = 0; T < 2; ++T) ac[T] = mfma_bf16(a[T][0], b[0], ac[T]);
-}
-
 // Y^T += W . X^T over nsteps 16-k steps; X^T = the bf16 planes at `planes`
 // (plane stride pstride bytes, 64 pairs per 8-row group).  Weights kWD steps
 // ahead in the ring (slot d: steps = d mod kWD), B one step ahead.
@@ -137,25 +124,53 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing& w, __amdgpu_buffe
   uint4 b[2][3];
   ldb(0, 0, b[0]);
   ldb(0, 1, b[1]);
-  // each half's next-step B is read right after its products issue (hidden by the other half's)
+  // One step = 2 halves x 12 MFMAs.  Each B plane of a half is re-read for the
+  // next step, and each weight plane re-loaded kWD steps ahead, right after
+  // its last MFMA of this step, so the loads sit in MFMA gaps instead of in
+  // bursts; sched_barrier(0) pins the order (hipcc would otherwise sink the
+  // LDS reads next to their uses and merge the waits).
+  auto mm = [&](int pt, const uint4& av0, const uint4& av1, const uint4& bv) {
+    acc[2 * pt] = mfma_bf16(av0, bv, acc[2 * pt]);
+    acc[2 * pt + 1] = mfma_bf16(av1, bv, acc[2 * pt + 1]);
+  };
+  auto wl = [&](uint4 (&a)[2][3], int pl, int tw) {
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+      a[T][pl] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * 8 + T) * 3 * 1024, 0));
+  };
+  auto bl = [&](int tn, int pt, int pl) {
+    if (!(PNR_ABLATE & 64))   // (64: timing only, B fixed)
+      b[pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
+  };
   auto step = [&](uint4 (&a)[2][3], int t) {
     const int tn = t + 1 < nsteps ? t + 1 : t;
-    // sched_barrier(0) pins this order: hipcc otherwise sinks the B reads next
-    // to their MFMAs (exposed LDS latency) and merges the weight waits
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
-      if (PNR_ABLATE & 32) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_bf16(a[T][0], b[pt][0], acc[2 * pt + T]);
-      } else {
-        products(acc + 2 * pt, a, b[pt]);
-      }
+      mm(pt, a[0][2], a[1][2], b[pt][0]);                      // W2.X0
       __builtin_amdgcn_sched_barrier(0);
-      if (!(PNR_ABLATE & 64)) ldb(tn, pt, b[pt]);   // (64: timing only, B fixed)
+      if (pt == 1) wl(a, 2, t + kWD);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(pt, a[0][1], a[1][1], b[pt][1]);                      // W1.X1
+      mm(pt, a[0][0], a[1][0], b[pt][2]);                      // W0.X2
+      __builtin_amdgcn_sched_barrier(0);
+      bl(tn, pt, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(pt, a[0][1], a[1][1], b[pt][0]);                      // W1.X0
+      __builtin_amdgcn_sched_barrier(0);
+      if (pt == 1) wl(a, 1, t + kWD);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(pt, a[0][0], a[1][0], b[pt][1]);                      // W0.X1
+      __builtin_amdgcn_sched_barrier(0);
+      bl(tn, pt, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(pt, a[0][0], a[1][0], b[pt][0]);                      // W0.X0
+      __builtin_amdgcn_sched_barrier(0);
+      bl(tn, pt, 0);
+      if (pt == 1) wl(a, 0, t + kWD);   // packs carry kWD zero steps
       __builtin_amdgcn_sched_barrier(0);
     }
-    load_w(a, rs, voff, t + kWD);   // packs carry kWD zero steps
-    __builtin_amdgcn_sched_barrier(0);
   };
   int t = 0;
 #pragma unroll 1
@@ -218,7 +233,36 @@ __device__ __forceinline__ void store_group(char* planes, int pstride, int g, in
 
 // producer wave pw (0..3), lane = pair column: gather + weights + PE planes of `tile`
 // into buffer nb (neural_points.py:788-799, point_aggregators.py:421-429, 775-804).
-__device__ __forceinline__ void gather(const X3Args& A, int64_t tile, int nb, char* lds, int pw, int lane,
+// The gather is split in three stages so its dependent loads travel across
+// barriers (the producers' barriers wait on LDS only): the sample row (stage
+// 0, tile start), then pidx / sample positions / dir row (stage 1, S1b), then
+// the point rows and everything computed from them (gather, during block1.2).
+struct GatherState {
+  int64_t row;
+  int pid;
+  float sw[3], sp[3];
+  int64_t dmap;
+  bool active;
+};
+
+__device__ __forceinline__ void gather_row(const X3Args& A, int64_t tile, int lane, GatherState& g) {
+  const int64_t v = tile * kXTS + (lane >> 3);
+  g.active = v < eff_n(A.s);
+  g.row = g.active ? sample_row(A.s, v) : 0;
+}
+
+__device__ __forceinline__ void gather_sample(const X3Args& A, int lane, GatherState& g) {
+  const int k = lane & 7, K = A.s.K;
+  g.pid = (g.active && k < K) ? A.s.pidx[g.row * K + k] : -1;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    g.sw[a] = g.active ? A.s.sample_w[g.row * 3 + a] : 0.f;
+    g.sp[a] = g.active ? A.s.sample_p[g.row * 3 + a] : 0.f;
+  }
+  g.dmap = A.s.dir_map ? (int64_t)A.s.dir_map[g.row] : g.row;
+}
+
+__device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, int nb, char* lds, int pw, int lane,
                                        float (&dr6)[6]) {
   float Rw[9];
 #pragma unroll
@@ -232,26 +276,20 @@ __device__ __forceinline__ void gather(const X3Args& A, int64_t tile, int nb, ch
   }
   const int j = lane >> 3, k = lane & 7;
   const int K = A.s.K;
-  const int64_t n = eff_n(A.s);
-  const int64_t v = tile * kXTS + j;
-  const bool active = v < n;
-  const int64_t row = active ? sample_row(A.s, v) : 0;
-  int64_t prow = -1;
-  bool valid = false;
-  if (active && k < K) {
-    const int pid = A.s.pidx[row * K + k];
-    valid = pid >= 0;
-    prow = valid ? pid : 0;   // torch.clamp(sample_pidx, min=0)
-  }
-  float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
-  if (active) {
-    const int64_t drow = dir_row(A.s, row);
+  const bool active = g.active;
+  const int64_t row = g.row;
+  const bool valid = g.pid >= 0;
+  const int64_t prow = valid ? g.pid : (active && k < K ? 0 : -1);   // torch.clamp(sample_pidx, min=0)
+  float sw[3], sp[3], vd[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      sw[a] = A.s.sample_w[row * 3 + a];
-      sp[a] = A.s.sample_p[row * 3 + a];
-      vd[a] = A.s.dirs[drow * 3 + a];
-    }
+  for (int a = 0; a < 3; ++a) {
+    sw[a] = g.sw[a];
+    sp[a] = g.sp[a];
+  }
+  if (active) {
+    const int64_t drow = g.dmap / A.s.dir_div;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) vd[a] = A.s.dirs[drow * 3 + a];
   }
   float pw3[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, col[3] = {0.f, 0.f, 0.f}, pdir[3] = {0.f, 0.f, 0.f};
   float cf = 1.f;
@@ -308,15 +346,15 @@ __device__ __forceinline__ void gather(const X3Args& A, int64_t tile, int nb, ch
 
 // 5-band PE of the rotated 6-d distance of this lane's pair -> rows 2e (sin),
 // 2e + 1 (cos), e = 5 ch + f, of the PE planes; producer wave pw takes e = pw (mod 4)
-__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6]) {
-  if (pw == 0) {   // rows 60..63: the 4th 16-k step reads them
+__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6], int e_lo, int e_hi) {
+  if (pw == 0 && e_lo == 0) {   // rows 60..63: the 4th 16-k step reads them
     char* pz = lds + kOffPE + (7 * kXT + lane) * 16 + 8;
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
   }
   if (!(PNR_ABLATE & 2)) {
 #pragma unroll 1
-    for (int e = pw; e < 30; e += 4) {
+    for (int e = e_lo + pw; e < e_hi; e += 4) {
       const int ch = e / 5, f = e - 5 * ch;
       float dc = dr6[0];
       dc = ch == 1 ? dr6[1] : dc;
@@ -337,8 +375,37 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
   }
 }
 
-// Consumer: block1.0 (distance half) .. block3.2, alpha and K sums of one tile
-// per iteration.  Barriers S1..S8 pair with the producer loop's.
+// Tile schedule (8 barriers per tile; consumers C = waves 0..3, producers P = 4..7):
+//   C: acc = W1b . PE           | P: park P1(tile), finalize alpha of the previous tile
+//   S1  C: acc += P1 (parked)   |
+//   S1b C: store act1, bias     |
+//   S2  C: block1.2             | P: gather(next)
+//   S3  C: store act2, extras   | P: fetch P1(next) (registers), PE planes part 1
+//   S4  C: block3.0             |
+//   S5  C: store act3, bias     | P: PE planes part 2
+//   S6  C: block3.2, K sums, alpha partials
+//   S7
+// The consumers never wait on a producer phase shorter than the layer it
+// overlaps; the P1 rows travel during block3.0 / block3.2.
+#define X3_SYNC() __syncthreads()
+
+__device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int buf, int64_t tile, int lane) {
+  if (PNR_ABLATE & 4) return;
+  const int64_t n = eff_n(A.s);
+  const int j = lane >> 3, k = lane & 7;
+  const float* apart = reinterpret_cast<const float*>(lds + kOffAp);
+  const float* wtL = reinterpret_cast<const float*>(lds + kOffWt) + buf * kXT;
+  const int* sflag = reinterpret_cast<const int*>(lds + kOffSf) + buf * kXTS;
+  const float pa = apart[lane] + apart[kXT + lane] + apart[2 * kXT + lane] + apart[3 * kXT + lane] + A.w.ba[0];
+  const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
+  const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
+  const int64_t vo = tile * kXTS + j;
+  if (k == 0 && vo < n) {
+    A.vmask[vo] = sflag[j];
+    if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
+  }
+}
+
 __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wid, int lane) {
   const int c = lane & 31, h = lane >> 5;
   const int64_t n = eff_n(A.s);
@@ -355,7 +422,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
   WRing wr;
   f32x16 acc[4];
   prime(wr, r1, voff);
-  __syncthreads();   // S0: the first tile's inputs and P1 are in LDS
+  X3_SYNC();   // S0: the first tile's PE planes, extras and weights are in LDS
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][0] = wall_clock64();
 #endif
@@ -363,7 +430,14 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     const int buf = it & 1;
     X3_TR(0, 0);
-    // acc = P1 (block1.0 point half + bias) from LDS
+    // ------------------------------------------------------------ block1.0 = P1 + W1[:, 224:] . PE_5
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    layer(acc, wr, r1, voff, PE, kPlaneP, 4, lane);
+    prime(wr, r2, voff);
+    X3_TR(0, 1);
+    X3_SYNC();   // S1: P1 parked, PE planes consumed
+    X3_TR(0, 2);
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
@@ -372,17 +446,12 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         for (int q = 0; q < 4; ++q) {
           const float4 v4 = *reinterpret_cast<const float4*>(P1L + (32 * pt + c) * kP1Pitch + 32 * (T0 + T) + 8 * q +
                                                              4 * h);
-          acc[2 * pt + T][4 * q] = v4.x;
-          acc[2 * pt + T][4 * q + 1] = v4.y;
-          acc[2 * pt + T][4 * q + 2] = v4.z;
-          acc[2 * pt + T][4 * q + 3] = v4.w;
+          acc[2 * pt + T][4 * q] += v4.x;
+          acc[2 * pt + T][4 * q + 1] += v4.y;
+          acc[2 * pt + T][4 * q + 2] += v4.z;
+          acc[2 * pt + T][4 * q + 3] += v4.w;
         }
-    // ------------------------------------------------------------ block1.0, distance half
-    X3_TR(0, 1);
-    layer(acc, wr, r1, voff, PE, kPlaneP, 4, lane);
-    prime(wr, r2, voff);
-    X3_TR(0, 2);
-    __syncthreads();   // S1: PE planes and the parked P1 consumed
+    X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
     X3_TR(0, 3);
     store_act(acc, XP, neg, lane, T0);
     if (wid == 0) {
@@ -396,13 +465,13 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
     X3_TR(0, 4);
-    __syncthreads();   // S2
+    X3_SYNC();   // S2
     X3_TR(0, 5);
     // ------------------------------------------------------------ block1.2
     layer(acc, wr, r2, voff, XP, kPlaneX, 17, lane);
     prime(wr, r3, voff);
     X3_TR(0, 6);
-    __syncthreads();   // S3
+    X3_SYNC();   // S3
     X3_TR(0, 7);
     store_act(acc, XP, neg, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
@@ -414,13 +483,13 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
-    __syncthreads();   // S4
+    X3_SYNC();   // S4
     X3_TR(0, 8);
     // ------------------------------------------------------------ block3.0
     layer(acc, wr, r3, voff, XP, kPlaneX, 17, lane);
     prime(wr, r4, voff);
     X3_TR(0, 9);
-    __syncthreads();   // S5
+    X3_SYNC();   // S5
     X3_TR(0, 10);
     store_act(acc, XP, neg, lane, T0);
     if (wid == 0) {
@@ -431,9 +500,9 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
-    __syncthreads();   // S6
+    X3_SYNC();   // S6
     X3_TR(0, 11);
-    // ------------------------------------------------------------ block3.2, alpha, K sums
+    // ------------------------------------------------------------ block3.2, alpha partials, K sums
     layer(acc, wr, r4, voff, XP, kPlaneX, 17, lane);
     prime(wr, r1, voff);   // the next tile's block1.0
     X3_TR(0, 12);
@@ -448,7 +517,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         const float wtp = wtL[32 * pt + c];
         const int sj = (32 * pt + c) >> 3;
         const int64_t vo = tile * kXTS + sj;
-        const bool wr = vo < n && sflag[sj];
+        const bool wrt = vo < n && sflag[sj];
 #pragma unroll
         for (int T = 0; T < 2; ++T) {
           float v[16];
@@ -481,7 +550,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                 float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xf, 0xf, false));
             w2[q] = (b0 ? w4[q + 2] : w4[q]) + recv;
           }
-          if (wr)
+          if (wrt)
             __builtin_nontemporal_store(
                 (f32x2n){w2[0], w2[1]},
                 reinterpret_cast<f32x2n*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h));
@@ -494,23 +563,8 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
       }
     }
     X3_TR(0, 13);
-    __syncthreads();   // S7: layer-input planes free (the producers park the next P1 there)
+    X3_SYNC();   // S7: layer-input planes free (the producers park the next P1 there), alpha partials ready
     X3_TR(0, 14);
-    if (wid == 0 && !(PNR_ABLATE & 4)) {
-      const int j = lane >> 3, k = lane & 7;
-      const float* wtL = reinterpret_cast<const float*>(lds + kOffWt) + buf * kXT;
-      const int* sflag = reinterpret_cast<const int*>(lds + kOffSf) + buf * kXTS;
-      const float pa = apart[lane] + apart[kXT + lane] + apart[2 * kXT + lane] + apart[3 * kXT + lane] + A.w.ba[0];
-      const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
-      const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
-      const int64_t vo = tile * kXTS + j;
-      if (k == 0 && vo < n) {
-        A.vmask[vo] = sflag[j];
-        if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
-      }
-    }
-    __syncthreads();   // S8: next P1 parked
-    X3_TR(0, 15);
   }
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][1] = wall_clock64();
@@ -519,65 +573,83 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 
 // Producer wave pw: P1 rows 16 pw .. 16 pw + 15 of a tile (1 KB each, one
 // coalesced float4 per lane per row) into registers.
-__device__ __forceinline__ void fetch_p1(float4 (&r)[16], const X3Args& A, const int* prow, int pw, int lane) {
+__device__ __forceinline__ unsigned fetch_p1(f32x4n (&r)[16], const X3Args& A, const int* prow, int pw, int lane) {
+  // branch-free: every lane loads (row 0 for an empty slot) and zeroes afterwards,
+  // so the 16 loads issue back to back; streamed once -> non-temporal (keeps the
+  // weight packs in L2)
+  int64_t rows[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int pr = prow[16 * pw + i];
-    const int64_t p1r = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
-    // streamed once: non-temporal, so the rows do not evict the weight packs from L2
-    r[i] = (p1r >= 0 && !(PNR_ABLATE & 1))
-               ? __builtin_bit_cast(float4, __builtin_nontemporal_load(
-                                                reinterpret_cast<const f32x4n*>(A.p1 + p1r * kHid) + lane))
-               : make_float4(0.f, 0.f, 0.f, 0.f);
+    rows[i] = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
+  }
+  unsigned empty = 0;   // bit i: row i has no point (zeroed when parked, so the loads are not waited on here)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    r[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4n*>(A.p1 + (rows[i] < 0 ? 0 : rows[i]) * kHid) +
+                                      lane);
+    if (rows[i] < 0 || (PNR_ABLATE & 1)) empty |= 1u << i;
+  }
+  return empty;
+}
+
+__device__ __forceinline__ void park_p1(const f32x4n (&r)[16], unsigned empty, char* lds, int pw, int lane) {
+  float* P1L = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f32x4n z = {0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4n*>(P1L + (16 * pw + i) * kP1Pitch + 4 * lane) = ((empty >> i) & 1) ? z : r[i];
   }
 }
 
-__device__ __forceinline__ void park_p1(const float4 (&r)[16], char* lds, int pw, int lane) {
-  float* P1L = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(P1L + (16 * pw + i) * kP1Pitch + 4 * lane) = r[i];
-}
-
-// Producer: while the consumers run tile i, prepare tile i + 1 (gather, PE
-// planes, extras, weights) during block1.2 and fetch its P1 rows during
-// block3.0 / block3.2; park them in LDS once the consumers are done with the
-// layer-input planes.
 __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw, int lane) {
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kXTS);
-  float4 p1r[16];
+#if PNR_X3_PRIO
+  __builtin_amdgcn_s_setprio(PNR_X3_PRIO);   // producer issue priority over the MFMA stream
+#endif
+  f32x4n p1r[16];
+  unsigned p1e = 0;
   float dr6[6];
-  gather(A, blockIdx.x, 0, lds, pw, lane, dr6);
-  pe_planes(lds, pw, lane, dr6);
-  __syncthreads();   // (prologue) prow of the first tile visible to all producers
-  fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr), pw, lane);
-  park_p1(p1r, lds, pw, lane);
-  __syncthreads();   // S0
+  GatherState g;
+  gather_row(A, blockIdx.x, lane, g);
+  gather_sample(A, lane, g);
+  gather(A, g, 0, lds, pw, lane, dr6);
+  pe_planes(lds, pw, lane, dr6, 0, 30);
+  X3_SYNC();   // P0: prow of the first tile visible to all producers
+  p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr), pw, lane);
+  X3_SYNC();   // S0
   int it = 0;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     const int nbuf = (it & 1) ^ 1;
     const int64_t next = tile + gridDim.x;
     X3_TR(1, 0);
-    __syncthreads();   // S1
-    __syncthreads();   // S2
-    // during block1.2: gather (nbuf's arrays are free: their last reader was the previous tile's finalize)
-    if (!(PNR_ABLATE & 256)) gather(A, next, nbuf, lds, pw, lane, dr6);   // (256: timing only, no producer work)
+    park_p1(p1r, p1e, lds, pw, lane);   // the layer-input planes are free since the last S7
+    gather_row(A, next, lane, g);
     X3_TR(1, 1);
-    __syncthreads();   // S3: the next tile's point rows are in LDS
-    if (!(PNR_ABLATE & 256)) fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr) + nbuf * kXT, pw, lane);
+    X3_SYNC();   // S1
+    // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
+    if (pw == 0 && it > 0) finalize_alpha(A, lds, nbuf, tile - gridDim.x, lane);
+    X3_SYNC();   // S1b
+    gather_sample(A, lane, g);
+    X3_SYNC();   // S2
     X3_TR(1, 2);
-    __syncthreads();   // S4
-    if (!(PNR_ABLATE & 256)) pe_planes(lds, pw, lane, dr6);   // during block3.0 (the PE planes were freed at S1)
+    // during block1.2: gather (nbuf's arrays are free: their last reader was the previous finalize)
+    if (!(PNR_ABLATE & 256)) gather(A, g, nbuf, lds, pw, lane, dr6);
     X3_TR(1, 3);
-    __syncthreads();   // S5
-    __syncthreads();   // S6
-    __syncthreads();   // S7
+    X3_SYNC();   // S3: the next tile's point rows are in LDS
+    // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
+    if (!(PNR_ABLATE & 256)) p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr) + nbuf * kXT, pw, lane);
     X3_TR(1, 4);
-    park_p1(p1r, lds, pw, lane);
+    X3_SYNC();   // S4
+    if (!(PNR_ABLATE & 256)) pe_planes(lds, pw, lane, dr6, 0, 16);   // during block3.0 (PE planes free since S1)
+    X3_SYNC();   // S5
     X3_TR(1, 5);
-    __syncthreads();   // S8
-    X3_TR(1, 6);
+    X3_SYNC();   // S6
+    if (!(PNR_ABLATE & 256)) pe_planes(lds, pw, lane, dr6, 16, 30);   // during block3.2
+    X3_SYNC();   // S7
   }
+  if (pw == 0 && it > 0) finalize_alpha(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
 }
 
 __global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) {
@@ -586,7 +658,7 @@ __global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) {
   // alpha_branch.0 weights for the consumers' tail
   if (threadIdx.x < kHid) reinterpret_cast<float*>(lds + kOffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
   if (wid < 4) {
-    __syncthreads();   // (prologue)
+    X3_SYNC();   // P0
     consumer_loop(A, lds, wid, lane);
   } else {
     producer_loop(A, lds, wid - 4, lane);

@@ -15,14 +15,14 @@ from scenes import oracle_points, scene
 pytestmark = pytest.mark.gpu
 
 
-def _renderer(sc, cuda, params):
+def _renderer(sc, cuda, params, precision="fp32"):
     from pointnerf_amd.aggregator import PointAggregator
     from pointnerf_amd.renderer import NeuralPoints, NeuralPointsRayMarching
     agg = PointAggregator(sc["opt"]).to(cuda)
     agg.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
                        torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]))
-    return NeuralPointsRayMarching(sc["opt"], np_, agg.eval())
+    return NeuralPointsRayMarching(sc["opt"], np_, agg.eval(), precision=precision)
 
 
 def _render(m, sc, cuda, rd=None):
@@ -34,10 +34,15 @@ def _render(m, sc, cuda, rd=None):
     return [t.cpu() for t in out]
 
 
-def test_full_size_properties(cuda):
+# fp32: the reference arithmetic; fp32x3: the fp32-accurate split-bf16 path (same tolerances)
+PRECISIONS = ["fp32", "fp32x3"]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_full_size_properties(cuda, precision):
     sc = scene(2_000_000, H=800, W=800, theta=-40.0, default_conf=0.15)
     params = formula_params(salt=0.9)
-    m = _renderer(sc, cuda, params)
+    m = _renderer(sc, cuda, params, precision)
     a = _render(m, sc, cuda)
     b = _render(m, sc, cuda)
     for x, y in zip(a, b):
@@ -57,11 +62,12 @@ def test_full_size_properties(cuda):
     np.testing.assert_allclose(a[1].numpy()[few], ref["coarse_point_opacity"], atol=2e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("SR,K", [(128, 1), (1, 8), (24, 3)])
-def test_sr_k_extremes_vs_oracle(cuda, SR, K):
+def test_sr_k_extremes_vs_oracle(cuda, SR, K, precision):
     sc = scene(20000, H=32, W=32, theta=80.0, SR=SR, K=K)
     params = formula_params(salt=0.25)
-    got = _render(_renderer(sc, cuda, params), sc, cuda)
+    got = _render(_renderer(sc, cuda, params, precision), sc, cuda)
     ref = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"])
     assert np.array_equal(got[3].numpy(), ref["ray_mask"])
     assert ref["ray_mask"].sum() > 50
@@ -69,12 +75,13 @@ def test_sr_k_extremes_vs_oracle(cuda, SR, K):
     np.testing.assert_allclose(got[1].numpy(), ref["coarse_point_opacity"], atol=2e-4, rtol=1e-4)
 
 
-def test_voxel_capacity_overflow_matches_oracle(cuda):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_voxel_capacity_overflow_matches_oracle(cuda, precision):
     """P smaller than the densest voxel: both sides drop the same (highest-index)
     points -- the deterministic replacement of the reference's curand reservoir."""
     sc = scene(20000, H=32, W=32, theta=20.0, P=2)
     params = formula_params(salt=0.55)
-    m = _renderer(sc, cuda, params)
+    m = _renderer(sc, cuda, params, precision)
     got = _render(m, sc, cuda)
     st = m.neural_points.querier.grid.stats()
     g = O.grid_build(sc["opt"], sc["xyz"])
@@ -87,8 +94,9 @@ def test_voxel_capacity_overflow_matches_oracle(cuda):
     np.testing.assert_allclose(got[0].numpy(), ref["coarse_raycolor"], atol=2e-4, rtol=1e-4)
 
 
-def test_empty_ray_batch(cuda):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_empty_ray_batch(cuda, precision):
     sc = scene(5000, H=4, W=4)
-    m = _renderer(sc, cuda, formula_params())
+    m = _renderer(sc, cuda, formula_params(), precision)
     out = _render(m, sc, cuda, sc["raydir"][:0])
     assert out[0].shape == (0, 128) and out[3].shape == (0,)

@@ -41,8 +41,9 @@ def _setup(sc, cuda, params=None, seed=0):
     return agg.eval(), np_
 
 
-def _both(agg, np_, sc, cuda):
-    """fp32 and fp32x3 features on one query -> (f32 [Sv,129], x3 [Sv,129])."""
+def _both(agg, np_, sc, cuda, used=False):
+    """fp32 and fp32x3 features on one query -> (f32 [Sv,129], x3 [Sv,129]);
+    used: P1 only for the referenced points (the training-batch layout)."""
     from pointnerf_amd import _lib as L
     cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
     rd = torch.from_numpy(sc["raydir"]).to(cuda).contiguous()
@@ -53,16 +54,23 @@ def _both(agg, np_, sc, cuda):
                   bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(), bufs.fill_rs.data_ptr(),
                   sc["opt"].SR, sc["opt"].K)
     pts, _keep = np_.tables(cp, cr)
+    n_p1 = pts.n
+    if used:
+        from pointnerf_amd.train import used_points
+        u = used_points(bufs.pidx[:cnt["S_filled"] * sc["opt"].K], pts.n)
+        pts.used, pts.n_used, pts.used_map = u[0].data_ptr(), u[0].numel(), u[1].data_ptr()
+        n_p1 = u[0].numel()
     mlp, _k1 = agg.packed()
     mlpx, _k2 = agg.packed_x3()
     outs = []
     for fn, extra in (("pnr_aggregate_fwd", ()), ("pnr_aggregate_fwd_x3", (L.ctypes.byref(mlpx),))):
         f = torch.zeros((Sv, 129), device=cuda)
-        scr = L.aggregate_scratch(Sv, pts.n, cuda)
+        scr = L.aggregate_scratch(Sv, n_p1, cuda)
         L.check(getattr(L.lib(), fn)(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), *extra, L.ptr(f),
                                      None, None, L.ptr(scr), scr.numel() * 4, L.stream_ptr(cuda)), fn)
         outs.append(f)
     torch.cuda.synchronize()
+    _keep_used = u if used else None   # noqa: F841 (keeps the used tables alive until here)
     return outs[0].cpu().numpy(), outs[1].cpu().numpy()
 
 
@@ -79,6 +87,16 @@ def _oracle_features(sc, params, f64=False):
                                     gth["sample_pnt_mask"], q["sample_loc"], q["sample_loc_w"],
                                     q["sample_ray_dirs"])
     return np.asarray(ref)[rv]
+
+
+def test_x3_used_subset_equals_full(cuda):
+    """P1 for the referenced points only (pts.used, the training layout) gives
+    bit-identical features to P1 for every point."""
+    sc = scene(20000, H=40, W=40, default_conf=None)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.4))
+    _, a = _both(agg, np_, sc, cuda)
+    _, b = _both(agg, np_, sc, cuda, used=True)
+    assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("salt", [0.3, None])

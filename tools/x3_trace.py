@@ -29,8 +29,9 @@ def main():
     assert fn(buf, 2 * 64 * 16) == 0
     t = np.frombuffer(buf, dtype=np.uint64).reshape(2, 64, 16).astype(np.int64)
     c = t[0, 8:60]
-    names = ["p1 read", "layer1 issue", "S1 wait", "store1", "S2 wait", "layer2 issue", "S3 wait", "store2+S4",
-             "layer3 issue", "S5 wait", "store3+S6", "layer4 issue", "tail", "S7 wait", "finalize+S8"]
+    names = ["layer1", "S1 wait", "P1 add+S1b", "store1", "S2 wait", "layer2", "S3 wait", "store2+S4", "layer3",
+             "S5 wait", "store3+S6", "layer4", "tail", "S7 wait"]
+    c = c[:, :15]
     d = np.diff(c, axis=1)
     tile = c[1:, 0] - c[:-1, 0]
     print("consumer wave 0, cycles per tile (median over tiles 8..59): total", int(np.median(tile)))
@@ -47,8 +48,8 @@ def main():
     order = np.argsort(-dur)[:8]
     print("slowest blocks:", [(int(i), round(float(dur[i]))) for i in order])
     p = t[1, 8:60]
-    pn = ["gather", "S1 wait + pe", "S2 wait", "fetch..S7 wait", "park", "S8 wait"]
-    dp = np.diff(p[:, :7], axis=1)
+    pn = ["park+finalize", "S1..S2 wait", "gather", "S3 wait+fetch", "S4+pe1+S5"]
+    dp = np.diff(p[:, :6], axis=1)
     print("producer wave 4")
     for i, nme in enumerate(pn):
         print(f"  {nme:14s} {int(np.median(dp[:, i])):7d}")
