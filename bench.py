@@ -34,6 +34,7 @@ FLOP_PER_SAMPLE = 137_216   # colour-branch GEMM FLOPs per valid sample
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
+PMC_FILES = {"fp32": "r01_fp32_pmc_aggregate.json", "fp32x3": "r01_pmc_aggregate_x3.json"}
 
 
 def parse():
@@ -330,9 +331,11 @@ def main():
     total_samples = H * W * SR * world * args.steps      # every rank renders one frame's worth
     value = total_samples / t_max / 1e6
     if rank == 0:
+        # HBM bytes per aggregate launch from the committed PMC passes of this same command
+        # (tools/prof_bench.sh -> tools/profile_summary.py; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r01_pmc_aggregate.json")
-        if os.path.exists(pmc):
+        pmc = os.path.join(ROOT, "profiles", PMC_FILES.get(args.dtype, ""))
+        if args.dtype in PMC_FILES and os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
@@ -341,16 +344,6 @@ def main():
         # fp32x3: every fp32 MAC costs 6 bf16 MFMA products -> fp32-equivalent ceiling = bf16 dense / 6
         peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "fp32x3": round(BF16_MFMA_PEAK_TFLOPS / 6, 1),
                 "bf16": BF16_MFMA_PEAK_TFLOPS}[args.dtype]
-        pmc_x3 = os.path.join(ROOT, "profiles", "r01_pmc_aggregate_x3.json")
-        if args.dtype == "fp32x3":
-            traffic = None
-            if os.path.exists(pmc_x3):
-                try:
-                    traffic = json.load(open(pmc_x3)).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
-        elif args.dtype != "fp32":
-            traffic = None   # the committed PMC summaries are for the fp32 / fp32x3 kernels
         out = {
             "metric": "Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref",
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,

@@ -14,11 +14,16 @@ import os
 import shutil
 import sys
 
-AGG = ("k_point_pre", "k_pairs", "k_color")
+AGG_BY_DTYPE = {"fp32": ("k_point_pre", "k_pairs", "k_color"),
+                "fp32x3": ("k_point_pre", "k_pairs_x3", "k_color"),
+                "bf16": ("k_point_pre_b", "k_pairs_b", "k_color_b")}
+MOPS = {"fp32": "SQ_INSTS_VALU_MFMA_MOPS_F32", "fp32x3": "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+        "bf16": "SQ_INSTS_VALU_MFMA_MOPS_BF16"}
+AGG = AGG_BY_DTYPE["fp32"]
 
 
 def short(name):
-    n = name.split("(")[0].replace("pnr::", "").replace("void ", "")
+    n = name.replace("(anonymous namespace)::", "").split("(")[0].replace("pnr::", "").replace("void ", "")
     return n.split("<")[0]
 
 
@@ -34,7 +39,10 @@ def per_kernel(path, counters):
 
 
 def main():
+    global AGG
     src, tag = sys.argv[1], sys.argv[2]
+    dtype = sys.argv[3] if len(sys.argv) > 3 else "fp32"
+    AGG = AGG_BY_DTYPE[dtype]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -45,8 +53,8 @@ def main():
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), {"FETCH_SIZE"})
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), {"WRITE_SIZE"})
     mfma = per_kernel(os.path.join(src, "mfma", "run_counter_collection.csv"),
-                      {"SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU_MFMA_MOPS_F32"})
-    out = {"source": "tools/prof_bench.sh -> tools/profile_summary.py", "kernels": {}}
+                      {"SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", MOPS[dtype]})
+    out = {"source": "tools/prof_bench.sh -> tools/profile_summary.py", "dtype": dtype, "kernels": {}}
     tot_bytes, tot_ns = 0.0, 0.0
     for k in AGG:
         avg_ns = float(stats[k]["AverageNs"])
@@ -64,7 +72,8 @@ def main():
     out["hbm_bytes_per_launch"] = tot_bytes
     out["avg_launch_ms_rocprof"] = tot_ns / 1e6
     out["avg_launch_ms_bench_events"] = bench["roofline"]["avg_launch_ms"]
-    json.dump(out, open(os.path.join(prof, f"{tag}_pmc_aggregate.json"), "w"), indent=1)
+    name = f"{tag}_pmc_aggregate.json" if dtype == "fp32" else f"{tag}_pmc_aggregate_{dtype.replace('fp32', '')}.json"
+    json.dump(out, open(os.path.join(prof, name), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
