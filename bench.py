@@ -34,7 +34,8 @@ FLOP_PER_SAMPLE = 137_216   # colour-branch GEMM FLOPs per valid sample
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
-PMC_FILES = {"fp32": "r01_fp32_pmc_aggregate.json", "fp32x3": "r01_pmc_aggregate_x3.json"}
+PMC_FILES = {"fp32": "r01_fp32_pmc_aggregate.json", "fp32x3": "r01_pmc_aggregate_x3.json",
+             "fp32h2": "r01_pmc_aggregate_h2.json"}
 
 
 def parse():
@@ -57,10 +58,12 @@ def parse():
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
     ap.add_argument("--train-rays", type=int, default=3600, help="rays per train step (random_sample_size 60^2)")
-    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "bf16"), default="fp32x3",
-                    help="MLP arithmetic: fp32x3 (headline) = the reference's fp32 GEMMs as exact 3-way bf16 splits "
+    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "fp32h2", "bf16"), default="fp32h2",
+                    help="MLP arithmetic: fp32h2 (headline, see below); fp32x3 = the reference's fp32 GEMMs as exact 3-way bf16 splits "
                          "(6 cross products) on v_mfma_f32_32x32x16_bf16, fp32-accurate (error vs an fp64 oracle "
-                         "equal to native fp32's); fp32 = native v_mfma_f32_32x32x2_f32; bf16 = bf16 operands "
+                         "equal to native fp32's); fp32h2 = the same GEMMs as 2-way f16 splits (3 products) on "
+                         "v_mfma_f32_32x32x16_f16, fp32-accurate; fp32 = native v_mfma_f32_32x32x2_f32; "
+                         "bf16 = bf16 operands "
                          "(SURVEY config c5)")
     return ap.parse_args()
 
@@ -319,6 +322,8 @@ def main():
     else:
         t_max = t_local
     torch.cuda.synchronize()
+    if args.dtype == "fp32h2" and not agg.h2_range_ok():
+        raise RuntimeError("fp32h2: an activation left the f16 range; the renders are invalid")
     # per-stage times from HIP events recorded on the launch stream
     per = {}
     for name, a, b in stage.get("_ev", []):
@@ -342,18 +347,22 @@ def main():
                 traffic = None
         achieved = flops_per_launch / avg_agg_s / 1e12 if avg_agg_s > 0 else 0.0
         # fp32x3: every fp32 MAC costs 6 bf16 MFMA products -> fp32-equivalent ceiling = bf16 dense / 6
+        # fp32h2: 3 f16 MFMA products per fp32 MAC -> f16 dense (= bf16 dense) / 3
         peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "fp32x3": round(BF16_MFMA_PEAK_TFLOPS / 6, 1),
-                "bf16": BF16_MFMA_PEAK_TFLOPS}[args.dtype]
+                "fp32h2": round(BF16_MFMA_PEAK_TFLOPS / 3, 1), "bf16": BF16_MFMA_PEAK_TFLOPS}[args.dtype]
         out = {
             "metric": "Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref",
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if args.dtype in ("fp32", "fp32x3") else args.dtype,
+            "dtype": "fp32" if args.dtype in ("fp32", "fp32x3", "fp32h2") else args.dtype,
             "arith": {"fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
                       "fp32x3": "fp32-accurate: exact 3-way bf16 split of each fp32 operand, 6 cross products on "
                                 "v_mfma_f32_32x32x16_bf16, fp32 accumulation (error vs an fp64 oracle = native "
                                 "fp32's, tests/test_gpu_x3.py)",
+                      "fp32h2": "fp32-accurate: 2-way f16 split of each fp32 operand (x = xh + 2^-11 xl), 3 "
+                                "products on v_mfma_f32_32x32x16_f16, fp32 accumulation (error vs an fp64 oracle "
+                                "~ native fp32's, tests/test_gpu_x3.py)",
                       "bf16": "bf16 operands, fp32 accumulation"}[args.dtype],
             "data": "synthetic (seeded lego-like 2M-point cloud, random-init lego viewmlp weights)",
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
@@ -365,11 +374,14 @@ def main():
                              "fp32": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
                              "fp32x3": "pnr_aggregate_fwd_x3 = k_point_pre + k_pairs_x3 (bf16x3 split, "
                                        "v_mfma_f32_32x32x16_bf16) + k_color",
+                             "fp32h2": "pnr_aggregate_fwd_h2 = k_point_pre + k_pairs_h2 (f16x2 split, "
+                                       "v_mfma_f32_32x32x16_f16) + k_color",
                              "bf16": "pnr_aggregate_fwd_bf16 = k_point_pre_b + k_pairs_b + k_color_b "
                                      "(v_mfma_f32_32x32x16_bf16)"}[args.dtype],
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                          "peak_note": {"fp32": "fp32 MFMA dense peak",
                                        "fp32x3": "fp32-equivalent: bf16 MFMA dense peak / 6 products per fp32 MAC",
+                                       "fp32h2": "fp32-equivalent: f16 MFMA dense peak / 3 products per fp32 MAC",
                                        "bf16": "bf16 MFMA dense peak"}[args.dtype],
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},

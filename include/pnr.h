@@ -289,6 +289,31 @@ int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s, const pnr_
                          float* out_feat, float* out_weight, float* out_conf, void* scratch,
                          size_t scratch_bytes, void* stream);
 
+/* fp32-accurate aggregation on f16 MFMA (same contract and scratch as
+ * pnr_aggregate_fwd; replaces the same reference call,
+ * point_aggregators.py:729-816 / 488-646).  Each fp32 operand is split into
+ * two f16 terms, x = xh + 2^-11 xl (xh = f16(x), xl = f16((x - xh) 2^11),
+ * round to nearest even), and block1.0's distance half, block1.2, block3.0 and
+ * block3.2 run as three products, 2^-11 (2^11 Wh.Xh + Wh.Xl + Wl.Xh), on
+ * v_mfma_f32_32x32x16_f16 with fp32 accumulation: the split and the dropped
+ * Wl.Xl term are each below one fp32 rounding of the product.  Packs from
+ * pointnerf_amd.aggregator.frag_pack_h2: layer weights pre-scaled by 2^-s
+ * (|W 2^-s| < 16 so 2^11 Wh stays in f16), planes [t][T][Wh, Wl][lane][8],
+ * scale[l] = 2^(s_l - 11).  Activations must stay inside the f16 range
+ * (|x| < 65504): a launch where one does not sets *range_flag = 1 (device
+ * int, caller-owned, may be NULL) and its outputs are not valid. */
+typedef struct {
+  const void* w1bh;   /* block1.0 columns 224..283 */
+  const void* w2h;    /* block1.2 + bias           */
+  const void* w3h;    /* block3.0 + bias           */
+  const void* w4h;    /* block3.2 + bias           */
+  float scale[4];
+  int32_t* range_flag;
+} pnr_mlp_h2;
+int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_h2* wh,
+                         float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                         size_t scratch_bytes, void* stream);
+
 /* PointAggregator.forward signature (pre-gathered tensors): pts tables are the
  * gathered [rows*K, C] tensors, s->pidx must be NULL (pair row = row*K + k),
  * pts->pers required, validity from pair_mask[rows*K] (sample_pnt_mask). */

@@ -101,6 +101,11 @@ class MlpX3(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("w1bx", "w2x", "w3x", "w4x")]
 
 
+class MlpH2(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w1bh", "w2h", "w3h", "w4h")] + [("scale", c_float * 4),
+                                                                       ("range_flag", c_void_p)]
+
+
 class MlpBwd(ctypes.Structure):
     _fields_ = [("w4t", c_void_p), ("w3t", c_void_p), ("w2t", c_void_p), ("w3e", c_void_p)]
 
@@ -124,6 +129,8 @@ SIGNATURES = {
     "pnr_aggregate_fwd": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpX3), c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_h2": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpH2), c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -137,6 +138,47 @@ def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Ten
     return F.view(-1)
 
 
+H2_PAD = X3_PAD   # same weight ring depth in k_pairs_h2
+H2_WMAX = 16.0    # |W 2^-s| < 16, so 2^11 Wh (made in registers) stays inside f16
+
+
+def split2_f16(W: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp32 W -> f16 (Wh, Wl) with W ~= Wh + 2^-11 Wl: Wh = f16(W), Wl =
+    f16((W - Wh) 2^11), round-to-nearest-even (as splith in agg_common.h);
+    |W - Wh - 2^-11 Wl| <= 2^-24 |W| in the f16 normal range."""
+    W = W.float()
+    wh = W.to(torch.float16)
+    wl = ((W - wh.float()) * 2048.0).to(torch.float16)
+    return wh, wl
+
+
+def frag_pack_h2(W: torch.Tensor, bias: torch.Tensor | None = None) -> tuple[torch.Tensor, float]:
+    """Split-f16 A-operand packs for pnr_aggregate_fwd_h2 -> (pack, layer scale):
+    F[t][T][plane][lane][j] = plane of (2^-s W')[32T + (lane & 31)][16t + 8(lane >> 5) + j],
+    W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus H2_PAD zero ones, planes
+    (Wh, Wl) of split2_f16; s >= 0 the smallest power of two with
+    max|2^-s W'| < H2_WMAX; scale = 2^(s - 11) (the kernel's accumulator factor)."""
+    out_f, kin = W.shape
+    assert out_f % 32 == 0
+    cols = kin + (1 if bias is not None else 0)
+    tot = (cols + 15) // 16 + H2_PAD
+    NT = out_f // 32
+    Wp = torch.zeros((out_f, 16 * tot), dtype=torch.float32, device=W.device)
+    Wp[:, :kin] = W.float()
+    if bias is not None:
+        Wp[:, kin] = bias.float()
+    amax = float(Wp.abs().max()) if Wp.numel() else 0.0
+    if not np.isfinite(amax):
+        raise L.PnrError("frag_pack_h2: non-finite weight")
+    s = 0
+    while amax * 2.0 ** -s >= H2_WMAX:
+        s += 1
+    Wp = (Wp * 2.0 ** -s).view(out_f, tot, 2, 8)                       # k = 16t + 8h + j
+    planes = torch.stack(split2_f16(Wp), 0)                             # [2][out][t][h][j]
+    F = planes.view(2, NT, 32, tot, 2, 8).permute(3, 1, 0, 4, 2, 5).contiguous()   # [t][T][pl][h][r][j]
+    return F.view(-1), 2.0 ** (s - 11)
+
+
 def frag_unpack(F: torch.Tensor, kin: int, out_f: int = 256) -> torch.Tensor:
     NT = out_f // 32
     tot = F.numel() // (NT * 64)
@@ -241,6 +283,32 @@ class PointAggregator(nn.Module):
         m = L.MlpX3(*(t[k].data_ptr() for k in ("w1bx", "w2x", "w3x", "w4x")))
         self._packedx3, self._packedx3_key = (m, t), key
         return self._packedx3
+
+    def packed_h2(self) -> tuple[L.MlpH2, dict]:
+        """Split-f16 packs of block1.0[:, 224:], block1.2, block3.0, block3.2
+        for pnr_aggregate_fwd_h2 (used with packed(); cached like it).  The
+        dict holds the device range flag (`range_flag`, int32[1])."""
+        ps = list(self.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if getattr(self, "_packedh2", None) is not None and key == self._packedh2_key:
+            return self._packedh2
+        with torch.no_grad():
+            b1, b3 = self.block1, self.block3
+            packs = [frag_pack_h2(b1[0].weight[:, 224:]), frag_pack_h2(b1[2].weight, b1[2].bias),
+                     frag_pack_h2(b3[0].weight, b3[0].bias), frag_pack_h2(b3[2].weight, b3[2].bias)]
+        flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
+        t = dict(w1bh=packs[0][0], w2h=packs[1][0], w3h=packs[2][0], w4h=packs[3][0], range_flag=flag)
+        m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
+                    (L.c_float * 4)(*(p[1] for p in packs)), flag.data_ptr())
+        self._packedh2, self._packedh2_key = (m, t), key
+        return self._packedh2
+
+    def h2_range_ok(self) -> bool:
+        """False when a pnr_aggregate_fwd_h2 launch since the packs were built
+        saw an activation outside the f16 range (its outputs are invalid).
+        Reads a device flag (synchronises)."""
+        pk = getattr(self, "_packedh2", None)
+        return pk is None or int(pk[1]["range_flag"].item()) == 0
 
     def set_rw2c(self, rw2c: torch.Tensor | None):
         """Uniform Rw2c of the point cloud (neural_points.py:289; eye by default)."""

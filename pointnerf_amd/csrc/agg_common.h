@@ -88,9 +88,50 @@ __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, cons
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
 }
 
-// aggregate_x3.hip: the pairs stage of pnr_aggregate_fwd_x3
-int launch_pairs_x3(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const pnr_mlp_x3& wx,
-                    const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
-                    float* out_conf, hipStream_t st);
+// ---------------------------------------------------------------------------
+// Exact-enough 2-way fp16 split for the fp32-accurate f16-MFMA GEMMs
+// (aggregate_x3.hip, pnr_aggregate_fwd_h2): x = xh + 2^-11 xl with
+// xh = f16(x), xl = f16((x - xh) * 2^11), round-to-nearest-even; x - xh is exact
+// in fp32 and |x - xh| <= 2^-12 |x| (normal range), so xl keeps the next 11
+// bits and the split error is <= 2^-24 |x|.  W . X = 2^-11 (Ws.Xh + Wh.Xl + Wl.Xh)
+// with Ws = 2^11 Wh (exact in f16: the weight pack is pre-scaled so |W| < 16):
+// three products on v_mfma_f32_32x32x16_f16 instead of six; the dropped term
+// 2^-22 Wl.Xl is <= 2^-24 |w x|.
+__device__ __forceinline__ void splith(float a, float b, unsigned& x0, unsigned& x1) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  const h2 hi = __builtin_convertvector(v, h2);
+  const f2 r = (v - __builtin_convertvector(hi, f2)) * 2048.f;
+  const h2 lo = __builtin_convertvector(r, h2);
+  x0 = __builtin_bit_cast(unsigned, hi);
+  x1 = __builtin_bit_cast(unsigned, lo);
+}
+
+__device__ __forceinline__ f32x16 mfma_f16(const uint4& a, const uint4& b, const f32x16& c) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+// 8 f16 values x 2^11 (exact: the packs keep |Wh| < 16)
+__device__ __forceinline__ uint4 f16x8_scale2048(const uint4& a) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  return __builtin_bit_cast(uint4, __builtin_bit_cast(h8, a) * (h8)((_Float16)2048.f));
+}
+
+// aggregate_x3.hip: the pairs stage of pnr_aggregate_fwd_x3 (H = false: 3-way
+// bf16 split, six products) and pnr_aggregate_fwd_h2 (H = true: 2-way f16
+// split, three products).  packs: block1.0[:, 224:], block1.2, block3.0,
+// block3.2; scale: per-layer output factor (1 for the bf16 packs);
+// range_flag: set to 1 when an f16-split activation leaves the f16 range.
+struct SplitW {
+  const void* pack[4];
+  float scale[4];
+  int32_t* range_flag;
+};
+template <bool H>
+int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
+                       const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
+                       float* out_conf, hipStream_t st);
 
 }  // namespace pnr

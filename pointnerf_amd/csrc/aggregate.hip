@@ -1254,7 +1254,44 @@ extern "C" int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s,
   hipStream_t st = as_stream(stream);
   // k_point_pre (fp32 P1) -> k_pairs_x3 (aggregate_x3.hip) -> k_color
   if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
-  if ((rc = launch_pairs_x3(a.pts, a.s, a.w, *wx, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf, st)))
+  SplitW sw = {{wx->w1bx, wx->w2x, wx->w3x, wx->w4x}, {1.f, 1.f, 1.f, 1.f}, nullptr};
+  if ((rc = launch_pairs_split<false>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
+                                      st)))
+    return rc;
+  return launch_t<false>(a, st, kStageColor);
+}
+
+extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                    const pnr_mlp_h2* wh, float* out_feat, float* out_weight, float* out_conf,
+                                    void* scratch, size_t scratch_bytes, void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
+  PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_h2: need pers or camera");
+  PNR_CHECK_ARG(s->pidx, "aggregate_h2: pidx required");
+  PNR_CHECK_ARG(wh && wh->w1bh && wh->w2h && wh->w3h && wh->w4h, "aggregate_h2: null split weight pack");
+  PNR_CHECK_ARG(w->neg_slope >= 0.f && w->neg_slope <= 1.f, "aggregate_h2: LeakyReLU slope must be in [0, 1]");
+  PNR_CHECK_ARG((((uintptr_t)wh->w1bh | (uintptr_t)wh->w2h | (uintptr_t)wh->w3h | (uintptr_t)wh->w4h) & 15) == 0,
+                "aggregate_h2: split packs must be 16-B aligned");
+  for (int i = 0; i < 4; ++i)
+    PNR_CHECK_ARG(wh->scale[i] > 0.f && wh->scale[i] < 1e30f, "aggregate_h2: bad layer scale %d", i);
+  if (s->n_max <= 0) return PNR_OK;
+  AggArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  a.pair_mask = nullptr;
+  hipStream_t st = as_stream(stream);
+  SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
+               {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
+               wh->range_flag};
+  // k_point_pre (fp32 P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color
+  if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
+  if ((rc = launch_pairs_split<true>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
+                                     st)))
     return rc;
   return launch_t<false>(a, st, kStageColor);
 }

@@ -1,13 +1,19 @@
-// fp32-accurate k_pairs on bf16 MFMA (pnr_aggregate_fwd_x3): block1.0's
-// distance half, block1.2, block3.0 and block3.2 for 64 (sample, neighbour)
-// pairs per tile, as in aggregate.hip's k_pairs, with every fp32 GEMM done as
-// an exact 3-way bf16 split (see agg_common.h, split2).
+// fp32-accurate k_pairs on 16-bit MFMA: block1.0's distance half, block1.2,
+// block3.0 and block3.2 for 64 (sample, neighbour) pairs per tile, as in
+// aggregate.hip's k_pairs, with every fp32 GEMM done on split operands
+// (agg_common.h):
+//   * k_pairs_x3 (pnr_aggregate_fwd_x3): exact 3-way bf16 split, six cross
+//     products per 16-k step on v_mfma_f32_32x32x16_bf16 (split2);
+//   * k_pairs_h2 (pnr_aggregate_fwd_h2): 2-way f16 split with a 2^11-scaled low
+//     half, three products on v_mfma_f32_32x32x16_f16 (splith) -- half the
+//     MFMA work, two activation planes instead of three.
+// Both are one kernel body templated on H (false: bf16 x3, true: f16 h2).
 //
 // Producer / consumer workgroup (one 8-wave workgroup per CU):
 //   * consumers (waves 0..3) own neuron tiles {2w, 2w+1} x both 32-pair halves
-//     and run the MFMA stream: 6 products per 16-k step, weights from split
-//     packs three steps ahead (buffer loads), B fragments = three ds_read_b128 of
-//     the bf16 planes of the layer input.  Each activation is split ONCE, by the
+//     and run the MFMA stream: 6 (x3) / 3 (h2) products per 16-k step, weights
+//     from split packs three steps ahead (buffer loads), B fragments = one
+//     ds_read_b128 per plane of the layer input.  Each activation is split ONCE, by the
 //     wave that produced it, when it is stored (not once per consuming wave).
 //   * producers (waves 4..7) prepare the NEXT tile while the consumers run
 //     block1.2 of the current one: gather (pidx, xyz, w2pers, colour, dir,
@@ -15,10 +21,10 @@
 //     the block3.0 extras -- so the gather latency and the sincos never stall
 //     the MFMA pipe.  The consumers prefetch the next tile's per-point
 //     block1.0 half (P1) into registers during block3.2.
-// LDS (135 KB): layer-input planes [3][34 row groups][64 pairs][8 bf16]
+// LDS (135 KB x3, 100 KB h2): layer-input planes [NPL][34 row groups][64 pairs][8 x 16 bit]
 // (rows 0..271; row group g, pair c at (g*64 + c)*16 B, so a B fragment is one
 // conflict-free ds_read_b128 and an accumulator quad one ds_write_b64 per
-// plane), next-tile PE planes [3][8][64][8], and double-buffered per-tile
+// plane), next-tile PE planes [NPL][8][64][8], and double-buffered per-tile
 // extras / weights / point rows / sample flags.
 #include "agg_common.h"
 
@@ -35,17 +41,27 @@ constexpr int kXG = 34;            // 8-row groups of a layer input (272 rows)
 constexpr int kPG = 8;             // 8-row groups of the distance PE (64 rows)
 constexpr int kPlaneX = kXG * kXT * 16;
 constexpr int kPlaneP = kPG * kXT * 16;
-constexpr int kOffPE = 3 * kPlaneX;
-constexpr int kOffEx = kOffPE + 3 * kPlaneP;     // float [2][8][64]
-constexpr int kOffWt = kOffEx + 2 * 8 * kXT * 4;  // float [2][64]
-constexpr int kOffPr = kOffWt + 2 * kXT * 4;      // int   [2][64]
-constexpr int kOffSf = kOffPr + 2 * kXT * 4;      // int   [2][8]
-constexpr int kOffAp = kOffSf + 2 * kXTS * 4;     // float [4][64]
-constexpr int kOffWa = kOffAp + 4 * kXT * 4;      // float [256] alpha_branch.0 weights
-constexpr size_t kX3Lds = (size_t)kOffWa + kHid * 4;
 constexpr int kP1Pitch = kHid + 4;                 // floats per parked P1 row (conflict-free b128 reads)
-static_assert(kXT * kP1Pitch * 4 <= 3 * kPlaneX, "parked P1 fits the layer-input area");
-static_assert(kX3Lds <= 160 * 1024, "LDS budget");
+
+// Per-variant layout: NPL activation planes (x3: 3 bf16, h2: 2 f16), NPW weight
+// planes per (k-step, neuron tile) in the packs (x3: W0 W1 W2; h2: Wh Wl).
+template <bool H>
+struct XL {
+  static constexpr int NPL = H ? 2 : 3;
+  static constexpr int NPW = H ? 2 : 3;
+  static constexpr unsigned kOne = H ? 0x3C00u : 0x3F80u;   // 1.0 (bias input row)
+  static constexpr int OffPE = NPL * kPlaneX;
+  static constexpr int OffEx = OffPE + NPL * kPlaneP;       // float [2][8][64]
+  static constexpr int OffWt = OffEx + 2 * 8 * kXT * 4;    // float [2][64]
+  static constexpr int OffPr = OffWt + 2 * kXT * 4;        // int   [2][64]
+  static constexpr int OffSf = OffPr + 2 * kXT * 4;        // int   [2][8]
+  static constexpr int OffAp = OffSf + 2 * kXTS * 4;       // float [4][64]
+  static constexpr int OffWa = OffAp + 4 * kXT * 4;        // float [256] alpha_branch.0 weights
+  static constexpr size_t Lds = (size_t)OffWa + kHid * 4;
+  static_assert(kXT * kP1Pitch * 4 <= NPL * kPlaneX, "parked P1 fits the layer-input area");
+  static_assert(Lds <= 160 * 1024, "LDS budget");
+};
+constexpr float kF16Max = 65504.f;
 
 #ifndef PNR_X3_PRIO
 #define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
@@ -74,7 +90,7 @@ struct X3Args {
   pnr_points pts;
   pnr_samples s;
   pnr_mlp w;
-  pnr_mlp_x3 wx;
+  SplitW wx;
   const float* p1;
   float* hid;
   int32_t* vmask;
@@ -87,41 +103,47 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-// this wave's 2 neuron tiles of k-step t, 3 planes each; voff = (T0 * 3 * 64 + lane) * 16
-__device__ __forceinline__ void load_w(uint4 (&a)[2][3], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
+// this wave's 2 neuron tiles of k-step t, NPW planes each; voff = (T0 * NPW * 64 + lane) * 16
+template <bool H>
+__device__ __forceinline__ void load_w(uint4 (&a)[2][XL<H>::NPW], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
+  constexpr int NPW = XL<H>::NPW;
 #pragma unroll
   for (int T = 0; T < 2; ++T)
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NPW; ++pl)
       a[T][pl] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * 8 + T) * 3 * 1024, 0));
+                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * 8 + T) * NPW * 1024, 0));
 }
 
 constexpr int kWD = 3;   // weight ring depth (k-steps in flight); the packs carry kWD zero steps
 
+template <bool H>
 struct WRing {
-  uint4 a[kWD][2][3];
+  uint4 a[kWD][2][XL<H>::NPW];
 };
 
-__device__ __forceinline__ void prime(WRing& w, __amdgpu_buffer_rsrc_t rs, int voff) {
+template <bool H>
+__device__ __forceinline__ void prime(WRing<H>& w, __amdgpu_buffer_rsrc_t rs, int voff) {
 #pragma unroll
-  for (int d = 0; d < kWD; ++d) load_w(w.a[d], rs, voff, d);
+  for (int d = 0; d < kWD; ++d) load_w<H>(w.a[d], rs, voff, d);
 }
 
 // Y^T += W . X^T over nsteps 16-k steps; X^T = the bf16 planes at `planes`
 // (plane stride pstride bytes, 64 pairs per 8-row group).  Weights kWD steps
 // ahead in the ring (slot d: steps = d mod kWD), B one step ahead.
-__device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing& w, __amdgpu_buffer_rsrc_t rs, int voff,
+template <bool H>
+__device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_buffer_rsrc_t rs, int voff,
                                       const char* planes, int pstride, int nsteps, int lane) {
+  constexpr int NPL = XL<H>::NPL, NPW = XL<H>::NPW;
   const int c = lane & 31, h = lane >> 5;
   const char* base = planes + (h * kXT + c) * 16;
-  auto ldb = [&](int t, int pt, uint4 (&bb)[3]) {
+  auto ldb = [&](int t, int pt, uint4 (&bb)[NPL]) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NPL; ++pl)
       bb[pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * t * kXT + 32 * pt) * 16);
   };
-  uint4 b[2][3];
+  uint4 b[2][NPL];
   ldb(0, 0, b[0]);
   ldb(0, 1, b[1]);
   // One step = 2 halves x 12 MFMAs.  Each B plane of a half is re-read for the
@@ -130,46 +152,75 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing& w, __amdgpu_buffe
   // bursts; sched_barrier(0) pins the order (hipcc would otherwise sink the
   // LDS reads next to their uses and merge the waits).
   auto mm = [&](int pt, const uint4& av0, const uint4& av1, const uint4& bv) {
-    acc[2 * pt] = mfma_bf16(av0, bv, acc[2 * pt]);
-    acc[2 * pt + 1] = mfma_bf16(av1, bv, acc[2 * pt + 1]);
+    if constexpr (H) {
+      acc[2 * pt] = mfma_f16(av0, bv, acc[2 * pt]);
+      acc[2 * pt + 1] = mfma_f16(av1, bv, acc[2 * pt + 1]);
+    } else {
+      acc[2 * pt] = mfma_bf16(av0, bv, acc[2 * pt]);
+      acc[2 * pt + 1] = mfma_bf16(av1, bv, acc[2 * pt + 1]);
+    }
   };
-  auto wl = [&](uint4 (&a)[2][3], int pl, int tw) {
+  auto wl = [&](uint4 (&a)[2][NPW], int pl, int tw) {
 #pragma unroll
     for (int T = 0; T < 2; ++T)
       a[T][pl] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * 8 + T) * 3 * 1024, 0));
+                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * 8 + T) * NPW * 1024, 0));
   };
   auto bl = [&](int tn, int pt, int pl) {
     if (!(PNR_ABLATE & 64))   // (64: timing only, B fixed)
       b[pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
   };
-  auto step = [&](uint4 (&a)[2][3], int t) {
+  // h2 step per half: Ws.Xh, Wl.Xh, Wh.Xl (Ws = 2^11 Wh, made in registers)
+  auto step_h = [&](uint4 (&a)[2][NPW], int t) {
     const int tn = t + 1 < nsteps ? t + 1 : t;
+    const uint4 s0 = f16x8_scale2048(a[0][0]), s1 = f16x8_scale2048(a[1][0]);
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
-      mm(pt, a[0][2], a[1][2], b[pt][0]);                      // W2.X0
+      mm(pt, s0, s1, b[pt][0]);                                // Ws.Xh
       __builtin_amdgcn_sched_barrier(0);
-      if (pt == 1) wl(a, 2, t + kWD);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(pt, a[0][1], a[1][1], b[pt][1]);                      // W1.X1
-      mm(pt, a[0][0], a[1][0], b[pt][2]);                      // W0.X2
-      __builtin_amdgcn_sched_barrier(0);
-      bl(tn, pt, 2);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(pt, a[0][1], a[1][1], b[pt][0]);                      // W1.X0
+      mm(pt, a[0][1], a[1][1], b[pt][0]);                      // Wl.Xh
       __builtin_amdgcn_sched_barrier(0);
       if (pt == 1) wl(a, 1, t + kWD);
+      bl(tn, pt, 0);
       __builtin_amdgcn_sched_barrier(0);
-      mm(pt, a[0][0], a[1][0], b[pt][1]);                      // W0.X1
+      mm(pt, a[0][0], a[1][0], b[pt][1]);                      // Wh.Xl
       __builtin_amdgcn_sched_barrier(0);
       bl(tn, pt, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(pt, a[0][0], a[1][0], b[pt][0]);                      // W0.X0
-      __builtin_amdgcn_sched_barrier(0);
-      bl(tn, pt, 0);
       if (pt == 1) wl(a, 0, t + kWD);   // packs carry kWD zero steps
       __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto step = [&](uint4 (&a)[2][NPW], int t) {
+    if constexpr (H) {
+      step_h(a, t);
+    } else {
+      const int tn = t + 1 < nsteps ? t + 1 : t;
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        mm(pt, a[0][2], a[1][2], b[pt][0]);                      // W2.X0
+        __builtin_amdgcn_sched_barrier(0);
+        if (pt == 1) wl(a, 2, t + kWD);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(pt, a[0][1], a[1][1], b[pt][1]);                      // W1.X1
+        mm(pt, a[0][0], a[1][0], b[pt][2]);                      // W0.X2
+        __builtin_amdgcn_sched_barrier(0);
+        bl(tn, pt, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(pt, a[0][1], a[1][1], b[pt][0]);                      // W1.X0
+        __builtin_amdgcn_sched_barrier(0);
+        if (pt == 1) wl(a, 1, t + kWD);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(pt, a[0][0], a[1][0], b[pt][1]);                      // W0.X1
+        __builtin_amdgcn_sched_barrier(0);
+        bl(tn, pt, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(pt, a[0][0], a[1][0], b[pt][0]);                      // W0.X0
+        __builtin_amdgcn_sched_barrier(0);
+        bl(tn, pt, 0);
+        if (pt == 1) wl(a, 0, t + kWD);   // packs carry kWD zero steps
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   int t = 0;
@@ -183,9 +234,36 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing& w, __amdgpu_buffe
     if (t + d < nsteps) step(w.a[d], t + d);   // the ring then holds padding; prime() refills it
 }
 
-// lrelu(acc) -> layer-input planes, rows 32(T0+T) + 8q + 4h + i: one ds_write_b64 per plane and quad
-__device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, float s, int lane, int T0) {
+// lrelu(mul * acc) -> layer-input planes, rows 32(T0+T) + 8q + 4h + i: one
+// ds_write_b64 per plane and quad.  h2: amax tracks max |activation| (f16 range).
+template <bool H>
+__device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, float s, float mul, int lane,
+                                          int T0, float& amax) {
   const int c = lane & 31, h = lane >> 5;
+  if constexpr (H) {
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x16& v = acc[2 * pt + T];
+          float y[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float x = v[4 * q + i] * mul;
+            y[i] = fmaxf(x, s * x);
+            amax = fmaxf(amax, fabsf(y[i]));
+          }
+          unsigned a0, a1, b0, b1;
+          splith(y[0], y[1], a0, a1);
+          splith(y[2], y[3], b0, b1);
+          char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
+          *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
+          *reinterpret_cast<uint2*>(d + kPlaneX) = make_uint2(a1, b1);
+        }
+    return;
+  }
   if (PNR_ABLATE & 128) {   // timing only: no split (hi plane = bf16(x), other planes untouched)
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt)
@@ -218,8 +296,23 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
       }
 }
 
-// 8 fp32 rows of one pair -> row group g of the three planes (ds_write_b128 each)
-__device__ __forceinline__ void store_group(char* planes, int pstride, int g, int pair, const float (&v)[8]) {
+// 8 fp32 rows of one pair -> row group g of the NPL planes (ds_write_b128 each)
+template <bool H>
+__device__ __forceinline__ void store_group(char* planes, int pstride, int g, int pair, const float (&v)[8],
+                                            float& amax) {
+  if constexpr (H) {
+    uint4 p0, p1;
+    splith(v[0], v[1], p0.x, p1.x);
+    splith(v[2], v[3], p0.y, p1.y);
+    splith(v[4], v[5], p0.z, p1.z);
+    splith(v[6], v[7], p0.w, p1.w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
+    char* d = planes + (g * kXT + pair) * 16;
+    *reinterpret_cast<uint4*>(d) = p0;
+    *reinterpret_cast<uint4*>(d + pstride) = p1;
+    return;
+  }
   uint4 p0, p1, p2;
   split2(v[0], v[1], p0.x, p1.x, p2.x);
   split2(v[2], v[3], p0.y, p1.y, p2.y);
@@ -262,8 +355,10 @@ __device__ __forceinline__ void gather_sample(const X3Args& A, int lane, GatherS
   g.dmap = A.s.dir_map ? (int64_t)A.s.dir_map[g.row] : g.row;
 }
 
+template <bool H>
 __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, int nb, char* lds, int pw, int lane,
                                        float (&dr6)[6]) {
+  using L = XL<H>;
   float Rw[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
@@ -331,12 +426,12 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
     mat3(Rw, pdir, drot);
     const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
     const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
-    float* exL = reinterpret_cast<float*>(lds + kOffEx) + nb * 8 * kXT;
+    float* exL = reinterpret_cast<float*>(lds + L::OffEx) + nb * 8 * kXT;
 #pragma unroll
     for (int e = 0; e < 8; ++e) exL[e * kXT + lane] = ex[e];
-    reinterpret_cast<float*>(lds + kOffWt)[nb * kXT + lane] = wn * confc;
-    reinterpret_cast<int*>(lds + kOffPr)[nb * kXT + lane] = valid ? (int)prow : -1;
-    if (k == 0) reinterpret_cast<int*>(lds + kOffSf)[nb * kXTS + j] = active && samp_valid;
+    reinterpret_cast<float*>(lds + L::OffWt)[nb * kXT + lane] = wn * confc;
+    reinterpret_cast<int*>(lds + L::OffPr)[nb * kXT + lane] = valid ? (int)prow : -1;
+    if (k == 0) reinterpret_cast<int*>(lds + L::OffSf)[nb * kXTS + j] = active && samp_valid;
     if (active && k < K) {
       if (A.out_weight) A.out_weight[row * K + k] = wn;
       if (A.out_conf) A.out_conf[row * K + k] = confc;
@@ -346,11 +441,13 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
 
 // 5-band PE of the rotated 6-d distance of this lane's pair -> rows 2e (sin),
 // 2e + 1 (cos), e = 5 ch + f, of the PE planes; producer wave pw takes e = pw (mod 4)
+template <bool H>
 __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6], int e_lo, int e_hi) {
+  using L = XL<H>;
   if (pw == 0 && e_lo == 0) {   // rows 60..63: the 4th 16-k step reads them
-    char* pz = lds + kOffPE + (7 * kXT + lane) * 16 + 8;
+    char* pz = lds + L::OffPE + (7 * kXT + lane) * 16 + 8;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
+    for (int pl = 0; pl < L::NPL; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
   }
   if (!(PNR_ABLATE & 2)) {
 #pragma unroll 1
@@ -364,13 +461,20 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
       dc = ch == 5 ? dr6[5] : dc;
       float sn, cs;
       sincosf(dc * (float)(1 << f), &sn, &cs);
-      unsigned x0, x1, x2;
-      split2(sn, cs, x0, x1, x2);
       const int r = 2 * e;
-      char* d = lds + kOffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
-      *reinterpret_cast<unsigned*>(d) = x0;
-      *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
-      *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
+      char* d = lds + L::OffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
+      if constexpr (H) {
+        unsigned x0, x1;
+        splith(sn, cs, x0, x1);
+        *reinterpret_cast<unsigned*>(d) = x0;
+        *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+      } else {
+        unsigned x0, x1, x2;
+        split2(sn, cs, x0, x1, x2);
+        *reinterpret_cast<unsigned*>(d) = x0;
+        *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+        *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
+      }
     }
   }
 }
@@ -389,13 +493,15 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
 // overlaps; the P1 rows travel during block3.0 / block3.2.
 #define X3_SYNC() __syncthreads()
 
+template <bool H>
 __device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int buf, int64_t tile, int lane) {
+  using L = XL<H>;
   if (PNR_ABLATE & 4) return;
   const int64_t n = eff_n(A.s);
   const int j = lane >> 3, k = lane & 7;
-  const float* apart = reinterpret_cast<const float*>(lds + kOffAp);
-  const float* wtL = reinterpret_cast<const float*>(lds + kOffWt) + buf * kXT;
-  const int* sflag = reinterpret_cast<const int*>(lds + kOffSf) + buf * kXTS;
+  const float* apart = reinterpret_cast<const float*>(lds + L::OffAp);
+  const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + buf * kXT;
+  const int* sflag = reinterpret_cast<const int*>(lds + L::OffSf) + buf * kXTS;
   const float pa = apart[lane] + apart[kXT + lane] + apart[2 * kXT + lane] + apart[3 * kXT + lane] + A.w.ba[0];
   const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
   const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
@@ -406,22 +512,28 @@ __device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int b
   }
 }
 
+template <bool H>
 __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wid, int lane) {
+  using L = XL<H>;
   const int c = lane & 31, h = lane >> 5;
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kXTS);
   const float neg = A.w.neg_slope;
   char* XP = lds;
-  const char* PE = lds + kOffPE;
+  const char* PE = lds + L::OffPE;
   const float* P1L = reinterpret_cast<const float*>(lds);   // P1 rows parked in the XP area between tiles
-  float* apart = reinterpret_cast<float*>(lds + kOffAp);
-  const float* waL = reinterpret_cast<const float*>(lds + kOffWa);
+  float* apart = reinterpret_cast<float*>(lds + L::OffAp);
+  const float* waL = reinterpret_cast<const float*>(lds + L::OffWa);
   const int T0 = 2 * wid;
-  const int voff = (T0 * 3 * 64 + lane) * 16;
-  const __amdgpu_buffer_rsrc_t r1 = rsrc(A.wx.w1bx), r2 = rsrc(A.wx.w2x), r3 = rsrc(A.wx.w3x), r4 = rsrc(A.wx.w4x);
-  WRing wr;
+  const int voff = (T0 * L::NPW * 64 + lane) * 16;
+  const __amdgpu_buffer_rsrc_t r1 = rsrc(A.wx.pack[0]), r2 = rsrc(A.wx.pack[1]), r3 = rsrc(A.wx.pack[2]),
+                               r4 = rsrc(A.wx.pack[3]);
+  // layer output factors (h2: 2^(s-11) of the pre-scaled f16 packs; x3: 1, unused)
+  const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
+  float amax = 0.f;   // h2: max |split activation| (f16 range check)
+  WRing<H> wr;
   f32x16 acc[4];
-  prime(wr, r1, voff);
+  prime<H>(wr, r1, voff);
   X3_SYNC();   // S0: the first tile's PE planes, extras and weights are in LDS
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][0] = wall_clock64();
@@ -433,8 +545,8 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     // ------------------------------------------------------------ block1.0 = P1 + W1[:, 224:] . PE_5
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
-    layer(acc, wr, r1, voff, PE, kPlaneP, 4, lane);
-    prime(wr, r2, voff);
+    layer<H>(acc, wr, r1, voff, PE, kPlaneP, 4, lane);
+    prime<H>(wr, r2, voff);
     X3_TR(0, 1);
     X3_SYNC();   // S1: P1 parked, PE planes consumed
     X3_TR(0, 2);
@@ -446,19 +558,26 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         for (int q = 0; q < 4; ++q) {
           const float4 v4 = *reinterpret_cast<const float4*>(P1L + (32 * pt + c) * kP1Pitch + 32 * (T0 + T) + 8 * q +
                                                              4 * h);
-          acc[2 * pt + T][4 * q] += v4.x;
-          acc[2 * pt + T][4 * q + 1] += v4.y;
-          acc[2 * pt + T][4 * q + 2] += v4.z;
-          acc[2 * pt + T][4 * q + 3] += v4.w;
+          if constexpr (H) {
+            acc[2 * pt + T][4 * q] = fmaf(acc[2 * pt + T][4 * q], sc1, v4.x);
+            acc[2 * pt + T][4 * q + 1] = fmaf(acc[2 * pt + T][4 * q + 1], sc1, v4.y);
+            acc[2 * pt + T][4 * q + 2] = fmaf(acc[2 * pt + T][4 * q + 2], sc1, v4.z);
+            acc[2 * pt + T][4 * q + 3] = fmaf(acc[2 * pt + T][4 * q + 3], sc1, v4.w);
+          } else {
+            acc[2 * pt + T][4 * q] += v4.x;
+            acc[2 * pt + T][4 * q + 1] += v4.y;
+            acc[2 * pt + T][4 * q + 2] += v4.z;
+            acc[2 * pt + T][4 * q + 3] += v4.w;
+          }
         }
     X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
     X3_TR(0, 3);
-    store_act(acc, XP, neg, lane, T0);
+    store_act<H>(acc, XP, neg, 1.f, lane, T0, amax);
     if (wid == 0) {
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
+      for (int pl = 0; pl < L::NPL; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
         *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (32 * kXT + lane) * 16) =
-            make_uint4(pl == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+            make_uint4(pl == 0 ? L::kOne : 0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (33 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
       }
     }
@@ -468,47 +587,47 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     X3_SYNC();   // S2
     X3_TR(0, 5);
     // ------------------------------------------------------------ block1.2
-    layer(acc, wr, r2, voff, XP, kPlaneX, 17, lane);
-    prime(wr, r3, voff);
+    layer<H>(acc, wr, r2, voff, XP, kPlaneX, 17, lane);
+    prime<H>(wr, r3, voff);
     X3_TR(0, 6);
     X3_SYNC();   // S3
     X3_TR(0, 7);
-    store_act(acc, XP, neg, lane, T0);
+    store_act<H>(acc, XP, neg, sc2, lane, T0, amax);
     if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
-      const float* exL = reinterpret_cast<const float*>(lds + kOffEx) + buf * 8 * kXT;
+      const float* exL = reinterpret_cast<const float*>(lds + L::OffEx) + buf * 8 * kXT;
       float ex[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) ex[e] = exL[e * kXT + lane];
-      store_group(XP, kPlaneX, 32, lane, ex);
+      store_group<H>(XP, kPlaneX, 32, lane, ex, amax);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
     X3_SYNC();   // S4
     X3_TR(0, 8);
     // ------------------------------------------------------------ block3.0
-    layer(acc, wr, r3, voff, XP, kPlaneX, 17, lane);
-    prime(wr, r4, voff);
+    layer<H>(acc, wr, r3, voff, XP, kPlaneX, 17, lane);
+    prime<H>(wr, r4, voff);
     X3_TR(0, 9);
     X3_SYNC();   // S5
     X3_TR(0, 10);
-    store_act(acc, XP, neg, lane, T0);
+    store_act<H>(acc, XP, neg, sc3, lane, T0, amax);
     if (wid == 0) {
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < L::NPL; ++pl)
         *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (32 * kXT + lane) * 16) =
-            make_uint4(pl == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+            make_uint4(pl == 0 ? L::kOne : 0u, 0u, 0u, 0u);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
     X3_SYNC();   // S6
     X3_TR(0, 11);
     // ------------------------------------------------------------ block3.2, alpha partials, K sums
-    layer(acc, wr, r4, voff, XP, kPlaneX, 17, lane);
-    prime(wr, r1, voff);   // the next tile's block1.0
+    layer<H>(acc, wr, r4, voff, XP, kPlaneX, 17, lane);
+    prime<H>(wr, r1, voff);   // the next tile's block1.0
     X3_TR(0, 12);
     if (!(PNR_ABLATE & 4)) {
-      const float* wtL = reinterpret_cast<const float*>(lds + kOffWt) + buf * kXT;
-      const int* sflag = reinterpret_cast<const int*>(lds + kOffSf) + buf * kXTS;
+      const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + buf * kXT;
+      const int* sflag = reinterpret_cast<const int*>(lds + L::OffSf) + buf * kXTS;
       float pa_part[2] = {0.f, 0.f};
       const int i8 = c & 7;
       const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
@@ -523,7 +642,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
           float v[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float hv = lrelu(acc[2 * pt + T][r], neg);
+            const float hv = lrelu(H ? acc[2 * pt + T][r] * sc4 : acc[2 * pt + T][r], neg);
             pa_part[pt] += waL[32 * (T0 + T) + acc_row(r, h)] * hv;
             v[r] = wtp * hv;
           }
@@ -569,6 +688,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][1] = wall_clock64();
 #endif
+  if (H && A.wx.range_flag && !(amax < kF16Max)) atomicOr(A.wx.range_flag, 1);   // also catches NaN
 }
 
 // Producer wave pw: P1 rows 16 pw .. 16 pw + 15 of a tile (1 KB each, one
@@ -602,7 +722,9 @@ __device__ __forceinline__ void park_p1(const f32x4n (&r)[16], unsigned empty, c
   }
 }
 
+template <bool H>
 __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw, int lane) {
+  using L = XL<H>;
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kXTS);
 #if PNR_X3_PRIO
@@ -614,10 +736,10 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   GatherState g;
   gather_row(A, blockIdx.x, lane, g);
   gather_sample(A, lane, g);
-  gather(A, g, 0, lds, pw, lane, dr6);
-  pe_planes(lds, pw, lane, dr6, 0, 30);
+  gather<H>(A, g, 0, lds, pw, lane, dr6);
+  pe_planes<H>(lds, pw, lane, dr6, 0, 30);
   X3_SYNC();   // P0: prow of the first tile visible to all producers
-  p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr), pw, lane);
+  p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
   X3_SYNC();   // S0
   int it = 0;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
@@ -629,41 +751,46 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_TR(1, 1);
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
-    if (pw == 0 && it > 0) finalize_alpha(A, lds, nbuf, tile - gridDim.x, lane);
+    if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, tile - gridDim.x, lane);
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
     X3_TR(1, 2);
     // during block1.2: gather (nbuf's arrays are free: their last reader was the previous finalize)
-    if (!(PNR_ABLATE & 256)) gather(A, g, nbuf, lds, pw, lane, dr6);
+    if (!(PNR_ABLATE & 256)) gather<H>(A, g, nbuf, lds, pw, lane, dr6);
     X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
-    if (!(PNR_ABLATE & 256)) p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + kOffPr) + nbuf * kXT, pw, lane);
+    if (!(PNR_ABLATE & 256))
+      p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
     X3_TR(1, 4);
     X3_SYNC();   // S4
-    if (!(PNR_ABLATE & 256)) pe_planes(lds, pw, lane, dr6, 0, 16);   // during block3.0 (PE planes free since S1)
+    if (!(PNR_ABLATE & 256)) pe_planes<H>(lds, pw, lane, dr6, 0, 16);   // during block3.0 (PE planes free since S1)
     X3_SYNC();   // S5
     X3_TR(1, 5);
     X3_SYNC();   // S6
-    if (!(PNR_ABLATE & 256)) pe_planes(lds, pw, lane, dr6, 16, 30);   // during block3.2
+    if (!(PNR_ABLATE & 256)) pe_planes<H>(lds, pw, lane, dr6, 16, 30);   // during block3.2
     X3_SYNC();   // S7
   }
-  if (pw == 0 && it > 0) finalize_alpha(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
+  if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
 }
 
-__global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) {
+template <bool H>
+__device__ __forceinline__ void pairs_body(const X3Args& A) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // alpha_branch.0 weights for the consumers' tail
-  if (threadIdx.x < kHid) reinterpret_cast<float*>(lds + kOffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
+  if (threadIdx.x < kHid) reinterpret_cast<float*>(lds + XL<H>::OffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
   if (wid < 4) {
     X3_SYNC();   // P0
-    consumer_loop(A, lds, wid, lane);
+    consumer_loop<H>(A, lds, wid, lane);
   } else {
-    producer_loop(A, lds, wid - 4, lane);
+    producer_loop<H>(A, lds, wid - 4, lane);
   }
 }
+
+__global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) { pairs_body<false>(A); }
+__global__ void __launch_bounds__(512, 1) k_pairs_h2(X3Args A) { pairs_body<true>(A); }
 
 }  // namespace
 
@@ -683,13 +810,14 @@ extern "C" int pnr_debug_x3_blocks(unsigned long long* out, int n) {
 }
 #endif
 
-int launch_pairs_x3(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const pnr_mlp_x3& wx,
-                    const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
-                    float* out_conf, hipStream_t st) {
+template <bool H>
+int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
+                       const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
+                       float* out_conf, hipStream_t st) {
+  const void* fn = H ? reinterpret_cast<const void*>(&k_pairs_h2) : reinterpret_cast<const void*>(&k_pairs_x3);
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_x3),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kX3Lds));
+    PNR_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)XL<H>::Lds));
     attr = true;
   }
   X3Args a;
@@ -704,9 +832,16 @@ int launch_pairs_x3(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& 
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   const int64_t tiles = cdiv(s.n_max, kXTS);
-  hipLaunchKernelGGL(k_pairs_x3, dim3(grid_for(tiles, 1, 256)), dim3(512), kX3Lds, st, a);
+  if (H)
+    hipLaunchKernelGGL(k_pairs_h2, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
+  else
+    hipLaunchKernelGGL(k_pairs_x3, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
+template int launch_pairs_split<false>(const pnr_points&, const pnr_samples&, const pnr_mlp&, const SplitW&,
+                                       const float*, float*, int32_t*, float*, float*, float*, hipStream_t);
+template int launch_pairs_split<true>(const pnr_points&, const pnr_samples&, const pnr_mlp&, const SplitW&,
+                                      const float*, float*, int32_t*, float*, float*, float*, hipStream_t);
 
 }  // namespace pnr

@@ -97,8 +97,10 @@ class NeuralPoints(nn.Module):
 
 # fp32: the reference's arithmetic on v_mfma_f32_32x32x2_f32.  fp32x3: the same
 # fp32 GEMMs as exact 3-way bf16 splits on v_mfma_f32_32x32x16_bf16 (six cross
-# products, fp32-accurate; pnr_aggregate_fwd_x3).  bf16: bf16 operands (config c5).
-PRECISIONS = ("fp32", "fp32x3", "bf16")
+# products, fp32-accurate; pnr_aggregate_fwd_x3).  fp32h2: the same GEMMs as 2-way
+# f16 splits on v_mfma_f32_32x32x16_f16 (three products, fp32-accurate;
+# pnr_aggregate_fwd_h2).  bf16: bf16 operands (config c5).
+PRECISIONS = ("fp32", "fp32x3", "fp32h2", "bf16")
 
 
 class NeuralPointsRayMarching(nn.Module):
@@ -163,6 +165,8 @@ class NeuralPointsRayMarching(nn.Module):
         mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
         if self.precision == "fp32x3":
             mlpx, _keepx = self.aggregator.packed_x3()
+        elif self.precision == "fp32h2":
+            mlph, _keeph = self.aggregator.packed_h2()
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
         chunk = max(1, self.chunk_rays or R)
@@ -201,6 +205,11 @@ class NeuralPointsRayMarching(nn.Module):
                                                      L.ctypes.byref(mlpx), L.ptr(feat), None, None, L.ptr(scratch),
                                                      scratch.numel() * 4, L.stream_ptr(dev)),
                         "pnr_aggregate_fwd_x3")
+            elif self.precision == "fp32h2":
+                L.check(L.lib().pnr_aggregate_fwd_h2(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
+                                                     L.ctypes.byref(mlph), L.ptr(feat), None, None, L.ptr(scratch),
+                                                     scratch.numel() * 4, L.stream_ptr(dev)),
+                        "pnr_aggregate_fwd_h2")
             else:
                 L.check(L.lib().pnr_aggregate_fwd(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                                   L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,

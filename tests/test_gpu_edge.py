@@ -34,8 +34,9 @@ def _render(m, sc, cuda, rd=None):
     return [t.cpu() for t in out]
 
 
-# fp32: the reference arithmetic; fp32x3: the fp32-accurate split-bf16 path (same tolerances)
-PRECISIONS = ["fp32", "fp32x3"]
+# fp32: the reference arithmetic; fp32x3 / fp32h2: the fp32-accurate split-bf16 /
+# split-f16 paths (same tolerances)
+PRECISIONS = ["fp32", "fp32x3", "fp32h2"]
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

@@ -1,4 +1,6 @@
-"""fp32-accurate split-bf16 aggregation (pnr_aggregate_fwd_x3) vs the CPU oracle.
+"""fp32-accurate split aggregation vs the CPU oracle: pnr_aggregate_fwd_x3
+(3-way bf16 split, six products) and pnr_aggregate_fwd_h2 (2-way f16 split,
+three products).
 
 Same tolerance as the fp32 path (north_star "stated fp32 tolerance"):
 |d| <= 1e-4 + 1e-4*|ref| against the fp32 oracle, rendered colour within 2e-4
@@ -41,8 +43,11 @@ def _setup(sc, cuda, params=None, seed=0):
     return agg.eval(), np_
 
 
-def _both(agg, np_, sc, cuda, used=False):
-    """fp32 and fp32x3 features on one query -> (f32 [Sv,129], x3 [Sv,129]);
+SPLITS = ["x3", "h2"]
+
+
+def _both(agg, np_, sc, cuda, used=False, variant="x3"):
+    """fp32 and split-path features on one query -> (f32 [Sv,129], split [Sv,129]);
     used: P1 only for the referenced points (the training-batch layout)."""
     from pointnerf_amd import _lib as L
     cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
@@ -61,15 +66,17 @@ def _both(agg, np_, sc, cuda, used=False):
         pts.used, pts.n_used, pts.used_map = u[0].data_ptr(), u[0].numel(), u[1].data_ptr()
         n_p1 = u[0].numel()
     mlp, _k1 = agg.packed()
-    mlpx, _k2 = agg.packed_x3()
+    mlpx, _k2 = agg.packed_x3() if variant == "x3" else agg.packed_h2()
     outs = []
-    for fn, extra in (("pnr_aggregate_fwd", ()), ("pnr_aggregate_fwd_x3", (L.ctypes.byref(mlpx),))):
+    for fn, extra in (("pnr_aggregate_fwd", ()), (f"pnr_aggregate_fwd_{variant}", (L.ctypes.byref(mlpx),))):
         f = torch.zeros((Sv, 129), device=cuda)
         scr = L.aggregate_scratch(Sv, n_p1, cuda)
         L.check(getattr(L.lib(), fn)(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), *extra, L.ptr(f),
                                      None, None, L.ptr(scr), scr.numel() * 4, L.stream_ptr(cuda)), fn)
         outs.append(f)
     torch.cuda.synchronize()
+    if variant == "h2":
+        assert agg.h2_range_ok()
     _keep_used = u if used else None   # noqa: F841 (keeps the used tables alive until here)
     return outs[0].cpu().numpy(), outs[1].cpu().numpy()
 
@@ -89,24 +96,26 @@ def _oracle_features(sc, params, f64=False):
     return np.asarray(ref)[rv]
 
 
-def test_x3_used_subset_equals_full(cuda):
+@pytest.mark.parametrize("variant", SPLITS)
+def test_x3_used_subset_equals_full(cuda, variant):
     """P1 for the referenced points only (pts.used, the training layout) gives
     bit-identical features to P1 for every point."""
     sc = scene(20000, H=40, W=40, default_conf=None)
     agg, np_ = _setup(sc, cuda, formula_params(salt=0.4))
-    _, a = _both(agg, np_, sc, cuda)
-    _, b = _both(agg, np_, sc, cuda, used=True)
+    _, a = _both(agg, np_, sc, cuda, variant=variant)
+    _, b = _both(agg, np_, sc, cuda, used=True, variant=variant)
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("variant", SPLITS)
 @pytest.mark.parametrize("salt", [0.3, None])
-def test_x3_features_vs_oracle_fp32_and_fp64(cuda, salt):
+def test_x3_features_vs_oracle_fp32_and_fp64(cuda, salt, variant):
     """salt 0.3: closed-form weights (tests/golden/formula.py); None: the
     aggregator's own random init (xavier, networks.py:163-172)."""
     sc = scene(20000, H=40, W=40, default_conf=None)
     agg, np_ = _setup(sc, cuda, None if salt is None else formula_params(salt=salt))
     params = {k: v.detach().cpu().numpy() for k, v in agg.state_dict().items()}
-    f32, x3 = _both(agg, np_, sc, cuda)
+    f32, x3 = _both(agg, np_, sc, cuda, variant=variant)
     want = _oracle_features(sc, params)
     assert want.shape == x3.shape and want.shape[0] > 500
     np.testing.assert_allclose(x3, want, atol=ATOL, rtol=RTOL)
@@ -116,17 +125,18 @@ def test_x3_features_vs_oracle_fp32_and_fp64(cuda, salt):
     ex3 = np.abs(x3.astype(np.float64) - want64)
     scale = np.abs(want64).max()
     print(f"\nerr vs f64 (max, rms) / max|ref| {scale:.3g}: fp32 {e32.max():.3g} {np.sqrt((e32 ** 2).mean()):.3g}"
-          f"  fp32x3 {ex3.max():.3g} {np.sqrt((ex3 ** 2).mean()):.3g}")
+          f"  fp32{variant} {ex3.max():.3g} {np.sqrt((ex3 ** 2).mean()):.3g}")
     assert ex3.max() <= 2.0 * e32.max() + 1e-7 * scale
     assert np.sqrt((ex3 ** 2).mean()) <= 1.5 * np.sqrt((e32 ** 2).mean()) + 1e-8 * scale
 
 
-def test_x3_render_vs_oracle(cuda):
+@pytest.mark.parametrize("variant", SPLITS)
+def test_x3_render_vs_oracle(cuda, variant):
     from pointnerf_amd.renderer import NeuralPointsRayMarching
     sc = scene(30000, H=48, W=48, theta=200.0, default_conf=None)
     params = formula_params(salt=0.1)
     agg, np_ = _setup(sc, cuda, params)
-    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32x3")
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32" + variant)
     args = [torch.from_numpy(sc[k]).to(cuda) for k in ("campos", "camrot", "raydir")]
     with torch.no_grad():
         c, op, bg, mask = m.render_rays(*args, 2.0, 6.0, torch.from_numpy(sc["bg"]).to(cuda))
@@ -138,3 +148,38 @@ def test_x3_render_vs_oracle(cuda):
     np.testing.assert_allclose(x, y, atol=2e-4, rtol=1e-4)
     psnr = 10 * np.log10(float(np.abs(y).max()) ** 2 / max(float(np.mean((x - y) ** 2)), 1e-30))
     assert psnr >= 60.0, psnr
+
+
+def test_h2_large_weights_prescaled(cuda):
+    """Weights far above the f16 range of 2^11 Wh are pre-scaled in the pack
+    (scale = 2^(s-11)); features stay within the fp32 tolerance."""
+    sc = scene(20000, H=32, W=32, default_conf=None)
+    params = formula_params(salt=0.3)
+    params = dict(params)
+    for k in ("block1.2.weight", "block3.2.weight"):
+        params[k] = params[k] * np.float32(64.0)   # |W| up to ~64x: s > 0 for those layers
+    for k in ("block3.0.weight", "block3.0.bias"):
+        params[k] = params[k] / np.float32(64.0)   # keep activations O(1)
+    for k in ("color_branch.0.weight",):
+        params[k] = params[k] / np.float32(64.0)
+    agg, np_ = _setup(sc, cuda, params)
+    f32, h2 = _both(agg, np_, sc, cuda, variant="h2")
+    want = _oracle_features(sc, {k: v.detach().cpu().numpy() for k, v in agg.state_dict().items()})
+    np.testing.assert_allclose(h2, want, atol=ATOL, rtol=RTOL)
+
+
+def test_h2_range_flag(cuda):
+    """An activation beyond the f16 range sets the launch's range flag (the
+    outputs of such a launch are invalid and the caller is told)."""
+    from pointnerf_amd.renderer import NeuralPointsRayMarching
+    sc = scene(20000, H=32, W=32, default_conf=None)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.3))
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32h2")
+    args = [torch.from_numpy(sc[k]).to(cuda) for k in ("campos", "camrot", "raydir")]
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    with torch.no_grad():
+        m.render_rays(*args, 2.0, 6.0, bg)
+        assert agg.h2_range_ok()
+        agg.block1[2].bias.fill_(1e6)            # block1.2 outputs ~1e6 > 65504 (repacked: new version)
+        m.render_rays(*args, 2.0, 6.0, bg)
+    assert not agg.h2_range_ok()

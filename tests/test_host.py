@@ -78,3 +78,26 @@ def test_product_fails_loudly_without_gpu():
     from pointnerf_amd.options import lego_opt
     with pytest.raises(L.PnrError):
         lighting_fast_querier(torch.device("cpu"), lego_opt())
+
+
+def test_frag_pack_h2_split_exactness():
+    """frag_pack_h2: Wh + 2^-11 Wl reproduces the pre-scaled weights within
+    2^-24 relative (f16 normal range), scale = 2^(s-11) with |W 2^-s| < 16,
+    and the zero padding steps are zero."""
+    import torch
+    from pointnerf_amd.aggregator import H2_PAD, frag_pack_h2
+    g = torch.Generator().manual_seed(0)
+    for mag in (0.1, 40.0):
+        W = torch.randn(256, 60, generator=g) * mag
+        b = torch.randn(256, generator=g) * mag
+        F, scale = frag_pack_h2(W, b)
+        s = round(np.log2(scale)) + 11
+        assert s >= 0 and (W.abs().max() * 2.0 ** -s) < 16 and (s == 0 or W.abs().max() * 2.0 ** -(s - 1) >= 16)
+        tot = (61 + 15) // 16 + H2_PAD
+        P = F.view(tot, 8, 2, 2, 32, 8).float()            # [t][T][pl][h][r][j]
+        rec = P[:, :, 0] + P[:, :, 1] / 2048.0               # [t][T][h][r][j]
+        rec = rec.permute(1, 3, 0, 2, 4).reshape(256, 16 * tot)
+        want = torch.cat([W, b[:, None]], 1) * 2.0 ** -s
+        err = (rec[:, :61].double() - want.double()).abs()
+        assert float((err - 2.0 ** -23 * want.double().abs()).max()) <= 2.0 ** -35
+        assert float(rec[:, 61:].abs().max()) == 0.0

@@ -1,13 +1,17 @@
 #!/bin/bash
 # Dev tool: bench.py line + rocprofv3 kernel-trace stats + separate PMC passes
 # (FETCH_SIZE / WRITE_SIZE / MFMA busy) of the same command, into gpurun_out/$1.
-#   DTYPE=fp32|fp32x3|bf16 (default fp32x3, the bench headline); fold with
+#   DTYPE=fp32|fp32x3|bf16 (default fp32h2, the bench headline); fold with
 #   python tools/profile_summary.py gpurun_out/$1 <tag> $DTYPE
 set -e
 export TMPDIR=/tmp
 O=gpurun_out/${1:-benchprof}
-DTYPE=${DTYPE:-fp32x3}
-if [ "$DTYPE" = fp32 ]; then MOPS=SQ_INSTS_VALU_MFMA_MOPS_F32; else MOPS=SQ_INSTS_VALU_MFMA_MOPS_BF16; fi
+DTYPE=${DTYPE:-fp32h2}
+case $DTYPE in
+  fp32) MOPS=SQ_INSTS_VALU_MFMA_MOPS_F32 ;;
+  fp32h2) MOPS=SQ_INSTS_VALU_MFMA_MOPS_F16 ;;
+  *) MOPS=SQ_INSTS_VALU_MFMA_MOPS_BF16 ;;
+esac
 mkdir -p $O
 timeout -k 10 400 python bench.py --dtype $DTYPE > $O/bench.json 2> $O/bench.err
 B="python bench.py --no-cpu-baseline --dtype $DTYPE"
