@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 2
+#define PNR_ABI_VERSION 3
 
 enum {
   PNR_OK = 0,
@@ -301,7 +301,11 @@ int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s, const pnr_
  * (|W 2^-s| < 16 so 2^11 Wh stays in f16), planes [t][T][Wh, Wl][lane][8],
  * scale[l] = 2^(s_l - 11).  Activations must stay inside the f16 range
  * (|x| < 65504): a launch where one does not sets *range_flag = 1 (device
- * int, caller-owned, may be NULL) and its outputs are not valid. */
+ * int, caller-owned, may be NULL) and its outputs are not valid.
+ * Colour branch (point_aggregators.py:630-638): with wc1a..wc3h set it runs on
+ * the same f16-split MFMA (k_color_h2; color_branch.0 split into columns
+ * 0..143 and 144..279 + bias, both packed with ONE layer scale cscale[0]);
+ * with wc1a NULL on the fp32 MFMA (k_color) like pnr_aggregate_fwd. */
 typedef struct {
   const void* w1bh;   /* block1.0 columns 224..283 */
   const void* w2h;    /* block1.2 + bias           */
@@ -309,6 +313,11 @@ typedef struct {
   const void* w4h;    /* block3.2 + bias           */
   float scale[4];
   int32_t* range_flag;
+  const void* wc1a;   /* color_branch.0 columns 0..143          (NULL: fp32 colour branch) */
+  const void* wc1b;   /* color_branch.0 columns 144..279 + bias */
+  const void* wc2h;   /* color_branch.2 + bias                  */
+  const void* wc3h;   /* color_branch.4 + bias                  */
+  float cscale[3];
 } pnr_mlp_h2;
 int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_h2* wh,
                          float* out_feat, float* out_weight, float* out_conf, void* scratch,

@@ -138,7 +138,7 @@ def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Ten
     return F.view(-1)
 
 
-H2_PAD = X3_PAD   # same weight ring depth in k_pairs_h2
+H2_PAD = 8        # >= the weight ring depth of k_pairs_h2 / k_color_h2 (PNR_H2_WD)
 H2_WMAX = 16.0    # |W 2^-s| < 16, so 2^11 Wh (made in registers) stays inside f16
 
 
@@ -152,7 +152,21 @@ def split2_f16(W: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return wh, wl
 
 
-def frag_pack_h2(W: torch.Tensor, bias: torch.Tensor | None = None) -> tuple[torch.Tensor, float]:
+def h2_shift(W: torch.Tensor, bias: torch.Tensor | None = None) -> int:
+    """Smallest s >= 0 with max|2^-s [W | bias]| < H2_WMAX (frag_pack_h2)."""
+    amax = float(W.abs().max()) if W.numel() else 0.0
+    if bias is not None and bias.numel():
+        amax = max(amax, float(bias.abs().max()))
+    if not np.isfinite(amax):
+        raise L.PnrError("frag_pack_h2: non-finite weight")
+    s = 0
+    while amax * 2.0 ** -s >= H2_WMAX:
+        s += 1
+    return s
+
+
+def frag_pack_h2(W: torch.Tensor, bias: torch.Tensor | None = None,
+                 shift: int | None = None) -> tuple[torch.Tensor, float]:
     """Split-f16 A-operand packs for pnr_aggregate_fwd_h2 -> (pack, layer scale):
     F[t][T][plane][lane][j] = plane of (2^-s W')[32T + (lane & 31)][16t + 8(lane >> 5) + j],
     W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus H2_PAD zero ones, planes
@@ -167,12 +181,9 @@ def frag_pack_h2(W: torch.Tensor, bias: torch.Tensor | None = None) -> tuple[tor
     Wp[:, :kin] = W.float()
     if bias is not None:
         Wp[:, kin] = bias.float()
-    amax = float(Wp.abs().max()) if Wp.numel() else 0.0
-    if not np.isfinite(amax):
-        raise L.PnrError("frag_pack_h2: non-finite weight")
-    s = 0
-    while amax * 2.0 ** -s >= H2_WMAX:
-        s += 1
+    s = h2_shift(Wp) if shift is None else int(shift)   # shift: one scale for the parts of a split layer
+    if float(Wp.abs().max()) * 2.0 ** -s >= H2_WMAX:
+        raise L.PnrError("frag_pack_h2: shift too small for the weights")
     Wp = (Wp * 2.0 ** -s).view(out_f, tot, 2, 8)                       # k = 16t + 8h + j
     planes = torch.stack(split2_f16(Wp), 0)                             # [2][out][t][h][j]
     F = planes.view(2, NT, 32, tot, 2, 8).permute(3, 1, 0, 4, 2, 5).contiguous()   # [t][T][pl][h][r][j]
@@ -293,15 +304,34 @@ class PointAggregator(nn.Module):
         if getattr(self, "_packedh2", None) is not None and key == self._packedh2_key:
             return self._packedh2
         with torch.no_grad():
-            b1, b3 = self.block1, self.block3
+            b1, b3, cb = self.block1, self.block3, self.color_branch
             packs = [frag_pack_h2(b1[0].weight[:, 224:]), frag_pack_h2(b1[2].weight, b1[2].bias),
                      frag_pack_h2(b3[0].weight, b3[0].bias), frag_pack_h2(b3[2].weight, b3[2].bias)]
+            # colour layer 1 in two 144-row halves sharing one scale (k_color_h2)
+            s1 = h2_shift(cb[0].weight, cb[0].bias)
+            cpacks = [frag_pack_h2(cb[0].weight[:, :144], shift=s1),
+                      frag_pack_h2(cb[0].weight[:, 144:], cb[0].bias, shift=s1),
+                      frag_pack_h2(cb[2].weight, cb[2].bias), frag_pack_h2(cb[4].weight, cb[4].bias)]
         flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
-        t = dict(w1bh=packs[0][0], w2h=packs[1][0], w3h=packs[2][0], w4h=packs[3][0], range_flag=flag)
+        t = dict(w1bh=packs[0][0], w2h=packs[1][0], w3h=packs[2][0], w4h=packs[3][0], range_flag=flag,
+                 wc1a=cpacks[0][0], wc1b=cpacks[1][0], wc2h=cpacks[2][0], wc3h=cpacks[3][0])
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
-                    (L.c_float * 4)(*(p[1] for p in packs)), flag.data_ptr())
+                    (L.c_float * 4)(*(p[1] for p in packs)), flag.data_ptr(),
+                    *(t[k].data_ptr() for k in ("wc1a", "wc1b", "wc2h", "wc3h")),
+                    (L.c_float * 3)(cpacks[1][1], cpacks[2][1], cpacks[3][1]))
         self._packedh2, self._packedh2_key = (m, t), key
         return self._packedh2
+
+    def h2_key(self):
+        """Identity of the current weights (storage + version of every
+        parameter), the key packed_h2() caches on."""
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def h2_reset_range(self):
+        """Clear the h2 range flag (after the caller has acted on it)."""
+        pk = getattr(self, "_packedh2", None)
+        if pk is not None:
+            pk[1]["range_flag"].zero_()
 
     def h2_range_ok(self) -> bool:
         """False when a pnr_aggregate_fwd_h2 launch since the packs were built

@@ -100,7 +100,11 @@ __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, cons
 __device__ __forceinline__ void splith(float a, float b, unsigned& x0, unsigned& x1) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#if defined(PNR_ABLATE) && (PNR_ABLATE & 1024)   // timing only: flush |x| < 2^-13 (no f16 subnormals)
+  const f2 v = {fabsf(a) < 1.220703125e-4f ? 0.f : a, fabsf(b) < 1.220703125e-4f ? 0.f : b};
+#else
   const f2 v = {a, b};
+#endif
   const h2 hi = __builtin_convertvector(v, h2);
   const f2 r = (v - __builtin_convertvector(hi, f2)) * 2048.f;
   const h2 lo = __builtin_convertvector(r, h2);
@@ -133,5 +137,9 @@ template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
                        const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
                        float* out_conf, hipStream_t st);
+// k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
+// color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
+int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
+                    int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st);
 
 }  // namespace pnr

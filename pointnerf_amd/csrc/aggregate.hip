@@ -1274,6 +1274,13 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
                 "aggregate_h2: split packs must be 16-B aligned");
   for (int i = 0; i < 4; ++i)
     PNR_CHECK_ARG(wh->scale[i] > 0.f && wh->scale[i] < 1e30f, "aggregate_h2: bad layer scale %d", i);
+  if (wh->wc1a) {
+    PNR_CHECK_ARG(wh->wc1b && wh->wc2h && wh->wc3h, "aggregate_h2: partial colour-branch packs");
+    PNR_CHECK_ARG((((uintptr_t)wh->wc1a | (uintptr_t)wh->wc1b | (uintptr_t)wh->wc2h | (uintptr_t)wh->wc3h) & 15) == 0,
+                  "aggregate_h2: colour packs must be 16-B aligned");
+    for (int i = 0; i < 3; ++i)
+      PNR_CHECK_ARG(wh->cscale[i] > 0.f && wh->cscale[i] < 1e30f, "aggregate_h2: bad colour layer scale %d", i);
+  }
   if (s->n_max <= 0) return PNR_OK;
   AggArgs a;
   a.pts = *pts;
@@ -1288,11 +1295,15 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
   SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
                {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
                wh->range_flag};
-  // k_point_pre (fp32 P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color
+  // k_point_pre (fp32 P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color_h2 / k_color
   if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
   if ((rc = launch_pairs_split<true>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
                                      st)))
     return rc;
+  if (wh->wc1a) {
+    const void* cp[4] = {wh->wc1a, wh->wc1b, wh->wc2h, wh->wc3h};
+    return launch_color_h2(a.s, a.w, cp, wh->cscale, wh->range_flag, a.hid, a.vmask, out_feat, st);
+  }
   return launch_t<false>(a, st, kStageColor);
 }
 

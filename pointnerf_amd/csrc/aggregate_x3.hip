@@ -66,6 +66,9 @@ constexpr float kF16Max = 65504.f;
 #ifndef PNR_X3_PRIO
 #define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
 #endif
+#ifndef PNR_CONS_PRIO
+#define PNR_CONS_PRIO 0
+#endif
 #ifndef PNR_TRACE
 #define PNR_TRACE 0   // dev-only: per-phase s_memtime stamps of block 0 (pnr_debug_x3_trace)
 #endif
@@ -104,7 +107,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
 }
 
 // this wave's 2 neuron tiles of k-step t, NPW planes each; voff = (T0 * NPW * 64 + lane) * 16
-template <bool H>
+template <bool H, int NTK = 8>
 __device__ __forceinline__ void load_w(uint4 (&a)[2][XL<H>::NPW], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
   constexpr int NPW = XL<H>::NPW;
 #pragma unroll
@@ -113,29 +116,34 @@ __device__ __forceinline__ void load_w(uint4 (&a)[2][XL<H>::NPW], __amdgpu_buffe
     for (int pl = 0; pl < NPW; ++pl)
       a[T][pl] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * 8 + T) * NPW * 1024, 0));
+                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * NTK + T) * NPW * 1024, 0));
 }
 
-constexpr int kWD = 3;   // weight ring depth (k-steps in flight); the packs carry kWD zero steps
-
+// weight ring depth (k-steps in flight); the packs carry >= kWD zero steps
+// (X3_PAD / H2_PAD in aggregator.py)
+#ifndef PNR_H2_WD
+#define PNR_H2_WD 3
+#endif
 template <bool H>
 struct WRing {
+  static constexpr int kWD = H ? PNR_H2_WD : 3;
   uint4 a[kWD][2][XL<H>::NPW];
 };
 
-template <bool H>
+template <bool H, int NTK = 8>
 __device__ __forceinline__ void prime(WRing<H>& w, __amdgpu_buffer_rsrc_t rs, int voff) {
 #pragma unroll
-  for (int d = 0; d < kWD; ++d) load_w<H>(w.a[d], rs, voff, d);
+  for (int d = 0; d < WRing<H>::kWD; ++d) load_w<H, NTK>(w.a[d], rs, voff, d);
 }
 
 // Y^T += W . X^T over nsteps 16-k steps; X^T = the bf16 planes at `planes`
 // (plane stride pstride bytes, 64 pairs per 8-row group).  Weights kWD steps
-// ahead in the ring (slot d: steps = d mod kWD), B one step ahead.
-template <bool H>
+// ahead in the ring (slot d: steps = d mod kWD), B one step ahead.  NTK: neuron
+// tiles per k-step in the pack (256 outputs: 8, the colour branch: 4).
+template <bool H, int NTK = 8>
 __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_buffer_rsrc_t rs, int voff,
                                       const char* planes, int pstride, int nsteps, int lane) {
-  constexpr int NPL = XL<H>::NPL, NPW = XL<H>::NPW;
+  constexpr int NPL = XL<H>::NPL, NPW = XL<H>::NPW, kWD = WRing<H>::kWD;
   const int c = lane & 31, h = lane >> 5;
   const char* base = planes + (h * kXT + c) * 16;
   auto ldb = [&](int t, int pt, uint4 (&bb)[NPL]) {
@@ -165,16 +173,26 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
     for (int T = 0; T < 2; ++T)
       a[T][pl] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * 8 + T) * NPW * 1024, 0));
+                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * NTK + T) * NPW * 1024, 0));
   };
   auto bl = [&](int tn, int pt, int pl) {
     if (!(PNR_ABLATE & 64))   // (64: timing only, B fixed)
       b[pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
   };
   // h2 step per half: Ws.Xh, Wl.Xh, Wh.Xl (Ws = 2^11 Wh, made in registers)
-  auto step_h = [&](uint4 (&a)[2][NPW], int t) {
+  // Ws = 2^11 Wh of the NEXT step is made in the middle of this one (scl), so
+  // the v_pk_mul_f16 results are never waited on by the MFMA right after them.
+  uint4 scl[2];
+  auto scale_next = [&](const uint4 (&an)[2][NPW], int T) {   // one tile per MFMA gap (4 v_pk_mul_f16)
+    scl[T] = (PNR_ABLATE & 512) ? an[T][0] : f16x8_scale2048(an[T][0]);   // (512: timing only)
+  };
+  if constexpr (H) {
+    scale_next(w.a[0], 0);
+    scale_next(w.a[0], 1);
+  }
+  auto step_h = [&](uint4 (&a)[2][NPW], const uint4 (&an)[2][NPW], int t) {
     const int tn = t + 1 < nsteps ? t + 1 : t;
-    const uint4 s0 = f16x8_scale2048(a[0][0]), s1 = f16x8_scale2048(a[1][0]);
+    const uint4 s0 = scl[0], s1 = scl[1];
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       mm(pt, s0, s1, b[pt][0]);                                // Ws.Xh
@@ -182,18 +200,20 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
       mm(pt, a[0][1], a[1][1], b[pt][0]);                      // Wl.Xh
       __builtin_amdgcn_sched_barrier(0);
       if (pt == 1) wl(a, 1, t + kWD);
+      if (pt == 0) scale_next(an, 0);
       bl(tn, pt, 0);
       __builtin_amdgcn_sched_barrier(0);
       mm(pt, a[0][0], a[1][0], b[pt][1]);                      // Wh.Xl
       __builtin_amdgcn_sched_barrier(0);
       bl(tn, pt, 1);
+      if (pt == 0) scale_next(an, 1);
       if (pt == 1) wl(a, 0, t + kWD);   // packs carry kWD zero steps
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto step = [&](uint4 (&a)[2][NPW], int t) {
+  auto step = [&](uint4 (&a)[2][NPW], const uint4 (&an)[2][NPW], int t) {
     if constexpr (H) {
-      step_h(a, t);
+      step_h(a, an, t);
     } else {
       const int tn = t + 1 < nsteps ? t + 1 : t;
 #pragma unroll
@@ -227,18 +247,18 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
 #pragma unroll 1
   for (; t + kWD <= nsteps; t += kWD) {
 #pragma unroll
-    for (int d = 0; d < kWD; ++d) step(w.a[d], t + d);
+    for (int d = 0; d < kWD; ++d) step(w.a[d], w.a[(d + 1) % kWD], t + d);
   }
 #pragma unroll
   for (int d = 0; d < kWD - 1; ++d)
-    if (t + d < nsteps) step(w.a[d], t + d);   // the ring then holds padding; prime() refills it
+    if (t + d < nsteps) step(w.a[d], w.a[d + 1], t + d);   // the ring then holds padding; prime() refills it
 }
 
 // lrelu(mul * acc) -> layer-input planes, rows 32(T0+T) + 8q + 4h + i: one
 // ds_write_b64 per plane and quad.  h2: amax tracks max |activation| (f16 range).
 template <bool H>
 __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, float s, float mul, int lane,
-                                          int T0, float& amax) {
+                                          int T0, float& amax, int pstride = kPlaneX) {
   const int c = lane & 31, h = lane >> 5;
   if constexpr (H) {
 #pragma unroll
@@ -260,7 +280,7 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
           splith(y[2], y[3], b0, b1);
           char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
           *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
-          *reinterpret_cast<uint2*>(d + kPlaneX) = make_uint2(a1, b1);
+          *reinterpret_cast<uint2*>(d + pstride) = make_uint2(a1, b1);
         }
     return;
   }
@@ -440,40 +460,39 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
 }
 
 // 5-band PE of the rotated 6-d distance of this lane's pair -> rows 2e (sin),
-// 2e + 1 (cos), e = 5 ch + f, of the PE planes; producer wave pw takes e = pw (mod 4)
-template <bool H>
-__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6], int e_lo, int e_hi) {
+// 2e + 1 (cos), e = 5 ch + f, of the PE planes, for channels [CH0, CH1);
+// producer wave pw takes the frequencies f = pw (mod 4) of every channel.  The
+// channel loop is unrolled (dr6[ch] stays in registers) and f is wave-uniform.
+template <bool H, int CH0, int CH1>
+__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6]) {
   using L = XL<H>;
-  if (pw == 0 && e_lo == 0) {   // rows 60..63: the 4th 16-k step reads them
+  if (pw == 0 && CH0 == 0) {   // rows 60..63: the 4th 16-k step reads them
     char* pz = lds + L::OffPE + (7 * kXT + lane) * 16 + 8;
 #pragma unroll
     for (int pl = 0; pl < L::NPL; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
   }
   if (!(PNR_ABLATE & 2)) {
+    const int f0 = __builtin_amdgcn_readfirstlane(pw);
+#pragma unroll
+    for (int ch = CH0; ch < CH1; ++ch) {
 #pragma unroll 1
-    for (int e = e_lo + pw; e < e_hi; e += 4) {
-      const int ch = e / 5, f = e - 5 * ch;
-      float dc = dr6[0];
-      dc = ch == 1 ? dr6[1] : dc;
-      dc = ch == 2 ? dr6[2] : dc;
-      dc = ch == 3 ? dr6[3] : dc;
-      dc = ch == 4 ? dr6[4] : dc;
-      dc = ch == 5 ? dr6[5] : dc;
-      float sn, cs;
-      sincosf(dc * (float)(1 << f), &sn, &cs);
-      const int r = 2 * e;
-      char* d = lds + L::OffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
-      if constexpr (H) {
-        unsigned x0, x1;
-        splith(sn, cs, x0, x1);
-        *reinterpret_cast<unsigned*>(d) = x0;
-        *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
-      } else {
-        unsigned x0, x1, x2;
-        split2(sn, cs, x0, x1, x2);
-        *reinterpret_cast<unsigned*>(d) = x0;
-        *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
-        *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
+      for (int f = f0; f < 5; f += 4) {
+        float sn, cs;
+        sincosf(dr6[ch] * (float)(1 << f), &sn, &cs);
+        const int r = 2 * (5 * ch + f);
+        char* d = lds + L::OffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
+        if constexpr (H) {
+          unsigned x0, x1;
+          splith(sn, cs, x0, x1);
+          *reinterpret_cast<unsigned*>(d) = x0;
+          *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+        } else {
+          unsigned x0, x1, x2;
+          split2(sn, cs, x0, x1, x2);
+          *reinterpret_cast<unsigned*>(d) = x0;
+          *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+          *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
+        }
       }
     }
   }
@@ -531,6 +550,9 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
   // layer output factors (h2: 2^(s-11) of the pre-scaled f16 packs; x3: 1, unused)
   const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
   float amax = 0.f;   // h2: max |split activation| (f16 range check)
+#if PNR_CONS_PRIO
+  __builtin_amdgcn_s_setprio(PNR_CONS_PRIO);   // consumer (MFMA) issue priority
+#endif
   WRing<H> wr;
   f32x16 acc[4];
   prime<H>(wr, r1, voff);
@@ -737,7 +759,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   gather_row(A, blockIdx.x, lane, g);
   gather_sample(A, lane, g);
   gather<H>(A, g, 0, lds, pw, lane, dr6);
-  pe_planes<H>(lds, pw, lane, dr6, 0, 30);
+  pe_planes<H, 0, 6>(lds, pw, lane, dr6);
   X3_SYNC();   // P0: prow of the first tile visible to all producers
   p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
   X3_SYNC();   // S0
@@ -765,11 +787,11 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
       p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
     X3_TR(1, 4);
     X3_SYNC();   // S4
-    if (!(PNR_ABLATE & 256)) pe_planes<H>(lds, pw, lane, dr6, 0, 16);   // during block3.0 (PE planes free since S1)
+    if (!(PNR_ABLATE & 256)) pe_planes<H, 0, 3>(lds, pw, lane, dr6);   // during block3.0 (PE planes free since S1)
     X3_SYNC();   // S5
     X3_TR(1, 5);
     X3_SYNC();   // S6
-    if (!(PNR_ABLATE & 256)) pe_planes<H>(lds, pw, lane, dr6, 16, 30);   // during block3.2
+    if (!(PNR_ABLATE & 256)) pe_planes<H, 3, 6>(lds, pw, lane, dr6);   // during block3.2
     X3_SYNC();   // S7
   }
   if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
@@ -792,7 +814,182 @@ __device__ __forceinline__ void pairs_body(const X3Args& A) {
 __global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) { pairs_body<false>(A); }
 __global__ void __launch_bounds__(512, 1) k_pairs_h2(X3Args A) { pairs_body<true>(A); }
 
+// ---------------------------------------------------------------------------
+// k_color_h2: the colour branch 280 -> 128 -> 128 -> 128 (LeakyReLU each,
+// point_aggregators.py:630-638) on the input [hid (K-summed features),
+// PE_4(R.viewdir) sin block, cos block] (:506-512), as fp32-accurate f16-split
+// GEMMs on the machinery of k_pairs_h2.  A 2-wave workgroup owns 64 valid
+// samples; wave w owns output tiles {2w, 2w+1} for both 32-sample halves (the
+// `layer` step: every weight fragment and every B fragment feeds two MFMAs).
+// Layer inputs sit in split planes [2][18 row groups][64 samples][8 f16]
+// (37 KB, four workgroups = two waves per SIMD per CU, so one workgroup's hid
+// loads hide behind another's MFMAs): colour layer 1 runs as two 144-row halves
+// (packs wc1a = columns 0..143, wc1b = columns 144..279 + bias), layers 2 and
+// 3 as 129-row GEMMs with the bias row.
+constexpr int kCG = 18;                       // 8-row groups per half (144 rows)
+constexpr int kCPlane = kCG * kXT * 16;       // bytes per f16 plane
+constexpr size_t kColH2Lds = 2 * (size_t)kCPlane;
+
+struct ColH2Args {
+  pnr_samples s;
+  pnr_mlp w;
+  const void* pack[4];   // wc1a, wc1b, wc2, wc3 (frag_pack_h2, 4 neuron tiles per k-step)
+  float scale[3];        // per-layer output factor 2^(s - 11)
+  int32_t* range_flag;
+  const float* hid;
+  const int32_t* vmask;
+  float* out_feat;
+};
+
+// hid rows [g0, g0 + ng) x 8 of the tile's 64 samples -> planes (zero rows for
+// samples past n or without a valid neighbour, as k_color).  Item (sample s,
+// group gl) per lane: 16 samples x 4 groups per wave-instruction, so a global
+// read is 16 rows x 128 contiguous bytes and an LDS write 16 x 16 contiguous bytes.
+__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t v0, int64_t n, int g0, int ng,
+                                               float& amax) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 10; ++u) {
+    const int q = 2 * u + wid;
+    const int s = (lane & 15) + 16 * (q & 3), gl = (lane >> 4) + 4 * (q >> 2);
+    if (gl >= ng) continue;
+    const int64_t v = v0 + s;
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (v < n && A.vmask[v] != 0) {
+      const f32x4n* src = reinterpret_cast<const f32x4n*>(A.hid + v * kHid + 8 * (g0 + gl));
+      const f32x4n a = __builtin_nontemporal_load(src), b = __builtin_nontemporal_load(src + 1);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    }
+    store_group<true>(lds, kCPlane, gl, s, x, amax);
+  }
+}
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) k_color_h2(ColH2Args A) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t n = eff_n(A.s);
+  const int64_t ntiles = cdiv(n, kXT);
+  const float neg = A.w.neg_slope;
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  const int T0 = 2 * wid;
+  const int voff = (T0 * 2 * 64 + lane) * 16;
+  const __amdgpu_buffer_rsrc_t r1a = rsrc(A.pack[0]), r1b = rsrc(A.pack[1]), r2 = rsrc(A.pack[2]),
+                               r3 = rsrc(A.pack[3]);
+  float amax = 0.f;
+  WRing<true> wr;
+  f32x16 acc[4];
+  prime<true, 4>(wr, r1a, voff);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t v0 = tile * kXT;
+    // ---------------------------------------------------- layer 1, input rows 0..143 (hid)
+    color_load_hid(A, lds, v0, n, 0, kCG, amax);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    layer<true, 4>(acc, wr, r1a, voff, lds, kCPlane, 9, lane);
+    prime<true, 4>(wr, r1b, voff);
+    __syncthreads();
+    // ---------------------------------------------------- rows 144..255 (hid), 256..279 (view PE), 280 (bias)
+    color_load_hid(A, lds, v0, n, kCG, 14, amax);
+    if (wid == 0) {   // lane = sample: PE_4 of the rotated view direction (k_color's order)
+      const int64_t v = v0 + lane;
+      float vrot[3] = {0.f, 0.f, 0.f};
+      if (v < n) {
+        const int64_t drow = dir_row(A.s, sample_row(A.s, v));
+        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+        mat3(Rw, vd, vrot);
+      }
+      float pe[32];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          float sn, cs;
+          sincosf(vrot[ch] * (float)(1 << f), &sn, &cs);
+          pe[4 * ch + f] = sn;
+          pe[12 + 4 * ch + f] = cs;
+        }
+      pe[24] = 1.f;
+#pragma unroll
+      for (int i = 25; i < 32; ++i) pe[i] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float g8[8] = {pe[8 * q], pe[8 * q + 1], pe[8 * q + 2], pe[8 * q + 3],
+                             pe[8 * q + 4], pe[8 * q + 5], pe[8 * q + 6], pe[8 * q + 7]};
+        store_group<true>(lds, kCPlane, 14 + q, lane, g8, amax);
+      }
+    }
+    __syncthreads();
+    layer<true, 4>(acc, wr, r1b, voff, lds, kCPlane, 9, lane);
+    prime<true, 4>(wr, r2, voff);
+    __syncthreads();
+    // ---------------------------------------------------- layer 2
+    store_act<true>(acc, lds, neg, A.scale[0], lane, T0, amax, kCPlane);
+    if (wid == 0) {   // row 128 = 1 (bias column), 129..143 = 0
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        *reinterpret_cast<uint4*>(lds + pl * kCPlane + (16 * kXT + lane) * 16) =
+            make_uint4(pl == 0 ? XL<true>::kOne : 0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(lds + pl * kCPlane + (17 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    __syncthreads();
+    layer<true, 4>(acc, wr, r2, voff, lds, kCPlane, 9, lane);
+    prime<true, 4>(wr, r3, voff);
+    __syncthreads();
+    // ---------------------------------------------------- layer 3 (bias rows kept)
+    store_act<true>(acc, lds, neg, A.scale[1], lane, T0, amax, kCPlane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    __syncthreads();
+    layer<true, 4>(acc, wr, r3, voff, lds, kCPlane, 9, lane);
+    prime<true, 4>(wr, r1a, voff);   // the next tile
+    // out_feat[v, 1 + 32 (T0 + T) + row] (valid samples only; the others keep their zeros)
+    const float sc3 = A.scale[2];
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int64_t v = v0 + 32 * pt + c;
+      if (v >= n || A.vmask[v] == 0) continue;
+      float* o = A.out_feat + v * (kC + 1) + 1;
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[32 * (T0 + T) + acc_row(r, h)] = lrelu(acc[2 * pt + T][r] * sc3, neg);
+    }
+    __syncthreads();   // the planes are rewritten by the next tile's loads
+  }
+  if (A.range_flag && !(amax < kF16Max)) atomicOr(A.range_flag, 1);   // also catches NaN
+}
+
 }  // namespace
+
+int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
+                    int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_h2),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kColH2Lds));
+    attr = true;
+  }
+  ColH2Args a;
+  a.s = s;
+  a.w = w;
+  for (int i = 0; i < 4; ++i) a.pack[i] = pack[i];
+  for (int i = 0; i < 3; ++i) a.scale[i] = scale[i];
+  a.range_flag = range_flag;
+  a.hid = hid;
+  a.vmask = vmask;
+  a.out_feat = out_feat;
+  hipLaunchKernelGGL(k_color_h2, dim3(grid_for(cdiv(s.n_max, kXT), 1, 256 * 4)), dim3(128), kColH2Lds, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
 
 #if PNR_TRACE
 extern "C" int pnr_debug_x3_trace(unsigned long long* out, int n) {

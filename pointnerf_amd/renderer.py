@@ -112,6 +112,8 @@ class NeuralPointsRayMarching(nn.Module):
         if precision not in PRECISIONS:
             raise L.PnrError(f"precision {precision!r}: one of {PRECISIONS}")
         self.precision = precision
+        self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
+        self.h2_fallbacks = 0
         self.opt = opt
         self.neural_points = neural_points
         self.aggregator = aggregator if aggregator is not None else PointAggregator(opt).to(neural_points.device)
@@ -139,7 +141,32 @@ class NeuralPointsRayMarching(nn.Module):
         unchanged since the previous render_rays call (e.g. the other partial
         frames of one multi-GPU step), so block1.0's per-point half (P1, which
         does not depend on the camera) is taken from that call's scratch
-        instead of recomputed.  The ray chunks of one call always share it."""
+        instead of recomputed.  The ray chunks of one call always share it.
+
+        fp32h2: the f16 split holds activations below 65504 only.  Each call
+        reads the launches' range flag once (a 4-byte read after the last
+        chunk); if an activation left the f16 range, the call is rendered again
+        on the fp32x3 path (bf16 split: same accuracy, fp32 range) and h2 stays
+        off for these weights until they change (``h2_fallbacks`` counts it)."""
+        prec = self.precision
+        if prec == "fp32h2" and self._h2_blocked_key is not None:
+            if self._h2_blocked_key == self.aggregator.h2_key():
+                prec = "fp32x3"
+            else:
+                self._h2_blocked_key = None
+        n_ev = len(events) if events is not None else 0
+        out = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1)
+        if prec == "fp32h2" and not self.aggregator.h2_range_ok():
+            self.aggregator.h2_reset_range()
+            self._h2_blocked_key = self.aggregator.h2_key()
+            self.h2_fallbacks += 1
+            if events is not None:
+                del events[n_ev:]
+            out = self._render_rays("fp32x3", campos, camrot, raydir, near, far, bg_color, force_grid, events,
+                                    False)
+        return out
+
+    def _render_rays(self, precision, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1):
         opt = self.opt
         dev = raydir.device
         L.require_gpu(raydir)
@@ -161,11 +188,11 @@ class NeuralPointsRayMarching(nn.Module):
                 raise L.PnrError("bg_color must have 1 or 128 channels")
         campos = campos.reshape(3).float().contiguous()
         camrot = camrot.reshape(3, 3).float().contiguous()
-        bf16 = self.precision == "bf16"
+        bf16 = precision == "bf16"
         mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
-        if self.precision == "fp32x3":
+        if precision == "fp32x3":
             mlpx, _keepx = self.aggregator.packed_x3()
-        elif self.precision == "fp32h2":
+        elif precision == "fp32h2":
             mlph, _keeph = self.aggregator.packed_h2()
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
@@ -200,12 +227,12 @@ class NeuralPointsRayMarching(nn.Module):
                                                        L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
                                                        L.stream_ptr(dev)),
                         "pnr_aggregate_fwd_bf16")
-            elif self.precision == "fp32x3":
+            elif precision == "fp32x3":
                 L.check(L.lib().pnr_aggregate_fwd_x3(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                                      L.ctypes.byref(mlpx), L.ptr(feat), None, None, L.ptr(scratch),
                                                      scratch.numel() * 4, L.stream_ptr(dev)),
                         "pnr_aggregate_fwd_x3")
-            elif self.precision == "fp32h2":
+            elif precision == "fp32h2":
                 L.check(L.lib().pnr_aggregate_fwd_h2(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
                                                      L.ctypes.byref(mlph), L.ptr(feat), None, None, L.ptr(scratch),
                                                      scratch.numel() * 4, L.stream_ptr(dev)),

@@ -46,7 +46,7 @@ def _setup(sc, cuda, params=None, seed=0):
 SPLITS = ["x3", "h2"]
 
 
-def _both(agg, np_, sc, cuda, used=False, variant="x3"):
+def _both(agg, np_, sc, cuda, used=False, variant="x3", check_range=True):
     """fp32 and split-path features on one query -> (f32 [Sv,129], split [Sv,129]);
     used: P1 only for the referenced points (the training-batch layout)."""
     from pointnerf_amd import _lib as L
@@ -75,7 +75,7 @@ def _both(agg, np_, sc, cuda, used=False, variant="x3"):
                                      None, None, L.ptr(scr), scr.numel() * 4, L.stream_ptr(cuda)), fn)
         outs.append(f)
     torch.cuda.synchronize()
-    if variant == "h2":
+    if variant == "h2" and check_range:
         assert agg.h2_range_ok()
     _keep_used = u if used else None   # noqa: F841 (keeps the used tables alive until here)
     return outs[0].cpu().numpy(), outs[1].cpu().numpy()
@@ -162,24 +162,49 @@ def test_h2_large_weights_prescaled(cuda):
         params[k] = params[k] / np.float32(64.0)   # keep activations O(1)
     for k in ("color_branch.0.weight",):
         params[k] = params[k] / np.float32(64.0)
+    params["color_branch.2.weight"] = params["color_branch.2.weight"] * np.float32(64.0)   # colour pack s > 0
+    params["color_branch.4.weight"] = params["color_branch.4.weight"] / np.float32(64.0)
     agg, np_ = _setup(sc, cuda, params)
     f32, h2 = _both(agg, np_, sc, cuda, variant="h2")
     want = _oracle_features(sc, {k: v.detach().cpu().numpy() for k, v in agg.state_dict().items()})
     np.testing.assert_allclose(h2, want, atol=ATOL, rtol=RTOL)
 
 
-def test_h2_range_flag(cuda):
-    """An activation beyond the f16 range sets the launch's range flag (the
-    outputs of such a launch are invalid and the caller is told)."""
+def test_h2_range_flag_and_fallback(cuda):
+    """An activation beyond the f16 range sets the launch's range flag; the
+    renderer then renders the call again on fp32x3 (bf16 split: same accuracy,
+    fp32 range) -- bit-identical to an fp32x3 render -- and keeps h2 off for
+    those weights until they change."""
     from pointnerf_amd.renderer import NeuralPointsRayMarching
     sc = scene(20000, H=32, W=32, default_conf=None)
     agg, np_ = _setup(sc, cuda, formula_params(salt=0.3))
     m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32h2")
+    mx = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32x3")
     args = [torch.from_numpy(sc[k]).to(cuda) for k in ("campos", "camrot", "raydir")]
     bg = torch.from_numpy(sc["bg"]).to(cuda)
     with torch.no_grad():
         m.render_rays(*args, 2.0, 6.0, bg)
-        assert agg.h2_range_ok()
+        assert agg.h2_range_ok() and m.h2_fallbacks == 0
         agg.block1[2].bias.fill_(1e6)            # block1.2 outputs ~1e6 > 65504 (repacked: new version)
+        got = m.render_rays(*args, 2.0, 6.0, bg)
+        assert m.h2_fallbacks == 1 and agg.h2_range_ok()   # flag consumed by the fallback
+        want = mx.render_rays(*args, 2.0, 6.0, bg)
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
+        again = m.render_rays(*args, 2.0, 6.0, bg)   # blocked weights: straight to fp32x3
+        assert m.h2_fallbacks == 1 and agg.h2_range_ok()
+        for a, b in zip(again, want):
+            assert torch.equal(a, b)
+        agg.block1[2].bias.fill_(0.0)            # new weights: h2 again, no trip
         m.render_rays(*args, 2.0, 6.0, bg)
+        assert m.h2_fallbacks == 1 and m._h2_blocked_key is None and agg.h2_range_ok()
+
+
+def test_h2_raw_launch_sets_range_flag(cuda):
+    """pnr_aggregate_fwd_h2 itself: out-of-range activation -> *range_flag = 1."""
+    sc = scene(20000, H=32, W=32, default_conf=None)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.3))
+    with torch.no_grad():
+        agg.block1[2].bias.fill_(1e6)
+    _both(agg, np_, sc, cuda, variant="h2", check_range=False)
     assert not agg.h2_range_ok()

@@ -15,7 +15,7 @@ def main():
     import bench
     dev = torch.device("cuda:0")
     opt, pts, feats, agg, model = bench.build_scene(argparse.Namespace(points=2_000_000), dev)
-    model.precision = "fp32x3"
+    model.precision = os.environ.get("PNR_PREC", "fp32h2")
     campos, camrot, rd = bench.cameras(1, 800, 800)[0]
     cp, cr, rd = [torch.from_numpy(x).to(dev) for x in (campos, camrot, rd)]
     bg = torch.rand(128, device=dev)
