@@ -300,17 +300,19 @@ int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s, const pnr_
  * pointnerf_amd.aggregator.frag_pack_h2: layer weights pre-scaled by 2^-s
  * (|W 2^-s| < 16 so 2^11 Wh stays in f16), planes [t][T][Wh, Wl][lane][8],
  * scale[l] = 2^(s_l - 11).  Activations must stay inside the f16 range
- * (|x| < 65504): a launch where one does not sets *range_flag = 1 (device
- * int, caller-owned, may be NULL) and its outputs are not valid.
+ * (|x| < 65504): one that does not has an infinite high half, which makes
+ * every output it reaches inf or NaN; a launch with a non-finite output sets
+ * *range_flag = 1 (device int, caller-owned, may be NULL) and its outputs are
+ * not valid (the renderer then re-renders on pnr_aggregate_fwd_x3).
  * Colour branch (point_aggregators.py:630-638): with wc1a..wc3h set it runs on
  * the same f16-split MFMA (k_color_h2; color_branch.0 split into columns
  * 0..143 and 144..279 + bias, both packed with ONE layer scale cscale[0]);
  * with wc1a NULL on the fp32 MFMA (k_color) like pnr_aggregate_fwd. */
 typedef struct {
-  const void* w1bh;   /* block1.0 columns 224..283 */
-  const void* w2h;    /* block1.2 + bias           */
-  const void* w3h;    /* block3.0 + bias           */
-  const void* w4h;    /* block3.2 + bias           */
+  const void* w1bh;   /* block1.0 columns 224..283                              */
+  const void* w2h;    /* block1.2, NO bias column (the kernel adds w->b2 in fp32) */
+  const void* w3h;    /* block3.0 + bias                                         */
+  const void* w4h;    /* block3.2, NO bias column (the kernel adds w->b4 in fp32) */
   float scale[4];
   int32_t* range_flag;
   const void* wc1a;   /* color_branch.0 columns 0..143          (NULL: fp32 colour branch) */

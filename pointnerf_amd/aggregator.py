@@ -305,8 +305,10 @@ class PointAggregator(nn.Module):
             return self._packedh2
         with torch.no_grad():
             b1, b3, cb = self.block1, self.block3, self.color_branch
-            packs = [frag_pack_h2(b1[0].weight[:, 224:]), frag_pack_h2(b1[2].weight, b1[2].bias),
-                     frag_pack_h2(b3[0].weight, b3[0].bias), frag_pack_h2(b3[2].weight, b3[2].bias)]
+            # block1.2 / block3.2 without the bias column: k_pairs_h2 starts their
+            # accumulators at bias / scale (pnr_mlp b2 / b4)
+            packs = [frag_pack_h2(b1[0].weight[:, 224:]), frag_pack_h2(b1[2].weight),
+                     frag_pack_h2(b3[0].weight, b3[0].bias), frag_pack_h2(b3[2].weight)]
             # colour layer 1 in two 144-row halves sharing one scale (k_color_h2)
             s1 = h2_shift(cb[0].weight, cb[0].bias)
             cpacks = [frag_pack_h2(cb[0].weight[:, :144], shift=s1),

@@ -61,7 +61,6 @@ struct XL {
   static_assert(kXT * kP1Pitch * 4 <= NPL * kPlaneX, "parked P1 fits the layer-input area");
   static_assert(Lds <= 160 * 1024, "LDS budget");
 };
-constexpr float kF16Max = 65504.f;
 
 #ifndef PNR_X3_PRIO
 #define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
@@ -255,10 +254,12 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
 }
 
 // lrelu(mul * acc) -> layer-input planes, rows 32(T0+T) + 8q + 4h + i: one
-// ds_write_b64 per plane and quad.  h2: amax tracks max |activation| (f16 range).
+// ds_write_b64 per plane and quad.  (h2: an activation beyond the f16 range
+// becomes an infinite high half; the launch detects it from its non-finite
+// outputs, see the range flag, instead of testing every activation.)
 template <bool H>
 __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, float s, float mul, int lane,
-                                          int T0, float& amax, int pstride = kPlaneX) {
+                                          int T0, int pstride = kPlaneX) {
   const int c = lane & 31, h = lane >> 5;
   if constexpr (H) {
 #pragma unroll
@@ -273,7 +274,6 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
           for (int i = 0; i < 4; ++i) {
             const float x = v[4 * q + i] * mul;
             y[i] = fmaxf(x, s * x);
-            amax = fmaxf(amax, fabsf(y[i]));
           }
           unsigned a0, a1, b0, b1;
           splith(y[0], y[1], a0, a1);
@@ -316,18 +316,41 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
       }
 }
 
+// h2: block1.2 / block3.2 biases start the accumulators (acc = b / scale,
+// exact: the scale is a power of two) instead of riding in the GEMM as an
+// extra input row, so those layers take 16 k-steps instead of 17.
+template <bool H>
+__device__ __forceinline__ void acc_init(f32x16 (&acc)[4], const float* bias, float inv_scale, int lane, int T0) {
+  if constexpr (H) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(bias + 32 * (T0 + T) + 8 * q + 4 * h);
+        const float v[4] = {b.x * inv_scale, b.y * inv_scale, b.z * inv_scale, b.w * inv_scale};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[T][4 * q + i] = v[i];
+          acc[2 + T][4 * q + i] = v[i];
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+  }
+}
+constexpr int kBiasSteps(bool H) { return H ? 16 : 17; }   // block1.2 / block3.2 k-steps
+
 // 8 fp32 rows of one pair -> row group g of the NPL planes (ds_write_b128 each)
 template <bool H>
-__device__ __forceinline__ void store_group(char* planes, int pstride, int g, int pair, const float (&v)[8],
-                                            float& amax) {
+__device__ __forceinline__ void store_group(char* planes, int pstride, int g, int pair, const float (&v)[8]) {
   if constexpr (H) {
     uint4 p0, p1;
     splith(v[0], v[1], p0.x, p1.x);
     splith(v[2], v[3], p0.y, p1.y);
     splith(v[4], v[5], p0.z, p1.z);
     splith(v[6], v[7], p0.w, p1.w);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
     char* d = planes + (g * kXT + pair) * 16;
     *reinterpret_cast<uint4*>(d) = p0;
     *reinterpret_cast<uint4*>(d + pstride) = p1;
@@ -460,41 +483,54 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
 }
 
 // 5-band PE of the rotated 6-d distance of this lane's pair -> rows 2e (sin),
-// 2e + 1 (cos), e = 5 ch + f, of the PE planes, for channels [CH0, CH1);
-// producer wave pw takes the frequencies f = pw (mod 4) of every channel.  The
-// channel loop is unrolled (dr6[ch] stays in registers) and f is wave-uniform.
-template <bool H, int CH0, int CH1>
+// 2e + 1 (cos), e = 5 ch + f, of the PE planes (networks.py:175-190).
+// Producer wave pw owns channel ch = pw (PART 0) and ch = 4 + pw (PART 1, pw < 2).
+// Per channel two sincosf (f = 0 and 2) and three angle doublings
+// (sin 2a = 2 sin a cos a, cos 2a = (c - s)(c + s): f = 1 from 0, 3 from 2, 4
+// from 3), as k_point_pre's 3-band PE: at most two doublings from a sincosf.
+template <bool H>
+__device__ __forceinline__ void pe_store(char* lds, int lane, int e, float sn, float cs) {
+  using L = XL<H>;
+  const int r = 2 * e;
+  char* d = lds + L::OffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
+  if constexpr (H) {
+    unsigned x0, x1;
+    splith(sn, cs, x0, x1);
+    *reinterpret_cast<unsigned*>(d) = x0;
+    *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+  } else {
+    unsigned x0, x1, x2;
+    split2(sn, cs, x0, x1, x2);
+    *reinterpret_cast<unsigned*>(d) = x0;
+    *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
+    *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
+  }
+}
+
+template <bool H, int PART>
 __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6]) {
   using L = XL<H>;
-  if (pw == 0 && CH0 == 0) {   // rows 60..63: the 4th 16-k step reads them
+  if (pw == 0 && PART == 0) {   // rows 60..63: the 4th 16-k step reads them
     char* pz = lds + L::OffPE + (7 * kXT + lane) * 16 + 8;
 #pragma unroll
     for (int pl = 0; pl < L::NPL; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
   }
-  if (!(PNR_ABLATE & 2)) {
-    const int f0 = __builtin_amdgcn_readfirstlane(pw);
+  if (PNR_ABLATE & 2) return;
+  const int mine = __builtin_amdgcn_readfirstlane(PART == 0 ? pw : 4 + pw);
 #pragma unroll
-    for (int ch = CH0; ch < CH1; ++ch) {
-#pragma unroll 1
-      for (int f = f0; f < 5; f += 4) {
-        float sn, cs;
-        sincosf(dr6[ch] * (float)(1 << f), &sn, &cs);
-        const int r = 2 * (5 * ch + f);
-        char* d = lds + L::OffPE + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
-        if constexpr (H) {
-          unsigned x0, x1;
-          splith(sn, cs, x0, x1);
-          *reinterpret_cast<unsigned*>(d) = x0;
-          *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
-        } else {
-          unsigned x0, x1, x2;
-          split2(sn, cs, x0, x1, x2);
-          *reinterpret_cast<unsigned*>(d) = x0;
-          *reinterpret_cast<unsigned*>(d + kPlaneP) = x1;
-          *reinterpret_cast<unsigned*>(d + 2 * kPlaneP) = x2;
-        }
-      }
-    }
+  for (int ch = 4 * PART; ch < (PART == 0 ? 4 : 6); ++ch) {
+    if (ch != mine) continue;   // wave-uniform
+    float s0, c0, s2, c2;
+    sincosf(dr6[ch], &s0, &c0);
+    sincosf(dr6[ch] * 4.f, &s2, &c2);
+    const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
+    const float s3 = 2.f * s2 * c2, c3 = (c2 - s2) * (c2 + s2);
+    const float s4 = 2.f * s3 * c3, c4 = (c3 - s3) * (c3 + s3);
+    pe_store<H>(lds, lane, 5 * ch + 0, s0, c0);
+    pe_store<H>(lds, lane, 5 * ch + 1, s1, c1);
+    pe_store<H>(lds, lane, 5 * ch + 2, s2, c2);
+    pe_store<H>(lds, lane, 5 * ch + 3, s3, c3);
+    pe_store<H>(lds, lane, 5 * ch + 4, s4, c4);
   }
 }
 
@@ -549,7 +585,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                                r4 = rsrc(A.wx.pack[3]);
   // layer output factors (h2: 2^(s-11) of the pre-scaled f16 packs; x3: 1, unused)
   const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
-  float amax = 0.f;   // h2: max |split activation| (f16 range check)
+  float chk = 0.f;   // h2: 0 * (tail outputs), NaN once any of them is not finite
 #if PNR_CONS_PRIO
   __builtin_amdgcn_s_setprio(PNR_CONS_PRIO);   // consumer (MFMA) issue priority
 #endif
@@ -594,7 +630,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         }
     X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
     X3_TR(0, 3);
-    store_act<H>(acc, XP, neg, 1.f, lane, T0, amax);
+    store_act<H>(acc, XP, neg, 1.f, lane, T0);
     if (wid == 0) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
@@ -603,24 +639,23 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (33 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    acc_init<H>(acc, A.w.b2, 1.f / sc2, lane, T0);
     X3_TR(0, 4);
     X3_SYNC();   // S2
     X3_TR(0, 5);
     // ------------------------------------------------------------ block1.2
-    layer<H>(acc, wr, r2, voff, XP, kPlaneX, 17, lane);
+    layer<H>(acc, wr, r2, voff, XP, kPlaneX, kBiasSteps(H), lane);
     prime<H>(wr, r3, voff);
     X3_TR(0, 6);
     X3_SYNC();   // S3
     X3_TR(0, 7);
-    store_act<H>(acc, XP, neg, sc2, lane, T0, amax);
+    store_act<H>(acc, XP, neg, sc2, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
       const float* exL = reinterpret_cast<const float*>(lds + L::OffEx) + buf * 8 * kXT;
       float ex[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) ex[e] = exL[e * kXT + lane];
-      store_group<H>(XP, kPlaneX, 32, lane, ex, amax);
+      store_group<H>(XP, kPlaneX, 32, lane, ex);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
@@ -632,19 +667,18 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     X3_TR(0, 9);
     X3_SYNC();   // S5
     X3_TR(0, 10);
-    store_act<H>(acc, XP, neg, sc3, lane, T0, amax);
-    if (wid == 0) {
+    store_act<H>(acc, XP, neg, sc3, lane, T0);
+    if (wid == 0 && !H) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl)
         *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (32 * kXT + lane) * 16) =
             make_uint4(pl == 0 ? L::kOne : 0u, 0u, 0u, 0u);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    acc_init<H>(acc, A.w.b4, 1.f / sc4, lane, T0);
     X3_SYNC();   // S6
     X3_TR(0, 11);
     // ------------------------------------------------------------ block3.2, alpha partials, K sums
-    layer<H>(acc, wr, r4, voff, XP, kPlaneX, 17, lane);
+    layer<H>(acc, wr, r4, voff, XP, kPlaneX, kBiasSteps(H), lane);
     prime<H>(wr, r1, voff);   // the next tile's block1.0
     X3_TR(0, 12);
     if (!(PNR_ABLATE & 4)) {
@@ -691,12 +725,14 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                 float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xf, 0xf, false));
             w2[q] = (b0 ? w4[q + 2] : w4[q]) + recv;
           }
+          if (H) chk = fmaf(0.f, w2[0] + w2[1], chk);
           if (wrt)
             __builtin_nontemporal_store(
                 (f32x2n){w2[0], w2[1]},
                 reinterpret_cast<f32x2n*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h));
         }
         pa_part[pt] += __shfl_xor(pa_part[pt], 32);
+        if (H) chk = fmaf(0.f, pa_part[pt], chk);
       }
       if (h == 0) {
         apart[wid * kXT + c] = pa_part[0];
@@ -710,7 +746,9 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][1] = wall_clock64();
 #endif
-  if (H && A.wx.range_flag && !(amax < kF16Max)) atomicOr(A.wx.range_flag, 1);   // also catches NaN
+  // an f16-split activation beyond 65504 has an infinite high half: every output
+  // it reaches is then inf or NaN (0 x inf = NaN on the empty pairs' zero weights)
+  if (H && A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
 }
 
 // Producer wave pw: P1 rows 16 pw .. 16 pw + 15 of a tile (1 KB each, one
@@ -759,7 +797,8 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   gather_row(A, blockIdx.x, lane, g);
   gather_sample(A, lane, g);
   gather<H>(A, g, 0, lds, pw, lane, dr6);
-  pe_planes<H, 0, 6>(lds, pw, lane, dr6);
+  pe_planes<H, 0>(lds, pw, lane, dr6);
+  pe_planes<H, 1>(lds, pw, lane, dr6);
   X3_SYNC();   // P0: prow of the first tile visible to all producers
   p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
   X3_SYNC();   // S0
@@ -779,19 +818,19 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_SYNC();   // S2
     X3_TR(1, 2);
     // during block1.2: gather (nbuf's arrays are free: their last reader was the previous finalize)
-    if (!(PNR_ABLATE & 256)) gather<H>(A, g, nbuf, lds, pw, lane, dr6);
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, lds, pw, lane, dr6);
     X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
-    if (!(PNR_ABLATE & 256))
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1))
       p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
     X3_TR(1, 4);
     X3_SYNC();   // S4
-    if (!(PNR_ABLATE & 256)) pe_planes<H, 0, 3>(lds, pw, lane, dr6);   // during block3.0 (PE planes free since S1)
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 0>(lds, pw, lane, dr6);   // during block3.0 (PE planes free since S1)
     X3_SYNC();   // S5
     X3_TR(1, 5);
     X3_SYNC();   // S6
-    if (!(PNR_ABLATE & 256)) pe_planes<H, 3, 6>(lds, pw, lane, dr6);   // during block3.2
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 1>(lds, pw, lane, dr6);   // during block3.2
     X3_SYNC();   // S7
   }
   if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
@@ -845,8 +884,7 @@ struct ColH2Args {
 // samples past n or without a valid neighbour, as k_color).  Item (sample s,
 // group gl) per lane: 16 samples x 4 groups per wave-instruction, so a global
 // read is 16 rows x 128 contiguous bytes and an LDS write 16 x 16 contiguous bytes.
-__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t v0, int64_t n, int g0, int ng,
-                                               float& amax) {
+__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t v0, int64_t n, int g0, int ng) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int u = 0; u < 10; ++u) {
@@ -861,7 +899,7 @@ __device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, in
       x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
       x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
     }
-    store_group<true>(lds, kCPlane, gl, s, x, amax);
+    store_group<true>(lds, kCPlane, gl, s, x);
   }
 }
 
@@ -879,14 +917,14 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int voff = (T0 * 2 * 64 + lane) * 16;
   const __amdgpu_buffer_rsrc_t r1a = rsrc(A.pack[0]), r1b = rsrc(A.pack[1]), r2 = rsrc(A.pack[2]),
                                r3 = rsrc(A.pack[3]);
-  float amax = 0.f;
+  float chk = 0.f;   // 0 * (outputs): NaN once any output is not finite (see k_pairs_h2)
   WRing<true> wr;
   f32x16 acc[4];
   prime<true, 4>(wr, r1a, voff);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t v0 = tile * kXT;
     // ---------------------------------------------------- layer 1, input rows 0..143 (hid)
-    color_load_hid(A, lds, v0, n, 0, kCG, amax);
+    color_load_hid(A, lds, v0, n, 0, kCG);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
@@ -894,7 +932,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r1b, voff);
     __syncthreads();
     // ---------------------------------------------------- rows 144..255 (hid), 256..279 (view PE), 280 (bias)
-    color_load_hid(A, lds, v0, n, kCG, 14, amax);
+    color_load_hid(A, lds, v0, n, kCG, 14);
     if (wid == 0) {   // lane = sample: PE_4 of the rotated view direction (k_color's order)
       const int64_t v = v0 + lane;
       float vrot[3] = {0.f, 0.f, 0.f};
@@ -920,7 +958,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int q = 0; q < 4; ++q) {
         const float g8[8] = {pe[8 * q], pe[8 * q + 1], pe[8 * q + 2], pe[8 * q + 3],
                              pe[8 * q + 4], pe[8 * q + 5], pe[8 * q + 6], pe[8 * q + 7]};
-        store_group<true>(lds, kCPlane, 14 + q, lane, g8, amax);
+        store_group<true>(lds, kCPlane, 14 + q, lane, g8);
       }
     }
     __syncthreads();
@@ -928,7 +966,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r2, voff);
     __syncthreads();
     // ---------------------------------------------------- layer 2
-    store_act<true>(acc, lds, neg, A.scale[0], lane, T0, amax, kCPlane);
+    store_act<true>(acc, lds, neg, A.scale[0], lane, T0, kCPlane);
     if (wid == 0) {   // row 128 = 1 (bias column), 129..143 = 0
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) {
@@ -944,7 +982,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r3, voff);
     __syncthreads();
     // ---------------------------------------------------- layer 3 (bias rows kept)
-    store_act<true>(acc, lds, neg, A.scale[1], lane, T0, amax, kCPlane);
+    store_act<true>(acc, lds, neg, A.scale[1], lane, T0, kCPlane);
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
     __syncthreads();
@@ -952,6 +990,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r1a, voff);   // the next tile
     // out_feat[v, 1 + 32 (T0 + T) + row] (valid samples only; the others keep their zeros)
     const float sc3 = A.scale[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) chk = fmaf(0.f, acc[i][r] + acc[i][r + 1], chk);
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int64_t v = v0 + 32 * pt + c;
@@ -964,7 +1006,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     __syncthreads();   // the planes are rewritten by the next tile's loads
   }
-  if (A.range_flag && !(amax < kF16Max)) atomicOr(A.range_flag, 1);   // also catches NaN
+  if (A.range_flag && chk != 0.f) atomicOr(A.range_flag, 1);   // non-finite output: see k_pairs_h2
 }
 
 }  // namespace

@@ -208,3 +208,18 @@ def test_h2_raw_launch_sets_range_flag(cuda):
         agg.block1[2].bias.fill_(1e6)
     _both(agg, np_, sc, cuda, variant="h2", check_range=False)
     assert not agg.h2_range_ok()
+
+
+def test_h2_colour_branch_overflow_sets_flag(cuda):
+    """Overflow only inside the colour branch (k_color_h2): colour layer-1
+    outputs ~1e6 leave the f16 range -> non-finite outputs -> range flag."""
+    sc = scene(20000, H=32, W=32, default_conf=None)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.3))
+    with torch.no_grad():
+        agg.color_branch[0].bias.fill_(1e6)
+    _both(agg, np_, sc, cuda, variant="h2", check_range=False)
+    assert not agg.h2_range_ok()
+    agg.h2_reset_range()
+    with torch.no_grad():
+        agg.color_branch[0].bias.fill_(0.0)
+    _both(agg, np_, sc, cuda, variant="h2")   # asserts the flag stays clear

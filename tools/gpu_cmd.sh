@@ -1,5 +1,5 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py -x -q -s --timeout 200 --timeout-method thread > gpurun_out/t_x3.log 2>&1
+REPS=3 bash tools/ab.sh ref pe
