@@ -52,12 +52,17 @@ struct XL {
   static constexpr unsigned kOne = H ? 0x3C00u : 0x3F80u;   // 1.0 (bias input row)
   static constexpr int OffPE = NPL * kPlaneX;
   static constexpr int OffEx = OffPE + NPL * kPlaneP;       // float [2][8][64]
-  static constexpr int OffWt = OffEx + 2 * 8 * kXT * 4;    // float [2][64]
-  static constexpr int OffPr = OffWt + 2 * kXT * 4;        // int   [2][64]
-  static constexpr int OffSf = OffPr + 2 * kXT * 4;        // int   [2][8]
-  static constexpr int OffAp = OffSf + 2 * kXTS * 4;       // float [4][64]
+  // blend-weight / sample-flag slots: h2 runs a tile's tail one tile later on
+  // the producers (three slots in flight), x3 on the consumers (two)
+  static constexpr int NWB = H ? 3 : 2;
+  static constexpr int OffWt = OffEx + 2 * 8 * kXT * 4;    // float [NWB][64]
+  static constexpr int OffPr = OffWt + NWB * kXT * 4;      // int   [2][64]
+  static constexpr int OffSf = OffPr + 2 * kXT * 4;        // int   [NWB][8]
+  static constexpr int OffAp = OffSf + NWB * kXTS * 4;     // float [4][64] (x3: alpha partials)
   static constexpr int OffWa = OffAp + 4 * kXT * 4;        // float [256] alpha_branch.0 weights
-  static constexpr size_t Lds = (size_t)OffWa + kHid * 4;
+  static constexpr int OffH4 = OffWa + kHid * 4;           // h2: float [64][kP1Pitch] block3.2 accumulators
+  static constexpr size_t Lds = (size_t)OffH4 + (H ? kXT * kP1Pitch * 4 : 0);
+  static_assert(OffSf % 16 == 0 && OffWa % 16 == 0 && OffH4 % 16 == 0, "16-B aligned LDS arrays");
   static_assert(kXT * kP1Pitch * 4 <= NPL * kPlaneX, "parked P1 fits the layer-input area");
   static_assert(Lds <= 160 * 1024, "LDS budget");
 };
@@ -253,6 +258,24 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
     if (t + d < nsteps) step(w.a[d], w.a[d + 1], t + d);   // the ring then holds padding; prime() refills it
 }
 
+// (x0, x1) -> f16 split of y = lrelu(x mul) (splith's planes: hi = f16(y),
+// lo = f16((y - hi) 2^11), bit-identical), from Y = 2^11 y = max(x k, x ks)
+// (k = 2^11 mul, ks = k s; mul is a power of two, so Y is exact) with four
+// v_fma_mix ops: hi = f16(Y 2^-11), lo = f16(Y - 2^11 hi), one rounding each.
+// 4 VALU per pair of values (+ the packed lrelu) instead of splith's 6.
+__device__ __forceinline__ void lrelu_splith(float x0, float x1, float k, float ks, unsigned& hi, unsigned& lo) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 x = {x0, x1};
+  const f2 Y = __builtin_elementwise_max(x * k, x * ks);
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %0, %5, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %0, %5, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(Y.x), "v"(Y.y), "s"(0x1p-11f), "s"(-2048.f));
+}
+
 // lrelu(mul * acc) -> layer-input planes, rows 32(T0+T) + 8q + 4h + i: one
 // ds_write_b64 per plane and quad.  (h2: an activation beyond the f16 range
 // becomes an infinite high half; the launch detects it from its non-finite
@@ -262,6 +285,7 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
                                           int T0, int pstride = kPlaneX) {
   const int c = lane & 31, h = lane >> 5;
   if constexpr (H) {
+    const float k = 2048.f * mul, ks = k * s;   // exact: mul is a power of two
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
@@ -269,15 +293,9 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const f32x16& v = acc[2 * pt + T];
-          float y[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float x = v[4 * q + i] * mul;
-            y[i] = fmaxf(x, s * x);
-          }
           unsigned a0, a1, b0, b1;
-          splith(y[0], y[1], a0, a1);
-          splith(y[2], y[3], b0, b1);
+          lrelu_splith(v[4 * q], v[4 * q + 1], k, ks, a0, a1);
+          lrelu_splith(v[4 * q + 2], v[4 * q + 3], k, ks, b0, b1);
           char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
           *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
           *reinterpret_cast<uint2*>(d + pstride) = make_uint2(a1, b1);
@@ -399,7 +417,7 @@ __device__ __forceinline__ void gather_sample(const X3Args& A, int lane, GatherS
 }
 
 template <bool H>
-__device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, int nb, char* lds, int pw, int lane,
+__device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, int nb, int nw, char* lds, int pw, int lane,
                                        float (&dr6)[6]) {
   using L = XL<H>;
   float Rw[9];
@@ -472,9 +490,9 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
     float* exL = reinterpret_cast<float*>(lds + L::OffEx) + nb * 8 * kXT;
 #pragma unroll
     for (int e = 0; e < 8; ++e) exL[e * kXT + lane] = ex[e];
-    reinterpret_cast<float*>(lds + L::OffWt)[nb * kXT + lane] = wn * confc;
+    reinterpret_cast<float*>(lds + L::OffWt)[nw * kXT + lane] = wn * confc;
     reinterpret_cast<int*>(lds + L::OffPr)[nb * kXT + lane] = valid ? (int)prow : -1;
-    if (k == 0) reinterpret_cast<int*>(lds + L::OffSf)[nb * kXTS + j] = active && samp_valid;
+    if (k == 0) reinterpret_cast<int*>(lds + L::OffSf)[nw * kXTS + j] = active && samp_valid;
     if (active && k < K) {
       if (A.out_weight) A.out_weight[row * K + k] = wn;
       if (A.out_conf) A.out_conf[row * K + k] = confc;
@@ -585,7 +603,6 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                                r4 = rsrc(A.wx.pack[3]);
   // layer output factors (h2: 2^(s-11) of the pre-scaled f16 packs; x3: 1, unused)
   const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
-  float chk = 0.f;   // h2: 0 * (tail outputs), NaN once any of them is not finite
 #if PNR_CONS_PRIO
   __builtin_amdgcn_s_setprio(PNR_CONS_PRIO);   // consumer (MFMA) issue priority
 #endif
@@ -681,7 +698,21 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     layer<H>(acc, wr, r4, voff, XP, kPlaneX, kBiasSteps(H), lane);
     prime<H>(wr, r1, voff);   // the next tile's block1.0
     X3_TR(0, 12);
-    if (!(PNR_ABLATE & 4)) {
+    if constexpr (H) {
+      // block3.2 accumulators -> LDS [pair][row] for the producers' tail (next tile):
+      // one ds_write_b128 per accumulator quad, conflict-free at kP1Pitch
+      float* H4 = reinterpret_cast<float*>(lds + L::OffH4);
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x16& v = acc[2 * pt + T];
+            *reinterpret_cast<float4*>(H4 + (32 * pt + c) * kP1Pitch + 32 * (T0 + T) + 8 * q + 4 * h) =
+                make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+          }
+    } else if (!(PNR_ABLATE & 4)) {
       const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + buf * kXT;
       const int* sflag = reinterpret_cast<const int*>(lds + L::OffSf) + buf * kXTS;
       float pa_part[2] = {0.f, 0.f};
@@ -725,14 +756,12 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                 float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xf, 0xf, false));
             w2[q] = (b0 ? w4[q + 2] : w4[q]) + recv;
           }
-          if (H) chk = fmaf(0.f, w2[0] + w2[1], chk);
           if (wrt)
             __builtin_nontemporal_store(
                 (f32x2n){w2[0], w2[1]},
                 reinterpret_cast<f32x2n*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h));
         }
         pa_part[pt] += __shfl_xor(pa_part[pt], 32);
-        if (H) chk = fmaf(0.f, pa_part[pt], chk);
       }
       if (h == 0) {
         apart[wid * kXT + c] = pa_part[0];
@@ -746,9 +775,6 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][1] = wall_clock64();
 #endif
-  // an f16-split activation beyond 65504 has an infinite high half: every output
-  // it reaches is then inf or NaN (0 x inf = NaN on the empty pairs' zero weights)
-  if (H && A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
 }
 
 // Producer wave pw: P1 rows 16 pw .. 16 pw + 15 of a tile (1 KB each, one
@@ -782,6 +808,86 @@ __device__ __forceinline__ void park_p1(const f32x4n (&r)[16], unsigned empty, c
   }
 }
 
+// h2 tile tail on the producers (one tile late, during the consumers' block1.2):
+// from the block3.2 accumulators the consumers parked in H4, per sample j of
+// the tile (wave pw: samples 2pw, 2pw + 1; lane & 31 = neurons 8ng .. 8ng + 7)
+//   h = lrelu(acc * scale)                    point_aggregators.py (block3)
+//   hid[j] = sum_k wt_k h_k                   (K sums, :622-628)
+//   alpha_k = act(wa . h_k + ba), alpha_j = sum_k wt_k alpha_k   (:608-614)
+// the dot over 256 neurons is a reduce-scatter over the 32 lanes.  chk picks
+// up every output as 0 * x: NaN once one is not finite (an f16-split
+// activation beyond 65504 has an infinite high half, and every output it
+// reaches is inf or NaN, 0 x inf on the empty pairs' zero weights included).
+struct TailState {
+  float hs[8], pa[8];
+};
+
+// PART 0: pairs k = 0..3 of every sample; PART 1: k = 4..7, the reductions and
+// the stores (the halves run in two producer segments, see producer_loop)
+template <int PART>
+__device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int slot, int64_t tile, int pw, int lane,
+                                              TailState& ts, float& chk) {
+  using L = XL<true>;
+  if (PNR_ABLATE & 4) return;
+  const int64_t n = eff_n(A.s);
+  const int j = 2 * pw + (lane >> 5), ng = lane & 31;
+  const float* H4 = reinterpret_cast<const float*>(lds + L::OffH4);
+  const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + slot * kXT + 8 * j;
+  const int sf = reinterpret_cast<const int*>(lds + L::OffSf)[slot * kXTS + j];
+  const float* waL = reinterpret_cast<const float*>(lds + L::OffWa) + 8 * ng;
+  const float sc = A.wx.scale[3], neg = A.w.neg_slope;
+  const float4 wa0 = *reinterpret_cast<const float4*>(waL), wa1 = *reinterpret_cast<const float4*>(waL + 4);
+  const float wa[8] = {wa0.x, wa0.y, wa0.z, wa0.w, wa1.x, wa1.y, wa1.z, wa1.w};
+  const float4 wt0 = *reinterpret_cast<const float4*>(wtL), wt1 = *reinterpret_cast<const float4*>(wtL + 4);
+  const float wt[8] = {wt0.x, wt0.y, wt0.z, wt0.w, wt1.x, wt1.y, wt1.z, wt1.w};
+  float (&hs)[8] = ts.hs;
+  float (&pa)[8] = ts.pa;
+#pragma unroll
+  for (int k = 4 * PART; k < 4 * PART + 4; ++k) {
+    const float* row = H4 + (8 * j + k) * kP1Pitch + 8 * ng;
+    const float4 a = *reinterpret_cast<const float4*>(row), b = *reinterpret_cast<const float4*>(row + 4);
+    const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    float p = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float hv = lrelu(x[i] * sc, neg);
+      p = fmaf(wa[i], hv, p);
+      hs[i] = k == 0 ? wt[0] * hv : fmaf(wt[k], hv, hs[i]);
+    }
+    pa[k] = p;
+  }
+  if (PART == 0) return;
+  // reduce-scatter of pa[0..7] over the 32 lanes: lane ng ends with pair k = ng >> 2
+  const bool b4 = (ng & 16) != 0, b3 = (ng & 8) != 0, b2 = (ng & 4) != 0;
+  float r4[4], r2[2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r4[q] = (b4 ? pa[q + 4] : pa[q]) + __shfl_xor(b4 ? pa[q] : pa[q + 4], 16);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) r2[q] = (b3 ? r4[q + 2] : r4[q]) + __shfl_xor(b3 ? r4[q] : r4[q + 2], 8);
+  float r1 = (b2 ? r2[1] : r2[0]) + __shfl_xor(b2 ? r2[0] : r2[1], 4);
+  r1 += __shfl_xor(r1, 2);
+  r1 += __shfl_xor(r1, 1);
+  const float pk = r1 + A.w.ba[0];
+  const float alpha_k = A.w.act_super ? softplus(pk - 1.f) : fmaxf(pk, 0.f);
+  float as = wtL[ng >> 2] * alpha_k;   // each k held by 4 lanes: sum over bits 2..4
+  as += __shfl_xor(as, 4);
+  as += __shfl_xor(as, 8);
+  as += __shfl_xor(as, 16);
+  chk = fmaf(0.f, (hs[0] + hs[1]) + (hs[2] + hs[3]) + (hs[4] + hs[5]) + (hs[6] + hs[7]) + as, chk);
+  const int64_t vo = tile * kXTS + j;
+  if (vo < n) {
+    if (ng == 0) {
+      A.vmask[vo] = sf;
+      if (sf) A.out_feat[vo * (kC + 1)] = as;
+    }
+    if (sf) {
+      f32x4n* dst = reinterpret_cast<f32x4n*>(A.hid + vo * kHid + 8 * ng);
+      __builtin_nontemporal_store((f32x4n){hs[0], hs[1], hs[2], hs[3]}, dst);
+      __builtin_nontemporal_store((f32x4n){hs[4], hs[5], hs[6], hs[7]}, dst + 1);
+    }
+  }
+}
+
 template <bool H>
 __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw, int lane) {
   using L = XL<H>;
@@ -796,15 +902,18 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   GatherState g;
   gather_row(A, blockIdx.x, lane, g);
   gather_sample(A, lane, g);
-  gather<H>(A, g, 0, lds, pw, lane, dr6);
+  gather<H>(A, g, 0, 0, lds, pw, lane, dr6);
   pe_planes<H, 0>(lds, pw, lane, dr6);
   pe_planes<H, 1>(lds, pw, lane, dr6);
   X3_SYNC();   // P0: prow of the first tile visible to all producers
   p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
   X3_SYNC();   // S0
+  float chk = 0.f;   // h2 tails: 0 * outputs (producer_tail)
+  TailState ts;
   int it = 0;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     const int nbuf = (it & 1) ^ 1;
+    const int nw = H ? (it + 1) % 3 : nbuf;   // Wt / Sf slot of the next tile
     const int64_t next = tile + gridDim.x;
     X3_TR(1, 0);
     park_p1(p1r, p1e, lds, pw, lane);   // the layer-input planes are free since the last S7
@@ -812,13 +921,16 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_TR(1, 1);
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
-    if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, tile - gridDim.x, lane);
+    if (!H && pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, tile - gridDim.x, lane);
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
     X3_TR(1, 2);
-    // during block1.2: gather (nbuf's arrays are free: their last reader was the previous finalize)
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, lds, pw, lane, dr6);
+    // during block1.2: gather of the next tile (its slots are free: their last
+    // readers were the previous finalize / tail)
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, nw, lds, pw, lane, dr6);
+    if constexpr (H)   // first half of the previous tile's tail
+      if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
     X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
@@ -827,13 +939,27 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_TR(1, 4);
     X3_SYNC();   // S4
     if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 0>(lds, pw, lane, dr6);   // during block3.0 (PE planes free since S1)
+    // (h2) during block3.0: the second half of the previous tile's tail (its
+    // accumulators are overwritten after this tile's S6)
+    if constexpr (H)
+      if (it > 0) producer_tail<1>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
     X3_SYNC();   // S5
     X3_TR(1, 5);
     X3_SYNC();   // S6
     if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 1>(lds, pw, lane, dr6);   // during block3.2
     X3_SYNC();   // S7
   }
-  if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
+  if constexpr (H) {
+    // the last tile's tail (its accumulators were parked before the final S7)
+    if (it > 0) {
+      const int64_t last = blockIdx.x + (int64_t)(it - 1) * gridDim.x;
+      producer_tail<0>(A, lds, (it - 1) % 3, last, pw, lane, ts, chk);
+      producer_tail<1>(A, lds, (it - 1) % 3, last, pw, lane, ts, chk);
+    }
+    if (A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
+  } else {
+    if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
+  }
 }
 
 template <bool H>

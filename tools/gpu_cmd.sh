@@ -1,5 +1,6 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py -x -q -s --timeout 200 --timeout-method thread > gpurun_out/t_x3.log 2>&1
-REPS=3 bash tools/ab.sh ref pe
+timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_x3.log 2>&1
+PNR_LIB=tools/_ablate/trace/libpnr.so timeout -k 10 200 python tools/x3_trace.py > gpurun_out/trace_h2_tail.txt 2>&1
+REPS=2 bash tools/ab.sh prev
