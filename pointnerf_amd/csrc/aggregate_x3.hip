@@ -70,6 +70,9 @@ struct XL {
 #ifndef PNR_X3_PRIO
 #define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
 #endif
+#ifndef PNR_TAIL0_EARLY
+#define PNR_TAIL0_EARLY 0   // dev: first tail half in S1..S1b instead of after the gather
+#endif
 #ifndef PNR_CONS_PRIO
 #define PNR_CONS_PRIO 0
 #endif
@@ -502,10 +505,10 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
 
 // 5-band PE of the rotated 6-d distance of this lane's pair -> rows 2e (sin),
 // 2e + 1 (cos), e = 5 ch + f, of the PE planes (networks.py:175-190).
-// Producer wave pw owns channel ch = pw (PART 0) and ch = 4 + pw (PART 1, pw < 2).
-// Per channel two sincosf (f = 0 and 2) and three angle doublings
-// (sin 2a = 2 sin a cos a, cos 2a = (c - s)(c + s): f = 1 from 0, 3 from 2, 4
-// from 3), as k_point_pre's 3-band PE: at most two doublings from a sincosf.
+// Producer wave pw owns channel ch = pw (PART 0) and ch = 4 + pw (PART 1, pw < 2),
+// one sincosf per band, as the reference (angle doubling was measured 0.3 ms
+// faster but rounded differently where the compiler inlined it in the prologue
+// and in the loop, which made a sample's bits depend on its tile).
 template <bool H>
 __device__ __forceinline__ void pe_store(char* lds, int lane, int e, float sn, float cs) {
   using L = XL<H>;
@@ -538,12 +541,12 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
 #pragma unroll
   for (int ch = 4 * PART; ch < (PART == 0 ? 4 : 6); ++ch) {
     if (ch != mine) continue;   // wave-uniform
-    float s0, c0, s2, c2;
+    float s0, c0, s1, c1, s2, c2, s3, c3, s4, c4;
     sincosf(dr6[ch], &s0, &c0);
+    sincosf(dr6[ch] * 2.f, &s1, &c1);
     sincosf(dr6[ch] * 4.f, &s2, &c2);
-    const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
-    const float s3 = 2.f * s2 * c2, c3 = (c2 - s2) * (c2 + s2);
-    const float s4 = 2.f * s3 * c3, c4 = (c3 - s3) * (c3 + s3);
+    sincosf(dr6[ch] * 8.f, &s3, &c3);
+    sincosf(dr6[ch] * 16.f, &s4, &c4);
     pe_store<H>(lds, lane, 5 * ch + 0, s0, c0);
     pe_store<H>(lds, lane, 5 * ch + 1, s1, c1);
     pe_store<H>(lds, lane, 5 * ch + 2, s2, c2);
@@ -922,6 +925,10 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
     if (!H && pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, tile - gridDim.x, lane);
+#if PNR_TAIL0_EARLY
+    if constexpr (H)   // first half of the previous tile's tail (during the consumers' P1 add / store1)
+      if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
+#endif
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
@@ -929,8 +936,10 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // during block1.2: gather of the next tile (its slots are free: their last
     // readers were the previous finalize / tail)
     if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, nw, lds, pw, lane, dr6);
+#if !PNR_TAIL0_EARLY
     if constexpr (H)   // first half of the previous tile's tail
       if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
+#endif
     X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)

@@ -1,6 +1,5 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_x3.log 2>&1
-PNR_LIB=tools/_ablate/trace/libpnr.so timeout -k 10 200 python tools/x3_trace.py > gpurun_out/trace_h2_tail.txt 2>&1
-REPS=2 bash tools/ab.sh prev
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1
+bash tools/prof_bench.sh r01h2b
