@@ -70,9 +70,6 @@ struct XL {
 #ifndef PNR_X3_PRIO
 #define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
 #endif
-#ifndef PNR_TAIL0_EARLY
-#define PNR_TAIL0_EARLY 0   // dev: first tail half in S1..S1b instead of after the gather
-#endif
 #ifndef PNR_CONS_PRIO
 #define PNR_CONS_PRIO 0
 #endif
@@ -651,6 +648,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
     X3_TR(0, 3);
     store_act<H>(acc, XP, neg, 1.f, lane, T0);
+    X3_TR(0, 15);   // (store_act alone, tools/x3_trace.py)
     if (wid == 0) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
@@ -925,10 +923,6 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
     if (!H && pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, tile - gridDim.x, lane);
-#if PNR_TAIL0_EARLY
-    if constexpr (H)   // first half of the previous tile's tail (during the consumers' P1 add / store1)
-      if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
-#endif
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
@@ -936,10 +930,8 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // during block1.2: gather of the next tile (its slots are free: their last
     // readers were the previous finalize / tail)
     if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, nw, lds, pw, lane, dr6);
-#if !PNR_TAIL0_EARLY
     if constexpr (H)   // first half of the previous tile's tail
       if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
-#endif
     X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)

@@ -9,6 +9,7 @@ for N in "$@"; do
     b=$(basename $f .hip)
     extra=""
     if [ "$b" = query ] || [ "$b" = grid ]; then extra="-ffp-contract=off"; fi
+    if [ "$b" = aggregate_x3 ]; then extra="-fno-slp-vectorize"; fi
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -munsafe-fp-atomics -Iinclude $extra \
       -DPNR_ABLATE=$N -c $f -o tools/_ablate/$N/$b.o &
     objs="$objs tools/_ablate/$N/$b.o"

@@ -2,4 +2,4 @@ set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1
-bash tools/prof_bench.sh r01h2b
+REPS=2 bash tools/ab.sh head

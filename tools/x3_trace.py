@@ -37,6 +37,8 @@ def main():
     print("consumer wave 0, cycles per tile (median over tiles 8..59): total", int(np.median(tile)))
     for i, nme in enumerate(names):
         print(f"  {nme:14s} {int(np.median(d[:, i])):7d}")
+    s15 = t[0, 8:60, 15] - t[0, 8:60, 3]
+    print(f"  (store_act of store1 alone: {int(np.median(s15))})")
     blk = (ctypes.c_ulonglong * (1024 * 2))()
     assert L.lib().pnr_debug_x3_blocks(blk, 2048) == 0
     b = np.frombuffer(blk, dtype=np.uint64).reshape(1024, 2).astype(np.int64)
