@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 3
+#define PNR_ABI_VERSION 4
 
 enum {
   PNR_OK = 0,
@@ -320,6 +320,9 @@ typedef struct {
   const void* wc2h;   /* color_branch.2 + bias                  */
   const void* wc3h;   /* color_branch.4 + bias                  */
   float cscale[3];
+  const void* w1ah;   /* block1.0 columns 0..223 + bias: the per-point half P1 on
+                         f16-split MFMA (k_point_pre_h2; NULL: fp32 k_point_pre) */
+  float scale1a;
 } pnr_mlp_h2;
 int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_h2* wh,
                          float* out_feat, float* out_weight, float* out_conf, void* scratch,

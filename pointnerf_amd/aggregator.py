@@ -314,13 +314,16 @@ class PointAggregator(nn.Module):
             cpacks = [frag_pack_h2(cb[0].weight[:, :144], shift=s1),
                       frag_pack_h2(cb[0].weight[:, 144:], cb[0].bias, shift=s1),
                       frag_pack_h2(cb[2].weight, cb[2].bias), frag_pack_h2(cb[4].weight, cb[4].bias)]
+            # block1.0's per-point half (k_point_pre_h2)
+            p1pack = frag_pack_h2(b1[0].weight[:, :224], b1[0].bias)
         flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
         t = dict(w1bh=packs[0][0], w2h=packs[1][0], w3h=packs[2][0], w4h=packs[3][0], range_flag=flag,
-                 wc1a=cpacks[0][0], wc1b=cpacks[1][0], wc2h=cpacks[2][0], wc3h=cpacks[3][0])
+                 wc1a=cpacks[0][0], wc1b=cpacks[1][0], wc2h=cpacks[2][0], wc3h=cpacks[3][0], w1ah=p1pack[0])
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
                     (L.c_float * 4)(*(p[1] for p in packs)), flag.data_ptr(),
                     *(t[k].data_ptr() for k in ("wc1a", "wc1b", "wc2h", "wc3h")),
-                    (L.c_float * 3)(cpacks[1][1], cpacks[2][1], cpacks[3][1]))
+                    (L.c_float * 3)(cpacks[1][1], cpacks[2][1], cpacks[3][1]),
+                    t["w1ah"].data_ptr(), p1pack[1])
         self._packedh2, self._packedh2_key = (m, t), key
         return self._packedh2
 

@@ -137,6 +137,10 @@ template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
                        const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
                        float* out_conf, hipStream_t st);
+// k_point_pre_h2 (aggregate_x3.hip): P1 = W1[:, :224].[emb, PE_3(emb)] + b1 on
+// f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
+int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
+                        hipStream_t st);
 // k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
 // color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],

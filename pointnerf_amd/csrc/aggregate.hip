@@ -1274,6 +1274,9 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
                 "aggregate_h2: split packs must be 16-B aligned");
   for (int i = 0; i < 4; ++i)
     PNR_CHECK_ARG(wh->scale[i] > 0.f && wh->scale[i] < 1e30f, "aggregate_h2: bad layer scale %d", i);
+  if (wh->w1ah)
+    PNR_CHECK_ARG(((uintptr_t)wh->w1ah & 15) == 0 && wh->scale1a > 0.f && wh->scale1a < 1e30f,
+                  "aggregate_h2: bad block1.0 point-half pack");
   if (wh->wc1a) {
     PNR_CHECK_ARG(wh->wc1b && wh->wc2h && wh->wc3h, "aggregate_h2: partial colour-branch packs");
     PNR_CHECK_ARG((((uintptr_t)wh->wc1a | (uintptr_t)wh->wc1b | (uintptr_t)wh->wc2h | (uintptr_t)wh->wc3h) & 15) == 0,
@@ -1295,8 +1298,13 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
   SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
                {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
                wh->range_flag};
-  // k_point_pre (fp32 P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color_h2 / k_color
-  if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
+  // k_point_pre_h2 / k_point_pre (P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color_h2 / k_color
+  if (wh->w1ah) {
+    if (!a.pts.p1_ready && (rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a, wh->range_flag, a.p1, st)))
+      return rc;
+  } else if ((rc = launch_t<false>(a, st, kStagePre))) {
+    return rc;
+  }
   if ((rc = launch_pairs_split<true>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
                                      st)))
     return rc;

@@ -1136,7 +1136,121 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
   if (A.range_flag && chk != 0.f) atomicOr(A.range_flag, 1);   // non-finite output: see k_pairs_h2
 }
 
+// ---------------------------------------------------------------------------
+// k_point_pre_h2: the per-point half of block1.0, P1[p] = W1[:, :224] .
+// [emb_p, PE_3(emb_p)] + b1 (k_point_pre's split of the 284-input Linear,
+// aggregate.hip), as an fp32-accurate f16-split GEMM on the `layer` machinery:
+// a 4-wave workgroup owns 64 points (wave w: neuron tiles {2w, 2w+1} x both
+// halves), inputs in split planes [2][30 row groups][64 points][8] (rows: emb
+// 0..31, PE 32 + 6c + {sin, cos} x 3 bands (angle doubling as k_point_pre),
+// bias row 224), 61 KB: two workgroups per CU.  P1 rows stay fp32.
+constexpr int kPG1 = 30;                      // 8-row groups (240 rows = 15 k-steps)
+constexpr int kP1Plane = kPG1 * kXT * 16;
+constexpr size_t kP1H2Lds = 2 * (size_t)kP1Plane;
+
+struct P1H2Args {
+  pnr_points pts;
+  const void* pack;     // W1[:, :224] + b1, frag_pack_h2
+  float scale;
+  int32_t* range_flag;
+  float* p1;
+};
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_point_pre_h2(P1H2Args A) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;
+  const int64_t ntiles = cdiv(np, kXT);
+  const int T0 = 2 * wid;
+  const int voff = (T0 * 2 * 64 + lane) * 16;
+  const __amdgpu_buffer_rsrc_t rw = rsrc(A.pack);
+  float chk = 0.f;   // 0 * outputs: NaN once one is not finite (an input beyond the f16 range)
+  WRing<true> wr;
+  f32x16 acc[4];
+  prime<true>(wr, rw, voff);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // thread (point lane, channel block wid): emb channels 8 wid .. 8 wid + 7 and their PE
+    {
+      const int64_t pt = tile * kXT + lane;
+      const bool act = pt < np;
+      const int64_t prow = act ? (A.pts.used ? (int64_t)A.pts.used[pt] : pt) : 0;
+      float e[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (act) {
+        const float4 a = reinterpret_cast<const float4*>(A.pts.emb + prow * kEmb + 8 * wid)[0];
+        const float4 b = reinterpret_cast<const float4*>(A.pts.emb + prow * kEmb + 8 * wid)[1];
+        e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w; e[4] = b.x; e[5] = b.y; e[6] = b.z; e[7] = b.w;
+      }
+      store_group<true>(lds, kP1Plane, wid, lane, e);
+      float pe[48];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {   // networks.py:175-190 order: rows 32 + 6c + {s0, c0, s1, c1, s2, c2}
+        float s0, c0;
+        sincosf(e[u], &s0, &c0);
+        const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
+        const float s2 = 2.f * s1 * c1, c2 = (c1 - s1) * (c1 + s1);
+        pe[6 * u] = s0; pe[6 * u + 1] = c0; pe[6 * u + 2] = s1;
+        pe[6 * u + 3] = c1; pe[6 * u + 4] = s2; pe[6 * u + 5] = c2;
+      }
+#pragma unroll
+      for (int g = 0; g < 6; ++g) {
+        const float g8[8] = {pe[8 * g], pe[8 * g + 1], pe[8 * g + 2], pe[8 * g + 3],
+                             pe[8 * g + 4], pe[8 * g + 5], pe[8 * g + 6], pe[8 * g + 7]};
+        store_group<true>(lds, kP1Plane, 4 + 6 * wid + g, lane, g8);
+      }
+      if (wid == 0) {   // row 224 = 1 (bias column), 225..239 = 0
+        const float one[8] = {1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        store_group<true>(lds, kP1Plane, 28, lane, one);
+        store_group<true>(lds, kP1Plane, 29, lane, zero);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    layer<true>(acc, wr, rw, voff, lds, kP1Plane, 15, lane);
+    prime<true>(wr, rw, voff);   // the next tile
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int64_t prow = tile * kXT + 32 * pt + c;   // P1 row (index into used when set)
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x16& v = acc[2 * pt + T];
+          const float4 o = make_float4(v[4 * q] * A.scale, v[4 * q + 1] * A.scale, v[4 * q + 2] * A.scale,
+                                       v[4 * q + 3] * A.scale);
+          chk = fmaf(0.f, (o.x + o.y) + (o.z + o.w), chk);
+          if (prow < np)
+            *reinterpret_cast<float4*>(A.p1 + prow * kHid + 32 * (T0 + T) + 8 * q + 4 * h) = o;
+        }
+    }
+    __syncthreads();   // the planes are rewritten by the next tile
+  }
+  if (A.range_flag && chk != 0.f) atomicOr(A.range_flag, 1);
+}
+
 }  // namespace
+
+int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
+                        hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre_h2),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kP1H2Lds));
+    attr = true;
+  }
+  P1H2Args a;
+  a.pts = pts;
+  a.pack = pack;
+  a.scale = scale;
+  a.range_flag = range_flag;
+  a.p1 = p1;
+  const int64_t np = pts.used ? pts.n_used : pts.n;
+  hipLaunchKernelGGL(k_point_pre_h2, dim3(grid_for(cdiv(np, kXT), 1, 256 * 2)), dim3(256), kP1H2Lds, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
 
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
                     int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st) {

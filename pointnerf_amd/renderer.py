@@ -220,7 +220,7 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
             e2 = mark()
-            scratch, ready = self._agg_scratch(max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0)
+            scratch, ready = self._agg_scratch(max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
             pts.p1_ready = int(ready)
             if bf16:
                 L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
@@ -255,15 +255,16 @@ class NeuralPointsRayMarching(nn.Module):
         self.last_counts = totals
         return ray_color, opacity, is_bg, ray_mask
 
-    def _agg_scratch(self, n_max, n_points, dev, bf16, reuse):
+    def _agg_scratch(self, n_max, n_points, dev, bf16, reuse, precision="fp32"):
         """Persistent aggregate scratch (P1 lives at its start, see
         pnr_points.p1_ready) -> (tensor, P1 already valid).  The P1 is valid
         when reuse is requested and the embedding storage, block1.0 and the
         precision match the call that wrote it."""
         emb = self.neural_points.points_embeding
         b1 = self.aggregator.block1[0]
-        key = (bf16, n_points, emb.data_ptr(), emb._version, b1.weight.data_ptr(), b1.weight._version,
-               b1.bias.data_ptr(), b1.bias._version)
+        # fp32h2 computes P1 on f16-split MFMA (k_point_pre_h2), the other fp32 paths on fp32 MFMA
+        key = (bf16, precision == "fp32h2", n_points, emb.data_ptr(), emb._version, b1.weight.data_ptr(),
+               b1.weight._version, b1.bias.data_ptr(), b1.bias._version)
         need = (L.aggregate_scratch_bf16 if bf16 else L.aggregate_scratch)
         nb = L.c_size_t(0)
         fn = L.lib().pnr_aggregate_scratch_bytes_bf16 if bf16 else L.lib().pnr_aggregate_scratch_bytes
