@@ -372,7 +372,7 @@ def main():
                              "fp32": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
                              "fp32x3": "pnr_aggregate_fwd_x3 = k_point_pre + k_pairs_x3 (bf16x3 split, "
                                        "v_mfma_f32_32x32x16_bf16) + k_color",
-                             "fp32h2": "pnr_aggregate_fwd_h2 = k_point_pre + k_pairs_h2 + k_color_h2 (f16x2 split, "
+                             "fp32h2": "pnr_aggregate_fwd_h2 = k_point_pre_h2 + k_pairs_h2 + k_color_h2 (f16x2 split, "
                                        "v_mfma_f32_32x32x16_f16)",
                              "bf16": "pnr_aggregate_fwd_bf16 = k_point_pre_b + k_pairs_b + k_color_b "
                                      "(v_mfma_f32_32x32x16_bf16)"}[args.dtype],

@@ -16,7 +16,7 @@ import sys
 
 AGG_BY_DTYPE = {"fp32": ("k_point_pre", "k_pairs", "k_color"),
                 "fp32x3": ("k_point_pre", "k_pairs_x3", "k_color"),
-                "fp32h2": ("k_point_pre", "k_pairs_h2", "k_color_h2"),
+                "fp32h2": ("k_point_pre_h2", "k_pairs_h2", "k_color_h2"),
                 "bf16": ("k_point_pre_b", "k_pairs_b", "k_color_b")}
 MOPS = {"fp32": "SQ_INSTS_VALU_MFMA_MOPS_F32", "fp32x3": "SQ_INSTS_VALU_MFMA_MOPS_BF16",
         "fp32h2": "SQ_INSTS_VALU_MFMA_MOPS_F16",
