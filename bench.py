@@ -47,7 +47,11 @@ def parse():
     ap.add_argument("--hw", type=int, default=800)
     ap.add_argument("--no-grid-rebuild", action="store_true",
                     help="reuse the voxel grid across steps (default: rebuild every step)")
-    ap.add_argument("--no-gather", action="store_true", help="skip the tile all-gather (N > 1)")
+    ap.add_argument("--no-gather", action="store_true", help="skip the all-gather of rendered rays (N > 1)")
+    ap.add_argument("--shard", choices=("frames", "tiles"), default="frames",
+                    help="N > 1 ray batches: frames = each rank renders whole frames (frame f on rank f mod N, "
+                         "one all-gather of the step's N frames); tiles = every frame split in interleaved 16x16 "
+                         "pixel tiles over the ranks (N partial frames per rank per step)")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="diagnostic (single process): do rank 0's share of an N-rank step (N partial frames of "
                          "1/N of the rays, no collective) to project per-rank overheads of the N-GPU run")
@@ -251,7 +255,7 @@ def main():
     cams = cameras(8, H, W)
     SR = opt.SR
     # per-(frame, rank) pixel lists: step s renders frames s*world .. s*world+world-1
-    shard_world = world
+    shard_world = world if args.shard == "tiles" else 1   # partial frames per rank per step
     if world == 1 and args.emulate_world > 1:
         shard_world = args.emulate_world
     dev_cams = []
@@ -260,8 +264,9 @@ def main():
                          torch.from_numpy(rd).to(device)))
     bg = torch.from_numpy(np.random.default_rng(1).uniform(size=128).astype(np.float32)).to(device)
 
-    from pointnerf_amd.parallel import TileShard
+    from pointnerf_amd.parallel import FrameShard, TileShard
     shards = {}
+    fshard = FrameShard(rank, world) if (world > 1 and args.shard == "frames") else None
 
     def my_rays(frame):
         ci = frame % len(cams)
@@ -280,6 +285,8 @@ def main():
         frames = []
         for f in range(shard_world):
             frame = s * shard_world + f
+            if fshard is not None:
+                frame = fshard.frame_of(s)   # whole frame s*N + rank
             ci, rd, sh = my_rays(frame)
             campos, camrot, _ = dev_cams[ci]
             ev = [] if timed else None
@@ -296,9 +303,10 @@ def main():
                 stage["flops"] += c["n_pairs"] * FLOP_PER_PAIR + c["S_valid"] * FLOP_PER_SAMPLE
                 stage["_ev"] = stage.get("_ev", []) + ev
             if world > 1 and not args.no_gather:
-                # RCCL all-gather of the rendered 16x16 tiles: every rank holds the frame
-                # (async: the tiles travel over xGMI while the next partial frame renders)
-                frames.append(sh.assemble_async(color))
+                # RCCL all-gather of the rendered rays (async: they travel over xGMI while
+                # the next frame renders): tiles -> every rank holds the frame; frames ->
+                # every rank holds the step's N frames
+                frames.append((fshard or sh).assemble_async(color))
             else:
                 frames.append(color)
         return [f.wait() if hasattr(f, "wait") else f for f in frames]
@@ -366,8 +374,10 @@ def main():
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "grid_rebuild_per_step": not args.no_grid_rebuild,
-                       "parallelism": f"dp{world} (16x16 ray tiles, async RCCL all_gather of tiles)" if world > 1
-                       else "single GPU"},
+                       "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
+                                       f"step's frames)" if args.shard == "frames" else
+                                       f"dp{world} (16x16 ray tiles, async RCCL all_gather of tiles)")
+                       if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "kernel": {
                              "fp32": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",
                              "fp32x3": "pnr_aggregate_fwd_x3 = k_point_pre + k_pairs_x3 (bf16x3 split, "

@@ -1167,17 +1167,23 @@ __global__ void k_point_pe3_bwd(const float* __restrict__ emb, const float* __re
 
 static size_t scratch_need(int64_t n_max, int64_t n_points) {
   const int64_t nm = n_max > 0 ? n_max : 1;
-  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
+  // + 4 ints: the split kernels' tile counter (k_pairs_x3 / k_pairs_h2)
+  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 4 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
          sizeof(float);
 }
 
-// scratch = P1 [n_p1, 256] | hid [n_max, 256] | vmask: P1 first, so its place
-// does not depend on n_max and a later call may reuse it (pnr_points.p1_ready)
+// scratch = P1 [n_p1, 256] | hid [n_max, 256] | vmask | tile counter: P1 first,
+// so its place does not depend on n_max and a later call may reuse it
+// (pnr_points.p1_ready)
 static void carve(AggArgs& a, void* scratch, int64_t n_max, int64_t n_p1) {
   const int64_t nm = n_max > 0 ? n_max : 1;
   a.p1 = static_cast<float*>(scratch);
   a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
   a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
+}
+static int32_t* tile_counter(const AggArgs& a, int64_t n_max) {
+  const int64_t nm = n_max > 0 ? n_max : 1;
+  return a.vmask + cdiv(nm, 4) * 4;
 }
 
 int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, float* out_feat,
@@ -1256,7 +1262,7 @@ extern "C" int pnr_aggregate_fwd_x3(const pnr_points* pts, const pnr_samples* s,
   if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
   SplitW sw = {{wx->w1bx, wx->w2x, wx->w3x, wx->w4x}, {1.f, 1.f, 1.f, 1.f}, nullptr};
   if ((rc = launch_pairs_split<false>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
-                                      st)))
+                                      tile_counter(a, s->n_max), st)))
     return rc;
   return launch_t<false>(a, st, kStageColor);
 }
@@ -1306,7 +1312,7 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
     return rc;
   }
   if ((rc = launch_pairs_split<true>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
-                                     st)))
+                                     tile_counter(a, s->n_max), st)))
     return rc;
   if (wh->wc1a) {
     const void* cp[4] = {wh->wc1a, wh->wc1b, wh->wc2h, wh->wc3h};

@@ -61,7 +61,8 @@ struct XL {
   static constexpr int OffAp = OffSf + NWB * kXTS * 4;     // float [4][64] (x3: alpha partials)
   static constexpr int OffWa = OffAp + 4 * kXT * 4;        // float [256] alpha_branch.0 weights
   static constexpr int OffH4 = OffWa + kHid * 4;           // h2: float [64][kP1Pitch] block3.2 accumulators
-  static constexpr size_t Lds = (size_t)OffH4 + (H ? kXT * kP1Pitch * 4 : 0);
+  static constexpr int OffTq = OffH4 + (H ? kXT * kP1Pitch * 4 : 0);   // int [4] tile of iteration i at i % 4
+  static constexpr size_t Lds = (size_t)OffTq + 16;
   static_assert(OffSf % 16 == 0 && OffWa % 16 == 0 && OffH4 % 16 == 0, "16-B aligned LDS arrays");
   static_assert(kXT * kP1Pitch * 4 <= NPL * kPlaneX, "parked P1 fits the layer-input area");
   static_assert(Lds <= 160 * 1024, "LDS budget");
@@ -104,7 +105,17 @@ struct X3Args {
   float* out_feat;
   float* out_weight;
   float* out_conf;
+  int32_t* tile_ctr;   // zeroed per launch: tiles past the first gridDim.x are handed out in order
 };
+
+// Dynamic tile schedule: each workgroup starts on tile blockIdx.x and takes
+// the next free tile from tile_ctr when it starts the one before (producer
+// wave 0, lane 0, one tile ahead; the index travels through LDS ring TQ), so
+// workgroups that start late or run slow (another kernel on the CU, an RCCL
+// copy) take fewer tiles instead of finishing late.
+__device__ __forceinline__ int64_t take_tile(const X3Args& A) {
+  return (int64_t)gridDim.x + atomicAdd(A.tile_ctr, 1);
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
@@ -613,8 +624,9 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #if PNR_TRACE
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][0] = wall_clock64();
 #endif
+  const int* TQ = reinterpret_cast<const int*>(lds + L::OffTq);
   int it = 0;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile = TQ[(it + 1) & 3], ++it) {
     const int buf = it & 1;
     X3_TR(0, 0);
     // ------------------------------------------------------------ block1.0 = P1 + W1[:, 224:] . PE_5
@@ -906,23 +918,29 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   gather<H>(A, g, 0, 0, lds, pw, lane, dr6);
   pe_planes<H, 0>(lds, pw, lane, dr6);
   pe_planes<H, 1>(lds, pw, lane, dr6);
-  X3_SYNC();   // P0: prow of the first tile visible to all producers
+  int* TQ = reinterpret_cast<int*>(lds + L::OffTq);
+  if (pw == 0 && lane == 0) TQ[1] = (int)take_tile(A);
+  X3_SYNC();   // P0: prow of the first tile visible to all producers, TQ[1] too
   p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
   X3_SYNC();   // S0
   float chk = 0.f;   // h2 tails: 0 * outputs (producer_tail)
   TailState ts;
   int it = 0;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+  int64_t prev = -1;   // the previous iteration's tile (its tail / alpha run one tile late)
+  for (int64_t tile = blockIdx.x; tile < ntiles; prev = tile, tile = TQ[(it + 1) & 3], ++it) {
     const int nbuf = (it & 1) ^ 1;
     const int nw = H ? (it + 1) % 3 : nbuf;   // Wt / Sf slot of the next tile
-    const int64_t next = tile + gridDim.x;
+    const int64_t next = TQ[(it + 1) & 3];
+    // the tile after next, published before S1 (only while this workgroup goes on:
+    // a tile taken by a workgroup that stops would be lost)
+    if (pw == 0 && lane == 0) TQ[(it + 2) & 3] = next < ntiles ? (int)take_tile(A) : (int)ntiles;
     X3_TR(1, 0);
     park_p1(p1r, p1e, lds, pw, lane);   // the layer-input planes are free since the last S7
     gather_row(A, next, lane, g);
     X3_TR(1, 1);
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
-    if (!H && pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, tile - gridDim.x, lane);
+    if (!H && pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, prev, lane);
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
@@ -931,7 +949,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // readers were the previous finalize / tail)
     if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, nw, lds, pw, lane, dr6);
     if constexpr (H)   // first half of the previous tile's tail
-      if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
+      if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
     X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
@@ -943,7 +961,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // (h2) during block3.0: the second half of the previous tile's tail (its
     // accumulators are overwritten after this tile's S6)
     if constexpr (H)
-      if (it > 0) producer_tail<1>(A, lds, (it + 2) % 3, tile - gridDim.x, pw, lane, ts, chk);
+      if (it > 0) producer_tail<1>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
     X3_SYNC();   // S5
     X3_TR(1, 5);
     X3_SYNC();   // S6
@@ -953,13 +971,12 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   if constexpr (H) {
     // the last tile's tail (its accumulators were parked before the final S7)
     if (it > 0) {
-      const int64_t last = blockIdx.x + (int64_t)(it - 1) * gridDim.x;
-      producer_tail<0>(A, lds, (it - 1) % 3, last, pw, lane, ts, chk);
-      producer_tail<1>(A, lds, (it - 1) % 3, last, pw, lane, ts, chk);
+      producer_tail<0>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
+      producer_tail<1>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
     }
     if (A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
   } else {
-    if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, blockIdx.x + (int64_t)(it - 1) * gridDim.x, lane);
+    if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, prev, lane);
   }
 }
 
@@ -1293,7 +1310,7 @@ extern "C" int pnr_debug_x3_blocks(unsigned long long* out, int n) {
 template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
                        const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
-                       float* out_conf, hipStream_t st) {
+                       float* out_conf, int32_t* tile_ctr, hipStream_t st) {
   const void* fn = H ? reinterpret_cast<const void*>(&k_pairs_h2) : reinterpret_cast<const void*>(&k_pairs_x3);
   static bool attr = false;
   if (!attr) {
@@ -1311,6 +1328,8 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
+  a.tile_ctr = tile_ctr;
+  PNR_HIP(hipMemsetAsync(tile_ctr, 0, sizeof(int32_t), st));
   const int64_t tiles = cdiv(s.n_max, kXTS);
   if (H)
     hipLaunchKernelGGL(k_pairs_h2, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
@@ -1320,8 +1339,10 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
   return PNR_OK;
 }
 template int launch_pairs_split<false>(const pnr_points&, const pnr_samples&, const pnr_mlp&, const SplitW&,
-                                       const float*, float*, int32_t*, float*, float*, float*, hipStream_t);
+                                       const float*, float*, int32_t*, float*, float*, float*, int32_t*,
+                                       hipStream_t);
 template int launch_pairs_split<true>(const pnr_points&, const pnr_samples&, const pnr_mlp&, const SplitW&,
-                                      const float*, float*, int32_t*, float*, float*, float*, hipStream_t);
+                                      const float*, float*, int32_t*, float*, float*, float*, int32_t*,
+                                      hipStream_t);
 
 }  // namespace pnr

@@ -3,11 +3,15 @@
 Each ray's output depends only on the (replicated) point table, the MLP
 weights and the ray itself (qpiw.py:442-528 threads are per sample; the
 aggregator and composite are per ray), so the path shards by rays with no
-exchange until the rendered tiles are assembled.  Pixels are dealt in
-interleaved 16x16 tiles, round robin over ranks and rotated per frame so the
-object-centred load balances; one all-gather over RCCL (xGMI) assembles the
-frame on every rank.  One process per GPU, torch.distributed "nccl" (= RCCL
-on ROCm); the same code runs on "gloo" for the CPU tests.
+exchange until the rendered tiles are assembled.  Two ray batchings:
+  * TileShard: pixels of one frame dealt in interleaved 16x16 tiles, round
+    robin over ranks and rotated per frame so the object-centred load
+    balances; one all-gather assembles the frame on every rank;
+  * FrameShard: each rank renders whole frames (frame f on rank f mod N);
+    one all-gather per step gives every rank the step's N frames.  One render
+    call per rank per frame, so no per-call overhead grows with N.
+One process per GPU, torch.distributed "nccl" (= RCCL on ROCm); the same code
+runs on "gloo" for the CPU tests.
 """
 from __future__ import annotations
 
@@ -75,3 +79,35 @@ class _Gather:
         self.work.wait()
         buf = self.buf if self.buf is not None else torch.cat(self.parts)
         return buf.index_select(0, self.shard.src.to(buf.device))
+
+
+class FrameShard:
+    """Whole-frame ray batches: rank r renders frames r, r + N, r + 2N, ...;
+    assemble_async all-gathers one [P, C] frame from every rank into the
+    step's [N, P, C] stack (frame r of the step from rank r)."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+
+    def frame_of(self, step: int) -> int:
+        return step * self.world + self.rank
+
+    def assemble_async(self, local: torch.Tensor, group=None) -> "_FrameGather":
+        import torch.distributed as dist
+        local = local.contiguous()
+        if dist.get_backend(group) == "nccl":
+            buf = torch.empty((self.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+            work = dist.all_gather_into_tensor(buf, local, group=group, async_op=True)
+            return _FrameGather(work, buf, None)
+        lst = [torch.empty_like(local) for _ in range(self.world)]
+        work = dist.all_gather(lst, local, group=group, async_op=True)
+        return _FrameGather(work, None, lst)
+
+
+class _FrameGather:
+    def __init__(self, work, buf, parts):
+        self.work, self.buf, self.parts = work, buf, parts
+
+    def wait(self) -> torch.Tensor:
+        self.work.wait()
+        return self.buf if self.buf is not None else torch.stack(self.parts)

@@ -72,3 +72,50 @@ def test_two_rank_render_assembles_full_frame():
     want = np.concatenate([full["coarse_raycolor"], full["coarse_is_background"]], 1)
     for got in outs:
         np.testing.assert_allclose(got, want, atol=1e-5, rtol=1e-5)
+
+
+def _frame_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests"), os.path.join(root, "tests", "golden")]
+    import torch.distributed as dist
+    from pointnerf_amd.parallel import FrameShard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fs = FrameShard(rank, world)
+    params = formula_params(salt=0.4)
+    outs = []
+    for step in range(2):
+        frame = fs.frame_of(step)   # whole frame step * world + rank, one camera per frame
+        sc = scene(8000, H=24, W=24, theta=60.0 + 45.0 * frame)
+        r = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"])
+        local = torch.from_numpy(np.concatenate([r["coarse_raycolor"], r["coarse_is_background"]], 1))
+        outs.append(fs.assemble_async(local).wait().numpy())
+    if rank == 0:
+        q.put(outs)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_frame_shards_gather_every_frame():
+    """FrameShard (bench --shard frames): rank r renders frames r, r + 2, ...;
+    after each step's all-gather every rank holds both frames, in frame order,
+    equal to single-process renders."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_frame_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    params = formula_params(salt=0.4)
+    for step, got in enumerate(outs):
+        assert got.shape[0] == 2
+        for r in range(2):
+            sc = scene(8000, H=24, W=24, theta=60.0 + 45.0 * (step * 2 + r))
+            full = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"])
+            want = np.concatenate([full["coarse_raycolor"], full["coarse_is_background"]], 1)
+            np.testing.assert_allclose(got[r], want, atol=1e-5, rtol=1e-5)
