@@ -309,17 +309,26 @@ def main():
                 frames.append((fshard or sh).assemble_async(color))
             else:
                 frames.append(color)
-        return [f.wait() if hasattr(f, "wait") else f for f in frames]
+        return frames
+
+    def finish(handles):
+        # the step's gathered frames; on RCCL wait() only orders the current
+        # stream after the collective, so the host is not blocked
+        return [f.wait() if hasattr(f, "wait") else f for f in handles]
 
     for s in range(args.warmup):
-        step(s, False)
+        finish(step(s, False))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    prev = []
     for s in range(args.steps):
-        step(args.warmup + s, True)
+        cur = step(args.warmup + s, True)
+        finish(prev)   # step s-1's all-gather travelled over xGMI while step s rendered
+        prev = cur
+    finish(prev)       # the last step's frames are gathered inside the timed region
     torch.cuda.synchronize()
     t_local = time.perf_counter() - t0
     if dist:

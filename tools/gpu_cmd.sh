@@ -1,6 +1,5 @@
+set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_edge.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t_x3.log 2>&1
-REPS=2 bash tools/ab.sh head
-PNR_LIB=tools/_ablate/trace/libpnr.so timeout -k 10 200 python tools/x3_trace.py > gpurun_out/trace_dyn.txt 2>&1
-true
+PNR_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/bench2f.log 2>&1
+timeout -k 10 400 python bench.py > gpurun_out/bench1.log 2>&1
