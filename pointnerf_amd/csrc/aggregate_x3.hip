@@ -134,6 +134,9 @@ __device__ __forceinline__ void load_w(uint4 (&a)[2][XL<H>::NPW], __amdgpu_buffe
                      rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * NTK + T) * NPW * 1024, 0));
 }
 
+#ifndef PNR_H2_BD
+#define PNR_H2_BD 2   // h2: B fragments (LDS) read this many k-steps ahead
+#endif
 // weight ring depth (k-steps in flight); the packs carry >= kWD zero steps
 // (X3_PAD / H2_PAD in aggregator.py)
 #ifndef PNR_H2_WD
@@ -166,9 +169,15 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
     for (int pl = 0; pl < NPL; ++pl)
       bb[pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * t * kXT + 32 * pt) * 16);
   };
-  uint4 b[2][NPL];
-  ldb(0, 0, b[0]);
-  ldb(0, 1, b[1]);
+  // B fragments BD steps ahead (slot = step mod BD)
+  constexpr int BD = H ? PNR_H2_BD : 1;
+  uint4 b[BD][2][NPL];
+#pragma unroll
+  for (int sl = 0; sl < BD; ++sl) {
+    const int t0 = sl < nsteps ? sl : nsteps - 1;
+    ldb(t0, 0, b[sl][0]);
+    ldb(t0, 1, b[sl][1]);
+  }
   // One step = 2 halves x 12 MFMAs.  Each B plane of a half is re-read for the
   // next step, and each weight plane re-loaded kWD steps ahead, right after
   // its last MFMA of this step, so the loads sit in MFMA gaps instead of in
@@ -190,9 +199,9 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
                      rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * NTK + T) * NPW * 1024, 0));
   };
-  auto bl = [&](int tn, int pt, int pl) {
+  auto bl = [&](int bs, int tn, int pt, int pl) {
     if (!(PNR_ABLATE & 64))   // (64: timing only, B fixed)
-      b[pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
+      b[bs][pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
   };
   // h2 step per half: Ws.Xh, Wl.Xh, Wh.Xl (Ws = 2^11 Wh, made in registers)
   // Ws = 2^11 Wh of the NEXT step is made in the middle of this one (scl), so
@@ -205,68 +214,70 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
     scale_next(w.a[0], 0);
     scale_next(w.a[0], 1);
   }
-  auto step_h = [&](uint4 (&a)[2][NPW], const uint4 (&an)[2][NPW], int t) {
-    const int tn = t + 1 < nsteps ? t + 1 : t;
+  auto step_h = [&](uint4 (&a)[2][NPW], const uint4 (&an)[2][NPW], int t, int bs) {
+    const int tn = t + BD < nsteps ? t + BD : nsteps - 1;
     const uint4 s0 = scl[0], s1 = scl[1];
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
-      mm(pt, s0, s1, b[pt][0]);                                // Ws.Xh
+      mm(pt, s0, s1, b[bs][pt][0]);                                // Ws.Xh
       __builtin_amdgcn_sched_barrier(0);
-      mm(pt, a[0][1], a[1][1], b[pt][0]);                      // Wl.Xh
+      mm(pt, a[0][1], a[1][1], b[bs][pt][0]);                      // Wl.Xh
       __builtin_amdgcn_sched_barrier(0);
       if (pt == 1) wl(a, 1, t + kWD);
       if (pt == 0) scale_next(an, 0);
-      bl(tn, pt, 0);
+      bl(bs, tn, pt, 0);
       __builtin_amdgcn_sched_barrier(0);
-      mm(pt, a[0][0], a[1][0], b[pt][1]);                      // Wh.Xl
+      mm(pt, a[0][0], a[1][0], b[bs][pt][1]);                      // Wh.Xl
       __builtin_amdgcn_sched_barrier(0);
-      bl(tn, pt, 1);
+      bl(bs, tn, pt, 1);
       if (pt == 0) scale_next(an, 1);
       if (pt == 1) wl(a, 0, t + kWD);   // packs carry kWD zero steps
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto step = [&](uint4 (&a)[2][NPW], const uint4 (&an)[2][NPW], int t) {
+  auto step = [&](uint4 (&a)[2][NPW], const uint4 (&an)[2][NPW], int t, int bs) {
     if constexpr (H) {
-      step_h(a, an, t);
+      step_h(a, an, t, bs);
     } else {
-      const int tn = t + 1 < nsteps ? t + 1 : t;
+      const int tn = t + BD < nsteps ? t + BD : nsteps - 1;
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) {
-        mm(pt, a[0][2], a[1][2], b[pt][0]);                      // W2.X0
+        mm(pt, a[0][2], a[1][2], b[bs][pt][0]);                      // W2.X0
         __builtin_amdgcn_sched_barrier(0);
         if (pt == 1) wl(a, 2, t + kWD);
         __builtin_amdgcn_sched_barrier(0);
-        mm(pt, a[0][1], a[1][1], b[pt][1]);                      // W1.X1
-        mm(pt, a[0][0], a[1][0], b[pt][2]);                      // W0.X2
+        mm(pt, a[0][1], a[1][1], b[bs][pt][1]);                      // W1.X1
+        mm(pt, a[0][0], a[1][0], b[bs][pt][2]);                      // W0.X2
         __builtin_amdgcn_sched_barrier(0);
-        bl(tn, pt, 2);
+        bl(bs, tn, pt, 2);
         __builtin_amdgcn_sched_barrier(0);
-        mm(pt, a[0][1], a[1][1], b[pt][0]);                      // W1.X0
+        mm(pt, a[0][1], a[1][1], b[bs][pt][0]);                      // W1.X0
         __builtin_amdgcn_sched_barrier(0);
         if (pt == 1) wl(a, 1, t + kWD);
         __builtin_amdgcn_sched_barrier(0);
-        mm(pt, a[0][0], a[1][0], b[pt][1]);                      // W0.X1
+        mm(pt, a[0][0], a[1][0], b[bs][pt][1]);                      // W0.X1
         __builtin_amdgcn_sched_barrier(0);
-        bl(tn, pt, 1);
+        bl(bs, tn, pt, 1);
         __builtin_amdgcn_sched_barrier(0);
-        mm(pt, a[0][0], a[1][0], b[pt][0]);                      // W0.X0
+        mm(pt, a[0][0], a[1][0], b[bs][pt][0]);                      // W0.X0
         __builtin_amdgcn_sched_barrier(0);
-        bl(tn, pt, 0);
+        bl(bs, tn, pt, 0);
         if (pt == 1) wl(a, 0, t + kWD);   // packs carry kWD zero steps
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
+  // unrolled by U = lcm(kWD, BD) so the weight and B slots are compile-time
+  constexpr int U = (BD == 2 && kWD % 2) ? 2 * kWD : kWD;
   int t = 0;
 #pragma unroll 1
-  for (; t + kWD <= nsteps; t += kWD) {
+  for (; t + U <= nsteps; t += U) {
 #pragma unroll
-    for (int d = 0; d < kWD; ++d) step(w.a[d], w.a[(d + 1) % kWD], t + d);
+    for (int d = 0; d < U; ++d) step(w.a[d % kWD], w.a[(d + 1) % kWD], t + d, d % BD);
   }
 #pragma unroll
-  for (int d = 0; d < kWD - 1; ++d)
-    if (t + d < nsteps) step(w.a[d], w.a[d + 1], t + d);   // the ring then holds padding; prime() refills it
+  for (int d = 0; d < U - 1; ++d)   // the ring then holds padding; prime() refills it
+    if (t + d < nsteps) step(w.a[d % kWD], w.a[(d + 1) % kWD], t + d, d % BD);
 }
 
 // (x0, x1) -> f16 split of y = lrelu(x mul) (splith's planes: hi = f16(y),
