@@ -1039,21 +1039,32 @@ struct ColH2Args {
 // samples past n or without a valid neighbour, as k_color).  Item (sample s,
 // group gl) per lane: 16 samples x 4 groups per wave-instruction, so a global
 // read is 16 rows x 128 contiguous bytes and an LDS write 16 x 16 contiguous bytes.
-__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t v0, int64_t n, int g0, int ng) {
+// vm: bit s = sample v0 + s is valid (< n, a valid neighbour); every item's
+// loads are issued unconditionally (row v0 stands in for an invalid sample and
+// is zeroed afterwards), so the loads of all items are in flight together.
+__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t v0, uint64_t vm, int g0,
+                                               int ng) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  f32x4n ra[10], rb[10];
 #pragma unroll
   for (int u = 0; u < 10; ++u) {
     const int q = 2 * u + wid;
     const int s = (lane & 15) + 16 * (q & 3), gl = (lane >> 4) + 4 * (q >> 2);
+    if (4 * (q >> 2) >= ng) continue;   // wave-uniform: no group of this item is loaded
+    const int64_t v = ((vm >> s) & 1) ? v0 + s : v0;
+    const f32x4n* src = reinterpret_cast<const f32x4n*>(A.hid + v * kHid + 8 * (g0 + (gl < ng ? gl : 0)));
+    ra[u] = __builtin_nontemporal_load(src);
+    rb[u] = __builtin_nontemporal_load(src + 1);
+  }
+#pragma unroll
+  for (int u = 0; u < 10; ++u) {
+    const int q = 2 * u + wid;
+    const int s = (lane & 15) + 16 * (q & 3), gl = (lane >> 4) + 4 * (q >> 2);
+    if (4 * (q >> 2) >= ng) continue;
     if (gl >= ng) continue;
-    const int64_t v = v0 + s;
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (v < n && A.vmask[v] != 0) {
-      const f32x4n* src = reinterpret_cast<const f32x4n*>(A.hid + v * kHid + 8 * (g0 + gl));
-      const f32x4n a = __builtin_nontemporal_load(src), b = __builtin_nontemporal_load(src + 1);
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-      x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-    }
+    const bool ok = (vm >> s) & 1;
+    const float x[8] = {ok ? ra[u].x : 0.f, ok ? ra[u].y : 0.f, ok ? ra[u].z : 0.f, ok ? ra[u].w : 0.f,
+                        ok ? rb[u].x : 0.f, ok ? rb[u].y : 0.f, ok ? rb[u].z : 0.f, ok ? rb[u].w : 0.f};
     store_group<true>(lds, kCPlane, gl, s, x);
   }
 }
@@ -1078,8 +1089,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
   prime<true, 4>(wr, r1a, voff);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t v0 = tile * kXT;
+    const uint64_t vm = __ballot(v0 + lane < n && A.vmask[v0 + lane] != 0);   // sample validity, one load
     // ---------------------------------------------------- layer 1, input rows 0..143 (hid)
-    color_load_hid(A, lds, v0, n, 0, kCG);
+    color_load_hid(A, lds, v0, vm, 0, kCG);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
@@ -1087,7 +1099,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r1b, voff);
     __syncthreads();
     // ---------------------------------------------------- rows 144..255 (hid), 256..279 (view PE), 280 (bias)
-    color_load_hid(A, lds, v0, n, kCG, 14);
+    color_load_hid(A, lds, v0, vm, kCG, 14);
     if (wid == 0) {   // lane = sample: PE_4 of the rotated view direction (k_color's order)
       const int64_t v = v0 + lane;
       float vrot[3] = {0.f, 0.f, 0.f};
@@ -1152,7 +1164,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int64_t v = v0 + 32 * pt + c;
-      if (v >= n || A.vmask[v] == 0) continue;
+      if (!((vm >> (32 * pt + c)) & 1)) continue;
       float* o = A.out_feat + v * (kC + 1) + 1;
 #pragma unroll
       for (int T = 0; T < 2; ++T)
