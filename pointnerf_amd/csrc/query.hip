@@ -86,6 +86,73 @@ __global__ void __launch_bounds__(kQBlock) k_fill_list(int64_t R, int SR, const 
   if ((threadIdx.x & 63) == 0 && hit) atomicAdd(counts + 2, hit);
 }
 
+// One accepted-or-rejected candidate record of query_neigh_along_ray_layered
+// (qpiw.py:494-518): radius test, fill phase, then strict-closer replacement of
+// the first farthest entry.
+template <int KMAX>
+__device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int K, float r2, float buf[KMAX],
+                                          int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
+  const float xv = __fsub_rn(v.x, p[0]);
+  const float yv = __fsub_rn(v.y, p[1]);
+  const float zv = __fsub_rn(v.z, p[2]);
+  const float d2 = __fadd_rn(__fadd_rn(__fmul_rn(xv, xv), __fmul_rn(yv, yv)), __fmul_rn(zv, zv));
+  if (!(r2 == 0.f || d2 <= r2)) return;
+  const int pid = __float_as_int(v.w);
+  if (kid < K) {
+    // fill phase (qpiw.py:500-506)
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      if (i == kid) {
+        out[i] = pid;
+        buf[i] = d2;
+      }
+    }
+    if (d2 > far2) {
+      far2 = d2;
+      far_ind = kid;
+    }
+    ++kid;
+  } else {
+    ++kid;
+    // replace phase (qpiw.py:507-518): strictly closer than the
+    // current farthest, then rescan for the first maximum.
+    if (d2 < far2) {
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        if (i == far_ind) {
+          out[i] = pid;
+          buf[i] = d2;
+        }
+      }
+      far2 = d2;
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        if (i < K && buf[i] > far2) {
+          far2 = buf[i];
+          far_ind = i;
+        }
+      }
+    }
+  }
+}
+
+// All records of one occupied voxel, in slot order, fetched 4 at a time
+// (memory-level parallelism) and visited in order.
+template <int KMAX>
+__device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
+                                         float buf[KMAX], int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
+  for (int g0 = 0; g0 < cnt; g0 += 4) {
+    float4 vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (g0 + u >= cnt) break;
+      knn_visit<KMAX>(vb[u], p, K, r2, buf, out, kid, far_ind, far2);
+    }
+  }
+}
+
 // query_neigh_along_ray_layered (qpiw.py:442-528) for one sample.  KMAX is the
 // compile-time buffer size, K <= KMAX the runtime neighbour count.
 template <int KMAX>
@@ -105,6 +172,32 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
   }
   int kid = 0, far_ind = 0;
   float far2 = 0.f;
+  if (layers == 2) {
+    // query 3x3x3 (every shipped config): the 27 cells in the reference's
+    // traversal order (layer 0 = the centre, then layer 1 = x -> y -> z minus the
+    // centre).  The slot and count lookups of all 27 cells are issued together
+    // instead of as 27 dependent chains; the visit order is unchanged.
+    int slot[27], cnt[27];
+#pragma unroll
+    for (int j = 0; j < 27; ++j) {
+      const int x = j == 0 ? 0 : ((j <= 13 ? j - 1 : j) / 9) - 1;
+      const int y = j == 0 ? 0 : (((j <= 13 ? j - 1 : j) / 3) % 3) - 1;
+      const int z = j == 0 ? 0 : ((j <= 13 ? j - 1 : j) % 3) - 1;
+      const int cx = fx + x, cy = fy + y, cz = fz + z;
+      const bool in = (unsigned)cx < (unsigned)g.dims[0] && (unsigned)cy < (unsigned)g.dims[1] &&
+                      (unsigned)cz < (unsigned)g.dims[2];
+      slot[j] = in ? coor_2_occ[((int64_t)cx * g.dims[1] + cy) * g.dims[2] + cz] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < 27; ++j) cnt[j] = slot[j] >= 0 ? min(g.P, occ_numpnts[slot[j]]) : 0;
+#pragma unroll
+    for (int j = 0; j < 27; ++j) {
+      if (j == 1 && kid >= K) break;   // layer 0 already saw >= K candidates (qpiw.py:526)
+      n_cand += cnt[j];
+      knn_cell<KMAX>(occ_pts + (int64_t)max(slot[j], 0) * g.P, cnt[j], p, K, r2, buf, out, kid, far_ind, far2);
+    }
+    return kid < K ? kid : K;
+  }
   for (int layer = 0; layer < layers; ++layer) {
     const int x0 = max(-fx, -layer), x1 = min(g.dims[0] - fx, layer + 1);
     const int y0 = max(-fy, -layer), y1 = min(g.dims[1] - fy, layer + 1);
@@ -118,60 +211,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
           if (slot < 0) continue;
           const int cnt = min(g.P, occ_numpnts[slot]);
           n_cand += cnt;
-          const float4* rec = occ_pts + (int64_t)slot * g.P;
-          // records fetched 4 at a time (memory-level parallelism), visited in order
-          for (int g0 = 0; g0 < cnt; g0 += 4) {
-            float4 vb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-            if (g0 + u >= cnt) break;
-            const float4 v = vb[u];
-            const float xv = __fsub_rn(v.x, p[0]);
-            const float yv = __fsub_rn(v.y, p[1]);
-            const float zv = __fsub_rn(v.z, p[2]);
-            const float d2 = __fadd_rn(__fadd_rn(__fmul_rn(xv, xv), __fmul_rn(yv, yv)), __fmul_rn(zv, zv));
-            if (!(r2 == 0.f || d2 <= r2)) continue;
-            const int pid = __float_as_int(v.w);
-            if (kid < K) {
-              // fill phase (qpiw.py:500-506)
-#pragma unroll
-              for (int i = 0; i < KMAX; ++i) {
-                if (i == kid) {
-                  out[i] = pid;
-                  buf[i] = d2;
-                }
-              }
-              if (d2 > far2) {
-                far2 = d2;
-                far_ind = kid;
-              }
-              ++kid;
-            } else {
-              ++kid;
-              // replace phase (qpiw.py:507-518): strictly closer than the
-              // current farthest, then rescan for the first maximum.
-              if (d2 < far2) {
-#pragma unroll
-                for (int i = 0; i < KMAX; ++i) {
-                  if (i == far_ind) {
-                    out[i] = pid;
-                    buf[i] = d2;
-                  }
-                }
-                far2 = d2;
-#pragma unroll
-                for (int i = 0; i < KMAX; ++i) {
-                  if (i < K && buf[i] > far2) {
-                    far2 = buf[i];
-                    far_ind = i;
-                  }
-                }
-              }
-            }
-            }
-          }
+          knn_cell<KMAX>(occ_pts + (int64_t)slot * g.P, cnt, p, K, r2, buf, out, kid, far_ind, far2);
         }
       }
     }
