@@ -1165,8 +1165,12 @@ __global__ void k_point_pe3_bwd(const float* __restrict__ emb, const float* __re
   }
 }
 
+// hid rows for n_max samples rounded up to whole 64-sample tiles (the h2
+// planes layout, kHidTile in aggregate_x3.hip)
+static int64_t hid_rows(int64_t n_max) { return cdiv(n_max > 0 ? n_max : 1, 64) * 64; }
+
 static size_t scratch_need(int64_t n_max, int64_t n_points) {
-  const int64_t nm = n_max > 0 ? n_max : 1;
+  const int64_t nm = hid_rows(n_max);
   // + 4 ints: the split kernels' tile counter (k_pairs_x3 / k_pairs_h2)
   return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 4 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
          sizeof(float);
@@ -1176,13 +1180,13 @@ static size_t scratch_need(int64_t n_max, int64_t n_points) {
 // so its place does not depend on n_max and a later call may reuse it
 // (pnr_points.p1_ready)
 static void carve(AggArgs& a, void* scratch, int64_t n_max, int64_t n_p1) {
-  const int64_t nm = n_max > 0 ? n_max : 1;
+  const int64_t nm = hid_rows(n_max);
   a.p1 = static_cast<float*>(scratch);
   a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
   a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
 }
 static int32_t* tile_counter(const AggArgs& a, int64_t n_max) {
-  const int64_t nm = n_max > 0 ? n_max : 1;
+  const int64_t nm = hid_rows(n_max);
   return a.vmask + cdiv(nm, 4) * 4;
 }
 

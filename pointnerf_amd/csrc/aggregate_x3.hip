@@ -37,6 +37,13 @@ namespace {
 
 constexpr int kXT = 64;            // pairs per tile
 constexpr int kXTS = kXT / kKN;    // samples per tile
+// h2 K-summed features (k_pairs_h2 -> k_color_h2): f16-split planes, per tile of
+// 64 samples [plane 2][row group 32][64 samples][8 f16] = the colour kernel's
+// LDS image, so one global_load_lds wave-instruction copies one group (1 KB).
+// Samples without a valid neighbour are never written (the colour kernel
+// ignores their columns).
+constexpr int kHidPlane = 32 * 64 * 16;
+constexpr int kHidTile = 2 * kHidPlane;
 constexpr int kXG = 34;            // 8-row groups of a layer input (272 rows)
 constexpr int kPG = 8;             // 8-row groups of the distance PE (64 rows)
 constexpr int kPlaneX = kXG * kXT * 16;
@@ -904,10 +911,16 @@ __device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int sl
       A.vmask[vo] = sf;
       if (sf) A.out_feat[vo * (kC + 1)] = as;
     }
-    if (sf) {
-      f32x4n* dst = reinterpret_cast<f32x4n*>(A.hid + vo * kHid + 8 * ng);
-      __builtin_nontemporal_store((f32x4n){hs[0], hs[1], hs[2], hs[3]}, dst);
-      __builtin_nontemporal_store((f32x4n){hs[4], hs[5], hs[6], hs[7]}, dst + 1);
+    if (sf) {   // hid rows 8ng..8ng+7 as one 16-B piece per plane (kHidTile layout)
+      typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
+      unsigned a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) splith(hs[2 * i], hs[2 * i + 1], a[i], b[i]);
+      const u32x4n p0 = {a[0], a[1], a[2], a[3]}, p1 = {b[0], b[1], b[2], b[3]};
+      u32x4n* dst = reinterpret_cast<u32x4n*>(reinterpret_cast<char*>(A.hid) + (vo / kXT) * kHidTile +
+                                              (ng * kXT + vo % kXT) * 16);
+      dst[0] = p0;   // plain stores: the tile's 4 producer waves fill each 128-B line in
+      dst[kHidPlane / 16] = p1;   // 32-B pieces, merged in L2 (nontemporal: +1.4 ms)
     }
   }
 }
@@ -1035,37 +1048,18 @@ struct ColH2Args {
   float* out_feat;
 };
 
-// hid rows [g0, g0 + ng) x 8 of the tile's 64 samples -> planes (zero rows for
-// samples past n or without a valid neighbour, as k_color).  Item (sample s,
-// group gl) per lane: 16 samples x 4 groups per wave-instruction, so a global
-// read is 16 rows x 128 contiguous bytes and an LDS write 16 x 16 contiguous bytes.
-// vm: bit s = sample v0 + s is valid (< n, a valid neighbour); every item's
-// loads are issued unconditionally (row v0 stands in for an invalid sample and
-// is zeroed afterwards), so the loads of all items are in flight together.
-__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t v0, uint64_t vm, int g0,
-                                               int ng) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  f32x4n ra[10], rb[10];
+// hid row groups [G0, G0 + NG) of the tile's 64 samples (both planes) ->
+// plane groups 0..NG-1, by global_load_lds: no VGPR staging, no split work
+// (k_pairs_h2 stored the planes).  Wave w copies plane w.
+template <int G0, int NG>
+__device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t tile) {
+  const int lane = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const char* src = reinterpret_cast<const char*>(A.hid) + tile * kHidTile + lane * 16;
 #pragma unroll
-  for (int u = 0; u < 10; ++u) {
-    const int q = 2 * u + wid;
-    const int s = (lane & 15) + 16 * (q & 3), gl = (lane >> 4) + 4 * (q >> 2);
-    if (4 * (q >> 2) >= ng) continue;   // wave-uniform: no group of this item is loaded
-    const int64_t v = ((vm >> s) & 1) ? v0 + s : v0;
-    const f32x4n* src = reinterpret_cast<const f32x4n*>(A.hid + v * kHid + 8 * (g0 + (gl < ng ? gl : 0)));
-    ra[u] = __builtin_nontemporal_load(src);
-    rb[u] = __builtin_nontemporal_load(src + 1);
-  }
-#pragma unroll
-  for (int u = 0; u < 10; ++u) {
-    const int q = 2 * u + wid;
-    const int s = (lane & 15) + 16 * (q & 3), gl = (lane >> 4) + 4 * (q >> 2);
-    if (4 * (q >> 2) >= ng) continue;
-    if (gl >= ng) continue;
-    const bool ok = (vm >> s) & 1;
-    const float x[8] = {ok ? ra[u].x : 0.f, ok ? ra[u].y : 0.f, ok ? ra[u].z : 0.f, ok ? ra[u].w : 0.f,
-                        ok ? rb[u].x : 0.f, ok ? rb[u].y : 0.f, ok ? rb[u].z : 0.f, ok ? rb[u].w : 0.f};
-    store_group<true>(lds, kCPlane, gl, s, x);
+  for (int g = 0; g < NG; ++g) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + pl * kHidPlane + (G0 + g) * kXT * 16),
+        (__attribute__((address_space(3))) void*)(lds + pl * kCPlane + g * kXT * 16), 16, 0, 0);
   }
 }
 
@@ -1091,7 +1085,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int64_t v0 = tile * kXT;
     const uint64_t vm = __ballot(v0 + lane < n && A.vmask[v0 + lane] != 0);   // sample validity, one load
     // ---------------------------------------------------- layer 1, input rows 0..143 (hid)
-    color_load_hid(A, lds, v0, vm, 0, kCG);
+    color_load_hid<0, kCG>(A, lds, tile);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
@@ -1099,7 +1093,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r1b, voff);
     __syncthreads();
     // ---------------------------------------------------- rows 144..255 (hid), 256..279 (view PE), 280 (bias)
-    color_load_hid(A, lds, v0, vm, kCG, 14);
+    color_load_hid<kCG, 14>(A, lds, tile);
     if (wid == 0) {   // lane = sample: PE_4 of the rotated view direction (k_color's order)
       const int64_t v = v0 + lane;
       float vrot[3] = {0.f, 0.f, 0.f};
@@ -1158,9 +1152,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     // out_feat[v, 1 + 32 (T0 + T) + row] (valid samples only; the others keep their zeros)
     const float sc3 = A.scale[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)   // valid columns only: the others hold stale plane data
+      if ((vm >> (32 * (i >> 1) + c)) & 1)
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) chk = fmaf(0.f, acc[i][r] + acc[i][r + 1], chk);
+        for (int r = 0; r < 16; r += 2) chk = fmaf(0.f, acc[i][r] + acc[i][r + 1], chk);
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int64_t v = v0 + 32 * pt + c;
