@@ -1,7 +1,7 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out/abl
-timeout -k 10 300 python -u -m pytest tests/test_gpu_query.py tests/test_gpu_edge.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_q.log 2>&1
-for N in default prev; do
+PNR_LIB=tools/_ablate/oct/libpnr.so timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_x3.log 2>&1
+for N in default oct; do
   if [ $N = default ]; then L=""; else L=tools/_ablate/$N/libpnr.so; fi
   if [ -n "$L" ]; then export PNR_LIB=$L; else unset PNR_LIB; fi
   rm -rf gpurun_out/abl/$N
