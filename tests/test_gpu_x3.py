@@ -46,7 +46,7 @@ def _setup(sc, cuda, params=None, seed=0):
 SPLITS = ["x3", "h2"]
 
 
-def _both(agg, np_, sc, cuda, used=False, variant="x3", check_range=True):
+def _both(agg, np_, sc, cuda, used=False, variant="x3", check_range=True, scratch_fill=None):
     """fp32 and split-path features on one query -> (f32 [Sv,129], split [Sv,129]);
     used: P1 only for the referenced points (the training-batch layout)."""
     from pointnerf_amd import _lib as L
@@ -71,6 +71,8 @@ def _both(agg, np_, sc, cuda, used=False, variant="x3", check_range=True):
     for fn, extra in (("pnr_aggregate_fwd", ()), (f"pnr_aggregate_fwd_{variant}", (L.ctypes.byref(mlpx),))):
         f = torch.zeros((Sv, 129), device=cuda)
         scr = L.aggregate_scratch(Sv, n_p1, cuda)
+        if scratch_fill is not None:
+            scr.fill_(scratch_fill)
         L.check(getattr(L.lib(), fn)(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), *extra, L.ptr(f),
                                      None, None, L.ptr(scr), scr.numel() * 4, L.stream_ptr(cuda)), fn)
         outs.append(f)
@@ -223,3 +225,16 @@ def test_h2_colour_branch_overflow_sets_flag(cuda):
     with torch.no_grad():
         agg.color_branch[0].bias.fill_(0.0)
     _both(agg, np_, sc, cuda, variant="h2")   # asserts the flag stays clear
+
+
+def test_h2_stale_scratch_ignored(cuda):
+    """k_color_h2 copies the f16-split hid planes of whole 64-sample tiles; rows
+    past n (and of samples without a neighbour) are never written by k_pairs_h2.
+    Scratch full of NaN must change neither the features (bit for bit) nor the
+    range flag (_both asserts it stays clear)."""
+    sc = scene(20000, H=32, W=32, default_conf=None)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.3))
+    _, poisoned = _both(agg, np_, sc, cuda, variant="h2", scratch_fill=float("nan"))
+    _, clean = _both(agg, np_, sc, cuda, variant="h2", scratch_fill=0.0)
+    assert poisoned.shape[0] % 64 != 0   # a partial last tile is exercised
+    assert np.array_equal(poisoned, clean)
