@@ -1171,8 +1171,8 @@ static int64_t hid_rows(int64_t n_max) { return cdiv(n_max > 0 ? n_max : 1, 64) 
 
 static size_t scratch_need(int64_t n_max, int64_t n_points) {
   const int64_t nm = hid_rows(n_max);
-  // + 4 ints: the split kernels' tile counter (k_pairs_x3 / k_pairs_h2)
-  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 4 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
+  // + 8 ints: the split kernels' tile counters (k_pairs_x3 / k_pairs_h2, one per XCD group)
+  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 8 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
          sizeof(float);
 }
 

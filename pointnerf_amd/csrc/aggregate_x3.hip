@@ -120,8 +120,33 @@ struct X3Args {
 // wave 0, lane 0, one tile ahead; the index travels through LDS ring TQ), so
 // workgroups that start late or run slow (another kernel on the CU, an RCCL
 // copy) take fewer tiles instead of finishing late.
-__device__ __forceinline__ int64_t take_tile(const X3Args& A) {
-  return (int64_t)gridDim.x + atomicAdd(A.tile_ctr, 1);
+//
+// XCD-aware (large launches): blocks b and b + 8 share an XCD (round-robin
+// dispatch, MI355X_MICROARCH "Workgroup dispatch"), so block group b % 8 works
+// through its own contiguous eighth of the tiles with its own counter and then
+// helps the other groups.  Neighbouring tiles (the same or adjacent rays) share
+// most of their points, so their P1 rows are re-read from that XCD's L2.
+#ifndef PNR_XCD_TILES
+#define PNR_XCD_TILES 1
+#endif
+__device__ __forceinline__ bool xcd_mode(int64_t nt) { return PNR_XCD_TILES && nt >= 2 * (int64_t)gridDim.x + 16; }
+__device__ __forceinline__ int64_t xcd_lo(int64_t nt, int x) { return nt * x / 8; }
+__device__ __forceinline__ int64_t xcd_nb(int x) { return ((int)gridDim.x - x + 7) / 8; }   // blocks of group x
+
+__device__ __forceinline__ int64_t first_tile(int64_t nt) {
+  if (!xcd_mode(nt)) return blockIdx.x;
+  return xcd_lo(nt, blockIdx.x & 7) + (blockIdx.x >> 3);
+}
+
+__device__ __forceinline__ int64_t take_tile(const X3Args& A, int64_t nt) {
+  if (!xcd_mode(nt)) return (int64_t)gridDim.x + atomicAdd(A.tile_ctr, 1);
+  const int x0 = blockIdx.x & 7;
+  for (int i = 0; i < 8; ++i) {
+    const int x = (x0 + i) & 7;
+    const int64_t t = xcd_lo(nt, x) + xcd_nb(x) + atomicAdd(A.tile_ctr + x, 1);
+    if (t < xcd_lo(nt, x + 1)) return t;
+  }
+  return nt;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
@@ -644,7 +669,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #endif
   const int* TQ = reinterpret_cast<const int*>(lds + L::OffTq);
   int it = 0;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile = TQ[(it + 1) & 3], ++it) {
+  for (int64_t tile = first_tile(ntiles); tile < ntiles; tile = TQ[(it + 1) & 3], ++it) {
     const int buf = it & 1;
     X3_TR(0, 0);
     // ------------------------------------------------------------ block1.0 = P1 + W1[:, 224:] . PE_5
@@ -937,13 +962,13 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   unsigned p1e = 0;
   float dr6[6];
   GatherState g;
-  gather_row(A, blockIdx.x, lane, g);
+  gather_row(A, first_tile(ntiles), lane, g);
   gather_sample(A, lane, g);
   gather<H>(A, g, 0, 0, lds, pw, lane, dr6);
   pe_planes<H, 0>(lds, pw, lane, dr6);
   pe_planes<H, 1>(lds, pw, lane, dr6);
   int* TQ = reinterpret_cast<int*>(lds + L::OffTq);
-  if (pw == 0 && lane == 0) TQ[1] = (int)take_tile(A);
+  if (pw == 0 && lane == 0) TQ[1] = (int)take_tile(A, ntiles);
   X3_SYNC();   // P0: prow of the first tile visible to all producers, TQ[1] too
   p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
   X3_SYNC();   // S0
@@ -951,13 +976,13 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   TailState ts;
   int it = 0;
   int64_t prev = -1;   // the previous iteration's tile (its tail / alpha run one tile late)
-  for (int64_t tile = blockIdx.x; tile < ntiles; prev = tile, tile = TQ[(it + 1) & 3], ++it) {
+  for (int64_t tile = first_tile(ntiles); tile < ntiles; prev = tile, tile = TQ[(it + 1) & 3], ++it) {
     const int nbuf = (it & 1) ^ 1;
     const int nw = H ? (it + 1) % 3 : nbuf;   // Wt / Sf slot of the next tile
     const int64_t next = TQ[(it + 1) & 3];
     // the tile after next, published before S1 (only while this workgroup goes on:
     // a tile taken by a workgroup that stops would be lost)
-    if (pw == 0 && lane == 0) TQ[(it + 2) & 3] = next < ntiles ? (int)take_tile(A) : (int)ntiles;
+    if (pw == 0 && lane == 0) TQ[(it + 2) & 3] = next < ntiles ? (int)take_tile(A, ntiles) : (int)ntiles;
     X3_TR(1, 0);
     park_p1(p1r, p1e, lds, pw, lane);   // the layer-input planes are free since the last S7
     gather_row(A, next, lane, g);
@@ -1347,7 +1372,7 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.tile_ctr = tile_ctr;
-  PNR_HIP(hipMemsetAsync(tile_ctr, 0, sizeof(int32_t), st));
+  PNR_HIP(hipMemsetAsync(tile_ctr, 0, 8 * sizeof(int32_t), st));
   const int64_t tiles = cdiv(s.n_max, kXTS);
   if (H)
     hipLaunchKernelGGL(k_pairs_h2, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
