@@ -1,4 +1,7 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1 && \
-bash tools/prof_bench.sh r01f
+mkdir -p gpurun_out/prec
+REPS=2 bash tools/ab.sh pr2 pr1c1
+unset PNR_LIB
+for D in fp32 fp32x3 bf16; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --dtype $D > gpurun_out/prec/$D.json 2> gpurun_out/prec/$D.err || exit 1
+done
