@@ -1,7 +1,4 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out/prec
-REPS=2 bash tools/ab.sh pr2 pr1c1
-unset PNR_LIB
-for D in fp32 fp32x3 bf16; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --dtype $D > gpurun_out/prec/$D.json 2> gpurun_out/prec/$D.err || exit 1
-done
+mkdir -p gpurun_out
+REPS=2 bash tools/ab.sh sp3
+PNR_LIB=tools/_ablate/sp3t/libpnr.so timeout -k 10 300 python tools/x3_trace.py > gpurun_out/trace_sp3.log 2>&1
