@@ -55,7 +55,8 @@ def parse():
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="diagnostic (single process): do rank 0's share of an N-rank step (N partial frames of "
                          "1/N of the rays, no collective) to project per-rank overheads of the N-GPU run")
-    ap.add_argument("--cpu-rays", type=int, default=1500, help="rays in the CPU-baseline sample")
+    ap.add_argument("--cpu-rays", type=int, default=12000,
+                    help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--mode", choices=("render", "train"), default="render",
@@ -98,44 +99,116 @@ def cameras(n_frames, H, W):
     return cams
 
 
+def cpu_threads():
+    """Host threads of the CPU baseline: the process's CPU share (OMP_NUM_THREADS
+    on the GPU box, else the affinity mask), never more than os.cpu_count()."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
 def cpu_baseline(args, opt, pts, feats, agg, cam, H, W):
     """The oracle (CPU port of the reference path) on a bounded sample of the
     same workload: grid build once + query/aggregate/composite of a random
-    subset of one frame's rays, extrapolated to the frame."""
+    subset of one frame's rays, extrapolated to the frame.  Returns (baseline
+    dict, sampled ray indices, the oracle's render of them)."""
     try:
         from threadpoolctl import threadpool_limits
     except Exception:  # pragma: no cover
         threadpool_limits = None
     from oracle import oracle as O
-    threads = 16
+    threads = cpu_threads()
     ctx = threadpool_limits(limits=threads) if threadpool_limits else None
     torch.set_num_threads(threads)
+    O.set_threads(threads)
     emb, color, dirs, conf = feats
     points = dict(xyz=pts, emb=emb.numpy(), color=color.numpy(), dir=dirs.numpy(), conf=conf.numpy())
     params = {k: v.detach().cpu().numpy() for k, v in agg.state_dict().items()}
     campos, camrot, rd = cam
     rng = np.random.default_rng(0)
-    sel = rng.choice(rd.shape[0], size=min(args.cpu_rays, rd.shape[0]), replace=False)
+    sel = np.sort(rng.choice(rd.shape[0], size=min(args.cpu_rays, rd.shape[0]), replace=False))
     bg = np.random.default_rng(1).uniform(size=128).astype(np.float32)
     t0 = time.perf_counter()
     grid = O.grid_build(opt, pts)
     t1 = time.perf_counter()
     q = O.query_points(opt, pts, campos, camrot, rd[sel], near=opt.near_plane, far=opt.far_plane, grid=grid)
-    O.render(opt, points, params, campos, camrot, rd[sel], bg, q=q)
+    ref = O.render(opt, points, params, campos, camrot, rd[sel], bg, q=q)
     t2 = time.perf_counter()
     if ctx is not None:
         ctx.__exit__(None, None, None)
     R = H * W
     t_frame = (t1 - t0) + (t2 - t1) * R / len(sel)
-    return {"value": round(R * opt.SR / t_frame / 1e6, 4), "unit": "Mray-samples/s", "cores": threads,
-            "kind": "port",
-            "sample": (f"oracle/ (C query, 1 thread; NumPy fp32 aggregate/composite, BLAS {threads} threads) "
-                       f"on {len(sel)} random rays of one {H}x{W} frame, {args.points} points: grid build "
-                       f"{t1 - t0:.2f}s + sample {t2 - t1:.2f}s, extrapolated to the frame "
-                       f"({t_frame:.1f}s/frame)")}
+    out = {"value": round(R * opt.SR / t_frame / 1e6, 4), "unit": "Mray-samples/s", "cores": threads,
+           "kind": "port",
+           "sample": (f"oracle/ (C query: serial grid build + OpenMP ray/sample loops; NumPy fp32 "
+                      f"aggregate/composite, BLAS) with {threads} threads (os.cpu_count() = {os.cpu_count()}) on "
+                      f"{len(sel)} random rays of one {H}x{W} frame, {args.points} points: grid build "
+                      f"{t1 - t0:.2f}s + sample {t2 - t1:.2f}s, extrapolated to the frame "
+                      f"({t_frame:.1f}s/frame)")}
+    return out, sel, ref
+
+
+def psnr_db(a, b):
+    """10 log10(peak^2 / MSE) with peak = max|b| (the reference values)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    mse = float(np.mean((a - b) ** 2))
+    return round(10 * np.log10(float(np.abs(b).max()) ** 2 / max(mse, 1e-300)), 2)
 
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def executed_roofline(args, stage, launches, avg_agg_s):
+    """The aggregate's EXECUTED matrix work against the dense peak of the MFMA
+    it runs on: per pair 428 032 fp32 FLOP (block1.0's 224 point columns are
+    evaluated once per point, not per pair: 114 688 FLOP x N points), per valid
+    sample 137 216; fp32h2 issues 3 f16 products per fp32 MAC (2.5 PF dense
+    f16), bf16 one bf16 product, fp32 / fp32x3 reported on their own peak."""
+    n = max(launches, 1)
+    ex = (stage["pairs"] * 428_032 + stage["valid"] * FLOP_PER_SAMPLE) / n + args.points * 114_688
+    mult, peak = {"fp32h2": (3, BF16_MFMA_PEAK_TFLOPS), "bf16": (1, BF16_MFMA_PEAK_TFLOPS),
+                  "fp32x3": (6, BF16_MFMA_PEAK_TFLOPS), "fp32": (1, FP32_MFMA_PEAK_TFLOPS)}[args.dtype]
+    tf = mult * ex / avg_agg_s / 1e12 if avg_agg_s > 0 else 0.0
+    return {"fp32_flops_per_launch": ex, "mfma_products_per_fp32_mac": mult, "achieved": round(tf, 2),
+            "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4)}
+
+
+@torch.no_grad()
+def accuracy_vs_oracle(model, opt, cam, bg, sel, ref):
+    """The metric's PSNR half: the GPU render of the CPU-baseline rays against
+    the oracle's render of the same rays (same points, weights, cameras)."""
+    campos, camrot, rd = cam
+    idx = torch.from_numpy(sel).to(rd.device)
+    color, _, _, mask = model.render_rays(campos, camrot, rd[idx].contiguous(), opt.near_plane, opt.far_plane, bg)
+    got = color.cpu().numpy()
+    want = ref["coarse_raycolor"]
+    hit = ref["ray_mask"] > 0
+    return {"oracle_rays": int(len(sel)), "oracle_rays_hit": int(hit.sum()),
+            "ray_mask_equal": bool(np.array_equal(mask.cpu().numpy(), ref["ray_mask"])),
+            "psnr_vs_oracle_db": psnr_db(got[hit], want[hit]),
+            "max_abs_err_vs_oracle": float(np.abs(got - want).max())}
+
+
+@torch.no_grad()
+def accuracy_vs_x3(model, opt, cam, bg, dtype):
+    """Full frame: the headline arithmetic against fp32x3 (exact fp32 products,
+    test_gpu_x3.py) on the same frame, outside the timed region."""
+    campos, camrot, rd = cam
+    a = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg)
+    prec = model.precision
+    model.precision = "fp32x3"
+    try:
+        b = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg)
+    finally:
+        model.precision = prec
+    hit = (b[3] > 0).cpu().numpy()
+    x, y = a[0].cpu().numpy(), b[0].cpu().numpy()
+    return {f"psnr_{dtype}_vs_fp32x3_full_frame_db": psnr_db(x[hit], y[hit]),
+            f"max_abs_err_{dtype}_vs_fp32x3_full_frame": float(np.abs(x - y).max()),
+            "full_frame_rays_hit": int(hit.sum())}
 
 
 def stage_rooflines(args, opt, model, stage, per, launches):
@@ -370,7 +443,7 @@ def main():
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if args.dtype in ("fp32", "fp32x3", "fp32h2") else args.dtype,
+            "dtype": args.dtype,
             "arith": {"fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
                       "fp32x3": "fp32-accurate: exact 3-way bf16 split of each fp32 operand, 6 cross products on "
                                 "v_mfma_f32_32x32x16_bf16, fp32 accumulation (error vs an fp64 oracle = native "
@@ -401,7 +474,8 @@ def main():
                                        "fp32h2": "fp32-equivalent: f16 MFMA dense peak / 3 products per fp32 MAC",
                                        "bf16": "bf16 MFMA dense peak"}[args.dtype],
                          "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3)},
+                         "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3),
+                         "executed": executed_roofline(args, stage, launches, avg_agg_s)},
             "stages_ms": {k: round(float(np.mean(v)), 3) for k, v in per.items()},
             "frames_per_s": round(world * args.steps / t_max, 3),
             "rays_per_s_M": round(H * W * world * args.steps / t_max / 1e6, 3),
@@ -416,11 +490,16 @@ def main():
         if shard_world != world:
             out["config"]["emulated_world"] = shard_world   # diagnostic: rank 0's share of an N-rank step
         out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per, launches)
+        acc = {}
         if not args.no_cpu_baseline and world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args, opt, pts, feats, agg, cams[0], H, W)
+                out["cpu_baseline"], sel, ref = cpu_baseline(args, opt, pts, feats, agg, cams[0], H, W)
+                acc.update(accuracy_vs_oracle(model, opt, dev_cams[0], bg, sel, ref))
             except Exception as e:  # the baseline must never hide the GPU number
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if world == 1 and args.dtype in ("fp32h2", "bf16"):
+            acc.update(accuracy_vs_x3(model, opt, dev_cams[0], bg, args.dtype))
+        out["accuracy"] = acc
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

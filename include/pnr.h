@@ -38,6 +38,10 @@
  *                           models/rendering/diff_ray_marching.py:509-555
  *   pnr_ray_march_fwd    <- ray_march on dense [B,R,SR,C+1] features
  *                           models/rendering/diff_ray_marching.py:509-555
+ *   pnr_rgb_head_fwd/bwd <- the upstream colour head the fork commented out:
+ *                           color_branch Linear(128,3) + raw2out_color
+ *                           models/aggregators/point_aggregators.py:343, 269-273, 637-638
+ *                           (radiance_render [..., 1:4], diff_render_func.py:48-50)
  */
 #ifndef PNR_H_
 #define PNR_H_
@@ -49,7 +53,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 4
+#define PNR_ABI_VERSION 5
 
 enum {
   PNR_OK = 0,
@@ -465,6 +469,21 @@ typedef struct {
 int pnr_neural_render_scratch_bytes(int32_t H, int32_t W, size_t* out);
 int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const pnr_neural_render_w* w,
                           float* out_rgb, void* scratch, size_t scratch_bytes, void* stream);
+
+/* ------------------------------------------------------ upstream RGB head
+ * C_out = 3 mode (shading_color_channel_num 3): for v < min(*n_dev, n_max)
+ * (n_dev may be NULL), with feat rows of ld >= 129 floats [alpha, f_1..f_128]:
+ *   out[v, 0] = feat[v, 0]
+ *   out[v, 1 + j] = raw2out_color(sum_c w[j*128 + c] f_c + b[j]),  j < 3
+ *   raw2out_color(x) = sigmoid(x) * (1 + 2e-3) - 1e-3 if act_super > 0, else sigmoid(x)
+ * Backward: d_feat[v, 0] = d_out[v, 0], d_feat[v, 1 + c] = sum_j g_j w[j, c] for
+ * the same rows (other rows untouched); d_wb[3, 129] += (d W | d b) (atomic
+ * accumulation: the caller zeroes it). */
+int pnr_rgb_head_fwd(const float* feat, int64_t ld, const int32_t* n_dev, int64_t n_max, const float* w,
+                     const float* b, int32_t act_super, float* out, void* stream);
+int pnr_rgb_head_bwd(const float* d_out, const float* feat, int64_t ld, const int32_t* n_dev, int64_t n_max,
+                     const float* w, const float* b, int32_t act_super, float* d_feat, float* d_wb,
+                     void* stream);
 
 /* ------------------------------------------------------------- utilities */
 /* Exclusive scan of n int32 values (n_dev: optional device-side length <= n,

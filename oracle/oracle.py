@@ -45,11 +45,18 @@ def _load():
         lib.oracle_ray_march.restype = None
         lib.oracle_ray_march.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, P, P, P, P, P, P]
+        lib.oracle_set_threads.restype = None
+        lib.oracle_set_threads.argtypes = [ctypes.c_int]
         lib.oracle_knn.restype = ctypes.c_int64
         lib.oracle_knn.argtypes = [P, P, ctypes.c_int64, P, P, P, P, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_float, P, P, P, P]
         _lib = lib
     return _lib
+
+
+def set_threads(n: int):
+    """OpenMP threads of the C query's ray / sample loops (results do not depend on it)."""
+    _load().oracle_set_threads(int(n))
 
 
 def _p(a: np.ndarray):
@@ -209,6 +216,7 @@ def query_points(opt, xyz, campos, camrot, raydir, mid_t=None, near=None, far=No
     flat = np.ascontiguousarray(sloc_w[smask])
     pidx_f = np.full((flat.shape[0], K), -1, np.int32)
     ks = np.ascontiguousarray(np.asarray(opt.kernel_size, np.int32))
+    assert K <= 64, "oracle_knn keeps at most 64 neighbours"
     if flat.shape[0]:
         lib.oracle_knn(_p(xyz), _p(flat), flat.shape[0], _p(shift), _p(vs), _p(dims), _p(ks), K,
                        opt.P, float(hp["radius_limit2"]), _p(grid["coor_2_occ"]),
@@ -371,6 +379,15 @@ def aggregate(params, sampled_color, sampled_Rw2c, sampled_dir, sampled_conf, sa
     c = np.concatenate([f, vpe], -1)
     for name in ("color_branch.0", "color_branch.2", "color_branch.4"):
         c = _lrelu(_lin(c, params, name), neg_slope)
+    if C == 3:
+        # upstream colour head, commented out in the fork: the final Linear(in, 3)
+        # (point_aggregators.py:343) and raw2out_color (:269-273, :637): sigmoid,
+        # then * (1 + 2e-3) - 1e-3 when act_super > 0 (parity unpinned: no
+        # reference code path runs it)
+        z = _lin(c, params, "color_branch.6").astype(np.float64)
+        c = (1.0 / (1.0 + np.exp(-z))).astype(F32)
+        if act_super > 0:
+            c = (c * F32(1 + 2e-3) - F32(1e-3)).astype(F32)
     flat = out.reshape(-1, C + 1)
     flat[ray_valid.reshape(-1)] = np.concatenate([alpha, c], -1)
     return out, ray_valid, w, confc

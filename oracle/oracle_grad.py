@@ -19,7 +19,7 @@ F = torch.float32
 
 def positional_encoding(x: torch.Tensor, freqs: int, ori: bool = False) -> torch.Tensor:
     # networks.py:175-190: bands 2^f, no pi; interleaved sin/cos per (channel, band)
-    bands = 2.0 ** torch.arange(freqs, dtype=F)
+    bands = 2.0 ** torch.arange(freqs, dtype=x.dtype)
     pts = (x[..., None] * bands).reshape(x.shape[:-1] + (-1,))
     if ori:
         return torch.cat([x, torch.sin(pts), torch.cos(pts)], -1)
@@ -35,7 +35,10 @@ def aggregate(params: dict, sampled_color, sampled_dir, sampled_conf, sampled_em
               sampled_xyz, sample_pnt_mask, sample_loc, sample_loc_w, sample_ray_dirs, rw2c=None,
               neg_slope: float = 0.01, act_super: int = 1, C: int = 128):
     """Inputs [R,SR,K,.] (B dropped), params name -> tensor (requires_grad as
-    wanted).  Returns features [R,SR,C+1], ray_valid, weight, conf_coefficient."""
+    wanted).  Returns features [R,SR,C+1], ray_valid, weight, conf_coefficient.
+    Evaluated in the dtype of sampled_embedding (fp32 = the reference; fp64 =
+    the high-precision truth the fp32 errors are measured against)."""
+    F = sampled_embedding.dtype
     mask = sample_pnt_mask.bool()
     R, SR, K = mask.shape
     ray_valid = mask.any(-1)
@@ -81,6 +84,10 @@ def aggregate(params: dict, sampled_color, sampled_dir, sampled_conf, sampled_em
     c = torch.cat([f, vpe], -1)
     for n in ("color_branch.0", "color_branch.2", "color_branch.4"):
         c = act(lin(c, n))
+    if C == 3:   # upstream head: Linear(128, 3) + raw2out_color (point_aggregators.py:343, 269-273)
+        c = torch.sigmoid(lin(c, "color_branch.6"))
+        if act_super > 0:
+            c = c * (1 + 2e-3) - 1e-3
     out = torch.zeros((R * SR, C + 1), dtype=F).index_put((rv.nonzero()[:, 0],), torch.cat([alpha, c], -1))
     return out.view(R, SR, C + 1), ray_valid, w, confc
 
@@ -88,7 +95,7 @@ def aggregate(params: dict, sampled_color, sampled_dir, sampled_conf, sampled_em
 def ray_march(ray_dist, ray_valid, ray_features, bg_color=None):
     """diff_ray_marching.py:509-555 with radiance_render / alpha_blend; inputs
     [NR,SR], [NR,SR], [NR,SR,C+1]; returns ray_color [NR,C] (+ bg)."""
-    sigma = ray_features[..., 0] * ray_valid.to(F)
+    sigma = ray_features[..., 0] * ray_valid.to(ray_features.dtype)
     opacity = 1 - torch.exp(-sigma * ray_dist)
     acc = torch.cumprod(1.0 - opacity + 1e-10, dim=-1)
     T = torch.cat([torch.ones_like(acc[..., :1]), acc[..., :-1]], -1)

@@ -31,6 +31,9 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <string.h>
 
 static int vox(float p, float shift, float vs) { return (int)floorf((p - shift) / vs); }
@@ -106,6 +109,8 @@ void oracle_ray_march(const float campos[3], const float* raydir, int64_t R, con
                       int tvals_per_ray, int D, int SR, const float shift[3], const float vs[3],
                       const int dims[3], const uint8_t* coor_occ, int32_t* n_filled,
                       int32_t* slot_d) {
+  /* rays are independent (one thread per ray in the reference): parallel over rays */
+#pragma omp parallel for schedule(dynamic, 256)
   for (int64_t r = 0; r < R; ++r) {
     int cnt = 0;
     const float* tv = tvals + (tvals_per_ray ? r * D : 0);
@@ -130,8 +135,10 @@ int64_t oracle_knn(const float* xyz, const float* loc, int64_t n_samples, const 
                    float radius_limit2, const int32_t* coor_2_occ, const int32_t* occ_numpnts,
                    const int32_t* occ_2_pnts, int32_t* pidx) {
   int64_t pairs = 0;
-  float* buf = (float*)malloc(sizeof(float) * (size_t)K);
+  /* samples are independent (one thread per sample in the reference) */
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : pairs)
   for (int64_t s = 0; s < n_samples; ++s) {
+    float buf[64];
     const float cx = loc[s * 3], cy = loc[s * 3 + 1], cz = loc[s * 3 + 2];
     const int fx = vox(cx, shift[0], vs[0]), fy = vox(cy, shift[1], vs[1]), fz = vox(cz, shift[2], vs[2]);
     int32_t* out = pidx + s * K;
@@ -185,6 +192,15 @@ int64_t oracle_knn(const float* xyz, const float* loc, int64_t n_samples, const 
     }
     pairs += kid < K ? kid : K;
   }
-  free(buf);
   return pairs;
+}
+
+/* OpenMP thread count of the ray / sample loops (the grid build stays serial:
+ * its slot order is the serial schedule). */
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
 }

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class PnrError(RuntimeError):
@@ -162,6 +162,10 @@ SIGNATURES = {
     "pnr_neural_render_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
     "pnr_neural_render_fwd": (c_int, [c_void_p, c_int32, c_int32, P(NeuralRenderW), c_void_p, c_void_p, c_size_t,
                                       c_void_p]),
+    "pnr_rgb_head_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p,
+                                 c_void_p]),
+    "pnr_rgb_head_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32,
+                                 c_void_p, c_void_p, c_void_p]),
     "pnr_scan_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
     "pnr_exclusive_scan_i32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),

@@ -24,11 +24,16 @@ SUPPORTED = dict(which_agg_model="viewmlp", agg_intrp_order=2, agg_distance_kern
                  num_viewdir_freqs=4, shading_feature_num=256, shading_feature_mlp_layer1=2,
                  shading_feature_mlp_layer2=0, shading_feature_mlp_layer3=2,
                  shading_alpha_mlp_layer=1, shading_color_mlp_layer=4,
-                 shading_color_channel_num=128, apply_pnt_mask=1, agg_weight_norm=1)
+                 apply_pnt_mask=1, agg_weight_norm=1)
+# C_out: 128 = the fork (colour head cut, point_aggregators.py:343, 637-638);
+# 3 = upstream (Linear(128, 3) + raw2out_color restored, rgb_head.hip)
+COLOR_CHANNELS = (128, 3)
 
 
 def check_supported(opt):
     bad = {k: (getattr(opt, k, v), v) for k, v in SUPPORTED.items() if getattr(opt, k, v) != v}
+    if getattr(opt, "shading_color_channel_num", 128) not in COLOR_CHANNELS:
+        bad["shading_color_channel_num"] = (opt.shading_color_channel_num, COLOR_CHANNELS)
     if getattr(opt, "dist_xyz_deno", 0.0) != 0.0:
         bad["dist_xyz_deno"] = (opt.dist_xyz_deno, 0.0)
     for k in ("agg_feat_xyz_mode", "agg_alpha_xyz_mode", "agg_color_xyz_mode"):
@@ -215,8 +220,11 @@ class PointAggregator(nn.Module):
         self.block1 = nn.Sequential(nn.Linear(284, 256), mk(), nn.Linear(256, 256), mk())
         self.block3 = nn.Sequential(nn.Linear(263, 256), mk(), nn.Linear(256, 256), mk())
         self.alpha_branch = nn.Sequential(nn.Linear(256, 1))
-        self.color_branch = nn.Sequential(nn.Linear(280, 128), mk(), nn.Linear(128, 128), mk(),
-                                          nn.Linear(128, 128), mk())
+        self.C = int(getattr(opt, "shading_color_channel_num", 128))
+        cb = [nn.Linear(280, 128), mk(), nn.Linear(128, 128), mk(), nn.Linear(128, 128), mk()]
+        if self.C == 3:   # upstream colour head (point_aggregators.py:343): color_branch.6
+            cb.append(nn.Linear(128, 3))
+        self.color_branch = nn.Sequential(*cb)
         for s in (self.block1, self.block3, self.alpha_branch, self.color_branch):
             _init_seq(s)
         self._packed = None
@@ -345,6 +353,27 @@ class PointAggregator(nn.Module):
         pk = getattr(self, "_packedh2", None)
         return pk is None or int(pk[1]["range_flag"].item()) == 0
 
+    def rgb_head(self):
+        """(W [3,128], b [3]) of the upstream colour head color_branch.6 (C_out = 3)."""
+        lin = self.color_branch[6]
+        return lin.weight.detach().float().contiguous(), lin.bias.detach().float().contiguous()
+
+    def apply_rgb_head(self, feat: torch.Tensor, n_dev=None, n: int | None = None) -> torch.Tensor:
+        """[n, 129] decoded features -> [n, 4] = [alpha, raw2out_color(color_branch.6(f))]
+        on pnr_rgb_head_fwd (point_aggregators.py:343, 269-273, 637-638), or
+        through RgbHeadFn when gradients are wanted."""
+        n = feat.shape[0] if n is None else int(n)
+        if torch.is_grad_enabled() and (feat.requires_grad or self.color_branch[6].weight.requires_grad):
+            from .train import RgbHeadFn
+            lin = self.color_branch[6]
+            return RgbHeadFn.apply(feat, lin.weight, lin.bias, self.act_super, n_dev, n)
+        w, b = self.rgb_head()
+        out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=feat.device)[:n]
+        L.check(L.lib().pnr_rgb_head_fwd(L.ptr(feat), feat.stride(0), L.ptr(n_dev), n, L.ptr(w), L.ptr(b),
+                                         self.act_super, L.ptr(out), L.stream_ptr(feat.device)),
+                "pnr_rgb_head_fwd")
+        return out
+
     def set_rw2c(self, rw2c: torch.Tensor | None):
         """Uniform Rw2c of the point cloud (neural_points.py:289; eye by default)."""
         with torch.no_grad():
@@ -364,13 +393,13 @@ class PointAggregator(nn.Module):
         B, R, SR, K = sample_pnt_mask.shape
         rows = B * R * SR
         dev = sample_loc_w.device
-        C = 128
+        C = 128   # the decoded features; the upstream head (C_out = 3) is applied at the end
         ray_valid = torch.any(sample_pnt_mask, dim=-1)
         weight = torch.empty((rows, K), dtype=torch.float32, device=dev)
         conf = torch.empty((rows, K), dtype=torch.float32, device=dev)
         if rows == 0:
-            out = torch.zeros((rows, C + 1), dtype=torch.float32, device=dev)
-            return out.view(B, R, SR, C + 1), ray_valid, weight.view(B, R, SR, K), conf.view(B, R, SR, K)
+            out = torch.zeros((rows, self.C + 1), dtype=torch.float32, device=dev)
+            return out.view(B, R, SR, self.C + 1), ray_valid, weight.view(B, R, SR, K), conf.view(B, R, SR, K)
 
         def flat(t, c):
             return None if t is None else t.reshape(-1, c).float().contiguous()
@@ -420,8 +449,11 @@ class PointAggregator(nn.Module):
             else:
                 conf = torch.ones((rows, K), dtype=torch.float32, device=dev)
         weight, conf = weight.view(B, R, SR, K), conf.view(B, R, SR, K)
+        if self.C == 3:
+            out = self.apply_rgb_head(out)
+            out = out * ray_valid.reshape(-1, 1).to(out.dtype)   # output_placeholder zeros (:643-645)
         o = self.opt
         if (getattr(o, "sparse_loss_weight", 0) <= 0 and "conf_coefficient" not in getattr(o, "zero_one_loss_items", [])
                 and getattr(o, "prob", 0) == 0):
             weight, conf = None, None
-        return out.view(B, R, SR, C + 1), ray_valid, weight, conf
+        return out.view(B, R, SR, self.C + 1), ray_valid, weight, conf

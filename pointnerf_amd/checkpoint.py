@@ -82,7 +82,7 @@ def prune(points: NeuralPoints, thresh: float):
     o = points.opt
     mask = points.points_conf.detach()[0, :, 0] >= thresh
     with torch.no_grad():
-        points.xyz = _param(points.xyz[mask, :], getattr(o, "xyz_grad", 0) > 0)
+        points.xyz = _param(points.xyz[mask, :], False)
         points.points_embeding = _param(points.points_embeding[:, mask, :], getattr(o, "feat_grad", 1) > 0)
         points.points_conf = _param(points.points_conf[:, mask, :], getattr(o, "conf_grad", 1) > 0)
         if points.points_dir is not None:
@@ -97,7 +97,7 @@ def grow_points(points: NeuralPoints, add_xyz, add_embedding, add_color=None, ad
     o = points.opt
     dev = points.xyz.device
     with torch.no_grad():
-        points.xyz = _param(torch.cat([points.xyz, add_xyz.to(dev).float()], 0), getattr(o, "xyz_grad", 0) > 0)
+        points.xyz = _param(torch.cat([points.xyz, add_xyz.to(dev).float()], 0), False)
         points.points_embeding = _param(torch.cat([points.points_embeding, add_embedding.to(dev).float()[None]], 1),
                                         getattr(o, "feat_grad", 1) > 0)
         if points.points_conf is not None:

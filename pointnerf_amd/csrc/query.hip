@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(kQBlock) k_march(QRays q, QGrid g, int SR,
       const int y = vox_coord(p[1], g.shift[1], g.vs[1]);
       const int z = vox_coord(p[2], g.shift[2], g.vs[2]);
       if (x < 0 || x >= g.dims[0] || y < 0 || y >= g.dims[1] || z < 0 || z >= g.dims[2]) continue;
-      const int id = (x * g.dims[1] + y) * g.dims[2] + z;
+      const int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
       if ((occ_bits[id >> 5] >> (id & 31)) & 1u) {
         slot_d[r * SR + n] = (uint16_t)d;
         ++n;
@@ -206,7 +206,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
       for (int y = y0; y < y1; ++y) {
         for (int z = z0; z < z1; ++z) {
           if (max(abs(z), max(abs(x), abs(y))) != layer) continue;
-          const int cell = ((fx + x) * g.dims[1] + (fy + y)) * g.dims[2] + (fz + z);
+          const int64_t cell = ((int64_t)(fx + x) * g.dims[1] + (fy + y)) * g.dims[2] + (fz + z);
           const int slot = coor_2_occ[cell];
           if (slot < 0) continue;
           const int cnt = min(g.P, occ_numpnts[slot]);

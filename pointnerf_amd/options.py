@@ -29,9 +29,34 @@ LEGO = dict(
 )
 
 
+# Per-scene overrides of the other BASELINE configs (the flag values each
+# reference script passes; everything else as in lego.sh).
+FLAGSETS = {
+    "lego": {},
+    # dev_scripts/w_n360/ship.sh (config c3)
+    "ship": dict(ranges=[-1.277, -1.300, -0.550, 1.371, 1.349, 0.729], P=10, max_o=1500000),
+    # dev_scripts/w_scannet_etf/scene101.sh (config c4)
+    "scene101": dict(vsize=[0.008, 0.008, 0.008], ranges=[-10.0, -10.0, -10.0, 10.0, 10.0, 10.0], SR=24, P=30,
+                     max_o=2000000, near_plane=0.1, far_plane=8.0, default_conf=-1.0),
+    # dev_scripts/w_tt_ft/truck.sh (config c5): kernel 5 = three Chebyshev shells, query (dilation) 3
+    "truck": dict(vsize=[0.002, 0.002, 0.002], kernel_size=[5, 5, 5], query_size=[3, 3, 3],
+                  ranges=[-1.125, -0.598, -1.052, 0.795, 0.203, 1.029], SR=40, P=10, max_o=1600000,
+                  near_plane=0.0, far_plane=3.5, default_conf=0.1),
+}
+
+
 def lego_opt(**over):
     o = dict(LEGO)
     o.update(over)
     if o["query_size"][0] == 0:
         o["query_size"] = list(o["kernel_size"])
     return SimpleNamespace(**o)
+
+
+def flagset_opt(name: str, **over):
+    """Flag set of one reference scene script (FLAGSETS) plus overrides."""
+    if name not in FLAGSETS:
+        raise KeyError(f"unknown flag set {name!r}: one of {sorted(FLAGSETS)}")
+    o = dict(FLAGSETS[name])
+    o.update(over)
+    return lego_opt(**o)

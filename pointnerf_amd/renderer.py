@@ -32,6 +32,9 @@ class NeuralPoints(nn.Module):
                  Rw2c=None):
         super().__init__()
         self.opt = opt
+        if getattr(opt, "xyz_grad", 0) > 0:
+            raise L.PnrError("xyz_grad > 0 (point-position gradients, neural_points.py:270) is not "
+                             "implemented by libpnr's backward; run with --xyz_grad 0")
         self.device = torch.device(device)
         self.xyz = nn.Parameter(torch.zeros((0, 3), device=self.device), requires_grad=False)
         self.points_embeding = nn.Parameter(torch.zeros((1, 0, 32), device=self.device))
@@ -44,10 +47,14 @@ class NeuralPoints(nn.Module):
         self.querier = lighting_fast_querier(self.device, opt)
 
     def set_points(self, xyz, embedding, color=None, dirs=None, conf=None, Rw2c=None):
-        """set_points (neural_points.py:480-546) with point_*_mode '1'."""
+        """set_points (neural_points.py:480-546) with point_*_mode '1'.
+        xyz gradients (--xyz_grad 1, neural_points.py:270) are not implemented
+        by the HIP backward: refused here instead of silently dropped."""
+        if getattr(self.opt, "xyz_grad", 0) > 0:
+            raise L.PnrError("xyz_grad > 0 (point-position gradients, neural_points.py:270) is not "
+                             "implemented by libpnr's backward; run with --xyz_grad 0")
         dev = self.device
-        self.xyz = nn.Parameter(xyz.to(dev).float().reshape(-1, 3).contiguous(),
-                                requires_grad=getattr(self.opt, "xyz_grad", 0) > 0)
+        self.xyz = nn.Parameter(xyz.to(dev).float().reshape(-1, 3).contiguous(), requires_grad=False)
         self.points_embeding = nn.Parameter(embedding.to(dev).float().reshape(1, -1, 32).contiguous())
         self.points_color = None if color is None else nn.Parameter(color.to(dev).float().reshape(1, -1, 3).contiguous())
         self.points_dir = None if dirs is None else nn.Parameter(dirs.to(dev).float().reshape(1, -1, 3).contiguous())
@@ -125,10 +132,24 @@ class NeuralPointsRayMarching(nn.Module):
             from .neural_render import NeuralRenderer
             self.neural_render_2d = NeuralRenderer(input_dim=128).to(neural_points.device)
         self.last_counts = None
+        self._rw2c_key = None
         if getattr(opt, "which_render_func", "radiance") != "radiance" or \
                 getattr(opt, "which_blend_func", "alpha") != "alpha" or \
                 getattr(opt, "which_tonemap_func", "off") != "off":
             raise L.PnrError("libpnr implements radiance render, alpha blend and tone map 'off'")
+
+    def _sync_rw2c(self):
+        """The aggregator renders with NeuralPoints.Rw2c (neural_points.py:289;
+        applied to view dirs, distances and point dirs at
+        point_aggregators.py:506, 526, 566): copied into the aggregator's
+        buffer whenever the points' Rw2c tensor (storage or version) changes."""
+        rw = self.neural_points.Rw2c
+        key = (rw.data_ptr(), rw._version, tuple(rw.shape))
+        if key != self._rw2c_key:
+            if rw.dim() != 2:
+                raise L.PnrError("per-point Rw2c is not implemented by libpnr (uniform Rw2c only)")
+            self.aggregator.set_rw2c(rw.detach())
+            self._rw2c_key = key
 
     @torch.no_grad()
     def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None,
@@ -148,6 +169,7 @@ class NeuralPointsRayMarching(nn.Module):
         chunk); if an activation left the f16 range, the call is rendered again
         on the fp32x3 path (bf16 split: same accuracy, fp32 range) and h2 stays
         off for these weights until they change (``h2_fallbacks`` counts it)."""
+        self._sync_rw2c()
         prec = self.precision
         if prec == "fp32h2" and self._h2_blocked_key is not None:
             if self._h2_blocked_key == self.aggregator.h2_key():
@@ -175,7 +197,8 @@ class NeuralPointsRayMarching(nn.Module):
         if force_grid:
             q.grid.key = None
         R = raydir.shape[0]
-        SR, K, C = opt.SR, opt.K, 128
+        SR, K = opt.SR, opt.K
+        C = self.aggregator.C          # 128 (fork) or 3 (upstream RGB head)
         f32 = dict(dtype=torch.float32, device=dev)
         ray_color = torch.empty((R, C), **f32)
         opacity = torch.empty((R, SR), **f32)
@@ -185,7 +208,7 @@ class NeuralPointsRayMarching(nn.Module):
         if bg is not None and bg.numel() != C:
             bg = bg.expand(C).contiguous() if bg.numel() == 1 else None
             if bg is None:
-                raise L.PnrError("bg_color must have 1 or 128 channels")
+                raise L.PnrError(f"bg_color must have 1 or {C} channels")
         campos = campos.reshape(3).float().contiguous()
         camrot = camrot.reshape(3, 3).float().contiguous()
         bf16 = precision == "bf16"
@@ -215,7 +238,7 @@ class NeuralPointsRayMarching(nn.Module):
             for k in totals:
                 totals[k] += cnt[k]
             Sv = cnt["S_valid"]
-            feat = torch.empty((max(Sv, 1), C + 1), **f32)
+            feat = torch.empty((max(Sv, 1), 129), **f32)
             s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
@@ -242,6 +265,8 @@ class NeuralPointsRayMarching(nn.Module):
                                                   L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
                                                   L.stream_ptr(dev)),
                         "pnr_aggregate_fwd")
+            if C == 3:   # upstream colour head: [alpha, rgb] rows
+                feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
             e3 = mark()
             cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
             L.check(L.lib().pnr_composite_fwd(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),
@@ -286,13 +311,15 @@ class NeuralPointsRayMarching(nn.Module):
         [R,C] (requires grad w.r.t. points_embeding / color / dir / conf and the
         aggregator parameters), opacity [R,SR], is_bg [R], ray_mask [R]."""
         from .train import AggregateFn, AggSpec, CompositeFn, CompositeSpec, agg_params
+        self._sync_rw2c()
         opt = self.opt
         dev = raydir.device
         L.require_gpu(raydir)
         np_ = self.neural_points
         q = np_.querier
         R = raydir.shape[0]
-        SR, K, C = opt.SR, opt.K, 128
+        SR, K = opt.SR, opt.K
+        C = self.aggregator.C
         bg = bg_color.to(dev).float().reshape(-1).contiguous() if bg_color is not None else None
         if bg is not None and bg.numel() == 1:
             bg = bg.expand(C).contiguous()
@@ -319,6 +346,8 @@ class NeuralPointsRayMarching(nn.Module):
                        used=used)
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
                                  tab(np_.points_dir, 3), tab(np_.points_conf, 1), *agg_params(self.aggregator))
+        if C == 3:
+            feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
         cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
         cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(bg, campos, camrot, rd, hp))
         out = CompositeFn.apply(cspec, feat)
@@ -378,8 +407,14 @@ class NeuralPointsRayMarching(nn.Module):
         far_v = float(torch.max(far).item()) if torch.is_tensor(far) else float(far)
         if "bg_ray" in kargs:
             bg_color = None
-        color, opacity, is_bg, ray_mask = self.render_rays(campos, camrotc2w, raydir.reshape(-1, 3),
-                                                           near_v, far_v, bg_color)
+        # training loop (model(...) then loss.backward(), as run/train_ft.py does):
+        # differentiable path; evaluation / no_grad: the fused forward
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            color, opacity, is_bg, ray_mask = self.render_rays_train(campos, camrotc2w, raydir.reshape(-1, 3),
+                                                                     near_v, far_v, bg_color)
+        else:
+            color, opacity, is_bg, ray_mask = self.render_rays(campos, camrotc2w, raydir.reshape(-1, 3),
+                                                               near_v, far_v, bg_color)
         R = color.shape[0]
         mask_f = ray_mask.float().view(1, R, 1)
         out = dict(coarse_raycolor=color.view(1, R, -1), coarse_point_opacity=opacity.view(1, R, -1),

@@ -223,6 +223,34 @@ class AggregateFn(torch.autograd.Function):
         return tuple(out)
 
 
+class RgbHeadFn(torch.autograd.Function):
+    """[n, 4] = [feat[:, 0], raw2out_color(feat[:, 1:] W^T + b)] -- the upstream
+    colour head (point_aggregators.py:343, 269-273, 637-638) on pnr_rgb_head_fwd,
+    backward on pnr_rgb_head_bwd (d feat, d W, d b)."""
+
+    @staticmethod
+    def forward(ctx, feat, weight, bias, act_super, n_dev, n):
+        dev = feat.device
+        f = feat.detach().contiguous()
+        w, b = weight.detach().float().contiguous(), bias.detach().float().contiguous()
+        out = torch.zeros((max(f.shape[0], 1), 4), dtype=torch.float32, device=dev)[:f.shape[0]]
+        L.check(L.lib().pnr_rgb_head_fwd(L.ptr(f), f.stride(0), L.ptr(n_dev), int(n), L.ptr(w), L.ptr(b),
+                                         int(act_super), L.ptr(out), L.stream_ptr(dev)), "pnr_rgb_head_fwd")
+        ctx.f, ctx.w, ctx.b, ctx.act, ctx.n_dev, ctx.n = f, w, b, int(act_super), n_dev, int(n)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        dev = d_out.device
+        d_out = d_out.contiguous()
+        d_feat = torch.zeros_like(ctx.f)
+        d_wb = torch.zeros((3, 129), dtype=torch.float32, device=dev)
+        L.check(L.lib().pnr_rgb_head_bwd(L.ptr(d_out), L.ptr(ctx.f), ctx.f.stride(0), L.ptr(ctx.n_dev), ctx.n,
+                                         L.ptr(ctx.w), L.ptr(ctx.b), ctx.act, L.ptr(d_feat), L.ptr(d_wb),
+                                         L.stream_ptr(dev)), "pnr_rgb_head_bwd")
+        return d_feat, d_wb[:, :128].contiguous(), d_wb[:, 128].contiguous(), None, None, None
+
+
 class CompositeSpec:
     def __init__(self, rays, qp, bufs, cp, R, SR, C, keep=()):
         self.rays, self.qp, self.bufs, self.cp = rays, qp, bufs, cp

@@ -31,3 +31,7 @@ def formula_params(shapes=LEGO_SHAPES, salt=0.0):
         out[name + ".weight"] = w.astype(np.float32)
         out[name + ".bias"] = b.astype(np.float32)
     return out
+
+# upstream model (C_out = 3): the colour head the fork commented out,
+# color_branch.6 = Linear(128, 3) (point_aggregators.py:343)
+UPSTREAM_SHAPES = dict(LEGO_SHAPES, **{"color_branch.6": (3, 128)})

@@ -36,6 +36,8 @@ def test_library_exports_every_header_symbol(built):
     exported = set(re.findall(r" T (pnr_[a-z0-9_]+)", out))
     missing = set(header_functions()) - exported
     assert not missing, missing
+    extra = exported - set(header_functions())     # no debug / ablation entry points in the product
+    assert not extra, extra
 
 
 def test_ctypes_binding_covers_header_and_loads(built):

@@ -101,3 +101,41 @@ def test_frag_pack_h2_split_exactness():
         err = (rec[:, :61].double() - want.double()).abs()
         assert float((err - 2.0 ** -23 * want.double().abs()).max()) <= 2.0 ** -35
         assert float(rec[:, 61:].abs().max()) == 0.0
+
+
+def test_flagsets_match_scene_scripts():
+    """options.FLAGSETS = the values dev_scripts/{w_n360/ship, w_scannet_etf/scene101,
+    w_tt_ft/truck}.sh pass (the BASELINE c3 / c4 / c5 scenes)."""
+    from pointnerf_amd.options import flagset_opt
+    s = flagset_opt("ship")
+    assert (s.P, s.max_o, s.SR, s.kernel_size, s.vsize) == (10, 1500000, 80, [3, 3, 3], [0.004] * 3)
+    assert s.ranges == [-1.277, -1.300, -0.550, 1.371, 1.349, 0.729]
+    c = flagset_opt("scene101")
+    assert (c.SR, c.P, c.max_o, c.near_plane, c.far_plane, c.vsize) == (24, 30, 2000000, 0.1, 8.0, [0.008] * 3)
+    t = flagset_opt("truck")
+    assert (t.kernel_size, t.query_size, t.vsize, t.SR, t.P, t.near_plane, t.far_plane) == \
+        ([5, 5, 5], [3, 3, 3], [0.002] * 3, 40, 10, 0.0, 3.5)
+    assert flagset_opt("lego").P == 9
+
+
+def test_scene_points_cap_and_fixed_bbox():
+    """Synthetic flag-set clouds never overflow P (the reference's reservoir on
+    overflow has no reproducible result) and their grid is the one the cap used."""
+    from pointnerf_amd import synthetic as S
+    from pointnerf_amd.options import flagset_opt
+    for name, n in [("ship", 20000), ("scene101", 40000), ("truck", 30000)]:
+        o = flagset_opt(name)
+        p = S.scene_points(name, n, o, seed=2)
+        assert p.shape == (n, 3) and p.dtype == np.float32
+        g = O.grid_build(o, p)
+        assert g["occ_numpnts"].max() <= o.P - 1
+        assert np.all(p >= np.asarray(o.ranges[:3], np.float32)) and np.all(p <= np.asarray(o.ranges[3:], np.float32))
+
+
+def test_xyz_grad_is_refused():
+    import pytest
+    from pointnerf_amd import _lib as L
+    from pointnerf_amd.options import lego_opt
+    from pointnerf_amd.renderer import NeuralPoints
+    with pytest.raises(L.PnrError, match="xyz_grad"):
+        NeuralPoints(lego_opt(xyz_grad=1), "cpu")
