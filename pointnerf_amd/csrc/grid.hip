@@ -248,6 +248,69 @@ __global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const
   }
 }
 
+// ---------------------------------------------------------------- query index
+// Voxels that hold >= 1 kept point (coor_2_occ >= 0 and occ_numpnts > 0: the
+// slot-0 voxel under slot0_drop and the truncated ones are skipped exactly as
+// the reference's loop `g < min(P, occ_numpnts)` skips them), one byte per cell.
+__global__ void __launch_bounds__(kBlock) k_mark_held(int n_slots, GridDev g, const int32_t* __restrict__ occ_numpnts,
+                                                      const int32_t* __restrict__ occ_2_coor,
+                                                      uint8_t* __restrict__ bytes) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
+    if (occ_numpnts[s] <= 0 || occ_2_coor[s * 3] < 0) continue;
+    bytes[((int64_t)occ_2_coor[s * 3] * g.dims[1] + occ_2_coor[s * 3 + 1]) * g.dims[2] + occ_2_coor[s * 3 + 2]] = 1;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_pack_held(const uint8_t* __restrict__ bytes, int64_t words,
+                                                      uint2* __restrict__ qw, int32_t* __restrict__ wcnt) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    const uint4* b = reinterpret_cast<const uint4*>(bytes + 32 * w);
+    const uint4 lo = b[0], hi = b[1];
+    const unsigned v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bits |= ((v[q] >> (8 * k)) & 0xffu ? 1u : 0u) << (4 * q + k);
+    qw[w].x = bits;
+    wcnt[w] = __popc(bits);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_word_rank(int64_t words, const int32_t* __restrict__ wrank,
+                                                      uint2* __restrict__ qw) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words;
+       w += (int64_t)gridDim.x * blockDim.x)
+    qw[w].y = (uint32_t)wrank[w];
+}
+
+__global__ void __launch_bounds__(kBlock) k_rank_slots(int n_slots, GridDev g, const int32_t* __restrict__ occ_numpnts,
+                                                       const int32_t* __restrict__ occ_2_coor,
+                                                       const uint2* __restrict__ qw, int32_t* __restrict__ rank_slot,
+                                                       int32_t* __restrict__ rank_cnt) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
+    if (occ_numpnts[s] <= 0 || occ_2_coor[s * 3] < 0) continue;
+    const int64_t cell =
+        ((int64_t)occ_2_coor[s * 3] * g.dims[1] + occ_2_coor[s * 3 + 1]) * g.dims[2] + occ_2_coor[s * 3 + 2];
+    const uint2 wd = qw[cell >> 5];
+    const int r = (int)wd.y + __popc(wd.x & ((1u << (cell & 31)) - 1u));
+    rank_slot[r] = s;
+    rank_cnt[r] = min(g.P, occ_numpnts[s]);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_fill_recs(GridDev g, const int32_t* __restrict__ n_ranks,
+                                                      const int32_t* __restrict__ rank_slot,
+                                                      const int32_t* __restrict__ rec_off,
+                                                      const float4* __restrict__ occ_pts, float4* __restrict__ recs) {
+  const int nr = *n_ranks;
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += gridDim.x * blockDim.x) {
+    const int s = rank_slot[r], o = rec_off[r], c = rec_off[r + 1] - o;
+    for (int q = 0; q < c; ++q) recs[o + q] = occ_pts[(int64_t)s * g.P + q];
+  }
+}
+
 }  // namespace pnr
 
 using namespace pnr;
@@ -281,14 +344,17 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   int rc;
   const int64_t words = cdiv(gvol, 32);
   const int64_t cap_o = p->max_o;
-  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->first_pt.ensure(gvol * 4 > words * 32 ? gvol * 4 : words * 32)) ||
+  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->first_pt.ensure(gvol * 4 > words * 36 + 16 ? gvol * 4 : words * 36 + 16)) ||
       (rc = h->occ_bits.ensure(words * 4)) || (rc = h->occ_numpnts.ensure(cap_o * 4)) ||
       (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
       (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->slot_cursor.ensure(cap_o * 4)) ||
       (rc = h->slot_off.ensure((cap_o + 1) * 4)) || (rc = h->pt_cell.ensure(n * 4)) ||
       (rc = h->pt_flag.ensure(n * 4)) || (rc = h->pt_slot.ensure((n + 1) * 4)) ||
       (rc = h->bucket.ensure(n * 4)) || (rc = h->counters.ensure(8 * 4)) ||
-      (rc = h->scan_tmp.ensure(scan_scratch_bytes(n > cap_o ? n : cap_o))))
+      (rc = h->scan_tmp.ensure(scan_scratch_bytes(n > cap_o ? (n > words ? n : words) : (cap_o > words ? cap_o : words)))) ||
+      (rc = h->q_words.ensure(words * 8)) || (rc = h->q_wcnt.ensure((words + 1) * 4)) ||
+      (rc = h->q_rank_slot.ensure(cap_o * 4)) || (rc = h->q_rank_cnt.ensure(cap_o * 4)) ||
+      (rc = h->q_rec_off.ensure((cap_o + 1) * 4)) || (rc = h->q_recs.ensure(n * sizeof(float4))))
     return rc;
   int32_t* coor_2_occ = h->coor_2_occ.as<int32_t>();
   int32_t* first_pt = h->first_pt.as<int32_t>();
@@ -352,6 +418,32 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   hipLaunchKernelGGL(k_select, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
                      xyz_dev, occ_numpnts, slot_off, bucket, occ_pts, counters);
   PNR_LAUNCH_CHECK();
+
+  // query index: held voxels ranked in cell order (k_knn's tables)
+  {
+    uint2* qw = h->q_words.as<uint2>();
+    int32_t* wcnt = h->q_wcnt.as<int32_t>();
+    int32_t* wrank = h->first_pt.as<int32_t>() + words * 8;   // after the cell bytes (32 B per word)
+    PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
+    hipLaunchKernelGGL(k_mark_held, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
+                       occ_numpnts, occ_2_coor, occ_bytes);
+    PNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pack_held, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, qw, wcnt);
+    PNR_LAUNCH_CHECK();
+    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+      return rc;
+    hipLaunchKernelGGL(k_word_rank, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, words, wrank, qw);
+    PNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_rank_slots, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
+                       occ_numpnts, occ_2_coor, qw, h->q_rank_slot.as<int32_t>(), h->q_rank_cnt.as<int32_t>());
+    PNR_LAUNCH_CHECK();
+    if ((rc = exclusive_scan(h->q_rank_cnt.as<int32_t>(), cap_o, counters + 4, h->q_rec_off.as<int32_t>(),
+                             counters + 5, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+      return rc;
+    hipLaunchKernelGGL(k_fill_recs, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, g, counters + 4,
+                       h->q_rank_slot.as<int32_t>(), h->q_rec_off.as<int32_t>(), occ_pts, h->q_recs.as<float4>());
+    PNR_LAUNCH_CHECK();
+  }
 
   int32_t cnt[8];
   PNR_HIP(hipMemcpyAsync(cnt, counters, sizeof(cnt), hipMemcpyDeviceToHost, st));

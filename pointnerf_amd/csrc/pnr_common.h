@@ -144,13 +144,24 @@ struct pnr_handle {
   DevBuf bucket;          // int32 [N]
   DevBuf counters;        // int32 [8]
   DevBuf scan_tmp;
+  // Query index (what k_knn reads; the slot tables above stay the reference's
+  // view for export / parity): the voxels that hold points, ranked in x-major
+  // cell order, so a sample's 3x3x3 neighbourhood is found from a bitmap that
+  // stays in L2 and its records sit near each other in HBM.
+  DevBuf q_words;         // uint2 [gvol/32] {bits: cell holds >= 1 kept point, rank of the word's first cell}
+  DevBuf q_wcnt;          // int32 [gvol/32] scratch: popcount per word
+  DevBuf q_rank_slot;     // int32 [max_o]   slot of rank r (scratch)
+  DevBuf q_rank_cnt;      // int32 [max_o]   min(P, points) of rank r (scratch)
+  DevBuf q_rec_off;       // int32 [max_o+1] first record of rank r (exclusive scan of q_rank_cnt)
+  DevBuf q_recs;          // float4 [N]      {x, y, z, bitcast(id)} in rank order, per voxel ascending id
   int64_t n_points = 0;
   pnr_grid_stats stats{};
   bool built = false;
   void release_all() {
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &first_pt, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &slot_cursor, &slot_off, &pt_cell, &pt_flag, &pt_slot, &bucket,
-                     &counters, &scan_tmp};
+                     &counters, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
+                     &q_rec_off, &q_recs};
     for (DevBuf* b : all) b->release();
   }
 };

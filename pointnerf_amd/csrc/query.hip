@@ -17,6 +17,17 @@
 namespace pnr {
 
 constexpr int kQBlock = 256;
+#ifndef PNR_KNN_WAVES
+#define PNR_KNN_WAVES 8   // k_knn is load-latency bound: registers capped for 8 waves per SIMD (A/B: 0 -> 2.73 ms, 8 -> 2.33 ms query)
+#endif
+#ifndef PNR_KNN_BATCH
+#define PNR_KNN_BATCH 2   // candidate records fetched together (A/B: 1 -> 2.38, 2 -> 2.33, 4 -> 2.92 ms query)
+#endif
+#if PNR_KNN_WAVES
+#define PNR_KNN_ATTR __attribute__((amdgpu_waves_per_eu(PNR_KNN_WAVES)))
+#else
+#define PNR_KNN_ATTR
+#endif
 
 struct QGrid {
   float shift[3], vs[3];
@@ -141,26 +152,39 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
 template <int KMAX>
 __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
                                          float buf[KMAX], int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
-  for (int g0 = 0; g0 < cnt; g0 += 4) {
-    float4 vb[4];
+  for (int g0 = 0; g0 < cnt; g0 += PNR_KNN_BATCH) {
+    float4 vb[PNR_KNN_BATCH];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < PNR_KNN_BATCH; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PNR_KNN_BATCH; ++u) {
       if (g0 + u >= cnt) break;
       knn_visit<KMAX>(vb[u], p, K, r2, buf, out, kid, far_ind, far2);
     }
   }
 }
 
+// The query index of one cell (grid.hip "query index"): held = the voxel keeps
+// >= 1 point; then its records are recs[off .. off + cnt).  Cells outside the
+// grid are not held (the reference's loop bounds skip them).
+struct QIndex {
+  const uint2* words;      // {held bits, rank of the word's first cell}
+  const int32_t* rec_off;  // [ranks + 1]
+  const float4* recs;
+};
+
+__device__ __forceinline__ int held_rank(const uint2 wd, int bit) {
+  return ((wd.x >> bit) & 1u) ? (int)wd.y + __popc(wd.x & ((1u << bit) - 1u)) : -1;
+}
+
 // query_neigh_along_ray_layered (qpiw.py:442-528) for one sample.  KMAX is the
-// compile-time buffer size, K <= KMAX the runtime neighbour count.
+// compile-time buffer size, K <= KMAX the runtime neighbour count.  Cells are
+// visited in the reference's order (Chebyshev layer, then x -> y -> z); a cell
+// whose voxel holds no point contributes nothing there either, so only held
+// cells are looked up (bitmap + rank: no per-cell table of the whole grid).
 template <int KMAX>
 __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, int layers, float r2,
-                                       const int32_t* __restrict__ coor_2_occ,
-                                       const int32_t* __restrict__ occ_numpnts,
-                                       const float4* __restrict__ occ_pts, int32_t out[KMAX],
-                                       int& n_cand) {
+                                       const QIndex& qi, int32_t out[KMAX], int& n_cand) {
   const int fx = vox_coord(p[0], g.shift[0], g.vs[0]);
   const int fy = vox_coord(p[1], g.shift[1], g.vs[1]);
   const int fz = vox_coord(p[2], g.shift[2], g.vs[2]);
@@ -173,28 +197,56 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
   int kid = 0, far_ind = 0;
   float far2 = 0.f;
   if (layers == 2) {
-    // query 3x3x3 (every shipped config): the 27 cells in the reference's
-    // traversal order (layer 0 = the centre, then layer 1 = x -> y -> z minus the
-    // centre).  The slot and count lookups of all 27 cells are issued together
-    // instead of as 27 dependent chains; the visit order is unchanged.
-    int slot[27], cnt[27];
-#pragma unroll
-    for (int j = 0; j < 27; ++j) {
-      const int x = j == 0 ? 0 : ((j <= 13 ? j - 1 : j) / 9) - 1;
-      const int y = j == 0 ? 0 : (((j <= 13 ? j - 1 : j) / 3) % 3) - 1;
-      const int z = j == 0 ? 0 : ((j <= 13 ? j - 1 : j) % 3) - 1;
-      const int cx = fx + x, cy = fy + y, cz = fz + z;
-      const bool in = (unsigned)cx < (unsigned)g.dims[0] && (unsigned)cy < (unsigned)g.dims[1] &&
-                      (unsigned)cz < (unsigned)g.dims[2];
-      slot[j] = in ? coor_2_occ[((int64_t)cx * g.dims[1] + cy) * g.dims[2] + cz] : -1;
+    // query 3x3x3 (every shipped config but truck).  The 9 (x, y) columns of
+    // the neighbourhood are runs of 3 consecutive cells (z fastest), and held
+    // voxels are ranked in cell order with their records stored in rank order
+    // (grid.hip "query index"), so the records of a column's run are ONE
+    // contiguous range, already in the reference's visit order (z ascending):
+    //   pos(c) = held cells before cell c = word rank + popcount below c's bit,
+    //   column records = [rec_off[pos(z_lo)], rec_off[pos(z_hi) + held(z_hi)]).
+    // Traversal (qpiw.py:481-527): layer 0 = the centre cell, then layer 1 =
+    // columns x -> y, each run z -> (the centre skipped in its column).
+    if ((unsigned)fz >= (unsigned)g.dims[2]) return 0;   // never: filled samples lie in held-dilated cells
+    const int zlo = fz > 0 ? fz - 1 : fz, zhi = fz + 1 < g.dims[2] ? fz + 1 : fz;
+    auto pos = [&](int64_t c, int& held) -> int {
+      const uint2 wd = qi.words[c >> 5];
+      const int b = (int)(c & 31);
+      held = (wd.x >> b) & 1u;
+      return (int)wd.y + __popc(wd.x & ((1u << b) - 1u));
+    };
+    auto range = [&](int o, int e) {
+      n_cand += e - o;
+      knn_cell<KMAX>(qi.recs + o, e - o, p, K, r2, buf, out, kid, far_ind, far2);
+    };
+    // layer 0: the centre cell
+    const int64_t cc = ((int64_t)fx * g.dims[1] + fy) * g.dims[2] + fz;
+    int hc;
+    const int pc = pos(cc, hc);
+    int oc = 0, ec = 0;
+    if (hc) {
+      oc = qi.rec_off[pc];
+      ec = qi.rec_off[pc + 1];
+      range(oc, ec);
     }
-#pragma unroll
-    for (int j = 0; j < 27; ++j) cnt[j] = slot[j] >= 0 ? min(g.P, occ_numpnts[slot[j]]) : 0;
-#pragma unroll
-    for (int j = 0; j < 27; ++j) {
-      if (j == 1 && kid >= K) break;   // layer 0 already saw >= K candidates (qpiw.py:526)
-      n_cand += cnt[j];
-      knn_cell<KMAX>(occ_pts + (int64_t)max(slot[j], 0) * g.P, cnt[j], p, K, r2, buf, out, kid, far_ind, far2);
+    if (kid < K) {   // layer 0 already saw >= K candidates: done (qpiw.py:526)
+#pragma unroll 1
+      for (int col = 0; col < 9; ++col) {
+        const int cx = fx + col / 3 - 1, cy = fy + col % 3 - 1;
+        if ((unsigned)cx >= (unsigned)g.dims[0] || (unsigned)cy >= (unsigned)g.dims[1]) continue;
+        const int64_t base = ((int64_t)cx * g.dims[1] + cy) * g.dims[2];
+        int hlo, hhi;
+        const int plo = pos(base + zlo, hlo);
+        const int phi = pos(base + zhi, hhi);
+        const int pend = phi + hhi;
+        if (pend == plo) continue;   // no held cell in the run
+        const int o = qi.rec_off[plo], e = qi.rec_off[pend];
+        if (col != 4) {
+          range(o, e);
+        } else {   // centre column: the run minus the centre cell
+          range(o, hc ? oc : qi.rec_off[pc]);
+          range(hc ? ec : qi.rec_off[pc], e);
+        }
+      }
     }
     return kid < K ? kid : K;
   }
@@ -207,11 +259,12 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
         for (int z = z0; z < z1; ++z) {
           if (max(abs(z), max(abs(x), abs(y))) != layer) continue;
           const int64_t cell = ((int64_t)(fx + x) * g.dims[1] + (fy + y)) * g.dims[2] + (fz + z);
-          const int slot = coor_2_occ[cell];
-          if (slot < 0) continue;
-          const int cnt = min(g.P, occ_numpnts[slot]);
-          n_cand += cnt;
-          knn_cell<KMAX>(occ_pts + (int64_t)slot * g.P, cnt, p, K, r2, buf, out, kid, far_ind, far2);
+          const int r = held_rank(qi.words[cell >> 5], (int)(cell & 31));
+          if (r < 0) continue;
+          const int o = qi.rec_off[r];
+          const int cn = qi.rec_off[r + 1] - o;
+          n_cand += cn;
+          knn_cell<KMAX>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
         }
       }
     }
@@ -221,24 +274,56 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 }
 
 template <int KMAX>
-__global__ void __launch_bounds__(kQBlock) k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
-                                                 const int32_t* __restrict__ coor_2_occ,
-                                                 const int32_t* __restrict__ occ_numpnts,
-                                                 const float4* __restrict__ occ_pts,
-                                                 const uint16_t* __restrict__ slot_d,
+__global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
+                                                 QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
                                                  int32_t* __restrict__ ray_vcnt,
                                                  float* __restrict__ sample_w,
-                                                 float* __restrict__ sample_p, int32_t* counts) {
+                                                 float* __restrict__ sample_p, int32_t* counts, int vec_pidx) {
   const int64_t S = counts[0];
   const float c[3] = {q.campos[0], q.campos[1], q.campos[2]};
   float Rm[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Rm[i] = q.camrot[i];
   int pairs = 0, n_cand = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < S;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  // A block takes 256 consecutive filled samples (~a dozen neighbouring rays of
+  // one pixel row) and hands them to its lanes ordered by shading slot: lanes
+  // of a wave then hold the same slot of adjacent rays, whose neighbourhoods
+  // overlap, so their record loads share cache lines (the sample -> outputs
+  // mapping is unchanged; only which lane computes which sample).
+  __shared__ int hist[kQBlock], perm[kQBlock];
+  const bool by_slot = SR <= kQBlock;   // (A/B: lanes in fill order 3.45 ms query, by slot 2.94)
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int64_t base = blockIdx.x * (int64_t)kQBlock; base < S; base += (int64_t)gridDim.x * kQBlock) {
+    int64_t i = base + tid;
+    if (by_slot) {
+      const int n_in = (int)min((int64_t)kQBlock, S - base);
+      hist[tid] = 0;
+      __syncthreads();
+      const int s0 = tid < n_in ? fill_rs[base + tid] % SR : 0;
+      const int at = tid < n_in ? atomicAdd(&hist[s0], 1) : 0;
+      __syncthreads();
+      if (tid < 64) {   // exclusive scan of hist[0 .. 256) by wave 0, 4 entries per lane
+        const int a0 = hist[4 * lane], a1 = hist[4 * lane + 1], a2 = hist[4 * lane + 2], a3 = hist[4 * lane + 3];
+        int t = a0 + a1 + a2 + a3, incl = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_up(incl, o);
+          if (lane >= o) incl += v;
+        }
+        const int ex = incl - t;
+        hist[4 * lane] = ex;
+        hist[4 * lane + 1] = ex + a0;
+        hist[4 * lane + 2] = ex + a0 + a1;
+        hist[4 * lane + 3] = ex + a0 + a1 + a2;
+      }
+      __syncthreads();
+      if (tid < n_in) perm[hist[s0] + at] = tid;
+      __syncthreads();
+      i = tid < n_in ? base + perm[tid] : S;
+    }
+    if (i >= S) continue;
     const int rs = fill_rs[i];
     const int64_t r = rs / SR;
     const int d = slot_d[rs];
@@ -252,11 +337,17 @@ __global__ void __launch_bounds__(kQBlock) k_knn(QRays q, QGrid g, int SR, int K
       sample_p[i * 3 + a] = pp[a];
     }
     int32_t out[KMAX];
-    const int nk = knn_one<KMAX>(p, g, K, layers, r2, coor_2_occ, occ_numpnts, occ_pts, out, n_cand);
-    for (int k = 0; k < K; ++k) {
+    const int nk = knn_one<KMAX>(p, g, K, layers, r2, qi, out, n_cand);
+    if (KMAX == 8 && K == 8 && vec_pidx) {   // two 16-B stores (pidx 16-B aligned)
+      int4* o4 = reinterpret_cast<int4*>(pidx + i * 8);
+      o4[0] = make_int4(out[0], out[1], out[2], out[3]);
+      o4[1] = make_int4(out[4 % KMAX], out[5 % KMAX], out[6 % KMAX], out[7 % KMAX]);
+    } else {
+      for (int k = 0; k < K; ++k) {
 #pragma unroll
-      for (int j = 0; j < KMAX; ++j)
-        if (j == k) pidx[i * K + k] = out[j];
+        for (int j = 0; j < KMAX; ++j)
+          if (j == k) pidx[i * K + k] = out[j];
+      }
     }
     vflag[i] = nk > 0;
     if (nk > 0) atomicAdd(ray_vcnt + r, 1);
@@ -403,11 +494,15 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   PNR_LAUNCH_CHECK();
   const int layers = (qp->kernel_size[0] + 1) / 2;
   const unsigned gk = grid_for(RS, kQBlock, 256 * 16);
+  const int vec = ((uintptr_t)b->pidx & 15) == 0;
+  QIndex qi;
+  qi.words = h->q_words.as<uint2>();
+  qi.rec_off = h->q_rec_off.as<int32_t>();
+  qi.recs = h->q_recs.as<float4>();
 #define PNR_KNN(KM)                                                                              \
   hipLaunchKernelGGL(k_knn<KM>, dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
-                     qp->radius_limit2, h->coor_2_occ.as<int32_t>(), h->occ_numpnts.as<int32_t>(), \
-                     h->occ_pts.as<float4>(), b->slot_d, b->fill_rs, b->pidx, b->vflag,           \
-                     b->ray_vcnt, b->sample_w, b->sample_p, b->counts)
+                     qp->radius_limit2, qi, b->slot_d, b->fill_rs, b->pidx, b->vflag,             \
+                     b->ray_vcnt, b->sample_w, b->sample_p, b->counts, vec)
   if (qp->K <= 8) PNR_KNN(8);
   else if (qp->K <= 16) PNR_KNN(16);
   else PNR_KNN(32);
