@@ -6,7 +6,7 @@ SRCS := $(wildcard $(SRC_DIR)/*.hip)
 OBJS := $(patsubst $(SRC_DIR)/%.hip,build/%.o,$(SRCS))
 LIB := pointnerf_amd/libpnr.so
 HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -Wall -Wno-unused-result \
-            -munsafe-fp-atomics -Iinclude
+            -munsafe-fp-atomics -fvisibility=hidden -Iinclude
 
 all: $(LIB) oracle
 

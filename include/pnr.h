@@ -52,6 +52,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
+#pragma GCC visibility push(default)
 
 #define PNR_ABI_VERSION 5
 
@@ -494,6 +496,7 @@ int pnr_exclusive_scan_i32(const int32_t* in, int64_t n, const int32_t* n_dev, i
                            int32_t* total_dev, void* scratch, size_t scratch_bytes,
                            void* stream);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif

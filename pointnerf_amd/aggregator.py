@@ -158,15 +158,22 @@ def split2_f16(W: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
 
 
 def h2_shift(W: torch.Tensor, bias: torch.Tensor | None = None) -> int:
-    """Smallest s >= 0 with max|2^-s [W | bias]| < H2_WMAX (frag_pack_h2)."""
+    """The s with H2_WMAX / 2 <= max|2^-s [W | bias]| < H2_WMAX (frag_pack_h2), s may be
+    negative: a layer of small weights is scaled UP so its high halves stay in the f16
+    normal range (2^-14) and the split keeps its 22 significant bits; s = 0 for an
+    all-zero layer."""
     amax = float(W.abs().max()) if W.numel() else 0.0
     if bias is not None and bias.numel():
         amax = max(amax, float(bias.abs().max()))
     if not np.isfinite(amax):
         raise L.PnrError("frag_pack_h2: non-finite weight")
+    if amax == 0.0:
+        return 0
     s = 0
     while amax * 2.0 ** -s >= H2_WMAX:
         s += 1
+    while s > -100 and amax * 2.0 ** -(s - 1) < H2_WMAX:
+        s -= 1
     return s
 
 
@@ -175,8 +182,8 @@ def frag_pack_h2(W: torch.Tensor, bias: torch.Tensor | None = None,
     """Split-f16 A-operand packs for pnr_aggregate_fwd_h2 -> (pack, layer scale):
     F[t][T][plane][lane][j] = plane of (2^-s W')[32T + (lane & 31)][16t + 8(lane >> 5) + j],
     W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus H2_PAD zero ones, planes
-    (Wh, Wl) of split2_f16; s >= 0 the smallest power of two with
-    max|2^-s W'| < H2_WMAX; scale = 2^(s - 11) (the kernel's accumulator factor)."""
+    (Wh, Wl) of split2_f16; s (h2_shift, may be negative) puts max|2^-s W'| in
+    [H2_WMAX/2, H2_WMAX); scale = 2^(s - 11) (the kernel's accumulator factor)."""
     out_f, kin = W.shape
     assert out_f % 32 == 0
     cols = kin + (1 if bias is not None else 0)

@@ -1335,14 +1335,14 @@ int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pa
 }
 
 #if PNR_TRACE
-extern "C" int pnr_debug_x3_trace(unsigned long long* out, int n) {
+extern "C" __attribute__((visibility("default"))) int pnr_debug_x3_trace(unsigned long long* out, int n) {
   const size_t want = sizeof(g_x3_trace);
   if (!out || (size_t)n * sizeof(unsigned long long) < want) return PNR_EINVAL;
   PNR_HIP(hipDeviceSynchronize());
   PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_trace), want));
   return PNR_OK;
 }
-extern "C" int pnr_debug_x3_blocks(unsigned long long* out, int n) {
+extern "C" __attribute__((visibility("default"))) int pnr_debug_x3_blocks(unsigned long long* out, int n) {
   if (!out || (size_t)n * sizeof(unsigned long long) < sizeof(g_x3_blk)) return PNR_EINVAL;
   PNR_HIP(hipDeviceSynchronize());
   PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_blk), sizeof(g_x3_blk)));

@@ -82,17 +82,21 @@ def test_product_fails_loudly_without_gpu():
 
 def test_frag_pack_h2_split_exactness():
     """frag_pack_h2: Wh + 2^-11 Wl reproduces the pre-scaled weights within
-    2^-24 relative (f16 normal range), scale = 2^(s-11) with |W 2^-s| < 16,
-    and the zero padding steps are zero."""
+    2^-24 relative (f16 normal range), scale = 2^(s-11) with 8 <= max|W' 2^-s| < 16
+    (small layers scaled up, s < 0), and the zero padding steps are zero."""
     import torch
-    from pointnerf_amd.aggregator import H2_PAD, frag_pack_h2
+    from pointnerf_amd.aggregator import H2_PAD, frag_pack_h2, h2_shift
     g = torch.Generator().manual_seed(0)
-    for mag in (0.1, 40.0):
+    assert h2_shift(torch.zeros(4, 4)) == 0
+    for mag in (1e-4, 0.1, 40.0):
         W = torch.randn(256, 60, generator=g) * mag
         b = torch.randn(256, generator=g) * mag
         F, scale = frag_pack_h2(W, b)
         s = round(np.log2(scale)) + 11
-        assert s >= 0 and (W.abs().max() * 2.0 ** -s) < 16 and (s == 0 or W.abs().max() * 2.0 ** -(s - 1) >= 16)
+        amax = float(torch.cat([W, b[:, None]], 1).abs().max())
+        assert 8 <= amax * 2.0 ** -s < 16
+        if mag < 1:
+            assert s < 0
         tot = (61 + 15) // 16 + H2_PAD
         P = F.view(tot, 8, 2, 2, 32, 8).float()            # [t][T][pl][h][r][j]
         rec = P[:, :, 0] + P[:, :, 1] / 2048.0               # [t][T][h][r][j]
