@@ -52,6 +52,9 @@ def parse():
                     help="N > 1 ray batches: frames = each rank renders whole frames (frame f on rank f mod N, "
                          "one all-gather of the step's N frames); tiles = every frame split in interleaved 16x16 "
                          "pixel tiles over the ranks (N partial frames per rank per step)")
+    ap.add_argument("--tile-layout", choices=("bands", "tiles16"), default="bands",
+                    help="--shard tiles: bands = N row bands per frame, band b of frame f on rank (b+f) mod N "
+                         "(every rank renders every band once per step); tiles16 = interleaved 16x16 tiles")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="diagnostic (single process): do rank 0's share of an N-rank step (N partial frames of "
                          "1/N of the rays, no collective) to project per-rank overheads of the N-GPU run")
@@ -347,7 +350,7 @@ def main():
             return ci, dev_cams[ci][2], None
         key = (frame % shard_world, ci)
         if key not in shards:
-            sh = TileShard(H, W, rank, shard_world, frame % shard_world, device)
+            sh = TileShard(H, W, rank, shard_world, frame % shard_world, device, layout=args.tile_layout)
             shards[key] = (sh, sh.select(dev_cams[ci][2]))
         sh, rd = shards[key]
         return ci, rd, sh
@@ -355,29 +358,36 @@ def main():
     stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0, "cand": 0, "rays": 0}
 
     def step(s, timed):
-        frames = []
+        # every render call of the step is issued without a host sync
+        # (render_rays(sync=False)); model.finish() is the step's one sync: it
+        # checks the deferred feature-buffer sizes / f16 range and returns the counts
+        parts = []
+        ev_step = [] if timed else None
         for f in range(shard_world):
             frame = s * shard_world + f
             if fshard is not None:
                 frame = fshard.frame_of(s)   # whole frame s*N + rank
             ci, rd, sh = my_rays(frame)
             campos, camrot, _ = dev_cams[ci]
-            ev = [] if timed else None
             color, opac, is_bg, mask = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
-                                                         force_grid=(f == 0 and not args.no_grid_rebuild), events=ev,
-                                                         reuse_p1=f > 0)
-            if timed:
-                c = model.last_counts
+                                                         force_grid=(f == 0 and not args.no_grid_rebuild),
+                                                         events=ev_step, reuse_p1=f > 0, sync=False)
+            parts.append((sh, color, rd.shape[0]))
+        counts = model.finish()
+        if timed:
+            for c, (_, _, nr) in zip(counts, parts):
                 stage["pairs"] += c["n_pairs"]
                 stage["valid"] += c["S_valid"]
                 stage["filled"] += c["S_filled"]
                 stage["cand"] += c["n_cand"]
-                stage["rays"] += rd.shape[0]
+                stage["rays"] += nr
                 stage["flops"] += c["n_pairs"] * FLOP_PER_PAIR + c["S_valid"] * FLOP_PER_SAMPLE
-                stage["_ev"] = stage.get("_ev", []) + ev
+            stage["_ev"] = stage.get("_ev", []) + ev_step
+        frames = []
+        for sh, color, _ in parts:
             if world > 1 and not args.no_gather:
                 # RCCL all-gather of the rendered rays (async: they travel over xGMI while
-                # the next frame renders): tiles -> every rank holds the frame; frames ->
+                # the next step renders): tiles -> every rank holds the frame; frames ->
                 # every rank holds the step's N frames
                 frames.append((fshard or sh).assemble_async(color))
             else:
@@ -395,6 +405,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    rerenders0 = model.overflow_rerenders
     t0 = time.perf_counter()
     prev = []
     for s in range(args.steps):
@@ -487,6 +498,9 @@ def main():
             # frames re-rendered on fp32x3 because an activation left the f16 range
             # (renderer.render_rays; 0 for these weights)
             out["h2_fallbacks"] = int(model.h2_fallbacks)
+        # sync-free render calls re-rendered because their valid samples outgrew the
+        # feature buffer sized from earlier frames (renderer.finish; 0 after warm-up)
+        out["overflow_rerenders"] = int(model.overflow_rerenders - rerenders0)
         if shard_world != world:
             out["config"]["emulated_world"] = shard_world   # diagnostic: rank 0's share of an N-rank step
         out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per, launches)

@@ -55,7 +55,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 5
+#define PNR_ABI_VERSION 6
 
 enum {
   PNR_OK = 0,
@@ -94,9 +94,10 @@ typedef struct {
  * Deterministic: voxel slots are assigned in ascending order of the first
  * point index that lands in each voxel (the serial order of claim_occ), points
  * inside a voxel are kept in ascending index order (first P of them).  Tables
- * are reallocated only when dims/max_o/P grow.  One host sync (to read the
- * occupied-voxel count for overflow detection).  Returns PNR_OK even on
- * max_o / P overflow; inspect pnr_grid_stats. */
+ * are reallocated only when dims/max_o/P grow.  No host sync: the build
+ * counters travel to pinned host memory behind an event that only
+ * pnr_grid_stats_get waits on.  Returns PNR_OK even on max_o / P overflow;
+ * inspect pnr_grid_stats. */
 int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
                    const pnr_grid_params* p, void* stream);
 
@@ -108,7 +109,7 @@ typedef struct {
   int32_t max_points_per_voxel;
   int32_t dims[3];
 } pnr_grid_stats;
-int pnr_grid_stats_get(pnr_handle* h, pnr_grid_stats* out); /* syncs */
+int pnr_grid_stats_get(pnr_handle* h, pnr_grid_stats* out); /* waits for the last build */
 
 /* Copy the grid tables out (inspection / parity tests; any pointer may be NULL):
  * coor_2_occ[gvol] (-1 empty), occ_bits[ceil(gvol/32)] dilated occupancy
@@ -423,6 +424,11 @@ typedef struct {
   int32_t raydist_mode_unit;
   int32_t C;            /* 128 */
   const float* bg_color;/* [C] device                                           */
+  int64_t feat_rows;    /* rows of feat (0 = unbounded).  A valid sample whose row is
+                           >= feat_rows (more valid samples than the caller sized feat
+                           for, counts[1] > feat_rows) is composited as empty and never
+                           read: the output is then wrong but the call is memory-safe,
+                           and the caller re-renders with a larger feat (renderer.py). */
 } pnr_composite_params;
 
 int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q,

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class PnrError(RuntimeError):
@@ -89,7 +89,7 @@ class Samples(ctypes.Structure):
 
 class CompositeParams(ctypes.Structure):
     _fields_ = [("vsize_z", c_float), ("raydist_mode_unit", c_int32), ("C", c_int32),
-                ("bg_color", c_void_p)]
+                ("bg_color", c_void_p), ("feat_rows", c_int64)]
 
 
 class AggSaved(ctypes.Structure):

@@ -83,6 +83,7 @@ struct CompArgs {
   const int32_t* valid_off;
   const float* sample_p;
   const float* feat;
+  int64_t feat_rows;   // rows of feat: valid samples at or past it are not read (capacity overflow)
   float vsize_z;
   int unit;
   int C;
@@ -133,7 +134,8 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
       z[q] = filled ? a.sample_p[i * 3 + 2] : (s < SR ? zo : -INFINITY);
       const bool val = filled && a.vflag[i];
       vrow[q] = val ? a.valid_off[i] : -1;
-      sig[q] = val ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
+      if (vrow[q] >= a.feat_rows) vrow[q] = -1;   // capacity overflow: the caller re-renders
+      sig[q] = vrow[q] >= 0 ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
     }
     // cummax over slots (neural_points_volumetric_model.py:293)
     float cm0 = wave_max_scan_incl(z[0]);
@@ -359,7 +361,8 @@ __global__ void __launch_bounds__(kCBlock) k_composite_bwd(CompBwdArgs A) {
       z[q] = filled ? a.sample_p[i * 3 + 2] : (s < SR ? zo : -INFINITY);
       const bool val = filled && a.vflag[i];
       vrow[q] = val ? a.valid_off[i] : -1;
-      sig[q] = val ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
+      if (vrow[q] >= a.feat_rows) vrow[q] = -1;   // capacity overflow: the caller re-renders
+      sig[q] = vrow[q] >= 0 ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
     }
     float cm0 = wave_max_scan_incl(z[0]);
     float cm1 = fmaxf(wave_max_scan_incl(z[1]), __shfl(cm0, 63));
@@ -486,6 +489,7 @@ extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q
   a.valid_off = b->valid_off;
   a.sample_p = b->sample_p;
   a.feat = feat;
+  a.feat_rows = c->feat_rows > 0 ? c->feat_rows : INT64_MAX;
   a.vsize_z = c->vsize_z;
   a.unit = c->raydist_mode_unit;
   a.C = c->C;
@@ -536,6 +540,7 @@ extern "C" int pnr_composite_bwd(const pnr_rays* rays, const pnr_query_params* q
   a.f.valid_off = b->valid_off;
   a.f.sample_p = b->sample_p;
   a.f.feat = feat;
+  a.f.feat_rows = c->feat_rows > 0 ? c->feat_rows : INT64_MAX;
   a.f.vsize_z = c->vsize_z;
   a.f.unit = c->raydist_mode_unit;
   a.f.C = c->C;

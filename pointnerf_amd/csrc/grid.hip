@@ -445,17 +445,15 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
     PNR_LAUNCH_CHECK();
   }
 
-  int32_t cnt[8];
-  PNR_HIP(hipMemcpyAsync(cnt, counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
-  PNR_HIP(hipStreamSynchronize(st));
+  if (!h->host_cnt) PNR_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->host_cnt), 8 * sizeof(int32_t)));
+  if (!h->stats_ev) PNR_HIP(hipEventCreateWithFlags(&h->stats_ev, hipEventDisableTiming));
+  if (h->stats_pending) PNR_HIP(hipEventSynchronize(h->stats_ev));   // the previous build's copy is done
+  PNR_HIP(hipMemcpyAsync(h->host_cnt, counters, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  PNR_HIP(hipEventRecord(h->stats_ev, st));
+  h->stats_pending = true;
   h->gp = *p;
   h->gvol = gvol;
   h->n_points = n;
-  h->stats.n_voxels = cnt[0];
-  h->stats.n_voxels_kept = cnt[0] < p->max_o ? cnt[0] : p->max_o;
-  h->stats.n_points_in_grid = cnt[1];
-  h->stats.n_points_dropped = cnt[2];
-  h->stats.max_points_per_voxel = cnt[3];
   for (int a = 0; a < 3; ++a) h->stats.dims[a] = p->dims[a];
   h->built = true;
   return PNR_OK;
@@ -494,6 +492,16 @@ extern "C" int pnr_grid_export(pnr_handle* h, int32_t* coor_2_occ, uint32_t* occ
 extern "C" int pnr_grid_stats_get(pnr_handle* h, pnr_grid_stats* out) {
   PNR_CHECK_ARG(h && out, "grid_stats: null pointer");
   PNR_CHECK_ARG(h->built, "grid_stats: grid not built");
+  if (h->stats_pending) {
+    PNR_HIP(hipEventSynchronize(h->stats_ev));
+    const int32_t* cnt = h->host_cnt;
+    h->stats.n_voxels = cnt[0];
+    h->stats.n_voxels_kept = cnt[0] < h->gp.max_o ? cnt[0] : h->gp.max_o;
+    h->stats.n_points_in_grid = cnt[1];
+    h->stats.n_points_dropped = cnt[2];
+    h->stats.max_points_per_voxel = cnt[3];
+    h->stats_pending = false;
+  }
   *out = h->stats;
   return PNR_OK;
 }

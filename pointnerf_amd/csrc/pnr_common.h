@@ -157,7 +157,17 @@ struct pnr_handle {
   int64_t n_points = 0;
   pnr_grid_stats stats{};
   bool built = false;
+  // build counters read back without blocking the build: pinned copy + event,
+  // waited on by pnr_grid_stats_get only
+  int32_t* host_cnt = nullptr;
+  hipEvent_t stats_ev = nullptr;
+  bool stats_pending = false;
   void release_all() {
+    if (host_cnt) (void)hipHostFree(host_cnt);
+    if (stats_ev) (void)hipEventDestroy(stats_ev);
+    host_cnt = nullptr;
+    stats_ev = nullptr;
+    stats_pending = false;
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &first_pt, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &slot_cursor, &slot_off, &pt_cell, &pt_flag, &pt_slot, &bucket,
                      &counters, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,

@@ -4,9 +4,14 @@ Each ray's output depends only on the (replicated) point table, the MLP
 weights and the ray itself (qpiw.py:442-528 threads are per sample; the
 aggregator and composite are per ray), so the path shards by rays with no
 exchange until the rendered tiles are assembled.  Two ray batchings:
-  * TileShard: pixels of one frame dealt in interleaved 16x16 tiles, round
-    robin over ranks and rotated per frame so the object-centred load
-    balances; one all-gather assembles the frame on every rank;
+  * TileShard: one frame split over the ranks, one all-gather assembles it on
+    every rank.  Layout "bands" (default): N horizontal bands of whole pixel
+    rows, band b of frame f on rank (b + f) mod N, so over the N frames of a
+    step every rank renders every band once (the same pixel count and, up to
+    the per-frame view change, the same work) while its rays stay as
+    spatially coherent as a whole frame's (neighbouring rays share neighbour
+    points in L2).  Layout "tiles16": interleaved 16x16 tiles dealt round
+    robin (finer balance, 1/N of the spatial coherence);
   * FrameShard: each rank renders whole frames (frame f on rank f mod N);
     one all-gather per step gives every rank the step's N frames.  One render
     call per rank per frame, so no per-call overhead grows with N.
@@ -21,8 +26,13 @@ import torch
 TILE = 16
 
 
-def tile_owner(H: int, W: int, world: int, frame: int = 0) -> np.ndarray:
+def tile_owner(H: int, W: int, world: int, frame: int = 0, layout: str = "bands") -> np.ndarray:
     """[H*W] rank owning each pixel (row-major pixel order)."""
+    if layout == "bands":
+        band = (np.arange(H) * world) // H                    # H rows in `world` near-equal bands
+        return np.repeat((band + frame) % world, W)
+    if layout != "tiles16":
+        raise ValueError(f"layout {layout!r}: 'bands' or 'tiles16'")
     ty, tx = np.meshgrid(np.arange(H) // TILE, np.arange(W) // TILE, indexing="ij")
     tiles_x = (W + TILE - 1) // TILE
     return ((ty * tiles_x + tx + frame) % world).reshape(-1)
@@ -31,9 +41,9 @@ def tile_owner(H: int, W: int, world: int, frame: int = 0) -> np.ndarray:
 class TileShard:
     """This rank's share of a frame and the bookkeeping to reassemble it."""
 
-    def __init__(self, H: int, W: int, rank: int, world: int, frame: int = 0, device=None):
-        own = tile_owner(H, W, world, frame)
-        self.H, self.W, self.rank, self.world = H, W, rank, world
+    def __init__(self, H: int, W: int, rank: int, world: int, frame: int = 0, device=None, layout: str = "bands"):
+        own = tile_owner(H, W, world, frame, layout)
+        self.H, self.W, self.rank, self.world, self.layout = H, W, rank, world, layout
         self.counts = np.bincount(own, minlength=world)
         self.max_count = int(self.counts.max())
         self.pixels = [np.nonzero(own == r)[0] for r in range(world)]

@@ -102,6 +102,22 @@ class NeuralPoints(nn.Module):
                 ray_mask, vsize, 0)
 
 
+class _RenderState:
+    """Device buffers one render stream reuses: the query buffers and the
+    aggregate scratch (whose head holds P1, see pnr_points.p1_ready)."""
+
+    def __init__(self):
+        self.bufs = None
+        self.scratch = None
+        self.scratch_key = None
+
+
+def _counts_dict(c):
+    """The 8 query counters (pnr_query_bufs.counts) as QueryBuffers.read_counts() returns them."""
+    n_cand = (int(c[6]) & 0xffffffff) | (int(c[7]) << 32)
+    return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand)
+
+
 # fp32: the reference's arithmetic on v_mfma_f32_32x32x2_f32.  fp32x3: the same
 # fp32 GEMMs as exact 3-way bf16 splits on v_mfma_f32_32x32x16_bf16 (six cross
 # products, fp32-accurate; pnr_aggregate_fwd_x3).  fp32h2: the same GEMMs as 2-way
@@ -125,7 +141,10 @@ class NeuralPointsRayMarching(nn.Module):
         self.neural_points = neural_points
         self.aggregator = aggregator if aggregator is not None else PointAggregator(opt).to(neural_points.device)
         self.chunk_rays = chunk_rays
-        self._bufs = None
+        self._state = _RenderState()     # query buffers + aggregate scratch of the eager path
+        self._pending = []               # render_rays(sync=False) calls awaiting finish()
+        self._sv_per_ray = None          # largest valid samples per ray seen (feature-buffer sizing)
+        self.overflow_rerenders = 0
         # fork's 2-D CNN after the composite (neural_points_volumetric_model.py:258-260, 343-344)
         self.neural_render_2d = None
         if getattr(opt, "neural_render", "none") == "cnn":
@@ -153,7 +172,7 @@ class NeuralPointsRayMarching(nn.Module):
 
     @torch.no_grad()
     def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None,
-                    reuse_p1=False):
+                    reuse_p1=False, sync=True):
         """Fused query -> aggregate -> composite for one ray batch [R,3].
         Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8).
         ``events``: optional list that receives (stage, start, end) HIP events
@@ -164,31 +183,105 @@ class NeuralPointsRayMarching(nn.Module):
         does not depend on the camera) is taken from that call's scratch
         instead of recomputed.  The ray chunks of one call always share it.
 
+        ``sync=False``: no host synchronisation at all.  The decoded-feature
+        buffer is sized from the largest valid-sample count per ray seen so far
+        (x 1.25) instead of this batch's count, and the two checks a
+        synchronous call makes -- the count fits, the fp32h2 activations stayed
+        in range -- are deferred to ``finish()``, which re-renders a call that
+        failed either of them into the same output tensors.  The outputs are
+        valid once ``finish()`` returned.  The first call (no estimate yet)
+        runs synchronously.
+
         fp32h2: the f16 split holds activations below 65504 only.  Each call
         reads the launches' range flag once (a 4-byte read after the last
         chunk); if an activation left the f16 range, the call is rendered again
         on the fp32x3 path (bf16 split: same accuracy, fp32 range) and h2 stays
         off for these weights until they change (``h2_fallbacks`` counts it)."""
         self._sync_rw2c()
+        prec = self._precision_now()
+        if not sync and self._sv_per_ray is not None:
+            out, rec = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events,
+                                         reuse_p1, self._state, capacity=self._capacity_per_ray())
+            rec["args"] = (campos, camrot, raydir, near, far, bg_color, force_grid, reuse_p1)
+            rec["out"] = out
+            self._pending.append(rec)
+            return out
+        n_ev = len(events) if events is not None else 0
+        out, _ = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1,
+                                   self._state)
+        if prec == "fp32h2" and not self.aggregator.h2_range_ok():
+            self._block_h2()
+            if events is not None:
+                del events[n_ev:]
+            out, _ = self._render_rays("fp32x3", campos, camrot, raydir, near, far, bg_color, force_grid, events,
+                                       False, self._state)
+        return out
+
+    def _precision_now(self):
         prec = self.precision
         if prec == "fp32h2" and self._h2_blocked_key is not None:
             if self._h2_blocked_key == self.aggregator.h2_key():
                 prec = "fp32x3"
             else:
                 self._h2_blocked_key = None
-        n_ev = len(events) if events is not None else 0
-        out = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1)
-        if prec == "fp32h2" and not self.aggregator.h2_range_ok():
-            self.aggregator.h2_reset_range()
-            self._h2_blocked_key = self.aggregator.h2_key()
-            self.h2_fallbacks += 1
-            if events is not None:
-                del events[n_ev:]
-            out = self._render_rays("fp32x3", campos, camrot, raydir, near, far, bg_color, force_grid, events,
-                                    False)
-        return out
+        return prec
 
-    def _render_rays(self, precision, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1):
+    def _block_h2(self):
+        self.aggregator.h2_reset_range()
+        self._h2_blocked_key = self.aggregator.h2_key()
+        self.h2_fallbacks += 1
+
+    def _capacity_per_ray(self):
+        return self._sv_per_ray * 1.25
+
+    def _observe(self, counts, rays):
+        r = counts["S_valid"] / max(rays, 1)
+        self._sv_per_ray = r if self._sv_per_ray is None else max(self._sv_per_ray, r)
+
+    @torch.no_grad()
+    def finish(self):
+        """Complete every ``render_rays(sync=False)`` call issued since the last
+        finish(): one host synchronisation, then the deferred checks.  A call
+        whose valid samples overflowed its feature buffer, or (fp32h2) any call
+        when an activation left the f16 range, is rendered again synchronously
+        into its own output tensors.  Returns the per-call sample counts (the
+        ``last_counts`` dict of each call, in issue order)."""
+        pend, self._pending = self._pending, []
+        if not pend:
+            return []
+        pend[-1]["event"].synchronize()
+        range_bad = any(r["precision"] == "fp32h2" for r in pend) and not self.aggregator.h2_range_ok()
+        if range_bad:
+            self._block_h2()
+        counts = []
+        for rec in pend:
+            tot = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
+            over = False
+            for (cap, rays), h in zip(rec["caps"], rec["host"].tolist()):
+                c = _counts_dict(h)
+                self._observe(c, rays)
+                over |= c["S_valid"] > cap
+                for k in tot:
+                    tot[k] += c[k]
+            if over or (range_bad and rec["precision"] == "fp32h2"):
+                cp, cr, rd, near, far, bg, fg, reuse = rec["args"]
+                prec = "fp32x3" if rec["precision"] == "fp32h2" and range_bad else rec["precision"]
+                out, _ = self._render_rays(prec, cp, cr, rd, near, far, bg, fg, None, False, self._state)
+                for dst, src in zip(rec["out"], out):
+                    dst.copy_(src)
+                tot = dict(self.last_counts)
+                self.overflow_rerenders += int(over)
+            counts.append(tot)
+        self.last_counts = counts[-1]
+        return counts
+
+    def _render_rays(self, precision, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1,
+                     state, capacity=None, keep=None, record=True):
+        """One render call.  capacity None: size the feature buffer from this
+        batch's counts (one host sync per chunk); else capacity = valid samples
+        per ray the feature buffer is sized for (no sync; the per-chunk counts
+        are copied to pinned host memory behind an event, returned in the
+        record for finish() / RenderGraph.check())."""
         opt = self.opt
         dev = raydir.device
         L.require_gpu(raydir)
@@ -213,13 +306,23 @@ class NeuralPointsRayMarching(nn.Module):
         camrot = camrot.reshape(3, 3).float().contiguous()
         bf16 = precision == "bf16"
         mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
+        mlpx = mlph = _keepx = _keeph = None
         if precision == "fp32x3":
             mlpx, _keepx = self.aggregator.packed_x3()
         elif precision == "fp32h2":
             mlph, _keeph = self.aggregator.packed_h2()
+        if keep is not None:   # RenderGraph: the captured launches point into these packs
+            keep += [mlp, _keepw, mlpx, _keepx, mlph, _keeph]
         pts, _keepp = np_.tables(campos, camrot)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
         chunk = max(1, self.chunk_rays or R)
+        n_chunks = max(1, -(-R // chunk))
+        rec = None
+        if capacity is not None:
+            host = torch.empty((n_chunks, 8), dtype=torch.int32, pin_memory=True) if record else None
+            dcounts = None if record else torch.empty((n_chunks, 8), dtype=torch.int32, device=dev)
+            rec = dict(precision=precision, caps=[], host=host, dcounts=dcounts)
+
         def mark():
             if events is None:
                 return None
@@ -227,23 +330,28 @@ class NeuralPointsRayMarching(nn.Module):
             e.record()
             return e
 
-        for r0 in range(0, R, chunk):
+        for ci, r0 in enumerate(range(0, R, chunk)):
             r1 = min(R, r0 + chunk)
             rd = raydir[r0:r1].contiguous()
             e0 = mark()
-            bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=self._bufs)
+            bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=state.bufs)
             e1 = mark()
-            self._bufs = bufs
-            cnt = bufs.read_counts()
-            for k in totals:
-                totals[k] += cnt[k]
-            Sv = cnt["S_valid"]
+            state.bufs = bufs
+            if capacity is None:
+                cnt = bufs.read_counts()
+                for k in totals:
+                    totals[k] += cnt[k]
+                self._observe(cnt, r1 - r0)
+                Sv = cnt["S_valid"]
+            else:
+                Sv = min(int((r1 - r0) * capacity) + 1024, (r1 - r0) * SR)
+                rec["caps"].append((Sv, r1 - r0))
             feat = torch.empty((max(Sv, 1), 129), **f32)
             s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K)
             e2 = mark()
-            scratch, ready = self._agg_scratch(max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
+            scratch, ready = self._agg_scratch(state, max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
             pts.p1_ready = int(ready)
             if bf16:
                 L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
@@ -268,19 +376,29 @@ class NeuralPointsRayMarching(nn.Module):
             if C == 3:   # upstream colour head: [alpha, rgb] rows
                 feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
             e3 = mark()
-            cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
+            cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg), max(Sv, 1))
             L.check(L.lib().pnr_composite_fwd(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),
                                               L.ctypes.byref(cp), L.ptr(feat), L.ptr(ray_color[r0:r1]),
                                               L.ptr(opacity[r0:r1]), L.ptr(is_bg[r0:r1]),
                                               L.ptr(ray_mask[r0:r1]), L.stream_ptr(dev)),
                     "pnr_composite_fwd")
+            if rec is not None:
+                if record:
+                    rec["host"][ci].copy_(bufs.counts, non_blocking=True)
+                else:
+                    rec["dcounts"][ci].copy_(bufs.counts)
             if events is not None:
                 e4 = mark()
                 events += [("query", e0, e1), ("aggregate", e2, e3), ("composite", e3, e4)]
-        self.last_counts = totals
-        return ray_color, opacity, is_bg, ray_mask
+        if rec is not None:
+            if record:
+                rec["event"] = torch.cuda.Event()
+                rec["event"].record()
+        else:
+            self.last_counts = totals
+        return (ray_color, opacity, is_bg, ray_mask), rec
 
-    def _agg_scratch(self, n_max, n_points, dev, bf16, reuse, precision="fp32"):
+    def _agg_scratch(self, state, n_max, n_points, dev, bf16, reuse, precision="fp32"):
         """Persistent aggregate scratch (P1 lives at its start, see
         pnr_points.p1_ready) -> (tensor, P1 already valid).  The P1 is valid
         when reuse is requested and the embedding storage, block1.0 and the
@@ -294,13 +412,13 @@ class NeuralPointsRayMarching(nn.Module):
         nb = L.c_size_t(0)
         fn = L.lib().pnr_aggregate_scratch_bytes_bf16 if bf16 else L.lib().pnr_aggregate_scratch_bytes
         L.check(fn(int(n_max), int(n_points), L.ctypes.byref(nb)), "aggregate scratch bytes")
-        buf = getattr(self, "_scratch", None)
+        buf = state.scratch
         if buf is None or buf.device != dev or buf.numel() * 4 < int(nb.value):
             buf = need(int(n_max * 1.25) + 1024, n_points, dev)   # headroom: n_max varies per batch
-            self._scratch = buf
-            self._scratch_key = None
-        ready = reuse and self._scratch_key == key
-        self._scratch_key = key
+            state.scratch = buf
+            state.scratch_key = None
+        ready = reuse and state.scratch_key == key
+        state.scratch_key = key
         return buf, ready
 
     def render_rays_train(self, campos, camrot, raydir, near, far, bg_color):
@@ -427,3 +545,82 @@ class NeuralPointsRayMarching(nn.Module):
             out["final_coarse_raycolor"] = self.neural_render_2d(
                 out["coarse_raycolor"].reshape(1, img_h, img_w, -1)).reshape(1, -1, 3)
         return out
+
+
+class RenderGraph:
+    """One ray batch's full render (query -> aggregate -> composite) captured
+    in a HIP graph and replayed without any host work beyond the launch:
+    SURVEY 8(f) rank 2 (the reference syncs at qpiw.py:656, 716 and
+    neural_points.py:786).  The graph owns its query buffers, aggregate
+    scratch and outputs; the camera and ray directions are static input
+    tensors that ``replay`` refreshes in place.  Capture requires an already
+    built grid and fixed weights (the launches point at the current grid
+    tables and weight packs; rebuild the graph after either changes).
+
+    The feature buffer is sized from an eager render of the same batch
+    (valid samples x ``margin``); ``check()`` reads the replay's counts and
+    the fp32h2 range flag (one host sync) and returns False when the replay
+    overflowed that size or an activation left the f16 range -- then render
+    that frame with ``render_rays`` instead."""
+
+    def __init__(self, model: NeuralPointsRayMarching, campos, camrot, raydir, near, far, bg_color,
+                 margin: float = 1.25):
+        L.require_gpu(raydir)
+        self.model = model
+        dev = raydir.device
+        self.campos = campos.reshape(3).float().to(dev).clone()
+        self.camrot = camrot.reshape(3, 3).float().to(dev).clone()
+        self.raydir = raydir.reshape(-1, 3).float().contiguous().clone()
+        self.near, self.far = near, far
+        self.bg = None if bg_color is None else bg_color.to(dev).float().reshape(-1).contiguous().clone()
+        model._sync_rw2c()
+        self.precision = model._precision_now()
+        R = self.raydir.shape[0]
+        chunk = max(1, model.chunk_rays or R)
+        self.state = _RenderState()
+        # eager render: builds nothing new (grid must exist), sizes the buffers
+        model._render_rays(self.precision, self.campos, self.camrot, self.raydir, near, far, self.bg, False, None,
+                           False, self.state)
+        self.eager_counts = dict(model.last_counts)
+        cap = margin * max(self.eager_counts["S_valid"], 1) / max(min(chunk, R), 1)
+        self.keep = []
+        stream = torch.cuda.Stream(dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):   # warm-up on a side stream (allocations, packs)
+            model._render_rays(self.precision, self.campos, self.camrot, self.raydir, near, far, self.bg, False,
+                               None, False, self.state, capacity=cap, record=False)
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out, self.rec = model._render_rays(self.precision, self.campos, self.camrot, self.raydir, near, far,
+                                                    self.bg, False, None, False, self.state, capacity=cap,
+                                                    keep=self.keep, record=False)
+        self.capacity = cap
+
+    def replay(self, campos=None, camrot=None, raydir=None):
+        """Render the batch again (new camera / rays copied into the static
+        inputs first); returns (ray_color, opacity, is_bg, ray_mask), tensors the
+        graph owns and overwrites on the next replay."""
+        if campos is not None:
+            self.campos.copy_(campos.reshape(3))
+        if camrot is not None:
+            self.camrot.copy_(camrot.reshape(3, 3))
+        if raydir is not None:
+            self.raydir.copy_(raydir.reshape(-1, 3))
+        self.graph.replay()
+        return self.out
+
+    def check(self) -> bool:
+        """True when the last replay's outputs are valid: every chunk's valid
+        samples fit the captured feature buffer and (fp32h2) no activation left
+        the f16 range.  Synchronises."""
+        ok = True
+        for (cap, rays), h in zip(self.rec["caps"], self.rec["dcounts"].cpu().tolist()):
+            c = _counts_dict(h)
+            self.last_counts = c
+            ok &= c["S_valid"] <= cap
+        if self.precision == "fp32h2" and not self.model.aggregator.h2_range_ok():
+            self.model.aggregator.h2_reset_range()
+            ok = False
+        return ok

@@ -34,8 +34,8 @@ def _worker(rank, world, port, q):
     sc = scene(8000, H=H, W=W, theta=60.0)
     params = formula_params(salt=0.4)
     outs = []
-    for frame in range(2):
-        sh = TileShard(H, W, rank, world, frame)
+    for frame in range(4):
+        sh = TileShard(H, W, rank, world, frame, layout="bands" if frame < 2 else "tiles16")
         rd = sh.select(torch.from_numpy(sc["raydir"])).numpy()
         r = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], rd, sc["bg"])
         local = torch.from_numpy(np.concatenate([r["coarse_raycolor"], r["coarse_is_background"]], 1))
@@ -50,9 +50,32 @@ def test_tile_split_covers_every_pixel_once():
     from pointnerf_amd.parallel import tile_owner
     for world in (1, 2, 3, 8):
         for frame in range(3):
-            own = tile_owner(800, 800, world, frame)
+            own = tile_owner(800, 800, world, frame, "tiles16")
             c = np.bincount(own, minlength=world)
             assert c.sum() == 640000 and c.max() - c.min() <= 256   # at most one 16x16 tile apart
+
+
+def test_band_shards_800_8_ranks_bookkeeping():
+    """bench --shard tiles at 800x800 on 8 ranks (the driver's N = 8 run): per
+    frame every pixel has exactly one owner, each rank's share is whole pixel
+    rows (contiguous, row-major), the gathered-row map is a permutation, and
+    over the 8 frames of a step every rank renders every band exactly once."""
+    from pointnerf_amd.parallel import TileShard, tile_owner
+    H = W = 800
+    world = 8
+    seen = np.zeros((world, world), dtype=np.int64)   # [rank, band] pixels over a step
+    for frame in range(world):
+        own = tile_owner(H, W, world, frame)
+        assert np.bincount(own, minlength=world).tolist() == [H * W // world] * world
+        shards = [TileShard(H, W, r, world, frame) for r in range(world)]
+        for r, sh in enumerate(shards):
+            px = sh.pixels[r]
+            assert px.size % W == 0 and np.array_equal(px, np.arange(px[0], px[0] + px.size))
+            band = (px[0] // W) * world // H
+            seen[r, band] += px.size
+        src = shards[0].src.numpy()
+        assert np.array_equal(np.sort(src), np.arange(H * W)) and shards[0].max_count == H * W // world
+    assert (seen == H * W // world).all()
 
 
 def test_two_rank_render_assembles_full_frame():
