@@ -9,9 +9,11 @@ points"): lego flag set (dev_scripts/w_n360/lego.sh), a seeded synthetic
 2,000,000-point lego-like cloud, 800x800 NeRF-synthetic cameras, forward
 render.  One step = every GPU renders one full frame's worth of rays through
 the whole hot path: voxel-grid build, query, fused gather+MLP aggregation,
-composite+fill_invalid; with N > 1 the step's N frames are split across ranks
-in interleaved 16x16 pixel tiles and the rendered tiles are all-gathered over
-RCCL (weak scaling: per-GPU work is fixed).  A ray-sample is one (ray,
+composite+fill_invalid; with N > 1 every one of the step's N frames is split
+across the ranks in N row bands (band b of frame f on rank (b + f) mod N, so
+each rank renders every band once per step), a rank renders its N bands as one
+multi-camera ray batch, and one RCCL all-gather of the rendered tiles gives
+every rank the step's N frames (weak scaling: per-GPU work is fixed).  A ray-sample is one (ray,
 shading-slot) entry of the dense H*W*SR grid the reference materialises
 (SURVEY 8(d)); value = all ranks' ray-samples / max-over-ranks time.
 """
@@ -48,13 +50,17 @@ def parse():
     ap.add_argument("--no-grid-rebuild", action="store_true",
                     help="reuse the voxel grid across steps (default: rebuild every step)")
     ap.add_argument("--no-gather", action="store_true", help="skip the all-gather of rendered rays (N > 1)")
-    ap.add_argument("--shard", choices=("frames", "tiles"), default="frames",
-                    help="N > 1 ray batches: frames = each rank renders whole frames (frame f on rank f mod N, "
-                         "one all-gather of the step's N frames); tiles = every frame split in interleaved 16x16 "
-                         "pixel tiles over the ranks (N partial frames per rank per step)")
+    ap.add_argument("--shard", choices=("frames", "tiles"), default="tiles",
+                    help="N > 1 ray batches: tiles (default) = every frame split over the ranks (--tile-layout), "
+                         "a rank's N partial frames of the step rendered as ONE multi-camera batch, ONE RCCL "
+                         "all-gather assembles the step's N frames on every rank; frames = each rank renders "
+                         "whole frames (frame f on rank f mod N, one all-gather of the step's N frames)")
     ap.add_argument("--tile-layout", choices=("bands", "tiles16"), default="bands",
                     help="--shard tiles: bands = N row bands per frame, band b of frame f on rank (b+f) mod N "
                          "(every rank renders every band once per step); tiles16 = interleaved 16x16 tiles")
+    ap.add_argument("--per-frame-calls", action="store_true",
+                    help="--shard tiles: one render call per partial frame (N calls per step) instead of one "
+                         "multi-camera batch (A/B of the per-call cost)")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="diagnostic (single process): do rank 0's share of an N-rank step (N partial frames of "
                          "1/N of the rays, no collective) to project per-rank overheads of the N-GPU run")
@@ -340,7 +346,7 @@ def main():
                          torch.from_numpy(rd).to(device)))
     bg = torch.from_numpy(np.random.default_rng(1).uniform(size=128).astype(np.float32)).to(device)
 
-    from pointnerf_amd.parallel import FrameShard, TileShard
+    from pointnerf_amd.parallel import FrameShard, StepShard, TileShard
     shards = {}
     fshard = FrameShard(rank, world) if (world > 1 and args.shard == "frames") else None
 
@@ -357,22 +363,44 @@ def main():
 
     stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0, "cand": 0, "rays": 0}
 
+    steps = {}
+
+    def step_batch(s):
+        """tiles mode: this rank's shares of the step's N frames as ONE ray batch
+        (per-ray camera index) + the StepShard that assembles them."""
+        cis = tuple((s * shard_world + i) % len(cams) for i in range(shard_world))
+        if cis not in steps:
+            st = StepShard([TileShard(H, W, rank, shard_world, i, device, layout=args.tile_layout)
+                            for i in range(shard_world)], device)
+            rd = st.select([dev_cams[ci][2] for ci in cis]).contiguous()
+            cp = torch.stack([dev_cams[ci][0] for ci in cis])
+            cr = torch.stack([dev_cams[ci][1] for ci in cis])
+            steps[cis] = (st, rd, cp, cr)
+        return steps[cis]
+
     def step(s, timed):
         # every render call of the step is issued without a host sync
         # (render_rays(sync=False)); model.finish() is the step's one sync: it
         # checks the deferred feature-buffer sizes / f16 range and returns the counts
         parts = []
         ev_step = [] if timed else None
-        for f in range(shard_world):
-            frame = s * shard_world + f
-            if fshard is not None:
-                frame = fshard.frame_of(s)   # whole frame s*N + rank
-            ci, rd, sh = my_rays(frame)
-            campos, camrot, _ = dev_cams[ci]
-            color, opac, is_bg, mask = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
-                                                         force_grid=(f == 0 and not args.no_grid_rebuild),
-                                                         events=ev_step, reuse_p1=f > 0, sync=False)
-            parts.append((sh, color, rd.shape[0]))
+        if shard_world > 1 and not args.per_frame_calls:
+            st, rd, cp, cr = step_batch(s)
+            color = model.render_rays(cp, cr, rd, opt.near_plane, opt.far_plane, bg,
+                                      force_grid=not args.no_grid_rebuild, events=ev_step, sync=False,
+                                      ray_cam=st.ray_cam)[0]
+            parts.append((st, color, rd.shape[0]))
+        else:
+            for f in range(shard_world):
+                frame = s * shard_world + f
+                if fshard is not None:
+                    frame = fshard.frame_of(s)   # whole frame s*N + rank
+                ci, rd, sh = my_rays(frame)
+                campos, camrot, _ = dev_cams[ci]
+                color = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
+                                          force_grid=(f == 0 and not args.no_grid_rebuild),
+                                          events=ev_step, reuse_p1=f > 0, sync=False)[0]
+                parts.append((sh, color, rd.shape[0]))
         counts = model.finish()
         if timed:
             for c, (_, _, nr) in zip(counts, parts):
@@ -387,8 +415,8 @@ def main():
         for sh, color, _ in parts:
             if world > 1 and not args.no_gather:
                 # RCCL all-gather of the rendered rays (async: they travel over xGMI while
-                # the next step renders): tiles -> every rank holds the frame; frames ->
-                # every rank holds the step's N frames
+                # the next step renders): tiles -> one all-gather assembles the step's N
+                # frames on every rank; frames -> every rank holds the step's N frames
                 frames.append((fshard or sh).assemble_async(color))
             else:
                 frames.append(color)
@@ -399,6 +427,9 @@ def main():
         # stream after the collective, so the host is not blocked
         return [f.wait() if hasattr(f, "wait") else f for f in handles]
 
+    if shard_world > 1 and not args.per_frame_calls:
+        for s in range(args.warmup + args.steps):   # ray batches + gather maps built outside the timed region
+            step_batch(s)
     for s in range(args.warmup):
         finish(step(s, False))
     torch.cuda.synchronize()
@@ -469,7 +500,8 @@ def main():
                        "grid_rebuild_per_step": not args.no_grid_rebuild,
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else
-                                       f"dp{world} (16x16 ray tiles, async RCCL all_gather of tiles)")
+                                       f"dp{world} ({args.tile_layout} ray shards of every frame, one multi-camera "
+                                       f"batch per rank per step, async RCCL all_gather of the tiles)")
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "kernel": {
                              "fp32": "pnr_aggregate_fwd = k_point_pre + k_pairs + k_color (v_mfma_f32_32x32x2_f32)",

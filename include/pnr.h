@@ -55,7 +55,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 6
+#define PNR_ABI_VERSION 7
 
 enum {
   PNR_OK = 0,
@@ -123,13 +123,18 @@ int pnr_grid_export(pnr_handle* h, int32_t* coor_2_occ, uint32_t* occ_bits, int3
  * middle_point_ts (diff_ray_marching.py:369-385), either one table shared by
  * every ray (tvals_per_ray = 0, jitter = 0) or one row per ray. */
 typedef struct {
-  const float* campos_dev;    /* [3]                                   */
-  const float* camrot_dev;    /* [3,3] row-major camrotc2w             */
+  const float* campos_dev;    /* [3]  ([n_cams,3] with ray_cam)        */
+  const float* camrot_dev;    /* [3,3] row-major camrotc2w ([n_cams,3,3] with ray_cam) */
   const float* raydir_dev;    /* [R,3]                                 */
   const float* tvals_dev;     /* [D] or [R,D]                          */
   int64_t R;
   int32_t D;
   int32_t tvals_per_ray;
+  const int32_t* ray_cam;     /* NULL: every ray from the one camera; else [R] camera
+                                 index of each ray into campos/camrot: several frames'
+                                 (partial) ray batches rendered as ONE batch (one
+                                 query / aggregate / composite launch each), e.g. the
+                                 N band shares of a multi-GPU step                      */
 } pnr_rays;
 
 typedef struct {
@@ -237,6 +242,9 @@ typedef struct {
                                 else  dirs row = dir_map[sample row] / dir_div     */
   int32_t dir_div;
   int32_t K;
+  const int32_t* ray_cam;    /* NULL: pts->campos / camrot is the one camera; else the
+                                camera of dirs row r is ray_cam[r] into the pts tables
+                                campos[n_cams,3] / camrot[n_cams,3,3] (pnr_rays.ray_cam) */
 } pnr_samples;
 
 /* For every entry v < min(*n_dev, n_max) of samp_list (row = samp_list[v], or

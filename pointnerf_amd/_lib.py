@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class PnrError(RuntimeError):
@@ -39,7 +39,8 @@ class GridStats(ctypes.Structure):
 
 class Rays(ctypes.Structure):
     _fields_ = [("campos_dev", c_void_p), ("camrot_dev", c_void_p), ("raydir_dev", c_void_p),
-                ("tvals_dev", c_void_p), ("R", c_int64), ("D", c_int32), ("tvals_per_ray", c_int32)]
+                ("tvals_dev", c_void_p), ("R", c_int64), ("D", c_int32), ("tvals_per_ray", c_int32),
+                ("ray_cam", c_void_p)]
 
 
 class QueryParams(ctypes.Structure):
@@ -84,7 +85,7 @@ class Points(ctypes.Structure):
 class Samples(ctypes.Structure):
     _fields_ = [("samp_list", c_void_p), ("n_dev", c_void_p), ("n_max", c_int64), ("pidx", c_void_p),
                 ("sample_w", c_void_p), ("sample_p", c_void_p), ("dirs", c_void_p),
-                ("dir_map", c_void_p), ("dir_div", c_int32), ("K", c_int32)]
+                ("dir_map", c_void_p), ("dir_div", c_int32), ("K", c_int32), ("ray_cam", c_void_p)]
 
 
 class CompositeParams(ctypes.Structure):

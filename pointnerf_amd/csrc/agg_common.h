@@ -44,6 +44,25 @@ __device__ __forceinline__ int64_t dir_row(const pnr_samples& s, int64_t row) {
   return (s.dir_map ? (int64_t)s.dir_map[row] : row) / s.dir_div;
 }
 
+// Perspective coordinates of a gathered point (qpiw.py:102-109 w2pers) under the
+// camera of the pair's ray: the launch's one camera (cam_c / cam_R, loaded once)
+// or, for a multi-camera ray batch (pnr_samples.ray_cam), the ray's entry of the
+// camera tables pts.campos[n_cams][3] / pts.camrot[n_cams][9].
+__device__ __forceinline__ void pair_pers(const pnr_points& P, const pnr_samples& S, int64_t ray, const float pw[3],
+                                          const float cam_c[3], const float cam_R[9], float pp[3]) {
+  if (S.ray_cam) {
+    const int64_t cam = S.ray_cam[ray];
+    float c[3], R[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c[i] = P.campos[cam * 3 + i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = P.camrot[cam * 9 + i];
+    world_to_pers(pw, c, R, pp);
+  } else {
+    world_to_pers(pw, cam_c, cam_R, pp);
+  }
+}
+
 __device__ __forceinline__ int64_t eff_n(const pnr_samples& s) {
   int64_t n = s.n_max;
   if (s.n_dev) {

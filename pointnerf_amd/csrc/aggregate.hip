@@ -465,8 +465,9 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
       }
     }
     float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
+    int64_t drow = 0;
     if (active) {
-      const int64_t drow = dir_row(A.s, row);
+      drow = dir_row(A.s, row);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         sw[a] = A.s.sample_w[row * 3 + a];
@@ -488,7 +489,7 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
 #pragma unroll
         for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
       } else {
-        world_to_pers(pw, cam_c, cam_R, pp);
+        pair_pers(A.pts, A.s, drow, pw, cam_c, cam_R, pp);
       }
     }
     if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];

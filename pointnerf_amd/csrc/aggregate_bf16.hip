@@ -248,8 +248,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
         prow = valid ? pid : 0;
       }
       float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
+      int64_t drow = 0;
       if (active) {
-        const int64_t drow = dir_row(A.s, row);
+        drow = dir_row(A.s, row);
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
           sw[a] = A.s.sample_w[row * 3 + a];
@@ -271,7 +272,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
 #pragma unroll
           for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
         } else {
-          world_to_pers(pw, cam_c, cam_R, pp);
+          pair_pers(A.pts, A.s, drow, pw, cam_c, cam_R, pp);
         }
       }
       if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];

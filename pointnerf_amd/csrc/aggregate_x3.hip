@@ -496,8 +496,8 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
     sw[a] = g.sw[a];
     sp[a] = g.sp[a];
   }
+  const int64_t drow = active ? g.dmap / A.s.dir_div : 0;
   if (active) {
-    const int64_t drow = g.dmap / A.s.dir_div;
 #pragma unroll
     for (int a = 0; a < 3; ++a) vd[a] = A.s.dirs[drow * 3 + a];
   }
@@ -514,7 +514,7 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
 #pragma unroll
       for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
     } else {
-      world_to_pers(pw3, cam_c, cam_R, pp);
+      pair_pers(A.pts, A.s, drow, pw3, cam_c, cam_R, pp);
     }
   }
   if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];

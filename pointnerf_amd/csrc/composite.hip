@@ -74,6 +74,7 @@ __device__ __forceinline__ SlotOut march_slots(float sig0, float dist0, float si
 struct CompArgs {
   const float* campos;
   const float* camrot;
+  const int32_t* ray_cam;   // NULL: one camera; else camera index per ray
   int64_t R;
   int SR;
   const int32_t* n_filled;
@@ -94,23 +95,27 @@ struct CompArgs {
   int8_t* ray_mask;
 };
 
+// Camera-space depth of the world origin: the z of every unfilled slot
+// (sample_loc_w = 0, neural_points_volumetric_model.py:293) for camera `cam`.
+__device__ float origin_depth(const CompArgs& a, int64_t cam) {
+  float c[3], Rm[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) c[i] = a.campos[cam * 3 + i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rm[i] = a.camrot[cam * 9 + i];
+  const float zero[3] = {0.f, 0.f, 0.f};
+  float pc[3];
+  world_to_cam(zero, c, Rm, pc);
+  return pc[2];
+}
+
 __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int SR = a.SR, C = a.C, CF = C + 1;
   // depth of the world origin: the z of every unfilled slot (sample_loc_w = 0)
-  float zo;
-  {
-    const float c[3] = {a.campos[0], a.campos[1], a.campos[2]};
-    float Rm[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) Rm[i] = a.camrot[i];
-    const float zero[3] = {0.f, 0.f, 0.f};
-    float pc[3];
-    world_to_cam(zero, c, Rm, pc);
-    zo = pc[2];
-  }
+  const float zo0 = origin_depth(a, 0);
   const float vz = a.vsize_z, two_vz = 2.f * a.vsize_z;
   for (int64_t r = wave0; r < a.R; r += nwaves) {
     const bool mask = a.ray_vcnt[r] > 0;
@@ -124,6 +129,7 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
       continue;
     }
     const int n = a.n_filled[r], off = a.ray_off[r];
+    const float zo = a.ray_cam ? origin_depth(a, a.ray_cam[r]) : zo0;
     float z[2], sig[2];
     int vrow[2];
 #pragma unroll
@@ -335,22 +341,13 @@ __global__ void __launch_bounds__(kCBlock) k_composite_bwd(CompBwdArgs A) {
   const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int SR = a.SR, C = a.C, CF = C + 1;
-  float zo;
-  {
-    const float c[3] = {a.campos[0], a.campos[1], a.campos[2]};
-    float Rm[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) Rm[i] = a.camrot[i];
-    const float zero[3] = {0.f, 0.f, 0.f};
-    float pc[3];
-    world_to_cam(zero, c, Rm, pc);
-    zo = pc[2];
-  }
+  const float zo0 = origin_depth(a, 0);
   const float vz = a.vsize_z, two_vz = 2.f * a.vsize_z;
   for (int64_t r = wave0; r < a.R; r += nwaves) {
     if (a.ray_vcnt[r] <= 0) continue;   // background ray: no feature gradient
     // forward recompute (same as k_composite)
     const int n = a.n_filled[r], off = a.ray_off[r];
+    const float zo = a.ray_cam ? origin_depth(a, a.ray_cam[r]) : zo0;
     float z[2], sig[2];
     int vrow[2];
 #pragma unroll
@@ -480,6 +477,7 @@ extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q
   CompArgs a;
   a.campos = rays->campos_dev;
   a.camrot = rays->camrot_dev;
+  a.ray_cam = rays->ray_cam;
   a.R = rays->R;
   a.SR = q->SR;
   a.n_filled = b->n_filled;
@@ -531,6 +529,7 @@ extern "C" int pnr_composite_bwd(const pnr_rays* rays, const pnr_query_params* q
   CompBwdArgs a;
   a.f.campos = rays->campos_dev;
   a.f.camrot = rays->camrot_dev;
+  a.f.ray_cam = rays->ray_cam;
   a.f.R = rays->R;
   a.f.SR = q->SR;
   a.f.n_filled = b->n_filled;

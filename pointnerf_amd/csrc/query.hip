@@ -43,7 +43,17 @@ struct QRays {
   int64_t R;
   int D;
   int per_ray;
+  const int32_t* ray_cam;   // NULL: one camera; else camera index per ray
 };
+
+// Camera of ray r: the batch's one camera or its entry of the camera tables.
+__device__ __forceinline__ int64_t cam_of(const QRays& q, int64_t r) { return q.ray_cam ? (int64_t)q.ray_cam[r] : 0; }
+__device__ __forceinline__ void load_cam(const QRays& q, int64_t cam, float c[3], float R[9]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) c[i] = q.campos[cam * 3 + i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = q.camrot[cam * 9 + i];
+}
 
 __device__ __forceinline__ float tval(const QRays& q, int64_t r, int d) {
   return q.tvals[(q.per_ray ? r * q.D : 0) + d];
@@ -61,9 +71,10 @@ __global__ void __launch_bounds__(kQBlock) k_march(QRays q, QGrid g, int SR,
                                                    const uint32_t* __restrict__ occ_bits,
                                                    int32_t* __restrict__ n_filled,
                                                    uint16_t* __restrict__ slot_d) {
-  const float c[3] = {q.campos[0], q.campos[1], q.campos[2]};
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < q.R;
        r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cam = cam_of(q, r);
+    const float c[3] = {q.campos[cam * 3], q.campos[cam * 3 + 1], q.campos[cam * 3 + 2]};
     const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
     int n = 0;
     for (int d = 0; d < q.D && n < SR; ++d) {
@@ -282,10 +293,8 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
                                                  float* __restrict__ sample_w,
                                                  float* __restrict__ sample_p, int32_t* counts, int vec_pidx) {
   const int64_t S = counts[0];
-  const float c[3] = {q.campos[0], q.campos[1], q.campos[2]};
-  float Rm[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rm[i] = q.camrot[i];
+  float c[3], Rm[9];
+  load_cam(q, 0, c, Rm);
   int pairs = 0, n_cand = 0;
   // A block takes 256 consecutive filled samples (~a dozen neighbouring rays of
   // one pixel row) and hands them to its lanes ordered by shading slot: lanes
@@ -328,6 +337,7 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
     const int64_t r = rs / SR;
     const int d = slot_d[rs];
     const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
+    if (q.ray_cam) load_cam(q, q.ray_cam[r], c, Rm);
     float p[3], pp[3];
     ray_point(c, dir, tval(q, r, d), p);
     world_to_pers(p, c, Rm, pp);
@@ -383,18 +393,15 @@ __global__ void __launch_bounds__(kQBlock) k_compact(QRays q, int SR, int K, int
                                                      int32_t* __restrict__ o_pidx, float* __restrict__ o_loc,
                                                      float* __restrict__ o_loc_w,
                                                      float* __restrict__ o_dirs, int8_t* __restrict__ ray_mask) {
-  const float c[3] = {q.campos[0], q.campos[1], q.campos[2]};
-  float Rm[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rm[i] = q.camrot[i];
   const float zero[3] = {0.f, 0.f, 0.f};
-  float origin_p[3];
-  world_to_pers(zero, c, Rm, origin_p);
   const int64_t total = q.R * SR;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = e / SR;
     const int s = (int)(e - r * SR);
+    float c[3], Rm[9], origin_p[3];
+    load_cam(q, cam_of(q, r), c, Rm);
+    world_to_pers(zero, c, Rm, origin_p);
     const bool m = ray_vcnt[r] > 0;
     if (s == 0) ray_mask[r] = m ? 1 : 0;
     if (!m) continue;
@@ -431,6 +438,7 @@ QRays to_qrays(const pnr_rays* r) {
   q.R = r->R;
   q.D = r->D;
   q.per_ray = r->tvals_per_ray;
+  q.ray_cam = r->ray_cam;
   return q;
 }
 

@@ -91,6 +91,62 @@ class _Gather:
         return buf.index_select(0, self.shard.src.to(buf.device))
 
 
+class StepShard:
+    """A rank's shares of the N frames of one step rendered as ONE ray batch
+    (NeuralPointsRayMarching.render_rays with ray_cam: one query / aggregate /
+    composite launch for all N partial frames) and assembled with ONE
+    all-gather: rank r's rows are its share of frame 0, then of frame 1, ...;
+    wait() returns the N full frames [H*W, C] in step order."""
+
+    def __init__(self, shards: list, device=None):
+        self.shards = shards
+        self.world = shards[0].world
+        rank = shards[0].rank
+        # per frame: rows of every rank's share, padded per rank to the step's max
+        per_rank = np.array([[sh.counts[r] for sh in shards] for r in range(self.world)])   # [world, frames]
+        self.sizes = per_rank[rank].tolist()
+        self.max_count = int(per_rank.sum(1).max())
+        offs = np.concatenate([np.zeros((self.world, 1), np.int64), np.cumsum(per_rank, 1)], 1)
+        self.src = []
+        for f, sh in enumerate(shards):
+            src = np.empty(sh.H * sh.W, dtype=np.int64)
+            for r in range(self.world):
+                src[sh.pixels[r]] = r * self.max_count + offs[r, f] + np.arange(sh.pixels[r].size)
+            self.src.append(torch.from_numpy(src).to(device) if device is not None else torch.from_numpy(src))
+        idx = np.concatenate([sh.pixels[rank] for sh in shards])
+        self.idx = torch.from_numpy(idx).to(device) if device is not None else torch.from_numpy(idx)
+        cam = np.repeat(np.arange(len(shards), dtype=np.int32), self.sizes)
+        self.ray_cam = torch.from_numpy(cam).to(device) if device is not None else torch.from_numpy(cam)
+
+    def select(self, per_frame: list) -> torch.Tensor:
+        """This rank's rays of the step: rows of each frame's [H*W, ...] tensor
+        (per_frame[f]) it owns, concatenated in frame order."""
+        return torch.cat([t.index_select(0, sh.idx.to(t.device)) for t, sh in zip(per_frame, self.shards)])
+
+    def assemble_async(self, local: torch.Tensor, group=None) -> "_StepGather":
+        import torch.distributed as dist
+        C = local.shape[1]
+        pad = local.new_zeros((self.max_count, C))
+        pad[: local.shape[0]] = local
+        if dist.get_backend(group) == "nccl":
+            buf = torch.empty((self.world * self.max_count, C), dtype=local.dtype, device=local.device)
+            work = dist.all_gather_into_tensor(buf, pad, group=group, async_op=True)
+            return _StepGather(self, work, buf, None)
+        lst = [torch.empty_like(pad) for _ in range(self.world)]
+        work = dist.all_gather(lst, pad, group=group, async_op=True)
+        return _StepGather(self, work, None, lst)
+
+
+class _StepGather:
+    def __init__(self, step, work, buf, parts):
+        self.step, self.work, self.buf, self.parts = step, work, buf, parts
+
+    def wait(self) -> list:
+        self.work.wait()
+        buf = self.buf if self.buf is not None else torch.cat(self.parts)
+        return [buf.index_select(0, src.to(buf.device)) for src in self.step.src]
+
+
 class FrameShard:
     """Whole-frame ray batches: rank r renders frames r, r + N, r + 2N, ...;
     assemble_async all-gathers one [P, C] frame from every rank into the

@@ -197,14 +197,24 @@ def query_params(opt, hp) -> L.QueryParams:
     return qp
 
 
-def make_rays(campos, camrot, raydir, tvals, per_ray: bool) -> L.Rays:
+def make_rays(campos, camrot, raydir, tvals, per_ray: bool, ray_cam=None) -> L.Rays:
     r = L.Rays()
     r.campos_dev, r.camrot_dev = campos.data_ptr(), camrot.data_ptr()
     r.raydir_dev, r.tvals_dev = raydir.data_ptr(), tvals.data_ptr()
     r.R = raydir.shape[0]
     r.D = tvals.shape[-1]
     r.tvals_per_ray = 1 if per_ray else 0
+    r.ray_cam = None if ray_cam is None else ray_cam.data_ptr()
     return r
+
+
+def camera_tables(campos, camrot, ray_cam=None):
+    """(campos, camrot) as the kernels read them: [3] / [3,3] for one camera,
+    [n_cams,3] / [n_cams,3,3] tables when ray_cam (int32 [R]) picks a camera
+    per ray (pnr_rays.ray_cam)."""
+    if ray_cam is None:
+        return campos.reshape(3).contiguous().float(), camrot.reshape(3, 3).contiguous().float()
+    return campos.reshape(-1, 3).contiguous().float(), camrot.reshape(-1, 3, 3).contiguous().float()
 
 
 class lighting_fast_querier:  # noqa: N801  (reference class name)
@@ -246,20 +256,24 @@ class lighting_fast_querier:  # noqa: N801  (reference class name)
             return self._tv_cache[key], False
         return ray_mid_t(near, far, D, R=R, jitter=jitter, device=device).contiguous(), True
 
-    def run(self, point_xyz_w, ray_dirs, cam_pos, cam_rot, near_depth, far_depth, bufs=None):
-        """Device-side query of one ray batch; returns (bufs, hp, rays, qp)."""
+    def run(self, point_xyz_w, ray_dirs, cam_pos, cam_rot, near_depth, far_depth, bufs=None, ray_cam=None):
+        """Device-side query of one ray batch; returns (bufs, hp, rays, qp).
+        ray_cam (int32 [R], optional): camera of each ray, cam_pos / cam_rot
+        then being [n_cams,3] / [n_cams,3,3] tables (a multi-frame batch)."""
         xyz = point_xyz_w.reshape(-1, 3).contiguous()
         hp = self.grid.build(self.opt, xyz)
         raydir = ray_dirs.reshape(-1, 3).contiguous().float()
-        campos = cam_pos.reshape(3).contiguous().float()
-        camrot = cam_rot.reshape(3, 3).contiguous().float()
+        campos, camrot = camera_tables(cam_pos, cam_rot, ray_cam)
         R = raydir.shape[0]
         tv, per_ray = self.tvals(near_depth, far_depth, R, raydir.device)
-        rays = make_rays(campos, camrot, raydir, tv, per_ray)
+        if ray_cam is not None:
+            ray_cam = ray_cam.to(torch.int32).contiguous()
+            assert ray_cam.shape[0] == R
+        rays = make_rays(campos, camrot, raydir, tv, per_ray, ray_cam)
         if bufs is None or not bufs.fits(R, self.opt.SR, self.opt.K):
             bufs = QueryBuffers(R, self.opt.SR, self.opt.K, raydir.device)
         qp = self.grid.query(self.opt, hp, rays, bufs)
-        bufs._keep = (raydir, campos, camrot, tv)  # keep alive for the async kernels
+        bufs._keep = (raydir, campos, camrot, tv, ray_cam)  # keep alive for the async kernels
         return bufs, hp, rays, qp
 
     def query_points(self, pixel_idx_tensor, point_xyz_pers_tensor, point_xyz_w_tensor,

@@ -172,7 +172,7 @@ class NeuralPointsRayMarching(nn.Module):
 
     @torch.no_grad()
     def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None,
-                    reuse_p1=False, sync=True):
+                    reuse_p1=False, sync=True, ray_cam=None):
         """Fused query -> aggregate -> composite for one ray batch [R,3].
         Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8).
         ``events``: optional list that receives (stage, start, end) HIP events
@@ -182,6 +182,9 @@ class NeuralPointsRayMarching(nn.Module):
         frames of one multi-GPU step), so block1.0's per-point half (P1, which
         does not depend on the camera) is taken from that call's scratch
         instead of recomputed.  The ray chunks of one call always share it.
+        ``ray_cam`` (int32 [R], optional): camera index of each ray into
+        campos [n_cams,3] / camrot [n_cams,3,3] -- several frames' rays
+        rendered as one batch (``render_views``).
 
         ``sync=False``: no host synchronisation at all.  The decoded-feature
         buffer is sized from the largest valid-sample count per ray seen so far
@@ -201,21 +204,40 @@ class NeuralPointsRayMarching(nn.Module):
         prec = self._precision_now()
         if not sync and self._sv_per_ray is not None:
             out, rec = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events,
-                                         reuse_p1, self._state, capacity=self._capacity_per_ray())
-            rec["args"] = (campos, camrot, raydir, near, far, bg_color, force_grid, reuse_p1)
+                                         reuse_p1, self._state, capacity=self._capacity_per_ray(), ray_cam=ray_cam)
+            rec["args"] = (campos, camrot, raydir, near, far, bg_color, force_grid, reuse_p1, ray_cam)
             rec["out"] = out
             self._pending.append(rec)
             return out
         n_ev = len(events) if events is not None else 0
         out, _ = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1,
-                                   self._state)
+                                   self._state, ray_cam=ray_cam)
         if prec == "fp32h2" and not self.aggregator.h2_range_ok():
             self._block_h2()
             if events is not None:
                 del events[n_ev:]
             out, _ = self._render_rays("fp32x3", campos, camrot, raydir, near, far, bg_color, force_grid, events,
-                                       False, self._state)
+                                       False, self._state, ray_cam=ray_cam)
         return out
+
+    def render_views(self, views, near, far, bg_color, force_grid=False, events=None, reuse_p1=False, sync=True):
+        """Render several frames' ray batches -- views = [(campos [3], camrot
+        [3,3], raydir [R_i,3]), ...], e.g. the N band shares one rank renders
+        per multi-GPU step -- as ONE batch: one query, one aggregate and one
+        composite launch over all of them (pnr_rays.ray_cam), so no per-call
+        cost grows with the number of views.  Returns one (ray_color, opacity,
+        is_bg, ray_mask) tuple per view (views of the batch outputs); last_counts
+        / finish() report the batch."""
+        dev = views[0][2].device
+        campos = torch.stack([v[0].reshape(3).float() for v in views]).to(dev)
+        camrot = torch.stack([v[1].reshape(3, 3).float() for v in views]).to(dev)
+        sizes = [int(v[2].shape[0]) for v in views]
+        raydir = torch.cat([v[2].reshape(-1, 3).float() for v in views]).contiguous()
+        ray_cam = torch.repeat_interleave(torch.arange(len(views), dtype=torch.int32, device=dev),
+                                          torch.tensor(sizes, device=dev), output_size=sum(sizes))
+        out = self.render_rays(campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1, sync,
+                               ray_cam=ray_cam)
+        return [tuple(t.split(sizes)[i] for t in out) for i in range(len(views))]
 
     def _precision_now(self):
         prec = self.precision
@@ -264,9 +286,10 @@ class NeuralPointsRayMarching(nn.Module):
                 for k in tot:
                     tot[k] += c[k]
             if over or (range_bad and rec["precision"] == "fp32h2"):
-                cp, cr, rd, near, far, bg, fg, reuse = rec["args"]
+                cp, cr, rd, near, far, bg, fg, reuse, rcam = rec["args"]
                 prec = "fp32x3" if rec["precision"] == "fp32h2" and range_bad else rec["precision"]
-                out, _ = self._render_rays(prec, cp, cr, rd, near, far, bg, fg, None, False, self._state)
+                out, _ = self._render_rays(prec, cp, cr, rd, near, far, bg, fg, None, False, self._state,
+                                           ray_cam=rcam)
                 for dst, src in zip(rec["out"], out):
                     dst.copy_(src)
                 tot = dict(self.last_counts)
@@ -276,7 +299,7 @@ class NeuralPointsRayMarching(nn.Module):
         return counts
 
     def _render_rays(self, precision, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1,
-                     state, capacity=None, keep=None, record=True):
+                     state, capacity=None, keep=None, record=True, ray_cam=None):
         """One render call.  capacity None: size the feature buffer from this
         batch's counts (one host sync per chunk); else capacity = valid samples
         per ray the feature buffer is sized for (no sync; the per-chunk counts
@@ -302,8 +325,10 @@ class NeuralPointsRayMarching(nn.Module):
             bg = bg.expand(C).contiguous() if bg.numel() == 1 else None
             if bg is None:
                 raise L.PnrError(f"bg_color must have 1 or {C} channels")
-        campos = campos.reshape(3).float().contiguous()
-        camrot = camrot.reshape(3, 3).float().contiguous()
+        from .querier import camera_tables
+        campos, camrot = camera_tables(campos, camrot, ray_cam)
+        if ray_cam is not None:
+            ray_cam = ray_cam.to(device=dev, dtype=torch.int32).contiguous()
         bf16 = precision == "bf16"
         mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
         mlpx = mlph = _keepx = _keeph = None
@@ -333,8 +358,9 @@ class NeuralPointsRayMarching(nn.Module):
         for ci, r0 in enumerate(range(0, R, chunk)):
             r1 = min(R, r0 + chunk)
             rd = raydir[r0:r1].contiguous()
+            rc = None if ray_cam is None else ray_cam[r0:r1]
             e0 = mark()
-            bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=state.bufs)
+            bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=state.bufs, ray_cam=rc)
             e1 = mark()
             state.bufs = bufs
             if capacity is None:
@@ -349,7 +375,7 @@ class NeuralPointsRayMarching(nn.Module):
             feat = torch.empty((max(Sv, 1), 129), **f32)
             s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
-                          bufs.fill_rs.data_ptr(), SR, K)
+                          bufs.fill_rs.data_ptr(), SR, K, L.ptr(rc))
             e2 = mark()
             scratch, ready = self._agg_scratch(state, max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
             pts.p1_ready = int(ready)

@@ -142,3 +142,49 @@ def test_two_rank_frame_shards_gather_every_frame():
             full = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"])
             want = np.concatenate([full["coarse_raycolor"], full["coarse_is_background"]], 1)
             np.testing.assert_allclose(got[r], want, atol=1e-5, rtol=1e-5)
+
+
+def _step_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests"), os.path.join(root, "tests", "golden")]
+    import torch.distributed as dist
+    from pointnerf_amd.parallel import StepShard, TileShard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    params = formula_params(salt=0.4)
+    scs = [scene(8000, H=24, W=24, theta=60.0 + 90.0 * f) for f in range(world)]
+    st = StepShard([TileShard(24, 24, rank, world, f) for f in range(world)])
+    rd = st.select([torch.from_numpy(sc["raydir"]) for sc in scs]).numpy()
+    cam = st.ray_cam.numpy()
+    rows = []
+    for f, sc in enumerate(scs):   # the oracle renders each camera's rows of the one batch
+        r = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], rd[cam == f], sc["bg"])
+        rows.append(np.concatenate([r["coarse_raycolor"], r["coarse_is_background"]], 1))
+    local = torch.from_numpy(np.concatenate(rows))
+    q.put((rank, [t.numpy() for t in st.assemble_async(local).wait()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_step_shard_one_gather_assembles_every_frame():
+    """StepShard (bench --shard tiles): each rank's band shares of the step's
+    frames form ONE batch (frame order, ray_cam = frame) and ONE all-gather
+    assembles every frame on every rank, equal to single-process renders."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    params = formula_params(salt=0.4)
+    for f in range(2):
+        sc = scene(8000, H=24, W=24, theta=60.0 + 90.0 * f)
+        full = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"])
+        want = np.concatenate([full["coarse_raycolor"], full["coarse_is_background"]], 1)
+        for r in range(2):
+            np.testing.assert_allclose(got[r][f], want, atol=1e-5, rtol=1e-5)

@@ -51,6 +51,20 @@ def _worker(rank, world, port, precision, layout, q):
     bg = torch.from_numpy(sc["bg"]).to(cuda)
     outs = []
     handles = []
+    if layout == "batch":   # bench --shard tiles: the step's band shares as ONE multi-camera batch
+        from pointnerf_amd.parallel import StepShard
+        scs = [scene(20000, H=H, W=W, theta=th) for th in THETAS]
+        st = StepShard([TileShard(H, W, rank, world, f, cuda) for f in range(len(THETAS))], cuda)
+        rd = st.select([torch.from_numpy(x["raydir"]).to(cuda) for x in scs]).contiguous()
+        cp = torch.stack([torch.from_numpy(x["campos"]).to(cuda) for x in scs])
+        cr = torch.stack([torch.from_numpy(x["camrot"]).to(cuda) for x in scs])
+        m.render_rays(cp, cr, rd, 2.0, 6.0, bg, ray_cam=st.ray_cam)
+        color = m.render_rays(cp, cr, rd, 2.0, 6.0, bg, sync=False, ray_cam=st.ray_cam)[0]
+        m.finish()
+        q.put((rank, [t.numpy() for t in st.assemble_async(color.cpu()).wait()]))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     for f, th in enumerate(THETAS):
         s2 = scene(20000, H=H, W=W, theta=th)
         cp, cr, rd = (torch.from_numpy(s2[k]).to(cuda) for k in ("campos", "camrot", "raydir"))
@@ -67,7 +81,7 @@ def _worker(rank, world, port, precision, layout, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["bands", "tiles16"])
+@pytest.mark.parametrize("layout", ["bands", "tiles16", "batch"])
 def test_two_rank_libpnr_render_assembles_frames(cuda, layout):
     precision = "fp32h2"
     ctx = mp.get_context("spawn")

@@ -96,3 +96,30 @@ def test_render_graph_flags_overflow(cuda):
     g = RenderGraph(m, cp, cr, rd, 2.0, 6.0, bg, margin=0.5)
     g.replay()
     assert not g.check()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "fp32h2", "bf16"])
+def test_render_views_one_batch_equals_per_view(cuda, precision):
+    """render_views: several cameras' ray batches (the band shares of one
+    multi-GPU step) in ONE query / aggregate / composite launch (per-ray
+    camera index) give the per-camera renders: bitwise on the split paths
+    (fp32x3 / fp32h2, the headline); the native-fp32 and bf16 pair kernels sum
+    a tile's colour features in a tile-position-dependent order (measured
+    <= 6e-8 / 4e-7), so there within 1e-6, with identical ray masks."""
+    sc, cams = _cams(cuda, thetas=(30.0, 150.0, 260.0))
+    m = _renderer(sc, cuda, formula_params(salt=0.9))
+    m.precision = precision
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    views = [(cp, cr, rd[i::3].contiguous()) for i, (cp, cr, rd) in enumerate(cams)]
+    want = [[t.clone() for t in m.render_rays(cp, cr, rd, 2.0, 6.0, bg)] for cp, cr, rd in views]
+    got = m.render_views(views, 2.0, 6.0, bg)
+    got2 = m.render_views(views, 2.0, 6.0, bg, sync=False)
+    m.finish()
+    for res in (got, got2):
+        for w, g in zip(want, res):
+            if precision in ("fp32x3", "fp32h2"):
+                assert _eq(w, g)
+            else:
+                assert torch.equal(w[3], g[3])
+                for x, y in zip(w[:3], g[:3]):
+                    assert float((x - y).abs().max()) <= 1e-6
