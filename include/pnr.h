@@ -38,6 +38,8 @@
  *                           models/rendering/diff_ray_marching.py:509-555
  *   pnr_ray_march_fwd    <- ray_march on dense [B,R,SR,C+1] features
  *                           models/rendering/diff_ray_marching.py:509-555
+ *   pnr_vox_closest      <- construct_vox_points_closest (point-cloud init down-sampling)
+ *                           models/mvs/mvs_utils.py:537-561
  *   pnr_rgb_head_fwd/bwd <- the upstream colour head the fork commented out:
  *                           color_branch Linear(128,3) + raw2out_color
  *                           models/aggregators/point_aggregators.py:343, 269-273, 637-638
@@ -500,6 +502,22 @@ int pnr_rgb_head_fwd(const float* feat, int64_t ld, const int32_t* n_dev, int64_
 int pnr_rgb_head_bwd(const float* d_out, const float* feat, int64_t ld, const int32_t* n_dev, int64_t n_max,
                      const float* w, const float* b, int32_t act_super, float* d_feat, float* d_wb,
                      void* stream);
+
+/* ------------------------------------------------- point-cloud initialisation
+ * construct_vox_points_closest(xyz, vox_res) (models/mvs/mvs_utils.py:537-561,
+ * space_min = None: the form every reference driver calls, train_ddp.py:135):
+ * the cube of edge max(max - min) * 1.05 around the points' bbox centre cut in
+ * vox_res^3 voxels (torch's fp32 op order), the occupied voxels in
+ * lexicographic (x, y, z) order (torch.unique(dim=0)).  For voxel v < counts[0]:
+ * grid_idx[v,3] its cell, centroid[v,3] = mean of its points (summed in ascending
+ * point order, scatter_mean), min_idx[v] = its point closest to the centroid
+ * (scatter_min; ties to the smallest index).  inv_idx[N] (may be NULL) = voxel
+ * of every point.  Outputs sized for N voxels; counts[0] = voxels, counts[1] = 1
+ * when a cell coordinate left +-2^20 (outputs invalid).  No host sync. */
+int pnr_vox_closest_scratch_bytes(int64_t n, size_t* out);
+int pnr_vox_closest(const float* xyz_dev, int64_t n, int32_t vox_res, float* centroid, int32_t* grid_idx,
+                    int64_t* min_idx, int32_t* inv_idx, int32_t* counts, void* scratch, size_t scratch_bytes,
+                    void* stream);
 
 /* ------------------------------------------------------------- utilities */
 /* Exclusive scan of n int32 values (n_dev: optional device-side length <= n,

@@ -167,6 +167,9 @@ SIGNATURES = {
                                  c_void_p]),
     "pnr_rgb_head_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32,
                                  c_void_p, c_void_p, c_void_p]),
+    "pnr_vox_closest_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
+    "pnr_vox_closest": (c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_size_t, c_void_p]),
     "pnr_scan_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
     "pnr_exclusive_scan_i32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),

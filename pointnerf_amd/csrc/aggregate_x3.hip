@@ -503,7 +503,13 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
   }
   float pw3[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, col[3] = {0.f, 0.f, 0.f}, pdir[3] = {0.f, 0.f, 0.f};
   float cf = 1.f;
-  if (valid) {
+  if (valid && (PNR_ABLATE & 4096)) {   // timing only: no point-table loads
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      pw3[a] = sw[a] + 0.01f * (a + 1);
+      pp[a] = sp[a] + 0.01f;
+    }
+  } else if (valid) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       pw3[a] = A.pts.xyz[prow * 3 + a];

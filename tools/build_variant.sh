@@ -10,7 +10,7 @@ objs=""
 for f in pointnerf_amd/csrc/*.hip; do
   b=$(basename $f .hip)
   extra=""
-  if [ "$b" = query ] || [ "$b" = grid ]; then extra="-ffp-contract=off"; fi
+  if [ "$b" = query ] || [ "$b" = grid ] || [ "$b" = voxelize ]; then extra="-ffp-contract=off"; fi
   if [ "$b" = aggregate_x3 ]; then extra="-fno-slp-vectorize"; fi
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -munsafe-fp-atomics -Iinclude $extra $D \
     -c $f -o tools/_ablate/$N/$b.o &
