@@ -92,7 +92,9 @@ def build_scene(args, device):
     emb, color, dirs, conf = S.point_features(args.points, seed=0, default_conf=opt.default_conf)
     torch.manual_seed(0)
     agg = PointAggregator(opt).to(device).eval()   # random-init weights (xavier, networks.py:163-172)
-    np_ = NeuralPoints(opt, device, torch.from_numpy(pts), emb, color, dirs, conf)
+    # bf16 (config c5): the embedding table itself in bf16 (104 B per point)
+    emb_dtype = torch.bfloat16 if getattr(args, "dtype", "fp32h2") == "bf16" else torch.float32
+    np_ = NeuralPoints(opt, device, torch.from_numpy(pts), emb, color, dirs, conf, emb_dtype=emb_dtype)
     model = NeuralPointsRayMarching(opt, np_, agg)
     return opt, pts, (emb, color, dirs, conf), agg, model
 
@@ -498,6 +500,7 @@ def main():
             "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "grid_rebuild_per_step": not args.no_grid_rebuild,
+                       "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else
                                        f"dp{world} ({args.tile_layout} ray shards of every frame, one multi-camera "

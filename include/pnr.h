@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 7
+#define PNR_ABI_VERSION 8
 
 enum {
   PNR_OK = 0,
@@ -230,6 +230,10 @@ typedef struct {
                            the same emb / used rows / block1.0, e.g. the other ray
                            batches of one step), so the per-point pass is skipped.
                            Camera-independent.  0 = compute it (always safe).     */
+  const uint16_t* emb_bf16; /* [N,32] bf16 embedding table (SURVEY config c5: 104 B per
+                           point instead of 168), read instead of emb by
+                           pnr_aggregate_fwd_bf16 when set (emb may then be NULL);
+                           the fp32 paths ignore it                                  */
 } pnr_points;
 
 typedef struct {

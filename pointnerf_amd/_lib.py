@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class PnrError(RuntimeError):
@@ -79,7 +79,7 @@ class Points(ctypes.Structure):
     _fields_ = [("n", c_int64), ("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
                 ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p),
                 ("used", c_void_p), ("n_used", c_int64), ("used_map", c_void_p),
-                ("p1_ready", c_int32)]
+                ("p1_ready", c_int32), ("emb_bf16", c_void_p)]
 
 
 class Samples(ctypes.Structure):

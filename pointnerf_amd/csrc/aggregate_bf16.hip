@@ -147,11 +147,24 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
       const bool act = pt < np;
       const int64_t prow = act ? (A.pts.used ? (int64_t)A.pts.used[pt] : pt) : 0;
       const float* e = A.pts.emb + prow * kEmb + 16 * half;
+      const uint2* eb = reinterpret_cast<const uint2*>(A.pts.emb_bf16 + prow * kEmb + 16 * half);
       uint16_t* xc = Xb + col * kPB;
 #pragma unroll 2
       for (int q = 0; q < 4; ++q) {
-        const float4 e4 = act ? reinterpret_cast<const float4*>(e)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+        float ev[4] = {0.f, 0.f, 0.f, 0.f};
+        if (act && A.pts.emb_bf16) {   // bf16 table (config c5): 8 B per 4 channels
+          const uint2 b = eb[q];
+          ev[0] = __uint_as_float(b.x << 16);
+          ev[1] = __uint_as_float(b.x & 0xffff0000u);
+          ev[2] = __uint_as_float(b.y << 16);
+          ev[3] = __uint_as_float(b.y & 0xffff0000u);
+        } else if (act) {
+          const float4 e4 = reinterpret_cast<const float4*>(e)[q];
+          ev[0] = e4.x;
+          ev[1] = e4.y;
+          ev[2] = e4.z;
+          ev[3] = e4.w;
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int ch = 16 * half + 4 * q + u;
@@ -583,13 +596,14 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
                                       float* out_feat, float* out_weight, float* out_conf, void* scratch,
                                       size_t scratch_bytes, void* stream) {
   PNR_CHECK_ARG(pts && s && w && out_feat, "aggregate_bf16: null pointer");
-  PNR_CHECK_ARG(pts->xyz && pts->emb && s->pidx, "aggregate_bf16: point xyz/emb and pidx required");
+  PNR_CHECK_ARG(pts->xyz && (pts->emb || pts->emb_bf16) && s->pidx, "aggregate_bf16: point xyz/emb and pidx required");
   PNR_CHECK_ARG(s->sample_w && s->sample_p && s->dirs && s->dir_div >= 1, "aggregate_bf16: sample arrays required");
   PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate_bf16: K=%d unsupported (1..8)", s->K);
   PNR_CHECK_ARG(w->w1af && w->w1bf && w->w2f && w->w3f && w->w4f && w->wa && w->ba && w->wc1f && w->wc2f && w->wc3f,
                 "aggregate_bf16: null weight");
-  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
-                "aggregate_bf16: emb and scratch must be 16-B aligned");
+  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0 && ((uintptr_t)pts->emb_bf16 & 7) == 0 &&
+                    ((uintptr_t)scratch & 15) == 0,
+                "aggregate_bf16: emb (16 B), emb_bf16 (8 B) and scratch (16 B) must be aligned");
   PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_bf16: need pers or camera");
   PNR_CHECK_ARG(!pts->used || pts->used_map, "aggregate_bf16: used list needs used_map");
   const int64_t n_p1 = pts->used ? pts->n_used : pts->n;

@@ -29,8 +29,15 @@ class NeuralPoints(nn.Module):
     """Point table of neural_points.NeuralPoints (world-coordinate querier)."""
 
     def __init__(self, opt, device, xyz=None, embedding=None, color=None, dirs=None, conf=None,
-                 Rw2c=None):
+                 Rw2c=None, emb_dtype=torch.float32):
+        """emb_dtype torch.bfloat16 stores points_embeding in bf16 (SURVEY config
+        c5: 104 B per point instead of 168; the bf16 render path reads it
+        directly, the fp32 paths from an fp32 copy; training needs fp32)."""
         super().__init__()
+        if emb_dtype not in (torch.float32, torch.bfloat16):
+            raise L.PnrError(f"emb_dtype {emb_dtype}: float32 or bfloat16")
+        self.emb_dtype = emb_dtype
+        self._emb32 = (None, None)
         self.opt = opt
         if getattr(opt, "xyz_grad", 0) > 0:
             raise L.PnrError("xyz_grad > 0 (point-position gradients, neural_points.py:270) is not "
@@ -55,20 +62,45 @@ class NeuralPoints(nn.Module):
                              "implemented by libpnr's backward; run with --xyz_grad 0")
         dev = self.device
         self.xyz = nn.Parameter(xyz.to(dev).float().reshape(-1, 3).contiguous(), requires_grad=False)
-        self.points_embeding = nn.Parameter(embedding.to(dev).float().reshape(1, -1, 32).contiguous())
+        self.points_embeding = nn.Parameter(embedding.to(dev).to(self.emb_dtype).reshape(1, -1, 32).contiguous())
         self.points_color = None if color is None else nn.Parameter(color.to(dev).float().reshape(1, -1, 3).contiguous())
         self.points_dir = None if dirs is None else nn.Parameter(dirs.to(dev).float().reshape(1, -1, 3).contiguous())
         self.points_conf = None if conf is None else nn.Parameter(conf.to(dev).float().reshape(1, -1, 1).contiguous())
         self.Rw2c = torch.eye(3, device=dev) if Rw2c is None else Rw2c.to(dev).float()
 
-    def tables(self, campos=None, camrot=None) -> tuple[L.Points, tuple]:
-        keep = (self.xyz.detach().contiguous(), self.points_embeding.detach().reshape(-1, 32).contiguous(),
+    def embedding_fp32(self) -> torch.Tensor:
+        """points_embeding as fp32 [N,32] (the table itself, or a copy of the bf16
+        table cached on its storage and version)."""
+        e = self.points_embeding.detach().reshape(-1, 32)
+        if e.dtype == torch.float32:
+            return e.contiguous()
+        key = (e.data_ptr(), self.points_embeding._version, e.shape[0])
+        if self._emb32[0] != key:
+            self._emb32 = (key, e.float().contiguous())
+        return self._emb32[1]
+
+    def tables(self, campos=None, camrot=None, bf16: bool = False) -> tuple[L.Points, tuple]:
+        """pnr_points of the table; bf16 (the bf16 aggregate) passes a bf16
+        embedding table as emb_bf16 instead of an fp32 one."""
+        e = self.points_embeding.detach().reshape(-1, 32)
+        use_b = bf16 and e.dtype == torch.bfloat16
+        keep = (self.xyz.detach().contiguous(), None if use_b else self.embedding_fp32(),
                 None if self.points_color is None else self.points_color.detach().reshape(-1, 3).contiguous(),
                 None if self.points_dir is None else self.points_dir.detach().reshape(-1, 3).contiguous(),
-                None if self.points_conf is None else self.points_conf.detach().reshape(-1).contiguous())
-        p = L.Points(keep[0].shape[0], keep[0].data_ptr(), None, keep[1].data_ptr(), L.ptr(keep[2]), L.ptr(keep[3]),
+                None if self.points_conf is None else self.points_conf.detach().reshape(-1).contiguous(),
+                e.contiguous() if use_b else None)
+        p = L.Points(keep[0].shape[0], keep[0].data_ptr(), None, L.ptr(keep[1]), L.ptr(keep[2]), L.ptr(keep[3]),
                      L.ptr(keep[4]), L.ptr(campos), L.ptr(camrot))
+        p.emb_bf16 = L.ptr(keep[5])
         return p, keep
+
+    def bytes_per_point(self) -> int:
+        """HBM bytes of one point's parameters (168 fp32, 104 with a bf16 embedding)."""
+        b = 12 + 32 * self.points_embeding.element_size()
+        for t, c in ((self.points_color, 3), (self.points_dir, 3), (self.points_conf, 1)):
+            if t is not None:
+                b += c * t.element_size()
+        return b
 
     def w2pers(self, point_xyz, camrotc2w, campos):
         """neural_points.py:687-693."""
@@ -91,7 +123,7 @@ class NeuralPoints(nn.Module):
         mask = sample_pidx >= 0
         B, R, SR, K = sample_pidx.shape
         idx = torch.clamp(sample_pidx, min=0).view(-1).long()
-        cat = torch.cat([self.xyz[None, ...], pers, self.points_embeding], dim=-1)
+        cat = torch.cat([self.xyz[None, ...], pers, self.points_embeding.float()], dim=-1)
         g = torch.index_select(cat, 1, idx).view(B, R, SR, K, cat.shape[-1])
 
         def sel(t, c):
@@ -338,7 +370,7 @@ class NeuralPointsRayMarching(nn.Module):
             mlph, _keeph = self.aggregator.packed_h2()
         if keep is not None:   # RenderGraph: the captured launches point into these packs
             keep += [mlp, _keepw, mlpx, _keepx, mlph, _keeph]
-        pts, _keepp = np_.tables(campos, camrot)
+        pts, _keepp = np_.tables(campos, camrot, bf16=bf16)
         totals = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
         chunk = max(1, self.chunk_rays or R)
         n_chunks = max(1, -(-R // chunk))
@@ -455,6 +487,8 @@ class NeuralPointsRayMarching(nn.Module):
         [R,C] (requires grad w.r.t. points_embeding / color / dir / conf and the
         aggregator parameters), opacity [R,SR], is_bg [R], ray_mask [R]."""
         from .train import AggregateFn, AggSpec, CompositeFn, CompositeSpec, agg_params
+        if self.neural_points.points_embeding.dtype != torch.float32:
+            raise L.PnrError("training needs an fp32 points_embeding (NeuralPoints(emb_dtype=torch.float32))")
         self._sync_rw2c()
         opt = self.opt
         dev = raydir.device

@@ -41,13 +41,14 @@ def _oracle_query(name, n, H, view=1):
                           near=sc["near"], far=sc["far"])
 
 
-def _model(sc, cuda, params, precision="fp32", train=False):
+def _model(sc, cuda, params, precision="fp32", train=False, emb_dtype=torch.float32):
     from pointnerf_amd.aggregator import PointAggregator
     from pointnerf_amd.renderer import NeuralPoints, NeuralPointsRayMarching
     agg = PointAggregator(sc["opt"]).to(cuda)
     agg.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
-                       torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]))
+                       torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]),
+                       emb_dtype=emb_dtype)
     return NeuralPointsRayMarching(sc["opt"], np_, agg.train() if train else agg.eval(), precision=precision)
 
 
@@ -144,15 +145,27 @@ def test_flagset_render_vs_oracle(cuda, name, precision):
     assert getattr(m, "h2_fallbacks", 0) == 0
 
 
-def test_c5_truck_bf16_vs_oracle(cuda):
-    """c5: bf16 point features + bf16 MFMA MLP at truck flags -- same query
-    (bit-exact ray mask), image within 40 dB PSNR of the fp32 oracle."""
+@pytest.mark.parametrize("emb_dtype", [torch.float32, torch.bfloat16])
+def test_c5_truck_bf16_vs_oracle(cuda, emb_dtype):
+    """c5: bf16 point features (the embedding table itself stored in bf16:
+    104 B per point) + bf16 MFMA MLP at truck flags -- same query (bit-exact
+    ray mask), image within 40 dB PSNR of the fp32 oracle; the fp32 paths
+    render a bf16 table from its fp32 copy."""
     sc = _flag_scene("truck", DENSE["truck"], 48)
     params = formula_params(salt=0.35)
-    got = _render(_model(sc, cuda, params, "bf16"), sc, cuda)
+    m = _model(sc, cuda, params, "bf16", emb_dtype=emb_dtype)
+    assert m.neural_points.bytes_per_point() == (104 if emb_dtype == torch.bfloat16 else 168)
+    got = _render(m, sc, cuda)
     ref = O.render(sc["opt"], oracle_points(sc), params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"],
                    q=_oracle_query("truck", DENSE["truck"], 48))
     _check_render(got, ref, min_psnr=40.0, tol=False)
+    if emb_dtype == torch.bfloat16:   # fp32 path on the same bf16 table = the oracle on bf16-rounded embeddings
+        m.precision = "fp32"
+        got32 = _render(m, sc, cuda)
+        pts = dict(oracle_points(sc), emb=torch.from_numpy(sc["emb"]).bfloat16().float().numpy())
+        ref32 = O.render(sc["opt"], pts, params, sc["campos"], sc["camrot"], sc["raydir"], sc["bg"],
+                         q=_oracle_query("truck", DENSE["truck"], 48))
+        _check_render(got32, ref32)
 
 
 # ------------------------------------------------------------------------- c1
