@@ -13,7 +13,8 @@ from .aggregator import PointAggregator, frag_pack, frag_unpack  # noqa: F401
 from .options import lego_opt  # noqa: F401
 from .querier import lighting_fast_querier, ray_mid_t, hyperparameters_from_bbox  # noqa: F401
 from .ray_march import ray_march, radiance_render, alpha_blend, no_tone_map  # noqa: F401
-from .renderer import NeuralPoints, NeuralPointsRayMarching  # noqa: F401
+from .renderer import NeuralPoints, NeuralPointsRayMarching, RenderGraph  # noqa: F401
+from .voxelize import construct_vox_points_closest  # noqa: F401
 from .neural_render import NeuralRenderer  # noqa: F401
 from .checkpoint import load_ray_marching, save_ray_marching, prune, grow_points  # noqa: F401
 from .aggregator import frag_pack_bf16  # noqa: F401
