@@ -1036,454 +1036,6 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_pairs_h2 with skewed streams (PNR_H2_SKEW, the default for h2).  Each
-// consumer wave runs its two neuron tiles T0 = 2w and T1 = 2w + 1 as two MFMA
-// streams, T1 half a layer behind T0, every layer's k-steps in E/O order: first
-// the rows of the E tiles (0, 2, 4, 6: every wave's T0 output), then the O rows
-// (T1's).  When T0 finishes a layer its activation store (lrelu + f16 split +
-// LDS writes: VALU) runs in the MFMA gaps of T1's last half, and T1's store in
-// the gaps of T0's first half of the next layer, which reads only E rows -- the
-// MFMA pipe no longer idles through a store phase (the in-order version spent
-// 9.6 k of 41.8 k cycles per tile there).  Per layer transition 3 barriers:
-//   B0  every T1 stream is past the E rows (the T0 stores may overwrite them)
-//   B1  every T0 store is visible (T0 starts the next layer on the E rows)
-//   B2  every T1 store is visible (the O rows of the next layer are readable)
-// The k-order changes the fp32 accumulation order (not the arithmetic).
-#ifndef PNR_H2_SKEW
-#define PNR_H2_SKEW 0   // measured 1-2 % slower than the in-order kernel: off
-#endif
-
-__device__ __forceinline__ constexpr int kord_eo(int t, int ns) {   // local step -> k-step
-  return t >= ns ? t : (t < 8 ? 4 * (t >> 1) + (t & 1) : (t < 16 ? 4 * ((t - 8) >> 1) + 2 + (t & 1) : 16));
-}
-__device__ __forceinline__ constexpr int kstep(int t, int ns, bool eo) { return eo ? kord_eo(t, ns) : t; }
-
-struct SStream {
-  uint4 w[3][2];      // weight ring [local step mod 3][Wh, Wl]
-  uint4 b[2][2][2];   // B fragments [local step mod 2][pair half][hi, lo]
-  uint4 ws;           // 2^11 Wh of the next step (made in registers)
-};
-
-template <int T>
-__device__ __forceinline__ void s_wload(SStream& S, int slot, __amdgpu_buffer_rsrc_t rs, int voff, int kt) {
-#pragma unroll
-  for (int pl = 0; pl < 2; ++pl)
-    S.w[slot][pl] =
-        __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + pl * 1024, (kt * 8 + T) * 2 * 1024, 0));
-}
-__device__ __forceinline__ void s_bload(SStream& S, int slot, const char* base, int pstride, int kt) {
-#pragma unroll
-  for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
-      S.b[slot][pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * kt * kXT + 32 * pt) * 16);
-}
-// weights of local steps 0..2 (issued early: they travel during a store / barrier)
-template <int T>
-__device__ __forceinline__ void s_wprime(SStream& S, __amdgpu_buffer_rsrc_t rs, int voff, int ns, bool eo) {
-#pragma unroll
-  for (int d = 0; d < 3; ++d) s_wload<T>(S, d, rs, voff, kstep(d, ns, eo));
-}
-// B of local steps 0, 1 and Ws of step 0 (after the barrier that publishes the layer input)
-__device__ __forceinline__ void s_start(SStream& S, const char* base, int pstride, int ns, bool eo) {
-  s_bload(S, 0, base, pstride, kstep(0, ns, eo));
-  s_bload(S, 1, base, pstride, kstep(1 < ns ? 1 : 0, ns, eo));
-  S.ws = f16x8_scale2048(S.w[0][0]);
-}
-// B of local steps t, t + 1 again: the prefetch of a stream's next steps can
-// cross a barrier that only then publishes their rows (T0's O rows after B2)
-__device__ __forceinline__ void s_rebload(SStream& S, const char* base, int pstride, int t, int ns, bool eo) {
-  s_bload(S, t & 1, base, pstride, kstep(t, ns, eo));
-  s_bload(S, (t + 1) & 1, base, pstride, kstep(t + 1 < ns ? t + 1 : ns - 1, ns, eo));
-}
-// MFMA i (0..5) of local step t: Ws.Xh, Ws.Xh, Wl.Xh, Wl.Xh, Wh.Xl, Wh.Xl over the two pair halves
-template <int T>
-__device__ __forceinline__ void s_mfma(f32x16 (&acc)[4], const SStream& S, int t, int i) {
-  const int pt = i & 1, sl = t % 3, bs = t & 1;
-  const uint4& a = i < 2 ? S.ws : (i < 4 ? S.w[sl][1] : S.w[sl][0]);
-  acc[2 * pt + T] = mfma_f16(a, S.b[bs][pt][i < 4 ? 0 : 1], acc[2 * pt + T]);
-}
-// The refills of local step t, spread over its MFMA gaps (after MFMA i) so the
-// loads never come in a burst and each lands >= 1.5 steps before its use:
-//   i = 0: lo B planes of step t + 1 (slot of step t - 1: its last reader was MFMA 5)
-//   i = 3: hi B planes of step t + 2 and Wl of step t + 3 into t's slots
-//   i = 4: Ws of step t + 1 = 2^11 Wh (loaded two steps ago)
-//   i = 5: Wh of step t + 3 into t's slot
-template <int T>
-__device__ __forceinline__ void s_gap(SStream& S, __amdgpu_buffer_rsrc_t rs, int voff, const char* base,
-                                      int pstride, int t, int ns, bool eo, int i) {
-  auto bplane = [&](int tb, int pl) {
-    tb = tb < ns ? tb : ns - 1;
-    const int kb = kstep(tb, ns, eo);
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-      S.b[tb & 1][pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * kb * kXT + 32 * pt) * 16);
-  };
-  auto wplane = [&](int wp) {   // packs carry >= 3 zero steps
-    S.w[t % 3][wp] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rs, voff + wp * 1024, (kstep(t + 3, ns, eo) * 8 + T) * 2 * 1024, 0));
-  };
-  if (i == 0 && t + 1 < ns) bplane(t + 1, 1);
-  if (i == 3) {
-    if (t + 2 < ns) bplane(t + 2, 0);
-    wplane(1);
-  }
-  if (i == 4) S.ws = f16x8_scale2048(S.w[(t + 1) % 3][0]);
-  if (i == 5) wplane(0);
-}
-
-// stream T alone, local steps [t0, t0 + N); fill(j, i) runs in the gap after MFMA i of step j
-template <int T, int N, typename F>
-__device__ __forceinline__ void s_run(f32x16 (&acc)[4], SStream& S, __amdgpu_buffer_rsrc_t rs, int voff,
-                                      const char* base, int pstride, int t0, int ns, bool eo, F&& fill) {
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      s_mfma<T>(acc, S, t0 + j, i);
-      __builtin_amdgcn_sched_barrier(0);
-      s_gap<T>(S, rs, voff, base, pstride, t0 + j, ns, eo, i);
-      fill(j, i);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-// both streams, N steps each (T0 from t0, T1 from t1), MFMAs alternating
-template <int N>
-__device__ __forceinline__ void s_run2(f32x16 (&acc)[4], SStream& S0, SStream& S1, __amdgpu_buffer_rsrc_t rs0,
-                                       __amdgpu_buffer_rsrc_t rs1, int voff, const char* base, int pstride, int t0,
-                                       int ns0, bool eo0, int t1, int ns1, bool eo1) {
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      s_mfma<0>(acc, S0, t0 + j, i);
-      __builtin_amdgcn_sched_barrier(0);
-      s_gap<0>(S0, rs0, voff, base, pstride, t0 + j, ns0, eo0, i);
-      __builtin_amdgcn_sched_barrier(0);
-      s_mfma<1>(acc, S1, t1 + j, i);
-      __builtin_amdgcn_sched_barrier(0);
-      s_gap<1>(S1, rs1, voff, base, pstride, t1 + j, ns1, eo1, i);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-
-// One eighth (pair half pt = u / 4, quad q = u % 4) of neuron tile Ts's
-// activation store (store_act's arithmetic, bit-identical), in five parts of
-// <= 6 single-issue VALU / LDS ops, one per MFMA gap: an MFMA leaves ~24 of
-// its 32 cycles to other instructions of the same wave, so bigger fills delay
-// the next MFMA instead of hiding (MI355X_MICROARCH, "price of one filler").
-struct StorePart {
-  float y0, y1;
-  unsigned a0, a1, b0, b1;
-};
-__device__ __forceinline__ void split_y(float y0, float y1, unsigned& hi, unsigned& lo) {
-  asm volatile(
-      "v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
-      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
-      "v_fma_mixlo_f16 %1, %0, %5, %2 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %1, %0, %5, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-      : "=&v"(hi), "=&v"(lo)
-      : "v"(y0), "v"(y1), "s"(0x1p-11f), "s"(-2048.f));
-}
-template <int Ts>
-__device__ __forceinline__ void store_part(const f32x16 (&acc)[4], StorePart& p, char* planes, float k, float ks,
-                                           int lane, int T0, int u, int part) {
-  const int pt = u >> 2, q = u & 3, c = lane & 31, h = lane >> 5;
-  const f32x16& v = acc[2 * pt + Ts];
-  if (PNR_ABLATE & 8192) return;   // timing only: no activation stores
-  if (part == 0 || part == 2) {      // Y = 2^11 lrelu(x mul) = max(x k, x ks)
-    const int r = 4 * q + part;
-    p.y0 = fmaxf(v[r] * k, v[r] * ks);
-    p.y1 = fmaxf(v[r + 1] * k, v[r + 1] * ks);
-  }
-  if (part == 1) split_y(p.y0, p.y1, p.a0, p.a1);
-  if (part == 3) split_y(p.y0, p.y1, p.b0, p.b1);
-  if (part == 4) {
-    char* d = planes + ((4 * (T0 + Ts) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
-    *reinterpret_cast<uint2*>(d) = make_uint2(p.a0, p.b0);
-    *reinterpret_cast<uint2*>(d + kPlaneX) = make_uint2(p.a1, p.b1);
-  }
-}
-// the 40 parts of one tile's store over the 48 MFMA gaps of an 8-step phase:
-// step j, gap i -> part (unit j, part PART_OF[i]) with gaps 4 left to the Ws scaling
-__device__ __forceinline__ constexpr int store_slot(int i) { return i == 1 ? 0 : i == 2 ? 1 : i == 3 ? 2 : i == 5 ? 3 : i == 0 ? 4 : -1; }
-
-// one eighth of tile Ts's block3.2 accumulators -> the H4 park (the producers' tail)
-template <int Ts>
-__device__ __forceinline__ void park_part(const f32x16 (&acc)[4], float* H4, int lane, int T0, int u) {
-  const int pt = u >> 2, q = u & 3, c = lane & 31, h = lane >> 5;
-  const f32x16& v = acc[2 * pt + Ts];
-  *reinterpret_cast<float4*>(H4 + (32 * pt + c) * kP1Pitch + 32 * (T0 + Ts) + 8 * q + 4 * h) =
-      make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-}
-// acc of neuron tile Ts for a layer that starts from its bias (b / scale) or from 0
-template <int Ts>
-__device__ __forceinline__ void acc_start(f32x16 (&acc)[4], const float* bias, float inv_scale, int lane, int T0) {
-  const int h = lane >> 5;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (bias) {
-      const float4 b = *reinterpret_cast<const float4*>(bias + 32 * (T0 + Ts) + 8 * q + 4 * h);
-      v[0] = b.x * inv_scale;
-      v[1] = b.y * inv_scale;
-      v[2] = b.z * inv_scale;
-      v[3] = b.w * inv_scale;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[Ts][4 * q + i] = v[i];
-      acc[2 + Ts][4 * q + i] = v[i];
-    }
-  }
-}
-
-__device__ __forceinline__ void consumer_loop_s(const X3Args& A, char* lds, int wid, int lane) {
-  using L = XL<true>;
-  const int c = lane & 31, h = lane >> 5;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, kXTS);
-  const float neg = A.w.neg_slope;
-  char* XP = lds;
-  const float* P1L = reinterpret_cast<const float*>(lds);
-  float* H4 = reinterpret_cast<float*>(lds + L::OffH4);
-  const int T0 = 2 * wid;
-  const int voff = (T0 * 2 * 64 + lane) * 16;
-  const __amdgpu_buffer_rsrc_t r1 = rsrc(A.wx.pack[0]), r2 = rsrc(A.wx.pack[1]), r3 = rsrc(A.wx.pack[2]),
-                               r4 = rsrc(A.wx.pack[3]);
-  const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
-  const char* bX = XP + (h * kXT + c) * 16;                // B base: layer-input planes
-  const char* bP = lds + L::OffPE + (h * kXT + c) * 16;     // B base: PE planes
-  const float k2 = 2048.f * sc2, ks2 = k2 * neg, k3 = 2048.f * sc3, ks3 = k3 * neg;
-  auto none = [](int, int) {};
-  SStream S0, S1;
-  f32x16 acc[4];
-  s_wprime<0>(S0, r1, voff, 4, false);
-  s_wprime<1>(S1, r1, voff, 4, false);
-  X3_SYNC();   // S0: the first tile's PE planes, extras and weights are in LDS
-  const int* TQ = reinterpret_cast<const int*>(lds + L::OffTq);
-  int it = 0;
-  for (int64_t tile = first_tile(ntiles); tile < ntiles; tile = TQ[(it + 1) & 3], ++it) {
-    const int buf = it & 1;
-    X3_TR(0, 0);
-    // ------------------------------------------------ block1.0 distance half: both streams
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
-    s_start(S0, bP, kPlaneP, 4, false);
-    s_start(S1, bP, kPlaneP, 4, false);
-    s_run2<4>(acc, S0, S1, r1, r1, voff, bP, kPlaneP, 0, 4, false, 0, 4, false);
-    s_wprime<0>(S0, r2, voff, 16, true);
-    X3_TR(0, 1);
-    X3_SYNC();   // S1: P1 parked, PE planes consumed
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-      for (int T = 0; T < 2; ++T)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v4 = *reinterpret_cast<const float4*>(P1L + (32 * pt + c) * kP1Pitch + 32 * (T0 + T) + 8 * q +
-                                                             4 * h);
-          acc[2 * pt + T][4 * q] = fmaf(acc[2 * pt + T][4 * q], sc1, v4.x);
-          acc[2 * pt + T][4 * q + 1] = fmaf(acc[2 * pt + T][4 * q + 1], sc1, v4.y);
-          acc[2 * pt + T][4 * q + 2] = fmaf(acc[2 * pt + T][4 * q + 2], sc1, v4.z);
-          acc[2 * pt + T][4 * q + 3] = fmaf(acc[2 * pt + T][4 * q + 3], sc1, v4.w);
-        }
-    X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
-    X3_TR(0, 2);
-    store_act<true>(acc, XP, neg, 1.f, lane, T0);
-    if (wid == 0) {   // rows 256..271: the parked P1 was here; block3.0's 17th step reads them (extras later)
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (32 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(XP + pl * kPlaneX + (33 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-    acc_start<0>(acc, A.w.b2, 1.f / sc2, lane, T0);
-    acc_start<1>(acc, A.w.b2, 1.f / sc2, lane, T0);
-    s_wprime<1>(S1, r2, voff, 16, true);
-    X3_TR(0, 3);
-    X3_SYNC();   // S2
-    X3_TR(0, 4);
-    // ------------------------------------------------ block1.2: T0 E | T0 O + T1 E | T1 O + store T0
-    s_start(S0, bX, kPlaneX, 16, true);
-    s_run<0, 8>(acc, S0, r2, voff, bX, kPlaneX, 0, 16, true, none);
-    s_start(S1, bX, kPlaneX, 16, true);
-    s_run2<8>(acc, S0, S1, r2, r2, voff, bX, kPlaneX, 8, 16, true, 0, 16, true);
-    s_wprime<0>(S0, r3, voff, 17, true);
-    X3_TR(0, 5);
-    X3_SYNC();   // Ba0
-    X3_TR(0, 6);
-    {
-      StorePart p;
-      s_run<1, 8>(acc, S1, r2, voff, bX, kPlaneX, 8, 16, true, [&](int j, int i) {
-        if (store_slot(i) >= 0 && (store_slot(i) < 4 || j > 0)) store_part<0>(acc, p, XP, k2, ks2, lane, T0, store_slot(i) == 4 ? j - 1 : j, store_slot(i));
-      });
-      store_part<0>(acc, p, XP, k2, ks2, lane, T0, 7, 4);   // the last unit's LDS writes
-    }
-    acc_start<0>(acc, nullptr, 0.f, lane, T0);
-    s_wprime<1>(S1, r3, voff, 17, true);
-    X3_TR(0, 7);
-    X3_SYNC();   // Ba1: T0's act2 (E rows) visible
-    X3_TR(0, 8);
-    // ------------------------------------------------ block3.0: T0 E + store T1 | T0 O + T1 E | T1 O + store T0
-    if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
-      const float* exL = reinterpret_cast<const float*>(lds + L::OffEx) + buf * 8 * kXT;
-      float ex[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ex[e] = exL[e * kXT + lane];
-      store_group<true>(XP, kPlaneX, 32, lane, ex);
-    }
-    s_start(S0, bX, kPlaneX, 17, true);
-    {
-      StorePart p;
-      s_run<0, 8>(acc, S0, r3, voff, bX, kPlaneX, 0, 17, true, [&](int j, int i) {
-        if (store_slot(i) >= 0 && (store_slot(i) < 4 || j > 0)) store_part<1>(acc, p, XP, k2, ks2, lane, T0, store_slot(i) == 4 ? j - 1 : j, store_slot(i));
-      });
-      store_part<1>(acc, p, XP, k2, ks2, lane, T0, 7, 4);
-    }
-    acc_start<1>(acc, nullptr, 0.f, lane, T0);
-    X3_TR(0, 9);
-    X3_SYNC();   // Ba2: T1's act2 (O rows) and the extras visible
-    s_rebload(S0, bX, kPlaneX, 8, 17, true);   // T0's O rows were prefetched before Ba2
-    s_start(S1, bX, kPlaneX, 17, true);
-    s_run2<8>(acc, S0, S1, r3, r3, voff, bX, kPlaneX, 8, 17, true, 0, 17, true);
-    s_run<0, 1>(acc, S0, r3, voff, bX, kPlaneX, 16, 17, true, none);
-    s_wprime<0>(S0, r4, voff, 16, true);
-    X3_TR(0, 10);
-    X3_SYNC();   // Bb0
-    {
-      StorePart p;
-      s_run<1, 9>(acc, S1, r3, voff, bX, kPlaneX, 8, 17, true, [&](int j, int i) {
-        if (store_slot(i) >= 0 && (store_slot(i) < 4 ? j < 8 : (j > 0 && j < 9))) store_part<0>(acc, p, XP, k3, ks3, lane, T0, store_slot(i) == 4 ? j - 1 : j, store_slot(i));
-      });
-    }
-    acc_start<0>(acc, A.w.b4, 1.f / sc4, lane, T0);
-    s_wprime<1>(S1, r4, voff, 16, true);
-    X3_TR(0, 11);
-    X3_SYNC();   // Bb1: T0's act3 visible
-    // ------------------------------------------------ block3.2: T0 E + store T1 | T0 O + T1 E | T1 O + park T0
-    s_start(S0, bX, kPlaneX, 16, true);
-    {
-      StorePart p;
-      s_run<0, 8>(acc, S0, r4, voff, bX, kPlaneX, 0, 16, true, [&](int j, int i) {
-        if (store_slot(i) >= 0 && (store_slot(i) < 4 || j > 0)) store_part<1>(acc, p, XP, k3, ks3, lane, T0, store_slot(i) == 4 ? j - 1 : j, store_slot(i));
-      });
-      store_part<1>(acc, p, XP, k3, ks3, lane, T0, 7, 4);
-    }
-    acc_start<1>(acc, A.w.b4, 1.f / sc4, lane, T0);
-    X3_TR(0, 12);
-    X3_SYNC();   // Bb2: T1's act3 visible; the producers' tail is done with H4
-    s_rebload(S0, bX, kPlaneX, 8, 16, true);
-    s_start(S1, bX, kPlaneX, 16, true);
-    s_run2<8>(acc, S0, S1, r4, r4, voff, bX, kPlaneX, 8, 16, true, 0, 16, true);
-    s_wprime<0>(S0, r1, voff, 4, false);   // the next tile's block1.0
-    s_run<1, 8>(acc, S1, r4, voff, bX, kPlaneX, 8, 16, true, [&](int j, int i) {
-      if (i == 2) park_part<0>(acc, H4, lane, T0, j);
-    });
-    s_wprime<1>(S1, r1, voff, 4, false);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) park_part<1>(acc, H4, lane, T0, u);
-    X3_TR(0, 13);
-    X3_SYNC();   // S7: layer-input planes free (the producers park the next P1 there)
-    X3_TR(0, 14);
-  }
-}
-
-// The next tile's 30 distance-PE items (channel ch, band f; e = 5 ch + f) dealt
-// round robin to the 4 producer waves (wave pw: e = pw + 4 i) and done in three
-// parts of items [I0, I1) so each fits the consumer window it overlaps
-// (networks.py:175-190: sin / cos of x 2^f, one sincosf per item as the reference).
-template <int I0, int I1>
-__device__ __forceinline__ void pe_items(char* lds, int pw, int lane, const float (&dr6)[6]) {
-  using L = XL<true>;
-  if (I0 == 0 && pw == 0) {   // rows 60..63: the 4th 16-k step reads them
-    char* pz = lds + L::OffPE + (7 * kXT + lane) * 16 + 8;
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
-  }
-  if (PNR_ABLATE & 2) return;
-  const int w = __builtin_amdgcn_readfirstlane(pw);
-#pragma unroll
-  for (int i = I0; i < I1; ++i) {
-    const int e = w + 4 * i;
-    if (e >= 30) break;   // wave-uniform
-    const int ch = e / 5, f = e - 5 * ch;
-    const float x = ch == 0 ? dr6[0] : ch == 1 ? dr6[1] : ch == 2 ? dr6[2] : ch == 3 ? dr6[3] : ch == 4 ? dr6[4] : dr6[5];
-    float sn, cs;
-    sincosf(x * (float)(1 << f), &sn, &cs);
-    pe_store<true>(lds, lane, e, sn, cs);
-  }
-}
-
-// Producer schedule matching consumer_loop_s's 10 barriers per tile.
-__device__ __forceinline__ void producer_loop_s(const X3Args& A, char* lds, int pw, int lane) {
-  using L = XL<true>;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, kXTS);
-#if PNR_X3_PRIO
-  __builtin_amdgcn_s_setprio(PNR_X3_PRIO);
-#endif
-  f32x4n p1r[16];
-  unsigned p1e = 0;
-  float dr6[6];
-  GatherState g;
-  gather_row(A, first_tile(ntiles), lane, g);
-  gather_sample(A, lane, g);
-  gather<true>(A, g, 0, 0, lds, pw, lane, dr6);
-  pe_items<0, 8>(lds, pw, lane, dr6);
-  int* TQ = reinterpret_cast<int*>(lds + L::OffTq);
-  if (pw == 0 && lane == 0) TQ[1] = (int)take_tile(A, ntiles);
-  X3_SYNC();   // P0
-  p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr), pw, lane);
-  X3_SYNC();   // S0
-  float chk = 0.f;
-  TailState ts;
-  int it = 0;
-  int64_t prev = -1;
-  for (int64_t tile = first_tile(ntiles); tile < ntiles; prev = tile, tile = TQ[(it + 1) & 3], ++it) {
-    const int nbuf = (it & 1) ^ 1;
-    const int nw = (it + 1) % 3;
-    const int64_t next = TQ[(it + 1) & 3];
-    if (pw == 0 && lane == 0) TQ[(it + 2) & 3] = next < ntiles ? (int)take_tile(A, ntiles) : (int)ntiles;
-    X3_TR(1, 0);
-    park_p1(p1r, p1e, lds, pw, lane);
-    gather_row(A, next, lane, g);
-    X3_SYNC();   // S1
-    X3_SYNC();   // S1b
-    gather_sample(A, lane, g);
-    X3_SYNC();   // S2
-    X3_TR(1, 1);
-    const bool work = !((PNR_ABLATE & 2048) && it > 1);   // (2048: timing only, no producer work)
-    if (work) gather<true>(A, g, nbuf, nw, lds, pw, lane, dr6);   // block1.2 window
-    X3_TR(1, 2);
-    X3_SYNC();   // Ba0: the next tile's point rows are in LDS
-    if (work) p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
-    X3_TR(1, 3);
-    X3_SYNC();   // Ba1
-    if (work && it > 0) producer_tail<0>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
-    X3_SYNC();   // Ba2
-    if (work) pe_items<0, 3>(lds, pw, lane, dr6);
-    X3_TR(1, 4);
-    X3_SYNC();   // Bb0
-    if (work && it > 0) producer_tail<1>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
-    X3_TR(1, 5);
-    X3_SYNC();   // Bb1
-    if (work) pe_items<3, 5>(lds, pw, lane, dr6);
-    X3_SYNC();   // Bb2: H4 free for the consumers' park
-    if (work) pe_items<5, 8>(lds, pw, lane, dr6);
-    X3_TR(1, 6);
-    X3_SYNC();   // S7
-  }
-  if (it > 0) {
-    producer_tail<0>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
-    producer_tail<1>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
-  }
-  if (A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
-}
-
 template <bool H>
 __device__ __forceinline__ void pairs_body(const X3Args& A) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1492,11 +1044,9 @@ __device__ __forceinline__ void pairs_body(const X3Args& A) {
   if (threadIdx.x < kHid) reinterpret_cast<float*>(lds + XL<H>::OffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
   if (wid < 4) {
     X3_SYNC();   // P0
-    if constexpr (H && PNR_H2_SKEW) consumer_loop_s(A, lds, wid, lane);
-    else consumer_loop<H>(A, lds, wid, lane);
+    consumer_loop<H>(A, lds, wid, lane);
   } else {
-    if constexpr (H && PNR_H2_SKEW) producer_loop_s(A, lds, wid - 4, lane);
-    else producer_loop<H>(A, lds, wid - 4, lane);
+    producer_loop<H>(A, lds, wid - 4, lane);
   }
 }
 
@@ -1556,7 +1106,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
   for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
   const int T0 = 2 * wid;
-  const int voff = (T0 * 2 * 64 + lane) * 16;
+  const int voff = (T0 * XL<true>::NPW * 64 + lane) * 16;
   const __amdgpu_buffer_rsrc_t r1a = rsrc(A.pack[0]), r1b = rsrc(A.pack[1]), r2 = rsrc(A.pack[2]),
                                r3 = rsrc(A.pack[3]);
   float chk = 0.f;   // 0 * (outputs): NaN once any output is not finite (see k_pairs_h2)
@@ -1680,7 +1230,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;
   const int64_t ntiles = cdiv(np, kXT);
   const int T0 = 2 * wid;
-  const int voff = (T0 * 2 * 64 + lane) * 16;
+  const int voff = (T0 * XL<true>::NPW * 64 + lane) * 16;
   const __amdgpu_buffer_rsrc_t rw = rsrc(A.pack);
   float chk = 0.f;   // 0 * outputs: NaN once one is not finite (an input beyond the f16 range)
   WRing<true> wr;

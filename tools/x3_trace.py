@@ -28,24 +28,6 @@ def main():
     fn.restype = ctypes.c_int
     assert fn(buf, 2 * 64 * 16) == 0
     t = np.frombuffer(buf, dtype=np.uint64).reshape(2, 64, 16).astype(np.int64)
-    if os.environ.get("PNR_SKEW_TRACE"):   # consumer_loop_s stamps
-        c = t[0, 8:60, :15]
-        d = np.diff(c, axis=1)
-        tile = c[1:, 0] - c[:-1, 0]
-        names = ["block1.0", "S1+P1 add+S1b", "store act1", "S2 wait", "1.2 T0E+dual", "Ba0 wait", "1.2 T1O+st T0",
-                 "Ba1 wait", "3.0 T0E+st T1", "Ba2+dual+T0 16", "Bb0+T1O+st T0", "Bb1+T0E+st T1",
-                 "Bb2+dual+T1O+park", "S7 wait"]
-        print("consumer wave 0 (skewed streams), cycles per tile (median over tiles 8..59): total",
-              int(np.median(tile)))
-        for i, nme in enumerate(names):
-            print(f"  {nme:22s} {int(np.median(d[:, i])):7d}")
-        p = t[1, 8:60, :7]
-        dp = np.diff(p, axis=1)
-        pn = ["park+S1..S2", "gather", "Ba0+fetch+tail0", "Ba1..pe0", "Bb0+tail1", "Bb1..pe1"]
-        print("producer wave 4")
-        for i, nme in enumerate(pn):
-            print(f"  {nme:22s} {int(np.median(dp[:, i])):7d}")
-        return
     c = t[0, 8:60]
     names = ["layer1", "S1 wait", "P1 add+S1b", "store1", "S2 wait", "layer2", "S3 wait", "store2+S4", "layer3",
              "S5 wait", "store3+S6", "layer4", "tail", "S7 wait"]
