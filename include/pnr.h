@@ -422,6 +422,12 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
 int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t* out);
 int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
                 float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream);
+/* Same contract and scratch, fp32-accurate on bf16 MFMA: A and B split exactly
+ * into three bf16 terms each, the six cross products of weight >= 2^-16 with
+ * fp32 accumulation (the fp32x3 arithmetic of pnr_aggregate_fwd_x3; error vs an
+ * fp64 GEMM ~ native fp32's).  The training path's default. */
+int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
+                   float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream);
 
 /* X1[p] = [emb_p, PE_3(emb_p)] (block1.0 columns 0..223) for p < n, and the
  * matching backward d_emb[p] += dX1[p] . dX1/d emb (networks.py:175-190). */

@@ -150,6 +150,8 @@ SIGNATURES = {
     "pnr_gemm_tn_scratch_bytes": (c_int, [c_int64, c_int32, c_int32, P(c_size_t)]),
     "pnr_gemm_tn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),
+    "pnr_gemm_tn_x3": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                               c_void_p, c_size_t, c_void_p]),
     "pnr_point_pe3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_point_pe3_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_composite_bwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams), c_void_p,
@@ -223,9 +225,10 @@ def aggregate_scratch(n_max: int, n_points: int, device) -> torch.Tensor:
     return torch.empty((int(nb.value) + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
-def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False):
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = True):
     """C = A^T B (A [K,M], B [K,N], fp32 row-major with unit column stride) on
-    pnr_gemm_tn; returns C [M,N] (and A's column sums when colsum)."""
+    pnr_gemm_tn_x3 (fp32-accurate on bf16 MFMA; x3=False: pnr_gemm_tn, native
+    fp32 MFMA); returns C [M,N] (and A's column sums when colsum)."""
     K, M = A.shape
     N = B.shape[1]
     assert B.shape[0] == K and A.stride(1) == 1 and B.stride(1) == 1
@@ -234,8 +237,9 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False):
     scratch = torch.empty(max(int(nb.value) // 4, 1), dtype=torch.float32, device=A.device)
     C = torch.empty((M, N), dtype=torch.float32, device=A.device)
     cs = torch.empty(M, dtype=torch.float32, device=A.device) if colsum else None
-    check(lib().pnr_gemm_tn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
-                            scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")
+    fn = lib().pnr_gemm_tn_x3 if x3 else lib().pnr_gemm_tn
+    check(fn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
+             scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")
     return (C, cs) if colsum else C
 
 

@@ -14,7 +14,7 @@
 // SIMD); every split writes its own partial C, summed in a fixed order by a
 // two-level reduction: deterministic, no float atomics.  Column sums of A
 // (the bias gradients) ride along as an extra partial row.
-#include "pnr_common.h"
+#include "agg_common.h"
 
 namespace pnr {
 
@@ -132,6 +132,123 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) k_gemm_tn_part(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------- x3 variant
+// fp32-accurate C = A^T B on bf16 MFMA (pnr_gemm_tn_x3): every operand split
+// exactly into three bf16 terms (agg_common.h split2) and the six cross
+// products of weight >= 2^-16 summed with fp32 accumulation (the forward's
+// fp32x3 arithmetic): 6 v_mfma_f32_32x32x16_bf16 per 16 k-rows instead of 8
+// v_mfma_f32_32x32x2_f32 per 2.  Per K split one 8-wave workgroup owns all of C
+// as before; 16-row chunks of A and B are staged in LDS as split planes
+// ([plane][row][k], 48-B lines), double-buffered: the next chunk's global loads
+// are in flight during this chunk's MFMAs, split and written after them.  Wave w
+// owns M tiles 2(w % 4) .. +1 x N tiles 4(w / 4) .. +3 (8 accumulators).
+constexpr int kXK = 16;                 // k rows per chunk (one bf16 MFMA k-step)
+constexpr int kXPitch = 24;             // bf16 per LDS line (16 k + 8 pad)
+constexpr int kXPlane = 256 * kXPitch;  // bf16 per plane (256 rows)
+constexpr size_t kXLds = 2 * 2 * 3 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 72 KB
+
+__global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t glds[];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int64_t k_begin = (int64_t)blockIdx.x * g.kchunk;
+  const int64_t k_end = k_begin + g.kchunk < g.K ? k_begin + g.kchunk : g.K;
+  const int64_t stride = (int64_t)g.M * g.N + g.M;
+  float* out = g.part + (int64_t)blockIdx.x * stride;
+  // staging role: column col of A and of B, k rows 8 kh .. 8 kh + 7 of a chunk
+  const int col = tid & 255, kh = tid >> 8;
+  const bool stA = col < g.M, stB = col < g.N;
+  float csum = 0.f;
+  float va[8], vb[8];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t r = k0 + 8 * kh + j;
+      const bool ok = r < k_end;
+      va[j] = ok && stA ? g.A[r * g.lda + col] : 0.f;
+      vb[j] = ok && stB ? g.B[r * g.ldb + col] : 0.f;
+    }
+  };
+  auto put = [&](int buf) {
+    uint16_t* base = glds + (size_t)buf * 6 * kXPlane + col * kXPitch + 8 * kh;
+    uint4 pa[3], pb[3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      csum += va[2 * q] + va[2 * q + 1];
+      unsigned x0, x1, x2;
+      split2(va[2 * q], va[2 * q + 1], x0, x1, x2);
+      reinterpret_cast<unsigned*>(&pa[0])[q] = x0;
+      reinterpret_cast<unsigned*>(&pa[1])[q] = x1;
+      reinterpret_cast<unsigned*>(&pa[2])[q] = x2;
+      split2(vb[2 * q], vb[2 * q + 1], x0, x1, x2);
+      reinterpret_cast<unsigned*>(&pb[0])[q] = x0;
+      reinterpret_cast<unsigned*>(&pb[1])[q] = x1;
+      reinterpret_cast<unsigned*>(&pb[2])[q] = x2;
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      *reinterpret_cast<uint4*>(base + p * kXPlane) = pa[p];
+      *reinterpret_cast<uint4*>(base + (3 + p) * kXPlane) = pb[p];
+    }
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x16){0.f};
+  const int mt0 = 2 * (wid & 3), nt0 = 4 * (wid >> 2);
+  load(k_begin);
+  put(0);
+  __syncthreads();
+  int it = 0;
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += kXK, ++it) {
+    const int buf = it & 1;
+    const bool more = k0 + kXK < k_end;
+    if (more) load(k0 + kXK);   // in flight during the MFMAs
+    const uint16_t* lb = glds + (size_t)buf * 6 * kXPlane + c * kXPitch + 8 * h;
+    uint4 a[2][3];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[mi][p] = *reinterpret_cast<const uint4*>(lb + p * kXPlane + 32 * (mt0 + mi) * kXPitch);
+    // per N tile: its B planes, then the six products of both M tiles, smallest
+    // terms first (A2B0, A1B1, A0B2, A1B0, A0B1, A0B0)
+    constexpr int kPa[6] = {2, 1, 0, 1, 0, 0}, kPb[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      if (32 * (nt0 + ni) >= g.N) continue;
+      uint4 b[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        b[p] = *reinterpret_cast<const uint4*>(lb + (3 + p) * kXPlane + 32 * (nt0 + ni) * kXPitch);
+#pragma unroll
+      for (int e = 0; e < 6; ++e)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          if (32 * (mt0 + mi) < g.M) acc[mi][ni] = mfma_bf16(a[mi][kPa[e]], b[kPb[e]], acc[mi][ni]);
+    }
+    if (more) put(buf ^ 1);
+    __syncthreads();
+  }
+  // C/D layout: row = (r&3) + 8(r>>2) + 4h, col = c
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int m0 = 32 * (mt0 + mi), n0 = 32 * (nt0 + ni);
+      if (m0 >= g.M || n0 >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[(int64_t)(m0 + (r & 3) + 8 * (r >> 2) + 4 * h) * g.N + n0 + c] = acc[mi][ni][r];
+    }
+  if (g.colsum) {   // column sums of A: the two k-halves of every column
+    float* red = reinterpret_cast<float*>(glds);
+    __syncthreads();
+    if (kh == 1) red[col] = csum;
+    __syncthreads();
+    if (kh == 0 && stA) out[(int64_t)g.M * g.N + col] = csum + red[col];
+  }
+}
+
 // out[grp][i] = sum_{s in group grp} part[s][i] in split order (float4 lanes).
 __global__ void k_reduce_splits(const float* __restrict__ part, int64_t n4, int nsplit, int group,
                                 float* __restrict__ out) {
@@ -155,7 +272,7 @@ static void gemm_plan(int64_t K, int* nsplit, int64_t* kchunk) {
   const int64_t maxs = K / 128 > 0 ? K / 128 : 1;    // >= 128 k-rows per split
   if (s > maxs) s = maxs;
   int64_t kc = cdiv(K > 0 ? K : 1, s);
-  kc = cdiv(kc, 2 * kGUnroll) * (2 * kGUnroll);
+  kc = cdiv(kc, 16) * 16;   // whole 16-row chunks (x3) and 2 * kGUnroll pipeline stages (fp32)
   *kchunk = kc;
   *nsplit = (int)(K > 0 ? cdiv(K, kc) : 1);
 }
@@ -178,9 +295,8 @@ extern "C" int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t
   return PNR_OK;
 }
 
-extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
-                           int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
-                           void* stream) {
+static int gemm_tn_impl(bool x3, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
+                        int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream) {
   PNR_CHECK_ARG(C && scratch && (K == 0 || (A && B)), "gemm_tn: null pointer");
   PNR_CHECK_ARG(M > 0 && N > 0 && M % 32 == 0 && N % 32 == 0 && M <= 32 * kGWaves && N <= 32 * kGMaxNT,
                 "gemm_tn: M, N must be multiples of 32 in [32, 256]");
@@ -207,7 +323,17 @@ extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t 
   g.kchunk = kc;
   g.part = static_cast<float*>(scratch);
   g.colsum = colsum_a != nullptr;
-  hipLaunchKernelGGL(k_gemm_tn_part, dim3(ns), dim3(64 * kGWaves), 0, st, g);
+  if (x3) {
+    static bool attr = false;
+    if (!attr) {
+      PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_x3_part),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_gemm_tn_x3_part, dim3(ns), dim3(512), kXLds, st, g);
+  } else {
+    hipLaunchKernelGGL(k_gemm_tn_part, dim3(ns), dim3(64 * kGWaves), 0, st, g);
+  }
   PNR_LAUNCH_CHECK();
   // two-level ordered reduction: groups of kGGroup splits, then the groups
   const int64_t stride = (int64_t)M * N + M;   // multiple of 4 (M % 32 == 0)
@@ -224,4 +350,16 @@ extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t 
   if (colsum_a)
     PNR_HIP(hipMemcpyAsync(colsum_a, g.part + (size_t)M * N, (size_t)M * sizeof(float), hipMemcpyDeviceToDevice, st));
   return PNR_OK;
+}
+
+extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
+                           int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
+                           void* stream) {
+  return gemm_tn_impl(false, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
+}
+
+extern "C" int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
+                              int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
+                              void* stream) {
+  return gemm_tn_impl(true, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
 }

@@ -3,13 +3,15 @@
 ``AggregateFn`` and ``CompositeFn`` are torch.autograd.Functions whose forward
 runs ``pnr_aggregate_fwd_train`` / ``pnr_composite_fwd`` and whose backward runs
 
-  colour branch backward      3 small GEMMs per layer on hipBLASLt (torch.matmul)
+  colour branch backward      weight gradients on pnr_gemm_tn_x3, the small dX
+                              products (n x 128 x 128) on hipBLASLt (torch.matmul)
   pnr_aggregate_bwd_pairs     fused per-pair dX chain on MFMA (k_pairs_bwd): alpha
                               branch + K-sum backward, block3.2^T / block3.0^T /
                               block1.2^T, LeakyReLU masks, weight / conf / colour /
                               dir gradients, scatter-add of dz1 into the per-point
                               block1.0 partial (the gather's index_add)
-  weight gradients            dW = dZ^T X over all pairs: plain GEMMs (hipBLASLt)
+  weight gradients            dW = dZ^T X over all pairs: pnr_gemm_tn_x3 (split-K,
+                              fp32-accurate bf16x3 MFMA, deterministic reduction)
   pnr_point_pe3(_bwd)         block1.0's point half: dW1[:, :224] = dP1^T X1,
                               d emb = PE_3 backward of dP1 W1[:, :224]
   pnr_composite_bwd           reverse scans of the alpha composite
@@ -159,13 +161,19 @@ class AggregateFn(torch.autograd.Function):
         vm = (sv["vmask"][:n] != 0).float()[:, None]
         dc = d_feat[:n, 1:] * vm
         hc1, hc2, hc3 = sv["hc1"][:n], sv["hc2"][:n], sv["hc3"][:n]
-        y0 = torch.cat([sv["hid"][:n], sv["vpe"][:n]], 1)
-        dz = _lrelu_grad(dc, hc3, slope)
-        grads["color_branch.4.weight"], grads["color_branch.4.bias"] = dz.t() @ hc2, dz.sum(0)
-        dz = _lrelu_grad(dz @ P["color_branch.4.weight"], hc2, slope)
-        grads["color_branch.2.weight"], grads["color_branch.2.bias"] = dz.t() @ hc1, dz.sum(0)
-        dz = _lrelu_grad(dz @ P["color_branch.2.weight"], hc1, slope)
-        grads["color_branch.0.weight"], grads["color_branch.0.bias"] = dz.t() @ y0, dz.sum(0)
+        # weight gradients dW = dZ^T X on pnr_gemm_tn_x3 (bias = column sums); the
+        # small dX = dZ W products (n x 128 x 128) stay on hipBLASLt
+        dz = _lrelu_grad(dc, hc3, slope).contiguous()
+        grads["color_branch.4.weight"], grads["color_branch.4.bias"] = L.gemm_tn(dz, hc2.contiguous(), colsum=True)
+        dz = _lrelu_grad(dz @ P["color_branch.4.weight"], hc2, slope).contiguous()
+        grads["color_branch.2.weight"], grads["color_branch.2.bias"] = L.gemm_tn(dz, hc1.contiguous(), colsum=True)
+        dz = _lrelu_grad(dz @ P["color_branch.2.weight"], hc1, slope).contiguous()
+        gC0 = torch.empty((128, 280), **f32)
+        gC0[:, :256], grads["color_branch.0.bias"] = L.gemm_tn(dz, sv["hid"][:n], colsum=True)
+        vpe32 = torch.zeros((n, 32), **f32)
+        vpe32[:, :24] = sv["vpe"][:n]
+        gC0[:, 256:] = L.gemm_tn(dz, vpe32)[:, :24]
+        grads["color_branch.0.weight"] = gC0
         d_hid = torch.zeros((max(n_max, 1), 256), **f32)
         d_hid[:n] = dz @ P["color_branch.0.weight"][:, :256]
         # ---- per-pair chain on MFMA

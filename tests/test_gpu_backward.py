@@ -158,18 +158,27 @@ def test_train_step_reduces_loss(cuda):
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("K,M,N", [(235001, 256, 256), (4097, 256, 224), (37, 256, 32), (0, 128, 64)])
-def test_gemm_tn_vs_torch(cuda, K, M, N):
+@pytest.mark.parametrize("x3", [False, True])
+@pytest.mark.parametrize("K,M,N", [(235001, 256, 256), (4097, 256, 224), (37, 256, 32), (0, 128, 64),
+                                   (1000, 32, 64)])
+def test_gemm_tn_vs_torch(cuda, K, M, N, x3):
+    """pnr_gemm_tn (fp32 MFMA) and pnr_gemm_tn_x3 (bf16x3 split, the training
+    default) against an fp64 GEMM; x3's error within 2x native fp32's."""
     from pointnerf_amd import _lib as L
     g = torch.Generator(device=cuda).manual_seed(K + N)
-    A = torch.randn((K, M), device=cuda, generator=g)
+    A = torch.randn((K, M), device=cuda, generator=g) * torch.rand((1, M), device=cuda, generator=g) * 3
     B = torch.randn((K, N + 8), device=cuda, generator=g)[:, :N]        # ldb > N
-    C, cs = L.gemm_tn(A, B, colsum=True)
-    ref = (A.double().t() @ B.double()).float()
+    C, cs = L.gemm_tn(A, B, colsum=True, x3=x3)
+    ref64 = A.double().t() @ B.double()
+    ref = ref64.float()
     close(C, ref, "C", rel=1e-4, scale=2e-6)
     close(cs, A.double().sum(0).float(), "colsum", rel=1e-4, scale=2e-6)
-    C2 = L.gemm_tn(A, B)
+    C2 = L.gemm_tn(A, B, x3=x3)
     assert torch.equal(C, C2)          # deterministic split-K reduction
+    if x3 and K > 0:
+        e3 = float((C.double() - ref64).abs().max())
+        e32 = float((L.gemm_tn(A, B, x3=False).double() - ref64).abs().max())
+        assert e3 <= 2 * e32 + 1e-12, (e3, e32)
 
 
 def test_conf_coefficient_and_zero_one_loss(cuda):
