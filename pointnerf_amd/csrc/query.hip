@@ -12,6 +12,8 @@
 // Positions are recomputed from (ray, candidate index) with the reference's
 // fp32 operation order, so every kernel sees bit-identical sample positions
 // without materialising raypos[R,400,3] (3.1 GB for an 800^2 frame).
+#include <algorithm>
+
 #include "pnr_common.h"
 
 namespace pnr {
@@ -21,7 +23,13 @@ constexpr int kQBlock = 256;
 #define PNR_KNN_WAVES 8   // k_knn is load-latency bound: registers capped for 8 waves per SIMD (A/B: 0 -> 2.73 ms, 8 -> 2.33 ms query)
 #endif
 #ifndef PNR_KNN_BATCH
-#define PNR_KNN_BATCH 2   // candidate records fetched together (A/B: 1 -> 2.38, 2 -> 2.33, 4 -> 2.92 ms query)
+#define PNR_KNN_BATCH 1   // candidate records fetched together (A/B, with the up-front lookups: 1 -> 2.12, 2 -> 2.15 ms query)
+#endif
+#ifndef PNR_KNN_XCD
+#define PNR_KNN_XCD 2   // 0: grid-stride; 1: static XCD ranges; 2: per-XCD counters + stealing
+#endif
+#ifndef PNR_KNN_GRID
+#define PNR_KNN_GRID 2048   // blocks: one full-occupancy wave of the chip (8 per CU)
 #endif
 #if PNR_KNN_WAVES
 #define PNR_KNN_ATTR __attribute__((amdgpu_waves_per_eu(PNR_KNN_WAVES)))
@@ -158,8 +166,7 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
   }
 }
 
-// All records of one occupied voxel, in slot order, fetched 4 at a time
-// (memory-level parallelism) and visited in order.
+// All records of one record range, in order, PNR_KNN_BATCH loads in flight.
 template <int KMAX>
 __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
                                          float buf[KMAX], int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
@@ -193,7 +200,7 @@ __device__ __forceinline__ int held_rank(const uint2 wd, int bit) {
 // visited in the reference's order (Chebyshev layer, then x -> y -> z); a cell
 // whose voxel holds no point contributes nothing there either, so only held
 // cells are looked up (bitmap + rank: no per-cell table of the whole grid).
-template <int KMAX>
+template <int KMAX, int LAYERS>
 __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, int layers, float r2,
                                        const QIndex& qi, int32_t out[KMAX], int& n_cand) {
   const int fx = vox_coord(p[0], g.shift[0], g.vs[0]);
@@ -207,7 +214,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
   }
   int kid = 0, far_ind = 0;
   float far2 = 0.f;
-  if (layers == 2) {
+  if (LAYERS == 2) {
     // query 3x3x3 (every shipped config but truck).  The 9 (x, y) columns of
     // the neighbourhood are runs of 3 consecutive cells (z fastest), and held
     // voxels are ranked in cell order with their records stored in rank order
@@ -219,45 +226,68 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
     // columns x -> y, each run z -> (the centre skipped in its column).
     if ((unsigned)fz >= (unsigned)g.dims[2]) return 0;   // never: filled samples lie in held-dilated cells
     const int zlo = fz > 0 ? fz - 1 : fz, zhi = fz + 1 < g.dims[2] ? fz + 1 : fz;
-    auto pos = [&](int64_t c, int& held) -> int {
-      const uint2 wd = qi.words[c >> 5];
-      const int b = (int)(c & 31);
-      held = (wd.x >> b) & 1u;
-      return (int)wd.y + __popc(wd.x & ((1u << b) - 1u));
-    };
     auto range = [&](int o, int e) {
       n_cand += e - o;
       knn_cell<KMAX>(qi.recs + o, e - o, p, K, r2, buf, out, kid, far_ind, far2);
     };
-    // layer 0: the centre cell
-    const int64_t cc = ((int64_t)fx * g.dims[1] + fy) * g.dims[2] + fz;
-    int hc;
-    const int pc = pos(cc, hc);
-    int oc = 0, ec = 0;
-    if (hc) {
-      oc = qi.rec_off[pc];
-      ec = qi.rec_off[pc + 1];
-      range(oc, ec);
+    // Every index lookup of the 27 cells is issued up front: one round of 9-18
+    // independent word loads (a column's 3-cell run spans <= 2 words; the
+    // centre cell is in column 4's), one round of rec_off loads, then the 11
+    // record ranges (centre, columns 0-3, column 4 below / above the centre,
+    // columns 5-8) walked by ONE visit loop in the reference's order (A/B vs
+    // 9 x 2 dependent lookup rounds: DESIGN.md 13).  32-bit cell indices (this
+    // kernel is launched only for grids of < 2^32 cells) keep addresses 1 VGPR.
+    int lo[9], hi[9];
+    int pc = 0, hc = 0;
+#pragma unroll
+    for (int col = 0; col < 9; ++col) {
+      const int cx = fx + col / 3 - 1, cy = fy + col % 3 - 1;
+      const bool in = (unsigned)cx < (unsigned)g.dims[0] && (unsigned)cy < (unsigned)g.dims[1];
+      const uint32_t base = ((uint32_t)cx * (uint32_t)g.dims[1] + (uint32_t)cy) * (uint32_t)g.dims[2];
+      const uint32_t clo = base + zlo, chi = base + zhi;
+      const uint2 a = in ? qi.words[clo >> 5] : make_uint2(0u, 0u);
+      const uint2 b = in && (chi >> 5) != (clo >> 5) ? qi.words[chi >> 5] : a;
+      lo[col] = (int)a.y + __popc(a.x & ((1u << (clo & 31)) - 1u));
+      hi[col] = (int)b.y + __popc(b.x & ((1u << (chi & 31)) - 1u)) + (int)((b.x >> (chi & 31)) & 1u);
+      if (col == 4) {
+        const uint32_t cc = base + fz;
+        const uint2 w = (cc >> 5) == (clo >> 5) ? a : b;
+        hc = (w.x >> (cc & 31)) & 1u;
+        pc = (int)w.y + __popc(w.x & ((1u << (cc & 31)) - 1u));
+      }
     }
-    if (kid < K) {   // layer 0 already saw >= K candidates: done (qpiw.py:526)
-#pragma unroll 1
-      for (int col = 0; col < 9; ++col) {
-        const int cx = fx + col / 3 - 1, cy = fy + col % 3 - 1;
-        if ((unsigned)cx >= (unsigned)g.dims[0] || (unsigned)cy >= (unsigned)g.dims[1]) continue;
-        const int64_t base = ((int64_t)cx * g.dims[1] + cy) * g.dims[2];
-        int hlo, hhi;
-        const int plo = pos(base + zlo, hlo);
-        const int phi = pos(base + zhi, hhi);
-        const int pend = phi + hhi;
-        if (pend == plo) continue;   // no held cell in the run
-        const int o = qi.rec_off[plo], e = qi.rec_off[pend];
-        if (col != 4) {
-          range(o, e);
-        } else {   // centre column: the run minus the centre cell
-          range(o, hc ? oc : qi.rec_off[pc]);
-          range(hc ? ec : qi.rec_off[pc], e);
+#pragma unroll
+    for (int col = 0; col < 9; ++col) {
+      if (hi[col] == lo[col]) continue;   // no held cell in the run
+      lo[col] = qi.rec_off[lo[col]];
+      hi[col] = qi.rec_off[hi[col]];
+    }
+    // centre records [pco, pce); empty when the centre voxel holds no point
+    const int pco = lo[4] == hi[4] ? lo[4] : qi.rec_off[pc];
+    const int pce = hc ? qi.rec_off[pc + 1] : pco;
+    auto sel = [&](int rg, int& o, int& e) {
+      o = pco;
+      e = pce;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int r = j < 5 ? j + 1 : j + 2;   // range slot of column j (column 4: slots 5, 6)
+        if (rg == r) {
+          o = lo[j];
+          e = j == 4 ? pco : hi[j];
         }
       }
+      if (rg == 6) {
+        o = pce;
+        e = hi[4];
+      }
+    };
+#pragma unroll 1
+    for (int rg = 0; rg < 11; ++rg) {
+      if (rg == 1 && kid >= K) break;   // layer 0 already saw >= K candidates (qpiw.py:526)
+      int o, e;
+      sel(rg, o, e);
+      if (o == e) continue;
+      range(o, e);
     }
     return kid < K ? kid : K;
   }
@@ -284,14 +314,17 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
   return kid < K ? kid : K;
 }
 
-template <int KMAX>
+// LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
+// layered loop inlined beside it costs registers); 0: any layer count.
+template <int KMAX, int LAYERS>
 __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
                                                  int32_t* __restrict__ ray_vcnt,
                                                  float* __restrict__ sample_w,
-                                                 float* __restrict__ sample_p, int32_t* counts, int vec_pidx) {
+                                                 float* __restrict__ sample_p, int32_t* counts, int vec_pidx,
+                                                 int32_t* __restrict__ xcd_ctr) {
   const int64_t S = counts[0];
   float c[3], Rm[9];
   load_cam(q, 0, c, Rm);
@@ -304,7 +337,38 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
   __shared__ int hist[kQBlock], perm[kQBlock];
   const bool by_slot = SR <= kQBlock;   // (A/B: lanes in fill order 3.45 ms query, by slot 2.94)
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int64_t base = blockIdx.x * (int64_t)kQBlock; base < S; base += (int64_t)gridDim.x * kQBlock) {
+  // XCD-aware chunking (grid a multiple of 8; blocks b, b + 8, ... share an
+  // XCD): XCD x walks the contiguous chunk range [C x / 8, C (x + 1) / 8) of the
+  // sample list, so at any moment its L2 holds the records of a few image rows
+  // instead of every XCD touching the same wide window (A/B in DESIGN.md 13).
+  const int64_t C = (S + kQBlock - 1) / kQBlock;
+  const bool xcd = PNR_KNN_XCD && (gridDim.x & 7) == 0;
+  const int xg = xcd ? (int)(blockIdx.x & 7) : 0;
+  const int64_t c_lo = xcd ? C * xg / 8 : 0, c_hi = xcd ? C * (xg + 1) / 8 : C;
+  const int64_t c_step = xcd ? gridDim.x / 8 : gridDim.x;
+  // PNR_KNN_XCD 2: chunks handed out in order by a per-XCD counter, and an XCD
+  // whose range is exhausted takes chunks from the next XCDs' ranges (the
+  // bands' per-sample costs differ, so static ranges finish unevenly).
+  const bool dyn = PNR_KNN_XCD == 2 && xcd;
+  __shared__ int64_t s_ch;
+  auto next_chunk = [&](int64_t prev) -> int64_t {
+    if (!dyn) return prev < 0 ? c_lo + (xcd ? blockIdx.x >> 3 : blockIdx.x) : prev + c_step;
+    __syncthreads();   // every thread has read s_ch of the previous chunk
+    if (tid == 0) {
+      int64_t got = C;
+      for (int k = 0; k < 8 && got == C; ++k) {
+        const int y = (xg + k) & 7;
+        const int64_t t = C * y / 8 + atomicAdd(xcd_ctr + y, 1);
+        if (t < C * (y + 1) / 8) got = t;
+      }
+      s_ch = got;
+    }
+    __syncthreads();
+    return s_ch;
+  };
+  const int64_t c_end = dyn ? C : c_hi;
+  for (int64_t ch = next_chunk(-1); ch < c_end; ch = next_chunk(ch)) {
+    const int64_t base = ch * kQBlock;
     int64_t i = base + tid;
     if (by_slot) {
       const int n_in = (int)min((int64_t)kQBlock, S - base);
@@ -347,7 +411,7 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
       sample_p[i * 3 + a] = pp[a];
     }
     int32_t out[KMAX];
-    const int nk = knn_one<KMAX>(p, g, K, layers, r2, qi, out, n_cand);
+    const int nk = knn_one<KMAX, LAYERS>(p, g, K, layers, r2, qi, out, n_cand);
     if (KMAX == 8 && K == 8 && vec_pidx) {   // two 16-B stores (pidx 16-B aligned)
       int4* o4 = reinterpret_cast<int4*>(pidx + i * 8);
       o4[0] = make_int4(out[0], out[1], out[2], out[3]);
@@ -448,7 +512,7 @@ using namespace pnr;
 
 extern "C" int pnr_query_scratch_bytes(int64_t R, int32_t SR, size_t* out) {
   PNR_CHECK_ARG(out && R >= 0 && SR > 0, "query_scratch_bytes: bad args");
-  *out = scan_scratch_bytes(R * SR + 1);
+  *out = std::max<size_t>(scan_scratch_bytes(R * SR + 1), 64);   // >= k_knn's 8 chunk counters
   return PNR_OK;
 }
 
@@ -473,7 +537,7 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
                     b->sample_p && b->counts && b->scratch,
                 "query: null buffer");
   const int64_t R = rays->R, RS = R * qp->SR;
-  PNR_CHECK_ARG(b->scratch_bytes >= scan_scratch_bytes(RS + 1), "query: scratch too small");
+  PNR_CHECK_ARG(b->scratch_bytes >= std::max<size_t>(scan_scratch_bytes(RS + 1), 64), "query: scratch too small");
   hipStream_t st = as_stream(stream);
   QRays q = to_qrays(rays);
   QGrid g;
@@ -501,16 +565,23 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
                      b->n_filled, b->ray_off, b->fill_rs, b->counts);
   PNR_LAUNCH_CHECK();
   const int layers = (qp->kernel_size[0] + 1) / 2;
-  const unsigned gk = grid_for(RS, kQBlock, 256 * 16);
+  // the 3x3x3 kernel indexes cells in 32 bits
+  const bool q3 = layers == 2 && (int64_t)g.dims[0] * g.dims[1] * g.dims[2] < (int64_t(1) << 32);
+  unsigned gk = grid_for(RS, kQBlock, PNR_KNN_GRID);
+  if (gk >= 8) gk &= ~7u;   // whole XCD groups (k_knn's chunk walk)
+  // k_knn's per-XCD chunk counters: the head of the scan scratch, free between
+  // the fill-list and valid-list scans (stream order)
+  if (PNR_KNN_XCD == 2) PNR_HIP(hipMemsetAsync(b->scratch, 0, 8 * sizeof(int32_t), st));
   const int vec = ((uintptr_t)b->pidx & 15) == 0;
   QIndex qi;
   qi.words = h->q_words.as<uint2>();
   qi.rec_off = h->q_rec_off.as<int32_t>();
   qi.recs = h->q_recs.as<float4>();
 #define PNR_KNN(KM)                                                                              \
-  hipLaunchKernelGGL(k_knn<KM>, dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
+  hipLaunchKernelGGL((q3 ? k_knn<KM, 2> : k_knn<KM, 0>), dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
                      qp->radius_limit2, qi, b->slot_d, b->fill_rs, b->pidx, b->vflag,             \
-                     b->ray_vcnt, b->sample_w, b->sample_p, b->counts, vec)
+                     b->ray_vcnt, b->sample_w, b->sample_p, b->counts, vec,                       \
+                     reinterpret_cast<int32_t*>(b->scratch))
   if (qp->K <= 8) PNR_KNN(8);
   else if (qp->K <= 16) PNR_KNN(16);
   else PNR_KNN(32);
