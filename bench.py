@@ -68,6 +68,8 @@ def parse():
                     help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--train-precision", choices=("fp32x3", "fp32"), default="fp32x3",
+                    help="--mode train: the training forward's per-pair chain (fp32x3 split-bf16 MFMA or native fp32)")
     ap.add_argument("--mode", choices=("render", "train"), default="render",
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
@@ -258,6 +260,7 @@ def run_train(args, device):
     points_embeding/color/dir/conf and the aggregator."""
     opt, pts, feats, agg, model = build_scene(args, device)
     agg.train()
+    model.train_precision = args.train_precision
     H = W = args.hw
     cams = cameras(8, H, W)
     dev_cams = [tuple(torch.from_numpy(x).to(device) for x in c) for c in cams]
@@ -299,7 +302,8 @@ def run_train(args, device):
         "metric": "train steps/s (fwd+bwd+Adam, 3600-ray batches), 2M neural points",
         "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32", "data": "synthetic (seeded lego-like point cloud, random target colours)",
+        "dtype": "fp32", "train_forward": args.train_precision,
+        "data": "synthetic (seeded lego-like point cloud, random target colours)",
         "config": {"workload": f"finetune step, {args.train_rays} random rays of {H}x{W} frames, {args.points} points",
                    "K": opt.K, "SR": opt.SR},
         "ray_samples_per_s_M": round(args.train_rays * opt.SR / (ms * 1e-3) / 1e6, 3),

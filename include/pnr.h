@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 8
+#define PNR_ABI_VERSION 9
 
 enum {
   PNR_OK = 0,
@@ -391,6 +391,14 @@ typedef struct {
 int pnr_aggregate_fwd_train(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                             const pnr_agg_saved* saved, float* out_feat, float* out_weight,
                             float* out_conf, void* scratch, size_t scratch_bytes, void* stream);
+/* pnr_aggregate_fwd_train with the per-pair chain (block1.0 pair half, block1.2,
+ * block3.0, block3.2) on the fp32x3 split-bf16 MFMA kernel of pnr_aggregate_fwd_x3
+ * (wx: packed_x3); same saved arrays and outputs, fp32-accurate (not bitwise
+ * the native-fp32 forward).  P1 and the colour branch stay on the fp32 kernels. */
+int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                               const pnr_mlp_x3* wx, const pnr_agg_saved* saved, float* out_feat,
+                               float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
+                               void* stream);
 /* Same, for the PointAggregator.forward mirror (pre-gathered tables, pair_mask). */
 int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                    const uint8_t* pair_mask, const pnr_agg_saved* saved,

@@ -155,7 +155,7 @@ struct SplitW {
 template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
                        const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
-                       float* out_conf, int32_t* tile_ctr, hipStream_t st);
+                       float* out_conf, int32_t* tile_ctr, hipStream_t st, const pnr_agg_saved* sv = nullptr);
 // k_point_pre_h2 (aggregate_x3.hip): P1 = W1[:, :224].[emb, PE_3(emb)] + b1 on
 // f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,

@@ -1382,6 +1382,42 @@ extern "C" int pnr_aggregate_fwd_train(const pnr_points* pts, const pnr_samples*
   return launch(a, as_stream(stream), true);
 }
 
+extern "C" int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                          const pnr_mlp_x3* wx, const pnr_agg_saved* saved, float* out_feat,
+                                          float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
+                                          void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
+  if ((rc = check_saved(saved))) return rc;
+  PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_train_x3: need pers or camera");
+  PNR_CHECK_ARG(s->pidx, "aggregate_train_x3: pidx required");
+  PNR_CHECK_ARG(wx && wx->w1bx && wx->w2x && wx->w3x && wx->w4x, "aggregate_train_x3: null split weight pack");
+  PNR_CHECK_ARG(w->neg_slope >= 0.f && w->neg_slope <= 1.f, "aggregate_train_x3: LeakyReLU slope must be in [0, 1]");
+  PNR_CHECK_ARG((((uintptr_t)wx->w1bx | (uintptr_t)wx->w2x | (uintptr_t)wx->w3x | (uintptr_t)wx->w4x) & 15) == 0,
+                "aggregate_train_x3: split packs must be 16-B aligned");
+  if (s->n_max <= 0) return PNR_OK;
+  AggArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
+  a.sv = *saved;
+  a.hid = saved->hid;
+  a.vmask = saved->vmask;
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  a.pair_mask = nullptr;
+  hipStream_t st = as_stream(stream);
+  // k_point_pre (fp32 P1) -> k_pairs_x3_train (aggregate_x3.hip) -> k_color<true>
+  if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
+  SplitW sw = {{wx->w1bx, wx->w2x, wx->w3x, wx->w4x}, {1.f, 1.f, 1.f, 1.f}, nullptr};
+  if ((rc = launch_pairs_split<false>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
+                                      tile_counter(a, s->n_max), st, saved)))
+    return rc;
+  return launch_t<true>(a, st, kStageColor);
+}
+
 extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                               const uint8_t* pair_mask, const pnr_agg_saved* saved,
                                               float* out_feat, float* out_weight, float* out_conf,

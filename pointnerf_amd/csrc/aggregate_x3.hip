@@ -113,6 +113,7 @@ struct X3Args {
   float* out_weight;
   float* out_conf;
   int32_t* tile_ctr;   // zeroed per launch: tiles past the first gridDim.x are handed out in order
+  pnr_agg_saved sv;    // k_pairs_x3_train: activations kept for the backward (aggregate.hip layout)
 };
 
 // Dynamic tile schedule: each workgroup starts on tile blockIdx.x and takes
@@ -447,6 +448,7 @@ __device__ __forceinline__ void store_group(char* planes, int pstride, int g, in
 // 0, tile start), then pidx / sample positions / dir row (stage 1, S1b), then
 // the point rows and everything computed from them (gather, during block1.2).
 struct GatherState {
+  int64_t tile;
   int64_t row;
   int pid;
   float sw[3], sp[3];
@@ -456,6 +458,7 @@ struct GatherState {
 
 __device__ __forceinline__ void gather_row(const X3Args& A, int64_t tile, int lane, GatherState& g) {
   const int64_t v = tile * kXTS + (lane >> 3);
+  g.tile = tile;
   g.active = v < eff_n(A.s);
   g.row = g.active ? sample_row(A.s, v) : 0;
 }
@@ -471,7 +474,7 @@ __device__ __forceinline__ void gather_sample(const X3Args& A, int lane, GatherS
   g.dmap = A.s.dir_map ? (int64_t)A.s.dir_map[g.row] : g.row;
 }
 
-template <bool H>
+template <bool H, bool TR = false>
 __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, int nb, int nw, char* lds, int pw, int lane,
                                        float (&dr6)[6]) {
   using L = XL<H>;
@@ -558,6 +561,17 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
       if (A.out_weight) A.out_weight[row * K + k] = wn;
       if (A.out_conf) A.out_conf[row * K + k] = confc;
     }
+    if (TR && active) {   // training saves, k_pairs<true>'s layout (aggregate.hip)
+      const int64_t pr = g.tile * kXT + lane;
+      float4* x = reinterpret_cast<float4*>(A.sv.x3e + pr * 32);
+      x[0] = make_float4(ex[0], ex[1], ex[2], ex[3]);
+      x[1] = make_float4(ex[4], ex[5], ex[6], ex[7]);
+#pragma unroll
+      for (int e = 2; e < 8; ++e) x[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      A.sv.wt[pr] = wn * confc;
+      A.sv.wn[pr] = wn;
+      A.sv.prow[pr] = valid ? (int32_t)prow : -1;
+    }
   }
 }
 
@@ -586,13 +600,16 @@ __device__ __forceinline__ void pe_store(char* lds, int lane, int e, float sn, f
   }
 }
 
-template <bool H, int PART>
-__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6]) {
+template <bool H, int PART, bool TR = false>
+__device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const float (&dr6)[6],
+                                          const X3Args* A = nullptr, const GatherState* g = nullptr) {
   using L = XL<H>;
+  float* pe5 = TR && g->active ? A->sv.pe5 + (g->tile * kXT + lane) * 64 : nullptr;   // training: [pair][64]
   if (pw == 0 && PART == 0) {   // rows 60..63: the 4th 16-k step reads them
     char* pz = lds + L::OffPE + (7 * kXT + lane) * 16 + 8;
 #pragma unroll
     for (int pl = 0; pl < L::NPL; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
+    if (TR && pe5) *reinterpret_cast<float4*>(pe5 + 60) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (PNR_ABLATE & 2) return;
   const int mine = __builtin_amdgcn_readfirstlane(PART == 0 ? pw : 4 + pw);
@@ -610,6 +627,11 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
     pe_store<H>(lds, lane, 5 * ch + 2, s2, c2);
     pe_store<H>(lds, lane, 5 * ch + 3, s3, c3);
     pe_store<H>(lds, lane, 5 * ch + 4, s4, c4);
+    if (TR && pe5) {
+      const float sv[10] = {s0, c0, s1, c1, s2, c2, s3, c3, s4, c4};
+#pragma unroll
+      for (int i = 0; i < 10; i += 2) *reinterpret_cast<float2*>(pe5 + 10 * ch + i) = make_float2(sv[i], sv[i + 1]);
+    }
   }
 }
 
@@ -627,7 +649,7 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
 // overlaps; the P1 rows travel during block3.0 / block3.2.
 #define X3_SYNC() __syncthreads()
 
-template <bool H>
+template <bool H, bool TR = false>
 __device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int buf, int64_t tile, int lane) {
   using L = XL<H>;
   if (PNR_ABLATE & 4) return;
@@ -640,13 +662,41 @@ __device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int b
   const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
   const float alpha_s = xor8_sum(wtL[lane] * alpha_k);   // point_aggregators.py:608-614
   const int64_t vo = tile * kXTS + j;
+  if (TR && vo < n) A.sv.pa[tile * kXT + lane] = pa;
   if (k == 0 && vo < n) {
     A.vmask[vo] = sflag[j];
     if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
   }
 }
 
-template <bool H>
+// Training save of a layer's pre-activations (x3, scale 1): lrelu -> dst[pair][256]
+// and the LeakyReLU derivative bits mask[pair][16 layer + 2T + h] (bit r: register
+// r of neuron tile T, lane half h), the layout of aggregate.hip's save_pairs_q.
+__device__ __forceinline__ void save_act_train(const X3Args& A, const f32x16 (&acc)[4], float* dst, int layer,
+                                               int64_t tile, int64_t n, float neg, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) {
+    const int col = 32 * pt + c;
+    if (tile * kXTS + (col >> 3) >= n) continue;
+    const int64_t pr = tile * kXT + col;
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+      const f32x16& v = acc[2 * pt + T];
+      unsigned bits = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(dst + pr * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
+            make_float4(lrelu(v[4 * q], neg), lrelu(v[4 * q + 1], neg), lrelu(v[4 * q + 2], neg),
+                        lrelu(v[4 * q + 3], neg));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bits |= (v[r] > 0.f ? 1u : 0u) << r;
+      A.sv.mask[pr * 64 + 16 * layer + 2 * (T0 + T) + h] = (uint16_t)bits;
+    }
+  }
+}
+
+template <bool H, bool TR = false>
 __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wid, int lane) {
   using L = XL<H>;
   const int c = lane & 31, h = lane >> 5;
@@ -710,6 +760,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
     X3_TR(0, 3);
     store_act<H>(acc, XP, neg, 1.f, lane, T0);
+    if constexpr (TR) save_act_train(A, acc, A.sv.h1, 0, tile, n, neg, lane, T0);
     X3_TR(0, 15);   // (store_act alone, tools/x3_trace.py)
     if (wid == 0) {
 #pragma unroll
@@ -730,6 +781,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     X3_SYNC();   // S3
     X3_TR(0, 7);
     store_act<H>(acc, XP, neg, sc2, lane, T0);
+    if constexpr (TR) save_act_train(A, acc, A.sv.h2, 1, tile, n, neg, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
       const float* exL = reinterpret_cast<const float*>(lds + L::OffEx) + buf * 8 * kXT;
       float ex[8];
@@ -748,6 +800,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     X3_SYNC();   // S5
     X3_TR(0, 10);
     store_act<H>(acc, XP, neg, sc3, lane, T0);
+    if constexpr (TR) save_act_train(A, acc, A.sv.h3, 2, tile, n, neg, lane, T0);
     if (wid == 0 && !H) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl)
@@ -776,6 +829,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                 make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
           }
     } else if (!(PNR_ABLATE & 4)) {
+      if constexpr (TR) save_act_train(A, acc, A.sv.h4, 3, tile, n, neg, lane, T0);
       const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + buf * kXT;
       const int* sflag = reinterpret_cast<const int*>(lds + L::OffSf) + buf * kXTS;
       float pa_part[2] = {0.f, 0.f};
@@ -957,7 +1011,7 @@ __device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int sl
   }
 }
 
-template <bool H>
+template <bool H, bool TR = false>
 __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw, int lane) {
   using L = XL<H>;
   const int64_t n = eff_n(A.s);
@@ -971,9 +1025,9 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   GatherState g;
   gather_row(A, first_tile(ntiles), lane, g);
   gather_sample(A, lane, g);
-  gather<H>(A, g, 0, 0, lds, pw, lane, dr6);
-  pe_planes<H, 0>(lds, pw, lane, dr6);
-  pe_planes<H, 1>(lds, pw, lane, dr6);
+  gather<H, TR>(A, g, 0, 0, lds, pw, lane, dr6);
+  pe_planes<H, 0, TR>(lds, pw, lane, dr6, &A, &g);
+  pe_planes<H, 1, TR>(lds, pw, lane, dr6, &A, &g);
   int* TQ = reinterpret_cast<int*>(lds + L::OffTq);
   if (pw == 0 && lane == 0) TQ[1] = (int)take_tile(A, ntiles);
   X3_SYNC();   // P0: prow of the first tile visible to all producers, TQ[1] too
@@ -996,14 +1050,14 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_TR(1, 1);
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
-    if (!H && pw == 0 && it > 0) finalize_alpha<H>(A, lds, nbuf, prev, lane);
+    if (!H && pw == 0 && it > 0) finalize_alpha<H, TR>(A, lds, nbuf, prev, lane);
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
     X3_TR(1, 2);
     // during block1.2: gather of the next tile (its slots are free: their last
     // readers were the previous finalize / tail)
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H>(A, g, nbuf, nw, lds, pw, lane, dr6);
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H, TR>(A, g, nbuf, nw, lds, pw, lane, dr6);
     if constexpr (H)   // first half of the previous tile's tail
       if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
     X3_TR(1, 3);
@@ -1013,7 +1067,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
       p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
     X3_TR(1, 4);
     X3_SYNC();   // S4
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 0>(lds, pw, lane, dr6);   // during block3.0 (PE planes free since S1)
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 0, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.0 (PE planes free since S1)
     // (h2) during block3.0: the second half of the previous tile's tail (its
     // accumulators are overwritten after this tile's S6)
     if constexpr (H)
@@ -1021,7 +1075,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     X3_SYNC();   // S5
     X3_TR(1, 5);
     X3_SYNC();   // S6
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 1>(lds, pw, lane, dr6);   // during block3.2
+    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 1, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.2
     X3_SYNC();   // S7
   }
   if constexpr (H) {
@@ -1032,11 +1086,11 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     }
     if (A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
   } else {
-    if (pw == 0 && it > 0) finalize_alpha<H>(A, lds, (it - 1) & 1, prev, lane);
+    if (pw == 0 && it > 0) finalize_alpha<H, TR>(A, lds, (it - 1) & 1, prev, lane);
   }
 }
 
-template <bool H>
+template <bool H, bool TR = false>
 __device__ __forceinline__ void pairs_body(const X3Args& A) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1044,14 +1098,16 @@ __device__ __forceinline__ void pairs_body(const X3Args& A) {
   if (threadIdx.x < kHid) reinterpret_cast<float*>(lds + XL<H>::OffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
   if (wid < 4) {
     X3_SYNC();   // P0
-    consumer_loop<H>(A, lds, wid, lane);
+    consumer_loop<H, TR>(A, lds, wid, lane);
   } else {
-    producer_loop<H>(A, lds, wid - 4, lane);
+    producer_loop<H, TR>(A, lds, wid - 4, lane);
   }
 }
 
 __global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) { pairs_body<false>(A); }
 __global__ void __launch_bounds__(512, 1) k_pairs_h2(X3Args A) { pairs_body<true>(A); }
+// training forward (pnr_aggregate_fwd_train_x3): k_pairs_x3 + the saves of k_pairs<true>
+__global__ void __launch_bounds__(512, 1) k_pairs_x3_train(X3Args A) { pairs_body<false, true>(A); }
 
 // ---------------------------------------------------------------------------
 // k_color_h2: the colour branch 280 -> 128 -> 128 -> 128 (LeakyReLU each,
@@ -1085,6 +1141,7 @@ struct ColH2Args {
 // (k_pairs_h2 stored the planes).  Wave w copies plane w.
 template <int G0, int NG>
 __device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t tile) {
+  if (PNR_ABLATE & 16384) return;   // timing only: no hid loads (stale planes)
   const int lane = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const char* src = reinterpret_cast<const char*>(A.hid) + tile * kHidTile + lane * 16;
 #pragma unroll
@@ -1191,7 +1248,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int64_t v = v0 + 32 * pt + c;
-      if (!((vm >> (32 * pt + c)) & 1)) continue;
+      if (!((vm >> (32 * pt + c)) & 1) || (PNR_ABLATE & 32768)) continue;   // (32768: timing only, no stores)
       float* o = A.out_feat + v * (kC + 1) + 1;
 #pragma unroll
       for (int T = 0; T < 2; ++T)
@@ -1360,12 +1417,14 @@ extern "C" __attribute__((visibility("default"))) int pnr_debug_x3_blocks(unsign
 template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
                        const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
-                       float* out_conf, int32_t* tile_ctr, hipStream_t st) {
-  const void* fn = H ? reinterpret_cast<const void*>(&k_pairs_h2) : reinterpret_cast<const void*>(&k_pairs_x3);
-  static bool attr = false;
-  if (!attr) {
+                       float* out_conf, int32_t* tile_ctr, hipStream_t st, const pnr_agg_saved* sv) {
+  PNR_CHECK_ARG(!(H && sv), "pairs_split: training saves are x3-only");
+  const void* fn = H ? reinterpret_cast<const void*>(&k_pairs_h2)
+                     : (sv ? reinterpret_cast<const void*>(&k_pairs_x3_train) : reinterpret_cast<const void*>(&k_pairs_x3));
+  static bool attr[2] = {false, false};
+  if (!attr[sv ? 1 : 0]) {
     PNR_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)XL<H>::Lds));
-    attr = true;
+    attr[sv ? 1 : 0] = true;
   }
   X3Args a;
   a.pts = pts;
@@ -1379,10 +1438,14 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   a.tile_ctr = tile_ctr;
+  if (sv) a.sv = *sv;
+  else memset(&a.sv, 0, sizeof(a.sv));
   PNR_HIP(hipMemsetAsync(tile_ctr, 0, 8 * sizeof(int32_t), st));
   const int64_t tiles = cdiv(s.n_max, kXTS);
   if (H)
     hipLaunchKernelGGL(k_pairs_h2, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
+  else if (sv)
+    hipLaunchKernelGGL(k_pairs_x3_train, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
   else
     hipLaunchKernelGGL(k_pairs_x3, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
   PNR_LAUNCH_CHECK();
@@ -1390,9 +1453,9 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
 }
 template int launch_pairs_split<false>(const pnr_points&, const pnr_samples&, const pnr_mlp&, const SplitW&,
                                        const float*, float*, int32_t*, float*, float*, float*, int32_t*,
-                                       hipStream_t);
+                                       hipStream_t, const pnr_agg_saved*);
 template int launch_pairs_split<true>(const pnr_points&, const pnr_samples&, const pnr_mlp&, const SplitW&,
                                       const float*, float*, int32_t*, float*, float*, float*, int32_t*,
-                                      hipStream_t);
+                                      hipStream_t, const pnr_agg_saved*);
 
 }  // namespace pnr

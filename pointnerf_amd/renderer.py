@@ -167,6 +167,10 @@ class NeuralPointsRayMarching(nn.Module):
         if precision not in PRECISIONS:
             raise L.PnrError(f"precision {precision!r}: one of {PRECISIONS}")
         self.precision = precision
+        # render_rays_train's per-pair forward: "fp32x3" (split-bf16 MFMA,
+        # fp32-accurate, the default) or "fp32" (native fp32 MFMA)
+        self.train_precision = "fp32x3"
+        self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
         self.h2_fallbacks = 0
         self.opt = opt
@@ -520,8 +524,11 @@ class NeuralPointsRayMarching(nn.Module):
         # block1.0's point half only for the points this batch references
         from .train import used_points
         used = used_points(bufs.pidx[:cnt["S_filled"] * K], n)
+        if self.train_precision not in ("fp32", "fp32x3"):
+            raise L.PnrError(f"train_precision {self.train_precision!r}: 'fp32x3' or 'fp32'")
         spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd),
-                       used=used)
+                       used=used, x3=self.train_precision == "fp32x3")
+        spec.keep_saved = self.keep_train_saved
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
                                  tab(np_.points_dir, 3), tab(np_.points_conf, 1), *agg_params(self.aggregator))
         if C == 3:
@@ -533,6 +540,8 @@ class NeuralPointsRayMarching(nn.Module):
         # zero_one loss (point_aggregators.py:810-816): gradiant_clamp of the
         # gathered conf, empty slots gather point 0 (torch.clamp(pidx, 0))
         self.last_train_aux = {}
+        if self.keep_train_saved:
+            self.last_train_aux["saved"] = spec.saved
         if np_.points_conf is not None:
             Rv = cnt["R_valid"]
             f32 = dict(dtype=torch.float32, device=dev)

@@ -1,7 +1,9 @@
 """Autograd through the HIP path (the per-scene finetune step).
 
 ``AggregateFn`` and ``CompositeFn`` are torch.autograd.Functions whose forward
-runs ``pnr_aggregate_fwd_train`` / ``pnr_composite_fwd`` and whose backward runs
+runs ``pnr_aggregate_fwd_train`` (native-fp32 MFMA) or ``pnr_aggregate_fwd_train_x3``
+(the per-pair chain on the fp32x3 split-bf16 MFMA kernel, the training default)
+/ ``pnr_composite_fwd`` and whose backward runs
 
   colour branch backward      weight gradients on pnr_gemm_tn_x3, the small dX
                               products (n x 128 x 128) on hipBLASLt (torch.matmul)
@@ -92,8 +94,10 @@ def _lrelu_grad(dy, h, slope):
 class AggSpec:
     """Non-tensor description of one aggregate call (structs + keep-alive)."""
 
-    def __init__(self, agg, samples: L.Samples, n: int, pts_extra: dict, pair_mask=None, keep=(), used=None):
+    def __init__(self, agg, samples: L.Samples, n: int, pts_extra: dict, pair_mask=None, keep=(), used=None,
+                 x3: bool = False):
         self.agg, self.samples, self.n = agg, samples, int(n)
+        self.x3 = bool(x3)              # per-pair chain on pnr_aggregate_fwd_train_x3 (fp32x3 split MFMA)
         self.used = used                # optional (used[int32], used_map[int32]) point subset
         self.pts_extra = pts_extra      # xyz / pers / campos / camrot pointers (no grad)
         self.pair_mask = pair_mask
@@ -126,7 +130,14 @@ class AggregateFn(torch.autograd.Function):
         sv = Saved(n_max, dev)
         feat = torch.zeros((max(n_max, 1), 129), dtype=torch.float32, device=dev)
         scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
-        if spec.pair_mask is None:
+        keepx = None
+        if spec.pair_mask is None and spec.x3:
+            wx, keepx = agg.packed_x3()
+            L.check(L.lib().pnr_aggregate_fwd_train_x3(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
+                                                       ctypes.byref(wx), ctypes.byref(sv.c), L.ptr(feat), None, None,
+                                                       L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
+                    "pnr_aggregate_fwd_train_x3")
+        elif spec.pair_mask is None:
             L.check(L.lib().pnr_aggregate_fwd_train(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
                                                     ctypes.byref(sv.c), L.ptr(feat), None, None, L.ptr(scratch),
                                                     scratch.numel() * 4, L.stream_ptr(dev)),
@@ -137,7 +148,9 @@ class AggregateFn(torch.autograd.Function):
                                                            None, None, L.ptr(scratch), scratch.numel() * 4,
                                                            L.stream_ptr(dev)),
                     "pnr_aggregate_fwd_train_masked")
-        ctx.spec, ctx.sv, ctx.pts, ctx.tabs, ctx.mlp, ctx.keepw = spec, sv, pts, tabs, mlp, keepw
+        ctx.spec, ctx.sv, ctx.pts, ctx.tabs, ctx.mlp, ctx.keepw = spec, sv, pts, tabs, mlp, (keepw, keepx)
+        if getattr(spec, "keep_saved", False):
+            spec.saved = sv                 # tests: the kept activations of this forward
         ctx.has = (color is not None, dirs is not None, conf is not None)
         ctx.shapes = (emb.shape, None if conf is None else conf.shape)
         ctx.save_for_backward(*params)

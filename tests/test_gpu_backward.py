@@ -78,12 +78,16 @@ def _train_model(sc, cuda, params):
     return NeuralPointsRayMarching(sc["opt"], np_, agg.train())
 
 
-def test_render_train_grads_vs_oracle(cuda):
+@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])
+def test_render_train_grads_vs_oracle(cuda, train_precision):
     """End to end: loss = <G, ray_color> through query -> aggregate -> composite;
-    every point-table and MLP gradient vs torch autograd of the CPU oracle."""
+    every point-table and MLP gradient vs torch autograd of the CPU oracle, with
+    the training forward's per-pair chain on native fp32 MFMA and on the fp32x3
+    split kernel (the default)."""
     sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
     params = formula_params(salt=0.3)
     m = _train_model(sc, cuda, params)
+    m.train_precision = train_precision
     campos = torch.from_numpy(sc["campos"]).to(cuda)
     camrot = torch.from_numpy(sc["camrot"]).to(cuda)
     rd = torch.from_numpy(sc["raydir"]).to(cuda)
@@ -133,6 +137,41 @@ def test_render_train_grads_vs_oracle(cuda):
         # slope than on the CPU (forward sums differ in order)
         check(p.grad, pp[k].grad, "d " + k, scale=3e-4)
     assert not errs, errs
+
+
+def test_train_forward_x3_saves_match_fp32(cuda):
+    """pnr_aggregate_fwd_train_x3 keeps the same activations as the native-fp32
+    training forward: point rows and vmask equal; gather-side floats (the two
+    kernels are separate compilation units whose FMA contraction of the distance
+    terms may differ in the last bit) within 1e-6, PE_5 within 3e-5 (band 4
+    multiplies an argument ulp by 16); h1..h4 / alpha pre-activation / hid within fp32 accumulation noise;
+    LeakyReLU derivative bits equal except where the pre-activation is within
+    that noise of 0."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.45))
+    m.keep_train_saved = True
+    campos, camrot = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    out = {}
+    for tp in ("fp32", "fp32x3"):
+        m.train_precision = tp
+        color = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0]
+        out[tp] = (color.detach().clone(), m.last_train_aux["saved"], int(m.last_counts["S_valid"]))
+    (c32, s32, n), (c3, s3, n3) = out["fp32"], out["fp32x3"]
+    assert n == n3 and n > 100
+    P = n * 8
+    assert torch.equal(s32["prow"][:P], s3["prow"][:P])
+    assert torch.equal(s32["vmask"][:n], s3["vmask"][:n])
+    for k in ("x3e", "wt", "wn"):
+        close(s3[k][:P], s32[k][:P], k, rel=1e-5, scale=1e-6)
+    close(s3["pe5"][:P], s32["pe5"][:P], "pe5", rel=0, scale=3e-5)
+    for k, rows in (("h1", P), ("h2", P), ("h3", P), ("h4", P), ("pa", P), ("hid", n)):
+        a, b = s3[k][:rows], s32[k][:rows]
+        close(a, b, k, rel=1e-4, scale=2e-6)
+    bits = (s32["mask"][:P].int() ^ s3["mask"][:P].int())
+    flips = int(sum(int(((bits >> i) & 1).sum()) for i in range(16)))
+    assert flips <= 1e-5 * P * 1024, flips
+    close(c3, c32, "ray_color", rel=1e-4, scale=1e-6)
 
 
 def test_train_step_reduces_loss(cuda):
