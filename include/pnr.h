@@ -419,6 +419,17 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             const float* d_feat, const float* d_hid, float* dz1, float* dz2,
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
+/* Same, with the three dX GEMMs on fp32x3 split-bf16 MFMA: wbx = frag_pack_x3 of
+ * block3.2.weight^T, block3.0.weight[:, :256]^T, block1.2.weight^T (aggregator.py;
+ * 16-B aligned); wb supplies w3e (w4t / w3t / w2t unused, may be NULL). */
+typedef struct {
+  const void* w4tx; const void* w3tx; const void* w2tx;
+} pnr_mlp_bwd_x3;
+int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                               const pnr_mlp_bwd* wb, const pnr_mlp_bwd_x3* wbx, const pnr_agg_saved* saved,
+                               const float* d_feat, const float* d_hid, float* dz1, float* dz2, float* dz3,
+                               float* dz4, float* dpa, float* d_p1, float* d_color, float* d_dir,
+                               float* d_conf, void* stream);
 
 /* Weight-gradient GEMM (replaces the dW = dY^T X of torch's nn.Linear autograd
  * for block1.0/1.2/3.0/3.2, point_aggregators.py:276-348 trained by

@@ -113,6 +113,10 @@ class MlpBwd(ctypes.Structure):
     _fields_ = [("w4t", c_void_p), ("w3t", c_void_p), ("w2t", c_void_p), ("w3e", c_void_p)]
 
 
+class MlpBwdX3(ctypes.Structure):
+    _fields_ = [("w4tx", c_void_p), ("w3tx", c_void_p), ("w2tx", c_void_p)]
+
+
 P = ctypes.POINTER
 # name -> (restype, argtypes); exactly the functions include/pnr.h declares.
 SIGNATURES = {
@@ -149,6 +153,9 @@ SIGNATURES = {
     "pnr_aggregate_bwd_pairs": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(AggSaved), c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_aggregate_bwd_pairs_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(MlpBwdX3), P(AggSaved),
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_gemm_tn_scratch_bytes": (c_int, [c_int64, c_int32, c_int32, P(c_size_t)]),
     "pnr_gemm_tn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),

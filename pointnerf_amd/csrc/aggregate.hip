@@ -847,6 +847,7 @@ struct BwdArgs {
   float* d_color;        // [N,3] (+=) or null
   float* d_dir;          // [N,3] (+=) or null
   float* d_conf;         // [N]   (+=) or null
+  const void* wx[3];     // k_pairs_bwd<true>: frag_pack_x3 of W4^T, W3[:, :256]^T, W2^T
 };
 
 constexpr int kBwdLdsFloats = 66 * kQP + 4 * kTP /*dot parts*/ + 4 * 7 * kTP /*extras parts*/;
@@ -943,6 +944,97 @@ __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsign
   }
 }
 
+// ---- fp32x3 dX GEMMs of k_pairs_bwd<true>: the transposed weights as exact
+// 3-way bf16 splits (frag_pack_x3: F[t][T][plane][lane][8], X3_PAD zero steps),
+// the B fragments read from the fp32 quad rows and split into three bf16
+// planes in registers (split2, exact), six cross products per 16-k step on
+// v_mfma_f32_32x32x16_bf16 (smallest first) -- the arithmetic of the fp32x3
+// forward (aggregate_x3.hip) on k_pairs_bwd's LDS layout.
+constexpr int kX3D = 3;   // weight ring depth (k-steps in flight) <= X3_PAD
+struct X3QRing {
+  uint4 a[kX3D][2][3];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x3q_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+// this wave's two neuron tiles of k-step t, three planes each; voff = (T0 * 3 * 64 + lane) * 16
+__device__ __forceinline__ void x3q_load(uint4 (&a)[2][3], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
+#pragma unroll
+  for (int T = 0; T < 2; ++T)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      a[T][pl] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + pl * 1024,
+                                                                                   (t * 8 + T) * 3 * 1024, 0));
+}
+
+__device__ __forceinline__ void x3q_prime(X3QRing& w, __amdgpu_buffer_rsrc_t rs, int voff) {
+#pragma unroll
+  for (int d = 0; d < kX3D; ++d) x3q_load(w.a[d], rs, voff, d);
+}
+
+// B fragment of k-step t, pair half pt: inputs 16t + 8h .. +7 of pair 32pt + c
+// (quad rows 4t + 2h, 4t + 2h + 1; each float4 holds neurons (0, 2, 1, 3))
+__device__ __forceinline__ void x3q_b(const float* X, int t, int pt, int lane, uint4 (&b)[3]) {
+  const int c = lane & 31, h = lane >> 5;
+  const float* xb = X + (4 * t + 2 * h) * kQP + 4 * (32 * pt + c);
+  const float4 q0 = *reinterpret_cast<const float4*>(xb);
+  const float4 q1 = *reinterpret_cast<const float4*>(xb + kQP);
+  unsigned w0[4], w1[4], w2[4];
+  split2(q0.x, q0.z, w0[0], w1[0], w2[0]);
+  split2(q0.y, q0.w, w0[1], w1[1], w2[1]);
+  split2(q1.x, q1.z, w0[2], w1[2], w2[2]);
+  split2(q1.y, q1.w, w0[3], w1[3], w2[3]);
+  b[0] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
+  b[1] = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+  b[2] = make_uint4(w2[0], w2[1], w2[2], w2[3]);
+}
+
+// acc[2 pt + T] += W^T . X over nsteps 16-k steps (weights kX3D steps ahead
+// in the ring, the next step's B split while this step's MFMAs run)
+__device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], X3QRing& w, __amdgpu_buffer_rsrc_t rs, int voff,
+                                              const float* X, int nsteps, int lane) {
+  uint4 b[2][3];
+  x3q_b(X, 0, 0, lane, b[0]);
+  x3q_b(X, 0, 1, lane, b[1]);
+  auto step = [&](uint4 (&a)[2][3], int t) {
+    uint4 bn[2][3];
+    const int tn = t + 1 < nsteps ? t + 1 : t;
+    x3q_b(X, tn, 0, lane, bn[0]);
+    x3q_b(X, tn, 1, lane, bn[1]);
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        f32x16 v = acc[2 * pt + T];
+        v = mfma_bf16(a[T][2], b[pt][0], v);   // W2.X0
+        v = mfma_bf16(a[T][1], b[pt][1], v);   // W1.X1
+        v = mfma_bf16(a[T][0], b[pt][2], v);   // W0.X2
+        v = mfma_bf16(a[T][1], b[pt][0], v);   // W1.X0
+        v = mfma_bf16(a[T][0], b[pt][1], v);   // W0.X1
+        v = mfma_bf16(a[T][0], b[pt][0], v);   // W0.X0
+        acc[2 * pt + T] = v;
+      }
+    }
+    x3q_load(a, rs, voff, t + kX3D);   // packs carry kX3D zero steps
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) b[pt][pl] = bn[pt][pl];
+  };
+  int t = 0;
+#pragma unroll 1
+  for (; t + kX3D <= nsteps; t += kX3D) {
+#pragma unroll
+    for (int d = 0; d < kX3D; ++d) step(w.a[d], t + d);
+  }
+#pragma unroll
+  for (int d = 0; d < kX3D - 1; ++d)
+    if (t + d < nsteps) step(w.a[d], t + d);
+}
+
+template <bool X3>
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   float* X = lds_dyn;                   // quad rows [66][kQP]
@@ -958,11 +1050,17 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   float Rw[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
-  const float* w4t = A.wb.w4t + T0 * 64;
-  const float* w3t = A.wb.w3t + T0 * 64;
-  const float* w2t = A.wb.w2t + T0 * 64;
+  const float* w4t = X3 ? nullptr : A.wb.w4t + T0 * 64;
+  const float* w3t = X3 ? nullptr : A.wb.w3t + T0 * 64;
+  const float* w2t = X3 ? nullptr : A.wb.w2t + T0 * 64;
   float ring[kQD][kNTW];
-  prime_q<kNTW>(ring, w4t, lane);
+  X3QRing xr;
+  const int xvoff = (T0 * 3 * 64 + lane) * 16;
+  const __amdgpu_buffer_rsrc_t x4 = x3q_rsrc(A.wx[0]), x3 = x3q_rsrc(A.wx[1]), x2 = x3q_rsrc(A.wx[2]);
+  if constexpr (X3)
+    x3q_prime(xr, x4, xvoff);
+  else
+    prime_q<kNTW>(ring, w4t, lane);
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // ---------------------------------------------------------- per-pair scalars (lane = pair)
@@ -1034,8 +1132,13 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     unsigned mk[kPTW * kNTW];
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 2, tile, n, lane, T0);
-    mlp_layer_q<kNTW, kPTW>(acc, ring, w4t, X, 128, lane);
-    prime_q<kNTW>(ring, w3t, lane);
+    if constexpr (X3) {
+      mlp_layer_x3q(acc, xr, x4, xvoff, X, 16, lane);
+      x3q_prime(xr, x3, xvoff);
+    } else {
+      mlp_layer_q<kNTW, kPTW>(acc, ring, w4t, X, 128, lane);
+      prime_q<kNTW>(ring, w3t, lane);
+    }
     __syncthreads();
     lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[2], tile, n, slope, lane, T0);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
@@ -1063,8 +1166,13 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 1, tile, n, lane, T0);
-    mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
-    prime_q<kNTW>(ring, w2t, lane);
+    if constexpr (X3) {
+      mlp_layer_x3q(acc, xr, x3, xvoff, X, 16, lane);
+      x3q_prime(xr, x2, xvoff);
+    } else {
+      mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
+      prime_q<kNTW>(ring, w2t, lane);
+    }
     // colour / dir gradients of the pair (wave 0, lane = pair; exP is not
     // overwritten before the next tile's barrier)
     if (wid == 0 && active) {
@@ -1102,8 +1210,13 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 0, tile, n, lane, T0);
-    mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
-    prime_q<kNTW>(ring, w4t, lane);   // the next tile
+    if constexpr (X3) {
+      mlp_layer_x3q(acc, xr, x2, xvoff, X, 16, lane);
+      x3q_prime(xr, x4, xvoff);   // the next tile
+    } else {
+      mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
+      prime_q<kNTW>(ring, w4t, lane);   // the next tile
+    }
     lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[0], tile, n, slope, lane, T0);
     // block1.0 point half: d P1[p] += dz1 (the P1 gather's backward).  dz1 goes
     // through LDS so each pair's 1-KB row is added with 4 coalesced 256-B
@@ -1444,15 +1557,17 @@ extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_s
   return launch(a, as_stream(stream), true);
 }
 
-extern "C" int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
-                                       const pnr_mlp_bwd* wb, const pnr_agg_saved* saved,
-                                       const float* d_feat, const float* d_hid, float* dz1, float* dz2,
-                                       float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
-                                       float* d_dir, float* d_conf, void* stream) {
+static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_bwd* wb,
+                     const pnr_mlp_bwd_x3* wbx, const pnr_agg_saved* saved, const float* d_feat,
+                     const float* d_hid, float* dz1, float* dz2, float* dz3, float* dz4, float* dpa, float* d_p1,
+                     float* d_color, float* d_dir, float* d_conf, void* stream) {
   int rc;
   PNR_CHECK_ARG(pts && s && w && wb, "aggregate_bwd: null pointer");
   if ((rc = check_saved(saved))) return rc;
-  PNR_CHECK_ARG(wb->w4t && wb->w3t && wb->w2t && wb->w3e && w->wa, "aggregate_bwd: null weight");
+  PNR_CHECK_ARG(wb->w3e && w->wa && (wbx || (wb->w4t && wb->w3t && wb->w2t)), "aggregate_bwd: null weight");
+  PNR_CHECK_ARG(!wbx || (wbx->w4tx && wbx->w3tx && wbx->w2tx &&
+                         (((uintptr_t)wbx->w4tx | (uintptr_t)wbx->w3tx | (uintptr_t)wbx->w2tx) & 15) == 0),
+                "aggregate_bwd_x3: null or unaligned split weight pack");
   PNR_CHECK_ARG(d_feat && d_hid && dz1 && dz2 && dz3 && dz4 && dpa && d_p1, "aggregate_bwd: null buffer");
   PNR_CHECK_ARG((((uintptr_t)d_hid | (uintptr_t)dz1 | (uintptr_t)dz2 | (uintptr_t)dz3 | (uintptr_t)dz4) & 15) == 0,
                 "aggregate_bwd: gradient buffers must be 16-B aligned");
@@ -1462,7 +1577,9 @@ extern "C" int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples*
   hipStream_t st = as_stream(stream);
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBwdLdsBytes));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBwdLdsBytes));
     attr = true;
   }
@@ -1483,10 +1600,37 @@ extern "C" int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples*
   a.d_color = d_color;
   a.d_dir = d_dir;
   a.d_conf = d_conf;
+  a.wx[0] = wbx ? wbx->w4tx : nullptr;
+  a.wx[1] = wbx ? wbx->w3tx : nullptr;
+  a.wx[2] = wbx ? wbx->w2tx : nullptr;
   const int64_t tiles = cdiv(s->n_max, kTS);
-  hipLaunchKernelGGL(k_pairs_bwd, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes, st, a);
+  if (wbx)
+    hipLaunchKernelGGL(k_pairs_bwd<true>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
+                       st, a);
+  else
+    hipLaunchKernelGGL(k_pairs_bwd<false>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
+                       st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
+}
+
+extern "C" int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                       const pnr_mlp_bwd* wb, const pnr_agg_saved* saved,
+                                       const float* d_feat, const float* d_hid, float* dz1, float* dz2,
+                                       float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
+                                       float* d_dir, float* d_conf, void* stream) {
+  return bwd_pairs(pts, s, w, wb, nullptr, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
+                   d_conf, stream);
+}
+
+extern "C" int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                          const pnr_mlp_bwd* wb, const pnr_mlp_bwd_x3* wbx,
+                                          const pnr_agg_saved* saved, const float* d_feat, const float* d_hid,
+                                          float* dz1, float* dz2, float* dz3, float* dz4, float* dpa, float* d_p1,
+                                          float* d_color, float* d_dir, float* d_conf, void* stream) {
+  PNR_CHECK_ARG(wbx, "aggregate_bwd_x3: null split weight packs");
+  return bwd_pairs(pts, s, w, wb, wbx, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
+                   d_conf, stream);
 }
 
 extern "C" int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* stream) {

@@ -341,15 +341,18 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
   // XCD): XCD x walks the contiguous chunk range [C x / 8, C (x + 1) / 8) of the
   // sample list, so at any moment its L2 holds the records of a few image rows
   // instead of every XCD touching the same wide window (A/B in DESIGN.md 13).
+  // PNR_KNN_XCD 2: chunks handed out in order by a per-XCD counter, and an XCD
+  // whose range is exhausted takes chunks from the next XCDs' ranges (the
+  // bands' per-sample costs differ, so static ranges finish unevenly).  Small
+  // launches (a training batch's few hundred chunks) walk the plain grid
+  // stride: there the counters' contention costs more than the locality gains.
   const int64_t C = (S + kQBlock - 1) / kQBlock;
-  const bool xcd = PNR_KNN_XCD && (gridDim.x & 7) == 0;
+  const bool whole = (gridDim.x & 7) == 0;
+  const bool dyn = PNR_KNN_XCD == 2 && whole && C >= 4 * (int64_t)gridDim.x;
+  const bool xcd = dyn || (PNR_KNN_XCD == 1 && whole);
   const int xg = xcd ? (int)(blockIdx.x & 7) : 0;
   const int64_t c_lo = xcd ? C * xg / 8 : 0, c_hi = xcd ? C * (xg + 1) / 8 : C;
   const int64_t c_step = xcd ? gridDim.x / 8 : gridDim.x;
-  // PNR_KNN_XCD 2: chunks handed out in order by a per-XCD counter, and an XCD
-  // whose range is exhausted takes chunks from the next XCDs' ranges (the
-  // bands' per-sample costs differ, so static ranges finish unevenly).
-  const bool dyn = PNR_KNN_XCD == 2 && xcd;
   __shared__ int64_t s_ch;
   auto next_chunk = [&](int64_t prev) -> int64_t {
     if (!dyn) return prev < 0 ? c_lo + (xcd ? blockIdx.x >> 3 : blockIdx.x) : prev + c_step;
@@ -358,8 +361,10 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
       int64_t got = C;
       for (int k = 0; k < 8 && got == C; ++k) {
         const int y = (xg + k) & 7;
-        const int64_t t = C * y / 8 + atomicAdd(xcd_ctr + y, 1);
-        if (t < C * (y + 1) / 8) got = t;
+        const int64_t lo = C * y / 8, hi = C * (y + 1) / 8;
+        if (lo + *reinterpret_cast<volatile const int32_t*>(xcd_ctr + y) >= hi) continue;   // exhausted: no RMW
+        const int64_t t = lo + atomicAdd(xcd_ctr + y, 1);
+        if (t < hi) got = t;
       }
       s_ch = got;
     }

@@ -7,7 +7,9 @@ runs ``pnr_aggregate_fwd_train`` (native-fp32 MFMA) or ``pnr_aggregate_fwd_train
 
   colour branch backward      weight gradients on pnr_gemm_tn_x3, the small dX
                               products (n x 128 x 128) on hipBLASLt (torch.matmul)
-  pnr_aggregate_bwd_pairs     fused per-pair dX chain on MFMA (k_pairs_bwd): alpha
+  pnr_aggregate_bwd_pairs     fused per-pair dX chain on MFMA (k_pairs_bwd; with
+  (_x3)                       train_precision fp32x3 its three dX GEMMs on split-bf16
+                              MFMA, fp32-accurate): alpha
                               branch + K-sum backward, block3.2^T / block3.0^T /
                               block1.2^T, LeakyReLU masks, weight / conf / colour /
                               dir gradients, scatter-add of dz1 into the per-point
@@ -31,7 +33,7 @@ import ctypes
 import torch
 
 from . import _lib as L
-from .aggregator import frag_pack
+from .aggregator import frag_pack, frag_pack_x3
 
 _PARAM_NAMES = ("block1.0.weight", "block1.0.bias", "block1.2.weight", "block1.2.bias",
                 "block3.0.weight", "block3.0.bias", "block3.2.weight", "block3.2.bias",
@@ -45,14 +47,22 @@ def agg_params(agg) -> list:
     return [d[n] for n in _PARAM_NAMES]
 
 
-def packed_bwd(agg):
-    """Transposed fragment packs for the backward GEMMs (pnr_mlp_bwd)."""
+def packed_bwd(agg, x3: bool = False):
+    """Transposed fragment packs for the backward GEMMs: (pnr_mlp_bwd, None, keep)
+    with native-fp32 packs, or (pnr_mlp_bwd with w3e only, pnr_mlp_bwd_x3, keep)
+    with split-bf16 packs (frag_pack_x3) for pnr_aggregate_bwd_pairs_x3."""
     with torch.no_grad():
         W3 = agg.block3[0].weight
-        t = dict(w4t=frag_pack(agg.block3[2].weight.t()), w3t=frag_pack(W3[:, :256].t()),
-                 w2t=frag_pack(agg.block1[2].weight.t()), w3e=W3[:, 256:263].float().contiguous())
-    m = L.MlpBwd(*(t[k].data_ptr() for k in ("w4t", "w3t", "w2t", "w3e")))
-    return m, t
+        mats = dict(w4t=agg.block3[2].weight.t(), w3t=W3[:, :256].t(), w2t=agg.block1[2].weight.t())
+        t = dict(w3e=W3[:, 256:263].float().contiguous())
+        if x3:
+            t.update({k + "x": frag_pack_x3(v) for k, v in mats.items()})
+        else:
+            t.update({k: frag_pack(v) for k, v in mats.items()})
+    if x3:
+        m = L.MlpBwd(None, None, None, t["w3e"].data_ptr())
+        return m, L.MlpBwdX3(*(t[k].data_ptr() for k in ("w4tx", "w3tx", "w2tx"))), t
+    return L.MlpBwd(*(t[k].data_ptr() for k in ("w4t", "w3t", "w2t", "w3e"))), None, t
 
 
 class Saved:
@@ -200,13 +210,17 @@ class AggregateFn(torch.autograd.Function):
         d_color = torch.zeros((N, 3), **f32) if has_c else None
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
         d_conf = torch.zeros(N, **f32) if has_f else None
-        wb, _keepb = packed_bwd(agg)
-        L.check(L.lib().pnr_aggregate_bwd_pairs(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
-                                                ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(sv.c),
-                                                L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3),
-                                                L.ptr(dz4), L.ptr(dpa), L.ptr(d_p1), L.ptr(d_color), L.ptr(d_dir),
-                                                L.ptr(d_conf), L.stream_ptr(dev)),
-                "pnr_aggregate_bwd_pairs")
+        wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3)
+        bufs = (L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3), L.ptr(dz4), L.ptr(dpa),
+                L.ptr(d_p1), L.ptr(d_color), L.ptr(d_dir), L.ptr(d_conf), L.stream_ptr(dev))
+        if wbx is not None:
+            L.check(L.lib().pnr_aggregate_bwd_pairs_x3(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                       ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(wbx),
+                                                       ctypes.byref(sv.c), *bufs), "pnr_aggregate_bwd_pairs_x3")
+        else:
+            L.check(L.lib().pnr_aggregate_bwd_pairs(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                    ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(sv.c),
+                                                    *bufs), "pnr_aggregate_bwd_pairs")
         m = n * 8
         dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
         h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
