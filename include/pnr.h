@@ -419,6 +419,15 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             const float* d_feat, const float* d_hid, float* dz1, float* dz2,
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
+/* Device weight packing (aggregator.py frag_pack / frag_pack_x3, one launch per
+ * matrix): kind 0 = fp32 fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)],
+ * ceil(cols / 2) + pad_steps k-steps; kind 1 = fp32x3 split-bf16 fragments
+ * F[t][T][plane][h][r][j] = plane of W'[32T + r][16t + 8h + j], ceil(cols / 16) +
+ * pad_steps k-steps; W' = [W | bias | 0] (cols = kin + 1 with a bias),
+ * W[o][k] = W[o * ld_row + k * ld_col] (element strides), out_f % 32 == 0. */
+int pnr_pack_weights(int32_t kind, const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f,
+                     int32_t kin, const float* bias, int32_t pad_steps, void* out, size_t out_bytes,
+                     void* stream);
 /* Same, with the three dX GEMMs on fp32x3 split-bf16 MFMA: wbx = frag_pack_x3 of
  * block3.2.weight^T, block3.0.weight[:, :256]^T, block1.2.weight^T (aggregator.py;
  * 16-B aligned); wb supplies w3e (w4t / w3t / w2t unused, may be NULL). */

@@ -69,12 +69,34 @@ def _init_seq(seq: nn.Sequential):
 PREFETCH_PAD = 8   # kPackPad in aggregate.hip: zero k-steps appended for the weight prefetch
 
 
+def _pack_device(kind: int, W: torch.Tensor, bias: torch.Tensor | None, pad: int) -> torch.Tensor:
+    """pnr_pack_weights: the pack of a CUDA weight (any strides) in one launch."""
+    out_f, kin = W.shape
+    assert out_f % 32 == 0
+    cols = kin + (1 if bias is not None else 0)
+    W = W.detach().float()
+    b = None if bias is None else bias.detach().float().contiguous()
+    if kind == 0:
+        n = ((cols + 1) // 2 + pad) * (out_f // 32) * 64
+        out = torch.empty(n, dtype=torch.float32, device=W.device)
+    else:
+        n = ((cols + 15) // 16 + pad) * (out_f // 32) * 64 * 3 * 8
+        out = torch.empty(n, dtype=torch.bfloat16, device=W.device)
+    L.check(L.lib().pnr_pack_weights(kind, W.data_ptr(), W.stride(0), W.stride(1), out_f, kin, L.ptr(b), pad,
+                                     out.data_ptr(), out.numel() * out.element_size(), L.stream_ptr(W.device)),
+            "pnr_pack_weights")
+    return out
+
+
 def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """[out, Kin] nn.Linear weight (out a multiple of 32) and bias -> MFMA
     A-operand fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)]
     of W' = [W | bias | 0]: the bias rides in the GEMM as input column Kin
     (the kernel sets X^T row Kin to 1).  ceil((Kin+1)/2) k-steps plus
-    PREFETCH_PAD zero ones."""
+    PREFETCH_PAD zero ones.  CUDA weights are packed by pnr_pack_weights (one
+    launch); this torch restatement packs host tensors (and is the test's check)."""
+    if W.is_cuda:
+        return _pack_device(0, W, bias, PREFETCH_PAD)
     out_f, kin = W.shape
     assert out_f % 32 == 0
     cols = kin + (1 if bias is not None else 0)
@@ -127,7 +149,10 @@ def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Ten
     """Split-bf16 A-operand packs for pnr_aggregate_fwd_x3:
     F[t][T][plane][lane][j] = plane of W'[32T + (lane & 31)][16t + 8(lane >> 5) + j],
     W' = [W | bias | 0], ceil((Kin+1)/16) k-steps plus X3_PAD zero ones; planes
-    from split3_bf16 (W' == plane0 + plane1 + plane2 exactly)."""
+    from split3_bf16 (W' == plane0 + plane1 + plane2 exactly).  CUDA weights:
+    pnr_pack_weights (bitwise the same planes, one launch)."""
+    if W.is_cuda:
+        return _pack_device(1, W, bias, X3_PAD)
     out_f, kin = W.shape
     assert out_f % 32 == 0
     cols = kin + (1 if bias is not None else 0)

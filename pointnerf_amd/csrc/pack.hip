@@ -1,0 +1,79 @@
+// Weight fragment packing on the device (aggregator.frag_pack / frag_pack_x3):
+// one launch per matrix instead of a dozen small torch ops, so a training step
+// (weights change every step, every pack is rebuilt) is not launch-bound.
+//   kind 0 (fp32, v_mfma_f32_32x32x2_f32):  F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)]
+//   kind 1 (fp32x3, v_mfma_f32_32x32x16_bf16): F[t][T][plane][h][r][j] = plane of W'[32T + r][16t + 8h + j]
+//     (planes: exact 3-way bf16 split, round-to-nearest-even, = aggregator.split3_bf16)
+// W' = [W | bias | 0] (bias = input column kin when given), W[o][k] at
+// W + o * ld_row + k * ld_col (a transposed view packs without a copy).
+#include "agg_common.h"
+
+namespace pnr {
+
+__device__ __forceinline__ float wprime(const float* W, int64_t lr, int64_t lc, int kin, const float* bias, int o,
+                                        int k) {
+  if (k < kin) return W[o * lr + k * lc];
+  return (k == kin && bias) ? bias[o] : 0.f;
+}
+
+__global__ void k_pack_fp32(const float* __restrict__ W, int64_t lr, int64_t lc, int NT, int kin,
+                            const float* __restrict__ bias, int64_t total, float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    const int64_t tT = i >> 6;
+    const int T = (int)(tT % NT), t = (int)(tT / NT);
+    out[i] = wprime(W, lr, lc, kin, bias, 32 * T + (lane & 31), 2 * t + (lane >> 5));
+  }
+}
+
+// one thread per (t, T, h, r): 8 inputs -> one uint4 per plane
+__global__ void k_pack_x3(const float* __restrict__ W, int64_t lr, int64_t lc, int NT, int kin,
+                          const float* __restrict__ bias, int64_t total, uint4* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i & 31), h = (int)((i >> 5) & 1);
+    const int64_t tT = i >> 6;
+    const int T = (int)(tT % NT), t = (int)(tT / NT);
+    const int o = 32 * T + r, k0 = 16 * t + 8 * h;
+    unsigned w[3][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      split2(wprime(W, lr, lc, kin, bias, o, k0 + 2 * q), wprime(W, lr, lc, kin, bias, o, k0 + 2 * q + 1), w[0][q],
+             w[1][q], w[2][q]);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      out[((tT * 3 + pl) * 2 + h) * 32 + r] = make_uint4(w[pl][0], w[pl][1], w[pl][2], w[pl][3]);
+  }
+}
+
+}  // namespace pnr
+
+using namespace pnr;
+
+extern "C" int pnr_pack_weights(int32_t kind, const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f,
+                                int32_t kin, const float* bias, int32_t pad_steps, void* out, size_t out_bytes,
+                                void* stream) {
+  PNR_CHECK_ARG(kind == 0 || kind == 1, "pack_weights: kind %d (0: fp32, 1: fp32x3)", kind);
+  PNR_CHECK_ARG(W && out && out_f > 0 && out_f % 32 == 0 && kin > 0 && pad_steps >= 0,
+                "pack_weights: bad args (out_f %d, kin %d)", out_f, kin);
+  PNR_CHECK_ARG(((uintptr_t)out & 15) == 0, "pack_weights: output must be 16-B aligned");
+  const int cols = kin + (bias ? 1 : 0);
+  const int NT = out_f / 32;
+  hipStream_t st = as_stream(stream);
+  if (kind == 0) {
+    const int64_t tot = (cols + 1) / 2 + pad_steps;
+    const int64_t total = tot * NT * 64;
+    PNR_CHECK_ARG(out_bytes >= (size_t)total * 4, "pack_weights: output too small (%zu < %lld)", out_bytes,
+                  (long long)total * 4);
+    hipLaunchKernelGGL(k_pack_fp32, dim3(grid_for(total, 256)), dim3(256), 0, st, W, ld_row, ld_col, NT, kin, bias,
+                       total, static_cast<float*>(out));
+  } else {
+    const int64_t tot = (cols + 15) / 16 + pad_steps;
+    const int64_t total = tot * NT * 64;   // threads: (t, T, h, r)
+    PNR_CHECK_ARG(out_bytes >= (size_t)total * 3 * 16, "pack_weights: output too small (%zu < %lld)", out_bytes,
+                  (long long)total * 48);
+    hipLaunchKernelGGL(k_pack_x3, dim3(grid_for(total, 256)), dim3(256), 0, st, W, ld_row, ld_col, NT, kin, bias,
+                       total, static_cast<uint4*>(out));
+  }
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}

@@ -25,6 +25,9 @@ constexpr int kQBlock = 256;
 #ifndef PNR_KNN_BATCH
 #define PNR_KNN_BATCH 1   // candidate records fetched together (A/B, with the up-front lookups: 1 -> 2.12, 2 -> 2.15 ms query)
 #endif
+#ifndef PNR_KNN_BATCH_SMALL
+#define PNR_KNN_BATCH_SMALL 2   // small launches (a few waves per CU: latency, not occupancy, bound)
+#endif
 #ifndef PNR_KNN_XCD
 #define PNR_KNN_XCD 2   // 0: grid-stride; 1: static XCD ranges; 2: per-XCD counters + stealing
 #endif
@@ -167,15 +170,15 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
 }
 
 // All records of one record range, in order, PNR_KNN_BATCH loads in flight.
-template <int KMAX>
+template <int KMAX, int KB>
 __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
                                          float buf[KMAX], int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
-  for (int g0 = 0; g0 < cnt; g0 += PNR_KNN_BATCH) {
-    float4 vb[PNR_KNN_BATCH];
+  for (int g0 = 0; g0 < cnt; g0 += KB) {
+    float4 vb[KB];
 #pragma unroll
-    for (int u = 0; u < PNR_KNN_BATCH; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < KB; ++u) vb[u] = g0 + u < cnt ? rec[g0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < PNR_KNN_BATCH; ++u) {
+    for (int u = 0; u < KB; ++u) {
       if (g0 + u >= cnt) break;
       knn_visit<KMAX>(vb[u], p, K, r2, buf, out, kid, far_ind, far2);
     }
@@ -200,7 +203,7 @@ __device__ __forceinline__ int held_rank(const uint2 wd, int bit) {
 // visited in the reference's order (Chebyshev layer, then x -> y -> z); a cell
 // whose voxel holds no point contributes nothing there either, so only held
 // cells are looked up (bitmap + rank: no per-cell table of the whole grid).
-template <int KMAX, int LAYERS>
+template <int KMAX, int LAYERS, int KB>
 __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, int layers, float r2,
                                        const QIndex& qi, int32_t out[KMAX], int& n_cand) {
   const int fx = vox_coord(p[0], g.shift[0], g.vs[0]);
@@ -228,7 +231,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
     const int zlo = fz > 0 ? fz - 1 : fz, zhi = fz + 1 < g.dims[2] ? fz + 1 : fz;
     auto range = [&](int o, int e) {
       n_cand += e - o;
-      knn_cell<KMAX>(qi.recs + o, e - o, p, K, r2, buf, out, kid, far_ind, far2);
+      knn_cell<KMAX, KB>(qi.recs + o, e - o, p, K, r2, buf, out, kid, far_ind, far2);
     };
     // Every index lookup of the 27 cells is issued up front: one round of 9-18
     // independent word loads (a column's 3-cell run spans <= 2 words; the
@@ -305,7 +308,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
           const int o = qi.rec_off[r];
           const int cn = qi.rec_off[r + 1] - o;
           n_cand += cn;
-          knn_cell<KMAX>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
+          knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
         }
       }
     }
@@ -316,7 +319,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 
 // LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
 // layered loop inlined beside it costs registers); 0: any layer count.
-template <int KMAX, int LAYERS>
+template <int KMAX, int LAYERS, int KB>
 __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
@@ -354,6 +357,7 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
   const int64_t c_lo = xcd ? C * xg / 8 : 0, c_hi = xcd ? C * (xg + 1) / 8 : C;
   const int64_t c_step = xcd ? gridDim.x / 8 : gridDim.x;
   __shared__ int64_t s_ch;
+  unsigned done = 0;   // (thread 0) XCD ranges this block found exhausted: never polled again
   auto next_chunk = [&](int64_t prev) -> int64_t {
     if (!dyn) return prev < 0 ? c_lo + (xcd ? blockIdx.x >> 3 : blockIdx.x) : prev + c_step;
     __syncthreads();   // every thread has read s_ch of the previous chunk
@@ -361,10 +365,10 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
       int64_t got = C;
       for (int k = 0; k < 8 && got == C; ++k) {
         const int y = (xg + k) & 7;
-        const int64_t lo = C * y / 8, hi = C * (y + 1) / 8;
-        if (lo + *reinterpret_cast<volatile const int32_t*>(xcd_ctr + y) >= hi) continue;   // exhausted: no RMW
-        const int64_t t = lo + atomicAdd(xcd_ctr + y, 1);
-        if (t < hi) got = t;
+        if ((done >> y) & 1u) continue;
+        const int64_t t = C * y / 8 + atomicAdd(xcd_ctr + y, 1);
+        if (t < C * (y + 1) / 8) got = t;
+        else done |= 1u << y;
       }
       s_ch = got;
     }
@@ -416,7 +420,7 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
       sample_p[i * 3 + a] = pp[a];
     }
     int32_t out[KMAX];
-    const int nk = knn_one<KMAX, LAYERS>(p, g, K, layers, r2, qi, out, n_cand);
+    const int nk = knn_one<KMAX, LAYERS, KB>(p, g, K, layers, r2, qi, out, n_cand);
     if (KMAX == 8 && K == 8 && vec_pidx) {   // two 16-B stores (pidx 16-B aligned)
       int4* o4 = reinterpret_cast<int4*>(pidx + i * 8);
       o4[0] = make_int4(out[0], out[1], out[2], out[3]);
@@ -570,6 +574,9 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
                      b->n_filled, b->ray_off, b->fill_rs, b->counts);
   PNR_LAUNCH_CHECK();
   const int layers = (qp->kernel_size[0] + 1) / 2;
+  // launches of < 4 M sample slots (training batches): fewer waves than the
+  // chip holds, so more records in flight per lane
+  const bool small = RS < (int64_t(4) << 20);
   // the 3x3x3 kernel indexes cells in 32 bits
   const bool q3 = layers == 2 && (int64_t)g.dims[0] * g.dims[1] * g.dims[2] < (int64_t(1) << 32);
   unsigned gk = grid_for(RS, kQBlock, PNR_KNN_GRID);
@@ -583,7 +590,8 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   qi.rec_off = h->q_rec_off.as<int32_t>();
   qi.recs = h->q_recs.as<float4>();
 #define PNR_KNN(KM)                                                                              \
-  hipLaunchKernelGGL((q3 ? k_knn<KM, 2> : k_knn<KM, 0>), dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
+  hipLaunchKernelGGL((q3 ? (small ? k_knn<KM, 2, PNR_KNN_BATCH_SMALL> : k_knn<KM, 2, PNR_KNN_BATCH>)           \
+                          : k_knn<KM, 0, PNR_KNN_BATCH_SMALL>), dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
                      qp->radius_limit2, qi, b->slot_d, b->fill_rs, b->pidx, b->vflag,             \
                      b->ray_vcnt, b->sample_w, b->sample_p, b->counts, vec,                       \
                      reinterpret_cast<int32_t*>(b->scratch))

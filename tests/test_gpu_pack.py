@@ -1,0 +1,23 @@
+"""pnr_pack_weights (device fragment packing) against aggregator.py's torch
+restatement on the host: bitwise, fp32 and fp32x3 packs, with and without a
+bias column, contiguous and transposed (strided) weights."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape,bias,transposed", [((256, 263), True, False), ((256, 60), False, False),
+                                                   ((128, 280), True, False), ((256, 256), False, True),
+                                                   ((256, 7), False, False), ((32, 33), True, True)])
+def test_device_pack_equals_torch(cuda, shape, bias, transposed):
+    from pointnerf_amd.aggregator import frag_pack, frag_pack_x3
+    g = torch.Generator().manual_seed(shape[0] + shape[1])
+    out_f, kin = shape
+    W = torch.randn((kin, out_f) if transposed else (out_f, kin), generator=g) * 0.3
+    W = W.t() if transposed else W
+    b = torch.randn(out_f, generator=g) if bias else None
+    Wd = W.to(cuda) if not transposed else W.t().contiguous().to(cuda).t()   # keep the strided view on the GPU
+    bd = None if b is None else b.to(cuda)
+    assert torch.equal(frag_pack(Wd, bd).cpu(), frag_pack(W, b))
+    assert torch.equal(frag_pack_x3(Wd, bd).cpu().view(torch.int16), frag_pack_x3(W, b).view(torch.int16))
