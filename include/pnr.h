@@ -419,6 +419,14 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             const float* d_feat, const float* d_hid, float* dz1, float* dz2,
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
+/* d_p1[row(p)] = sum of dz1[pair] over the pairs of point p, given the pairs'
+ * point rows sorted (stable: each point's pairs in pair order, a deterministic
+ * sum) and the pair index of each sorted entry: the atomic-free alternative to
+ * pnr_aggregate_bwd_pairs' d_p1 (pass d_p1 = NULL there).  row(p) = used_map[p]
+ * (or p when used_map is NULL); rows of points without pairs are not written;
+ * negative point rows (empty pairs) are skipped. */
+int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,
+                        const int32_t* used_map, float* d_p1, void* stream);
 /* Device weight packing (aggregator.py frag_pack / frag_pack_x3, one launch per
  * matrix): kind 0 = fp32 fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)],
  * ceil(cols / 2) + pad_steps k-steps; kind 1 = fp32x3 split-bf16 fragments

@@ -934,7 +934,7 @@ __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsign
       const unsigned b = mk[pt * NT + T];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = act ? (((b >> r) & 1u) ? v[r] : v[r] * slope) : 0.f;
-      if (act) {
+      if (act && !(PNR_ABLATE & 131072)) {   // (131072: timing only, no dz stores)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<float4*>(dst + pair * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
@@ -995,6 +995,7 @@ __device__ __forceinline__ void x3q_b(const float* X, int t, int pt, int lane, u
 // in the ring, the next step's B split while this step's MFMAs run)
 __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], X3QRing& w, __amdgpu_buffer_rsrc_t rs, int voff,
                                               const float* X, int nsteps, int lane) {
+  if (PNR_ABLATE & 262144) return;   // timing only: no dX GEMMs
   uint4 b[2][3];
   x3q_b(X, 0, 0, lane, b[0]);
   x3q_b(X, 0, 1, lane, b[1]);
@@ -1003,20 +1004,15 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], X3QRing& w, __am
     const int tn = t + 1 < nsteps ? t + 1 : t;
     x3q_b(X, tn, 0, lane, bn[0]);
     x3q_b(X, tn, 1, lane, bn[1]);
+    // products smallest first (W2.X0, W1.X1, W0.X2, W1.X0, W0.X1, W0.X0), each
+    // over the four accumulators in turn: four independent MFMA chains
+    constexpr int kPa[6] = {2, 1, 0, 1, 0, 0}, kPb[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
+    for (int p = 0; p < 6; ++p)
 #pragma unroll
-      for (int T = 0; T < 2; ++T) {
-        f32x16 v = acc[2 * pt + T];
-        v = mfma_bf16(a[T][2], b[pt][0], v);   // W2.X0
-        v = mfma_bf16(a[T][1], b[pt][1], v);   // W1.X1
-        v = mfma_bf16(a[T][0], b[pt][2], v);   // W0.X2
-        v = mfma_bf16(a[T][1], b[pt][0], v);   // W1.X0
-        v = mfma_bf16(a[T][0], b[pt][1], v);   // W0.X1
-        v = mfma_bf16(a[T][0], b[pt][0], v);   // W0.X0
-        acc[2 * pt + T] = v;
-      }
-    }
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_bf16(a[T][kPa[p]], b[pt][kPb[p]], acc[2 * pt + T]);
     x3q_load(a, rs, voff, t + kX3D);   // packs carry kX3D zero steps
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt)
@@ -1047,9 +1043,6 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kTS);
   const float slope = A.w.neg_slope;
-  float Rw[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
   const float* w4t = X3 ? nullptr : A.wb.w4t + T0 * 64;
   const float* w3t = X3 ? nullptr : A.wb.w3t + T0 * 64;
   const float* w2t = X3 ? nullptr : A.wb.w2t + T0 * 64;
@@ -1162,19 +1155,8 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       for (int e = 0; e < 7; ++e) exP[(wid * 7 + e) * kTP + lane] = ex[e];
     }
     __syncthreads();
-    // ---------------------------------------------------------- block3.0^T: dh2 = W3[:, :256]^T dz3
-#pragma unroll
-    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
-    load_masks<kNTW, kPTW>(mk, A.sv.mask, 1, tile, n, lane, T0);
-    if constexpr (X3) {
-      mlp_layer_x3q(acc, xr, x3, xvoff, X, 16, lane);
-      x3q_prime(xr, x2, xvoff);
-    } else {
-      mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
-      prime_q<kNTW>(ring, w2t, lane);
-    }
-    // colour / dir gradients of the pair (wave 0, lane = pair; exP is not
-    // overwritten before the next tile's barrier)
+    // colour / dir gradients of the pair (wave 0, lane = pair), before the
+    // block3.0^T GEMM: its registers stay free for the GEMM
     if (wid == 0 && active) {
       const int32_t pr = A.sv.prow[pair];
       if (pr >= 0) {
@@ -1192,6 +1174,9 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
           const int64_t row = sample_row(A.s, v);
           const int64_t drow = dir_row(A.s, row);
           const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+          float Rw[9];   // loaded here, not kept live across the tile's GEMMs
+#pragma unroll
+          for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
           float vrot[3];
           mat3(Rw, vd, vrot);
           const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
@@ -1201,6 +1186,17 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
             atomicAdd(A.d_dir + (int64_t)pr * 3 + i, Rw[i] * gd[0] + Rw[3 + i] * gd[1] + Rw[6 + i] * gd[2]);
         }
       }
+    }
+    // ---------------------------------------------------------- block3.0^T: dh2 = W3[:, :256]^T dz3
+#pragma unroll
+    for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
+    load_masks<kNTW, kPTW>(mk, A.sv.mask, 1, tile, n, lane, T0);
+    if constexpr (X3) {
+      mlp_layer_x3q(acc, xr, x3, xvoff, X, 16, lane);
+      x3q_prime(xr, x2, xvoff);
+    } else {
+      mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
+      prime_q<kNTW>(ring, w2t, lane);
     }
     __syncthreads();
     lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[1], tile, n, slope, lane, T0);
@@ -1221,7 +1217,9 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // block1.0 point half: d P1[p] += dz1 (the P1 gather's backward).  dz1 goes
     // through LDS so each pair's 1-KB row is added with 4 coalesced 256-B
     // atomic wave instructions (wave w: pairs 16w..16w+15, lane = neuron).
+    // d_p1 == NULL: the caller reduces dz1 per point instead (pnr_pairs_to_points).
     __syncthreads();                 // every wave is done reading X (W2^T GEMM)
+    if (A.d_p1 == nullptr || (PNR_ABLATE & 65536)) continue;   // (65536: timing only)
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     __syncthreads();
     for (int i = 0; i < kTP / kPairWaves; ++i) {
@@ -1237,6 +1235,29 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       }
     }
     __syncthreads();
+  }
+}
+
+// d P1 rows from dz1 without atomics: pairs sorted by point row (stable, so
+// each point's pairs in pair order -- a deterministic sum); one wave per run of
+// equal rows, lane = 4 neurons (float4).
+__global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const int32_t* __restrict__ pair_of,
+                                  int64_t P, const float* __restrict__ dz1, const int32_t* __restrict__ used_map,
+                                  float* __restrict__ d_p1) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
+    const int32_t pr = prow_sorted[i];
+    if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
+    float4 s = reinterpret_cast<const float4*>(dz1 + (int64_t)pair_of[i] * kHid)[lane];
+    for (int64_t j = i + 1; j < P && prow_sorted[j] == pr; ++j) {
+      const float4 v = reinterpret_cast<const float4*>(dz1 + (int64_t)pair_of[j] * kHid)[lane];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
   }
 }
 
@@ -1514,6 +1535,7 @@ extern "C" int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_sampl
   a.s = *s;
   a.w = *w;
   carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
+  int32_t* tile_ctr = tile_counter(a, s->n_max);   // in the scratch (before vmask is redirected to the saved one)
   a.sv = *saved;
   a.hid = saved->hid;
   a.vmask = saved->vmask;
@@ -1526,7 +1548,7 @@ extern "C" int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_sampl
   if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
   SplitW sw = {{wx->w1bx, wx->w2x, wx->w3x, wx->w4x}, {1.f, 1.f, 1.f, 1.f}, nullptr};
   if ((rc = launch_pairs_split<false>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
-                                      tile_counter(a, s->n_max), st, saved)))
+                                      tile_ctr, st, saved)))
     return rc;
   return launch_t<true>(a, st, kStageColor);
 }
@@ -1568,7 +1590,7 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
   PNR_CHECK_ARG(!wbx || (wbx->w4tx && wbx->w3tx && wbx->w2tx &&
                          (((uintptr_t)wbx->w4tx | (uintptr_t)wbx->w3tx | (uintptr_t)wbx->w2tx) & 15) == 0),
                 "aggregate_bwd_x3: null or unaligned split weight pack");
-  PNR_CHECK_ARG(d_feat && d_hid && dz1 && dz2 && dz3 && dz4 && dpa && d_p1, "aggregate_bwd: null buffer");
+  PNR_CHECK_ARG(d_feat && d_hid && dz1 && dz2 && dz3 && dz4 && dpa, "aggregate_bwd: null buffer");
   PNR_CHECK_ARG((((uintptr_t)d_hid | (uintptr_t)dz1 | (uintptr_t)dz2 | (uintptr_t)dz3 | (uintptr_t)dz4) & 15) == 0,
                 "aggregate_bwd: gradient buffers must be 16-B aligned");
   PNR_CHECK_ARG(s->dirs && s->dir_div >= 1, "aggregate_bwd: sample dirs required");
@@ -1631,6 +1653,17 @@ extern "C" int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_sampl
   PNR_CHECK_ARG(wbx, "aggregate_bwd_x3: null split weight packs");
   return bwd_pairs(pts, s, w, wb, wbx, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
                    d_conf, stream);
+}
+
+extern "C" int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,
+                                   const int32_t* used_map, float* d_p1, void* stream) {
+  PNR_CHECK_ARG(P >= 0 && (P == 0 || (prow_sorted && pair_of && dz1 && d_p1)), "pairs_to_points: bad args");
+  PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1) & 15) == 0, "pairs_to_points: rows must be 16-B aligned");
+  if (P == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_pairs_to_points, dim3(grid_for(P, 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
+                     pair_of, P, dz1, used_map, d_p1);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
 }
 
 extern "C" int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* stream) {

@@ -211,8 +211,10 @@ class AggregateFn(torch.autograd.Function):
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
         d_conf = torch.zeros(N, **f32) if has_f else None
         wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3)
+        # d_p1 = NULL: the per-point sums of dz1 come from pnr_pairs_to_points below
+        # (pairs sorted by point: no atomics, deterministic) instead of the kernel's atomics
         bufs = (L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3), L.ptr(dz4), L.ptr(dpa),
-                L.ptr(d_p1), L.ptr(d_color), L.ptr(d_dir), L.ptr(d_conf), L.stream_ptr(dev))
+                None, L.ptr(d_color), L.ptr(d_dir), L.ptr(d_conf), L.stream_ptr(dev))
         if wbx is not None:
             L.check(L.lib().pnr_aggregate_bwd_pairs_x3(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
                                                        ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(wbx),
@@ -222,6 +224,11 @@ class AggregateFn(torch.autograd.Function):
                                                     ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(sv.c),
                                                     *bufs), "pnr_aggregate_bwd_pairs")
         m = n * 8
+        prow_sorted, pair_of = torch.sort(sv["prow"][:m], stable=True)
+        pair_of = pair_of.to(torch.int32)
+        L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1),
+                                            L.ptr(None if spec.used is None else spec.used[1]), L.ptr(d_p1),
+                                            L.stream_ptr(dev)), "pnr_pairs_to_points")
         dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
         h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
         # dW = dZ^T X over all pairs: split-K MFMA GEMM (pnr_gemm_tn), bias = column sums
