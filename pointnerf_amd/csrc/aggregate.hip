@@ -950,6 +950,9 @@ __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsign
 // planes in registers (split2, exact), six cross products per 16-k step on
 // v_mfma_f32_32x32x16_bf16 (smallest first) -- the arithmetic of the fp32x3
 // forward (aggregate_x3.hip) on k_pairs_bwd's LDS layout.
+#ifndef PNR_BWD_BPREF
+#define PNR_BWD_BPREF 0   // B fragments of the next step split ahead (more VGPRs)
+#endif
 constexpr int kX3D = 3;   // weight ring depth (k-steps in flight) <= X3_PAD
 struct X3QRing {
   uint4 a[kX3D][2][3];
@@ -992,18 +995,29 @@ __device__ __forceinline__ void x3q_b(const float* X, int t, int pt, int lane, u
 }
 
 // acc[2 pt + T] += W^T . X over nsteps 16-k steps (weights kX3D steps ahead
-// in the ring, the next step's B split while this step's MFMAs run)
-__device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], X3QRing& w, __amdgpu_buffer_rsrc_t rs, int voff,
+// in the ring)
+// (the ring is primed here, not ahead across the tile's other phases: 72 VGPRs
+// live through the whole tile made the kernel spill)
+__device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_rsrc_t rs, int voff,
                                               const float* X, int nsteps, int lane) {
   if (PNR_ABLATE & 262144) return;   // timing only: no dX GEMMs
+  X3QRing w;
+  x3q_prime(w, rs, voff);
   uint4 b[2][3];
   x3q_b(X, 0, 0, lane, b[0]);
   x3q_b(X, 0, 1, lane, b[1]);
   auto step = [&](uint4 (&a)[2][3], int t) {
+#if PNR_BWD_BPREF
     uint4 bn[2][3];
     const int tn = t + 1 < nsteps ? t + 1 : t;
     x3q_b(X, tn, 0, lane, bn[0]);
     x3q_b(X, tn, 1, lane, bn[1]);
+#else
+    if (t > 0) {
+      x3q_b(X, t, 0, lane, b[0]);
+      x3q_b(X, t, 1, lane, b[1]);
+    }
+#endif
     // products smallest first (W2.X0, W1.X1, W0.X2, W1.X0, W0.X1, W0.X0), each
     // over the four accumulators in turn: four independent MFMA chains
     constexpr int kPa[6] = {2, 1, 0, 1, 0, 0}, kPb[6] = {0, 1, 2, 0, 1, 0};
@@ -1014,10 +1028,12 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], X3QRing& w, __am
 #pragma unroll
         for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_bf16(a[T][kPa[p]], b[pt][kPb[p]], acc[2 * pt + T]);
     x3q_load(a, rs, voff, t + kX3D);   // packs carry kX3D zero steps
+#if PNR_BWD_BPREF
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) b[pt][pl] = bn[pt][pl];
+#endif
   };
   int t = 0;
 #pragma unroll 1
@@ -1047,13 +1063,9 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   const float* w3t = X3 ? nullptr : A.wb.w3t + T0 * 64;
   const float* w2t = X3 ? nullptr : A.wb.w2t + T0 * 64;
   float ring[kQD][kNTW];
-  X3QRing xr;
   const int xvoff = (T0 * 3 * 64 + lane) * 16;
   const __amdgpu_buffer_rsrc_t x4 = x3q_rsrc(A.wx[0]), x3 = x3q_rsrc(A.wx[1]), x2 = x3q_rsrc(A.wx[2]);
-  if constexpr (X3)
-    x3q_prime(xr, x4, xvoff);
-  else
-    prime_q<kNTW>(ring, w4t, lane);
+  if constexpr (!X3) prime_q<kNTW>(ring, w4t, lane);
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // ---------------------------------------------------------- per-pair scalars (lane = pair)
@@ -1126,8 +1138,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     unsigned mk[kPTW * kNTW];
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 2, tile, n, lane, T0);
     if constexpr (X3) {
-      mlp_layer_x3q(acc, xr, x4, xvoff, X, 16, lane);
-      x3q_prime(xr, x3, xvoff);
+      mlp_layer_x3q(acc, x4, xvoff, X, 16, lane);
     } else {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w4t, X, 128, lane);
       prime_q<kNTW>(ring, w3t, lane);
@@ -1138,7 +1149,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
     // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
     wave_sync();
-    {
+    if constexpr (!X3) {
       float ex[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
@@ -1156,8 +1167,11 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     }
     __syncthreads();
     // colour / dir gradients of the pair (wave 0, lane = pair), before the
-    // block3.0^T GEMM: its registers stay free for the GEMM
-    if (wid == 0 && active) {
+    // block3.0^T GEMM: its registers stay free for the GEMM.  The pair's
+    // indices are recomputed here rather than kept live across the GEMMs.
+    if (!X3 && wid == 0 && tile * kTS + (lane >> 3) < n) {
+      const int64_t pair = tile * kTP + lane;
+      const int64_t v = tile * kTS + (lane >> 3);
       const int32_t pr = A.sv.prow[pair];
       if (pr >= 0) {
         float g[7];
@@ -1192,8 +1206,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 1, tile, n, lane, T0);
     if constexpr (X3) {
-      mlp_layer_x3q(acc, xr, x3, xvoff, X, 16, lane);
-      x3q_prime(xr, x2, xvoff);
+      mlp_layer_x3q(acc, x3, xvoff, X, 16, lane);
     } else {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
       prime_q<kNTW>(ring, w2t, lane);
@@ -1207,8 +1220,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 0, tile, n, lane, T0);
     if constexpr (X3) {
-      mlp_layer_x3q(acc, xr, x2, xvoff, X, 16, lane);
-      x3q_prime(xr, x4, xvoff);   // the next tile
+      mlp_layer_x3q(acc, x2, xvoff, X, 16, lane);
     } else {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
       prime_q<kNTW>(ring, w4t, lane);   // the next tile
@@ -1235,6 +1247,50 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       }
     }
     __syncthreads();
+  }
+}
+
+// block3.0 extras backward of k_pairs_bwd<true> as its own pass over the pairs:
+// g_e = sum_n W3[n, 256 + e] dz3[pair][n] -> d colour (e 0..2) and d dir (e 3..6,
+// through R.dir - R.v and <R.dir, R.v>).  One wave per 64 pairs, lane = pair.
+__global__ void __launch_bounds__(256) k_extras_bwd(BwdArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = eff_n(A.s);
+  const int64_t P = n * kKN;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t w = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); w * 64 < P; w += waves) {
+    const int64_t pair = w * 64 + lane;
+    if (pair >= P) continue;
+    const int32_t pr = A.sv.prow[pair];
+    if (pr < 0) continue;
+    float g[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float4* z4 = reinterpret_cast<const float4*>(A.dz[2] + pair * kHid);
+#pragma unroll 4
+    for (int u = 0; u < kHid / 4; ++u) {
+      const float4 z = z4[u];
+      const float zv[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 7; ++e) g[e] += A.wb.w3e[(4 * u + i) * 7 + e] * zv[i];
+    }
+    if (A.d_color) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) atomicAdd(A.d_color + (int64_t)pr * 3 + a, g[a]);
+    }
+    if (A.d_dir) {
+      float Rw[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+      const int64_t drow = dir_row(A.s, sample_row(A.s, pair / kKN));
+      const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+      float vrot[3];
+      mat3(Rw, vd, vrot);
+      const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        atomicAdd(A.d_dir + (int64_t)pr * 3 + i, Rw[i] * gd[0] + Rw[3 + i] * gd[1] + Rw[6 + i] * gd[2]);
+    }
   }
 }
 
@@ -1626,10 +1682,13 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
   a.wx[1] = wbx ? wbx->w3tx : nullptr;
   a.wx[2] = wbx ? wbx->w2tx : nullptr;
   const int64_t tiles = cdiv(s->n_max, kTS);
-  if (wbx)
+  if (wbx) {
     hipLaunchKernelGGL(k_pairs_bwd<true>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
                        st, a);
-  else
+    PNR_LAUNCH_CHECK();
+    if (d_color || d_dir)
+      hipLaunchKernelGGL(k_extras_bwd, dim3(grid_for(cdiv(s->n_max * kKN, 64), 4, 2048)), dim3(256), 0, st, a);
+  } else
     hipLaunchKernelGGL(k_pairs_bwd<false>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
                        st, a);
   PNR_LAUNCH_CHECK();
