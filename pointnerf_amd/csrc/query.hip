@@ -105,6 +105,48 @@ __global__ void __launch_bounds__(kQBlock) k_march(QRays q, QGrid g, int SR,
   }
 }
 
+// k_march for small ray batches (a training batch: a few thousand rays, far
+// fewer lanes than the chip holds): 16 lanes per ray test 16 consecutive
+// candidates at a time, a ballot orders the group's hits, so a ray's first SR
+// hits get the same slots as k_march's serial walk (same positions, same bits)
+// in ~D/16 dependent steps instead of D.
+constexpr int64_t kMarchCoopRays = 32768;
+__global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, QGrid g, int SR,
+                                                        const uint32_t* __restrict__ occ_bits,
+                                                        int32_t* __restrict__ n_filled,
+                                                        uint16_t* __restrict__ slot_d) {
+  const int lane = threadIdx.x & 63, gl = lane & 15;
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; r < q.R;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+    const int64_t cam = cam_of(q, r);
+    const float c[3] = {q.campos[cam * 3], q.campos[cam * 3 + 1], q.campos[cam * 3 + 2]};
+    const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
+    int n = 0;   // hits so far: the same in every lane of the group
+    for (int d0 = 0; d0 < q.D && n < SR; d0 += 16) {
+      const int d = d0 + gl;
+      bool hit = false;
+      if (d < q.D) {
+        float p[3];
+        ray_point(c, dir, tval(q, r, d), p);
+        const int x = vox_coord(p[0], g.shift[0], g.vs[0]);
+        const int y = vox_coord(p[1], g.shift[1], g.vs[1]);
+        const int z = vox_coord(p[2], g.shift[2], g.vs[2]);
+        if (!(x < 0 || x >= g.dims[0] || y < 0 || y >= g.dims[1] || z < 0 || z >= g.dims[2])) {
+          const int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
+          hit = (occ_bits[id >> 5] >> (id & 31)) & 1u;
+        }
+      }
+      const unsigned m = (unsigned)(__ballot(hit) >> (lane & 48)) & 0xffffu;
+      if (hit) {
+        const int pos = n + __popc(m & ((1u << gl) - 1u));
+        if (pos < SR) slot_d[r * SR + pos] = (uint16_t)d;
+      }
+      n += __popc(m);
+    }
+    if (gl == 0) n_filled[r] = n < SR ? n : SR;
+  }
+}
+
 __global__ void __launch_bounds__(kQBlock) k_fill_list(int64_t R, int SR, const int32_t* __restrict__ n_filled,
                                                        const int32_t* __restrict__ ray_off,
                                                        int32_t* __restrict__ fill_rs, int32_t* counts) {
@@ -564,8 +606,12 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
     PNR_HIP(hipMemsetAsync(b->valid_off, 0, sizeof(int32_t), st));
     return PNR_OK;
   }
-  hipLaunchKernelGGL(k_march, dim3(grid_for(R, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
-                     h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
+  if (R <= kMarchCoopRays)   // few rays: 16 lanes per ray (latency), else one (throughput)
+    hipLaunchKernelGGL(k_march_coop, dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
+                       h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
+  else
+    hipLaunchKernelGGL(k_march, dim3(grid_for(R, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
+                       h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   PNR_LAUNCH_CHECK();
   if ((rc = exclusive_scan(b->n_filled, R, nullptr, b->ray_off, b->counts + 0, b->scratch,
                            b->scratch_bytes, st)))

@@ -129,3 +129,25 @@ def test_scan_matches_cumsum(cuda):
         ref = np.concatenate([[0], np.cumsum(x.cpu().numpy())])
         assert np.array_equal(out.cpu().numpy(), ref)
         assert int(tot.item()) == ref[-1]
+
+
+def test_coop_march_equals_serial_march(cuda):
+    """k_march_coop (batches of <= 32768 rays: 16 lanes per ray, ballot-ordered
+    hits) and k_march (larger batches: one lane per ray) give the same slots:
+    the first 3000 rays of a 160x240 frame queried alone vs inside the frame."""
+    sc = scene(20000, H=160, W=240, theta=75.0)
+    q = _engine(sc, cuda)
+    xyz = torch.from_numpy(sc["xyz"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    R, SR = rd.shape[0], sc["opt"].SR
+    assert R > 32768
+    big, _, _, _ = q.run(xyz, rd, cp, cr, 2.0, 6.0)
+    nf_big = big.n_filled[:3000].clone()
+    sd_big = big.slot_d[: R * SR].view(R, SR)[:3000].clone()
+    small, _, _, _ = q.run(xyz, rd[:3000].contiguous(), cp, cr, 2.0, 6.0)
+    nf = small.n_filled[:3000]
+    assert torch.equal(nf, nf_big) and int(nf.sum()) > 1000
+    sd = small.slot_d[: 3000 * SR].view(3000, SR)
+    keep = torch.arange(SR, device=cuda)[None, :] < nf[:, None]
+    assert torch.equal(sd[keep], sd_big[keep])
