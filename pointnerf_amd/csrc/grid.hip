@@ -225,16 +225,32 @@ __global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const
     const int off = slot_off[s];
     const int keep = min(cnt, g.P);
     int prev = -1;
-    for (int q = 0; q < keep; ++q) {
-      int best = 0x7fffffff;
-      for (int j = 0; j < cnt; ++j) {
-        int v = bucket[off + j];
-        best = (v > prev && v < best) ? v : best;
+    if (cnt <= 16) {
+      // the (typical) small voxel: its ids in registers, one round of loads
+      int vals[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) vals[j] = j < cnt ? bucket[off + j] : 0x7fffffff;
+      for (int q = 0; q < keep; ++q) {
+        int best = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) best = (vals[j] > prev && vals[j] < best) ? vals[j] : best;
+        prev = best;
+        occ_pts[(int64_t)s * g.P + q] =
+            make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
+                        __int_as_float(best));
       }
-      prev = best;
-      occ_pts[(int64_t)s * g.P + q] =
-          make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
-                      __int_as_float(best));
+    } else {
+      for (int q = 0; q < keep; ++q) {
+        int best = 0x7fffffff;
+        for (int j = 0; j < cnt; ++j) {
+          int v = bucket[off + j];
+          best = (v > prev && v < best) ? v : best;
+        }
+        prev = best;
+        occ_pts[(int64_t)s * g.P + q] =
+            make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
+                        __int_as_float(best));
+      }
     }
     dropped += cnt - keep;
     mx = max(mx, cnt);
