@@ -419,6 +419,15 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             const float* d_feat, const float* d_hid, float* dz1, float* dz2,
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
+/* The points referenced by a query's neighbour rows (pnr_points.used /
+ * used_map for a training batch): flags[n_points] (scratch), used_map[p] = rank
+ * of p among the referenced points or -1, used[0 .. *n_used_dev) = the referenced
+ * points ascending; rows pidx[0 .. (*n_samples_dev) * K) (n_samples_dev NULL:
+ * cap_samples).  No host synchronisation (the count stays on the device). */
+int pnr_used_points_scratch_bytes(int64_t n_points, size_t* out);
+int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev, int32_t K, int64_t cap_samples,
+                    int64_t n_points, int32_t* flags, int32_t* used_map, int32_t* used, int32_t* n_used_dev,
+                    void* scratch, size_t scratch_bytes, void* stream);
 /* d_p1[row(p)] = sum of dz1[pair] over the pairs of point p, given the pairs'
  * point rows sorted (stable: each point's pairs in pair order, a deterministic
  * sum) and the pair index of each sorted entry: the atomic-free alternative to

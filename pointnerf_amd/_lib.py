@@ -156,6 +156,9 @@ SIGNATURES = {
     "pnr_aggregate_bwd_pairs_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(MlpBwdX3), P(AggSaved),
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_used_points_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
+    "pnr_used_points": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_pairs_to_points": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_pack_weights": (c_int, [c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,
                                  c_void_p, c_size_t, c_void_p]),

@@ -1294,6 +1294,26 @@ __global__ void __launch_bounds__(256) k_extras_bwd(BwdArgs A) {
   }
 }
 
+// pnr_used_points: flag the points referenced by the first (*n_dev) samples'
+// neighbour rows, rank them (scan), list them in ascending order.
+__global__ void k_mark_used(const int32_t* __restrict__ pidx, const int32_t* __restrict__ n_dev, int K, int64_t cap,
+                            int32_t* __restrict__ flags) {
+  const int64_t n = (n_dev ? (int64_t)*n_dev : cap) * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t p = pidx[i];
+    if (p >= 0) flags[p] = 1;
+  }
+}
+
+__global__ void k_used_list(const int32_t* __restrict__ flags, int64_t n_points, int32_t* __restrict__ used_map,
+                            int32_t* __restrict__ used) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n_points;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    if (flags[p]) used[used_map[p]] = (int32_t)p;
+    else used_map[p] = -1;
+  }
+}
+
 // d P1 rows from dz1 without atomics: pairs sorted by point row (stable, so
 // each point's pairs in pair order -- a deterministic sum); one wave per run of
 // equal rows, lane = 4 neurons (float4).
@@ -1712,6 +1732,31 @@ extern "C" int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_sampl
   PNR_CHECK_ARG(wbx, "aggregate_bwd_x3: null split weight packs");
   return bwd_pairs(pts, s, w, wb, wbx, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
                    d_conf, stream);
+}
+
+extern "C" int pnr_used_points_scratch_bytes(int64_t n_points, size_t* out) {
+  PNR_CHECK_ARG(out && n_points >= 0, "used_points_scratch_bytes: bad args");
+  *out = scan_scratch_bytes(n_points);
+  return PNR_OK;
+}
+
+extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev, int32_t K, int64_t cap_samples,
+                               int64_t n_points, int32_t* flags, int32_t* used_map, int32_t* used, int32_t* n_used_dev,
+                               void* scratch, size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(pidx && flags && used_map && used && n_used_dev && K > 0 && cap_samples >= 0 && n_points > 0,
+                "used_points: bad args");
+  hipStream_t st = as_stream(stream);
+  PNR_HIP(hipMemsetAsync(flags, 0, (size_t)n_points * sizeof(int32_t), st));
+  if (cap_samples > 0) {
+    hipLaunchKernelGGL(k_mark_used, dim3(grid_for(cap_samples * K, 256)), dim3(256), 0, st, pidx, n_samples_dev, K,
+                       cap_samples, flags);
+    PNR_LAUNCH_CHECK();
+  }
+  int rc;
+  if ((rc = exclusive_scan(flags, n_points, nullptr, used_map, n_used_dev, scratch, scratch_bytes, st, 0))) return rc;
+  hipLaunchKernelGGL(k_used_list, dim3(grid_for(n_points, 256)), dim3(256), 0, st, flags, n_points, used_map, used);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
 }
 
 extern "C" int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,

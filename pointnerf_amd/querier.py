@@ -102,7 +102,8 @@ class QueryBuffers:
         c = self.counts.cpu()
         n_cand = int(c[6:8].view(torch.int64).item())
         c = c.tolist()
-        return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand)
+        return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand,
+                    n_used=c[5])   # n_used: pnr_used_points' count when the caller put it in counts[5]
 
 
 class GridHandle:

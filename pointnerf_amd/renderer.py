@@ -510,6 +510,10 @@ class NeuralPointsRayMarching(nn.Module):
         rd = raydir.float().contiguous()
         xyz = np_.xyz.detach().contiguous()
         bufs, hp, rays, qp = q.run(xyz, rd, campos, camrot, near, far, bufs=None)
+        # block1.0's point half only for the points this batch references (device
+        # list, its count read with the query counts: one host sync)
+        from .train import used_points_device
+        used_buf, used_map = used_points_device(bufs, K, xyz.shape[0])
         cnt = bufs.read_counts()
         self.last_counts = cnt
         Sv = cnt["S_valid"]
@@ -521,9 +525,7 @@ class NeuralPointsRayMarching(nn.Module):
         def tab(t, c):
             return None if t is None else t.reshape(n, c)
 
-        # block1.0's point half only for the points this batch references
-        from .train import used_points
-        used = used_points(bufs.pidx[:cnt["S_filled"] * K], n)
+        used = (used_buf[:cnt["n_used"]], used_map)
         if self.train_precision not in ("fp32", "fp32x3"):
             raise L.PnrError(f"train_precision {self.train_precision!r}: 'fp32x3' or 'fp32'")
         spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd),
@@ -567,14 +569,20 @@ class NeuralPointsRayMarching(nn.Module):
         of the empty-slot entries)."""
         pidx = self.last_train_aux["sample_pidx"]
         conf = self.neural_points.points_conf.reshape(-1)
-        ids = pidx[pidx >= 0].long()
-        counts = torch.bincount(ids, minlength=conf.numel()).float()
-        counts[0] += (pidx < 0).sum()
-        used = counts > 0
-        c = conf[used]
-        cc = c - (c - torch.clamp(c, 1e-4, 1.0)).detach()        # gradiant_clamp
+        ids = pidx.reshape(-1).long()
+        N = conf.numel()
+        # entries per point (integers, exact in fp32), empty slots on point 0; no
+        # boolean indexing, so no host synchronisation: points with no entry
+        # contribute 0 * f(conf) (finite: conf is clamped) and no gradient.  The
+        # empty slots (most entries) are counted in 1024 spare bins first, not by
+        # atomics all on point 0.
+        spare = N + torch.arange(ids.numel(), device=ids.device) % 1024
+        counts = torch.zeros(N + 1024, dtype=torch.float32, device=conf.device)
+        counts.index_add_(0, torch.where(ids >= 0, ids, spare), torch.ones_like(ids, dtype=torch.float32))
+        counts = counts[:N] + torch.nn.functional.pad(counts[N:].sum().reshape(1), (0, N - 1))
+        cc = conf - (conf - torch.clamp(conf, 1e-4, 1.0)).detach()   # gradiant_clamp
         v = torch.clamp(cc, zero_epsilon, 1 - zero_epsilon)
-        return torch.sum(counts[used] * (torch.log(v) + torch.log(1 - v))) / pidx.numel()
+        return torch.sum(counts * (torch.log(v) + torch.log(1 - v))) / pidx.numel()
 
     @staticmethod
     def zero_one_loss(val, zero_epsilon: float = 1e-3):

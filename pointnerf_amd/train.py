@@ -87,6 +87,23 @@ class Saved:
         return self.t[k]
 
 
+def used_points_device(bufs, K: int, n_points: int):
+    """pnr_used_points on a query's buffers, count into bufs.counts[5] (read with
+    the other counts by the caller's one read_counts()): (used [N] buffer,
+    used_map [N]) -- slice used[:n_used] after the read."""
+    dev = bufs.pidx.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    flags, used_map, used = (torch.empty(n_points, **i32) for _ in range(3))
+    nb = L.c_size_t(0)
+    L.check(L.lib().pnr_used_points_scratch_bytes(n_points, L.ctypes.byref(nb)), "pnr_used_points_scratch_bytes")
+    scratch = torch.empty(max(int(nb.value), 16), dtype=torch.uint8, device=dev)
+    cap = bufs.pidx.numel() // K
+    L.check(L.lib().pnr_used_points(L.ptr(bufs.pidx), L.ptr(bufs.counts), K, cap, n_points, L.ptr(flags),
+                                    L.ptr(used_map), L.ptr(used), L.c_void_p(bufs.counts.data_ptr() + 20),
+                                    L.ptr(scratch), scratch.numel(), L.stream_ptr(dev)), "pnr_used_points")
+    return used, used_map
+
+
 def used_points(pidx: torch.Tensor, n_points: int):
     """(used, used_map): sorted point rows referenced by a query's sample_pidx
     and the inverse map (-1 = unreferenced) -- pnr_points.used / used_map."""

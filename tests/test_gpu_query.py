@@ -151,3 +151,21 @@ def test_coop_march_equals_serial_march(cuda):
     sd = small.slot_d[: 3000 * SR].view(3000, SR)
     keep = torch.arange(SR, device=cuda)[None, :] < nf[:, None]
     assert torch.equal(sd[keep], sd_big[keep])
+
+
+def test_used_points_device_equals_torch(cuda):
+    """pnr_used_points (device list + map, count in counts[5]) == the torch
+    restatement train.used_points on the query's filled rows."""
+    from pointnerf_amd.train import used_points, used_points_device
+    sc = scene(20000, H=40, W=40, theta=50.0)
+    q = _engine(sc, cuda)
+    xyz = torch.from_numpy(sc["xyz"]).to(cuda)
+    bufs, _, _, _ = q.run(xyz, torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["campos"]).to(cuda),
+                          torch.from_numpy(sc["camrot"]).to(cuda), 2.0, 6.0)
+    K, N = sc["opt"].K, xyz.shape[0]
+    used_buf, used_map = used_points_device(bufs, K, N)
+    c = bufs.read_counts()
+    u_ref, m_ref = used_points(bufs.pidx[: c["S_filled"] * K], N)
+    assert c["n_used"] == u_ref.numel() > 100
+    assert torch.equal(used_buf[: c["n_used"]], u_ref)
+    assert torch.equal(used_map, m_ref)
