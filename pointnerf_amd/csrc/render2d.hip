@@ -36,10 +36,13 @@ struct ConvArgs {
   const float* wf;     // fragment-packed [ROWS, 9 * Cin] (k = tap * Cin + ci), ROWS = 32 * NT
   const float* bias;   // [ROWS] (trunk bias, rgb bias, zeros)
   int cout;            // trunk output channels (0 = rgb only)
-  float* out;          // [H, W, cout] = lrelu(trunk)   (cout > 0)
+  float* out;          // [H, W, ldo] = lrelu(trunk)   (cout > 0)
   float* rgb;          // [H, W, 3] accumulated (first stage writes, later add)
-  int rgb_mode;        // 0: rgb = part, 1: rgb += part, 2: out_rgb = sigmoid(rgb + part)
+  int rgb_mode;        // 0: rgb = part, 1: rgb += part, 2: out_rgb = sigmoid(rgb + part),
+                       // 3: backward data gradient: out = acc * lrelu'(act) (act may be NULL), no bias
   float slope;
+  int ldo;             // floats per output pixel row (>= cout)
+  const float* act;    // [H, W, cout] forward activation whose LeakyReLU mask applies (mode 3)
 };
 
 template <int NT>
@@ -110,7 +113,20 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
     }
     // epilogue: rows 0..cout-1 trunk (lrelu), rows cout..cout+2 rgb
     const int xo = x0 + 32 * wid + c;
-    if (xo < a.W) {
+    if (xo < a.W && a.rgb_mode == 3) {
+      const int64_t pix = (int64_t)y * a.W + xo;
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (co < a.cout) {
+            // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
+            const float m = a.act == nullptr || a.act[pix * a.cout + co] > 0.f ? 1.f : a.slope;
+            a.out[pix * a.ldo + co] = acc[T][r] * m;
+          }
+        }
+    } else if (xo < a.W) {
       const int64_t pix = (int64_t)y * a.W + xo;
 #pragma unroll
       for (int T = 0; T < NT; ++T)
@@ -119,7 +135,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
           const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
           const float v = acc[T][r] + a.bias[co];
           if (co < a.cout) {
-            a.out[pix * a.cout + co] = v > 0.f ? v : v * a.slope;
+            a.out[pix * a.ldo + co] = v > 0.f ? v : v * a.slope;
           } else if (co < a.cout + 3) {
             float* o = a.rgb + pix * 3 + (co - a.cout);
             if (a.rgb_mode == 0) *o = v;
@@ -141,6 +157,154 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
   }
   const int64_t tiles = (int64_t)a.H * ((a.W + kRPx - 1) / kRPx);
   hipLaunchKernelGGL(k_conv3x3<NT>, dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+// ------------------------------------------------------------------ backward
+// Per stage the stacked rows' output gradient dY = [d trunk (pre-activation),
+// d rgb, zeros] is one [H, W, M] image ("cat" buffer, M = the stage's stacked
+// rows).  Its data gradient is a forward 3x3 convolution of dY with the
+// flipped, channel-transposed weights (k_conv3x3 in mode 3, the LeakyReLU mask
+// of the layer below in the epilogue); its weight gradient
+//   dW[m, tap, ci] = sum_p dY[p, m] X[p + off(tap), ci],  db[m] = sum_p dY[p, m]
+// is k_conv_wgrad: an implicit-GEMM A^T B over the pixels on fp32 MFMA (lane
+// order as pnr_gemm_tn: A rows and shifted B rows read straight from HBM,
+// 128-B segments), one wave per (pixel split, tap, 32-channel column tile),
+// partials summed over the splits in a fixed order (deterministic).
+
+// g = d_out * s (1 - s) (the sigmoid's gradient on the saved output s) into the
+// rgb slots of the three cat buffers; their pad channels zeroed.
+__global__ void k_nr_rgb_grad(const float* __restrict__ d_out, const float* __restrict__ out_rgb, int64_t npix,
+                              float* __restrict__ cat2, float* __restrict__ cat1, float* __restrict__ cat0) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    float g[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float s = out_rgb[p * 3 + j];
+      g[j] = d_out[p * 3 + j] * (s * (1.f - s));
+    }
+    float* c2 = cat2 + p * 32;   // [g, 0 x 29]
+    float* c1 = cat1 + p * 64;   // [dz1 (32), g, 0 x 29]
+    float* c0 = cat0 + p * 96;   // [dz0 (64), g, 0 x 29]
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const float v = j < 3 ? g[j] : 0.f;
+      c2[j] = v;
+      c1[32 + j] = v;
+      c0[64 + j] = v;
+    }
+  }
+}
+
+struct WgradArgs {
+  const float* dy;     // [npix, M]
+  const float* x;      // [npix, Cin] forward input of the stage
+  int H, W, M, Cin;
+  int64_t chunk;       // pixels per split (even)
+  float* part;         // [nsplit][M * 9 * Cin + M]
+};
+
+template <int MT>
+__global__ void __launch_bounds__(64) k_conv_wgrad(WgradArgs a) {
+  const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
+  const int split = blockIdx.x, tap = blockIdx.y, nt = blockIdx.z;
+  const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+  const int npix = a.H * a.W;                 // < 2^31 (checked by the caller)
+  const int p0 = split * (int)a.chunk;
+  const int p1 = p0 + (int)a.chunk < npix ? p0 + (int)a.chunk : npix;
+  const int ci = 32 * nt + c;
+  const bool colsum = tap == 0 && nt == 0;
+  f32x16r acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = (f32x16r){0.f};
+  float cs[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) cs[t] = 0.f;
+  // 4 pixel pairs per step: their loads issued together, then 4 MFMAs per tile
+  for (int q = p0; q < p1; q += 8) {   // wave-uniform trip count
+    float av[4][MT], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = q + 2 * u + h;
+      const bool ok = p < p1;
+      const int y = p / a.W, x = p - y * a.W;
+      const int ys = y + dy, xs = x + dx;
+      const bool in = ok && ys >= 0 && ys < a.H && xs >= 0 && xs < a.W;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) av[u][t] = ok ? a.dy[(int64_t)p * a.M + 32 * t + c] : 0.f;
+      bv[u] = in ? a.x[((int64_t)ys * a.W + xs) * a.Cin + ci] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][t], bv[u], acc[t], 0, 0, 0);
+        cs[t] += av[u][t];
+      }
+  }
+  const int N = 9 * a.Cin;
+  float* out = a.part + (int64_t)split * ((int64_t)a.M * N + a.M);
+  // C/D layout: row = (r&3) + 8(r>>2) + 4h, col = c
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + tap * a.Cin + ci] = acc[t][r];
+  if (colsum) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const float s = cs[t] + __shfl_xor(cs[t], 32);
+      if (h == 0) out[(int64_t)a.M * N + 32 * t + c] = s;
+    }
+  }
+}
+
+// out[i] = sum_s part[s][i], s ascending (fixed order).
+__global__ void k_sum_splits(const float* __restrict__ part, int64_t n, int nsplit, float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int q = 0; q < nsplit; ++q) s += part[(int64_t)q * n + i];
+    out[i] = s;
+  }
+}
+
+static void wgrad_plan(int64_t npix, int M, int Cin, int* nsplit, int64_t* chunk) {
+  const int waves_per_split = 9 * (Cin / 32);
+  int64_t s = cdiv((int64_t)2048, (int64_t)waves_per_split);   // ~8 waves per CU
+  const int64_t maxs = npix / 256 > 0 ? npix / 256 : 1;         // >= 256 pixels per split
+  if (s > maxs) s = maxs;
+  int64_t ch = cdiv(npix > 0 ? npix : 1, s);
+  ch = cdiv(ch, 2) * 2;
+  *chunk = ch;
+  *nsplit = (int)(npix > 0 ? cdiv(npix, ch) : 1);
+  (void)M;
+}
+
+static size_t wgrad_scratch(int64_t npix, int M, int Cin) {
+  int ns;
+  int64_t ch;
+  wgrad_plan(npix, M, Cin, &ns, &ch);
+  return (size_t)ns * ((size_t)M * 9 * Cin + M) * sizeof(float);
+}
+
+template <int MT>
+static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin, float* part, float* dw,
+                        hipStream_t st) {
+  WgradArgs g;
+  g.dy = dyb;
+  g.x = x;
+  g.H = H;
+  g.W = W;
+  g.M = 32 * MT;
+  g.Cin = Cin;
+  int ns;
+  wgrad_plan((int64_t)H * W, g.M, Cin, &ns, &g.chunk);
+  g.part = part;
+  hipLaunchKernelGGL(k_conv_wgrad<MT>, dim3(ns, 9, Cin / 32), dim3(64), 0, st, g);
+  PNR_LAUNCH_CHECK();
+  const int64_t n = (int64_t)g.M * 9 * Cin + g.M;
+  hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, part, n, ns, dw);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
@@ -172,12 +336,14 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.H = H;
   a.W = W;
   a.slope = w->neg_slope;
+  a.act = nullptr;
   // stage 0: x (128) -> net0 (64) + rgb = conv_rgb0(x)
   a.in = x;
   a.Cin = 128;
   a.wf = w->wf0;
   a.bias = w->b0;
   a.cout = 64;
+  a.ldo = 64;
   a.out = net0;
   a.rgb = out_rgb;
   a.rgb_mode = 0;
@@ -188,6 +354,7 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.wf = w->wf1;
   a.bias = w->b1;
   a.cout = 32;
+  a.ldo = 32;
   a.out = net1;
   a.rgb_mode = 1;
   if ((rc = launch_conv<2>(a, st))) return rc;
@@ -197,7 +364,89 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.wf = w->wf2;
   a.bias = w->b2;
   a.cout = 0;
+  a.ldo = 0;
   a.out = nullptr;
   a.rgb_mode = 2;
   return launch_conv<1>(a, st);
+}
+
+extern "C" int pnr_neural_render_bwd_scratch_bytes(int32_t H, int32_t W, size_t* out) {
+  PNR_CHECK_ARG(out && H >= 0 && W >= 0, "neural_render_bwd_scratch_bytes: bad args");
+  const int64_t npix = (int64_t)H * W;
+  size_t part = wgrad_scratch(npix, 96, 128);
+  const size_t p1 = wgrad_scratch(npix, 64, 64), p2 = wgrad_scratch(npix, 32, 32);
+  if (p1 > part) part = p1;
+  if (p2 > part) part = p2;
+  *out = (size_t)npix * (32 + 64 + 96) * sizeof(float) + part;
+  return PNR_OK;
+}
+
+extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, const float* out_rgb,
+                                     const float* d_out, int32_t H, int32_t W, const pnr_neural_render_wt* wt,
+                                     float* d_x, float* dw0, float* dw1, float* dw2, void* scratch,
+                                     size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(x && fwd_scratch && out_rgb && d_out && wt && d_x && dw0 && dw1 && dw2 && scratch,
+                "neural_render_bwd: null pointer");
+  PNR_CHECK_ARG(wt->wt0 && wt->wt1 && wt->wt2, "neural_render_bwd: null weight");
+  PNR_CHECK_ARG(H >= 0 && W >= 0 && (int64_t)H * W < (1ll << 30), "neural_render_bwd: bad image size");
+  PNR_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)fwd_scratch & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+                "neural_render_bwd: x, fwd_scratch and scratch must be 16-B aligned");
+  size_t need;
+  pnr_neural_render_bwd_scratch_bytes(H, W, &need);
+  PNR_CHECK_ARG(scratch_bytes >= need, "neural_render_bwd: scratch too small");
+  hipStream_t st = as_stream(stream);
+  const int64_t npix = (int64_t)H * W;
+  if (npix == 0) {
+    PNR_HIP(hipMemsetAsync(dw0, 0, (96 * 9 * 128 + 96) * sizeof(float), st));
+    PNR_HIP(hipMemsetAsync(dw1, 0, (64 * 9 * 64 + 64) * sizeof(float), st));
+    PNR_HIP(hipMemsetAsync(dw2, 0, (32 * 9 * 32 + 32) * sizeof(float), st));
+    return PNR_OK;
+  }
+  const float* net0 = fwd_scratch;
+  const float* net1 = fwd_scratch + (size_t)npix * 64;
+  float* cat2 = static_cast<float*>(scratch);
+  float* cat1 = cat2 + (size_t)npix * 32;
+  float* cat0 = cat1 + (size_t)npix * 64;
+  float* part = cat0 + (size_t)npix * 96;
+  hipLaunchKernelGGL(k_nr_rgb_grad, dim3(grid_for(npix, 256, 2048)), dim3(256), 0, st, d_out, out_rgb, npix, cat2,
+                     cat1, cat0);
+  PNR_LAUNCH_CHECK();
+  int rc;
+  ConvArgs a;
+  a.H = H;
+  a.W = W;
+  a.slope = wt->neg_slope;
+  a.bias = nullptr;
+  a.rgb = nullptr;
+  a.rgb_mode = 3;
+  // stage 2: d net1 = conv(cat2 = [g, 0], flipped conv_rgb.2), masked by net1 -> cat1[:, :32]
+  a.in = cat2;
+  a.Cin = 32;
+  a.wf = wt->wt2;
+  a.cout = 32;
+  a.ldo = 64;
+  a.out = cat1;
+  a.act = net1;
+  if ((rc = launch_conv<1>(a, st))) return rc;
+  if ((rc = launch_wgrad<1>(cat2, net1, H, W, 32, part, dw2, st))) return rc;
+  // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
+  a.in = cat1;
+  a.Cin = 64;
+  a.wf = wt->wt1;
+  a.cout = 64;
+  a.ldo = 96;
+  a.out = cat0;
+  a.act = net0;
+  if ((rc = launch_conv<2>(a, st))) return rc;
+  if ((rc = launch_wgrad<2>(cat1, net0, H, W, 64, part, dw1, st))) return rc;
+  // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
+  a.in = cat0;
+  a.Cin = 96;
+  a.wf = wt->wt0;
+  a.cout = 128;
+  a.ldo = 128;
+  a.out = d_x;
+  a.act = nullptr;
+  if ((rc = launch_conv<4>(a, st))) return rc;
+  return launch_wgrad<3>(cat0, x, H, W, 128, part, dw0, st);
 }

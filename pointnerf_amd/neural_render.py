@@ -5,10 +5,13 @@ models/neural_render/neural_renderer.py:7-104 for the configuration the fork
 builds, ``NeuralRenderer(input_dim=128)`` (neural_points_volumetric_model.py:258-260):
 n_feat 128 (conv_in = identity), img_size 64 -> 2 blocks, rgb skips, no norm,
 LeakyReLU(0.2), final sigmoid -- so ``neural_render_2d.*`` checkpoint keys load.
-Forward (no grad) runs ``pnr_neural_render_fwd``: three fused implicit-GEMM 3x3
-convolutions on fp32 MFMA.  With autograd enabled the same module computes with
-torch convolutions (MIOpen) so the finetune step can train it; the HIP kernels
-are inference-only in this round.
+Forward runs ``pnr_neural_render_fwd``: three fused implicit-GEMM 3x3
+convolutions on fp32 MFMA.  With autograd enabled ``NeuralRenderFn`` keeps the
+forward's activations and its backward runs ``pnr_neural_render_bwd`` (data
+gradients as flipped-weight convolutions on the same kernel, weight gradients
+as implicit-GEMM reductions over the pixels, deterministic), the gradients of
+the reference's torch autograd through neural_renderer.py:81-104.
+``forward_torch`` is the torch-convolution restatement the tests check against.
 """
 from __future__ import annotations
 
@@ -67,6 +70,25 @@ class NeuralRenderer(nn.Module):
         self._packed, self._packed_key = (w, t), key
         return self._packed
 
+    @staticmethod
+    def _stack_t(trunk, rgb, rows):
+        """Data-gradient weights of a stage: the stacked [rows, cin, 3, 3] weights
+        flipped and transposed to [cin, 9 * rows] (k = (ky'*3 + kx') * rows + j,
+        value W[j, ci, 2 - ky', 2 - kx']), fragment-packed (pnr_neural_render_wt)."""
+        ws = ([trunk.weight] if trunk is not None else []) + [rgb.weight]
+        W = torch.cat(ws, 0).float()
+        cin = W.shape[1]
+        Wp = torch.zeros((rows, cin, 3, 3), dtype=torch.float32, device=W.device)
+        Wp[: W.shape[0]] = W
+        return frag_pack(Wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, 9 * rows).contiguous())
+
+    def packed_t(self):
+        with torch.no_grad():
+            t = dict(wt0=self._stack_t(self.conv_layers[0], self.conv_rgb[0], 96),
+                     wt1=self._stack_t(self.conv_layers[1], self.conv_rgb[1], 64),
+                     wt2=self._stack_t(None, self.conv_rgb[2], 32))
+        return L.NeuralRenderWT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(), 0.2), t
+
     def forward_torch(self, x):
         """neural_renderer.py:81-104 with torch convolutions (autograd path)."""
         x = x.permute(0, 3, 1, 2)
@@ -77,10 +99,8 @@ class NeuralRenderer(nn.Module):
             rgb = rgb + self.conv_rgb[i + 1](net)
         return torch.sigmoid(rgb).permute(0, 2, 3, 1)
 
-    def forward(self, x):
-        """x [1, H, W, 128] -> rgb [1, H, W, 3]."""
-        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
-            return self.forward_torch(x)
+    def _fwd(self, x):
+        """pnr_neural_render_fwd -> (rgb [H*W, 3], x [H*W, 128], forward scratch)."""
         L.require_gpu(x)
         B, H, W, C = x.shape
         if B != 1 or C != 128:
@@ -93,4 +113,59 @@ class NeuralRenderer(nn.Module):
         w, _keep = self.packed()
         L.check(L.lib().pnr_neural_render_fwd(L.ptr(xc), H, W, L.ctypes.byref(w), L.ptr(out), L.ptr(scratch),
                                               scratch.numel() * 4, L.stream_ptr(x.device)), "pnr_neural_render_fwd")
-        return out.view(1, H, W, 3)
+        return out, xc, scratch
+
+    def forward(self, x):
+        """x [1, H, W, 128] -> rgb [1, H, W, 3]."""
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return NeuralRenderFn.apply(x, self, *self.parameters())
+        out, _, _ = self._fwd(x)
+        return out.view(1, *x.shape[1:3], 3)
+
+
+class NeuralRenderFn(torch.autograd.Function):
+    """Autograd of NeuralRenderer on libpnr: forward pnr_neural_render_fwd (its
+    net0 / net1 kept), backward pnr_neural_render_bwd -> d x and the gradients of
+    conv_layers.{0,1} / conv_rgb.{0,1,2} weight and bias (parameters() order)."""
+
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        out, xc, scratch = mod._fwd(x.detach())
+        ctx.mod, ctx.shape = mod, x.shape
+        ctx.save_for_backward(xc, scratch, out)
+        return out.view(1, *x.shape[1:3], 3)
+
+    @staticmethod
+    def backward(ctx, d_out):
+        xc, fscr, out = ctx.saved_tensors
+        mod = ctx.mod
+        _, H, W, _ = ctx.shape
+        dev = xc.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        d_out = d_out.reshape(H * W, 3).float().contiguous()
+        wt, _keep = mod.packed_t()
+        nb = L.c_size_t(0)
+        L.check(L.lib().pnr_neural_render_bwd_scratch_bytes(H, W, L.ctypes.byref(nb)),
+                "pnr_neural_render_bwd_scratch_bytes")
+        scratch = torch.empty(max(int(nb.value) // 4, 4), **f32)
+        d_x = torch.empty((H * W, 128), **f32)
+        dws = [torch.empty(M * 9 * cin + M, **f32) for M, cin in ((96, 128), (64, 64), (32, 32))]
+        L.check(L.lib().pnr_neural_render_bwd(L.ptr(xc), L.ptr(fscr), L.ptr(out), L.ptr(d_out), H, W,
+                                              L.ctypes.byref(wt), L.ptr(d_x), *(L.ptr(d) for d in dws),
+                                              L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
+                "pnr_neural_render_bwd")
+
+        def split(dw, M, cin, cout):
+            w = dw[: M * 9 * cin].view(M, 3, 3, cin).permute(0, 3, 1, 2)
+            b = dw[M * 9 * cin:]
+            return (w[:cout], b[:cout]), (w[cout:cout + 3], b[cout:cout + 3])
+
+        (gw0, gb0), (gr0, grb0) = split(dws[0], 96, 128, 64)
+        (gw1, gb1), (gr1, grb1) = split(dws[1], 64, 64, 32)
+        _, (gr2, grb2) = split(dws[2], 32, 32, 0)
+        grads = {"conv_layers.0.weight": gw0, "conv_layers.0.bias": gb0, "conv_layers.1.weight": gw1,
+                 "conv_layers.1.bias": gb1, "conv_rgb.0.weight": gr0, "conv_rgb.0.bias": grb0,
+                 "conv_rgb.1.weight": gr1, "conv_rgb.1.bias": grb1, "conv_rgb.2.weight": gr2,
+                 "conv_rgb.2.bias": grb2}
+        pg = [grads[n].contiguous() for n, _ in mod.named_parameters()]
+        return (d_x.view(ctx.shape), None, *pg)
