@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 9
+#define PNR_ABI_VERSION 10
 
 enum {
   PNR_OK = 0,
@@ -462,8 +462,9 @@ int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, cons
  * mvs_points_volumetric_model.py:102-123 setup_optimizer):
  * C[M,N] = A^T B over K rows (A[K,M], B[K,N] row-major,
  * leading dimensions lda/ldb), colsum_a[M] = column sums of A (bias gradient,
- * may be NULL).  M, N multiples of 32.  Split-K on MFMA with a deterministic
- * ordered reduction; scratch of pnr_gemm_tn_scratch_bytes(K, M, N). */
+ * may be NULL).  M, N multiples of 32; scratch, C and colsum_a 16-B aligned.
+ * Split-K on MFMA with a deterministic ordered reduction (its last level writes
+ * C and colsum_a directly); scratch of pnr_gemm_tn_scratch_bytes(K, M, N). */
 int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t* out);
 int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
                 float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream);
@@ -473,6 +474,15 @@ int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_
  * fp64 GEMM ~ native fp32's).  The training path's default. */
 int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
                    float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream);
+
+/* Data-gradient product of the backward (dX = dZ W of an nn.Linear, replacing
+ * the autograd mm of color_branch / block1.0, point_aggregators.py:488-646):
+ * C[M,N] = A[M,K] B[K,N], row-major with unit column strides, exact fp32
+ * products on fp32 MFMA; with act != NULL each C[m,n] is multiplied by the
+ * LeakyReLU derivative of the saved activation act[m,n] (1 if > 0, else slope).
+ * N a multiple of 32 in [32, 256]; any M >= 0, K > 0. */
+int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K, int32_t N,
+                const float* act, int64_t ld_act, float slope, float* C, int64_t ldc, void* stream);
 
 /* X1[p] = [emb_p, PE_3(emb_p)] (block1.0 columns 0..223) for p < n, and the
  * matching backward d_emb[p] += dX1[p] . dX1/d emb (networks.py:175-190). */
@@ -542,6 +552,30 @@ typedef struct {
 int pnr_neural_render_scratch_bytes(int32_t H, int32_t W, size_t* out);
 int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const pnr_neural_render_w* w,
                           float* out_rgb, void* scratch, size_t scratch_bytes, void* stream);
+
+/* Backward of pnr_neural_render_fwd (the autograd of neural_renderer.py:81-104
+ * that the reference's finetune step takes through torch convolutions).
+ * fwd_scratch = the forward's scratch after that call (net0[H,W,64] then
+ * net1[H,W,32]); out_rgb its output; d_out = dL/d out_rgb.  Per stage the
+ * data-gradient weights are the stacked rows of pnr_neural_render_w flipped
+ * and transposed: rows = the stage's input channels ci (128 / 64 / 32),
+ * columns k = (ky'*3 + kx')*M + j with value Wstack[j][ci][2-ky'][2-kx'],
+ * j < M = 96 / 64 / 32 stacked rows (trunk, rgb, zero), frag_pack-ed.
+ * Writes d_x[H,W,128] and dw_s = [M, 9*cin] stacked weight gradients (layout of
+ * the forward's stacked rows before packing) followed by db_s[M]:
+ * dw0 [96*1152 + 96], dw1 [64*576 + 64], dw2 [32*288 + 32].  Fixed-order
+ * reductions: bitwise repeatable. */
+typedef struct {
+  const float* wt0;   /* 128 rows x 9*96 */
+  const float* wt1;   /* 64 rows x 9*64 */
+  const float* wt2;   /* 32 rows x 9*32 */
+  float neg_slope;
+} pnr_neural_render_wt;
+
+int pnr_neural_render_bwd_scratch_bytes(int32_t H, int32_t W, size_t* out);
+int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, const float* out_rgb, const float* d_out,
+                          int32_t H, int32_t W, const pnr_neural_render_wt* wt, float* d_x, float* dw0,
+                          float* dw1, float* dw2, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ------------------------------------------------------ upstream RGB head
  * C_out = 3 mode (shading_color_channel_num 3): for v < min(*n_dev, n_max)

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class PnrError(RuntimeError):
@@ -67,6 +67,10 @@ class Mlp(ctypes.Structure):
 class NeuralRenderW(ctypes.Structure):
     _fields_ = [("wf0", c_void_p), ("b0", c_void_p), ("wf1", c_void_p), ("b1", c_void_p), ("wf2", c_void_p),
                 ("b2", c_void_p), ("neg_slope", c_float)]
+
+
+class NeuralRenderWT(ctypes.Structure):
+    _fields_ = [("wt0", c_void_p), ("wt1", c_void_p), ("wt2", c_void_p), ("neg_slope", c_float)]
 
 
 class MlpBf16(ctypes.Structure):
@@ -167,6 +171,8 @@ SIGNATURES = {
                             c_void_p, c_size_t, c_void_p]),
     "pnr_gemm_tn_x3": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                                c_void_p, c_size_t, c_void_p]),
+    "pnr_gemm_nn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int64,
+                            c_float, c_void_p, c_int64, c_void_p]),
     "pnr_point_pe3": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_point_pe3_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_composite_bwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams), c_void_p,
@@ -180,6 +186,9 @@ SIGNATURES = {
     "pnr_neural_render_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
     "pnr_neural_render_fwd": (c_int, [c_void_p, c_int32, c_int32, P(NeuralRenderW), c_void_p, c_void_p, c_size_t,
                                       c_void_p]),
+    "pnr_neural_render_bwd_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
+    "pnr_neural_render_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, P(NeuralRenderWT),
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_rgb_head_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p,
                                  c_void_p]),
     "pnr_rgb_head_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32,
@@ -256,6 +265,23 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = T
     check(fn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
              scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")
     return (C, cs) if colsum else C
+
+
+def gemm_nn(A: torch.Tensor, B: torch.Tensor, act: torch.Tensor | None = None, slope: float = 0.0,
+            out: torch.Tensor | None = None):
+    """C = A B (A [M,K], B [K,N], unit column strides) on pnr_gemm_nn (exact fp32
+    products, fp32 MFMA); with act: C *= where(act > 0, 1, slope) (the LeakyReLU
+    derivative of the saved activation).  out: optional [M,N] destination view."""
+    M, K = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == K and A.stride(1) == 1 and B.stride(1) == 1
+    assert act is None or (act.shape == (M, N) and act.stride(1) == 1)
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device) if out is None else out
+    assert C.shape == (M, N) and C.stride(1) == 1
+    check(lib().pnr_gemm_nn(ptr(A), A.stride(0), ptr(B), B.stride(0), M, K, N, ptr(act),
+                            act.stride(0) if act is not None else 0, float(slope), ptr(C), C.stride(0),
+                            stream_ptr(A.device)), "pnr_gemm_nn")
+    return C
 
 
 def aggregate_scratch_bf16(n_max: int, n_points: int, device) -> torch.Tensor:

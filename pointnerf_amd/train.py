@@ -5,8 +5,8 @@ runs ``pnr_aggregate_fwd_train`` (native-fp32 MFMA) or ``pnr_aggregate_fwd_train
 (the per-pair chain on the fp32x3 split-bf16 MFMA kernel, the training default)
 / ``pnr_composite_fwd`` and whose backward runs
 
-  colour branch backward      weight gradients on pnr_gemm_tn_x3, the small dX
-                              products (n x 128 x 128) on hipBLASLt (torch.matmul)
+  colour branch backward      weight gradients on pnr_gemm_tn_x3, the dX products
+                              (n x 128 x 128, LeakyReLU derivative fused) on pnr_gemm_nn
   pnr_aggregate_bwd_pairs     fused per-pair dX chain on MFMA (k_pairs_bwd; with
   (_x3)                       train_precision fp32x3 its three dX GEMMs on split-bf16
                               MFMA, fp32-accurate): alpha
@@ -202,12 +202,12 @@ class AggregateFn(torch.autograd.Function):
         dc = d_feat[:n, 1:] * vm
         hc1, hc2, hc3 = sv["hc1"][:n], sv["hc2"][:n], sv["hc3"][:n]
         # weight gradients dW = dZ^T X on pnr_gemm_tn_x3 (bias = column sums); the
-        # small dX = dZ W products (n x 128 x 128) stay on hipBLASLt
+        # dX = dZ W products with the LeakyReLU derivative fused on pnr_gemm_nn
         dz = _lrelu_grad(dc, hc3, slope).contiguous()
         grads["color_branch.4.weight"], grads["color_branch.4.bias"] = L.gemm_tn(dz, hc2.contiguous(), colsum=True)
-        dz = _lrelu_grad(dz @ P["color_branch.4.weight"], hc2, slope).contiguous()
+        dz = L.gemm_nn(dz, P["color_branch.4.weight"], act=hc2, slope=slope)
         grads["color_branch.2.weight"], grads["color_branch.2.bias"] = L.gemm_tn(dz, hc1.contiguous(), colsum=True)
-        dz = _lrelu_grad(dz @ P["color_branch.2.weight"], hc1, slope).contiguous()
+        dz = L.gemm_nn(dz, P["color_branch.2.weight"], act=hc1, slope=slope)
         gC0 = torch.empty((128, 280), **f32)
         gC0[:, :256], grads["color_branch.0.bias"] = L.gemm_tn(dz, sv["hid"][:n], colsum=True)
         vpe32 = torch.zeros((n, 32), **f32)
@@ -215,7 +215,7 @@ class AggregateFn(torch.autograd.Function):
         gC0[:, 256:] = L.gemm_tn(dz, vpe32)[:, :24]
         grads["color_branch.0.weight"] = gC0
         d_hid = torch.zeros((max(n_max, 1), 256), **f32)
-        d_hid[:n] = dz @ P["color_branch.0.weight"][:, :256]
+        L.gemm_nn(dz, P["color_branch.0.weight"][:, :256], out=d_hid[:n])
         # ---- per-pair chain on MFMA
         Pn = max(n_max, 1) * 8
         dz1, dz2, dz3, dz4 = (torch.empty((Pn, 256), **f32) for _ in range(4))
@@ -268,7 +268,7 @@ class AggregateFn(torch.autograd.Function):
         gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True)   # sum_p dP1 = sum_pairs dz1
         gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m])[:, :60]
         grads["block1.0.weight"] = gW1
-        dx1 = (d_p1 @ P["block1.0.weight"][:, :224]).contiguous()
+        dx1 = (d_p1 @ P["block1.0.weight"][:, :224]).contiguous()   # plain GEMM: hipBLASLt
         d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
         L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb_u), L.stream_ptr(dev)),
                 "pnr_point_pe3_bwd")

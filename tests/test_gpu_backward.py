@@ -220,6 +220,26 @@ def test_gemm_tn_vs_torch(cuda, K, M, N, x3):
         assert e3 <= 2 * e32 + 1e-12, (e3, e32)
 
 
+@pytest.mark.parametrize("M,K,N,masked", [(30001, 128, 128, True), (129, 128, 256, False), (5, 256, 224, False),
+                                          (0, 128, 128, True), (1000, 37, 64, True)])
+def test_gemm_nn_vs_torch(cuda, M, K, N, masked):
+    """pnr_gemm_nn (the colour-branch / block1.0 data-gradient products, LeakyReLU
+    derivative fused) against an fp64 product; ldb > N like W[:, :256]."""
+    from pointnerf_amd import _lib as L
+    g = torch.Generator(device=cuda).manual_seed(M + K + N)
+    A = torch.randn((M, K), device=cuda, generator=g)
+    B = torch.randn((K, N + 24), device=cuda, generator=g)[:, :N]
+    act = torch.randn((M, N), device=cuda, generator=g) if masked else None
+    C = L.gemm_nn(A, B, act=act, slope=0.2)
+    ref = A.double() @ B.double()
+    if masked:
+        ref = torch.where(act > 0, ref, ref * 0.2)
+    assert C.shape == (M, N)
+    if M:
+        close(C, ref.float(), "C", rel=1e-5, scale=2e-6)
+    assert torch.equal(C, L.gemm_nn(A, B, act=act, slope=0.2))
+
+
 def test_conf_coefficient_and_zero_one_loss(cuda):
     """conf_coefficient [1, R'', SR, K] (empty slots gather point 0, as
     torch.clamp(pidx, 0) does in the reference) and the zero_one loss gradient
