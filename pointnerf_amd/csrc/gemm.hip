@@ -429,7 +429,8 @@ static void launch_gemm_nn(const GemmNNArgs& g, hipStream_t st) {
   // 1.32x faster than one 256-row workgroup per CU at 200 k x 256 x 224); short M
   // (the ~30 k-row colour-branch batches): 64-row workgroups, so the grid still
   // spans the CUs
-  if (g.M >= 256 * 512) {
+  // (and NT 5..7 at any M: their 4-way column split over WM = 2's waves is uneven)
+  if (g.M >= 256 * 512 || (NT >= 5 && NT <= 7)) {
     hipLaunchKernelGGL((k_gemm_nn<NT, 4>), dim3((unsigned)cdiv(g.M, (int64_t)128)), dim3(512), 0, st, g);
   } else {
     hipLaunchKernelGGL((k_gemm_nn<NT, 2>), dim3((unsigned)cdiv(g.M, (int64_t)64)), dim3(512), 0, st, g);

@@ -6,7 +6,8 @@ runs ``pnr_aggregate_fwd_train`` (native-fp32 MFMA) or ``pnr_aggregate_fwd_train
 / ``pnr_composite_fwd`` and whose backward runs
 
   colour branch backward      weight gradients on pnr_gemm_tn_x3, the dX products
-                              (n x 128 x 128, LeakyReLU derivative fused) on pnr_gemm_nn
+                              (n x 128 x 128, LeakyReLU derivative fused) and block1.0's
+                              point-half dX1 = dP1 W1[:, :224] on pnr_gemm_nn
   pnr_aggregate_bwd_pairs     fused per-pair dX chain on MFMA (k_pairs_bwd; with
   (_x3)                       train_precision fp32x3 its three dX GEMMs on split-bf16
                               MFMA, fp32-accurate): alpha
@@ -268,7 +269,7 @@ class AggregateFn(torch.autograd.Function):
         gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True)   # sum_p dP1 = sum_pairs dz1
         gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m])[:, :60]
         grads["block1.0.weight"] = gW1
-        dx1 = (d_p1 @ P["block1.0.weight"][:, :224]).contiguous()   # plain GEMM: hipBLASLt
+        dx1 = L.gemm_nn(d_p1, P["block1.0.weight"][:, :224])
         d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
         L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb_u), L.stream_ptr(dev)),
                 "pnr_point_pe3_bwd")
