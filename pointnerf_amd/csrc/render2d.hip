@@ -39,13 +39,14 @@ struct ConvArgs {
   float* out;          // [H, W, ldo] = lrelu(trunk)   (cout > 0)
   float* rgb;          // [H, W, 3] accumulated (first stage writes, later add)
   int rgb_mode;        // 0: rgb = part, 1: rgb += part, 2: out_rgb = sigmoid(rgb + part),
-                       // 3: backward data gradient: out = acc * lrelu'(act) (act may be NULL), no bias
+                       // (BWD kernels: data gradient, out = acc * lrelu'(act), act may be NULL, no bias)
   float slope;
   int ldo;             // floats per output pixel row (>= cout)
   const float* act;    // [H, W, cout] forward activation whose LeakyReLU mask applies (mode 3)
 };
 
-template <int NT>
+// BWD: 0 forward, 1 data gradient, 2 data gradient times the LeakyReLU mask of a.act
+template <int NT, int BWD>
 __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_r[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -113,7 +114,8 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
     }
     // epilogue: rows 0..cout-1 trunk (lrelu), rows cout..cout+2 rgb
     const int xo = x0 + 32 * wid + c;
-    if (xo < a.W && a.rgb_mode == 3) {
+    if (BWD) {
+      if (xo >= a.W) continue;
       const int64_t pix = (int64_t)y * a.W + xo;
 #pragma unroll
       for (int T = 0; T < NT; ++T)
@@ -122,7 +124,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
           const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
           if (co < a.cout) {
             // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
-            const float m = a.act == nullptr || a.act[pix * a.cout + co] > 0.f ? 1.f : a.slope;
+            const float m = BWD == 1 || a.act[pix * a.cout + co] > 0.f ? 1.f : a.slope;
             a.out[pix * a.ldo + co] = acc[T][r] * m;
           }
         }
@@ -147,16 +149,16 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   }
 }
 
-template <int NT>
+template <int NT, int BWD = 0>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3<NT>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3<NT, BWD>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRLds));
     attr = true;
   }
   const int64_t tiles = (int64_t)a.H * ((a.W + kRPx - 1) / kRPx);
-  hipLaunchKernelGGL(k_conv3x3<NT>, dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
+  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
@@ -168,10 +170,9 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
 // flipped, channel-transposed weights (k_conv3x3 in mode 3, the LeakyReLU mask
 // of the layer below in the epilogue); its weight gradient
 //   dW[m, tap, ci] = sum_p dY[p, m] X[p + off(tap), ci],  db[m] = sum_p dY[p, m]
-// is k_conv_wgrad: an implicit-GEMM A^T B over the pixels on fp32 MFMA (lane
-// order as pnr_gemm_tn: A rows and shifted B rows read straight from HBM,
-// 128-B segments), one wave per (pixel split, tap, 32-channel column tile),
-// partials summed over the splits in a fixed order (deterministic).
+// is k_conv_wgrad: an implicit-GEMM A^T B over the pixels on fp32 MFMA, dY and
+// X chunks staged in LDS (below), partials summed over the pixel splits in a
+// fixed order (deterministic).
 
 // g = d_out * s (1 - s) (the sigmoid's gradient on the saved output s) into the
 // rgb slots of the three cat buffers; their pad channels zeroed.
@@ -201,63 +202,120 @@ struct WgradArgs {
   const float* dy;     // [npix, M]
   const float* x;      // [npix, Cin] forward input of the stage
   int H, W, M, Cin;
-  int64_t chunk;       // pixels per split (even)
+  int64_t chunk;       // pixels per split (multiple of 32)
   float* part;         // [nsplit][M * 9 * Cin + M]
 };
 
-template <int MT>
-__global__ void __launch_bounds__(64) k_conv_wgrad(WgradArgs a) {
-  const int lane = threadIdx.x, c = lane & 31, h = lane >> 5;
-  const int split = blockIdx.x, tap = blockIdx.y, nt = blockIdx.z;
-  const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-  const int npix = a.H * a.W;                 // < 2^31 (checked by the caller)
-  const int p0 = split * (int)a.chunk;
-  const int p1 = p0 + (int)a.chunk < npix ? p0 + (int)a.chunk : npix;
-  const int ci = 32 * nt + c;
-  const bool colsum = tap == 0 && nt == 0;
-  f32x16r acc[MT];
+// One 4-wave workgroup per (pixel split, kernel row ky): all M rows x the 3 taps
+// (ky, 0..2) x all Cin columns of dW.  Per 32-pixel chunk the dY rows
+// (32 x M, contiguous) and the 34 source pixels of the row above / at / below
+// (p0 + (ky-1) W - 1 .. +33, contiguous, zero outside the image) are staged in LDS
+// with float4 loads, the next chunk's loads in flight during this chunk's MFMAs;
+// a lane's B operand for tap kx is the staged pixel (p - p0) + kx, zeroed when
+// x + kx - 1 leaves the row.  So every dY element is read from HBM 3 times and
+// every X element 3 times (not 9 x Cin/32 and 9 x M/32 as one wave per tap and
+// tile would).  Wave w: column tiles j = w, w + 4, w + 8 of the 3 Cin/32
+// (tap, channel-tile) pairs, all M/32 row tiles.
+template <int MT, int NC>
+__global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
+  constexpr int M = 32 * MT, C = 32 * NC;
+  constexpr int PA = M % 64 == 0 ? M + 32 : M;      // LDS pitches: half-waves 32 banks apart
+  constexpr int PB = C % 64 == 0 ? C + 32 : C;
+  constexpr int NA4 = 32 * M / 4, NB4 = 34 * C / 4;
+  constexpr int RA = (NA4 + 255) / 256, RB = (NB4 + 255) / 256;
+  constexpr int NJ = 3 * NC, JW = (NJ + 3) / 4;     // column tiles, per wave
+  __shared__ __attribute__((aligned(16))) float as[32 * PA];
+  __shared__ __attribute__((aligned(16))) float bs[34 * PB];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int split = blockIdx.x, ky = blockIdx.y;
+  const int npix = a.H * a.W;                 // < 2^30 (checked by the caller)
+  const int pbeg = split * (int)a.chunk;
+  const int pend = pbeg + (int)a.chunk < npix ? pbeg + (int)a.chunk : npix;
+  float4 ra[RA], rb[RB];
+  auto load = [&](int p0) {
 #pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = (f32x16r){0.f};
-  float cs[MT];
+    for (int j = 0; j < RA; ++j) {
+      const int i = tid + 256 * j, e = 4 * i, r = e / M;
+      ra[j] = i < NA4 && p0 + r < pend ? *reinterpret_cast<const float4*>(a.dy + (int64_t)p0 * M + e)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int s0 = p0 + (ky - 1) * a.W - 1;
 #pragma unroll
-  for (int t = 0; t < MT; ++t) cs[t] = 0.f;
-  // 4 pixel pairs per step: their loads issued together, then 4 MFMAs per tile
-  for (int q = p0; q < p1; q += 8) {   // wave-uniform trip count
-    float av[4][MT], bv[4];
+    for (int j = 0; j < RB; ++j) {
+      const int i = tid + 256 * j, e = 4 * i, r = e / C, ci = e - r * C;
+      const int sp = s0 + r;
+      rb[j] = i < NB4 && sp >= 0 && sp < npix ? *reinterpret_cast<const float4*>(a.x + (int64_t)sp * C + ci)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto put = [&]() {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = q + 2 * u + h;
-      const bool ok = p < p1;
-      const int y = p / a.W, x = p - y * a.W;
-      const int ys = y + dy, xs = x + dx;
-      const bool in = ok && ys >= 0 && ys < a.H && xs >= 0 && xs < a.W;
-#pragma unroll
-      for (int t = 0; t < MT; ++t) av[u][t] = ok ? a.dy[(int64_t)p * a.M + 32 * t + c] : 0.f;
-      bv[u] = in ? a.x[((int64_t)ys * a.W + xs) * a.Cin + ci] : 0.f;
+    for (int j = 0; j < RA; ++j) {
+      const int i = tid + 256 * j, e = 4 * i, r = e / M, m = e - r * M;
+      if (i < NA4) *reinterpret_cast<float4*>(as + r * PA + m) = ra[j];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int j = 0; j < RB; ++j) {
+      const int i = tid + 256 * j, e = 4 * i, r = e / C, ci = e - r * C;
+      if (i < NB4) *reinterpret_cast<float4*>(bs + r * PB + ci) = rb[j];
+    }
+  };
+  f32x16r acc[JW][MT];
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][t], bv[u], acc[t], 0, 0, 0);
-        cs[t] += av[u][t];
+  for (int u = 0; u < JW; ++u)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[u][t] = (f32x16r){0.f};
+  float cs = 0.f;
+  load(pbeg);
+  put();
+  __syncthreads();
+  for (int p0 = pbeg; p0 < pend; p0 += 32) {
+    const bool more = p0 + 32 < pend;
+    if (more) load(p0 + 32);   // in flight during the MFMAs
+    if (ky == 0 && tid < M) {
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) cs += as[r * PA + tid];
+    }
+#pragma unroll 4
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int kp = 2 * s2 + h;
+      const int x = (p0 + kp) % a.W;
+      float av[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) av[t] = as[kp * PA + 32 * t + c];
+#pragma unroll
+      for (int u = 0; u < JW; ++u) {
+        const int j = wid + 4 * u;
+        if (j < NJ) {
+          const int kx = j / NC, nc = j - kx * NC;
+          const int xs = x + kx - 1;
+          const float b = xs >= 0 && xs < a.W ? bs[(kp + kx) * PB + 32 * nc + c] : 0.f;
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], b, acc[u][t], 0, 0, 0);
+        }
       }
+    }
+    __syncthreads();
+    if (more) {
+      put();
+      __syncthreads();
+    }
   }
-  const int N = 9 * a.Cin;
-  float* out = a.part + (int64_t)split * ((int64_t)a.M * N + a.M);
+  const int N = 9 * C;
+  float* out = a.part + (int64_t)split * ((int64_t)M * N + M);
   // C/D layout: row = (r&3) + 8(r>>2) + 4h, col = c
 #pragma unroll
-  for (int t = 0; t < MT; ++t)
+  for (int u = 0; u < JW; ++u) {
+    const int j = wid + 4 * u;
+    if (j >= NJ) continue;
+    const int kx = j / NC, nc = j - kx * NC;
+    const int col = (3 * ky + kx) * C + 32 * nc + c;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + tap * a.Cin + ci] = acc[t][r];
-  if (colsum) {
+    for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const float s = cs[t] + __shfl_xor(cs[t], 32);
-      if (h == 0) out[(int64_t)a.M * N + 32 * t + c] = s;
-    }
+      for (int r = 0; r < 16; ++r) out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + col] = acc[u][t][r];
   }
+  if (ky == 0 && tid < M) out[(int64_t)M * N + tid] = cs;
 }
 
 // out[i] = sum_s part[s][i], s ascending (fixed order).
@@ -270,15 +328,16 @@ __global__ void k_sum_splits(const float* __restrict__ part, int64_t n, int nspl
 }
 
 static void wgrad_plan(int64_t npix, int M, int Cin, int* nsplit, int64_t* chunk) {
-  const int waves_per_split = 9 * (Cin / 32);
-  int64_t s = cdiv((int64_t)2048, (int64_t)waves_per_split);   // ~8 waves per CU
-  const int64_t maxs = npix / 256 > 0 ? npix / 256 : 1;         // >= 256 pixels per split
+  // ~2 workgroups per CU over the 3 kernel rows, >= 8 chunks of 32 pixels per split
+  int64_t s = cdiv((int64_t)512, (int64_t)3);
+  const int64_t maxs = cdiv(npix > 0 ? npix : 1, (int64_t)256);
   if (s > maxs) s = maxs;
   int64_t ch = cdiv(npix > 0 ? npix : 1, s);
-  ch = cdiv(ch, 2) * 2;
+  ch = cdiv(ch, 32) * 32;
   *chunk = ch;
   *nsplit = (int)(npix > 0 ? cdiv(npix, ch) : 1);
   (void)M;
+  (void)Cin;
 }
 
 static size_t wgrad_scratch(int64_t npix, int M, int Cin) {
@@ -288,7 +347,7 @@ static size_t wgrad_scratch(int64_t npix, int M, int Cin) {
   return (size_t)ns * ((size_t)M * 9 * Cin + M) * sizeof(float);
 }
 
-template <int MT>
+template <int MT, int NC>
 static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin, float* part, float* dw,
                         hipStream_t st) {
   WgradArgs g;
@@ -301,7 +360,7 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
   int ns;
   wgrad_plan((int64_t)H * W, g.M, Cin, &ns, &g.chunk);
   g.part = part;
-  hipLaunchKernelGGL(k_conv_wgrad<MT>, dim3(ns, 9, Cin / 32), dim3(64), 0, st, g);
+  hipLaunchKernelGGL((k_conv_wgrad<MT, NC>), dim3(ns, 3), dim3(256), 0, st, g);
   PNR_LAUNCH_CHECK();
   const int64_t n = (int64_t)g.M * 9 * Cin + g.M;
   hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, part, n, ns, dw);
@@ -427,8 +486,8 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.ldo = 64;
   a.out = cat1;
   a.act = net1;
-  if ((rc = launch_conv<1>(a, st))) return rc;
-  if ((rc = launch_wgrad<1>(cat2, net1, H, W, 32, part, dw2, st))) return rc;
+  if ((rc = launch_conv<1, 2>(a, st))) return rc;
+  if ((rc = launch_wgrad<1, 1>(cat2, net1, H, W, 32, part, dw2, st))) return rc;
   // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
   a.in = cat1;
   a.Cin = 64;
@@ -437,8 +496,8 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.ldo = 96;
   a.out = cat0;
   a.act = net0;
-  if ((rc = launch_conv<2>(a, st))) return rc;
-  if ((rc = launch_wgrad<2>(cat1, net0, H, W, 64, part, dw1, st))) return rc;
+  if ((rc = launch_conv<2, 2>(a, st))) return rc;
+  if ((rc = launch_wgrad<2, 2>(cat1, net0, H, W, 64, part, dw1, st))) return rc;
   // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
   a.in = cat0;
   a.Cin = 96;
@@ -447,6 +506,6 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.ldo = 128;
   a.out = d_x;
   a.act = nullptr;
-  if ((rc = launch_conv<4>(a, st))) return rc;
-  return launch_wgrad<3>(cat0, x, H, W, 128, part, dw0, st);
+  if ((rc = launch_conv<4, 1>(a, st))) return rc;
+  return launch_wgrad<3, 4>(cat0, x, H, W, 128, part, dw0, st);
 }
