@@ -28,7 +28,12 @@ constexpr int kRPx = 128;              // pixels per workgroup (4 waves x 32)
 constexpr int kRCh = 32;               // input channels staged per LDS chunk
 constexpr int kRPitch = kRCh + 1;      // floats per staged pixel
 constexpr int kRRowPx = kRPx + 2;      // staged pixels per input row (halo 1)
-constexpr size_t kRLds = (size_t)3 * kRRowPx * kRPitch * sizeof(float);
+// Output rows per workgroup tile.  2 (every weight fragment feeding two rows'
+// MFMAs, 4 staged input rows) measured 3.01 vs 2.93 ms for the 800x800 forward,
+// 4 rows 3.56 ms: weight fetch is not what bounds the kernel; 1 is kept.
+constexpr int kROut = 1;
+constexpr int kRRows = kROut + 2;      // staged input rows
+constexpr size_t kRLds = (size_t)kRRows * kRRowPx * kRPitch * sizeof(float);
 
 struct ConvArgs {
   const float* in;     // [H, W, Cin]
@@ -52,20 +57,22 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int segs = (a.W + kRPx - 1) / kRPx;
-  const int64_t ntiles = (int64_t)a.H * segs;
+  const int64_t ntiles = (int64_t)((a.H + kROut - 1) / kROut) * segs;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int y = (int)(tile / segs);
+    const int y0 = (int)(tile / segs) * kROut;
     const int x0 = (int)(tile % segs) * kRPx;
-    f32x16r acc[NT];
+    f32x16r acc[kROut][NT];
 #pragma unroll
-    for (int T = 0; T < NT; ++T) acc[T] = (f32x16r){0.f};
+    for (int o = 0; o < kROut; ++o)
+#pragma unroll
+      for (int T = 0; T < NT; ++T) acc[o][T] = (f32x16r){0.f};
     for (int ci0 = 0; ci0 < a.Cin; ci0 += kRCh) {
-      // stage rows y-1..y+1, pixels x0-1 .. x0+128, channels ci0 .. ci0+31 (zero padded)
-      for (int i = threadIdx.x; i < 3 * kRRowPx * (kRCh / 4); i += blockDim.x) {
+      // stage rows y0-1 .. y0+kROut, pixels x0-1 .. x0+128, channels ci0 .. ci0+31 (zero padded)
+      for (int i = threadIdx.x; i < kRRows * kRRowPx * (kRCh / 4); i += blockDim.x) {
         const int q = i % (kRCh / 4);
         const int px = (i / (kRCh / 4)) % kRRowPx;
         const int r = i / ((kRCh / 4) * kRRowPx);
-        const int yy = y - 1 + r, xx = x0 - 1 + px;
+        const int yy = y0 - 1 + r, xx = x0 - 1 + px;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
           v = *reinterpret_cast<const float4*>(a.in + ((int64_t)yy * a.W + xx) * a.Cin + ci0 + 4 * q);
@@ -76,7 +83,8 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
         d[3] = v.w;
       }
       __syncthreads();
-      // this wave's 32 pixels: x0 + 32 wid + c
+      // this wave's 32 pixels: x0 + 32 wid + c, of both output rows: every weight
+      // fragment feeds kROut * NT MFMAs
       const int pcol = 32 * wid + c;
       // k-steps of this chunk in (tap, channel-pair) order; weight fragments
       // are software-pipelined kRW steps ahead across tap boundaries
@@ -100,9 +108,13 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
           if (i < kSteps) {
             const int tap = i / (kRCh / 2), s = i % (kRCh / 2);
             const int dy = tap / 3, dx = tap % 3;
-            const float b = lds_r[(dy * kRRowPx + pcol + dx) * kRPitch + h + 2 * s];
 #pragma unroll
-            for (int T = 0; T < NT; ++T) acc[T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[T], 0, 0, 0);
+            for (int o = 0; o < kROut; ++o) {
+              const float b = lds_r[((dy + o) * kRRowPx + pcol + dx) * kRPitch + h + 2 * s];
+#pragma unroll
+              for (int T = 0; T < NT; ++T)
+                acc[o][T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[o][T], 0, 0, 0);
+            }
             if (i + kRW < kSteps) {
 #pragma unroll
               for (int T = 0; T < NT; ++T) wr[d][T] = wp[(wstep(i + kRW) * NT + T) * 64];
@@ -114,37 +126,40 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
     }
     // epilogue: rows 0..cout-1 trunk (lrelu), rows cout..cout+2 rgb
     const int xo = x0 + 32 * wid + c;
-    if (BWD) {
-      if (xo >= a.W) continue;
+#pragma unroll
+    for (int o = 0; o < kROut; ++o) {
+      const int y = y0 + o;
+      if (xo >= a.W || y >= a.H) continue;
       const int64_t pix = (int64_t)y * a.W + xo;
+      if (BWD) {
 #pragma unroll
-      for (int T = 0; T < NT; ++T)
+        for (int T = 0; T < NT; ++T)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (co < a.cout) {
-            // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
-            const float m = BWD == 1 || a.act[pix * a.cout + co] > 0.f ? 1.f : a.slope;
-            a.out[pix * a.ldo + co] = acc[T][r] * m;
+          for (int r = 0; r < 16; ++r) {
+            const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (co < a.cout) {
+              // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
+              const float m = BWD == 1 || a.act[pix * a.cout + co] > 0.f ? 1.f : a.slope;
+              a.out[pix * a.ldo + co] = acc[o][T][r] * m;
+            }
           }
-        }
-    } else if (xo < a.W) {
-      const int64_t pix = (int64_t)y * a.W + xo;
+      } else {
 #pragma unroll
-      for (int T = 0; T < NT; ++T)
+        for (int T = 0; T < NT; ++T)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float v = acc[T][r] + a.bias[co];
-          if (co < a.cout) {
-            a.out[pix * a.ldo + co] = v > 0.f ? v : v * a.slope;
-          } else if (co < a.cout + 3) {
-            float* o = a.rgb + pix * 3 + (co - a.cout);
-            if (a.rgb_mode == 0) *o = v;
-            else if (a.rgb_mode == 1) *o += v;
-            else *o = 1.f / (1.f + expf(-(*o + v)));
+          for (int r = 0; r < 16; ++r) {
+            const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float v = acc[o][T][r] + a.bias[co];
+            if (co < a.cout) {
+              a.out[pix * a.ldo + co] = v > 0.f ? v : v * a.slope;
+            } else if (co < a.cout + 3) {
+              float* op = a.rgb + pix * 3 + (co - a.cout);
+              if (a.rgb_mode == 0) *op = v;
+              else if (a.rgb_mode == 1) *op += v;
+              else *op = 1.f / (1.f + expf(-(*op + v)));
+            }
           }
-        }
+      }
     }
   }
 }
@@ -157,7 +172,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRLds));
     attr = true;
   }
-  const int64_t tiles = (int64_t)a.H * ((a.W + kRPx - 1) / kRPx);
+  const int64_t tiles = (int64_t)((a.H + kROut - 1) / kROut) * ((a.W + kRPx - 1) / kRPx);
   hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
