@@ -32,6 +32,9 @@ constexpr int kRRowPx = kRPx + 2;      // staged pixels per input row (halo 1)
 // MFMAs, 4 staged input rows) measured 3.01 vs 2.93 ms for the 800x800 forward,
 // 4 rows 3.56 ms: weight fetch is not what bounds the kernel; 1 is kept.
 constexpr int kROut = 1;
+#ifndef PNR_CONV_ABL
+#define PNR_CONV_ABL 0   // timing ablations only (tools/build_variant.sh)
+#endif
 constexpr int kRRows = kROut + 2;      // staged input rows
 constexpr size_t kRLds = (size_t)kRRows * kRRowPx * kRPitch * sizeof(float);
 
@@ -68,7 +71,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       for (int T = 0; T < NT; ++T) acc[o][T] = (f32x16r){0.f};
     for (int ci0 = 0; ci0 < a.Cin; ci0 += kRCh) {
       // stage rows y0-1 .. y0+kROut, pixels x0-1 .. x0+128, channels ci0 .. ci0+31 (zero padded)
-      for (int i = threadIdx.x; i < kRRows * kRRowPx * (kRCh / 4); i += blockDim.x) {
+      for (int i = threadIdx.x; (PNR_CONV_ABL & 4) == 0 && i < kRRows * kRRowPx * (kRCh / 4); i += blockDim.x) {
         const int q = i % (kRCh / 4);
         const int px = (i / (kRCh / 4)) % kRRowPx;
         const int r = i / ((kRCh / 4) * kRRowPx);
@@ -92,6 +95,8 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       constexpr int kSteps = 9 * (kRCh / 2);
       const float* wp = a.wf + lane;
       auto wstep = [&](int i) {   // global k-step of chunk step i
+#if PNR_CONV_ABL & 1
+        return i & 1;               // ablation: weight fragments from L1
         const int tap = i / (kRCh / 2), s = i % (kRCh / 2);
         return (tap * a.Cin + ci0) / 2 + s;
       };
@@ -110,7 +115,11 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
             const int dy = tap / 3, dx = tap % 3;
 #pragma unroll
             for (int o = 0; o < kROut; ++o) {
+#if PNR_CONV_ABL & 2
+              const float b = lds_r[pcol * kRPitch + h + (s & 1)];   // ablation: fixed B rows
+#else
               const float b = lds_r[((dy + o) * kRRowPx + pcol + dx) * kRPitch + h + 2 * s];
+#endif
 #pragma unroll
               for (int T = 0; T < NT; ++T)
                 acc[o][T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[o][T], 0, 0, 0);
@@ -122,6 +131,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
           }
         }
       }
+#endif
       __syncthreads();
     }
     // epilogue: rows 0..cout-1 trunk (lrelu), rows cout..cout+2 rgb
@@ -166,14 +176,17 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
 
 template <int NT, int BWD = 0>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
+  // (weight fragments staged in LDS per 8 k-steps, double-buffered, for the 4
+  // waves measured 3.19 vs 2.93 ms forward: the extra barriers cost more)
+  const size_t lds = kRLds;
   static bool attr = false;
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3<NT, BWD>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRLds));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   const int64_t tiles = (int64_t)((a.H + kROut - 1) / kROut) * ((a.W + kRPx - 1) / kRPx);
-  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
+  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), lds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
