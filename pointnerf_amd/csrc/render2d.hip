@@ -32,8 +32,13 @@ constexpr int kRRowPx = kRPx + 2;      // staged pixels per input row (halo 1)
 // MFMAs, 4 staged input rows) measured 3.01 vs 2.93 ms for the 800x800 forward,
 // 4 rows 3.56 ms: weight fetch is not what bounds the kernel; 1 is kept.
 constexpr int kROut = 1;
+// Timing ablations (tools/build_variant.sh, 800x800 forward 2.95 ms): 1 = weight
+// fragments from L1 (2.01 ms), 2 = fixed B rows (2.53), 4 = no input staging
+// (2.53), 7 = all three (1.71).  Staging the weight fragments in LDS per 8
+// k-steps for the 4 waves (double-buffered) measured 3.19 ms: the extra barriers
+// cost more than the L2 fetch they save; not kept.
 #ifndef PNR_CONV_ABL
-#define PNR_CONV_ABL 0   // timing ablations only (tools/build_variant.sh)
+#define PNR_CONV_ABL 0
 #endif
 constexpr int kRRows = kROut + 2;      // staged input rows
 constexpr size_t kRLds = (size_t)kRRows * kRRowPx * kRPitch * sizeof(float);
@@ -97,6 +102,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       auto wstep = [&](int i) {   // global k-step of chunk step i
 #if PNR_CONV_ABL & 1
         return i & 1;               // ablation: weight fragments from L1
+#endif
         const int tap = i / (kRCh / 2), s = i % (kRCh / 2);
         return (tap * a.Cin + ci0) / 2 + s;
       };
@@ -131,7 +137,6 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
           }
         }
       }
-#endif
       __syncthreads();
     }
     // epilogue: rows 0..cout-1 trunk (lrelu), rows cout..cout+2 rgb
@@ -176,17 +181,14 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
 
 template <int NT, int BWD = 0>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
-  // (weight fragments staged in LDS per 8 k-steps, double-buffered, for the 4
-  // waves measured 3.19 vs 2.93 ms forward: the extra barriers cost more)
-  const size_t lds = kRLds;
   static bool attr = false;
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3<NT, BWD>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRLds));
     attr = true;
   }
   const int64_t tiles = (int64_t)((a.H + kROut - 1) / kROut) * ((a.W + kRPx - 1) / kRPx);
-  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
