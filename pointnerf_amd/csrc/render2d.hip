@@ -37,6 +37,9 @@ constexpr int kROut = 1;
 // (2.53), 7 = all three (1.71).  Staging the weight fragments in LDS per 8
 // k-steps for the 4 waves (double-buffered) measured 3.19 ms: the extra barriers
 // cost more than the L2 fetch they save; not kept.
+#ifndef PNR_CONV_RW
+#define PNR_CONV_RW 6   // weight-fragment prefetch depth in k-steps (12 / 18: same 2.94 ms)
+#endif
 #ifndef PNR_CONV_ABL
 #define PNR_CONV_ABL 0
 #endif
@@ -96,7 +99,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       const int pcol = 32 * wid + c;
       // k-steps of this chunk in (tap, channel-pair) order; weight fragments
       // are software-pipelined kRW steps ahead across tap boundaries
-      constexpr int kRW = 6;
+      constexpr int kRW = PNR_CONV_RW;
       constexpr int kSteps = 9 * (kRCh / 2);
       const float* wp = a.wf + lane;
       auto wstep = [&](int i) {   // global k-step of chunk step i
