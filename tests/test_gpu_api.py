@@ -206,3 +206,37 @@ def test_module_forward_trains(cuda):
     assert not out2["coarse_raycolor"].requires_grad
     np.testing.assert_allclose(out2["coarse_raycolor"].cpu().numpy(), out["coarse_raycolor"].detach().cpu().numpy(),
                                atol=1e-5, rtol=1e-5)
+
+
+def test_module_neural_render_cnn_trains(cuda):
+    """opt.neural_render = "cnn" (neural_points_volumetric_model.py:258-260,
+    343-344) in the training loop: final_coarse_raycolor is differentiable through
+    NeuralRenderFn (pnr_neural_render_bwd) down to the point embeddings, the
+    aggregator and the 2-D renderer's own parameters; the gradient reaching the
+    composited feature image equals torch autograd of the fp64 restatement."""
+    H = W = 24
+    sc = scene(8000, H=H, W=W, theta=10.0, default_conf=None, neural_render="cnn")
+    m = _model(sc, cuda, formula_params(salt=0.7), train=True)
+    m.train()
+    out = m(**_inputs(sc, cuda), h=H, w=W)
+    final = out["final_coarse_raycolor"]
+    assert final.shape == (1, H * W, 3) and final.requires_grad
+    g = torch.randn(final.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+    (final * g).sum().backward()
+    nr = m.neural_render_2d
+    for n, p in nr.named_parameters():
+        assert p.grad is not None and float(p.grad.abs().sum()) > 0, n
+    assert float(m.neural_points.points_embeding.grad.abs().sum()) > 0
+    assert float(m.aggregator.block1[0].weight.grad.abs().sum()) > 0
+    # the 2-D renderer's input gradient vs torch autograd in fp64
+    coarse = out["coarse_raycolor"].detach().reshape(1, H, W, -1)
+    x1 = coarse.clone().requires_grad_(True)
+    (nr(x1) * g.reshape(1, H, W, 3)).sum().backward()
+    from pointnerf_amd.neural_render import NeuralRenderer
+    nr64 = NeuralRenderer(input_dim=128)
+    nr64.load_state_dict({k: v.detach().cpu() for k, v in nr.state_dict().items()})
+    nr64 = nr64.double().to(cuda)
+    x2 = coarse.double().requires_grad_(True)
+    (nr64.forward_torch(x2) * g.double().reshape(1, H, W, 3)).sum().backward()
+    err = float((x1.grad.double() - x2.grad).abs().max())
+    assert err <= 2e-5 * max(float(x2.grad.abs().max()), 1e-3), err
