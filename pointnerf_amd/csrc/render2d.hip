@@ -59,6 +59,7 @@ struct ConvArgs {
   float slope;
   int ldo;             // floats per output pixel row (>= cout)
   const float* act;    // [H, W, cout] forward activation whose LeakyReLU mask applies (mode 3)
+  int cin_real;        // input channels >= cin_real are zero padding: their k-steps are skipped
 };
 
 // BWD: 0 forward, 1 data gradient, 2 data gradient times the LeakyReLU mask of a.act
@@ -119,21 +120,26 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
 #pragma unroll
         for (int d = 0; d < kRW; ++d) {
           const int i = i0 + d;
+          // (channel pairs wholly in the zero padding of the backward's cat images
+          // -- the 3 rgb-gradient channels padded to 32 -- add nothing: their
+          // MFMAs are skipped)
           if (i < kSteps) {
             const int tap = i / (kRCh / 2), s = i % (kRCh / 2);
             const int dy = tap / 3, dx = tap % 3;
+            if (BWD == 0 || ci0 + 2 * s < a.cin_real) {
 #pragma unroll
-            for (int o = 0; o < kROut; ++o) {
+              for (int o = 0; o < kROut; ++o) {
 #if PNR_CONV_ABL & 2
-              const float b = lds_r[pcol * kRPitch + h + (s & 1)];   // ablation: fixed B rows
+                const float b = lds_r[pcol * kRPitch + h + (s & 1)];   // ablation: fixed B rows
 #else
-              const float b = lds_r[((dy + o) * kRRowPx + pcol + dx) * kRPitch + h + 2 * s];
+                const float b = lds_r[((dy + o) * kRRowPx + pcol + dx) * kRPitch + h + 2 * s];
 #endif
 #pragma unroll
-              for (int T = 0; T < NT; ++T)
-                acc[o][T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[o][T], 0, 0, 0);
+                for (int T = 0; T < NT; ++T)
+                  acc[o][T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[o][T], 0, 0, 0);
+              }
             }
-            if (i + kRW < kSteps) {
+            if (i + kRW < kSteps) {   // the ring refill runs for skipped steps too
 #pragma unroll
               for (int T = 0; T < NT; ++T) wr[d][T] = wp[(wstep(i + kRW) * NT + T) * 64];
             }
@@ -429,6 +435,7 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.W = W;
   a.slope = w->neg_slope;
   a.act = nullptr;
+  a.cin_real = 1 << 30;
   // stage 0: x (128) -> net0 (64) + rgb = conv_rgb0(x)
   a.in = x;
   a.Cin = 128;
@@ -514,6 +521,7 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   // stage 2: d net1 = conv(cat2 = [g, 0], flipped conv_rgb.2), masked by net1 -> cat1[:, :32]
   a.in = cat2;
   a.Cin = 32;
+  a.cin_real = 3;         // [g, 0 x 29]
   a.wf = wt->wt2;
   a.cout = 32;
   a.ldo = 64;
@@ -524,6 +532,7 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
   a.in = cat1;
   a.Cin = 64;
+  a.cin_real = 32 + 3;    // [dz1, g, 0 x 29]
   a.wf = wt->wt1;
   a.cout = 64;
   a.ldo = 96;
@@ -534,6 +543,7 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
   a.in = cat0;
   a.Cin = 96;
+  a.cin_real = 64 + 3;    // [dz0, g, 0 x 29]
   a.wf = wt->wt0;
   a.cout = 128;
   a.ldo = 128;
