@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 10
+#define PNR_ABI_VERSION 11
 
 enum {
   PNR_OK = 0,
@@ -538,15 +538,18 @@ int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const flo
  * on the composited feature image x[H,W,128] (row-major pixels = ray order):
  * out_rgb[H,W,3] = sigmoid(conv_rgb0(x) + conv_rgb1(net0) + conv_rgb2(net1)),
  * net0 = lrelu_0.2(conv_layers.0(x)), net1 = lrelu_0.2(conv_layers.1(net0)),
- * all 3x3 / stride 1 / pad 1.  Weights per stage s: the trunk conv's and the
- * rgb conv's [cout, cin, 3, 3] weights stacked as rows (trunk first, then the 3
- * rgb rows, zero rows to a multiple of 32), columns k = (ky*3 + kx) * cin + ci,
- * fragment-packed like pnr_mlp (frag_pack, no bias column); b_s = the stacked biases. */
+ * all 3x3 / stride 1 / pad 1.  Per stage s the trunk conv's [cout, cin, 3, 3]
+ * weights as rows, columns k = (ky*3 + kx) * cin + ci, fragment-packed like
+ * pnr_mlp (frag_pack, no bias column), b_s its bias; the rgb conv's weights
+ * row-major [3, 9 * cin] (same k order, not packed: they run on VALU beside the
+ * trunk's MFMAs) and its 3 biases. */
 typedef struct {
-  const float* wf0; const float* b0;   /* conv_layers.0 (128->64) + conv_rgb.0 (128->3): 96 rows */
-  const float* wf1; const float* b1;   /* conv_layers.1 (64->32)  + conv_rgb.1 (64->3):  64 rows */
-  const float* wf2; const float* b2;   /* conv_rgb.2 (32->3):                            32 rows */
-  float neg_slope;                     /* 0.2 */
+  const float* wf0; const float* b0;       /* conv_layers.0 (128->64): 64 rows */
+  const float* wf1; const float* b1;       /* conv_layers.1 (64->32):  32 rows */
+  const float* wrgb0; const float* brgb0;  /* conv_rgb.0 (128->3) */
+  const float* wrgb1; const float* brgb1;  /* conv_rgb.1 (64->3) */
+  const float* wrgb2; const float* brgb2;  /* conv_rgb.2 (32->3) */
+  float neg_slope;                         /* 0.2 */
 } pnr_neural_render_w;
 
 int pnr_neural_render_scratch_bytes(int32_t H, int32_t W, size_t* out);
@@ -557,7 +560,7 @@ int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const pnr_neural
  * that the reference's finetune step takes through torch convolutions).
  * fwd_scratch = the forward's scratch after that call (net0[H,W,64] then
  * net1[H,W,32]); out_rgb its output; d_out = dL/d out_rgb.  Per stage the
- * data-gradient weights are the stacked rows of pnr_neural_render_w flipped
+ * data-gradient weights are the stage's stacked [trunk; rgb; zero] rows flipped
  * and transposed: rows = the stage's input channels ci (128 / 64 / 32),
  * columns k = (ky'*3 + kx')*M + j with value Wstack[j][ci][2-ky'][2-kx'],
  * j < M = 96 / 64 / 32 stacked rows (trunk, rgb, zero), frag_pack-ed.

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class PnrError(RuntimeError):
@@ -65,8 +65,8 @@ class Mlp(ctypes.Structure):
 
 
 class NeuralRenderW(ctypes.Structure):
-    _fields_ = [("wf0", c_void_p), ("b0", c_void_p), ("wf1", c_void_p), ("b1", c_void_p), ("wf2", c_void_p),
-                ("b2", c_void_p), ("neg_slope", c_float)]
+    _fields_ = [(n, c_void_p) for n in ("wf0", "b0", "wf1", "b1", "wrgb0", "brgb0", "wrgb1", "brgb1", "wrgb2",
+                                        "brgb2")] + [("neg_slope", c_float)]
 
 
 class NeuralRenderWT(ctypes.Structure):

@@ -12,8 +12,10 @@
 //
 // CDNA4 mapping: each stage is one launch of k_conv3x3, an implicit GEMM on
 // v_mfma_f32_32x32x2_f32 (exact fp32): rows = output channels of the stage's
-// trunk conv AND its rgb skip conv stacked (64+3 -> 96, 32+3 -> 64, 0+3 -> 32),
-// columns = 32 consecutive pixels of an image row, k = (tap, input channel).
+// trunk conv (64, 32, none), columns = 32 consecutive pixels of an image row,
+// k = (tap, input channel); the 3-channel rgb skip conv runs on VALU in the
+// MFMAs' shadow (each lane already holds the B operand value it needs: 3 FMAs
+// per k-step) instead of as a 32-row MFMA tile with 29 zero rows.
 // A 4-wave workgroup owns 128 pixels of one row; the 3 input rows x 130
 // pixels of a 32-channel slice are staged in LDS (pixel pitch 33 floats,
 // conflict-free B reads), so each input element is read from HBM ~3 times
@@ -60,6 +62,8 @@ struct ConvArgs {
   int ldo;             // floats per output pixel row (>= cout)
   const float* act;    // [H, W, cout] forward activation whose LeakyReLU mask applies (mode 3)
   int cin_real;        // input channels >= cin_real are zero padding: their k-steps are skipped
+  const float* wrgb;   // forward: the stage's rgb conv [3, 9 * Cin] (k = tap * Cin + ci), on VALU
+  const float* brgb;   // [3]
 };
 
 // BWD: 0 forward, 1 data gradient, 2 data gradient times the LeakyReLU mask of a.act
@@ -70,10 +74,12 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   const int c = lane & 31, h = lane >> 5;
   const int segs = (a.W + kRPx - 1) / kRPx;
   const int64_t ntiles = (int64_t)((a.H + kROut - 1) / kROut) * segs;
+  constexpr int NTA = NT > 0 ? NT : 1;   // (NT = 0: the rgb-only last forward stage)
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int y0 = (int)(tile / segs) * kROut;
     const int x0 = (int)(tile % segs) * kRPx;
-    f32x16r acc[kROut][NT];
+    f32x16r acc[kROut][NTA];
+    float racc[3] = {0.f, 0.f, 0.f};   // forward: this lane's half of the pixel's rgb sums
 #pragma unroll
     for (int o = 0; o < kROut; ++o)
 #pragma unroll
@@ -110,11 +116,12 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
         const int tap = i / (kRCh / 2), s = i % (kRCh / 2);
         return (tap * a.Cin + ci0) / 2 + s;
       };
-      float wr[kRW][NT];
+      float wr[kRW][NTA];
 #pragma unroll
       for (int d = 0; d < kRW; ++d)
 #pragma unroll
         for (int T = 0; T < NT; ++T) wr[d][T] = wp[(wstep(d) * NT + T) * 64];
+      (void)wr;
 #pragma unroll
       for (int i0 = 0; i0 < kSteps; i0 += kRW) {
 #pragma unroll
@@ -137,6 +144,17 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
 #pragma unroll
                 for (int T = 0; T < NT; ++T)
                   acc[o][T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[o][T], 0, 0, 0);
+                if (BWD == 0) {
+                  // the 3 rgb rows on VALU in the MFMAs' shadow: lane (c, h) holds
+                  // channel ci0 + 2 s + h of its pixel's tap; both weights are uniform
+                  // (scalar loads), the lane picks its own
+                  const float* wq = a.wrgb + tap * a.Cin + ci0 + 2 * s;
+#pragma unroll
+                  for (int j = 0; j < 3; ++j) {
+                    const float w0 = wq[j * 9 * a.Cin], w1 = wq[j * 9 * a.Cin + 1];
+                    racc[j] = fmaf(h ? w1 : w0, b, racc[j]);
+                  }
+                }
               }
             }
             if (i + kRW < kSteps) {   // the ring refill runs for skipped steps too
@@ -148,8 +166,11 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       }
       __syncthreads();
     }
-    // epilogue: rows 0..cout-1 trunk (lrelu), rows cout..cout+2 rgb
+    // epilogue: trunk rows 0..cout-1 (lrelu) from the MFMA tiles; forward: the
+    // rgb sums of the lane halves (even / odd channels) combined, + bias
     const int xo = x0 + 32 * wid + c;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) racc[j] += __shfl_xor(racc[j], 32);
 #pragma unroll
     for (int o = 0; o < kROut; ++o) {
       const int y = y0 + o;
@@ -174,15 +195,18 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
           for (int r = 0; r < 16; ++r) {
             const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
             const float v = acc[o][T][r] + a.bias[co];
-            if (co < a.cout) {
-              a.out[pix * a.ldo + co] = v > 0.f ? v : v * a.slope;
-            } else if (co < a.cout + 3) {
-              float* op = a.rgb + pix * 3 + (co - a.cout);
-              if (a.rgb_mode == 0) *op = v;
-              else if (a.rgb_mode == 1) *op += v;
-              else *op = 1.f / (1.f + expf(-(*op + v)));
-            }
+            a.out[pix * a.ldo + co] = v > 0.f ? v : v * a.slope;
           }
+        if (h == 0) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const float v = racc[j] + a.brgb[j];
+            float* op = a.rgb + pix * 3 + j;
+            if (a.rgb_mode == 0) *op = v;
+            else if (a.rgb_mode == 1) *op += v;
+            else *op = 1.f / (1.f + expf(-(*op + v)));
+          }
+        }
       }
     }
   }
@@ -420,7 +444,9 @@ extern "C" int pnr_neural_render_scratch_bytes(int32_t H, int32_t W, size_t* out
 extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const pnr_neural_render_w* w,
                                      float* out_rgb, void* scratch, size_t scratch_bytes, void* stream) {
   PNR_CHECK_ARG(x && w && out_rgb && scratch, "neural_render: null pointer");
-  PNR_CHECK_ARG(w->wf0 && w->b0 && w->wf1 && w->b1 && w->wf2 && w->b2, "neural_render: null weight");
+  PNR_CHECK_ARG(w->wf0 && w->b0 && w->wf1 && w->b1 && w->wrgb0 && w->brgb0 && w->wrgb1 && w->brgb1 && w->wrgb2 &&
+                    w->brgb2,
+                "neural_render: null weight");
   PNR_CHECK_ARG(H >= 0 && W >= 0, "neural_render: bad image size");
   PNR_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
                 "neural_render: x and scratch must be 16-B aligned");
@@ -436,7 +462,7 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.slope = w->neg_slope;
   a.act = nullptr;
   a.cin_real = 1 << 30;
-  // stage 0: x (128) -> net0 (64) + rgb = conv_rgb0(x)
+  // stage 0: x (128) -> net0 (64) on MFMA + rgb = conv_rgb0(x) on VALU
   a.in = x;
   a.Cin = 128;
   a.wf = w->wf0;
@@ -446,7 +472,9 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.out = net0;
   a.rgb = out_rgb;
   a.rgb_mode = 0;
-  if ((rc = launch_conv<3>(a, st))) return rc;
+  a.wrgb = w->wrgb0;
+  a.brgb = w->brgb0;
+  if ((rc = launch_conv<2>(a, st))) return rc;
   // stage 1: net0 (64) -> net1 (32), rgb += conv_rgb1(net0)
   a.in = net0;
   a.Cin = 64;
@@ -456,17 +484,21 @@ extern "C" int pnr_neural_render_fwd(const float* x, int32_t H, int32_t W, const
   a.ldo = 32;
   a.out = net1;
   a.rgb_mode = 1;
-  if ((rc = launch_conv<2>(a, st))) return rc;
-  // stage 2: out = sigmoid(rgb + conv_rgb2(net1))
+  a.wrgb = w->wrgb1;
+  a.brgb = w->brgb1;
+  if ((rc = launch_conv<1>(a, st))) return rc;
+  // stage 2: out = sigmoid(rgb + conv_rgb2(net1)), rgb only
   a.in = net1;
   a.Cin = 32;
-  a.wf = w->wf2;
-  a.bias = w->b2;
+  a.wf = nullptr;
+  a.bias = nullptr;
   a.cout = 0;
   a.ldo = 0;
   a.out = nullptr;
   a.rgb_mode = 2;
-  return launch_conv<1>(a, st);
+  a.wrgb = w->wrgb2;
+  a.brgb = w->brgb2;
+  return launch_conv<0>(a, st);
 }
 
 extern "C" int pnr_neural_render_bwd_scratch_bytes(int32_t H, int32_t W, size_t* out) {

@@ -41,20 +41,16 @@ class NeuralRenderer(nn.Module):
         self._packed_key = None
 
     @staticmethod
-    def _stack(trunk, rgb):
-        """[cout, cin, 3, 3] weights of trunk (or None) and rgb conv -> rows x
-        (tap-major k = (ky*3+kx)*cin + ci), zero rows to a multiple of 32."""
-        ws = ([trunk.weight] if trunk is not None else []) + [rgb.weight]
-        bs = ([trunk.bias] if trunk is not None else []) + [rgb.bias]
-        W = torch.cat(ws, 0).float()
-        b = torch.cat(bs, 0).float()
-        rows = (W.shape[0] + 31) // 32 * 32
-        cin = W.shape[1]
-        W2 = torch.zeros((rows, 9 * cin), dtype=torch.float32, device=W.device)
-        W2[: W.shape[0]] = W.permute(0, 2, 3, 1).reshape(W.shape[0], 9 * cin)
-        bias = torch.zeros(rows, dtype=torch.float32, device=W.device)
-        bias[: b.shape[0]] = b
-        return frag_pack(W2), bias
+    def _trunk(conv):
+        """[cout, cin, 3, 3] trunk weights -> fragment-packed rows (k = (ky*3 + kx)*cin + ci), bias."""
+        W = conv.weight.float()
+        return frag_pack(W.permute(0, 2, 3, 1).reshape(W.shape[0], -1).contiguous()), conv.bias.float().contiguous()
+
+    @staticmethod
+    def _rgb(conv):
+        """[3, cin, 3, 3] rgb weights -> row-major [3, 9 * cin] (same k order), bias [3]."""
+        W = conv.weight.float()
+        return W.permute(0, 2, 3, 1).reshape(3, -1).contiguous(), conv.bias.float().contiguous()
 
     def packed(self):
         ps = list(self.parameters())
@@ -62,11 +58,12 @@ class NeuralRenderer(nn.Module):
         if self._packed is not None and key == self._packed_key:
             return self._packed
         with torch.no_grad():
-            wf0, b0 = self._stack(self.conv_layers[0], self.conv_rgb[0])
-            wf1, b1 = self._stack(self.conv_layers[1], self.conv_rgb[1])
-            wf2, b2 = self._stack(None, self.conv_rgb[2])
-        t = dict(wf0=wf0, b0=b0, wf1=wf1, b1=b1, wf2=wf2, b2=b2)
-        w = L.NeuralRenderW(*(t[k].data_ptr() for k in ("wf0", "b0", "wf1", "b1", "wf2", "b2")), 0.2)
+            wf0, b0 = self._trunk(self.conv_layers[0])
+            wf1, b1 = self._trunk(self.conv_layers[1])
+            r = [self._rgb(cv) for cv in self.conv_rgb]
+        t = dict(wf0=wf0, b0=b0, wf1=wf1, b1=b1, wrgb0=r[0][0], brgb0=r[0][1], wrgb1=r[1][0], brgb1=r[1][1],
+                 wrgb2=r[2][0], brgb2=r[2][1])
+        w = L.NeuralRenderW(*(t[k].data_ptr() for k, _ in L.NeuralRenderW._fields_[:-1]), 0.2)
         self._packed, self._packed_key = (w, t), key
         return self._packed
 
