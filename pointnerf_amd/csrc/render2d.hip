@@ -279,7 +279,7 @@ struct WgradArgs {
 // every X element 3 times (not 9 x Cin/32 and 9 x M/32 as one wave per tap and
 // tile would).  Wave w: column tiles j = w, w + 4, w + 8 of the 3 Cin/32
 // (tap, channel-tile) pairs, all M/32 row tiles.
-template <int MT, int NC>
+template <int MT, int NC, bool VR>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
   constexpr int M = 32 * MT, C = 32 * NC;
   constexpr int PA = M % 64 == 0 ? M + 32 : M;      // LDS pitches: half-waves 32 banks apart
@@ -323,11 +323,22 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
       if (i < NB4) *reinterpret_cast<float4*>(bs + r * PB + ci) = rb[j];
     }
   };
-  f32x16r acc[JW][MT];
+  // VR: row tiles 0 .. MT-2 (the trunk's dz rows) on MFMA; the last tile holds
+  // the 3 rgb-gradient rows (+ 29 zero rows): those 3 rows run on VALU, each lane
+  // multiplying its B value by the 3 g values of its pixel (LDS broadcasts).
+  // (stage 1, MT = 2: measured 0.85 -> 1.0 ms with VR, so there all rows stay on MFMA)
+  constexpr int MTM = VR ? MT - 1 : MT, MTA = MTM > 0 ? MTM : 1, NR = VR ? 3 : 0;
+  f32x16r acc[JW][MTA];
 #pragma unroll
   for (int u = 0; u < JW; ++u)
 #pragma unroll
-    for (int t = 0; t < MT; ++t) acc[u][t] = (f32x16r){0.f};
+    for (int t = 0; t < MTM; ++t) acc[u][t] = (f32x16r){0.f};
+  float racc[JW][3];
+#pragma unroll
+  for (int u = 0; u < JW; ++u)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) racc[u][j] = 0.f;
+  (void)racc;
   float cs = 0.f;
   load(pbeg);
   put();
@@ -343,9 +354,11 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
     for (int s2 = 0; s2 < 16; ++s2) {
       const int kp = 2 * s2 + h;
       const int x = (p0 + kp) % a.W;
-      float av[MT];
+      float av[MTA], gv[3];
 #pragma unroll
-      for (int t = 0; t < MT; ++t) av[t] = as[kp * PA + 32 * t + c];
+      for (int t = 0; t < MTM; ++t) av[t] = as[kp * PA + 32 * t + c];
+#pragma unroll
+      for (int jj = 0; jj < NR; ++jj) gv[jj] = as[kp * PA + 32 * MTM + jj];
 #pragma unroll
       for (int u = 0; u < JW; ++u) {
         const int j = wid + 4 * u;
@@ -354,7 +367,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
           const int xs = x + kx - 1;
           const float b = xs >= 0 && xs < a.W ? bs[(kp + kx) * PB + 32 * nc + c] : 0.f;
 #pragma unroll
-          for (int t = 0; t < MT; ++t) acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], b, acc[u][t], 0, 0, 0);
+          for (int t = 0; t < MTM; ++t) acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], b, acc[u][t], 0, 0, 0);
+#pragma unroll
+          for (int jj = 0; jj < NR; ++jj) racc[u][jj] = fmaf(gv[jj], b, racc[u][jj]);
         }
       }
     }
@@ -374,17 +389,28 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
     const int kx = j / NC, nc = j - kx * NC;
     const int col = (3 * ky + kx) * C + 32 * nc + c;
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MTM; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + col] = acc[u][t][r];
+#pragma unroll
+    for (int jj = 0; jj < NR; ++jj) {   // the two lane halves' pixels combined
+      const float v = racc[u][jj] + __shfl_xor(racc[u][jj], 32);
+      if (h == 0) out[(int64_t)(32 * MTM + jj) * N + col] = v;
+    }
   }
   if (ky == 0 && tid < M) out[(int64_t)M * N + tid] = cs;
 }
 
-// out[i] = sum_s part[s][i], s ascending (fixed order).
-__global__ void k_sum_splits(const float* __restrict__ part, int64_t n, int nsplit, float* __restrict__ out) {
+// out[i] = sum_s part[s][i], s ascending (fixed order); entries [z0, z1) (the
+// zero-padding rows no split writes) are 0.
+__global__ void k_sum_splits(const float* __restrict__ part, int64_t n, int nsplit, float* __restrict__ out,
+                             int64_t z0, int64_t z1) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
+    if (i >= z0 && i < z1) {
+      out[i] = 0.f;
+      continue;
+    }
     for (int q = 0; q < nsplit; ++q) s += part[(int64_t)q * n + i];
     out[i] = s;
   }
@@ -410,7 +436,7 @@ static size_t wgrad_scratch(int64_t npix, int M, int Cin) {
   return (size_t)ns * ((size_t)M * 9 * Cin + M) * sizeof(float);
 }
 
-template <int MT, int NC>
+template <int MT, int NC, bool VR>
 static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin, float* part, float* dw,
                         hipStream_t st) {
   WgradArgs g;
@@ -423,10 +449,11 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
   int ns;
   wgrad_plan((int64_t)H * W, g.M, Cin, &ns, &g.chunk);
   g.part = part;
-  hipLaunchKernelGGL((k_conv_wgrad<MT, NC>), dim3(ns, 3), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((k_conv_wgrad<MT, NC, VR>), dim3(ns, 3), dim3(256), 0, st, g);
   PNR_LAUNCH_CHECK();
   const int64_t n = (int64_t)g.M * 9 * Cin + g.M;
-  hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, part, n, ns, dw);
+  const int64_t z0 = VR ? (int64_t)(g.M - 32 + 3) * 9 * Cin : 0, z1 = VR ? (int64_t)g.M * 9 * Cin : 0;   // pad rows
+  hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, part, n, ns, dw, z0, z1);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
@@ -560,7 +587,7 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.out = cat1;
   a.act = net1;
   if ((rc = launch_conv<1, 2>(a, st))) return rc;
-  if ((rc = launch_wgrad<1, 1>(cat2, net1, H, W, 32, part, dw2, st))) return rc;
+  if ((rc = launch_wgrad<1, 1, true>(cat2, net1, H, W, 32, part, dw2, st))) return rc;
   // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
   a.in = cat1;
   a.Cin = 64;
@@ -571,7 +598,7 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.out = cat0;
   a.act = net0;
   if ((rc = launch_conv<2, 2>(a, st))) return rc;
-  if ((rc = launch_wgrad<2, 2>(cat1, net0, H, W, 64, part, dw1, st))) return rc;
+  if ((rc = launch_wgrad<2, 2, false>(cat1, net0, H, W, 64, part, dw1, st))) return rc;
   // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
   a.in = cat0;
   a.Cin = 96;
@@ -582,5 +609,5 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.out = d_x;
   a.act = nullptr;
   if ((rc = launch_conv<4, 1>(a, st))) return rc;
-  return launch_wgrad<3, 4>(cat0, x, H, W, 128, part, dw0, st);
+  return launch_wgrad<3, 4, true>(cat0, x, H, W, 128, part, dw0, st);
 }
