@@ -27,7 +27,9 @@ namespace pnr {
 typedef float f32x16r __attribute__((ext_vector_type(16)));
 
 constexpr int kRPx = 128;              // pixels per workgroup (4 waves x 32)
-constexpr int kRCh = 32;               // input channels staged per LDS chunk
+// input channels staged per LDS chunk (16: half the LDS, more workgroups per
+// CU, twice the barriers -- measured 2.50 -> 3.18 ms forward, not kept)
+constexpr int kRCh = 32;
 constexpr int kRPitch = kRCh + 1;      // floats per staged pixel
 constexpr int kRRowPx = kRPx + 2;      // staged pixels per input row (halo 1)
 // Output rows per workgroup tile.  2 (every weight fragment feeding two rows'
