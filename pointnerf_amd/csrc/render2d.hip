@@ -69,6 +69,8 @@ struct ConvArgs {
 };
 
 // BWD: 0 forward, 1 data gradient, 2 data gradient times the LeakyReLU mask of a.act
+// (Cin as a template constant, folding every address to immediates, measured
+// 2.57 vs 2.50 ms forward: the runtime Cin is kept.)
 template <int NT, int BWD>
 __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_r[];
