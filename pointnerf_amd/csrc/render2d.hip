@@ -216,6 +216,9 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   }
 }
 
+#ifndef PNR_CONV_GRID
+#define PNR_CONV_GRID (256 * 3)   // workgroups of the persistent tile loop (one per tile: same time)
+#endif
 template <int NT, int BWD = 0>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
   static bool attr = false;
@@ -225,7 +228,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     attr = true;
   }
   const int64_t tiles = (int64_t)((a.H + kROut - 1) / kROut) * ((a.W + kRPx - 1) / kRPx);
-  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, 256 * 3)), dim3(256), kRLds, st, a);
+  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, PNR_CONV_GRID)), dim3(256), kRLds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
