@@ -286,6 +286,8 @@ struct WgradArgs {
 // every X element 3 times (not 9 x Cin/32 and 9 x M/32 as one wave per tap and
 // tile would).  Wave w: column tiles j = w, w + 4, w + 8 of the 3 Cin/32
 // (tap, channel-tile) pairs, all M/32 row tiles.
+// (Dealing stage 1's 12 (column, row) tile pairs 3 per wave instead of 4 / 4 /
+// 2 / 2 measured no faster: fwd + bwd 8.17 vs 8.10 ms.)
 template <int MT, int NC, bool VR>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgradArgs a) {
   constexpr int M = 32 * MT, C = 32 * NC;
