@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 11
+#define PNR_ABI_VERSION 12
 
 enum {
   PNR_OK = 0,
@@ -587,13 +587,16 @@ int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, const float*
  *   out[v, 1 + j] = raw2out_color(sum_c w[j*128 + c] f_c + b[j]),  j < 3
  *   raw2out_color(x) = sigmoid(x) * (1 + 2e-3) - 1e-3 if act_super > 0, else sigmoid(x)
  * Backward: d_feat[v, 0] = d_out[v, 0], d_feat[v, 1 + c] = sum_j g_j w[j, c] for
- * the same rows (other rows untouched); d_wb[3, 129] += (d W | d b) (atomic
- * accumulation: the caller zeroes it). */
+ * the same rows (other rows untouched); d_wb[3, 129] = (d W | d b), written (not
+ * accumulated): PNR_HEAD_BWD_BLOCKS workgroups write per-block partial sums into
+ * the caller's partials[PNR_HEAD_BWD_BLOCKS * 3 * 129] floats, which a second
+ * launch adds in block order (bitwise repeatable, no float atomics). */
+#define PNR_HEAD_BWD_BLOCKS 512
 int pnr_rgb_head_fwd(const float* feat, int64_t ld, const int32_t* n_dev, int64_t n_max, const float* w,
                      const float* b, int32_t act_super, float* out, void* stream);
 int pnr_rgb_head_bwd(const float* d_out, const float* feat, int64_t ld, const int32_t* n_dev, int64_t n_max,
                      const float* w, const float* b, int32_t act_super, float* d_feat, float* d_wb,
-                     void* stream);
+                     float* partials, void* stream);
 
 /* ------------------------------------------------- point-cloud initialisation
  * construct_vox_points_closest(xyz, vox_res) (models/mvs/mvs_utils.py:537-561,

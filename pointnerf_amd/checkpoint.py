@@ -98,7 +98,9 @@ def grow_points(points: NeuralPoints, add_xyz, add_embedding, add_color=None, ad
     dev = points.xyz.device
     with torch.no_grad():
         points.xyz = _param(torch.cat([points.xyz, add_xyz.to(dev).float()], 0), False)
-        points.points_embeding = _param(torch.cat([points.points_embeding, add_embedding.to(dev).float()[None]], 1),
+        # keep the table's dtype (a bf16 table stays bf16: torch.cat would promote it)
+        emb_t = points.points_embeding.dtype
+        points.points_embeding = _param(torch.cat([points.points_embeding, add_embedding.to(dev).to(emb_t)[None]], 1),
                                         getattr(o, "feat_grad", 1) > 0)
         if points.points_conf is not None:
             points.points_conf = _param(torch.cat([points.points_conf, add_conf.to(dev).float()[None]], 1),

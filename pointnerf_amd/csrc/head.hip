@@ -64,14 +64,15 @@ __global__ void __launch_bounds__(kHBlock) k_rgb_head(const float* __restrict__ 
 }
 
 // d_feat[v, 1 + c] = sum_j g_j W[j, c] with g_j = d_out[v, 1 + j] * d raw2out / dx;
-// d_feat[v, 0] = d_out[v, 0].  d_wb[j*129 + c] (c < 128: d W, c = 128: d b) is
-// accumulated per block and added with one atomic per entry and block.
+// d_feat[v, 0] = d_out[v, 0].  d_wb[j*129 + c] (c < 128: d W, c = 128: d b):
+// each of the kHeadBwdBlocks blocks writes its partial sums to partials[block]
+// and k_rgb_head_wsum adds them in block order (bitwise repeatable, no atomics).
 __global__ void __launch_bounds__(kHBlock) k_rgb_head_bwd(const float* __restrict__ d_out,
                                                           const float* __restrict__ feat, int64_t ld,
                                                           const int32_t* __restrict__ n_dev, int64_t n_max,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ b, int act_super,
-                                                          float* __restrict__ d_feat, float* __restrict__ d_wb) {
+                                                          float* __restrict__ d_feat, float* __restrict__ partials) {
   __shared__ float acc[kHBlock / 32][3][129];
   const int64_t n = n_dev ? min((int64_t)*n_dev, n_max) : n_max;
   const int lane = threadIdx.x & 31, hw = threadIdx.x >> 5;
@@ -125,8 +126,18 @@ __global__ void __launch_bounds__(kHBlock) k_rgb_head_bwd(const float* __restric
     float s = 0.f;
 #pragma unroll
     for (int h = 0; h < kHBlock / 32; ++h) s += (&acc[h][0][0])[i];
-    atomicAdd(d_wb + i, s);
+    partials[(int64_t)blockIdx.x * 3 * 129 + i] = s;
   }
+}
+
+// d_wb[i] = sum over blocks of partials[block][i], in block order.
+__global__ void __launch_bounds__(kHBlock) k_rgb_head_wsum(const float* __restrict__ partials, int nblk,
+                                                           float* __restrict__ d_wb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * 129) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partials[(int64_t)b * 3 * 129 + i];
+  d_wb[i] = s;
 }
 
 }  // namespace pnr
@@ -145,12 +156,16 @@ extern "C" int pnr_rgb_head_fwd(const float* feat, int64_t ld, const int32_t* n_
 
 extern "C" int pnr_rgb_head_bwd(const float* d_out, const float* feat, int64_t ld, const int32_t* n_dev,
                                 int64_t n_max, const float* w, const float* b, int32_t act_super, float* d_feat,
-                                float* d_wb, void* stream) {
-  PNR_CHECK_ARG(d_out && feat && w && b && d_feat && d_wb && n_max >= 0 && ld >= 129,
+                                float* d_wb, float* partials, void* stream) {
+  PNR_CHECK_ARG(d_out && feat && w && b && d_feat && d_wb && partials && n_max >= 0 && ld >= 129,
                 "rgb_head_bwd: bad arguments");
-  if (n_max == 0) return PNR_OK;
-  hipLaunchKernelGGL(k_rgb_head_bwd, dim3(grid_for(n_max, kHBlock / 32, 256 * 2)), dim3(kHBlock), 0,
-                     as_stream(stream), d_out, feat, ld, n_dev, n_max, w, b, act_super, d_feat, d_wb);
+  hipStream_t st = as_stream(stream);
+  if (n_max == 0) return hipMemsetAsync(d_wb, 0, 3 * 129 * sizeof(float), st) == hipSuccess ? PNR_OK : PNR_EHIP;
+  hipLaunchKernelGGL(k_rgb_head_bwd, dim3(PNR_HEAD_BWD_BLOCKS), dim3(kHBlock), 0, st, d_out, feat, ld, n_dev, n_max,
+                     w, b, act_super, d_feat, partials);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_rgb_head_wsum, dim3(cdiv(3 * 129, kHBlock)), dim3(kHBlock), 0, st, partials,
+                     PNR_HEAD_BWD_BLOCKS, d_wb);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

@@ -237,12 +237,20 @@ class NeuralPointsRayMarching(nn.Module):
         on the fp32x3 path (bf16 split: same accuracy, fp32 range) and h2 stays
         off for these weights until they change (``h2_fallbacks`` counts it)."""
         self._sync_rw2c()
+        if self._pending and (sync or self._sv_per_ray is None):
+            # a synchronous call reads (and may clear) the shared range flag and the
+            # counts: complete the pending sync-free calls first so none of their
+            # checks is lost
+            self.finish()
         prec = self._precision_now()
         if not sync and self._sv_per_ray is not None:
             out, rec = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events,
                                          reuse_p1, self._state, capacity=self._capacity_per_ray(), ray_cam=ray_cam)
             rec["args"] = (campos, camrot, raydir, near, far, bg_color, force_grid, reuse_p1, ray_cam)
             rec["out"] = out
+            # what a re-render in finish() must find unchanged (weights, grid)
+            rec["h2_key"] = self.aggregator.h2_key()
+            rec["grid_key"] = self.neural_points.querier.grid.key
             self._pending.append(rec)
             return out
         n_ev = len(events) if events is not None else 0
@@ -308,9 +316,23 @@ class NeuralPointsRayMarching(nn.Module):
         if not pend:
             return []
         pend[-1]["event"].synchronize()
-        range_bad = any(r["precision"] == "fp32h2" for r in pend) and not self.aggregator.h2_range_ok()
+        # every fp32h2 call's own range flag (the packs -- and their flag -- are
+        # rebuilt when the weights change between calls)
+        flags = {}
+        for r in pend:
+            f = r.get("range_flag")
+            if f is not None and f.data_ptr() not in flags:
+                flags[f.data_ptr()] = (f, int(f.item()) != 0)
+        range_bad = any(bad for _, bad in flags.values())
         if range_bad:
-            self._block_h2()
+            cur = self.aggregator.h2_key()
+            for f, bad in flags.values():
+                if bad:
+                    f.zero_()
+            self.aggregator.h2_reset_range()
+            if any(r["h2_key"] == cur for r in pend if r.get("range_flag") is not None):
+                self._h2_blocked_key = cur
+            self.h2_fallbacks += 1
         counts = []
         for rec in pend:
             tot = dict(S_filled=0, S_valid=0, R_hit=0, R_valid=0, n_pairs=0, n_cand=0)
@@ -321,9 +343,14 @@ class NeuralPointsRayMarching(nn.Module):
                 over |= c["S_valid"] > cap
                 for k in tot:
                     tot[k] += c[k]
-            if over or (range_bad and rec["precision"] == "fp32h2"):
+            f = rec.get("range_flag")
+            rec_bad = f is not None and flags[f.data_ptr()][1]
+            if over or rec_bad:
+                if rec["h2_key"] != self.aggregator.h2_key() or rec["grid_key"] != self.neural_points.querier.grid.key:
+                    raise L.PnrError("a render_rays(sync=False) call must be re-rendered, but the weights or the "
+                                     "points changed before finish(): call finish() before modifying the model")
                 cp, cr, rd, near, far, bg, fg, reuse, rcam = rec["args"]
-                prec = "fp32x3" if rec["precision"] == "fp32h2" and range_bad else rec["precision"]
+                prec = "fp32x3" if rec_bad else rec["precision"]
                 out, _ = self._render_rays(prec, cp, cr, rd, near, far, bg, fg, None, False, self._state,
                                            ray_cam=rcam)
                 for dst, src in zip(rec["out"], out):
@@ -382,7 +409,8 @@ class NeuralPointsRayMarching(nn.Module):
         if capacity is not None:
             host = torch.empty((n_chunks, 8), dtype=torch.int32, pin_memory=True) if record else None
             dcounts = None if record else torch.empty((n_chunks, 8), dtype=torch.int32, device=dev)
-            rec = dict(precision=precision, caps=[], host=host, dcounts=dcounts)
+            rec = dict(precision=precision, caps=[], host=host, dcounts=dcounts,
+                       range_flag=_keeph["range_flag"] if _keeph is not None else None)
 
         def mark():
             if events is None:

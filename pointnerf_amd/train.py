@@ -304,10 +304,11 @@ class RgbHeadFn(torch.autograd.Function):
         dev = d_out.device
         d_out = d_out.contiguous()
         d_feat = torch.zeros_like(ctx.f)
-        d_wb = torch.zeros((3, 129), dtype=torch.float32, device=dev)
+        d_wb = torch.empty((3, 129), dtype=torch.float32, device=dev)
+        partials = torch.empty((L.HEAD_BWD_BLOCKS, 3, 129), dtype=torch.float32, device=dev)
         L.check(L.lib().pnr_rgb_head_bwd(L.ptr(d_out), L.ptr(ctx.f), ctx.f.stride(0), L.ptr(ctx.n_dev), ctx.n,
                                          L.ptr(ctx.w), L.ptr(ctx.b), ctx.act, L.ptr(d_feat), L.ptr(d_wb),
-                                         L.stream_ptr(dev)), "pnr_rgb_head_bwd")
+                                         L.ptr(partials), L.stream_ptr(dev)), "pnr_rgb_head_bwd")
         return d_feat, d_wb[:, :128].contiguous(), d_wb[:, 128].contiguous(), None, None, None
 
 

@@ -83,6 +83,14 @@ def test_rgb_head_backward_vs_torch(cuda):
     for a, e, name in zip(x, r, ("feat", "W", "b")):
         np.testing.assert_allclose(a.grad.cpu().numpy(), e.grad.numpy(), atol=1e-4 * float(e.grad.abs().max()),
                                    rtol=1e-4, err_msg=name)
+    # d W / d b: per-block partials summed in block order -> bitwise repeatable
+    first = [t.grad.clone() for t in x]
+    for t in x:
+        t.grad = None
+    out = RgbHeadFn.apply(x[0], x[1], x[2], 1, None, n)
+    (out * d.to(cuda)).sum().backward()
+    for a, f, name in zip(x, first, ("feat", "W", "b")):
+        assert torch.equal(a.grad, f), f"rgb head d{name} not repeatable"
 
 
 def test_rgb_head_train_grads_vs_oracle(cuda):

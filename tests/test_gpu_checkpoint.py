@@ -97,3 +97,26 @@ def test_prune_and_grow_rebuild_grid(cuda):
                      dirs=sc["dir"][order], conf=sc["conf"][order])
     for a, b in zip(_render(m, sc, cuda), _render(direct2, sc, cuda)):
         assert torch.equal(a, b)
+
+
+def test_grow_and_prune_keep_bf16_table(cuda):
+    """A bf16 embedding table stays bf16 through prune / grow (the 104 B/point
+    footprint of config c5), and the bf16 render path keeps reading it."""
+    from pointnerf_amd.aggregator import PointAggregator
+    from pointnerf_amd.checkpoint import grow_points, prune
+    from pointnerf_amd.renderer import NeuralPoints, NeuralPointsRayMarching
+    sc = scene(8000, H=24, W=24)
+    t = lambda k: torch.from_numpy(sc[k])  # noqa: E731
+    np_ = NeuralPoints(sc["opt"], cuda, t("xyz"), t("emb"), t("color"), t("dir"), t("conf"), emb_dtype=torch.bfloat16)
+    agg = PointAggregator(sc["opt"]).to(cuda)
+    agg.load_state_dict({k: torch.from_numpy(v) for k, v in formula_params(salt=0.6).items()})
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg.eval(), precision="bf16")
+    keep = sc["conf"][:, 0] >= 0.5
+    prune(np_, 0.5)
+    assert np_.points_embeding.dtype == torch.bfloat16
+    d = ~keep
+    grow_points(np_, t("xyz")[d], t("emb")[d], t("color")[d], t("dir")[d], t("conf")[d])
+    assert np_.points_embeding.dtype == torch.bfloat16 and np_.points_embeding.shape[1] == sc["xyz"].shape[0]
+    assert np_.bytes_per_point() == 104
+    c, _, mask = _render(m, sc, cuda)
+    assert int(mask.sum()) > 0 and torch.isfinite(c).all()

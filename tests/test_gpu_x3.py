@@ -202,6 +202,39 @@ def test_h2_range_flag_and_fallback(cuda):
         assert m.h2_fallbacks == 1 and m._h2_blocked_key is None and agg.h2_range_ok()
 
 
+def test_h2_mixed_sync_and_async_calls_keep_range_check(cuda):
+    """a synchronous render_rays issued while sync=False calls are
+    pending completes them first, so a pending call whose activations left the
+    f16 range is re-rendered on fp32x3 (none is returned invalid); re-rendering
+    after the weights changed raises instead of silently using new weights."""
+    from pointnerf_amd import _lib as L
+    from pointnerf_amd.renderer import NeuralPointsRayMarching
+    sc = scene(20000, H=32, W=32, default_conf=None)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.3))
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32h2")
+    mx = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32x3")
+    args = [torch.from_numpy(sc[k]).to(cuda) for k in ("campos", "camrot", "raydir")]
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    with torch.no_grad():
+        m.render_rays(*args, 2.0, 6.0, bg)             # first call: synchronous, sizes the buffers
+        agg.block1[2].bias.fill_(1e6)                   # every h2 launch now overflows
+        pend = m.render_rays(*args, 2.0, 6.0, bg, sync=False)
+        assert len(m._pending) == 1
+        sync_out = m.render_rays(*args, 2.0, 6.0, bg)   # must finish the pending call first
+        assert not m._pending and m.h2_fallbacks >= 1
+        want = mx.render_rays(*args, 2.0, 6.0, bg)
+        for a, b, c in zip(pend, sync_out, want):
+            assert torch.equal(a, c) and torch.equal(b, c)
+        # weights changed between an overflowing sync=False call and finish(): refuse
+        agg.block1[2].bias.fill_(0.0)
+        m.render_rays(*args, 2.0, 6.0, bg)              # h2 again (new weights)
+        agg.block1[2].bias.fill_(1e6)
+        m.render_rays(*args, 2.0, 6.0, bg, sync=False)
+        agg.block1[2].bias.fill_(2e6)
+        with pytest.raises(L.PnrError):
+            m.finish()
+
+
 def test_h2_raw_launch_sets_range_flag(cuda):
     """pnr_aggregate_fwd_h2 itself: out-of-range activation -> *range_flag = 1."""
     sc = scene(20000, H=32, W=32, default_conf=None)
