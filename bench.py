@@ -45,10 +45,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--points", type=int, default=2_000_000)
-    ap.add_argument("--hw", type=int, default=800)
-    ap.add_argument("--no-grid-rebuild", action="store_true",
-                    help="reuse the voxel grid across steps (default: rebuild every step)")
+    ap.add_argument("--config", choices=tuple(CONFIGS), default="headline",
+                    help="workload: headline = BASELINE's metric (lego flags, 2M points, 800x800); c4 = scene101 "
+                         "flags, 10M points, 1296x968; c5 = truck flags, 20M points (overflowing max_o and P: "
+                         "seeded reservoir), 1920x1080, bf16 table + bf16 MFMA")
+    ap.add_argument("--points", type=int, default=None, help="override the config's point count")
+    ap.add_argument("--hw", type=int, default=None, help="override H = W (headline config only)")
+    ap.add_argument("--grid-rebuild", action="store_true",
+                    help="rebuild the voxel grid inside every timed step (default: the grid persists across "
+                         "frames, as the points do not change; its build is timed on its own line)")
     ap.add_argument("--no-gather", action="store_true", help="skip the all-gather of rendered rays (N > 1)")
     ap.add_argument("--shard", choices=("frames", "tiles"), default="tiles",
                     help="N > 1 ray batches: tiles (default) = every frame split over the ranks (--tile-layout), "
@@ -64,8 +69,9 @@ def parse():
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="diagnostic (single process): do rank 0's share of an N-rank step (N partial frames of "
                          "1/N of the rays, no collective) to project per-rank overheads of the N-GPU run")
-    ap.add_argument("--cpu-rays", type=int, default=12000,
-                    help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check)")
+    ap.add_argument("--cpu-rays", type=int, default=None,
+                    help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check); "
+                         "default 12000 (headline), 3000 (c4, c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--train-precision", choices=("fp32x3", "fp32"), default="fp32x3",
@@ -74,23 +80,46 @@ def parse():
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
     ap.add_argument("--train-rays", type=int, default=3600, help="rays per train step (random_sample_size 60^2)")
-    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "fp32h2", "bf16"), default="fp32h2",
+    ap.add_argument("--dtype", choices=("fp32", "fp32x3", "fp32h2", "bf16"), default=None,
                     help="MLP arithmetic: fp32h2 (headline, see below); fp32x3 = the reference's fp32 GEMMs as exact 3-way bf16 splits "
                          "(6 cross products) on v_mfma_f32_32x32x16_bf16, fp32-accurate (error vs an fp64 oracle "
                          "equal to native fp32's); fp32h2 = the same GEMMs as 2-way f16 splits (3 products) on "
                          "v_mfma_f32_32x32x16_f16, fp32-accurate; fp32 = native v_mfma_f32_32x32x2_f32; "
                          "bf16 = bf16 operands "
-                         "(SURVEY config c5)")
-    return ap.parse_args()
+                         "(SURVEY config c5); default: the config's")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    args.points = args.points or cfg["points"]
+    args.H, args.W = (args.hw, args.hw) if (args.hw and args.config == "headline") else (cfg["H"], cfg["W"])
+    args.hw = args.H
+    args.dtype = args.dtype or cfg["dtype"]
+    args.cpu_rays = args.cpu_rays or (12000 if args.config == "headline" else 3000)
+    return args
+
+
+# BASELINE.json configs measured by this script (SURVEY 8(d) "Configs as concrete inputs")
+CONFIGS = {
+    "headline": dict(flags="lego", points=2_000_000, H=800, W=800, dtype="fp32h2",
+                     metric="Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref"),
+    "c4": dict(flags="scene101", points=10_000_000, H=968, W=1296, dtype="fp32h2",
+               metric="Mray-samples/sec at 1296x968, K=8, 10M neural points (config c4, scene101 flags)"),
+    "c5": dict(flags="truck", points=20_000_000, H=1080, W=1920, dtype="bf16", cap=-1, scatter=0.1,
+               metric="Mray-samples/sec at 1920x1080, K=8, 20M neural points (config c5, truck flags, bf16)"),
+}
 
 
 def build_scene(args, device):
     from pointnerf_amd import synthetic as S
     from pointnerf_amd.aggregator import PointAggregator
-    from pointnerf_amd.options import lego_opt
+    from pointnerf_amd.options import flagset_opt
     from pointnerf_amd.renderer import NeuralPoints, NeuralPointsRayMarching
-    opt = lego_opt()
-    pts = S.lego_like_points(args.points, seed=0)
+    cfg = CONFIGS[args.config]
+    opt = flagset_opt(cfg["flags"])
+    if cfg["flags"] == "lego":
+        pts = S.lego_like_points(args.points, seed=0)
+    else:
+        pts = S.scene_points(cfg["flags"], args.points, opt, seed=0, cap=cfg.get("cap"),
+                             scatter=cfg.get("scatter", 0.0))
     emb, color, dirs, conf = S.point_features(args.points, seed=0, default_conf=opt.default_conf)
     torch.manual_seed(0)
     agg = PointAggregator(opt).to(device).eval()   # random-init weights (xavier, networks.py:163-172)
@@ -101,13 +130,20 @@ def build_scene(args, device):
     return opt, pts, (emb, color, dirs, conf), agg, model
 
 
-def cameras(n_frames, H, W):
+def cameras(n_frames, H, W, flags="lego"):
+    """n_frames views of the config's camera path: the NeRF-synthetic orbit for
+    lego, the scene's own views otherwise (synthetic.scene_camera)."""
     from pointnerf_amd import synthetic as S
-    f = S.lego_focal(H)
     cams = []
     for i in range(n_frames):
-        theta = -180.0 + 360.0 * i / max(n_frames, 1)
-        campos, camrot = S.camera(theta, -30.0, 4.0)
+        if flags == "lego":
+            theta = -180.0 + 360.0 * i / max(n_frames, 1)
+            campos, camrot = S.camera(theta, -30.0, 4.0)
+            f = S.lego_focal(H)
+        else:
+            campos, camrot = S.scene_camera(flags, i, n_frames)
+            W0, _, f0 = S.SCENE_INTRINSICS[flags]
+            f = f0 * W / W0
         cams.append((campos, camrot, S.pixel_rays(H, W, f, camrot)))
     return cams
 
@@ -224,11 +260,33 @@ def accuracy_vs_x3(model, opt, cam, bg, dtype):
             "full_frame_rays_hit": int(hit.sum())}
 
 
-def stage_rooflines(args, opt, model, stage, per, launches):
+def time_grid_build(model, opt, reps=3):
+    """Forced rebuilds of the persistent voxel grid (pnr_points_bbox + its host
+    read + pnr_grid_build), wall time between two synchronisations, and the
+    build's overflow statistics (seeded reservoir)."""
+    q = model.neural_points.querier
+    xyz = model.neural_points.xyz.detach().contiguous()
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        q.grid.build(opt, xyz, force=True)
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    st = q.grid.stats()
+    return {"ms": round(float(np.median(ts)), 3), "n_voxels": int(st["n_voxels"]),
+            "n_voxels_kept": int(st["n_voxels_kept"]), "n_points_dropped": int(st["n_points_dropped"]),
+            "max_o": int(opt.max_o), "P": int(opt.P), "dims": [int(d) for d in st["dims"]],
+            "overflow_policy": getattr(opt, "max_o_policy", "reservoir") + " (seeded, grid_seed "
+                               f"{int(getattr(opt, 'grid_seed', 0))})"}
+
+
+def stage_rooflines(args, opt, model, stage, per, launches, grid=None):
     """SURVEY 8(d) compulsory-byte formulas for the memory/latency-bound stages,
     per frame, against HBM peak (informational; the headline roofline is the
-    aggregate's).  query = grid build + march + KNN + compactions (the bench
-    rebuilds the grid every frame)."""
+    aggregate's).  query = march + KNN + compactions (+ the grid build when
+    --grid-rebuild puts it in every step); grid_build = the persistent grid's
+    build on its own."""
     n = max(launches, 1)
     dims = model.neural_points.querier.grid.hp["dims"]
     cells = int(np.prod(np.asarray(dims, dtype=np.int64)))
@@ -241,14 +299,22 @@ def stage_rooflines(args, opt, model, stage, per, launches):
     march_b = R * D * 4 + R * 16
     knn_b = S * 27 * 8 + cand * 16
     comp_b = V * (C + 1) * 4 + R * (C + 1 + SR) * 4
+    q_b = march_b + knn_b + (grid_b if args.grid_rebuild else 0)
     res = {}
-    for name, b in (("query", grid_b + march_b + knn_b), ("composite", comp_b)):
+    for name, b in (("query", q_b), ("composite", comp_b)):
         ms = float(np.mean(per.get(name, [0.0])))
         gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         res[name] = {"bytes": int(b), "ms": round(ms, 3), "achieved_GBs": round(gbs, 1),
                      "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
-    res["query"]["parts_bytes"] = {"grid_build": int(grid_b), "march": int(march_b), "knn": int(knn_b)}
+    res["query"]["parts_bytes"] = {"march": int(march_b), "knn": int(knn_b)}
+    if args.grid_rebuild:
+        res["query"]["parts_bytes"]["grid_build"] = int(grid_b)
     res["query"]["knn_candidates"] = int(cand)
+    if grid is not None:
+        gbs = grid_b / (grid["ms"] * 1e-3) / 1e9 if grid["ms"] > 0 else 0.0
+        res["grid_build"] = {"bytes": int(grid_b), "ms": grid["ms"], "achieved_GBs": round(gbs, 1),
+                             "frac_hbm": round(gbs / HBM_PEAK_GBS, 4),
+                             "note": "wall time incl. the bbox host read; not inside the timed steps"}
     return res
 
 
@@ -337,10 +403,11 @@ def main():
             dist.init_process_group(backend)
     from pointnerf_amd import _lib as L
 
-    H = W = args.hw
+    H, W = args.H, args.W
+    cfg = CONFIGS[args.config]
     opt, pts, feats, agg, model = build_scene(args, device)
     model.precision = args.dtype
-    cams = cameras(8, H, W)
+    cams = cameras(8, H, W, cfg["flags"])
     SR = opt.SR
     # per-(frame, rank) pixel lists: step s renders frames s*world .. s*world+world-1
     shard_world = world if args.shard == "tiles" else 1   # partial frames per rank per step
@@ -370,6 +437,17 @@ def main():
     stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0, "cand": 0, "rays": 0}
 
     steps = {}
+    # shader clock under load: one probe wave per timed step on a side stream,
+    # beside the step's kernels (pnr_clock_probe, ~10 ms of s_sleep)
+    probe = {"stream": torch.cuda.Stream(device), "out": torch.zeros(max(args.steps, 1), device=device), "n": 0}
+
+    def clock_probe():
+        if probe["n"] >= probe["out"].numel():
+            return
+        with torch.cuda.stream(probe["stream"]):
+            L.check(L.lib().pnr_clock_probe(L.ptr(probe["out"][probe["n"]:]), 20000, L.stream_ptr(device)),
+                    "pnr_clock_probe")
+        probe["n"] += 1
 
     def step_batch(s):
         """tiles mode: this rank's shares of the step's N frames as ONE ray batch
@@ -393,7 +471,7 @@ def main():
         if shard_world > 1 and not args.per_frame_calls:
             st, rd, cp, cr = step_batch(s)
             color = model.render_rays(cp, cr, rd, opt.near_plane, opt.far_plane, bg,
-                                      force_grid=not args.no_grid_rebuild, events=ev_step, sync=False,
+                                      force_grid=args.grid_rebuild, events=ev_step, sync=False,
                                       ray_cam=st.ray_cam)[0]
             parts.append((st, color, rd.shape[0]))
         else:
@@ -404,9 +482,11 @@ def main():
                 ci, rd, sh = my_rays(frame)
                 campos, camrot, _ = dev_cams[ci]
                 color = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
-                                          force_grid=(f == 0 and not args.no_grid_rebuild),
+                                          force_grid=(f == 0 and args.grid_rebuild),
                                           events=ev_step, reuse_p1=f > 0, sync=False)[0]
                 parts.append((sh, color, rd.shape[0]))
+        if timed:
+            clock_probe()
         counts = model.finish()
         if timed:
             for c, (_, _, nr) in zip(counts, parts):
@@ -476,7 +556,7 @@ def main():
         # (tools/prof_bench.sh -> tools/profile_summary.py; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
         traffic = None
         pmc = os.path.join(ROOT, "profiles", PMC_FILES.get(args.dtype, ""))
-        if args.dtype in PMC_FILES and os.path.exists(pmc):
+        if args.config == "headline" and args.dtype in PMC_FILES and os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
@@ -487,7 +567,7 @@ def main():
         peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "fp32x3": round(BF16_MFMA_PEAK_TFLOPS / 6, 1),
                 "fp32h2": round(BF16_MFMA_PEAK_TFLOPS / 3, 1), "bf16": BF16_MFMA_PEAK_TFLOPS}[args.dtype]
         out = {
-            "metric": "Mray-samples/sec at 800x800, K=8, 2M neural points; PSNR delta vs ref",
+            "metric": cfg["metric"],
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -500,10 +580,12 @@ def main():
                                 "products on v_mfma_f32_32x32x16_f16, fp32 accumulation (error vs an fp64 oracle "
                                 "~ native fp32's, tests/test_gpu_x3.py)",
                       "bf16": "bf16 operands, fp32 accumulation"}[args.dtype],
-            "data": "synthetic (seeded lego-like 2M-point cloud, random-init lego viewmlp weights)",
-            "config": {"workload": f"lego {H}x{W} forward render, K={opt.K}, SR={SR}, {args.points} points",
+            "data": (f"synthetic (seeded {cfg['flags']}-like {args.points / 1e6:g}M-point cloud, random-init "
+                     f"{cfg['flags']} viewmlp weights)"),
+            "config": {"workload": f"{cfg['flags']} {W}x{H} forward render, K={opt.K}, SR={SR}, {args.points} points"
+                                   + ("" if args.config == "headline" else f" (BASELINE config {args.config})"),
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
-                       "grid_rebuild_per_step": not args.no_grid_rebuild,
+                       "max_o": int(opt.max_o), "grid_rebuild_per_step": bool(args.grid_rebuild),
                        "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else
@@ -542,7 +624,14 @@ def main():
         out["overflow_rerenders"] = int(model.overflow_rerenders - rerenders0)
         if shard_world != world:
             out["config"]["emulated_world"] = shard_world   # diagnostic: rank 0's share of an N-rank step
-        out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per, launches)
+        # the shader clock the step's kernels ran at (pnr_clock_probe beside them)
+        clk = probe["out"][:probe["n"]].cpu().numpy()
+        clk = clk[clk > 0]
+        out["sclk_mhz_in_run"] = round(float(np.median(clk)), 1) if len(clk) else None
+        # the voxel grid persists across frames (the points do not change); its
+        # build (bbox read + 8 kernels + scans) on its own line
+        out["grid_build"] = time_grid_build(model, opt)
+        out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per, launches, out["grid_build"])
         acc = {}
         if not args.no_cpu_baseline and world == 1:
             try:

@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 12
+#define PNR_ABI_VERSION 13
 
 enum {
   PNR_OK = 0,
@@ -90,24 +90,32 @@ typedef struct {
   int32_t P;            /* points kept per voxel (flag --P)                       */
   int32_t slot0_drop;   /* 1 = reproduce `voxel_idx > 0` (qpiw.py:372): the voxel
                            given slot 0 keeps no points; 0 = keep them          */
+  uint64_t seed;        /* seed of the overflow reservoir (the reference: time()) */
 } pnr_grid_params;
 
 /* Build the persistent sparse voxel tables from xyz[N,3] (device, fp32).
  * Deterministic: voxel slots are assigned in ascending order of the first
  * point index that lands in each voxel (the serial order of claim_occ), points
- * inside a voxel are kept in ascending index order (first P of them).  Tables
- * are reallocated only when dims/max_o/P grow.  No host sync: the build
- * counters travel to pinned host memory behind an event that only
- * pnr_grid_stats_get waits on.  Returns PNR_OK even on max_o / P overflow;
- * inspect pnr_grid_stats. */
+ * inside a voxel are kept in ascending index order.  On overflow -- more
+ * occupied voxels than max_o, more points than P in a voxel -- the reference's
+ * reservoir replacement (qpiw.py:289-298, 377-384: uniform random subsets, time
+ * seed) becomes a seeded one: the max_o voxels with the smallest key
+ * hash32(seed, first point) << 32 | first point are kept (slots in first-point
+ * order), and a voxel keeps the P points with the smallest key
+ * hash32(seed + 0x632BE59BD9B4E019, id) << 32 | id (ascending id); hash32 =
+ * splitmix64 finaliser of seed ^ id * 0x9E3779B97F4A7C15, high 32 bits.  Tables
+ * are reallocated only when dims/max_o/P grow; grids up to 2^36 cells (int64
+ * cell indices).  No host sync: the build counters travel to pinned host memory
+ * behind an event that only pnr_grid_stats_get waits on.  Returns PNR_OK on
+ * overflow; inspect pnr_grid_stats. */
 int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
                    const pnr_grid_params* p, void* stream);
 
 typedef struct {
   int64_t n_points_in_grid;   /* points whose voxel is inside dims            */
   int64_t n_voxels;           /* occupied voxels (before max_o truncation)    */
-  int64_t n_voxels_kept;      /* min(n_voxels, max_o)                         */
-  int64_t n_points_dropped;   /* points beyond P in their voxel               */
+  int64_t n_voxels_kept;      /* min(n_voxels, max_o) (the reservoir's voxels) */
+  int64_t n_points_dropped;   /* points of kept voxels beyond P (not in the reservoir) */
   int32_t max_points_per_voxel;
   int32_t dims[3];
 } pnr_grid_stats;
@@ -615,6 +623,11 @@ int pnr_vox_closest(const float* xyz_dev, int64_t n, int32_t vox_res, float* cen
                     void* stream);
 
 /* ------------------------------------------------------------- utilities */
+/* Diagnostics: out_dev[0] = the shader clock (MHz) one wave measured over
+ * `spins` s_sleep slices (s_memtime cycles / s_memrealtime 100 MHz ticks);
+ * launched beside running kernels it reports the clock under that load. */
+int pnr_clock_probe(float* out_dev, int32_t spins, void* stream);
+
 /* Exclusive scan of n int32 values (n_dev: optional device-side length <= n,
  * entries past it are treated as 0 and out[] is written up to n_dev+1);
  * total written to *total_dev (may be NULL). */

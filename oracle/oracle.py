@@ -41,7 +41,7 @@ def _load():
         P = ctypes.c_void_p
         lib.oracle_grid_build.restype = ctypes.c_int64
         lib.oracle_grid_build.argtypes = [P, ctypes.c_int64, P, P, P, P, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_int, P, P, P, P]
+                                          ctypes.c_int, ctypes.c_uint64, P, P, P, P]
         lib.oracle_ray_march.restype = None
         lib.oracle_ray_march.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, P, P, P, P, P, P]
@@ -155,7 +155,8 @@ def w2pers(p, campos, camrot):
 
 # ----------------------------------------------------------------------- query
 def grid_build(opt, xyz, hp=None):
-    """build_occ_vox (qpiw.py:546-611) via query_ref.c."""
+    """build_occ_vox (qpiw.py:546-611) via query_ref.c; max_o / P overflow keeps
+    the seeded reservoir's uniform subsets (opt.grid_seed, query_ref.c)."""
     lib = _load()
     xyz = np.ascontiguousarray(np.asarray(xyz, F32).reshape(-1, 3))
     hp = hp or get_hyperparameters(opt, xyz)
@@ -170,6 +171,7 @@ def grid_build(opt, xyz, hp=None):
     vs = np.ascontiguousarray(hp["vsize_s"].astype(F32))
     n_occ = lib.oracle_grid_build(_p(xyz), xyz.shape[0], _p(shift), _p(vs), _p(dims), _p(qs),
                                   opt.max_o, opt.P, int(getattr(opt, "slot0_drop", 1)),
+                                  int(getattr(opt, "grid_seed", 0)),
                                   _p(coor_2_occ), _p(coor_occ), _p(occ_numpnts), _p(occ_2_pnts))
     return dict(hp=hp, coor_2_occ=coor_2_occ, coor_occ=coor_occ, occ_numpnts=occ_numpnts,
                 occ_2_pnts=occ_2_pnts.reshape(opt.max_o, opt.P), n_occ=int(n_occ))

@@ -13,10 +13,15 @@
  *   mask_raypos          query_point_indices_worldcoords.py:390-414
  *   cumsum SR pick + get_shadingloc  query_point_indices_worldcoords.py:655-677, 417-439
  *   query_neigh_along_ray_layered    query_point_indices_worldcoords.py:442-528
- * Reservoir replacement on max_o / P overflow (curand seeded with time(),
- * qpiw.py:289-298, 377-384) has no reproducible result; the oracle drops the
- * overflowing voxel / point instead (the library does the same), and the
- * tests keep their inputs below both capacities.
+ * Overflow (qpiw.py:289-298, 377-384): the reference replaces slots with
+ * reservoir sampling (Algorithm R, curand seeded with time()), whose result is
+ * a uniform random subset -- max_o of the occupied voxels, P of a voxel's
+ * points -- with no reproducible draw.  Oracle and library draw the same
+ * uniform subsets from a seeded hash instead ("seeded reservoir"): the kept
+ * voxels are the max_o with the smallest key (hash32(seed, first point) << 32
+ * | first point), numbered in first-point order; a voxel keeps the P points
+ * with the smallest key (hash32(seed + PNR_PT_SALT, id) << 32 | id), in
+ * ascending index order.  Without overflow both reduce to the serial order.
  *
  * Parity status: the reference's query is CUDA C inside a Python string that
  * pycuda JIT-compiles; it needs cuda.h / curand_kernel.h / pycuda, none of
@@ -38,46 +43,77 @@
 
 static int vox(float p, float shift, float vs) { return (int)floorf((p - shift) / vs); }
 
-/* Grid tables (serial claim_occ -> map_coor2occ -> fill_occ2pnts).
- * coor_2_occ[gvol] (-1 empty), coor_occ[gvol] (0/1 dilated), occ_numpnts[max_o],
- * occ_2_pnts[max_o*P] (-1), returns the number of occupied voxels (occ_idx). */
+/* the seeded reservoir's keys (same integer arithmetic as pnr_common.h) */
+#define PNR_PT_SALT 0x632BE59BD9B4E019ull
+static uint32_t hash32(uint64_t seed, uint32_t id) {
+  uint64_t z = seed ^ ((uint64_t)id * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+static uint64_t vkey(uint64_t seed, uint32_t id) { return ((uint64_t)hash32(seed, id) << 32) | id; }
+static uint64_t pkey(uint64_t seed, uint32_t id) { return ((uint64_t)hash32(seed + PNR_PT_SALT, id) << 32) | id; }
+static int cmp_u64(const void* a, const void* b) {
+  uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+static int cmp_i32(const void* a, const void* b) {
+  int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* Grid tables (serial claim_occ -> map_coor2occ -> fill_occ2pnts, seeded
+ * reservoir on overflow).  coor_2_occ[gvol] (-1 empty), coor_occ[gvol] (0/1
+ * dilated), occ_numpnts[max_o] (points that reached the voxel, as the
+ * reference's counter: may exceed P), occ_2_pnts[max_o*P] (-1); returns the
+ * number of occupied voxels (occ_idx, before the max_o cut). */
 int64_t oracle_grid_build(const float* xyz, int64_t n, const float shift[3], const float vs[3],
-                          const int dims[3], const int qs[3], int max_o, int P, int slot0_drop,
+                          const int dims[3], const int qs[3], int max_o, int P, int slot0_drop, uint64_t seed,
                           int32_t* coor_2_occ, uint8_t* coor_occ, int32_t* occ_numpnts,
                           int32_t* occ_2_pnts) {
   const int64_t gvol = (int64_t)dims[0] * dims[1] * dims[2];
-  int32_t* occ_2_coor = (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)max_o);
+  int64_t* pcell = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int32_t* first = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1)); /* first point of voxel v */
   for (int64_t i = 0; i < gvol; ++i) {
     coor_2_occ[i] = -1;
     coor_occ[i] = 0;
   }
-  for (int64_t i = 0; i < (int64_t)max_o * 3; ++i) occ_2_coor[i] = -1;
   for (int64_t i = 0; i < max_o; ++i) occ_numpnts[i] = 0;
   for (int64_t i = 0; i < (int64_t)max_o * P; ++i) occ_2_pnts[i] = -1;
   int64_t occ_idx = 0;
-  /* claim_occ */
+  /* claim_occ: voxels in first-point order (coor_2_occ temporarily = voxel number) */
   for (int64_t i = 0; i < n; ++i) {
     int c[3];
     for (int a = 0; a < 3; ++a) c[a] = vox(xyz[i * 3 + a], shift[a], vs[a]);
+    pcell[i] = -1;
     if (c[0] < 0 || c[0] >= dims[0] || c[1] < 0 || c[1] >= dims[1] || c[2] < 0 || c[2] >= dims[2])
       continue;
     int64_t cell = ((int64_t)c[0] * dims[1] + c[1]) * dims[2] + c[2];
+    pcell[i] = cell;
     if (coor_2_occ[cell] == -1) {
-      coor_2_occ[cell] = 0;
-      int64_t tmp = occ_idx++;
-      if (tmp < max_o) {
-        occ_2_coor[tmp * 3 + 0] = c[0];
-        occ_2_coor[tmp * 3 + 1] = c[1];
-        occ_2_coor[tmp * 3 + 2] = c[2];
-      }
+      coor_2_occ[cell] = (int32_t)occ_idx;
+      first[occ_idx++] = (int32_t)i;
     }
   }
+  /* reservoir over the voxels: keep the max_o smallest keys */
+  uint64_t thr = ~0ull;
+  if (occ_idx > max_o) {
+    uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)occ_idx);
+    for (int64_t v = 0; v < occ_idx; ++v) keys[v] = vkey(seed, (uint32_t)first[v]);
+    qsort(keys, (size_t)occ_idx, sizeof(uint64_t), cmp_u64);
+    thr = keys[max_o - 1];
+    free(keys);
+  }
   for (int64_t i = 0; i < gvol; ++i) coor_2_occ[i] = -1; /* qpiw.py:575 */
-  /* map_coor2occ (dilation by query_size) */
-  for (int64_t s = 0; s < occ_idx && s < max_o; ++s) {
-    int c0 = occ_2_coor[s * 3], c1 = occ_2_coor[s * 3 + 1], c2 = occ_2_coor[s * 3 + 2];
-    if (c0 < 0) continue;
-    coor_2_occ[((int64_t)c0 * dims[1] + c1) * dims[2] + c2] = (int32_t)s;
+  /* map_coor2occ: kept voxels numbered in first-point order, dilation by query_size */
+  int64_t s = 0;
+  for (int64_t v = 0; v < occ_idx; ++v) {
+    if (vkey(seed, (uint32_t)first[v]) > thr) continue;
+    const int64_t cell = pcell[first[v]];
+    const int c0 = (int)(cell / ((int64_t)dims[1] * dims[2])), c1 = (int)((cell / dims[2]) % dims[1]),
+              c2 = (int)(cell % dims[2]);
+    coor_2_occ[cell] = (int32_t)s++;
     int x0 = c0 - qs[0] / 2 > 0 ? c0 - qs[0] / 2 : 0;
     int x1 = c0 + (qs[0] + 1) / 2 < dims[0] ? c0 + (qs[0] + 1) / 2 : dims[0];
     int y0 = c1 - qs[1] / 2 > 0 ? c1 - qs[1] / 2 : 0;
@@ -88,19 +124,39 @@ int64_t oracle_grid_build(const float* xyz, int64_t n, const float shift[3], con
       for (int y = y0; y < y1; ++y)
         for (int z = z0; z < z1; ++z) coor_occ[((int64_t)x * dims[1] + y) * dims[2] + z] = 1;
   }
-  /* fill_occ2pnts */
+  /* fill_occ2pnts: every point of a kept voxel (ascending index) ... */
+  const int64_t nk = s;
+  int64_t* off = (int64_t*)calloc((size_t)nk + 1, sizeof(int64_t));
   for (int64_t i = 0; i < n; ++i) {
-    int c[3];
-    for (int a = 0; a < 3; ++a) c[a] = vox(xyz[i * 3 + a], shift[a], vs[a]);
-    if (c[0] < 0 || c[0] >= dims[0] || c[1] < 0 || c[1] >= dims[1] || c[2] < 0 || c[2] >= dims[2])
-      continue;
-    int32_t v = coor_2_occ[((int64_t)c[0] * dims[1] + c[1]) * dims[2] + c[2]];
-    if (slot0_drop ? (v > 0) : (v >= 0)) {
-      int32_t tmp = occ_numpnts[v]++;
-      if (tmp < P) occ_2_pnts[(int64_t)v * P + tmp] = (int32_t)i;
-    }
+    if (pcell[i] < 0) continue;
+    int32_t v = coor_2_occ[pcell[i]];
+    if (slot0_drop ? (v > 0) : (v >= 0)) ++off[v + 1];
   }
-  free(occ_2_coor);
+  for (int64_t v = 0; v < nk; ++v) off[v + 1] += off[v];
+  int32_t* ids = (int32_t*)malloc(sizeof(int32_t) * (size_t)(off[nk] > 0 ? off[nk] : 1));
+  for (int64_t i = 0; i < n; ++i) {
+    if (pcell[i] < 0) continue;
+    int32_t v = coor_2_occ[pcell[i]];
+    if (slot0_drop ? (v > 0) : (v >= 0)) ids[off[v] + occ_numpnts[v]++] = (int32_t)i;
+  }
+  /* ... of which a voxel keeps P: the P smallest point keys, ascending index */
+  for (int64_t v = 0; v < nk; ++v) {
+    const int64_t cnt = off[v + 1] - off[v];
+    int32_t* vi = ids + off[v];
+    if (cnt > P) {
+      uint64_t* k = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)cnt);
+      for (int64_t j = 0; j < cnt; ++j) k[j] = pkey(seed, (uint32_t)vi[j]);
+      qsort(k, (size_t)cnt, sizeof(uint64_t), cmp_u64);
+      for (int j = 0; j < P; ++j) vi[j] = (int32_t)(k[j] & 0xffffffffu);
+      qsort(vi, (size_t)P, sizeof(int32_t), cmp_i32);
+      free(k);
+    }
+    for (int j = 0; j < cnt && j < P; ++j) occ_2_pnts[v * P + j] = vi[j];
+  }
+  free(ids);
+  free(off);
+  free(first);
+  free(pcell);
   return occ_idx;
 }
 

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 12
+ABI_VERSION = 13
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -29,7 +29,7 @@ class PnrError(RuntimeError):
 class GridParams(ctypes.Structure):
     _fields_ = [("shift", c_float * 3), ("vsize", c_float * 3), ("dims", c_int32 * 3),
                 ("query_size", c_int32 * 3), ("max_o", c_int32), ("P", c_int32),
-                ("slot0_drop", c_int32)]
+                ("slot0_drop", c_int32), ("seed", ctypes.c_uint64)]
 
 
 class GridStats(ctypes.Structure):
@@ -126,6 +126,7 @@ P = ctypes.POINTER
 # name -> (restype, argtypes); exactly the functions include/pnr.h declares.
 SIGNATURES = {
     "pnr_abi_version": (c_int, []),
+    "pnr_clock_probe": (c_int, [c_void_p, c_int32, c_void_p]),
     "pnr_last_error": (ctypes.c_char_p, []),
     "pnr_create": (c_int, [c_int, P(c_void_p)]),
     "pnr_destroy": (c_int, [c_void_p]),

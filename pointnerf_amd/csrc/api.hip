@@ -44,3 +44,22 @@ extern "C" int pnr_destroy(pnr_handle* h) {
   delete h;
   return PNR_OK;
 }
+
+// Shader clock under load (bench diagnostics): one wave spins for `spins`
+// s_sleep slices between two (s_memtime, s_memrealtime) pairs; out[0] = shader
+// cycles / (100 MHz real-time ticks) * 100 = the SCLK in MHz the wave saw
+// (MI355X_MICROARCH "DVFS give-back" item 6).  Launched on a side stream while
+// the timed kernels run, it reports the clock they ran at.
+__global__ void k_clock_probe(float* out, int spins) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < spins; ++i) __builtin_amdgcn_s_sleep(8);
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) out[0] = r1 > r0 ? (float)(c1 - c0) / (float)(r1 - r0) * 100.f : 0.f;
+}
+
+extern "C" int pnr_clock_probe(float* out_dev, int32_t spins, void* stream) {
+  PNR_CHECK_ARG(out_dev && spins > 0, "clock_probe: bad arguments");
+  hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, pnr::as_stream(stream), out_dev, spins);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}

@@ -13,7 +13,16 @@
 // = 35.5 MB), one dilated-occupancy BITMAP (1 bit per cell: 1.1 MB, stays in
 // every XCD's L2 for the ray march), and a slot-major float4 table
 // {x, y, z, point id} of P entries per slot so the KNN loop reads one 16-B
-// record per candidate instead of an index plus a 12-B xyz gather.
+// record per candidate instead of an index plus a 12-B xyz gather.  Cell
+// indices are int64 (a +-10 m scene101 range at 16 mm voxels is 1.95e9 cells).
+//
+// Overflow (more occupied voxels than max_o, more points than P in a voxel):
+// the reference's reservoir replacement (qpiw.py:289-298, 377-384) keeps a
+// uniform random subset with a time seed; here the same uniform subsets come
+// from a seeded hash (pnr_common.h res_vkey / res_pkey): the max_o voxels of
+// smallest key, found by an 8-pass radix select on the device (no host sync),
+// and per voxel the P points of smallest key.  Without overflow the tables
+// are exactly the serial order.
 #include "pnr_common.h"
 
 namespace pnr {
@@ -85,28 +94,29 @@ struct GridDev {
   float shift[3], vs[3];
   int dims[3], qs[3];
   int max_o, P, slot0_drop;
+  uint64_t seed;
 };
 
-__device__ __forceinline__ int cell_of(const float* p, const GridDev& g, int c[3]) {
+__device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int c[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) c[a] = vox_coord(p[a], g.shift[a], g.vs[a]);
   if (c[0] < 0 || c[0] >= g.dims[0] || c[1] < 0 || c[1] >= g.dims[1] || c[2] < 0 ||
       c[2] >= g.dims[2])
     return -1;
-  return (c[0] * g.dims[1] + c[1]) * g.dims[2] + c[2];
+  return ((int64_t)c[0] * g.dims[1] + c[1]) * g.dims[2] + c[2];
 }
 
 // claim_occ's voxel coordinate + first-claimer (qpiw.py:262-283), made
 // order-free: the claimer is the smallest point index of the voxel.
 __global__ void __launch_bounds__(kBlock) k_cells(const float* __restrict__ xyz, int64_t n, GridDev g,
-                                                  int32_t* __restrict__ pt_cell,
+                                                  int64_t* __restrict__ pt_cell,
                                                   int32_t* __restrict__ first_pt, int32_t* counters) {
   int in_grid = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
     int c[3];
-    int cell = cell_of(p, g, c);
+    const int64_t cell = cell_of(p, g, c);
     pt_cell[i] = cell;
     if (cell >= 0) {
       atomicMin(first_pt + cell, (int)i);
@@ -117,20 +127,85 @@ __global__ void __launch_bounds__(kBlock) k_cells(const float* __restrict__ xyz,
   if ((threadIdx.x & 63) == 0 && in_grid) atomicAdd(counters + 1, in_grid);
 }
 
-__global__ void __launch_bounds__(kBlock) k_first_flags(int64_t n, const int32_t* __restrict__ pt_cell,
+__global__ void __launch_bounds__(kBlock) k_first_flags(int64_t n, const int64_t* __restrict__ pt_cell,
                                                         const int32_t* __restrict__ first_pt,
                                                         int32_t* __restrict__ flag) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int cell = pt_cell[i];
+    const int64_t cell = pt_cell[i];
     flag[i] = (cell >= 0 && first_pt[cell] == (int)i) ? 1 : 0;
   }
+}
+
+// ---- voxel reservoir (claim_occ overflow, qpiw.py:283-298): radix select of
+// the key of rank max_o - 1 among the occupied voxels' keys, 8 bits per pass,
+// most significant first.  SelState lives in device memory; hist[256] beside it.
+struct SelState {
+  unsigned long long prefix;   // key bits fixed so far (after the last pass: the threshold key)
+  unsigned long long k;        // rank still to find below the fixed prefix
+  int all;                     // 1: n_voxels <= max_o, every voxel kept
+  int pad;
+};
+
+__global__ void k_sel_init(const int32_t* __restrict__ n_vox, int max_o, SelState* st, uint32_t* hist) {
+  hist[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    st->all = *n_vox <= max_o;
+    st->prefix = 0;
+    st->k = (unsigned long long)(max_o - 1);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_sel_hist(int64_t n, const int32_t* __restrict__ flag, uint64_t seed,
+                                                     int shift, const SelState* __restrict__ st,
+                                                     uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const bool all = st->all;
+  const unsigned long long prefix = st->prefix;
+  const unsigned long long hi = shift >= 56 ? 0ull : (~0ull << (shift + 8));
+  if (!all) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+      if (!flag[i]) continue;
+      const unsigned long long key = res_vkey(seed, (uint32_t)i);
+      if (((key ^ prefix) & hi) == 0) atomicAdd(&h[(key >> shift) & 255u], 1u);
+    }
+  }
+  __syncthreads();
+  if (!all && h[threadIdx.x]) atomicAdd(hist + threadIdx.x, h[threadIdx.x]);
+}
+
+__global__ void k_sel_pick(int shift, SelState* st, uint32_t* hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = hist[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0 && !st->all) {
+    unsigned long long cum = 0;
+    int d = 0;
+    for (; d < 255; ++d) {
+      if (cum + h[d] > st->k) break;
+      cum += h[d];
+    }
+    st->prefix |= (unsigned long long)d << shift;
+    st->k -= cum;
+  }
+  hist[threadIdx.x] = 0;
+}
+
+// keep the first point of a voxel only when its voxel is among the max_o kept
+__global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, const SelState* __restrict__ st,
+                                                      int32_t* __restrict__ flag) {
+  if (st->all) return;
+  const unsigned long long thr = st->prefix;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (flag[i] && res_vkey(seed, (uint32_t)i) > thr) flag[i] = 0;
 }
 
 // map_coor2occ (qpiw.py:305-340): slot -> coor_2_occ, dilation of the
 // occupancy by query_size (bitmap, atomicOr).
 __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz, int64_t n, GridDev g,
-                                                  const int32_t* __restrict__ pt_cell,
+                                                  const int64_t* __restrict__ pt_cell,
                                                   const int32_t* __restrict__ flag,
                                                   const int32_t* __restrict__ pt_slot,
                                                   int32_t* __restrict__ coor_2_occ,
@@ -139,13 +214,13 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (!flag[i]) continue;
-    int slot = pt_slot[i];
-    if (slot >= g.max_o) continue;  // deterministic truncation (reference: reservoir)
-    int cell = pt_cell[i];
+    const int slot = pt_slot[i];
+    if (slot >= g.max_o) continue;  // never: the reservoir kept <= max_o voxels
+    const int64_t cell = pt_cell[i];
     int c[3];
-    c[2] = cell % g.dims[2];
-    c[1] = (cell / g.dims[2]) % g.dims[1];
-    c[0] = cell / (g.dims[2] * g.dims[1]);
+    c[2] = (int)(cell % g.dims[2]);
+    c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
+    c[0] = (int)(cell / ((int64_t)g.dims[2] * g.dims[1]));
     coor_2_occ[cell] = slot;
     occ_2_coor[slot * 3 + 0] = c[0];
     occ_2_coor[slot * 3 + 1] = c[1];
@@ -181,38 +256,39 @@ __global__ void __launch_bounds__(kBlock) k_pack_bits(const uint8_t* __restrict_
 
 // fill_occ2pnts (qpiw.py:342-387) part 1: per-voxel counts.  `voxel_idx > 0`
 // (qpiw.py:372) when slot0_drop: the voxel holding slot 0 gets no points.
-__global__ void __launch_bounds__(kBlock) k_count(int64_t n, GridDev g, const int32_t* __restrict__ pt_cell,
+__global__ void __launch_bounds__(kBlock) k_count(int64_t n, GridDev g, const int64_t* __restrict__ pt_cell,
                                                   const int32_t* __restrict__ coor_2_occ,
                                                   int32_t* __restrict__ occ_numpnts) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int cell = pt_cell[i];
+    const int64_t cell = pt_cell[i];
     if (cell < 0) continue;
-    int slot = coor_2_occ[cell];
+    const int slot = coor_2_occ[cell];
     if (slot < 0 || (g.slot0_drop && slot == 0)) continue;
     atomicAdd(occ_numpnts + slot, 1);
   }
 }
 
 // part 2: bucket every point of a kept voxel (arrival order arbitrary).
-__global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, GridDev g, const int32_t* __restrict__ pt_cell,
+__global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, GridDev g, const int64_t* __restrict__ pt_cell,
                                                     const int32_t* __restrict__ coor_2_occ,
                                                     const int32_t* __restrict__ slot_off,
                                                     int32_t* __restrict__ cursor,
                                                     int32_t* __restrict__ bucket) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int cell = pt_cell[i];
+    const int64_t cell = pt_cell[i];
     if (cell < 0) continue;
-    int slot = coor_2_occ[cell];
+    const int slot = coor_2_occ[cell];
     if (slot < 0 || (g.slot0_drop && slot == 0)) continue;
-    int pos = atomicAdd(cursor + slot, 1);
+    const int pos = atomicAdd(cursor + slot, 1);
     bucket[slot_off[slot] + pos] = (int)i;
   }
 }
 
-// part 3: per slot keep the P smallest point ids in ascending order (the
-// serial arrival order), write {xyz, id} records.
+// part 3: per slot write {xyz, id} records of the kept points in ascending id
+// order: all of them (the serial arrival order) when they fit P, else the P of
+// smallest reservoir key (res_pkey; the reference: reservoir with a time seed).
 __global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const float* __restrict__ xyz,
                                                    const int32_t* __restrict__ occ_numpnts,
                                                    const int32_t* __restrict__ slot_off,
@@ -225,7 +301,31 @@ __global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const
     const int off = slot_off[s];
     const int keep = min(cnt, g.P);
     int prev = -1;
-    if (cnt <= 16) {
+    if (cnt > g.P) {
+      // reservoir: threshold = the P-th smallest key of the voxel's points
+      uint64_t thr = 0;
+      bool first = true;
+      for (int q = 0; q < g.P; ++q) {
+        uint64_t best = ~0ull;
+        for (int j = 0; j < cnt; ++j) {
+          const uint64_t k = res_pkey(g.seed, (uint32_t)bucket[off + j]);
+          if ((first || k > thr) && k < best) best = k;
+        }
+        thr = best;
+        first = false;
+      }
+      for (int q = 0; q < keep; ++q) {
+        int best = 0x7fffffff;
+        for (int j = 0; j < cnt; ++j) {
+          const int v = bucket[off + j];
+          if (v > prev && v < best && res_pkey(g.seed, (uint32_t)v) <= thr) best = v;
+        }
+        prev = best;
+        occ_pts[(int64_t)s * g.P + q] =
+            make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
+                        __int_as_float(best));
+      }
+    } else if (cnt <= 16) {
       // the (typical) small voxel: its ids in registers, one round of loads
       int vals[16];
 #pragma unroll
@@ -353,8 +453,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   PNR_CHECK_ARG(p->max_o > 0 && p->P > 0, "grid_build: max_o and P must be > 0");
   PNR_CHECK_ARG(p->vsize[0] > 0 && p->vsize[1] > 0 && p->vsize[2] > 0, "grid_build: vsize <= 0");
   const int64_t gvol = (int64_t)p->dims[0] * p->dims[1] * p->dims[2];
-  PNR_CHECK_ARG(gvol < (int64_t)1 << 31, "grid_build: grid of %lld cells exceeds int32 indexing",
-                (long long)gvol);
+  PNR_CHECK_ARG(gvol < (int64_t)1 << 36, "grid_build: grid of %lld cells", (long long)gvol);
   PNR_HIP(hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
   int rc;
@@ -364,9 +463,10 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
       (rc = h->occ_bits.ensure(words * 4)) || (rc = h->occ_numpnts.ensure(cap_o * 4)) ||
       (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
       (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->slot_cursor.ensure(cap_o * 4)) ||
-      (rc = h->slot_off.ensure((cap_o + 1) * 4)) || (rc = h->pt_cell.ensure(n * 4)) ||
+      (rc = h->slot_off.ensure((cap_o + 1) * 4)) || (rc = h->pt_cell.ensure(n * 8)) ||
       (rc = h->pt_flag.ensure(n * 4)) || (rc = h->pt_slot.ensure((n + 1) * 4)) ||
       (rc = h->bucket.ensure(n * 4)) || (rc = h->counters.ensure(8 * 4)) ||
+      (rc = h->sel.ensure(sizeof(SelState) + 256 * 4)) ||
       (rc = h->scan_tmp.ensure(scan_scratch_bytes(n > cap_o ? (n > words ? n : words) : (cap_o > words ? cap_o : words)))) ||
       (rc = h->q_words.ensure(words * 8)) || (rc = h->q_wcnt.ensure((words + 1) * 4)) ||
       (rc = h->q_rank_slot.ensure(cap_o * 4)) || (rc = h->q_rank_cnt.ensure(cap_o * 4)) ||
@@ -380,7 +480,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   int32_t* occ_2_coor = h->occ_2_coor.as<int32_t>();
   int32_t* slot_cursor = h->slot_cursor.as<int32_t>();
   int32_t* slot_off = h->slot_off.as<int32_t>();
-  int32_t* pt_cell = h->pt_cell.as<int32_t>();
+  int64_t* pt_cell = h->pt_cell.as<int64_t>();
   int32_t* pt_flag = h->pt_flag.as<int32_t>();
   int32_t* pt_slot = h->pt_slot.as<int32_t>();
   int32_t* bucket = h->bucket.as<int32_t>();
@@ -396,6 +496,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   g.max_o = p->max_o;
   g.P = p->P;
   g.slot0_drop = p->slot0_drop;
+  g.seed = p->seed;
 
   PNR_HIP(hipMemsetAsync(first_pt, 0x7f, (size_t)gvol * 4, st));
   PNR_HIP(hipMemsetAsync(coor_2_occ, 0xff, (size_t)gvol * 4, st));
@@ -413,6 +514,24 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p,
                            h->scan_tmp.bytes, st)))
     return rc;
+  if (n > cap_o) {
+    // more points than max_o: the occupied voxels may overflow it (counters[0]
+    // holds their number on the device); keep the reservoir's max_o of them
+    SelState* ss = h->sel.as<SelState>();
+    uint32_t* hist = reinterpret_cast<uint32_t*>(ss + 1);
+    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, counters, (int)cap_o, ss, hist);
+    PNR_LAUNCH_CHECK();
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      hipLaunchKernelGGL(k_sel_hist, dim3(gp), dim3(kBlock), 0, st, n, pt_flag, g.seed, shift, ss, hist);
+      PNR_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(256), 0, st, shift, ss, hist);
+      PNR_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_sel_apply, dim3(gp), dim3(kBlock), 0, st, n, g.seed, ss, pt_flag);
+    PNR_LAUNCH_CHECK();
+    if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 6, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+      return rc;
+  }
   // first_pt is dead after k_first_flags: its storage (4 B/cell) holds the
   // dilated occupancy bytes (32 * words <= 4 * gvol bytes)
   uint8_t* occ_bytes = reinterpret_cast<uint8_t*>(first_pt);

@@ -91,6 +91,24 @@ __device__ __forceinline__ void world_to_pers(const float p[3], const float c[3]
   out[2] = xc[2];
 }
 
+// Seeded reservoir of the grid build (max_o / P overflow, qpiw.py:289-298,
+// 377-384): a uniform random subset chosen by the smallest keys
+// hash32(seed, id) << 32 | id (oracle/query_ref.c states the same keys).
+constexpr uint64_t kPtSalt = 0x632BE59BD9B4E019ull;
+__host__ __device__ inline uint32_t res_hash32(uint64_t seed, uint32_t id) {
+  uint64_t z = seed ^ ((uint64_t)id * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+__host__ __device__ inline uint64_t res_vkey(uint64_t seed, uint32_t id) {
+  return ((uint64_t)res_hash32(seed, id) << 32) | id;
+}
+__host__ __device__ inline uint64_t res_pkey(uint64_t seed, uint32_t id) {
+  return ((uint64_t)res_hash32(seed + kPtSalt, id) << 32) | id;
+}
+
 // Sum over the 64 lanes of a wave.
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll
@@ -138,11 +156,12 @@ struct pnr_handle {
   DevBuf occ_2_coor;      // int32 [max_o*3]
   DevBuf slot_cursor;     // int32 [max_o]
   DevBuf slot_off;        // int32 [max_o+1]
-  DevBuf pt_cell;         // int32 [N]
+  DevBuf pt_cell;         // int64 [N]      cell of every point, -1 outside the grid
   DevBuf pt_flag;         // int32 [N]
   DevBuf pt_slot;         // int32 [N+1]
   DevBuf bucket;          // int32 [N]
   DevBuf counters;        // int32 [8]
+  DevBuf sel;             // voxel reservoir: radix-select state + 256-bin histogram
   DevBuf scan_tmp;
   // Query index (what k_knn reads; the slot tables above stay the reference's
   // view for export / parity): the voxels that hold points, ranked in x-major
@@ -170,7 +189,7 @@ struct pnr_handle {
     stats_pending = false;
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &first_pt, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &slot_cursor, &slot_off, &pt_cell, &pt_flag, &pt_slot, &bucket,
-                     &counters, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
+                     &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
                      &q_rec_off, &q_recs};
     for (DevBuf* b : all) b->release();
   }

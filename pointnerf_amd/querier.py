@@ -8,7 +8,10 @@ so ``NeuralPoints.__init__`` (neural_points.py:330-331) can select it with
   * the voxel grid is persistent: rebuilt only when the point tensor changes
     (the reference rebuilds it for every ray chunk, qpiw.py:626);
   * slot assignment is deterministic (serial order of claim_occ); max_o / P
-    overflow drops instead of reservoir-sampling with a time seed;
+    overflow keeps the same uniform random subsets as the reference's
+    reservoir replacement, drawn from a seeded hash (opt.grid_seed) instead of
+    curand(time()) (qpiw.py:289-298, 377-384); opt.max_o_policy = "grow"
+    raises max_o to the occupied-voxel count instead (SURVEY 8(d) c5);
   * no pycuda context: everything runs on torch's current HIP stream.
 """
 from __future__ import annotations
@@ -142,9 +145,12 @@ class GridHandle:
         xyz = xyz.reshape(-1, 3)
         L.require_gpu(xyz)
         assert xyz.dtype == torch.float32 and xyz.is_contiguous()
+        policy = getattr(opt, "max_o_policy", "reservoir")
+        if policy not in ("reservoir", "grow"):
+            raise L.PnrError(f"max_o_policy {policy!r}: 'reservoir' (the reference's semantics) or 'grow'")
         key = (xyz.data_ptr(), xyz._version, xyz.shape[0], tuple(opt.vsize), tuple(opt.vscale),
                tuple(opt.kernel_size), tuple(opt.query_size), tuple(opt.ranges), opt.max_o, opt.P,
-               int(getattr(opt, "slot0_drop", 1)))
+               int(getattr(opt, "slot0_drop", 1)), int(getattr(opt, "grid_seed", 0)), policy)
         if not force and key == self.key:
             return self.hp
         mn, mx = self.bbox(xyz)
@@ -156,15 +162,28 @@ class GridHandle:
         gp.query_size[:] = [int(x) for x in opt.query_size]
         gp.max_o, gp.P = int(opt.max_o), int(opt.P)
         gp.slot0_drop = int(getattr(opt, "slot0_drop", 1))
+        gp.seed = int(getattr(opt, "grid_seed", 0))
         L.check(L.lib().pnr_grid_build(self.h, L.ptr(xyz), xyz.shape[0], L.ctypes.byref(gp),
                                        L.stream_ptr(xyz.device)), "pnr_grid_build")
+        if policy == "grow" and xyz.shape[0] > gp.max_o:
+            # max_o raised to the occupied voxels (one host read of the count, once per
+            # point-cloud version): no voxel is dropped, the reservoir only acts on P
+            nv = self._stats_raw().n_voxels
+            if nv > gp.max_o:
+                gp.max_o = int(nv)
+                L.check(L.lib().pnr_grid_build(self.h, L.ptr(xyz), xyz.shape[0], L.ctypes.byref(gp),
+                                               L.stream_ptr(xyz.device)), "pnr_grid_build")
         self.key, self.hp = key, hp
-        self._max_o, self._P = int(opt.max_o), int(opt.P)
+        self._max_o, self._P = int(gp.max_o), int(opt.P)
         return hp
 
-    def stats(self):
+    def _stats_raw(self):
         s = L.GridStats()
         L.check(L.lib().pnr_grid_stats_get(self.h, L.ctypes.byref(s)), "pnr_grid_stats_get")
+        return s
+
+    def stats(self):
+        s = self._stats_raw()
         return dict(n_points_in_grid=s.n_points_in_grid, n_voxels=s.n_voxels,
                     n_voxels_kept=s.n_voxels_kept, n_points_dropped=s.n_points_dropped,
                     max_points_per_voxel=s.max_points_per_voxel, dims=list(s.dims))

@@ -128,14 +128,33 @@ SCENE_SHAPES = {
 }
 
 
-def scene_points(name: str, n_points: int, opt, seed: int = 0, cap: int | None = None) -> np.ndarray:
+def scene_points(name: str, n_points: int, opt, seed: int = 0, cap: int | None = None,
+                 scatter: float = 0.0) -> np.ndarray:
     """[n_points, 3] float32 surface samples of SCENE_SHAPES[name] inside opt.ranges,
     with <= cap (default P - 1) points in every voxel of the grid the querier
     builds for them (qpiw.py:48-81: the bbox of the returned points clipped to
     ranges): the six extreme points of the oversampled set are always kept, so
-    the bbox -- hence the grid origin the cap was computed on -- is fixed."""
+    the bbox -- hence the grid origin the cap was computed on -- is fixed.
+    cap < 0: no cap (the cloud may overflow P and max_o: the reference's
+    reservoir case); scatter: that fraction of the points spread uniformly over
+    the ranges (stray MVS points, one per voxel -- what makes a real cloud
+    occupy more voxels than max_o)."""
     from .querier import hyperparameters_from_bbox
     cap = int(opt.P) - 1 if cap is None else int(cap)
+    if cap < 0:
+        rng = np.random.default_rng(seed)
+        lo, hi = np.asarray(opt.ranges[:3], np.float32), np.asarray(opt.ranges[3:], np.float32)
+        n_sc = int(round(n_points * scatter))
+        parts, need = [], n_points - n_sc
+        while need > 0:   # surface samples, rejection-clipped to the ranges
+            m = int(need * 1.1) + 1000
+            p = np.concatenate([f(rng, max(1, int(m * w))) for w, f in SCENE_SHAPES[name]]).astype(np.float32)
+            p = p[np.all((p >= lo) & (p <= hi), axis=1)][:need]
+            parts.append(p)
+            need -= len(p)
+        parts.append((lo + rng.uniform(size=(n_sc, 3)) * (hi - lo)).astype(np.float32))
+        pts = np.concatenate(parts)
+        return pts[rng.permutation(len(pts))]
     for factor in (1.8, 3.0, 5.0, 8.0):   # oversample until the capped set holds n_points
         rng = np.random.default_rng(seed)
         over = int(n_points * factor) + 1000

@@ -22,10 +22,13 @@ def oracle_points(sc):
     return dict(xyz=sc["xyz"], emb=sc["emb"], color=sc["color"], dir=sc["dir"], conf=sc["conf"])
 
 
-def flag_scene(name, n_points=30000, H=48, W=None, view=1, seed=0, default_conf=None, **opt_over):
+def flag_scene(name, n_points=30000, H=48, W=None, view=1, seed=0, default_conf=None, cap=None, scatter=0.0,
+               **opt_over):
     """A seeded scene of one reference flag set (pointnerf_amd.options.FLAGSETS:
     lego / ship / scene101 / truck) at a reduced resolution: the flag set's own
-    camera model (synthetic.SCENE_INTRINSICS, focal scaled to W) and views."""
+    camera model (synthetic.SCENE_INTRINSICS, focal scaled to W) and views.
+    cap / scatter: synthetic.scene_points (cap < 0: an uncapped cloud that may
+    overflow max_o / P)."""
     from pointnerf_amd.options import flagset_opt
     opt = flagset_opt(name, **opt_over)
     W0, H0, f0 = S.SCENE_INTRINSICS[name]
@@ -34,7 +37,7 @@ def flag_scene(name, n_points=30000, H=48, W=None, view=1, seed=0, default_conf=
     if name == "lego":
         pts = S.lego_like_points(n_points, seed=seed)
     else:
-        pts = S.scene_points(name, n_points, opt, seed=seed)
+        pts = S.scene_points(name, n_points, opt, seed=seed, cap=cap, scatter=scatter)
     if default_conf is None and getattr(opt, "default_conf", -1.0) > 0:
         default_conf = opt.default_conf
     emb, color, dirs, conf = S.point_features(n_points, seed=seed, default_conf=default_conf)

@@ -104,3 +104,62 @@ def test_single_point_and_no_hits():
     assert q["sample_pidx"].shape[1:] == (80, 8)
     q2 = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], -sc["raydir"], near=2.0, far=6.0)
     assert q2["sample_pidx"].shape[0] == 0 and q2["ray_mask"].sum() == 0
+
+
+def _hash32(seed, i):
+    """res_hash32 (pnr_common.h / query_ref.c) in Python integers."""
+    m = (1 << 64) - 1
+    z = (seed ^ (i * 0x9E3779B97F4A7C15)) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    z ^= z >> 31
+    return z >> 32
+
+
+def test_overflow_reservoir_keeps_seeded_subsets():
+    """max_o and P overflow (qpiw.py:289-298, 377-384): the reference keeps
+    uniform random subsets by reservoir replacement with a time seed; the
+    oracle (and libpnr) keep the subsets of smallest seeded key -- the max_o
+    voxels of smallest hash32(seed, first point), numbered in first-point
+    order, and per voxel the P points of smallest hash32(seed + salt, id),
+    ascending -- restated here independently."""
+    sc = scene(4000)
+    x = sc["xyz"]
+    sc["xyz"] = np.concatenate([x, x + np.float32(2e-4), x - np.float32(2e-4)]).astype(np.float32)
+    opt = sc["opt"]
+    opt.slot0_drop = 0
+    opt.P = 2
+    base = O.grid_build(opt, sc["xyz"])
+    n_vox = base["n_occ"]
+    opt.max_o = int(n_vox * 0.6)
+    salt = 0x632BE59BD9B4E019
+    kept_sets = []
+    for seed in (0, 7):
+        opt.grid_seed = seed
+        g = O.grid_build(opt, sc["xyz"])
+        assert g["n_occ"] == n_vox
+        hp = g["hp"]
+        c = np.floor((sc["xyz"] - hp["shift"]) / hp["vsize_s"]).astype(np.int64)
+        dims = hp["dims"]
+        flat = (c[:, 0] * dims[1] + c[:, 1]) * dims[2] + c[:, 2]
+        flat[~np.all((c >= 0) & (c < dims), 1)] = -1
+        _, first = np.unique(flat, return_index=True)
+        first = np.sort(first[flat[first] >= 0])
+        assert len(first) == n_vox
+        vkeys = [(_hash32(seed, int(i)) << 32) | int(i) for i in first]
+        thr = sorted(vkeys)[opt.max_o - 1]
+        kept = [int(i) for i, k in zip(first, vkeys) if k <= thr]       # first-point order
+        assert len(kept) == opt.max_o
+        assert np.array_equal(g["coor_2_occ"][flat[kept]], np.arange(opt.max_o))
+        assert int((g["coor_2_occ"] >= 0).sum()) == opt.max_o
+        over = 0
+        for s, f in enumerate(kept[:300]):
+            mem = np.nonzero(flat == flat[f])[0]
+            assert g["occ_numpnts"][s] == len(mem)                 # the reference's counter: all arrivals
+            want = mem if len(mem) <= opt.P else np.sort(
+                sorted(mem, key=lambda i: (_hash32(seed + salt, int(i)) << 32) | int(i))[:opt.P])
+            over += len(mem) > opt.P
+            assert np.array_equal(g["occ_2_pnts"][s][:min(len(mem), opt.P)], want)
+        assert over > 10
+        kept_sets.append(set(kept))
+    assert kept_sets[0] != kept_sets[1]                             # the seed draws the subset

@@ -1,9 +1,29 @@
-# Dev tool: GPU test suite + headline bench on the gpurun box (logs under gpurun_out/$1).
+#!/bin/bash
+# Dev tool: one GPU session on the gpurun box, logs under gpurun_out/$1.
+#   STEPS="tests bench c4 c5 prof"  (any subset, in this order)
+#   TESTS="tests/..."                 pytest selection (default: all -m gpu)
+# Every GPU step has its own time limit; the first failure ends the call.
 export TMPDIR=/tmp
-out=gpurun_out/${1:-run}
-mkdir -p $out
-shift
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $out/t_gpu.log 2>&1 || { tail -30 $out/t_gpu.log; exit 1; }
-tail -3 $out/t_gpu.log
-timeout -k 10 400 python bench.py > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
-cat $out/bench.json
+O=gpurun_out/${1:-run}
+mkdir -p $O
+STEPS=${STEPS:-"tests bench"}
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 900 --timeout-method thread \
+        > $O/t_gpu.log 2>&1 || { tail -40 $O/t_gpu.log; exit 1; }
+      tail -3 $O/t_gpu.log ;;
+    bench)
+      timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+      cut -c1-600 $O/bench.json ;;
+    c4|c5)
+      timeout -k 10 600 python bench.py --config $s --steps 5 --warmup 2 > $O/bench_$s.json 2> $O/bench_$s.err \
+        || { tail -20 $O/bench_$s.err; exit 1; }
+      timeout -k 10 600 python bench.py --config $s --steps 3 --warmup 1 --emulate-world 8 --no-cpu-baseline \
+        > $O/bench_${s}_ew8.json 2> $O/bench_${s}_ew8.err || { tail -20 $O/bench_${s}_ew8.err; exit 1; }
+      cut -c1-400 $O/bench_$s.json ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
+        python bench.py --no-cpu-baseline > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; } ;;
+  esac
+done
