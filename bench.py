@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check); "
                          "default 12000 (headline), 3000 (c4, c5)")
+    ap.add_argument("--pairs-kernel", choices=("wt", "as"), default="wt",
+                    help="fp32h2 pairs stage: k_pairs_h2 (wt) or the activation-stationary k_pairs_as (as)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--train-precision", choices=("fp32x3", "fp32"), default="fp32x3",
@@ -123,6 +125,7 @@ def build_scene(args, device):
     emb, color, dirs, conf = S.point_features(args.points, seed=0, default_conf=opt.default_conf)
     torch.manual_seed(0)
     agg = PointAggregator(opt).to(device).eval()   # random-init weights (xavier, networks.py:163-172)
+    agg.pairs_kernel = args.pairs_kernel
     # bf16 (config c5): the embedding table itself in bf16 (104 B per point)
     emb_dtype = torch.bfloat16 if getattr(args, "dtype", "fp32h2") == "bf16" else torch.float32
     np_ = NeuralPoints(opt, device, torch.from_numpy(pts), emb, color, dirs, conf, emb_dtype=emb_dtype)
@@ -587,6 +590,7 @@ def main():
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "max_o": int(opt.max_o), "grid_rebuild_per_step": bool(args.grid_rebuild),
                        "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
+                       "pairs_kernel": {"wt": "k_pairs_h2", "as": "k_pairs_as"}[args.pairs_kernel],
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else
                                        f"dp{world} ({args.tile_layout} ray shards of every frame, one multi-camera "

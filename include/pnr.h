@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 13
+#define PNR_ABI_VERSION 14
 
 enum {
   PNR_OK = 0,
@@ -352,6 +352,18 @@ typedef struct {
   const void* w1ah;   /* block1.0 columns 0..223 + bias: the per-point half P1 on
                          f16-split MFMA (k_point_pre_h2; NULL: fp32 k_point_pre) */
   float scale1a;
+  /* activation-stationary pairs stage (k_pairs_as; NULL: k_pairs_h2 on w1bh..w4h).
+   * as_pack: 53 k-steps x 24 KB: for each step t, planes (2^11 Wh, Wl, k_L Wh) x 8
+   * neuron tiles x 64 lanes x 8 f16 of split2_f16(2^-s_L W_L[32T + (lane & 31),
+   * col(t, lane >> 5, j)]) for block1.0[:, 224:] (4 steps), block1.2 (16), block3.0
+   * + bias (17), block3.2 (16) -- the input columns in accumulator order
+   * (aggregator.as_columns), k_1 = 1, k_L = 2^(s_{L-1}); s_1..s_3 >= 0.
+   * as_tabs [3][2][128]: b2 / as_scale[1], b4 / as_scale[3], alpha_branch.0 weights,
+   * each for lane half h in accumulator order (row 32T + acc_row(r, h) at T*16 + r).
+   * as_scale: 2^(s_L - 11).  Needs w1ah (P1 is then written / as_scale[0]). */
+  const void* as_pack;
+  const float* as_tabs;
+  float as_scale[4];
 } pnr_mlp_h2;
 int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_h2* wh,
                          float* out_feat, float* out_weight, float* out_conf, void* scratch,

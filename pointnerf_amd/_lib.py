@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 13
+ABI_VERSION = 14
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -111,7 +111,8 @@ class MlpH2(ctypes.Structure):
     _fields_ = ([(n, c_void_p) for n in ("w1bh", "w2h", "w3h", "w4h")] + [("scale", c_float * 4),
                                                                         ("range_flag", c_void_p)] +
                 [(n, c_void_p) for n in ("wc1a", "wc1b", "wc2h", "wc3h")] + [("cscale", c_float * 3)] +
-                [("w1ah", c_void_p), ("scale1a", c_float)])
+                [("w1ah", c_void_p), ("scale1a", c_float)] +
+                [("as_pack", c_void_p), ("as_tabs", c_void_p), ("as_scale", c_float * 4)])
 
 
 class MlpBwd(ctypes.Structure):

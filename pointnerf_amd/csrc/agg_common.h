@@ -160,6 +160,23 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
 // f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
                         hipStream_t st);
+// k_pairs_as (aggregate_as.hip): the activation-stationary fp32h2 pairs stage.
+// pack: 53 k-steps x 24 KB (planes 2^11 Wh, Wl, k Wh of block1.0[:, 224:],
+// block1.2, block3.0 + bias, block3.2, input columns permuted to the
+// accumulator layout); tabs [3][2][128]: b2 / sc2, b4 / sc4, alpha weights in
+// accumulator order; scale: sc1..sc4 (sc = 2^(s - 11), s >= 0 for layers 1-3);
+// p1 = block1.0's point half / sc1.
+struct AsPack {
+  const void* pack;
+  const float* tabs;
+  float scale[4];
+  int32_t* range_flag;
+};
+// k_pair_rec -> k_pairs_as; rec = 4 planes of as_rec_stride(n_max) 16-B pair records
+inline int64_t as_rec_stride(int64_t n_max) { return ((n_max > 0 ? n_max : 1) + 15) / 16 * 16 * 8; }
+int launch_pairs_as(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const AsPack& ap, const float* p1,
+                    float* hid, int32_t* vmask, float* out_feat, float* out_weight, float* out_conf,
+                    int32_t* blk_ctr, uint4* rec, hipStream_t st);
 // k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
 // color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],

@@ -1382,9 +1382,11 @@ static int64_t hid_rows(int64_t n_max) { return cdiv(n_max > 0 ? n_max : 1, 64) 
 
 static size_t scratch_need(int64_t n_max, int64_t n_points) {
   const int64_t nm = hid_rows(n_max);
-  // + 8 ints: the split kernels' tile counters (k_pairs_x3 / k_pairs_h2, one per XCD group)
-  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 8 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
-         sizeof(float);
+  // + 8 ints: the split kernels' tile counters (k_pairs_x3 / k_pairs_h2, one per XCD group), padded to 16 B
+  // + k_pairs_as's pair records (kRecPlanes x as_rec_stride 16-B entries)
+  return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 16 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
+             sizeof(float) +
+         (size_t)4 * as_rec_stride(n_max) * 16;
 }
 
 // scratch = P1 [n_p1, 256] | hid [n_max, 256] | vmask | tile counter: P1 first,
@@ -1399,6 +1401,9 @@ static void carve(AggArgs& a, void* scratch, int64_t n_max, int64_t n_p1) {
 static int32_t* tile_counter(const AggArgs& a, int64_t n_max) {
   const int64_t nm = hid_rows(n_max);
   return a.vmask + cdiv(nm, 4) * 4;
+}
+static uint4* pair_records(const AggArgs& a, int64_t n_max) {
+  return reinterpret_cast<uint4*>(tile_counter(a, n_max) + 16);
 }
 
 int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, float* out_feat,
@@ -1519,6 +1524,23 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
   SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
                {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
                wh->range_flag};
+  if (wh->as_pack) {
+    // k_point_pre_h2 (P1 / sc1) -> k_pairs_as (aggregate_as.hip) -> k_color_h2
+    PNR_CHECK_ARG(wh->w1ah && wh->as_tabs && wh->wc1a, "aggregate_h2: k_pairs_as needs w1ah, as_tabs, colour packs");
+    PNR_CHECK_ARG((((uintptr_t)wh->as_pack | (uintptr_t)wh->as_tabs) & 15) == 0, "aggregate_h2: as packs must be 16-B aligned");
+    for (int i = 0; i < 4; ++i)
+      PNR_CHECK_ARG(wh->as_scale[i] > 0.f && wh->as_scale[i] < 1e30f, "aggregate_h2: bad as_scale %d", i);
+    if (!a.pts.p1_ready &&
+        (rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a / wh->as_scale[0], wh->range_flag, a.p1, st)))
+      return rc;
+    AsPack ap = {wh->as_pack, wh->as_tabs, {wh->as_scale[0], wh->as_scale[1], wh->as_scale[2], wh->as_scale[3]},
+                 wh->range_flag};
+    if ((rc = launch_pairs_as(a.pts, a.s, a.w, ap, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
+                              tile_counter(a, s->n_max), pair_records(a, s->n_max), st)))
+      return rc;
+    const void* cp[4] = {wh->wc1a, wh->wc1b, wh->wc2h, wh->wc3h};
+    return launch_color_h2(a.s, a.w, cp, wh->cscale, wh->range_flag, a.hid, a.vmask, out_feat, st);
+  }
   // k_point_pre_h2 / k_point_pre (P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color_h2 / k_color
   if (wh->w1ah) {
     if (!a.pts.p1_ready && (rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a, wh->range_flag, a.p1, st)))
