@@ -131,7 +131,13 @@ __device__ __forceinline__ int64_t take_block(int32_t* ctr, int64_t nb) {
 // hi = f16(L m), lo = f16(L - hi / m)  (m = sc, nim = -1 / sc): one v_fma_mix each
 // (exact product, one rounding), written as fma + casts so the compiler sees (and
 // interleaves) plain VALU instructions.
-__device__ __forceinline__ float lrelu_s(float x, float s) { return fmaxf(x, x * s); }   // 0 <= s <= 1
+// 0 <= s <= 1: max(x, s x).  v_max_f32 by hand: fmaxf would first quiet x
+// (IEEE mode), one more VALU op per value; x is never a signalling NaN here.
+__device__ __forceinline__ float lrelu_s(float x, float s) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(x * s));
+  return r;
+}
 
 __device__ __forceinline__ void lrelu_mixsplit(float x0, float x1, float s, float m, float nim, unsigned& hi,
                                                unsigned& lo) {
@@ -297,8 +303,10 @@ __global__ void __launch_bounds__(256) k_pair_rec(RecArgs A) {
 struct Rec {
   uint4 a, b, xh, xl;
 };
-__device__ __forceinline__ void rec_load(const AsArgs& A, int64_t wtile, int lane, Rec& r) {
-  const int64_t pr = wtile * kWT + (lane & 31);
+// (a tile past the last block -- the drain tile, or a block index past nblk
+// from take_block -- reads tile 0's records, which rec_take then ignores)
+__device__ __forceinline__ void rec_load(const AsArgs& A, int64_t wtile, int64_t nblk, int lane, Rec& r) {
+  const int64_t pr = (wtile < nblk * 4 ? wtile : 0) * kWT + (lane & 31);
   r.a = A.rec[pr];
   r.b = A.rec[A.rec_stride + pr];
   r.xh = A.rec[2 * A.rec_stride + pr];
@@ -366,18 +374,34 @@ struct Stream {
 // `step` straight into ring slot `slot` (global_load_lds_dwordx4: LDS address
 // = M0 + 16 lane).  Inline asm, so hipcc's vmcnt bookkeeping never waits on it;
 // step_barrier() counts these loads itself.
-__device__ __forceinline__ void stream_dma_one(const Stream& S, int step, int slot, int i) {
-  // the step's base in SGPRs, opaque to hipcc: otherwise it hoists all 318
+// 4 (G 0) or 2 (G 1) of the wave's 6 pieces under one M0: the instruction
+// offset moves the global and the LDS address alike.
+template <int G>
+__device__ __forceinline__ void stream_dma_group(const Stream& S, int step, int slot) {
+  // the step's base in SGPRs, opaque to hipcc: otherwise it hoists all the
   // per-step addresses of a tile out of the loop (and spills them)
-  unsigned off = step * kStepBytes + i * 1024;
+  unsigned off = step * kStepBytes + G * 4096;
   asm volatile("" : "+s"(off));
   const char* base = S.pack + off;
-  const unsigned dst = __builtin_amdgcn_readfirstlane(S.ring + slot * kStepBytes + i * 1024);
+  const unsigned dst = S.ring + slot * kStepBytes + G * 4096;
   unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(S.lane_off), "s"(base), "s"(dst)
-               : "memory");
+  if constexpr (G == 0)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\tglobal_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:2048\n\tglobal_load_lds_dwordx4 %1, %2 offset:3072\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(S.lane_off), "s"(base), "s"(dst)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\tglobal_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(S.lane_off), "s"(base), "s"(dst)
+        : "memory");
 }
 
 constexpr int kFragRegs = 6;    // A fragment registers (24 divides by it: the rotation restarts every step)
@@ -422,7 +446,7 @@ __device__ __forceinline__ void kstep(char* lds, Stream& S, int wid, int lane, f
     constexpr int j = i + kFragDist, r = j % kFragRegs;
     acc[T] = mfma_f16(fr.w[i % kFragRegs], p == 2 ? xl : xh, acc[T]);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (i < 6) stream_dma_one(S, lstep, dslot, i);
+    if constexpr (i < 2) stream_dma_group<i>(S, lstep, dslot);
     work(ii);
     fr.w[r] = j < 24 ? read_plane(lds, slot, j % 8, j / 8, lane) : read_plane(lds, nslot, (j - 24) % 8, (j - 24) / 8, lane);
     __builtin_amdgcn_sched_barrier(0);
@@ -544,11 +568,34 @@ __device__ __forceinline__ void tail_step(const AsArgs& A, const char* lds, f32x
 // ------------------------------------------------------------- PE
 // value e of this lane half (e < 30): channel 3h + e / 10, band (e % 10) / 2,
 // sin (e even) / cos (e odd) -- W1 column 224 + 30h + e (networks.py:175-190 order)
+// sin / cos of |x| <= 3000: Cody-Waite reduction by a 3-part pi/2 (12 + 12 +
+// 24 bits: k C1 and k C2 exact for k < 2^12) and the cephes minimax polynomials
+// on |r| <= pi/4 -- <= 1.6 ulp (9.3e-8 absolute) against the exact values,
+// measured over 2M random arguments per decade up to 3000; larger arguments take
+// sincosf.  A third of sincosf's VALU cost on the MFMA stream.
+__device__ __forceinline__ void sincos_pe(float x, float& sn, float& cs) {
+  if (__builtin_expect(fabsf(x) > 3000.f, 0)) {
+    sincosf(x, &sn, &cs);
+    return;
+  }
+  const float k = rintf(x * 0.636619772367581343f);
+  float r = x - k * 1.5703125f;
+  r = r - k * 4.837512969970703125e-4f;
+  r = r - k * 7.549789954891837e-8f;
+  const float z = r * r;
+  const float s = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+  const float c = 1.f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
+  const int q = (int)k & 3;
+  const float s1 = (q & 1) ? c : s, c1 = (q & 1) ? s : c;
+  sn = (q & 2) ? -s1 : s1;
+  cs = ((q + 1) & 2) ? -c1 : c1;
+}
+
 template <int E2>   // one (sin, cos) pair: values 2 E2, 2 E2 + 1 -> k-step E2 / 4, f16 pair E2 % 4
 __device__ __forceinline__ void pe_pair(const float (&d3)[3], char* pe_lds, int lane) {
   constexpr int ch = (2 * E2) / 10, f = ((2 * E2) % 10) / 2;
   float sn, cs;
-  sincosf(d3[ch] * (float)(1 << f), &sn, &cs);
+  sincos_pe(d3[ch] * (float)(1 << f), sn, cs);
   unsigned hi, lo;
   splith(sn, cs, hi, lo);
   unsigned* d = reinterpret_cast<unsigned*>(pe_lds + ((E2 / 4) * 64 + lane) * 16) + (E2 % 4);
@@ -598,23 +645,24 @@ __global__ void __launch_bounds__(256, 1) k_pairs_as(AsArgs A) {
   for (int i = threadIdx.x; i < 3 * 2 * 128; i += 256) reinterpret_cast<float*>(lds + OffTab)[i] = A.tabs[i];
   int64_t blk = first_block(nblk);
   if (blk >= nblk) return;   // uniform over the workgroup: no barrier reached yet
-  // weight ring prologue: steps 0, 1 in slots 0, 1, step 2 staged
+  // weight ring prologue: steps 0..2 into slots 0..2
   Stream S;
   S.pack = A.pack + __builtin_amdgcn_readfirstlane(wid) * 6 * 1024;
   S.lane_off = lane * 16;
-  S.ring = (unsigned)(uintptr_t)(lds + OffRing) + wid * 6 * 1024;
+  S.ring = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds + OffRing) + wid * 6 * 1024);
   S.g = 0;
 #pragma unroll
-  for (int st = 0; st < 3; ++st)
-#pragma unroll
-    for (int i = 0; i < 6; ++i) stream_dma_one(S, st, st, i);
+  for (int st = 0; st < 3; ++st) {
+    stream_dma_group<0>(S, st, st);
+    stream_dma_group<1>(S, st, st);
+  }
   // first tile: gather, PE, P1
   char* pe_lds = lds + OffPE + wid * (2 * 4 * 64 * 16);
   auto ex_lds = [&](int parity) { return lds + OffEx + (parity * 4 + wid) * (2 * 64 * 16); };
   Next nx;
   {
     Rec r0;
-    rec_load(A, blk * 4 + wid, lane, r0);
+    rec_load(A, blk * 4 + wid, nblk, lane, r0);
     rec_take(r0, blk * 4 + wid, n, lane, nx, ex_lds(0));
   }
   static_for<0, 15>([&](auto e) { pe_pair<decltype(e)::value>(nx.d3, pe_lds, lane); });
@@ -662,7 +710,7 @@ __global__ void __launch_bounds__(256, 1) k_pairs_as(AsArgs A) {
       kstep(lds, S, wid, lane, Y, bh, bl, fr, [&](auto ii) {
         constexpr int i = decltype(ii)::value;
         if constexpr (t + 1 < kL2) conv_piece<i>(X[(t + 1) >> 1], (t + 1) & 1, slope, m1, nim1, cv);
-        if constexpr (i == 12 && t == 7) rec_load(A, nblk_next * 4 + wid, lane, rn);
+        if constexpr (i == 12 && t == 7) rec_load(A, nblk_next * 4 + wid, nblk, lane, rn);
         if constexpr (i == 18 && t == 11) rec_take(rn, nblk_next * 4 + wid, n, lane, nx, ex_lds(par ^ 1));
       });
       if constexpr (t + 1 < kL2) {

@@ -267,3 +267,40 @@ def test_conf_coefficient_and_zero_one_loss(cuda):
     (torch.mean(torch.log(ref_cc.clamp(1e-3, 1 - 1e-3)) + torch.log(1 - ref_cc.clamp(1e-3, 1 - 1e-3))) * 1e-4).backward()
     # point 0 sums the terms of every empty slot (thousands): looser scale term
     close(m.neural_points.points_conf.grad.reshape(-1), conf.grad, "d points_conf (zero_one)", scale=5e-4)
+
+
+@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])
+def test_train_backward_repeatable(cuda, train_precision):
+    """identical training steps give the same gradients.
+    Point-table gradients are float-atomic sums over pairs, so run to run they
+    may differ by summation order only (<= 1e-6 of the largest entry); the MLP
+    weight gradients come from block-ordered GEMMs and the per-pair dX rows are
+    written once, so those are bitwise equal."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.3))
+    m.train_precision = train_precision
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    outs = []
+    for _ in range(4):
+        for p in m.parameters():
+            p.grad = None
+        for p in m.neural_points.parameters():
+            p.grad = None
+        color = m.render_rays_train(cp, cr, rd, 2.0, 6.0, bg)[0]
+        G = torch.randn(color.shape, generator=torch.Generator().manual_seed(5)).to(cuda)
+        (color * G).sum().backward()
+        npt = m.neural_points
+        o = {k: getattr(npt, k).grad.clone() for k in ("points_color", "points_dir", "points_embeding", "points_conf")}
+        o.update({"mlp " + k: p.grad.clone() for k, p in m.aggregator.named_parameters()})
+        outs.append(o)
+    for k in outs[0]:
+        ref = outs[0][k]
+        big = float(ref.abs().max())
+        assert big > 0, k
+        for o in outs[1:]:
+            d = float((o[k] - ref).abs().max())
+            if k.startswith("mlp "):
+                assert d <= 1e-6 * big, (k, d, big)
+            else:
+                assert d <= 1e-6 * big, (k, d, big)
