@@ -327,9 +327,27 @@ def run_train(args, device):
     the first 3 colour channels vs a synthetic target + 1e-4 x the zero_one loss
     on conf_coefficient (ship.sh) -> backward through the HIP kernels -> Adam on
     points_embeding/color/dir/conf and the aggregator."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    reducer = None
+    if world > 1:
+        # data-parallel finetune (SURVEY 8(e)): each rank its own random rays, the
+        # DDP-mean gradients (parallel.GradReducer: one flat MLP all_reduce + the
+        # touched point rows), the same Adam step on every rank
+        import torch.distributed as dist
+        backend = os.environ.get("PNR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     opt, pts, feats, agg, model = build_scene(args, device)
     agg.train()
     model.train_precision = args.train_precision
+    if world > 1:
+        from pointnerf_amd.parallel import GradReducer
+        npt = model.neural_points
+        reducer = GradReducer(list(agg.parameters()),
+                              [npt.points_embeding, npt.points_color, npt.points_dir, npt.points_conf])
     H = W = args.hw
     cams = cameras(8, H, W)
     dev_cams = [tuple(torch.from_numpy(x).to(device) for x in c) for c in cams]
@@ -337,7 +355,7 @@ def run_train(args, device):
     target = torch.rand((H * W, 3), generator=torch.Generator().manual_seed(2)).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
     optim = torch.optim.Adam(params, lr=5e-4, fused=True)
-    gen = torch.Generator(device=device).manual_seed(0)
+    gen = torch.Generator(device=device).manual_seed(rank)
     stats = {"pairs": 0, "valid": 0, "filled": 0}
 
     def step(i, timed):
@@ -349,6 +367,8 @@ def run_train(args, device):
         if "conf_coefficient" in model.last_train_aux:   # ship.sh: zero_one_loss_weights 1e-4
             loss = loss + 1e-4 * model.zero_one_conf_loss()
         loss.backward()
+        if reducer is not None:
+            reducer.reduce(model.last_train_aux["touched_rows"])
         optim.step()
         if timed:
             c = model.last_counts
@@ -359,32 +379,51 @@ def run_train(args, device):
     for i in range(args.warmup):
         step(i, False)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, True)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt)
+        st = torch.tensor([stats["pairs"], stats["valid"], stats["filled"]], dtype=torch.float64, device=device)
+        dist.all_reduce(st)
+        stats = {"pairs": int(st[0]), "valid": int(st[1]), "filled": int(st[2])}
+        if rank != 0:
+            dist.destroy_process_group()
+            return
     k = max(args.steps, 1)
     flops = 3.0 * (stats["pairs"] * FLOP_PER_PAIR + stats["valid"] * FLOP_PER_SAMPLE) / k  # fwd + 2x bwd GEMMs
     ms = t / k * 1e3
     print(json.dumps({
         "metric": "train steps/s (fwd+bwd+Adam, 3600-ray batches), 2M neural points",
-        "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "train_forward": args.train_precision,
         "data": "synthetic (seeded lego-like point cloud, random target colours)",
         "config": {"workload": f"finetune step, {args.train_rays} random rays of {H}x{W} frames, {args.points} points",
                    "K": opt.K, "SR": opt.SR},
-        "ray_samples_per_s_M": round(args.train_rays * opt.SR / (ms * 1e-3) / 1e6, 3),
+        "ray_samples_per_s_M": round(world * args.train_rays * opt.SR / (ms * 1e-3) / 1e6, 3),
+        "parallelism": (f"dp{world}: {args.train_rays} rays per rank per step, DDP-mean gradients "
+                        f"(one flat MLP all_reduce + touched point rows all_gather)" if world > 1 else "single GPU"),
         "gemm_tflops_per_s": round(flops / (ms * 1e-3) / 1e12, 3),
         "counts_per_step": {k2: v // k for k2, v in stats.items()}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
     if args.mode == "train":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        return run_train(args, torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))))
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        return run_train(args, torch.device("cuda", local))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

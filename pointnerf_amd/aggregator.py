@@ -168,7 +168,7 @@ def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Ten
     return F.view(-1)
 
 
-H2_PAD = 8        # >= the weight ring depth of k_pairs_h2 / k_color_h2 (PNR_H2_WD)
+H2_PAD = 8        # >= the weight ring depth of k_pairs_h2 / k_color_h2 (WRing::kWD)
 H2_WMAX = 16.0    # |W 2^-s| < 16, so 2^11 Wh (made in registers) stays inside f16
 
 

@@ -119,11 +119,7 @@ __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, cons
 __device__ __forceinline__ void splith(float a, float b, unsigned& x0, unsigned& x1) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-#if defined(PNR_ABLATE) && (PNR_ABLATE & 1024)   // timing only: flush |x| < 2^-13 (no f16 subnormals)
-  const f2 v = {fabsf(a) < 1.220703125e-4f ? 0.f : a, fabsf(b) < 1.220703125e-4f ? 0.f : b};
-#else
   const f2 v = {a, b};
-#endif
   const h2 hi = __builtin_convertvector(v, h2);
   const f2 r = (v - __builtin_convertvector(hi, f2)) * 2048.f;
   const h2 lo = __builtin_convertvector(r, h2);

@@ -27,9 +27,6 @@
 // software-pipelined a few k-steps ahead.
 #include "agg_common.h"
 
-#ifndef PNR_ABLATE
-#define PNR_ABLATE 0  // dev-only timing ablations (tools/build_ablations.sh)
-#endif
 
 namespace pnr {
 
@@ -75,7 +72,7 @@ __device__ __forceinline__ void bias_rows(float* X, int kin, int lane) {
 template <int NT, int NTOT = NT>
 __device__ __forceinline__ void load_w(float (&a)[NT], const float* __restrict__ p, int t) {
 #pragma unroll
-  for (int T = 0; T < NT; ++T) a[T] = p[(((PNR_ABLATE & 8) ? (t & 3) : t) * NTOT + T) * 64];
+  for (int T = 0; T < NT; ++T) a[T] = p[(t * NTOT + T) * 64];
 }
 
 template <int NT>
@@ -381,10 +378,7 @@ __device__ __forceinline__ void save_pairs_q(const f32x16 (&acc)[PT * NT], float
   }
 }
 
-#ifndef PNR_PAIR_SUB
-#define PNR_PAIR_SUB 1   // tiles per workgroup sharing barriers (and weight-fragment fetches)
-#endif
-constexpr int kPairSub = PNR_PAIR_SUB;
+constexpr int kPairSub = 1;   // tiles per workgroup sharing barriers (and weight-fragment fetches)
 
 template <bool TRAIN>
 __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pairs(AggArgs A) {
@@ -446,7 +440,7 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
     for (int pt = 0; pt < kPTW; ++pt) {
       const int64_t pr_pt = __shfl(prow, 32 * pt + c);
       const bool v_pt = __shfl((int)valid, 32 * pt + c) != 0;
-      if (v_pt && !(PNR_ABLATE & 1)) {
+      if (v_pt) {
         const int64_t p1r = A.pts.used_map ? (int64_t)A.pts.used_map[pr_pt] : pr_pt;
         const float4* pr = reinterpret_cast<const float4*>(A.p1 + p1r * kHid);
 #pragma unroll
@@ -547,7 +541,7 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
     }
     // 5-band PE of the 6-d rotated distance -> rows 2e + {0: sin, 1: cos},
     // e = 5 ch + f (block1.0 columns 224..283); wave w owns e = w (mod 4)
-    if (!(PNR_ABLATE & 2)) {
+    {
 #pragma unroll 1
       for (int e = wid; e < 30; e += kPairWaves) {
         const int ch = e / 5, f = e - 5 * ch;
@@ -607,7 +601,7 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
     mlp_layer_q<kNTW, kPTW>(acc, ring, w4, X, 129, lane);
     prime_q<kNTW>(ring, w1b, lane);                   // the next tile's layer 1
     if (TRAIN) save_pairs_q<kNTW, kPTW>(acc, A.sv.h4, A.sv.mask, 3, tile, n, neg, lane, T0);
-    if (!(PNR_ABLATE & 4)) {
+    {
       // ---------------------------------------------------------- alpha + K sums from registers
       // h4 = lrelu(acc) never goes to LDS.  alpha: each lane dots its 32 rows of
       // the wave's 64 neurons with W_a, the two lane halves and the 4 waves are
@@ -934,7 +928,7 @@ __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsign
       const unsigned b = mk[pt * NT + T];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = act ? (((b >> r) & 1u) ? v[r] : v[r] * slope) : 0.f;
-      if (act && !(PNR_ABLATE & 131072)) {   // (131072: timing only, no dz stores)
+      if (act) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<float4*>(dst + pair * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
@@ -950,9 +944,6 @@ __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsign
 // planes in registers (split2, exact), six cross products per 16-k step on
 // v_mfma_f32_32x32x16_bf16 (smallest first) -- the arithmetic of the fp32x3
 // forward (aggregate_x3.hip) on k_pairs_bwd's LDS layout.
-#ifndef PNR_BWD_BPREF
-#define PNR_BWD_BPREF 0   // B fragments of the next step split ahead (more VGPRs)
-#endif
 constexpr int kX3D = 3;   // weight ring depth (k-steps in flight) <= X3_PAD
 struct X3QRing {
   uint4 a[kX3D][2][3];
@@ -1000,24 +991,16 @@ __device__ __forceinline__ void x3q_b(const float* X, int t, int pt, int lane, u
 // live through the whole tile made the kernel spill)
 __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_rsrc_t rs, int voff,
                                               const float* X, int nsteps, int lane) {
-  if (PNR_ABLATE & 262144) return;   // timing only: no dX GEMMs
   X3QRing w;
   x3q_prime(w, rs, voff);
   uint4 b[2][3];
   x3q_b(X, 0, 0, lane, b[0]);
   x3q_b(X, 0, 1, lane, b[1]);
   auto step = [&](uint4 (&a)[2][3], int t) {
-#if PNR_BWD_BPREF
-    uint4 bn[2][3];
-    const int tn = t + 1 < nsteps ? t + 1 : t;
-    x3q_b(X, tn, 0, lane, bn[0]);
-    x3q_b(X, tn, 1, lane, bn[1]);
-#else
     if (t > 0) {
       x3q_b(X, t, 0, lane, b[0]);
       x3q_b(X, t, 1, lane, b[1]);
     }
-#endif
     // products smallest first (W2.X0, W1.X1, W0.X2, W1.X0, W0.X1, W0.X0), each
     // over the four accumulators in turn: four independent MFMA chains
     constexpr int kPa[6] = {2, 1, 0, 1, 0, 0}, kPb[6] = {0, 1, 2, 0, 1, 0};
@@ -1028,12 +1011,6 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_
 #pragma unroll
         for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_bf16(a[T][kPa[p]], b[pt][kPb[p]], acc[2 * pt + T]);
     x3q_load(a, rs, voff, t + kX3D);   // packs carry kX3D zero steps
-#if PNR_BWD_BPREF
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) b[pt][pl] = bn[pt][pl];
-#endif
   };
   int t = 0;
 #pragma unroll 1
@@ -1231,7 +1208,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // atomic wave instructions (wave w: pairs 16w..16w+15, lane = neuron).
     // d_p1 == NULL: the caller reduces dz1 per point instead (pnr_pairs_to_points).
     __syncthreads();                 // every wave is done reading X (W2^T GEMM)
-    if (A.d_p1 == nullptr || (PNR_ABLATE & 65536)) continue;   // (65536: timing only)
+    if (A.d_p1 == nullptr) continue;
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     __syncthreads();
     for (int i = 0; i < kTP / kPairWaves; ++i) {

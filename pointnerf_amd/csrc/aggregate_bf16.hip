@@ -20,9 +20,6 @@
 // MFMAs.  ~78 KB of LDS per workgroup -> 2 per CU (2 waves per SIMD).
 #include "agg_common.h"
 
-#ifndef PNR_ABLATE
-#define PNR_ABLATE 0  // dev-only timing ablations (tools/build_ablations.sh)
-#endif
 
 namespace pnr {
 
@@ -89,7 +86,7 @@ __device__ __forceinline__ void mlp_layer_b(f32x16 (&acc)[PT * NT], const uint4*
 #pragma unroll
     for (int T = 0; T < NT; ++T) {
       a0[T] = a1[T];
-      a1[T] = p[((((PNR_ABLATE & 8) ? 0 : t) + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
+      a1[T] = p[((t + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
     }
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) x[pt] = y[pt];
@@ -328,7 +325,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       // 5-band PE of the rotated distance -> rows 2e, 2e+1 (e = 5 ch + f); role r: e = r (mod 2)
       uint16_t* xc = Xb + col * kPB;
 #pragma unroll 1
-      for (int e = role; e < ((PNR_ABLATE & 2) ? 0 : 30); e += 2) {
+      for (int e = role; e < 30; e += 2) {
         const int ch = e / 5, f = e - 5 * ch;
         float dc = dr6[0];
         dc = ch == 1 ? dr6[1] : dc;
@@ -350,7 +347,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       const int64_t p1r = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        if (p1r >= 0 && !(PNR_ABLATE & 1)) {
+        if (p1r >= 0) {
           const uint4* src = reinterpret_cast<const uint4*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 16 * h);
           const uint4 u0 = src[0], u1 = src[1];
           const unsigned w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
@@ -406,7 +403,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     mlp_layer_b<2, kBPT, 8, kPB>(acc, w4, Xb, 17, lane);
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
-    if (!(PNR_ABLATE & 4)) {
+    {
     float pa_part[kBPT] = {0.f, 0.f, 0.f, 0.f};
     const int i8 = c & 7;
     const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;

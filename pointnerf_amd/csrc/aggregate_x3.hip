@@ -28,9 +28,6 @@
 // extras / weights / point rows / sample flags.
 #include "agg_common.h"
 
-#ifndef PNR_ABLATE
-#define PNR_ABLATE 0  // dev-only timing ablations (tools/build_ablations.sh)
-#endif
 
 namespace pnr {
 namespace {
@@ -75,28 +72,7 @@ struct XL {
   static_assert(Lds <= 160 * 1024, "LDS budget");
 };
 
-#ifndef PNR_X3_PRIO
-#define PNR_X3_PRIO 3   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
-#endif
-#ifndef PNR_CONS_PRIO
-#define PNR_CONS_PRIO 0
-#endif
-#ifndef PNR_TRACE
-#define PNR_TRACE 0   // dev-only: per-phase s_memtime stamps of block 0 (pnr_debug_x3_trace)
-#endif
-#if PNR_TRACE
-__device__ unsigned long long g_x3_trace[2][64][16];
-__device__ unsigned long long g_x3_blk[1024][2];   // per block: loop start, loop end (consumer wave 0)
-#define X3_TR(role, ev)                                                        \
-  do {                                                                         \
-    if (blockIdx.x == 0 && (threadIdx.x & 255) == 0 && it < 64)                \
-      g_x3_trace[role][it][ev] = clock64();                                    \
-  } while (0)
-#else
-#define X3_TR(role, ev) \
-  do {                  \
-  } while (0)
-#endif
+constexpr int kProducerPrio = 3;   // producer wave priority (s_setprio): measured 0: 110.6, 2: 110.1, 3: 109.6 ms
 
 typedef float f32x2n __attribute__((ext_vector_type(2)));
 typedef float f32x4n __attribute__((ext_vector_type(4)));
@@ -127,10 +103,7 @@ struct X3Args {
 // through its own contiguous eighth of the tiles with its own counter and then
 // helps the other groups.  Neighbouring tiles (the same or adjacent rays) share
 // most of their points, so their P1 rows are re-read from that XCD's L2.
-#ifndef PNR_XCD_TILES
-#define PNR_XCD_TILES 1
-#endif
-__device__ __forceinline__ bool xcd_mode(int64_t nt) { return PNR_XCD_TILES && nt >= 2 * (int64_t)gridDim.x + 16; }
+__device__ __forceinline__ bool xcd_mode(int64_t nt) { return nt >= 2 * (int64_t)gridDim.x + 16; }
 __device__ __forceinline__ int64_t xcd_lo(int64_t nt, int x) { return nt * x / 8; }
 __device__ __forceinline__ int64_t xcd_nb(int x) { return ((int)gridDim.x - x + 7) / 8; }   // blocks of group x
 
@@ -164,20 +137,14 @@ __device__ __forceinline__ void load_w(uint4 (&a)[2][XL<H>::NPW], __amdgpu_buffe
     for (int pl = 0; pl < NPW; ++pl)
       a[T][pl] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (t & 1) : t) * NTK + T) * NPW * 1024, 0));
+                     rs, voff + pl * 1024, (t * NTK + T) * NPW * 1024, 0));
 }
 
-#ifndef PNR_H2_BD
-#define PNR_H2_BD 2   // h2: B fragments (LDS) read this many k-steps ahead
-#endif
 // weight ring depth (k-steps in flight); the packs carry >= kWD zero steps
 // (X3_PAD / H2_PAD in aggregator.py)
-#ifndef PNR_H2_WD
-#define PNR_H2_WD 3
-#endif
 template <bool H>
 struct WRing {
-  static constexpr int kWD = H ? PNR_H2_WD : 3;
+  static constexpr int kWD = 3;
   uint4 a[kWD][2][XL<H>::NPW];
 };
 
@@ -203,7 +170,7 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
       bb[pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * t * kXT + 32 * pt) * 16);
   };
   // B fragments BD steps ahead (slot = step mod BD)
-  constexpr int BD = H ? PNR_H2_BD : 1;
+  constexpr int BD = H ? 2 : 1;   // h2: B fragments (LDS) read two k-steps ahead
   uint4 b[BD][2][NPL];
 #pragma unroll
   for (int sl = 0; sl < BD; ++sl) {
@@ -230,18 +197,17 @@ __device__ __forceinline__ void layer(f32x16 (&acc)[4], WRing<H>& w, __amdgpu_bu
     for (int T = 0; T < 2; ++T)
       a[T][pl] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                     rs, voff + pl * 1024, (((PNR_ABLATE & 8) ? (tw & 1) : tw) * NTK + T) * NPW * 1024, 0));
+                     rs, voff + pl * 1024, (tw * NTK + T) * NPW * 1024, 0));
   };
   auto bl = [&](int bs, int tn, int pt, int pl) {
-    if (!(PNR_ABLATE & 64))   // (64: timing only, B fixed)
-      b[bs][pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
+    b[bs][pt][pl] = *reinterpret_cast<const uint4*>(base + pl * pstride + (2 * tn * kXT + 32 * pt) * 16);
   };
   // h2 step per half: Ws.Xh, Wl.Xh, Wh.Xl (Ws = 2^11 Wh, made in registers)
   // Ws = 2^11 Wh of the NEXT step is made in the middle of this one (scl), so
   // the v_pk_mul_f16 results are never waited on by the MFMA right after them.
   uint4 scl[2];
   auto scale_next = [&](const uint4 (&an)[2][NPW], int T) {   // one tile per MFMA gap (4 v_pk_mul_f16)
-    scl[T] = (PNR_ABLATE & 512) ? an[T][0] : f16x8_scale2048(an[T][0]);   // (512: timing only)
+    scl[T] = f16x8_scale2048(an[T][0]);
   };
   if constexpr (H) {
     scale_next(w.a[0], 0);
@@ -339,7 +305,6 @@ template <bool H>
 __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, float s, float mul, int lane,
                                           int T0, int pstride = kPlaneX) {
   const int c = lane & 31, h = lane >> 5;
-  if (PNR_ABLATE & 8192) return;   // timing only: no activation stores (stale planes)
   if constexpr (H) {
     const float k = 2048.f * mul, ks = k * s;   // exact: mul is a power of two
 #pragma unroll
@@ -355,20 +320,6 @@ __device__ __forceinline__ void store_act(const f32x16 (&acc)[4], char* planes, 
           char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
           *reinterpret_cast<uint2*>(d) = make_uint2(a0, b0);
           *reinterpret_cast<uint2*>(d + pstride) = make_uint2(a1, b1);
-        }
-    return;
-  }
-  if (PNR_ABLATE & 128) {   // timing only: no split (hi plane = bf16(x), other planes untouched)
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-      for (int T = 0; T < 2; ++T)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x16& v = acc[2 * pt + T];
-          char* d = planes + ((4 * (T0 + T) + q) * kXT + 32 * pt + c) * 16 + 8 * h;
-          *reinterpret_cast<uint2*>(d) = make_uint2(cvt_bf16x2(lrelu(v[4 * q], s), lrelu(v[4 * q + 1], s)),
-                                                    cvt_bf16x2(lrelu(v[4 * q + 2], s), lrelu(v[4 * q + 3], s)));
         }
     return;
   }
@@ -507,13 +458,7 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
   }
   float pw3[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, col[3] = {0.f, 0.f, 0.f}, pdir[3] = {0.f, 0.f, 0.f};
   float cf = 1.f;
-  if (valid && (PNR_ABLATE & 4096)) {   // timing only: no point-table loads
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      pw3[a] = sw[a] + 0.01f * (a + 1);
-      pp[a] = sp[a] + 0.01f;
-    }
-  } else if (valid) {
+  if (valid) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       pw3[a] = A.pts.xyz[prow * 3 + a];
@@ -611,7 +556,6 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
     for (int pl = 0; pl < L::NPL; ++pl) *reinterpret_cast<uint2*>(pz + pl * kPlaneP) = make_uint2(0u, 0u);
     if (TR && pe5) *reinterpret_cast<float4*>(pe5 + 60) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (PNR_ABLATE & 2) return;
   const int mine = __builtin_amdgcn_readfirstlane(PART == 0 ? pw : 4 + pw);
 #pragma unroll
   for (int ch = 4 * PART; ch < (PART == 0 ? 4 : 6); ++ch) {
@@ -652,7 +596,6 @@ __device__ __forceinline__ void pe_planes(char* lds, int pw, int lane, const flo
 template <bool H, bool TR = false>
 __device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int buf, int64_t tile, int lane) {
   using L = XL<H>;
-  if (PNR_ABLATE & 4) return;
   const int64_t n = eff_n(A.s);
   const int j = lane >> 3, k = lane & 7;
   const float* apart = reinterpret_cast<const float*>(lds + L::OffAp);
@@ -714,29 +657,20 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                                r4 = rsrc(A.wx.pack[3]);
   // layer output factors (h2: 2^(s-11) of the pre-scaled f16 packs; x3: 1, unused)
   const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
-#if PNR_CONS_PRIO
-  __builtin_amdgcn_s_setprio(PNR_CONS_PRIO);   // consumer (MFMA) issue priority
-#endif
   WRing<H> wr;
   f32x16 acc[4];
   prime<H>(wr, r1, voff);
   X3_SYNC();   // S0: the first tile's PE planes, extras and weights are in LDS
-#if PNR_TRACE
-  if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][0] = wall_clock64();
-#endif
   const int* TQ = reinterpret_cast<const int*>(lds + L::OffTq);
   int it = 0;
   for (int64_t tile = first_tile(ntiles); tile < ntiles; tile = TQ[(it + 1) & 3], ++it) {
     const int buf = it & 1;
-    X3_TR(0, 0);
     // ------------------------------------------------------------ block1.0 = P1 + W1[:, 224:] . PE_5
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
     layer<H>(acc, wr, r1, voff, PE, kPlaneP, 4, lane);
     prime<H>(wr, r2, voff);
-    X3_TR(0, 1);
     X3_SYNC();   // S1: P1 parked, PE planes consumed
-    X3_TR(0, 2);
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
@@ -758,10 +692,8 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
           }
         }
     X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
-    X3_TR(0, 3);
     store_act<H>(acc, XP, neg, 1.f, lane, T0);
     if constexpr (TR) save_act_train(A, acc, A.sv.h1, 0, tile, n, neg, lane, T0);
-    X3_TR(0, 15);   // (store_act alone, tools/x3_trace.py)
     if (wid == 0) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
@@ -771,15 +703,11 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
       }
     }
     acc_init<H>(acc, A.w.b2, 1.f / sc2, lane, T0);
-    X3_TR(0, 4);
     X3_SYNC();   // S2
-    X3_TR(0, 5);
     // ------------------------------------------------------------ block1.2
     layer<H>(acc, wr, r2, voff, XP, kPlaneX, kBiasSteps(H), lane);
     prime<H>(wr, r3, voff);
-    X3_TR(0, 6);
     X3_SYNC();   // S3
-    X3_TR(0, 7);
     store_act<H>(acc, XP, neg, sc2, lane, T0);
     if constexpr (TR) save_act_train(A, acc, A.sv.h2, 1, tile, n, neg, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
@@ -792,13 +720,10 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
     X3_SYNC();   // S4
-    X3_TR(0, 8);
     // ------------------------------------------------------------ block3.0
     layer<H>(acc, wr, r3, voff, XP, kPlaneX, 17, lane);
     prime<H>(wr, r4, voff);
-    X3_TR(0, 9);
     X3_SYNC();   // S5
-    X3_TR(0, 10);
     store_act<H>(acc, XP, neg, sc3, lane, T0);
     if constexpr (TR) save_act_train(A, acc, A.sv.h3, 2, tile, n, neg, lane, T0);
     if (wid == 0 && !H) {
@@ -809,11 +734,9 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     }
     acc_init<H>(acc, A.w.b4, 1.f / sc4, lane, T0);
     X3_SYNC();   // S6
-    X3_TR(0, 11);
     // ------------------------------------------------------------ block3.2, alpha partials, K sums
     layer<H>(acc, wr, r4, voff, XP, kPlaneX, kBiasSteps(H), lane);
     prime<H>(wr, r1, voff);   // the next tile's block1.0
-    X3_TR(0, 12);
     if constexpr (H) {
       // block3.2 accumulators -> LDS [pair][row] for the producers' tail (next tile):
       // one ds_write_b128 per accumulator quad, conflict-free at kP1Pitch
@@ -828,7 +751,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
             *reinterpret_cast<float4*>(H4 + (32 * pt + c) * kP1Pitch + 32 * (T0 + T) + 8 * q + 4 * h) =
                 make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
           }
-    } else if (!(PNR_ABLATE & 4)) {
+    } else {
       if constexpr (TR) save_act_train(A, acc, A.sv.h4, 3, tile, n, neg, lane, T0);
       const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + buf * kXT;
       const int* sflag = reinterpret_cast<const int*>(lds + L::OffSf) + buf * kXTS;
@@ -885,13 +808,8 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         apart[wid * kXT + 32 + c] = pa_part[1];
       }
     }
-    X3_TR(0, 13);
     X3_SYNC();   // S7: layer-input planes free (the producers park the next P1 there), alpha partials ready
-    X3_TR(0, 14);
   }
-#if PNR_TRACE
-  if (threadIdx.x == 0 && blockIdx.x < 1024) g_x3_blk[blockIdx.x][1] = wall_clock64();
-#endif
 }
 
 // Producer wave pw: P1 rows 16 pw .. 16 pw + 15 of a tile (1 KB each, one
@@ -911,7 +829,7 @@ __device__ __forceinline__ unsigned fetch_p1(f32x4n (&r)[16], const X3Args& A, c
   for (int i = 0; i < 16; ++i) {
     r[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4n*>(A.p1 + (rows[i] < 0 ? 0 : rows[i]) * kHid) +
                                       lane);
-    if (rows[i] < 0 || (PNR_ABLATE & 1)) empty |= 1u << i;
+    if (rows[i] < 0) empty |= 1u << i;
   }
   return empty;
 }
@@ -945,7 +863,6 @@ template <int PART>
 __device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int slot, int64_t tile, int pw, int lane,
                                               TailState& ts, float& chk) {
   using L = XL<true>;
-  if (PNR_ABLATE & 4) return;
   const int64_t n = eff_n(A.s);
   const int j = 2 * pw + (lane >> 5), ng = lane & 31;
   const float* H4 = reinterpret_cast<const float*>(lds + L::OffH4);
@@ -1016,9 +933,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   using L = XL<H>;
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kXTS);
-#if PNR_X3_PRIO
-  __builtin_amdgcn_s_setprio(PNR_X3_PRIO);   // producer issue priority over the MFMA stream
-#endif
+  __builtin_amdgcn_s_setprio(kProducerPrio);   // producer issue priority over the MFMA stream
   f32x4n p1r[16];
   unsigned p1e = 0;
   float dr6[6];
@@ -1044,38 +959,31 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // the tile after next, published before S1 (only while this workgroup goes on:
     // a tile taken by a workgroup that stops would be lost)
     if (pw == 0 && lane == 0) TQ[(it + 2) & 3] = next < ntiles ? (int)take_tile(A, ntiles) : (int)ntiles;
-    X3_TR(1, 0);
     park_p1(p1r, p1e, lds, pw, lane);   // the layer-input planes are free since the last S7
     gather_row(A, next, lane, g);
-    X3_TR(1, 1);
     X3_SYNC();   // S1
     // alpha of the previous tile (its partials stay until this tile's K sums, after S6)
     if (!H && pw == 0 && it > 0) finalize_alpha<H, TR>(A, lds, nbuf, prev, lane);
     X3_SYNC();   // S1b
     gather_sample(A, lane, g);
     X3_SYNC();   // S2
-    X3_TR(1, 2);
     // during block1.2: gather of the next tile (its slots are free: their last
     // readers were the previous finalize / tail)
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) gather<H, TR>(A, g, nbuf, nw, lds, pw, lane, dr6);
+    gather<H, TR>(A, g, nbuf, nw, lds, pw, lane, dr6);
     if constexpr (H)   // first half of the previous tile's tail
       if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
-    X3_TR(1, 3);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1))
-      p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
-    X3_TR(1, 4);
+    p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
     X3_SYNC();   // S4
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 0, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.0 (PE planes free since S1)
+    pe_planes<H, 0, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.0 (PE planes free since S1)
     // (h2) during block3.0: the second half of the previous tile's tail (its
     // accumulators are overwritten after this tile's S6)
     if constexpr (H)
       if (it > 0) producer_tail<1>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
     X3_SYNC();   // S5
-    X3_TR(1, 5);
     X3_SYNC();   // S6
-    if (!(PNR_ABLATE & 256) && !((PNR_ABLATE & 2048) && it > 1)) pe_planes<H, 1, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.2
+    pe_planes<H, 1, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.2
     X3_SYNC();   // S7
   }
   if constexpr (H) {
@@ -1141,7 +1049,6 @@ struct ColH2Args {
 // (k_pairs_h2 stored the planes).  Wave w copies plane w.
 template <int G0, int NG>
 __device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, int64_t tile) {
-  if (PNR_ABLATE & 16384) return;   // timing only: no hid loads (stale planes)
   const int lane = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const char* src = reinterpret_cast<const char*>(A.hid) + tile * kHidTile + lane * 16;
 #pragma unroll
@@ -1248,7 +1155,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int64_t v = v0 + 32 * pt + c;
-      if (!((vm >> (32 * pt + c)) & 1) || (PNR_ABLATE & 32768)) continue;   // (32768: timing only, no stores)
+      if (!((vm >> (32 * pt + c)) & 1)) continue;
       float* o = A.out_feat + v * (kC + 1) + 1;
 #pragma unroll
       for (int T = 0; T < 2; ++T)
@@ -1398,21 +1305,6 @@ int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pa
   return PNR_OK;
 }
 
-#if PNR_TRACE
-extern "C" __attribute__((visibility("default"))) int pnr_debug_x3_trace(unsigned long long* out, int n) {
-  const size_t want = sizeof(g_x3_trace);
-  if (!out || (size_t)n * sizeof(unsigned long long) < want) return PNR_EINVAL;
-  PNR_HIP(hipDeviceSynchronize());
-  PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_trace), want));
-  return PNR_OK;
-}
-extern "C" __attribute__((visibility("default"))) int pnr_debug_x3_blocks(unsigned long long* out, int n) {
-  if (!out || (size_t)n * sizeof(unsigned long long) < sizeof(g_x3_blk)) return PNR_EINVAL;
-  PNR_HIP(hipDeviceSynchronize());
-  PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_blk), sizeof(g_x3_blk)));
-  return PNR_OK;
-}
-#endif
 
 template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,

@@ -19,26 +19,13 @@
 namespace pnr {
 
 constexpr int kQBlock = 256;
-#ifndef PNR_KNN_WAVES
-#define PNR_KNN_WAVES 8   // k_knn is load-latency bound: registers capped for 8 waves per SIMD (A/B: 0 -> 2.73 ms, 8 -> 2.33 ms query)
-#endif
-#ifndef PNR_KNN_BATCH
-#define PNR_KNN_BATCH 1   // candidate records fetched together (A/B, with the up-front lookups: 1 -> 2.12, 2 -> 2.15 ms query)
-#endif
-#ifndef PNR_KNN_BATCH_SMALL
-#define PNR_KNN_BATCH_SMALL 2   // small launches (a few waves per CU: latency, not occupancy, bound)
-#endif
-#ifndef PNR_KNN_XCD
-#define PNR_KNN_XCD 2   // 0: grid-stride; 1: static XCD ranges; 2: per-XCD counters + stealing
-#endif
-#ifndef PNR_KNN_GRID
-#define PNR_KNN_GRID 2048   // blocks: one full-occupancy wave of the chip (8 per CU)
-#endif
-#if PNR_KNN_WAVES
-#define PNR_KNN_ATTR __attribute__((amdgpu_waves_per_eu(PNR_KNN_WAVES)))
-#else
-#define PNR_KNN_ATTR
-#endif
+// k_knn is load-latency bound: registers capped for 8 waves per SIMD (A/B: no cap
+// 2.73 ms -> 8 waves 2.33 ms query); candidate records fetched one at a time
+// (A/B with the up-front lookups: 1 -> 2.12, 2 -> 2.15 ms), two for small launches
+// (a few waves per CU: latency, not occupancy, bound); one full-occupancy wave
+// of the chip (8 blocks per CU) walks the chunks.
+constexpr int kKnnBatch = 1, kKnnBatchSmall = 2;
+constexpr unsigned kKnnGrid = 2048;
 
 struct QGrid {
   float shift[3], vs[3];
@@ -211,7 +198,7 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
   }
 }
 
-// All records of one record range, in order, PNR_KNN_BATCH loads in flight.
+// All records of one record range, in order, KB loads in flight.
 template <int KMAX, int KB>
 __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
                                          float buf[KMAX], int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
@@ -362,7 +349,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 // LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
 // layered loop inlined beside it costs registers); 0: any layer count.
 template <int KMAX, int LAYERS, int KB>
-__global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
+__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8))) k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
@@ -386,15 +373,15 @@ __global__ void __launch_bounds__(kQBlock) PNR_KNN_ATTR k_knn(QRays q, QGrid g, 
   // XCD): XCD x walks the contiguous chunk range [C x / 8, C (x + 1) / 8) of the
   // sample list, so at any moment its L2 holds the records of a few image rows
   // instead of every XCD touching the same wide window (A/B in DESIGN.md 13).
-  // PNR_KNN_XCD 2: chunks handed out in order by a per-XCD counter, and an XCD
+  // Chunks are handed out in order by a per-XCD counter, and an XCD
   // whose range is exhausted takes chunks from the next XCDs' ranges (the
   // bands' per-sample costs differ, so static ranges finish unevenly).  Small
   // launches (a training batch's few hundred chunks) walk the plain grid
   // stride: there the counters' contention costs more than the locality gains.
   const int64_t C = (S + kQBlock - 1) / kQBlock;
   const bool whole = (gridDim.x & 7) == 0;
-  const bool dyn = PNR_KNN_XCD == 2 && whole && C >= 4 * (int64_t)gridDim.x;
-  const bool xcd = dyn || (PNR_KNN_XCD == 1 && whole);
+  const bool dyn = whole && C >= 4 * (int64_t)gridDim.x;
+  const bool xcd = dyn;
   const int xg = xcd ? (int)(blockIdx.x & 7) : 0;
   const int64_t c_lo = xcd ? C * xg / 8 : 0, c_hi = xcd ? C * (xg + 1) / 8 : C;
   const int64_t c_step = xcd ? gridDim.x / 8 : gridDim.x;
@@ -625,19 +612,19 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   const bool small = RS < (int64_t(4) << 20);
   // the 3x3x3 kernel indexes cells in 32 bits
   const bool q3 = layers == 2 && (int64_t)g.dims[0] * g.dims[1] * g.dims[2] < (int64_t(1) << 32);
-  unsigned gk = grid_for(RS, kQBlock, PNR_KNN_GRID);
+  unsigned gk = grid_for(RS, kQBlock, kKnnGrid);
   if (gk >= 8) gk &= ~7u;   // whole XCD groups (k_knn's chunk walk)
   // k_knn's per-XCD chunk counters: the head of the scan scratch, free between
   // the fill-list and valid-list scans (stream order)
-  if (PNR_KNN_XCD == 2) PNR_HIP(hipMemsetAsync(b->scratch, 0, 8 * sizeof(int32_t), st));
+  PNR_HIP(hipMemsetAsync(b->scratch, 0, 8 * sizeof(int32_t), st));
   const int vec = ((uintptr_t)b->pidx & 15) == 0;
   QIndex qi;
   qi.words = h->q_words.as<uint2>();
   qi.rec_off = h->q_rec_off.as<int32_t>();
   qi.recs = h->q_recs.as<float4>();
 #define PNR_KNN(KM)                                                                              \
-  hipLaunchKernelGGL((q3 ? (small ? k_knn<KM, 2, PNR_KNN_BATCH_SMALL> : k_knn<KM, 2, PNR_KNN_BATCH>)           \
-                          : k_knn<KM, 0, PNR_KNN_BATCH_SMALL>), dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
+  hipLaunchKernelGGL((q3 ? (small ? k_knn<KM, 2, kKnnBatchSmall> : k_knn<KM, 2, kKnnBatch>)           \
+                          : k_knn<KM, 0, kKnnBatchSmall>), dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
                      qp->radius_limit2, qi, b->slot_d, b->fill_rs, b->pidx, b->vflag,             \
                      b->ray_vcnt, b->sample_w, b->sample_p, b->counts, vec,                       \
                      reinterpret_cast<int32_t*>(b->scratch))

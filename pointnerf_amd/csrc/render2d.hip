@@ -41,12 +41,7 @@ constexpr int kROut = 1;
 // (2.53), 7 = all three (1.71).  Staging the weight fragments in LDS per 8
 // k-steps for the 4 waves (double-buffered) measured 3.19 ms: the extra barriers
 // cost more than the L2 fetch they save; not kept.
-#ifndef PNR_CONV_RW
-#define PNR_CONV_RW 6   // weight-fragment prefetch depth in k-steps (12 / 18: same 2.94 ms)
-#endif
-#ifndef PNR_CONV_ABL
-#define PNR_CONV_ABL 0
-#endif
+constexpr int kConvRW = 6;   // weight-fragment prefetch depth in k-steps (12 / 18: same 2.94 ms)
 constexpr int kRRows = kROut + 2;      // staged input rows
 constexpr size_t kRLds = (size_t)kRRows * kRRowPx * kRPitch * sizeof(float);
 
@@ -90,7 +85,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       for (int T = 0; T < NT; ++T) acc[o][T] = (f32x16r){0.f};
     for (int ci0 = 0; ci0 < a.Cin; ci0 += kRCh) {
       // stage rows y0-1 .. y0+kROut, pixels x0-1 .. x0+128, channels ci0 .. ci0+31 (zero padded)
-      for (int i = threadIdx.x; (PNR_CONV_ABL & 4) == 0 && i < kRRows * kRRowPx * (kRCh / 4); i += blockDim.x) {
+      for (int i = threadIdx.x; i < kRRows * kRRowPx * (kRCh / 4); i += blockDim.x) {
         const int q = i % (kRCh / 4);
         const int px = (i / (kRCh / 4)) % kRRowPx;
         const int r = i / ((kRCh / 4) * kRRowPx);
@@ -110,13 +105,10 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
       const int pcol = 32 * wid + c;
       // k-steps of this chunk in (tap, channel-pair) order; weight fragments
       // are software-pipelined kRW steps ahead across tap boundaries
-      constexpr int kRW = PNR_CONV_RW;
+      constexpr int kRW = kConvRW;
       constexpr int kSteps = 9 * (kRCh / 2);
       const float* wp = a.wf + lane;
       auto wstep = [&](int i) {   // global k-step of chunk step i
-#if PNR_CONV_ABL & 1
-        return i & 1;               // ablation: weight fragments from L1
-#endif
         const int tap = i / (kRCh / 2), s = i % (kRCh / 2);
         return (tap * a.Cin + ci0) / 2 + s;
       };
@@ -140,11 +132,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
             if (BWD == 0 || ci0 + 2 * s < a.cin_real) {
 #pragma unroll
               for (int o = 0; o < kROut; ++o) {
-#if PNR_CONV_ABL & 2
-                const float b = lds_r[pcol * kRPitch + h + (s & 1)];   // ablation: fixed B rows
-#else
                 const float b = lds_r[((dy + o) * kRRowPx + pcol + dx) * kRPitch + h + 2 * s];
-#endif
 #pragma unroll
                 for (int T = 0; T < NT; ++T)
                   acc[o][T] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[d][T], b, acc[o][T], 0, 0, 0);
@@ -216,9 +204,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3(ConvArgs a) {
   }
 }
 
-#ifndef PNR_CONV_GRID
-#define PNR_CONV_GRID (256 * 3)   // workgroups of the persistent tile loop (one per tile: same time)
-#endif
+constexpr int kConvGrid = 256 * 3;   // workgroups of the persistent tile loop (one per tile: same time)
 template <int NT, int BWD = 0>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
   static bool attr = false;
@@ -228,7 +214,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     attr = true;
   }
   const int64_t tiles = (int64_t)((a.H + kROut - 1) / kROut) * ((a.W + kRPx - 1) / kRPx);
-  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, PNR_CONV_GRID)), dim3(256), kRLds, st, a);
+  hipLaunchKernelGGL((k_conv3x3<NT, BWD>), dim3(grid_for(tiles, 1, kConvGrid)), dim3(256), kRLds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

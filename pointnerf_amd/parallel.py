@@ -177,3 +177,92 @@ class _FrameGather:
     def wait(self) -> torch.Tensor:
         self.work.wait()
         return self.buf if self.buf is not None else torch.stack(self.parts)
+
+
+class GradReducer:
+    """The data-parallel finetune step's gradient reduction.
+
+    The reference wraps its whole net -- aggregator MLP and the neural point
+    table as nn.Parameters -- in DistributedDataParallel (base_model.py:61-71,
+    train_ddp.py:803-804), i.e. a mean all-reduce of every gradient.  Here the
+    same mean is built for this path's sparsity: the MLP gradients (~0.5 MB) go
+    as ONE flat all_reduce; the point table's gradients (N x 39 floats, 312 MB
+    at 2 M points, zero outside the rows the rank's batch touched) go as the
+    touched rows only -- an all-gather of (row ids, rows) and an index_add on
+    every rank -- so the bytes on xGMI scale with the batch, not the table.
+    After reduce() every rank holds the same gradients: the mean over ranks,
+    equal (up to summation order) to one process stepping the union batch
+    with a loss averaged per rank."""
+
+    def __init__(self, dense_params, point_params, group=None):
+        self.dense = [p for p in dense_params if p.requires_grad]
+        self.points = [p for p in point_params if p is not None and p.requires_grad]
+        self.group = group
+        # point tables as [rows, channels] (the reference keeps them [1, N, C])
+        if self.points:
+            n = self.points[0].numel() // self.points[0].shape[-1]
+            for p in self.points:
+                if p.numel() // p.shape[-1] != n:
+                    raise ValueError("GradReducer: point parameters must share their row count")
+
+    @staticmethod
+    def _grad(p):
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        return p.grad
+
+    def _all_gather(self, t):
+        import torch.distributed as dist
+        world = dist.get_world_size(self.group)
+        if dist.get_backend(self.group) == "nccl":
+            buf = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(buf, t.contiguous(), group=self.group)
+            return buf
+        lst = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(lst, t.contiguous(), group=self.group)
+        return torch.stack(lst)
+
+    def reduce(self, touched: torch.Tensor | None = None):
+        """touched: this rank's point rows with a (possibly) non-zero gradient
+        (any integer dtype, duplicates allowed); None = every row (dense)."""
+        import torch.distributed as dist
+        world = dist.get_world_size(self.group)
+        if world == 1:
+            return
+        if self.dense:
+            flat = torch.cat([self._grad(p).reshape(-1) for p in self.dense])
+            dist.all_reduce(flat, group=self.group)
+            flat.div_(world)
+            o = 0
+            for p in self.dense:
+                k = p.numel()
+                p.grad.copy_(flat[o:o + k].view_as(p))
+                o += k
+        if not self.points:
+            return
+        dev = self.points[0].device
+        n = self.points[0].numel() // self.points[0].shape[-1]
+        if touched is None:
+            rows = torch.arange(n, device=dev)
+        else:
+            rows = torch.unique(touched.to(device=dev, dtype=torch.int64))
+        widths = [p.shape[-1] for p in self.points]
+        m = torch.tensor([rows.numel()], dtype=torch.int64, device=dev)
+        counts = self._all_gather(m).reshape(-1).cpu()
+        mx = int(counts.max())
+        ids = torch.full((mx,), -1, dtype=torch.int64, device=dev)
+        ids[:rows.numel()] = rows
+        vals = torch.zeros((mx, sum(widths)), dtype=self.points[0].dtype, device=dev)
+        if rows.numel():
+            vals[:rows.numel()] = torch.cat([self._grad(p).reshape(n, -1)[rows] for p in self.points], 1)
+        all_ids = self._all_gather(ids)      # [world, mx]
+        all_vals = self._all_gather(vals)    # [world, mx, D]
+        keep = all_ids.reshape(-1) >= 0
+        sel = all_ids.reshape(-1)[keep]
+        v = all_vals.reshape(-1, sum(widths))[keep].div_(world)
+        o = 0
+        for p, w in zip(self.points, widths):
+            g = self._grad(p).reshape(n, w)
+            g.zero_()
+            g.index_add_(0, sel, v[:, o:o + w])
+            o += w

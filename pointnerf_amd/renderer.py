@@ -569,7 +569,10 @@ class NeuralPointsRayMarching(nn.Module):
         # conf_coefficient [1, R'', SR, K] as the reference returns it for the
         # zero_one loss (point_aggregators.py:810-816): gradiant_clamp of the
         # gathered conf, empty slots gather point 0 (torch.clamp(pidx, 0))
-        self.last_train_aux = {}
+        # rows of the point table this batch can give a gradient: the referenced
+        # points, and point 0 (empty slots gather it in conf_coefficient) --
+        # parallel.GradReducer reduces only these across ranks
+        self.last_train_aux = {"touched_rows": torch.cat([used[0].long(), torch.zeros(1, dtype=torch.long, device=dev)])}
         if self.keep_train_saved:
             self.last_train_aux["saved"] = spec.saved
         if np_.points_conf is not None:

@@ -102,3 +102,71 @@ def test_two_rank_libpnr_render_assembles_frames(cuda, layout):
         want = m.render_rays(cp, cr, rd, 2.0, 6.0, bg)[0].cpu().numpy()
         for r in range(2):
             np.testing.assert_allclose(got[r][f], want, atol=1e-6, rtol=0)
+
+
+def _train_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests"), os.path.join(root, "tests", "golden")]
+    import torch.distributed as dist
+    from pointnerf_amd.parallel import GradReducer
+    from test_gpu_backward import _train_model
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cuda = torch.device("cuda:0")
+        torch.cuda.set_device(cuda)
+        sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+        params = formula_params(salt=0.3)
+        cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+        rd = torch.from_numpy(sc["raydir"]).to(cuda)
+        bg = torch.from_numpy(sc["bg"]).to(cuda)
+        G = torch.randn((rd.shape[0], 128), generator=torch.Generator().manual_seed(5)).to(cuda)
+
+        def grads(m, idx, scale):
+            for p in m.parameters():
+                p.grad = None
+            color = m.render_rays_train(cp, cr, rd[idx].contiguous(), 2.0, 6.0, bg)[0]
+            ((color * G[idx]).sum() * scale).backward()
+            npt = m.neural_points
+            return m, {**{k: getattr(npt, k) for k in ("points_embeding", "points_color", "points_dir",
+                                                          "points_conf")},
+                       **{"mlp " + k: p for k, p in m.aggregator.named_parameters()}}
+
+        # this rank's rays: every world-th ray; per-rank loss, DDP-mean gradients
+        m, ps = grads(_train_model(sc, cuda, params), torch.arange(rank, rd.shape[0], world, device=cuda), 1.0)
+        npt = m.neural_points
+        red = GradReducer(list(m.aggregator.parameters()),
+                          [npt.points_embeding, npt.points_color, npt.points_dir, npt.points_conf])
+        red.reduce(m.last_train_aux["touched_rows"])
+        if rank == 0:
+            # one process, all rays: the mean of the ranks' losses
+            _, ref = grads(_train_model(sc, cuda, params), torch.arange(rd.shape[0], device=cuda), 1.0 / world)
+            for k in ps:
+                a, b = ps[k].grad, ref[k].grad
+                big = float(b.abs().max())
+                d = float((a.reshape(b.shape) - b).abs().max())
+                assert big > 0 and d <= 2e-5 * big, (k, d, big)
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()[-1500:]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_finetune_step_equals_single_process():
+    """SURVEY 8(e) training: 2 ranks each backpropagate half the rays, GradReducer
+    averages (one flat MLP all_reduce + the touched point rows), and the result
+    equals one process backpropagating all the rays with the same total loss
+    (float-atomic point sums: up to 2e-5 of the largest entry)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res
