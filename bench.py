@@ -347,7 +347,7 @@ def run_train(args, device):
         from pointnerf_amd.parallel import GradReducer
         npt = model.neural_points
         reducer = GradReducer(list(agg.parameters()),
-                              [npt.points_embeding, npt.points_color, npt.points_dir, npt.points_conf])
+                              [npt.points_embeding, npt.points_color, npt.points_dir, npt.points_conf, npt.xyz])
     H = W = args.hw
     cams = cameras(8, H, W)
     dev_cams = [tuple(torch.from_numpy(x).to(device) for x in c) for c in cams]

@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 14
+#define PNR_ABI_VERSION 15
 
 enum {
   PNR_OK = 0,
@@ -476,6 +476,19 @@ int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, cons
                                const float* d_feat, const float* d_hid, float* dz1, float* dz2, float* dz3,
                                float* dz4, float* dpa, float* d_p1, float* d_color, float* d_dir,
                                float* d_conf, void* stream);
+/* Point-position gradient (--xyz_grad 1, neural_points.py:270; replaces the
+ * autograd of sampled_xyz / sampled_xyz_pers, neural_points.py:635, 788-799,
+ * through point_aggregators.py:775-804 and the PE_5 input of block1.0):
+ * d_xyz[N,3] += (atomically) the gradient through the world distance (PE_5
+ * channels 0..2 and the normalised inverse-distance weight) and the perspective
+ * deltas (PE_5 channels 3..5, w2pers of the pair's camera, qpiw.py:102-109).
+ * d_pe[n_max*8,64] = dz1 . W1[:, 224:284] (block1.0's PE_5 columns; 60..63
+ * unused, the pitch of pnr_agg_saved.pe5); saved,
+ * d_feat, d_hid as for pnr_aggregate_bwd_pairs; pts needs xyz and the camera
+ * tables (ray_cam-indexed for multi-camera batches). */
+int pnr_aggregate_bwd_xyz(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                          const pnr_agg_saved* saved, const float* d_feat, const float* d_hid,
+                          const float* d_pe, float* d_xyz, void* stream);
 
 /* Weight-gradient GEMM (replaces the dW = dY^T X of torch's nn.Linear autograd
  * for block1.0/1.2/3.0/3.2, point_aggregators.py:276-348 trained by

@@ -525,7 +525,7 @@ class PointAggregator(nn.Module):
                                     None if sampled_color is None else sampled_color.reshape(-1, 3).float(),
                                     None if sampled_dir is None else sampled_dir.reshape(-1, 3).float(),
                                     None if sampled_conf is None else sampled_conf.reshape(-1, 1).float(),
-                                    *agg_params(self))
+                                    None, *agg_params(self))
             out = out[:rows]
         else:
             out = torch.zeros((rows, C + 1), dtype=torch.float32, device=dev)

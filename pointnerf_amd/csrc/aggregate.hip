@@ -1733,6 +1733,136 @@ extern "C" int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_sampl
                    d_conf, stream);
 }
 
+// ---------------------------------------------------------------------------
+// d xyz (--xyz_grad 1, neural_points.py:270): the point position enters the
+// pair through sampled_xyz (neural_points.py:788-799) -- the world distance
+// d = p - s_w, rotated into PE_5's first three channels and giving the inverse-
+// distance weight w = 1 / max(|d|, 1e-6), normalised over the K slots
+// (point_aggregators.py:775-804) -- and through sampled_xyz_pers =
+// w2pers(p) (neural_points.py:635, qpiw.py:102-109), whose deltas
+// (x z - x_s z_s, y z - y_s z_s, z - z_s) are PE_5's last three channels.  One
+// thread per pair (8 lanes = a sample's K slots, xor8 sums the weight
+// normalisation), given d PE_5 = dz1 . W1[:, 224:284] (pnr_gemm_nn) and
+// d wt = d alpha a_k + <d hid, h4_k>; atomics into d_xyz.
+struct XyzBwdArgs {
+  pnr_points pts;
+  pnr_samples s;
+  pnr_mlp w;
+  pnr_agg_saved sv;
+  const float* d_feat;   // [n,129]
+  const float* d_hid;    // [n,256]
+  const float* d_pe;     // [n*8,64] (columns 60..63 unused)
+  float* d_xyz;          // [N,3] (+=)
+};
+
+__global__ void __launch_bounds__(256) k_xyz_bwd(XyzBwdArgs A) {
+  const int64_t n = eff_n(A.s);
+  const int64_t pair = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t v = pair >> 3;
+  if (v >= n) return;   // whole 8-lane groups
+  const int32_t pr = A.sv.prow[pair];
+  const bool valid = pr >= 0;
+  const int64_t row = sample_row(A.s, v);
+  float pw[3] = {0.f, 0.f, 0.f}, d[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    if (valid) pw[a] = A.pts.xyz[(int64_t)pr * 3 + a];
+    d[a] = pw[a] - A.s.sample_w[row * 3 + a];
+  }
+  const float nrm = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
+  const float S = xor8_sum(wl);
+  // d wt_k: alpha_s = sum_k wt_k a_k, f_s = sum_k wt_k h4_k
+  float dwt = 0.f;
+  if (valid && A.sv.vmask[v] != 0) {
+    const float pa = A.sv.pa[pair];
+    const float a_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
+    const float4* h4 = reinterpret_cast<const float4*>(A.sv.h4 + pair * kHid);
+    const float4* dh = reinterpret_cast<const float4*>(A.d_hid + v * kHid);
+    float dot = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < kHid / 4; ++q) {
+      const float4 x = h4[q], y = dh[q];
+      dot += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    }
+    dwt = A.d_feat[v * (kC + 1)] * a_k + dot;
+  }
+  // wt = wn clamp(conf), wn_k = wl_k / max(S, 1e-8)
+  const float confc = (valid && A.pts.conf) ? fminf(fmaxf(A.pts.conf[pr], 1e-4f), 1.f) : 1.f;
+  const float dwn = dwt * confc;
+  const float dS = S >= 1e-8f ? -xor8_sum(dwn * wl) / (S * S) : 0.f;
+  const float dwl = dwn / fmaxf(S, 1e-8f) + dS;
+  if (!valid) return;
+  float g[3] = {0.f, 0.f, 0.f};
+  if (nrm > 1e-6f) {
+    const float dn = -dwl / (nrm * nrm * nrm);   // d(1/|d|) / dd = -d / |d|^3
+#pragma unroll
+    for (int a = 0; a < 3; ++a) g[a] = dn * d[a];
+  }
+  // PE_5: value 2(5c + f) = sin(2^f x_c), + 1 = cos(2^f x_c)
+  const float* pe = A.sv.pe5 + pair * 64;
+  const float* gp = A.d_pe + pair * 64;
+  float dd[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    float acc = 0.f;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      const int j = 2 * (5 * c + f);
+      acc += (float)(1 << f) * (pe[j + 1] * gp[j] - pe[j] * gp[j + 1]);
+    }
+    dd[c] = acc;
+  }
+  // channels 0..2: R.d (d_i gets sum_j R[j][i] dd_j)
+  float Rw[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) g[i] += Rw[i] * dd[0] + Rw[3 + i] * dd[1] + Rw[6 + i] * dd[2];
+  // channels 3..5 through the perspective coordinates of the pair's camera
+  float c3[3], R[9];
+  const int64_t cam = A.s.ray_cam ? (int64_t)A.s.ray_cam[dir_row(A.s, row)] : 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) c3[i] = A.pts.campos[cam * 3 + i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = A.pts.camrot[cam * 9 + i];
+  float xc[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    xc[j] = (pw[0] - c3[0]) * R[j] + (pw[1] - c3[1]) * R[3 + j] + (pw[2] - c3[2]) * R[6 + j];
+  const float pp[3] = {xc[0] / xc[2], xc[1] / xc[2], xc[2]};
+  const float dp0 = dd[3] * pp[2], dp1 = dd[4] * pp[2], dp2 = dd[3] * pp[0] + dd[4] * pp[1] + dd[5];
+  const float iz = 1.f / xc[2];
+  const float dx0 = dp0 * iz, dx1 = dp1 * iz, dx2 = dp2 - (dp0 * pp[0] + dp1 * pp[1]) * iz;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) g[i] += R[i * 3] * dx0 + R[i * 3 + 1] * dx1 + R[i * 3 + 2] * dx2;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) atomicAdd(A.d_xyz + (int64_t)pr * 3 + i, g[i]);
+}
+
+extern "C" int pnr_aggregate_bwd_xyz(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                     const pnr_agg_saved* saved, const float* d_feat, const float* d_hid,
+                                     const float* d_pe, float* d_xyz, void* stream) {
+  PNR_CHECK_ARG(pts && s && w && saved && d_feat && d_hid && d_pe && d_xyz, "aggregate_bwd_xyz: null argument");
+  PNR_CHECK_ARG(pts->xyz && pts->campos && pts->camrot, "aggregate_bwd_xyz: need xyz and the camera tables");
+  PNR_CHECK_ARG(saved->prow && saved->pa && saved->h4 && saved->pe5 && saved->vmask,
+                "aggregate_bwd_xyz: missing saved activations");
+  PNR_CHECK_ARG(s->K <= kKN, "aggregate_bwd_xyz: K > %d", kKN);
+  if (s->n_max <= 0) return PNR_OK;
+  XyzBwdArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  a.sv = *saved;
+  a.d_feat = d_feat;
+  a.d_hid = d_hid;
+  a.d_pe = d_pe;
+  a.d_xyz = d_xyz;
+  hipLaunchKernelGGL(k_xyz_bwd, dim3((unsigned)cdiv(s->n_max * kKN, 256)), dim3(256), 0, as_stream(stream), a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
 extern "C" int pnr_used_points_scratch_bytes(int64_t n_points, size_t* out) {
   PNR_CHECK_ARG(out && n_points >= 0, "used_points_scratch_bytes: bad args");
   *out = scan_scratch_bytes(n_points);

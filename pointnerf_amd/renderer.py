@@ -39,9 +39,6 @@ class NeuralPoints(nn.Module):
         self.emb_dtype = emb_dtype
         self._emb32 = (None, None)
         self.opt = opt
-        if getattr(opt, "xyz_grad", 0) > 0:
-            raise L.PnrError("xyz_grad > 0 (point-position gradients, neural_points.py:270) is not "
-                             "implemented by libpnr's backward; run with --xyz_grad 0")
         self.device = torch.device(device)
         self.xyz = nn.Parameter(torch.zeros((0, 3), device=self.device), requires_grad=False)
         self.points_embeding = nn.Parameter(torch.zeros((1, 0, 32), device=self.device))
@@ -54,14 +51,12 @@ class NeuralPoints(nn.Module):
         self.querier = lighting_fast_querier(self.device, opt)
 
     def set_points(self, xyz, embedding, color=None, dirs=None, conf=None, Rw2c=None):
-        """set_points (neural_points.py:480-546) with point_*_mode '1'.
-        xyz gradients (--xyz_grad 1, neural_points.py:270) are not implemented
-        by the HIP backward: refused here instead of silently dropped."""
-        if getattr(self.opt, "xyz_grad", 0) > 0:
-            raise L.PnrError("xyz_grad > 0 (point-position gradients, neural_points.py:270) is not "
-                             "implemented by libpnr's backward; run with --xyz_grad 0")
+        """set_points (neural_points.py:480-546) with point_*_mode '1'; xyz is
+        trainable with --xyz_grad 1 (neural_points.py:270: the HIP backward's
+        pnr_aggregate_bwd_xyz, render_rays_train only)."""
         dev = self.device
-        self.xyz = nn.Parameter(xyz.to(dev).float().reshape(-1, 3).contiguous(), requires_grad=False)
+        self.xyz = nn.Parameter(xyz.to(dev).float().reshape(-1, 3).contiguous(),
+                                requires_grad=getattr(self.opt, "xyz_grad", 0) > 0)
         self.points_embeding = nn.Parameter(embedding.to(dev).to(self.emb_dtype).reshape(1, -1, 32).contiguous())
         self.points_color = None if color is None else nn.Parameter(color.to(dev).float().reshape(1, -1, 3).contiguous())
         self.points_dir = None if dirs is None else nn.Parameter(dirs.to(dev).float().reshape(1, -1, 3).contiguous())
@@ -560,7 +555,8 @@ class NeuralPointsRayMarching(nn.Module):
                        used=used, x3=self.train_precision == "fp32x3")
         spec.keep_saved = self.keep_train_saved
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
-                                 tab(np_.points_dir, 3), tab(np_.points_conf, 1), *agg_params(self.aggregator))
+                                 tab(np_.points_dir, 3), tab(np_.points_conf, 1),
+                                 np_.xyz if np_.xyz.requires_grad else None, *agg_params(self.aggregator))
         if C == 3:
             feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
         cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))

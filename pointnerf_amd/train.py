@@ -25,7 +25,7 @@ matching the autograd of point_aggregators.py:729-816 / 488-646,
 gradiant_clamp (:724-726), the gather (neural_points.py:788-799) and
 ray_march (diff_ray_marching.py:509-555).  Gradients are produced for
 points_embeding, points_color, points_dir, points_conf and every aggregator
-parameter; xyz gradients (xyz_grad) are not implemented.
+parameter; xyz gradients (xyz_grad) through pnr_aggregate_bwd_xyz.
 """
 from __future__ import annotations
 
@@ -134,10 +134,11 @@ class AggSpec:
 
 class AggregateFn(torch.autograd.Function):
     """feat[n_max, 129] = aggregate(point tables, MLP); differentiable in emb,
-    color, dir, conf and the 16 aggregator parameters."""
+    color, dir, conf, the 16 aggregator parameters and -- when xyz is given
+    (--xyz_grad 1; the fused renderer path) -- the point positions."""
 
     @staticmethod
-    def forward(ctx, spec: AggSpec, emb, color, dirs, conf, *params):
+    def forward(ctx, spec: AggSpec, emb, color, dirs, conf, xyz, *params):
         dev = emb.device
         agg = spec.agg
         s = spec.samples
@@ -180,6 +181,7 @@ class AggregateFn(torch.autograd.Function):
         if getattr(spec, "keep_saved", False):
             spec.saved = sv                 # tests: the kept activations of this forward
         ctx.has = (color is not None, dirs is not None, conf is not None)
+        ctx.xyz_shape = None if xyz is None else xyz.shape
         ctx.shapes = (emb.shape, None if conf is None else conf.shape)
         ctx.save_for_backward(*params)
         return feat
@@ -278,7 +280,19 @@ class AggregateFn(torch.autograd.Function):
         else:
             d_emb = torch.zeros((N, 32), **f32).index_copy_(0, used.long(), d_emb_u[:n_p1])
         emb_shape, conf_shape = ctx.shapes
-        out = [None, d_emb.view(emb_shape), d_color, d_dir, None if d_conf is None else d_conf.view(conf_shape)]
+        d_xyz = None
+        if ctx.xyz_shape is not None and ctx.needs_input_grad[5]:
+            # d PE_5 = dz1 . W1[:, 224:284], then the distance / weight / w2pers chain per pair
+            w1pe = torch.zeros((256, 64), **f32)          # N padded to the GEMM's 32-column tiles
+            w1pe[:, :60] = P["block1.0.weight"][:, 224:284]
+            d_pe = L.gemm_nn(dz1, w1pe)
+            d_xyz = torch.zeros((N, 3), **f32)
+            L.check(L.lib().pnr_aggregate_bwd_xyz(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                  ctypes.byref(ctx.mlp), ctypes.byref(sv.c), L.ptr(d_feat),
+                                                  L.ptr(d_hid), L.ptr(d_pe), L.ptr(d_xyz), L.stream_ptr(dev)),
+                    "pnr_aggregate_bwd_xyz")
+            d_xyz = d_xyz.view(ctx.xyz_shape)
+        out = [None, d_emb.view(emb_shape), d_color, d_dir, None if d_conf is None else d_conf.view(conf_shape), d_xyz]
         out += [grads[k] for k in _PARAM_NAMES]
         return tuple(out)
 

@@ -304,3 +304,65 @@ def test_train_backward_repeatable(cuda, train_precision):
                 assert d <= 1e-6 * big, (k, d, big)
             else:
                 assert d <= 1e-6 * big, (k, d, big)
+
+
+def _w2pers_torch(p, campos, camrot):
+    """qpiw.py:102-109 in torch (differentiable): (x/z, y/z, z) of R^T (p - c)."""
+    s = p - campos
+    xc = [s[..., 0] * camrot[0, j] + s[..., 1] * camrot[1, j] + s[..., 2] * camrot[2, j] for j in range(3)]
+    return torch.stack([xc[0] / xc[2], xc[1] / xc[2], xc[2]], -1)
+
+
+@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])
+def test_render_train_xyz_grad_vs_oracle(cuda, train_precision):
+    """--xyz_grad 1 (neural_points.py:270): d xyz through the world distance
+    (PE_5 channels 0..2, the normalised inverse-distance weights) and the
+    perspective deltas (w2pers, PE_5 channels 3..5) vs torch autograd of the CPU
+    oracle on the same neighbours -- in fp32 within the tolerance of the other
+    point gradients, and the fp64 oracle's error no larger than 2x the fp32
+    oracle's own."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    params = formula_params(salt=0.3)
+    sc["opt"] = type(sc["opt"])(**{**vars(sc["opt"]), "xyz_grad": 1})
+    m = _train_model(sc, cuda, params)
+    m.train_precision = train_precision
+    assert m.neural_points.xyz.requires_grad
+    campos = torch.from_numpy(sc["campos"]).to(cuda)
+    camrot = torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    color = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0]
+    G = torch.randn(color.shape, generator=torch.Generator().manual_seed(5)).to(cuda)
+    (color * G).sum().backward()
+    got = m.neural_points.xyz.grad.cpu().double()
+    opt = sc["opt"]
+    q = O.query_points(opt, sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
+    pidx = torch.from_numpy(q["sample_pidx"]).long()
+    mask = pidx >= 0
+    idx = pidx.clamp(min=0).reshape(-1)
+    shp = tuple(pidx.shape)
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        xyz = torch.from_numpy(sc["xyz"]).to(dt).requires_grad_(True)
+        tp = {k: torch.from_numpy(np.ascontiguousarray(sc[k])).to(dt) for k in ("emb", "color", "dir", "conf")}
+        pp = {k: torch.from_numpy(v).to(dt) for k, v in params.items()}
+        pers = _w2pers_torch(xyz, torch.from_numpy(sc["campos"]).to(dt), torch.from_numpy(sc["camrot"]).to(dt))
+        gsel = lambda a, c: a.reshape(-1, c)[idx].reshape(shp + (c,))  # noqa: E731
+        feats, rv, _, _ = OG.aggregate(pp, gsel(tp["color"], 3), gsel(tp["dir"], 3), gsel(tp["conf"], 1),
+                                       gsel(tp["emb"], 32), gsel(pers, 3), gsel(xyz, 3), mask,
+                                       torch.from_numpy(q["sample_loc"]).to(dt),
+                                       torch.from_numpy(q["sample_loc_w"]).to(dt),
+                                       torch.from_numpy(q["sample_ray_dirs"]).to(dt))
+        rdist = torch.from_numpy(O.ray_dist(q["sample_loc"], rv.numpy(), opt.vsize[2], opt.raydist_mode_unit)).to(dt)
+        c_ref = OG.ray_march(rdist, rv, feats, torch.from_numpy(sc["bg"]).to(dt))
+        mk = torch.from_numpy(q["ray_mask"] > 0)
+        (c_ref * G.cpu()[mk].to(dt)).sum().backward()
+        refs[dt] = xyz.grad.double()
+    r32, r64 = refs[torch.float32], refs[torch.float64]
+    big = float(r64.abs().max())
+    assert big > 0
+    e = float((got - r64).abs().max())
+    e32 = float((r32 - r64).abs().max())
+    print(f"\nd xyz: max |ref| {big:.3g}, err vs fp64 {e:.3g} (fp32 oracle {e32:.3g})")
+    close(got.float(), r32.float(), "d xyz", scale=5e-5)
+    assert e <= 2.0 * e32 + 1e-6 * big, (e, e32, big)

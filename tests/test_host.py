@@ -135,11 +135,3 @@ def test_scene_points_cap_and_fixed_bbox():
         assert g["occ_numpnts"].max() <= o.P - 1
         assert np.all(p >= np.asarray(o.ranges[:3], np.float32)) and np.all(p <= np.asarray(o.ranges[3:], np.float32))
 
-
-def test_xyz_grad_is_refused():
-    import pytest
-    from pointnerf_amd import _lib as L
-    from pointnerf_amd.options import lego_opt
-    from pointnerf_amd.renderer import NeuralPoints
-    with pytest.raises(L.PnrError, match="xyz_grad"):
-        NeuralPoints(lego_opt(xyz_grad=1), "cpu")
