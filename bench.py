@@ -76,8 +76,9 @@ def parse():
                     help="fp32h2 pairs stage: k_pairs_h2 (wt) or the activation-stationary k_pairs_as (as)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
-    ap.add_argument("--train-precision", choices=("fp32x3", "fp32"), default="fp32x3",
-                    help="--mode train: the training forward's per-pair chain (fp32x3 split-bf16 MFMA or native fp32)")
+    ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32h2",
+                    help="--mode train: the training forward's per-pair chain (fp32h2 split-f16 MFMA, fp32x3 "
+                         "split-bf16 MFMA or native fp32)")
     ap.add_argument("--mode", choices=("render", "train"), default="render",
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
@@ -405,7 +406,7 @@ def run_train(args, device):
         "metric": "train steps/s (fwd+bwd+Adam, 3600-ray batches), 2M neural points",
         "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32", "train_forward": args.train_precision,
+        "dtype": "fp32", "train_forward": args.train_precision, "h2_fallbacks": int(model.h2_fallbacks),
         "data": "synthetic (seeded lego-like point cloud, random target colours)",
         "config": {"workload": f"finetune step, {args.train_rays} random rays of {H}x{W} frames, {args.points} points",
                    "K": opt.K, "SR": opt.SR},

@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 15
+#define PNR_ABI_VERSION 16
 
 enum {
   PNR_OK = 0,
@@ -420,6 +420,15 @@ int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_samples* s, cons
                                float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
                                void* stream);
 /* Same, for the PointAggregator.forward mirror (pre-gathered tables, pair_mask). */
+/* pnr_aggregate_fwd_train with the per-pair chain on the fp32h2 kernel of
+ * pnr_aggregate_fwd_h2 (k_pairs_h2 + the same saves; wh's w1bh / w2h / w3h / w4h
+ * packs and scales, the range flag as pnr_aggregate_fwd_h2: set when an
+ * activation left the f16 range, the caller then re-runs the step on
+ * pnr_aggregate_fwd_train_x3).  Saved layout and outputs as the fp32 call. */
+int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                               const pnr_mlp_h2* wh, const pnr_agg_saved* saved, float* out_feat,
+                               float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
+                               void* stream);
 int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                    const uint8_t* pair_mask, const pnr_agg_saved* saved,
                                    float* out_feat, float* out_weight, float* out_conf,
@@ -465,6 +474,15 @@ int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int6
 int pnr_pack_weights(int32_t kind, const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f,
                      int32_t kin, const float* bias, int32_t pad_steps, void* out, size_t out_bytes,
                      void* stream);
+/* fp32h2 packs (aggregator.py frag_pack_h2 with a given shift s, one launch):
+ * F[t][T][plane][h][r][j] = plane of (2^-s W')[32T + r][16t + 8h + j], planes
+ * (Wh, Wl): Wh = f16(x), Wl = f16((x - Wh) 2^11) (round to nearest even),
+ * ceil(cols / 16) + pad_steps k-steps; *range_flag |= 1 when some |2^-s W'| >= 16
+ * or is not finite (the pack is then unusable: the caller re-picks s).  The
+ * training step keeps s across steps and packs without a host sync. */
+int pnr_pack_weights_h2(const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f, int32_t kin,
+                        const float* bias, int32_t pad_steps, int32_t shift, int32_t* range_flag, void* out,
+                        size_t out_bytes, void* stream);
 /* Same, with the three dX GEMMs on fp32x3 split-bf16 MFMA: wbx = frag_pack_x3 of
  * block3.2.weight^T, block3.0.weight[:, :256]^T, block1.2.weight^T (aggregator.py;
  * 16-B aligned); wb supplies w3e (w4t / w3t / w2t unused, may be NULL). */
@@ -612,6 +630,42 @@ int pnr_neural_render_bwd_scratch_bytes(int32_t H, int32_t W, size_t* out);
 int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, const float* out_rgb, const float* d_out,
                           int32_t H, int32_t W, const pnr_neural_render_wt* wt, float* d_x, float* dw0,
                           float* dw1, float* dw2, void* scratch, size_t scratch_bytes, void* stream);
+
+/* The same renderer, forward and backward, with fp32 accuracy on f16 MFMA
+ * (fp32h2, the MLP's split: x = xh + 2^-11 xl per input value, W' = Wh +
+ * 2^-11 Wl per weight, three f16 products per 16 k).  Per stage s the stacked
+ * [trunk; rgb; 0] rows (96 / 64 / 32 rows, columns k = (ky*3 + kx)*cin + ci)
+ * as frag_pack_h2 packs wp_s with their scales ws_s = 2^(shift - 11), and the
+ * stacked biases b_s (96 / 64 / 32 floats: trunk, rgb, 0).  Each image is
+ * staged times a power of two chosen on the device from its max |value|, so
+ * any finite input magnitude keeps fp32-level relative accuracy (no range
+ * fallback, no host sync).  Scratch: net0[H,W,64], net1[H,W,32], then 256 B of
+ * absmax words (the backward reads them from fwd_scratch). */
+typedef struct {
+  const void* wp0; const void* wp1; const void* wp2;
+  float ws0, ws1, ws2;
+  const float* b0; const float* b1; const float* b2;
+  float neg_slope;
+} pnr_neural_render_h2w;
+
+/* Backward packs: the data-gradient weights of pnr_neural_render_wt (flipped,
+ * transposed stacks [128, 9*96], [64, 9*64], [32, 9*32]) as frag_pack_h2 packs
+ * with their scales.  Outputs as pnr_neural_render_bwd; data and weight
+ * gradients both on fp32h2 (fwd_scratch: pnr_neural_render_fwd_h2's, with its
+ * absmax words).  Fixed-order reductions: bitwise repeatable. */
+typedef struct {
+  const void* wt0; const void* wt1; const void* wt2;
+  float ws0, ws1, ws2;
+  float neg_slope;
+} pnr_neural_render_h2wt;
+
+int pnr_neural_render_h2_scratch_bytes(int32_t H, int32_t W, size_t* out);
+int pnr_neural_render_fwd_h2(const float* x, int32_t H, int32_t W, const pnr_neural_render_h2w* w,
+                             float* out_rgb, void* scratch, size_t scratch_bytes, void* stream);
+int pnr_neural_render_bwd_h2_scratch_bytes(int32_t H, int32_t W, size_t* out);
+int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch, const float* out_rgb, const float* d_out,
+                             int32_t H, int32_t W, const pnr_neural_render_h2wt* wt, float* d_x, float* dw0,
+                             float* dw1, float* dw2, void* scratch, size_t scratch_bytes, void* stream);
 
 /* ------------------------------------------------------ upstream RGB head
  * C_out = 3 mode (shading_color_channel_num 3): for v < min(*n_dev, n_max)

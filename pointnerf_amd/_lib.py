@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 15
+ABI_VERSION = 16
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -72,6 +72,16 @@ class NeuralRenderW(ctypes.Structure):
 
 class NeuralRenderWT(ctypes.Structure):
     _fields_ = [("wt0", c_void_p), ("wt1", c_void_p), ("wt2", c_void_p), ("neg_slope", c_float)]
+
+
+class NeuralRenderH2W(ctypes.Structure):
+    _fields_ = [("wp0", c_void_p), ("wp1", c_void_p), ("wp2", c_void_p), ("ws0", c_float), ("ws1", c_float),
+                ("ws2", c_float), ("b0", c_void_p), ("b1", c_void_p), ("b2", c_void_p), ("neg_slope", c_float)]
+
+
+class NeuralRenderH2WT(ctypes.Structure):
+    _fields_ = [("wt0", c_void_p), ("wt1", c_void_p), ("wt2", c_void_p), ("ws0", c_float), ("ws1", c_float),
+                ("ws2", c_float), ("neg_slope", c_float)]
 
 
 class MlpBf16(ctypes.Structure):
@@ -155,6 +165,8 @@ SIGNATURES = {
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpX3), P(AggSaved), c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_train_h2": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpH2), P(AggSaved), c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, P(AggSaved), c_void_p,
                                                c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_bwd_pairs": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(AggSaved), c_void_p,
@@ -169,6 +181,8 @@ SIGNATURES = {
     "pnr_used_points": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_pairs_to_points": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_pack_weights_h2": (c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32, c_int32,
+                                    c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_pack_weights": (c_int, [c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,
                                  c_void_p, c_size_t, c_void_p]),
     "pnr_gemm_tn_scratch_bytes": (c_int, [c_int64, c_int32, c_int32, P(c_size_t)]),
@@ -194,6 +208,13 @@ SIGNATURES = {
     "pnr_neural_render_bwd_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
     "pnr_neural_render_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, P(NeuralRenderWT),
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_neural_render_h2_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
+    "pnr_neural_render_fwd_h2": (c_int, [c_void_p, c_int32, c_int32, P(NeuralRenderH2W), c_void_p, c_void_p,
+                                         c_size_t, c_void_p]),
+    "pnr_neural_render_bwd_h2_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),
+    "pnr_neural_render_bwd_h2": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                                         P(NeuralRenderH2WT), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_size_t, c_void_p]),
     "pnr_rgb_head_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p,
                                  c_void_p]),
     "pnr_rgb_head_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32,

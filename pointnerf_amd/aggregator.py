@@ -88,6 +88,22 @@ def _pack_device(kind: int, W: torch.Tensor, bias: torch.Tensor | None, pad: int
     return out
 
 
+def _pack_h2_device(W: torch.Tensor, bias: torch.Tensor | None, shift: int, flag: torch.Tensor) -> torch.Tensor:
+    """pnr_pack_weights_h2: frag_pack_h2(W, bias, shift)[0] of a CUDA weight in one
+    launch (no host sync); flag (int32[1], device) raised when the shift is too small."""
+    out_f, kin = W.shape
+    assert out_f % 32 == 0
+    cols = kin + (1 if bias is not None else 0)
+    W = W.detach().float()
+    b = None if bias is None else bias.detach().float().contiguous()
+    n = ((cols + 15) // 16 + H2_PAD) * (out_f // 32) * 64 * 2 * 8
+    out = torch.empty(n, dtype=torch.float16, device=W.device)
+    L.check(L.lib().pnr_pack_weights_h2(W.data_ptr(), W.stride(0), W.stride(1), out_f, kin, L.ptr(b), H2_PAD,
+                                        int(shift), flag.data_ptr(), out.data_ptr(), out.numel() * 2,
+                                        L.stream_ptr(W.device)), "pnr_pack_weights_h2")
+    return out
+
+
 def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """[out, Kin] nn.Linear weight (out a multiple of 32) and bias -> MFMA
     A-operand fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)]
@@ -439,6 +455,38 @@ class PointAggregator(nn.Module):
                     (L.c_float * 4)(*(assc if use_as else (0.0,) * 4)))
         self._packedh2, self._packedh2_key = (m, t), key
         return self._packedh2
+
+    def packed_h2_train(self) -> tuple[L.MlpH2, dict]:
+        """fp32h2 packs of the per-pair chain (block1.0[:, 224:], block1.2,
+        block3.0, block3.2) for pnr_aggregate_fwd_train_h2, packed on the device
+        (pnr_pack_weights_h2: no host sync while the weights change every step)
+        with shifts kept from the last h2_shift pick; `range_flag` is raised by
+        the pack when a weight outgrew its shift and by the forward when an
+        activation left the f16 range -- the caller then calls
+        h2_train_reset() (shifts re-picked) and re-runs the step on fp32x3."""
+        key = self.h2_key()
+        if getattr(self, "_packedh2t", None) is not None and key == self._packedh2t_key:
+            return self._packedh2t
+        b1, b3 = self.block1, self.block3
+        mats = [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None)]
+        if getattr(self, "_h2t_shifts", None) is None:
+            with torch.no_grad():
+                self._h2t_shifts = [h2_shift(W, b) for W, b in mats]
+            self._h2t_flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
+        flag = self._h2t_flag
+        packs = [_pack_h2_device(W, b, s, flag) for (W, b), s in zip(mats, self._h2t_shifts)]
+        t = dict(w1bh=packs[0], w2h=packs[1], w3h=packs[2], w4h=packs[3], range_flag=flag)
+        m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
+                    (L.c_float * 4)(*(2.0 ** (s - 11) for s in self._h2t_shifts)), flag.data_ptr(),
+                    None, None, None, None, (L.c_float * 3)(0.0, 0.0, 0.0), None, 0.0, None, None,
+                    (L.c_float * 4)(0.0, 0.0, 0.0, 0.0))
+        self._packedh2t, self._packedh2t_key = (m, t), key
+        return self._packedh2t
+
+    def h2_train_reset(self):
+        """After a raised training range flag: shifts re-picked at the next pack."""
+        self._h2t_shifts = None
+        self._packedh2t = None
 
     def h2_key(self):
         """Identity of the current weights (storage + version of every

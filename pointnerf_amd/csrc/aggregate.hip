@@ -1628,6 +1628,47 @@ extern "C" int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_sampl
   return launch_t<true>(a, st, kStageColor);
 }
 
+extern "C" int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                          const pnr_mlp_h2* wh, const pnr_agg_saved* saved, float* out_feat,
+                                          float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
+                                          void* stream) {
+  int rc;
+  if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
+  if ((rc = check_saved(saved))) return rc;
+  PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_train_h2: need pers or camera");
+  PNR_CHECK_ARG(s->pidx, "aggregate_train_h2: pidx required");
+  PNR_CHECK_ARG(wh && wh->w1bh && wh->w2h && wh->w3h && wh->w4h, "aggregate_train_h2: null split weight pack");
+  PNR_CHECK_ARG(w->neg_slope >= 0.f && w->neg_slope <= 1.f, "aggregate_train_h2: LeakyReLU slope must be in [0, 1]");
+  PNR_CHECK_ARG((((uintptr_t)wh->w1bh | (uintptr_t)wh->w2h | (uintptr_t)wh->w3h | (uintptr_t)wh->w4h) & 15) == 0,
+                "aggregate_train_h2: split packs must be 16-B aligned");
+  for (int i = 0; i < 4; ++i)
+    PNR_CHECK_ARG(wh->scale[i] > 0.f && wh->scale[i] < 1e30f, "aggregate_train_h2: bad layer scale %d", i);
+  if (s->n_max <= 0) return PNR_OK;
+  AggArgs a;
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  carve(a, scratch, s->n_max, pts->used ? pts->n_used : pts->n);
+  int32_t* tile_ctr = tile_counter(a, s->n_max);   // in the scratch (before vmask is redirected to the saved one)
+  a.sv = *saved;
+  a.hid = saved->hid;
+  a.vmask = saved->vmask;
+  a.out_feat = out_feat;
+  a.out_weight = out_weight;
+  a.out_conf = out_conf;
+  a.pair_mask = nullptr;
+  hipStream_t st = as_stream(stream);
+  // k_point_pre (fp32 P1) -> k_pairs_h2_train (aggregate_x3.hip) -> k_color<true>
+  if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
+  SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
+               {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
+               wh->range_flag};
+  if ((rc = launch_pairs_split<true>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
+                                     tile_ctr, st, saved)))
+    return rc;
+  return launch_t<true>(a, st, kStageColor);
+}
+
 extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                               const uint8_t* pair_mask, const pnr_agg_saved* saved,
                                               float* out_feat, float* out_weight, float* out_conf,

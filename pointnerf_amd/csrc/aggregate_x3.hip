@@ -612,11 +612,13 @@ __device__ __forceinline__ void finalize_alpha(const X3Args& A, char* lds, int b
   }
 }
 
-// Training save of a layer's pre-activations (x3, scale 1): lrelu -> dst[pair][256]
+// Training save of a layer's pre-activations acc * sc (sc: the h2 layer's output
+// factor, 1 on x3 -- the same product store_act rounds): lrelu -> dst[pair][256]
 // and the LeakyReLU derivative bits mask[pair][16 layer + 2T + h] (bit r: register
 // r of neuron tile T, lane half h), the layout of aggregate.hip's save_pairs_q.
+template <bool H>
 __device__ __forceinline__ void save_act_train(const X3Args& A, const f32x16 (&acc)[4], float* dst, int layer,
-                                               int64_t tile, int64_t n, float neg, int lane, int T0) {
+                                               int64_t tile, int64_t n, float neg, int lane, int T0, float sc) {
   const int c = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int pt = 0; pt < 2; ++pt) {
@@ -625,7 +627,8 @@ __device__ __forceinline__ void save_act_train(const X3Args& A, const f32x16 (&a
     const int64_t pr = tile * kXT + col;
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
-      const f32x16& v = acc[2 * pt + T];
+      f32x16 v = acc[2 * pt + T];
+      if constexpr (H) v = v * sc;
       unsigned bits = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -693,7 +696,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
         }
     X3_SYNC();   // S1b: the parked P1 read by every consumer (the planes overwrite it)
     store_act<H>(acc, XP, neg, 1.f, lane, T0);
-    if constexpr (TR) save_act_train(A, acc, A.sv.h1, 0, tile, n, neg, lane, T0);
+    if constexpr (TR) save_act_train<H>(A, acc, A.sv.h1, 0, tile, n, neg, lane, T0, 1.f);
     if (wid == 0) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl) {   // row 256 = 1 (bias column), 257..271 = 0 (the parked P1 was here)
@@ -709,7 +712,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     prime<H>(wr, r3, voff);
     X3_SYNC();   // S3
     store_act<H>(acc, XP, neg, sc2, lane, T0);
-    if constexpr (TR) save_act_train(A, acc, A.sv.h2, 1, tile, n, neg, lane, T0);
+    if constexpr (TR) save_act_train<H>(A, acc, A.sv.h2, 1, tile, n, neg, lane, T0, sc2);
     if (wid == 0) {   // block3.0 inputs 256..263: colour, R.dir - R.v, <R.dir, R.v>, bias
       const float* exL = reinterpret_cast<const float*>(lds + L::OffEx) + buf * 8 * kXT;
       float ex[8];
@@ -725,7 +728,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     prime<H>(wr, r4, voff);
     X3_SYNC();   // S5
     store_act<H>(acc, XP, neg, sc3, lane, T0);
-    if constexpr (TR) save_act_train(A, acc, A.sv.h3, 2, tile, n, neg, lane, T0);
+    if constexpr (TR) save_act_train<H>(A, acc, A.sv.h3, 2, tile, n, neg, lane, T0, sc3);
     if (wid == 0 && !H) {
 #pragma unroll
       for (int pl = 0; pl < L::NPL; ++pl)
@@ -738,6 +741,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
     layer<H>(acc, wr, r4, voff, XP, kPlaneX, kBiasSteps(H), lane);
     prime<H>(wr, r1, voff);   // the next tile's block1.0
     if constexpr (H) {
+      if constexpr (TR) save_act_train<H>(A, acc, A.sv.h4, 3, tile, n, neg, lane, T0, sc4);
       // block3.2 accumulators -> LDS [pair][row] for the producers' tail (next tile):
       // one ds_write_b128 per accumulator quad, conflict-free at kP1Pitch
       float* H4 = reinterpret_cast<float*>(lds + L::OffH4);
@@ -752,7 +756,7 @@ __device__ __forceinline__ void consumer_loop(const X3Args& A, char* lds, int wi
                 make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
           }
     } else {
-      if constexpr (TR) save_act_train(A, acc, A.sv.h4, 3, tile, n, neg, lane, T0);
+      if constexpr (TR) save_act_train<H>(A, acc, A.sv.h4, 3, tile, n, neg, lane, T0, 1.f);
       const float* wtL = reinterpret_cast<const float*>(lds + L::OffWt) + buf * kXT;
       const int* sflag = reinterpret_cast<const int*>(lds + L::OffSf) + buf * kXTS;
       float pa_part[2] = {0.f, 0.f};
@@ -859,7 +863,7 @@ struct TailState {
 
 // PART 0: pairs k = 0..3 of every sample; PART 1: k = 4..7, the reductions and
 // the stores (the halves run in two producer segments, see producer_loop)
-template <int PART>
+template <int PART, bool TR = false>
 __device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int slot, int64_t tile, int pw, int lane,
                                               TailState& ts, float& chk) {
   using L = XL<true>;
@@ -902,6 +906,7 @@ __device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int sl
   r1 += __shfl_xor(r1, 2);
   r1 += __shfl_xor(r1, 1);
   const float pk = r1 + A.w.ba[0];
+  if (TR && (ng & 3) == 0 && tile * kXTS + j < n) A.sv.pa[tile * kXT + 8 * j + (ng >> 2)] = pk;
   const float alpha_k = A.w.act_super ? softplus(pk - 1.f) : fmaxf(pk, 0.f);
   float as = wtL[ng >> 2] * alpha_k;   // each k held by 4 lanes: sum over bits 2..4
   as += __shfl_xor(as, 4);
@@ -914,7 +919,13 @@ __device__ __forceinline__ void producer_tail(const X3Args& A, char* lds, int sl
       A.vmask[vo] = sf;
       if (sf) A.out_feat[vo * (kC + 1)] = as;
     }
-    if (sf) {   // hid rows 8ng..8ng+7 as one 16-B piece per plane (kHidTile layout)
+    if (TR) {   // training: fp32 hid rows [n][256] for the fp32 colour branch (k_color<true>)
+      if (sf) {
+        float4* dst = reinterpret_cast<float4*>(A.hid + vo * kHid + 8 * ng);
+        dst[0] = make_float4(hs[0], hs[1], hs[2], hs[3]);
+        dst[1] = make_float4(hs[4], hs[5], hs[6], hs[7]);
+      }
+    } else if (sf) {   // hid rows 8ng..8ng+7 as one 16-B piece per plane (kHidTile layout)
       typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
       unsigned a[4], b[4];
 #pragma unroll
@@ -971,7 +982,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // readers were the previous finalize / tail)
     gather<H, TR>(A, g, nbuf, nw, lds, pw, lane, dr6);
     if constexpr (H)   // first half of the previous tile's tail
-      if (it > 0) producer_tail<0>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
+      if (it > 0) producer_tail<0, TR>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
     X3_SYNC();   // S3: the next tile's point rows are in LDS
     // the P1 rows travel during block3.0 / block3.2 (loads stay in flight across the barriers)
     p1e = fetch_p1(p1r, A, reinterpret_cast<const int*>(lds + L::OffPr) + nbuf * kXT, pw, lane);
@@ -980,7 +991,7 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
     // (h2) during block3.0: the second half of the previous tile's tail (its
     // accumulators are overwritten after this tile's S6)
     if constexpr (H)
-      if (it > 0) producer_tail<1>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
+      if (it > 0) producer_tail<1, TR>(A, lds, (it + 2) % 3, prev, pw, lane, ts, chk);
     X3_SYNC();   // S5
     X3_SYNC();   // S6
     pe_planes<H, 1, TR>(lds, pw, lane, dr6, &A, &g);   // during block3.2
@@ -989,8 +1000,8 @@ __device__ __forceinline__ void producer_loop(const X3Args& A, char* lds, int pw
   if constexpr (H) {
     // the last tile's tail (its accumulators were parked before the final S7)
     if (it > 0) {
-      producer_tail<0>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
-      producer_tail<1>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
+      producer_tail<0, TR>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
+      producer_tail<1, TR>(A, lds, (it - 1) % 3, prev, pw, lane, ts, chk);
     }
     if (A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
   } else {
@@ -1016,6 +1027,8 @@ __global__ void __launch_bounds__(512, 1) k_pairs_x3(X3Args A) { pairs_body<fals
 __global__ void __launch_bounds__(512, 1) k_pairs_h2(X3Args A) { pairs_body<true>(A); }
 // training forward (pnr_aggregate_fwd_train_x3): k_pairs_x3 + the saves of k_pairs<true>
 __global__ void __launch_bounds__(512, 1) k_pairs_x3_train(X3Args A) { pairs_body<false, true>(A); }
+// training forward on fp32h2 (pnr_aggregate_fwd_train_h2): k_pairs_h2 + the same saves, hid in fp32 rows
+__global__ void __launch_bounds__(512, 1) k_pairs_h2_train(X3Args A) { pairs_body<true, true>(A); }
 
 // ---------------------------------------------------------------------------
 // k_color_h2: the colour branch 280 -> 128 -> 128 -> 128 (LeakyReLU each,
@@ -1310,10 +1323,9 @@ template <bool H>
 int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const SplitW& wx,
                        const float* p1, float* hid, int32_t* vmask, float* out_feat, float* out_weight,
                        float* out_conf, int32_t* tile_ctr, hipStream_t st, const pnr_agg_saved* sv) {
-  PNR_CHECK_ARG(!(H && sv), "pairs_split: training saves are x3-only");
-  const void* fn = H ? reinterpret_cast<const void*>(&k_pairs_h2)
+  const void* fn = H ? (sv ? reinterpret_cast<const void*>(&k_pairs_h2_train) : reinterpret_cast<const void*>(&k_pairs_h2))
                      : (sv ? reinterpret_cast<const void*>(&k_pairs_x3_train) : reinterpret_cast<const void*>(&k_pairs_x3));
-  static bool attr[2] = {false, false};
+  static bool attr[2] = {false, false};   // (per H instantiation)
   if (!attr[sv ? 1 : 0]) {
     PNR_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)XL<H>::Lds));
     attr[sv ? 1 : 0] = true;
@@ -1334,7 +1346,9 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
   else memset(&a.sv, 0, sizeof(a.sv));
   PNR_HIP(hipMemsetAsync(tile_ctr, 0, 8 * sizeof(int32_t), st));
   const int64_t tiles = cdiv(s.n_max, kXTS);
-  if (H)
+  if (H && sv)
+    hipLaunchKernelGGL(k_pairs_h2_train, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
+  else if (H)
     hipLaunchKernelGGL(k_pairs_h2, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
   else if (sv)
     hipLaunchKernelGGL(k_pairs_x3_train, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);

@@ -4,6 +4,9 @@
 //   kind 0 (fp32, v_mfma_f32_32x32x2_f32):  F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)]
 //   kind 1 (fp32x3, v_mfma_f32_32x32x16_bf16): F[t][T][plane][h][r][j] = plane of W'[32T + r][16t + 8h + j]
 //     (planes: exact 3-way bf16 split, round-to-nearest-even, = aggregator.split3_bf16)
+//   pnr_pack_weights_h2 (fp32h2, v_mfma_f32_32x32x16_f16): F[t][T][plane][h][r][j] = plane of
+//     (2^-s W')[32T + r][16t + 8h + j], planes (Wh, Wl) of splith (= aggregator.frag_pack_h2
+//     with a given shift s); the flag is raised when some |2^-s W'| >= 16 or is not finite
 // W' = [W | bias | 0] (bias = input column kin when given), W[o][k] at
 // W + o * ld_row + k * ld_col (a transposed view packs without a copy).
 #include "agg_common.h"
@@ -45,9 +48,51 @@ __global__ void k_pack_x3(const float* __restrict__ W, int64_t lr, int64_t lc, i
   }
 }
 
+__global__ void k_pack_h2(const float* __restrict__ W, int64_t lr, int64_t lc, int NT, int kin,
+                          const float* __restrict__ bias, int64_t total, float sc, int32_t* __restrict__ flag,
+                          uint4* __restrict__ out) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i & 31), h = (int)((i >> 5) & 1);
+    const int64_t tT = i >> 6;
+    const int T = (int)(tT % NT), t = (int)(tT / NT);
+    const int o = 32 * T + r, k0 = 16 * t + 8 * h;
+    unsigned w[2][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float a = wprime(W, lr, lc, kin, bias, o, k0 + 2 * q) * sc;
+      const float b = wprime(W, lr, lc, kin, bias, o, k0 + 2 * q + 1) * sc;
+      bad |= !(fabsf(a) < 16.f) || !(fabsf(b) < 16.f);
+      splith(a, b, w[0][q], w[1][q]);
+    }
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      out[((tT * 2 + pl) * 2 + h) * 32 + r] = make_uint4(w[pl][0], w[pl][1], w[pl][2], w[pl][3]);
+  }
+  if (bad && flag) atomicOr(flag, 1);
+}
+
 }  // namespace pnr
 
 using namespace pnr;
+
+extern "C" int pnr_pack_weights_h2(const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f, int32_t kin,
+                                   const float* bias, int32_t pad_steps, int32_t shift, int32_t* range_flag,
+                                   void* out, size_t out_bytes, void* stream) {
+  PNR_CHECK_ARG(W && out && out_f > 0 && out_f % 32 == 0 && kin > 0 && pad_steps >= 0 && shift > -120 && shift < 120,
+                "pack_weights_h2: bad args (out_f %d, kin %d, shift %d)", out_f, kin, shift);
+  PNR_CHECK_ARG(((uintptr_t)out & 15) == 0, "pack_weights_h2: output must be 16-B aligned");
+  const int cols = kin + (bias ? 1 : 0);
+  const int NT = out_f / 32;
+  const int64_t tot = (cols + 15) / 16 + pad_steps;
+  const int64_t total = tot * NT * 64;   // threads: (t, T, h, r)
+  PNR_CHECK_ARG(out_bytes >= (size_t)total * 2 * 16, "pack_weights_h2: output too small (%zu < %lld)", out_bytes,
+                (long long)total * 32);
+  hipLaunchKernelGGL(k_pack_h2, dim3(grid_for(total, 256)), dim3(256), 0, as_stream(stream), W, ld_row, ld_col, NT,
+                     kin, bias, total, ldexpf(1.f, -shift), range_flag, static_cast<uint4*>(out));
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
 
 extern "C" int pnr_pack_weights(int32_t kind, const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f,
                                 int32_t kin, const float* bias, int32_t pad_steps, void* out, size_t out_bytes,

@@ -21,6 +21,7 @@
 // conflict-free B reads), so each input element is read from HBM ~3 times
 // (once per output row) instead of 9.  Zero padding 1 as in the reference.
 #include "pnr_common.h"
+#include "agg_common.h"
 
 namespace pnr {
 
@@ -453,6 +454,416 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
   return PNR_OK;
 }
 
+// ------------------------------------------------------------- fp32h2 convs
+// The same convolutions with fp32 accuracy on v_mfma_f32_32x32x16_f16 (the
+// MLP's fp32h2 split, DESIGN §13, applied to the 2-D renderer): every staged
+// input value x is split as x = xh + 2^-11 xl (f16 planes, splith) and every
+// weight as W' = Wh + 2^-11 Wl (frag_pack_h2, per-stage scale 2^-s so
+// |W'| < 16), and W.x = 2^-11 (Ws.xh + Wl.xh + Wh.xl), Ws = 2^11 Wh: three f16
+// products with fp32 accumulation per 16 k, instead of eight 32x32x2 fp32
+// MFMAs (5.3x the MFMA rate).
+// Range: each image is staged times 2^e (exact), e chosen on the device from
+// the image's max |value| (an absmax word its producer atomicMax-es: the
+// previous stage's epilogue, k_nr_absmax, or the rgb-gradient kernel) so that
+// max |x 2^e| lies in [2^14, 2^15): no f16 overflow for any input magnitude,
+// and tiny images (gradients) keep their relative precision; no host sync and
+// no fallback path.  The stacked rows [trunk; rgb; 0] all run as MFMA tiles
+// (the rgb rows' tile: 3 live rows of 32; the MFMAs are cheap at this rate).
+constexpr int kHPx = 128;                 // pixels per tile (4 waves x 32)
+constexpr int kHCh = 32;                  // input channels per LDS chunk (2 k-steps per tap)
+constexpr int kHPitch = 40;               // f16 per staged pixel per plane: 80 B, ds_read_b128 conflict-free
+constexpr int kHRowPx = kHPx + 2;
+constexpr int kHWD = 3;                   // weight fragments prefetched this many k-steps ahead
+template <int RO>
+constexpr size_t conv_h2_lds() {
+  return (size_t)(RO + 2) * kHRowPx * 2 * kHPitch * sizeof(_Float16);
+}
+
+// 2^e with max|x| 2^e in [2^14, 2^15) from the image's absmax bits (1 for an
+// all-zero or non-finite image, whose infs / NaNs then propagate as in fp32).
+__device__ __forceinline__ float img_scale(const unsigned* w) {
+  const float m = __uint_as_float(*w);
+  if (!(m > 0.f) || !(m <= 3.0e38f)) return 1.f;
+  int E;
+  (void)frexpf(m, &E);
+  int e = 15 - E;
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  return ldexpf(1.f, e);
+}
+// running max |v|; a NaN counts as +inf (its image then stages unscaled)
+__device__ __forceinline__ float amax_upd(float m, float v) {
+  const float a = fabsf(v);
+  return a != a ? __builtin_inff() : fmaxf(m, a);
+}
+__device__ __forceinline__ void amax_commit(float m, unsigned* w) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(w, __float_as_uint(m));
+}
+
+__global__ void k_nr_absmax(const float4* __restrict__ x, int64_t n4, unsigned* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x[i];
+    m = amax_upd(amax_upd(amax_upd(amax_upd(m, v.x), v.y), v.z), v.w);
+  }
+  amax_commit(m, out);
+}
+
+struct ConvH2Args {
+  const float* in;          // [H, W, Cin] fp32, Cin % 32 == 0
+  int H, W, Cin;
+  const unsigned* in_max;   // absmax bits of `in`
+  const uint4* wp;          // frag_pack_h2 of the stacked rows [32 NT, 9 Cin] (k = tap * Cin + ci)
+  float wscale;             // its 2^(s - 11)
+  const float* bias;        // forward: [32 NT] stacked biases (trunk, rgb, 0)
+  int cout;                 // trunk rows (forward) / rows written (data gradient)
+  float* out;               // [H, W, ldo]
+  int ldo;
+  unsigned* out_max;        // absmax bits of `out` (may be NULL)
+  float* rgb;               // forward: [H, W, 3], rows cout .. cout + 2 (rgb_mode as ConvArgs)
+  int rgb_mode;
+  float slope;
+  const float* act;         // BWD 2: [H, W, cout] forward activation whose LeakyReLU mask applies
+  int cin_real;             // BWD: input channels >= cin_real are zero padding (skipped)
+};
+
+// BWD: 0 forward, 1 data gradient, 2 data gradient times lrelu'(act).  RO
+// output rows per tile; a 4-wave workgroup owns RO rows x 128 pixels, wave w
+// pixels 32 w .. 32 w + 31 of every row.
+template <int NT, int BWD, int RO>
+__global__ void __launch_bounds__(256, 2) k_conv3x3_h2(ConvH2Args a) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
+  constexpr int PL = (RO + 2) * kHRowPx * kHPitch;   // f16 per plane
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int segs = (a.W + kHPx - 1) / kHPx;
+  const int64_t ntiles = (int64_t)((a.H + RO - 1) / RO) * segs;
+  const float xs = img_scale(a.in_max);
+  const float osc = a.wscale / xs;
+  const int ktap = a.Cin / 16;             // k-steps per tap
+  const uint4* wp = a.wp + lane;
+  float amax = 0.f;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int y0 = (int)(tile / segs) * RO;
+    const int x0 = (int)(tile % segs) * kHPx;
+    f32x16 acc[RO][NT];
+#pragma unroll
+    for (int o = 0; o < RO; ++o)
+#pragma unroll
+      for (int T = 0; T < NT; ++T) acc[o][T] = (f32x16){0.f};
+    for (int ci0 = 0; ci0 < a.Cin; ci0 += kHCh) {
+      int nreal = kHCh;   // staged channels: chunks' zero-padding tails of the backward's cat images skipped
+      if (BWD) {
+        const int r = a.cin_real - ci0;
+        nreal = r <= 0 ? 0 : (r >= kHCh ? kHCh : (r + 15) / 16 * 16);
+      }
+      if (nreal == 0) break;
+      const int nq = nreal / 4;
+      for (int i = threadIdx.x; i < (RO + 2) * kHRowPx * nq; i += 256) {
+        const int q = i % nq;
+        const int px = (i / nq) % kHRowPx;
+        const int r = i / (nq * kHRowPx);
+        const int yy = y0 - 1 + r, xx = x0 - 1 + px;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+          v = *reinterpret_cast<const float4*>(a.in + ((int64_t)yy * a.W + xx) * a.Cin + ci0 + 4 * q);
+        unsigned h0, h1, l0, l1;
+        splith(v.x * xs, v.y * xs, h0, l0);
+        splith(v.z * xs, v.w * xs, h1, l1);
+        _Float16* d = lds_h + (r * kHRowPx + px) * kHPitch + 4 * q;
+        *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(d + PL) = make_uint2(l0, l1);
+      }
+      __syncthreads();
+      const int pcol = 32 * wid + c;
+      // chunk step i = 2 tap + s: k-step tap * ktap + ci0 / 16 + s; weights kHWD steps ahead
+      auto wstep = [&](int i) { return (i >> 1) * ktap + (ci0 >> 4) + (i & 1); };
+      uint4 wh[kHWD][NT], wl[kHWD][NT];
+#pragma unroll
+      for (int d = 0; d < kHWD; ++d)
+#pragma unroll
+        for (int T = 0; T < NT; ++T) {
+          wh[d][T] = wp[((wstep(d) * NT + T) * 2 + 0) * 64];
+          wl[d][T] = wp[((wstep(d) * NT + T) * 2 + 1) * 64];
+        }
+#pragma unroll
+      for (int i0 = 0; i0 < 18; i0 += kHWD) {
+#pragma unroll
+        for (int d = 0; d < kHWD; ++d) {
+          const int i = i0 + d;
+          const int tap = i >> 1, s = i & 1;
+          const int dy = tap / 3, dx = tap % 3;
+          if (!BWD || 16 * s < nreal) {
+            uint4 xh[RO], xl[RO];
+#pragma unroll
+            for (int o = 0; o < RO; ++o) {
+              const _Float16* b = lds_h + ((dy + o) * kHRowPx + pcol + dx) * kHPitch + 16 * s + 8 * h;
+              xh[o] = *reinterpret_cast<const uint4*>(b);
+              xl[o] = *reinterpret_cast<const uint4*>(b + PL);
+            }
+#pragma unroll
+            for (int T = 0; T < NT; ++T) {
+              const uint4 ws = f16x8_scale2048(wh[d][T]);
+#pragma unroll
+              for (int o = 0; o < RO; ++o) {
+                acc[o][T] = mfma_f16(ws, xh[o], acc[o][T]);
+                acc[o][T] = mfma_f16(wl[d][T], xh[o], acc[o][T]);
+                acc[o][T] = mfma_f16(wh[d][T], xl[o], acc[o][T]);
+              }
+            }
+          }
+          if (i + kHWD < 18) {   // refills run for skipped steps too (in-bounds: the pack's zero tail)
+#pragma unroll
+            for (int T = 0; T < NT; ++T) {
+              wh[d][T] = wp[((wstep(i + kHWD) * NT + T) * 2 + 0) * 64];
+              wl[d][T] = wp[((wstep(i + kHWD) * NT + T) * 2 + 1) * 64];
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // epilogue.  C/D layout: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h, pixel c
+    const int xo = x0 + 32 * wid + c;
+#pragma unroll
+    for (int o = 0; o < RO; ++o) {
+      const int y = y0 + o;
+      if (xo >= a.W || y >= a.H) continue;
+      const int64_t pix = (int64_t)y * a.W + xo;
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float v = acc[o][T][r] * osc;
+          if (BWD) {
+            if (co < a.cout) {
+              // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
+              if (BWD == 2 && !(a.act[pix * a.cout + co] > 0.f)) v *= a.slope;
+              a.out[pix * a.ldo + co] = v;
+              amax = amax_upd(amax, v);
+            }
+          } else if (co < a.cout) {
+            v += a.bias[co];
+            v = v > 0.f ? v : v * a.slope;
+            a.out[pix * a.ldo + co] = v;
+            amax = amax_upd(amax, v);
+          } else if (co < a.cout + 3) {
+            v += a.bias[co];
+            float* op = a.rgb + pix * 3 + (co - a.cout);
+            if (a.rgb_mode == 0) *op = v;
+            else if (a.rgb_mode == 1) *op += v;
+            else *op = 1.f / (1.f + expf(-(*op + v)));
+          }
+        }
+    }
+  }
+  if (a.out_max) amax_commit(amax, a.out_max);
+}
+
+template <int NT, int BWD>
+static int launch_conv_h2(const ConvH2Args& a, hipStream_t st) {
+  constexpr int RO = 1;
+  static bool attr = false;
+  if (!attr) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3_h2<NT, BWD, RO>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv_h2_lds<RO>()));
+    attr = true;
+  }
+  const int64_t tiles = (int64_t)((a.H + RO - 1) / RO) * ((a.W + kHPx - 1) / kHPx);
+  hipLaunchKernelGGL((k_conv3x3_h2<NT, BWD, RO>), dim3(grid_for(tiles, 1, 256 * 4)), dim3(256), conv_h2_lds<RO>(),
+                     st, a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+// Weight gradient on fp32h2: dW[m, (3 ky + kx) C + ci] = sum_p dY[p, m] X[p + (ky-1) W + kx - 1, ci]
+// (zero where x + kx - 1 leaves the row or the source leaves the image), db[m] = sum_p dY[p, m].
+// Both operands are activations, so both are split and scaled: dY staged times
+// 2^e with max in [8, 16) (so Ys = 2^11 Yh stays in f16), X times 2^e' with max
+// in [2^14, 2^15); dW = 2^-11 (Ys.Xh + Yl.Xh + Yh.Xl) / (2^e 2^e').  k = pixel:
+// per 32-pixel chunk (two 16-pixel k-steps) dY is staged transposed as
+// [plane][m][32 px] and X as three kx-shifted copies [kx][plane][ci][32 px]
+// (the row-edge and image-edge zeros applied while staging), each lane
+// transposing 8 pixels x 4 channels in registers; 80-B rows, conflict-free
+// ds_read_b128 A and B fragments.  One 4-wave workgroup per (pixel split, ky);
+// wave w takes column tiles j = w, w + 4, w + 8 of the 3 NC (kx, channel-tile)
+// pairs x all MT row tiles.  db from the fp32 values while staging (ky = 0
+// blocks).  Partials per split, summed in fixed order (k_sum_splits).
+template <int MT, int NC>
+__global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const unsigned* y_max, const unsigned* x_max) {
+  constexpr int M = 32 * MT, C = 32 * NC;
+  constexpr int PA = M * kHPitch, PB = C * kHPitch;      // f16 per plane
+  constexpr int NJ = 3 * NC, JW = (NJ + 3) / 4;
+  __shared__ __attribute__((aligned(16))) _Float16 as_h[2 * PA];
+  __shared__ __attribute__((aligned(16))) _Float16 bs_h[3 * 2 * PB];
+  __shared__ float dbs[4][M];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int split = blockIdx.x, ky = blockIdx.y;
+  const int npix = a.H * a.W;
+  const int pbeg = split * (int)a.chunk;
+  const int pend = pbeg + (int)a.chunk < npix ? pbeg + (int)a.chunk : npix;
+  // dY to max [8, 16), X to max [2^14, 2^15)
+  float ys = img_scale(y_max) * (1.f / 2048.f);
+  const float xs = img_scale(x_max);
+  const float osc = 1.f / (2048.f * ys * xs);
+  f32x16 acc[JW][MT];
+#pragma unroll
+  for (int u = 0; u < JW; ++u)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[u][t] = (f32x16){0.f};
+  float db[4] = {0.f, 0.f, 0.f, 0.f};
+  // staging tasks: A: tid < M -> (m quad qa, pixel octet oa); B: (kx, ci quad, octet)
+  const int qa = tid % (M / 4), oa = tid / (M / 4);
+  auto put8x4 = [](_Float16* base, int pitch_pl, const float4 (&v)[8], float s) {
+    // 8 pixels x 4 channels -> per channel k: [hi 8 px] at base + k * kHPitch, lo at + pitch_pl
+    const float* f = reinterpret_cast<const float*>(v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      unsigned hi[4], lo[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) splith(f[8 * j + k] * s, f[8 * j + 4 + k] * s, hi[j], lo[j]);
+      *reinterpret_cast<uint4*>(base + k * kHPitch) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+      *reinterpret_cast<uint4*>(base + k * kHPitch + pitch_pl) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    }
+  };
+  for (int p0 = pbeg; p0 < pend; p0 += 32) {
+    if (tid < M) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = p0 + 8 * oa + j;
+        v[j] = p < pend ? *reinterpret_cast<const float4*>(a.dy + (int64_t)p * M + 4 * qa)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        db[0] += v[j].x;
+        db[1] += v[j].y;
+        db[2] += v[j].z;
+        db[3] += v[j].w;
+      }
+      put8x4(as_h + (4 * qa) * kHPitch + 8 * oa, PA, v, ys);
+    }
+    for (int i = tid; i < 3 * C; i += 256) {
+      const int kx = i / C, r = i % C, q = r % (C / 4), o = r / (C / 4);
+      float4 v[8];
+      const int pf = p0 + 8 * o;
+      int x = pf % a.W;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = pf + j;
+        const int sp = p + (ky - 1) * a.W + kx - 1, xsrc = x + kx - 1;
+        v[j] = p < pend && sp >= 0 && sp < npix && xsrc >= 0 && xsrc < a.W
+                   ? *reinterpret_cast<const float4*>(a.x + (int64_t)sp * C + 4 * q)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        x = x + 1 == a.W ? 0 : x + 1;
+      }
+      put8x4(bs_h + kx * 2 * PB + (4 * q) * kHPitch + 8 * o, PB, v, xs);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 ys_[MT], yl_[MT], yh_[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const _Float16* pa = as_h + (32 * t + c) * kHPitch + 16 * s + 8 * h;
+        yh_[t] = *reinterpret_cast<const uint4*>(pa);
+        yl_[t] = *reinterpret_cast<const uint4*>(pa + PA);
+        ys_[t] = f16x8_scale2048(yh_[t]);
+      }
+#pragma unroll
+      for (int u = 0; u < JW; ++u) {
+        const int j = wid + 4 * u;
+        if (j < NJ) {
+          const int kx = j / NC, nc = j - kx * NC;
+          const _Float16* pb = bs_h + kx * 2 * PB + (32 * nc + c) * kHPitch + 16 * s + 8 * h;
+          const uint4 xh = *reinterpret_cast<const uint4*>(pb);
+          const uint4 xl = *reinterpret_cast<const uint4*>(pb + PB);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            acc[u][t] = mfma_f16(ys_[t], xh, acc[u][t]);
+            acc[u][t] = mfma_f16(yl_[t], xh, acc[u][t]);
+            acc[u][t] = mfma_f16(yh_[t], xl, acc[u][t]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int N = 9 * C;
+  float* out = a.part + (int64_t)split * ((int64_t)M * N + M);
+#pragma unroll
+  for (int u = 0; u < JW; ++u) {
+    const int j = wid + 4 * u;
+    if (j >= NJ) continue;
+    const int kx = j / NC, nc = j - kx * NC;
+    const int col = (3 * ky + kx) * C + 32 * nc + c;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + col] = acc[u][t][r] * osc;
+  }
+  if (ky == 0) {   // db: the four pixel octets' sums per channel, octet order
+    if (tid < M) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dbs[oa][4 * qa + k] = db[k];
+    }
+    __syncthreads();
+    if (tid < M) out[(int64_t)M * N + tid] = ((dbs[0][tid] + dbs[1][tid]) + dbs[2][tid]) + dbs[3][tid];
+  }
+}
+
+template <int MT, int NC>
+static int launch_wgrad_h2(const float* dyb, const unsigned* y_max, const float* x, const unsigned* x_max, int H,
+                           int W, float* part, float* dw, hipStream_t st) {
+  WgradArgs g;
+  g.dy = dyb;
+  g.x = x;
+  g.H = H;
+  g.W = W;
+  g.M = 32 * MT;
+  g.Cin = 32 * NC;
+  int ns;
+  wgrad_plan((int64_t)H * W, g.M, g.Cin, &ns, &g.chunk);
+  g.part = part;
+  hipLaunchKernelGGL((k_conv_wgrad_h2<MT, NC>), dim3(ns, 3), dim3(256), 0, st, g, y_max, x_max);
+  PNR_LAUNCH_CHECK();
+  const int64_t n = (int64_t)g.M * 9 * g.Cin + g.M;
+  hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, part, n, ns, dw, (int64_t)0,
+                     (int64_t)0);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+// k_nr_rgb_grad plus max |g| into the absmax words of the three cat images
+__global__ void k_nr_rgb_grad_h2(const float* __restrict__ d_out, const float* __restrict__ out_rgb, int64_t npix,
+                                 float* __restrict__ cat2, float* __restrict__ cat1, float* __restrict__ cat0,
+                                 unsigned* __restrict__ words) {
+  float m = 0.f;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    float g[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float s = out_rgb[p * 3 + j];
+      g[j] = d_out[p * 3 + j] * (s * (1.f - s));
+      m = amax_upd(m, g[j]);
+    }
+    float* c2 = cat2 + p * 32;
+    float* c1 = cat1 + p * 64;
+    float* c0 = cat0 + p * 96;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const float v = j < 3 ? g[j] : 0.f;
+      c2[j] = v;
+      c1[32 + j] = v;
+      c0[64 + j] = v;
+    }
+  }
+  amax_commit(m, words + 0);
+  amax_commit(m, words + 1);
+  amax_commit(m, words + 2);
+}
+
 }  // namespace pnr
 
 using namespace pnr;
@@ -605,4 +1016,170 @@ extern "C" int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, c
   a.act = nullptr;
   if ((rc = launch_conv<4, 1>(a, st))) return rc;
   return launch_wgrad<3, 4, true>(cat0, x, H, W, 128, part, dw0, st);
+}
+
+// ---------------------------------------------------------------- fp32h2 ABI
+extern "C" int pnr_neural_render_h2_scratch_bytes(int32_t H, int32_t W, size_t* out) {
+  PNR_CHECK_ARG(out && H >= 0 && W >= 0, "neural_render_h2_scratch_bytes: bad args");
+  *out = (size_t)H * W * (64 + 32) * sizeof(float) + 256;
+  return PNR_OK;
+}
+
+extern "C" int pnr_neural_render_fwd_h2(const float* x, int32_t H, int32_t W, const pnr_neural_render_h2w* w,
+                                        float* out_rgb, void* scratch, size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(x && w && out_rgb && scratch, "neural_render_h2: null pointer");
+  PNR_CHECK_ARG(w->wp0 && w->wp1 && w->wp2 && w->b0 && w->b1 && w->b2, "neural_render_h2: null weight");
+  PNR_CHECK_ARG(H >= 0 && W >= 0, "neural_render_h2: bad image size");
+  PNR_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+                "neural_render_h2: x and scratch must be 16-B aligned");
+  size_t need;
+  pnr_neural_render_h2_scratch_bytes(H, W, &need);
+  PNR_CHECK_ARG(scratch_bytes >= need, "neural_render_h2: scratch too small");
+  if (H == 0 || W == 0) return PNR_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t npix = (int64_t)H * W;
+  float* net0 = static_cast<float*>(scratch);
+  float* net1 = net0 + (size_t)npix * 64;
+  unsigned* words = reinterpret_cast<unsigned*>(net1 + (size_t)npix * 32);   // max |x|, |net0|, |net1|
+  PNR_HIP(hipMemsetAsync(words, 0, 16, st));
+  hipLaunchKernelGGL(k_nr_absmax, dim3(grid_for(npix * 32, 256, 2048)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(x), npix * 32, words);
+  PNR_LAUNCH_CHECK();
+  int rc;
+  ConvH2Args a;
+  a.H = H;
+  a.W = W;
+  a.slope = w->neg_slope;
+  a.act = nullptr;
+  a.cin_real = 1 << 30;
+  a.rgb = out_rgb;
+  // stage 0: x (128) -> [net0 (64), rgb = conv_rgb0(x)]
+  a.in = x;
+  a.Cin = 128;
+  a.in_max = words;
+  a.wp = static_cast<const uint4*>(w->wp0);
+  a.wscale = w->ws0;
+  a.bias = w->b0;
+  a.cout = 64;
+  a.out = net0;
+  a.ldo = 64;
+  a.out_max = words + 1;
+  a.rgb_mode = 0;
+  if ((rc = launch_conv_h2<3, 0>(a, st))) return rc;
+  // stage 1: net0 (64) -> [net1 (32), rgb += conv_rgb1(net0)]
+  a.in = net0;
+  a.Cin = 64;
+  a.in_max = words + 1;
+  a.wp = static_cast<const uint4*>(w->wp1);
+  a.wscale = w->ws1;
+  a.bias = w->b1;
+  a.cout = 32;
+  a.out = net1;
+  a.ldo = 32;
+  a.out_max = words + 2;
+  a.rgb_mode = 1;
+  if ((rc = launch_conv_h2<2, 0>(a, st))) return rc;
+  // stage 2: out = sigmoid(rgb + conv_rgb2(net1))
+  a.in = net1;
+  a.Cin = 32;
+  a.in_max = words + 2;
+  a.wp = static_cast<const uint4*>(w->wp2);
+  a.wscale = w->ws2;
+  a.bias = w->b2;
+  a.cout = 0;
+  a.out = nullptr;
+  a.ldo = 0;
+  a.out_max = nullptr;
+  a.rgb_mode = 2;
+  return launch_conv_h2<1, 0>(a, st);
+}
+
+extern "C" int pnr_neural_render_bwd_h2_scratch_bytes(int32_t H, int32_t W, size_t* out) {
+  PNR_CHECK_ARG(out && H >= 0 && W >= 0, "neural_render_bwd_h2_scratch_bytes: bad args");
+  return pnr_neural_render_bwd_scratch_bytes(H, W, out) == PNR_OK ? (*out += 256, PNR_OK) : PNR_EINVAL;
+}
+
+extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch, const float* out_rgb,
+                                        const float* d_out, int32_t H, int32_t W, const pnr_neural_render_h2wt* wt,
+                                        float* d_x, float* dw0, float* dw1, float* dw2, void* scratch,
+                                        size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(x && fwd_scratch && out_rgb && d_out && wt && d_x && dw0 && dw1 && dw2 && scratch,
+                "neural_render_bwd_h2: null pointer");
+  PNR_CHECK_ARG(wt->wt0 && wt->wt1 && wt->wt2, "neural_render_bwd_h2: null weight");
+  PNR_CHECK_ARG(H >= 0 && W >= 0 && (int64_t)H * W < (1ll << 30), "neural_render_bwd_h2: bad image size");
+  PNR_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)fwd_scratch & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+                "neural_render_bwd_h2: x, fwd_scratch and scratch must be 16-B aligned");
+  size_t need;
+  pnr_neural_render_bwd_h2_scratch_bytes(H, W, &need);
+  PNR_CHECK_ARG(scratch_bytes >= need, "neural_render_bwd_h2: scratch too small");
+  hipStream_t st = as_stream(stream);
+  const int64_t npix = (int64_t)H * W;
+  if (npix == 0) {
+    PNR_HIP(hipMemsetAsync(dw0, 0, (96 * 9 * 128 + 96) * sizeof(float), st));
+    PNR_HIP(hipMemsetAsync(dw1, 0, (64 * 9 * 64 + 64) * sizeof(float), st));
+    PNR_HIP(hipMemsetAsync(dw2, 0, (32 * 9 * 32 + 32) * sizeof(float), st));
+    return PNR_OK;
+  }
+  const float* net0 = fwd_scratch;
+  const float* net1 = fwd_scratch + (size_t)npix * 64;
+  const unsigned* fwords = reinterpret_cast<const unsigned*>(net1 + (size_t)npix * 32);   // the forward's max words
+  float* cat2 = static_cast<float*>(scratch);
+  float* cat1 = cat2 + (size_t)npix * 32;
+  float* cat0 = cat1 + (size_t)npix * 64;
+  unsigned* words = reinterpret_cast<unsigned*>(cat0 + (size_t)npix * 96);   // max |cat2|, |cat1|, |cat0|
+  float* part = cat0 + (size_t)npix * 96 + 64;
+  PNR_HIP(hipMemsetAsync(words, 0, 16, st));
+  hipLaunchKernelGGL(k_nr_rgb_grad_h2, dim3(grid_for(npix, 256, 2048)), dim3(256), 0, st, d_out, out_rgb, npix, cat2,
+                     cat1, cat0, words);
+  PNR_LAUNCH_CHECK();
+  int rc;
+  ConvH2Args a;
+  a.H = H;
+  a.W = W;
+  a.slope = wt->neg_slope;
+  a.bias = nullptr;
+  a.rgb = nullptr;
+  a.rgb_mode = 3;
+  // stage 2: d net1 = conv(cat2 = [g, 0], flipped conv_rgb.2), masked by net1 -> cat1[:, :32]
+  a.in = cat2;
+  a.Cin = 32;
+  a.in_max = words + 0;
+  a.cin_real = 3;
+  a.wp = static_cast<const uint4*>(wt->wt2);
+  a.wscale = wt->ws2;
+  a.cout = 32;
+  a.ldo = 64;
+  a.out = cat1;
+  a.out_max = words + 1;
+  a.act = net1;
+  if ((rc = launch_conv_h2<1, 2>(a, st))) return rc;
+  if ((rc = launch_wgrad_h2<1, 1>(cat2, words + 0, net1, fwords + 2, H, W, part, dw2, st))) return rc;
+  // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
+  a.in = cat1;
+  a.Cin = 64;
+  a.in_max = words + 1;
+  a.cin_real = 32 + 3;
+  a.wp = static_cast<const uint4*>(wt->wt1);
+  a.wscale = wt->ws1;
+  a.cout = 64;
+  a.ldo = 96;
+  a.out = cat0;
+  a.out_max = words + 2;
+  a.act = net0;
+  if ((rc = launch_conv_h2<2, 2>(a, st))) return rc;
+  if ((rc = launch_wgrad_h2<2, 2>(cat1, words + 1, net0, fwords + 1, H, W, part, dw1, st))) return rc;
+  // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
+  a.in = cat0;
+  a.Cin = 96;
+  a.in_max = words + 2;
+  a.cin_real = 64 + 3;
+  a.wp = static_cast<const uint4*>(wt->wt0);
+  a.wscale = wt->ws0;
+  a.cout = 128;
+  a.ldo = 128;
+  a.out = d_x;
+  a.out_max = nullptr;
+  a.act = nullptr;
+  if ((rc = launch_conv_h2<4, 1>(a, st))) return rc;
+  return launch_wgrad_h2<3, 4>(cat0, words + 2, x, fwords + 0, H, W, part, dw0, st);
 }

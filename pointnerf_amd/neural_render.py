@@ -5,8 +5,10 @@ models/neural_render/neural_renderer.py:7-104 for the configuration the fork
 builds, ``NeuralRenderer(input_dim=128)`` (neural_points_volumetric_model.py:258-260):
 n_feat 128 (conv_in = identity), img_size 64 -> 2 blocks, rgb skips, no norm,
 LeakyReLU(0.2), final sigmoid -- so ``neural_render_2d.*`` checkpoint keys load.
-Forward runs ``pnr_neural_render_fwd``: three fused implicit-GEMM 3x3
-convolutions on fp32 MFMA.  With autograd enabled ``NeuralRenderFn`` keeps the
+Forward runs ``pnr_neural_render_fwd_h2`` (``precision="fp32h2"``, the
+default): three fused implicit-GEMM 3x3 convolutions on f16 MFMA with the
+fp32h2 operand split (fp32 accuracy), or ``pnr_neural_render_fwd``
+(``precision="fp32"``) on fp32 MFMA.  With autograd enabled ``NeuralRenderFn`` keeps the
 forward's activations and its backward runs ``pnr_neural_render_bwd`` (data
 gradients as flipped-weight convolutions on the same kernel, weight gradients
 as implicit-GEMM reductions over the pixels, deterministic), the gradients of
@@ -22,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib as L
-from .aggregator import frag_pack
+from .aggregator import frag_pack, frag_pack_h2
 
 
 class NeuralRenderer(nn.Module):
@@ -39,6 +41,7 @@ class NeuralRenderer(nn.Module):
                                        nn.Conv2d(32, 3, 3, 1, 1)])
         self._packed = None
         self._packed_key = None
+        self.precision = "fp32h2"      # or "fp32": the convolutions on fp32 MFMA
 
     @staticmethod
     def _trunk(conv):
@@ -68,23 +71,61 @@ class NeuralRenderer(nn.Module):
         return self._packed
 
     @staticmethod
-    def _stack_t(trunk, rgb, rows):
+    def _stack(trunk, rgb, rows):
+        """A stage's stacked [trunk; rgb; 0] conv weights [rows, cin, 3, 3] and biases [rows]."""
+        convs = ([trunk] if trunk is not None else []) + [rgb]
+        W = torch.cat([cv.weight for cv in convs], 0).float()
+        b = torch.cat([cv.bias for cv in convs], 0).float()
+        Wp = torch.zeros((rows,) + tuple(W.shape[1:]), dtype=torch.float32, device=W.device)
+        bp = torch.zeros(rows, dtype=torch.float32, device=W.device)
+        Wp[: W.shape[0]] = W
+        bp[: b.shape[0]] = b
+        return Wp, bp
+
+    @classmethod
+    def _stack_t(cls, trunk, rgb, rows):
         """Data-gradient weights of a stage: the stacked [rows, cin, 3, 3] weights
         flipped and transposed to [cin, 9 * rows] (k = (ky'*3 + kx') * rows + j,
-        value W[j, ci, 2 - ky', 2 - kx']), fragment-packed (pnr_neural_render_wt)."""
-        ws = ([trunk.weight] if trunk is not None else []) + [rgb.weight]
-        W = torch.cat(ws, 0).float()
-        cin = W.shape[1]
-        Wp = torch.zeros((rows, cin, 3, 3), dtype=torch.float32, device=W.device)
-        Wp[: W.shape[0]] = W
-        return frag_pack(Wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, 9 * rows).contiguous())
+        value W[j, ci, 2 - ky', 2 - kx']) (pnr_neural_render_wt before packing)."""
+        Wp, _ = cls._stack(trunk, rgb, rows)
+        cin = Wp.shape[1]
+        return Wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, 9 * rows).contiguous()
+
+    def _stages(self):
+        return ((self.conv_layers[0], self.conv_rgb[0], 96), (self.conv_layers[1], self.conv_rgb[1], 64),
+                (None, self.conv_rgb[2], 32))
 
     def packed_t(self):
         with torch.no_grad():
-            t = dict(wt0=self._stack_t(self.conv_layers[0], self.conv_rgb[0], 96),
-                     wt1=self._stack_t(self.conv_layers[1], self.conv_rgb[1], 64),
-                     wt2=self._stack_t(None, self.conv_rgb[2], 32))
+            t = {f"wt{i}": frag_pack(self._stack_t(*st)) for i, st in enumerate(self._stages())}
         return L.NeuralRenderWT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(), 0.2), t
+
+    def packed_h2(self):
+        """fp32h2 forward packs: per stage frag_pack_h2 of the stacked rows
+        (k = (ky*3 + kx)*cin + ci) with its scale, and the stacked biases."""
+        ps = list(self.parameters())
+        key = ("h2",) + tuple((p.data_ptr(), p._version) for p in ps)
+        if self._packed is not None and key == self._packed_key:
+            return self._packed
+        t, sc = {}, []
+        with torch.no_grad():
+            for i, st in enumerate(self._stages()):
+                Wp, bp = self._stack(*st)
+                t[f"wp{i}"], s = frag_pack_h2(Wp.permute(0, 2, 3, 1).reshape(Wp.shape[0], -1).contiguous())
+                t[f"b{i}"] = bp.contiguous()
+                sc.append(s)
+        w = L.NeuralRenderH2W(t["wp0"].data_ptr(), t["wp1"].data_ptr(), t["wp2"].data_ptr(), *sc,
+                              t["b0"].data_ptr(), t["b1"].data_ptr(), t["b2"].data_ptr(), 0.2)
+        self._packed, self._packed_key = (w, t), key
+        return self._packed
+
+    def packed_t_h2(self):
+        t, sc = {}, []
+        with torch.no_grad():
+            for i, st in enumerate(self._stages()):
+                t[f"wt{i}"], s = frag_pack_h2(self._stack_t(*st))
+                sc.append(s)
+        return L.NeuralRenderH2WT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(), *sc, 0.2), t
 
     def forward_torch(self, x):
         """neural_renderer.py:81-104 with torch convolutions (autograd path)."""
@@ -104,12 +145,16 @@ class NeuralRenderer(nn.Module):
             raise L.PnrError("NeuralRenderer expects [1, H, W, 128]")
         xc = x.reshape(H * W, 128).float().contiguous()
         out = torch.empty((H * W, 3), dtype=torch.float32, device=x.device)
+        h2 = self.precision == "fp32h2"
+        sfx = "_h2" if h2 else ""
         nb = L.c_size_t(0)
-        L.check(L.lib().pnr_neural_render_scratch_bytes(H, W, L.ctypes.byref(nb)), "pnr_neural_render_scratch_bytes")
+        L.check(getattr(L.lib(), f"pnr_neural_render{sfx}_scratch_bytes")(H, W, L.ctypes.byref(nb)),
+                "pnr_neural_render_scratch_bytes")
         scratch = torch.empty(max(int(nb.value) // 4, 4), dtype=torch.float32, device=x.device)
-        w, _keep = self.packed()
-        L.check(L.lib().pnr_neural_render_fwd(L.ptr(xc), H, W, L.ctypes.byref(w), L.ptr(out), L.ptr(scratch),
-                                              scratch.numel() * 4, L.stream_ptr(x.device)), "pnr_neural_render_fwd")
+        w, _keep = self.packed_h2() if h2 else self.packed()
+        L.check(getattr(L.lib(), f"pnr_neural_render_fwd{sfx}")(
+            L.ptr(xc), H, W, L.ctypes.byref(w), L.ptr(out), L.ptr(scratch), scratch.numel() * 4,
+            L.stream_ptr(x.device)), "pnr_neural_render_fwd")
         return out, xc, scratch
 
     def forward(self, x):
@@ -128,7 +173,7 @@ class NeuralRenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mod, *params):
         out, xc, scratch = mod._fwd(x.detach())
-        ctx.mod, ctx.shape = mod, x.shape
+        ctx.mod, ctx.shape, ctx.h2 = mod, x.shape, mod.precision == "fp32h2"
         ctx.save_for_backward(xc, scratch, out)
         return out.view(1, *x.shape[1:3], 3)
 
@@ -140,14 +185,15 @@ class NeuralRenderFn(torch.autograd.Function):
         dev = xc.device
         f32 = dict(dtype=torch.float32, device=dev)
         d_out = d_out.reshape(H * W, 3).float().contiguous()
-        wt, _keep = mod.packed_t()
+        wt, _keep = mod.packed_t_h2() if ctx.h2 else mod.packed_t()
+        sfx = "_h2" if ctx.h2 else ""
         nb = L.c_size_t(0)
-        L.check(L.lib().pnr_neural_render_bwd_scratch_bytes(H, W, L.ctypes.byref(nb)),
+        L.check(getattr(L.lib(), f"pnr_neural_render_bwd{sfx}_scratch_bytes")(H, W, L.ctypes.byref(nb)),
                 "pnr_neural_render_bwd_scratch_bytes")
         scratch = torch.empty(max(int(nb.value) // 4, 4), **f32)
         d_x = torch.empty((H * W, 128), **f32)
         dws = [torch.empty(M * 9 * cin + M, **f32) for M, cin in ((96, 128), (64, 64), (32, 32))]
-        L.check(L.lib().pnr_neural_render_bwd(L.ptr(xc), L.ptr(fscr), L.ptr(out), L.ptr(d_out), H, W,
+        L.check(getattr(L.lib(), f"pnr_neural_render_bwd{sfx}")(L.ptr(xc), L.ptr(fscr), L.ptr(out), L.ptr(d_out), H, W,
                                               L.ctypes.byref(wt), L.ptr(d_x), *(L.ptr(d) for d in dws),
                                               L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
                 "pnr_neural_render_bwd")

@@ -164,7 +164,7 @@ class NeuralPointsRayMarching(nn.Module):
         self.precision = precision
         # render_rays_train's per-pair forward: "fp32x3" (split-bf16 MFMA,
         # fp32-accurate, the default) or "fp32" (native fp32 MFMA)
-        self.train_precision = "fp32x3"
+        self.train_precision = "fp32h2"   # per-pair forward chain: fp32h2 (f16 MFMA) / fp32x3 / fp32
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
         self.h2_fallbacks = 0
@@ -549,14 +549,16 @@ class NeuralPointsRayMarching(nn.Module):
             return None if t is None else t.reshape(n, c)
 
         used = (used_buf[:cnt["n_used"]], used_map)
-        if self.train_precision not in ("fp32", "fp32x3"):
-            raise L.PnrError(f"train_precision {self.train_precision!r}: 'fp32x3' or 'fp32'")
+        if self.train_precision not in ("fp32", "fp32x3", "fp32h2"):
+            raise L.PnrError(f"train_precision {self.train_precision!r}: 'fp32h2', 'fp32x3' or 'fp32'")
         spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd),
-                       used=used, x3=self.train_precision == "fp32x3")
+                       used=used, x3=self.train_precision == "fp32x3", h2=self.train_precision == "fp32h2")
         spec.keep_saved = self.keep_train_saved
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
                                  tab(np_.points_dir, 3), tab(np_.points_conf, 1),
                                  np_.xyz if np_.xyz.requires_grad else None, *agg_params(self.aggregator))
+        if spec.h2_fallback:
+            self.h2_fallbacks += 1
         if C == 3:
             feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
         cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))

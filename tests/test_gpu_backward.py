@@ -78,7 +78,7 @@ def _train_model(sc, cuda, params):
     return NeuralPointsRayMarching(sc["opt"], np_, agg.train())
 
 
-@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])
+@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3", "fp32h2"])
 def test_render_train_grads_vs_oracle(cuda, train_precision):
     """End to end: loss = <G, ray_color> through query -> aggregate -> composite;
     every point-table and MLP gradient vs torch autograd of the CPU oracle, with
@@ -157,7 +157,29 @@ def test_train_forward_x3_saves_match_fp32(cuda):
         m.train_precision = tp
         color = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0]
         out[tp] = (color.detach().clone(), m.last_train_aux["saved"], int(m.last_counts["S_valid"]))
-    (c32, s32, n), (c3, s3, n3) = out["fp32"], out["fp32x3"]
+    _check_saves_match(out["fp32"], out["fp32x3"])
+
+
+def test_train_forward_h2_saves_match_fp32(cuda):
+    """pnr_aggregate_fwd_train_h2 (k_pairs_h2 with the training saves, fp32 hid
+    rows) keeps the activations of the native-fp32 training forward, within the
+    same bounds as the fp32x3 forward; no range fallback on these weights."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.45))
+    m.keep_train_saved = True
+    campos, camrot = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    out = {}
+    for tp in ("fp32", "fp32h2"):
+        m.train_precision = tp
+        color = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0]
+        out[tp] = (color.detach().clone(), m.last_train_aux["saved"], int(m.last_counts["S_valid"]))
+    assert m.h2_fallbacks == 0
+    _check_saves_match(out["fp32"], out["fp32h2"])
+
+
+def _check_saves_match(ref, got):
+    (c32, s32, n), (c3, s3, n3) = ref, got
     assert n == n3 and n > 100
     P = n * 8
     assert torch.equal(s32["prow"][:P], s3["prow"][:P])
@@ -269,7 +291,7 @@ def test_conf_coefficient_and_zero_one_loss(cuda):
     close(m.neural_points.points_conf.grad.reshape(-1), conf.grad, "d points_conf (zero_one)", scale=5e-4)
 
 
-@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])
+@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3", "fp32h2"])
 def test_train_backward_repeatable(cuda, train_precision):
     """identical training steps give the same gradients.
     Point-table gradients are float-atomic sums over pairs, so run to run they
@@ -313,7 +335,7 @@ def _w2pers_torch(p, campos, camrot):
     return torch.stack([xc[0] / xc[2], xc[1] / xc[2], xc[2]], -1)
 
 
-@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])
+@pytest.mark.parametrize("train_precision", ["fp32", "fp32x3", "fp32h2"])
 def test_render_train_xyz_grad_vs_oracle(cuda, train_precision):
     """--xyz_grad 1 (neural_points.py:270): d xyz through the world distance
     (PE_5 channels 0..2, the normalised inverse-distance weights) and the

@@ -22,6 +22,15 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --config $s --steps 3 --warmup 1 --emulate-world 8 --no-cpu-baseline \
         > $O/bench_${s}_ew8.json 2> $O/bench_${s}_ew8.err || { tail -20 $O/bench_${s}_ew8.err; exit 1; }
       cut -c1-400 $O/bench_$s.json ;;
+    nr)
+      timeout -k 10 300 python tools/nr_bench.py > $O/nr.json 2> $O/nr.err || { tail -20 $O/nr.err; exit 1; }
+      cat $O/nr.json
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/nrstats -o run -- \
+        python tools/nr_bench.py > $O/nrstats.log 2>&1 || { tail -20 $O/nrstats.log; exit 1; } ;;
+    tnr)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_neural_render.py -m gpu -x -v --timeout 120 \
+        --timeout-method thread > $O/t_nr.log 2>&1 || { tail -40 $O/t_nr.log; exit 1; }
+      tail -3 $O/t_nr.log ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
         python bench.py --no-cpu-baseline > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; } ;;
