@@ -76,7 +76,7 @@ def parse():
                     help="fp32h2 pairs stage: k_pairs_h2 (wt) or the activation-stationary k_pairs_as (as)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
-    ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32h2",
+    ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32x3",
                     help="--mode train: the training forward's per-pair chain (fp32h2 split-f16 MFMA, fp32x3 "
                          "split-bf16 MFMA or native fp32)")
     ap.add_argument("--mode", choices=("render", "train"), default="render",

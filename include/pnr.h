@@ -422,7 +422,9 @@ int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_samples* s, cons
 /* Same, for the PointAggregator.forward mirror (pre-gathered tables, pair_mask). */
 /* pnr_aggregate_fwd_train with the per-pair chain on the fp32h2 kernel of
  * pnr_aggregate_fwd_h2 (k_pairs_h2 + the same saves; wh's w1bh / w2h / w3h / w4h
- * packs and scales, the range flag as pnr_aggregate_fwd_h2: set when an
+ * packs and scales, and w1ah / scale1a when set: P1 on k_point_pre_h2, else on
+ * fp32 MFMA; the colour packs are unused: the colour branch runs the fp32
+ * training kernel), the range flag as pnr_aggregate_fwd_h2: set when an
  * activation left the f16 range, the caller then re-runs the step on
  * pnr_aggregate_fwd_train_x3).  Saved layout and outputs as the fp32 call. */
 int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
@@ -483,6 +485,13 @@ int pnr_pack_weights(int32_t kind, const float* W, int64_t ld_row, int64_t ld_co
 int pnr_pack_weights_h2(const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f, int32_t kin,
                         const float* bias, int32_t pad_steps, int32_t shift, int32_t* range_flag, void* out,
                         size_t out_bytes, void* stream);
+/* pnr_pack_weights_h2 with the shift picked on the device (no host read of the
+ * weights): s such that max |2^-s W'| lies in [8, 16) (0 for an all-zero or
+ * non-finite W', as aggregator.h2_shift), scale_dev[0] = 2^(s - 11) (the
+ * consumer's accumulator factor), scale_dev[1] is scratch. */
+int pnr_pack_weights_h2_dev(const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f, int32_t kin,
+                            const float* bias, int32_t pad_steps, float* scale_dev, void* out, size_t out_bytes,
+                            void* stream);
 /* Same, with the three dX GEMMs on fp32x3 split-bf16 MFMA: wbx = frag_pack_x3 of
  * block3.2.weight^T, block3.0.weight[:, :256]^T, block1.2.weight^T (aggregator.py;
  * 16-B aligned); wb supplies w3e (w4t / w3t / w2t unused, may be NULL). */
@@ -635,7 +644,8 @@ int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, const float*
  * (fp32h2, the MLP's split: x = xh + 2^-11 xl per input value, W' = Wh +
  * 2^-11 Wl per weight, three f16 products per 16 k).  Per stage s the stacked
  * [trunk; rgb; 0] rows (96 / 64 / 32 rows, columns k = (ky*3 + kx)*cin + ci)
- * as frag_pack_h2 packs wp_s with their scales ws_s = 2^(shift - 11), and the
+ * as frag_pack_h2 packs wp_s with their scales ws[s] = 2^(shift - 11) in device
+ * memory (pnr_pack_weights_h2_dev: packs rebuilt without a host sync), and the
  * stacked biases b_s (96 / 64 / 32 floats: trunk, rgb, 0).  Each image is
  * staged times a power of two chosen on the device from its max |value|, so
  * any finite input magnitude keeps fp32-level relative accuracy (no range
@@ -643,7 +653,8 @@ int pnr_neural_render_bwd(const float* x, const float* fwd_scratch, const float*
  * absmax words (the backward reads them from fwd_scratch). */
 typedef struct {
   const void* wp0; const void* wp1; const void* wp2;
-  float ws0, ws1, ws2;
+  const float* ws;                          /* device [6]: stage s's scale at ws[2 s] (pnr_pack_weights_h2_dev's
+                                               scale_dev = ws + 2 s; ws[2 s + 1] its scratch) */
   const float* b0; const float* b1; const float* b2;
   float neg_slope;
 } pnr_neural_render_h2w;
@@ -655,7 +666,7 @@ typedef struct {
  * absmax words).  Fixed-order reductions: bitwise repeatable. */
 typedef struct {
   const void* wt0; const void* wt1; const void* wt2;
-  float ws0, ws1, ws2;
+  const float* ws;                          /* device [6], as pnr_neural_render_h2w */
   float neg_slope;
 } pnr_neural_render_h2wt;
 

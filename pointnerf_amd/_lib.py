@@ -75,13 +75,12 @@ class NeuralRenderWT(ctypes.Structure):
 
 
 class NeuralRenderH2W(ctypes.Structure):
-    _fields_ = [("wp0", c_void_p), ("wp1", c_void_p), ("wp2", c_void_p), ("ws0", c_float), ("ws1", c_float),
-                ("ws2", c_float), ("b0", c_void_p), ("b1", c_void_p), ("b2", c_void_p), ("neg_slope", c_float)]
+    _fields_ = [("wp0", c_void_p), ("wp1", c_void_p), ("wp2", c_void_p), ("ws", c_void_p), ("b0", c_void_p),
+                ("b1", c_void_p), ("b2", c_void_p), ("neg_slope", c_float)]
 
 
 class NeuralRenderH2WT(ctypes.Structure):
-    _fields_ = [("wt0", c_void_p), ("wt1", c_void_p), ("wt2", c_void_p), ("ws0", c_float), ("ws1", c_float),
-                ("ws2", c_float), ("neg_slope", c_float)]
+    _fields_ = [("wt0", c_void_p), ("wt1", c_void_p), ("wt2", c_void_p), ("ws", c_void_p), ("neg_slope", c_float)]
 
 
 class MlpBf16(ctypes.Structure):
@@ -183,6 +182,8 @@ SIGNATURES = {
     "pnr_pairs_to_points": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_pack_weights_h2": (c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32, c_int32,
                                     c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_pack_weights_h2_dev": (c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,
+                                        c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_pack_weights": (c_int, [c_int32, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,
                                  c_void_p, c_size_t, c_void_p]),
     "pnr_gemm_tn_scratch_bytes": (c_int, [c_int64, c_int32, c_int32, P(c_size_t)]),

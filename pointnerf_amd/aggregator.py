@@ -104,6 +104,23 @@ def _pack_h2_device(W: torch.Tensor, bias: torch.Tensor | None, shift: int, flag
     return out
 
 
+def pack_h2_dev(W: torch.Tensor, bias: torch.Tensor | None, scale_out: torch.Tensor) -> torch.Tensor:
+    """pnr_pack_weights_h2_dev: frag_pack_h2(W, bias)[0] of a CUDA weight with the
+    shift picked on the device (no host sync); scale_out (float32[2], device) gets
+    the layer scale 2^(s - 11) in [0] ([1]: scratch)."""
+    out_f, kin = W.shape
+    assert out_f % 32 == 0 and scale_out.numel() >= 2
+    cols = kin + (1 if bias is not None else 0)
+    W = W.detach().float()
+    b = None if bias is None else bias.detach().float().contiguous()
+    n = ((cols + 15) // 16 + H2_PAD) * (out_f // 32) * 64 * 2 * 8
+    out = torch.empty(n, dtype=torch.float16, device=W.device)
+    L.check(L.lib().pnr_pack_weights_h2_dev(W.data_ptr(), W.stride(0), W.stride(1), out_f, kin, L.ptr(b), H2_PAD,
+                                            scale_out.data_ptr(), out.data_ptr(), out.numel() * 2,
+                                            L.stream_ptr(W.device)), "pnr_pack_weights_h2_dev")
+    return out
+
+
 def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """[out, Kin] nn.Linear weight (out a multiple of 32) and bias -> MFMA
     A-operand fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)]
@@ -458,7 +475,8 @@ class PointAggregator(nn.Module):
 
     def packed_h2_train(self) -> tuple[L.MlpH2, dict]:
         """fp32h2 packs of the per-pair chain (block1.0[:, 224:], block1.2,
-        block3.0, block3.2) for pnr_aggregate_fwd_train_h2, packed on the device
+        block3.0, block3.2) and of block1.0's point half (P1 on k_point_pre_h2)
+        for pnr_aggregate_fwd_train_h2, packed on the device
         (pnr_pack_weights_h2: no host sync while the weights change every step)
         with shifts kept from the last h2_shift pick; `range_flag` is raised by
         the pack when a weight outgrew its shift and by the forward when an
@@ -468,17 +486,19 @@ class PointAggregator(nn.Module):
         if getattr(self, "_packedh2t", None) is not None and key == self._packedh2t_key:
             return self._packedh2t
         b1, b3 = self.block1, self.block3
-        mats = [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None)]
+        mats = [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None),
+                (b1[0].weight[:, :224], b1[0].bias)]   # the last: block1.0's point half (k_point_pre_h2)
         if getattr(self, "_h2t_shifts", None) is None:
             with torch.no_grad():
                 self._h2t_shifts = [h2_shift(W, b) for W, b in mats]
             self._h2t_flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
         flag = self._h2t_flag
         packs = [_pack_h2_device(W, b, s, flag) for (W, b), s in zip(mats, self._h2t_shifts)]
-        t = dict(w1bh=packs[0], w2h=packs[1], w3h=packs[2], w4h=packs[3], range_flag=flag)
+        t = dict(w1bh=packs[0], w2h=packs[1], w3h=packs[2], w4h=packs[3], w1ah=packs[4], range_flag=flag)
+        sc = [2.0 ** (s - 11) for s in self._h2t_shifts]
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
-                    (L.c_float * 4)(*(2.0 ** (s - 11) for s in self._h2t_shifts)), flag.data_ptr(),
-                    None, None, None, None, (L.c_float * 3)(0.0, 0.0, 0.0), None, 0.0, None, None,
+                    (L.c_float * 4)(*sc[:4]), flag.data_ptr(),
+                    None, None, None, None, (L.c_float * 3)(0.0, 0.0, 0.0), t["w1ah"].data_ptr(), sc[4], None, None,
                     (L.c_float * 4)(0.0, 0.0, 0.0, 0.0))
         self._packedh2t, self._packedh2t_key = (m, t), key
         return self._packedh2t

@@ -1658,8 +1658,15 @@ extern "C" int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_sampl
   a.out_conf = out_conf;
   a.pair_mask = nullptr;
   hipStream_t st = as_stream(stream);
-  // k_point_pre (fp32 P1) -> k_pairs_h2_train (aggregate_x3.hip) -> k_color<true>
-  if ((rc = launch_t<false>(a, st, kStagePre))) return rc;
+  // k_point_pre_h2 (P1 on fp32h2 when wh->w1ah is given) / k_point_pre -> k_pairs_h2_train
+  // (aggregate_x3.hip) -> k_color<true>
+  if (wh->w1ah) {
+    PNR_CHECK_ARG(((uintptr_t)wh->w1ah & 15) == 0 && wh->scale1a > 0.f && wh->scale1a < 1e30f,
+                  "aggregate_train_h2: bad block1.0 point-half pack");
+    if ((rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a, wh->range_flag, a.p1, st))) return rc;
+  } else if ((rc = launch_t<false>(a, st, kStagePre))) {
+    return rc;
+  }
   SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
                {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
                wh->range_flag};

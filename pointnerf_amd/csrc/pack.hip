@@ -72,9 +72,87 @@ __global__ void k_pack_h2(const float* __restrict__ W, int64_t lr, int64_t lc, i
   if (bad && flag) atomicOr(flag, 1);
 }
 
+// The shift picked on the device (pnr_pack_weights_h2_dev): k_w_absmax folds
+// max |W'| into sc[1] (as bits), k_pack_h2_dev picks s with max |2^-s W'| in
+// [8, 16) -- frag_pack_h2's h2_shift -- writes sc[0] = 2^(s - 11) and packs.
+__global__ void k_w_absmax(const float* __restrict__ W, int64_t lr, int64_t lc, int out_f, int kin,
+                           const float* __restrict__ bias, unsigned* __restrict__ word) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const int64_t total = (int64_t)out_f * (kin + 1);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(i / (kin + 1)), k = (int)(i % (kin + 1));
+    const float a = fabsf(wprime(W, lr, lc, kin, bias, o, k));
+    m = a != a ? __builtin_inff() : fmaxf(m, a);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+    if (m > 0.f) atomicMax(word, __float_as_uint(m));
+  }
+}
+
+// 2^-s with max 2^-s in [8, 16) (s = 0 for an all-zero or non-finite W: the
+// non-finite weights then reach the outputs as in fp32)
+__device__ __forceinline__ int pick_shift(float m) {
+  if (!(m > 0.f) || !(m <= 3.0e38f)) return 0;
+  int E;
+  (void)frexpf(m, &E);   // m = f 2^E, f in [0.5, 1): m 2^-(E-4) in [8, 16)
+  return E - 4;
+}
+
+__global__ void k_pack_h2_dev(const float* __restrict__ W, int64_t lr, int64_t lc, int NT, int kin,
+                              const float* __restrict__ bias, int64_t total, float* __restrict__ sc,
+                              uint4* __restrict__ out) {
+  const int sft = pick_shift(__uint_as_float(reinterpret_cast<const unsigned*>(sc)[1]));
+  const float f = ldexpf(1.f, -sft);
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc[0] = ldexpf(1.f, sft - 11);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i & 31), h = (int)((i >> 5) & 1);
+    const int64_t tT = i >> 6;
+    const int T = (int)(tT % NT), t = (int)(tT / NT);
+    const int o = 32 * T + r, k0 = 16 * t + 8 * h;
+    unsigned w[2][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      splith(wprime(W, lr, lc, kin, bias, o, k0 + 2 * q) * f, wprime(W, lr, lc, kin, bias, o, k0 + 2 * q + 1) * f,
+             w[0][q], w[1][q]);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      out[((tT * 2 + pl) * 2 + h) * 32 + r] = make_uint4(w[pl][0], w[pl][1], w[pl][2], w[pl][3]);
+  }
+}
+
 }  // namespace pnr
 
 using namespace pnr;
+
+extern "C" int pnr_pack_weights_h2_dev(const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f, int32_t kin,
+                                       const float* bias, int32_t pad_steps, float* scale_dev, void* out,
+                                       size_t out_bytes, void* stream) {
+  PNR_CHECK_ARG(W && out && scale_dev && out_f > 0 && out_f % 32 == 0 && kin > 0 && pad_steps >= 0,
+                "pack_weights_h2_dev: bad args (out_f %d, kin %d)", out_f, kin);
+  PNR_CHECK_ARG(((uintptr_t)out & 15) == 0 && ((uintptr_t)scale_dev & 7) == 0,
+                "pack_weights_h2_dev: output must be 16-B and scale 8-B aligned");
+  const int cols = kin + (bias ? 1 : 0);
+  const int NT = out_f / 32;
+  const int64_t tot = (cols + 15) / 16 + pad_steps;
+  const int64_t total = tot * NT * 64;
+  PNR_CHECK_ARG(out_bytes >= (size_t)total * 2 * 16, "pack_weights_h2_dev: output too small (%zu < %lld)", out_bytes,
+                (long long)total * 32);
+  hipStream_t st = as_stream(stream);
+  PNR_HIP(hipMemsetAsync(scale_dev + 1, 0, sizeof(float), st));
+  hipLaunchKernelGGL(k_w_absmax, dim3(grid_for((int64_t)out_f * (kin + 1), 256, 64)), dim3(256), 0, st, W, ld_row,
+                     ld_col, out_f, kin, bias, reinterpret_cast<unsigned*>(scale_dev + 1));
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_pack_h2_dev, dim3(grid_for(total, 256)), dim3(256), 0, st, W, ld_row, ld_col, NT, kin, bias,
+                     total, scale_dev, static_cast<uint4*>(out));
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
 
 extern "C" int pnr_pack_weights_h2(const float* W, int64_t ld_row, int64_t ld_col, int32_t out_f, int32_t kin,
                                    const float* bias, int32_t pad_steps, int32_t shift, int32_t* range_flag,

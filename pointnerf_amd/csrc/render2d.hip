@@ -470,13 +470,24 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
 // no fallback path.  The stacked rows [trunk; rgb; 0] all run as MFMA tiles
 // (the rgb rows' tile: 3 live rows of 32; the MFMAs are cheap at this rate).
 constexpr int kHPx = 128;                 // pixels per tile (4 waves x 32)
-constexpr int kHCh = 32;                  // input channels per LDS chunk (2 k-steps per tap)
-constexpr int kHPitch = 40;               // f16 per staged pixel per plane: 80 B, ds_read_b128 conflict-free
+constexpr int kHPitch = 40;               // wgrad images: f16 per staged row (32 px + 8): 80 B, conflict-free
+#ifndef PNR_CONV_RO
+#define PNR_CONV_RO 1
+#endif
+#ifndef PNR_CONV_CH
+#define PNR_CONV_CH 32
+#endif
+constexpr int kConvRO = PNR_CONV_RO, kConvCH = PNR_CONV_CH;   // conv tile: output rows, staged channels
 constexpr int kHRowPx = kHPx + 2;
 constexpr int kHWD = 3;                   // weight fragments prefetched this many k-steps ahead
-template <int RO>
+constexpr int kWS = 16;                   // absmax words 64 B apart (no shared L2 line between them)
+// staged f16 per pixel per plane for a CH-channel chunk: 80 B (32 ch) / 48 B (16 ch)
+// rows, 5 / 3 16-B slots: the ds_read_b128 lane groups hit 16 distinct slots
+template <int CH>
+constexpr int conv_pitch() { return CH + 8; }
+template <int RO, int CH>
 constexpr size_t conv_h2_lds() {
-  return (size_t)(RO + 2) * kHRowPx * 2 * kHPitch * sizeof(_Float16);
+  return (size_t)(RO + 2) * kHRowPx * 2 * conv_pitch<CH>() * sizeof(_Float16);
 }
 
 // 2^e with max|x| 2^e in [2^14, 2^15) from the image's absmax bits (1 for an
@@ -501,13 +512,16 @@ __device__ __forceinline__ void amax_commit(float m, unsigned* w) {
   if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(w, __float_as_uint(m));
 }
 
+__device__ __forceinline__ void amax_commit_block(float& m, unsigned* w, float* red);
+
 __global__ void k_nr_absmax(const float4* __restrict__ x, int64_t n4, unsigned* __restrict__ out) {
+  __shared__ float red[4];
   float m = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     const float4 v = x[i];
     m = amax_upd(amax_upd(amax_upd(amax_upd(m, v.x), v.y), v.z), v.w);
   }
-  amax_commit(m, out);
+  amax_commit_block(m, out, red);
 }
 
 struct ConvH2Args {
@@ -515,7 +529,7 @@ struct ConvH2Args {
   int H, W, Cin;
   const unsigned* in_max;   // absmax bits of `in`
   const uint4* wp;          // frag_pack_h2 of the stacked rows [32 NT, 9 Cin] (k = tap * Cin + ci)
-  float wscale;             // its 2^(s - 11)
+  const float* wscale;      // its 2^(s - 11) (device)
   const float* bias;        // forward: [32 NT] stacked biases (trunk, rgb, 0)
   int cout;                 // trunk rows (forward) / rows written (data gradient)
   float* out;               // [H, W, ldo]
@@ -528,152 +542,218 @@ struct ConvH2Args {
   int cin_real;             // BWD: input channels >= cin_real are zero padding (skipped)
 };
 
+// Block max of per-thread |value| maxima -> one atomicMax per workgroup (every
+// wave's atomic to one word serialises in L2: measured +0.2 ms per launch).
+__device__ __forceinline__ void amax_commit_block(float& m, unsigned* w, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+    if (m > 0.f) atomicMax(w, __float_as_uint(m));
+  }
+}
+
 // BWD: 0 forward, 1 data gradient, 2 data gradient times lrelu'(act).  RO
 // output rows per tile; a 4-wave workgroup owns RO rows x 128 pixels, wave w
-// pixels 32 w .. 32 w + 31 of every row.
-template <int NT, int BWD, int RO>
+// pixels 32 w .. 32 w + 31 of every row.  The (tile, chunk) sequence is
+// software-pipelined: the next chunk's global loads (the next tile's first
+// chunk after a tile's last) are issued into registers before this chunk's
+// MFMAs and split into the LDS planes after them.
+template <int NT, int BWD, int RO, int CH>
 __global__ void __launch_bounds__(256, 2) k_conv3x3_h2(ConvH2Args a) {
   extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
-  constexpr int PL = (RO + 2) * kHRowPx * kHPitch;   // f16 per plane
+  constexpr int PH = conv_pitch<CH>();
+  constexpr int PL = (RO + 2) * kHRowPx * PH;    // f16 per plane
+  constexpr int NST = ((RO + 2) * kHRowPx * (CH / 4) + 255) / 256;   // staged float4 per thread
+  constexpr int KS = 9 * (CH / 16);              // k-steps per chunk
+  __shared__ float red[4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int segs = (a.W + kHPx - 1) / kHPx;
   const int64_t ntiles = (int64_t)((a.H + RO - 1) / RO) * segs;
   const float xs = img_scale(a.in_max);
-  const float osc = a.wscale / xs;
+  const float osc = *a.wscale / xs;
   const int ktap = a.Cin / 16;             // k-steps per tap
   const uint4* wp = a.wp + lane;
+  constexpr int WD = NT >= 4 ? 2 : kHWD;   // weight ring depth (NT = 4: 2 k-steps, no spills)
   float amax = 0.f;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int y0 = (int)(tile / segs) * RO;
-    const int x0 = (int)(tile % segs) * kHPx;
-    f32x16 acc[RO][NT];
+  // staged channels of chunk ci0 (the backward's cat images: zero-padding tails skipped)
+  auto nreal_of = [&](int ci0) {
+    if (!BWD) return ci0 < a.Cin ? CH : 0;
+    const int r = (ci0 < a.Cin ? a.cin_real : 0) - ci0;
+    return r <= 0 ? 0 : (r >= CH ? CH : (r + 15) / 16 * 16);
+  };
+  float4 pre[NST];
+  // branch-free: every lane loads (an in-image pixel for the halo / padding
+  // slots) and zeroes afterwards, so the loads issue back to back and stay in
+  // flight across the MFMAs (sched_barrier: not sunk to their use)
+  unsigned pre_ok = 0;
+  auto load = [&](int64_t tile, int ci0, int nq) {
+    const int y0 = (int)(tile / segs) * RO, x0 = (int)(tile % segs) * kHPx;
+    pre_ok = 0;
 #pragma unroll
-    for (int o = 0; o < RO; ++o)
+    for (int u = 0; u < NST; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int q = i % nq, px = (i / nq) % kHRowPx, r = i / (nq * kHRowPx);
+      const int yy = y0 - 1 + r, xx = x0 - 1 + px;
+      const bool ok = r < RO + 2 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      const int yc = ok ? yy : 0, xc = ok ? xx : 0;
+      pre[u] = *reinterpret_cast<const float4*>(a.in + ((int64_t)yc * a.W + xc) * a.Cin + ci0 + 4 * (ok ? q : 0));
+      pre_ok |= (unsigned)ok << u;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto put = [&](int nq) {
 #pragma unroll
-      for (int T = 0; T < NT; ++T) acc[o][T] = (f32x16){0.f};
-    for (int ci0 = 0; ci0 < a.Cin; ci0 += kHCh) {
-      int nreal = kHCh;   // staged channels: chunks' zero-padding tails of the backward's cat images skipped
-      if (BWD) {
-        const int r = a.cin_real - ci0;
-        nreal = r <= 0 ? 0 : (r >= kHCh ? kHCh : (r + 15) / 16 * 16);
+    for (int u = 0; u < NST; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int q = i % nq, px = (i / nq) % kHRowPx, r = i / (nq * kHRowPx);
+      if (r >= RO + 2) continue;
+      const float sc = (pre_ok >> u) & 1u ? xs : 0.f;   // (a NaN / inf pixel of the halo: 0 * x is not 0)
+      const float4 v = (pre_ok >> u) & 1u ? pre[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+      unsigned h0, h1, l0, l1;
+      splith(v.x * sc, v.y * sc, h0, l0);
+      splith(v.z * sc, v.w * sc, h1, l1);
+      _Float16* d = lds_h + (r * kHRowPx + px) * PH + 4 * q;
+      *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(d + PL) = make_uint2(l0, l1);
+    }
+  };
+  f32x16 acc[RO][NT];
+  int64_t tile = blockIdx.x;
+  int ci0 = 0, nreal = nreal_of(0);
+  if (tile < ntiles) load(tile, 0, nreal / 4);
+  while (tile < ntiles) {
+    if (ci0 == 0) {
+#pragma unroll
+      for (int o = 0; o < RO; ++o)
+#pragma unroll
+        for (int T = 0; T < NT; ++T) acc[o][T] = (f32x16){0.f};
+    }
+    put(nreal / 4);
+    __syncthreads();
+    int nci0 = ci0 + CH;
+    int64_t ntile = tile;
+    int nnreal = nreal_of(nci0);
+    if (nnreal == 0) {
+      nci0 = 0;
+      ntile = tile + gridDim.x;
+      nnreal = nreal_of(0);
+    }
+    const int pcol = 32 * wid + c;
+    // chunk step i = (CH / 16) tap + s: k-step tap * ktap + ci0 / 16 + s; weights WD steps ahead
+    auto wstep = [&](int i) { return (i / (CH / 16)) * ktap + (ci0 >> 4) + i % (CH / 16); };
+    uint4 wh[WD][NT], wl[WD][NT];
+#pragma unroll
+    for (int d = 0; d < WD; ++d)
+#pragma unroll
+      for (int T = 0; T < NT; ++T) {
+        wh[d][T] = wp[((wstep(d) * NT + T) * 2 + 0) * 64];
+        wl[d][T] = wp[((wstep(d) * NT + T) * 2 + 1) * 64];
       }
-      if (nreal == 0) break;
-      const int nq = nreal / 4;
-      for (int i = threadIdx.x; i < (RO + 2) * kHRowPx * nq; i += 256) {
-        const int q = i % nq;
-        const int px = (i / nq) % kHRowPx;
-        const int r = i / (nq * kHRowPx);
-        const int yy = y0 - 1 + r, xx = x0 - 1 + px;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-          v = *reinterpret_cast<const float4*>(a.in + ((int64_t)yy * a.W + xx) * a.Cin + ci0 + 4 * q);
-        unsigned h0, h1, l0, l1;
-        splith(v.x * xs, v.y * xs, h0, l0);
-        splith(v.z * xs, v.w * xs, h1, l1);
-        _Float16* d = lds_h + (r * kHRowPx + px) * kHPitch + 4 * q;
-        *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(d + PL) = make_uint2(l0, l1);
-      }
-      __syncthreads();
-      const int pcol = 32 * wid + c;
-      // chunk step i = 2 tap + s: k-step tap * ktap + ci0 / 16 + s; weights kHWD steps ahead
-      auto wstep = [&](int i) { return (i >> 1) * ktap + (ci0 >> 4) + (i & 1); };
-      uint4 wh[kHWD][NT], wl[kHWD][NT];
+    __builtin_amdgcn_sched_barrier(0);
+    // the next chunk's staging loads, in flight during the MFMAs (issued after the
+    // weight ring's first loads: vmcnt counts in order, so the first MFMAs do not
+    // wait for them; the ring's refills still do, WD steps later)
+    if (ntile < ntiles) load(ntile, nci0, nnreal / 4);
 #pragma unroll
-      for (int d = 0; d < kHWD; ++d)
+    for (int i0 = 0; i0 < KS; i0 += WD) {
 #pragma unroll
-        for (int T = 0; T < NT; ++T) {
-          wh[d][T] = wp[((wstep(d) * NT + T) * 2 + 0) * 64];
-          wl[d][T] = wp[((wstep(d) * NT + T) * 2 + 1) * 64];
-        }
+      for (int d = 0; d < WD; ++d) {
+        const int i = i0 + d;
+        if (i >= KS) break;
+        const int tap = i / (CH / 16), s = i % (CH / 16);
+        const int dy = tap / 3, dx = tap % 3;
+        if (!BWD || 16 * s < nreal) {
+          uint4 xh[RO], xl[RO];
 #pragma unroll
-      for (int i0 = 0; i0 < 18; i0 += kHWD) {
+          for (int o = 0; o < RO; ++o) {
+            const _Float16* b = lds_h + ((dy + o) * kHRowPx + pcol + dx) * PH + 16 * s + 8 * h;
+            xh[o] = *reinterpret_cast<const uint4*>(b);
+            xl[o] = *reinterpret_cast<const uint4*>(b + PL);
+          }
 #pragma unroll
-        for (int d = 0; d < kHWD; ++d) {
-          const int i = i0 + d;
-          const int tap = i >> 1, s = i & 1;
-          const int dy = tap / 3, dx = tap % 3;
-          if (!BWD || 16 * s < nreal) {
-            uint4 xh[RO], xl[RO];
+          for (int T = 0; T < NT; ++T) {
+            const uint4 ws = f16x8_scale2048(wh[d][T]);
 #pragma unroll
             for (int o = 0; o < RO; ++o) {
-              const _Float16* b = lds_h + ((dy + o) * kHRowPx + pcol + dx) * kHPitch + 16 * s + 8 * h;
-              xh[o] = *reinterpret_cast<const uint4*>(b);
-              xl[o] = *reinterpret_cast<const uint4*>(b + PL);
-            }
-#pragma unroll
-            for (int T = 0; T < NT; ++T) {
-              const uint4 ws = f16x8_scale2048(wh[d][T]);
-#pragma unroll
-              for (int o = 0; o < RO; ++o) {
-                acc[o][T] = mfma_f16(ws, xh[o], acc[o][T]);
-                acc[o][T] = mfma_f16(wl[d][T], xh[o], acc[o][T]);
-                acc[o][T] = mfma_f16(wh[d][T], xl[o], acc[o][T]);
-              }
-            }
-          }
-          if (i + kHWD < 18) {   // refills run for skipped steps too (in-bounds: the pack's zero tail)
-#pragma unroll
-            for (int T = 0; T < NT; ++T) {
-              wh[d][T] = wp[((wstep(i + kHWD) * NT + T) * 2 + 0) * 64];
-              wl[d][T] = wp[((wstep(i + kHWD) * NT + T) * 2 + 1) * 64];
+              acc[o][T] = mfma_f16(ws, xh[o], acc[o][T]);
+              acc[o][T] = mfma_f16(wl[d][T], xh[o], acc[o][T]);
+              acc[o][T] = mfma_f16(wh[d][T], xl[o], acc[o][T]);
             }
           }
         }
+        if (i + WD < KS) {   // refills run for skipped steps too (in-bounds: the pack's zero tail)
+#pragma unroll
+          for (int T = 0; T < NT; ++T) {
+            wh[d][T] = wp[((wstep(i + WD) * NT + T) * 2 + 0) * 64];
+            wl[d][T] = wp[((wstep(i + WD) * NT + T) * 2 + 1) * 64];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);   // the refills stay WD steps ahead of their use
       }
-      __syncthreads();
     }
-    // epilogue.  C/D layout: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h, pixel c
-    const int xo = x0 + 32 * wid + c;
+    __syncthreads();
+    if (nci0 == 0) {
+      // epilogue.  C/D layout: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h, pixel c
+      const int y0 = (int)(tile / segs) * RO, x0 = (int)(tile % segs) * kHPx;
+      const int xo = x0 + 32 * wid + c;
 #pragma unroll
-    for (int o = 0; o < RO; ++o) {
-      const int y = y0 + o;
-      if (xo >= a.W || y >= a.H) continue;
-      const int64_t pix = (int64_t)y * a.W + xo;
+      for (int o = 0; o < RO; ++o) {
+        const int y = y0 + o;
+        if (xo >= a.W || y >= a.H) continue;
+        const int64_t pix = (int64_t)y * a.W + xo;
 #pragma unroll
-      for (int T = 0; T < NT; ++T)
+        for (int T = 0; T < NT; ++T)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float v = acc[o][T][r] * osc;
-          if (BWD) {
-            if (co < a.cout) {
-              // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
-              if (BWD == 2 && !(a.act[pix * a.cout + co] > 0.f)) v *= a.slope;
+          for (int r = 0; r < 16; ++r) {
+            const int co = 32 * T + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = acc[o][T][r] * osc;
+            if (BWD) {
+              if (co < a.cout) {
+                // LeakyReLU'(z) from the saved output: sign(lrelu(z)) = sign(z), slope > 0
+                if (BWD == 2 && !(a.act[pix * a.cout + co] > 0.f)) v *= a.slope;
+                a.out[pix * a.ldo + co] = v;
+                amax = amax_upd(amax, v);
+              }
+            } else if (co < a.cout) {
+              v += a.bias[co];
+              v = v > 0.f ? v : v * a.slope;
               a.out[pix * a.ldo + co] = v;
               amax = amax_upd(amax, v);
+            } else if (co < a.cout + 3) {
+              v += a.bias[co];
+              float* op = a.rgb + pix * 3 + (co - a.cout);
+              if (a.rgb_mode == 0) *op = v;
+              else if (a.rgb_mode == 1) *op += v;
+              else *op = 1.f / (1.f + expf(-(*op + v)));
             }
-          } else if (co < a.cout) {
-            v += a.bias[co];
-            v = v > 0.f ? v : v * a.slope;
-            a.out[pix * a.ldo + co] = v;
-            amax = amax_upd(amax, v);
-          } else if (co < a.cout + 3) {
-            v += a.bias[co];
-            float* op = a.rgb + pix * 3 + (co - a.cout);
-            if (a.rgb_mode == 0) *op = v;
-            else if (a.rgb_mode == 1) *op += v;
-            else *op = 1.f / (1.f + expf(-(*op + v)));
           }
-        }
+      }
     }
+    tile = ntile;
+    ci0 = nci0;
+    nreal = nnreal;
   }
-  if (a.out_max) amax_commit(amax, a.out_max);
+  if (a.out_max) amax_commit_block(amax, a.out_max, red);
 }
 
+// Tile shape per stage (RO output rows, CH-channel chunks): measured in DESIGN §12.
 template <int NT, int BWD>
 static int launch_conv_h2(const ConvH2Args& a, hipStream_t st) {
-  constexpr int RO = 1;
+  constexpr int RO = NT >= 4 ? 1 : kConvRO, CH = kConvCH;   // (NT = 4 at RO = 2 spills)
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3_h2<NT, BWD, RO>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv_h2_lds<RO>()));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3x3_h2<NT, BWD, RO, CH>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv_h2_lds<RO, CH>()));
     attr = true;
   }
   const int64_t tiles = (int64_t)((a.H + RO - 1) / RO) * ((a.W + kHPx - 1) / kHPx);
-  hipLaunchKernelGGL((k_conv3x3_h2<NT, BWD, RO>), dim3(grid_for(tiles, 1, 256 * 4)), dim3(256), conv_h2_lds<RO>(),
-                     st, a);
+  constexpr size_t lds = conv_h2_lds<RO, CH>();
+  hipLaunchKernelGGL((k_conv3x3_h2<NT, BWD, RO, CH>), dim3(grid_for(tiles, 1, 256 * 4)), dim3(256), lds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
@@ -694,6 +774,7 @@ static int launch_conv_h2(const ConvH2Args& a, hipStream_t st) {
 template <int MT, int NC>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const unsigned* y_max, const unsigned* x_max) {
   constexpr int M = 32 * MT, C = 32 * NC;
+  static_assert(M + C <= 256, "one staging task per thread");
   constexpr int PA = M * kHPitch, PB = C * kHPitch;      // f16 per plane
   constexpr int NJ = 3 * NC, JW = (NJ + 3) / 4;
   __shared__ __attribute__((aligned(16))) _Float16 as_h[2 * PA];
@@ -705,7 +786,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
   const int pbeg = split * (int)a.chunk;
   const int pend = pbeg + (int)a.chunk < npix ? pbeg + (int)a.chunk : npix;
   // dY to max [8, 16), X to max [2^14, 2^15)
-  float ys = img_scale(y_max) * (1.f / 2048.f);
+  const float ys = img_scale(y_max) * (1.f / 2048.f);
   const float xs = img_scale(x_max);
   const float osc = 1.f / (2048.f * ys * xs);
   f32x16 acc[JW][MT];
@@ -714,61 +795,92 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[u][t] = (f32x16){0.f};
   float db[4] = {0.f, 0.f, 0.f, 0.f};
-  // staging tasks: A: tid < M -> (m quad qa, pixel octet oa); B: (kx, ci quad, octet)
-  const int qa = tid % (M / 4), oa = tid / (M / 4);
-  auto put8x4 = [](_Float16* base, int pitch_pl, const float4 (&v)[8], float s) {
-    // 8 pixels x 4 channels -> per channel k: [hi 8 px] at base + k * kHPitch, lo at + pitch_pl
-    const float* f = reinterpret_cast<const float*>(v);
+  // staging task of this thread (one per chunk): tid < C -> X channel quad qb of
+  // pixel octet ob: the 10 source pixels p - 1 .. p + 8 of its 8 pixels (one load
+  // each), from which the three kx-shifted copies are cut; C <= tid < C + M -> dY
+  // channel quad qa of pixel octet oa.
+  const bool tb = tid < C, ta = !tb && tid < C + M;
+  const int qb = tid % (C / 4), ob = tid / (C / 4);
+  const int qa = (tid - C) % (M / 4), oa = (tid - C) / (M / 4);
+  float4 v[10];
+  auto load = [&](int p0) {
+    if (tb) {
+      const int s0 = p0 + 8 * ob + (ky - 1) * a.W - 1;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      unsigned hi[4], lo[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) splith(f[8 * j + k] * s, f[8 * j + 4 + k] * s, hi[j], lo[j]);
-      *reinterpret_cast<uint4*>(base + k * kHPitch) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-      *reinterpret_cast<uint4*>(base + k * kHPitch + pitch_pl) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-    }
-  };
-  for (int p0 = pbeg; p0 < pend; p0 += 32) {
-    if (tid < M) {
-      float4 v[8];
+      for (int j = 0; j < 10; ++j) {
+        const int sp = s0 + j;
+        v[j] = sp >= 0 && sp < npix ? *reinterpret_cast<const float4*>(a.x + (int64_t)sp * C + 4 * qb)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else if (ta) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int p = p0 + 8 * oa + j;
         v[j] = p < pend ? *reinterpret_cast<const float4*>(a.dy + (int64_t)p * M + 4 * qa)
                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  // 8 pixels x 4 channels (pixel jj = v[jj + sh], zero where !(ok >> jj & 1)) ->
+  // per channel k: [hi 8 px] at base + k * kHPitch, lo at + pitch_pl
+  auto put8x4 = [&](_Float16* base, int pitch_pl, int sh, unsigned ok, float sc) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      unsigned hi[4], lo[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* f0 = reinterpret_cast<const float*>(&v[2 * j + sh]);
+        const float* f1 = reinterpret_cast<const float*>(&v[2 * j + 1 + sh]);
+        const float e0 = (ok >> (2 * j)) & 1u ? f0[k] * sc : 0.f;
+        const float e1 = (ok >> (2 * j + 1)) & 1u ? f1[k] * sc : 0.f;
+        splith(e0, e1, hi[j], lo[j]);
+      }
+      *reinterpret_cast<uint4*>(base + k * kHPitch) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+      *reinterpret_cast<uint4*>(base + k * kHPitch + pitch_pl) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    }
+  };
+  auto put = [&](int p0) {
+    if (tb) {
+      // output pixel p = p0 + 8 ob + jj takes source jj + kx for copy kx: zero where
+      // p >= pend or x(p) + kx - 1 leaves the row (the image edges were zeroed by the load)
+      const int pf = p0 + 8 * ob;
+      unsigned okp = 0, okl = 0, okr = 0;   // p < pend; x > 0 (kx = 0); x < W - 1 (kx = 2)
+      int x = pf % a.W;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        okp |= (unsigned)(pf + jj < pend) << jj;
+        okl |= (unsigned)(x > 0) << jj;
+        okr |= (unsigned)(x < a.W - 1) << jj;
+        x = x + 1 == a.W ? 0 : x + 1;
+      }
+      _Float16* base = bs_h + (4 * qb) * kHPitch + 8 * ob;
+      put8x4(base, PB, 0, okp & okl, xs);
+      put8x4(base + 2 * PB, PB, 1, okp, xs);
+      put8x4(base + 4 * PB, PB, 2, okp & okr, xs);
+    } else if (ta) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
         db[0] += v[j].x;
         db[1] += v[j].y;
         db[2] += v[j].z;
         db[3] += v[j].w;
       }
-      put8x4(as_h + (4 * qa) * kHPitch + 8 * oa, PA, v, ys);
+      put8x4(as_h + (4 * qa) * kHPitch + 8 * oa, PA, 0, 0xffu, ys);
     }
-    for (int i = tid; i < 3 * C; i += 256) {
-      const int kx = i / C, r = i % C, q = r % (C / 4), o = r / (C / 4);
-      float4 v[8];
-      const int pf = p0 + 8 * o;
-      int x = pf % a.W;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int p = pf + j;
-        const int sp = p + (ky - 1) * a.W + kx - 1, xsrc = x + kx - 1;
-        v[j] = p < pend && sp >= 0 && sp < npix && xsrc >= 0 && xsrc < a.W
-                   ? *reinterpret_cast<const float4*>(a.x + (int64_t)sp * C + 4 * q)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        x = x + 1 == a.W ? 0 : x + 1;
-      }
-      put8x4(bs_h + kx * 2 * PB + (4 * q) * kHPitch + 8 * o, PB, v, xs);
-    }
+  };
+  if (pbeg < pend) load(pbeg);
+  for (int p0 = pbeg; p0 < pend; p0 += 32) {
+    put(p0);
     __syncthreads();
+    if (p0 + 32 < pend) load(p0 + 32);   // in flight during the MFMAs
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      uint4 ys_[MT], yl_[MT], yh_[MT];
+      uint4 yl_[MT], yh_[MT];   // (Ys = 2^11 Yh made per use: 4 v_pk_mul, 12 fewer VGPRs live)
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const _Float16* pa = as_h + (32 * t + c) * kHPitch + 16 * s + 8 * h;
         yh_[t] = *reinterpret_cast<const uint4*>(pa);
         yl_[t] = *reinterpret_cast<const uint4*>(pa + PA);
-        ys_[t] = f16x8_scale2048(yh_[t]);
       }
 #pragma unroll
       for (int u = 0; u < JW; ++u) {
@@ -780,7 +892,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
           const uint4 xl = *reinterpret_cast<const uint4*>(pb + PB);
 #pragma unroll
           for (int t = 0; t < MT; ++t) {
-            acc[u][t] = mfma_f16(ys_[t], xh, acc[u][t]);
+            acc[u][t] = mfma_f16(f16x8_scale2048(yh_[t]), xh, acc[u][t]);
             acc[u][t] = mfma_f16(yl_[t], xh, acc[u][t]);
             acc[u][t] = mfma_f16(yh_[t], xl, acc[u][t]);
           }
@@ -804,7 +916,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
         out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + col] = acc[u][t][r] * osc;
   }
   if (ky == 0) {   // db: the four pixel octets' sums per channel, octet order
-    if (tid < M) {
+    if (ta) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) dbs[oa][4 * qa + k] = db[k];
     }
@@ -859,9 +971,12 @@ __global__ void k_nr_rgb_grad_h2(const float* __restrict__ d_out, const float* _
       c0[64 + j] = v;
     }
   }
-  amax_commit(m, words + 0);
-  amax_commit(m, words + 1);
-  amax_commit(m, words + 2);
+  __shared__ float red[4];
+  amax_commit_block(m, words + 0 * kWS, red);
+  if (threadIdx.x == 0 && m > 0.f) {   // (m: the block max after the commit's reduction)
+    atomicMax(words + 1 * kWS, __float_as_uint(m));
+    atomicMax(words + 2 * kWS, __float_as_uint(m));
+  }
 }
 
 }  // namespace pnr
@@ -1028,7 +1143,7 @@ extern "C" int pnr_neural_render_h2_scratch_bytes(int32_t H, int32_t W, size_t* 
 extern "C" int pnr_neural_render_fwd_h2(const float* x, int32_t H, int32_t W, const pnr_neural_render_h2w* w,
                                         float* out_rgb, void* scratch, size_t scratch_bytes, void* stream) {
   PNR_CHECK_ARG(x && w && out_rgb && scratch, "neural_render_h2: null pointer");
-  PNR_CHECK_ARG(w->wp0 && w->wp1 && w->wp2 && w->b0 && w->b1 && w->b2, "neural_render_h2: null weight");
+  PNR_CHECK_ARG(w->wp0 && w->wp1 && w->wp2 && w->ws && w->b0 && w->b1 && w->b2, "neural_render_h2: null weight");
   PNR_CHECK_ARG(H >= 0 && W >= 0, "neural_render_h2: bad image size");
   PNR_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
                 "neural_render_h2: x and scratch must be 16-B aligned");
@@ -1041,8 +1156,8 @@ extern "C" int pnr_neural_render_fwd_h2(const float* x, int32_t H, int32_t W, co
   float* net0 = static_cast<float*>(scratch);
   float* net1 = net0 + (size_t)npix * 64;
   unsigned* words = reinterpret_cast<unsigned*>(net1 + (size_t)npix * 32);   // max |x|, |net0|, |net1|
-  PNR_HIP(hipMemsetAsync(words, 0, 16, st));
-  hipLaunchKernelGGL(k_nr_absmax, dim3(grid_for(npix * 32, 256, 2048)), dim3(256), 0, st,
+  PNR_HIP(hipMemsetAsync(words, 0, 256, st));
+  hipLaunchKernelGGL(k_nr_absmax, dim3(grid_for(npix * 32, 256, 1024)), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(x), npix * 32, words);
   PNR_LAUNCH_CHECK();
   int rc;
@@ -1056,35 +1171,35 @@ extern "C" int pnr_neural_render_fwd_h2(const float* x, int32_t H, int32_t W, co
   // stage 0: x (128) -> [net0 (64), rgb = conv_rgb0(x)]
   a.in = x;
   a.Cin = 128;
-  a.in_max = words;
+  a.in_max = words + 0 * kWS;
   a.wp = static_cast<const uint4*>(w->wp0);
-  a.wscale = w->ws0;
+  a.wscale = w->ws + 0;
   a.bias = w->b0;
   a.cout = 64;
   a.out = net0;
   a.ldo = 64;
-  a.out_max = words + 1;
+  a.out_max = words + 1 * kWS;
   a.rgb_mode = 0;
   if ((rc = launch_conv_h2<3, 0>(a, st))) return rc;
   // stage 1: net0 (64) -> [net1 (32), rgb += conv_rgb1(net0)]
   a.in = net0;
   a.Cin = 64;
-  a.in_max = words + 1;
+  a.in_max = words + 1 * kWS;
   a.wp = static_cast<const uint4*>(w->wp1);
-  a.wscale = w->ws1;
+  a.wscale = w->ws + 4;
   a.bias = w->b1;
   a.cout = 32;
   a.out = net1;
   a.ldo = 32;
-  a.out_max = words + 2;
+  a.out_max = words + 2 * kWS;
   a.rgb_mode = 1;
   if ((rc = launch_conv_h2<2, 0>(a, st))) return rc;
   // stage 2: out = sigmoid(rgb + conv_rgb2(net1))
   a.in = net1;
   a.Cin = 32;
-  a.in_max = words + 2;
+  a.in_max = words + 2 * kWS;
   a.wp = static_cast<const uint4*>(w->wp2);
-  a.wscale = w->ws2;
+  a.wscale = w->ws + 4;
   a.bias = w->b2;
   a.cout = 0;
   a.out = nullptr;
@@ -1105,7 +1220,7 @@ extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch
                                         size_t scratch_bytes, void* stream) {
   PNR_CHECK_ARG(x && fwd_scratch && out_rgb && d_out && wt && d_x && dw0 && dw1 && dw2 && scratch,
                 "neural_render_bwd_h2: null pointer");
-  PNR_CHECK_ARG(wt->wt0 && wt->wt1 && wt->wt2, "neural_render_bwd_h2: null weight");
+  PNR_CHECK_ARG(wt->wt0 && wt->wt1 && wt->wt2 && wt->ws, "neural_render_bwd_h2: null weight");
   PNR_CHECK_ARG(H >= 0 && W >= 0 && (int64_t)H * W < (1ll << 30), "neural_render_bwd_h2: bad image size");
   PNR_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)fwd_scratch & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
                 "neural_render_bwd_h2: x, fwd_scratch and scratch must be 16-B aligned");
@@ -1128,8 +1243,8 @@ extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch
   float* cat0 = cat1 + (size_t)npix * 64;
   unsigned* words = reinterpret_cast<unsigned*>(cat0 + (size_t)npix * 96);   // max |cat2|, |cat1|, |cat0|
   float* part = cat0 + (size_t)npix * 96 + 64;
-  PNR_HIP(hipMemsetAsync(words, 0, 16, st));
-  hipLaunchKernelGGL(k_nr_rgb_grad_h2, dim3(grid_for(npix, 256, 2048)), dim3(256), 0, st, d_out, out_rgb, npix, cat2,
+  PNR_HIP(hipMemsetAsync(words, 0, 256, st));
+  hipLaunchKernelGGL(k_nr_rgb_grad_h2, dim3(grid_for(npix, 256, 512)), dim3(256), 0, st, d_out, out_rgb, npix, cat2,
                      cat1, cat0, words);
   PNR_LAUNCH_CHECK();
   int rc;
@@ -1143,43 +1258,43 @@ extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch
   // stage 2: d net1 = conv(cat2 = [g, 0], flipped conv_rgb.2), masked by net1 -> cat1[:, :32]
   a.in = cat2;
   a.Cin = 32;
-  a.in_max = words + 0;
+  a.in_max = words + 0 * kWS;
   a.cin_real = 3;
   a.wp = static_cast<const uint4*>(wt->wt2);
-  a.wscale = wt->ws2;
+  a.wscale = wt->ws + 4;
   a.cout = 32;
   a.ldo = 64;
   a.out = cat1;
-  a.out_max = words + 1;
+  a.out_max = words + 1 * kWS;
   a.act = net1;
   if ((rc = launch_conv_h2<1, 2>(a, st))) return rc;
-  if ((rc = launch_wgrad_h2<1, 1>(cat2, words + 0, net1, fwords + 2, H, W, part, dw2, st))) return rc;
+  if ((rc = launch_wgrad_h2<1, 1>(cat2, words + 0, net1, fwords + 2 * kWS, H, W, part, dw2, st))) return rc;
   // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
   a.in = cat1;
   a.Cin = 64;
-  a.in_max = words + 1;
+  a.in_max = words + 1 * kWS;
   a.cin_real = 32 + 3;
   a.wp = static_cast<const uint4*>(wt->wt1);
-  a.wscale = wt->ws1;
+  a.wscale = wt->ws + 4;
   a.cout = 64;
   a.ldo = 96;
   a.out = cat0;
-  a.out_max = words + 2;
+  a.out_max = words + 2 * kWS;
   a.act = net0;
   if ((rc = launch_conv_h2<2, 2>(a, st))) return rc;
-  if ((rc = launch_wgrad_h2<2, 2>(cat1, words + 1, net0, fwords + 1, H, W, part, dw1, st))) return rc;
+  if ((rc = launch_wgrad_h2<2, 2>(cat1, words + 1 * kWS, net0, fwords + 1 * kWS, H, W, part, dw1, st))) return rc;
   // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
   a.in = cat0;
   a.Cin = 96;
-  a.in_max = words + 2;
+  a.in_max = words + 2 * kWS;
   a.cin_real = 64 + 3;
   a.wp = static_cast<const uint4*>(wt->wt0);
-  a.wscale = wt->ws0;
+  a.wscale = wt->ws + 0;
   a.cout = 128;
   a.ldo = 128;
   a.out = d_x;
   a.out_max = nullptr;
   a.act = nullptr;
   if ((rc = launch_conv_h2<4, 1>(a, st))) return rc;
-  return launch_wgrad_h2<3, 4>(cat0, words + 2, x, fwords + 0, H, W, part, dw0, st);
+  return launch_wgrad_h2<3, 4>(cat0, words + 2 * kWS, x, fwords + 0 * kWS, H, W, part, dw0, st);
 }

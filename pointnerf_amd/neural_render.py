@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib as L
-from .aggregator import frag_pack, frag_pack_h2
+from .aggregator import frag_pack, pack_h2_dev
 
 
 class NeuralRenderer(nn.Module):
@@ -95,37 +95,53 @@ class NeuralRenderer(nn.Module):
         return ((self.conv_layers[0], self.conv_rgb[0], 96), (self.conv_layers[1], self.conv_rgb[1], 64),
                 (None, self.conv_rgb[2], 32))
 
+    def _key(self, tag):
+        return (tag,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+
     def packed_t(self):
+        key = self._key("t")
+        if getattr(self, "_packed_t", None) is not None and self._packed_t_key == key:
+            return self._packed_t
         with torch.no_grad():
             t = {f"wt{i}": frag_pack(self._stack_t(*st)) for i, st in enumerate(self._stages())}
-        return L.NeuralRenderWT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(), 0.2), t
+        self._packed_t = L.NeuralRenderWT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(), 0.2), t
+        self._packed_t_key = key
+        return self._packed_t
 
     def packed_h2(self):
-        """fp32h2 forward packs: per stage frag_pack_h2 of the stacked rows
-        (k = (ky*3 + kx)*cin + ci) with its scale, and the stacked biases."""
-        ps = list(self.parameters())
-        key = ("h2",) + tuple((p.data_ptr(), p._version) for p in ps)
+        """fp32h2 forward packs: per stage the stacked rows (k = (ky*3 + kx)*cin + ci)
+        packed on the device with a device-picked shift (pnr_pack_weights_h2_dev:
+        no host sync, so a training step repacks freely), the scales in one
+        device array, and the stacked biases."""
+        key = self._key("h2")
         if self._packed is not None and key == self._packed_key:
             return self._packed
-        t, sc = {}, []
+        dev = self.conv_rgb[0].weight.device
+        t = {"ws": torch.zeros(6, dtype=torch.float32, device=dev)}
         with torch.no_grad():
             for i, st in enumerate(self._stages()):
                 Wp, bp = self._stack(*st)
-                t[f"wp{i}"], s = frag_pack_h2(Wp.permute(0, 2, 3, 1).reshape(Wp.shape[0], -1).contiguous())
+                t[f"wp{i}"] = pack_h2_dev(Wp.permute(0, 2, 3, 1).reshape(Wp.shape[0], -1).contiguous(), None,
+                                          t["ws"][2 * i:2 * i + 2])
                 t[f"b{i}"] = bp.contiguous()
-                sc.append(s)
-        w = L.NeuralRenderH2W(t["wp0"].data_ptr(), t["wp1"].data_ptr(), t["wp2"].data_ptr(), *sc,
+        w = L.NeuralRenderH2W(t["wp0"].data_ptr(), t["wp1"].data_ptr(), t["wp2"].data_ptr(), t["ws"].data_ptr(),
                               t["b0"].data_ptr(), t["b1"].data_ptr(), t["b2"].data_ptr(), 0.2)
         self._packed, self._packed_key = (w, t), key
         return self._packed
 
     def packed_t_h2(self):
-        t, sc = {}, []
+        key = self._key("th2")
+        if getattr(self, "_packed_t", None) is not None and self._packed_t_key == key:
+            return self._packed_t
+        dev = self.conv_rgb[0].weight.device
+        t = {"ws": torch.zeros(6, dtype=torch.float32, device=dev)}
         with torch.no_grad():
             for i, st in enumerate(self._stages()):
-                t[f"wt{i}"], s = frag_pack_h2(self._stack_t(*st))
-                sc.append(s)
-        return L.NeuralRenderH2WT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(), *sc, 0.2), t
+                t[f"wt{i}"] = pack_h2_dev(self._stack_t(*st), None, t["ws"][2 * i:2 * i + 2])
+        self._packed_t = L.NeuralRenderH2WT(t["wt0"].data_ptr(), t["wt1"].data_ptr(), t["wt2"].data_ptr(),
+                                            t["ws"].data_ptr(), 0.2), t
+        self._packed_t_key = key
+        return self._packed_t
 
     def forward_torch(self, x):
         """neural_renderer.py:81-104 with torch convolutions (autograd path)."""

@@ -164,7 +164,7 @@ class NeuralPointsRayMarching(nn.Module):
         self.precision = precision
         # render_rays_train's per-pair forward: "fp32x3" (split-bf16 MFMA,
         # fp32-accurate, the default) or "fp32" (native fp32 MFMA)
-        self.train_precision = "fp32h2"   # per-pair forward chain: fp32h2 (f16 MFMA) / fp32x3 / fp32
+        self.train_precision = "fp32x3"   # per-pair forward chain: fp32x3 (split-bf16 MFMA) / fp32h2 / fp32
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
         self.h2_fallbacks = 0

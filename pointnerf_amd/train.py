@@ -164,6 +164,7 @@ class AggregateFn(torch.autograd.Function):
         scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
         keepx = None
         run_x3 = spec.pair_mask is None and spec.x3
+        done = False
         if spec.pair_mask is None and spec.h2:
             wh, keepx = agg.packed_h2_train()
             L.check(L.lib().pnr_aggregate_fwd_train_h2(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
@@ -171,11 +172,14 @@ class AggregateFn(torch.autograd.Function):
                                                        L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
                     "pnr_aggregate_fwd_train_h2")
             run_x3 = int(keepx["range_flag"].item()) != 0   # a weight or an activation left the f16 range
+            done = not run_x3
             if run_x3:
                 agg.h2_train_reset()
                 spec.h2_fallback = True
                 feat.zero_()
-        if run_x3:
+        if done:
+            pass
+        elif run_x3:
             wx, keepx = agg.packed_x3()
             L.check(L.lib().pnr_aggregate_fwd_train_x3(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
                                                        ctypes.byref(wx), ctypes.byref(sv.c), L.ptr(feat), None, None,

@@ -44,3 +44,19 @@ def test_device_pack_h2_equals_torch(cuda, shape, bias, transposed):
     assert int(flag.item()) == 0
     _pack_h2_device(Wd, bd, s - 1, flag)
     assert int(flag.item()) == 1
+
+
+@pytest.mark.parametrize("shape,bias,scale", [((96, 1152), False, 0.03), ((128, 864), False, 3e-6),
+                                              ((256, 263), True, 40.0), ((32, 33), True, 1.0)])
+def test_device_pack_h2_dev_picks_the_shift(cuda, shape, bias, scale):
+    """pnr_pack_weights_h2_dev (shift picked on the device, no host sync) ==
+    frag_pack_h2 bitwise, and its device scale == frag_pack_h2's 2^(s - 11)."""
+    from pointnerf_amd.aggregator import frag_pack_h2, pack_h2_dev
+    g = torch.Generator().manual_seed(shape[0] * 7 + shape[1])
+    W = torch.randn(shape, generator=g) * scale
+    b = torch.randn(shape[0], generator=g) * scale if bias else None
+    ref, sc = frag_pack_h2(W, b)
+    s_out = torch.zeros(2, dtype=torch.float32, device=cuda)
+    got = pack_h2_dev(W.to(cuda), None if b is None else b.to(cuda), s_out)
+    assert torch.equal(got.cpu().view(torch.int16), ref.view(torch.int16))
+    assert float(s_out[0]) == sc

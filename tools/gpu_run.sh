@@ -27,6 +27,28 @@ for s in $STEPS; do
       cat $O/nr.json
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/nrstats -o run -- \
         python tools/nr_bench.py > $O/nrstats.log 2>&1 || { tail -20 $O/nrstats.log; exit 1; } ;;
+    tnew)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_neural_render.py tests/test_gpu_pack.py tests/test_gpu_backward.py \
+        -m gpu -x -v --timeout 300 --timeout-method thread > $O/t_new.log 2>&1 || { tail -40 $O/t_new.log; exit 1; }
+      tail -3 $O/t_new.log ;;
+    train)
+      timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 > $O/train.json 2> $O/train.err \
+        || { tail -20 $O/train.err; exit 1; }
+      timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 --train-precision fp32h2 > $O/train_h2.json \
+        2> $O/train_h2.err || { tail -20 $O/train_h2.err; exit 1; }
+      cut -c1-400 $O/train.json $O/train_h2.json ;;
+    trainprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trstats -o run -- \
+        python bench.py --mode train --steps 20 --warmup 3 > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
+    nrab)   # the 2-D renderer tile-shape variants in tools/_var (built on the CPU side)
+      for v in tools/_var/libpnr_*.so; do
+        PNR_LIB=$PWD/$v timeout -k 10 200 python tools/nr_bench.py > $O/nrab_$(basename $v .so).json 2>> $O/nrab.err \
+          || { tail -20 $O/nrab.err; exit 1; }
+        echo $v; cat $O/nrab_$(basename $v .so).json
+      done ;;
+    dbg)
+      timeout -k 10 200 python tools/_var/dbg_h2_train.py > $O/dbg.log 2>&1 || { tail -30 $O/dbg.log; exit 1; }
+      cat $O/dbg.log ;;
     tnr)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_neural_render.py -m gpu -x -v --timeout 120 \
         --timeout-method thread > $O/t_nr.log 2>&1 || { tail -40 $O/t_nr.log; exit 1; }
