@@ -472,10 +472,10 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
 constexpr int kHPx = 128;                 // pixels per tile (4 waves x 32)
 constexpr int kHPitch = 40;               // wgrad images: f16 per staged row (32 px + 8): 80 B, conflict-free
 #ifndef PNR_CONV_RO
-#define PNR_CONV_RO 1
+#define PNR_CONV_RO 2
 #endif
 #ifndef PNR_CONV_CH
-#define PNR_CONV_CH 32
+#define PNR_CONV_CH 16
 #endif
 constexpr int kConvRO = PNR_CONV_RO, kConvCH = PNR_CONV_CH;   // conv tile: output rows, staged channels
 constexpr int kHRowPx = kHPx + 2;
@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(256, 2) k_conv3x3_h2(ConvH2Args a) {
   const float osc = *a.wscale / xs;
   const int ktap = a.Cin / 16;             // k-steps per tap
   const uint4* wp = a.wp + lane;
-  constexpr int WD = NT >= 4 ? 2 : kHWD;   // weight ring depth (NT = 4: 2 k-steps, no spills)
+  constexpr int WD = NT * RO >= 4 ? 2 : kHWD;   // weight ring depth (2 k-steps where 3 would spill)
   float amax = 0.f;
   // staged channels of chunk ci0 (the backward's cat images: zero-padding tails skipped)
   auto nreal_of = [&](int ci0) {
