@@ -412,13 +412,13 @@ __global__ void k_sum_splits(const float* __restrict__ part, int64_t n, int nspl
   }
 }
 
-static void wgrad_plan(int64_t npix, int M, int Cin, int* nsplit, int64_t* chunk) {
-  // ~2 workgroups per CU over the 3 kernel rows, >= 8 chunks of 32 pixels per split
+static void wgrad_plan(int64_t npix, int M, int Cin, int* nsplit, int64_t* chunk, int px = 32) {
+  // ~2 workgroups per CU over the 3 kernel rows, >= 8 chunks of px pixels per split
   int64_t s = cdiv((int64_t)512, (int64_t)3);
-  const int64_t maxs = cdiv(npix > 0 ? npix : 1, (int64_t)256);
+  const int64_t maxs = cdiv(npix > 0 ? npix : 1, (int64_t)8 * px);
   if (s > maxs) s = maxs;
   int64_t ch = cdiv(npix > 0 ? npix : 1, s);
-  ch = cdiv(ch, 32) * 32;
+  ch = cdiv(ch, px) * px;
   *chunk = ch;
   *nsplit = (int)(npix > 0 ? cdiv(npix, ch) : 1);
   (void)M;
@@ -470,7 +470,6 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
 // no fallback path.  The stacked rows [trunk; rgb; 0] all run as MFMA tiles
 // (the rgb rows' tile: 3 live rows of 32; the MFMAs are cheap at this rate).
 constexpr int kHPx = 128;                 // pixels per tile (4 waves x 32)
-constexpr int kHPitch = 40;               // wgrad images: f16 per staged row (32 px + 8): 80 B, conflict-free
 #ifndef PNR_CONV_RO
 #define PNR_CONV_RO 2
 #endif
@@ -763,23 +762,27 @@ static int launch_conv_h2(const ConvH2Args& a, hipStream_t st) {
 // Both operands are activations, so both are split and scaled: dY staged times
 // 2^e with max in [8, 16) (so Ys = 2^11 Yh stays in f16), X times 2^e' with max
 // in [2^14, 2^15); dW = 2^-11 (Ys.Xh + Yl.Xh + Yh.Xl) / (2^e 2^e').  k = pixel:
-// per 32-pixel chunk (two 16-pixel k-steps) dY is staged transposed as
-// [plane][m][32 px] and X as three kx-shifted copies [kx][plane][ci][32 px]
+// per PX-pixel chunk (PX / 16 k-steps; 64 for the two small stages, whose
+// chunks are otherwise latency-bound, 32 for stage 0's 224 staging tasks) dY is
+// staged transposed as [plane][m][PX px] and X as three kx-shifted copies
+// [kx][plane][ci][PX px]
 // (the row-edge and image-edge zeros applied while staging), each lane
-// transposing 8 pixels x 4 channels in registers; 80-B rows, conflict-free
-// ds_read_b128 A and B fragments.  One 4-wave workgroup per (pixel split, ky);
+// transposing 8 pixels x 4 channels in registers; 80-B / 144-B rows (5 / 9
+// 16-B slots, odd: conflict-free ds_read_b128 A and B fragments).  One 4-wave workgroup per (pixel split, ky);
 // wave w takes column tiles j = w, w + 4, w + 8 of the 3 NC (kx, channel-tile)
 // pairs x all MT row tiles.  db from the fp32 values while staging (ky = 0
 // blocks).  Partials per split, summed in fixed order (k_sum_splits).
-template <int MT, int NC>
+template <int MT, int NC, int PX>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const unsigned* y_max, const unsigned* x_max) {
   constexpr int M = 32 * MT, C = 32 * NC;
-  static_assert(M + C <= 256, "one staging task per thread");
-  constexpr int PA = M * kHPitch, PB = C * kHPitch;      // f16 per plane
+  constexpr int NO = PX / 8;                            // pixel octets per chunk
+  static_assert((M + C) / 4 * NO <= 256, "one staging task per thread");
+  constexpr int PIT = PX + 8;                           // f16 per staged row: 80 B (32 px) / 144 B (64 px)
+  constexpr int PA = M * PIT, PB = C * PIT;             // f16 per plane
   constexpr int NJ = 3 * NC, JW = (NJ + 3) / 4;
   __shared__ __attribute__((aligned(16))) _Float16 as_h[2 * PA];
   __shared__ __attribute__((aligned(16))) _Float16 bs_h[3 * 2 * PB];
-  __shared__ float dbs[4][M];
+  __shared__ float dbs[NO][M];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int split = blockIdx.x, ky = blockIdx.y;
   const int npix = a.H * a.W;
@@ -799,9 +802,10 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
   // pixel octet ob: the 10 source pixels p - 1 .. p + 8 of its 8 pixels (one load
   // each), from which the three kx-shifted copies are cut; C <= tid < C + M -> dY
   // channel quad qa of pixel octet oa.
-  const bool tb = tid < C, ta = !tb && tid < C + M;
+  const bool tb = tid < C / 4 * NO, ta = !tb && tid < (C + M) / 4 * NO;
   const int qb = tid % (C / 4), ob = tid / (C / 4);
-  const int qa = (tid - C) % (M / 4), oa = (tid - C) / (M / 4);
+  const int ta_i = tid - C / 4 * NO;
+  const int qa = ta_i % (M / 4), oa = ta_i / (M / 4);
   float4 v[10];
   auto load = [&](int p0) {
     if (tb) {
@@ -822,7 +826,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
     }
   };
   // 8 pixels x 4 channels (pixel jj = v[jj + sh], zero where !(ok >> jj & 1)) ->
-  // per channel k: [hi 8 px] at base + k * kHPitch, lo at + pitch_pl
+  // per channel k: [hi 8 px] at base + k * PIT, lo at + pitch_pl
   auto put8x4 = [&](_Float16* base, int pitch_pl, int sh, unsigned ok, float sc) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -835,8 +839,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
         const float e1 = (ok >> (2 * j + 1)) & 1u ? f1[k] * sc : 0.f;
         splith(e0, e1, hi[j], lo[j]);
       }
-      *reinterpret_cast<uint4*>(base + k * kHPitch) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-      *reinterpret_cast<uint4*>(base + k * kHPitch + pitch_pl) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+      *reinterpret_cast<uint4*>(base + k * PIT) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+      *reinterpret_cast<uint4*>(base + k * PIT + pitch_pl) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
     }
   };
   auto put = [&](int p0) {
@@ -853,7 +857,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
         okr |= (unsigned)(x < a.W - 1) << jj;
         x = x + 1 == a.W ? 0 : x + 1;
       }
-      _Float16* base = bs_h + (4 * qb) * kHPitch + 8 * ob;
+      _Float16* base = bs_h + (4 * qb) * PIT + 8 * ob;
       put8x4(base, PB, 0, okp & okl, xs);
       put8x4(base + 2 * PB, PB, 1, okp, xs);
       put8x4(base + 4 * PB, PB, 2, okp & okr, xs);
@@ -865,20 +869,20 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
         db[2] += v[j].z;
         db[3] += v[j].w;
       }
-      put8x4(as_h + (4 * qa) * kHPitch + 8 * oa, PA, 0, 0xffu, ys);
+      put8x4(as_h + (4 * qa) * PIT + 8 * oa, PA, 0, 0xffu, ys);
     }
   };
   if (pbeg < pend) load(pbeg);
-  for (int p0 = pbeg; p0 < pend; p0 += 32) {
+  for (int p0 = pbeg; p0 < pend; p0 += PX) {
     put(p0);
     __syncthreads();
-    if (p0 + 32 < pend) load(p0 + 32);   // in flight during the MFMAs
+    if (p0 + PX < pend) load(p0 + PX);   // in flight during the MFMAs
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < PX / 16; ++s) {
       uint4 yl_[MT], yh_[MT];   // (Ys = 2^11 Yh made per use: 4 v_pk_mul, 12 fewer VGPRs live)
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        const _Float16* pa = as_h + (32 * t + c) * kHPitch + 16 * s + 8 * h;
+        const _Float16* pa = as_h + (32 * t + c) * PIT + 16 * s + 8 * h;
         yh_[t] = *reinterpret_cast<const uint4*>(pa);
         yl_[t] = *reinterpret_cast<const uint4*>(pa + PA);
       }
@@ -887,7 +891,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
         const int j = wid + 4 * u;
         if (j < NJ) {
           const int kx = j / NC, nc = j - kx * NC;
-          const _Float16* pb = bs_h + kx * 2 * PB + (32 * nc + c) * kHPitch + 16 * s + 8 * h;
+          const _Float16* pb = bs_h + kx * 2 * PB + (32 * nc + c) * PIT + 16 * s + 8 * h;
           const uint4 xh = *reinterpret_cast<const uint4*>(pb);
           const uint4 xl = *reinterpret_cast<const uint4*>(pb + PB);
 #pragma unroll
@@ -915,17 +919,22 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_h2(WgradArgs a, const uns
       for (int r = 0; r < 16; ++r)
         out[(int64_t)(32 * t + (r & 3) + 8 * (r >> 2) + 4 * h) * N + col] = acc[u][t][r] * osc;
   }
-  if (ky == 0) {   // db: the four pixel octets' sums per channel, octet order
+  if (ky == 0) {   // db: the pixel octets' sums per channel, octet order
     if (ta) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) dbs[oa][4 * qa + k] = db[k];
     }
     __syncthreads();
-    if (tid < M) out[(int64_t)M * N + tid] = ((dbs[0][tid] + dbs[1][tid]) + dbs[2][tid]) + dbs[3][tid];
+    if (tid < M) {
+      float sdb = dbs[0][tid];
+#pragma unroll
+      for (int o = 1; o < NO; ++o) sdb += dbs[o][tid];
+      out[(int64_t)M * N + tid] = sdb;
+    }
   }
 }
 
-template <int MT, int NC>
+template <int MT, int NC, int PX>
 static int launch_wgrad_h2(const float* dyb, const unsigned* y_max, const float* x, const unsigned* x_max, int H,
                            int W, float* part, float* dw, hipStream_t st) {
   WgradArgs g;
@@ -936,9 +945,9 @@ static int launch_wgrad_h2(const float* dyb, const unsigned* y_max, const float*
   g.M = 32 * MT;
   g.Cin = 32 * NC;
   int ns;
-  wgrad_plan((int64_t)H * W, g.M, g.Cin, &ns, &g.chunk);
+  wgrad_plan((int64_t)H * W, g.M, g.Cin, &ns, &g.chunk, PX);
   g.part = part;
-  hipLaunchKernelGGL((k_conv_wgrad_h2<MT, NC>), dim3(ns, 3), dim3(256), 0, st, g, y_max, x_max);
+  hipLaunchKernelGGL((k_conv_wgrad_h2<MT, NC, PX>), dim3(ns, 3), dim3(256), 0, st, g, y_max, x_max);
   PNR_LAUNCH_CHECK();
   const int64_t n = (int64_t)g.M * 9 * g.Cin + g.M;
   hipLaunchKernelGGL(k_sum_splits, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, part, n, ns, dw, (int64_t)0,
@@ -1268,7 +1277,7 @@ extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch
   a.out_max = words + 1 * kWS;
   a.act = net1;
   if ((rc = launch_conv_h2<1, 2>(a, st))) return rc;
-  if ((rc = launch_wgrad_h2<1, 1>(cat2, words + 0, net1, fwords + 2 * kWS, H, W, part, dw2, st))) return rc;
+  if ((rc = launch_wgrad_h2<1, 1, 64>(cat2, words + 0, net1, fwords + 2 * kWS, H, W, part, dw2, st))) return rc;
   // stage 1: d net0 = conv(cat1 = [dz1, g, 0], flipped [conv_layers.1; conv_rgb.1]), masked by net0
   a.in = cat1;
   a.Cin = 64;
@@ -1282,7 +1291,7 @@ extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch
   a.out_max = words + 2 * kWS;
   a.act = net0;
   if ((rc = launch_conv_h2<2, 2>(a, st))) return rc;
-  if ((rc = launch_wgrad_h2<2, 2>(cat1, words + 1 * kWS, net0, fwords + 1 * kWS, H, W, part, dw1, st))) return rc;
+  if ((rc = launch_wgrad_h2<2, 2, 64>(cat1, words + 1 * kWS, net0, fwords + 1 * kWS, H, W, part, dw1, st))) return rc;
   // stage 0: d x = conv(cat0 = [dz0, g, 0], flipped [conv_layers.0; conv_rgb.0])
   a.in = cat0;
   a.Cin = 96;
@@ -1296,5 +1305,5 @@ extern "C" int pnr_neural_render_bwd_h2(const float* x, const float* fwd_scratch
   a.out_max = nullptr;
   a.act = nullptr;
   if ((rc = launch_conv_h2<4, 1>(a, st))) return rc;
-  return launch_wgrad_h2<3, 4>(cat0, words + 2 * kWS, x, fwords + 0 * kWS, H, W, part, dw0, st);
+  return launch_wgrad_h2<3, 4, 32>(cat0, words + 2 * kWS, x, fwords + 0 * kWS, H, W, part, dw0, st);
 }

@@ -170,3 +170,58 @@ def test_dp_finetune_step_equals_single_process():
     for p in ps:
         p.join(60)
     assert all(v == "ok" for v in res.values()), res
+
+
+def _rccl_worker(port, q):
+    """One rank on the box's GPU over the "nccl" backend (= RCCL): every RCCL
+    branch of parallel.py runs (all_gather_into_tensor of tiles, step batches,
+    frames and GradReducer's row gathers, a flat all_reduce)."""
+    try:
+        import torch.distributed as dist
+        from pointnerf_amd.parallel import FrameShard, GradReducer, StepShard, TileShard
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cuda = torch.device("cuda:0")
+        torch.cuda.set_device(cuda)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        assert dist.get_backend() == "nccl"
+        g = torch.Generator(device="cpu").manual_seed(3)
+        frames = [torch.randn((H * W, 5), generator=g).to(cuda) for _ in THETAS]
+        errs = []
+        for layout in ("bands", "tiles16"):
+            sh = TileShard(H, W, 0, 1, 0, cuda, layout=layout)
+            if not torch.equal(sh.assemble(sh.select(frames[0])), frames[0]):
+                errs.append("TileShard " + layout)
+        st = StepShard([TileShard(H, W, 0, 1, f, cuda) for f in range(len(THETAS))], cuda)
+        got = st.assemble_async(st.select(frames)).wait()
+        if not all(torch.equal(a, b) for a, b in zip(got, frames)):
+            errs.append("StepShard")
+        fr = FrameShard(0, 1).assemble_async(frames[1]).wait()
+        if not (fr.shape == (1, H * W, 5) and torch.equal(fr[0], frames[1])):
+            errs.append("FrameShard")
+        t = torch.arange(12, dtype=torch.float32, device=cuda).reshape(3, 4)
+        gr = GradReducer([], [])
+        if not torch.equal(gr._all_gather(t)[0], t):
+            errs.append("GradReducer._all_gather")
+        x = torch.ones(7, device=cuda)
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+        if not torch.equal(x, torch.ones(7, device=cuda)):
+            errs.append("all_reduce")
+        dist.destroy_process_group()
+        q.put(errs)
+    except Exception as e:   # noqa: BLE001 -- reported to the parent
+        q.put([repr(e)])
+
+
+def test_rccl_branches_single_rank():
+    """The RCCL (backend "nccl") branches of TileShard / StepShard / FrameShard /
+    GradReducer execute on the GPU box and assemble exactly (one rank: the
+    8-GPU run is the driver's; RCCL does not allow two ranks on one GPU)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    errs = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0, p.exitcode
+    assert errs == [], errs
