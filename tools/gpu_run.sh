@@ -53,6 +53,8 @@ for s in $STEPS; do
       timeout -k 10 300 python -u -m pytest tests/test_gpu_neural_render.py -m gpu -x -v --timeout 120 \
         --timeout-method thread > $O/t_nr.log 2>&1 || { tail -40 $O/t_nr.log; exit 1; }
       tail -3 $O/t_nr.log ;;
+    benchprof)   # bench line + kernel stats + PMC passes (tools/prof_bench.sh), folded by tools/profile_summary.py
+      bash tools/prof_bench.sh $(basename $O)/bp || { tail -20 $O/bp/*.log; exit 1; } ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
         python bench.py --no-cpu-baseline > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; } ;;
