@@ -505,10 +505,9 @@ def main():
             steps[cis] = (st, rd, cp, cr)
         return steps[cis]
 
-    def step(s, timed):
+    def issue(s, timed):
         # every render call of the step is issued without a host sync
-        # (render_rays(sync=False)); model.finish() is the step's one sync: it
-        # checks the deferred feature-buffer sizes / f16 range and returns the counts
+        # (render_rays(sync=False)); complete() holds the step's one sync
         parts = []
         ev_step = [] if timed else None
         if shard_world > 1 and not args.per_frame_calls:
@@ -530,7 +529,14 @@ def main():
                 parts.append((sh, color, rd.shape[0]))
         if timed:
             clock_probe()
-        counts = model.finish()
+        return parts, ev_step, timed
+
+    def complete(st):
+        # model.finish(upto) waits for this step's calls only (the next step's are
+        # already queued behind them, so the GPU does not idle while the host
+        # checks the deferred feature-buffer sizes / f16 range) and returns the counts
+        parts, ev_step, timed = st
+        counts = model.finish(upto=len(parts))
         if timed:
             for c, (_, _, nr) in zip(counts, parts):
                 stage["pairs"] += c["n_pairs"]
@@ -559,6 +565,9 @@ def main():
     if shard_world > 1 and not args.per_frame_calls:
         for s in range(args.warmup + args.steps):   # ray batches + gather maps built outside the timed region
             step_batch(s)
+    def step(s, timed):
+        return complete(issue(s, timed))
+
     for s in range(args.warmup):
         finish(step(s, False))
     torch.cuda.synchronize()
@@ -568,10 +577,12 @@ def main():
     rerenders0 = model.overflow_rerenders
     t0 = time.perf_counter()
     prev = []
-    for s in range(args.steps):
-        cur = step(args.warmup + s, True)
-        finish(prev)   # step s-1's all-gather travelled over xGMI while step s rendered
-        prev = cur
+    pend = issue(args.warmup, True)
+    for s in range(1, args.steps + 1):
+        nxt = issue(args.warmup + s, True) if s < args.steps else None   # queued before step s-1's sync
+        cur = complete(pend)
+        finish(prev)   # step s-2's all-gather travelled over xGMI while steps s-1 and s rendered
+        prev, pend = cur, nxt
     finish(prev)       # the last step's frames are gathered inside the timed region
     torch.cuda.synchronize()
     t_local = time.perf_counter() - t0

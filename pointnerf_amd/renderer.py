@@ -300,17 +300,38 @@ class NeuralPointsRayMarching(nn.Module):
         self._sv_per_ray = r if self._sv_per_ray is None else max(self._sv_per_ray, r)
 
     @torch.no_grad()
-    def finish(self):
+    def finish(self, upto=None):
         """Complete every ``render_rays(sync=False)`` call issued since the last
-        finish(): one host synchronisation, then the deferred checks.  A call
-        whose valid samples overflowed its feature buffer, or (fp32h2) any call
-        when an activation left the f16 range, is rendered again synchronously
-        into its own output tensors.  Returns the per-call sample counts (the
-        ``last_counts`` dict of each call, in issue order)."""
-        pend, self._pending = self._pending, []
+        finish() -- or only the oldest ``upto`` of them, so the caller can keep
+        the next calls queued on the GPU while the host checks these: one host
+        synchronisation (on the last completed call), then the deferred checks.
+        A call whose valid samples overflowed its feature buffer, or (fp32h2) any
+        call when an activation left the f16 range, is rendered again
+        synchronously into its own output tensors (a raised range flag is shared
+        by the calls still in flight, so then every pending call is completed and
+        the later ones' counts are kept for the next finish()).  Returns the
+        per-call sample counts (the ``last_counts`` dict of each call, in issue
+        order)."""
+        done = getattr(self, "_done", [])
+        n_all = len(done) + len(self._pending)
+        k = n_all if upto is None else min(int(upto), n_all)
+        need = k - len(done)
+        if need > 0:
+            head = self._pending[:need]
+            head[-1]["event"].synchronize()
+            if need < len(self._pending) and any(int(r["range_flag"].item()) != 0 for r in head
+                                                 if r.get("range_flag") is not None):
+                head = self._pending
+                head[-1]["event"].synchronize()
+            self._pending = self._pending[len(head):]
+            done = done + self._complete(head)
+        self._done = done[k:]
+        return done[:k]
+
+    def _complete(self, pend):
+        """finish()'s checks on calls whose last kernels have completed."""
         if not pend:
             return []
-        pend[-1]["event"].synchronize()
         # every fp32h2 call's own range flag (the packs -- and their flag -- are
         # rebuilt when the weights change between calls)
         flags = {}

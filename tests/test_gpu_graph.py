@@ -44,6 +44,33 @@ def test_async_render_equals_sync(cuda, precision):
         assert _eq(w, g)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32h2"])
+def test_partial_finish_keeps_later_calls_queued(cuda, precision):
+    """finish(upto=k) completes the oldest k sync-free calls only (bench.py
+    issues step s + 1 before completing step s); the rest complete at the next
+    finish() -- counts in issue order, outputs equal to the synchronous renders;
+    an overflowing call among them is re-rendered in place."""
+    sc, cams = _cams(cuda, thetas=(30.0, 200.0, 120.0))
+    m = _renderer(sc, cuda, formula_params(salt=0.4))
+    m.precision = precision
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    want, counts = [], []
+    for cp, cr, rd in cams:
+        want.append([t.clone() for t in m.render_rays(cp, cr, rd, 2.0, 6.0, bg)])
+        counts.append(dict(m.last_counts))
+    got = [m.render_rays(cp, cr, rd, 2.0, 6.0, bg, sync=False) for cp, cr, rd in cams[:2]]
+    assert m.finish(upto=1) == counts[:1]
+    assert len(m._pending) == 1
+    got.append(m.render_rays(*cams[2], 2.0, 6.0, bg, sync=False))
+    assert m.finish(upto=1) == counts[1:2]
+    m._sv_per_ray = 0.01            # the next call overflows its estimated feature buffer
+    got.append(m.render_rays(*cams[0], 2.0, 6.0, bg, sync=False))
+    assert m.finish() == [counts[2], counts[0]]
+    assert m.overflow_rerenders == 1
+    for w, g in zip(want + [want[0]], got):
+        assert _eq(w, g)
+
+
 def test_async_overflow_rerenders_in_place(cuda):
     """A sync-free call whose valid samples outgrow the estimated feature
     buffer is composited memory-safely (rows past the buffer never read) and
