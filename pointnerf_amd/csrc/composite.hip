@@ -16,6 +16,10 @@
 namespace pnr {
 
 constexpr int kCBlock = 256;
+#ifndef PNR_COMP_ROWS
+#define PNR_COMP_ROWS 8
+#endif
+constexpr int kCRows = PNR_COMP_ROWS;   // feature rows in flight per ray (a ray has ~8 valid samples)
 
 __device__ __forceinline__ float wave_max_scan_incl(float v) {
   const int lane = threadIdx.x & 63;
@@ -165,15 +169,15 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
     if (lane + 64 < SR) a.opacity[r * SR + lane + 64] = so.op1;
     const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
     // colour = sum_s w_s * features[s, 1:] + bg * T_bg  (lane = channel)
-    // valid slots in slot order, 4 feature rows in flight per iteration
+    // valid slots in slot order, kCRows feature rows in flight per iteration
     // (same accumulation order as a plain slot loop)
     float col0 = 0.f, col1 = 0.f;
     unsigned long long m0 = __ballot(vrow[0] >= 0), m1 = __ballot(vrow[1] >= 0);
     while (m0 | m1) {
-      int vr[4];
-      float w[4];
+      int vr[kCRows];
+      float w[kCRows];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kCRows; ++u) {
         vr[u] = -1;
         w[u] = 0.f;
         if (m0) {
@@ -188,15 +192,15 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
           w[u] = __shfl(w1, src);
         }
       }
-      float f0[4], f1[4];
+      float f0[kCRows], f1[kCRows];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kCRows; ++u) {
         const float* f = a.feat + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * CF + 1;
         f0[u] = (vr[u] >= 0 && lane < C) ? f[lane] : 0.f;
         f1[u] = (vr[u] >= 0 && lane + 64 < C) ? f[lane + 64] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kCRows; ++u) {
         if (vr[u] < 0) break;
         col0 += w[u] * f0[u];
         col1 += w[u] * f1[u];

@@ -49,6 +49,12 @@ for s in $STEPS; do
     dbg)
       timeout -k 10 200 python tools/_var/dbg_h2_train.py > $O/dbg.log 2>&1 || { tail -30 $O/dbg.log; exit 1; }
       cat $O/dbg.log ;;
+    compab)   # composite rows-in-flight variants (tools/_var), two rounds
+      for rnd in 1 2; do for v in tools/_var/libpnr_comp*.so; do
+        PNR_LIB=$PWD/$v timeout -k 10 200 python tools/agg_bench.py --precision fp32h2 --reps 5 >> $O/compab.jsonl 2>> $O/compab.err \
+          || { tail -20 $O/compab.err; exit 1; }
+      done; done
+      python -c "import json; [print(d['lib'][-20:], d['stages_ms'], d['checksum']) for d in map(json.loads, open('$O/compab.jsonl'))]" ;;
     tnr)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_neural_render.py -m gpu -x -v --timeout 120 \
         --timeout-method thread > $O/t_nr.log 2>&1 || { tail -40 $O/t_nr.log; exit 1; }
