@@ -372,6 +372,14 @@ int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_
 /* PointAggregator.forward signature (pre-gathered tensors): pts tables are the
  * gathered [rows*K, C] tensors, s->pidx must be NULL (pair row = row*K + k),
  * pts->pers required, validity from pair_mask[rows*K] (sample_pnt_mask). */
+/* block1.0's per-point half alone (k_point_pre_h2): P1 rows of every point (of
+ * pts->used when set) into the head of an aggregate scratch -- the rows
+ * pnr_aggregate_fwd_h2 reads with pts->p1_ready = 1.  P1 depends on the points
+ * and weights only, so the renderer issues it on a side stream beside the
+ * (latency-bound) query instead of in front of the pairs kernel; wh's w1ah /
+ * scale1a / range_flag as pnr_aggregate_fwd_h2. */
+int pnr_point_pre_h2(const pnr_points* pts, const pnr_mlp_h2* wh, void* scratch, size_t scratch_bytes,
+                     void* stream);
 int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                              const uint8_t* pair_mask, float* out_feat, float* out_weight,
                              float* out_conf, void* scratch, size_t scratch_bytes, void* stream);

@@ -153,6 +153,7 @@ SIGNATURES = {
                                   c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpX3), c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
+    "pnr_point_pre_h2": (c_int, [P(Points), P(MlpH2), c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_h2": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpH2), c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, c_void_p,

@@ -1535,6 +1535,21 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
   return launch_t<false>(a, st, kStageColor);
 }
 
+extern "C" int pnr_point_pre_h2(const pnr_points* pts, const pnr_mlp_h2* wh, void* scratch, size_t scratch_bytes,
+                                void* stream) {
+  PNR_CHECK_ARG(pts && wh && pts->emb && scratch, "point_pre_h2: null pointer");
+  PNR_CHECK_ARG(wh->w1ah && ((uintptr_t)wh->w1ah & 15) == 0 && wh->scale1a > 0.f && wh->scale1a < 1e30f,
+                "point_pre_h2: bad block1.0 point-half pack");
+  PNR_CHECK_ARG(((uintptr_t)pts->emb & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+                "point_pre_h2: emb and scratch must be 16-B aligned");
+  const int64_t n_p1 = pts->used ? pts->n_used : pts->n;
+  PNR_CHECK_ARG(n_p1 >= 0 && scratch_bytes >= (size_t)(n_p1 > 0 ? n_p1 : 1) * kHid * sizeof(float),
+                "point_pre_h2: scratch too small for the P1 rows");
+  if (n_p1 == 0) return PNR_OK;
+  return launch_point_pre_h2(*pts, wh->w1ah, wh->scale1a, wh->range_flag, static_cast<float*>(scratch),
+                             as_stream(stream));
+}
+
 extern "C" int pnr_aggregate_fwd_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                         const uint8_t* pair_mask, float* out_feat, float* out_weight,
                                         float* out_conf, void* scratch, size_t scratch_bytes,

@@ -137,6 +137,7 @@ class _RenderState:
         self.bufs = None
         self.scratch = None
         self.scratch_key = None
+        self.side = None   # fp32h2: the side stream P1 runs on
 
 
 def _counts_dict(c):
@@ -165,6 +166,7 @@ class NeuralPointsRayMarching(nn.Module):
         # render_rays_train's per-pair forward: "fp32x3" (split-bf16 MFMA,
         # fp32-accurate, the default) or "fp32" (native fp32 MFMA)
         self.train_precision = "fp32x3"   # per-pair forward chain: fp32x3 (split-bf16 MFMA) / fp32h2 / fp32
+        self.p1_side_stream = True        # fp32h2 sync-free calls: P1 beside the query (see _render_rays)
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
         self.h2_fallbacks = 0
@@ -428,12 +430,43 @@ class NeuralPointsRayMarching(nn.Module):
             rec = dict(precision=precision, caps=[], host=host, dcounts=dcounts,
                        range_flag=_keeph["range_flag"] if _keeph is not None else None)
 
-        def mark():
+        def mark(stream=None):
             if events is None:
                 return None
             e = torch.cuda.Event(enable_timing=True)
-            e.record()
+            e.record(stream)
             return e
+
+        # fp32h2: block1.0's per-point half (P1) depends on the points and weights
+        # only, so it runs on a side stream beside the query (which is latency
+        # bound and leaves the MFMA pipes idle) instead of in front of k_pairs_h2;
+        # the aggregate waits on its event.  Sync-free calls only (their feature
+        # buffer, hence the scratch holding P1, is sized before the query), not
+        # under graph capture.
+        p1_side = None
+        if (precision == "fp32h2" and capacity is not None and keep is None and self.p1_side_stream
+                and self.aggregator.pairs_kernel == "wt"):
+            c0 = min(chunk, R)
+            Sv0 = min(int(c0 * capacity) + 1024, c0 * SR)
+            scr0, ready0 = self._agg_scratch(state, max(Sv0, 1), pts.n, dev, bf16, reuse_p1, precision)
+            if not ready0:
+                if getattr(state, "side", None) is None:
+                    state.side = torch.cuda.Stream(device=dev)
+                main = torch.cuda.current_stream(dev)
+                ev_in = torch.cuda.Event()
+                ev_in.record(main)
+                side = state.side
+                side.wait_event(ev_in)
+                s0 = mark(side)
+                L.check(L.lib().pnr_point_pre_h2(L.ctypes.byref(pts), L.ctypes.byref(mlph), L.ptr(scr0),
+                                                 scr0.numel() * 4, L.c_void_p(side.cuda_stream)), "pnr_point_pre_h2")
+                s1 = mark(side)
+                ev_p1 = torch.cuda.Event()
+                ev_p1.record(side)
+                scr0.record_stream(side)
+                p1_side = ev_p1
+                if events is not None:
+                    events.append(("p1", s0, s1))
 
         for ci, r0 in enumerate(range(0, R, chunk)):
             r1 = min(R, r0 + chunk)
@@ -458,6 +491,9 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.fill_rs.data_ptr(), SR, K, L.ptr(rc))
             e2 = mark()
             scratch, ready = self._agg_scratch(state, max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
+            if p1_side is not None:   # P1 written into this same scratch by the side stream
+                torch.cuda.current_stream(dev).wait_event(p1_side)
+                ready = True
             pts.p1_ready = int(ready)
             if bf16:
                 L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
