@@ -285,16 +285,17 @@ def time_grid_build(model, opt, reps=3):
                                f"{int(getattr(opt, 'grid_seed', 0))})"}
 
 
-def isolated_stage_times(model, opt, cam, bg, reps=3):
-    """Per-stage HIP-event times of one frame with every stage on the launch
-    stream (P1 not beside the query), outside the timed region: the stage
-    rooflines describe each stage alone, while the headline value includes the
-    side stream's overlap."""
+def isolated_stage_times(model, opt, frames, bg):
+    """Per-stage HIP-event times of the timed steps' frames rendered again with
+    every stage on the launch stream (P1 not beside the query), outside the
+    timed region: the stage rooflines describe each stage alone (same frames,
+    so the same counts), while the headline value includes the side stream's
+    overlap."""
     side = model.p1_side_stream
     model.p1_side_stream = False
     per = {}
     try:
-        for _ in range(reps):
+        for cam in frames:
             ev = []
             model.render_rays(*cam, opt.near_plane, opt.far_plane, bg, events=ev, sync=False)
             model.finish()
@@ -714,8 +715,10 @@ def main():
         # build (bbox read + 8 kernels + scans) on its own line
         out["grid_build"] = time_grid_build(model, opt)
         per_stage = per
-        if "p1" in per:   # the timed steps ran P1 beside the query: time the stages alone for their rooflines
-            per_stage = isolated_stage_times(model, opt, dev_cams[0], bg)
+        if "p1" in per and shard_world == 1:
+            # the timed steps ran P1 beside the query: their frames again, stages alone, for the stage rooflines
+            per_stage = isolated_stage_times(model, opt, [dev_cams[(args.warmup + i) % len(dev_cams)]
+                                                          for i in range(args.steps)], bg)
             out["stages_ms_isolated"] = {k: [round(float(x), 3) for x in v] for k, v in per_stage.items()}
         out["stage_rooflines"] = stage_rooflines(args, opt, model, stage, per_stage, launches, out["grid_build"])
         acc = {}
