@@ -444,8 +444,12 @@ class NeuralPointsRayMarching(nn.Module):
         # buffer, hence the scratch holding P1, is sized before the query), not
         # under graph capture.
         p1_side = None
+        # (only while P1 is the smaller job: P1 costs ~0.5 us per point, the query
+        # ~3.5 us per ray -- measured 0.99 vs 2.25 ms at 2 M points / 640 k rays; at
+        # 10 M points / 1.25 M rays the 5.8 ms P1 outlasted the query and the overlap
+        # gained nothing)
         if (precision == "fp32h2" and capacity is not None and keep is None and self.p1_side_stream
-                and self.aggregator.pairs_kernel == "wt"):
+                and self.aggregator.pairs_kernel == "wt" and pts.n <= 4 * R):
             c0 = min(chunk, R)
             Sv0 = min(int(c0 * capacity) + 1024, c0 * SR)
             scr0, ready0 = self._agg_scratch(state, max(Sv0, 1), pts.n, dev, bf16, reuse_p1, precision)
