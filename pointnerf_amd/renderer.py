@@ -167,6 +167,7 @@ class NeuralPointsRayMarching(nn.Module):
         # fp32-accurate, the default) or "fp32" (native fp32 MFMA)
         self.train_precision = "fp32x3"   # per-pair forward chain: fp32x3 (split-bf16 MFMA) / fp32h2 / fp32
         self.p1_side_stream = True        # fp32h2 sync-free calls: P1 beside the query (see _render_rays)
+        self.p1_side_max_points_per_ray = 4.0
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
         self.h2_fallbacks = 0
@@ -449,7 +450,7 @@ class NeuralPointsRayMarching(nn.Module):
         # 10 M points / 1.25 M rays the 5.8 ms P1 outlasted the query and the overlap
         # gained nothing)
         if (precision == "fp32h2" and capacity is not None and keep is None and self.p1_side_stream
-                and self.aggregator.pairs_kernel == "wt" and pts.n <= 4 * R):
+                and self.aggregator.pairs_kernel == "wt" and pts.n <= self.p1_side_max_points_per_ray * R):
             c0 = min(chunk, R)
             Sv0 = min(int(c0 * capacity) + 1024, c0 * SR)
             scr0, ready0 = self._agg_scratch(state, max(Sv0, 1), pts.n, dev, bf16, reuse_p1, precision)

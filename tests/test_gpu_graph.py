@@ -71,6 +71,25 @@ def test_partial_finish_keeps_later_calls_queued(cuda, precision):
         assert _eq(w, g)
 
 
+def test_side_stream_p1_equals_sync(cuda):
+    """fp32h2 sync-free calls run P1 (pnr_point_pre_h2) on a side stream beside
+    the query and the aggregate waits on it: renders bitwise equal to the
+    synchronous path (P1 inline), over two cameras and a re-use of the scratch."""
+    sc, cams = _cams(cuda)
+    m = _renderer(sc, cuda, formula_params(salt=0.4))
+    m.precision = "fp32h2"
+    m.p1_side_max_points_per_ray = 1e9   # the test scene has more points than rays
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    want = [[t.clone() for t in m.render_rays(cp, cr, rd, 2.0, 6.0, bg)] for cp, cr, rd in cams]
+    for _ in range(2):
+        ev = []
+        got = [m.render_rays(cp, cr, rd, 2.0, 6.0, bg, sync=False, events=ev) for cp, cr, rd in cams]
+        m.finish()
+        assert sum(1 for name, _, _ in ev if name == "p1") == len(cams)
+        for w, g in zip(want, got):
+            assert _eq(w, g)
+
+
 def test_async_overflow_rerenders_in_place(cuda):
     """A sync-free call whose valid samples outgrow the estimated feature
     buffer is composited memory-safely (rows past the buffer never read) and
