@@ -470,13 +470,10 @@ static int launch_wgrad(const float* dyb, const float* x, int H, int W, int Cin,
 // no fallback path.  The stacked rows [trunk; rgb; 0] all run as MFMA tiles
 // (the rgb rows' tile: 3 live rows of 32; the MFMAs are cheap at this rate).
 constexpr int kHPx = 128;                 // pixels per tile (4 waves x 32)
-#ifndef PNR_CONV_RO
-#define PNR_CONV_RO 2
-#endif
-#ifndef PNR_CONV_CH
-#define PNR_CONV_CH 16
-#endif
-constexpr int kConvRO = PNR_CONV_RO, kConvCH = PNR_CONV_CH;   // conv tile: output rows, staged channels
+// conv tile: output rows x staged channels per chunk (A/B on one box, 800^2
+// forward / forward + backward: 1 x 32 1.35 / 4.55 ms, 1 x 16 1.23 / 4.68,
+// 2 x 16 1.00 / 4.31 -- kept; 2 x 32 spills at NT = 3)
+constexpr int kConvRO = 2, kConvCH = 16;
 constexpr int kHRowPx = kHPx + 2;
 constexpr int kHWD = 3;                   // weight fragments prefetched this many k-steps ahead
 constexpr int kWS = 16;                   // absmax words 64 B apart (no shared L2 line between them)
