@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 16
+#define PNR_ABI_VERSION 17
 
 enum {
   PNR_OK = 0,
@@ -439,6 +439,17 @@ int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, cons
                                const pnr_mlp_h2* wh, const pnr_agg_saved* saved, float* out_feat,
                                float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
                                void* stream);
+/* pnr_aggregate_fwd_train_h2 with its fallback on the device (v17): after the h2
+ * chain, k_point_pre (when P1 ran on fp32h2) and the native-fp32 k_pairs<train>
+ * are launched over the same outputs and saves, and each workgroup returns at
+ * once unless *wh->range_flag != 0 -- so a raised flag never needs a host read
+ * inside the step (the caller reads it later, asynchronously, to re-pick the
+ * shifts).  wh->range_flag is required.  Outputs: those of the h2 call when the
+ * flag stays down, those of pnr_aggregate_fwd_train when it is raised. */
+int pnr_aggregate_fwd_train_h2_guarded(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                       const pnr_mlp_h2* wh, const pnr_agg_saved* saved, float* out_feat,
+                                       float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
+                                       void* stream);
 int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
                                    const uint8_t* pair_mask, const pnr_agg_saved* saved,
                                    float* out_feat, float* out_weight, float* out_conf,

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 16
+ABI_VERSION = 17
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -167,6 +167,8 @@ SIGNATURES = {
                                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train_h2": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpH2), P(AggSaved), c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_train_h2_guarded": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpH2), P(AggSaved), c_void_p,
+                                                   c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train_masked": (c_int, [P(Points), P(Samples), P(Mlp), c_void_p, P(AggSaved), c_void_p,
                                                c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_bwd_pairs": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(AggSaved), c_void_p,

@@ -480,8 +480,8 @@ class PointAggregator(nn.Module):
         (pnr_pack_weights_h2: no host sync while the weights change every step)
         with shifts kept from the last h2_shift pick; `range_flag` is raised by
         the pack when a weight outgrew its shift and by the forward when an
-        activation left the f16 range -- the caller then calls
-        h2_train_reset() (shifts re-picked) and re-runs the step on fp32x3."""
+        activation left the f16 range -- the guarded forward then runs its
+        fp32 fallback on the device, and h2_train_poll() re-picks the shifts."""
         key = self.h2_key()
         if getattr(self, "_packedh2t", None) is not None and key == self._packedh2t_key:
             return self._packedh2t
@@ -507,6 +507,32 @@ class PointAggregator(nn.Module):
         """After a raised training range flag: shifts re-picked at the next pack."""
         self._h2t_shifts = None
         self._packedh2t = None
+
+    def h2_train_launched(self):
+        """After a pnr_aggregate_fwd_train_h2_guarded launch: its range flag is
+        copied to pinned host memory behind an event, read by a later
+        h2_train_poll() -- the step itself never waits for it (the guarded
+        forward already ran its fp32 fallback on the device when the flag was up)."""
+        if getattr(self, "_h2t_host", None) is None:
+            self._h2t_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._h2t_host.copy_(self._h2t_flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._h2t_pending = ev
+
+    def h2_train_poll(self, wait: bool = False) -> bool:
+        """True once per raised flag of an earlier guarded forward (that step ran
+        on the fp32 fallback): the shifts are then re-picked at the next pack.
+        Does not block unless `wait`."""
+        ev = getattr(self, "_h2t_pending", None)
+        if ev is None or not (wait or ev.query()):
+            return False
+        ev.synchronize()
+        self._h2t_pending = None
+        if int(self._h2t_host[0]) == 0:
+            return False
+        self.h2_train_reset()
+        return True
 
     def h2_key(self):
         """Identity of the current weights (storage + version of every

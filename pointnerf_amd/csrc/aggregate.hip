@@ -50,7 +50,11 @@ struct AggArgs {
   float* out_conf;
   const uint8_t* pair_mask;   // mirror path: validity per (row, k); pidx == NULL
   pnr_agg_saved sv;           // training forward: activations kept for the backward
+  const int32_t* run_if = nullptr;   // set: the kernel runs only when *run_if != 0 (the guarded h2 forward's fallback)
 };
+
+// The guarded fallback: every workgroup leaves at once unless the h2 range flag is raised.
+__device__ __forceinline__ bool skip_run(const AggArgs& A) { return A.run_if && *A.run_if == 0; }
 
 template <int NT>
 __device__ __forceinline__ void zero_acc(f32x16 (&acc)[NT]) {
@@ -149,6 +153,7 @@ __device__ __forceinline__ void wave_sync() {
 // and gathered per pair instead of being recomputed for every (sample,
 // neighbour) pair that references the point (~22x reuse at 2 M points).
 __global__ void __launch_bounds__(kAggBlock, 1) k_point_pre(AggArgs A) {
+  if (skip_run(A)) return;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* X = lds_dyn + wid * kWaveLds;
@@ -382,6 +387,7 @@ constexpr int kPairSub = 1;   // tiles per workgroup sharing barriers (and weigh
 
 template <bool TRAIN>
 __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pairs(AggArgs A) {
+  if (skip_run(A)) return;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   const int sub = (threadIdx.x >> 6) / kPairWaves;   // which of the workgroup's tiles
   float* X = lds_dyn + sub * kPairsLdsFloats;  // quad rows [kQRows][kQP]
@@ -692,6 +698,7 @@ constexpr size_t kColLdsBytes = (size_t)kColQRows * kQP * sizeof(float);
 
 template <bool TRAIN>
 __global__ void __launch_bounds__(64 * kColWaves, 2) k_color(AggArgs A) {
+  if (skip_run(A)) return;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   float* X = lds_dyn;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1643,10 +1650,9 @@ extern "C" int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_sampl
   return launch_t<true>(a, st, kStageColor);
 }
 
-extern "C" int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
-                                          const pnr_mlp_h2* wh, const pnr_agg_saved* saved, float* out_feat,
-                                          float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
-                                          void* stream) {
+static int fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_h2* wh,
+                        const pnr_agg_saved* saved, float* out_feat, float* out_weight, float* out_conf,
+                        void* scratch, size_t scratch_bytes, void* stream, bool guarded) {
   int rc;
   if ((rc = check_common(pts, s, w, out_feat, static_cast<float*>(scratch), scratch_bytes))) return rc;
   if ((rc = check_saved(saved))) return rc;
@@ -1688,7 +1694,28 @@ extern "C" int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_sampl
   if ((rc = launch_pairs_split<true>(a.pts, a.s, a.w, sw, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
                                      tile_ctr, st, saved)))
     return rc;
+  if (guarded) {   // the native-fp32 chain over the same outputs, run on the device only if the flag is up
+    AggArgs f = a;
+    f.run_if = wh->range_flag;
+    f.pts.p1_ready = wh->w1ah ? 0 : 1;   // P1 again on fp32 when k_point_pre_h2 made it
+    if ((rc = launch_t<true>(f, st, kStagePre | kStagePairs))) return rc;
+  }
   return launch_t<true>(a, st, kStageColor);
+}
+
+extern "C" int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                          const pnr_mlp_h2* wh, const pnr_agg_saved* saved, float* out_feat,
+                                          float* out_weight, float* out_conf, void* scratch, size_t scratch_bytes,
+                                          void* stream) {
+  return fwd_train_h2(pts, s, w, wh, saved, out_feat, out_weight, out_conf, scratch, scratch_bytes, stream, false);
+}
+
+extern "C" int pnr_aggregate_fwd_train_h2_guarded(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                                  const pnr_mlp_h2* wh, const pnr_agg_saved* saved,
+                                                  float* out_feat, float* out_weight, float* out_conf,
+                                                  void* scratch, size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(wh && wh->range_flag, "aggregate_train_h2_guarded: range_flag required");
+  return fwd_train_h2(pts, s, w, wh, saved, out_feat, out_weight, out_conf, scratch, scratch_bytes, stream, true);
 }
 
 extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,

@@ -2,8 +2,8 @@
 // layered K-nearest search, and the R -> R' -> R'' compactions.
 //
 // Replaces query_grid_point_index (query_point_indices_worldcoords.py:614-721):
-//   mask_raypos (qpiw.py:390-414)          -> k_march (bitmap probe, early exit at SR)
-//   cumsum slot pick + get_shadingloc       -> k_march writes slot s of the first SR
+//   mask_raypos (qpiw.py:390-414)          -> k_march_coop (bitmap probe, early exit at SR)
+//   cumsum slot pick + get_shadingloc       -> k_march_coop writes slot s of the first SR
 //     (qpiw.py:655-677, 417-439)               occupied candidates directly
 //   query_neigh_along_ray_layered           -> k_knn (same traversal order, same
 //     (qpiw.py:442-528)                        K-buffer replacement rule)
@@ -63,53 +63,34 @@ __device__ __forceinline__ void ray_point(const float c[3], const float dir[3], 
   p[2] = ray_at(c[2], dir[2], t);
 }
 
-// mask_raypos + SR pick: the first SR candidates whose cell is set in the
-// dilated occupancy (qpiw.py:406-413, 664-665).
-__global__ void __launch_bounds__(kQBlock) k_march(QRays q, QGrid g, int SR,
-                                                   const uint32_t* __restrict__ occ_bits,
-                                                   int32_t* __restrict__ n_filled,
-                                                   uint16_t* __restrict__ slot_d) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < q.R;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t cam = cam_of(q, r);
-    const float c[3] = {q.campos[cam * 3], q.campos[cam * 3 + 1], q.campos[cam * 3 + 2]};
-    const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
-    int n = 0;
-    for (int d = 0; d < q.D && n < SR; ++d) {
-      float p[3];
-      ray_point(c, dir, tval(q, r, d), p);
-      const int x = vox_coord(p[0], g.shift[0], g.vs[0]);
-      const int y = vox_coord(p[1], g.shift[1], g.vs[1]);
-      const int z = vox_coord(p[2], g.shift[2], g.vs[2]);
-      if (x < 0 || x >= g.dims[0] || y < 0 || y >= g.dims[1] || z < 0 || z >= g.dims[2]) continue;
-      const int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
-      if ((occ_bits[id >> 5] >> (id & 31)) & 1u) {
-        slot_d[r * SR + n] = (uint16_t)d;
-        ++n;
-      }
-    }
-    n_filled[r] = n;
-  }
-}
-
-// k_march for small ray batches (a training batch: a few thousand rays, far
-// fewer lanes than the chip holds): 16 lanes per ray test 16 consecutive
-// candidates at a time, a ballot orders the group's hits, so a ray's first SR
-// hits get the same slots as k_march's serial walk (same positions, same bits)
-// in ~D/16 dependent steps instead of D.
+// mask_raypos + SR pick (qpiw.py:406-413, 664-665): the first SR candidates
+// whose cell is set in the dilated occupancy.  G lanes per ray test G
+// consecutive candidates at a time and a ballot orders the group's hits, so a
+// ray's first SR hits get the slots of a serial walk along the ray (same
+// positions, same bits) in ~D/G dependent steps instead of D; 16 lanes for
+// small ray batches (a training batch: far fewer rays than the chip holds).
 constexpr int64_t kMarchCoopRays = 32768;
+// Whole frames too: 8 lanes per ray, one workgroup per 32 rays, no grid cap
+// (A/B over 4 bench cameras, two rounds, bit-identical pidx: one lane per ray
+// with the 2048-block cap 2.218 / 2.210 / 2.047 / 2.167 ms query, uncapped
+// 2.238 / 2.242 / 2.055 / 2.176, 4 lanes 2.186 / 2.194 / 2.056 / 2.149, 8 lanes
+// 2.175 / 2.187 / 2.054 / 2.140, 16 lanes 2.191 / 2.204 / 2.075 / 2.150): the
+// per-ray tvals rows are read 32 B at a time instead of one lane per 1.6 KB row.
+constexpr int kMarchLanes = 8;
+constexpr unsigned kMarchGridCap = 1u << 20;
+template <int G>
 __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, QGrid g, int SR,
                                                         const uint32_t* __restrict__ occ_bits,
                                                         int32_t* __restrict__ n_filled,
                                                         uint16_t* __restrict__ slot_d) {
-  const int lane = threadIdx.x & 63, gl = lane & 15;
-  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; r < q.R;
-       r += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G; r < q.R;
+       r += ((int64_t)gridDim.x * blockDim.x) / G) {
     const int64_t cam = cam_of(q, r);
     const float c[3] = {q.campos[cam * 3], q.campos[cam * 3 + 1], q.campos[cam * 3 + 2]};
     const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
     int n = 0;   // hits so far: the same in every lane of the group
-    for (int d0 = 0; d0 < q.D && n < SR; d0 += 16) {
+    for (int d0 = 0; d0 < q.D && n < SR; d0 += G) {
       const int d = d0 + gl;
       bool hit = false;
       if (d < q.D) {
@@ -123,7 +104,7 @@ __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, QGrid g, int SR
           hit = (occ_bits[id >> 5] >> (id & 31)) & 1u;
         }
       }
-      const unsigned m = (unsigned)(__ballot(hit) >> (lane & 48)) & 0xffffu;
+      const unsigned m = (unsigned)(__ballot(hit) >> (lane & (64 - G))) & (G == 32 ? 0xffffffffu : (1u << G) - 1u);
       if (hit) {
         const int pos = n + __popc(m & ((1u << gl) - 1u));
         if (pos < SR) slot_d[r * SR + pos] = (uint16_t)d;
@@ -593,12 +574,12 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
     PNR_HIP(hipMemsetAsync(b->valid_off, 0, sizeof(int32_t), st));
     return PNR_OK;
   }
-  if (R <= kMarchCoopRays)   // few rays: 16 lanes per ray (latency), else one (throughput)
-    hipLaunchKernelGGL(k_march_coop, dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
+  if (R <= kMarchCoopRays)   // few rays: 16 lanes per ray (latency)
+    hipLaunchKernelGGL(k_march_coop<16>, dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
                        h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   else
-    hipLaunchKernelGGL(k_march, dim3(grid_for(R, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
-                       h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
+    hipLaunchKernelGGL(k_march_coop<kMarchLanes>, dim3(grid_for(R * kMarchLanes, kQBlock, kMarchGridCap)),
+                       dim3(kQBlock), 0, st, q, g, qp->SR, h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   PNR_LAUNCH_CHECK();
   if ((rc = exclusive_scan(b->n_filled, R, nullptr, b->ray_off, b->counts + 0, b->scratch,
                            b->scratch_bytes, st)))

@@ -128,7 +128,8 @@ class AggSpec:
         self.h2 = bool(h2)              # forward per-pair chain on pnr_aggregate_fwd_train_h2 (fp32h2, f16 MFMA)
         self.x3 = bool(x3) or self.h2   # per-pair chain on pnr_aggregate_fwd_train_x3 (fp32x3 split MFMA);
                                         # the backward's dX chain on fp32x3 with either forward
-        self.h2_fallback = False        # the h2 forward's range flag was raised: this call ran on fp32x3
+        self.h2_fallback = False        # an earlier h2 forward's range flag was found raised (that call ran
+                                        # its native-fp32 fallback on the device)
         self.used = used                # optional (used[int32], used_map[int32]) point subset
         self.pts_extra = pts_extra      # xyz / pers / campos / camrot pointers (no grad)
         self.pair_mask = pair_mask
@@ -164,21 +165,15 @@ class AggregateFn(torch.autograd.Function):
         scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
         keepx = None
         run_x3 = spec.pair_mask is None and spec.x3
-        done = False
         if spec.pair_mask is None and spec.h2:
+            # an earlier step's raised flag (its fallback already ran): shifts re-picked now
+            spec.h2_fallback = agg.h2_train_poll()
             wh, keepx = agg.packed_h2_train()
-            L.check(L.lib().pnr_aggregate_fwd_train_h2(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),
-                                                       ctypes.byref(wh), ctypes.byref(sv.c), L.ptr(feat), None, None,
-                                                       L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
-                    "pnr_aggregate_fwd_train_h2")
-            run_x3 = int(keepx["range_flag"].item()) != 0   # a weight or an activation left the f16 range
-            done = not run_x3
-            if run_x3:
-                agg.h2_train_reset()
-                spec.h2_fallback = True
-                feat.zero_()
-        if done:
-            pass
+            L.check(L.lib().pnr_aggregate_fwd_train_h2_guarded(
+                ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp), ctypes.byref(wh), ctypes.byref(sv.c),
+                L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
+                "pnr_aggregate_fwd_train_h2_guarded")
+            agg.h2_train_launched()
         elif run_x3:
             wx, keepx = agg.packed_x3()
             L.check(L.lib().pnr_aggregate_fwd_train_x3(ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp),

@@ -178,6 +178,41 @@ def test_train_forward_h2_saves_match_fp32(cuda):
     _check_saves_match(out["fp32"], out["fp32h2"])
 
 
+def test_train_h2_guarded_fallback(cuda):
+    """A raised range flag in the h2 training forward (forced here: every shift
+    12 below its pick, so the pack flags every weight) runs the native-fp32
+    chain on the device inside the same call -- no host read in the step: the
+    render and the kept activations equal train_precision fp32's bit for bit.
+    The next forward finds the flag (h2_train_poll), counts the fallback and
+    re-picks the shifts, and runs on fp32h2 again."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.45))
+    m.keep_train_saved = True
+    campos, camrot = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    m.train_precision = "fp32"
+    c32 = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0].detach().clone()
+    s32 = m.last_train_aux["saved"]
+    n = int(m.last_counts["S_valid"])
+    agg = m.aggregator
+    agg.packed_h2_train()
+    agg._h2t_shifts = [s - 12 for s in agg._h2t_shifts]
+    agg._packedh2t = None
+    m.train_precision = "fp32h2"
+    ch = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0].detach().clone()
+    sh = m.last_train_aux["saved"]
+    assert torch.equal(ch, c32)
+    P = n * 8
+    for k in ("prow", "x3e", "wt", "wn", "pe5", "h1", "h2", "h3", "h4", "pa", "mask"):
+        assert torch.equal(sh[k][:P], s32[k][:P]), k
+    assert torch.equal(sh["hid"][:n], s32["hid"][:n]) and torch.equal(sh["vmask"][:n], s32["vmask"][:n])
+    assert m.h2_fallbacks == 0 and agg.h2_train_poll(wait=True) and agg._h2t_shifts is None
+    c2 = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0].detach().clone()
+    assert not agg.h2_train_poll(wait=True)
+    close(c2, c32, "ray_color", rel=1e-4, scale=1e-6)
+    assert not torch.equal(c2, c32)   # on fp32h2 again: fp32-accurate, not bitwise fp32
+
+
 def test_train_h2_grads_vs_x3(cuda):
     """train_precision fp32h2 (the forward chain on f16-split MFMA, 3 products)
     vs fp32x3 (6 products, ~exact): the kept activations agree to fp32 noise

@@ -132,9 +132,10 @@ def test_scan_matches_cumsum(cuda):
 
 
 def test_coop_march_equals_serial_march(cuda):
-    """k_march_coop (batches of <= 32768 rays: 16 lanes per ray, ballot-ordered
-    hits) and k_march (larger batches: one lane per ray) give the same slots:
-    the first 3000 rays of a 160x240 frame queried alone vs inside the frame."""
+    """k_march_coop<16> (batches of <= 32768 rays: 16 lanes per ray) and
+    k_march_coop<8> (larger batches) give the same slots, those of a serial walk
+    along the ray (the oracle tests): the first 3000 rays of a 160x240 frame
+    queried alone vs inside the frame."""
     sc = scene(20000, H=160, W=240, theta=75.0)
     q = _engine(sc, cuda)
     xyz = torch.from_numpy(sc["xyz"]).to(cuda)

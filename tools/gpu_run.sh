@@ -39,7 +39,7 @@ for s in $STEPS; do
       cut -c1-400 $O/train.json $O/train_h2.json ;;
     trainprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trstats -o run -- \
-        python bench.py --mode train --steps 20 --warmup 3 > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
+        python bench.py --mode train --steps 20 --warmup 3 --train-precision ${TP:-fp32x3} > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
     nrab)   # the 2-D renderer tile-shape variants in tools/_var (built on the CPU side)
       for v in tools/_var/libpnr_*.so; do
         PNR_LIB=$PWD/$v timeout -k 10 200 python tools/nr_bench.py > $O/nrab_$(basename $v .so).json 2>> $O/nrab.err \
@@ -55,6 +55,12 @@ for s in $STEPS; do
           || { tail -20 $O/compab.err; exit 1; }
       done; done
       python -c "import json; [print(d['lib'][-20:], d['stages_ms'], d['checksum']) for d in map(json.loads, open('$O/compab.jsonl'))]" ;;
+    qab)   # query-stage variants (tools/_var/libpnr_q*.so), two rounds
+      for rnd in 1 2; do for v in tools/_var/libpnr_q*.so; do
+        PNR_LIB=$PWD/$v timeout -k 10 200 python tools/query_bench.py >> $O/qab.jsonl 2>> $O/qab.err \
+          || { tail -20 $O/qab.err; exit 1; }
+      done; done
+      python -c "import json; [print(d['lib'][-12:], [c['query_ms'] for c in d['cams']], [c['pidx_checksum'] for c in d['cams']]) for d in map(json.loads, open('$O/qab.jsonl'))]" ;;
     tnr)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_neural_render.py -m gpu -x -v --timeout 120 \
         --timeout-method thread > $O/t_nr.log 2>&1 || { tail -40 $O/t_nr.log; exit 1; }
