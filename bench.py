@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32x3",
                     help="--mode train: the training forward's per-pair chain (fp32h2 split-f16 MFMA, fp32x3 "
                          "split-bf16 MFMA or native fp32)")
+    ap.add_argument("--optimizer", choices=("hip", "torch"), default="hip",
+                    help="--mode train: Adam on pnr_adam_step (pointnerf_amd.optim.Adam) or torch's fused Adam")
     ap.add_argument("--mode", choices=("render", "train"), default="render",
                     help="render: the headline forward frame render; train: the per-scene finetune "
                          "step (SURVEY config c3: fwd + bwd + Adam on random ray batches)")
@@ -377,7 +379,11 @@ def run_train(args, device):
     bg = torch.from_numpy(np.random.default_rng(1).uniform(size=128).astype(np.float32)).to(device)
     target = torch.rand((H * W, 3), generator=torch.Generator().manual_seed(2)).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
-    optim = torch.optim.Adam(params, lr=5e-4, fused=True)
+    if args.optimizer == "hip":
+        from pointnerf_amd.optim import Adam
+        optim = Adam(params, lr=5e-4)
+    else:
+        optim = torch.optim.Adam(params, lr=5e-4, fused=True)
     gen = torch.Generator(device=device).manual_seed(rank)
     stats = {"pairs": 0, "valid": 0, "filled": 0}
 
@@ -429,6 +435,7 @@ def run_train(args, device):
         "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "train_forward": args.train_precision, "h2_fallbacks": int(model.h2_fallbacks),
+        "optimizer": "pnr_adam_step" if args.optimizer == "hip" else "torch.optim.Adam(fused=True)",
         "data": "synthetic (seeded lego-like point cloud, random target colours)",
         "config": {"workload": f"finetune step, {args.train_rays} random rays of {H}x{W} frames, {args.points} points",
                    "K": opt.K, "SR": opt.SR},

@@ -731,6 +731,19 @@ int pnr_vox_closest(const float* xyz_dev, int64_t n, int32_t vox_res, float* cen
                     int64_t* min_idx, int32_t* inv_idx, int32_t* counts, void* scratch, size_t scratch_bytes,
                     void* stream);
 
+/* ------------------------------------------------------------- optimizer */
+/* One Adam step (torch.optim.Adam, amsgrad = False: the optimizer of the
+ * reference's training loop, train_ddp.py / mvs_points_volumetric_model.py:102-123)
+ * over n_tensors contiguous fp32 tensors: params[i], grads[i], exp_avg[i],
+ * exp_avg_sq[i] of numel[i] elements each (device pointers; the tables
+ * themselves are host arrays).  `step` is the 1-based step count of all of them
+ * (bias corrections 1 - beta^step and 1 - beta in double on the host, as torch's
+ * python-float hyperparameters, then rounded to fp32).  Updates params, exp_avg,
+ * exp_avg_sq in place; no host sync. */
+int pnr_adam_step(int32_t n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2,
+                  double eps, double weight_decay, int64_t step, void* stream);
+
 /* ------------------------------------------------------------- utilities */
 /* Diagnostics: out_dev[0] = the shader clock (MHz) one wave measured over
  * `spins` s_sleep slices (s_memtime cycles / s_memrealtime 100 MHz ticks);

@@ -137,6 +137,8 @@ P = ctypes.POINTER
 SIGNATURES = {
     "pnr_abi_version": (c_int, []),
     "pnr_clock_probe": (c_int, [c_void_p, c_int32, c_void_p]),
+    "pnr_adam_step": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_double,
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_int64, c_void_p]),
     "pnr_last_error": (ctypes.c_char_p, []),
     "pnr_create": (c_int, [c_int, P(c_void_p)]),
     "pnr_destroy": (c_int, [c_void_p]),
