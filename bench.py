@@ -37,7 +37,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector p
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
 PMC_FILES = {"fp32": "r01_fp32_pmc_aggregate.json", "fp32x3": "r01_pmc_aggregate_x3.json",
-             "fp32h2": "r03_final_pmc_aggregate_h2.json"}
+             "fp32h2": "r03s3_final_pmc_aggregate_h2.json"}
 
 
 def parse():
