@@ -1,0 +1,30 @@
+"""Host logic of pointnerf_amd.optim.Adam (no GPU): hyperparameter checks as
+torch.optim.Adam's, parameters without gradients skipped without a launch,
+and anything but dense contiguous fp32 CUDA parameters refused loudly (no CPU
+fallback: the step is pnr_adam_step only)."""
+import pytest
+import torch
+
+from pointnerf_amd import _lib as L
+from pointnerf_amd.optim import Adam
+
+
+@pytest.mark.parametrize("kw", [dict(lr=-1.0), dict(eps=-1e-8), dict(betas=(1.0, 0.999)),
+                                dict(betas=(0.9, -0.1)), dict(weight_decay=-0.1)])
+def test_adam_rejects_bad_hyperparameters(kw):
+    with pytest.raises(ValueError):
+        Adam([torch.nn.Parameter(torch.zeros(3))], **kw)
+
+
+def test_adam_skips_params_without_grad():
+    p = torch.nn.Parameter(torch.ones(5))
+    opt = Adam([p], lr=1e-3)
+    opt.step()                      # no gradient: nothing to launch
+    assert torch.equal(p.detach(), torch.ones(5)) and not opt.state
+
+
+def test_adam_refuses_cpu_params():
+    p = torch.nn.Parameter(torch.ones(5))
+    p.grad = torch.ones(5)
+    with pytest.raises(L.PnrError):
+        Adam([p]).step()
