@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(64 * kGWaves, 1) k_gemm_tn_part(GemmArgs g) {
 constexpr int kXK = 16;                 // k rows per chunk (one bf16 MFMA k-step)
 constexpr int kXPitch = 24;             // bf16 per LDS line (16 k + 8 pad)
 constexpr int kXPlane = 256 * kXPitch;  // bf16 per plane (256 rows)
-constexpr size_t kXLds = 2 * 2 * 3 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 72 KB
+constexpr size_t kXLds = 2 * 2 * 3 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 144 KB
 
 __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t glds[];

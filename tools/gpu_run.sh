@@ -61,6 +61,12 @@ for s in $STEPS; do
           || { tail -20 $O/qab.err; exit 1; }
       done; done
       python -c "import json; [print(d['lib'][-12:], [c['query_ms'] for c in d['cams']], [c['pidx_checksum'] for c in d['cams']]) for d in map(json.loads, open('$O/qab.jsonl'))]" ;;
+    gab)   # weight-gradient GEMM variants (tools/_var/libpnr_g*.so, tools/_var/gemm_ab.py)
+      for v in tools/_var/libpnr_g*.so; do
+        PNR_LIB=$PWD/$v timeout -k 10 120 python tools/_var/gemm_ab.py >> $O/gab.jsonl 2>> $O/gab.err \
+          || { tail -20 $O/gab.err; exit 1; }
+      done
+      cat $O/gab.jsonl ;;
     tnr)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_neural_render.py -m gpu -x -v --timeout 120 \
         --timeout-method thread > $O/t_nr.log 2>&1 || { tail -40 $O/t_nr.log; exit 1; }
