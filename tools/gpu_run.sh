@@ -61,9 +61,9 @@ for s in $STEPS; do
           || { tail -20 $O/qab.err; exit 1; }
       done; done
       python -c "import json; [print(d['lib'][-12:], [c['query_ms'] for c in d['cams']], [c['pidx_checksum'] for c in d['cams']]) for d in map(json.loads, open('$O/qab.jsonl'))]" ;;
-    gab)   # weight-gradient GEMM variants (tools/_var/libpnr_g*.so, tools/_var/gemm_ab.py)
+    gab)   # weight-gradient GEMM variants (tools/_var/libpnr_g*.so) on tools/gemm_bench.py
       for v in tools/_var/libpnr_g*.so; do
-        PNR_LIB=$PWD/$v timeout -k 10 120 python tools/_var/gemm_ab.py >> $O/gab.jsonl 2>> $O/gab.err \
+        PNR_LIB=$PWD/$v timeout -k 10 120 python tools/gemm_bench.py >> $O/gab.jsonl 2>> $O/gab.err \
           || { tail -20 $O/gab.err; exit 1; }
       done
       cat $O/gab.jsonl ;;
