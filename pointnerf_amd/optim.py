@@ -17,6 +17,19 @@ import torch
 from . import _lib as L
 
 
+def _bump_versions(ps):
+    """The kernel writes the parameters through raw pointers, which autograd's
+    version counters do not see; callers that cache derived data per parameter
+    version (the aggregator's weight packs, keyed on p._version) must see the
+    update as torch's in-place ops would report it."""
+    setv = getattr(torch._C._autograd, "_unsafe_set_version_counter", None)
+    if setv is not None:
+        setv(tuple(ps), tuple(p._version + 1 for p in ps))
+    else:                       # older torch: a 1-element in-place no-op per parameter
+        for p in ps:
+            p.data.view(-1)[:1].add_(0)
+
+
 class Adam(torch.optim.Optimizer):
     """torch.optim.Adam(params, lr, betas, eps, weight_decay) on pnr_adam_step."""
 
@@ -59,4 +72,5 @@ class Adam(torch.optim.Optimizer):
                 L.check(L.lib().pnr_adam_step(n, *ptrs, numel, float(group["lr"]), float(b1), float(b2),
                                               float(group["eps"]), float(group["weight_decay"]), int(t),
                                               L.stream_ptr(dev)), "pnr_adam_step")
+                _bump_versions([i[0] for i in items])
         return loss

@@ -270,17 +270,17 @@ def _check_saves_match(ref, got):
     close(c3, c32, "ray_color", rel=1e-4, scale=1e-6)
 
 
-def test_train_step_reduces_loss(cuda):
-    """A few Adam steps on the point features + MLP lower a colour loss."""
+def _train_losses(cuda, make_opt, tp="fp32x3"):
     sc = scene(8000, H=24, W=24, theta=10.0, default_conf=None)
     m = _train_model(sc, cuda, formula_params(salt=0.7))
+    m.train_precision = tp
     campos = torch.from_numpy(sc["campos"]).to(cuda)
     camrot = torch.from_numpy(sc["camrot"]).to(cuda)
     rd = torch.from_numpy(sc["raydir"]).to(cuda)
     bg = torch.from_numpy(sc["bg"]).to(cuda)
     target = torch.rand((rd.shape[0], 3), generator=torch.Generator().manual_seed(3)).to(cuda)
     ps = [p for p in m.parameters() if p.requires_grad]
-    optim = torch.optim.Adam(ps, lr=1e-3)
+    optim = make_opt(ps)
     losses = []
     for _ in range(6):
         optim.zero_grad()
@@ -289,8 +289,29 @@ def test_train_step_reduces_loss(cuda):
         loss.backward()
         optim.step()
         losses.append(float(loss.detach()))
+    return losses, ps
+
+
+def test_train_step_reduces_loss(cuda):
+    """A few Adam steps on the point features + MLP lower a colour loss."""
+    losses, _ = _train_losses(cuda, lambda ps: torch.optim.Adam(ps, lr=1e-3))
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("tp", ["fp32x3", "fp32h2"])
+def test_train_loop_hip_adam_matches_torch_adam(cuda, tp):
+    """The finetune loop with pointnerf_amd.optim.Adam (pnr_adam_step) follows
+    the one with torch.optim.Adam: same losses step by step and the same
+    parameters after 6 steps, within fp32 rounding carried through the loop
+    (the two Adams differ by contraction order only, tests/test_gpu_optim.py)."""
+    from pointnerf_amd.optim import Adam
+    l_t, p_t = _train_losses(cuda, lambda ps: torch.optim.Adam(ps, lr=1e-3), tp)
+    l_h, p_h = _train_losses(cuda, lambda ps: Adam(ps, lr=1e-3), tp)
+    assert l_h[-1] < l_h[0]
+    np.testing.assert_allclose(l_h, l_t, rtol=1e-4, atol=1e-7)
+    for a, b in zip(p_h, p_t):
+        close(a, b, "param", rel=1e-4, scale=1e-4)
 
 
 @pytest.mark.parametrize("x3", [False, True])

@@ -33,6 +33,7 @@ def test_adam_matches_torch(cuda, wd, fused):
     mine = Adam(a, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd)
     ref = torch.optim.Adam(b, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd, fused=fused,
                            foreach=None if fused else False)
+    v0 = [p._version for p in a]
     for it in range(6):
         gs = _grads(a, 100 + it)
         for p, q, g in zip(a, b, gs):
@@ -41,6 +42,7 @@ def test_adam_matches_torch(cuda, wd, fused):
             a[2].grad = b[2].grad = None
         mine.step()
         ref.step()
+    assert all(p._version > v for p, v in zip(a, v0))   # caches keyed on the version see the update
     for i, (p, q) in enumerate(zip(a, b)):
         d = (p.detach() - q.detach()).abs()
         tol = 1e-6 * q.detach().abs() + 1e-9

@@ -28,3 +28,13 @@ def test_adam_refuses_cpu_params():
     p.grad = torch.ones(5)
     with pytest.raises(L.PnrError):
         Adam([p]).step()
+
+
+def test_version_bump_marks_parameters_changed():
+    """Raw-pointer updates must advance p._version (the aggregator's weight packs
+    are cached on it): the helper the step calls after each launch."""
+    from pointnerf_amd.optim import _bump_versions
+    ps = [torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(2, 2))]
+    v0 = [p._version for p in ps]
+    _bump_versions(ps)
+    assert [p._version for p in ps] == [v + 1 for v in v0]
