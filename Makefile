@@ -20,10 +20,6 @@ build/query.o build/grid.o build/voxelize.o: HIPFLAGS += -ffp-contract=off
 # issues at a fraction of the rate of scalar VALU beside the MFMA stream
 # (MI355X_MICROARCH "price of one filler"; measured 1 % on the aggregate).
 build/aggregate_x3.o: HIPFLAGS += -fno-slp-vectorize
-# k_pairs_as runs its gather / PE in the prologue and inside the loop: no FMA
-# contraction, so both copies round alike and a sample's bits never depend on
-# which tile of its workgroup it fell in (tests: renders are ray-independent).
-build/aggregate_as.o: HIPFLAGS += -fno-slp-vectorize -ffp-contract=off
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)

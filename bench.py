@@ -43,8 +43,8 @@ PMC_FILES = {"fp32": "r01_fp32_pmc_aggregate.json", "fp32x3": "r01_pmc_aggregate
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)   # the driver's own K / W (BENCH_rNN.json)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=tuple(CONFIGS), default="headline",
                     help="workload: headline = BASELINE's metric (lego flags, 2M points, 800x800); c4 = scene101 "
                          "flags, 10M points, 1296x968; c5 = truck flags, 20M points (overflowing max_o and P: "
@@ -72,8 +72,6 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check); "
                          "default 12000 (headline), 3000 (c4, c5)")
-    ap.add_argument("--pairs-kernel", choices=("wt", "as"), default="wt",
-                    help="fp32h2 pairs stage: k_pairs_h2 (wt) or the activation-stationary k_pairs_as (as)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32x3",
@@ -128,7 +126,6 @@ def build_scene(args, device):
     emb, color, dirs, conf = S.point_features(args.points, seed=0, default_conf=opt.default_conf)
     torch.manual_seed(0)
     agg = PointAggregator(opt).to(device).eval()   # random-init weights (xavier, networks.py:163-172)
-    agg.pairs_kernel = args.pairs_kernel
     # bf16 (config c5): the embedding table itself in bf16 (104 B per point)
     emb_dtype = torch.bfloat16 if getattr(args, "dtype", "fp32h2") == "bf16" else torch.float32
     np_ = NeuralPoints(opt, device, torch.from_numpy(pts), emb, color, dirs, conf, emb_dtype=emb_dtype)
@@ -575,6 +572,7 @@ def main():
                 stage["rays"] += nr
                 stage["flops"] += c["n_pairs"] * FLOP_PER_PAIR + c["S_valid"] * FLOP_PER_SAMPLE
             stage["_ev"] = stage.get("_ev", []) + ev_step
+            stage["_step_pairs"] = stage.get("_step_pairs", []) + [sum(c["n_pairs"] for c in counts)]
         frames = []
         for sh, color, _ in parts:
             if world > 1 and not args.no_gather:
@@ -675,7 +673,6 @@ def main():
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "max_o": int(opt.max_o), "grid_rebuild_per_step": bool(args.grid_rebuild),
                        "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
-                       "pairs_kernel": {"wt": "k_pairs_h2", "as": "k_pairs_as"}[args.pairs_kernel],
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else
                                        f"dp{world} ({args.tile_layout} ray shards of every frame, one multi-camera "
@@ -718,6 +715,20 @@ def main():
         clk = probe["out"][:probe["n"]].cpu().numpy()
         clk = clk[clk > 0]
         out["sclk_mhz_in_run"] = round(float(np.median(clk)), 1) if len(clk) else None
+        # per timed step: its frame's camera, valid pairs, aggregate span and probed
+        # clock -- the bench cycles 8 cameras whose views differ in pair count, so a
+        # K-step mean depends on which cameras the K steps cover
+        sp = stage.get("_step_pairs", [])
+        if shard_world == 1 and len(sp) == len(agg_ms):
+            out["per_step"] = {"camera": [(args.warmup + i) % len(cams) for i in range(len(sp))],
+                               "valid_pairs": [int(x) for x in sp],
+                               "aggregate_ms": [round(float(x), 3) for x in agg_ms],
+                               "sclk_mhz": [round(float(x), 1) for x in probe["out"][:probe["n"]].cpu().numpy()],
+                               "ns_per_kpair": [round(float(a) * 1e6 / max(int(p), 1) * 1e3, 4)
+                                                for a, p in zip(agg_ms, sp)]}
+            r = np.array(agg_ms)
+            out["per_step"]["aggregate_spread"] = {"min": round(float(r.min()), 3), "max": round(float(r.max()), 3),
+                                                   "cv": round(float(r.std() / r.mean()), 4)}
         # the voxel grid persists across frames (the points do not change); its
         # build (bbox read + 8 kernels + scans) on its own line
         out["grid_build"] = time_grid_build(model, opt)

@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 17
+#define PNR_ABI_VERSION 18
 
 enum {
   PNR_OK = 0,
@@ -242,6 +242,11 @@ typedef struct {
                            point instead of 168), read instead of emb by
                            pnr_aggregate_fwd_bf16 when set (emb may then be NULL);
                            the fp32 paths ignore it                                  */
+  const float* rw2c;    /* [N,3,3] per-point Rw2c (neural_points.py:799 gathers it when
+                           Rw2c.dim() > 2), or NULL = the uniform pnr_mlp.rw2c.  A pair's
+                           world distance and point dir are rotated by its point's
+                           matrix, a sample's view dir by the matrix of its slot-0
+                           neighbour (point_aggregators.py:492-496, 506, 526, 566)     */
 } pnr_points;
 
 typedef struct {
@@ -352,18 +357,6 @@ typedef struct {
   const void* w1ah;   /* block1.0 columns 0..223 + bias: the per-point half P1 on
                          f16-split MFMA (k_point_pre_h2; NULL: fp32 k_point_pre) */
   float scale1a;
-  /* activation-stationary pairs stage (k_pairs_as; NULL: k_pairs_h2 on w1bh..w4h).
-   * as_pack: 53 k-steps x 24 KB: for each step t, planes (2^11 Wh, Wl, k_L Wh) x 8
-   * neuron tiles x 64 lanes x 8 f16 of split2_f16(2^-s_L W_L[32T + (lane & 31),
-   * col(t, lane >> 5, j)]) for block1.0[:, 224:] (4 steps), block1.2 (16), block3.0
-   * + bias (17), block3.2 (16) -- the input columns in accumulator order
-   * (aggregator.as_columns), k_1 = 1, k_L = 2^(s_{L-1}); s_1..s_3 >= 0.
-   * as_tabs [3][2][128]: b2 / as_scale[1], b4 / as_scale[3], alpha_branch.0 weights,
-   * each for lane half h in accumulator order (row 32T + acc_row(r, h) at T*16 + r).
-   * as_scale: 2^(s_L - 11).  Needs w1ah (P1 is then written / as_scale[0]). */
-  const void* as_pack;
-  const float* as_tabs;
-  float as_scale[4];
 } pnr_mlp_h2;
 int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_h2* wh,
                          float* out_feat, float* out_weight, float* out_conf, void* scratch,
@@ -610,6 +603,38 @@ int pnr_composite_bwd(const pnr_rays* rays, const pnr_query_params* q,
 int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
                       const float* bg, int64_t NR, int32_t SR, int32_t C,
                       const float* d_ray_color, float* d_feat, void* stream);
+
+/* Full reverse mode of pnr_ray_march_fwd (ray_march is differentiable in every
+ * output, diff_ray_marching.py:509-555, called in training at
+ * neural_points_volumetric_model.py:314): d_feat[NR,SR,C+1] and, when
+ * d_ray_dist != NULL, d ray_dist[NR,SR], from d_ray_color[NR,C] and the optional
+ * (NULL = 0) d_opacity / d_acc_T / d_blend_w [NR,SR] and d_bg_T [NR].  The
+ * bg_color gradient is pnr_weighted_colsum(bg_T, d_ray_color). */
+int pnr_ray_march_bwd_ex(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
+                         const float* bg, int64_t NR, int32_t SR, int32_t C, const float* d_ray_color,
+                         const float* d_opacity, const float* d_acc_T, const float* d_blend_w,
+                         const float* d_bg_T, float* d_feat, float* d_ray_dist, void* stream);
+
+/* out[c] = sum_r w[r] x[r,c] (R rows, C <= 128 columns), bitwise repeatable: the
+ * learned background's gradient (mvs_points_volumetric_model.py:92-94 optimises
+ * bg_color).  For pnr_composite_fwd's rays w = is_bg (bg_T of a hit ray, 1 for a
+ * background ray filled by fill_invalid, neural_points_volumetric_model.py:373-375),
+ * x = d ray_color; for pnr_ray_march_fwd w = bg_T.  partials: device floats of
+ * pnr_weighted_colsum_scratch_floats(C). */
+int pnr_weighted_colsum_scratch_floats(int32_t C, int64_t* out);
+int pnr_weighted_colsum(const float* w, const float* x, int64_t R, int32_t C, float* out, float* partials,
+                        void* stream);
+
+/* The training outputs NeuralPointsRayMarching.forward adds to its dict
+ * (neural_points_volumetric_model.py:335-338) in pnr_query_compact's row order
+ * (the first rows_max of the R'' rays with a neighbour): weight[R'',SR,K] = the
+ * aggregator's normalised inverse-distance weight before the conf factor
+ * (point_aggregators.py:421-429, 803-804; 0 for empty slots), blend_weight[R'',SR]
+ * = opacity * acc_T of ray_march from pnr_composite_fwd's opacity[R,SR].  Either
+ * output may be NULL. */
+int pnr_march_aux(const pnr_rays* rays, const pnr_query_params* q, const pnr_query_bufs* b,
+                  const float* xyz, const float* opacity, int64_t rows_max, float* weight,
+                  float* blend_weight, void* stream);
 
 /* -------------------------------------------------------- 2-D neural renderer
  * NeuralRenderer(input_dim=128) (models/neural_render/neural_renderer.py:24-104,

@@ -301,9 +301,12 @@ def gather(points, sample_pidx, campos, camrot):
     def g(a, c):
         return None if a is None else np.asarray(a, F32).reshape(-1, c)[idx].reshape(shp + (c,))
 
+    rw = points.get("Rw2c")
+    if rw is not None and np.asarray(rw).ndim > 2:   # per-point Rw2c (neural_points.py:799)
+        rw = np.asarray(rw, F32).reshape(-1, 9)[idx].reshape(shp + (3, 3))
     return dict(sampled_color=g(points.get("color"), 3), sampled_dir=g(points.get("dir"), 3),
                 sampled_conf=g(points.get("conf"), 1), sampled_embedding=g(points["emb"], 32),
-                sampled_xyz_pers=g(pers, 3), sampled_xyz=g(xyz, 3), sample_pnt_mask=mask)
+                sampled_xyz_pers=g(pers, 3), sampled_xyz=g(xyz, 3), sample_pnt_mask=mask, sampled_Rw2c=rw)
 
 
 def _lin(x, params, name):
@@ -347,24 +350,32 @@ def aggregate(params, sampled_color, sampled_Rw2c, sampled_dir, sampled_conf, sa
     confc = np.clip(conf, F32(1e-4), F32(1)).astype(F32)
     wt = (w * confc).astype(F32)
     Rw = np.eye(3, dtype=F32) if sampled_Rw2c is None else np.asarray(sampled_Rw2c, F32)
-    RwT = Rw.T
+    per_pair = Rw.ndim > 2   # [R,SR,K,3,3] gathered per pair (point_aggregators.py:492-496)
+
+    def rot(x, Rm):          # x @ Rm^T per row (Rm [3,3] or one [3,3] per row)
+        if Rm.ndim == 2:
+            return (x @ Rm.T).astype(F32)
+        return np.einsum("ni,nji->nj", x, Rm).astype(F32)
+
     out = np.zeros((R, SR, C + 1), F32)
     if not ray_valid.any():
         return out, ray_valid, w, confc
     pm = mask.reshape(-1)
-    vd = np.asarray(sample_ray_dirs, F32).reshape(-1, 3) @ RwT
+    Rpair = Rw.reshape(-1, 3, 3)[pm] if per_pair else Rw
+    Rray = Rw[:, :, 0].reshape(-1, 3, 3) if per_pair else Rw   # slot 0's matrix rotates the view dir
+    vd = rot(np.asarray(sample_ray_dirs, F32).reshape(-1, 3), Rray)
     vpe = positional_encoding(vd, 4, ori=True)
     ori_v, vpe = vpe[:, :3], vpe[:, 3:]
     vpe = vpe[ray_valid.reshape(-1)]
     d = dists.reshape(-1, 6)[pm].copy()
-    d[:, :3] = d[:, :3] @ RwT
+    d[:, :3] = rot(d[:, :3], Rpair)
     d = positional_encoding(d, 5)
     e = np.asarray(sampled_embedding, F32).reshape(-1, 32)[pm]
     feat = np.concatenate([e, positional_encoding(e, 3), d], -1)
     feat = _lrelu(_lin(feat, params, "block1.0"), neg_slope)
     feat = _lrelu(_lin(feat, params, "block1.2"), neg_slope)
     col = np.asarray(sampled_color, F32).reshape(-1, 3)[pm]
-    sdir = np.asarray(sampled_dir, F32).reshape(-1, 3)[pm] @ RwT
+    sdir = rot(np.asarray(sampled_dir, F32).reshape(-1, 3)[pm], Rpair)
     ov = np.repeat(ori_v[:, None, :], K, 1).reshape(-1, 3)[pm]
     feat = np.concatenate([feat, col, sdir - ov, (sdir * ov).sum(-1, keepdims=True)], -1).astype(F32)
     feat = _lrelu(_lin(feat, params, "block3.0"), neg_slope)
@@ -432,7 +443,7 @@ def render(opt, points, params, campos, camrot, raydir, bg_color, mid_t=None, q=
                          near=opt.near_plane, far=opt.far_plane)
     g = gather(points, q["sample_pidx"], campos, camrot)
     neg = 0.01 if opt.act_type == "LeakyReLU" else 0.0
-    feats, rv, w, cc = aggregate(params, g["sampled_color"], points.get("Rw2c"), g["sampled_dir"],
+    feats, rv, w, cc = aggregate(params, g["sampled_color"], g["sampled_Rw2c"], g["sampled_dir"],
                                  g["sampled_conf"], g["sampled_embedding"], g["sampled_xyz_pers"],
                                  g["sampled_xyz"], g["sample_pnt_mask"], q["sample_loc"],
                                  q["sample_loc_w"], q["sample_ray_dirs"], neg_slope=neg,

@@ -52,23 +52,31 @@ def aggregate(params: dict, sampled_color, sampled_dir, sampled_conf, sampled_em
     confc = gradiant_clamp(sampled_conf[..., 0]) if sampled_conf is not None else torch.ones_like(w)
     wt = w * confc
     Rw = torch.eye(3, dtype=F) if rw2c is None else rw2c
-    RwT = Rw.t()
+    per_pair = Rw.dim() > 2   # [R,SR,K,3,3] gathered per pair (point_aggregators.py:492-496)
+
+    def rot(x, Rm):           # x @ Rm^T per row
+        if Rm.dim() == 2:
+            return x @ Rm.t()
+        return (x[:, None, :] @ Rm.transpose(-1, -2)).squeeze(-2)
+
     act = lambda x: torch.nn.functional.leaky_relu(x, neg_slope)  # noqa: E731
     lin = lambda x, n: x @ params[n + ".weight"].t() + params[n + ".bias"]  # noqa: E731
     pm = mask.reshape(-1)
-    vd = sample_ray_dirs.reshape(-1, 3) @ RwT
+    Rpair = Rw.reshape(-1, 3, 3)[pm] if per_pair else Rw
+    Rray = Rw[:, :, 0].reshape(-1, 3, 3) if per_pair else Rw   # slot 0's matrix rotates the view dir
+    vd = rot(sample_ray_dirs.reshape(-1, 3), Rray)
     vpe = positional_encoding(vd, 4, ori=True)
     ori_v, vpe = vpe[:, :3], vpe[:, 3:]
     vpe = vpe[ray_valid.reshape(-1)]
     d = dists.reshape(-1, 6)[pm]
-    d = torch.cat([d[:, :3] @ RwT, d[:, 3:]], -1)
+    d = torch.cat([rot(d[:, :3], Rpair), d[:, 3:]], -1)
     d = positional_encoding(d, 5)
     e = sampled_embedding.reshape(-1, 32)[pm]
     x = torch.cat([e, positional_encoding(e, 3), d], -1)
     x = act(lin(x, "block1.0"))
     x = act(lin(x, "block1.2"))
     col = sampled_color.reshape(-1, 3)[pm]
-    sdir = sampled_dir.reshape(-1, 3)[pm] @ RwT
+    sdir = rot(sampled_dir.reshape(-1, 3)[pm], Rpair)
     ov = ori_v[:, None, :].expand(-1, K, -1).reshape(-1, 3)[pm]
     x = torch.cat([x, col, sdir - ov, (sdir * ov).sum(-1, keepdim=True)], -1)
     x = act(lin(x, "block3.0"))
@@ -104,3 +112,19 @@ def ray_march(ray_dist, ray_valid, ray_features, bg_color=None):
     if bg_color is not None:
         color = color + bg_color[None, :] * acc[..., -1:]
     return color
+
+
+def ray_march_full(ray_dist, ray_valid, ray_features, bg_color=None):
+    """Every differentiable output of diff_ray_marching.py:509-555:
+    (ray_color [NR,C], opacity, acc_transmission (exclusive), blend_weight
+    [NR,SR], background_transmission [NR,1])."""
+    sigma = ray_features[..., 0] * ray_valid.to(ray_features.dtype)
+    opacity = 1 - torch.exp(-sigma * ray_dist)
+    acc = torch.cumprod(1.0 - opacity + 1e-10, dim=-1)
+    bgT = acc[..., -1:]
+    T = torch.cat([torch.ones_like(acc[..., :1]), acc[..., :-1]], -1)
+    bw = opacity * T
+    color = (bw[..., None] * ray_features[..., 1:]).sum(-2)
+    if bg_color is not None:
+        color = color + bg_color[None, :] * bgT
+    return color, opacity, T, bw, bgT

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 17
+ABI_VERSION = 18
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -93,7 +93,7 @@ class Points(ctypes.Structure):
     _fields_ = [("n", c_int64), ("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
                 ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p),
                 ("used", c_void_p), ("n_used", c_int64), ("used_map", c_void_p),
-                ("p1_ready", c_int32), ("emb_bf16", c_void_p)]
+                ("p1_ready", c_int32), ("emb_bf16", c_void_p), ("rw2c", c_void_p)]
 
 
 class Samples(ctypes.Structure):
@@ -120,8 +120,7 @@ class MlpH2(ctypes.Structure):
     _fields_ = ([(n, c_void_p) for n in ("w1bh", "w2h", "w3h", "w4h")] + [("scale", c_float * 4),
                                                                         ("range_flag", c_void_p)] +
                 [(n, c_void_p) for n in ("wc1a", "wc1b", "wc2h", "wc3h")] + [("cscale", c_float * 3)] +
-                [("w1ah", c_void_p), ("scale1a", c_float)] +
-                [("as_pack", c_void_p), ("as_tabs", c_void_p), ("as_scale", c_float * 4)])
+                [("w1ah", c_void_p), ("scale1a", c_float)])
 
 
 class MlpBwd(ctypes.Structure):
@@ -204,6 +203,13 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p]),
     "pnr_ray_march_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                   c_void_p, c_void_p, c_void_p]),
+    "pnr_ray_march_bwd_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+    "pnr_weighted_colsum_scratch_floats": (c_int, [c_int32, P(c_int64)]),
+    "pnr_weighted_colsum": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
+    "pnr_march_aux": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), c_void_p, c_void_p, c_int64, c_void_p,
+                              c_void_p, c_void_p]),
     "pnr_composite_fwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams),
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_ray_march_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
@@ -325,3 +331,18 @@ def aggregate_scratch_bf16(n_max: int, n_points: int, device) -> torch.Tensor:
 
 def stream_ptr(device=None):
     return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def weighted_colsum(w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """out[c] = sum_r w[r] x[r, c] on pnr_weighted_colsum (deterministic): the
+    background colour's gradient from d ray_color and is_bg / bg_T."""
+    w = w.reshape(-1).float().contiguous()
+    x = x.reshape(w.numel(), -1).float().contiguous()
+    C = x.shape[1]
+    n = ctypes.c_int64(0)
+    check(lib().pnr_weighted_colsum_scratch_floats(C, ctypes.byref(n)), "pnr_weighted_colsum_scratch_floats")
+    part = torch.empty(int(n.value), dtype=torch.float32, device=x.device)
+    out = torch.empty(C, dtype=torch.float32, device=x.device)
+    check(lib().pnr_weighted_colsum(ptr(w), ptr(x), w.numel(), C, ptr(out), ptr(part), stream_ptr(x.device)),
+          "pnr_weighted_colsum")
+    return out

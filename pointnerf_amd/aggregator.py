@@ -260,67 +260,6 @@ def frag_pack_h2(W: torch.Tensor, bias: torch.Tensor | None = None,
     return F.view(-1), 2.0 ** (s - 11)
 
 
-def _acc_row(r: int, h: int) -> int:
-    """Row of accumulator register r in lane half h (32x32 MFMA C layout, agg_common.h acc_row)."""
-    return (r & 3) + 8 * (r >> 2) + 4 * h
-
-
-def as_columns(layer: int) -> list[list[list[int]]]:
-    """k_pairs_as input columns: cols[t][h][j] = the input column whose value lane
-    half h holds as k-row j of k-step t (-1 = zero row).  Layers 2-4 take the
-    previous layer's accumulator as it stands: step t = neuron tile t // 2, registers
-    8 (t % 2) .. + 7 of the lane; layer 3 adds a step of the 8 extras (columns
-    256..263, 263 = the bias column) in lane half 0; layer 1 (block1.0's PE5
-    columns 224..283) gives lane half h the 30 values of distance channels 3h ..
-    3h + 2 (column 224 + 30 h + v)."""
-    if layer == 1:
-        return [[[224 + 30 * h + 8 * t + j if 8 * t + j < 30 else -1 for j in range(8)] for h in range(2)]
-                for t in range(4)]
-    steps = [[[32 * (t >> 1) + _acc_row(8 * (t & 1) + j, h) for j in range(8)] for h in range(2)] for t in range(16)]
-    if layer == 3:
-        steps.append([[256 + j for j in range(8)], [-1] * 8])
-    return steps
-
-
-def frag_pack_as(Wfull: torch.Tensor, layer: int, s: int, k: float) -> torch.Tensor:
-    """k_pairs_as A-operand pack of one layer: [t][plane][T][lane][j] f16 with
-    planes (2^11 Wh, Wl, k Wh) of split2_f16(2^-s W[32T + (lane & 31), col(t, lane >> 5, j)])."""
-    cols = torch.tensor(as_columns(layer), dtype=torch.long, device=Wfull.device)   # [t][2][8]
-    Wz = torch.cat([Wfull.float(), torch.zeros((Wfull.shape[0], 1), device=Wfull.device)], 1)
-    sel = Wz[:, torch.where(cols >= 0, cols, Wz.shape[1] - 1)]                      # [256][t][2][8]
-    wp = sel * 2.0 ** -s
-    wh, wl = split2_f16(wp)
-    ws = (wh.float() * 2048.0).to(torch.float16)
-    wk = (wh.float() * k).to(torch.float16)
-    if not (torch.isfinite(ws.float()).all() and torch.isfinite(wk.float()).all()):
-        raise L.PnrError("frag_pack_as: a weight plane left the f16 range")
-    planes = torch.stack([ws, wl, wk], 0)                                             # [3][256][t][2][8]
-    nt = cols.shape[0]
-    return planes.view(3, 8, 32, nt, 2, 8).permute(3, 0, 1, 4, 2, 5).contiguous().view(-1)   # [t][pl][T][h][r][j]
-
-
-def pack_as(b1, b3, alpha_w):
-    """The four k_pairs_as layer packs (53 k-steps), the accumulator-order tables
-    (b2 / sc2, b4 / sc4, alpha weights) and the layer scales sc_L = 2^(s_L - 11),
-    s_L >= 0 for layers 1-3 so the f16 split of their outputs needs no rescale."""
-    W1 = b1[0].weight.detach()
-    W2, bb2 = b1[2].weight.detach(), b1[2].bias.detach()
-    W3 = torch.cat([b3[0].weight.detach(), b3[0].bias.detach()[:, None]], 1)
-    W4, bb4 = b3[2].weight.detach(), b3[2].bias.detach()
-    s1 = max(0, h2_shift(W1[:, 224:]))
-    s2 = max(0, h2_shift(W2))
-    s3 = max(0, h2_shift(W3))
-    s4 = h2_shift(W4)
-    packs = [frag_pack_as(W1, 1, s1, 1.0), frag_pack_as(W2, 2, s2, 2.0 ** s1),
-             frag_pack_as(W3, 3, s3, 2.0 ** s2), frag_pack_as(W4, 4, s4, 2.0 ** s3)]
-    sc = [2.0 ** (x - 11) for x in (s1, s2, s3, s4)]
-    rows = torch.tensor([[32 * T + _acc_row(r, h) for T in range(8) for r in range(16)] for h in range(2)],
-                        dtype=torch.long, device=W2.device)                           # [2][128]
-    tabs = torch.stack([bb2.float()[rows] / sc[1], bb4.float()[rows] / sc[3],
-                        alpha_w.detach().float().reshape(-1)[rows]]).contiguous()     # [3][2][128]
-    return torch.cat(packs).contiguous(), tabs.view(-1), sc
-
-
 def frag_unpack(F: torch.Tensor, kin: int, out_f: int = 256) -> torch.Tensor:
     NT = out_f // 32
     tot = F.numel() // (NT * 64)
@@ -355,9 +294,6 @@ class PointAggregator(nn.Module):
             _init_seq(s)
         self._packed = None
         self._packed_key = None
-        # fp32h2 pairs stage: "wt" = k_pairs_h2 (weight-stationary tiles), "as" =
-        # k_pairs_as (activation-stationary, weights streamed through LDS)
-        self.pairs_kernel = "wt"
         self.register_buffer("rw2c", torch.eye(3), persistent=False)
 
     # ---------------------------------------------------------------- weights
@@ -436,9 +372,6 @@ class PointAggregator(nn.Module):
         """Split-f16 packs of block1.0[:, 224:], block1.2, block3.0, block3.2
         for pnr_aggregate_fwd_h2 (used with packed(); cached like it).  The
         dict holds the device range flag (`range_flag`, int32[1])."""
-        if self.pairs_kernel not in ("wt", "as"):
-            raise L.PnrError(f"pairs_kernel {self.pairs_kernel!r}: 'wt' or 'as'")
-        use_as = self.pairs_kernel == "as"
         key = self.h2_key()
         if getattr(self, "_packedh2", None) is not None and key == self._packedh2_key:
             return self._packedh2
@@ -455,21 +388,14 @@ class PointAggregator(nn.Module):
                       frag_pack_h2(cb[2].weight, cb[2].bias), frag_pack_h2(cb[4].weight, cb[4].bias)]
             # block1.0's per-point half (k_point_pre_h2)
             p1pack = frag_pack_h2(b1[0].weight[:, :224], b1[0].bias)
-            # the activation-stationary pairs stage (k_pairs_as), when selected
-            if use_as:
-                aspack, astabs, assc = pack_as(b1, b3, self.alpha_branch[0].weight)
         flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
         t = dict(w1bh=packs[0][0], w2h=packs[1][0], w3h=packs[2][0], w4h=packs[3][0], range_flag=flag,
                  wc1a=cpacks[0][0], wc1b=cpacks[1][0], wc2h=cpacks[2][0], wc3h=cpacks[3][0], w1ah=p1pack[0])
-        if use_as:
-            t.update(as_pack=aspack, as_tabs=astabs)
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
                     (L.c_float * 4)(*(p[1] for p in packs)), flag.data_ptr(),
                     *(t[k].data_ptr() for k in ("wc1a", "wc1b", "wc2h", "wc3h")),
                     (L.c_float * 3)(cpacks[1][1], cpacks[2][1], cpacks[3][1]),
-                    t["w1ah"].data_ptr(), p1pack[1],
-                    aspack.data_ptr() if use_as else None, astabs.data_ptr() if use_as else None,
-                    (L.c_float * 4)(*(assc if use_as else (0.0,) * 4)))
+                    t["w1ah"].data_ptr(), p1pack[1])
         self._packedh2, self._packedh2_key = (m, t), key
         return self._packedh2
 
@@ -498,8 +424,7 @@ class PointAggregator(nn.Module):
         sc = [2.0 ** (s - 11) for s in self._h2t_shifts]
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
                     (L.c_float * 4)(*sc[:4]), flag.data_ptr(),
-                    None, None, None, None, (L.c_float * 3)(0.0, 0.0, 0.0), t["w1ah"].data_ptr(), sc[4], None, None,
-                    (L.c_float * 4)(0.0, 0.0, 0.0, 0.0))
+                    None, None, None, None, (L.c_float * 3)(0.0, 0.0, 0.0), t["w1ah"].data_ptr(), sc[4])
         self._packedh2t, self._packedh2t_key = (m, t), key
         return self._packedh2t
 
@@ -536,8 +461,8 @@ class PointAggregator(nn.Module):
 
     def h2_key(self):
         """Identity of the current weights (storage + version of every
-        parameter) and the pairs kernel, the key packed_h2() caches on."""
-        return tuple((p.data_ptr(), p._version) for p in self.parameters()) + (self.pairs_kernel,)
+        parameter), the key packed_h2() caches on."""
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def h2_reset_range(self):
         """Clear the h2 range flag (after the caller has acted on it)."""
@@ -585,11 +510,15 @@ class PointAggregator(nn.Module):
         """point_aggregators.py:729-816 -> (features [B,R,SR,C+1], ray_valid
         [B,R,SR], weight, conf_coefficient)."""
         L.require_gpu(sample_loc_w)
-        if sampled_Rw2c is not None and sampled_Rw2c.dim() != 2:
-            raise L.PnrError("per-point Rw2c is not implemented by libpnr (uniform Rw2c only)")
-        if sampled_Rw2c is not None:
-            self.set_rw2c(sampled_Rw2c.to(self.rw2c.device))
         B, R, SR, K = sample_pnt_mask.shape
+        # uniform [3,3] or gathered per pair [B,R,SR,K,3,3] (neural_points.py:799): the
+        # per-pair table is pnr_points.rw2c of the pair-table launch
+        rw_pairs = None
+        if sampled_Rw2c is not None and sampled_Rw2c.dim() != 2:
+            rw_pairs = sampled_Rw2c.detach().reshape(B * R * SR * K, 9).float().contiguous()
+            self.set_rw2c(None)
+        elif sampled_Rw2c is not None:
+            self.set_rw2c(sampled_Rw2c.to(self.rw2c.device))
         rows = B * R * SR
         dev = sample_loc_w.device
         C = 128   # the decoded features; the upstream head (C_out = 3) is applied at the end
@@ -613,8 +542,8 @@ class PointAggregator(nn.Module):
                                         any(p.requires_grad for p in self.parameters())):
             # training path: autograd through pnr_aggregate_fwd_train / _bwd_pairs (train.py)
             from .train import AggSpec, AggregateFn, agg_params
-            spec = AggSpec(self, s, rows, dict(xyz=keep["xyz"], pers=keep["pers"]), pair_mask=keep["mask"],
-                           keep=(keep,))
+            spec = AggSpec(self, s, rows, dict(xyz=keep["xyz"], pers=keep["pers"], rw2c=rw_pairs),
+                           pair_mask=keep["mask"], keep=(keep, rw_pairs))
             out = AggregateFn.apply(spec, sampled_embedding.reshape(-1, 32).float(),
                                     None if sampled_color is None else sampled_color.reshape(-1, 3).float(),
                                     None if sampled_dir is None else sampled_dir.reshape(-1, 3).float(),
@@ -627,6 +556,7 @@ class PointAggregator(nn.Module):
                         conf=flat(sampled_conf, 1))
             pts = L.Points(rows * K, keep["xyz"].data_ptr(), keep["pers"].data_ptr(), keep["emb"].data_ptr(),
                            L.ptr(keep["color"]), L.ptr(keep["dir"]), L.ptr(keep["conf"]), None, None)
+            pts.rw2c = L.ptr(rw_pairs)
             mlp, _ = self.packed()
             scratch = L.aggregate_scratch(rows, rows * K, dev)
             L.check(L.lib().pnr_aggregate_fwd_masked(L.ctypes.byref(pts), L.ctypes.byref(s),

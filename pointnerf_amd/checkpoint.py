@@ -45,9 +45,7 @@ def load_ray_marching(path: str, opt, device, epoch_is_best: bool = False) -> Ne
     dc = float(getattr(opt, "default_conf", -1.0))
     if conf is None and epoch_is_best and 0.0 < dc <= 1.0:
         conf = torch.full((1, n, 1), dc)
-    rw = np_sd.get("Rw2c")
-    if rw is not None and rw.dim() != 2:
-        raise L.PnrError("per-point Rw2c is not implemented by libpnr (uniform Rw2c only)")
+    rw = np_sd.get("Rw2c")   # [3,3] uniform or [N,3,3] per point (neural_points.py:289, 799)
     points = NeuralPoints(opt, device, xyz, np_sd["points_embeding"], np_sd.get("points_color"),
                           np_sd.get("points_dir"), conf, Rw2c=rw)
     agg = PointAggregator(opt).to(device)
@@ -55,7 +53,7 @@ def load_ray_marching(path: str, opt, device, epoch_is_best: bool = False) -> Ne
     missing, unexpected = agg.load_state_dict(agg_sd, strict=False)
     model = NeuralPointsRayMarching(opt, points, agg)
     model.load_report = dict(missing=list(missing), unexpected=list(unexpected))
-    if rw is not None:
+    if rw is not None and rw.dim() == 2:
         agg.set_rw2c(rw)
     return model
 
@@ -64,7 +62,7 @@ def save_ray_marching(model: NeuralPointsRayMarching, path: str):
     """save_networks (base_model.py:99-116): the module's state_dict, CPU tensors."""
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     np_ = model.neural_points
-    if np_.Rw2c is not None and not torch.equal(np_.Rw2c.cpu(), torch.eye(3)):
+    if np_.Rw2c is not None and (np_.Rw2c.dim() != 2 or not torch.equal(np_.Rw2c.cpu(), torch.eye(3))):
         sd["neural_points.Rw2c"] = np_.Rw2c.detach().cpu()
     torch.save(sd, path)
 
@@ -76,28 +74,34 @@ def _param(t, grad_flag):
 
 
 def prune(points: NeuralPoints, thresh: float):
-    """neural_points.py:350-373: keep points with conf >= thresh."""
+    """neural_points.py:350-373: keep points with conf >= thresh (a per-point
+    Rw2c is kept for the surviving points, :370-372; xyz stays trainable with
+    --xyz_grad 1, :353)."""
     if points.points_conf is None:
         raise L.PnrError("prune needs points_conf")
     o = points.opt
     mask = points.points_conf.detach()[0, :, 0] >= thresh
     with torch.no_grad():
-        points.xyz = _param(points.xyz[mask, :], False)
+        points.xyz = _param(points.xyz[mask, :], getattr(o, "xyz_grad", 0) > 0)
         points.points_embeding = _param(points.points_embeding[:, mask, :], getattr(o, "feat_grad", 1) > 0)
         points.points_conf = _param(points.points_conf[:, mask, :], getattr(o, "conf_grad", 1) > 0)
         if points.points_dir is not None:
             points.points_dir = _param(points.points_dir[:, mask, :], getattr(o, "dir_grad", 1) > 0)
         if points.points_color is not None:
             points.points_color = _param(points.points_color[:, mask, :], getattr(o, "color_grad", 1) > 0)
+        if points.Rw2c is not None and points.Rw2c.dim() > 2:
+            points.Rw2c = points.Rw2c[mask].contiguous()
     return int((~mask).sum())
 
 
-def grow_points(points: NeuralPoints, add_xyz, add_embedding, add_color=None, add_dir=None, add_conf=None):
-    """neural_points.py:376-401: append points (add_* are [M, C])."""
+def grow_points(points: NeuralPoints, add_xyz, add_embedding, add_color=None, add_dir=None, add_conf=None,
+                add_Rw2c=None):
+    """neural_points.py:376-401: append points (add_* are [M, C]; add_Rw2c
+    [M,3,3] when the cloud carries a per-point Rw2c, :400-402)."""
     o = points.opt
     dev = points.xyz.device
     with torch.no_grad():
-        points.xyz = _param(torch.cat([points.xyz, add_xyz.to(dev).float()], 0), False)
+        points.xyz = _param(torch.cat([points.xyz, add_xyz.to(dev).float()], 0), getattr(o, "xyz_grad", 0) > 0)
         # keep the table's dtype (a bf16 table stays bf16: torch.cat would promote it)
         emb_t = points.points_embeding.dtype
         points.points_embeding = _param(torch.cat([points.points_embeding, add_embedding.to(dev).to(emb_t)[None]], 1),
@@ -111,3 +115,7 @@ def grow_points(points: NeuralPoints, add_xyz, add_embedding, add_color=None, ad
         if points.points_color is not None:
             points.points_color = _param(torch.cat([points.points_color, add_color.to(dev).float()[None]], 1),
                                          getattr(o, "color_grad", 1) > 0)
+        if points.Rw2c is not None and points.Rw2c.dim() > 2:
+            if add_Rw2c is None:
+                raise L.PnrError("grow_points: the cloud has a per-point Rw2c, add_Rw2c [M,3,3] is required")
+            points.Rw2c = torch.cat([points.Rw2c, add_Rw2c.to(dev).float().reshape(-1, 3, 3)], 0).contiguous()

@@ -36,6 +36,30 @@ __device__ __forceinline__ void mat3(const float* R, const float v[3], float o[3
   for (int j = 0; j < 3; ++j) o[j] = v[0] * R[j * 3 + 0] + v[1] * R[j * 3 + 1] + v[2] * R[j * 3 + 2];
 }
 
+// Per-point Rw2c (pnr_points.rw2c, [N][9]; neural_points.py:799 gathers it per
+// pair when Rw2c.dim() > 2): o = R_p v for the point of row prow.  A pair's world
+// distance and point dir use its own point's matrix, a sample's view dir the
+// matrix of its slot-0 neighbour (point_aggregators.py:492-496, 506, 526, 566).
+// The kernels compute the uniform-Rw2c values first and overwrite them with
+// these under a wave-uniform `pts.rw2c != NULL` test, so the uniform path's
+// code is unchanged.
+__device__ __forceinline__ void rot_point(const float* rw_pp, int64_t prow, const float v[3], float o[3]) {
+  const float* R = rw_pp + (prow > 0 ? prow : 0) * 9;
+  float m[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m[i] = R[i];
+  mat3(m, v, o);
+}
+
+// Point row whose Rw2c rotates the view dir of sample `row`: its slot-0
+// neighbour (sampled_Rw2c[..., 0, :, :], clamp(pidx, 0)), or in pair-table mode
+// (pnr_samples.pidx NULL) the sample's first pair row.
+__device__ __forceinline__ int64_t slot0_point(const pnr_samples& s, int64_t row) {
+  if (!s.pidx) return row * s.K;
+  const int32_t p = s.pidx[row * s.K];
+  return p > 0 ? p : 0;
+}
+
 __device__ __forceinline__ int64_t sample_row(const pnr_samples& s, int64_t v) {
   return s.samp_list ? (int64_t)s.samp_list[v] : v;
 }
@@ -156,26 +180,10 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
 // f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
                         hipStream_t st);
-// k_pairs_as (aggregate_as.hip): the activation-stationary fp32h2 pairs stage.
-// pack: 53 k-steps x 24 KB (planes 2^11 Wh, Wl, k Wh of block1.0[:, 224:],
-// block1.2, block3.0 + bias, block3.2, input columns permuted to the
-// accumulator layout); tabs [3][2][128]: b2 / sc2, b4 / sc4, alpha weights in
-// accumulator order; scale: sc1..sc4 (sc = 2^(s - 11), s >= 0 for layers 1-3);
-// p1 = block1.0's point half / sc1.
-struct AsPack {
-  const void* pack;
-  const float* tabs;
-  float scale[4];
-  int32_t* range_flag;
-};
-// k_pair_rec -> k_pairs_as; rec = 4 planes of as_rec_stride(n_max) 16-B pair records
-inline int64_t as_rec_stride(int64_t n_max) { return ((n_max > 0 ? n_max : 1) + 15) / 16 * 16 * 8; }
-int launch_pairs_as(const pnr_points& pts, const pnr_samples& s, const pnr_mlp& w, const AsPack& ap, const float* p1,
-                    float* hid, int32_t* vmask, float* out_feat, float* out_weight, float* out_conf,
-                    int32_t* blk_ctr, uint4* rec, hipStream_t st);
 // k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
 // color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
-                    int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st);
+                    int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st,
+                    const float* rw2c_pp);
 
 }  // namespace pnr

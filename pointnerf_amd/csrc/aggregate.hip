@@ -518,6 +518,11 @@ __global__ void __launch_bounds__(64 * kPairWaves * kPairSub, 2 / kPairSub) k_pa
     float vrot[3], drot[3];
     mat3(Rw, vd, vrot);
     mat3(Rw, pdir, drot);
+    if (A.pts.rw2c) {   // per-point Rw2c (agg_common.h rot_point)
+      rot_point(A.pts.rw2c, prow, d6, dr6);
+      rot_point(A.pts.rw2c, prow, pdir, drot);
+      rot_point(A.pts.rw2c, active ? slot0_point(A.s, row) : 0, vd, vrot);
+    }
     if (wid == 0) {
       // block3 inputs 256..263: colour(3), R.dir - R.v (3), <R.dir, R.v> (1), bias 1
       const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
@@ -735,6 +740,7 @@ __global__ void __launch_bounds__(64 * kColWaves, 2) k_color(AggArgs A) {
           const int64_t drow = dir_row(A.s, row);
           const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
           mat3(Rw, vd, vrot);
+          if (A.pts.rw2c) rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
         }
         const float x = wid == 0 ? vrot[0] : (wid == 1 ? vrot[1] : vrot[2]);
 #pragma unroll
@@ -1177,6 +1183,11 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
           for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
           float vrot[3];
           mat3(Rw, vd, vrot);
+          if (A.pts.rw2c) {   // per-point: view dir by the slot-0 matrix, d dir through the pair's
+            rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Rw[i] = A.pts.rw2c[(int64_t)pr * 9 + i];
+          }
           const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
           // drot_j = sum_i Rw[j][i] dir_i  ->  d dir_i = sum_j Rw[j][i] d drot_j
 #pragma unroll
@@ -1266,10 +1277,16 @@ __global__ void __launch_bounds__(256) k_extras_bwd(BwdArgs A) {
       float Rw[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
-      const int64_t drow = dir_row(A.s, sample_row(A.s, pair / kKN));
+      const int64_t row = sample_row(A.s, pair / kKN);
+      const int64_t drow = dir_row(A.s, row);
       const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
       float vrot[3];
       mat3(Rw, vd, vrot);
+      if (A.pts.rw2c) {   // per-point: view dir by the slot-0 matrix, d dir through the pair's
+        rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Rw[i] = A.pts.rw2c[(int64_t)pr * 9 + i];
+      }
       const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -1367,10 +1384,8 @@ static int64_t hid_rows(int64_t n_max) { return cdiv(n_max > 0 ? n_max : 1, 64) 
 static size_t scratch_need(int64_t n_max, int64_t n_points) {
   const int64_t nm = hid_rows(n_max);
   // + 8 ints: the split kernels' tile counters (k_pairs_x3 / k_pairs_h2, one per XCD group), padded to 16 B
-  // + k_pairs_as's pair records (kRecPlanes x as_rec_stride 16-B entries)
   return ((size_t)nm * kHid + (size_t)cdiv(nm, 4) * 4 + 16 + (size_t)(n_points > 0 ? n_points : 1) * kHid) *
-             sizeof(float) +
-         (size_t)4 * as_rec_stride(n_max) * 16;
+         sizeof(float);
 }
 
 // scratch = P1 [n_p1, 256] | hid [n_max, 256] | vmask | tile counter: P1 first,
@@ -1385,9 +1400,6 @@ static void carve(AggArgs& a, void* scratch, int64_t n_max, int64_t n_p1) {
 static int32_t* tile_counter(const AggArgs& a, int64_t n_max) {
   const int64_t nm = hid_rows(n_max);
   return a.vmask + cdiv(nm, 4) * 4;
-}
-static uint4* pair_records(const AggArgs& a, int64_t n_max) {
-  return reinterpret_cast<uint4*>(tile_counter(a, n_max) + 16);
 }
 
 int check_common(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, float* out_feat,
@@ -1508,23 +1520,6 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
   SplitW sw = {{wh->w1bh, wh->w2h, wh->w3h, wh->w4h},
                {wh->scale[0], wh->scale[1], wh->scale[2], wh->scale[3]},
                wh->range_flag};
-  if (wh->as_pack) {
-    // k_point_pre_h2 (P1 / sc1) -> k_pairs_as (aggregate_as.hip) -> k_color_h2
-    PNR_CHECK_ARG(wh->w1ah && wh->as_tabs && wh->wc1a, "aggregate_h2: k_pairs_as needs w1ah, as_tabs, colour packs");
-    PNR_CHECK_ARG((((uintptr_t)wh->as_pack | (uintptr_t)wh->as_tabs) & 15) == 0, "aggregate_h2: as packs must be 16-B aligned");
-    for (int i = 0; i < 4; ++i)
-      PNR_CHECK_ARG(wh->as_scale[i] > 0.f && wh->as_scale[i] < 1e30f, "aggregate_h2: bad as_scale %d", i);
-    if (!a.pts.p1_ready &&
-        (rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a / wh->as_scale[0], wh->range_flag, a.p1, st)))
-      return rc;
-    AsPack ap = {wh->as_pack, wh->as_tabs, {wh->as_scale[0], wh->as_scale[1], wh->as_scale[2], wh->as_scale[3]},
-                 wh->range_flag};
-    if ((rc = launch_pairs_as(a.pts, a.s, a.w, ap, a.p1, a.hid, a.vmask, out_feat, out_weight, out_conf,
-                              tile_counter(a, s->n_max), pair_records(a, s->n_max), st)))
-      return rc;
-    const void* cp[4] = {wh->wc1a, wh->wc1b, wh->wc2h, wh->wc3h};
-    return launch_color_h2(a.s, a.w, cp, wh->cscale, wh->range_flag, a.hid, a.vmask, out_feat, st);
-  }
   // k_point_pre_h2 / k_point_pre (P1) -> k_pairs_h2 (aggregate_x3.hip) -> k_color_h2 / k_color
   if (wh->w1ah) {
     if (!a.pts.p1_ready && (rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a, wh->range_flag, a.p1, st)))
@@ -1537,7 +1532,7 @@ extern "C" int pnr_aggregate_fwd_h2(const pnr_points* pts, const pnr_samples* s,
     return rc;
   if (wh->wc1a) {
     const void* cp[4] = {wh->wc1a, wh->wc1b, wh->wc2h, wh->wc3h};
-    return launch_color_h2(a.s, a.w, cp, wh->cscale, wh->range_flag, a.hid, a.vmask, out_feat, st);
+    return launch_color_h2(a.s, a.w, cp, wh->cscale, wh->range_flag, a.hid, a.vmask, out_feat, st, a.pts.rw2c);
   }
   return launch_t<false>(a, st, kStageColor);
 }
@@ -1907,6 +1902,10 @@ __global__ void __launch_bounds__(256) k_xyz_bwd(XyzBwdArgs A) {
   float Rw[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  if (A.pts.rw2c) {   // per-point Rw2c: the pair's own matrix
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rw[i] = A.pts.rw2c[(int64_t)pr * 9 + i];
+  }
 #pragma unroll
   for (int i = 0; i < 3; ++i) g[i] += Rw[i] * dd[0] + Rw[3 + i] * dd[1] + Rw[6 + i] * dd[2];
   // channels 3..5 through the perspective coordinates of the pair's camera

@@ -304,10 +304,15 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       dr6[3] = d6[3];
       dr6[4] = d6[4];
       dr6[5] = d6[5];
+      if (A.pts.rw2c) rot_point(A.pts.rw2c, prow, d6, dr6);   // per-point Rw2c (agg_common.h)
       if (role == 0) {
         float vrot[3], drot[3];
         mat3(Rw, vd, vrot);
         mat3(Rw, pdir, drot);
+        if (A.pts.rw2c) {
+          rot_point(A.pts.rw2c, prow, pdir, drot);
+          rot_point(A.pts.rw2c, active ? slot0_point(A.s, row) : 0, vd, vrot);
+        }
         const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
         const float ex[8] = {colr[0], colr[1], colr[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2],
                              dot, 1.f};
@@ -515,6 +520,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
         const int64_t drow = dir_row(A.s, row);
         const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
         mat3(Rw, vd, vrot);
+        if (A.pts.rw2c) rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
       }
       float pe[32];
 #pragma unroll

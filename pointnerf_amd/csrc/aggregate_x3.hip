@@ -484,6 +484,7 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
   dr6[3] = d6[3];
   dr6[4] = d6[4];
   dr6[5] = d6[5];
+  if (A.pts.rw2c) rot_point(A.pts.rw2c, prow, d6, dr6);   // per-point Rw2c (agg_common.h)
   if (pw == 0) {
     const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
     const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
@@ -494,6 +495,10 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
     float vrot[3], drot[3];
     mat3(Rw, vd, vrot);
     mat3(Rw, pdir, drot);
+    if (A.pts.rw2c) {
+      rot_point(A.pts.rw2c, prow, pdir, drot);
+      rot_point(A.pts.rw2c, active ? slot0_point(A.s, row) : 0, vd, vrot);
+    }
     const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
     const float ex[8] = {col[0], col[1], col[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2], dot, 1.f};
     float* exL = reinterpret_cast<float*>(lds + L::OffEx) + nb * 8 * kXT;
@@ -1055,6 +1060,7 @@ struct ColH2Args {
   const float* hid;
   const int32_t* vmask;
   float* out_feat;
+  const float* rw2c_pp;   // pnr_points.rw2c (per-point Rw2c) or NULL
 };
 
 // hid row groups [G0, G0 + NG) of the tile's 64 samples (both planes) ->
@@ -1107,9 +1113,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
       const int64_t v = v0 + lane;
       float vrot[3] = {0.f, 0.f, 0.f};
       if (v < n) {
-        const int64_t drow = dir_row(A.s, sample_row(A.s, v));
+        const int64_t row = sample_row(A.s, v);
+        const int64_t drow = dir_row(A.s, row);
         const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
         mat3(Rw, vd, vrot);
+        if (A.rw2c_pp) rot_point(A.rw2c_pp, slot0_point(A.s, row), vd, vrot);
       }
       float pe[32];
 #pragma unroll
@@ -1297,7 +1305,8 @@ int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, in
 }
 
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
-                    int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st) {
+                    int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st,
+                    const float* rw2c_pp) {
   static bool attr = false;
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_h2),
@@ -1313,6 +1322,7 @@ int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pa
   a.hid = hid;
   a.vmask = vmask;
   a.out_feat = out_feat;
+  a.rw2c_pp = rw2c_pp;
   hipLaunchKernelGGL(k_color_h2, dim3(grid_for(cdiv(s.n_max, kXT), 1, 256 * 4)), dim3(128), kColH2Lds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;

@@ -287,8 +287,13 @@ __device__ __forceinline__ float wave_sum_suffix_incl(float v) {
   return v;
 }
 
+// Extra per-slot output gradients of the dense ray_march (all differentiable in
+// the reference): dox = d opacity, dTx = d acc_transmission (exclusive T); a d
+// blend_weight is folded into gw by the caller.  d_dist (NULL = not wanted) is
+// the gradient with respect to ray_dist.
 __device__ __forceinline__ void march_slots_bwd(const float sig[2], const float dist[2], const float gw[2], float dbgT,
-                                                int SR, float dsig[2]) {
+                                                int SR, float dsig[2], const float dox[2] = nullptr,
+                                                const float dTx[2] = nullptr, float* ddist = nullptr) {
   const int lane = threadIdx.x & 63;
   const float op0 = 1.f - expf(-sig[0] * dist[0]);
   const float op1 = 1.f - expf(-sig[1] * dist[1]);
@@ -303,7 +308,7 @@ __device__ __forceinline__ void march_slots_bwd(const float sig[2], const float 
     e1 = tot0;
   }
   // dT (exclusive) per slot, then dP_i = dT_{i+1}
-  const float dT0 = gw[0] * op0, dT1 = gw[1] * op1;
+  const float dT0 = gw[0] * op0 + (dTx ? dTx[0] : 0.f), dT1 = gw[1] * op1 + (dTx ? dTx[1] : 0.f);
   float dP0 = __shfl_down(dT0, 1), dP1 = __shfl_down(dT1, 1);
   const float dT1_first = __shfl(dT1, 0);
   if (lane == 63) {
@@ -321,9 +326,14 @@ __device__ __forceinline__ void march_slots_bwd(const float sig[2], const float 
   const float s0 = wave_sum_suffix_incl(dP0 * i0) + tot1;
   const float df0 = (lane < SR) ? s0 / f0 : 0.f;
   const float df1 = (lane + 64 < SR) ? s1 / f1 : 0.f;
-  const float do0 = gw[0] * e0 - df0, do1 = gw[1] * e1 - df1;
-  dsig[0] = do0 * expf(-sig[0] * dist[0]) * dist[0];
-  dsig[1] = do1 * expf(-sig[1] * dist[1]) * dist[1];
+  const float do0 = gw[0] * e0 - df0 + (dox ? dox[0] : 0.f), do1 = gw[1] * e1 - df1 + (dox ? dox[1] : 0.f);
+  const float x0 = expf(-sig[0] * dist[0]), x1 = expf(-sig[1] * dist[1]);
+  dsig[0] = do0 * x0 * dist[0];
+  dsig[1] = do1 * x1 * dist[1];
+  if (ddist) {   // opacity = 1 - exp(-sigma dist): d dist = d opacity exp(-sigma dist) sigma
+    ddist[0] = do0 * x0 * sig[0];
+    ddist[1] = do1 * x1 * sig[1];
+  }
 }
 
 struct CompBwdArgs {
@@ -415,50 +425,193 @@ __global__ void __launch_bounds__(kCBlock) k_composite_bwd(CompBwdArgs A) {
   }
 }
 
-__global__ void __launch_bounds__(kCBlock) k_ray_march_dense_bwd(const float* __restrict__ ray_dist,
-                                                                 const uint8_t* __restrict__ ray_valid,
-                                                                 const float* __restrict__ feat,
-                                                                 const float* __restrict__ bg, int64_t NR, int SR,
-                                                                 int C, const float* __restrict__ d_color,
-                                                                 float* __restrict__ d_feat) {
+// Backward of k_ray_march_dense with respect to feat (and ray_dist), from the
+// gradients of every output: d ray_color [NR,C] and, each optional (NULL = 0),
+// d opacity / d acc_T / d blend_w [NR,SR] and d bg_T [NR].
+struct MarchBwdArgs {
+  const float* ray_dist;
+  const uint8_t* ray_valid;
+  const float* feat;
+  const float* bg;
+  int64_t NR;
+  int SR, C;
+  const float* d_color;
+  const float* d_opacity;
+  const float* d_acc_T;
+  const float* d_blend;
+  const float* d_bgT;
+  float* d_feat;
+  float* d_dist;
+};
+
+__global__ void __launch_bounds__(kCBlock) k_ray_march_dense_bwd(MarchBwdArgs A) {
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int CF = C + 1;
-  for (int64_t r = wave0; r < NR; r += nwaves) {
-    float sig[2], dist[2], vv[2];
+  const int SR = A.SR, C = A.C, CF = C + 1;
+  for (int64_t r = wave0; r < A.NR; r += nwaves) {
+    float sig[2], dist[2], vv[2], dox[2] = {0.f, 0.f}, dTx[2] = {0.f, 0.f}, gb[2] = {0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int s = lane + 64 * q;
       const bool in = s < SR;
       const int64_t e = r * SR + s;
-      vv[q] = (in && ray_valid[e]) ? 1.f : 0.f;
-      sig[q] = in ? feat[e * CF] * vv[q] : 0.f;
-      dist[q] = in ? ray_dist[e] : 0.f;
+      vv[q] = (in && A.ray_valid[e]) ? 1.f : 0.f;
+      sig[q] = in ? A.feat[e * CF] * vv[q] : 0.f;
+      dist[q] = in ? A.ray_dist[e] : 0.f;
+      if (in) {
+        if (A.d_opacity) dox[q] = A.d_opacity[e];
+        if (A.d_acc_T) dTx[q] = A.d_acc_T[e];
+        if (A.d_blend) gb[q] = A.d_blend[e];
+      }
     }
     const SlotOut so = march_slots(sig[0], dist[0], sig[1], dist[1], SR);
     const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
     float gw[2] = {0.f, 0.f};
-    float dbgT = 0.f;
+    float dbgT = A.d_bgT ? A.d_bgT[r] : 0.f;
     for (int c0 = 0; c0 < C; c0 += 64) {
       const int c = c0 + lane;
-      const float dcv = c < C ? d_color[r * C + c] : 0.f;
-      if (bg) dbgT += wave_sum_f32(c < C ? dcv * bg[c] : 0.f);
+      const float dcv = c < C ? A.d_color[r * C + c] : 0.f;
+      if (A.bg) dbgT += wave_sum_f32(c < C ? dcv * A.bg[c] : 0.f);
       for (int s = 0; s < SR; ++s) {
         const int q = s >> 6, src = s & 63;
         const float w = __shfl(q ? w1 : w0, src);
         const int64_t e = (r * SR + s) * CF + 1 + c;
-        const float gws = wave_sum_f32(c < C ? dcv * feat[e] : 0.f);
+        const float gws = wave_sum_f32(c < C ? dcv * A.feat[e] : 0.f);
         if (lane == src) gw[q] += gws;
-        if (c < C) d_feat[e] = w * dcv;
+        if (c < C) A.d_feat[e] = w * dcv;
       }
     }
-    float dsig[2];
-    march_slots_bwd(sig, dist, gw, dbgT, SR, dsig);
+    gw[0] += gb[0];   // blend_weight = opacity * acc_T
+    gw[1] += gb[1];
+    float dsig[2], dd[2];
+    march_slots_bwd(sig, dist, gw, dbgT, SR, dsig, dox, dTx, A.d_dist ? dd : nullptr);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int s = lane + 64 * q;
-      if (s < SR) d_feat[(r * SR + s) * CF] = dsig[q] * vv[q];
+      if (s < SR) {
+        A.d_feat[(r * SR + s) * CF] = dsig[q] * vv[q];
+        if (A.d_dist) A.d_dist[r * SR + s] = dd[q];
+      }
+    }
+  }
+}
+
+// out[c] = sum_r w[r] x[r, c] -- the background colour's gradient (w = is_bg of
+// k_composite: bg_T for a hit ray, 1 for a background ray, so both the ray_march
+// term bg * bg_T and fill_invalid's bg rows are covered; w = bg_T for the dense
+// ray_march).  Block b sums a contiguous ray range in a fixed order (4 waves over
+// strided rays, combined in wave order), then one block sums the block partials in
+// order: bitwise repeatable.
+constexpr int kColsumBlocks = 256;
+
+__global__ void __launch_bounds__(256) k_wcolsum_part(const float* __restrict__ w, const float* __restrict__ x,
+                                                      int64_t R, int C, float* __restrict__ part) {
+  __shared__ float red[4][128];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t per = cdiv(R, kColsumBlocks);
+  const int64_t r0 = blockIdx.x * per, r1 = r0 + per < R ? r0 + per : R;
+  float a0 = 0.f, a1 = 0.f;
+  for (int64_t r = r0 + wid; r < r1; r += 4) {
+    const float wr = w[r];
+    if (lane < C) a0 += wr * x[r * C + lane];
+    if (lane + 64 < C) a1 += wr * x[r * C + lane + 64];
+  }
+  red[wid][lane] = a0;
+  red[wid][lane + 64] = a1;
+  __syncthreads();
+  if (wid == 0) {
+    for (int c = lane; c < C; c += 64)
+      part[(int64_t)blockIdx.x * C + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  }
+}
+
+__global__ void __launch_bounds__(128) k_wcolsum_final(const float* __restrict__ part, int C, float* __restrict__ out) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f;
+  for (int b = 0; b < kColsumBlocks; ++b) a += part[(int64_t)b * C + c];
+  out[c] = a;
+}
+
+// Training aux outputs of NeuralPointsRayMarching.forward
+// (neural_points_volumetric_model.py:335-338) in the reference's compact layout
+// [R'', SR, ...] (rays with ray_vcnt > 0, in ray order): the aggregator's
+// normalised inverse-distance weight (point_aggregators.py:421-429, 803-804; the
+// value before the conf factor) and ray_march's blend_weight = opacity * acc_T
+// from the composite's opacity.  One wave per ray; lane = shading slot.
+struct AuxArgs {
+  int64_t R;
+  int SR, K;
+  const int32_t* n_filled;
+  const int32_t* ray_off;
+  const int32_t* ray_vcnt;
+  const int32_t* ray_row;
+  const int32_t* pidx;
+  const float* sample_w;
+  const float* xyz;
+  const float* opacity;
+  int64_t rows_max;
+  float* weight;
+  float* blend;
+};
+
+__global__ void __launch_bounds__(kCBlock) k_march_aux(AuxArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int SR = a.SR, K = a.K;
+  for (int64_t r = wave0; r < a.R; r += nwaves) {
+    if (a.ray_vcnt[r] <= 0) continue;
+    const int64_t row = a.ray_row[r];
+    if (row >= a.rows_max) continue;
+    if (a.blend) {
+      float op[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int s = lane + 64 * q;
+        op[q] = s < SR ? a.opacity[r * SR + s] : 0.f;
+      }
+      // the exclusive cumprod of k_composite's march_slots on the same opacities
+      const float f0 = (lane < SR) ? (1.f - op[0] + 1e-10f) : 1.f;
+      const float f1 = (lane + 64 < SR) ? (1.f - op[1] + 1e-10f) : 1.f;
+      const float i0 = wave_prod_scan_incl(f0);
+      const float tot0 = __shfl(i0, 63);
+      const float i1 = wave_prod_scan_incl(f1) * tot0;
+      float e0 = __shfl_up(i0, 1), e1 = __shfl_up(i1, 1);
+      if (lane == 0) {
+        e0 = 1.f;
+        e1 = tot0;
+      }
+      if (lane < SR) a.blend[row * SR + lane] = op[0] * e0;
+      if (lane + 64 < SR) a.blend[row * SR + lane + 64] = op[1] * e1;
+    }
+    if (a.weight) {
+      const int n = a.n_filled[r], off = a.ray_off[r];
+      for (int s = lane; s < SR; s += 64) {
+        float* wo = a.weight + (row * SR + s) * K;
+        if (s >= n) {
+          for (int k = 0; k < K; ++k) wo[k] = 0.f;
+          continue;
+        }
+        const int64_t i = off + s;
+        const float sw[3] = {a.sample_w[i * 3], a.sample_w[i * 3 + 1], a.sample_w[i * 3 + 2]};
+        float wl[16];
+        float sum = 0.f;
+        for (int k = 0; k < K; ++k) {
+          const int32_t p = a.pidx[i * K + k];
+          float v = 0.f;
+          if (p >= 0) {
+            const float d0 = a.xyz[(int64_t)p * 3] - sw[0], d1 = a.xyz[(int64_t)p * 3 + 1] - sw[1],
+                        d2 = a.xyz[(int64_t)p * 3 + 2] - sw[2];
+            v = 1.f / fmaxf(sqrtf(d0 * d0 + d1 * d1 + d2 * d2), 1e-6f);
+          }
+          wl[k] = v;
+          sum += v;
+        }
+        const float den = fmaxf(sum, 1e-8f);
+        for (int k = 0; k < K; ++k) wo[k] = wl[k] / den;
+      }
     }
   }
 }
@@ -559,16 +712,61 @@ extern "C" int pnr_composite_bwd(const pnr_rays* rays, const pnr_query_params* q
   return PNR_OK;
 }
 
-extern "C" int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
-                                 const float* bg, int64_t NR, int32_t SR, int32_t C, const float* d_ray_color,
-                                 float* d_feat, void* stream) {
+extern "C" int pnr_ray_march_bwd_ex(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
+                                    const float* bg, int64_t NR, int32_t SR, int32_t C, const float* d_ray_color,
+                                    const float* d_opacity, const float* d_acc_T, const float* d_blend_w,
+                                    const float* d_bg_T, float* d_feat, float* d_ray_dist, void* stream) {
   PNR_CHECK_ARG(ray_dist && ray_valid && feat && d_ray_color && d_feat, "ray_march_bwd: null pointer");
   PNR_CHECK_ARG(SR >= 1 && SR <= 128, "ray_march_bwd: SR=%d unsupported (1..128)", SR);
   PNR_CHECK_ARG(C >= 1, "ray_march_bwd: C must be >= 1");
   if (NR == 0) return PNR_OK;
+  MarchBwdArgs a = {ray_dist, ray_valid, feat, bg, NR, SR, C, d_ray_color, d_opacity, d_acc_T, d_blend_w, d_bg_T,
+                    d_feat, d_ray_dist};
   const unsigned grid = grid_for(NR * 64, kCBlock, 256 * 16);
-  hipLaunchKernelGGL(k_ray_march_dense_bwd, dim3(grid), dim3(kCBlock), 0, as_stream(stream), ray_dist, ray_valid,
-                     feat, bg, NR, SR, C, d_ray_color, d_feat);
+  hipLaunchKernelGGL(k_ray_march_dense_bwd, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,
+                                 const float* bg, int64_t NR, int32_t SR, int32_t C, const float* d_ray_color,
+                                 float* d_feat, void* stream) {
+  return pnr_ray_march_bwd_ex(ray_dist, ray_valid, feat, bg, NR, SR, C, d_ray_color, nullptr, nullptr, nullptr,
+                              nullptr, d_feat, nullptr, stream);
+}
+
+extern "C" int pnr_weighted_colsum_scratch_floats(int32_t C, int64_t* out) {
+  PNR_CHECK_ARG(out && C >= 1 && C <= 128, "weighted_colsum: C=%d unsupported (1..128)", C);
+  *out = (int64_t)kColsumBlocks * C;
+  return PNR_OK;
+}
+
+extern "C" int pnr_weighted_colsum(const float* w, const float* x, int64_t R, int32_t C, float* out, float* partials,
+                                   void* stream) {
+  PNR_CHECK_ARG(w && x && out && partials, "weighted_colsum: null pointer");
+  PNR_CHECK_ARG(C >= 1 && C <= 128, "weighted_colsum: C=%d unsupported (1..128)", C);
+  PNR_CHECK_ARG(R >= 0, "weighted_colsum: R < 0");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_wcolsum_part, dim3(kColsumBlocks), dim3(256), 0, st, w, x, R, C, partials);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_wcolsum_final, dim3(1), dim3(128), 0, st, partials, C, out);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_march_aux(const pnr_rays* rays, const pnr_query_params* q, const pnr_query_bufs* b,
+                             const float* xyz, const float* opacity, int64_t rows_max, float* weight,
+                             float* blend_weight, void* stream) {
+  PNR_CHECK_ARG(rays && q && b, "march_aux: null pointer");
+  PNR_CHECK_ARG(q->SR >= 1 && q->SR <= 128, "march_aux: SR=%d unsupported (1..128)", q->SR);
+  PNR_CHECK_ARG(q->K >= 1 && q->K <= 16, "march_aux: K=%d unsupported (1..16)", q->K);
+  PNR_CHECK_ARG(!weight || xyz, "march_aux: weight needs xyz");
+  PNR_CHECK_ARG(!blend_weight || opacity, "march_aux: blend_weight needs opacity");
+  if (rays->R == 0 || rows_max <= 0 || (!weight && !blend_weight)) return PNR_OK;
+  AuxArgs a = {rays->R, q->SR, q->K, b->n_filled, b->ray_off, b->ray_vcnt, b->ray_row, b->pidx, b->sample_w,
+               xyz, opacity, rows_max, weight, blend_weight};
+  const unsigned grid = grid_for(rays->R * 64, kCBlock, 256 * 16);
+  hipLaunchKernelGGL(k_march_aux, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

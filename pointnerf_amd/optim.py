@@ -23,11 +23,16 @@ def _bump_versions(ps):
     version (the aggregator's weight packs, keyed on p._version) must see the
     update as torch's in-place ops would report it."""
     setv = getattr(torch._C._autograd, "_unsafe_set_version_counter", None)
-    if setv is not None:
+    try:
+        if setv is None:
+            raise TypeError
         setv(tuple(ps), tuple(p._version + 1 for p in ps))
-    else:                       # older torch: a 1-element in-place no-op per parameter
-        for p in ps:
-            p.data.view(-1)[:1].add_(0)
+    except TypeError:
+        # older torch (no tuple API): a 1-element in-place no-op on the parameter
+        # itself -- p.data has its own version counter, which would not be seen
+        with torch.no_grad():
+            for p in ps:
+                p.view(-1)[:1].add_(0)
 
 
 class Adam(torch.optim.Optimizer):

@@ -61,7 +61,10 @@ class NeuralPoints(nn.Module):
         self.points_color = None if color is None else nn.Parameter(color.to(dev).float().reshape(1, -1, 3).contiguous())
         self.points_dir = None if dirs is None else nn.Parameter(dirs.to(dev).float().reshape(1, -1, 3).contiguous())
         self.points_conf = None if conf is None else nn.Parameter(conf.to(dev).float().reshape(1, -1, 1).contiguous())
-        self.Rw2c = torch.eye(3, device=dev) if Rw2c is None else Rw2c.to(dev).float()
+        # [3,3] uniform, or [N,3,3] per point (neural_points.py:289, 799; pnr_points.rw2c)
+        self.Rw2c = torch.eye(3, device=dev) if Rw2c is None else Rw2c.to(dev).float().contiguous()
+        if self.Rw2c.dim() == 3 and self.Rw2c.shape != (self.xyz.shape[0], 3, 3):
+            raise L.PnrError(f"per-point Rw2c must be [N,3,3], got {tuple(self.Rw2c.shape)}")
 
     def embedding_fp32(self) -> torch.Tensor:
         """points_embeding as fp32 [N,32] (the table itself, or a copy of the bf16
@@ -87,7 +90,19 @@ class NeuralPoints(nn.Module):
         p = L.Points(keep[0].shape[0], keep[0].data_ptr(), None, L.ptr(keep[1]), L.ptr(keep[2]), L.ptr(keep[3]),
                      L.ptr(keep[4]), L.ptr(campos), L.ptr(camrot))
         p.emb_bf16 = L.ptr(keep[5])
-        return p, keep
+        rw = self.rw2c_table()
+        p.rw2c = L.ptr(rw)
+        return p, keep + (rw,)
+
+    def rw2c_table(self):
+        """The per-point Rw2c as the kernels read it ([N,9] fp32), or None for a
+        uniform Rw2c (that one goes through the aggregator's pnr_mlp.rw2c)."""
+        rw = self.Rw2c
+        if rw is None or rw.dim() == 2:
+            return None
+        if rw.shape[0] != self.xyz.shape[0]:
+            raise L.PnrError(f"per-point Rw2c has {rw.shape[0]} rows, the cloud {self.xyz.shape[0]} points")
+        return rw.detach().reshape(-1, 9).float().contiguous()
 
     def bytes_per_point(self) -> int:
         """HBM bytes of one point's parameters (168 fp32, 104 with a bf16 embedding)."""
@@ -124,7 +139,8 @@ class NeuralPoints(nn.Module):
         def sel(t, c):
             return None if t is None else torch.index_select(t, 1, idx).view(B, R, SR, K, c)
 
-        return (sel(self.points_color, 3), self.Rw2c, sel(self.points_dir, 3), sel(self.points_conf, 1),
+        rw = self.Rw2c if self.Rw2c.dim() == 2 else torch.index_select(self.Rw2c, 0, idx).view(B, R, SR, K, 3, 3)
+        return (sel(self.points_color, 3), rw, sel(self.points_dir, 3), sel(self.points_conf, 1),
                 g[..., 6:], g[..., 3:6], g[..., :3], mask, sample_loc, sample_loc_w, sample_ray_dirs,
                 ray_mask, vsize, 0)
 
@@ -199,9 +215,9 @@ class NeuralPointsRayMarching(nn.Module):
         rw = self.neural_points.Rw2c
         key = (rw.data_ptr(), rw._version, tuple(rw.shape))
         if key != self._rw2c_key:
-            if rw.dim() != 2:
-                raise L.PnrError("per-point Rw2c is not implemented by libpnr (uniform Rw2c only)")
-            self.aggregator.set_rw2c(rw.detach())
+            # per-point [N,3,3]: the kernels read it from pnr_points.rw2c
+            # (NeuralPoints.tables), the uniform matrix stays the identity
+            self.aggregator.set_rw2c(rw.detach() if rw.dim() == 2 else None)
             self._rw2c_key = key
 
     @torch.no_grad()
@@ -238,8 +254,9 @@ class NeuralPointsRayMarching(nn.Module):
         if self._pending and (sync or self._sv_per_ray is None):
             # a synchronous call reads (and may clear) the shared range flag and the
             # counts: complete the pending sync-free calls first so none of their
-            # checks is lost
-            self.finish()
+            # checks is lost; their counts stay queued for the caller's next finish()
+            done = self.finish()
+            self._done = done + getattr(self, "_done", [])
         prec = self._precision_now()
         if not sync and self._sv_per_ray is not None:
             out, rec = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events,
@@ -322,7 +339,9 @@ class NeuralPointsRayMarching(nn.Module):
         if need > 0:
             head = self._pending[:need]
             head[-1]["event"].synchronize()
-            if need < len(self._pending) and any(int(r["range_flag"].item()) != 0 for r in head
+            # the range flags as copied to pinned memory behind each call's event (a
+            # .item() here would queue behind -- and wait for -- the later calls)
+            if need < len(self._pending) and any(int(r["range_host"][0]) != 0 for r in head
                                                  if r.get("range_flag") is not None):
                 head = self._pending
                 head[-1]["event"].synchronize()
@@ -340,8 +359,10 @@ class NeuralPointsRayMarching(nn.Module):
         flags = {}
         for r in pend:
             f = r.get("range_flag")
-            if f is not None and f.data_ptr() not in flags:
-                flags[f.data_ptr()] = (f, int(f.item()) != 0)
+            if f is not None:
+                bad = int(r["range_host"][0]) != 0   # this call's own copy (taken after its launches)
+                prev = flags.get(f.data_ptr())
+                flags[f.data_ptr()] = (f, bad or (prev is not None and prev[1]))
         range_bad = any(bad for _, bad in flags.values())
         if range_bad:
             cur = self.aggregator.h2_key()
@@ -450,7 +471,7 @@ class NeuralPointsRayMarching(nn.Module):
         # 10 M points / 1.25 M rays the 5.8 ms P1 outlasted the query and the overlap
         # gained nothing)
         if (precision == "fp32h2" and capacity is not None and keep is None and self.p1_side_stream
-                and self.aggregator.pairs_kernel == "wt" and pts.n <= self.p1_side_max_points_per_ray * R):
+                and pts.n <= self.p1_side_max_points_per_ray * R):
             c0 = min(chunk, R)
             Sv0 = min(int(c0 * capacity) + 1024, c0 * SR)
             scr0, ready0 = self._agg_scratch(state, max(Sv0, 1), pts.n, dev, bf16, reuse_p1, precision)
@@ -539,6 +560,12 @@ class NeuralPointsRayMarching(nn.Module):
                 events += [("query", e0, e1), ("aggregate", e2, e3), ("composite", e3, e4)]
         if rec is not None:
             if record:
+                if rec["range_flag"] is not None:
+                    # the fp32h2 range flag as it stands after this call's launches, to
+                    # pinned memory behind the call's event: finish() reads it without
+                    # a stream sync (which would wait for the calls queued after it)
+                    rec["range_host"] = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                    rec["range_host"].copy_(rec["range_flag"], non_blocking=True)
                 rec["event"] = torch.cuda.Event()
                 rec["event"].record()
         else:
@@ -613,7 +640,8 @@ class NeuralPointsRayMarching(nn.Module):
         used = (used_buf[:cnt["n_used"]], used_map)
         if self.train_precision not in ("fp32", "fp32x3", "fp32h2"):
             raise L.PnrError(f"train_precision {self.train_precision!r}: 'fp32h2', 'fp32x3' or 'fp32'")
-        spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot), keep=(bufs, rd),
+        spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot, rw2c=np_.rw2c_table()),
+                       keep=(bufs, rd),
                        used=used, x3=self.train_precision == "fp32x3", h2=self.train_precision == "fp32h2")
         spec.keep_saved = self.keep_train_saved
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
@@ -623,32 +651,74 @@ class NeuralPointsRayMarching(nn.Module):
             self.h2_fallbacks += 1
         if C == 3:
             feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
-        cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg))
-        cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(bg, campos, camrot, rd, hp))
-        out = CompositeFn.apply(cspec, feat)
-        # conf_coefficient [1, R'', SR, K] as the reference returns it for the
-        # zero_one loss (point_aggregators.py:810-816): gradiant_clamp of the
-        # gathered conf, empty slots gather point 0 (torch.clamp(pidx, 0))
+        cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, None)
+        cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(campos, camrot, rd, hp))
+        # bg: differentiable (the fork optimises bg_color, mvs_points_volumetric_model.py:92-94)
+        out = CompositeFn.apply(cspec, feat, bg)
         # rows of the point table this batch can give a gradient: the referenced
         # points, and point 0 (empty slots gather it in conf_coefficient) --
         # parallel.GradReducer reduces only these across ranks
         self.last_train_aux = {"touched_rows": torch.cat([used[0].long(), torch.zeros(1, dtype=torch.long, device=dev)])}
         if self.keep_train_saved:
             self.last_train_aux["saved"] = spec.saved
-        if np_.points_conf is not None:
-            Rv = cnt["R_valid"]
-            f32 = dict(dtype=torch.float32, device=dev)
-            pidx = torch.empty((1, Rv, SR, K), dtype=torch.int32, device=dev)
-            scratch3 = [torch.empty((1, Rv, SR, 3), **f32) for _ in range(3)]
-            rmask = torch.empty((1, R), dtype=torch.int8, device=dev)
-            L.check(L.lib().pnr_query_compact(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c), Rv,
-                                              L.ptr(pidx), L.ptr(scratch3[0]), L.ptr(scratch3[1]),
-                                              L.ptr(scratch3[2]), L.ptr(rmask), L.stream_ptr(dev)),
-                    "pnr_query_compact")
-            cf = np_.points_conf.reshape(-1)[pidx.clamp(min=0).long()]
-            self.last_train_aux["conf_coefficient"] = cf - (cf - torch.clamp(cf, 1e-4, 1.0)).detach()
-            self.last_train_aux["sample_pidx"] = pidx
+        if np_.points_conf is not None or self.wants_aux():
+            self.last_train_aux.update(self._march_aux(rays, qp, bufs, R, cnt["R_valid"], xyz, out[1]))
         return out
+
+    def wants_aux(self) -> bool:
+        """The reference aggregator returns weight / conf_coefficient (and the
+        module puts them with blend_weight into its output,
+        neural_points_volumetric_model.py:335-338) unless no loss reads them
+        (point_aggregators.py:814-815)."""
+        o = self.opt
+        return (getattr(o, "sparse_loss_weight", 0) > 0 or "conf_coefficient" in getattr(o, "zero_one_loss_items", ())
+                or getattr(o, "prob", 0) != 0)
+
+    def _march_aux(self, rays, qp, bufs, R, Rv, xyz, opacity):
+        """weight [1,R'',SR,K] (detached: the aggregator's normalised weight),
+        blend_weight [1,R'',SR,1] (detached), conf_coefficient [1,R'',SR,K]
+        (gradiant_clamp of the gathered conf: straight-through gradient to
+        points_conf, point_aggregators.py:724-726, 810-813; empty slots gather
+        point 0 as torch.clamp(pidx, 0) does; 1 without a conf table) and
+        sample_pidx, in pnr_query_compact's row order -- the reference's
+        [1, R'', SR, ...] tensors of the same rays."""
+        opt, np_ = self.opt, self.neural_points
+        SR, K = opt.SR, opt.K
+        dev = opacity.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        pidx = torch.empty((1, Rv, SR, K), dtype=torch.int32, device=dev)
+        scratch3 = [torch.empty((1, Rv, SR, 3), **f32) for _ in range(3)]
+        rmask = torch.empty((1, R), dtype=torch.int8, device=dev)
+        L.check(L.lib().pnr_query_compact(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c), Rv,
+                                          L.ptr(pidx), L.ptr(scratch3[0]), L.ptr(scratch3[1]),
+                                          L.ptr(scratch3[2]), L.ptr(rmask), L.stream_ptr(dev)),
+                "pnr_query_compact")
+        weight = torch.empty((1, Rv, SR, K), **f32)
+        blend = torch.empty((1, Rv, SR, 1), **f32)
+        op = opacity.detach().contiguous()
+        L.check(L.lib().pnr_march_aux(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),
+                                      L.ptr(xyz), L.ptr(op), Rv, L.ptr(weight), L.ptr(blend), L.stream_ptr(dev)),
+                "pnr_march_aux")
+        aux = {"weight": weight, "blend_weight": blend, "sample_pidx": pidx, "conf_coefficient": 1}
+        if np_.points_conf is not None:
+            cf = np_.points_conf.reshape(-1)[pidx.clamp(min=0).long()]
+            aux["conf_coefficient"] = cf - (cf - torch.clamp(cf, 1e-4, 1.0)).detach()
+        return aux
+
+    @torch.no_grad()
+    def eval_aux(self, campos, camrot, raydir, near, far, opacity):
+        """forward()'s weight / blend_weight / conf_coefficient for an
+        evaluation render (render_rays keeps no per-pair state): the batch's
+        query again, then pnr_query_compact + pnr_march_aux on the rendered
+        opacity.  conf_coefficient carries no graph here (no_grad render)."""
+        np_ = self.neural_points
+        dev = raydir.device
+        from .querier import camera_tables
+        cp, cr = camera_tables(campos, camrot, None)
+        xyz = np_.xyz.detach().contiguous()
+        bufs, hp, rays, qp = np_.querier.run(xyz, raydir.float().contiguous(), cp, cr, near, far, bufs=None)
+        cnt = bufs.read_counts()
+        return self._march_aux(rays, qp, bufs, raydir.shape[0], cnt["R_valid"], xyz, opacity)
 
     def zero_one_conf_loss(self, zero_epsilon: float = 1e-3):
         """zero_one_loss(conf_coefficient) of the last render_rays_train, computed
@@ -695,18 +765,27 @@ class NeuralPointsRayMarching(nn.Module):
             bg_color = None
         # training loop (model(...) then loss.backward(), as run/train_ft.py does):
         # differentiable path; evaluation / no_grad: the fused forward
-        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+        train = torch.is_grad_enabled() and self.training and (
+            any(p.requires_grad for p in self.parameters()) or (torch.is_tensor(bg_color) and bg_color.requires_grad))
+        if train:
             color, opacity, is_bg, ray_mask = self.render_rays_train(campos, camrotc2w, raydir.reshape(-1, 3),
                                                                      near_v, far_v, bg_color)
+            aux = self.last_train_aux if self.wants_aux() else None
         else:
             color, opacity, is_bg, ray_mask = self.render_rays(campos, camrotc2w, raydir.reshape(-1, 3),
                                                                near_v, far_v, bg_color)
+            aux = self.eval_aux(campos, camrotc2w, raydir.reshape(-1, 3), near_v, far_v, opacity) \
+                if self.wants_aux() else None
         R = color.shape[0]
         mask_f = ray_mask.float().view(1, R, 1)
         out = dict(coarse_raycolor=color.view(1, R, -1), coarse_point_opacity=opacity.view(1, R, -1),
                    coarse_is_background=is_bg.view(1, R, 1), ray_mask=ray_mask.view(1, R))
         out["coarse_mask"] = 1 - out["coarse_is_background"]
         out["queried_shading"] = (1 - mask_f).repeat(1, 1, 3)
+        if aux is not None:   # neural_points_volumetric_model.py:335-338
+            out["weight"] = aux["weight"]
+            out["blend_weight"] = aux["blend_weight"]
+            out["conf_coefficient"] = aux["conf_coefficient"]
         if self.neural_render_2d is not None:
             img_h = int(h.item()) if torch.is_tensor(h) else int(h)
             img_w = int(w.item()) if torch.is_tensor(w) else int(w)

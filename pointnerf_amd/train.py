@@ -154,6 +154,7 @@ class AggregateFn(torch.autograd.Function):
         pe = spec.pts_extra
         pts = L.Points(N, pe["xyz"].data_ptr(), L.ptr(pe.get("pers")), tabs[0].data_ptr(), L.ptr(tabs[1]),
                        L.ptr(tabs[2]), L.ptr(tabs[3]), L.ptr(pe.get("campos")), L.ptr(pe.get("camrot")))
+        pts.rw2c = L.ptr(pe.get("rw2c"))   # per-point Rw2c [N,9] or None
         n_p1 = N
         if spec.used is not None:
             used, used_map = spec.used
@@ -348,11 +349,16 @@ class CompositeSpec:
 
 
 class CompositeFn(torch.autograd.Function):
-    """ray_color[R, C] = composite(feat[S_valid, C+1]); opacity / is_bg / mask
-    are returned as non-differentiable outputs."""
+    """ray_color[R, C] = composite(feat[S_valid, C+1], bg[C]); opacity / is_bg /
+    mask are returned as non-differentiable outputs.  bg (optional) is the
+    learned background colour (mvs_points_volumetric_model.py:92-94): its
+    gradient is sum_r is_bg[r] d ray_color[r] -- bg_T for a hit ray (the
+    ray_march term, diff_ray_marching.py:544-546), 1 for a background ray
+    (fill_invalid, neural_points_volumetric_model.py:373-375) -- on
+    pnr_weighted_colsum."""
 
     @staticmethod
-    def forward(ctx, spec: CompositeSpec, feat):
+    def forward(ctx, spec: CompositeSpec, feat, bg=None):
         dev = feat.device
         f32 = dict(dtype=torch.float32, device=dev)
         R, SR, C = spec.R, spec.SR, spec.C
@@ -361,11 +367,13 @@ class CompositeFn(torch.autograd.Function):
         is_bg = torch.empty((R,), **f32)
         ray_mask = torch.empty((R,), dtype=torch.int8, device=dev)
         feat_c = feat.detach().contiguous()
+        bg_c = None if bg is None else bg.detach().float().reshape(-1).contiguous()
+        spec.cp.bg_color = L.ptr(bg_c)
         L.check(L.lib().pnr_composite_fwd(ctypes.byref(spec.rays), ctypes.byref(spec.qp), ctypes.byref(spec.bufs.c),
                                           ctypes.byref(spec.cp), L.ptr(feat_c), L.ptr(ray_color), L.ptr(opacity),
                                           L.ptr(is_bg), L.ptr(ray_mask), L.stream_ptr(dev)),
                 "pnr_composite_fwd")
-        ctx.spec, ctx.feat = spec, feat_c
+        ctx.spec, ctx.feat, ctx.bg, ctx.is_bg = spec, feat_c, bg_c, is_bg
         ctx.mark_non_differentiable(opacity, is_bg, ray_mask)
         return ray_color, opacity, is_bg, ray_mask
 
@@ -375,13 +383,17 @@ class CompositeFn(torch.autograd.Function):
         dev = ctx.feat.device
         d_feat = torch.zeros_like(ctx.feat)
         if d_color is None:
-            return None, d_feat
+            return None, d_feat, None
         d_color = d_color.contiguous()
+        spec.cp.bg_color = L.ptr(ctx.bg)
         L.check(L.lib().pnr_composite_bwd(ctypes.byref(spec.rays), ctypes.byref(spec.qp), ctypes.byref(spec.bufs.c),
                                           ctypes.byref(spec.cp), L.ptr(ctx.feat), L.ptr(d_color), L.ptr(d_feat),
                                           L.stream_ptr(dev)),
                 "pnr_composite_bwd")
-        return None, d_feat
+        d_bg = None
+        if ctx.bg is not None and ctx.needs_input_grad[2]:
+            d_bg = L.weighted_colsum(ctx.is_bg, d_color)
+        return None, d_feat, d_bg
 
 
 def ray_march_bwd(ray_dist, ray_valid, feat, bg, d_color):

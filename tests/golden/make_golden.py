@@ -44,8 +44,12 @@ def lego_agg_opt():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", choices=("all", "r04"), default="all",
+                    help="r04: only the round-4 fixtures (per-pair Rw2c aggregator, full ray_march backward)")
     args = ap.parse_args()
     sys.path.insert(0, args.ref)
+    if args.only == "r04":
+        return round4()
     from models.helpers.networks import positional_encoding
     from models.rendering.diff_ray_marching import near_far_linear_ray_generation, ray_march
     from models.rendering.diff_render_func import alpha_blend, radiance_render
@@ -154,6 +158,86 @@ def main():
     np.savez_compressed(os.path.join(HERE, "raymarch_bwd.npz"), g_color=g_color.numpy(),
                         g_features=rfg.grad.numpy())
     print("golden vectors written to", HERE)
+
+
+def round4():
+    """Round-4 fixtures (separate seed, the earlier files stay as they are):
+    aggregator_rw2c.npz -- PointAggregator.forward with a per-pair Rw2c
+    [1,R,SR,K,3,3] (neural_points.py:799 gathers one per point;
+    point_aggregators.py:492-496, 506, 526, 566) and the gradients of its gathered
+    inputs; raymarch_full_bwd.npz -- ray_march's gradients of ray_features,
+    ray_dist and bg_color for a loss on every output (ray_color, opacity,
+    acc_transmission, blend_weight, background_transmission)."""
+    from models.rendering.diff_ray_marching import ray_march
+    from models.rendering.diff_render_func import alpha_blend, radiance_render
+    from models.aggregators.point_aggregators import PointAggregator
+
+    rng = np.random.default_rng(4040)
+    torch.set_num_threads(1)
+    agg = PointAggregator(lego_agg_opt())
+    agg.load_state_dict({k: torch.from_numpy(v) for k, v in formula_params(salt=0.3).items()})
+    R, SR, K = 5, 9, 8
+    mask = rng.uniform(size=(1, R, SR, K)) < 0.75
+    mask[0, 1, 2, :] = False
+    mask[0, 3, :, 2:] = False
+    for r in range(R):           # the KNN fills slots in order: empty slots trail
+        for s_ in range(SR):
+            n = int(mask[0, r, s_].sum())
+            mask[0, r, s_] = False
+            mask[0, r, s_, :n] = True
+    sloc_w = rng.uniform(-0.5, 0.5, size=(1, R, SR, 3)).astype(np.float32)
+    sxyz = (sloc_w[..., None, :] + rng.normal(scale=0.008, size=(1, R, SR, K, 3))).astype(np.float32)
+    campos_a = np.array([0.2, -3.8, 1.7], np.float32)
+    rot = np.array([[0.99, 0.1, 0.0], [0.0, 0.3, -0.95], [-0.1, 0.95, 0.3]], np.float32)
+
+    def pers(p):
+        xc = (p - campos_a) @ rot
+        return np.stack([xc[..., 0] / xc[..., 2], xc[..., 1] / xc[..., 2], xc[..., 2]], -1).astype(np.float32)
+
+    # random proper rotations per pair (QR of Gaussian matrices)
+    q, rr = np.linalg.qr(rng.normal(size=(1, R, SR, K, 3, 3)))
+    q = q * np.sign(np.diagonal(rr, axis1=-2, axis2=-1))[..., None, :]
+    inputs = dict(
+        sampled_color=rng.normal(size=(1, R, SR, K, 3)).astype(np.float32),
+        sampled_dir=rng.normal(size=(1, R, SR, K, 3)).astype(np.float32),
+        sampled_conf=rng.uniform(-0.2, 1.3, size=(1, R, SR, K, 1)).astype(np.float32),
+        sampled_embedding=rng.uniform(-0.5, 0.5, size=(1, R, SR, K, 32)).astype(np.float32),
+        sampled_xyz_pers=pers(sxyz), sampled_xyz=sxyz, sample_pnt_mask=mask,
+        sample_loc=pers(sloc_w), sample_loc_w=sloc_w,
+        sample_ray_dirs=np.broadcast_to(rng.normal(size=(1, R, 1, 3)), (1, R, SR, 3)).astype(np.float32),
+        sampled_Rw2c=q.astype(np.float32))
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in inputs.items()}
+    for k in ("sampled_color", "sampled_dir", "sampled_conf", "sampled_embedding"):
+        t[k].requires_grad_(True)
+    feats, ray_valid, weight, conf = agg(t["sampled_color"], t["sampled_Rw2c"], t["sampled_dir"], t["sampled_conf"],
+                                         t["sampled_embedding"], t["sampled_xyz_pers"], t["sampled_xyz"],
+                                         t["sample_pnt_mask"], t["sample_loc"], t["sample_loc_w"],
+                                         t["sample_ray_dirs"], [0.004, 0.004, 0.004], 0)
+    g_feat = torch.tensor(rng.normal(size=tuple(feats.shape)), dtype=torch.float32)
+    (feats * g_feat).sum().backward()
+    grads = {"g_" + k: t[k].grad.numpy() for k in ("sampled_color", "sampled_dir", "sampled_conf",
+                                                  "sampled_embedding")}
+    np.savez_compressed(os.path.join(HERE, "aggregator_rw2c.npz"), features=feats.detach().numpy(),
+                        ray_valid=ray_valid.numpy(), weight=weight.detach().numpy(), g_feat=g_feat.numpy(),
+                        **grads, **{k: np.ascontiguousarray(v) for k, v in inputs.items()})
+
+    NR, SRm, C = 10, 20, 128
+    rd = torch.tensor(rng.uniform(0.0, 0.01, size=(1, NR, SRm)), dtype=torch.float32, requires_grad=True)
+    rv = torch.tensor(rng.uniform(size=(1, NR, SRm)) < 0.6)
+    rf = torch.tensor(np.concatenate([rng.uniform(0, 300, size=(1, NR, SRm, 1)),
+                                      rng.normal(size=(1, NR, SRm, C))], -1), dtype=torch.float32,
+                      requires_grad=True)
+    bg = torch.tensor(rng.uniform(size=(C,)), dtype=torch.float32, requires_grad=True)
+    out = ray_march(rd, rv, rf, radiance_render, alpha_blend, bg)
+    gs = [torch.tensor(rng.normal(size=tuple(out[i].shape)), dtype=torch.float32) for i in (0, 2, 3, 4, 5)]
+    loss = sum((out[i] * g).sum() for i, g in zip((0, 2, 3, 4, 5), gs))
+    loss.backward()
+    np.savez_compressed(os.path.join(HERE, "raymarch_full_bwd.npz"), ray_dist=rd.detach().numpy(),
+                        ray_valid=rv.numpy(), ray_features=rf.detach().numpy(), bg_color=bg.detach().numpy(),
+                        g_color=gs[0].numpy(), g_opacity=gs[1].numpy(), g_acc=gs[2].numpy(),
+                        g_blend=gs[3].numpy(), g_bgT=gs[4].numpy(), d_features=rf.grad.numpy(),
+                        d_ray_dist=rd.grad.numpy(), d_bg=bg.grad.numpy())
+    print("round-4 golden vectors written to", HERE)
 
 
 if __name__ == "__main__":

@@ -169,3 +169,40 @@ def test_render_views_one_batch_equals_per_view(cuda, precision):
                 assert torch.equal(w[3], g[3])
                 for x, y in zip(w[:3], g[:3]):
                     assert float((x - y).abs().max()) <= 1e-6
+
+
+def test_partial_finish_does_not_wait_for_later_calls(cuda):
+    """finish(upto=1) on fp32h2 reads call 1's range flag from the pinned copy
+    taken behind call 1's event, not with a stream sync: it returns while a
+    later call (queued behind a ~0.3 s spin kernel) is still running."""
+    from pointnerf_amd import _lib as L
+    sc, cams = _cams(cuda)
+    m = _renderer(sc, cuda, formula_params(salt=0.4))
+    m.precision = "fp32h2"
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    m.render_rays(*cams[0], 2.0, 6.0, bg)          # sizes the sync-free feature buffer
+    m.render_rays(*cams[0], 2.0, 6.0, bg, sync=False)
+    probe = torch.zeros(1, device=cuda)
+    L.check(L.lib().pnr_clock_probe(L.ptr(probe), 1200000, L.stream_ptr(cuda)), "pnr_clock_probe")
+    m.render_rays(*cams[1], 2.0, 6.0, bg, sync=False)
+    ev = torch.cuda.Event()
+    ev.record()
+    assert len(m.finish(upto=1)) == 1
+    assert not ev.query(), "finish(upto=1) waited for the later call"
+    assert len(m.finish()) == 1
+    assert ev.query()
+
+
+def test_sync_call_keeps_pending_counts(cuda):
+    """A synchronous render_rays drains the pending sync-free calls; their counts
+    stay queued, so the next finish() still returns one entry per issued call."""
+    sc, cams = _cams(cuda)
+    m = _renderer(sc, cuda, formula_params(salt=0.4))
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    m.render_rays(*cams[0], 2.0, 6.0, bg)
+    want = dict(m.last_counts)
+    m.render_rays(*cams[0], 2.0, 6.0, bg, sync=False)
+    m.render_rays(*cams[1], 2.0, 6.0, bg, sync=False)
+    m.render_rays(*cams[0], 2.0, 6.0, bg)           # synchronous: completes the two pending calls
+    got = m.finish()
+    assert len(got) == 2 and got[0] == want

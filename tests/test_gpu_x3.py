@@ -43,17 +43,13 @@ def _setup(sc, cuda, params=None, seed=0):
     return agg.eval(), np_
 
 
-SPLITS = ["x3", "h2", "as"]   # as: fp32h2 with the activation-stationary pairs kernel (k_pairs_as)
+SPLITS = ["x3", "h2"]
 
 
 def _both(agg, np_, sc, cuda, used=False, variant="x3", check_range=True, scratch_fill=None):
     """fp32 and split-path features on one query -> (f32 [Sv,129], split [Sv,129]);
-    used: P1 only for the referenced points (the training-batch layout).
-    variant "as" = pnr_aggregate_fwd_h2 with agg.pairs_kernel "as"."""
+    used: P1 only for the referenced points (the training-batch layout)."""
     from pointnerf_amd import _lib as L
-    if variant in ("h2", "as"):
-        agg.pairs_kernel = "as" if variant == "as" else "wt"
-        variant = "h2"
     cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
     rd = torch.from_numpy(sc["raydir"]).to(cuda).contiguous()
     bufs, hp, rays, qp = np_.querier.run(np_.xyz.detach(), rd, cp, cr, 2.0, 6.0)
@@ -142,8 +138,7 @@ def test_x3_render_vs_oracle(cuda, variant):
     sc = scene(30000, H=48, W=48, theta=200.0, default_conf=None)
     params = formula_params(salt=0.1)
     agg, np_ = _setup(sc, cuda, params)
-    agg.pairs_kernel = "as" if variant == "as" else "wt"
-    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32" + ("h2" if variant == "as" else variant))
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="fp32" + variant)
     args = [torch.from_numpy(sc[k]).to(cuda) for k in ("campos", "camrot", "raydir")]
     with torch.no_grad():
         c, op, bg, mask = m.render_rays(*args, 2.0, 6.0, torch.from_numpy(sc["bg"]).to(cuda))
@@ -157,7 +152,7 @@ def test_x3_render_vs_oracle(cuda, variant):
     assert psnr >= 60.0, psnr
 
 
-@pytest.mark.parametrize("variant", ["h2", "as"])
+@pytest.mark.parametrize("variant", ["h2"])
 def test_h2_large_weights_prescaled(cuda, variant):
     """Weights far above the f16 range of 2^11 Wh are pre-scaled in the pack
     (scale = 2^(s-11)); features stay within the fp32 tolerance."""
@@ -241,7 +236,7 @@ def test_h2_mixed_sync_and_async_calls_keep_range_check(cuda):
             m.finish()
 
 
-@pytest.mark.parametrize("variant", ["h2", "as"])
+@pytest.mark.parametrize("variant", ["h2"])
 def test_h2_raw_launch_sets_range_flag(cuda, variant):
     """pnr_aggregate_fwd_h2 itself: out-of-range activation -> *range_flag = 1."""
     sc = scene(20000, H=32, W=32, default_conf=None)
@@ -267,7 +262,7 @@ def test_h2_colour_branch_overflow_sets_flag(cuda):
     _both(agg, np_, sc, cuda, variant="h2")   # asserts the flag stays clear
 
 
-@pytest.mark.parametrize("variant", ["h2", "as"])
+@pytest.mark.parametrize("variant", ["h2"])
 def test_h2_stale_scratch_ignored(cuda, variant):
     """k_color_h2 copies the f16-split hid planes of whole 64-sample tiles; rows
     past n (and of samples without a neighbour) are never written by k_pairs_h2.

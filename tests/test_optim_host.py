@@ -38,3 +38,17 @@ def test_version_bump_marks_parameters_changed():
     v0 = [p._version for p in ps]
     _bump_versions(ps)
     assert [p._version for p in ps] == [v + 1 for v in v0]
+
+
+def test_version_bump_fallback_advances_parameter_version(monkeypatch):
+    """Without the tuple _unsafe_set_version_counter API (torch 2.1-2.3 take
+    (Tensor, int)) the fallback's in-place no-op must bump p._version itself,
+    not the separate counter of p.data."""
+    from pointnerf_amd import optim
+    monkeypatch.setattr(torch._C._autograd, "_unsafe_set_version_counter",
+                        lambda t, v: (_ for _ in ()).throw(TypeError("old signature")), raising=False)
+    ps = [torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(2, 2))]
+    v0 = [p._version for p in ps]
+    optim._bump_versions(ps)
+    assert all(p._version > v for p, v in zip(ps, v0))
+    assert all(float(p.abs().sum()) == 0.0 for p in ps)

@@ -58,3 +58,22 @@ def test_ray_march(golden_dir):
     np.testing.assert_allclose(T, g["acc_transmission"][0], atol=2e-7, rtol=1e-6)
     np.testing.assert_allclose(bw, g["blend_weight"][0], atol=2e-7, rtol=1e-6)
     np.testing.assert_allclose(bgT, g["background_transmission"][0], atol=2e-7, rtol=1e-6)
+
+
+def test_aggregator_per_pair_rw2c(golden_dir):
+    # PointAggregator.forward with a per-pair Rw2c [1,R,SR,K,3,3] (neural_points.py:799 gathers
+    # a per-point table; point_aggregators.py:492-496, 506, 526, 566), from the reference itself
+    g = load(golden_dir, "aggregator_rw2c.npz")
+    f, rv, w, cc = O.aggregate(formula_params(salt=0.3), g["sampled_color"][0], g["sampled_Rw2c"][0],
+                               g["sampled_dir"][0], g["sampled_conf"][0], g["sampled_embedding"][0],
+                               g["sampled_xyz_pers"][0], g["sampled_xyz"][0], g["sample_pnt_mask"][0],
+                               g["sample_loc"][0], g["sample_loc_w"][0], g["sample_ray_dirs"][0])
+    assert np.array_equal(rv, g["ray_valid"][0])
+    np.testing.assert_allclose(f, g["features"][0], atol=1e-6, rtol=1e-5)
+    np.testing.assert_allclose(w, g["weight"][0], atol=1e-6, rtol=1e-5)
+    # the rotation matters: the same inputs with the identity differ
+    f_eye = O.aggregate(formula_params(salt=0.3), g["sampled_color"][0], None, g["sampled_dir"][0],
+                        g["sampled_conf"][0], g["sampled_embedding"][0], g["sampled_xyz_pers"][0],
+                        g["sampled_xyz"][0], g["sample_pnt_mask"][0], g["sample_loc"][0],
+                        g["sample_loc_w"][0], g["sample_ray_dirs"][0])[0]
+    assert np.abs(f_eye - g["features"][0]).max() > 1e-3

@@ -51,3 +51,38 @@ def test_ray_march_grads_match_reference():
     (c * torch.from_numpy(gb["g_color"][0])).sum().backward()
     ref = gb["g_features"][0]
     np.testing.assert_allclose(rf.grad.numpy(), ref, atol=1e-6 + 1e-5 * np.abs(ref).max(), rtol=1e-4)
+
+
+def test_aggregate_grads_per_pair_rw2c():
+    # autograd of the reference's PointAggregator with a per-pair Rw2c (aggregator_rw2c.npz)
+    g = load("aggregator_rw2c.npz")
+    params = {k: torch.from_numpy(v) for k, v in formula_params(salt=0.3).items()}
+    t = {k: torch.from_numpy(np.ascontiguousarray(g[k][0])) for k in
+         ("sampled_color", "sampled_dir", "sampled_conf", "sampled_embedding", "sampled_xyz_pers",
+          "sampled_xyz", "sample_pnt_mask", "sample_loc", "sample_loc_w", "sample_ray_dirs", "sampled_Rw2c")}
+    for k in ("sampled_color", "sampled_dir", "sampled_conf", "sampled_embedding"):
+        t[k].requires_grad_(True)
+    out, _, _, _ = OG.aggregate(params, t["sampled_color"], t["sampled_dir"], t["sampled_conf"],
+                                t["sampled_embedding"], t["sampled_xyz_pers"], t["sampled_xyz"],
+                                t["sample_pnt_mask"], t["sample_loc"], t["sample_loc_w"], t["sample_ray_dirs"],
+                                rw2c=t["sampled_Rw2c"])
+    np.testing.assert_allclose(out.detach().numpy(), g["features"][0], atol=1e-6, rtol=1e-5)
+    (out * torch.from_numpy(g["g_feat"][0])).sum().backward()
+    for k in ("sampled_color", "sampled_dir", "sampled_conf", "sampled_embedding"):
+        ref = g["g_" + k][0]
+        np.testing.assert_allclose(t[k].grad.numpy(), ref, atol=1e-6 + 1e-5 * np.abs(ref).max(), rtol=1e-4,
+                                   err_msg=k)
+
+
+def test_ray_march_full_grads_match_reference():
+    # gradients of ray_features, ray_dist and bg_color for a loss on every ray_march output
+    g = load("raymarch_full_bwd.npz")
+    rd = torch.from_numpy(g["ray_dist"][0]).requires_grad_(True)
+    rf = torch.from_numpy(g["ray_features"][0]).requires_grad_(True)
+    bg = torch.from_numpy(g["bg_color"]).requires_grad_(True)
+    outs = OG.ray_march_full(rd, torch.from_numpy(g["ray_valid"][0]), rf, bg)
+    names = ("g_color", "g_opacity", "g_acc", "g_blend", "g_bgT")
+    loss = sum((o.reshape(g[n][0].shape) * torch.from_numpy(g[n][0])).sum() for o, n in zip(outs, names))
+    loss.backward()
+    for got, ref in ((rf.grad, g["d_features"][0]), (rd.grad, g["d_ray_dist"][0]), (bg.grad, g["d_bg"])):
+        np.testing.assert_allclose(got.numpy(), ref, atol=1e-6 + 1e-5 * np.abs(ref).max(), rtol=1e-4)

@@ -20,7 +20,7 @@ def main():
     a = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
-    ns = argparse.Namespace(points=a.points, config="headline", pairs_kernel="wt", dtype=a.precision)
+    ns = argparse.Namespace(points=a.points, config="headline", dtype=a.precision)
     opt, pts, feats, agg, model = bench.build_scene(ns, dev)
     model.precision = a.precision
     campos, camrot, rd = bench.cameras(1, a.hw, a.hw)[0]

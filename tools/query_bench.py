@@ -21,7 +21,7 @@ def main():
     a = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
-    opt, pts, feats, agg, model = bench.build_scene(argparse.Namespace(points=a.points, config="headline", pairs_kernel="wt", dtype="fp32h2"), dev)
+    opt, pts, feats, agg, model = bench.build_scene(argparse.Namespace(points=a.points, config="headline", dtype="fp32h2"), dev)
     q = model.neural_points.querier
     xyz = model.neural_points.xyz.detach()
     res = []
