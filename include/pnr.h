@@ -111,6 +111,30 @@ typedef struct {
 int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
                    const pnr_grid_params* p, void* stream);
 
+/* pnr_grid_build without a host read of the point bbox (training steps that
+ * move xyz, prune / grow: neural_points.py:350-402): get_hyperparameters
+ * (qpiw.py:48-81) runs on the device from the bbox -- min/max clipped to
+ * ranges and padded in fp32, dims = ceil((max - min) / vsize / vscale) in
+ * float64 as numpy promotes it -- so shift and dims equal the host formula's.
+ * The tables are allocated for dims_max (the dims of bbox = ranges, an upper
+ * bound); ranges must be set (min < max).  pnr_grid_geometry reads the exact
+ * shift / cell size / dims back (waits for the build). */
+typedef struct {
+  float ranges[6];      /* opt.ranges                                           */
+  float pad[3];         /* (vsize * vscale * kernel_size / 2) as get_hyperparameters rounds it (fp32) */
+  double vsize[3];      /* opt.vsize (Python floats)                            */
+  int32_t vscale[3];
+  float vsize_s[3];     /* fp32(vsize * vscale): the cell size                  */
+  int32_t dims_max[3];  /* dims of the bbox = ranges case                       */
+  int32_t query_size[3];
+  int32_t max_o;
+  int32_t P;
+  int32_t slot0_drop;
+  uint64_t seed;
+} pnr_grid_spec;
+int pnr_grid_build_dev(pnr_handle* h, const float* xyz_dev, int64_t n, const pnr_grid_spec* spec, void* stream);
+int pnr_grid_geometry(pnr_handle* h, float shift[3], float vsize[3], int32_t dims[3]);
+
 typedef struct {
   int64_t n_points_in_grid;   /* points whose voxel is inside dims            */
   int64_t n_voxels;           /* occupied voxels (before max_o truncation)    */
@@ -298,6 +322,10 @@ typedef struct {
   const float* rw2c;
   float neg_slope;
   int32_t act_super;
+  int32_t pair_buckets;  /* 1: the pairs stage runs each sample in a bucket of KT = 1, 2, 4 or 8
+                            neighbour slots (its last filled slot + 1; tiles of 128/KT samples x KT:
+                            sparse scenes skip the empty slots, point_aggregators.py:608-628's
+                            masked holders), same outputs; 0: every sample on 16 x 8 tiles */
 } pnr_mlp_bf16;
 
 int pnr_aggregate_scratch_bytes_bf16(int64_t n_max, int64_t n_points, size_t* out);

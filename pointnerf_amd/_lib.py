@@ -32,6 +32,13 @@ class GridParams(ctypes.Structure):
                 ("slot0_drop", c_int32), ("seed", ctypes.c_uint64)]
 
 
+class GridSpec(ctypes.Structure):
+    _fields_ = [("ranges", c_float * 6), ("pad", c_float * 3), ("vsize", ctypes.c_double * 3),
+                ("vscale", c_int32 * 3), ("vsize_s", c_float * 3), ("dims_max", c_int32 * 3),
+                ("query_size", c_int32 * 3), ("max_o", c_int32), ("P", c_int32), ("slot0_drop", c_int32),
+                ("seed", ctypes.c_uint64)]
+
+
 class GridStats(ctypes.Structure):
     _fields_ = [("n_points_in_grid", c_int64), ("n_voxels", c_int64), ("n_voxels_kept", c_int64),
                 ("n_points_dropped", c_int64), ("max_points_per_voxel", c_int32),
@@ -86,7 +93,7 @@ class NeuralRenderH2WT(ctypes.Structure):
 class MlpBf16(ctypes.Structure):
     _fields_ = [("w1af", c_void_p), ("w1bf", c_void_p), ("w2f", c_void_p), ("w3f", c_void_p), ("w4f", c_void_p),
                 ("wa", c_void_p), ("ba", c_void_p), ("wc1f", c_void_p), ("wc2f", c_void_p), ("wc3f", c_void_p),
-                ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32)]
+                ("rw2c", c_void_p), ("neg_slope", c_float), ("act_super", c_int32), ("pair_buckets", c_int32)]
 
 
 class Points(ctypes.Structure):
@@ -144,6 +151,8 @@ SIGNATURES = {
     "pnr_points_bbox": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_grid_build": (c_int, [c_void_p, c_void_p, c_int64, P(GridParams), c_void_p]),
     "pnr_grid_stats_get": (c_int, [c_void_p, P(GridStats)]),
+    "pnr_grid_build_dev": (c_int, [c_void_p, c_void_p, c_int64, P(GridSpec), c_void_p]),
+    "pnr_grid_geometry": (c_int, [c_void_p, P(c_float), P(c_float), P(c_int32)]),
     "pnr_grid_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_query_scratch_bytes": (c_int, [c_int64, c_int32, P(c_size_t)]),
     "pnr_query": (c_int, [c_void_p, P(Rays), P(QueryParams), P(QueryBufs), c_void_p]),

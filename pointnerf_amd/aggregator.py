@@ -295,6 +295,9 @@ class PointAggregator(nn.Module):
         self._packed = None
         self._packed_key = None
         self.register_buffer("rw2c", torch.eye(3), persistent=False)
+        # bf16 path: samples bucketed by filled neighbour slots (KT = 1/2/4/8 tiles; same
+        # outputs as 16 x 8 tiles, fewer empty MFMA columns on sparse scenes)
+        self.pair_buckets = True
 
     # ---------------------------------------------------------------- weights
     def packed(self) -> tuple[L.Mlp, dict]:
@@ -332,7 +335,8 @@ class PointAggregator(nn.Module):
     def packed_bf16(self) -> tuple[L.MlpBf16, dict]:
         """bf16 fragment packs for pnr_aggregate_fwd_bf16 (cached like packed())."""
         ps = list(self.parameters())
-        key = tuple((p.data_ptr(), p._version) for p in ps) + ((self.rw2c.data_ptr(), self.rw2c._version),)
+        key = tuple((p.data_ptr(), p._version) for p in ps) + ((self.rw2c.data_ptr(), self.rw2c._version),
+                                                                bool(self.pair_buckets))
         if getattr(self, "_packed16", None) is not None and key == self._packed16_key:
             return self._packed16
         with torch.no_grad():
@@ -350,6 +354,7 @@ class PointAggregator(nn.Module):
             setattr(m, k, v.data_ptr())
         m.neg_slope = float(self.neg_slope)
         m.act_super = self.act_super
+        m.pair_buckets = int(self.pair_buckets)
         self._packed16, self._packed16_key = (m, t), key
         return self._packed16
 

@@ -180,6 +180,25 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
 // f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
                         hipStream_t st);
+// Sample buckets by filled neighbour slots (buckets.hip): list = the sample
+// indices partitioned by bucket b (KT = 1 << b slots), bucket b at
+// [info[b], info[b] + info[4 + b]), in sample order within a bucket.
+struct PairBuckets {
+  int32_t* list;
+  int32_t* info;
+};
+int64_t bucket_scratch_ints(int64_t n_max);
+int launch_buckets(const pnr_samples& s, int32_t* scratch, PairBuckets* out, hipStream_t st);
+
+// xor-tree sum over the KT lanes of one sample (KT = 8: xor8_sum)
+template <int KT>
+__device__ __forceinline__ float xork_sum(float v) {
+  if constexpr (KT >= 2) v += __shfl_xor(v, 1);
+  if constexpr (KT >= 4) v += __shfl_xor(v, 2);
+  if constexpr (KT >= 8) v += __shfl_xor(v, 4);
+  return v;
+}
+
 // k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
 // color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],

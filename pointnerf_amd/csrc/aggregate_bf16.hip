@@ -207,24 +207,35 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 }
 
 // ---------------------------------------------------------------------------
-// k_pairs_b: gather + weights + PE_5 + the rest of block1, block3, alpha and
-// K-sums for 128 pairs per workgroup.
-constexpr int kBTS = kBT / kKN;   // samples per tile
-constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTS + 8 * kBT + kBT) * 4;
+// k_pairs_b<KT>: gather + weights + PE_5 + the rest of block1, block3, alpha and
+// K-sums for 128 pair columns per workgroup = 128 / KT samples x KT neighbour
+// slots (column = j KT + k).  KT = 8 with list == NULL: the samples 0..n-1 in
+// order, every slot (the unbucketed launch).  KT < 8: the samples of one bucket
+// of buckets.hip (list[0 .. *n_list)), whose slots >= KT are all empty -- the
+// outputs are the same numbers as the KT = 8 launch (the dropped slots carried
+// zero weights; the xor-tree and DPP reduce-scatter sums below pair the
+// remaining lanes exactly as the 8-lane trees do).
+constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
+constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT) * 4;
 
-__global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
+template <int KT>
+__global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const int32_t* bk_list, const int32_t* bk_info,
+                                                              int bucket) {
+  constexpr int SPT = kBT / KT;                            // samples per tile
   extern __shared__ __attribute__((aligned(16))) uint16_t xb_dyn[];
   uint16_t* Xb = xb_dyn;                                   // [128][kPB]
   float* wtL = reinterpret_cast<float*>(Xb + kBT * kPB);   // [128]
   float* apart = wtL + kBT;                                // [4][128]
-  int* sflag = reinterpret_cast<int*>(apart + 4 * kBT);    // [16]
-  float* exL = reinterpret_cast<float*>(sflag + kBTS);     // [8][128]
+  int* sflag = reinterpret_cast<int*>(apart + 4 * kBT);    // [SPT]
+  float* exL = reinterpret_cast<float*>(sflag + kBTSmax);  // [8][128]
   int* prowL = reinterpret_cast<int*>(exL + 8 * kBT);      // [128]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int K = A.s.K;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, kBTS);
+  // bucket samples list[0 .. n) (buckets.hip), or every sample in order
+  const int32_t* list = bk_list ? bk_list + bk_info[bucket] : nullptr;
+  const int64_t n = bk_list ? (int64_t)bk_info[4 + bucket] : eff_n(A.s);
+  const int64_t ntiles = cdiv(n, SPT);
   const float neg = A.w.neg_slope;
   float Rw[9];
 #pragma unroll
@@ -246,9 +257,10 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
     // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
     {
       const int col = threadIdx.x & (kBT - 1), role = threadIdx.x >> 7;
-      const int j = col >> 3, k = col & 7;
-      const int64_t v = tile * kBTS + j;
-      const bool active = v < n;
+      const int j = col / KT, k = col % KT;
+      const int64_t jv = tile * SPT + j;
+      const bool active = jv < n;
+      const int64_t v = active ? (list ? (int64_t)list[jv] : jv) : 0;
       const int64_t row = active ? sample_row(A.s, v) : 0;
       int64_t prow = -1;
       bool valid = false;
@@ -295,10 +307,10 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       d6[5] = pp[2] - sp[2];
       const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
       const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
-      const float wsum = xor8_sum(wl);
+      const float wsum = xork_sum<KT>(wl);
       const float wn = wl / fmaxf(wsum, 1e-8f);
       const float confc = fminf(fmaxf(cf, 1e-4f), 1.f);
-      const bool samp_valid = xor8_sum(valid ? 1.f : 0.f) > 0.f;
+      const bool samp_valid = xork_sum<KT>(valid ? 1.f : 0.f) > 0.f;
       float dr6[6];
       mat3(Rw, d6, dr6);
       dr6[3] = d6[3];
@@ -322,8 +334,21 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
         prowL[col] = valid ? (int)prow : -1;
         if (k == 0) sflag[j] = active && samp_valid;
         if (active && k < K) {
-          if (A.out_weight) A.out_weight[row * K + k] = wn;
-          if (A.out_conf) A.out_conf[row * K + k] = confc;
+          // the bucket's dropped slots (KT..K-1) are empty: weight 0, their gathered conf
+          if (A.out_weight) {
+            A.out_weight[row * K + k] = wn;
+            if (k == 0)
+              for (int kk = KT; kk < K; ++kk) A.out_weight[row * K + kk] = 0.f;
+          }
+          if (A.out_conf) {
+            A.out_conf[row * K + k] = confc;
+            if (k == 0)
+              for (int kk = KT; kk < K; ++kk) {
+                const int pid = A.s.pidx[row * K + kk];
+                const float c2 = A.pts.conf ? A.pts.conf[pid >= 0 ? pid : 0] : 1.f;
+                A.out_conf[row * K + kk] = fminf(fmaxf(c2, 1e-4f), 1.f);
+              }
+          }
         }
         *reinterpret_cast<uint2*>(Xb + col * kPB + 60) = make_uint2(0u, 0u);   // rows 60..63: k padding
       }
@@ -410,8 +435,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
     {
     float pa_part[kBPT] = {0.f, 0.f, 0.f, 0.f};
-    const int i8 = c & 7;
-    const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
+    const int ik = c % KT;   // the lane's slot within its sample
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
       float wa[16];
@@ -421,9 +445,10 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
       for (int pt = 0; pt < kBPT; ++pt) {
         const int col = 32 * pt + c;
         const float wtp = wtL[col];
-        const int sj = col >> 3;
-        const int64_t vo = tile * kBTS + sj;
-        const bool wr = vo < n && sflag[sj];
+        const int sj = col / KT;
+        const int64_t jv = tile * SPT + sj;
+        const bool wr = jv < n && sflag[sj];
+        const int64_t vo = wr ? (list ? (int64_t)list[jv] : jv) : 0;
         float vv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -431,31 +456,81 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
           pa_part[pt] += wa[r] * hv;
           vv[r] = wtp * hv;
         }
-        float w8[8], w4v[4], w2[2];
+        // K-sum of the sample's KT lanes as a DPP reduce-scatter: each lane keeps
+        // 16 / KT of the 16 accumulator rows (the 8-lane tree's pairing)
+        uint16_t* hrow = A.hid + vo * kHid + 32 * (T0 + T) + 4 * h;
+        if constexpr (KT == 8) {
+          const bool b2 = (ik & 4) != 0, b1 = (ik & 2) != 0, b0 = (ik & 1) != 0;
+          float w8[8], w4v[4], w2[2];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float send = b2 ? vv[q] : vv[q + 8];
-          const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x141,
-                                                                                0xf, 0xf, false));
-          w8[q] = (b2 ? vv[q + 8] : vv[q]) + recv;
-        }
+          for (int q = 0; q < 8; ++q) {
+            const float send = b2 ? vv[q] : vv[q + 8];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x141,
+                                                                                  0xf, 0xf, false));
+            w8[q] = (b2 ? vv[q + 8] : vv[q]) + recv;
+          }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float send = b1 ? w8[q] : w8[q + 4];
-          const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E,
-                                                                                0xf, 0xf, false));
-          w4v[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
-        }
+          for (int q = 0; q < 4; ++q) {
+            const float send = b1 ? w8[q] : w8[q + 4];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E,
+                                                                                  0xf, 0xf, false));
+            w4v[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
+          }
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const float send = b0 ? w4v[q] : w4v[q + 2];
-          const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
-                                                                                0xf, 0xf, false));
-          w2[q] = (b0 ? w4v[q + 2] : w4v[q]) + recv;
+          for (int q = 0; q < 2; ++q) {
+            const float send = b0 ? w4v[q] : w4v[q + 2];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
+                                                                                  0xf, 0xf, false));
+            w2[q] = (b0 ? w4v[q + 2] : w4v[q]) + recv;
+          }
+          if (wr) *reinterpret_cast<unsigned*>(hrow + ((2 * ik) & 3) + 8 * (ik >> 1)) = pack_bf16x2(w2[0], w2[1]);
+        } else if constexpr (KT == 4) {
+          // stages lane ^ 2, lane ^ 1: lane ik keeps registers 4 ik .. 4 ik + 3 = neurons 8 ik + q
+          const bool b1 = (ik & 2) != 0, b0 = (ik & 1) != 0;
+          float w8[8], w4v[4];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float send = b1 ? vv[q] : vv[q + 8];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E,
+                                                                                  0xf, 0xf, false));
+            w8[q] = (b1 ? vv[q + 8] : vv[q]) + recv;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float send = b0 ? w8[q] : w8[q + 4];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
+                                                                                  0xf, 0xf, false));
+            w4v[q] = (b0 ? w8[q + 4] : w8[q]) + recv;
+          }
+          if (wr)
+            *reinterpret_cast<uint2*>(hrow + 8 * ik) = make_uint2(pack_bf16x2(w4v[0], w4v[1]),
+                                                                  pack_bf16x2(w4v[2], w4v[3]));
+        } else if constexpr (KT == 2) {
+          // stage lane ^ 1: lane ik keeps registers 8 ik .. 8 ik + 7 = neurons 16 ik + {0..3, 8..11}
+          const bool b0 = (ik & 1) != 0;
+          float w8[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float send = b0 ? vv[q] : vv[q + 8];
+            const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
+                                                                                  0xf, 0xf, false));
+            w8[q] = (b0 ? vv[q + 8] : vv[q]) + recv;
+          }
+          if (wr) {
+            *reinterpret_cast<uint2*>(hrow + 16 * ik) = make_uint2(pack_bf16x2(w8[0], w8[1]),
+                                                                   pack_bf16x2(w8[2], w8[3]));
+            *reinterpret_cast<uint2*>(hrow + 16 * ik + 8) = make_uint2(pack_bf16x2(w8[4], w8[5]),
+                                                                       pack_bf16x2(w8[6], w8[7]));
+          }
+        } else {
+          // one slot: the lane's 16 registers are the sample's rows 8 g + 4 h + q
+          if (wr) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *reinterpret_cast<uint2*>(hrow + 8 * g) = make_uint2(pack_bf16x2(vv[4 * g], vv[4 * g + 1]),
+                                                                   pack_bf16x2(vv[4 * g + 2], vv[4 * g + 3]));
+          }
         }
-        if (wr)
-          *reinterpret_cast<unsigned*>(A.hid + vo * kHid + 32 * (T0 + T) + ((2 * i8) & 3) + 8 * (i8 >> 1) + 4 * h) =
-              pack_bf16x2(w2[0], w2[1]);
       }
     }
 #pragma unroll
@@ -467,12 +542,13 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A) {
     __syncthreads();
     if (wid < 2) {
       const int col = 64 * wid + lane;
-      const int j = col >> 3, k = col & 7;
+      const int j = col / KT, k = col % KT;
       const float pa = apart[col] + apart[kBT + col] + apart[2 * kBT + col] + apart[3 * kBT + col] + A.w.ba[0];
       const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
-      const float alpha_s = xor8_sum(wtL[col] * alpha_k);
-      const int64_t vo = tile * kBTS + j;
-      if (k == 0 && vo < n) {
+      const float alpha_s = xork_sum<KT>(wtL[col] * alpha_k);
+      const int64_t jv = tile * SPT + j;
+      if (k == 0 && jv < n) {
+        const int64_t vo = list ? (int64_t)list[jv] : jv;
         A.vmask[vo] = sflag[j];
         if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
       }
@@ -582,7 +658,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
 static size_t scratch_need_b(int64_t n_max, int64_t n_p1) {
   const int64_t nm = n_max > 0 ? n_max : 1;
   const int64_t np = n_p1 > 0 ? n_p1 : 1;
-  return (size_t)nm * kHid * 2 + (size_t)cdiv(nm, 4) * 16 + (size_t)np * kHid * 2;
+  // P1 | hid | vmask | pair buckets (buckets.hip)
+  return (size_t)nm * kHid * 2 + (size_t)cdiv(nm, 4) * 16 + (size_t)np * kHid * 2 +
+         (size_t)bucket_scratch_ints(nm) * 4;
 }
 
 }  // namespace pnr
@@ -617,8 +695,14 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre_b),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kBT * kPB * 2)));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<2>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<8>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_b), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kColorBLds));
     attr = true;
@@ -632,6 +716,7 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   a.p1 = static_cast<uint16_t*>(scratch);
   a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
   a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
+  int32_t* bk_scratch = a.vmask + cdiv(nm, 4) * 4;
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
@@ -640,8 +725,26 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
                        kBT * kPB * 2, st, a);
     PNR_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_pairs_b, dim3(grid_for(cdiv(nm, kBTS), 1, 256 * 2)), dim3(64 * kBWaves), kPairsBLds, st, a);
-  PNR_LAUNCH_CHECK();
+  if (w->pair_buckets) {
+    // samples partitioned by filled slots, one launch per bucket (the heaviest first)
+    PairBuckets bk;
+    int rc;
+    if ((rc = launch_buckets(a.s, bk_scratch, &bk, st))) return rc;
+    const unsigned g8 = grid_for(cdiv(nm, kBT / 8), 1, 256 * 2), g4 = grid_for(cdiv(nm, kBT / 4), 1, 256 * 2),
+                   g2 = grid_for(cdiv(nm, kBT / 2), 1, 256 * 2), g1 = grid_for(cdiv(nm, kBT), 1, 256 * 2);
+    hipLaunchKernelGGL(k_pairs_b<8>, dim3(g8), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 3);
+    PNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pairs_b<4>, dim3(g4), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 2);
+    PNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pairs_b<2>, dim3(g2), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 1);
+    PNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pairs_b<1>, dim3(g1), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 0);
+    PNR_LAUNCH_CHECK();
+  } else {
+    hipLaunchKernelGGL(k_pairs_b<8>, dim3(grid_for(cdiv(nm, kBT / 8), 1, 256 * 2)), dim3(64 * kBWaves), kPairsBLds,
+                       st, a, nullptr, nullptr, 3);
+    PNR_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(k_color_b, dim3(grid_for(cdiv(nm, kBT), 1, 256 * 2)), dim3(64 * kBWaves), kColorBLds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;

@@ -97,6 +97,51 @@ struct GridDev {
   uint64_t seed;
 };
 
+// the launch's by-value parameters with the geometry (shift, cell size, dims)
+// read from device memory (pnr_handle.geom)
+__device__ __forceinline__ GridDev with_geom(const GridDev& g0, const QGrid* __restrict__ geo) {
+  GridDev g = g0;
+  const QGrid G = *geo;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    g.shift[a] = G.shift[a];
+    g.vs[a] = G.vs[a];
+    g.dims[a] = G.dims[a];
+  }
+  return g;
+}
+
+// get_hyperparameters (qpiw.py:48-81) on the device from the point bbox, for a
+// build with opt.ranges set (no host read of the bbox): numpy's dtypes --
+// min/max clipped to ranges and padded in fp32, vdim = (max - min) / vsize in
+// float64 (vsize is a Python float list), dims = ceil(vdim / vscale) -- so shift
+// and dims are the host formula's bits.  dims are clamped to [1, the bound
+// the host allocated for].
+__global__ void k_grid_geom(const float* __restrict__ bbox, pnr_grid_spec sp, QGrid* __restrict__ geo) {
+  if (threadIdx.x != 0) return;
+  QGrid G;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float mn = fmaxf(bbox[a], sp.ranges[a]);
+    float mx = fminf(bbox[3 + a], sp.ranges[3 + a]);
+    mn = __fsub_rn(mn, sp.pad[a]);
+    mx = __fadd_rn(mx, sp.pad[a]);
+    const double vdim = __ddiv_rn((double)__fsub_rn(mx, mn), sp.vsize[a]);
+    double sd = ceil(__ddiv_rn(vdim, (double)sp.vscale[a]));
+    int d = sd >= 1.0 ? (int)sd : 1;
+    d = d < sp.dims_max[a] ? d : sp.dims_max[a];
+    G.shift[a] = mn;
+    G.vs[a] = sp.vsize_s[a];
+    G.dims[a] = d;
+  }
+  G.P = sp.P;
+  *geo = G;
+}
+
+__global__ void k_set_geom(QGrid G, QGrid* __restrict__ geo) {
+  if (threadIdx.x == 0) *geo = G;
+}
+
 __device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int c[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) c[a] = vox_coord(p[a], g.shift[a], g.vs[a]);
@@ -108,9 +153,10 @@ __device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int
 
 // claim_occ's voxel coordinate + first-claimer (qpiw.py:262-283), made
 // order-free: the claimer is the smallest point index of the voxel.
-__global__ void __launch_bounds__(kBlock) k_cells(const float* __restrict__ xyz, int64_t n, GridDev g,
-                                                  int64_t* __restrict__ pt_cell,
+__global__ void __launch_bounds__(kBlock) k_cells(const float* __restrict__ xyz, int64_t n, GridDev g0,
+                                                  const QGrid* __restrict__ geo, int64_t* __restrict__ pt_cell,
                                                   int32_t* __restrict__ first_pt, int32_t* counters) {
+  const GridDev g = with_geom(g0, geo);
   int in_grid = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -204,13 +250,14 @@ __global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, 
 
 // map_coor2occ (qpiw.py:305-340): slot -> coor_2_occ, dilation of the
 // occupancy by query_size (bitmap, atomicOr).
-__global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz, int64_t n, GridDev g,
-                                                  const int64_t* __restrict__ pt_cell,
+__global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz, int64_t n, GridDev g0,
+                                                  const QGrid* __restrict__ geo, const int64_t* __restrict__ pt_cell,
                                                   const int32_t* __restrict__ flag,
                                                   const int32_t* __restrict__ pt_slot,
                                                   int32_t* __restrict__ coor_2_occ,
                                                   int32_t* __restrict__ occ_2_coor,
                                                   uint8_t* __restrict__ occ_bytes) {
+  const GridDev g = with_geom(g0, geo);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (!flag[i]) continue;
@@ -368,9 +415,11 @@ __global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const
 // Voxels that hold >= 1 kept point (coor_2_occ >= 0 and occ_numpnts > 0: the
 // slot-0 voxel under slot0_drop and the truncated ones are skipped exactly as
 // the reference's loop `g < min(P, occ_numpnts)` skips them), one byte per cell.
-__global__ void __launch_bounds__(kBlock) k_mark_held(int n_slots, GridDev g, const int32_t* __restrict__ occ_numpnts,
+__global__ void __launch_bounds__(kBlock) k_mark_held(int n_slots, GridDev g0, const QGrid* __restrict__ geo,
+                                                      const int32_t* __restrict__ occ_numpnts,
                                                       const int32_t* __restrict__ occ_2_coor,
                                                       uint8_t* __restrict__ bytes) {
+  const GridDev g = with_geom(g0, geo);
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
     if (occ_numpnts[s] <= 0 || occ_2_coor[s * 3] < 0) continue;
     bytes[((int64_t)occ_2_coor[s * 3] * g.dims[1] + occ_2_coor[s * 3 + 1]) * g.dims[2] + occ_2_coor[s * 3 + 2]] = 1;
@@ -401,10 +450,12 @@ __global__ void __launch_bounds__(kBlock) k_word_rank(int64_t words, const int32
     qw[w].y = (uint32_t)wrank[w];
 }
 
-__global__ void __launch_bounds__(kBlock) k_rank_slots(int n_slots, GridDev g, const int32_t* __restrict__ occ_numpnts,
+__global__ void __launch_bounds__(kBlock) k_rank_slots(int n_slots, GridDev g0, const QGrid* __restrict__ geo,
+                                                       const int32_t* __restrict__ occ_numpnts,
                                                        const int32_t* __restrict__ occ_2_coor,
                                                        const uint2* __restrict__ qw, int32_t* __restrict__ rank_slot,
                                                        int32_t* __restrict__ rank_cnt) {
+  const GridDev g = with_geom(g0, geo);
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
     if (occ_numpnts[s] <= 0 || occ_2_coor[s * 3] < 0) continue;
     const int64_t cell =
@@ -445,17 +496,16 @@ extern "C" int pnr_points_bbox(const float* xyz_dev, int64_t n, float* out6_dev,
   return PNR_OK;
 }
 
-extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
-                              const pnr_grid_params* p, void* stream) {
-  PNR_CHECK_ARG(h && xyz_dev && p, "grid_build: null pointer");
+// The build proper (both entry points): p gives the allocation bounds (dims)
+// and the by-value parameters; the exact geometry is already in h->geom.
+static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const pnr_grid_params* p,
+                           hipStream_t st) {
   PNR_CHECK_ARG(n > 0 && n < (int64_t)1 << 31, "grid_build: point count %lld out of range", (long long)n);
   PNR_CHECK_ARG(p->dims[0] > 0 && p->dims[1] > 0 && p->dims[2] > 0, "grid_build: empty grid dims");
   PNR_CHECK_ARG(p->max_o > 0 && p->P > 0, "grid_build: max_o and P must be > 0");
   PNR_CHECK_ARG(p->vsize[0] > 0 && p->vsize[1] > 0 && p->vsize[2] > 0, "grid_build: vsize <= 0");
   const int64_t gvol = (int64_t)p->dims[0] * p->dims[1] * p->dims[2];
   PNR_CHECK_ARG(gvol < (int64_t)1 << 36, "grid_build: grid of %lld cells", (long long)gvol);
-  PNR_HIP(hipSetDevice(h->device));
-  hipStream_t st = as_stream(stream);
   int rc;
   const int64_t words = cdiv(gvol, 32);
   const int64_t cap_o = p->max_o;
@@ -485,6 +535,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   int32_t* pt_slot = h->pt_slot.as<int32_t>();
   int32_t* bucket = h->bucket.as<int32_t>();
   int32_t* counters = h->counters.as<int32_t>();
+  const QGrid* geo = h->geom.as<QGrid>();
 
   GridDev g;
   for (int a = 0; a < 3; ++a) {
@@ -506,7 +557,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   PNR_HIP(hipMemsetAsync(counters, 0, 8 * 4, st));
 
   const unsigned gp = grid_for(n, kBlock);
-  hipLaunchKernelGGL(k_cells, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, pt_cell, first_pt,
+  hipLaunchKernelGGL(k_cells, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, pt_cell, first_pt,
                      counters);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_first_flags, dim3(gp), dim3(kBlock), 0, st, n, pt_cell, first_pt, pt_flag);
@@ -536,7 +587,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   // dilated occupancy bytes (32 * words <= 4 * gvol bytes)
   uint8_t* occ_bytes = reinterpret_cast<uint8_t*>(first_pt);
   PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
-  hipLaunchKernelGGL(k_claim, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, pt_cell, pt_flag,
+  hipLaunchKernelGGL(k_claim, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, pt_cell, pt_flag,
                      pt_slot, coor_2_occ, occ_2_coor, occ_bytes);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, occ_bits);
@@ -560,7 +611,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
     int32_t* wcnt = h->q_wcnt.as<int32_t>();
     int32_t* wrank = h->first_pt.as<int32_t>() + words * 8;   // after the cell bytes (32 B per word)
     PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
-    hipLaunchKernelGGL(k_mark_held, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
+    hipLaunchKernelGGL(k_mark_held, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, geo,
                        occ_numpnts, occ_2_coor, occ_bytes);
     PNR_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pack_held, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, qw, wcnt);
@@ -569,7 +620,7 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
       return rc;
     hipLaunchKernelGGL(k_word_rank, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, words, wrank, qw);
     PNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_rank_slots, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
+    hipLaunchKernelGGL(k_rank_slots, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, geo,
                        occ_numpnts, occ_2_coor, qw, h->q_rank_slot.as<int32_t>(), h->q_rank_cnt.as<int32_t>());
     PNR_LAUNCH_CHECK();
     if ((rc = exclusive_scan(h->q_rank_cnt.as<int32_t>(), cap_o, counters + 4, h->q_rec_off.as<int32_t>(),
@@ -581,9 +632,11 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   }
 
   if (!h->host_cnt) PNR_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->host_cnt), 8 * sizeof(int32_t)));
+  if (!h->host_geom) PNR_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->host_geom), sizeof(QGrid)));
   if (!h->stats_ev) PNR_HIP(hipEventCreateWithFlags(&h->stats_ev, hipEventDisableTiming));
   if (h->stats_pending) PNR_HIP(hipEventSynchronize(h->stats_ev));   // the previous build's copy is done
   PNR_HIP(hipMemcpyAsync(h->host_cnt, counters, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  PNR_HIP(hipMemcpyAsync(h->host_geom, geo, sizeof(QGrid), hipMemcpyDeviceToHost, st));
   PNR_HIP(hipEventRecord(h->stats_ev, st));
   h->stats_pending = true;
   h->gp = *p;
@@ -591,6 +644,70 @@ extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
   h->n_points = n;
   for (int a = 0; a < 3; ++a) h->stats.dims[a] = p->dims[a];
   h->built = true;
+  return PNR_OK;
+}
+
+extern "C" int pnr_grid_build(pnr_handle* h, const float* xyz_dev, int64_t n,
+                              const pnr_grid_params* p, void* stream) {
+  PNR_CHECK_ARG(h && xyz_dev && p, "grid_build: null pointer");
+  PNR_HIP(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  int rc;
+  if ((rc = h->geom.ensure(sizeof(QGrid)))) return rc;
+  QGrid G;
+  for (int a = 0; a < 3; ++a) {
+    G.shift[a] = p->shift[a];
+    G.vs[a] = p->vsize[a];
+    G.dims[a] = p->dims[a];
+  }
+  G.P = p->P;
+  hipLaunchKernelGGL(k_set_geom, dim3(1), dim3(64), 0, st, G, h->geom.as<QGrid>());
+  PNR_LAUNCH_CHECK();
+  h->geom_on_device = false;
+  return grid_build_body(h, xyz_dev, n, p, st);
+}
+
+extern "C" int pnr_grid_build_dev(pnr_handle* h, const float* xyz_dev, int64_t n, const pnr_grid_spec* sp,
+                                  void* stream) {
+  PNR_CHECK_ARG(h && xyz_dev && sp, "grid_build_dev: null pointer");
+  PNR_CHECK_ARG(n > 0 && n < (int64_t)1 << 31, "grid_build_dev: point count %lld out of range", (long long)n);
+  for (int a = 0; a < 3; ++a) {
+    PNR_CHECK_ARG(sp->ranges[a] < sp->ranges[3 + a], "grid_build_dev: needs ranges (min < max)");
+    PNR_CHECK_ARG(sp->dims_max[a] > 0 && sp->vsize[a] > 0 && sp->vscale[a] > 0 && sp->vsize_s[a] > 0,
+                  "grid_build_dev: bad spec");
+  }
+  PNR_HIP(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  int rc;
+  if ((rc = h->geom.ensure(sizeof(QGrid))) || (rc = h->bbox.ensure(8 * sizeof(float)))) return rc;
+  // bbox -> geometry on the device (k_bbox's reduction, then get_hyperparameters)
+  if ((rc = pnr_points_bbox(xyz_dev, n, h->bbox.as<float>(), stream))) return rc;
+  hipLaunchKernelGGL(k_grid_geom, dim3(1), dim3(64), 0, st, h->bbox.as<float>(), *sp, h->geom.as<QGrid>());
+  PNR_LAUNCH_CHECK();
+  pnr_grid_params p{};
+  for (int a = 0; a < 3; ++a) {
+    p.shift[a] = sp->ranges[a] - sp->pad[a];   // unused by the kernels (geometry from h->geom)
+    p.vsize[a] = sp->vsize_s[a];
+    p.dims[a] = sp->dims_max[a];
+    p.query_size[a] = sp->query_size[a];
+  }
+  p.max_o = sp->max_o;
+  p.P = sp->P;
+  p.slot0_drop = sp->slot0_drop;
+  p.seed = sp->seed;
+  h->geom_on_device = true;
+  return grid_build_body(h, xyz_dev, n, &p, st);
+}
+
+extern "C" int pnr_grid_geometry(pnr_handle* h, float shift[3], float vsize[3], int32_t dims[3]) {
+  PNR_CHECK_ARG(h && h->built && h->host_geom, "grid_geometry: grid not built");
+  PNR_CHECK_ARG(shift && vsize && dims, "grid_geometry: null pointer");
+  PNR_HIP(hipEventSynchronize(h->stats_ev));
+  for (int a = 0; a < 3; ++a) {
+    shift[a] = h->host_geom->shift[a];
+    vsize[a] = h->host_geom->vs[a];
+    dims[a] = h->host_geom->dims[a];
+  }
   return PNR_OK;
 }
 
@@ -608,10 +725,16 @@ extern "C" int pnr_grid_export(pnr_handle* h, int32_t* coor_2_occ, uint32_t* occ
                                int32_t* occ_numpnts, int32_t* occ_2_pnts, void* stream) {
   PNR_CHECK_ARG(h && h->built, "grid_export: grid not built");
   hipStream_t st = as_stream(stream);
-  const int64_t words = cdiv(h->gvol, 32);
+  // the tables are laid out by the exact dims (pnr_grid_geometry: waits for the build)
+  float sh[3], vs[3];
+  int32_t dm[3];
+  int rc;
+  if ((rc = pnr_grid_geometry(h, sh, vs, dm))) return rc;
+  const int64_t gvol = (int64_t)dm[0] * dm[1] * dm[2];
+  const int64_t words = cdiv(gvol, 32);
   const int64_t cap_o = h->gp.max_o;
   if (coor_2_occ)
-    PNR_HIP(hipMemcpyAsync(coor_2_occ, h->coor_2_occ.p, h->gvol * 4, hipMemcpyDeviceToDevice, st));
+    PNR_HIP(hipMemcpyAsync(coor_2_occ, h->coor_2_occ.p, gvol * 4, hipMemcpyDeviceToDevice, st));
   if (occ_bits) PNR_HIP(hipMemcpyAsync(occ_bits, h->occ_bits.p, words * 4, hipMemcpyDeviceToDevice, st));
   if (occ_numpnts)
     PNR_HIP(hipMemcpyAsync(occ_numpnts, h->occ_numpnts.p, cap_o * 4, hipMemcpyDeviceToDevice, st));
@@ -635,6 +758,7 @@ extern "C" int pnr_grid_stats_get(pnr_handle* h, pnr_grid_stats* out) {
     h->stats.n_points_in_grid = cnt[1];
     h->stats.n_points_dropped = cnt[2];
     h->stats.max_points_per_voxel = cnt[3];
+    for (int a = 0; a < 3; ++a) h->stats.dims[a] = h->host_geom->dims[a];
     h->stats_pending = false;
   }
   *out = h->stats;

@@ -143,6 +143,15 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Grid geometry as the build and query kernels read it from device memory
+// (pnr_handle.geom): written by the host (pnr_grid_build) or derived from the
+// points' bbox on the device (pnr_grid_build_dev, no host sync).
+struct QGrid {
+  float shift[3], vs[3];
+  int dims[3];
+  int P;
+};
+
 // Persistent grid tables owned by a handle (built by pnr_grid_build).
 struct pnr_handle {
   int device = 0;
@@ -173,6 +182,10 @@ struct pnr_handle {
   DevBuf q_rank_cnt;      // int32 [max_o]   min(P, points) of rank r (scratch)
   DevBuf q_rec_off;       // int32 [max_o+1] first record of rank r (exclusive scan of q_rank_cnt)
   DevBuf q_recs;          // float4 [N]      {x, y, z, bitcast(id)} in rank order, per voxel ascending id
+  DevBuf geom;            // QGrid of the built grid (device)
+  DevBuf bbox;            // float [8] point bbox of the last pnr_grid_build_dev
+  QGrid* host_geom = nullptr;   // pinned copy of geom behind stats_ev
+  bool geom_on_device = false;  // gp.shift / dims are bounds, the exact geometry is geom (device)
   int64_t n_points = 0;
   pnr_grid_stats stats{};
   bool built = false;
@@ -183,6 +196,8 @@ struct pnr_handle {
   bool stats_pending = false;
   void release_all() {
     if (host_cnt) (void)hipHostFree(host_cnt);
+    if (host_geom) (void)hipHostFree(host_geom);
+    host_geom = nullptr;
     if (stats_ev) (void)hipEventDestroy(stats_ev);
     host_cnt = nullptr;
     stats_ev = nullptr;
@@ -190,7 +205,7 @@ struct pnr_handle {
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &first_pt, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &slot_cursor, &slot_off, &pt_cell, &pt_flag, &pt_slot, &bucket,
                      &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
-                     &q_rec_off, &q_recs};
+                     &q_rec_off, &q_recs, &geom, &bbox};
     for (DevBuf* b : all) b->release();
   }
 };

@@ -27,12 +27,6 @@ constexpr int kQBlock = 256;
 constexpr int kKnnBatch = 1, kKnnBatchSmall = 2;
 constexpr unsigned kKnnGrid = 2048;
 
-struct QGrid {
-  float shift[3], vs[3];
-  int dims[3];
-  int P;
-};
-
 struct QRays {
   const float* campos;
   const float* camrot;
@@ -79,10 +73,11 @@ constexpr int64_t kMarchCoopRays = 32768;
 constexpr int kMarchLanes = 8;
 constexpr unsigned kMarchGridCap = 1u << 20;
 template <int G>
-__global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, QGrid g, int SR,
+__global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __restrict__ gq, int SR,
                                                         const uint32_t* __restrict__ occ_bits,
                                                         int32_t* __restrict__ n_filled,
                                                         uint16_t* __restrict__ slot_d) {
+  const QGrid g = *gq;
   const int lane = threadIdx.x & 63, gl = lane & (G - 1);
   for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G; r < q.R;
        r += ((int64_t)gridDim.x * blockDim.x) / G) {
@@ -330,7 +325,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 // LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
 // layered loop inlined beside it costs registers); 0: any layer count.
 template <int KMAX, int LAYERS, int KB>
-__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8))) k_knn(QRays q, QGrid g, int SR, int K, int layers, float r2,
+__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
@@ -338,6 +333,7 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8)
                                                  float* __restrict__ sample_w,
                                                  float* __restrict__ sample_p, int32_t* counts, int vec_pidx,
                                                  int32_t* __restrict__ xcd_ctr) {
+  const QGrid g = *gq;
   const int64_t S = counts[0];
   float c[3], Rm[9];
   load_cam(q, 0, c, Rm);
@@ -559,13 +555,9 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   PNR_CHECK_ARG(b->scratch_bytes >= std::max<size_t>(scan_scratch_bytes(RS + 1), 64), "query: scratch too small");
   hipStream_t st = as_stream(stream);
   QRays q = to_qrays(rays);
-  QGrid g;
-  for (int a = 0; a < 3; ++a) {
-    g.shift[a] = h->gp.shift[a];
-    g.vs[a] = h->gp.vsize[a];
-    g.dims[a] = h->gp.dims[a];
-  }
-  g.P = h->gp.P;
+  // the grid's exact geometry lives on the device (h->geom); h->gp.dims bounds it
+  const QGrid* g_dev = h->geom.as<QGrid>();
+  const int* gdims = h->gp.dims;
   PNR_HIP(hipMemsetAsync(b->counts, 0, 8 * sizeof(int32_t), st));
   PNR_HIP(hipMemsetAsync(b->ray_vcnt, 0, (size_t)(R > 0 ? R : 1) * sizeof(int32_t), st));
   if (R == 0) {
@@ -575,11 +567,11 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
     return PNR_OK;
   }
   if (R <= kMarchCoopRays)   // few rays: 16 lanes per ray (latency)
-    hipLaunchKernelGGL(k_march_coop<16>, dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g, qp->SR,
+    hipLaunchKernelGGL(k_march_coop<16>, dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g_dev, qp->SR,
                        h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   else
     hipLaunchKernelGGL(k_march_coop<kMarchLanes>, dim3(grid_for(R * kMarchLanes, kQBlock, kMarchGridCap)),
-                       dim3(kQBlock), 0, st, q, g, qp->SR, h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
+                       dim3(kQBlock), 0, st, q, g_dev, qp->SR, h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   PNR_LAUNCH_CHECK();
   if ((rc = exclusive_scan(b->n_filled, R, nullptr, b->ray_off, b->counts + 0, b->scratch,
                            b->scratch_bytes, st)))
@@ -592,7 +584,7 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   // chip holds, so more records in flight per lane
   const bool small = RS < (int64_t(4) << 20);
   // the 3x3x3 kernel indexes cells in 32 bits
-  const bool q3 = layers == 2 && (int64_t)g.dims[0] * g.dims[1] * g.dims[2] < (int64_t(1) << 32);
+  const bool q3 = layers == 2 && (int64_t)gdims[0] * gdims[1] * gdims[2] < (int64_t(1) << 32);
   unsigned gk = grid_for(RS, kQBlock, kKnnGrid);
   if (gk >= 8) gk &= ~7u;   // whole XCD groups (k_knn's chunk walk)
   // k_knn's per-XCD chunk counters: the head of the scan scratch, free between
@@ -605,7 +597,7 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   qi.recs = h->q_recs.as<float4>();
 #define PNR_KNN(KM)                                                                              \
   hipLaunchKernelGGL((q3 ? (small ? k_knn<KM, 2, kKnnBatchSmall> : k_knn<KM, 2, kKnnBatch>)           \
-                          : k_knn<KM, 0, kKnnBatchSmall>), dim3(gk), dim3(kQBlock), 0, st, q, g, qp->SR, qp->K, layers,      \
+                          : k_knn<KM, 0, kKnnBatchSmall>), dim3(gk), dim3(kQBlock), 0, st, q, g_dev, qp->SR, qp->K, layers,      \
                      qp->radius_limit2, qi, b->slot_d, b->fill_rs, b->pidx, b->vflag,             \
                      b->ray_vcnt, b->sample_w, b->sample_p, b->counts, vec,                       \
                      reinterpret_cast<int32_t*>(b->scratch))

@@ -68,6 +68,60 @@ def hyperparameters_from_bbox(opt, min_xyz: np.ndarray, max_xyz: np.ndarray):
                 radius_limit2=np.float32(radius_limit_np ** 2), vsize=vsize_np, vscale=vscale_np)
 
 
+class GridHP(dict):
+    """get_hyperparameters' dict for a grid built on the device
+    (pnr_grid_build_dev): the point-independent entries are host values, the
+    bbox-derived ones (shift, dims, ranges) are read back from the device
+    geometry on first access (one wait for the build)."""
+
+    def __init__(self, handle, base):
+        super().__init__(base)
+        self._handle = handle
+
+    def __missing__(self, key):
+        if key not in ("shift", "dims", "ranges"):
+            raise KeyError(key)
+        sh, vs, dm = (L.c_float * 3)(), (L.c_float * 3)(), (L.c_int32 * 3)()
+        L.check(L.lib().pnr_grid_geometry(self._handle.h, sh, vs, dm), "pnr_grid_geometry")
+        shift = np.array(list(sh), np.float32)
+        dims = np.array(list(dm), np.int32)
+        # ranges_np = [min - pad, max + pad]: the min half is the shift; the max half is
+        # the clipped bbox max + pad (bbox read once here, off the hot path)
+        mx = np.asarray(self._handle.bbox_max(), np.float32)
+        ranges = np.asarray(self["opt_ranges"], np.float32)
+        mx = (np.minimum(mx, ranges[3:]) + self["pad"]).astype(np.float32)
+        self.update(shift=shift, dims=dims, ranges=np.concatenate([shift, mx]).astype(np.float32))
+        return dict.__getitem__(self, key)
+
+
+def grid_spec(opt):
+    """The point-independent half of get_hyperparameters (qpiw.py:48-81) as
+    pnr_grid_spec, plus the host dict entries; None when opt.ranges is unset
+    (the bbox then decides the extent: host path)."""
+    ranges = opt.ranges
+    if ranges is None or ranges[0] >= ranges[3]:
+        return None, None
+    vsize_np = opt.vsize
+    vscale_np = np.array(opt.vscale, dtype=np.int32)
+    scaled_vsize_np = (vsize_np * vscale_np).astype(np.float32)
+    pad = (scaled_vsize_np * opt.kernel_size / 2).astype(np.float32)
+    hp_max = hyperparameters_from_bbox(opt, np.asarray(ranges[:3], np.float32), np.asarray(ranges[3:], np.float32))
+    sp = L.GridSpec()
+    sp.ranges[:] = [float(x) for x in np.asarray(ranges, np.float32)]
+    sp.pad[:] = [float(x) for x in pad]
+    sp.vsize[:] = [float(x) for x in vsize_np]
+    sp.vscale[:] = [int(x) for x in vscale_np]
+    sp.vsize_s[:] = [float(x) for x in scaled_vsize_np]
+    sp.dims_max[:] = [int(x) for x in hp_max["dims"]]
+    sp.query_size[:] = [int(x) for x in opt.query_size]
+    sp.max_o, sp.P = int(opt.max_o), int(opt.P)
+    sp.slot0_drop = int(getattr(opt, "slot0_drop", 1))
+    sp.seed = int(getattr(opt, "grid_seed", 0))
+    base = {k: v for k, v in hp_max.items() if k not in ("shift", "dims", "ranges")}
+    base.update(pad=pad, opt_ranges=np.asarray(ranges, np.float32))
+    return sp, base
+
+
 class QueryBuffers:
     """Caller-owned device buffers of pnr_query (torch allocations)."""
 
@@ -139,6 +193,10 @@ class GridHandle:
         b = out.cpu().numpy()
         return b[:3], b[3:]
 
+    def bbox_max(self):
+        """Max corner of the last built cloud's bbox (host read; GridHP's ranges)."""
+        return self.bbox(self._xyz)[1]
+
     def build(self, opt, xyz: torch.Tensor, force: bool = False):
         """get_hyperparameters + build_occ_vox; skipped when the point tensor is
         unchanged (same storage, same version counter)."""
@@ -153,6 +211,16 @@ class GridHandle:
                int(getattr(opt, "slot0_drop", 1)), int(getattr(opt, "grid_seed", 0)), policy)
         if not force and key == self.key:
             return self.hp
+        sp, base = grid_spec(opt) if policy == "reservoir" else (None, None)
+        if sp is not None and not getattr(opt, "grid_host_bbox", False):
+            # no host sync: bbox -> get_hyperparameters -> build, all on the device
+            L.check(L.lib().pnr_grid_build_dev(self.h, L.ptr(xyz), xyz.shape[0], L.ctypes.byref(sp),
+                                               L.stream_ptr(xyz.device)), "pnr_grid_build_dev")
+            hp = GridHP(self, base)
+            self._xyz = xyz
+            self.key, self.hp = key, hp
+            self._max_o, self._P = int(sp.max_o), int(opt.P)
+            return hp
         mn, mx = self.bbox(xyz)
         hp = hyperparameters_from_bbox(opt, mn, mx)
         gp = L.GridParams()

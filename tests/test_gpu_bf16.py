@@ -94,3 +94,47 @@ def test_bf16_render_vs_oracle(cuda):
     x, y = c.cpu().numpy(), ref["coarse_raycolor"]
     psnr = 10 * np.log10(float(np.abs(y).max()) ** 2 / max(float(np.mean((x - y) ** 2)), 1e-30))
     assert psnr >= 40.0, psnr
+
+
+@pytest.mark.parametrize("flags", ["truck", "lego"])
+def test_bf16_pair_buckets_equal_unbucketed(cuda, flags):
+    """pair_buckets (samples on KT = 1/2/4/8-slot tiles by their last filled
+    neighbour slot, buckets.hip) computes the same numbers as the 16 x 8 tiles:
+    features, out_weight and out_conf bitwise equal -- on a truck-flag scene
+    (~2 neighbours per sample, every bucket populated) and a lego one."""
+    from pointnerf_amd import _lib as L
+    from scenes import flag_scene
+    sc = flag_scene(flags, n_points=60000 if flags == "truck" else 30000, H=64, view=0)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.6))
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda).contiguous()
+    bufs, hp, rays, qp = np_.querier.run(np_.xyz.detach(), rd, cp, cr, sc["near"], sc["far"])
+    cnt = bufs.read_counts()
+    Sv, K = cnt["S_valid"], sc["opt"].K
+    assert Sv > 1000
+    s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
+                  bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(), bufs.fill_rs.data_ptr(),
+                  sc["opt"].SR, K)
+    pts, keep = np_.tables(cp, cr)
+    outs = []
+    for bk in (False, True):
+        agg.pair_buckets = bk
+        mlp16, _k = agg.packed_bf16()
+        f = torch.full((Sv, 129), float("nan"), device=cuda)
+        rows = bufs.pidx.numel() // K
+        w = torch.full((rows, K), -1.0, device=cuda)
+        c = torch.full((rows, K), -1.0, device=cuda)
+        scr = L.aggregate_scratch_bf16(Sv, pts.n, cuda)
+        L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp16),
+                                               L.ptr(f), L.ptr(w), L.ptr(c), L.ptr(scr), scr.numel() * 4,
+                                               L.stream_ptr(cuda)), "bf16")
+        outs.append((f, w, c))
+    torch.cuda.synchronize()
+    (f0, w0, c0), (f1, w1, c1) = outs
+    assert torch.equal(torch.nan_to_num(f0, nan=7.0), torch.nan_to_num(f1, nan=7.0))
+    assert torch.equal(w0, w1) and torch.equal(c0, c1)
+    # the scene exercises the small buckets
+    pidx = bufs.pidx[:cnt["S_filled"] * K].view(-1, K)
+    need = ((pidx >= 0) * torch.arange(1, K + 1, device=cuda)).amax(1)
+    if flags == "truck":
+        assert int((need <= 1).sum()) > 100 and int(((need > 2) & (need <= 4)).sum()) > 100

@@ -170,3 +170,38 @@ def test_used_points_device_equals_torch(cuda):
     assert c["n_used"] == u_ref.numel() > 100
     assert torch.equal(used_buf[: c["n_used"]], u_ref)
     assert torch.equal(used_map, m_ref)
+
+
+@pytest.mark.parametrize("case", ["inside", "crossing", "shifted"])
+def test_device_geometry_equals_host(cuda, case):
+    """pnr_grid_build_dev (get_hyperparameters on the device, no host read of the
+    bbox) gives the host formula's shift / dims bits and the same tables and query
+    as the host-geometry build -- for a cloud inside the ranges, one crossing
+    them (clipped) and one in a corner (dims well below the allocation bound)."""
+    from types import SimpleNamespace
+    sc = scene(20000, H=24, W=24, theta=70.0)
+    xyz = sc["xyz"].copy()
+    if case == "crossing":
+        xyz[::7] *= 1.6
+    elif case == "shifted":
+        xyz = (xyz * 0.4 + np.array([0.35, 0.6, 0.6], np.float32)).astype(np.float32)
+    sc["xyz"] = xyz
+    q_dev = _engine(sc, cuda)
+    opt_host = SimpleNamespace(**{**vars(sc["opt"]), "grid_host_bbox": True})
+    from pointnerf_amd.querier import lighting_fast_querier
+    q_host = lighting_fast_querier(cuda, opt_host)
+    t = torch.from_numpy(xyz).to(cuda)
+    hp_d = q_dev.grid.build(sc["opt"], t)
+    assert type(hp_d).__name__ == "GridHP"
+    hp_h = q_host.grid.build(opt_host, t)
+    g = O.grid_build(sc["opt"], xyz)
+    for k in ("shift", "dims", "ranges"):
+        assert np.array_equal(np.asarray(hp_d[k]), np.asarray(hp_h[k])), k
+        assert np.array_equal(np.asarray(hp_d[k]), np.asarray(g["hp"][k])), k
+    td, th = q_dev.grid.export(), q_host.grid.export()
+    for k in td:
+        assert torch.equal(td[k], th[k]), k
+    _, od = _run(sc, cuda, q_dev)
+    _, oh = _run(sc, cuda, q_host)
+    for a, b in zip(od[:5], oh[:5]):
+        assert torch.equal(a, b)
