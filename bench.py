@@ -403,7 +403,7 @@ def run_train(args, device):
             loss = loss + 1e-4 * model.zero_one_conf_loss()
         loss.backward()
         if reducer is not None:
-            reducer.reduce(model.last_train_aux["touched_rows"])
+            reducer.reduce(model.last_train_aux["touched_rows"], model.last_train_aux["touched_count"])
         optim.step()
         if timed:
             c = model.last_counts

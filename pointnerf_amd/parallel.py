@@ -198,6 +198,7 @@ class GradReducer:
         self.dense = [p for p in dense_params if p.requires_grad]
         self.points = [p for p in point_params if p is not None and p.requires_grad]
         self.group = group
+        self._host_group = None   # gloo group for host-side integers (no device sync)
         # point tables as [rows, channels] (the reference keeps them [1, N, C])
         if self.points:
             n = self.points[0].numel() // self.points[0].shape[-1]
@@ -222,9 +223,29 @@ class GradReducer:
         dist.all_gather(lst, t.contiguous(), group=self.group)
         return torch.stack(lst)
 
-    def reduce(self, touched: torch.Tensor | None = None):
+    def _max_over_ranks(self, v: int) -> int:
+        """max of a host integer over the ranks, on the CPU (gloo): the padding
+        size of the row all-gather without a device -> host copy."""
+        import torch.distributed as dist
+        if dist.get_backend(self.group) == "gloo":
+            g = self.group
+        else:
+            if self._host_group is None:
+                ranks = None if self.group is None else dist.get_process_group_ranks(self.group)
+                self._host_group = dist.new_group(ranks=ranks, backend="gloo")
+            g = self._host_group
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+        return int(t.item())
+
+    def reduce(self, touched: torch.Tensor | None = None, count: int | None = None):
         """touched: this rank's point rows with a (possibly) non-zero gradient
-        (any integer dtype, duplicates allowed); None = every row (dense)."""
+        (any integer dtype); None = every row (dense).  With ``count`` (host
+        int = touched.numel()) the rows must be unique, -1 entries ignored --
+        what render_rays_train's last_train_aux["touched_rows"] holds -- and the
+        reduction never reads a device value on the host (the padding size is a
+        max over ranks of the host counts, on gloo); without it duplicates are
+        allowed (torch.unique, one sync)."""
         import torch.distributed as dist
         world = dist.get_world_size(self.group)
         if world == 1:
@@ -244,22 +265,28 @@ class GradReducer:
         n = self.points[0].numel() // self.points[0].shape[-1]
         if touched is None:
             rows = torch.arange(n, device=dev)
-        else:
+            count = n
+        elif count is None:
             rows = torch.unique(touched.to(device=dev, dtype=torch.int64))
+            count = rows.numel()
+        else:
+            rows = touched.to(device=dev, dtype=torch.int64).reshape(-1)
+            if rows.numel() != count:
+                raise ValueError(f"GradReducer.reduce: count {count} != touched.numel() {rows.numel()}")
         widths = [p.shape[-1] for p in self.points]
-        m = torch.tensor([rows.numel()], dtype=torch.int64, device=dev)
-        counts = self._all_gather(m).reshape(-1).cpu()
-        mx = int(counts.max())
+        mx = self._max_over_ranks(count)
         ids = torch.full((mx,), -1, dtype=torch.int64, device=dev)
-        ids[:rows.numel()] = rows
+        ids[:count] = rows
         vals = torch.zeros((mx, sum(widths)), dtype=self.points[0].dtype, device=dev)
-        if rows.numel():
-            vals[:rows.numel()] = torch.cat([self._grad(p).reshape(n, -1)[rows] for p in self.points], 1)
+        if count:
+            # -1 entries gather row 0 and are zeroed: padding adds exact zeros
+            src = rows.clamp(min=0)
+            vals[:count] = torch.cat([self._grad(p).reshape(n, -1)[src] for p in self.points], 1)
+            vals[:count] *= (rows >= 0).to(vals.dtype)[:, None]
         all_ids = self._all_gather(ids)      # [world, mx]
         all_vals = self._all_gather(vals)    # [world, mx, D]
-        keep = all_ids.reshape(-1) >= 0
-        sel = all_ids.reshape(-1)[keep]
-        v = all_vals.reshape(-1, sum(widths))[keep].div_(world)
+        sel = all_ids.reshape(-1).clamp(min=0)
+        v = all_vals.reshape(-1, sum(widths)).div_(world)
         o = 0
         for p, w in zip(self.points, widths):
             g = self._grad(p).reshape(n, w)

@@ -658,7 +658,13 @@ class NeuralPointsRayMarching(nn.Module):
         # rows of the point table this batch can give a gradient: the referenced
         # points, and point 0 (empty slots gather it in conf_coefficient) --
         # parallel.GradReducer reduces only these across ranks
-        self.last_train_aux = {"touched_rows": torch.cat([used[0].long(), torch.zeros(1, dtype=torch.long, device=dev)])}
+        # (unique: pnr_used_points lists each referenced point once, ascending; the
+        # appended point 0 is dropped (-1) when it is already referenced)
+        u = used[0].long()
+        zero = torch.zeros(1, dtype=torch.long, device=dev)
+        if u.numel():
+            zero = torch.where(u[:1] == 0, zero - 1, zero)
+        self.last_train_aux = {"touched_rows": torch.cat([u, zero]), "touched_count": int(u.numel()) + 1}
         if self.keep_train_saved:
             self.last_train_aux["saved"] = spec.saved
         if np_.points_conf is not None or self.wants_aux():

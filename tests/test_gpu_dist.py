@@ -138,7 +138,7 @@ def _train_worker(rank, world, port, q):
         npt = m.neural_points
         red = GradReducer(list(m.aggregator.parameters()),
                           [npt.points_embeding, npt.points_color, npt.points_dir, npt.points_conf])
-        red.reduce(m.last_train_aux["touched_rows"])
+        red.reduce(m.last_train_aux["touched_rows"], m.last_train_aux["touched_count"])
         if rank == 0:
             # one process, all rays: the mean of the ranks' losses
             _, ref = grads(_train_model(sc, cuda, params), torch.arange(rd.shape[0], device=cuda), 1.0 / world)

@@ -27,7 +27,7 @@ def _data(rank):
     return dense, [emb, col, conf], touched
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="dup"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -38,7 +38,12 @@ def _worker(rank, world, port, q):
         points = [torch.nn.Parameter(torch.zeros_like(t)) for t in point_g]
         for p, g in zip(dense + points, dense_g + point_g):
             p.grad = g.clone()
-        GradReducer(dense, points).reduce(touched)
+        if mode == "count":
+            # render_rays_train's form: unique rows, -1 placeholders, the count on the host
+            rows = torch.cat([torch.unique(touched), torch.tensor([-1, -1])])
+            GradReducer(dense, points).reduce(rows, rows.numel())
+        else:
+            GradReducer(dense, points).reduce(touched)
         # DDP's reference: the dense mean over ranks
         ref = [sum(_data(r)[0][i] for r in range(world)) / world for i in range(2)]
         refp = [sum(_data(r)[1][i] for r in range(world)) / world for i in range(3)]
@@ -57,12 +62,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_grad_reducer_equals_dense_mean(world):
+@pytest.mark.parametrize("world,mode", [(2, "dup"), (3, "dup"), (2, "count"), (3, "count")])
+def test_grad_reducer_equals_dense_mean(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
