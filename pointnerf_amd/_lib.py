@@ -346,7 +346,7 @@ def weighted_colsum(w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """out[c] = sum_r w[r] x[r, c] on pnr_weighted_colsum (deterministic): the
     background colour's gradient from d ray_color and is_bg / bg_T."""
     w = w.reshape(-1).float().contiguous()
-    x = x.reshape(w.numel(), -1).float().contiguous()
+    x = x.reshape(w.numel(), x.shape[-1]).float().contiguous()
     C = x.shape[1]
     n = ctypes.c_int64(0)
     check(lib().pnr_weighted_colsum_scratch_floats(C, ctypes.byref(n)), "pnr_weighted_colsum_scratch_floats")

@@ -154,6 +154,20 @@ class _RenderState:
         self.scratch = None
         self.scratch_key = None
         self.side = None   # fp32h2: the side stream P1 runs on
+        self.feat = None   # decoded features [rows, 129], reused by every call on this stream
+
+    def feat_rows(self, rows: int, dev) -> torch.Tensor:
+        """[rows, 129] view of the persistent feature buffer.  The calls of one
+        stream use it in stream order (a call's composite reads it before the
+        next call's aggregate writes it), so it is allocated once and grown by
+        1.5x: a multi-GB allocation inside a frame stalls the launch queue
+        (c5: 20 GB per frame)."""
+        rows = max(int(rows), 1)
+        if self.feat is None or self.feat.shape[0] < rows or self.feat.device != dev:
+            old = 0 if self.feat is None else self.feat.shape[0]
+            self.feat = None
+            self.feat = torch.empty((max(rows, int(1.5 * old)), 129), dtype=torch.float32, device=dev)
+        return self.feat[:rows]
 
 
 def _counts_dict(c):
@@ -162,6 +176,9 @@ def _counts_dict(c):
     return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand)
 
 
+# The default is fp32h2, the measured headline path (fp32-accurate: the same
+# render tolerance as fp32, tests/test_gpu_x3.py; an activation beyond f16's range
+# re-renders the call on fp32x3).
 # fp32: the reference's arithmetic on v_mfma_f32_32x32x2_f32.  fp32x3: the same
 # fp32 GEMMs as exact 3-way bf16 splits on v_mfma_f32_32x32x16_bf16 (six cross
 # products, fp32-accurate; pnr_aggregate_fwd_x3).  fp32h2: the same GEMMs as 2-way
@@ -174,7 +191,7 @@ class NeuralPointsRayMarching(nn.Module):
     """neural_points_volumetric_model.NeuralPointsRayMarching, fused HIP path."""
 
     def __init__(self, opt, neural_points: NeuralPoints, aggregator: PointAggregator | None = None,
-                 chunk_rays: int | None = None, precision: str = "fp32"):
+                 chunk_rays: int | None = None, precision: str = "fp32h2"):
         super().__init__()
         if precision not in PRECISIONS:
             raise L.PnrError(f"precision {precision!r}: one of {PRECISIONS}")
@@ -511,7 +528,7 @@ class NeuralPointsRayMarching(nn.Module):
             else:
                 Sv = min(int((r1 - r0) * capacity) + 1024, (r1 - r0) * SR)
                 rec["caps"].append((Sv, r1 - r0))
-            feat = torch.empty((max(Sv, 1), 129), **f32)
+            feat = state.feat_rows(Sv, dev)
             s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K, L.ptr(rc))
@@ -588,7 +605,11 @@ class NeuralPointsRayMarching(nn.Module):
         L.check(fn(int(n_max), int(n_points), L.ctypes.byref(nb)), "aggregate scratch bytes")
         buf = state.scratch
         if buf is None or buf.device != dev or buf.numel() * 4 < int(nb.value):
-            buf = need(int(n_max * 1.25) + 1024, n_points, dev)   # headroom: n_max varies per batch
+            # headroom (n_max varies per batch) and geometric growth: no allocation per frame
+            rows = max(int(n_max * 1.5) + 1024, int(1.5 * getattr(state, "scratch_rows", 0)))
+            state.scratch = buf = None
+            buf = need(rows, n_points, dev)
+            state.scratch_rows = rows
             state.scratch = buf
             state.scratch_key = None
         ready = reuse and state.scratch_key == key

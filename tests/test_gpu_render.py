@@ -30,7 +30,7 @@ def _renderer(sc, cuda, params, chunk=None):
     agg.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
                        torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]))
-    return NeuralPointsRayMarching(sc["opt"], np_, agg.eval(), chunk_rays=chunk)
+    return NeuralPointsRayMarching(sc["opt"], np_, agg.eval(), chunk_rays=chunk, precision="fp32")
 
 
 def _forward(m, sc, cuda):

@@ -17,7 +17,8 @@ import sys
 AGG_BY_DTYPE = {"fp32": ("k_point_pre", "k_pairs", "k_color"),
                 "fp32x3": ("k_point_pre", "k_pairs_x3", "k_color"),
                 "fp32h2": ("k_point_pre_h2", "k_pairs_h2", "k_color_h2"),
-                "bf16": ("k_point_pre_b", "k_pairs_b", "k_color_b")}
+                "bf16": ("k_point_pre_b", "k_bucket_hist", "k_bucket_scan", "k_bucket_scatter", "k_pairs_b",
+                         "k_color_b")}
 MOPS = {"fp32": "SQ_INSTS_VALU_MFMA_MOPS_F32", "fp32x3": "SQ_INSTS_VALU_MFMA_MOPS_BF16",
         "fp32h2": "SQ_INSTS_VALU_MFMA_MOPS_F16",
         "bf16": "SQ_INSTS_VALU_MFMA_MOPS_BF16"}
@@ -30,6 +31,9 @@ def short(name):
 
 
 def per_kernel(path, counters):
+    """Counter values per aggregate launch: summed over a kernel's dispatches
+    (the bf16 pairs stage is one dispatch per neighbour bucket), divided by the
+    number of launches (dispatches of the colour kernel, once per launch)."""
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
@@ -37,7 +41,8 @@ def per_kernel(path, counters):
         if k in AGG and r["Counter_Name"] in counters:
             sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
-    return {k: {c: v / len(disp[k]) for c, v in d.items()} for k, d in sums.items()}
+    launches = max(len(disp[AGG[-1]]), 1)
+    return {k: {c: v / launches for c, v in d.items()} for k, d in sums.items()}
 
 
 def main():
@@ -58,14 +63,17 @@ def main():
                       {"SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", MOPS[dtype]})
     out = {"source": "tools/prof_bench.sh -> tools/profile_summary.py", "dtype": dtype, "kernels": {}}
     tot_bytes, tot_ns = 0.0, 0.0
+    launches = max(int(stats[AGG[-1]]["Calls"]), 1)
     for k in AGG:
-        avg_ns = float(stats[k]["AverageNs"])
-        fb = fetch[k]["FETCH_SIZE"] * 1024 * 2      # KB -> B, gfx950 x2 correction
-        wb = write[k]["WRITE_SIZE"] * 1024
+        if k not in stats:
+            continue
+        avg_ns = float(stats[k]["TotalDurationNs"]) / launches   # per aggregate launch
+        fb = fetch.get(k, {}).get("FETCH_SIZE", 0.0) * 1024 * 2      # KB -> B, gfx950 x2 correction
+        wb = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
         m = mfma.get(k, {})
         gui = m.get("GRBM_GUI_ACTIVE", 0.0) / 8         # summed over 8 XCDs
         busy = m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / 1024   # per SIMD (256 CUs x 4)
-        out["kernels"][k] = {"calls": int(stats[k]["Calls"]), "avg_ms": avg_ns / 1e6,
+        out["kernels"][k] = {"calls": int(stats[k]["Calls"]), "ms_per_launch": avg_ns / 1e6,
                              "fetch_bytes": fb, "write_bytes": wb,
                              "mfma_busy_frac": busy / gui if gui else None,
                              "eff_clock_ghz_profiled": gui / avg_ns if gui else None}
