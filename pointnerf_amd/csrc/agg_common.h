@@ -190,6 +190,16 @@ struct PairBuckets {
 int64_t bucket_scratch_ints(int64_t n_max);
 int launch_buckets(const pnr_samples& s, int32_t* scratch, PairBuckets* out, hipStream_t st);
 
+// An add the compiler may not fuse with the multiply that produced an operand
+// (hipcc contracts a * b + c into one FMA by default).  The bucketed K-sums of
+// k_pairs_b rely on it: the KT = 8 tree adds rounded products to exact zeros
+// where a KT < 8 tree adds them to each other, so a fused first stage would
+// round differently between the two launches.
+__device__ __forceinline__ float add_nc(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
 // xor-tree sum over the KT lanes of one sample (KT = 8: xor8_sum)
 template <int KT>
 __device__ __forceinline__ float xork_sum(float v) {

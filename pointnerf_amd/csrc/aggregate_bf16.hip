@@ -467,21 +467,21 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
             const float send = b2 ? vv[q] : vv[q + 8];
             const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x141,
                                                                                   0xf, 0xf, false));
-            w8[q] = (b2 ? vv[q + 8] : vv[q]) + recv;
+            w8[q] = add_nc(b2 ? vv[q + 8] : vv[q], recv);
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float send = b1 ? w8[q] : w8[q + 4];
             const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E,
                                                                                   0xf, 0xf, false));
-            w4v[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
+            w4v[q] = add_nc(b1 ? w8[q + 4] : w8[q], recv);
           }
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const float send = b0 ? w4v[q] : w4v[q + 2];
             const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
                                                                                   0xf, 0xf, false));
-            w2[q] = (b0 ? w4v[q + 2] : w4v[q]) + recv;
+            w2[q] = add_nc(b0 ? w4v[q + 2] : w4v[q], recv);
           }
           if (wr) *reinterpret_cast<unsigned*>(hrow + ((2 * ik) & 3) + 8 * (ik >> 1)) = pack_bf16x2(w2[0], w2[1]);
         } else if constexpr (KT == 4) {
@@ -493,14 +493,14 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
             const float send = b1 ? vv[q] : vv[q + 8];
             const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E,
                                                                                   0xf, 0xf, false));
-            w8[q] = (b1 ? vv[q + 8] : vv[q]) + recv;
+            w8[q] = add_nc(b1 ? vv[q + 8] : vv[q], recv);
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float send = b0 ? w8[q] : w8[q + 4];
             const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
                                                                                   0xf, 0xf, false));
-            w4v[q] = (b0 ? w8[q + 4] : w8[q]) + recv;
+            w4v[q] = add_nc(b0 ? w8[q + 4] : w8[q], recv);
           }
           if (wr)
             *reinterpret_cast<uint2*>(hrow + 8 * ik) = make_uint2(pack_bf16x2(w4v[0], w4v[1]),
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
             const float send = b0 ? vv[q] : vv[q + 8];
             const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
                                                                                   0xf, 0xf, false));
-            w8[q] = (b0 ? vv[q + 8] : vv[q]) + recv;
+            w8[q] = add_nc(b0 ? vv[q + 8] : vv[q], recv);
           }
           if (wr) {
             *reinterpret_cast<uint2*>(hrow + 16 * ik) = make_uint2(pack_bf16x2(w8[0], w8[1]),

@@ -1,5 +1,10 @@
 export TMPDIR=/tmp
 O=gpurun_out/r04c; mkdir -p $O
-timeout -k 10 240 python tools/_dbg/bk.py > $O/bk.log 2>&1; cat $O/bk.log | tail -12
-timeout -k 10 600 python -u -m pytest tests/test_gpu_train_contract.py tests/test_gpu_query.py -m gpu -v --timeout 300 --timeout-method thread > $O/t.log 2>&1; tail -5 $O/t.log
-grep -E "^E  .*(Error|outside)" $O/t.log | head -20
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+timeout -k 10 240 python tools/_dbg/bk.py > $O/bk.log 2>&1; rc=$?; tail -12 $O/bk.log; ok $rc || exit $rc
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread > $O/t.log 2>&1; rc=$?
+tail -5 $O/t.log; grep -E "^E  .*(Error|outside)" $O/t.log | head -20; ok $rc || exit $rc
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || exit $?
+tail -1 $O/bench.log | cut -c1-400
+timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline > $O/bench_c5.log 2>&1 || exit $?
+tail -1 $O/bench_c5.log | cut -c1-400
