@@ -209,6 +209,16 @@ __device__ __forceinline__ float xork_sum(float v) {
   return v;
 }
 
+// xork_sum whose adds never fuse with the multiply producing v (k_pairs_b's
+// bucketed launches: every KT rounds a sample's sum like the 8-lane tree)
+template <int KT>
+__device__ __forceinline__ float xork_sum_nc(float v) {
+  if constexpr (KT >= 2) v = add_nc(v, __shfl_xor(v, 1));
+  if constexpr (KT >= 4) v = add_nc(v, __shfl_xor(v, 2));
+  if constexpr (KT >= 8) v = add_nc(v, __shfl_xor(v, 4));
+  return v;
+}
+
 // k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
 // color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],

@@ -216,6 +216,8 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 // zero weights; the xor-tree and DPP reduce-scatter sums below pair the
 // remaining lanes exactly as the 8-lane trees do).
 constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
+constexpr int kHP = kHid + 8;  // bf16 pitch of the staged hid rows (16-B aligned rows)
+static_assert(kBTSmax * kHP <= kBT * kPB, "staged hid rows must fit Xb");
 constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT) * 4;
 
 template <int KT>
@@ -307,7 +309,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       d6[5] = pp[2] - sp[2];
       const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
       const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
-      const float wsum = xork_sum<KT>(wl);
+      const float wsum = xork_sum_nc<KT>(wl);
       const float wn = wl / fmaxf(wsum, 1e-8f);
       const float confc = fminf(fmaxf(cf, 1e-4f), 1.f);
       const bool samp_valid = xork_sum<KT>(valid ? 1.f : 0.f) > 0.f;
@@ -432,6 +434,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     mlp_layer_b<2, kBPT, 8, kPB>(acc, w4, Xb, 17, lane);
+    __syncthreads();   // Xb is free: the K-sums are staged there (hid rows, kHP pitch)
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
     {
     float pa_part[kBPT] = {0.f, 0.f, 0.f, 0.f};
@@ -446,9 +449,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         const int col = 32 * pt + c;
         const float wtp = wtL[col];
         const int sj = col / KT;
-        const int64_t jv = tile * SPT + sj;
-        const bool wr = jv < n && sflag[sj];
-        const int64_t vo = wr ? (list ? (int64_t)list[jv] : jv) : 0;
         float vv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
         // K-sum of the sample's KT lanes as a DPP reduce-scatter: each lane keeps
         // 16 / KT of the 16 accumulator rows (the 8-lane tree's pairing)
-        uint16_t* hrow = A.hid + vo * kHid + 32 * (T0 + T) + 4 * h;
+        uint16_t* hrow = Xb + sj * kHP + 32 * (T0 + T) + 4 * h;   // staged row of sample sj
         if constexpr (KT == 8) {
           const bool b2 = (ik & 4) != 0, b1 = (ik & 2) != 0, b0 = (ik & 1) != 0;
           float w8[8], w4v[4], w2[2];
@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
                                                                                   0xf, 0xf, false));
             w2[q] = add_nc(b0 ? w4v[q + 2] : w4v[q], recv);
           }
-          if (wr) *reinterpret_cast<unsigned*>(hrow + ((2 * ik) & 3) + 8 * (ik >> 1)) = pack_bf16x2(w2[0], w2[1]);
+          *reinterpret_cast<unsigned*>(hrow + ((2 * ik) & 3) + 8 * (ik >> 1)) = pack_bf16x2(w2[0], w2[1]);
         } else if constexpr (KT == 4) {
           // stages lane ^ 2, lane ^ 1: lane ik keeps registers 4 ik .. 4 ik + 3 = neurons 8 ik + q
           const bool b1 = (ik & 2) != 0, b0 = (ik & 1) != 0;
@@ -502,9 +502,8 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
                                                                                   0xf, 0xf, false));
             w4v[q] = add_nc(b0 ? w8[q + 4] : w8[q], recv);
           }
-          if (wr)
-            *reinterpret_cast<uint2*>(hrow + 8 * ik) = make_uint2(pack_bf16x2(w4v[0], w4v[1]),
-                                                                  pack_bf16x2(w4v[2], w4v[3]));
+          *reinterpret_cast<uint2*>(hrow + 8 * ik) = make_uint2(pack_bf16x2(w4v[0], w4v[1]),
+                                                                pack_bf16x2(w4v[2], w4v[3]));
         } else if constexpr (KT == 2) {
           // stage lane ^ 1: lane ik keeps registers 8 ik .. 8 ik + 7 = neurons 16 ik + {0..3, 8..11}
           const bool b0 = (ik & 1) != 0;
@@ -516,20 +515,16 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
                                                                                   0xf, 0xf, false));
             w8[q] = add_nc(b0 ? vv[q + 8] : vv[q], recv);
           }
-          if (wr) {
-            *reinterpret_cast<uint2*>(hrow + 16 * ik) = make_uint2(pack_bf16x2(w8[0], w8[1]),
-                                                                   pack_bf16x2(w8[2], w8[3]));
-            *reinterpret_cast<uint2*>(hrow + 16 * ik + 8) = make_uint2(pack_bf16x2(w8[4], w8[5]),
-                                                                       pack_bf16x2(w8[6], w8[7]));
-          }
+          *reinterpret_cast<uint2*>(hrow + 16 * ik) = make_uint2(pack_bf16x2(w8[0], w8[1]),
+                                                                 pack_bf16x2(w8[2], w8[3]));
+          *reinterpret_cast<uint2*>(hrow + 16 * ik + 8) = make_uint2(pack_bf16x2(w8[4], w8[5]),
+                                                                     pack_bf16x2(w8[6], w8[7]));
         } else {
           // one slot: the lane's 16 registers are the sample's rows 8 g + 4 h + q
-          if (wr) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-              *reinterpret_cast<uint2*>(hrow + 8 * g) = make_uint2(pack_bf16x2(vv[4 * g], vv[4 * g + 1]),
-                                                                   pack_bf16x2(vv[4 * g + 2], vv[4 * g + 3]));
-          }
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<uint2*>(hrow + 8 * g) = make_uint2(pack_bf16x2(vv[4 * g], vv[4 * g + 1]),
+                                                                 pack_bf16x2(vv[4 * g + 2], vv[4 * g + 3]));
         }
       }
     }
@@ -540,12 +535,21 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       for (int pt = 0; pt < kBPT; ++pt) apart[wid * kBT + 32 * pt + c] = pa_part[pt];
     }
     __syncthreads();
+    // staged hid rows -> global, 16 B per thread (a wave writes two whole rows)
+    for (int i = threadIdx.x; i < SPT * (kHid / 8); i += 64 * kBWaves) {
+      const int r = i / (kHid / 8), q = i % (kHid / 8);
+      const int64_t jv = tile * SPT + r;
+      if (jv < n && sflag[r]) {
+        const int64_t vo = list ? (int64_t)list[jv] : jv;
+        reinterpret_cast<uint4*>(A.hid + vo * kHid)[q] = *reinterpret_cast<const uint4*>(Xb + r * kHP + 8 * q);
+      }
+    }
     if (wid < 2) {
       const int col = 64 * wid + lane;
       const int j = col / KT, k = col % KT;
       const float pa = apart[col] + apart[kBT + col] + apart[2 * kBT + col] + apart[3 * kBT + col] + A.w.ba[0];
       const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
-      const float alpha_s = xork_sum<KT>(wtL[col] * alpha_k);
+      const float alpha_s = xork_sum_nc<KT>(wtL[col] * alpha_k);
       const int64_t jv = tile * SPT + j;
       if (k == 0 && jv < n) {
         const int64_t vo = list ? (int64_t)list[jv] : jv;
@@ -561,6 +565,8 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 // ---------------------------------------------------------------------------
 // k_color_b: [hid, PE_4(view dir)] -> 128 -> 128 -> 128 for 128 samples.
 constexpr size_t kColorBLds = (size_t)kBT * kPBc * 2;
+constexpr int kOPitch = kC + 1;   // fp32 output staging pitch (odd: conflict-free column writes)
+static_assert((size_t)kBT * kOPitch * 4 <= kColorBLds, "output staging must fit the Xb tile");
 
 __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
   extern __shared__ __attribute__((aligned(16))) uint16_t xb_dyn[];
@@ -641,15 +647,26 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
 #pragma unroll
     for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
     mlp_layer_b<1, kBPT, 4, kPBc>(acc, w3, Xb, 9, lane);
+    // out_feat rows (valid samples only) through LDS: a lane holds 16 neurons of
+    // one sample, so direct stores would touch 32 rows (516 B apart) per
+    // instruction; staged, each store writes 64 consecutive channels of a row.
+    const uint64_t vm0 = __ballot(v0 + lane < n && A.vmask[v0 + lane] != 0);
+    const uint64_t vm1 = __ballot(v0 + 64 + lane < n && A.vmask[v0 + 64 + lane] != 0);
+    __syncthreads();   // every wave's layer-3 reads of Xb are done
+    float* Ob = reinterpret_cast<float*>(xb_dyn);   // [128][kOPitch] fp32
 #pragma unroll
-    for (int pt = 0; pt < kBPT; ++pt) {
-      const int64_t v = v0 + 32 * pt + c;
-      if (v >= n || A.vmask[v] == 0) continue;
-      float* o = A.out_feat + v * (kC + 1) + 1 + 32 * wid + 4 * h;
+    for (int pt = 0; pt < kBPT; ++pt)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
+        for (int i = 0; i < 4; ++i)
+          Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
+    __syncthreads();
+    for (int r = wid; r < kBT; r += kBWaves) {
+      if (!(((r < 64 ? vm0 : vm1) >> (r & 63)) & 1)) continue;
+      float* o = A.out_feat + (v0 + r) * (kC + 1) + 1;
+      o[lane] = Ob[r * kOPitch + lane];
+      o[64 + lane] = Ob[r * kOPitch + 64 + lane];
     }
     __syncthreads();
   }

@@ -1050,6 +1050,8 @@ __global__ void __launch_bounds__(512, 1) k_pairs_h2_train(X3Args A) { pairs_bod
 constexpr int kCG = 18;                       // 8-row groups per half (144 rows)
 constexpr int kCPlane = kCG * kXT * 16;       // bytes per f16 plane
 constexpr size_t kColH2Lds = 2 * (size_t)kCPlane;
+constexpr int kOPitch = kC + 1;   // fp32 output staging pitch
+static_assert((size_t)kXT * kOPitch * 4 <= kColH2Lds, "output staging must fit the planes");
 
 struct ColH2Args {
   pnr_samples s;
@@ -1173,15 +1175,24 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
       if ((vm >> (32 * (i >> 1) + c)) & 1)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) chk = fmaf(0.f, acc[i][r] + acc[i][r + 1], chk);
+    // staged through LDS (the planes are free once both waves' layer-3 reads are
+    // done): one store then writes 64 consecutive channels of a row instead of
+    // one float in each of 32 rows
+    __syncthreads();
+    float* Ob = reinterpret_cast<float*>(lds);   // [64][kOPitch] fp32
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const int64_t v = v0 + 32 * pt + c;
-      if (!((vm >> (32 * pt + c)) & 1)) continue;
-      float* o = A.out_feat + v * (kC + 1) + 1;
+    for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
       for (int T = 0; T < 2; ++T)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[32 * (T0 + T) + acc_row(r, h)] = lrelu(acc[2 * pt + T][r] * sc3, neg);
+        for (int r = 0; r < 16; ++r)
+          Ob[(32 * pt + c) * kOPitch + 32 * (T0 + T) + acc_row(r, h)] = lrelu(acc[2 * pt + T][r] * sc3, neg);
+    __syncthreads();
+    for (int r = wid; r < kXT; r += 2) {
+      if (!((vm >> r) & 1)) continue;
+      float* o = A.out_feat + (v0 + r) * (kC + 1) + 1;
+      o[lane] = Ob[r * kOPitch + lane];
+      o[64 + lane] = Ob[r * kOPitch + 64 + lane];
     }
     __syncthreads();   // the planes are rewritten by the next tile's loads
   }

@@ -13,7 +13,8 @@
 // (sums of the same non-zero terms in the same pairing order).
 //
 // Layout of the int32 scratch (bucket_scratch_ints): list [n_max] (bucket b's
-// samples at [info[b], info[b] + info[4 + b])) | info [8] | hist [nchunks][4].
+// samples at [info[b], info[b] + info[4 + b])) | info [8] | hist [nchunks][4] |
+// bucket of every sample (bytes, padded to 16 B).
 #include "agg_common.h"
 
 namespace pnr {
@@ -26,22 +27,36 @@ __device__ __forceinline__ int sample_bucket(const pnr_samples& s, int64_t v) {
   const int64_t row = sample_row(s, v);
   const int K = s.K;
   int need = 0;
-  for (int k = 0; k < K; ++k)
-    if (s.pidx[row * K + k] >= 0) need = k + 1;
+  if (K == 8 && ((uintptr_t)s.pidx & 15) == 0) {   // one 32-B row: two 16-B loads
+    const int4* p = reinterpret_cast<const int4*>(s.pidx + row * 8);
+    const int4 a = p[0], b = p[1];
+    const int q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (q[k] >= 0) need = k + 1;
+  } else {
+    for (int k = 0; k < K; ++k)
+      if (s.pidx[row * K + k] >= 0) need = k + 1;
+  }
   return need <= 1 ? 0 : (need <= 2 ? 1 : (need <= 4 ? 2 : 3));
 }
 
-__global__ void __launch_bounds__(kBkBlock) k_bucket_hist(pnr_samples s, int32_t* __restrict__ hist) {
+// Pass 1: bucket of every sample (one byte, read back by the scatter) and the
+// chunk's per-bucket counts.  Consecutive threads take consecutive samples, so
+// a wave's pidx rows are neighbours in the (ordered) sample list.
+__global__ void __launch_bounds__(kBkBlock) k_bucket_hist(pnr_samples s, uint8_t* __restrict__ bkt,
+                                                          int32_t* __restrict__ hist) {
   __shared__ int cnt[4];
   if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t n = eff_n(s);
-  const int64_t base = (int64_t)blockIdx.x * kBkChunk + threadIdx.x * kBkItems;
+  const int64_t base = (int64_t)blockIdx.x * kBkChunk + threadIdx.x;
   int c[4] = {0, 0, 0, 0};
   for (int i = 0; i < kBkItems; ++i) {
-    const int64_t v = base + i;
+    const int64_t v = base + i * kBkBlock;
     if (v < n) {
       const int b = sample_bucket(s, v);
+      bkt[v] = (uint8_t)b;
       c[0] += b == 0;
       c[1] += b == 1;
       c[2] += b == 2;
@@ -108,62 +123,50 @@ __global__ void __launch_bounds__(kBkScan) k_bucket_scan(int32_t* __restrict__ h
     }
 }
 
-__global__ void __launch_bounds__(kBkBlock) k_bucket_scatter(pnr_samples s, const int32_t* __restrict__ hist,
+// Pass 3: stable scatter.  The chunk's samples go in 8 rounds of 256
+// consecutive ones; within a round a sample's slot is its rank among the lower
+// lanes of its wave with the same bucket (ballot + popcount) after the lower
+// waves' counts and the earlier rounds' totals -- sample order within every
+// bucket, no atomics.
+__global__ void __launch_bounds__(kBkBlock) k_bucket_scatter(pnr_samples s, const uint8_t* __restrict__ bkt,
+                                                            const int32_t* __restrict__ hist,
                                                             int32_t* __restrict__ list) {
-  __shared__ int wsum[4][kBkBlock / 64];
+  constexpr int kW = kBkBlock / 64;
+  __shared__ int wcnt[kW][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t n = eff_n(s);
-  const int64_t base = (int64_t)blockIdx.x * kBkChunk + threadIdx.x * kBkItems;
-  int bk[kBkItems];
-  int c[4] = {0, 0, 0, 0};
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;   // lanes below this one
+  int run[4];
 #pragma unroll
+  for (int b = 0; b < 4; ++b) run[b] = hist[(int64_t)blockIdx.x * 4 + b];
   for (int i = 0; i < kBkItems; ++i) {
-    const int64_t v = base + i;
-    bk[i] = v < n ? sample_bucket(s, v) : -1;
-    c[0] += bk[i] == 0;
-    c[1] += bk[i] == 1;
-    c[2] += bk[i] == 2;
-    c[3] += bk[i] == 3;
-  }
-  // exclusive prefix of each bucket's count over the block's threads (in thread order)
-  int pre[4];
+    const int64_t v = (int64_t)blockIdx.x * kBkChunk + i * kBkBlock + threadIdx.x;
+    const int b = v < n ? (int)bkt[v] : -1;
+    int rank = 0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    int x = c[b];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o);
-      if (lane >= o) x += y;
+    for (int bb = 0; bb < 4; ++bb) {
+      const uint64_t m = __ballot(b == bb);
+      if (b == bb) rank = __popcll(m & lt);
+      if (lane == 0) wcnt[w][bb] = __popcll(m);
     }
-    if (lane == 63) wsum[b][w] = x;
-    pre[b] = x - c[b];
-  }
-  __syncthreads();
+    __syncthreads();
+    if (b >= 0) {
+      int pos = rank;
+      for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][b];
+      pos += b == 0 ? run[0] : (b == 1 ? run[1] : (b == 2 ? run[2] : run[3]));
+      list[pos] = (int32_t)v;
+    }
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    int add = hist[(int64_t)blockIdx.x * 4 + b];
-    for (int i = 0; i < w; ++i) add += wsum[b][i];
-    pre[b] += add;
-  }
+    for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-  for (int i = 0; i < kBkItems; ++i) {
-    const int b = bk[i];
-    if (b < 0) continue;
-    int pos = pre[0];
-    pos = b == 1 ? pre[1] : pos;
-    pos = b == 2 ? pre[2] : pos;
-    pos = b == 3 ? pre[3] : pos;
-    list[pos] = (int32_t)(base + i);
-    pre[0] += b == 0;
-    pre[1] += b == 1;
-    pre[2] += b == 2;
-    pre[3] += b == 3;
+      for (int ww = 0; ww < kW; ++ww) run[bb] += wcnt[ww][bb];
+    __syncthreads();
   }
 }
 
 int64_t bucket_scratch_ints(int64_t n_max) {
   const int64_t nm = n_max > 0 ? n_max : 1;
-  return cdiv(nm, 4) * 4 + 8 + cdiv(nm, kBkChunk) * 4;
+  return cdiv(nm, 4) * 4 + 8 + cdiv(nm, kBkChunk) * 4 + cdiv(nm, 16) * 4;   // .. | bucket bytes
 }
 
 int launch_buckets(const pnr_samples& s, int32_t* scratch, PairBuckets* out, hipStream_t st) {
@@ -172,11 +175,12 @@ int launch_buckets(const pnr_samples& s, int32_t* scratch, PairBuckets* out, hip
   out->list = scratch;
   out->info = scratch + cdiv(nm, 4) * 4;
   int32_t* hist = out->info + 8;
-  hipLaunchKernelGGL(k_bucket_hist, dim3((unsigned)nchunks), dim3(kBkBlock), 0, st, s, hist);
+  uint8_t* bkt = reinterpret_cast<uint8_t*>(hist + nchunks * 4);
+  hipLaunchKernelGGL(k_bucket_hist, dim3((unsigned)nchunks), dim3(kBkBlock), 0, st, s, bkt, hist);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBkScan), 0, st, hist, nchunks, out->info);
   PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)nchunks), dim3(kBkBlock), 0, st, s, hist, out->list);
+  hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)nchunks), dim3(kBkBlock), 0, st, s, bkt, hist, out->list);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

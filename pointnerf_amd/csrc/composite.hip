@@ -743,7 +743,7 @@ extern "C" int pnr_weighted_colsum_scratch_floats(int32_t C, int64_t* out) {
 
 extern "C" int pnr_weighted_colsum(const float* w, const float* x, int64_t R, int32_t C, float* out, float* partials,
                                    void* stream) {
-  PNR_CHECK_ARG(w && x && out && partials, "weighted_colsum: null pointer");
+  PNR_CHECK_ARG(((w && x) || R == 0) && out && partials, "weighted_colsum: null pointer");
   PNR_CHECK_ARG(C >= 1 && C <= 128, "weighted_colsum: C=%d unsupported (1..128)", C);
   PNR_CHECK_ARG(R >= 0, "weighted_colsum: R < 0");
   hipStream_t st = as_stream(stream);
