@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 18
+#define PNR_ABI_VERSION 19
 
 enum {
   PNR_OK = 0,
@@ -271,6 +271,10 @@ typedef struct {
                            world distance and point dir are rotated by its point's
                            matrix, a sample's view dir by the matrix of its slot-0
                            neighbour (point_aggregators.py:492-496, 506, 526, 566)     */
+  const int32_t* n_used_dev; /* optional device count of `used` (pnr_used_points writes it):
+                           the kernels then take min(n_used, *n_used_dev) rows, n_used
+                           being the capacity -- a training forward that never reads
+                           the count on the host (ABI 19)                               */
 } pnr_points;
 
 typedef struct {
@@ -581,6 +585,22 @@ int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int
  * products on fp32 MFMA; with act != NULL each C[m,n] is multiplied by the
  * LeakyReLU derivative of the saved activation act[m,n] (1 if > 0, else slope).
  * N a multiple of 32 in [32, 256]; any M >= 0, K > 0. */
+/* fp32-accurate C = A^T B on f16 MFMA (the fp32h2 arithmetic of the forward):
+ * A scaled by 2^e with max|A| 2^e in [4, 8) -- e from *a_absmax, the float bits
+ * of max |A| (pnr_absmax) -- both operands split x = xh + 2^-11 xl, three f16
+ * products per k-step (pnr_gemm_tn_x3 takes six bf16 ones).  An operand outside
+ * the split's range (|B| >= 2^15, a stale max, NaN / inf) sets *range_flag and
+ * the call's x3 kernel, launched behind the h2 one, then recomputes it: the
+ * result is always the fp32-accurate one.  The caller zeroes *range_flag (one
+ * flag can serve every call of a step) and may read it later to count fallbacks.
+ * Same M, N, scratch and colsum rules as pnr_gemm_tn. */
+int pnr_gemm_tn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
+                   float* C, float* colsum_a, const uint32_t* a_absmax, int32_t* range_flag, void* scratch,
+                   size_t scratch_bytes, void* stream);
+/* *out_bits = float bits of max |x[0, n)| (NaN if any x is NaN); partials:
+ * pnr_absmax_scratch_floats() device floats.  No host sync. */
+int pnr_absmax_scratch_floats(int64_t* out);
+int pnr_absmax(const float* x, int64_t n, float* partials, uint32_t* out_bits, void* stream);
 int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K, int32_t N,
                 const float* act, int64_t ld_act, float slope, float* C, int64_t ldc, void* stream);
 
@@ -650,6 +670,10 @@ int pnr_ray_march_bwd_ex(const float* ray_dist, const uint8_t* ray_valid, const 
  * x = d ray_color; for pnr_ray_march_fwd w = bg_T.  partials: device floats of
  * pnr_weighted_colsum_scratch_floats(C). */
 int pnr_weighted_colsum_scratch_floats(int32_t C, int64_t* out);
+/* Zero rows [0, min(*n_dev, n_cap)) of a row-major buffer (row_bytes % 4 == 0):
+ * the device-counted part of a capacity-sized buffer, no host read of the
+ * count (the sync-free training forward's feature / hid rows). */
+int pnr_zero_rows(void* p, int64_t row_bytes, const int32_t* n_dev, int64_t n_cap, void* stream);
 int pnr_weighted_colsum(const float* w, const float* x, int64_t R, int32_t C, float* out, float* partials,
                         void* stream);
 

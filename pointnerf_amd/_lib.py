@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 18
+ABI_VERSION = 19
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -100,7 +100,8 @@ class Points(ctypes.Structure):
     _fields_ = [("n", c_int64), ("xyz", c_void_p), ("pers", c_void_p), ("emb", c_void_p), ("color", c_void_p),
                 ("dir", c_void_p), ("conf", c_void_p), ("campos", c_void_p), ("camrot", c_void_p),
                 ("used", c_void_p), ("n_used", c_int64), ("used_map", c_void_p),
-                ("p1_ready", c_int32), ("emb_bf16", c_void_p), ("rw2c", c_void_p)]
+                ("p1_ready", c_int32), ("emb_bf16", c_void_p), ("rw2c", c_void_p),
+                ("n_used_dev", c_void_p)]
 
 
 class Samples(ctypes.Structure):
@@ -215,6 +216,11 @@ SIGNATURES = {
     "pnr_ray_march_bwd_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
+    "pnr_zero_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
+    "pnr_gemm_tn_h2": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_absmax_scratch_floats": (c_int, [P(c_int64)]),
+    "pnr_absmax": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "pnr_weighted_colsum_scratch_floats": (c_int, [c_int32, P(c_int64)]),
     "pnr_weighted_colsum": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     "pnr_march_aux": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), c_void_p, c_void_p, c_int64, c_void_p,
@@ -296,10 +302,32 @@ def aggregate_scratch(n_max: int, n_points: int, device) -> torch.Tensor:
     return torch.empty((int(nb.value) + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
-def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = True):
+class H2Gemm:
+    """State shared by the pnr_gemm_tn_h2 calls of one backward: the range flag
+    (zeroed here; raised -> those calls ran their x3 fallback on the device) and
+    the pnr_absmax scratch."""
+
+    def __init__(self, device):
+        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        n = ctypes.c_int64(0)
+        check(lib().pnr_absmax_scratch_floats(ctypes.byref(n)), "pnr_absmax_scratch_floats")
+        self.part = torch.empty(int(n.value), dtype=torch.float32, device=device)
+
+    def absmax(self, A: torch.Tensor) -> torch.Tensor:
+        """[1] int32 holding the float bits of max |A| (device, no sync)."""
+        out = torch.empty(1, dtype=torch.int32, device=A.device)
+        a = A if A.is_contiguous() else A.contiguous()
+        check(lib().pnr_absmax(ptr(a), a.numel(), ptr(self.part), ptr(out), stream_ptr(A.device)), "pnr_absmax")
+        return out
+
+
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = True, h2: H2Gemm | None = None,
+            a_absmax: torch.Tensor | None = None):
     """C = A^T B (A [K,M], B [K,N], fp32 row-major with unit column stride) on
     pnr_gemm_tn_x3 (fp32-accurate on bf16 MFMA; x3=False: pnr_gemm_tn, native
-    fp32 MFMA); returns C [M,N] (and A's column sums when colsum)."""
+    fp32 MFMA; h2: pnr_gemm_tn_h2, fp32-accurate on f16 MFMA with A's scale
+    from a_absmax or a pnr_absmax pass); returns C [M,N] (and A's column sums
+    when colsum)."""
     K, M = A.shape
     N = B.shape[1]
     assert B.shape[0] == K and A.stride(1) == 1 and B.stride(1) == 1
@@ -308,6 +336,12 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = T
     scratch = torch.empty(max(int(nb.value) // 4, 1), dtype=torch.float32, device=A.device)
     C = torch.empty((M, N), dtype=torch.float32, device=A.device)
     cs = torch.empty(M, dtype=torch.float32, device=A.device) if colsum else None
+    if h2 is not None:
+        am = a_absmax if a_absmax is not None else h2.absmax(A)
+        check(lib().pnr_gemm_tn_h2(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(am),
+                                   ptr(h2.flag), ptr(scratch), scratch.numel() * 4, stream_ptr(A.device)),
+              "pnr_gemm_tn_h2")
+        return (C, cs) if colsum else C
     fn = lib().pnr_gemm_tn_x3 if x3 else lib().pnr_gemm_tn
     check(fn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
              scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")

@@ -87,6 +87,18 @@ __device__ __forceinline__ void pair_pers(const pnr_points& P, const pnr_samples
   }
 }
 
+// Rows of block1.0's point half (P1): the used points (device count when given,
+// ABI 19) or every point.
+__device__ __forceinline__ int64_t p1_rows(const pnr_points& p) {
+  if (!p.used) return p.n;
+  int64_t n = p.n_used;
+  if (p.n_used_dev) {
+    const int64_t d = *p.n_used_dev;
+    n = d < n ? d : n;
+  }
+  return n;
+}
+
 __device__ __forceinline__ int64_t eff_n(const pnr_samples& s) {
   int64_t n = s.n_max;
   if (s.n_dev) {

@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(kAggBlock, 1) k_point_pre(AggArgs A) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* X = lds_dyn + wid * kWaveLds;
   const int m = lane & 31, h = lane >> 5;
-  const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;   // P1 rows
+  const int64_t np = p1_rows(A.pts);   // P1 rows
   const int64_t ntiles = cdiv(np, 32);
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
     const int64_t pt = tile * 32 + m;                         // P1 row

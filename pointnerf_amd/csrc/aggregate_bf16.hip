@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
   uint16_t* Xb = xb_dyn;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
-  const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;
+  const int64_t np = p1_rows(A.pts);   // P1 rows
   const int64_t ntiles = cdiv(np, kBT);
   const uint4* wf = reinterpret_cast<const uint4*>(A.w.w1af) + 2 * wid * 64;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -582,16 +582,35 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
   const uint4* w1 = reinterpret_cast<const uint4*>(A.w.wc1f) + wid * 64;
   const uint4* w2 = reinterpret_cast<const uint4*>(A.w.wc2f) + wid * 64;
   const uint4* w3 = reinterpret_cast<const uint4*>(A.w.wc3f) + wid * 64;
+  // hid rows of a tile (512 B each; zeros for masked samples) in 16 x 16-B
+  // chunks per thread, loaded one tile ahead: the next tile's loads are in flight
+  // during this tile's three layers (a chain of 16 dependent load rounds per tile
+  // otherwise: the kernel waited on HBM latency, not on HBM bandwidth)
+  constexpr int kHidChunks = kBT * (kHid / 8) / (64 * kBWaves);
+  uint4 hu[kHidChunks];
+  uint64_t vm0 = 0, vm1 = 0;   // the loaded tile's vmask bits
+  auto load_hid = [&](int64_t t) {
+    const int64_t b = t * kBT;
+    vm0 = __ballot(t < ntiles && b + lane < n && A.vmask[b + lane] != 0);
+    vm1 = __ballot(t < ntiles && b + 64 + lane < n && A.vmask[b + 64 + lane] != 0);
+#pragma unroll
+    for (int k = 0; k < kHidChunks; ++k) {
+      const int i = threadIdx.x + 64 * kBWaves * k;
+      const int col = i >> 5, q = i & 31;
+      const bool ok = ((col < 64 ? vm0 : vm1) >> (col & 63)) & 1;
+      hu[k] = ok ? reinterpret_cast<const uint4*>(A.hid + (b + col) * kHid)[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  load_hid(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t v0 = tile * kBT;
-    // hid rows (512 B each) -> Xb rows 0..255: 16 x 16-B chunks per thread
-    for (int i = threadIdx.x; i < kBT * 32; i += 64 * kBWaves) {
-      const int col = i >> 5, q = i & 31;
-      const int64_t v = v0 + col;
-      const bool ok = v < n && A.vmask[v] != 0;
-      const uint4 u = ok ? reinterpret_cast<const uint4*>(A.hid + v * kHid)[q] : make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(Xb + col * kPBc + 8 * q) = u;
+#pragma unroll
+    for (int k = 0; k < kHidChunks; ++k) {
+      const int i = threadIdx.x + 64 * kBWaves * k;
+      *reinterpret_cast<uint4*>(Xb + (i >> 5) * kPBc + 8 * (i & 31)) = hu[k];
     }
+    const uint64_t tm0 = vm0, tm1 = vm1;
+    load_hid(tile + gridDim.x);
     // view PE (ori dropped): rows 256 + 4ch + f = sin, 268 + 4ch + f = cos, bias 280, zeros to 287
     if (threadIdx.x < kBT) {
       const int col = threadIdx.x;
@@ -650,8 +669,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
     // out_feat rows (valid samples only) through LDS: a lane holds 16 neurons of
     // one sample, so direct stores would touch 32 rows (516 B apart) per
     // instruction; staged, each store writes 64 consecutive channels of a row.
-    const uint64_t vm0 = __ballot(v0 + lane < n && A.vmask[v0 + lane] != 0);
-    const uint64_t vm1 = __ballot(v0 + 64 + lane < n && A.vmask[v0 + 64 + lane] != 0);
     __syncthreads();   // every wave's layer-3 reads of Xb are done
     float* Ob = reinterpret_cast<float*>(xb_dyn);   // [128][kOPitch] fp32
 #pragma unroll
@@ -663,7 +680,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
           Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
     __syncthreads();
     for (int r = wid; r < kBT; r += kBWaves) {
-      if (!(((r < 64 ? vm0 : vm1) >> (r & 63)) & 1)) continue;
+      if (!(((r < 64 ? tm0 : tm1) >> (r & 63)) & 1)) continue;
       float* o = A.out_feat + (v0 + r) * (kC + 1) + 1;
       o[lane] = Ob[r * kOPitch + lane];
       o[64 + lane] = Ob[r * kOPitch + 64 + lane];

@@ -1223,7 +1223,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
-  const int64_t np = A.pts.used ? A.pts.n_used : A.pts.n;
+  const int64_t np = p1_rows(A.pts);   // P1 rows
   const int64_t ntiles = cdiv(np, kXT);
   const int T0 = 2 * wid;
   const int voff = (T0 * XL<true>::NPW * 64 + lane) * 16;

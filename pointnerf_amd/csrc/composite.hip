@@ -735,6 +735,37 @@ extern "C" int pnr_ray_march_bwd(const float* ray_dist, const uint8_t* ray_valid
                               nullptr, d_feat, nullptr, stream);
 }
 
+// Zero the device-counted rows of a capacity-sized buffer (pnr_zero_rows).
+__global__ void __launch_bounds__(256) k_zero_rows(uint32_t* __restrict__ p, int64_t row_words,
+                                                   const int32_t* __restrict__ n_dev, int64_t n_cap) {
+  int64_t n = *n_dev;
+  n = n < n_cap ? n : n_cap;
+  const int64_t words = n * row_words;
+  const int64_t w4 = words >> 2;
+  uint4* q = reinterpret_cast<uint4*>(p);
+  const bool vec = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (vec) {
+    for (int64_t j = i; j < w4; j += stride) q[j] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t j = 4 * w4 + i; j < words; j += stride) p[j] = 0u;
+  } else {
+    for (int64_t j = i; j < words; j += stride) p[j] = 0u;
+  }
+}
+
+extern "C" int pnr_zero_rows(void* p, int64_t row_bytes, const int32_t* n_dev, int64_t n_cap, void* stream) {
+  PNR_CHECK_ARG(n_dev && n_cap >= 0 && row_bytes > 0 && row_bytes % 4 == 0 && (p || n_cap == 0),
+                "zero_rows: bad args");
+  if (n_cap == 0) return PNR_OK;
+  const int64_t words = n_cap * (row_bytes / 4);
+  const int64_t blocks = cdiv(cdiv(words, 4), 256);
+  hipLaunchKernelGGL(k_zero_rows, dim3((unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048)), dim3(256), 0,
+                     as_stream(stream), static_cast<uint32_t*>(p), row_bytes / 4, n_dev, n_cap);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
 extern "C" int pnr_weighted_colsum_scratch_floats(int32_t C, int64_t* out) {
   PNR_CHECK_ARG(out && C >= 1 && C <= 128, "weighted_colsum: C=%d unsupported (1..128)", C);
   *out = (int64_t)kColsumBlocks * C;

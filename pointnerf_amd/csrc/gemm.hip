@@ -35,6 +35,9 @@ struct GemmArgs {
   int64_t kchunk;      // rows of K per split (multiple of 2 * kGUnroll)
   float* part;         // [nsplit][M*N + M]  (C partial, then colsum partial)
   int colsum;
+  const uint32_t* a_absmax;   // h2: bits of max |A| (pnr_absmax), picks A's power-of-two scale
+  int32_t* range_flag;        // h2: set when a scaled operand leaves the f16 split's range
+  const int32_t* run_if;      // x3: run only when *run_if != 0 (the h2 call's guarded fallback)
 };
 
 template <int NT>
@@ -148,6 +151,7 @@ constexpr int kXPlane = 256 * kXPitch;  // bf16 per plane (256 rows)
 constexpr size_t kXLds = 2 * 2 * 3 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 144 KB
 
 __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
+  if (g.run_if && *g.run_if == 0) return;   // guarded fallback of an h2 call whose operands fit
   extern __shared__ __attribute__((aligned(16))) uint16_t glds[];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int64_t k_begin = (int64_t)blockIdx.x * g.kchunk;
@@ -257,6 +261,201 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
     if (kh == 1) red[col] = csum;
     __syncthreads();
     if (kh == 0 && stA) out[(int64_t)g.M * g.N + col] = csum + red[col];
+  }
+}
+
+// ---------------------------------------------------------------- h2 variant
+// fp32-accurate C = A^T B on f16 MFMA (pnr_gemm_tn_h2), the forward's fp32h2
+// arithmetic (aggregate_x3.hip) for the weight gradients: A is scaled by 2^e so
+// that max |A| 2^e lies in [4, 8) (e from the device max pnr_absmax wrote, so
+// gradients of any magnitude use the f16 exponent range), both operands split
+// x = xh + 2^-11 xl (splith, exact residuals), and
+//   2^11 (A 2^e)^T B ~= (2^11 Ah)^T Bh + Ah^T Bl + Al^T Bh
+// -- three v_mfma_f32_32x32x16_f16 per 16 k-rows instead of x3's six bf16
+// products, two LDS planes per operand instead of three (96 KB double-buffered).
+// 2^11 Ah is exact in f16 (|Ah| < 8).  The dropped 2^-22 Al^T Bl and the split
+// residuals are <= ~2^-21 |a b| per product.  Operands outside the split's range
+// (|B| >= 2^15, a stale max, non-finite) raise range_flag: the caller launches
+// the x3 kernel behind this one with run_if = range_flag.
+constexpr size_t kHLds = 2 * 2 * 2 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 96 KB
+
+__global__ void __launch_bounds__(512, 1) k_gemm_tn_h2_part(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t glds[];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int64_t k_begin = (int64_t)blockIdx.x * g.kchunk;
+  const int64_t k_end = k_begin + g.kchunk < g.K ? k_begin + g.kchunk : g.K;
+  const int64_t stride = (int64_t)g.M * g.N + g.M;
+  float* out = g.part + (int64_t)blockIdx.x * stride;
+  // A's scale 2^e: max |A| 2^e in [4, 8)
+  int e = 0;
+  {
+    const float amax = __uint_as_float(*g.a_absmax);
+    if (amax > 0.f && amax <= 3.0e38f) {
+      int x;
+      frexpf(amax, &x);   // amax = f 2^x, f in [0.5, 1)
+      e = 3 - x;
+    }
+  }
+  const float sa = ldexpf(1.f, e);
+  const int col = tid & 255, kh = tid >> 8;
+  const bool stA = col < g.M, stB = col < g.N;
+  float csum = 0.f;
+  bool bad = false;   // a scaled A with |a| >= 8, a B with |b| >= 2^15, or a NaN / inf
+  auto load = [&](int64_t k0, float (&va)[8], float (&vb)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t r = k0 + 8 * kh + j;
+      const bool ok = r < k_end;
+      va[j] = ok && stA ? g.A[r * g.lda + col] : 0.f;
+      vb[j] = ok && stB ? g.B[r * g.ldb + col] : 0.f;
+    }
+  };
+  auto put = [&](int buf, const float (&va)[8], const float (&vb)[8]) {
+    uint16_t* base = glds + (size_t)buf * 4 * kXPlane + col * kXPitch + 8 * kh;
+    uint4 pa[2], pb[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float a0 = va[2 * q] * sa, a1 = va[2 * q + 1] * sa;
+      csum += va[2 * q] + va[2 * q + 1];
+      const bool ok = (fabsf(a0) < 8.f) && (fabsf(a1) < 8.f) && (fabsf(vb[2 * q]) < 32768.f) &&
+                      (fabsf(vb[2 * q + 1]) < 32768.f);   // false for NaN / inf too
+      bad = bad || !ok;
+      unsigned x0, x1;
+      splith(a0, a1, x0, x1);
+      reinterpret_cast<unsigned*>(&pa[0])[q] = x0;
+      reinterpret_cast<unsigned*>(&pa[1])[q] = x1;
+      splith(vb[2 * q], vb[2 * q + 1], x0, x1);
+      reinterpret_cast<unsigned*>(&pb[0])[q] = x0;
+      reinterpret_cast<unsigned*>(&pb[1])[q] = x1;
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      *reinterpret_cast<uint4*>(base + p * kXPlane) = pa[p];
+      *reinterpret_cast<uint4*>(base + (2 + p) * kXPlane) = pb[p];
+    }
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x16){0.f};
+  const int mt0 = 2 * (wid & 3), nt0 = 4 * (wid >> 2);
+  auto compute = [&](int buf) {
+    const uint16_t* lb = glds + (size_t)buf * 4 * kXPlane + c * kXPitch + 8 * h;
+    uint4 ah[2], al[2], as[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      ah[mi] = *reinterpret_cast<const uint4*>(lb + 32 * (mt0 + mi) * kXPitch);
+      al[mi] = *reinterpret_cast<const uint4*>(lb + kXPlane + 32 * (mt0 + mi) * kXPitch);
+      as[mi] = f16x8_scale2048(ah[mi]);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      if (32 * (nt0 + ni) >= g.N) continue;
+      const uint4 bh = *reinterpret_cast<const uint4*>(lb + 2 * kXPlane + 32 * (nt0 + ni) * kXPitch);
+      const uint4 bl = *reinterpret_cast<const uint4*>(lb + 3 * kXPlane + 32 * (nt0 + ni) * kXPitch);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        if (32 * (mt0 + mi) >= g.M) continue;
+        acc[mi][ni] = mfma_f16(al[mi], bh, acc[mi][ni]);   // smallest terms first
+        acc[mi][ni] = mfma_f16(ah[mi], bl, acc[mi][ni]);
+        acc[mi][ni] = mfma_f16(as[mi], bh, acc[mi][ni]);
+      }
+    }
+  };
+  float va[8], vb[8];
+  load(k_begin, va, vb);
+  put(0, va, vb);
+  __syncthreads();
+  int it1 = 0;
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += kXK, ++it1) {
+    const int buf = it1 & 1;
+    const bool more = k0 + kXK < k_end;
+    if (more) load(k0 + kXK, va, vb);
+    compute(buf);
+    if (more) put(buf ^ 1, va, vb);
+    __syncthreads();
+  }
+  if (bad) atomicOr(g.range_flag, 1);   // outside the split's range, or NaN / inf
+  const float unscale = ldexpf(1.f, -(e + 11));   // exact: a power of two
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int m0 = 32 * (mt0 + mi), n0 = 32 * (nt0 + ni);
+      if (m0 >= g.M || n0 >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        out[(int64_t)(m0 + (r & 3) + 8 * (r >> 2) + 4 * h) * g.N + n0 + c] = acc[mi][ni][r] * unscale;
+    }
+  if (g.colsum) {   // column sums of A (unscaled fp32): the two k-halves of every column
+    float* red = reinterpret_cast<float*>(glds);
+    __syncthreads();
+    if (kh == 1) red[col] = csum;
+    __syncthreads();
+    if (kh == 0 && stA) out[(int64_t)g.M * g.N + col] = csum + red[col];
+  }
+}
+
+// max |x| over x[0, n) as float bits (pnr_absmax): per-block maxima, then one
+// block (no atomics, no pre-zeroed output).  NaN propagates (the h2 GEMM then
+// raises its range flag and runs the x3 fallback).
+constexpr int kAbsBlocks = 1024;
+__global__ void __launch_bounds__(256) k_absmax_part(const float* __restrict__ x, int64_t n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? n / 4 : 0;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = x4[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    if (v.x != v.x || v.y != v.y || v.z != v.z || v.w != v.w) m = __int_as_float(0x7fc00000);
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = x[i];
+    m = fmaxf(m, fabsf(v));
+    if (v != v) m = __int_as_float(0x7fc00000);
+  }
+  const bool nan = m != m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const bool anynan = __any(nan);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = anynan ? __int_as_float(0x7fc00000) : m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    bool bn = false;
+    for (int w = 0; w < 4; ++w) {
+      bn |= red[w] != red[w];
+      r = fmaxf(r, red[w]);
+    }
+    part[blockIdx.x] = bn ? __int_as_float(0x7fc00000) : r;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_absmax_final(const float* __restrict__ part, int nb, uint32_t* __restrict__ out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  bool nan = false;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    const float v = part[i];
+    nan |= v != v;
+    m = fmaxf(m, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const bool anynan = __any(nan);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = anynan ? __int_as_float(0x7fc00000) : m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    bool bn = false;
+    for (int w = 0; w < 4; ++w) {
+      bn |= red[w] != red[w];
+      r = fmaxf(r, red[w]);
+    }
+    out[0] = __float_as_uint(bn ? __int_as_float(0x7fc00000) : r);
   }
 }
 
@@ -485,8 +684,10 @@ extern "C" int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t
   return PNR_OK;
 }
 
-static int gemm_tn_impl(bool x3, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
-                        int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream) {
+static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
+                        int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream,
+                        const uint32_t* a_absmax = nullptr, int32_t* range_flag = nullptr) {
+  const bool x3 = mode == 1, h2 = mode == 2;
   PNR_CHECK_ARG(C && scratch && (K == 0 || (A && B)), "gemm_tn: null pointer");
   PNR_CHECK_ARG(M > 0 && N > 0 && M % 32 == 0 && N % 32 == 0 && M <= 32 * kGWaves && N <= 32 * kGMaxNT,
                 "gemm_tn: M, N must be multiples of 32 in [32, 256]");
@@ -514,13 +715,23 @@ static int gemm_tn_impl(bool x3, const float* A, int64_t lda, const float* B, in
   g.kchunk = kc;
   g.part = static_cast<float*>(scratch);
   g.colsum = colsum_a != nullptr;
-  if (x3) {
-    static bool attr = false;
-    if (!attr) {
-      PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_x3_part),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
-      attr = true;
-    }
+  g.a_absmax = a_absmax;
+  g.range_flag = range_flag;
+  g.run_if = nullptr;
+  static bool attr = false;
+  if (!attr && (x3 || h2)) {
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_x3_part),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_h2_part),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHLds));
+    attr = true;
+  }
+  if (h2) {
+    hipLaunchKernelGGL(k_gemm_tn_h2_part, dim3(ns), dim3(512), kHLds, st, g);
+    PNR_LAUNCH_CHECK();
+    g.run_if = range_flag;   // the x3 kernel redoes the partials only when the flag is up
+    hipLaunchKernelGGL(k_gemm_tn_x3_part, dim3(ns), dim3(512), kXLds, st, g);
+  } else if (x3) {
     hipLaunchKernelGGL(k_gemm_tn_x3_part, dim3(ns), dim3(512), kXLds, st, g);
   } else {
     hipLaunchKernelGGL(k_gemm_tn_part, dim3(ns), dim3(64 * kGWaves), 0, st, g);
@@ -543,11 +754,36 @@ static int gemm_tn_impl(bool x3, const float* A, int64_t lda, const float* B, in
 extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
                            int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
                            void* stream) {
-  return gemm_tn_impl(false, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
+  return gemm_tn_impl(0, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
 }
 
 extern "C" int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
                               int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
                               void* stream) {
-  return gemm_tn_impl(true, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
+  return gemm_tn_impl(1, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
+}
+
+extern "C" int pnr_gemm_tn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
+                              int32_t N, float* C, float* colsum_a, const uint32_t* a_absmax, int32_t* range_flag,
+                              void* scratch, size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(a_absmax && range_flag, "gemm_tn_h2: a_absmax and range_flag required");
+  return gemm_tn_impl(2, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream, a_absmax,
+                      range_flag);
+}
+
+extern "C" int pnr_absmax_scratch_floats(int64_t* out) {
+  PNR_CHECK_ARG(out, "absmax_scratch_floats: null");
+  *out = kAbsBlocks;
+  return PNR_OK;
+}
+
+extern "C" int pnr_absmax(const float* x, int64_t n, float* partials, uint32_t* out_bits, void* stream) {
+  PNR_CHECK_ARG(partials && out_bits && n >= 0 && (x || n == 0), "absmax: bad args");
+  hipStream_t st = as_stream(stream);
+  const int nb = (int)(n > 0 ? (cdiv(n, 4 * 256) < kAbsBlocks ? cdiv(n, 4 * 256) : kAbsBlocks) : 1);
+  hipLaunchKernelGGL(k_absmax_part, dim3(nb), dim3(256), 0, st, x, n, partials);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_absmax_final, dim3(1), dim3(256), 0, st, partials, nb, out_bits);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
 }

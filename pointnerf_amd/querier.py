@@ -156,11 +156,37 @@ class QueryBuffers:
 
     def read_counts(self):
         """{S_filled, S_valid, R_hit, R_valid, n_pairs, n_cand} (one D2H copy, syncs)."""
-        c = self.counts.cpu()
-        n_cand = int(c[6:8].view(torch.int64).item())
-        c = c.tolist()
-        return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand,
-                    n_used=c[5])   # n_used: pnr_used_points' count when the caller put it in counts[5]
+        return counts_dict(self.counts.cpu())
+
+    def read_counts_async(self) -> "CountsHandle":
+        """The counts as they stand at this point of the stream, copied to pinned
+        memory behind an event: .get() waits for that event only, not for the
+        work enqueued after it (the training forward never drains the GPU)."""
+        return CountsHandle(self.counts)
+
+
+def counts_dict(c: torch.Tensor) -> dict:
+    n_cand = int(c[6:8].view(torch.int64).item())
+    c = c.tolist()
+    return dict(S_filled=c[0], S_valid=c[1], R_hit=c[2], R_valid=c[3], n_pairs=c[4], n_cand=n_cand,
+                n_used=c[5])   # n_used: pnr_used_points' count when the caller put it in counts[5]
+
+
+class CountsHandle:
+    """Pinned copy of a query's counts + the event after it (read_counts_async)."""
+
+    def __init__(self, counts: torch.Tensor):
+        self.host = torch.empty(counts.numel(), dtype=counts.dtype, pin_memory=True)
+        self.host.copy_(counts, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+        self._d = None
+
+    def get(self) -> dict:
+        if self._d is None:
+            self.event.synchronize()
+            self._d = counts_dict(self.host)
+        return self._d
 
 
 class GridHandle:

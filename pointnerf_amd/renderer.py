@@ -187,6 +187,37 @@ def _counts_dict(c):
 PRECISIONS = ("fp32", "fp32x3", "fp32h2", "bf16")
 
 
+class _TrainAux(dict):
+    """render_rays_train's last_train_aux: keys whose values need the batch's
+    host counts are computed when first read (so that the forward itself never
+    waits for the GPU); ``"k" in aux`` is true for them without computing."""
+
+    def __init__(self):
+        super().__init__()
+        self._lazy = {}
+
+    def lazy(self, keys, fn):
+        for k in keys:
+            self._lazy[k] = fn
+
+    def __contains__(self, k):
+        return dict.__contains__(self, k) or k in self._lazy
+
+    def __missing__(self, k):
+        fn = self._lazy.get(k)
+        if fn is None:
+            raise KeyError(k)
+        vals = fn()
+        for kk in list(self._lazy):
+            if self._lazy[kk] is fn:
+                del self._lazy[kk]
+        self.update(vals)
+        return dict.__getitem__(self, k)
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+
 class NeuralPointsRayMarching(nn.Module):
     """neural_points_volumetric_model.NeuralPointsRayMarching, fused HIP path."""
 
@@ -217,7 +248,8 @@ class NeuralPointsRayMarching(nn.Module):
         if getattr(opt, "neural_render", "none") == "cnn":
             from .neural_render import NeuralRenderer
             self.neural_render_2d = NeuralRenderer(input_dim=128).to(neural_points.device)
-        self.last_counts = None
+        self._last_counts = None
+        self._train_conf_src = None   # query buffers of the last render_rays_train (zero_one_conf_loss)
         self._rw2c_key = None
         if getattr(opt, "which_render_func", "radiance") != "radiance" or \
                 getattr(opt, "which_blend_func", "alpha") != "alpha" or \
@@ -616,6 +648,19 @@ class NeuralPointsRayMarching(nn.Module):
         state.scratch_key = key
         return buf, ready
 
+    @property
+    def last_counts(self):
+        """Sample counts of the last render call (dict); a training call leaves a
+        pending CountsHandle that is read here, when first asked for."""
+        c = self._last_counts
+        if c is not None and not isinstance(c, dict):
+            c = self._last_counts = c.get()
+        return c
+
+    @last_counts.setter
+    def last_counts(self, v):
+        self._last_counts = v
+
     def render_rays_train(self, campos, camrot, raydir, near, far, bg_color):
         """Differentiable render of one training ray batch [R,3] (SURVEY 8(a)
         a17): same query / aggregate / composite as render_rays, with autograd
@@ -644,13 +689,16 @@ class NeuralPointsRayMarching(nn.Module):
         xyz = np_.xyz.detach().contiguous()
         bufs, hp, rays, qp = q.run(xyz, rd, campos, camrot, near, far, bufs=None)
         # block1.0's point half only for the points this batch references (device
-        # list, its count read with the query counts: one host sync)
+        # list and count).  No host read here: the kernels take the device counts
+        # (samples: counts[1], used points: counts[5]) with capacity-sized
+        # buffers, and the counts travel to pinned memory behind an event that the
+        # backward (or last_counts) waits on -- the forward never drains the GPU.
         from .train import used_points_device
         used_buf, used_map = used_points_device(bufs, K, xyz.shape[0])
-        cnt = bufs.read_counts()
-        self.last_counts = cnt
-        Sv = cnt["S_valid"]
-        s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
+        counts = bufs.read_counts_async()
+        self.last_counts = counts
+        S_cap = R * SR
+        s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, S_cap, bufs.pidx.data_ptr(),
                       bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                       bufs.fill_rs.data_ptr(), SR, K)
         n = xyz.shape[0]
@@ -658,12 +706,13 @@ class NeuralPointsRayMarching(nn.Module):
         def tab(t, c):
             return None if t is None else t.reshape(n, c)
 
-        used = (used_buf[:cnt["n_used"]], used_map)
+        used = (used_buf, used_map, bufs.counts[5:6])
         if self.train_precision not in ("fp32", "fp32x3", "fp32h2"):
             raise L.PnrError(f"train_precision {self.train_precision!r}: 'fp32h2', 'fp32x3' or 'fp32'")
-        spec = AggSpec(self.aggregator, s, Sv, dict(xyz=xyz, campos=campos, camrot=camrot, rw2c=np_.rw2c_table()),
+        spec = AggSpec(self.aggregator, s, S_cap, dict(xyz=xyz, campos=campos, camrot=camrot, rw2c=np_.rw2c_table()),
                        keep=(bufs, rd),
-                       used=used, x3=self.train_precision == "fp32x3", h2=self.train_precision == "fp32h2")
+                       used=used, x3=self.train_precision == "fp32x3", h2=self.train_precision == "fp32h2",
+                       counts=counts)
         spec.keep_saved = self.keep_train_saved
         feat = AggregateFn.apply(spec, np_.points_embeding.reshape(n, 32), tab(np_.points_color, 3),
                                  tab(np_.points_dir, 3), tab(np_.points_conf, 1),
@@ -671,25 +720,36 @@ class NeuralPointsRayMarching(nn.Module):
         if spec.h2_fallback:
             self.h2_fallbacks += 1
         if C == 3:
-            feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
+            feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=S_cap)
         cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, None)
-        cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(campos, camrot, rd, hp))
+        cspec = CompositeSpec(rays, qp, bufs, cp, R, SR, C, keep=(campos, camrot, rd, hp), counts=counts)
         # bg: differentiable (the fork optimises bg_color, mvs_points_volumetric_model.py:92-94)
         out = CompositeFn.apply(cspec, feat, bg)
+        self._train_conf_src = bufs
+        aux = _TrainAux()
         # rows of the point table this batch can give a gradient: the referenced
         # points, and point 0 (empty slots gather it in conf_coefficient) --
         # parallel.GradReducer reduces only these across ranks
         # (unique: pnr_used_points lists each referenced point once, ascending; the
-        # appended point 0 is dropped (-1) when it is already referenced)
-        u = used[0].long()
-        zero = torch.zeros(1, dtype=torch.long, device=dev)
-        if u.numel():
-            zero = torch.where(u[:1] == 0, zero - 1, zero)
-        self.last_train_aux = {"touched_rows": torch.cat([u, zero]), "touched_count": int(u.numel()) + 1}
+        # appended point 0 is dropped (-1) when it is already referenced).  Read
+        # when asked for (the used count is a host value).
+
+        def touched():
+            nu = counts.get()["n_used"]
+            u = used_buf[:nu].long()
+            zero = torch.zeros(1, dtype=torch.long, device=dev)
+            if nu:
+                zero = torch.where(u[:1] == 0, zero - 1, zero)
+            return {"touched_rows": torch.cat([u, zero]), "touched_count": nu + 1}
+
+        aux.lazy(("touched_rows", "touched_count"), touched)
         if self.keep_train_saved:
-            self.last_train_aux["saved"] = spec.saved
+            aux["saved"] = spec.saved
         if np_.points_conf is not None or self.wants_aux():
-            self.last_train_aux.update(self._march_aux(rays, qp, bufs, R, cnt["R_valid"], xyz, out[1]))
+            op = out[1]
+            aux.lazy(("weight", "blend_weight", "sample_pidx", "conf_coefficient"),
+                     lambda: self._march_aux(rays, qp, bufs, R, counts.get()["R_valid"], xyz, op))
+        self.last_train_aux = aux
         return out
 
     def wants_aux(self) -> bool:
@@ -753,24 +813,27 @@ class NeuralPointsRayMarching(nn.Module):
         conf, so the mean over the [1, R'', SR, K] entries equals
         sum_p count_p f(conf_p) / entries (count_p = entries gathering point p,
         point 0 also collecting the empty slots) -- same value and gradient
-        without the gather's scatter-add backward (point 0 alone receives most
-        of the empty-slot entries)."""
-        pidx = self.last_train_aux["sample_pidx"]
+        without the gather's scatter-add backward.  The counts come from the
+        query's own neighbour lists on the device (the R'' rays' filled samples
+        hold every non-negative entry of sample_pidx; the other
+        R'' * SR * K - sum_p count_p entries are empty slots, gathered as point 0):
+        no host read of R'' and no compaction."""
+        bufs = self._train_conf_src
         conf = self.neural_points.points_conf.reshape(-1)
-        ids = pidx.reshape(-1).long()
         N = conf.numel()
-        # entries per point (integers, exact in fp32), empty slots on point 0; no
-        # boolean indexing, so no host synchronisation: points with no entry
-        # contribute 0 * f(conf) (finite: conf is clamped) and no gradient.  The
-        # empty slots (most entries) are counted in 1024 spare bins first, not by
-        # atomics all on point 0.
-        spare = N + torch.arange(ids.numel(), device=ids.device) % 1024
-        counts = torch.zeros(N + 1024, dtype=torch.float32, device=conf.device)
-        counts.index_add_(0, torch.where(ids >= 0, ids, spare), torch.ones_like(ids, dtype=torch.float32))
-        counts = counts[:N] + torch.nn.functional.pad(counts[N:].sum().reshape(1), (0, N - 1))
+        SR, K = self.opt.SR, self.opt.K
+        ids = bufs.pidx.long()
+        c = bufs.counts
+        # entries of the filled samples (counts[0] of them, K each) that name a point
+        ok = (torch.arange(ids.numel(), device=ids.device) < c[0].long() * K) & (ids >= 0)
+        counts = torch.zeros(N, dtype=torch.float32, device=conf.device)
+        counts.index_add_(0, torch.where(ok, ids, torch.zeros_like(ids)), ok.float())   # integers: exact
+        entries = c[3].double() * (SR * K)
+        empty = (entries - counts.sum(dtype=torch.float64)).float()
+        counts[0:1] += empty
         cc = conf - (conf - torch.clamp(conf, 1e-4, 1.0)).detach()   # gradiant_clamp
         v = torch.clamp(cc, zero_epsilon, 1 - zero_epsilon)
-        return torch.sum(counts * (torch.log(v) + torch.log(1 - v))) / pidx.numel()
+        return (torch.sum(counts * (torch.log(v) + torch.log(1 - v))) / entries).float()
 
     @staticmethod
     def zero_one_loss(val, zero_epsilon: float = 1e-3):

@@ -69,7 +69,7 @@ def packed_bwd(agg, x3: bool = False):
 class Saved:
     """Device activations kept by pnr_aggregate_fwd_train (pnr_agg_saved)."""
 
-    def __init__(self, n_max: int, device):
+    def __init__(self, n_max: int, device, n_dev=None):
         n = max(int(n_max), 1)
         f = dict(dtype=torch.float32, device=device)
         P = n * 8
@@ -78,7 +78,7 @@ class Saved:
                       pe5=torch.empty((P, 64), **f), x3e=torch.empty((P, 32), **f), pa=torch.empty(P, **f),
                       wt=torch.empty(P, **f), wn=torch.empty(P, **f),
                       prow=torch.empty(P, dtype=torch.int32, device=device),
-                      hid=torch.zeros((n, 256), **f), vpe=torch.empty((n, 24), **f),
+                      hid=_rows_zeroed((n, 256), n_dev, device), vpe=torch.empty((n, 24), **f),
                       hc1=torch.empty((n, 128), **f), hc2=torch.empty((n, 128), **f),
                       hc3=torch.empty((n, 128), **f), vmask=torch.empty(n, dtype=torch.int32, device=device),
                       mask=torch.empty((P, 64), dtype=torch.int16, device=device))
@@ -86,6 +86,18 @@ class Saved:
 
     def __getitem__(self, k):
         return self.t[k]
+
+
+def _rows_zeroed(shape, n_dev, device):
+    """fp32 [rows, cols] whose first *n_dev rows are zero (pnr_zero_rows: the
+    device-counted part of a capacity-sized buffer, no host read), or all rows
+    zero when n_dev is None / 0.  Rows past the count are never read."""
+    if not n_dev:
+        return torch.zeros(shape, dtype=torch.float32, device=device)
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    L.check(L.lib().pnr_zero_rows(L.ptr(t), t.shape[1] * 4, L.c_void_p(n_dev), t.shape[0], L.stream_ptr(device)),
+            "pnr_zero_rows")
+    return t
 
 
 def used_points_device(bufs, K: int, n_points: int):
@@ -123,14 +135,16 @@ class AggSpec:
     """Non-tensor description of one aggregate call (structs + keep-alive)."""
 
     def __init__(self, agg, samples: L.Samples, n: int, pts_extra: dict, pair_mask=None, keep=(), used=None,
-                 x3: bool = False, h2: bool = False):
+                 x3: bool = False, h2: bool = False, counts=None):
         self.agg, self.samples, self.n = agg, samples, int(n)
+        self.counts = counts            # querier.CountsHandle: n / used are then capacities, the true
+                                        # counts on the device (read by the backward, never the forward)
         self.h2 = bool(h2)              # forward per-pair chain on pnr_aggregate_fwd_train_h2 (fp32h2, f16 MFMA)
         self.x3 = bool(x3) or self.h2   # per-pair chain on pnr_aggregate_fwd_train_x3 (fp32x3 split MFMA);
                                         # the backward's dX chain on fp32x3 with either forward
         self.h2_fallback = False        # an earlier h2 forward's range flag was found raised (that call ran
                                         # its native-fp32 fallback on the device)
-        self.used = used                # optional (used[int32], used_map[int32]) point subset
+        self.used = used                # optional (used[int32], used_map[int32][, n_used device count])
         self.pts_extra = pts_extra      # xyz / pers / campos / camrot pointers (no grad)
         self.pair_mask = pair_mask
         self.keep = keep
@@ -157,12 +171,14 @@ class AggregateFn(torch.autograd.Function):
         pts.rw2c = L.ptr(pe.get("rw2c"))   # per-point Rw2c [N,9] or None
         n_p1 = N
         if spec.used is not None:
-            used, used_map = spec.used
+            used, used_map = spec.used[:2]
             pts.used, pts.n_used, pts.used_map = used.data_ptr(), used.numel(), used_map.data_ptr()
+            if len(spec.used) > 2:   # device count: used.numel() is the capacity
+                pts.n_used_dev = spec.used[2].data_ptr()
             n_p1 = used.numel()
         mlp, keepw = agg.packed()
-        sv = Saved(n_max, dev)
-        feat = torch.zeros((max(n_max, 1), 129), dtype=torch.float32, device=dev)
+        sv = Saved(n_max, dev, n_dev=s.n_dev)
+        feat = _rows_zeroed((max(n_max, 1), 129), s.n_dev, dev)
         scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
         keepx = None
         run_x3 = spec.pair_mask is None and spec.x3
@@ -209,7 +225,13 @@ class AggregateFn(torch.autograd.Function):
         P = dict(zip(_PARAM_NAMES, params))
         dev = d_feat.device
         n = spec.n
-        n_max = int(spec.samples.n_max)
+        used_list = None if spec.used is None else spec.used[0]
+        if spec.counts is not None:   # the forward ran on device counts: read them now (no drain)
+            cnt = spec.counts.get()
+            n = cnt["S_valid"]
+            if used_list is not None:
+                used_list = used_list[:cnt["n_used"]]
+        n_max = n
         N = ctx.tabs[0].shape[0]
         slope = float(agg.neg_slope)
         d_feat = d_feat.contiguous()
@@ -238,7 +260,7 @@ class AggregateFn(torch.autograd.Function):
         Pn = max(n_max, 1) * 8
         dz1, dz2, dz3, dz4 = (torch.empty((Pn, 256), **f32) for _ in range(4))
         dpa = torch.empty(Pn, **f32)
-        used = None if spec.used is None else spec.used[0]
+        used = used_list
         n_p1 = N if used is None else used.numel()
         d_p1 = torch.zeros((max(n_p1, 1), 256), **f32)
         has_c, has_d, has_f = ctx.has
@@ -259,6 +281,9 @@ class AggregateFn(torch.autograd.Function):
                                                     ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(sv.c),
                                                     *bufs), "pnr_aggregate_bwd_pairs")
         m = n * 8
+        # weight gradients on f16 MFMA (pnr_gemm_tn_h2) with the fp32h2 forward;
+        # fp32x3 keeps the bf16x3 GEMMs
+        hg = L.H2Gemm(dev) if spec.h2 else None
         prow_sorted, pair_of = torch.sort(sv["prow"][:m], stable=True)
         pair_of = pair_of.to(torch.int32)
         L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1),
@@ -267,15 +292,16 @@ class AggregateFn(torch.autograd.Function):
         dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
         h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
         # dW = dZ^T X over all pairs: split-K MFMA GEMM (pnr_gemm_tn), bias = column sums
-        grads["block3.2.weight"], grads["block3.2.bias"] = L.gemm_tn(dz4, h3, colsum=True)
+        grads["block3.2.weight"], grads["block3.2.bias"] = L.gemm_tn(dz4, h3, colsum=True, h2=hg)
         gW3 = torch.empty((256, 263), **f32)
-        gW3[:, :256], grads["block3.0.bias"] = L.gemm_tn(dz3, h2, colsum=True)
-        gW3[:, 256:] = L.gemm_tn(dz3, sv["x3e"][:m])[:, :7]
+        am3 = hg.absmax(dz3) if hg is not None else None
+        gW3[:, :256], grads["block3.0.bias"] = L.gemm_tn(dz3, h2, colsum=True, h2=hg, a_absmax=am3)
+        gW3[:, 256:] = L.gemm_tn(dz3, sv["x3e"][:m], h2=hg, a_absmax=am3)[:, :7]
         grads["block3.0.weight"] = gW3
-        grads["block1.2.weight"], grads["block1.2.bias"] = L.gemm_tn(dz2, h1, colsum=True)
+        grads["block1.2.weight"], grads["block1.2.bias"] = L.gemm_tn(dz2, h1, colsum=True, h2=hg)
         dpa32 = torch.zeros((m, 32), **f32)      # M padded to one 32-row MFMA tile
         dpa32[:, 0] = dpa
-        grads["alpha_branch.0.weight"] = L.gemm_tn(dpa32, h4)[:1]
+        grads["alpha_branch.0.weight"] = L.gemm_tn(dpa32, h4, h2=hg)[:1]
         grads["alpha_branch.0.bias"] = dpa.sum(0, keepdim=True)
         # ---- block1.0: pair half from dz1 / PE_5, point half from dP1 / X1
         emb = ctx.tabs[0] if used is None else ctx.tabs[0].index_select(0, used.long()).contiguous()
@@ -283,8 +309,8 @@ class AggregateFn(torch.autograd.Function):
         x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
         L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
         gW1 = torch.empty((256, 284), **f32)
-        gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True)   # sum_p dP1 = sum_pairs dz1
-        gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m])[:, :60]
+        gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True, h2=hg)   # sum_p dP1 = sum_pairs dz1
+        gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m], h2=hg)[:, :60]
         grads["block1.0.weight"] = gW1
         dx1 = L.gemm_nn(d_p1, P["block1.0.weight"][:, :224])
         d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
@@ -342,10 +368,11 @@ class RgbHeadFn(torch.autograd.Function):
 
 
 class CompositeSpec:
-    def __init__(self, rays, qp, bufs, cp, R, SR, C, keep=()):
+    def __init__(self, rays, qp, bufs, cp, R, SR, C, keep=(), counts=None):
         self.rays, self.qp, self.bufs, self.cp = rays, qp, bufs, cp
         self.R, self.SR, self.C = R, SR, C
         self.keep = keep
+        self.counts = counts   # set: feat is capacity-sized, its rows counted on the device (counts[1])
 
 
 class CompositeFn(torch.autograd.Function):
@@ -381,7 +408,10 @@ class CompositeFn(torch.autograd.Function):
     def backward(ctx, d_color, _d_op, _d_bg, _d_mask):
         spec = ctx.spec
         dev = ctx.feat.device
-        d_feat = torch.zeros_like(ctx.feat)
+        if spec.counts is not None and ctx.feat.dim() == 2:   # zero only the device-counted rows
+            d_feat = _rows_zeroed(tuple(ctx.feat.shape), spec.bufs.counts.data_ptr() + 4, dev)
+        else:
+            d_feat = torch.zeros_like(ctx.feat)
         if d_color is None:
             return None, d_feat, None
         d_color = d_color.contiguous()

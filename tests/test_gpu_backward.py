@@ -337,6 +337,65 @@ def test_gemm_tn_vs_torch(cuda, K, M, N, x3):
         assert e3 <= 2 * e32 + 1e-12, (e3, e32)
 
 
+@pytest.mark.parametrize("scale", [1e-9, 1.0, 3e4])
+@pytest.mark.parametrize("K,M,N", [(235001, 256, 256), (4097, 256, 224), (37, 256, 32), (0, 128, 64),
+                                   (1000, 32, 64)])
+def test_gemm_tn_h2_vs_torch(cuda, K, M, N, scale):
+    """pnr_gemm_tn_h2 (f16-split MFMA, A scaled by its device max: the fp32h2
+    backward's weight gradients) against an fp64 GEMM at gradient-like (1e-9),
+    unit and large A magnitudes: within the fp32 tolerance, error within 8x
+    native fp32's, deterministic, the range flag down."""
+    from pointnerf_amd import _lib as L
+    g = torch.Generator(device=cuda).manual_seed(K + N + 7)
+    A = torch.randn((K, M), device=cuda, generator=g) * torch.rand((1, M), device=cuda, generator=g) * 3 * scale
+    B = torch.randn((K, N + 8), device=cuda, generator=g)[:, :N]        # ldb > N
+    hg = L.H2Gemm(cuda)
+    C, cs = L.gemm_tn(A, B, colsum=True, h2=hg)
+    ref64 = A.double().t() @ B.double()
+    close(C, ref64.float(), "C", rel=1e-4, scale=2e-6)
+    close(cs, A.double().sum(0).float(), "colsum", rel=1e-4, scale=2e-6)
+    assert torch.equal(C, L.gemm_tn(A, B, h2=hg))
+    assert int(hg.flag.item()) == 0
+    if K > 0:
+        eh = float((C.double() - ref64).abs().max())
+        e32 = float((L.gemm_tn(A, B, x3=False).double() - ref64).abs().max())
+        assert eh <= 8 * e32 + 1e-30, (eh, e32)
+
+
+def test_gemm_tn_h2_range_fallback(cuda):
+    """An operand outside the f16 split's range (|B| >= 2^15, a NaN-free stale
+    A max) raises the flag, and the call's x3 kernel recomputes the result:
+    equal to pnr_gemm_tn_x3's bit for bit."""
+    from pointnerf_amd import _lib as L
+    g = torch.Generator(device=cuda).manual_seed(3)
+    A = torch.randn((5000, 256), device=cuda, generator=g)
+    B = torch.randn((5000, 128), device=cuda, generator=g)
+    B[1234, 7] = 1e6
+    hg = L.H2Gemm(cuda)
+    C = L.gemm_tn(A, B, h2=hg)
+    assert int(hg.flag.item()) == 1
+    assert torch.equal(C, L.gemm_tn(A, B, x3=True))
+    # a stale (too small) A max: scaled |A| >= 8 -> fallback too
+    hg2 = L.H2Gemm(cuda)
+    small = torch.tensor([torch.tensor(1e-3).view(torch.int32).item()], dtype=torch.int32, device=cuda)
+    C2 = L.gemm_tn(A, B[:, :64].contiguous(), h2=hg2, a_absmax=small)
+    assert int(hg2.flag.item()) == 1
+    assert torch.equal(C2, L.gemm_tn(A, B[:, :64].contiguous(), x3=True))
+
+
+def test_absmax(cuda):
+    from pointnerf_amd import _lib as L
+    hg = L.H2Gemm(cuda)
+    for n in (0, 1, 3, 1000, 4 * 1024 * 256 * 3 + 5):
+        x = torch.randn(n, device=cuda)
+        want = float(x.abs().max()) if n else 0.0
+        got = hg.absmax(x).view(torch.float32).item()
+        assert got == want, (n, got, want)
+    x = torch.randn(1000, device=cuda)
+    x[17] = float("nan")
+    assert np.isnan(hg.absmax(x).view(torch.float32).item())
+
+
 @pytest.mark.parametrize("M,K,N,masked", [(30001, 128, 128, True), (129, 128, 256, False), (5, 256, 224, False),
                                           (0, 128, 128, True), (1000, 37, 64, True)])
 def test_gemm_nn_vs_torch(cuda, M, K, N, masked):
