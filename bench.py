@@ -36,8 +36,12 @@ FLOP_PER_SAMPLE = 137_216   # colour-branch GEMM FLOPs per valid sample
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA dense = vector peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
-PMC_FILES = {"fp32": "r01_fp32_pmc_aggregate.json", "fp32x3": "r01_pmc_aggregate_x3.json",
-             "fp32h2": "r03s3_final_pmc_aggregate_h2.json"}
+# committed PMC passes (tools/prof_bench.sh -> tools/profile_summary.py) per (config, dtype)
+PMC_FILES = {("headline", "fp32"): "r01_fp32_pmc_aggregate.json",
+             ("headline", "fp32x3"): "r01_pmc_aggregate_x3.json",
+             ("headline", "fp32h2"): "r03s3_final_pmc_aggregate_h2.json",
+             ("c5", "bf16"): "r04_c5_pmc_aggregate_bf16.json",
+             ("c4", "fp32h2"): "r04_c4_pmc_aggregate_h2.json"}
 
 
 def parse():
@@ -650,8 +654,9 @@ def main():
         # HBM bytes per aggregate launch from the committed PMC passes of this same command
         # (tools/prof_bench.sh -> tools/profile_summary.py; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", PMC_FILES.get(args.dtype, ""))
-        if args.config == "headline" and args.dtype in PMC_FILES and os.path.exists(pmc):
+        pmc_name = PMC_FILES.get((args.config, args.dtype))
+        pmc = os.path.join(ROOT, "profiles", pmc_name or "")
+        if pmc_name and os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
@@ -702,6 +707,7 @@ def main():
                                        "fp32h2": "fp32-equivalent: f16 MFMA dense peak / 3 products per fp32 MAC",
                                        "bf16": "bf16 MFMA dense peak"}[args.dtype],
                          "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "traffic_source": f"profiles/{pmc_name}" if traffic is not None else None,
                          "flops_per_launch": flops_per_launch, "avg_launch_ms": round(avg_agg_s * 1e3, 3),
                          "executed": executed_roofline(args, stage, launches, avg_agg_s)},
             "stages_ms": {k: round(float(np.mean(v)), 3) for k, v in per.items()},

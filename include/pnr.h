@@ -597,6 +597,12 @@ int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int
 int pnr_gemm_tn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
                    float* C, float* colsum_a, const uint32_t* a_absmax, int32_t* range_flag, void* scratch,
                    size_t scratch_bytes, void* stream);
+/* pnr_gemm_nn on f16-split MFMA (the fp32h2 arithmetic): A scaled by its device
+ * max (*a_absmax), three f16 products per 16-k step; operands outside the split's
+ * range set *range_flag and the fp32 kernel, launched behind, recomputes C. */
+int pnr_gemm_nn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K, int32_t N,
+                   const float* act, int64_t ld_act, float slope, float* C, int64_t ldc, const uint32_t* a_absmax,
+                   int32_t* range_flag, void* stream);
 /* *out_bits = float bits of max |x[0, n)| (NaN if any x is NaN); partials:
  * pnr_absmax_scratch_floats() device floats.  No host sync. */
 int pnr_absmax_scratch_floats(int64_t* out);

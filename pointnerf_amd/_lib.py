@@ -219,6 +219,8 @@ SIGNATURES = {
     "pnr_zero_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
     "pnr_gemm_tn_h2": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pnr_gemm_nn_h2": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int64,
+                               c_float, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "pnr_absmax_scratch_floats": (c_int, [P(c_int64)]),
     "pnr_absmax": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "pnr_weighted_colsum_scratch_floats": (c_int, [c_int32, P(c_int64)]),
@@ -349,16 +351,24 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = T
 
 
 def gemm_nn(A: torch.Tensor, B: torch.Tensor, act: torch.Tensor | None = None, slope: float = 0.0,
-            out: torch.Tensor | None = None):
+            out: torch.Tensor | None = None, h2: "H2Gemm | None" = None, a_absmax: torch.Tensor | None = None):
     """C = A B (A [M,K], B [K,N], unit column strides) on pnr_gemm_nn (exact fp32
-    products, fp32 MFMA); with act: C *= where(act > 0, 1, slope) (the LeakyReLU
-    derivative of the saved activation).  out: optional [M,N] destination view."""
+    products, fp32 MFMA) or, with h2, pnr_gemm_nn_h2 (fp32-accurate f16-split
+    MFMA, A's scale from a_absmax or a pnr_absmax pass); with act: C *=
+    where(act > 0, 1, slope) (the LeakyReLU derivative of the saved activation).
+    out: optional [M,N] destination view."""
     M, K = A.shape
     N = B.shape[1]
     assert B.shape[0] == K and A.stride(1) == 1 and B.stride(1) == 1
     assert act is None or (act.shape == (M, N) and act.stride(1) == 1)
     C = torch.empty((M, N), dtype=torch.float32, device=A.device) if out is None else out
     assert C.shape == (M, N) and C.stride(1) == 1
+    if h2 is not None:
+        am = a_absmax if a_absmax is not None else h2.absmax(A)
+        check(lib().pnr_gemm_nn_h2(ptr(A), A.stride(0), ptr(B), B.stride(0), M, K, N, ptr(act),
+                                   act.stride(0) if act is not None else 0, float(slope), ptr(C), C.stride(0),
+                                   ptr(am), ptr(h2.flag), stream_ptr(A.device)), "pnr_gemm_nn_h2")
+        return C
     check(lib().pnr_gemm_nn(ptr(A), A.stride(0), ptr(B), B.stride(0), M, K, N, ptr(act),
                             act.stride(0) if act is not None else 0, float(slope), ptr(C), C.stride(0),
                             stream_ptr(A.device)), "pnr_gemm_nn")

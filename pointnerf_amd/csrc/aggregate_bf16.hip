@@ -354,20 +354,24 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
         *reinterpret_cast<uint2*>(Xb + col * kPB + 60) = make_uint2(0u, 0u);   // rows 60..63: k padding
       }
-      // 5-band PE of the rotated distance -> rows 2e, 2e+1 (e = 5 ch + f); role r: e = r (mod 2)
+      // 5-band PE of the rotated distance -> rows 2e, 2e+1 (e = 5 ch + f); role r:
+      // channels 3r .. 3r + 2.  One sincosf per channel, the higher bands by angle
+      // doubling (k_point_pre_b's PE_3): <= ~16 ulp at band 4, far below the bf16
+      // rounding of the MFMA operands.
       uint16_t* xc = Xb + col * kPB;
-#pragma unroll 1
-      for (int e = role; e < 30; e += 2) {
-        const int ch = e / 5, f = e - 5 * ch;
-        float dc = dr6[0];
-        dc = ch == 1 ? dr6[1] : dc;
-        dc = ch == 2 ? dr6[2] : dc;
-        dc = ch == 3 ? dr6[3] : dc;
-        dc = ch == 4 ? dr6[4] : dc;
-        dc = ch == 5 ? dr6[5] : dc;
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        const int ch = 3 * role + cc;
+        const float dc = role == 0 ? dr6[cc] : dr6[3 + cc];
         float sn, cs;
-        sincosf(dc * (float)(1 << f), &sn, &cs);
-        *reinterpret_cast<unsigned*>(xc + 2 * e) = pack_bf16x2(sn, cs);
+        sincosf(dc, &sn, &cs);
+#pragma unroll
+        for (int f = 0; f < 5; ++f) {
+          *reinterpret_cast<unsigned*>(xc + 2 * (5 * ch + f)) = pack_bf16x2(sn, cs);
+          const float s2 = 2.f * sn * cs, c2 = (cs - sn) * (cs + sn);
+          sn = s2;
+          cs = c2;
+        }
       }
     }
     __syncthreads();

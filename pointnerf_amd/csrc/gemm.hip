@@ -542,10 +542,14 @@ struct GemmNNArgs {
   int64_t M;
   int K, N;
   float slope;
+  const uint32_t* a_absmax;   // h2: bits of max |A|
+  int32_t* range_flag;        // h2: operand outside the f16 split's range
+  const int32_t* run_if;      // fp32: run only when *run_if != 0 (the h2 call's fallback)
 };
 
 template <int NT, int WM>
 __global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
+  if (g.run_if && *g.run_if == 0) return;   // guarded fallback of an h2 call whose operands fit
   constexpr int WN = 8 / WM;               // waves along N
   constexpr int NW = (NT + WN - 1) / WN;   // column tiles per wave (at most)
   constexpr int ROWS = 32 * WM;
@@ -623,6 +627,136 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
   }
 }
 
+// h2 variant (pnr_gemm_nn_h2): the same C = A B (x LeakyReLU derivative) on
+// f16-split MFMA -- A scaled by 2^e (max |A| 2^e in [4, 8), from *a_absmax),
+// both operands split x = xh + 2^-11 xl, C = 2^-(e+11) ((2^11 Ah) Bh + Ah Bl +
+// Al Bh): three v_mfma_f32_32x32x16_f16 per 16-k step where the fp32 kernel
+// issues eight v_mfma_f32_32x32x2_f32 of 64 cycles.  A workgroup owns 128 rows
+// (wave w: row tile w % 4, column tiles w / 4 + 2u); per 16-k chunk its A rows
+// ([row][k]) and B's columns ([n][k], the transpose staged on the fly) are split
+// into two f16 planes each, double-buffered in LDS (2 x 37 KB).  Out-of-range
+// operands (|B| >= 2^15, a stale max, NaN / inf) raise range_flag; the caller
+// launches the fp32 kernel behind it with run_if = range_flag.
+constexpr int kNHRows = 128;
+constexpr int kNHPlaneA = kNHRows * kXPitch;   // f16 per A plane
+constexpr int kNHPlaneB = 256 * kXPitch;       // f16 per B plane
+constexpr size_t kNHLds = 2 * (2 * (size_t)kNHPlaneA + 2 * (size_t)kNHPlaneB) * 2;
+
+template <int NT>
+__global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t nlds[];
+  constexpr int NW = (NT + 1) / 2;   // column tiles per wave (waves 0-3: even tiles, 4-7: odd)
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * kNHRows;
+  const int wm = wid & 3, wn = wid >> 2;
+  int e = 0;
+  {
+    const float amax = __uint_as_float(*g.a_absmax);
+    if (amax > 0.f && amax <= 3.0e38f) {
+      int x;
+      frexpf(amax, &x);
+      e = 3 - x;
+    }
+  }
+  const float sa = ldexpf(1.f, e);
+  bool bad = false;
+  // staging roles -- A: row tid >> 2, k (tid & 3) * 4 .. +3; B: column tid & 255, k 8 (tid >> 8) .. +7
+  const int ar = tid >> 2, ak = (tid & 3) * 4;
+  const int bn = tid & 255, bk = 8 * (tid >> 8);
+  const bool stB = bn < g.N;
+  float4 va;
+  float vb[8];
+  auto load = [&](int k0) {
+    const int64_t gr = row0 + ar;
+    const int kk = k0 + ak;
+    if (gr < g.M && kk + 3 < g.K) {
+      const float* src = g.A + gr * g.lda + kk;
+      va = (((uintptr_t)src & 15) == 0) ? *reinterpret_cast<const float4*>(src)
+                                         : make_float4(src[0], src[1], src[2], src[3]);
+    } else {
+      const float* src = g.A + (gr < g.M ? gr : 0) * g.lda;
+      va.x = gr < g.M && kk < g.K ? src[kk] : 0.f;
+      va.y = gr < g.M && kk + 1 < g.K ? src[kk + 1] : 0.f;
+      va.z = gr < g.M && kk + 2 < g.K ? src[kk + 2] : 0.f;
+      va.w = gr < g.M && kk + 3 < g.K ? src[kk + 3] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = k0 + bk + j;
+      vb[j] = stB && r < g.K ? g.B[(int64_t)r * g.ldb + bn] : 0.f;
+    }
+  };
+  auto put = [&](int buf) {
+    uint16_t* pa = nlds + (size_t)buf * (2 * kNHPlaneA + 2 * kNHPlaneB);
+    uint16_t* pb = pa + 2 * kNHPlaneA;
+    const float a0 = va.x * sa, a1 = va.y * sa, a2 = va.z * sa, a3 = va.w * sa;
+    bool ok = fabsf(a0) < 8.f && fabsf(a1) < 8.f && fabsf(a2) < 8.f && fabsf(a3) < 8.f;
+    unsigned h0, l0, h1, l1;
+    splith(a0, a1, h0, l0);
+    splith(a2, a3, h1, l1);
+    *reinterpret_cast<uint2*>(pa + ar * kXPitch + ak) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(pa + kNHPlaneA + ar * kXPitch + ak) = make_uint2(l0, l1);
+    uint4 bh, bl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ok = ok && fabsf(vb[2 * q]) < 32768.f && fabsf(vb[2 * q + 1]) < 32768.f;
+      unsigned x0, x1;
+      splith(vb[2 * q], vb[2 * q + 1], x0, x1);
+      reinterpret_cast<unsigned*>(&bh)[q] = x0;
+      reinterpret_cast<unsigned*>(&bl)[q] = x1;
+    }
+    *reinterpret_cast<uint4*>(pb + bn * kXPitch + bk) = bh;
+    *reinterpret_cast<uint4*>(pb + kNHPlaneB + bn * kXPitch + bk) = bl;
+    bad = bad || !ok;
+  };
+  f32x16 acc[NW];
+#pragma unroll
+  for (int u = 0; u < NW; ++u) acc[u] = (f32x16){0.f};
+  load(0);
+  put(0);
+  __syncthreads();
+  int it = 0;
+  for (int k0 = 0; k0 < g.K; k0 += 16, ++it) {
+    const int buf = it & 1;
+    const bool more = k0 + 16 < g.K;
+    if (more) load(k0 + 16);
+    const uint16_t* pa = nlds + (size_t)buf * (2 * kNHPlaneA + 2 * kNHPlaneB);
+    const uint16_t* pb = pa + 2 * kNHPlaneA;
+    const uint4 ah = *reinterpret_cast<const uint4*>(pa + (32 * wm + c) * kXPitch + 8 * h);
+    const uint4 al = *reinterpret_cast<const uint4*>(pa + kNHPlaneA + (32 * wm + c) * kXPitch + 8 * h);
+    const uint4 as = f16x8_scale2048(ah);
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int t = wn + 2 * u;
+      if (t >= NT) continue;
+      const uint4 bh = *reinterpret_cast<const uint4*>(pb + (32 * t + c) * kXPitch + 8 * h);
+      const uint4 bl = *reinterpret_cast<const uint4*>(pb + kNHPlaneB + (32 * t + c) * kXPitch + 8 * h);
+      acc[u] = mfma_f16(al, bh, acc[u]);   // smallest terms first
+      acc[u] = mfma_f16(ah, bl, acc[u]);
+      acc[u] = mfma_f16(as, bh, acc[u]);
+    }
+    if (more) put(buf ^ 1);
+    __syncthreads();
+  }
+  if (bad) atomicOr(g.range_flag, 1);
+  const float unscale = ldexpf(1.f, -(e + 11));
+  // C/D layout: row = (r&3) + 8(r>>2) + 4h (the A rows), col = c
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t m = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int t = wn + 2 * u;
+      if (t >= NT) continue;
+      const int n = 32 * t + c;
+      float v = acc[u][r] * unscale;
+      if (g.act != nullptr && !(g.act[m * g.ld_act + n] > 0.f)) v *= g.slope;
+      g.C[m * g.ldc + n] = v;
+    }
+  }
+}
+
 template <int NT>
 static void launch_gemm_nn(const GemmNNArgs& g, hipStream_t st) {
   // long M: 128-row workgroups, two per CU (<= 128 VGPRs, 54 KB LDS; measured
@@ -641,9 +775,9 @@ static void launch_gemm_nn(const GemmNNArgs& g, hipStream_t st) {
 
 using namespace pnr;
 
-extern "C" int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
-                           int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
-                           void* stream) {
+static int gemm_nn_impl(bool h2, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
+                        int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
+                        const uint32_t* a_absmax, int32_t* range_flag, void* stream) {
   PNR_CHECK_ARG(M == 0 || (A && B && C), "gemm_nn: null pointer");
   PNR_CHECK_ARG(M >= 0 && K > 0 && N > 0 && N % 32 == 0 && N <= 32 * kGMaxNT, "gemm_nn: N must be a multiple of 32 "
                 "in [32, 256], K > 0");
@@ -662,7 +796,35 @@ extern "C" int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t 
   g.K = K;
   g.N = N;
   g.slope = slope;
+  g.a_absmax = a_absmax;
+  g.range_flag = range_flag;
+  g.run_if = nullptr;
   hipStream_t st = as_stream(stream);
+  if (h2) {
+    static bool attr = false;
+    if (!attr) {
+#define PNR_NNH2_ATTR(T)                                                                                  \
+  PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nn_h2<T>),                          \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNHLds));
+      PNR_NNH2_ATTR(1) PNR_NNH2_ATTR(2) PNR_NNH2_ATTR(3) PNR_NNH2_ATTR(4)
+      PNR_NNH2_ATTR(5) PNR_NNH2_ATTR(6) PNR_NNH2_ATTR(7) PNR_NNH2_ATTR(8)
+#undef PNR_NNH2_ATTR
+      attr = true;
+    }
+    const dim3 grid((unsigned)cdiv(M, (int64_t)kNHRows));
+    switch (N / 32) {
+      case 1: hipLaunchKernelGGL(k_gemm_nn_h2<1>, grid, dim3(512), kNHLds, st, g); break;
+      case 2: hipLaunchKernelGGL(k_gemm_nn_h2<2>, grid, dim3(512), kNHLds, st, g); break;
+      case 3: hipLaunchKernelGGL(k_gemm_nn_h2<3>, grid, dim3(512), kNHLds, st, g); break;
+      case 4: hipLaunchKernelGGL(k_gemm_nn_h2<4>, grid, dim3(512), kNHLds, st, g); break;
+      case 5: hipLaunchKernelGGL(k_gemm_nn_h2<5>, grid, dim3(512), kNHLds, st, g); break;
+      case 6: hipLaunchKernelGGL(k_gemm_nn_h2<6>, grid, dim3(512), kNHLds, st, g); break;
+      case 7: hipLaunchKernelGGL(k_gemm_nn_h2<7>, grid, dim3(512), kNHLds, st, g); break;
+      default: hipLaunchKernelGGL(k_gemm_nn_h2<8>, grid, dim3(512), kNHLds, st, g); break;
+    }
+    PNR_LAUNCH_CHECK();
+    g.run_if = range_flag;   // the fp32 kernel below recomputes C only when the flag is up
+  }
   switch (N / 32) {
     case 1: launch_gemm_nn<1>(g, st); break;
     case 2: launch_gemm_nn<2>(g, st); break;
@@ -675,6 +837,19 @@ extern "C" int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t 
   }
   PNR_LAUNCH_CHECK();
   return PNR_OK;
+}
+
+extern "C" int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
+                           int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
+                           void* stream) {
+  return gemm_nn_impl(false, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, nullptr, nullptr, stream);
+}
+
+extern "C" int pnr_gemm_nn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
+                              int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
+                              const uint32_t* a_absmax, int32_t* range_flag, void* stream) {
+  PNR_CHECK_ARG(a_absmax && range_flag, "gemm_nn_h2: a_absmax and range_flag required");
+  return gemm_nn_impl(true, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, a_absmax, range_flag, stream);
 }
 
 

@@ -309,10 +309,11 @@ class AggregateFn(torch.autograd.Function):
         x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
         L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
         gW1 = torch.empty((256, 284), **f32)
-        gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True, h2=hg)   # sum_p dP1 = sum_pairs dz1
+        am_p1 = hg.absmax(d_p1) if hg is not None and n_p1 > 0 else None
+        gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True, h2=hg, a_absmax=am_p1)   # sum_p dP1 = sum_pairs dz1
         gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m], h2=hg)[:, :60]
         grads["block1.0.weight"] = gW1
-        dx1 = L.gemm_nn(d_p1, P["block1.0.weight"][:, :224])
+        dx1 = L.gemm_nn(d_p1, P["block1.0.weight"][:, :224], h2=hg, a_absmax=am_p1)
         d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
         L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb_u), L.stream_ptr(dev)),
                 "pnr_point_pe3_bwd")

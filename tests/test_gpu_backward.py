@@ -383,6 +383,39 @@ def test_gemm_tn_h2_range_fallback(cuda):
     assert torch.equal(C2, L.gemm_tn(A, B[:, :64].contiguous(), x3=True))
 
 
+@pytest.mark.parametrize("scale", [1e-9, 1.0])
+@pytest.mark.parametrize("M,K,N,masked", [(200001, 256, 224, False), (30001, 128, 128, True), (5, 256, 224, False),
+                                          (0, 128, 128, True), (1000, 37, 64, True)])
+def test_gemm_nn_h2_vs_torch(cuda, M, K, N, masked, scale):
+    """pnr_gemm_nn_h2 (the fp32h2 backward's dX1 = dP1 W1[:, :224]) against an
+    fp64 product, at gradient-like and unit A magnitudes: within the fp32
+    tolerance, error within 8x the fp32 kernel's, the range flag down; a B
+    entry >= 2^15 raises it and the fp32 kernel's result comes back."""
+    from pointnerf_amd import _lib as L
+    g = torch.Generator(device=cuda).manual_seed(M + K)
+    A = torch.randn((M, K), device=cuda, generator=g) * scale
+    W = torch.randn((K, N + 32), device=cuda, generator=g) * 0.1
+    B = W[:, :N]                                     # ldb > N
+    act = torch.randn((M, N), device=cuda, generator=g) if masked else None
+    hg = L.H2Gemm(cuda)
+    C = L.gemm_nn(A, B, act=act, slope=0.01, h2=hg)
+    ref = A.double() @ B.double()
+    if masked:
+        ref = torch.where(act.double() > 0, ref, ref * 0.01)
+    close(C, ref.float(), "C", rel=1e-4, scale=2e-6)
+    assert int(hg.flag.item()) == 0
+    if M > 0:
+        eh = float((C.double() - ref).abs().max())
+        e32 = float((L.gemm_nn(A, B, act=act, slope=0.01).double() - ref).abs().max())
+        assert eh <= 8 * e32 + 1e-30, (eh, e32)
+        W2 = W.clone()
+        W2[0, 3] = 1e6
+        hg2 = L.H2Gemm(cuda)
+        C2 = L.gemm_nn(A, W2[:, :N], act=act, slope=0.01, h2=hg2)
+        assert int(hg2.flag.item()) == 1
+        assert torch.equal(C2, L.gemm_nn(A, W2[:, :N], act=act, slope=0.01))
+
+
 def test_absmax(cuda):
     from pointnerf_amd import _lib as L
     hg = L.H2Gemm(cuda)
@@ -566,3 +599,38 @@ def test_render_train_xyz_grad_vs_oracle(cuda, train_precision, rw):
         return
     close(got.float(), r32.float(), "d xyz", scale=5e-5)
     assert e <= 2.0 * e32 + 1e-6 * big, (e, e32, big)
+
+
+@pytest.mark.parametrize("train_precision", ["fp32x3", "fp32h2"])
+def test_train_forward_does_not_wait_for_gpu(cuda, train_precision):
+    """render_rays_train + the loss (incl. the zero-one conf loss) are enqueued
+    without a host read: they return while a ~0.3 s spin kernel queued before
+    them is still running; the backward then reads the counts from the pinned
+    copy, and the step's gradients equal those of a step with no spin."""
+    from pointnerf_amd import _lib as L
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    params = formula_params(salt=0.3)
+    campos = torch.from_numpy(sc["campos"]).to(cuda)
+    camrot = torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda)
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    grads = []
+    for spin in (False, True):
+        m = _train_model(sc, cuda, params)
+        m.train_precision = train_precision
+        m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0].sum().backward()   # warm: packs, allocations
+        m.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        if spin:
+            probe = torch.zeros(1, device=cuda)
+            L.check(L.lib().pnr_clock_probe(L.ptr(probe), 1200000, L.stream_ptr(cuda)), "pnr_clock_probe")
+            ev = torch.cuda.Event()
+            ev.record()
+        color = m.render_rays_train(campos, camrot, rd, 2.0, 6.0, bg)[0]
+        loss = (color ** 2).mean() + 1e-4 * m.zero_one_conf_loss()
+        if spin:
+            assert not ev.query(), "the training forward waited for the GPU"
+        loss.backward()
+        grads.append([p.grad.clone() for p in m.parameters() if p.grad is not None])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)

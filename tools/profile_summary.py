@@ -56,14 +56,19 @@ def main():
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
     json.dump(bench, open(os.path.join(prof, f"{tag}_bench.json"), "w"), indent=1)
-    stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv")))}
+    # summed over a kernel's template instances (k_pairs_b<1/2/4/8>: one dispatch per bucket)
+    stats = collections.defaultdict(lambda: {"Calls": 0, "TotalDurationNs": 0.0})
+    for r in csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv"))):
+        st = stats[short(r["Name"])]
+        st["Calls"] = max(st["Calls"], int(r["Calls"]))
+        st["TotalDurationNs"] += float(r["TotalDurationNs"])
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), {"FETCH_SIZE"})
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), {"WRITE_SIZE"})
     mfma = per_kernel(os.path.join(src, "mfma", "run_counter_collection.csv"),
                       {"SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", MOPS[dtype]})
     out = {"source": "tools/prof_bench.sh -> tools/profile_summary.py", "dtype": dtype, "kernels": {}}
     tot_bytes, tot_ns = 0.0, 0.0
-    launches = max(int(stats[AGG[-1]]["Calls"]), 1)
+    launches = max(int(stats[AGG[-1]]["Calls"]), 1) if AGG[-1] in stats else 1
     for k in AGG:
         if k not in stats:
             continue
