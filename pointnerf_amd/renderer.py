@@ -825,9 +825,12 @@ class NeuralPointsRayMarching(nn.Module):
         ids = bufs.pidx.long()
         c = bufs.counts
         # entries of the filled samples (counts[0] of them, K each) that name a point
-        ok = (torch.arange(ids.numel(), device=ids.device) < c[0].long() * K) & (ids >= 0)
-        counts = torch.zeros(N, dtype=torch.float32, device=conf.device)
-        counts.index_add_(0, torch.where(ok, ids, torch.zeros_like(ids)), ok.float())   # integers: exact
+        pos = torch.arange(ids.numel(), device=ids.device)
+        ok = (pos < c[0].long() * K) & (ids >= 0)
+        # the other entries land in 1024 spare bins (no atomics piling on one address)
+        counts = torch.zeros(N + 1024, dtype=torch.float32, device=conf.device)
+        counts.index_add_(0, torch.where(ok, ids, N + pos % 1024), ok.float())   # integers: exact
+        counts = counts[:N]
         entries = c[3].double() * (SR * K)
         empty = (entries - counts.sum(dtype=torch.float64)).float()
         counts[0:1] += empty

@@ -402,7 +402,8 @@ def test_gemm_nn_h2_vs_torch(cuda, M, K, N, masked, scale):
     ref = A.double() @ B.double()
     if masked:
         ref = torch.where(act.double() > 0, ref, ref * 0.01)
-    close(C, ref.float(), "C", rel=1e-4, scale=2e-6)
+    if M > 0:
+        close(C, ref.float(), "C", rel=1e-4, scale=2e-6)
     assert int(hg.flag.item()) == 0
     if M > 0:
         eh = float((C.double() - ref).abs().max())
@@ -631,6 +632,9 @@ def test_train_forward_does_not_wait_for_gpu(cuda, train_precision):
         if spin:
             assert not ev.query(), "the training forward waited for the GPU"
         loss.backward()
-        grads.append([p.grad.clone() for p in m.parameters() if p.grad is not None])
-    for a, b in zip(*grads):
-        assert torch.equal(a, b)
+        grads.append([(n, p.grad.clone()) for n, p in m.named_parameters() if p.grad is not None])
+    for (n, a), (_, b) in zip(*grads):
+        if n.startswith("aggregator."):   # block-ordered GEMMs: bitwise
+            assert torch.equal(a, b), n
+        else:                             # point tables: float-atomic sums over pairs
+            assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max()), n
