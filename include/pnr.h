@@ -432,6 +432,9 @@ typedef struct {
   uint16_t* mask;  /* [n_max*8,64] LeakyReLU derivative bits of the four 256-wide layers
                       (layer l, tile T, lane half h: word 16l + 2T + h; bit r = pre-activation
                       of MFMA accumulator register r > 0), read by the backward            */
+  uint32_t* dz_absmax; /* optional [5]: pnr_aggregate_bwd_pairs(_x3) max-es |dz1..dz4| and
+                      |dpa| into it (float bits, atomic; the caller zeroes it): the scales
+                      of pnr_gemm_tn_h2 without a pnr_absmax pass (ABI 19)               */
 } pnr_agg_saved;
 
 /* Transposed weights for the backward GEMMs, fragment-packed like pnr_mlp
@@ -510,7 +513,9 @@ int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev, int32_t K
  * (or p when used_map is NULL); rows of points without pairs are not written;
  * negative point rows (empty pairs) are skipped. */
 int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,
-                        const int32_t* used_map, float* d_p1, void* stream);
+                        const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax, void* stream);
+/* d_p1_absmax (optional, ABI 19): max |d_p1| as float bits, atomically max-ed
+ * (the caller zeroes it) -- pnr_gemm_tn_h2 / pnr_gemm_nn_h2's scale for d_p1. */
 /* Device weight packing (aggregator.py frag_pack / frag_pack_x3, one launch per
  * matrix): kind 0 = fp32 fragments F[t][T][lane] = W'[32T + (lane & 31)][2t + (lane >> 5)],
  * ceil(cols / 2) + pad_steps k-steps; kind 1 = fp32x3 split-bf16 fragments

@@ -117,7 +117,7 @@ class CompositeParams(ctypes.Structure):
 
 class AggSaved(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("h1", "h2", "h3", "h4", "pe5", "x3e", "pa", "wt", "wn", "prow", "hid",
-                                        "vpe", "hc1", "hc2", "hc3", "vmask", "mask")]
+                                        "vpe", "hc1", "hc2", "hc3", "vmask", "mask", "dz_absmax")]
 
 
 class MlpX3(ctypes.Structure):
@@ -193,7 +193,7 @@ SIGNATURES = {
     "pnr_used_points_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
     "pnr_used_points": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_size_t, c_void_p]),
-    "pnr_pairs_to_points": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_pairs_to_points": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_pack_weights_h2": (c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32, c_int32,
                                     c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_pack_weights_h2_dev": (c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,

@@ -860,6 +860,14 @@ struct BwdArgs {
 constexpr int kBwdLdsFloats = 66 * kQP + 4 * kTP /*dot parts*/ + 4 * 7 * kTP /*extras parts*/;
 constexpr size_t kBwdLdsBytes = (size_t)kBwdLdsFloats * sizeof(float);
 
+// max |v| over a wave's lanes into an LDS slot (float bits compared as unsigned:
+// a NaN's bits exceed every finite and infinite value, so it propagates).
+__device__ __forceinline__ void wave_absmax_to(unsigned* slot, unsigned mb) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+  if ((threadIdx.x & 63) == 0 && mb) atomicMax(slot, mb);
+}
+
 // acc-layout float4 of a [pair][256] array for (half pt, tile T, quad q)
 __device__ __forceinline__ float4 ld_q(const float* base, int64_t pair, int T, int q, int h) {
   return *reinterpret_cast<const float4*>(base + pair * kHid + 32 * T + 8 * q + 4 * h);
@@ -885,8 +893,10 @@ __device__ __forceinline__ void store_q(const f32x16 (&acc)[PT * NT], float* X, 
 // slope >= 0); writes dz back into acc and to dst rows of active pairs.
 template <int NT, int PT>
 __device__ __forceinline__ void lrelu_bwd_q(f32x16 (&acc)[PT * NT], const float* h_saved, float* dst,
-                                            int64_t tile, int64_t n, float slope, int lane, int T0) {
+                                            int64_t tile, int64_t n, float slope, int lane, int T0,
+                                            unsigned* amx = nullptr) {
   const int c = lane & 31, h = lane >> 5;
+  unsigned mb = 0;
 #pragma unroll
   for (int pt = 0; pt < PT; ++pt) {
     const int col = 32 * pt + c;
@@ -906,8 +916,13 @@ __device__ __forceinline__ void lrelu_bwd_q(f32x16 (&acc)[PT * NT], const float*
         if (act)
           *reinterpret_cast<float4*>(dst + pair * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
               make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        if (amx) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mb = max(mb, __float_as_uint(fabsf(v[4 * q + i])));
+        }
       }
   }
+  if (amx) wave_absmax_to(amx, mb);
 }
 
 // dz = dh * lrelu'(z) from the saved derivative bits (words prefetched by
@@ -928,8 +943,10 @@ __device__ __forceinline__ void load_masks(unsigned (&mk)[PT * NT], const uint16
 
 template <int NT, int PT>
 __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsigned (&mk)[PT * NT], float* dst,
-                                            int64_t tile, int64_t n, float slope, int lane, int T0) {
+                                            int64_t tile, int64_t n, float slope, int lane, int T0,
+                                            unsigned* amx = nullptr) {
   const int c = lane & 31, h = lane >> 5;
+  unsigned mb = 0;
 #pragma unroll
   for (int pt = 0; pt < PT; ++pt) {
     const int col = 32 * pt + c;
@@ -947,8 +964,13 @@ __device__ __forceinline__ void lrelu_bwd_m(f32x16 (&acc)[PT * NT], const unsign
           *reinterpret_cast<float4*>(dst + pair * kHid + 32 * (T0 + T) + 8 * q + 4 * h) =
               make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
       }
+      if (amx) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mb = max(mb, __float_as_uint(fabsf(v[r])));
+      }
     }
   }
+  if (amx) wave_absmax_to(amx, mb);
 }
 
 // ---- fp32x3 dX GEMMs of k_pairs_bwd<true>: the transposed weights as exact
@@ -1056,6 +1078,11 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   const int xvoff = (T0 * 3 * 64 + lane) * 16;
   const __amdgpu_buffer_rsrc_t x4 = x3q_rsrc(A.wx[0]), x3 = x3q_rsrc(A.wx[1]), x2 = x3q_rsrc(A.wx[2]);
   if constexpr (!X3) prime_q<kNTW>(ring, w4t, lane);
+  // max |dz1..dz4|, |dpa| of this workgroup (pnr_agg_saved.dz_absmax: pnr_gemm_tn_h2's scales)
+  __shared__ unsigned amx[5];
+  unsigned* const am = A.sv.dz_absmax ? amx : nullptr;
+  if (threadIdx.x < 5) amx[threadIdx.x] = 0u;
+  __syncthreads();
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // ---------------------------------------------------------- per-pair scalars (lane = pair)
@@ -1078,6 +1105,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     }
     const float dpa = dalpha * wt * sig;   // d alpha_s / d pa_k
     if (wid == 0 && active) A.dpa[pair] = dpa;
+    if (am && wid == 0) wave_absmax_to(am + 4, active ? __float_as_uint(fabsf(dpa)) : 0u);
     // ---------------------------------------------------------- d h4 -> dz4 (acc layout)
     f32x16 acc[kPTW * kNTW];
     float dot[kPTW];
@@ -1110,7 +1138,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       dotp[wid * kTP + c] = dot[0];
       dotp[wid * kTP + 32 + c] = dot[1];
     }
-    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h4, A.dz[3], tile, n, slope, lane, T0);
+    lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h4, A.dz[3], tile, n, slope, lane, T0, am ? am + 3 : nullptr);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     __syncthreads();
     // d wt_k = d alpha_s a_k + <d f_s, h4_k>  ->  d conf_k (straight-through clamp, :724-726)
@@ -1134,7 +1162,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       prime_q<kNTW>(ring, w3t, lane);
     }
     __syncthreads();
-    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[2], tile, n, slope, lane, T0);
+    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[2], tile, n, slope, lane, T0, am ? am + 2 : nullptr);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
     // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
@@ -1207,7 +1235,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       prime_q<kNTW>(ring, w2t, lane);
     }
     __syncthreads();
-    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[1], tile, n, slope, lane, T0);
+    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[1], tile, n, slope, lane, T0, am ? am + 1 : nullptr);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
     __syncthreads();
     // ---------------------------------------------------------- block1.2^T: dh1 = W2^T dz2
@@ -1220,7 +1248,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
       prime_q<kNTW>(ring, w4t, lane);   // the next tile
     }
-    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[0], tile, n, slope, lane, T0);
+    lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[0], tile, n, slope, lane, T0, am ? am + 0 : nullptr);
     // block1.0 point half: d P1[p] += dz1 (the P1 gather's backward).  dz1 goes
     // through LDS so each pair's 1-KB row is added with 4 coalesced 256-B
     // atomic wave instructions (wave w: pairs 16w..16w+15, lane = neuron).
@@ -1242,6 +1270,10 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       }
     }
     __syncthreads();
+  }
+  if (am) {   // one global max per workgroup and array
+    __syncthreads();
+    if (threadIdx.x < 5 && amx[threadIdx.x]) atomicMax(A.sv.dz_absmax + threadIdx.x, amx[threadIdx.x]);
   }
 }
 
@@ -1320,9 +1352,13 @@ __global__ void k_used_list(const int32_t* __restrict__ flags, int64_t n_points,
 // equal rows, lane = 4 neurons (float4).
 __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const int32_t* __restrict__ pair_of,
                                   int64_t P, const float* __restrict__ dz1, const int32_t* __restrict__ used_map,
-                                  float* __restrict__ d_p1) {
+                                  float* __restrict__ d_p1, uint32_t* __restrict__ absmax) {
   const int lane = threadIdx.x & 63;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  __shared__ unsigned bmax;
+  if (threadIdx.x == 0) bmax = 0u;
+  __syncthreads();
+  unsigned mb = 0u;   // max |d_p1| of this lane's rows (float bits: NaN propagates)
   for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
     const int32_t pr = prow_sorted[i];
     if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
@@ -1335,6 +1371,13 @@ __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const
       s.w += v.w;
     }
     reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
+    mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
+             max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
+  }
+  if (absmax) {
+    wave_absmax_to(&bmax, mb);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax) atomicMax(absmax, bmax);
   }
 }
 
@@ -1978,12 +2021,12 @@ extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev
 }
 
 extern "C" int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,
-                                   const int32_t* used_map, float* d_p1, void* stream) {
+                                   const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax, void* stream) {
   PNR_CHECK_ARG(P >= 0 && (P == 0 || (prow_sorted && pair_of && dz1 && d_p1)), "pairs_to_points: bad args");
   PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1) & 15) == 0, "pairs_to_points: rows must be 16-B aligned");
   if (P == 0) return PNR_OK;
   hipLaunchKernelGGL(k_pairs_to_points, dim3(grid_for(P, 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
-                     pair_of, P, dz1, used_map, d_p1);
+                     pair_of, P, dz1, used_map, d_p1, d_p1_absmax);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

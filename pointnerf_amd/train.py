@@ -81,8 +81,13 @@ class Saved:
                       hid=_rows_zeroed((n, 256), n_dev, device), vpe=torch.empty((n, 24), **f),
                       hc1=torch.empty((n, 128), **f), hc2=torch.empty((n, 128), **f),
                       hc3=torch.empty((n, 128), **f), vmask=torch.empty(n, dtype=torch.int32, device=device),
-                      mask=torch.empty((P, 64), dtype=torch.int16, device=device))
+                      mask=torch.empty((P, 64), dtype=torch.int16, device=device),
+                      dz_absmax=torch.zeros(6, dtype=torch.int32, device=device))   # |dz1..dz4|, |dpa|, |d_p1|
         self.c = L.AggSaved(*(self.t[k].data_ptr() for k, _ in L.AggSaved._fields_))
+
+    def absmax(self, i: int):
+        """[1] int32 view: float bits of max |dz_{i+1}| (i < 4), |dpa| (4), |d_p1| (5)."""
+        return self.t["dz_absmax"][i:i + 1]
 
     def __getitem__(self, k):
         return self.t[k]
@@ -288,20 +293,21 @@ class AggregateFn(torch.autograd.Function):
         pair_of = pair_of.to(torch.int32)
         L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1),
                                             L.ptr(None if spec.used is None else spec.used[1]), L.ptr(d_p1),
-                                            L.stream_ptr(dev)), "pnr_pairs_to_points")
+                                            L.ptr(sv.absmax(5)), L.stream_ptr(dev)), "pnr_pairs_to_points")
         dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
         h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
         # dW = dZ^T X over all pairs: split-K MFMA GEMM (pnr_gemm_tn), bias = column sums
-        grads["block3.2.weight"], grads["block3.2.bias"] = L.gemm_tn(dz4, h3, colsum=True, h2=hg)
+        # A operands' scales: the maxima k_pairs_bwd / pnr_pairs_to_points wrote (no extra pass)
+        amx = sv.absmax
+        grads["block3.2.weight"], grads["block3.2.bias"] = L.gemm_tn(dz4, h3, colsum=True, h2=hg, a_absmax=amx(3))
         gW3 = torch.empty((256, 263), **f32)
-        am3 = hg.absmax(dz3) if hg is not None else None
-        gW3[:, :256], grads["block3.0.bias"] = L.gemm_tn(dz3, h2, colsum=True, h2=hg, a_absmax=am3)
-        gW3[:, 256:] = L.gemm_tn(dz3, sv["x3e"][:m], h2=hg, a_absmax=am3)[:, :7]
+        gW3[:, :256], grads["block3.0.bias"] = L.gemm_tn(dz3, h2, colsum=True, h2=hg, a_absmax=amx(2))
+        gW3[:, 256:] = L.gemm_tn(dz3, sv["x3e"][:m], h2=hg, a_absmax=amx(2))[:, :7]
         grads["block3.0.weight"] = gW3
-        grads["block1.2.weight"], grads["block1.2.bias"] = L.gemm_tn(dz2, h1, colsum=True, h2=hg)
+        grads["block1.2.weight"], grads["block1.2.bias"] = L.gemm_tn(dz2, h1, colsum=True, h2=hg, a_absmax=amx(1))
         dpa32 = torch.zeros((m, 32), **f32)      # M padded to one 32-row MFMA tile
         dpa32[:, 0] = dpa
-        grads["alpha_branch.0.weight"] = L.gemm_tn(dpa32, h4, h2=hg)[:1]
+        grads["alpha_branch.0.weight"] = L.gemm_tn(dpa32, h4, h2=hg, a_absmax=amx(4))[:1]
         grads["alpha_branch.0.bias"] = dpa.sum(0, keepdim=True)
         # ---- block1.0: pair half from dz1 / PE_5, point half from dP1 / X1
         emb = ctx.tabs[0] if used is None else ctx.tabs[0].index_select(0, used.long()).contiguous()
@@ -309,9 +315,9 @@ class AggregateFn(torch.autograd.Function):
         x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
         L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
         gW1 = torch.empty((256, 284), **f32)
-        am_p1 = hg.absmax(d_p1) if hg is not None and n_p1 > 0 else None
+        am_p1 = amx(5)
         gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True, h2=hg, a_absmax=am_p1)   # sum_p dP1 = sum_pairs dz1
-        gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m], h2=hg)[:, :60]
+        gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m], h2=hg, a_absmax=amx(0))[:, :60]
         grads["block1.0.weight"] = gW1
         dx1 = L.gemm_nn(d_p1, P["block1.0.weight"][:, :224], h2=hg, a_absmax=am_p1)
         d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
