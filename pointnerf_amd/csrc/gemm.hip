@@ -267,23 +267,70 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
 // ---------------------------------------------------------------- h2 variant
 // fp32-accurate C = A^T B on f16 MFMA (pnr_gemm_tn_h2), the forward's fp32h2
 // arithmetic (aggregate_x3.hip) for the weight gradients: A is scaled by 2^e so
-// that max |A| 2^e lies in [4, 8) (e from the device max pnr_absmax wrote, so
+// that max |A| 2^e lies in [4, 8) (e from the device max the producer wrote:
 // gradients of any magnitude use the f16 exponent range), both operands split
 // x = xh + 2^-11 xl (splith, exact residuals), and
 //   2^11 (A 2^e)^T B ~= (2^11 Ah)^T Bh + Ah^T Bl + Al^T Bh
 // -- three v_mfma_f32_32x32x16_f16 per 16 k-rows instead of x3's six bf16
-// products, two LDS planes per operand instead of three (96 KB double-buffered).
-// 2^11 Ah is exact in f16 (|Ah| < 8).  The dropped 2^-22 Al^T Bl and the split
-// residuals are <= ~2^-21 |a b| per product.  Operands outside the split's range
-// (|B| >= 2^15, a stale max, non-finite) raise range_flag: the caller launches
-// the x3 kernel behind this one with run_if = range_flag.
-constexpr size_t kHLds = 2 * 2 * 2 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 96 KB
+// products.  2^11 Ah is exact in f16 (|Ah| < 8).  The dropped 2^-22 Al^T Bl and
+// the split residuals are <= ~2^-21 |a b| per product.  Operands outside the
+// split's range (|B| >= 2^15, a stale max, non-finite) raise range_flag: the
+// caller launches the x3 kernel behind this one with run_if = range_flag.
+//
+// Staging: the raw fp32 rows of a 16-row chunk (A and B, one <= 1-KB row per
+// wave instruction) go global -> LDS by buffer_load ... lds (no VGPRs), three
+// chunks in flight in three LDS slots (the chunk loop is latency-bound with one
+// chunk of register-staged loads per CU: ~3.4 TB/s on a 256 x 256 x 240 k
+// product); rows past the split and columns past M / N read as zeros (out of
+// the buffer's range).  Per chunk: counted vmcnt for the oldest slot, barrier,
+// split into two f16 planes per operand (one LDS image), barrier, refill the
+// slot, MFMAs.  Raw s_barrier with explicit waits (a __syncthreads() would
+// drain the in-flight DMAs with vmcnt(0)).
+constexpr int kHRawRow = 1024;                        // bytes per staged row (256 fp32)
+constexpr int kHRawSlot = 2 * kXK * kHRawRow;         // A rows then B rows: 32 KB
+constexpr int kHSlots = 3;
+constexpr size_t kHPlanes = 4 * (size_t)kXPlane * 2;  // Ah, Al, Bh, Bl: 48 KB
+
+__device__ __forceinline__ void hw_barrier_lds() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only (vmcnt / expcnt left at their maxima)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds): LDS address = m0 +
+// lane * 16.  Issued as inline asm so that the compiler, which cannot tell the
+// three slots apart, does not drain every DMA with vmcnt(0) before each LDS
+// access; the kernel orders them itself (wait_vm before the barrier that
+// precedes a slot's reads, a barrier before a slot is refilled).
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i buf_desc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  return (v4i){(int)(uint32_t)a, (int)(uint32_t)((a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ void dma16(v4i desc, uint32_t voff, uint32_t lds_addr) {
+  // m0 is not named as a clobber (a reserved register): nothing else in the
+  // kernel's loop reads it (checked in the ISA: the only m0 writes are these)
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(desc), "s"(lds_addr)
+               : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {   // vmcnt(N), other counters unconstrained
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
 
 __global__ void __launch_bounds__(512, 1) k_gemm_tn_h2_part(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t glds[];
+  // two distinct LDS objects: the DMA destinations provably never alias the
+  // planes, so the compiler's waits for the DMAs stay out of the plane accesses
+  __shared__ __attribute__((aligned(16))) uint16_t glds[kHPlanes / 2];
+  __shared__ __attribute__((aligned(16))) char raw[kHSlots * kHRawSlot];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int64_t k_begin = (int64_t)blockIdx.x * g.kchunk;
   const int64_t k_end = k_begin + g.kchunk < g.K ? k_begin + g.kchunk : g.K;
+  const int nchunk = (int)cdiv(k_end - k_begin, (int64_t)kXK);
   const int64_t stride = (int64_t)g.M * g.N + g.M;
   float* out = g.part + (int64_t)blockIdx.x * stride;
   // A's scale 2^e: max |A| 2^e in [4, 8)
@@ -297,85 +344,99 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_h2_part(GemmArgs g) {
     }
   }
   const float sa = ldexpf(1.f, e);
+  // the split's rows as buffers: rows >= k_end and bytes past a row's M / N columns read 0
+  const uint32_t rowsA = (uint32_t)(k_end - k_begin);
+  const v4i rA = buf_desc(g.A + k_begin * g.lda, rowsA * (uint32_t)g.lda * 4u);
+  const v4i rB = buf_desc(g.B + k_begin * g.ldb, rowsA * (uint32_t)g.ldb * 4u);
+  const uint32_t raw0 = (uint32_t)reinterpret_cast<uintptr_t>(raw);   // LDS byte address
+  const bool inA = lane * 16 < g.M * 4, inB = lane * 16 < g.N * 4;
+  // wave w stages rows 2w, 2w + 1 of A and of B of every chunk
+  auto issue = [&](int chunk) {
+    const uint32_t slot = raw0 + (uint32_t)((chunk % kHSlots) * kHRawSlot);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = 2 * wid + j;
+      const uint32_t row = (uint32_t)(chunk * kXK + r);
+      const uint32_t oa = inA ? row * (uint32_t)g.lda * 4u + lane * 16 : 0x7ffffff0u;
+      const uint32_t ob = inB ? row * (uint32_t)g.ldb * 4u + lane * 16 : 0x7ffffff0u;
+      dma16(rA, oa, __builtin_amdgcn_readfirstlane(slot + r * kHRawRow));
+      dma16(rB, ob, __builtin_amdgcn_readfirstlane(slot + (kXK + r) * kHRawRow));
+    }
+  };
   const int col = tid & 255, kh = tid >> 8;
-  const bool stA = col < g.M, stB = col < g.N;
+  const bool stA = col < g.M;
   float csum = 0.f;
   bool bad = false;   // a scaled A with |a| >= 8, a B with |b| >= 2^15, or a NaN / inf
-  auto load = [&](int64_t k0, float (&va)[8], float (&vb)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t r = k0 + 8 * kh + j;
-      const bool ok = r < k_end;
-      va[j] = ok && stA ? g.A[r * g.lda + col] : 0.f;
-      vb[j] = ok && stB ? g.B[r * g.ldb + col] : 0.f;
-    }
-  };
-  auto put = [&](int buf, const float (&va)[8], const float (&vb)[8]) {
-    uint16_t* base = glds + (size_t)buf * 4 * kXPlane + col * kXPitch + 8 * kh;
-    uint4 pa[2], pb[2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float a0 = va[2 * q] * sa, a1 = va[2 * q + 1] * sa;
-      csum += va[2 * q] + va[2 * q + 1];
-      const bool ok = (fabsf(a0) < 8.f) && (fabsf(a1) < 8.f) && (fabsf(vb[2 * q]) < 32768.f) &&
-                      (fabsf(vb[2 * q + 1]) < 32768.f);   // false for NaN / inf too
-      bad = bad || !ok;
-      unsigned x0, x1;
-      splith(a0, a1, x0, x1);
-      reinterpret_cast<unsigned*>(&pa[0])[q] = x0;
-      reinterpret_cast<unsigned*>(&pa[1])[q] = x1;
-      splith(vb[2 * q], vb[2 * q + 1], x0, x1);
-      reinterpret_cast<unsigned*>(&pb[0])[q] = x0;
-      reinterpret_cast<unsigned*>(&pb[1])[q] = x1;
-    }
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      *reinterpret_cast<uint4*>(base + p * kXPlane) = pa[p];
-      *reinterpret_cast<uint4*>(base + (2 + p) * kXPlane) = pb[p];
-    }
-  };
   f32x16 acc[2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x16){0.f};
   const int mt0 = 2 * (wid & 3), nt0 = 4 * (wid >> 2);
-  auto compute = [&](int buf) {
-    const uint16_t* lb = glds + (size_t)buf * 4 * kXPlane + c * kXPitch + 8 * h;
-    uint4 ah[2], al[2], as[2];
+  for (int q = 0; q < kHSlots && q < nchunk; ++q) issue(q);
+  for (int it = 0; it < nchunk; ++it) {
+    // this wave's DMAs of chunk `it` are done when at most those of the chunks after it remain
+    const int ahead = nchunk - 1 - it < kHSlots - 1 ? nchunk - 1 - it : kHSlots - 1;
+    if (ahead >= 2) wait_vm<8>();
+    else if (ahead == 1) wait_vm<4>();
+    else wait_vm<0>();
+    hw_barrier_lds();
+    {   // split: column col of A and B, k rows 8 kh .. 8 kh + 7 of the chunk
+      const float* ra = reinterpret_cast<const float*>(raw + (it % kHSlots) * kHRawSlot) + col;
+      const float* rb = ra + kXK * (kHRawRow / 4);
+      uint4 pa[2], pb[2];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      ah[mi] = *reinterpret_cast<const uint4*>(lb + 32 * (mt0 + mi) * kXPitch);
-      al[mi] = *reinterpret_cast<const uint4*>(lb + kXPlane + 32 * (mt0 + mi) * kXPitch);
-      as[mi] = f16x8_scale2048(ah[mi]);
-    }
+      for (int q = 0; q < 4; ++q) {
+        const int r0 = 8 * kh + 2 * q;
+        const float v0 = ra[r0 * (kHRawRow / 4)], v1 = ra[(r0 + 1) * (kHRawRow / 4)];
+        const float b0 = rb[r0 * (kHRawRow / 4)], b1 = rb[(r0 + 1) * (kHRawRow / 4)];
+        const float a0 = v0 * sa, a1 = v1 * sa;
+        csum += v0 + v1;
+        const bool ok = (fabsf(a0) < 8.f) && (fabsf(a1) < 8.f) && (fabsf(b0) < 32768.f) && (fabsf(b1) < 32768.f);
+        bad = bad || !ok;
+        unsigned x0, x1;
+        splith(a0, a1, x0, x1);
+        reinterpret_cast<unsigned*>(&pa[0])[q] = x0;
+        reinterpret_cast<unsigned*>(&pa[1])[q] = x1;
+        splith(b0, b1, x0, x1);
+        reinterpret_cast<unsigned*>(&pb[0])[q] = x0;
+        reinterpret_cast<unsigned*>(&pb[1])[q] = x1;
+      }
+      uint16_t* base = glds + col * kXPitch + 8 * kh;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      if (32 * (nt0 + ni) >= g.N) continue;
-      const uint4 bh = *reinterpret_cast<const uint4*>(lb + 2 * kXPlane + 32 * (nt0 + ni) * kXPitch);
-      const uint4 bl = *reinterpret_cast<const uint4*>(lb + 3 * kXPlane + 32 * (nt0 + ni) * kXPitch);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        if (32 * (mt0 + mi) >= g.M) continue;
-        acc[mi][ni] = mfma_f16(al[mi], bh, acc[mi][ni]);   // smallest terms first
-        acc[mi][ni] = mfma_f16(ah[mi], bl, acc[mi][ni]);
-        acc[mi][ni] = mfma_f16(as[mi], bh, acc[mi][ni]);
+      for (int p = 0; p < 2; ++p) {
+        *reinterpret_cast<uint4*>(base + p * kXPlane) = pa[p];
+        *reinterpret_cast<uint4*>(base + (2 + p) * kXPlane) = pb[p];
       }
     }
-  };
-  float va[8], vb[8];
-  load(k_begin, va, vb);
-  put(0, va, vb);
-  __syncthreads();
-  int it1 = 0;
-  for (int64_t k0 = k_begin; k0 < k_end; k0 += kXK, ++it1) {
-    const int buf = it1 & 1;
-    const bool more = k0 + kXK < k_end;
-    if (more) load(k0 + kXK, va, vb);
-    compute(buf);
-    if (more) put(buf ^ 1, va, vb);
-    __syncthreads();
+    hw_barrier_lds();   // planes written; the raw slot fully read
+    if (it + kHSlots < nchunk) issue(it + kHSlots);
+    {   // MFMAs on the planes
+      const uint16_t* lb = glds + c * kXPitch + 8 * h;
+      uint4 ah[2], al[2], as[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        ah[mi] = *reinterpret_cast<const uint4*>(lb + 32 * (mt0 + mi) * kXPitch);
+        al[mi] = *reinterpret_cast<const uint4*>(lb + kXPlane + 32 * (mt0 + mi) * kXPitch);
+        as[mi] = f16x8_scale2048(ah[mi]);
+      }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        if (32 * (nt0 + ni) >= g.N) continue;
+        const uint4 bh = *reinterpret_cast<const uint4*>(lb + 2 * kXPlane + 32 * (nt0 + ni) * kXPitch);
+        const uint4 bl = *reinterpret_cast<const uint4*>(lb + 3 * kXPlane + 32 * (nt0 + ni) * kXPitch);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          if (32 * (mt0 + mi) >= g.M) continue;
+          acc[mi][ni] = mfma_f16(al[mi], bh, acc[mi][ni]);   // smallest terms first
+          acc[mi][ni] = mfma_f16(ah[mi], bl, acc[mi][ni]);
+          acc[mi][ni] = mfma_f16(as[mi], bh, acc[mi][ni]);
+        }
+      }
+    }
+    hw_barrier_lds();   // every wave is done reading the planes
   }
+  wait_vm<0>();
   if (bad) atomicOr(g.range_flag, 1);   // outside the split's range, or NaN / inf
   const float unscale = ldexpf(1.f, -(e + 11));   // exact: a power of two
 #pragma unroll
@@ -897,12 +958,10 @@ static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, i
   if (!attr && (x3 || h2)) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_x3_part),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_h2_part),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHLds));
     attr = true;
   }
   if (h2) {
-    hipLaunchKernelGGL(k_gemm_tn_h2_part, dim3(ns), dim3(512), kHLds, st, g);
+    hipLaunchKernelGGL(k_gemm_tn_h2_part, dim3(ns), dim3(512), 0, st, g);
     PNR_LAUNCH_CHECK();
     g.run_if = range_flag;   // the x3 kernel redoes the partials only when the flag is up
     hipLaunchKernelGGL(k_gemm_tn_x3_part, dim3(ns), dim3(512), kXLds, st, g);
