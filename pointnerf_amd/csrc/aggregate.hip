@@ -1327,6 +1327,58 @@ __global__ void __launch_bounds__(256) k_extras_bwd(BwdArgs A) {
   }
 }
 
+// k_extras_bwd's colour / dir scatter from precomputed g[pair][0..6] =
+// dz3[pair] . W3[:, 256 + e] (pnr_aggregate_bwd_extras).  Lane = pair.
+__global__ void __launch_bounds__(256) k_extras_apply(BwdArgs A, const float* __restrict__ g_rows, int64_t ldg) {
+  const int64_t n = eff_n(A.s);
+  const int64_t P = n * kKN;
+  for (int64_t pair = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; pair < P;
+       pair += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t pr = A.sv.prow[pair];
+    if (pr < 0) continue;
+    float g[7];
+#pragma unroll
+    for (int e = 0; e < 7; ++e) g[e] = g_rows[pair * ldg + e];
+    if (A.d_color) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) atomicAdd(A.d_color + (int64_t)pr * 3 + a, g[a]);
+    }
+    if (A.d_dir) {
+      float Rw[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+      const int64_t row = sample_row(A.s, pair / kKN);
+      const int64_t drow = dir_row(A.s, row);
+      const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+      float vrot[3];
+      mat3(Rw, vd, vrot);
+      if (A.pts.rw2c) {   // per-point: view dir by the slot-0 matrix, d dir through the pair's
+        rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Rw[i] = A.pts.rw2c[(int64_t)pr * 9 + i];
+      }
+      const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        atomicAdd(A.d_dir + (int64_t)pr * 3 + i, Rw[i] * gd[0] + Rw[3 + i] * gd[1] + Rw[6 + i] * gd[2]);
+    }
+  }
+}
+
+// Per-point entry counts of a query's neighbour lists: counts[p] += 1 for every
+// pidx entry p >= 0 of the first (*n_dev) samples (float atomics of integers:
+// exact and order-free below 2^24).
+__global__ void k_point_counts(const int32_t* __restrict__ pidx, const int32_t* __restrict__ n_dev, int K,
+                               int64_t cap, float* __restrict__ counts) {
+  int64_t ns = *n_dev;
+  ns = ns < cap ? ns : cap;
+  const int64_t n = ns * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t p = pidx[i];
+    if (p >= 0) atomicAdd(counts + p, 1.f);
+  }
+}
+
 // pnr_used_points: flag the points referenced by the first (*n_dev) samples'
 // neighbour rows, rank them (scan), list them in ascending order.
 __global__ void k_mark_used(const int32_t* __restrict__ pidx, const int32_t* __restrict__ n_dev, int K, int64_t cap,
@@ -1789,7 +1841,7 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
   int rc;
   PNR_CHECK_ARG(pts && s && w && wb, "aggregate_bwd: null pointer");
   if ((rc = check_saved(saved))) return rc;
-  PNR_CHECK_ARG(wb->w3e && w->wa && (wbx || (wb->w4t && wb->w3t && wb->w2t)), "aggregate_bwd: null weight");
+  PNR_CHECK_ARG((wb->w3e || wbx) && w->wa && (wbx || (wb->w4t && wb->w3t && wb->w2t)), "aggregate_bwd: null weight");
   PNR_CHECK_ARG(!wbx || (wbx->w4tx && wbx->w3tx && wbx->w2tx &&
                          (((uintptr_t)wbx->w4tx | (uintptr_t)wbx->w3tx | (uintptr_t)wbx->w2tx) & 15) == 0),
                 "aggregate_bwd_x3: null or unaligned split weight pack");
@@ -1833,7 +1885,10 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
     hipLaunchKernelGGL(k_pairs_bwd<true>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
                        st, a);
     PNR_LAUNCH_CHECK();
-    if (d_color || d_dir)
+    // wb->w3e == NULL: the caller runs the extras as g = dz3 W3[:, 256:263] on a GEMM
+    // and pnr_aggregate_bwd_extras (the per-pair row reads of k_extras_bwd are
+    // 64 rows per load instruction)
+    if ((d_color || d_dir) && wb->w3e)
       hipLaunchKernelGGL(k_extras_bwd, dim3(grid_for(cdiv(s->n_max * kKN, 64), 4, 2048)), dim3(256), 0, st, a);
   } else
     hipLaunchKernelGGL(k_pairs_bwd<false>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
@@ -2016,6 +2071,37 @@ extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev
   int rc;
   if ((rc = exclusive_scan(flags, n_points, nullptr, used_map, n_used_dev, scratch, scratch_bytes, st, 0))) return rc;
   hipLaunchKernelGGL(k_used_list, dim3(grid_for(n_points, 256)), dim3(256), 0, st, flags, n_points, used_map, used);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_aggregate_bwd_extras(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                        const pnr_agg_saved* saved, const float* g, int64_t ldg, float* d_color,
+                                        float* d_dir, void* stream) {
+  PNR_CHECK_ARG(pts && s && w && saved && saved->prow, "aggregate_bwd_extras: null pointer");
+  PNR_CHECK_ARG(ldg >= 7 && (g || s->n_max == 0), "aggregate_bwd_extras: g rows need >= 7 columns");
+  PNR_CHECK_ARG(!d_dir || (s->dirs && s->dir_div >= 1), "aggregate_bwd_extras: sample dirs required");
+  if (s->n_max <= 0 || (!d_color && !d_dir)) return PNR_OK;
+  BwdArgs a;
+  memset(&a, 0, sizeof(a));
+  a.pts = *pts;
+  a.s = *s;
+  a.w = *w;
+  a.sv = *saved;
+  a.d_color = d_color;
+  a.d_dir = d_dir;
+  hipLaunchKernelGGL(k_extras_apply, dim3(grid_for(s->n_max * kKN, 256, 2048)), dim3(256), 0, as_stream(stream), a,
+                     g, ldg);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_point_counts(const int32_t* pidx, const int32_t* n_dev, int32_t K, int64_t cap, float* counts,
+                                void* stream) {
+  PNR_CHECK_ARG(n_dev && K > 0 && cap >= 0 && (cap == 0 || (pidx && counts)), "point_counts: bad args");
+  if (cap == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_point_counts, dim3(grid_for(cap * K, 256, 2048)), dim3(256), 0, as_stream(stream), pidx,
+                     n_dev, K, cap, counts);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

@@ -822,15 +822,11 @@ class NeuralPointsRayMarching(nn.Module):
         conf = self.neural_points.points_conf.reshape(-1)
         N = conf.numel()
         SR, K = self.opt.SR, self.opt.K
-        ids = bufs.pidx.long()
         c = bufs.counts
         # entries of the filled samples (counts[0] of them, K each) that name a point
-        pos = torch.arange(ids.numel(), device=ids.device)
-        ok = (pos < c[0].long() * K) & (ids >= 0)
-        # the other entries land in 1024 spare bins (no atomics piling on one address)
-        counts = torch.zeros(N + 1024, dtype=torch.float32, device=conf.device)
-        counts.index_add_(0, torch.where(ok, ids, N + pos % 1024), ok.float())   # integers: exact
-        counts = counts[:N]
+        counts = torch.zeros(N, dtype=torch.float32, device=conf.device)
+        L.check(L.lib().pnr_point_counts(L.ptr(bufs.pidx), L.ptr(c), K, bufs.pidx.numel() // K, L.ptr(counts),
+                                         L.stream_ptr(conf.device)), "pnr_point_counts")   # integers: exact
         entries = c[3].double() * (SR * K)
         empty = (entries - counts.sum(dtype=torch.float64)).float()
         counts[0:1] += empty

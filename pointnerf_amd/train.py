@@ -259,7 +259,7 @@ class AggregateFn(torch.autograd.Function):
         vpe32[:, :24] = sv["vpe"][:n]
         gC0[:, 256:] = L.gemm_tn(dz, vpe32)[:, :24]
         grads["color_branch.0.weight"] = gC0
-        d_hid = torch.zeros((max(n_max, 1), 256), **f32)
+        d_hid = torch.empty((max(n_max, 1), 256), **f32)   # rows [0, n) written by the gemm_nn below
         L.gemm_nn(dz, P["color_branch.0.weight"][:, :256], out=d_hid[:n])
         # ---- per-pair chain on MFMA
         Pn = max(n_max, 1) * 8
@@ -267,12 +267,15 @@ class AggregateFn(torch.autograd.Function):
         dpa = torch.empty(Pn, **f32)
         used = used_list
         n_p1 = N if used is None else used.numel()
-        d_p1 = torch.zeros((max(n_p1, 1), 256), **f32)
+        d_p1 = torch.empty((max(n_p1, 1), 256), **f32)   # pnr_pairs_to_points writes every used row
         has_c, has_d, has_f = ctx.has
         d_color = torch.zeros((N, 3), **f32) if has_c else None
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
         d_conf = torch.zeros(N, **f32) if has_f else None
         wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3)
+        gemm_extras = wbx is not None and (has_c or has_d)
+        if gemm_extras:
+            wb.w3e = None   # the block3.0 extras run below as g = dz3 W3[:, 256:263] on a GEMM
         # d_p1 = NULL: the per-point sums of dz1 come from pnr_pairs_to_points below
         # (pairs sorted by point: no atomics, deterministic) instead of the kernel's atomics
         bufs = (L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3), L.ptr(dz4), L.ptr(dpa),
@@ -289,6 +292,15 @@ class AggregateFn(torch.autograd.Function):
         # weight gradients on f16 MFMA (pnr_gemm_tn_h2) with the fp32h2 forward;
         # fp32x3 keeps the bf16x3 GEMMs
         hg = L.H2Gemm(dev) if spec.h2 else None
+        if gemm_extras and m > 0:
+            # d colour / d dir of the block3.0 extras: g = dz3 W3[:, 256:263] (N padded to 32)
+            w3e = torch.zeros((256, 32), **f32)
+            w3e[:, :7] = P["block3.0.weight"][:, 256:263]
+            g_ex = L.gemm_nn(dz3[:m], w3e, h2=hg, a_absmax=sv.absmax(2) if hg is not None else None)
+            L.check(L.lib().pnr_aggregate_bwd_extras(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                     ctypes.byref(ctx.mlp), ctypes.byref(sv.c), L.ptr(g_ex), 32,
+                                                     L.ptr(d_color), L.ptr(d_dir), L.stream_ptr(dev)),
+                    "pnr_aggregate_bwd_extras")
         prow_sorted, pair_of = torch.sort(sv["prow"][:m], stable=True)
         pair_of = pair_of.to(torch.int32)
         L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1),
