@@ -78,7 +78,7 @@ def parse():
                          "default 12000 (headline), 3000 (c4, c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
-    ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32x3",
+    ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32h2",
                     help="--mode train: the training forward's per-pair chain (fp32h2 split-f16 MFMA, fp32x3 "
                          "split-bf16 MFMA or native fp32)")
     ap.add_argument("--optimizer", choices=("hip", "torch"), default="hip",

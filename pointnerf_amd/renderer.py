@@ -229,7 +229,9 @@ class NeuralPointsRayMarching(nn.Module):
         self.precision = precision
         # render_rays_train's per-pair forward: "fp32x3" (split-bf16 MFMA,
         # fp32-accurate, the default) or "fp32" (native fp32 MFMA)
-        self.train_precision = "fp32x3"   # per-pair forward chain: fp32x3 (split-bf16 MFMA) / fp32h2 / fp32
+        # training path: fp32h2 (forward chain and the weight / point-half gradient GEMMs on f16-split
+        # MFMA, the measured default) / fp32x3 (split-bf16 MFMA) / fp32
+        self.train_precision = "fp32h2"
         self.p1_side_stream = True        # fp32h2 sync-free calls: P1 beside the query (see _render_rays)
         self.p1_side_max_points_per_ray = 4.0
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations

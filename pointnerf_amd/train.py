@@ -267,7 +267,9 @@ class AggregateFn(torch.autograd.Function):
         dpa = torch.empty(Pn, **f32)
         used = used_list
         n_p1 = N if used is None else used.numel()
-        d_p1 = torch.empty((max(n_p1, 1), 256), **f32)   # pnr_pairs_to_points writes every used row
+        # pnr_pairs_to_points writes the row of every point some pair references: every
+        # row of a used-point list, only some of the whole table's
+        d_p1 = (torch.empty if used is not None else torch.zeros)((max(n_p1, 1), 256), **f32)
         has_c, has_d, has_f = ctx.has
         d_color = torch.zeros((N, 3), **f32) if has_c else None
         d_dir = torch.zeros((N, 3), **f32) if has_d else None

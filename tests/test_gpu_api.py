@@ -28,7 +28,9 @@ def _model(sc, cuda, params, precision="fp32", Rw2c=None, train=False):
     np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
                        torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]),
                        Rw2c=None if Rw2c is None else torch.from_numpy(Rw2c))
-    return NeuralPointsRayMarching(sc["opt"], np_, agg.train() if train else agg.eval(), precision=precision)
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg.train() if train else agg.eval(), precision=precision)
+    m.train_precision = "fp32x3"   # the strict oracle comparisons; fp32h2 (the default) has its own tests
+    return m
 
 
 def _inputs(sc, cuda):

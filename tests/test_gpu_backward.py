@@ -75,7 +75,9 @@ def _train_model(sc, cuda, params):
     agg.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
     np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
                        torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]))
-    return NeuralPointsRayMarching(sc["opt"], np_, agg.train(), precision="fp32")
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg.train(), precision="fp32")
+    m.train_precision = "fp32x3"   # the strict oracle comparisons; fp32h2 (the default) has its own tests
+    return m
 
 
 @pytest.mark.parametrize("train_precision", ["fp32", "fp32x3"])

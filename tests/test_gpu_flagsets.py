@@ -49,7 +49,9 @@ def _model(sc, cuda, params, precision="fp32", train=False, emb_dtype=torch.floa
     np_ = NeuralPoints(sc["opt"], cuda, torch.from_numpy(sc["xyz"]), torch.from_numpy(sc["emb"]),
                        torch.from_numpy(sc["color"]), torch.from_numpy(sc["dir"]), torch.from_numpy(sc["conf"]),
                        emb_dtype=emb_dtype)
-    return NeuralPointsRayMarching(sc["opt"], np_, agg.train() if train else agg.eval(), precision=precision)
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg.train() if train else agg.eval(), precision=precision)
+    m.train_precision = "fp32x3"   # the strict oracle comparisons; fp32h2 (the default) has its own tests
+    return m
 
 
 def _render(m, sc, cuda, rd=None):
