@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
 constexpr int kHP = kHid + 8;  // bf16 pitch of the staged hid rows (16-B aligned rows)
 static_assert(kBTSmax * kHP <= kBT * kPB, "staged hid rows must fit Xb");
-constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT) * 4;
+constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT + kBTSmax) * 4;
 
 template <int KT>
 __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const int32_t* bk_list, const int32_t* bk_info,
@@ -231,6 +231,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   int* sflag = reinterpret_cast<int*>(apart + 4 * kBT);    // [SPT]
   float* exL = reinterpret_cast<float*>(sflag + kBTSmax);  // [8][128]
   int* prowL = reinterpret_cast<int*>(exL + 8 * kBT);      // [128]
+  int* vL = prowL + kBT;                                   // [SPT] sample index of each tile row
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int K = A.s.K;
@@ -334,7 +335,10 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         for (int e = 0; e < 8; ++e) exL[e * kBT + col] = ex[e];
         wtL[col] = wn * confc;
         prowL[col] = valid ? (int)prow : -1;
-        if (k == 0) sflag[j] = active && samp_valid;
+        if (k == 0) {
+          sflag[j] = active && samp_valid;
+          vL[j] = (int)v;   // the list entry, read once here (not per store below)
+        }
         if (active && k < K) {
           // the bucket's dropped slots (KT..K-1) are empty: weight 0, their gathered conf
           if (A.out_weight) {
@@ -544,7 +548,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const int r = i / (kHid / 8), q = i % (kHid / 8);
       const int64_t jv = tile * SPT + r;
       if (jv < n && sflag[r]) {
-        const int64_t vo = list ? (int64_t)list[jv] : jv;
+        const int64_t vo = vL[r];
         reinterpret_cast<uint4*>(A.hid + vo * kHid)[q] = *reinterpret_cast<const uint4*>(Xb + r * kHP + 8 * q);
       }
     }
@@ -556,7 +560,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const float alpha_s = xork_sum_nc<KT>(wtL[col] * alpha_k);
       const int64_t jv = tile * SPT + j;
       if (k == 0 && jv < n) {
-        const int64_t vo = list ? (int64_t)list[jv] : jv;
+        const int64_t vo = vL[j];
         A.vmask[vo] = sflag[j];
         if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
       }
