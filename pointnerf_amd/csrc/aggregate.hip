@@ -1327,44 +1327,6 @@ __global__ void __launch_bounds__(256) k_extras_bwd(BwdArgs A) {
   }
 }
 
-// k_extras_bwd's colour / dir scatter from precomputed g[pair][0..6] =
-// dz3[pair] . W3[:, 256 + e] (pnr_aggregate_bwd_extras).  Lane = pair.
-__global__ void __launch_bounds__(256) k_extras_apply(BwdArgs A, const float* __restrict__ g_rows, int64_t ldg) {
-  const int64_t n = eff_n(A.s);
-  const int64_t P = n * kKN;
-  for (int64_t pair = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; pair < P;
-       pair += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t pr = A.sv.prow[pair];
-    if (pr < 0) continue;
-    float g[7];
-#pragma unroll
-    for (int e = 0; e < 7; ++e) g[e] = g_rows[pair * ldg + e];
-    if (A.d_color) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) atomicAdd(A.d_color + (int64_t)pr * 3 + a, g[a]);
-    }
-    if (A.d_dir) {
-      float Rw[9];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
-      const int64_t row = sample_row(A.s, pair / kKN);
-      const int64_t drow = dir_row(A.s, row);
-      const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
-      float vrot[3];
-      mat3(Rw, vd, vrot);
-      if (A.pts.rw2c) {   // per-point: view dir by the slot-0 matrix, d dir through the pair's
-        rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Rw[i] = A.pts.rw2c[(int64_t)pr * 9 + i];
-      }
-      const float gd[3] = {g[3] + vrot[0] * g[6], g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6]};
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        atomicAdd(A.d_dir + (int64_t)pr * 3 + i, Rw[i] * gd[0] + Rw[3 + i] * gd[1] + Rw[6 + i] * gd[2]);
-    }
-  }
-}
-
 // Per-point entry counts of a query's neighbour lists: counts[p] += 1 for every
 // pidx entry p >= 0 of the first (*n_dev) samples (float atomics of integers:
 // exact and order-free below 2^24).
@@ -1425,6 +1387,94 @@ __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const
     reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
     mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
              max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
+  }
+  if (absmax) {
+    wave_absmax_to(&bmax, mb);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax) atomicMax(absmax, bmax);
+  }
+}
+
+// pnr_pairs_to_points_ex: k_pairs_to_points plus the block3.0 extras' colour /
+// dir gradients of the same point run (k_extras_bwd without atomics): per pair
+// g_e = dz3[pair] . W3[:, 256 + e] (lane = 4 neurons, w3e in registers), summed
+// over the run in pair order before one wave reduction --
+//   d colour_p = sum_pairs g[0..2]
+//   d dir_p    = Rw_p^T sum_pairs (g[3..5] + vrot_pair g[6])
+// (Rw_p: the point's per-point Rw2c or the uniform one; vrot_pair: the pair's
+// view direction rotated as in the forward).  Every referenced point's rows are
+// written (the others keep the caller's zeros); deterministic.
+__global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, const int32_t* __restrict__ pair_of,
+                                     int64_t P, const float* __restrict__ dz1, const int32_t* __restrict__ used_map,
+                                     float* __restrict__ d_p1, uint32_t* __restrict__ absmax, BwdArgs A,
+                                     const float* __restrict__ dz3) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  __shared__ unsigned bmax;
+  if (threadIdx.x == 0) bmax = 0u;
+  __syncthreads();
+  unsigned mb = 0u;
+  float we[4][7];   // W3[4 lane + i, 256 + e]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 7; ++e) we[i][e] = A.wb.w3e[(4 * lane + i) * 7 + e];
+  float Ru[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Ru[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
+    const int32_t pr = prow_sorted[i];
+    if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // colour 3, dir 3, vrot * g6 3
+    for (int64_t j = i; j < P && prow_sorted[j] == pr; ++j) {
+      const int64_t pair = pair_of[j];
+      const float4 v = reinterpret_cast<const float4*>(dz1 + pair * kHid)[lane];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+      const float4 z = reinterpret_cast<const float4*>(dz3 + pair * kHid)[lane];
+      const float zv[4] = {z.x, z.y, z.z, z.w};
+      float g[7];
+#pragma unroll
+      for (int e = 0; e < 7; ++e) g[e] = we[0][e] * zv[0] + we[1][e] * zv[1] + we[2][e] * zv[2] + we[3][e] * zv[3];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) acc[e] += g[e];
+      if (A.d_dir) {   // the pair's rotated view direction (wave-uniform)
+        const int64_t row = sample_row(A.s, pair / kKN);
+        const int64_t drow = dir_row(A.s, row);
+        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+        float vrot[3];
+        mat3(Ru, vd, vrot);
+        if (A.pts.rw2c) rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
+        acc[6] += vrot[0] * g[6];
+        acc[7] += vrot[1] * g[6];
+        acc[8] += vrot[2] * g[6];
+      }
+    }
+    reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
+    mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
+             max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
+#pragma unroll
+    for (int e = 0; e < 9; ++e)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc[e] += __shfl_xor(acc[e], o);
+    if (lane == 0) {
+      if (A.d_color) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) A.d_color[(int64_t)pr * 3 + a] = acc[a];
+      }
+      if (A.d_dir) {
+        float Rw[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) Rw[q] = A.pts.rw2c ? A.pts.rw2c[(int64_t)pr * 9 + q] : Ru[q];
+        const float gd[3] = {acc[3] + acc[6], acc[4] + acc[7], acc[5] + acc[8]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+          A.d_dir[(int64_t)pr * 3 + a] = Rw[a] * gd[0] + Rw[3 + a] * gd[1] + Rw[6 + a] * gd[2];
+      }
+    }
   }
   if (absmax) {
     wave_absmax_to(&bmax, mb);
@@ -1885,9 +1935,8 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
     hipLaunchKernelGGL(k_pairs_bwd<true>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
                        st, a);
     PNR_LAUNCH_CHECK();
-    // wb->w3e == NULL: the caller runs the extras as g = dz3 W3[:, 256:263] on a GEMM
-    // and pnr_aggregate_bwd_extras (the per-pair row reads of k_extras_bwd are
-    // 64 rows per load instruction)
+    // wb->w3e == NULL: the caller runs the extras per point inside
+    // pnr_pairs_to_points_ex (no float atomics, coalesced dz3 rows)
     if ((d_color || d_dir) && wb->w3e)
       hipLaunchKernelGGL(k_extras_bwd, dim3(grid_for(cdiv(s->n_max * kKN, 64), 4, 2048)), dim3(256), 0, st, a);
   } else
@@ -2075,23 +2124,27 @@ extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev
   return PNR_OK;
 }
 
-extern "C" int pnr_aggregate_bwd_extras(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
-                                        const pnr_agg_saved* saved, const float* g, int64_t ldg, float* d_color,
-                                        float* d_dir, void* stream) {
-  PNR_CHECK_ARG(pts && s && w && saved && saved->prow, "aggregate_bwd_extras: null pointer");
-  PNR_CHECK_ARG(ldg >= 7 && (g || s->n_max == 0), "aggregate_bwd_extras: g rows need >= 7 columns");
-  PNR_CHECK_ARG(!d_dir || (s->dirs && s->dir_div >= 1), "aggregate_bwd_extras: sample dirs required");
-  if (s->n_max <= 0 || (!d_color && !d_dir)) return PNR_OK;
+extern "C" int pnr_pairs_to_points_ex(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P,
+                                      const float* dz1, const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax,
+                                      const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                      const float* w3e, const float* dz3, float* d_color, float* d_dir,
+                                      void* stream) {
+  PNR_CHECK_ARG(P >= 0 && (P == 0 || (prow_sorted && pair_of && dz1 && d_p1)), "pairs_to_points_ex: bad args");
+  PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1 | (uintptr_t)dz3) & 15) == 0,
+                "pairs_to_points_ex: rows must be 16-B aligned");
+  PNR_CHECK_ARG(pts && s && w && w3e && (P == 0 || dz3), "pairs_to_points_ex: null pointer");
+  PNR_CHECK_ARG(!d_dir || (s->dirs && s->dir_div >= 1), "pairs_to_points_ex: sample dirs required");
+  if (P == 0) return PNR_OK;
   BwdArgs a;
   memset(&a, 0, sizeof(a));
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  a.sv = *saved;
+  a.wb.w3e = w3e;
   a.d_color = d_color;
   a.d_dir = d_dir;
-  hipLaunchKernelGGL(k_extras_apply, dim3(grid_for(s->n_max * kKN, 256, 2048)), dim3(256), 0, as_stream(stream), a,
-                     g, ldg);
+  hipLaunchKernelGGL(k_pairs_to_points_ex, dim3(grid_for(P, 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
+                     pair_of, P, dz1, used_map, d_p1, d_p1_absmax, a, dz3);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

@@ -275,9 +275,12 @@ class AggregateFn(torch.autograd.Function):
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
         d_conf = torch.zeros(N, **f32) if has_f else None
         wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3)
-        gemm_extras = wbx is not None and (has_c or has_d)
-        if gemm_extras:
-            wb.w3e = None   # the block3.0 extras run below as g = dz3 W3[:, 256:263] on a GEMM
+        point_extras = wbx is not None and (has_c or has_d)
+        if point_extras:
+            # the block3.0 extras' colour / dir gradients: per point inside
+            # pnr_pairs_to_points_ex below (no float atomics), not in the pairs pass
+            w3e_rm = _keepb["w3e"]
+            wb.w3e = None
         # d_p1 = NULL: the per-point sums of dz1 come from pnr_pairs_to_points below
         # (pairs sorted by point: no atomics, deterministic) instead of the kernel's atomics
         bufs = (L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3), L.ptr(dz4), L.ptr(dpa),
@@ -294,20 +297,19 @@ class AggregateFn(torch.autograd.Function):
         # weight gradients on f16 MFMA (pnr_gemm_tn_h2) with the fp32h2 forward;
         # fp32x3 keeps the bf16x3 GEMMs
         hg = L.H2Gemm(dev) if spec.h2 else None
-        if gemm_extras and m > 0:
-            # d colour / d dir of the block3.0 extras: g = dz3 W3[:, 256:263] (N padded to 32)
-            w3e = torch.zeros((256, 32), **f32)
-            w3e[:, :7] = P["block3.0.weight"][:, 256:263]
-            g_ex = L.gemm_nn(dz3[:m], w3e, h2=hg, a_absmax=sv.absmax(2) if hg is not None else None)
-            L.check(L.lib().pnr_aggregate_bwd_extras(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
-                                                     ctypes.byref(ctx.mlp), ctypes.byref(sv.c), L.ptr(g_ex), 32,
-                                                     L.ptr(d_color), L.ptr(d_dir), L.stream_ptr(dev)),
-                    "pnr_aggregate_bwd_extras")
         prow_sorted, pair_of = torch.sort(sv["prow"][:m], stable=True)
         pair_of = pair_of.to(torch.int32)
-        L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1),
-                                            L.ptr(None if spec.used is None else spec.used[1]), L.ptr(d_p1),
-                                            L.ptr(sv.absmax(5)), L.stream_ptr(dev)), "pnr_pairs_to_points")
+        used_map = None if spec.used is None else spec.used[1]
+        if point_extras:
+            L.check(L.lib().pnr_pairs_to_points_ex(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1), L.ptr(used_map),
+                                                   L.ptr(d_p1), L.ptr(sv.absmax(5)), ctypes.byref(ctx.pts),
+                                                   ctypes.byref(spec.samples), ctypes.byref(ctx.mlp), L.ptr(w3e_rm),
+                                                   L.ptr(dz3), L.ptr(d_color), L.ptr(d_dir), L.stream_ptr(dev)),
+                    "pnr_pairs_to_points_ex")
+        else:
+            L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1), L.ptr(used_map),
+                                                L.ptr(d_p1), L.ptr(sv.absmax(5)), L.stream_ptr(dev)),
+                    "pnr_pairs_to_points")
         dz1, dz2, dz3, dz4, dpa = dz1[:m], dz2[:m], dz3[:m], dz4[:m], dpa[:m]
         h1, h2, h3, h4 = sv["h1"][:m], sv["h2"][:m], sv["h3"][:m], sv["h4"][:m]
         # dW = dZ^T X over all pairs: split-K MFMA GEMM (pnr_gemm_tn), bias = column sums
