@@ -247,20 +247,32 @@ class AggregateFn(torch.autograd.Function):
         dc = d_feat[:n, 1:] * vm
         hc1, hc2, hc3 = sv["hc1"][:n], sv["hc2"][:n], sv["hc3"][:n]
         # weight gradients dW = dZ^T X on pnr_gemm_tn_x3 (bias = column sums); the
-        # dX = dZ W products with the LeakyReLU derivative fused on pnr_gemm_nn
+        # dX = dZ W products with the LeakyReLU derivative fused on pnr_gemm_nn.
+        # fp32h2: both on the f16-split kernels (pnr_gemm_*_h2), dZ's scale from one
+        # pnr_absmax pass per layer (the colour batch is ~30 k rows)
+        hg = L.H2Gemm(dev) if spec.h2 else None
+
+        def amax(t):
+            return hg.absmax(t) if hg is not None and t.shape[0] > 0 else None
+
         dz = _lrelu_grad(dc, hc3, slope).contiguous()
-        grads["color_branch.4.weight"], grads["color_branch.4.bias"] = L.gemm_tn(dz, hc2.contiguous(), colsum=True)
-        dz = L.gemm_nn(dz, P["color_branch.4.weight"], act=hc2, slope=slope)
-        grads["color_branch.2.weight"], grads["color_branch.2.bias"] = L.gemm_tn(dz, hc1.contiguous(), colsum=True)
-        dz = L.gemm_nn(dz, P["color_branch.2.weight"], act=hc1, slope=slope)
+        am = amax(dz)
+        grads["color_branch.4.weight"], grads["color_branch.4.bias"] = L.gemm_tn(
+            dz, hc2.contiguous(), colsum=True, h2=hg, a_absmax=am)
+        dz = L.gemm_nn(dz, P["color_branch.4.weight"], act=hc2, slope=slope, h2=hg, a_absmax=am)
+        am = amax(dz)
+        grads["color_branch.2.weight"], grads["color_branch.2.bias"] = L.gemm_tn(
+            dz, hc1.contiguous(), colsum=True, h2=hg, a_absmax=am)
+        dz = L.gemm_nn(dz, P["color_branch.2.weight"], act=hc1, slope=slope, h2=hg, a_absmax=am)
+        am = amax(dz)
         gC0 = torch.empty((128, 280), **f32)
-        gC0[:, :256], grads["color_branch.0.bias"] = L.gemm_tn(dz, sv["hid"][:n], colsum=True)
+        gC0[:, :256], grads["color_branch.0.bias"] = L.gemm_tn(dz, sv["hid"][:n], colsum=True, h2=hg, a_absmax=am)
         vpe32 = torch.zeros((n, 32), **f32)
         vpe32[:, :24] = sv["vpe"][:n]
-        gC0[:, 256:] = L.gemm_tn(dz, vpe32)[:, :24]
+        gC0[:, 256:] = L.gemm_tn(dz, vpe32, h2=hg, a_absmax=am)[:, :24]
         grads["color_branch.0.weight"] = gC0
         d_hid = torch.empty((max(n_max, 1), 256), **f32)   # rows [0, n) written by the gemm_nn below
-        L.gemm_nn(dz, P["color_branch.0.weight"][:, :256], out=d_hid[:n])
+        L.gemm_nn(dz, P["color_branch.0.weight"][:, :256], out=d_hid[:n], h2=hg, a_absmax=am)
         # ---- per-pair chain on MFMA
         Pn = max(n_max, 1) * 8
         dz1, dz2, dz3, dz4 = (torch.empty((Pn, 256), **f32) for _ in range(4))
@@ -294,9 +306,8 @@ class AggregateFn(torch.autograd.Function):
                                                     ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(sv.c),
                                                     *bufs), "pnr_aggregate_bwd_pairs")
         m = n * 8
-        # weight gradients on f16 MFMA (pnr_gemm_tn_h2) with the fp32h2 forward;
-        # fp32x3 keeps the bf16x3 GEMMs
-        hg = L.H2Gemm(dev) if spec.h2 else None
+        # weight gradients on f16 MFMA (pnr_gemm_tn_h2, hg above) with the fp32h2
+        # forward; fp32x3 keeps the bf16x3 GEMMs
         prow_sorted, pair_of = torch.sort(sv["prow"][:m], stable=True)
         pair_of = pair_of.to(torch.int32)
         used_map = None if spec.used is None else spec.used[1]
