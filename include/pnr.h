@@ -514,17 +514,22 @@ int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev, int32_t K
  * negative point rows (empty pairs) are skipped. */
 int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,
                         const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax, void* stream);
-/* pnr_pairs_to_points plus the block3.0 extras' colour / dir gradients per point
- * (replaces the per-pair float atomics of pnr_aggregate_bwd_pairs_x3's extras
- * pass, skipped when pnr_mlp_bwd.w3e is NULL; ABI 19): for each referenced
- * point p, over its pairs in pair order, d_color[p] = sum g[0..2] and d_dir[p] =
- * Rw_p^T sum (g[3..5] + vrot g[6]), g_e = dz3[pair] . w3e[:, e] (w3e =
- * block3.0[:, 256:263] row-major [256,7]); rows of points without pairs keep
- * the caller's values.  Deterministic. */
+/* The block3.0 extras of pnr_aggregate_bwd_pairs_x3 without float atomics (ABI 19;
+ * that call skips its own extras pass when pnr_mlp_bwd.w3e is NULL):
+ * pnr_aggregate_bwd_extras_rows writes per pair g_pair[pair][0..7] = (g0, g1, g2,
+ * g3 + vrot0 g6, g4 + vrot1 g6, g5 + vrot2 g6, 0, 0), g_e = dz3[pair] . w3e[:, e]
+ * (w3e = block3.0[:, 256:263] row-major [256,7]), vrot the pair's view direction
+ * rotated as in the forward; pnr_pairs_to_points_ex is pnr_pairs_to_points plus,
+ * per referenced point p over its pairs in pair order, d_color[p] = sum g[0..2]
+ * and d_dir[p] = Rw_p^T sum g[3..5] (rw_pp [N,9] per-point, else rw_uniform [9],
+ * else identity) -- written, not added; deterministic. */
+int pnr_aggregate_bwd_extras_rows(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                  const pnr_agg_saved* saved, const float* w3e, const float* dz3, float* g_pair,
+                                  void* stream);
 int pnr_pairs_to_points_ex(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P, const float* dz1,
-                           const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax, const pnr_points* pts,
-                           const pnr_samples* s, const pnr_mlp* w, const float* w3e, const float* dz3,
-                           float* d_color, float* d_dir, void* stream);
+                           const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax, const float* g_pair,
+                           const float* rw_uniform, const float* rw_pp, float* d_color, float* d_dir,
+                           void* stream);
 /* counts[p] += number of entries p >= 0 in pidx rows [0, min(*n_dev, cap)) (K per
  * row); float counts, exact below 2^24 (the zero-one conf loss, ABI 19). */
 int pnr_point_counts(const int32_t* pidx, const int32_t* n_dev, int32_t K, int64_t cap, float* counts, void* stream);

