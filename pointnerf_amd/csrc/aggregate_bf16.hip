@@ -256,6 +256,21 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   const uint4* w3 = reinterpret_cast<const uint4*>(A.w.w3f) + T0 * 64;
   const uint4* w4 = reinterpret_cast<const uint4*>(A.w.w4f) + T0 * 64;
 
+  // The gather's dependent index chain (bucket list -> sample list -> neighbour
+  // id) for the NEXT tile runs one link per layer of this tile (pf_*), so a
+  // tile's gather starts from the neighbour id: two HBM round trips fewer on
+  // its critical path.
+  const int pf_col = threadIdx.x & (kBT - 1);
+  const int pf_j = pf_col / KT, pf_k = pf_col % KT;
+  auto pf_v = [&](int64_t t) -> int {   // sample-list entry of this column's sample, -1 past the end
+    const int64_t jv = t * SPT + pf_j;
+    return (t < ntiles && jv < n) ? (list ? list[jv] : (int)jv) : -1;
+  };
+  auto pf_row = [&](int v) -> int { return v >= 0 ? (int)sample_row(A.s, v) : -1; };
+  auto pf_pid = [&](int row) -> int { return (row >= 0 && pf_k < K) ? A.s.pidx[(int64_t)row * K + pf_k] : -1; };
+  int nx_v = pf_v(blockIdx.x);
+  int nx_row = pf_row(nx_v);
+  int nx_pid = pf_pid(nx_row);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
     {
@@ -263,12 +278,12 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const int j = col / KT, k = col % KT;
       const int64_t jv = tile * SPT + j;
       const bool active = jv < n;
-      const int64_t v = active ? (list ? (int64_t)list[jv] : jv) : 0;
-      const int64_t row = active ? sample_row(A.s, v) : 0;
+      const int64_t v = active ? (int64_t)nx_v : 0;
+      const int64_t row = active ? (int64_t)nx_row : 0;
       int64_t prow = -1;
       bool valid = false;
       if (active && k < K) {
-        const int pid = A.s.pidx[row * K + k];
+        const int pid = nx_pid;
         valid = pid >= 0;
         prow = valid ? pid : 0;
       }
@@ -401,6 +416,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
       }
     }
+    nx_v = pf_v(tile + gridDim.x);   // the next tile's chain, link 1
     // -------------------------------------------- block1: + W1[:, 224:284] . PE_5 (4 steps), block1.2
     mlp_layer_b<2, kBPT, 8, kPB>(acc, w1b, Xb, 4, lane);
     __syncthreads();
@@ -413,6 +429,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    nx_row = pf_row(nx_v);   // link 2
     mlp_layer_b<2, kBPT, 8, kPB>(acc, w2, Xb, 17, lane);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
@@ -430,6 +447,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     // -------------------------------------------- block3
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    nx_pid = pf_pid(nx_row);   // link 3
     mlp_layer_b<2, kBPT, 8, kPB>(acc, w3, Xb, 17, lane);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);

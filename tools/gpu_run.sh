@@ -34,12 +34,12 @@ for s in $STEPS; do
     train)
       timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 > $O/train.json 2> $O/train.err \
         || { tail -20 $O/train.err; exit 1; }
-      timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 --train-precision fp32h2 > $O/train_h2.json \
-        2> $O/train_h2.err || { tail -20 $O/train_h2.err; exit 1; }
-      cut -c1-400 $O/train.json $O/train_h2.json ;;
+      timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 --train-precision fp32x3 > $O/train_x3.json \
+        2> $O/train_x3.err || { tail -20 $O/train_x3.err; exit 1; }
+      cut -c1-400 $O/train.json $O/train_x3.json ;;
     trainprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trstats -o run -- \
-        python bench.py --mode train --steps 20 --warmup 3 --train-precision ${TP:-fp32x3} > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
+        python bench.py --mode train --steps 20 --warmup 3 --train-precision ${TP:-fp32h2} > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
     nrab)   # the 2-D renderer tile-shape variants in tools/_var (built on the CPU side)
       for v in tools/_var/libpnr_*.so; do
         PNR_LIB=$PWD/$v timeout -k 10 200 python tools/nr_bench.py > $O/nrab_$(basename $v .so).json 2>> $O/nrab.err \
