@@ -530,6 +530,17 @@ int pnr_pairs_to_points_ex(const int32_t* prow_sorted, const int32_t* pair_of, i
                            const int32_t* used_map, float* d_p1, uint32_t* d_p1_absmax, const float* g_pair,
                            const float* rw_uniform, const float* rw_pp, float* d_color, float* d_dir,
                            void* stream);
+/* zero_one_loss(conf_coefficient) (base_rendering_model.py:634-639) from per-point
+ * entry counts (pnr_point_counts): out[0] = mean over the E = (*r_valid) * srk
+ * entries of log(v) + log(1 - v), v = clamp(clamp(conf, 1e-4, 1), eps, 1 - eps),
+ * the E - sum(counts) empty entries gathered as point 0; out[1] = those empty
+ * entries, out[2] = E.  partials: 1024 device floats.  The backward: d_conf[p] =
+ * g[0] (counts[p] (+ out[1] at p = 0)) f'(v_p) / E where eps <= cc_p <= 1 - eps,
+ * else 0 (gradiant_clamp passes straight through).  Deterministic (ABI 19). */
+int pnr_zero_one_loss_fwd(const float* conf, const float* counts, int64_t N, const int32_t* r_valid, int64_t srk,
+                          float eps, float* partials, float* out, void* stream);
+int pnr_zero_one_loss_bwd(const float* conf, const float* counts, int64_t N, float eps, const float* fwd_out,
+                          const float* g, float* d_conf, void* stream);
 /* counts[p] += number of entries p >= 0 in pidx rows [0, min(*n_dev, cap)) (K per
  * row); float counts, exact below 2^24 (the zero-one conf loss, ABI 19). */
 int pnr_point_counts(const int32_t* pidx, const int32_t* n_dev, int32_t K, int64_t cap, float* counts, void* stream);

@@ -226,6 +226,9 @@ SIGNATURES = {
     "pnr_pairs_to_points_ex": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_point_counts": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
+    "pnr_zero_one_loss_fwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p,
+                                      c_void_p]),
+    "pnr_zero_one_loss_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_absmax_scratch_floats": (c_int, [P(c_int64)]),
     "pnr_absmax": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "pnr_weighted_colsum_scratch_floats": (c_int, [c_int32, P(c_int64)]),

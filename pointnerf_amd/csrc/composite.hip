@@ -766,6 +766,108 @@ extern "C" int pnr_zero_rows(void* p, int64_t row_bytes, const int32_t* n_dev, i
   return PNR_OK;
 }
 
+// zero_one_loss of conf_coefficient (base_rendering_model.py:634-639: mean of
+// log(v) + log(1 - v), v = clamp(cc, eps, 1 - eps)) from per-point entry counts
+// (pnr_zero_one_loss_fwd / _bwd): cc_p = clamp(conf_p, 1e-4, 1) (gradiant_clamp's
+// value, point_aggregators.py:724-726; its gradient passes straight through),
+// E = R'' SR K entries, the empty ones gathered as point 0.  Per-block partials
+// of (sum c_p f(v_p), sum c_p) in fixed order, then one block.
+constexpr int kZoBlocks = 512;
+__device__ __forceinline__ float zo_v(float conf, float eps) {
+  const float cc = fminf(fmaxf(conf, 1e-4f), 1.f);
+  return fminf(fmaxf(cc, eps), 1.f - eps);
+}
+__global__ void __launch_bounds__(256) k_zero_one_part(const float* __restrict__ conf, const float* __restrict__ cnt,
+                                                       int64_t N, float eps, float* __restrict__ part) {
+  __shared__ float r1[4], r0[4];
+  float s1 = 0.f, s0 = 0.f;
+  const int64_t per = cdiv(N, (int64_t)kZoBlocks);
+  const int64_t b0 = blockIdx.x * per, b1 = b0 + per < N ? b0 + per : N;
+  for (int64_t p = b0 + threadIdx.x; p < b1; p += 256) {
+    const float c = cnt[p];
+    if (c != 0.f) {
+      const float v = zo_v(conf[p], eps);
+      s1 += c * (logf(v) + logf(1.f - v));
+      s0 += c;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s0 += __shfl_xor(s0, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    r1[threadIdx.x >> 6] = s1;
+    r0[threadIdx.x >> 6] = s0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = ((r1[0] + r1[1]) + r1[2]) + r1[3];
+    part[2 * blockIdx.x + 1] = ((r0[0] + r0[1]) + r0[2]) + r0[3];
+  }
+}
+// out[0] = loss, out[1] = the empty entries E - sum c (gathered as point 0), out[2] = E
+__global__ void __launch_bounds__(64) k_zero_one_final(const float* __restrict__ part, const float* __restrict__ conf,
+                                                       const int32_t* __restrict__ r_valid, int64_t srk, float eps,
+                                                       float* __restrict__ out) {
+  float s1 = 0.f, s0 = 0.f;
+  for (int i = threadIdx.x; i < kZoBlocks; i += 64) {
+    s1 += part[2 * i];
+    s0 += part[2 * i + 1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s0 += __shfl_xor(s0, o);
+  }
+  if (threadIdx.x == 0) {
+    const float E = (float)((double)*r_valid * (double)srk);
+    const float empty = E - s0;
+    const float v0 = zo_v(conf[0], eps);
+    out[0] = E > 0.f ? (s1 + empty * (logf(v0) + logf(1.f - v0))) / E : 0.f;
+    out[1] = empty;
+    out[2] = E;
+  }
+}
+__global__ void __launch_bounds__(256) k_zero_one_bwd(const float* __restrict__ conf, const float* __restrict__ cnt,
+                                                      int64_t N, float eps, const float* __restrict__ fwd_out,
+                                                      const float* __restrict__ g, float* __restrict__ d_conf) {
+  const float E = fwd_out[2];
+  const float scale = E > 0.f ? g[0] / E : 0.f;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
+    const float c = cnt[p] + (p == 0 ? fwd_out[1] : 0.f);
+    float d = 0.f;
+    if (c != 0.f) {
+      const float cc = fminf(fmaxf(conf[p], 1e-4f), 1.f);
+      if (cc >= eps && cc <= 1.f - eps) {   // torch.clamp's gradient mask (inclusive)
+        const float v = cc;
+        d = c * scale * (1.f / v - 1.f / (1.f - v));
+      }
+    }
+    d_conf[p] = d;
+  }
+}
+
+extern "C" int pnr_zero_one_loss_fwd(const float* conf, const float* counts, int64_t N, const int32_t* r_valid,
+                                     int64_t srk, float eps, float* partials, float* out, void* stream) {
+  PNR_CHECK_ARG(conf && counts && r_valid && partials && out && N > 0 && srk > 0, "zero_one_loss_fwd: bad args");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_zero_one_part, dim3(kZoBlocks), dim3(256), 0, st, conf, counts, N, eps, partials);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_zero_one_final, dim3(1), dim3(64), 0, st, partials, conf, r_valid, srk, eps, out);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_zero_one_loss_bwd(const float* conf, const float* counts, int64_t N, float eps,
+                                     const float* fwd_out, const float* g, float* d_conf, void* stream) {
+  PNR_CHECK_ARG(conf && counts && fwd_out && g && d_conf && N > 0, "zero_one_loss_bwd: bad args");
+  hipLaunchKernelGGL(k_zero_one_bwd, dim3(grid_for(N, 256, 2048)), dim3(256), 0, as_stream(stream), conf, counts, N,
+                     eps, fwd_out, g, d_conf);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
 extern "C" int pnr_weighted_colsum_scratch_floats(int32_t C, int64_t* out) {
   PNR_CHECK_ARG(out && C >= 1 && C <= 128, "weighted_colsum: C=%d unsupported (1..128)", C);
   *out = (int64_t)kColsumBlocks * C;

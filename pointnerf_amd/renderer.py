@@ -187,6 +187,40 @@ def _counts_dict(c):
 PRECISIONS = ("fp32", "fp32x3", "fp32h2", "bf16")
 
 
+class _ZeroOneConfLoss(torch.autograd.Function):
+    """NeuralPointsRayMarching.zero_one_conf_loss on libpnr: the per-point entry
+    counts of the query's neighbour lists (pnr_point_counts), then one fused
+    reduction (pnr_zero_one_loss_fwd) and one backward kernel -- the same value
+    and gradient as torch's clamp / log / mean over the gathered [1, R'', SR, K]
+    conf_coefficient, in three launches and without host reads."""
+
+    @staticmethod
+    def forward(ctx, conf, bufs, SR, K, eps):
+        dev = conf.device
+        N = conf.numel()
+        c = conf.detach().float().contiguous()
+        counts = torch.zeros(N, dtype=torch.float32, device=dev)
+        L.check(L.lib().pnr_point_counts(L.ptr(bufs.pidx), L.ptr(bufs.counts), K, bufs.pidx.numel() // K,
+                                         L.ptr(counts), L.stream_ptr(dev)), "pnr_point_counts")
+        part = torch.empty(1024, dtype=torch.float32, device=dev)
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        L.check(L.lib().pnr_zero_one_loss_fwd(L.ptr(c), L.ptr(counts), N, L.c_void_p(bufs.counts.data_ptr() + 12),
+                                              SR * K, eps, L.ptr(part), L.ptr(out), L.stream_ptr(dev)),
+                "pnr_zero_one_loss_fwd")
+        ctx.save_for_backward(c, counts, out)
+        ctx.eps = eps
+        return out[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        c, counts, out = ctx.saved_tensors
+        d = torch.empty_like(c)
+        g = g.reshape(1).float().contiguous()
+        L.check(L.lib().pnr_zero_one_loss_bwd(L.ptr(c), L.ptr(counts), c.numel(), ctx.eps, L.ptr(out), L.ptr(g),
+                                              L.ptr(d), L.stream_ptr(c.device)), "pnr_zero_one_loss_bwd")
+        return d, None, None, None, None
+
+
 class _TrainAux(dict):
     """render_rays_train's last_train_aux: keys whose values need the batch's
     host counts are computed when first read (so that the forward itself never
@@ -822,21 +856,8 @@ class NeuralPointsRayMarching(nn.Module):
         no host read of R'' and no compaction."""
         bufs = self._train_conf_src
         conf = self.neural_points.points_conf.reshape(-1)
-        N = conf.numel()
-        SR, K = self.opt.SR, self.opt.K
-        c = bufs.counts
-        # entries of the filled samples (counts[0] of them, K each) that name a point
-        counts = torch.zeros(N, dtype=torch.float32, device=conf.device)
-        L.check(L.lib().pnr_point_counts(L.ptr(bufs.pidx), L.ptr(c), K, bufs.pidx.numel() // K, L.ptr(counts),
-                                         L.stream_ptr(conf.device)), "pnr_point_counts")   # integers: exact
-        entries = c[3].double() * (SR * K)
-        empty = (entries - counts.sum(dtype=torch.float64)).float()
-        counts[0:1] += empty
-        cc = conf - (conf - torch.clamp(conf, 1e-4, 1.0)).detach()   # gradiant_clamp
-        v = torch.clamp(cc, zero_epsilon, 1 - zero_epsilon)
-        return (torch.sum(counts * (torch.log(v) + torch.log(1 - v))) / entries).float()
+        return _ZeroOneConfLoss.apply(conf, bufs, self.opt.SR, self.opt.K, float(zero_epsilon))
 
-    @staticmethod
     def zero_one_loss(val, zero_epsilon: float = 1e-3):
         """base_rendering_model.py:630-641: mean(log(v) + log(1 - v)), v clamped
         to [eps, 1 - eps]."""

@@ -650,3 +650,30 @@ def test_train_forward_does_not_wait_for_gpu(cuda, train_precision):
             assert torch.equal(a, b), n
         else:                             # point tables: float-atomic sums over pairs
             assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max()), n
+
+
+def test_zero_one_conf_loss_matches_reference_formula(cuda):
+    """NeuralPointsRayMarching.zero_one_conf_loss (per-point counts + the fused
+    libpnr reduction) equals the reference's zero_one_loss over the gathered
+    conf_coefficient [1, R'', SR, K] (base_rendering_model.py:634-639), value and
+    d points_conf, with confidences spread across the clamp edges."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.3))
+    m.train_precision = "fp32h2"
+    conf = m.neural_points.points_conf
+    with torch.no_grad():   # values below 1e-4, in (eps, 1 - eps), above 1 - eps and above 1
+        g = torch.Generator().manual_seed(3)
+        conf.copy_((torch.rand(conf.shape, generator=g) * 1.2 - 0.1).to(cuda))
+        conf.view(-1)[:50] = 5e-4
+        conf.view(-1)[50:100] = 0.9995
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    m.render_rays_train(cp, cr, rd, 2.0, 6.0, bg)
+    loss = m.zero_one_conf_loss()
+    (gl,) = torch.autograd.grad(loss, conf)
+    cc = m.last_train_aux["conf_coefficient"]   # the reference-shaped tensor, straight-through to conf
+    val = torch.clamp(cc, 1e-3, 1 - 1e-3)
+    ref = torch.mean(torch.log(val) + torch.log(1 - val))
+    (gr,) = torch.autograd.grad(ref, conf)
+    assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref)) + 1e-7
+    close(gl, gr, "d points_conf", rel=1e-4, scale=1e-5)
