@@ -649,6 +649,12 @@ int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_
  * matching backward d_emb[p] += dX1[p] . dX1/d emb (networks.py:175-190). */
 int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* stream);
 int pnr_point_pe3_bwd(const float* emb, const float* d_x1, int64_t n, float* d_emb, void* stream);
+/* The same over a row list (ABI 19): X1[i] = PE_3(emb[rows[i]]) and
+ * d_emb[rows[i]] += the PE_3 backward of d_x1[i] (rows distinct: the used points) --
+ * no gathered copy of the embedding, no index_copy of its gradient. */
+int pnr_point_pe3_rows(const float* emb, const int32_t* rows, int64_t n, float* x1, void* stream);
+int pnr_point_pe3_bwd_rows(const float* emb, const int32_t* rows, const float* d_x1, int64_t n, float* d_emb,
+                           void* stream);
 
 /* -------------------------------------------------------------- composite
  * Fused ray_dist (cummax), alpha composite and fill_invalid for the full ray

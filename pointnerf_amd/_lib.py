@@ -226,6 +226,8 @@ SIGNATURES = {
     "pnr_pairs_to_points_ex": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_point_counts": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
+    "pnr_point_pe3_rows": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "pnr_point_pe3_bwd_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "pnr_zero_one_loss_fwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p,
                                       c_void_p]),
     "pnr_zero_one_loss_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),

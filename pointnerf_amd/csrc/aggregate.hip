@@ -1514,12 +1514,13 @@ __global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, co
 }
 
 // X1[p] = [emb, PE_3(emb)] (networks.py:175-190: channel d, band f -> 32 + 2(3d+f) + {sin, cos})
-__global__ void k_point_pe3(const float* __restrict__ emb, int64_t n, float* __restrict__ x1) {
+__global__ void k_point_pe3(const float* __restrict__ emb, const int32_t* __restrict__ rows, int64_t n,
+                            float* __restrict__ x1) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kEmb;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = i / kEmb;
     const int d = (int)(i - p * kEmb);
-    const float e = emb[i];
+    const float e = emb[(rows ? (int64_t)rows[p] : p) * kEmb + d];   // rows: the used points (a gather)
     float* o = x1 + p * 224;
     o[d] = e;
 #pragma unroll
@@ -1532,13 +1533,14 @@ __global__ void k_point_pe3(const float* __restrict__ emb, int64_t n, float* __r
   }
 }
 
-__global__ void k_point_pe3_bwd(const float* __restrict__ emb, const float* __restrict__ dx1, int64_t n,
-                                float* __restrict__ d_emb) {
+__global__ void k_point_pe3_bwd(const float* __restrict__ emb, const int32_t* __restrict__ rows,
+                                const float* __restrict__ dx1, int64_t n, float* __restrict__ d_emb) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kEmb;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = i / kEmb;
     const int d = (int)(i - p * kEmb);
-    const float e = emb[i];
+    const int64_t t = (rows ? (int64_t)rows[p] : p) * kEmb + d;   // rows: scatter into the full table
+    const float e = emb[t];
     const float* g = dx1 + p * 224;
     float acc = g[d];
 #pragma unroll
@@ -1548,7 +1550,7 @@ __global__ void k_point_pe3_bwd(const float* __restrict__ emb, const float* __re
       sincosf(e * b, &sn, &cs);
       acc += b * (cs * g[kEmb + 2 * (3 * d + f)] - sn * g[kEmb + 2 * (3 * d + f) + 1]);
     }
-    d_emb[i] += acc;
+    d_emb[t] += acc;
   }
 }
 
@@ -2214,7 +2216,8 @@ extern "C" int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pa
 extern "C" int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* stream) {
   PNR_CHECK_ARG(emb && x1 && n >= 0, "point_pe3: bad args");
   if (n == 0) return PNR_OK;
-  hipLaunchKernelGGL(k_point_pe3, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, n, x1);
+  hipLaunchKernelGGL(k_point_pe3, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, nullptr, n,
+                     x1);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
@@ -2222,8 +2225,26 @@ extern "C" int pnr_point_pe3(const float* emb, int64_t n, float* x1, void* strea
 extern "C" int pnr_point_pe3_bwd(const float* emb, const float* d_x1, int64_t n, float* d_emb, void* stream) {
   PNR_CHECK_ARG(emb && d_x1 && d_emb && n >= 0, "point_pe3_bwd: bad args");
   if (n == 0) return PNR_OK;
-  hipLaunchKernelGGL(k_point_pe3_bwd, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, d_x1,
-                     n, d_emb);
+  hipLaunchKernelGGL(k_point_pe3_bwd, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, nullptr,
+                     d_x1, n, d_emb);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_point_pe3_rows(const float* emb, const int32_t* rows, int64_t n, float* x1, void* stream) {
+  PNR_CHECK_ARG(emb && rows && x1 && n >= 0, "point_pe3_rows: bad args");
+  if (n == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_point_pe3, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, rows, n, x1);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
+extern "C" int pnr_point_pe3_bwd_rows(const float* emb, const int32_t* rows, const float* d_x1, int64_t n,
+                                      float* d_emb, void* stream) {
+  PNR_CHECK_ARG(emb && rows && d_x1 && d_emb && n >= 0, "point_pe3_bwd_rows: bad args");
+  if (n == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_point_pe3_bwd, dim3(grid_for(n * kEmb, 256)), dim3(256), 0, as_stream(stream), emb, rows,
+                     d_x1, n, d_emb);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

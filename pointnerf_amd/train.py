@@ -344,23 +344,27 @@ class AggregateFn(torch.autograd.Function):
         grads["alpha_branch.0.weight"] = L.gemm_tn(dpa32, h4, h2=hg, a_absmax=amx(4))[:1]
         grads["alpha_branch.0.bias"] = dpa.sum(0, keepdim=True)
         # ---- block1.0: pair half from dz1 / PE_5, point half from dP1 / X1
-        emb = ctx.tabs[0] if used is None else ctx.tabs[0].index_select(0, used.long()).contiguous()
+        emb = ctx.tabs[0]
         d_p1 = d_p1[:n_p1]
         x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
-        L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
+        if used is None:
+            L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
+        else:   # PE_3 of the used rows, read through the list (no gathered copy)
+            L.check(L.lib().pnr_point_pe3_rows(L.ptr(emb), L.ptr(used), n_p1, L.ptr(x1), L.stream_ptr(dev)),
+                    "pnr_point_pe3_rows")
         gW1 = torch.empty((256, 284), **f32)
         am_p1 = amx(5)
         gW1[:, :224], grads["block1.0.bias"] = L.gemm_tn(d_p1, x1, colsum=True, h2=hg, a_absmax=am_p1)   # sum_p dP1 = sum_pairs dz1
         gW1[:, 224:] = L.gemm_tn(dz1, sv["pe5"][:m], h2=hg, a_absmax=amx(0))[:, :60]
         grads["block1.0.weight"] = gW1
         dx1 = L.gemm_nn(d_p1, P["block1.0.weight"][:, :224], h2=hg, a_absmax=am_p1)
-        d_emb_u = torch.zeros((max(n_p1, 1), 32), **f32)
-        L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb_u), L.stream_ptr(dev)),
-                "pnr_point_pe3_bwd")
+        d_emb = torch.zeros((N, 32), **f32)
         if used is None:
-            d_emb = d_emb_u
-        else:
-            d_emb = torch.zeros((N, 32), **f32).index_copy_(0, used.long(), d_emb_u[:n_p1])
+            L.check(L.lib().pnr_point_pe3_bwd(L.ptr(emb), L.ptr(dx1), n_p1, L.ptr(d_emb), L.stream_ptr(dev)),
+                    "pnr_point_pe3_bwd")
+        else:   # straight into the used rows of the full gradient (no index_copy)
+            L.check(L.lib().pnr_point_pe3_bwd_rows(L.ptr(emb), L.ptr(used), L.ptr(dx1), n_p1, L.ptr(d_emb),
+                                                   L.stream_ptr(dev)), "pnr_point_pe3_bwd_rows")
         emb_shape, conf_shape = ctx.shapes
         d_xyz = None
         if ctx.xyz_shape is not None and ctx.needs_input_grad[5]:
