@@ -7,7 +7,9 @@
 // cloud version, deterministically, in the serial order of the reference
 // kernels (slot = rank of the first point index that lands in the voxel,
 // points inside a voxel in ascending index order), which is what the serial
-// execution of claim_occ/fill_occ2pnts produces when nothing overflows.
+// execution of claim_occ/fill_occ2pnts produces when nothing overflows.  The
+// points are grouped by a stable LSD radix sort of their cell keys, so
+// claimer, count and the ordered run of every voxel come without atomics.
 //
 // HBM layout (MI355X, 288 GB): one dense int32 cell->slot grid (lego 162x290x189
 // = 35.5 MB), one dilated-occupancy BITMAP (1 bit per cell: 1.1 MB, stays in
@@ -151,119 +153,282 @@ __device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int
   return ((int64_t)c[0] * g.dims[1] + c[1]) * g.dims[2] + c[2];
 }
 
-// claim_occ's voxel coordinate + first-claimer (qpiw.py:262-283), made
-// order-free: the claimer is the smallest point index of the voxel.
-__global__ void __launch_bounds__(kBlock) k_cells(const float* __restrict__ xyz, int64_t n, GridDev g0,
-                                                  const QGrid* __restrict__ geo, int64_t* __restrict__ pt_cell,
-                                                  int32_t* __restrict__ first_pt, int32_t* counters) {
+// ---- points grouped by voxel (claim_occ + fill_occ2pnts, qpiw.py:243-387),
+// order-free and without atomics: a point's key is its cell index, and a
+// stable LSD radix sort of (key, point id) lays the points of one voxel out as
+// one run in ascending id order.  The run's first id is the voxel's claimer
+// (the smallest point id: the serial claim_occ's winner), its length the
+// voxel's point count, and its first P ids the serial fill_occ2pnts order.
+// Points outside the grid carry the key `sentinel` (> every cell) and sort last.
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ xyz, int64_t n, GridDev g0,
+                                                      const QGrid* __restrict__ geo, K sentinel,
+                                                      K* __restrict__ keys) {
   const GridDev g = with_geom(g0, geo);
-  int in_grid = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
     int c[3];
     const int64_t cell = cell_of(p, g, c);
-    pt_cell[i] = cell;
-    if (cell >= 0) {
-      atomicMin(first_pt + cell, (int)i);
-      ++in_grid;
-    }
+    keys[i] = cell >= 0 ? (K)cell : sentinel;
   }
-  in_grid = wave_sum_i32(in_grid);
-  if ((threadIdx.x & 63) == 0 && in_grid) atomicAdd(counters + 1, in_grid);
 }
 
-__global__ void __launch_bounds__(kBlock) k_first_flags(int64_t n, const int64_t* __restrict__ pt_cell,
-                                                        const int32_t* __restrict__ first_pt,
-                                                        int32_t* __restrict__ flag) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t cell = pt_cell[i];
-    flag[i] = (cell >= 0 && first_pt[cell] == (int)i) ? 1 : 0;
+// LSD radix sort, 8 key bits per pass over tiles of kRsTile keys: per-tile
+// digit counts (k_rs_hist), their exclusive scan in digit-major order (the
+// device scan), then a stable scatter (k_rs_scatter) that ranks the tile in
+// LDS and writes each digit's keys of the tile as one contiguous run.
+constexpr int kRsItems = 16;
+constexpr int kRsTile = kBlock * kRsItems;  // 4096 keys
+
+template <typename K>
+__device__ __forceinline__ int rs_digit(K k, int shift) {
+  return (int)((k >> shift) & (K)255);
+}
+
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_rs_hist(const K* __restrict__ keys, int64_t n, int shift, int tiles,
+                                                    int32_t* __restrict__ hist) {
+  __shared__ int32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRsTile;
+#pragma unroll 4
+  for (int r = 0; r < kRsItems; ++r) {
+    const int64_t i = base + r * kBlock + threadIdx.x;
+    if (i < n) atomicAdd(&h[rs_digit(keys[i], shift)], 1);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// vin == nullptr: the values are the keys' positions (the point ids, pass 0)
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin, const int32_t* __restrict__ vin,
+                                                       int64_t n, int shift, int tiles,
+                                                       const int32_t* __restrict__ offs, K* __restrict__ kout,
+                                                       int32_t* __restrict__ vout) {
+  __shared__ K sk[kRsTile];
+  __shared__ int32_t sv[kRsTile];
+  __shared__ int32_t wcnt[kBlock / 64][256];  // this round's digit counts per wave
+  __shared__ int32_t run[256];                // digit counts of the earlier rounds, then digit starts
+  __shared__ int32_t gb[256];                 // output position of the tile's digit-d keys minus their LDS start
+  __shared__ int32_t wsum[kBlock / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kRsTile;
+  const int in_tile = (int)(n - base < kRsTile ? n - base : kRsTile);
+  const uint64_t below = (1ull << lane) - 1ull;
+  run[tid] = 0;
+#pragma unroll
+  for (int q = 0; q < kBlock / 64; ++q) wcnt[q][tid] = 0;
+  K key[kRsItems];
+  int32_t val[kRsItems], loc[kRsItems];
+#pragma unroll
+  for (int r = 0; r < kRsItems; ++r) {
+    const int e = r * kBlock + tid;
+    const bool ok = e < in_tile;
+    key[r] = ok ? kin[base + e] : (K)0;
+    val[r] = ok ? (vin ? vin[base + e] : (int32_t)(base + e)) : 0;
+  }
+  __syncthreads();
+  // stable rank inside the tile: item e = r * 256 + tid comes after every
+  // item of an earlier round, of a lower wave, and of a lower lane
+#pragma unroll
+  for (int r = 0; r < kRsItems; ++r) {
+    const bool ok = r * kBlock + tid < in_tile;
+    const int d = rs_digit(key[r], shift);
+    uint64_t peers = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t m = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? m : ~m;
+    }
+    const int rk = __popcll(peers & below);
+    if (ok && rk == 0) wcnt[w][d] = __popcll(peers);
+    __syncthreads();
+    int pre = run[d];
+    for (int q = 0; q < w; ++q) pre += wcnt[q][d];
+    loc[r] = pre + rk;
+    __syncthreads();
+    int add = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; ++q) {
+      add += wcnt[q][tid];
+      wcnt[q][tid] = 0;
+    }
+    run[tid] += add;
+    __syncthreads();
+  }
+  // digit starts inside the tile (exclusive scan of the 256 counts)
+  const int my = run[tid];
+  int inc = my;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  for (int q = 0; q < w; ++q) inc += wsum[q];
+  const int start = inc - my;
+  gb[tid] = offs[(int64_t)tid * tiles + blockIdx.x] - start;
+  run[tid] = start;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRsItems; ++r) {
+    if (r * kBlock + tid < in_tile) {
+      const int p = run[rs_digit(key[r], shift)] + loc[r];
+      sk[p] = key[r];
+      sv[p] = val[r];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRsItems; ++r) {
+    const int e = r * kBlock + tid;
+    if (e < in_tile) {
+      const K k = sk[e];
+      const int64_t pos = (int64_t)gb[rs_digit(k, shift)] + e;
+      kout[pos] = k;
+      vout[pos] = sv[e];
+    }
+  }
+}
+
+// Runs of the sorted keys: the claimer of each occupied voxel (flag + the
+// run's sorted position, indexed by point id) and one past the run's end
+// (indexed by cell); counters[1] = points inside the grid.
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_runs(const K* __restrict__ skey, const int32_t* __restrict__ sid,
+                                                 int64_t n, K sentinel, int32_t* __restrict__ pt_flag,
+                                                 int32_t* __restrict__ pt_run, int32_t* __restrict__ cell_end,
+                                                 int32_t* __restrict__ counters) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const K k = skey[j];
+    if (k == sentinel) continue;
+    if (j == 0 || skey[j - 1] != k) {
+      const int id = sid[j];
+      pt_flag[id] = 1;
+      pt_run[id] = (int)j;
+    }
+    const K nx = j + 1 < n ? skey[j + 1] : sentinel;
+    if (nx != k) {
+      cell_end[(int64_t)k] = (int)(j + 1);
+      if (nx == sentinel) counters[1] = (int)(j + 1);
+    }
   }
 }
 
 // ---- voxel reservoir (claim_occ overflow, qpiw.py:283-298): radix select of
 // the key of rank max_o - 1 among the occupied voxels' keys, 8 bits per pass,
-// most significant first.  SelState lives in device memory; hist[256] beside it.
+// most significant first.  Pass q counts into its own 256-bin histogram; every
+// later kernel re-derives the digits fixed so far from those histograms, so
+// no launch is spent on the pick.  Nothing runs when the voxels fit max_o.
+constexpr int kSelPasses = 8;
 struct SelState {
-  unsigned long long prefix;   // key bits fixed so far (after the last pass: the threshold key)
-  unsigned long long k;        // rank still to find below the fixed prefix
-  int all;                     // 1: n_voxels <= max_o, every voxel kept
-  int pad;
+  int32_t active;  // 1: more occupied voxels than max_o
+  int32_t pad;
 };
 
 __global__ void k_sel_init(const int32_t* __restrict__ n_vox, int max_o, SelState* st, uint32_t* hist) {
-  hist[threadIdx.x] = 0;
-  if (threadIdx.x == 0) {
-    st->all = *n_vox <= max_o;
-    st->prefix = 0;
-    st->k = (unsigned long long)(max_o - 1);
+  for (int i = threadIdx.x; i < kSelPasses * 256; i += blockDim.x) hist[i] = 0;
+  if (threadIdx.x == 0) st->active = *n_vox > max_o ? 1 : 0;
+}
+
+// Block of 256: s[0] = the key bits fixed by passes 0..npass-1, s[1] = the
+// rank still to find below them (the digit of pass q: the first whose running
+// count exceeds the rank, else 255).
+__device__ void sel_derive(const uint32_t* __restrict__ hist, int npass, int max_o, unsigned long long* s,
+                           uint32_t* wtot) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) {
+    s[0] = 0ull;
+    s[1] = (unsigned long long)(max_o - 1);
+  }
+  __syncthreads();
+  for (int q = 0; q < npass; ++q) {
+    const unsigned long long k = s[1];
+    const uint32_t v = hist[q * 256 + t];
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(inc, o);
+      if (lane >= o) inc += x;
+    }
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    for (int i = 0; i < w; ++i) inc += wtot[i];
+    const unsigned long long ex = inc - v;
+    if (ex <= k && (t == 255 || k < inc)) {
+      s[0] |= (unsigned long long)t << (56 - 8 * q);
+      s[1] = k - ex;
+    }
+    __syncthreads();
   }
 }
 
 __global__ void __launch_bounds__(kBlock) k_sel_hist(int64_t n, const int32_t* __restrict__ flag, uint64_t seed,
-                                                     int shift, const SelState* __restrict__ st,
+                                                     int pass, int max_o, const SelState* __restrict__ st,
                                                      uint32_t* __restrict__ hist) {
+  if (!st->active) return;
   __shared__ uint32_t h[256];
+  __shared__ unsigned long long s[2];
+  __shared__ uint32_t wtot[kBlock / 64];
   h[threadIdx.x] = 0;
-  __syncthreads();
-  const bool all = st->all;
-  const unsigned long long prefix = st->prefix;
+  sel_derive(hist, pass, max_o, s, wtot);
+  const unsigned long long prefix = s[0];
+  const int shift = 56 - 8 * pass;
   const unsigned long long hi = shift >= 56 ? 0ull : (~0ull << (shift + 8));
-  if (!all) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-      if (!flag[i]) continue;
-      const unsigned long long key = res_vkey(seed, (uint32_t)i);
-      if (((key ^ prefix) & hi) == 0) atomicAdd(&h[(key >> shift) & 255u], 1u);
-    }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!flag[i]) continue;
+    const unsigned long long key = res_vkey(seed, (uint32_t)i);
+    if (((key ^ prefix) & hi) == 0) atomicAdd(&h[(key >> shift) & 255u], 1u);
   }
   __syncthreads();
-  if (!all && h[threadIdx.x]) atomicAdd(hist + threadIdx.x, h[threadIdx.x]);
+  if (h[threadIdx.x]) atomicAdd(hist + pass * 256 + threadIdx.x, h[threadIdx.x]);
 }
 
-__global__ void k_sel_pick(int shift, SelState* st, uint32_t* hist) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = hist[threadIdx.x];
-  __syncthreads();
-  if (threadIdx.x == 0 && !st->all) {
-    unsigned long long cum = 0;
-    int d = 0;
-    for (; d < 255; ++d) {
-      if (cum + h[d] > st->k) break;
-      cum += h[d];
-    }
-    st->prefix |= (unsigned long long)d << shift;
-    st->k -= cum;
-  }
-  hist[threadIdx.x] = 0;
-}
-
-// keep the first point of a voxel only when its voxel is among the max_o kept
-__global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, const SelState* __restrict__ st,
-                                                      int32_t* __restrict__ flag) {
-  if (st->all) return;
-  const unsigned long long thr = st->prefix;
+// keep the claimer of a voxel only when its voxel is among the max_o kept
+__global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, int max_o,
+                                                      const SelState* __restrict__ st,
+                                                      const uint32_t* __restrict__ hist, int32_t* __restrict__ flag) {
+  if (!st->active) return;
+  __shared__ unsigned long long s[2];
+  __shared__ uint32_t wtot[kBlock / 64];
+  sel_derive(hist, kSelPasses, max_o, s, wtot);
+  const unsigned long long thr = s[0];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     if (flag[i] && res_vkey(seed, (uint32_t)i) > thr) flag[i] = 0;
 }
 
-// map_coor2occ (qpiw.py:305-340): slot -> coor_2_occ, dilation of the
-// occupancy by query_size (bitmap, atomicOr).
+// map_coor2occ + fill_occ2pnts (qpiw.py:305-387), one thread per kept
+// claimer: slot -> coor_2_occ / occ_2_coor, the dilation of the occupancy by
+// query_size (idempotent byte stores, packed into bits by k_pack_bits), the
+// voxel's point count (`voxel_idx > 0`, qpiw.py:372: under slot0_drop the
+// voxel holding slot 0 gets no points) and its {xyz, id} records in ascending
+// id order -- all of the run when it fits P, else the P of smallest reservoir
+// key (res_pkey; the reference: reservoir with a time seed).
+template <typename K>
 __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz, int64_t n, GridDev g0,
-                                                  const QGrid* __restrict__ geo, const int64_t* __restrict__ pt_cell,
-                                                  const int32_t* __restrict__ flag,
+                                                  const QGrid* __restrict__ geo, const K* __restrict__ skey,
+                                                  const int32_t* __restrict__ sid, const int32_t* __restrict__ flag,
                                                   const int32_t* __restrict__ pt_slot,
-                                                  int32_t* __restrict__ coor_2_occ,
-                                                  int32_t* __restrict__ occ_2_coor,
-                                                  uint8_t* __restrict__ occ_bytes) {
+                                                  const int32_t* __restrict__ pt_run,
+                                                  const int32_t* __restrict__ cell_end,
+                                                  int32_t* __restrict__ coor_2_occ, int32_t* __restrict__ occ_2_coor,
+                                                  uint8_t* __restrict__ occ_bytes, int32_t* __restrict__ occ_numpnts,
+                                                  float4* __restrict__ occ_pts, int32_t* counters) {
   const GridDev g = with_geom(g0, geo);
+  int dropped = 0, mx = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (!flag[i]) continue;
     const int slot = pt_slot[i];
     if (slot >= g.max_o) continue;  // never: the reservoir kept <= max_o voxels
-    const int64_t cell = pt_cell[i];
+    const int j = pt_run[i];
+    const int64_t cell = (int64_t)skey[j];
+    const int cnt = cell_end[cell] - j;
     int c[3];
     c[2] = (int)(cell % g.dims[2]);
     c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
@@ -277,10 +442,61 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
     const int z0 = max(0, c[2] - g.qs[2] / 2), z1 = min(g.dims[2], c[2] + (g.qs[2] + 1) / 2);
     for (int x = x0; x < x1; ++x)
       for (int y = y0; y < y1; ++y)
-        for (int z = z0; z < z1; ++z) {
-          // idempotent byte stores (no atomics); packed into bits by k_pack_bits
-          occ_bytes[((int64_t)x * g.dims[1] + y) * g.dims[2] + z] = 1;
+        for (int z = z0; z < z1; ++z) occ_bytes[((int64_t)x * g.dims[1] + y) * g.dims[2] + z] = 1;
+
+    const int cnt_kept = (g.slot0_drop && slot == 0) ? 0 : cnt;
+    occ_numpnts[slot] = cnt_kept;
+    const int keep = min(cnt_kept, g.P);
+    const int32_t* ids = sid + j;
+    float4* dst = occ_pts + (int64_t)slot * g.P;
+    if (cnt_kept > g.P) {
+      // reservoir: threshold = the P-th smallest key of the voxel's points
+      uint64_t thr = 0;
+      bool first = true;
+      for (int q = 0; q < g.P; ++q) {
+        uint64_t best = ~0ull;
+        for (int e = 0; e < cnt_kept; ++e) {
+          const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
+          if ((first || k > thr) && k < best) best = k;
         }
+        thr = best;
+        first = false;
+      }
+      int q = 0;
+      for (int e = 0; e < cnt_kept && q < keep; ++e) {  // the run is in ascending id order
+        const int v = ids[e];
+        if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
+        dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
+                               __int_as_float(v));
+      }
+    } else {
+      for (int q = 0; q < keep; ++q) {
+        const int v = ids[q];
+        dst[q] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
+                             __int_as_float(v));
+      }
+    }
+    dropped += cnt_kept - keep;
+    mx = max(mx, cnt_kept);
+  }
+  dropped = wave_sum_i32(dropped);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  __shared__ int red[2][kBlock / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = dropped;
+    red[1][w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int d = 0, m = 0;
+    for (int q = 0; q < kBlock / 64; ++q) {
+      d += red[0][q];
+      m = max(m, red[1][q]);
+    }
+    if (d) atomicAdd(counters + 2, d);
+    if (m) atomicMax(counters + 3, m);
   }
 }
 
@@ -298,116 +514,6 @@ __global__ void __launch_bounds__(kBlock) k_pack_bits(const uint8_t* __restrict_
 #pragma unroll
       for (int k = 0; k < 4; ++k) bits |= ((v[q] >> (8 * k)) & 0xffu ? 1u : 0u) << (4 * q + k);
     occ_bits[w] = bits;
-  }
-}
-
-// fill_occ2pnts (qpiw.py:342-387) part 1: per-voxel counts.  `voxel_idx > 0`
-// (qpiw.py:372) when slot0_drop: the voxel holding slot 0 gets no points.
-__global__ void __launch_bounds__(kBlock) k_count(int64_t n, GridDev g, const int64_t* __restrict__ pt_cell,
-                                                  const int32_t* __restrict__ coor_2_occ,
-                                                  int32_t* __restrict__ occ_numpnts) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t cell = pt_cell[i];
-    if (cell < 0) continue;
-    const int slot = coor_2_occ[cell];
-    if (slot < 0 || (g.slot0_drop && slot == 0)) continue;
-    atomicAdd(occ_numpnts + slot, 1);
-  }
-}
-
-// part 2: bucket every point of a kept voxel (arrival order arbitrary).
-__global__ void __launch_bounds__(kBlock) k_scatter(int64_t n, GridDev g, const int64_t* __restrict__ pt_cell,
-                                                    const int32_t* __restrict__ coor_2_occ,
-                                                    const int32_t* __restrict__ slot_off,
-                                                    int32_t* __restrict__ cursor,
-                                                    int32_t* __restrict__ bucket) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t cell = pt_cell[i];
-    if (cell < 0) continue;
-    const int slot = coor_2_occ[cell];
-    if (slot < 0 || (g.slot0_drop && slot == 0)) continue;
-    const int pos = atomicAdd(cursor + slot, 1);
-    bucket[slot_off[slot] + pos] = (int)i;
-  }
-}
-
-// part 3: per slot write {xyz, id} records of the kept points in ascending id
-// order: all of them (the serial arrival order) when they fit P, else the P of
-// smallest reservoir key (res_pkey; the reference: reservoir with a time seed).
-__global__ void __launch_bounds__(kBlock) k_select(int n_slots, GridDev g, const float* __restrict__ xyz,
-                                                   const int32_t* __restrict__ occ_numpnts,
-                                                   const int32_t* __restrict__ slot_off,
-                                                   const int32_t* __restrict__ bucket,
-                                                   float4* __restrict__ occ_pts, int32_t* counters) {
-  int dropped = 0, mx = 0;
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
-    const int cnt = occ_numpnts[s];
-    if (cnt == 0) continue;
-    const int off = slot_off[s];
-    const int keep = min(cnt, g.P);
-    int prev = -1;
-    if (cnt > g.P) {
-      // reservoir: threshold = the P-th smallest key of the voxel's points
-      uint64_t thr = 0;
-      bool first = true;
-      for (int q = 0; q < g.P; ++q) {
-        uint64_t best = ~0ull;
-        for (int j = 0; j < cnt; ++j) {
-          const uint64_t k = res_pkey(g.seed, (uint32_t)bucket[off + j]);
-          if ((first || k > thr) && k < best) best = k;
-        }
-        thr = best;
-        first = false;
-      }
-      for (int q = 0; q < keep; ++q) {
-        int best = 0x7fffffff;
-        for (int j = 0; j < cnt; ++j) {
-          const int v = bucket[off + j];
-          if (v > prev && v < best && res_pkey(g.seed, (uint32_t)v) <= thr) best = v;
-        }
-        prev = best;
-        occ_pts[(int64_t)s * g.P + q] =
-            make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
-                        __int_as_float(best));
-      }
-    } else if (cnt <= 16) {
-      // the (typical) small voxel: its ids in registers, one round of loads
-      int vals[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) vals[j] = j < cnt ? bucket[off + j] : 0x7fffffff;
-      for (int q = 0; q < keep; ++q) {
-        int best = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) best = (vals[j] > prev && vals[j] < best) ? vals[j] : best;
-        prev = best;
-        occ_pts[(int64_t)s * g.P + q] =
-            make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
-                        __int_as_float(best));
-      }
-    } else {
-      for (int q = 0; q < keep; ++q) {
-        int best = 0x7fffffff;
-        for (int j = 0; j < cnt; ++j) {
-          int v = bucket[off + j];
-          best = (v > prev && v < best) ? v : best;
-        }
-        prev = best;
-        occ_pts[(int64_t)s * g.P + q] =
-            make_float4(xyz[(int64_t)best * 3], xyz[(int64_t)best * 3 + 1], xyz[(int64_t)best * 3 + 2],
-                        __int_as_float(best));
-      }
-    }
-    dropped += cnt - keep;
-    mx = max(mx, cnt);
-  }
-  dropped = wave_sum_i32(dropped);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-  if ((threadIdx.x & 63) == 0) {
-    if (dropped) atomicAdd(counters + 2, dropped);
-    atomicMax(counters + 3, mx);
   }
 }
 
@@ -467,14 +573,17 @@ __global__ void __launch_bounds__(kBlock) k_rank_slots(int n_slots, GridDev g0, 
   }
 }
 
+// 16 lanes per rank: a voxel's records are one contiguous read and write
 __global__ void __launch_bounds__(kBlock) k_fill_recs(GridDev g, const int32_t* __restrict__ n_ranks,
                                                       const int32_t* __restrict__ rank_slot,
                                                       const int32_t* __restrict__ rec_off,
                                                       const float4* __restrict__ occ_pts, float4* __restrict__ recs) {
-  const int nr = *n_ranks;
-  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += gridDim.x * blockDim.x) {
+  const int64_t nr = *n_ranks;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nr * 16;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t >> 4;
     const int s = rank_slot[r], o = rec_off[r], c = rec_off[r + 1] - o;
-    for (int q = 0; q < c; ++q) recs[o + q] = occ_pts[(int64_t)s * g.P + q];
+    for (int q = (int)(t & 15); q < c; q += 16) recs[o + q] = occ_pts[(int64_t)s * g.P + q];
   }
 }
 
@@ -496,6 +605,81 @@ extern "C" int pnr_points_bbox(const float* xyz_dev, int64_t n, float* out6_dev,
   return PNR_OK;
 }
 
+// Sort, claim, count and fill (K: the cell key type, uint32 unless the grid
+// has 2^32 - 1 cells or more).
+template <typename K>
+static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const GridDev& g, int64_t gvol,
+                        int64_t words, int64_t cap_o, hipStream_t st) {
+  int rc;
+  const QGrid* geo = h->geom.as<QGrid>();
+  int32_t* counters = h->counters.as<int32_t>();
+  int32_t* pt_flag = h->pt_flag.as<int32_t>();
+  int32_t* pt_slot = h->pt_slot.as<int32_t>();
+  int32_t* pt_run = h->pt_run.as<int32_t>();
+  int32_t* cell_end = h->cell_end.as<int32_t>();
+  const K sentinel = (K)gvol;
+  const int bits = 64 - __builtin_clzll((unsigned long long)gvol);
+  const int passes = (bits + 7) / 8;
+  const int tiles = (int)cdiv(n, kRsTile);
+  const unsigned gp = grid_for(n, kBlock);
+
+  // (cell, point id) sorted by cell, ids ascending inside a cell
+  K* keys[2] = {h->sort_k[0].as<K>(), h->sort_k[1].as<K>()};
+  int32_t* vals[2] = {h->sort_v[0].as<int32_t>(), h->sort_v[1].as<int32_t>()};
+  hipLaunchKernelGGL(k_cell_keys<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, sentinel, keys[0]);
+  PNR_LAUNCH_CHECK();
+  int cur = 0;
+  for (int pass = 0; pass < passes; ++pass) {
+    const int shift = 8 * pass;
+    hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], n, shift, tiles,
+                       h->sort_hist.as<int32_t>());
+    PNR_LAUNCH_CHECK();
+    if ((rc = exclusive_scan(h->sort_hist.as<int32_t>(), (int64_t)256 * tiles, nullptr, h->sort_offs.as<int32_t>(),
+                             nullptr, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+      return rc;
+    hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], pass ? vals[cur] : nullptr, n,
+                       shift, tiles, h->sort_offs.as<int32_t>(), keys[cur ^ 1], vals[cur ^ 1]);
+    PNR_LAUNCH_CHECK();
+    cur ^= 1;
+  }
+  const K* skey = keys[cur];
+  const int32_t* sid = vals[cur];
+  hipLaunchKernelGGL(k_runs<K>, dim3(gp), dim3(kBlock), 0, st, skey, sid, n, sentinel, pt_flag, pt_run, cell_end,
+                     counters);
+  PNR_LAUNCH_CHECK();
+  // slot = rank of the claimer's point id (the serial claim order)
+  if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+    return rc;
+  if (n > cap_o) {
+    // more points than max_o: the occupied voxels may overflow it (counters[0]
+    // holds their number on the device); keep the reservoir's max_o of them
+    SelState* ss = h->sel.as<SelState>();
+    uint32_t* hist = reinterpret_cast<uint32_t*>(ss + 1);
+    const unsigned gs = grid_for(n, kBlock, 1024);
+    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, counters, (int)cap_o, ss, hist);
+    PNR_LAUNCH_CHECK();
+    for (int pass = 0; pass < kSelPasses; ++pass) {
+      hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(kBlock), 0, st, n, pt_flag, g.seed, pass, (int)cap_o, ss, hist);
+      PNR_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_sel_apply, dim3(gs), dim3(kBlock), 0, st, n, g.seed, (int)cap_o, ss, hist, pt_flag);
+    PNR_LAUNCH_CHECK();
+    if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 6, h->scan_tmp.p, h->scan_tmp.bytes, st, 0,
+                             &ss->active)))
+      return rc;
+  }
+  uint8_t* occ_bytes = h->cell_bytes.as<uint8_t>();
+  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
+  hipLaunchKernelGGL(k_claim<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, skey, sid, pt_flag, pt_slot,
+                     pt_run, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(), occ_bytes,
+                     h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), counters);
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words,
+                     h->occ_bits.as<uint32_t>());
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
+}
+
 // The build proper (both entry points): p gives the allocation bounds (dims)
 // and the by-value parameters; the exact geometry is already in h->geom.
 static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const pnr_grid_params* p,
@@ -509,31 +693,27 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   int rc;
   const int64_t words = cdiv(gvol, 32);
   const int64_t cap_o = p->max_o;
-  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->first_pt.ensure(gvol * 4 > words * 36 + 16 ? gvol * 4 : words * 36 + 16)) ||
-      (rc = h->occ_bits.ensure(words * 4)) || (rc = h->occ_numpnts.ensure(cap_o * 4)) ||
-      (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
-      (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->slot_cursor.ensure(cap_o * 4)) ||
-      (rc = h->slot_off.ensure((cap_o + 1) * 4)) || (rc = h->pt_cell.ensure(n * 8)) ||
+  const bool wide = gvol >= ((int64_t)1 << 32) - 1;   // the sentinel key gvol must fit the key type
+  const size_t kbytes = wide ? 8 : 4;
+  const int64_t hist_n = (int64_t)256 * cdiv(n, kRsTile) + 1;
+  int64_t scan_n = n;
+  for (int64_t m : {cap_o, words, hist_n}) scan_n = m > scan_n ? m : scan_n;
+  if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->cell_end.ensure(gvol * 4)) ||
+      (rc = h->cell_bytes.ensure(words * 36 + 16)) || (rc = h->occ_bits.ensure(words * 4)) ||
+      (rc = h->occ_numpnts.ensure(cap_o * 4)) || (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
+      (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->sort_k[0].ensure(n * kbytes)) ||
+      (rc = h->sort_k[1].ensure(n * kbytes)) || (rc = h->sort_v[0].ensure(n * 4)) ||
+      (rc = h->sort_v[1].ensure(n * 4)) || (rc = h->sort_hist.ensure(hist_n * 4)) ||
+      (rc = h->sort_offs.ensure(hist_n * 4)) || (rc = h->pt_run.ensure(n * 4)) ||
       (rc = h->pt_flag.ensure(n * 4)) || (rc = h->pt_slot.ensure((n + 1) * 4)) ||
-      (rc = h->bucket.ensure(n * 4)) || (rc = h->counters.ensure(8 * 4)) ||
-      (rc = h->sel.ensure(sizeof(SelState) + 256 * 4)) ||
-      (rc = h->scan_tmp.ensure(scan_scratch_bytes(n > cap_o ? (n > words ? n : words) : (cap_o > words ? cap_o : words)))) ||
+      (rc = h->counters.ensure(8 * 4)) || (rc = h->sel.ensure(sizeof(SelState) + kSelPasses * 256 * 4)) ||
+      (rc = h->scan_tmp.ensure(scan_scratch_bytes(scan_n))) ||
       (rc = h->q_words.ensure(words * 8)) || (rc = h->q_wcnt.ensure((words + 1) * 4)) ||
       (rc = h->q_rank_slot.ensure(cap_o * 4)) || (rc = h->q_rank_cnt.ensure(cap_o * 4)) ||
       (rc = h->q_rec_off.ensure((cap_o + 1) * 4)) || (rc = h->q_recs.ensure(n * sizeof(float4))))
     return rc;
-  int32_t* coor_2_occ = h->coor_2_occ.as<int32_t>();
-  int32_t* first_pt = h->first_pt.as<int32_t>();
-  uint32_t* occ_bits = h->occ_bits.as<uint32_t>();
   int32_t* occ_numpnts = h->occ_numpnts.as<int32_t>();
-  float4* occ_pts = h->occ_pts.as<float4>();
   int32_t* occ_2_coor = h->occ_2_coor.as<int32_t>();
-  int32_t* slot_cursor = h->slot_cursor.as<int32_t>();
-  int32_t* slot_off = h->slot_off.as<int32_t>();
-  int64_t* pt_cell = h->pt_cell.as<int64_t>();
-  int32_t* pt_flag = h->pt_flag.as<int32_t>();
-  int32_t* pt_slot = h->pt_slot.as<int32_t>();
-  int32_t* bucket = h->bucket.as<int32_t>();
   int32_t* counters = h->counters.as<int32_t>();
   const QGrid* geo = h->geom.as<QGrid>();
 
@@ -549,67 +729,21 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   g.slot0_drop = p->slot0_drop;
   g.seed = p->seed;
 
-  PNR_HIP(hipMemsetAsync(first_pt, 0x7f, (size_t)gvol * 4, st));
-  PNR_HIP(hipMemsetAsync(coor_2_occ, 0xff, (size_t)gvol * 4, st));
+  PNR_HIP(hipMemsetAsync(h->coor_2_occ.p, 0xff, (size_t)gvol * 4, st));
+  PNR_HIP(hipMemsetAsync(h->pt_flag.p, 0, (size_t)n * 4, st));
   PNR_HIP(hipMemsetAsync(occ_numpnts, 0, (size_t)cap_o * 4, st));
-  PNR_HIP(hipMemsetAsync(slot_cursor, 0, (size_t)cap_o * 4, st));
   PNR_HIP(hipMemsetAsync(occ_2_coor, 0xff, (size_t)cap_o * 12, st));
   PNR_HIP(hipMemsetAsync(counters, 0, 8 * 4, st));
-
-  const unsigned gp = grid_for(n, kBlock);
-  hipLaunchKernelGGL(k_cells, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, pt_cell, first_pt,
-                     counters);
-  PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_first_flags, dim3(gp), dim3(kBlock), 0, st, n, pt_cell, first_pt, pt_flag);
-  PNR_LAUNCH_CHECK();
-  if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p,
-                           h->scan_tmp.bytes, st)))
+  if ((rc = wide ? build_tables<uint64_t>(h, xyz_dev, n, g, gvol, words, cap_o, st)
+                 : build_tables<uint32_t>(h, xyz_dev, n, g, gvol, words, cap_o, st)))
     return rc;
-  if (n > cap_o) {
-    // more points than max_o: the occupied voxels may overflow it (counters[0]
-    // holds their number on the device); keep the reservoir's max_o of them
-    SelState* ss = h->sel.as<SelState>();
-    uint32_t* hist = reinterpret_cast<uint32_t*>(ss + 1);
-    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, counters, (int)cap_o, ss, hist);
-    PNR_LAUNCH_CHECK();
-    for (int shift = 56; shift >= 0; shift -= 8) {
-      hipLaunchKernelGGL(k_sel_hist, dim3(gp), dim3(kBlock), 0, st, n, pt_flag, g.seed, shift, ss, hist);
-      PNR_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(256), 0, st, shift, ss, hist);
-      PNR_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_sel_apply, dim3(gp), dim3(kBlock), 0, st, n, g.seed, ss, pt_flag);
-    PNR_LAUNCH_CHECK();
-    if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 6, h->scan_tmp.p, h->scan_tmp.bytes, st)))
-      return rc;
-  }
-  // first_pt is dead after k_first_flags: its storage (4 B/cell) holds the
-  // dilated occupancy bytes (32 * words <= 4 * gvol bytes)
-  uint8_t* occ_bytes = reinterpret_cast<uint8_t*>(first_pt);
-  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
-  hipLaunchKernelGGL(k_claim, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, pt_cell, pt_flag,
-                     pt_slot, coor_2_occ, occ_2_coor, occ_bytes);
-  PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, occ_bits);
-  PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_count, dim3(gp), dim3(kBlock), 0, st, n, g, pt_cell, coor_2_occ,
-                     occ_numpnts);
-  PNR_LAUNCH_CHECK();
-  if ((rc = exclusive_scan(occ_numpnts, cap_o, nullptr, slot_off, nullptr, h->scan_tmp.p,
-                           h->scan_tmp.bytes, st)))
-    return rc;
-  hipLaunchKernelGGL(k_scatter, dim3(gp), dim3(kBlock), 0, st, n, g, pt_cell, coor_2_occ,
-                     slot_off, slot_cursor, bucket);
-  PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_select, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g,
-                     xyz_dev, occ_numpnts, slot_off, bucket, occ_pts, counters);
-  PNR_LAUNCH_CHECK();
-
+  float4* occ_pts = h->occ_pts.as<float4>();
+  uint8_t* occ_bytes = h->cell_bytes.as<uint8_t>();
   // query index: held voxels ranked in cell order (k_knn's tables)
   {
     uint2* qw = h->q_words.as<uint2>();
     int32_t* wcnt = h->q_wcnt.as<int32_t>();
-    int32_t* wrank = h->first_pt.as<int32_t>() + words * 8;   // after the cell bytes (32 B per word)
+    int32_t* wrank = reinterpret_cast<int32_t*>(occ_bytes + words * 32);   // after the cell bytes
     PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
     hipLaunchKernelGGL(k_mark_held, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, geo,
                        occ_numpnts, occ_2_coor, occ_bytes);
@@ -626,7 +760,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
     if ((rc = exclusive_scan(h->q_rank_cnt.as<int32_t>(), cap_o, counters + 4, h->q_rec_off.as<int32_t>(),
                              counters + 5, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
-    hipLaunchKernelGGL(k_fill_recs, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, g, counters + 4,
+    hipLaunchKernelGGL(k_fill_recs, dim3(grid_for(cap_o * 16, kBlock)), dim3(kBlock), 0, st, g, counters + 4,
                        h->q_rank_slot.as<int32_t>(), h->q_rec_off.as<int32_t>(), occ_pts, h->q_recs.as<float4>());
     PNR_LAUNCH_CHECK();
   }

@@ -50,7 +50,8 @@ int64_t scan_blocks(int64_t n);
 size_t scan_scratch_bytes(int64_t n);
 int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
                    int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
-                   int as_flag = 0);  // as_flag: scan (in[i] != 0) instead of in[i]
+                   int as_flag = 0,   // as_flag: scan (in[i] != 0) instead of in[i]
+                   const int32_t* run_if = nullptr);  // device flag: 0 = leave out untouched
 
 // --------------------------------------------------------- device helpers
 // floor((p - shift) / vs) exactly as the reference kernels compute it in fp32
@@ -159,18 +160,20 @@ struct pnr_handle {
   int64_t gvol = 0;       // dims[0]*dims[1]*dims[2]
   DevBuf coor_2_occ;      // int32 [gvol]   cell -> slot, -1 = empty
   DevBuf occ_bits;        // uint32 [gvol/32] dilated occupancy bitmap
-  DevBuf first_pt;        // int32 [gvol]   smallest point id per cell
+  DevBuf cell_end;        // int32 [gvol]   one past the last sorted position of the cell's run (occupied cells only)
+  DevBuf cell_bytes;      // uint8 [32*words] + int32 [words+1]: occupancy bytes before packing, word ranks
   DevBuf occ_numpnts;     // int32 [max_o]  points that fell in the voxel
   DevBuf occ_pts;         // float4 [max_o*P] {x, y, z, bitcast(point id)}
   DevBuf occ_2_coor;      // int32 [max_o*3]
-  DevBuf slot_cursor;     // int32 [max_o]
-  DevBuf slot_off;        // int32 [max_o+1]
-  DevBuf pt_cell;         // int64 [N]      cell of every point, -1 outside the grid
+  DevBuf sort_k[2];       // uint32/uint64 [N] cell keys (ping-pong of the LSD radix sort)
+  DevBuf sort_v[2];       // int32 [N]      point ids riding with the keys
+  DevBuf sort_hist;       // int32 [256*tiles + 1] per-tile digit counts, then their exclusive scan
+  DevBuf sort_offs;       // int32 [256*tiles + 1]
+  DevBuf pt_run;          // int32 [N]      sorted position of a claimer's run (claimers only)
   DevBuf pt_flag;         // int32 [N]
   DevBuf pt_slot;         // int32 [N+1]
-  DevBuf bucket;          // int32 [N]
   DevBuf counters;        // int32 [8]
-  DevBuf sel;             // voxel reservoir: radix-select state + 256-bin histogram
+  DevBuf sel;             // voxel reservoir: radix-select state + 8 x 256-bin histograms
   DevBuf scan_tmp;
   // Query index (what k_knn reads; the slot tables above stay the reference's
   // view for export / parity): the voxels that hold points, ranked in x-major
@@ -202,9 +205,9 @@ struct pnr_handle {
     host_cnt = nullptr;
     stats_ev = nullptr;
     stats_pending = false;
-    DevBuf* all[] = {&coor_2_occ, &occ_bits, &first_pt, &occ_numpnts, &occ_pts, &occ_2_coor,
-                     &slot_cursor, &slot_off, &pt_cell, &pt_flag, &pt_slot, &bucket,
-                     &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
+    DevBuf* all[] = {&coor_2_occ, &occ_bits, &cell_end, &cell_bytes, &occ_numpnts, &occ_pts, &occ_2_coor,
+                     &sort_k[0], &sort_k[1], &sort_v[0], &sort_v[1], &sort_hist, &sort_offs,
+                     &pt_run, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
                      &q_rec_off, &q_recs, &geom, &bbox};
     for (DevBuf* b : all) b->release();
   }

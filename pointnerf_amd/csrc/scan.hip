@@ -53,8 +53,9 @@ __device__ __forceinline__ int load_item(const int32_t* in, int64_t i, int64_t n
 
 __global__ void __launch_bounds__(kScanBlock) k_scan_reduce(const int32_t* __restrict__ in, int64_t n,
                                                             const int32_t* n_dev, int as_flag,
-                                                            int32_t* __restrict__ sums) {
+                                                            int32_t* __restrict__ sums, const int32_t* run_if) {
   __shared__ int lds4[4];
+  if (run_if && *run_if == 0) return;
   const int64_t ne = eff_len(n, n_dev);
   const int64_t start = (int64_t)blockIdx.x * kScanTile;
   if (start >= ne) {
@@ -76,8 +77,9 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_reduce(const int32_t* __res
 // to out[n_eff] and total_dev.
 __global__ void __launch_bounds__(kScanBlock) k_scan_sums(int32_t* sums, int64_t nb, int64_t n,
                                                           const int32_t* n_dev, int32_t* out,
-                                                          int32_t* total_dev) {
+                                                          int32_t* total_dev, const int32_t* run_if) {
   __shared__ int lds4[4];
+  if (run_if && *run_if == 0) return;
   const int64_t per = cdiv(nb, kScanBlock);
   const int64_t b0 = threadIdx.x * per;
   int acc = 0;
@@ -98,9 +100,10 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_sums(int32_t* sums, int64_t
 __global__ void __launch_bounds__(kScanBlock) k_scan_final(const int32_t* __restrict__ in, int64_t n,
                                                            const int32_t* n_dev, int as_flag,
                                                            const int32_t* __restrict__ sums,
-                                                           int32_t* __restrict__ out) {
+                                                           int32_t* __restrict__ out, const int32_t* run_if) {
   __shared__ int tile[kScanTile];
   __shared__ int lds4[4];
+  if (run_if && *run_if == 0) return;
   const int64_t ne = eff_len(n, n_dev);
   const int64_t start = (int64_t)blockIdx.x * kScanTile;
   if (start >= ne) return;
@@ -138,7 +141,7 @@ size_t scan_scratch_bytes(int64_t n) { return (size_t)(scan_blocks(n) + 1) * siz
 
 int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
                    int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
-                   int as_flag) {
+                   int as_flag, const int32_t* run_if) {
   PNR_CHECK_ARG(in && out && scratch, "scan: null pointer");
   PNR_CHECK_ARG(n >= 0, "scan: negative length");
   const int64_t nb = scan_blocks(n);
@@ -146,11 +149,11 @@ int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* 
                 scratch_bytes, scan_scratch_bytes(n));
   PNR_CHECK_ARG(nb < (int64_t)1 << 31, "scan: too many tiles");
   int32_t* sums = static_cast<int32_t*>(scratch);
-  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums);
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, run_if);
   PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanBlock), 0, st, sums, nb, n, n_dev, out, total_dev);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanBlock), 0, st, sums, nb, n, n_dev, out, total_dev, run_if);
   PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, out);
+  hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, out, run_if);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

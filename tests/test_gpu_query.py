@@ -46,6 +46,30 @@ def test_grid_tables_bit_exact(cuda, slot0_drop):
         assert g["occ_numpnts"][0] == 0  # the fill_occ2pnts `voxel_idx > 0` quirk (qpiw.py:372)
 
 
+@pytest.mark.parametrize("n,max_o,P", [(20000, 1500, 1), (3, 8, 2), (70000, 400000, 9)])
+def test_grid_tables_bit_exact_sizes_and_overflow(cuda, n, max_o, P):
+    """The radix-sorted build across tile counts (1, 2 ragged ... 18 tiles of
+    4096 keys) and with both reservoirs active (max_o and P overflow)."""
+    sc = scene(max(n, 20000), max_o=max_o, P=P)
+    xyz = sc["xyz"][:n].copy()
+    q = _engine(sc, cuda)
+    q.grid.build(sc["opt"], torch.from_numpy(xyz).to(cuda))
+    g = O.grid_build(sc["opt"], xyz)
+    t = q.grid.export()
+    assert np.array_equal(t["coor_2_occ"].cpu().numpy(), g["coor_2_occ"])
+    assert np.array_equal(t["occ_numpnts"].cpu().numpy(), g["occ_numpnts"])
+    assert np.array_equal(t["occ_2_pnts"].cpu().numpy(), g["occ_2_pnts"])
+    bits = t["occ_bits"].cpu().numpy().view(np.uint32)
+    occ = ((bits[:, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(-1)[: g["coor_occ"].size]
+    assert np.array_equal(occ.astype(np.uint8), g["coor_occ"])
+    st = q.grid.stats()
+    assert st["n_voxels"] == g["n_occ"]
+    kept = g["occ_numpnts"][: min(max_o, g["n_occ"])]
+    assert st["n_points_dropped"] == int(np.maximum(kept - P, 0).sum())
+    if n == 20000:
+        assert g["n_occ"] > max_o and st["n_points_dropped"] > 0   # both reservoirs ran
+
+
 @pytest.mark.parametrize("K,theta", [(8, 30.0), (4, 130.0)])
 def test_query_points_bit_exact(cuda, K, theta):
     sc = scene(20000, H=48, W=40, theta=theta, K=K)

@@ -1,10 +1,13 @@
 export TMPDIR=/tmp
-O=gpurun_out/r04l; mkdir -p $O
+O=gpurun_out/r04m; mkdir -p $O
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_query.py -q -x --timeout 120 --timeout-method thread > $O/tq.log 2>&1 || { tail -30 $O/tq.log; exit 1; }
+tail -1 $O/tq.log
+timeout -k 10 120 python tools/grid_bench.py > $O/grid.json 2>&1 || exit $?; tail -1 $O/grid.json
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/grid_prof -o run -- python tools/grid_bench.py --reps 5 > $O/grid_prof.log 2>&1 || exit $?
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread > $O/t.log 2>&1; rc=$?
 tail -3 $O/t.log; grep -E "^(E  .*(Error|outside)|FAILED)" $O/t.log | head -20; ok $rc || exit $rc
 timeout -k 10 300 python bench.py --mode train > $O/train.json 2>&1 || exit $?; tail -1 $O/train.json | cut -c1-200
 timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || exit $?; tail -1 $O/bench.log | cut -c1-200
 timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline > $O/bench_c5.log 2>&1 || exit $?; tail -1 $O/bench_c5.log | cut -c1-200
-timeout -k 10 300 python tools/_var/run_timed.py > $O/timed.log 2>&1 || exit $?; grep KT= $O/timed.log
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/train_trace -o run -- python bench.py --mode train --steps 6 --warmup 3 --no-cpu-baseline > $O/train_trace.log 2>&1 || exit $?
