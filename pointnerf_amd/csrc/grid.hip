@@ -47,7 +47,21 @@ __global__ void k_bbox_init(unsigned* acc) {
 
 __global__ void __launch_bounds__(kBlock) k_bbox(const float* __restrict__ xyz, int64_t n, unsigned* acc) {
   unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0u, 0u, 0u};
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+  // 4 points (3 x 16 B) per thread and step when xyz is 16-B aligned, the rest one by one
+  const bool vec = (reinterpret_cast<uintptr_t>(xyz) & 15) == 0;
+  const int64_t n4 = vec ? n / 4 : 0;
+  const float4* x4 = reinterpret_cast<const float4*>(xyz);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 a = x4[i * 3], b = x4[i * 3 + 1], c = x4[i * 3 + 2];
+    const float v[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+      const unsigned o = f2ord(v[e]);
+      mn[e % 3] = min(mn[e % 3], o);
+      mx[e % 3] = max(mx[e % 3], o);
+    }
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -163,14 +177,28 @@ __device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int
 template <typename K>
 __global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ xyz, int64_t n, GridDev g0,
                                                       const QGrid* __restrict__ geo, K sentinel,
-                                                      K* __restrict__ keys) {
+                                                      K* __restrict__ keys, int64_t n_slots,
+                                                      int32_t* __restrict__ pt_flag,
+                                                      int32_t* __restrict__ occ_numpnts,
+                                                      int32_t* __restrict__ occ_2_coor, int32_t* __restrict__ counters) {
   const GridDev g = with_geom(g0, geo);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+  if (blockIdx.x == 0 && threadIdx.x < 8) counters[threadIdx.x] = 0;
+  const int64_t m = n > n_slots ? n : n_slots;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * blockDim.x) {
-    float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
-    int c[3];
-    const int64_t cell = cell_of(p, g, c);
-    keys[i] = cell >= 0 ? (K)cell : sentinel;
+    if (i < n) {
+      float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
+      int c[3];
+      const int64_t cell = cell_of(p, g, c);
+      keys[i] = cell >= 0 ? (K)cell : sentinel;
+      pt_flag[i] = 0;
+    }
+    if (i < n_slots) {   // the slot tables' empty state
+      occ_numpnts[i] = 0;
+      occ_2_coor[i * 3 + 0] = -1;
+      occ_2_coor[i * 3 + 1] = -1;
+      occ_2_coor[i * 3 + 2] = -1;
+    }
   }
 }
 
@@ -430,26 +458,28 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
     const int64_t cell = (int64_t)skey[j];
     const int cnt = cell_end[cell] - j;
     int c[3];
-    c[2] = (int)(cell % g.dims[2]);
-    c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
-    c[0] = (int)(cell / ((int64_t)g.dims[2] * g.dims[1]));
+    if (cell <= 0x7fffffff) {   // 32-bit division when the cell index fits
+      const int r = (int)cell / g.dims[2];
+      c[2] = (int)cell - r * g.dims[2];
+      c[0] = r / g.dims[1];
+      c[1] = r - c[0] * g.dims[1];
+    } else {
+      c[2] = (int)(cell % g.dims[2]);
+      c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
+      c[0] = (int)(cell / ((int64_t)g.dims[2] * g.dims[1]));
+    }
     coor_2_occ[cell] = slot;
     occ_2_coor[slot * 3 + 0] = c[0];
     occ_2_coor[slot * 3 + 1] = c[1];
     occ_2_coor[slot * 3 + 2] = c[2];
-    const int x0 = max(0, c[0] - g.qs[0] / 2), x1 = min(g.dims[0], c[0] + (g.qs[0] + 1) / 2);
-    const int y0 = max(0, c[1] - g.qs[1] / 2), y1 = min(g.dims[1], c[1] + (g.qs[1] + 1) / 2);
-    const int z0 = max(0, c[2] - g.qs[2] / 2), z1 = min(g.dims[2], c[2] + (g.qs[2] + 1) / 2);
-    for (int x = x0; x < x1; ++x)
-      for (int y = y0; y < y1; ++y)
-        for (int z = z0; z < z1; ++z) occ_bytes[((int64_t)x * g.dims[1] + y) * g.dims[2] + z] = 1;
+    occ_bytes[cell] = 1;   // dilated by query_size in k_dilate_zy / k_dilate_x
 
     const int cnt_kept = (g.slot0_drop && slot == 0) ? 0 : cnt;
     occ_numpnts[slot] = cnt_kept;
     const int keep = min(cnt_kept, g.P);
     const int32_t* ids = sid + j;
     float4* dst = occ_pts + (int64_t)slot * g.P;
-    if (cnt_kept > g.P) {
+    if (cnt_kept > g.P) {   // (the runs that fit P: k_fill_pts, one thread per point)
       // reservoir: threshold = the P-th smallest key of the voxel's points
       uint64_t thr = 0;
       bool first = true;
@@ -468,12 +498,6 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
         if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
         dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
                                __int_as_float(v));
-      }
-    } else {
-      for (int q = 0; q < keep; ++q) {
-        const int v = ids[q];
-        dst[q] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
-                             __int_as_float(v));
       }
     }
     dropped += cnt_kept - keep;
@@ -497,6 +521,86 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
     }
     if (d) atomicAdd(counters + 2, d);
     if (m) atomicMax(counters + 3, m);
+  }
+}
+
+// fill_occ2pnts' records of the voxels whose run fits P, one thread per
+// sorted point: the run starts at cell_end - count, so the point's record is
+// number j - start of its voxel's slot (runs in ascending id order).
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_fill_pts(const float* __restrict__ xyz, const K* __restrict__ skey,
+                                                     const int32_t* __restrict__ sid, int64_t n, K sentinel, int P,
+                                                     const int32_t* __restrict__ coor_2_occ,
+                                                     const int32_t* __restrict__ occ_numpnts,
+                                                     const int32_t* __restrict__ cell_end,
+                                                     float4* __restrict__ occ_pts) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const K k = skey[j];
+    if (k == sentinel) continue;
+    const int slot = coor_2_occ[(int64_t)k];
+    if (slot < 0) continue;                       // voxel not kept (max_o reservoir)
+    const int c = occ_numpnts[slot];
+    if (c == 0 || c > P) continue;                // slot-0 quirk / P reservoir (k_claim)
+    const int q = (int)j - (cell_end[(int64_t)k] - c);
+    const int v = sid[j];
+    occ_pts[(int64_t)slot * P + q] =
+        make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2], __int_as_float(v));
+  }
+}
+
+// The dilation of map_coor2occ (qpiw.py:321-337: every kept voxel c marks the
+// cells [c - qs/2, c + (qs+1)/2) of each axis, clipped to the grid) as a
+// separable box filter over occupancy bytes: cell v is marked when an
+// occupied voxel lies in [v - (qs+1)/2 + 1, v + qs/2] on every axis.  One wave
+// per (x, y) row of cells, lanes along z; 32-bit row arithmetic only.
+__device__ __forceinline__ void dil_range(int v, int qs, int dim, int& lo, int& hi) {
+  lo = max(0, v - (qs + 1) / 2 + 1);
+  hi = min(dim - 1, v + qs / 2);
+}
+
+// z and y: in = one byte per occupied cell, out = the zy-dilated bytes
+__global__ void __launch_bounds__(kBlock) k_dilate_zy(GridDev g0, const QGrid* __restrict__ geo,
+                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out) {
+  const GridDev g = with_geom(g0, geo);
+  const int rows = g.dims[0] * g.dims[1];
+  const int lane = threadIdx.x & 63;
+  for (int row = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); row < rows;
+       row += (int)((gridDim.x * blockDim.x) >> 6)) {
+    const int x = row / g.dims[1], y = row - x * g.dims[1];
+    int y0, y1;
+    dil_range(y, g.qs[1], g.dims[1], y0, y1);
+    for (int z = lane; z < g.dims[2]; z += 64) {
+      int z0, z1;
+      dil_range(z, g.qs[2], g.dims[2], z0, z1);
+      uint8_t m = 0;
+      for (int yy = y0; yy <= y1; ++yy) {
+        const uint8_t* r = in + ((int64_t)x * g.dims[1] + yy) * g.dims[2];
+        for (int zz = z0; zz <= z1; ++zz) m |= r[zz];
+      }
+      out[(int64_t)row * g.dims[2] + z] = m;
+    }
+  }
+}
+
+// x: in = the zy-dilated bytes, out = the dilated occupancy bytes
+__global__ void __launch_bounds__(kBlock) k_dilate_x(GridDev g0, const QGrid* __restrict__ geo,
+                                                     const uint8_t* __restrict__ in, uint8_t* __restrict__ out) {
+  const GridDev g = with_geom(g0, geo);
+  const int rows = g.dims[0] * g.dims[1];
+  const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+  const int lane = threadIdx.x & 63;
+  for (int row = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); row < rows;
+       row += (int)((gridDim.x * blockDim.x) >> 6)) {
+    const int x = row / g.dims[1];
+    int x0, x1;
+    dil_range(x, g.qs[0], g.dims[0], x0, x1);
+    const int64_t base = (int64_t)row * g.dims[2];
+    for (int z = lane; z < g.dims[2]; z += 64) {
+      uint8_t m = 0;
+      for (int xx = x0; xx <= x1; ++xx) m |= in[base + (int64_t)(xx - x) * plane + z];
+      out[base + z] = m;
+    }
   }
 }
 
@@ -598,7 +702,7 @@ extern "C" int pnr_points_bbox(const float* xyz_dev, int64_t n, float* out6_dev,
   unsigned* acc = reinterpret_cast<unsigned*>(out6_dev);
   hipLaunchKernelGGL(k_bbox_init, dim3(1), dim3(64), 0, st, acc);
   PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bbox, dim3(grid_for(n, kBlock, 512)), dim3(kBlock), 0, st, xyz_dev, n, acc);
+  hipLaunchKernelGGL(k_bbox, dim3(grid_for(cdiv(n, 4), kBlock, 512)), dim3(kBlock), 0, st, xyz_dev, n, acc);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_bbox_fin, dim3(1), dim3(64), 0, st, acc);
   PNR_LAUNCH_CHECK();
@@ -626,7 +730,9 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   // (cell, point id) sorted by cell, ids ascending inside a cell
   K* keys[2] = {h->sort_k[0].as<K>(), h->sort_k[1].as<K>()};
   int32_t* vals[2] = {h->sort_v[0].as<int32_t>(), h->sort_v[1].as<int32_t>()};
-  hipLaunchKernelGGL(k_cell_keys<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, sentinel, keys[0]);
+  hipLaunchKernelGGL(k_cell_keys<K>, dim3(grid_for(n > cap_o ? n : cap_o, kBlock)), dim3(kBlock), 0, st, xyz_dev,
+                     n, g, geo, sentinel, keys[0], cap_o, pt_flag, h->occ_numpnts.as<int32_t>(),
+                     h->occ_2_coor.as<int32_t>(), counters);
   PNR_LAUNCH_CHECK();
   int cur = 0;
   for (int pass = 0; pass < passes; ++pass) {
@@ -674,6 +780,18 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
                      pt_run, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(), occ_bytes,
                      h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), counters);
   PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_fill_pts<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, skey, sid, n, sentinel, g.P,
+                     h->coor_2_occ.as<int32_t>(), h->occ_numpnts.as<int32_t>(), cell_end, h->occ_pts.as<float4>());
+  PNR_LAUNCH_CHECK();
+  {
+    // cell_end is dead after k_fill_pts: its storage holds the zy-dilated bytes
+    uint8_t* zy = h->cell_end.as<uint8_t>();
+    const unsigned gr = grid_for(cdiv((int64_t)g.dims[0] * g.dims[1], kBlock / 64), kBlock, 4096);
+    hipLaunchKernelGGL(k_dilate_zy, dim3(gr), dim3(kBlock), 0, st, g, geo, occ_bytes, zy);
+    PNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dilate_x, dim3(gr), dim3(kBlock), 0, st, g, geo, zy, occ_bytes);
+    PNR_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(k_pack_bits, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words,
                      h->occ_bits.as<uint32_t>());
   PNR_LAUNCH_CHECK();
@@ -729,11 +847,8 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   g.slot0_drop = p->slot0_drop;
   g.seed = p->seed;
 
+  // (pt_flag, the slot tables and the counters are cleared by k_cell_keys)
   PNR_HIP(hipMemsetAsync(h->coor_2_occ.p, 0xff, (size_t)gvol * 4, st));
-  PNR_HIP(hipMemsetAsync(h->pt_flag.p, 0, (size_t)n * 4, st));
-  PNR_HIP(hipMemsetAsync(occ_numpnts, 0, (size_t)cap_o * 4, st));
-  PNR_HIP(hipMemsetAsync(occ_2_coor, 0xff, (size_t)cap_o * 12, st));
-  PNR_HIP(hipMemsetAsync(counters, 0, 8 * 4, st));
   if ((rc = wide ? build_tables<uint64_t>(h, xyz_dev, n, g, gvol, words, cap_o, st)
                  : build_tables<uint32_t>(h, xyz_dev, n, g, gvol, words, cap_o, st)))
     return rc;

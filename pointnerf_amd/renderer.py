@@ -858,6 +858,7 @@ class NeuralPointsRayMarching(nn.Module):
         conf = self.neural_points.points_conf.reshape(-1)
         return _ZeroOneConfLoss.apply(conf, bufs, self.opt.SR, self.opt.K, float(zero_epsilon))
 
+    @staticmethod
     def zero_one_loss(val, zero_epsilon: float = 1e-3):
         """base_rendering_model.py:630-641: mean(log(v) + log(1 - v)), v clamped
         to [eps, 1 - eps]."""

@@ -317,13 +317,16 @@ def test_train_loop_hip_adam_matches_torch_adam(cuda, tp):
             close(a, b, "param", rel=1e-4, scale=1e-4)
             continue
         # fp32h2: a LeakyReLU pre-activation within the split's noise of 0 can take
-        # the other slope in one loop (the two Adams round differently), and Adam's
-        # normalised step then moves those entries by up to ~lr: at most 1e-3 of
-        # the entries, none by more than 10 lr
+        # the other slope in one loop (the two Adams round differently).  One flip
+        # adds a rank-1 term to the weight gradient of every earlier layer
+        # (test_train_h2_grads_vs_x3), so the number of entries it moves is not
+        # small (measured 3 % of block1.0 moved by > 1e-4 of its max); Adam's
+        # normalised step moves each by ~lr at most (measured <= 0.17 lr), while a
+        # wrong gradient would move most entries by ~lr: mean |d| <= 0.05 lr and
+        # max |d| <= 10 lr
+        lr = 1e-3
         d = (a.detach().double() - b.detach().double()).abs().cpu()
-        tol = 1e-4 * d.new_tensor(float(b.abs().max())) + 1e-4 * b.detach().double().abs().cpu()
-        n_out = int((d > tol).sum())
-        assert n_out <= max(1, int(1e-3 * d.numel())) and float(d.max()) <= 10 * 1e-3, (n_out, d.numel(), float(d.max()))
+        assert float(d.mean()) <= 0.05 * lr and float(d.max()) <= 10 * lr, (d.numel(), float(d.mean()), float(d.max()))
 
 
 @pytest.mark.parametrize("x3", [False, True])
