@@ -70,9 +70,11 @@ constexpr int64_t kMarchCoopRays = 32768;
 // 2.238 / 2.242 / 2.055 / 2.176, 4 lanes 2.186 / 2.194 / 2.056 / 2.149, 8 lanes
 // 2.175 / 2.187 / 2.054 / 2.140, 16 lanes 2.191 / 2.204 / 2.075 / 2.150): the
 // per-ray tvals rows are read 32 B at a time instead of one lane per 1.6 KB row.
-constexpr int kMarchLanes = 8;
+constexpr int kMarchLanes = 8, kMarchUnroll = 4;
 constexpr unsigned kMarchGridCap = 1u << 20;
-template <int G>
+// U candidates per lane and step: the U bitmap loads of a lane are in flight
+// together, and the U ballots are taken in candidate order afterwards.
+template <int G, int U>
 __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __restrict__ gq, int SR,
                                                         const uint32_t* __restrict__ occ_bits,
                                                         int32_t* __restrict__ n_filled,
@@ -85,26 +87,34 @@ __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __
     const float c[3] = {q.campos[cam * 3], q.campos[cam * 3 + 1], q.campos[cam * 3 + 2]};
     const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
     int n = 0;   // hits so far: the same in every lane of the group
-    for (int d0 = 0; d0 < q.D && n < SR; d0 += G) {
-      const int d = d0 + gl;
-      bool hit = false;
-      if (d < q.D) {
-        float p[3];
-        ray_point(c, dir, tval(q, r, d), p);
-        const int x = vox_coord(p[0], g.shift[0], g.vs[0]);
-        const int y = vox_coord(p[1], g.shift[1], g.vs[1]);
-        const int z = vox_coord(p[2], g.shift[2], g.vs[2]);
-        if (!(x < 0 || x >= g.dims[0] || y < 0 || y >= g.dims[1] || z < 0 || z >= g.dims[2])) {
-          const int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
-          hit = (occ_bits[id >> 5] >> (id & 31)) & 1u;
+    for (int d0 = 0; d0 < q.D && n < SR; d0 += G * U) {
+      bool hit[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int d = d0 + u * G + gl;
+        hit[u] = false;
+        if (d < q.D) {
+          float p[3];
+          ray_point(c, dir, tval(q, r, d), p);
+          const int x = vox_coord(p[0], g.shift[0], g.vs[0]);
+          const int y = vox_coord(p[1], g.shift[1], g.vs[1]);
+          const int z = vox_coord(p[2], g.shift[2], g.vs[2]);
+          if (!(x < 0 || x >= g.dims[0] || y < 0 || y >= g.dims[1] || z < 0 || z >= g.dims[2])) {
+            const int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
+            hit[u] = (occ_bits[id >> 5] >> (id & 31)) & 1u;
+          }
         }
       }
-      const unsigned m = (unsigned)(__ballot(hit) >> (lane & (64 - G))) & (G == 32 ? 0xffffffffu : (1u << G) - 1u);
-      if (hit) {
-        const int pos = n + __popc(m & ((1u << gl) - 1u));
-        if (pos < SR) slot_d[r * SR + pos] = (uint16_t)d;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const unsigned m =
+            (unsigned)(__ballot(hit[u]) >> (lane & (64 - G))) & (G == 32 ? 0xffffffffu : (1u << G) - 1u);
+        if (hit[u]) {
+          const int pos = n + __popc(m & ((1u << gl) - 1u));
+          if (pos < SR) slot_d[r * SR + pos] = (uint16_t)(d0 + u * G + gl);
+        }
+        n += __popc(m);
       }
-      n += __popc(m);
     }
     if (gl == 0) n_filled[r] = n < SR ? n : SR;
   }
@@ -567,10 +577,10 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
     return PNR_OK;
   }
   if (R <= kMarchCoopRays)   // few rays: 16 lanes per ray (latency)
-    hipLaunchKernelGGL(k_march_coop<16>, dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g_dev, qp->SR,
+    hipLaunchKernelGGL((k_march_coop<16, 2>), dim3(grid_for(R * 16, kQBlock)), dim3(kQBlock), 0, st, q, g_dev, qp->SR,
                        h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   else
-    hipLaunchKernelGGL(k_march_coop<kMarchLanes>, dim3(grid_for(R * kMarchLanes, kQBlock, kMarchGridCap)),
+    hipLaunchKernelGGL((k_march_coop<kMarchLanes, kMarchUnroll>), dim3(grid_for(R * kMarchLanes, kQBlock, kMarchGridCap)),
                        dim3(kQBlock), 0, st, q, g_dev, qp->SR, h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   PNR_LAUNCH_CHECK();
   if ((rc = exclusive_scan(b->n_filled, R, nullptr, b->ray_off, b->counts + 0, b->scratch,
