@@ -323,22 +323,21 @@ __global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin
   }
 }
 
-// Runs of the sorted keys: the claimer of each occupied voxel (flag + the
-// run's sorted position, indexed by point id) and one past the run's end
-// (indexed by cell); counters[1] = points inside the grid.
+// Runs of the sorted keys: the claimer of each occupied voxel flagged by point
+// id (its rank is the slot), the run's first and one-past-last sorted
+// positions by cell; counters[1] = points inside the grid.
 template <typename K>
 __global__ void __launch_bounds__(kBlock) k_runs(const K* __restrict__ skey, const int32_t* __restrict__ sid,
                                                  int64_t n, K sentinel, int32_t* __restrict__ pt_flag,
-                                                 int32_t* __restrict__ pt_run, int32_t* __restrict__ cell_end,
+                                                 int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_end,
                                                  int32_t* __restrict__ counters) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
        j += (int64_t)gridDim.x * blockDim.x) {
     const K k = skey[j];
     if (k == sentinel) continue;
     if (j == 0 || skey[j - 1] != k) {
-      const int id = sid[j];
-      pt_flag[id] = 1;
-      pt_run[id] = (int)j;
+      pt_flag[sid[j]] = 1;
+      cell_start[(int64_t)k] = (int)j;
     }
     const K nx = j + 1 < n ? skey[j + 1] : sentinel;
     if (nx != k) {
@@ -430,78 +429,88 @@ __global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, 
     if (flag[i] && res_vkey(seed, (uint32_t)i) > thr) flag[i] = 0;
 }
 
-// map_coor2occ + fill_occ2pnts (qpiw.py:305-387), one thread per kept
-// claimer: slot -> coor_2_occ / occ_2_coor, the dilation of the occupancy by
-// query_size (idempotent byte stores, packed into bits by k_pack_bits), the
-// voxel's point count (`voxel_idx > 0`, qpiw.py:372: under slot0_drop the
-// voxel holding slot 0 gets no points) and its {xyz, id} records in ascending
-// id order -- all of the run when it fits P, else the P of smallest reservoir
-// key (res_pkey; the reference: reservoir with a time seed).
+// map_coor2occ + fill_occ2pnts (qpiw.py:305-387), one thread per sorted
+// point of a kept voxel.  The run's head (its claimer) writes slot ->
+// coor_2_occ / occ_2_coor, the occupancy byte (dilated by query_size in
+// k_dilate_zy / k_dilate_x), the voxel's point count (`voxel_idx > 0`,
+// qpiw.py:372: under slot0_drop the voxel holding slot 0 gets no points) and,
+// when the run exceeds P, the P records of smallest reservoir key (res_pkey;
+// the reference: reservoir with a time seed).  Runs that fit P: every point
+// writes its own record, number j - head (the run is in ascending id order).
 template <typename K>
 __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz, int64_t n, GridDev g0,
                                                   const QGrid* __restrict__ geo, const K* __restrict__ skey,
-                                                  const int32_t* __restrict__ sid, const int32_t* __restrict__ flag,
-                                                  const int32_t* __restrict__ pt_slot,
-                                                  const int32_t* __restrict__ pt_run,
+                                                  const int32_t* __restrict__ sid, K sentinel,
+                                                  const int32_t* __restrict__ flag, const int32_t* __restrict__ pt_slot,
+                                                  const int32_t* __restrict__ cell_start,
                                                   const int32_t* __restrict__ cell_end,
                                                   int32_t* __restrict__ coor_2_occ, int32_t* __restrict__ occ_2_coor,
                                                   uint8_t* __restrict__ occ_bytes, int32_t* __restrict__ occ_numpnts,
                                                   float4* __restrict__ occ_pts, int32_t* counters) {
   const GridDev g = with_geom(g0, geo);
   int dropped = 0, mx = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (!flag[i]) continue;
-    const int slot = pt_slot[i];
-    if (slot >= g.max_o) continue;  // never: the reservoir kept <= max_o voxels
-    const int j = pt_run[i];
-    const int64_t cell = (int64_t)skey[j];
-    const int cnt = cell_end[cell] - j;
-    int c[3];
-    if (cell <= 0x7fffffff) {   // 32-bit division when the cell index fits
-      const int r = (int)cell / g.dims[2];
-      c[2] = (int)cell - r * g.dims[2];
-      c[0] = r / g.dims[1];
-      c[1] = r - c[0] * g.dims[1];
-    } else {
-      c[2] = (int)(cell % g.dims[2]);
-      c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
-      c[0] = (int)(cell / ((int64_t)g.dims[2] * g.dims[1]));
-    }
-    coor_2_occ[cell] = slot;
-    occ_2_coor[slot * 3 + 0] = c[0];
-    occ_2_coor[slot * 3 + 1] = c[1];
-    occ_2_coor[slot * 3 + 2] = c[2];
-    occ_bytes[cell] = 1;   // dilated by query_size in k_dilate_zy / k_dilate_x
-
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const K key = skey[j];
+    if (key == sentinel) continue;
+    const int64_t cell = (int64_t)key;
+    const int h = cell_start[cell];
+    const int id0 = sid[h];
+    if (!flag[id0]) continue;          // voxel dropped by the max_o reservoir
+    const int slot = pt_slot[id0];
+    if (slot >= g.max_o) continue;     // never: the reservoir kept <= max_o voxels
+    const int cnt = cell_end[cell] - h;
     const int cnt_kept = (g.slot0_drop && slot == 0) ? 0 : cnt;
-    occ_numpnts[slot] = cnt_kept;
-    const int keep = min(cnt_kept, g.P);
-    const int32_t* ids = sid + j;
-    float4* dst = occ_pts + (int64_t)slot * g.P;
-    if (cnt_kept > g.P) {   // (the runs that fit P: k_fill_pts, one thread per point)
-      // reservoir: threshold = the P-th smallest key of the voxel's points
-      uint64_t thr = 0;
-      bool first = true;
-      for (int q = 0; q < g.P; ++q) {
-        uint64_t best = ~0ull;
-        for (int e = 0; e < cnt_kept; ++e) {
-          const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
-          if ((first || k > thr) && k < best) best = k;
+    if (j == h) {
+      int c[3];
+      if (cell <= 0x7fffffff) {   // 32-bit division when the cell index fits
+        const int r = (int)cell / g.dims[2];
+        c[2] = (int)cell - r * g.dims[2];
+        c[0] = r / g.dims[1];
+        c[1] = r - c[0] * g.dims[1];
+      } else {
+        c[2] = (int)(cell % g.dims[2]);
+        c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
+        c[0] = (int)(cell / ((int64_t)g.dims[2] * g.dims[1]));
+      }
+      coor_2_occ[cell] = slot;
+      occ_2_coor[slot * 3 + 0] = c[0];
+      occ_2_coor[slot * 3 + 1] = c[1];
+      occ_2_coor[slot * 3 + 2] = c[2];
+      occ_bytes[cell] = 1;
+      occ_numpnts[slot] = cnt_kept;
+      const int keep = min(cnt_kept, g.P);
+      if (cnt_kept > g.P) {
+        // reservoir: threshold = the P-th smallest key of the voxel's points
+        const int32_t* ids = sid + h;
+        float4* dst = occ_pts + (int64_t)slot * g.P;
+        uint64_t thr = 0;
+        bool first = true;
+        for (int q = 0; q < g.P; ++q) {
+          uint64_t best = ~0ull;
+          for (int e = 0; e < cnt_kept; ++e) {
+            const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
+            if ((first || k > thr) && k < best) best = k;
+          }
+          thr = best;
+          first = false;
         }
-        thr = best;
-        first = false;
+        int q = 0;
+        for (int e = 0; e < cnt_kept && q < keep; ++e) {  // ascending id order
+          const int v = ids[e];
+          if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
+          dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
+                                 __int_as_float(v));
+        }
       }
-      int q = 0;
-      for (int e = 0; e < cnt_kept && q < keep; ++e) {  // the run is in ascending id order
-        const int v = ids[e];
-        if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
-        dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
-                               __int_as_float(v));
-      }
+      dropped += cnt_kept - keep;
+      mx = max(mx, cnt_kept);
     }
-    dropped += cnt_kept - keep;
-    mx = max(mx, cnt_kept);
+    if (cnt_kept > 0 && cnt_kept <= g.P) {
+      const int v = sid[j];
+      occ_pts[(int64_t)slot * g.P + ((int)j - h)] =
+          make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2], __int_as_float(v));
+    }
   }
   dropped = wave_sum_i32(dropped);
 #pragma unroll
@@ -521,31 +530,6 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
     }
     if (d) atomicAdd(counters + 2, d);
     if (m) atomicMax(counters + 3, m);
-  }
-}
-
-// fill_occ2pnts' records of the voxels whose run fits P, one thread per
-// sorted point: the run starts at cell_end - count, so the point's record is
-// number j - start of its voxel's slot (runs in ascending id order).
-template <typename K>
-__global__ void __launch_bounds__(kBlock) k_fill_pts(const float* __restrict__ xyz, const K* __restrict__ skey,
-                                                     const int32_t* __restrict__ sid, int64_t n, K sentinel, int P,
-                                                     const int32_t* __restrict__ coor_2_occ,
-                                                     const int32_t* __restrict__ occ_numpnts,
-                                                     const int32_t* __restrict__ cell_end,
-                                                     float4* __restrict__ occ_pts) {
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    const K k = skey[j];
-    if (k == sentinel) continue;
-    const int slot = coor_2_occ[(int64_t)k];
-    if (slot < 0) continue;                       // voxel not kept (max_o reservoir)
-    const int c = occ_numpnts[slot];
-    if (c == 0 || c > P) continue;                // slot-0 quirk / P reservoir (k_claim)
-    const int q = (int)j - (cell_end[(int64_t)k] - c);
-    const int v = sid[j];
-    occ_pts[(int64_t)slot * P + q] =
-        make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2], __int_as_float(v));
   }
 }
 
@@ -719,7 +703,7 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   int32_t* counters = h->counters.as<int32_t>();
   int32_t* pt_flag = h->pt_flag.as<int32_t>();
   int32_t* pt_slot = h->pt_slot.as<int32_t>();
-  int32_t* pt_run = h->pt_run.as<int32_t>();
+  int32_t* cell_start = h->cell_start.as<int32_t>();
   int32_t* cell_end = h->cell_end.as<int32_t>();
   const K sentinel = (K)gvol;
   const int bits = 64 - __builtin_clzll((unsigned long long)gvol);
@@ -750,8 +734,8 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   }
   const K* skey = keys[cur];
   const int32_t* sid = vals[cur];
-  hipLaunchKernelGGL(k_runs<K>, dim3(gp), dim3(kBlock), 0, st, skey, sid, n, sentinel, pt_flag, pt_run, cell_end,
-                     counters);
+  hipLaunchKernelGGL(k_runs<K>, dim3(gp), dim3(kBlock), 0, st, skey, sid, n, sentinel, pt_flag, cell_start,
+                     cell_end, counters);
   PNR_LAUNCH_CHECK();
   // slot = rank of the claimer's point id (the serial claim order)
   if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p, h->scan_tmp.bytes, st)))
@@ -776,17 +760,14 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   }
   uint8_t* occ_bytes = h->cell_bytes.as<uint8_t>();
   PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
-  hipLaunchKernelGGL(k_claim<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, skey, sid, pt_flag, pt_slot,
-                     pt_run, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(), occ_bytes,
-                     h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), counters);
-  PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_fill_pts<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, skey, sid, n, sentinel, g.P,
-                     h->coor_2_occ.as<int32_t>(), h->occ_numpnts.as<int32_t>(), cell_end, h->occ_pts.as<float4>());
+  hipLaunchKernelGGL(k_claim<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, skey, sid, sentinel, pt_flag,
+                     pt_slot, cell_start, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(),
+                     occ_bytes, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), counters);
   PNR_LAUNCH_CHECK();
   {
-    // cell_end is dead after k_fill_pts: its storage holds the zy-dilated bytes
+    // cell_end is dead after k_claim: its storage holds the zy-dilated bytes
     uint8_t* zy = h->cell_end.as<uint8_t>();
-    const unsigned gr = grid_for(cdiv((int64_t)g.dims[0] * g.dims[1], kBlock / 64), kBlock, 4096);
+    const unsigned gr = grid_for((int64_t)g.dims[0] * g.dims[1] * 64, kBlock, 4096);   // one wave per row
     hipLaunchKernelGGL(k_dilate_zy, dim3(gr), dim3(kBlock), 0, st, g, geo, occ_bytes, zy);
     PNR_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_dilate_x, dim3(gr), dim3(kBlock), 0, st, g, geo, zy, occ_bytes);
@@ -822,7 +803,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
       (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->sort_k[0].ensure(n * kbytes)) ||
       (rc = h->sort_k[1].ensure(n * kbytes)) || (rc = h->sort_v[0].ensure(n * 4)) ||
       (rc = h->sort_v[1].ensure(n * 4)) || (rc = h->sort_hist.ensure(hist_n * 4)) ||
-      (rc = h->sort_offs.ensure(hist_n * 4)) || (rc = h->pt_run.ensure(n * 4)) ||
+      (rc = h->sort_offs.ensure(hist_n * 4)) || (rc = h->cell_start.ensure(gvol * 4)) ||
       (rc = h->pt_flag.ensure(n * 4)) || (rc = h->pt_slot.ensure((n + 1) * 4)) ||
       (rc = h->counters.ensure(8 * 4)) || (rc = h->sel.ensure(sizeof(SelState) + kSelPasses * 256 * 4)) ||
       (rc = h->scan_tmp.ensure(scan_scratch_bytes(scan_n))) ||

@@ -61,6 +61,19 @@ __device__ __forceinline__ int vox_coord(float p, float shift, float vs) {
   return (int)floorf(__fdiv_rn(__fsub_rn(p, shift), vs));
 }
 
+// vox_coord's value without the IEEE division on almost every call: t = x * inv
+// (inv = RN(1 / vs)) is within |e| 2^-22 of e = x / vs and RN(e) within |e| 2^-24,
+// so when t is farther than |t| 2^-20 from every integer, floor(t) is
+// floor(RN(e)); otherwise (an integer within reach, x = 0) the exact division.
+__device__ __forceinline__ int vox_coord_fast(float p, float shift, float vs, float inv) {
+  const float x = __fsub_rn(p, shift);
+  const float t = __fmul_rn(x, inv);
+  const float f = floorf(t);
+  const float m = __fmaf_rn(fabsf(t), 0x1p-20f, 0x1p-100f);
+  if (__fsub_rn(t, f) > m && __fsub_rn(__fadd_rn(f, 1.0f), t) > m) return (int)f;
+  return (int)floorf(__fdiv_rn(x, vs));
+}
+
 // raypos = campos + raydir * t  (diff_ray_marching.py:387: mul, then add).
 __device__ __forceinline__ float ray_at(float c, float d, float t) {
   return __fadd_rn(c, __fmul_rn(d, t));
@@ -169,7 +182,7 @@ struct pnr_handle {
   DevBuf sort_v[2];       // int32 [N]      point ids riding with the keys
   DevBuf sort_hist;       // int32 [256*tiles + 1] per-tile digit counts, then their exclusive scan
   DevBuf sort_offs;       // int32 [256*tiles + 1]
-  DevBuf pt_run;          // int32 [N]      sorted position of a claimer's run (claimers only)
+  DevBuf cell_start;      // int32 [gvol]   first sorted position of the cell's run (occupied cells only)
   DevBuf pt_flag;         // int32 [N]
   DevBuf pt_slot;         // int32 [N+1]
   DevBuf counters;        // int32 [8]
@@ -207,7 +220,7 @@ struct pnr_handle {
     stats_pending = false;
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &cell_end, &cell_bytes, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &sort_k[0], &sort_k[1], &sort_v[0], &sort_v[1], &sort_hist, &sort_offs,
-                     &pt_run, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
+                     &cell_start, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
                      &q_rec_off, &q_recs, &geom, &bbox};
     for (DevBuf* b : all) b->release();
   }

@@ -80,6 +80,7 @@ __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __
                                                         int32_t* __restrict__ n_filled,
                                                         uint16_t* __restrict__ slot_d) {
   const QGrid g = *gq;
+  const float inv[3] = {__fdiv_rn(1.0f, g.vs[0]), __fdiv_rn(1.0f, g.vs[1]), __fdiv_rn(1.0f, g.vs[2])};
   const int lane = threadIdx.x & 63, gl = lane & (G - 1);
   for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / G; r < q.R;
        r += ((int64_t)gridDim.x * blockDim.x) / G) {
@@ -96,9 +97,9 @@ __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __
         if (d < q.D) {
           float p[3];
           ray_point(c, dir, tval(q, r, d), p);
-          const int x = vox_coord(p[0], g.shift[0], g.vs[0]);
-          const int y = vox_coord(p[1], g.shift[1], g.vs[1]);
-          const int z = vox_coord(p[2], g.shift[2], g.vs[2]);
+          const int x = vox_coord_fast(p[0], g.shift[0], g.vs[0], inv[0]);
+          const int y = vox_coord_fast(p[1], g.shift[1], g.vs[1], inv[1]);
+          const int z = vox_coord_fast(p[2], g.shift[2], g.vs[2], inv[2]);
           if (!(x < 0 || x >= g.dims[0] || y < 0 || y >= g.dims[1] || z < 0 || z >= g.dims[2])) {
             const int64_t id = ((int64_t)x * g.dims[1] + y) * g.dims[2] + z;
             hit[u] = (occ_bits[id >> 5] >> (id & 31)) & 1u;
