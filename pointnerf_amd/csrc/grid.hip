@@ -206,8 +206,8 @@ __global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ 
 // digit counts (k_rs_hist), their exclusive scan in digit-major order (the
 // device scan), then a stable scatter (k_rs_scatter) that ranks the tile in
 // LDS and writes each digit's keys of the tile as one contiguous run.
-constexpr int kRsItems = 16;
-constexpr int kRsTile = kBlock * kRsItems;  // 4096 keys
+constexpr int kRsItems = 8;
+constexpr int kRsTile = kBlock * kRsItems;  // 2048 keys: ~4 tiles per CU at 2 M points
 
 template <typename K>
 __device__ __forceinline__ int rs_digit(K k, int shift) {
@@ -543,12 +543,15 @@ __device__ __forceinline__ void dil_range(int v, int qs, int dim, int& lo, int& 
   hi = min(dim - 1, v + qs / 2);
 }
 
-// z and y: in = one byte per occupied cell, out = the zy-dilated bytes
+// z and y: in = one byte per occupied cell, out = the zy-dilated bytes.  Up to
+// 3 x 3 contributing cells (query_size <= 3, every flag set) as independent
+// predicated loads, so a lane has them all in flight; larger boxes loop.
 __global__ void __launch_bounds__(kBlock) k_dilate_zy(GridDev g0, const QGrid* __restrict__ geo,
                                                       const uint8_t* __restrict__ in, uint8_t* __restrict__ out) {
   const GridDev g = with_geom(g0, geo);
   const int rows = g.dims[0] * g.dims[1];
   const int lane = threadIdx.x & 63;
+  const bool small = g.qs[1] <= 3 && g.qs[2] <= 3;
   for (int row = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); row < rows;
        row += (int)((gridDim.x * blockDim.x) >> 6)) {
     const int x = row / g.dims[1], y = row - x * g.dims[1];
@@ -558,9 +561,23 @@ __global__ void __launch_bounds__(kBlock) k_dilate_zy(GridDev g0, const QGrid* _
       int z0, z1;
       dil_range(z, g.qs[2], g.dims[2], z0, z1);
       uint8_t m = 0;
-      for (int yy = y0; yy <= y1; ++yy) {
-        const uint8_t* r = in + ((int64_t)x * g.dims[1] + yy) * g.dims[2];
-        for (int zz = z0; zz <= z1; ++zz) m |= r[zz];
+      if (small) {
+        uint8_t v[9];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+          for (int b = 0; b < 3; ++b) {
+            const bool ok = y0 + a <= y1 && z0 + b <= z1;
+            const int yy = ok ? y0 + a : y, zz = ok ? z0 + b : z;
+            v[a * 3 + b] = ok ? in[((int64_t)x * g.dims[1] + yy) * g.dims[2] + zz] : 0;
+          }
+#pragma unroll
+        for (int q = 0; q < 9; ++q) m |= v[q];
+      } else {
+        for (int yy = y0; yy <= y1; ++yy) {
+          const uint8_t* r = in + ((int64_t)x * g.dims[1] + yy) * g.dims[2];
+          for (int zz = z0; zz <= z1; ++zz) m |= r[zz];
+        }
       }
       out[(int64_t)row * g.dims[2] + z] = m;
     }
@@ -582,7 +599,14 @@ __global__ void __launch_bounds__(kBlock) k_dilate_x(GridDev g0, const QGrid* __
     const int64_t base = (int64_t)row * g.dims[2];
     for (int z = lane; z < g.dims[2]; z += 64) {
       uint8_t m = 0;
-      for (int xx = x0; xx <= x1; ++xx) m |= in[base + (int64_t)(xx - x) * plane + z];
+      if (g.qs[0] <= 3) {
+        uint8_t v[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) v[a] = x0 + a <= x1 ? in[base + (int64_t)(x0 + a - x) * plane + z] : 0;
+        m = v[0] | v[1] | v[2];
+      } else {
+        for (int xx = x0; xx <= x1; ++xx) m |= in[base + (int64_t)(xx - x) * plane + z];
+      }
       out[base + z] = m;
     }
   }
@@ -767,7 +791,7 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   {
     // cell_end is dead after k_claim: its storage holds the zy-dilated bytes
     uint8_t* zy = h->cell_end.as<uint8_t>();
-    const unsigned gr = grid_for((int64_t)g.dims[0] * g.dims[1] * 64, kBlock, 4096);   // one wave per row
+    const unsigned gr = grid_for((int64_t)g.dims[0] * g.dims[1] * 64, kBlock, 1 << 16);   // one wave per row
     hipLaunchKernelGGL(k_dilate_zy, dim3(gr), dim3(kBlock), 0, st, g, geo, occ_bytes, zy);
     PNR_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_dilate_x, dim3(gr), dim3(kBlock), 0, st, g, geo, zy, occ_bytes);

@@ -48,8 +48,8 @@ def test_grid_tables_bit_exact(cuda, slot0_drop):
 
 @pytest.mark.parametrize("n,max_o,P", [(20000, 1500, 1), (3, 8, 2), (70000, 400000, 9)])
 def test_grid_tables_bit_exact_sizes_and_overflow(cuda, n, max_o, P):
-    """The radix-sorted build across tile counts (1, 2 ragged ... 18 tiles of
-    4096 keys) and with both reservoirs active (max_o and P overflow)."""
+    """The radix-sorted build across tile counts (1, 10 and 35 ragged tiles of
+    2048 keys) and with both reservoirs active (max_o and P overflow)."""
     sc = scene(max(n, 20000), max_o=max_o, P=P)
     xyz = sc["xyz"][:n].copy()
     q = _engine(sc, cuda)
