@@ -17,14 +17,18 @@ sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 def main():
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--points", type=int, default=2_000_000)
+    ap.add_argument("--config", default="headline")
+    ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-oracle", action="store_true")
     a = ap.parse_args()
     import bench
+    cfg = bench.CONFIGS[a.config]
+    a.points = a.points or cfg["points"]
     from oracle import oracle as O
     dev = torch.device("cuda:0")
     opt, pts, feats, agg, model = bench.build_scene(
-        argparse.Namespace(points=a.points, config="headline", dtype="fp32h2"), dev)
+        argparse.Namespace(points=a.points, config=a.config, dtype=cfg["dtype"]), dev)
     q = model.neural_points.querier
     xyz = model.neural_points.xyz.detach().contiguous()
     ts = []
@@ -37,12 +41,16 @@ def main():
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     st = q.grid.stats()
-    g = O.grid_build(opt, pts)
-    t = q.grid.export()
-    exact = {k: bool(np.array_equal(t[k].cpu().numpy(), g[k])) for k in ("coor_2_occ", "occ_numpnts", "occ_2_pnts")}
-    print(json.dumps({"points": a.points, "build_ms_median": round(float(np.median(ts)), 4),
-                      "build_ms": [round(x, 4) for x in ts], "n_voxels": int(st["n_voxels"]),
-                      "oracle_n_occ": int(g["n_occ"]), "bit_exact": exact}))
+    out = {"config": a.config, "points": a.points, "build_ms_median": round(float(np.median(ts)), 4),
+           "build_ms": [round(x, 4) for x in ts], "n_voxels": int(st["n_voxels"]),
+           "n_voxels_kept": int(st["n_voxels_kept"]), "n_points_dropped": int(st["n_points_dropped"])}
+    if not a.no_oracle:
+        g = O.grid_build(opt, pts)
+        t = q.grid.export()
+        out["oracle_n_occ"] = int(g["n_occ"])
+        out["bit_exact"] = {k: bool(np.array_equal(t[k].cpu().numpy(), g[k]))
+                            for k in ("coor_2_occ", "occ_numpnts", "occ_2_pnts")}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
