@@ -1361,6 +1361,66 @@ __global__ void k_used_list(const int32_t* __restrict__ flags, int64_t n_points,
   }
 }
 
+// Sum of a run of pairs sorted by point row, in pair order (deterministic):
+// the run's positions are found 64 at a time with one ballot, the pair ids
+// loaded one per lane and broadcast, and four dz1 rows read before they are
+// added, so a wave keeps four row loads in flight instead of one.
+template <bool EX>
+__device__ __forceinline__ void run_sum(const int32_t* __restrict__ prow_sorted, const int32_t* __restrict__ pair_of,
+                                        int64_t P, int64_t i, int32_t pr, const float* __restrict__ dz1,
+                                        const float* __restrict__ g_pair, float4& s, float& ge) {
+  const int lane = threadIdx.x & 63;
+  bool first = true;
+  for (int64_t j0 = i;; j0 += 64) {
+    const int64_t jj = j0 + lane;
+    const int32_t pl = jj < P ? prow_sorted[jj] : -2;
+    const uint64_t same = __ballot(pl == pr);
+    const int len = same == ~0ull ? 64 : __builtin_ctzll(~same);
+    const int32_t mine = lane < len ? pair_of[jj] : 0;
+    int t = 0;
+    for (; t + 4 <= len; t += 4) {
+      int64_t pq[4];
+      float4 v[4];
+      float gq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pq[u] = __shfl(mine, t + u);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = reinterpret_cast<const float4*>(dz1 + pq[u] * kHid)[lane];
+        gq[u] = (EX && lane < 6) ? g_pair[pq[u] * 8 + lane] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (first && !EX) {
+          s = v[u];
+          first = false;
+        } else {
+          s.x += v[u].x;
+          s.y += v[u].y;
+          s.z += v[u].z;
+          s.w += v[u].w;
+        }
+        if (EX && lane < 6) ge += gq[u];
+      }
+    }
+    for (; t < len; ++t) {
+      const int64_t pq = __shfl(mine, t);
+      const float4 v = reinterpret_cast<const float4*>(dz1 + pq * kHid)[lane];
+      if (first && !EX) {
+        s = v;
+        first = false;
+      } else {
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+      if (EX && lane < 6) ge += g_pair[pq * 8 + lane];
+    }
+    if (len < 64) break;
+  }
+}
+
 // d P1 rows from dz1 without atomics: pairs sorted by point row (stable, so
 // each point's pairs in pair order -- a deterministic sum); one wave per run of
 // equal rows, lane = 4 neurons (float4).
@@ -1376,14 +1436,9 @@ __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const
   for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
     const int32_t pr = prow_sorted[i];
     if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
-    float4 s = reinterpret_cast<const float4*>(dz1 + (int64_t)pair_of[i] * kHid)[lane];
-    for (int64_t j = i + 1; j < P && prow_sorted[j] == pr; ++j) {
-      const float4 v = reinterpret_cast<const float4*>(dz1 + (int64_t)pair_of[j] * kHid)[lane];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ge = 0.f;
+    run_sum<false>(prow_sorted, pair_of, P, i, pr, dz1, nullptr, s, ge);
     reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
     mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
              max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
@@ -1482,15 +1537,7 @@ __global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, co
     if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     float ge = 0.f;   // lane e < 6: sum of g_pair[.][e]
-    for (int64_t j = i; j < P && prow_sorted[j] == pr; ++j) {
-      const int64_t pair = pair_of[j];
-      const float4 v = reinterpret_cast<const float4*>(dz1 + pair * kHid)[lane];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-      if (lane < 6) ge += g_pair[pair * 8 + lane];
-    }
+    run_sum<true>(prow_sorted, pair_of, P, i, pr, dz1, g_pair, s, ge);
     reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
     mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
              max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
