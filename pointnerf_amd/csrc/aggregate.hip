@@ -1433,15 +1433,24 @@ __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const
   if (threadIdx.x == 0) bmax = 0u;
   __syncthreads();
   unsigned mb = 0u;   // max |d_p1| of this lane's rows (float bits: NaN propagates)
-  for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
-    const int32_t pr = prow_sorted[i];
-    if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    float ge = 0.f;
-    run_sum<false>(prow_sorted, pair_of, P, i, pr, dz1, nullptr, s, ge);
-    reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
-    mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
-             max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
+  // 64 sorted positions per wave and step: one ballot finds the runs that start there
+  for (int64_t i0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; i0 < P; i0 += waves * 64) {
+    const int64_t ii = i0 + lane;
+    const int32_t pr_l = ii < P ? prow_sorted[ii] : -1;
+    const int32_t pv_l = ii > 0 && ii < P ? prow_sorted[ii - 1] : -1;
+    uint64_t starts = __ballot(pr_l >= 0 && (ii == 0 || pv_l != pr_l));
+    while (starts) {
+      const int l = __builtin_ctzll(starts);
+      starts &= starts - 1;
+      const int64_t i = i0 + l;
+      const int32_t pr = __shfl(pr_l, l);
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      float ge = 0.f;
+      run_sum<false>(prow_sorted, pair_of, P, i, pr, dz1, nullptr, s, ge);
+      reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
+      mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
+               max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
+    }
   }
   if (absmax) {
     wave_absmax_to(&bmax, mb);
@@ -1532,24 +1541,33 @@ __global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, co
   if (threadIdx.x == 0) bmax = 0u;
   __syncthreads();
   unsigned mb = 0u;
-  for (int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < P; i += waves) {
-    const int32_t pr = prow_sorted[i];
-    if (pr < 0 || (i > 0 && prow_sorted[i - 1] == pr)) continue;   // not the start of a run
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    float ge = 0.f;   // lane e < 6: sum of g_pair[.][e]
-    run_sum<true>(prow_sorted, pair_of, P, i, pr, dz1, g_pair, s, ge);
-    reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
-    mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
-             max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
-    const float g3 = __shfl(ge, 3), g4 = __shfl(ge, 4), g5 = __shfl(ge, 5);
-    if (lane < 3) {
-      if (d_color) d_color[(int64_t)pr * 3 + lane] = ge;
-      if (d_dir) {   // d dir_a = sum_j Rw[j][a] gd_j
-        const float* R = rw_pp ? rw_pp + (int64_t)pr * 9 : rw_uniform;
-        const float r0 = R ? R[lane] : (lane == 0 ? 1.f : 0.f);
-        const float r1 = R ? R[3 + lane] : (lane == 1 ? 1.f : 0.f);
-        const float r2 = R ? R[6 + lane] : (lane == 2 ? 1.f : 0.f);
-        d_dir[(int64_t)pr * 3 + lane] = r0 * g3 + r1 * g4 + r2 * g5;
+  // 64 sorted positions per wave and step: one ballot finds the runs that start there
+  for (int64_t i0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; i0 < P; i0 += waves * 64) {
+    const int64_t ii = i0 + lane;
+    const int32_t pr_l = ii < P ? prow_sorted[ii] : -1;
+    const int32_t pv_l = ii > 0 && ii < P ? prow_sorted[ii - 1] : -1;
+    uint64_t starts = __ballot(pr_l >= 0 && (ii == 0 || pv_l != pr_l));
+    while (starts) {
+      const int l = __builtin_ctzll(starts);
+      starts &= starts - 1;
+      const int64_t i = i0 + l;
+      const int32_t pr = __shfl(pr_l, l);
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      float ge = 0.f;   // lane e < 6: sum of g_pair[.][e]
+      run_sum<true>(prow_sorted, pair_of, P, i, pr, dz1, g_pair, s, ge);
+      reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
+      mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
+               max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
+      const float g3 = __shfl(ge, 3), g4 = __shfl(ge, 4), g5 = __shfl(ge, 5);
+      if (lane < 3) {
+        if (d_color) d_color[(int64_t)pr * 3 + lane] = ge;
+        if (d_dir) {   // d dir_a = sum_j Rw[j][a] gd_j
+          const float* R = rw_pp ? rw_pp + (int64_t)pr * 9 : rw_uniform;
+          const float r0 = R ? R[lane] : (lane == 0 ? 1.f : 0.f);
+          const float r1 = R ? R[3 + lane] : (lane == 1 ? 1.f : 0.f);
+          const float r2 = R ? R[6 + lane] : (lane == 2 ? 1.f : 0.f);
+          d_dir[(int64_t)pr * 3 + lane] = r0 * g3 + r1 * g4 + r2 * g5;
+        }
       }
     }
   }
@@ -2233,7 +2251,7 @@ extern "C" int pnr_pairs_to_points_ex(const int32_t* prow_sorted, const int32_t*
                 "pairs_to_points_ex: bad args");
   PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1) & 15) == 0, "pairs_to_points_ex: rows must be 16-B aligned");
   if (P == 0) return PNR_OK;
-  hipLaunchKernelGGL(k_pairs_to_points_ex, dim3(grid_for(P, 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
+  hipLaunchKernelGGL(k_pairs_to_points_ex, dim3(grid_for(cdiv(P, 64), 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
                      pair_of, P, dz1, used_map, d_p1, d_p1_absmax, g_pair, rw_uniform, rw_pp, d_color, d_dir);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
@@ -2254,7 +2272,7 @@ extern "C" int pnr_pairs_to_points(const int32_t* prow_sorted, const int32_t* pa
   PNR_CHECK_ARG(P >= 0 && (P == 0 || (prow_sorted && pair_of && dz1 && d_p1)), "pairs_to_points: bad args");
   PNR_CHECK_ARG((((uintptr_t)dz1 | (uintptr_t)d_p1) & 15) == 0, "pairs_to_points: rows must be 16-B aligned");
   if (P == 0) return PNR_OK;
-  hipLaunchKernelGGL(k_pairs_to_points, dim3(grid_for(P, 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
+  hipLaunchKernelGGL(k_pairs_to_points, dim3(grid_for(cdiv(P, 64), 4, 2048)), dim3(256), 0, as_stream(stream), prow_sorted,
                      pair_of, P, dz1, used_map, d_p1, d_p1_absmax);
   PNR_LAUNCH_CHECK();
   return PNR_OK;

@@ -446,7 +446,8 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
                                                   const int32_t* __restrict__ cell_end,
                                                   int32_t* __restrict__ coor_2_occ, int32_t* __restrict__ occ_2_coor,
                                                   uint8_t* __restrict__ occ_bytes, int32_t* __restrict__ occ_numpnts,
-                                                  float4* __restrict__ occ_pts, int32_t* counters) {
+                                                  float4* __restrict__ occ_pts, int32_t* __restrict__ slot_run,
+                                                  int32_t* counters) {
   const GridDev g = with_geom(g0, geo);
   int dropped = 0, mx = 0;
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
@@ -480,29 +481,7 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
       occ_bytes[cell] = 1;
       occ_numpnts[slot] = cnt_kept;
       const int keep = min(cnt_kept, g.P);
-      if (cnt_kept > g.P) {
-        // reservoir: threshold = the P-th smallest key of the voxel's points
-        const int32_t* ids = sid + h;
-        float4* dst = occ_pts + (int64_t)slot * g.P;
-        uint64_t thr = 0;
-        bool first = true;
-        for (int q = 0; q < g.P; ++q) {
-          uint64_t best = ~0ull;
-          for (int e = 0; e < cnt_kept; ++e) {
-            const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
-            if ((first || k > thr) && k < best) best = k;
-          }
-          thr = best;
-          first = false;
-        }
-        int q = 0;
-        for (int e = 0; e < cnt_kept && q < keep; ++e) {  // ascending id order
-          const int v = ids[e];
-          if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
-          dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
-                                 __int_as_float(v));
-        }
-      }
+      if (cnt_kept > g.P) slot_run[slot] = h;   // records by k_reservoir (one lane per voxel)
       dropped += cnt_kept - keep;
       mx = max(mx, cnt_kept);
     }
@@ -530,6 +509,42 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
     }
     if (d) atomicAdd(counters + 2, d);
     if (m) atomicMax(counters + 3, m);
+  }
+}
+
+// fill_occ2pnts' reservoir (qpiw.py:377-384) for the voxels whose run exceeds
+// P, one lane per slot (every lane of a wave a candidate voxel, not one in a
+// run's length as inside k_claim): the P points of smallest res_pkey, written in
+// ascending id order.
+__global__ void __launch_bounds__(kBlock) k_reservoir(int n_slots, GridDev g, const float* __restrict__ xyz,
+                                                      const int32_t* __restrict__ sid,
+                                                      const int32_t* __restrict__ occ_numpnts,
+                                                      const int32_t* __restrict__ slot_run,
+                                                      float4* __restrict__ occ_pts) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
+    const int cnt = occ_numpnts[s];
+    if (cnt <= g.P) continue;
+    const int32_t* ids = sid + slot_run[s];
+    float4* dst = occ_pts + (int64_t)s * g.P;
+    // threshold = the P-th smallest key of the voxel's points
+    uint64_t thr = 0;
+    bool first = true;
+    for (int q = 0; q < g.P; ++q) {
+      uint64_t best = ~0ull;
+      for (int e = 0; e < cnt; ++e) {
+        const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
+        if ((first || k > thr) && k < best) best = k;
+      }
+      thr = best;
+      first = false;
+    }
+    int q = 0;
+    for (int e = 0; e < cnt && q < g.P; ++e) {   // the run is in ascending id order
+      const int v = ids[e];
+      if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
+      dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
+                             __int_as_float(v));
+    }
   }
 }
 
@@ -786,7 +801,12 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
   hipLaunchKernelGGL(k_claim<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, skey, sid, sentinel, pt_flag,
                      pt_slot, cell_start, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(),
-                     occ_bytes, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), counters);
+                     occ_bytes, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), h->q_rank_slot.as<int32_t>(),
+                     counters);
+  PNR_LAUNCH_CHECK();
+  // q_rank_slot is scratch until the query index below: slot -> run start
+  hipLaunchKernelGGL(k_reservoir, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, xyz_dev, sid,
+                     h->occ_numpnts.as<int32_t>(), h->q_rank_slot.as<int32_t>(), h->occ_pts.as<float4>());
   PNR_LAUNCH_CHECK();
   {
     // cell_end is dead after k_claim: its storage holds the zy-dilated bytes
