@@ -1421,6 +1421,52 @@ __device__ __forceinline__ void run_sum(const int32_t* __restrict__ prow_sorted,
   }
 }
 
+// A run that ends inside the caller's 64-position chunk: its pair ids are the
+// chunk's lanes l .. l + len - 1 (`mine`), so only the dz1 rows are loaded.
+template <bool EX>
+__device__ __forceinline__ void run_sum_chunk(int32_t mine, int l, int len, const float* __restrict__ dz1,
+                                              const float* __restrict__ g_pair, float4& s, float& ge) {
+  const int lane = threadIdx.x & 63;
+  int t = 0;
+  for (; t + 4 <= len; t += 4) {
+    int64_t pq[4];
+    float4 v[4];
+    float gq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pq[u] = __shfl(mine, l + t + u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = reinterpret_cast<const float4*>(dz1 + pq[u] * kHid)[lane];
+      gq[u] = (EX && lane < 6) ? g_pair[pq[u] * 8 + lane] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (t + u == 0 && !EX) {
+        s = v[u];
+      } else {
+        s.x += v[u].x;
+        s.y += v[u].y;
+        s.z += v[u].z;
+        s.w += v[u].w;
+      }
+      if (EX && lane < 6) ge += gq[u];
+    }
+  }
+  for (; t < len; ++t) {
+    const int64_t pq = __shfl(mine, l + t);
+    const float4 v = reinterpret_cast<const float4*>(dz1 + pq * kHid)[lane];
+    if (t == 0 && !EX) {
+      s = v;
+    } else {
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    if (EX && lane < 6) ge += g_pair[pq * 8 + lane];
+  }
+}
+
 // d P1 rows from dz1 without atomics: pairs sorted by point row (stable, so
 // each point's pairs in pair order -- a deterministic sum); one wave per run of
 // equal rows, lane = 4 neurons (float4).
@@ -1438,15 +1484,19 @@ __global__ void k_pairs_to_points(const int32_t* __restrict__ prow_sorted, const
     const int64_t ii = i0 + lane;
     const int32_t pr_l = ii < P ? prow_sorted[ii] : -1;
     const int32_t pv_l = ii > 0 && ii < P ? prow_sorted[ii - 1] : -1;
+    const int32_t mine = ii < P ? pair_of[ii] : 0;
     uint64_t starts = __ballot(pr_l >= 0 && (ii == 0 || pv_l != pr_l));
+    const uint64_t bounds = __ballot(ii >= P || ii == 0 || pv_l != pr_l);   // a new value (or the end) begins
     while (starts) {
       const int l = __builtin_ctzll(starts);
       starts &= starts - 1;
       const int64_t i = i0 + l;
       const int32_t pr = __shfl(pr_l, l);
+      const uint64_t after = l == 63 ? 0ull : bounds & (~0ull << (l + 1));
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
       float ge = 0.f;
-      run_sum<false>(prow_sorted, pair_of, P, i, pr, dz1, nullptr, s, ge);
+      if (after) run_sum_chunk<false>(mine, l, __builtin_ctzll(after) - l, dz1, nullptr, s, ge);
+      else run_sum<false>(prow_sorted, pair_of, P, i, pr, dz1, nullptr, s, ge);   // runs past the chunk
       reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
       mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
                max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
@@ -1546,15 +1596,19 @@ __global__ void k_pairs_to_points_ex(const int32_t* __restrict__ prow_sorted, co
     const int64_t ii = i0 + lane;
     const int32_t pr_l = ii < P ? prow_sorted[ii] : -1;
     const int32_t pv_l = ii > 0 && ii < P ? prow_sorted[ii - 1] : -1;
+    const int32_t mine = ii < P ? pair_of[ii] : 0;
     uint64_t starts = __ballot(pr_l >= 0 && (ii == 0 || pv_l != pr_l));
+    const uint64_t bounds = __ballot(ii >= P || ii == 0 || pv_l != pr_l);   // a new value (or the end) begins
     while (starts) {
       const int l = __builtin_ctzll(starts);
       starts &= starts - 1;
       const int64_t i = i0 + l;
       const int32_t pr = __shfl(pr_l, l);
+      const uint64_t after = l == 63 ? 0ull : bounds & (~0ull << (l + 1));
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
       float ge = 0.f;   // lane e < 6: sum of g_pair[.][e]
-      run_sum<true>(prow_sorted, pair_of, P, i, pr, dz1, g_pair, s, ge);
+      if (after) run_sum_chunk<true>(mine, l, __builtin_ctzll(after) - l, dz1, g_pair, s, ge);
+      else run_sum<true>(prow_sorted, pair_of, P, i, pr, dz1, g_pair, s, ge);   // runs past the chunk
       reinterpret_cast<float4*>(d_p1 + (used_map ? (int64_t)used_map[pr] : (int64_t)pr) * kHid)[lane] = s;
       mb = max(max(mb, max(__float_as_uint(fabsf(s.x)), __float_as_uint(fabsf(s.y)))),
                max(__float_as_uint(fabsf(s.z)), __float_as_uint(fabsf(s.w))));
