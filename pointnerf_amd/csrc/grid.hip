@@ -513,60 +513,37 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
 }
 
 // fill_occ2pnts' reservoir (qpiw.py:377-384) for the voxels whose run exceeds
-// P: the P points of smallest res_pkey, written in ascending id order.  One
-// wave per voxel: a run of <= 64 points is ranked across the lanes (a key's
-// rank = how many keys of the run are smaller; keys are unique), longer runs
-// take the serial two-pass selection in lane 0.
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  const unsigned lo = (unsigned)__shfl((int)(unsigned)v, src);
-  const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), src);
-  return ((uint64_t)hi << 32) | lo;
-}
-
+// P, one lane per slot (every lane of a wave a candidate voxel, not one in a
+// run's length as inside k_claim): the P points of smallest res_pkey, written in
+// ascending id order.
 __global__ void __launch_bounds__(kBlock) k_reservoir(int n_slots, GridDev g, const float* __restrict__ xyz,
                                                       const int32_t* __restrict__ sid,
                                                       const int32_t* __restrict__ occ_numpnts,
                                                       const int32_t* __restrict__ slot_run,
                                                       float4* __restrict__ occ_pts) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t s = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; s < n_slots;
-       s += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
     const int cnt = occ_numpnts[s];
-    if (cnt <= g.P) continue;   // wave-uniform
+    if (cnt <= g.P) continue;
     const int32_t* ids = sid + slot_run[s];
-    float4* dst = occ_pts + s * g.P;
-    if (cnt <= 64) {
-      const int v = lane < cnt ? ids[lane] : 0;
-      const uint64_t key = lane < cnt ? res_pkey(g.seed, (uint32_t)v) : ~0ull;
-      int rank = 0;
-      for (int m = 0; m < cnt; ++m) rank += shfl_u64(key, m) < key ? 1 : 0;
-      const bool sel = lane < cnt && rank < g.P;
-      const uint64_t chosen = __ballot(sel);
-      if (sel) {
-        const int q = __popcll(chosen & ((1ull << lane) - 1ull));   // the run is in ascending id order
-        dst[q] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
+    float4* dst = occ_pts + (int64_t)s * g.P;
+    // threshold = the P-th smallest key of the voxel's points
+    uint64_t thr = 0;
+    bool first = true;
+    for (int q = 0; q < g.P; ++q) {
+      uint64_t best = ~0ull;
+      for (int e = 0; e < cnt; ++e) {
+        const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
+        if ((first || k > thr) && k < best) best = k;
+      }
+      thr = best;
+      first = false;
+    }
+    int q = 0;
+    for (int e = 0; e < cnt && q < g.P; ++e) {   // the run is in ascending id order
+      const int v = ids[e];
+      if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
+      dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
                              __int_as_float(v));
-      }
-    } else if (lane == 0) {
-      // threshold = the P-th smallest key of the voxel's points
-      uint64_t thr = 0;
-      bool first = true;
-      for (int q = 0; q < g.P; ++q) {
-        uint64_t best = ~0ull;
-        for (int e = 0; e < cnt; ++e) {
-          const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
-          if ((first || k > thr) && k < best) best = k;
-        }
-        thr = best;
-        first = false;
-      }
-      int q = 0;
-      for (int e = 0; e < cnt && q < g.P; ++e) {
-        const int v = ids[e];
-        if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
-        dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
-                               __int_as_float(v));
-      }
     }
   }
 }
@@ -828,7 +805,7 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
                      counters);
   PNR_LAUNCH_CHECK();
   // q_rank_slot is scratch until the query index below: slot -> run start
-  hipLaunchKernelGGL(k_reservoir, dim3(grid_for(cap_o * 64, kBlock, 8192)), dim3(kBlock), 0, st, (int)cap_o, g, xyz_dev, sid,
+  hipLaunchKernelGGL(k_reservoir, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, xyz_dev, sid,
                      h->occ_numpnts.as<int32_t>(), h->q_rank_slot.as<int32_t>(), h->occ_pts.as<float4>());
   PNR_LAUNCH_CHECK();
   {
