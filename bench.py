@@ -77,6 +77,8 @@ def parse():
                     help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check); "
                          "default 12000 (headline), 3000 (c4, c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train-line", action="store_true",
+                    help="headline run: skip the finetune-step measurement appended to the line ('train')")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--train-precision", choices=("fp32h2", "fp32x3", "fp32"), default="fp32h2",
                     help="--mode train: the training forward's per-pair chain (fp32h2 split-f16 MFMA, fp32x3 "
@@ -253,18 +255,26 @@ def accuracy_vs_x3(model, opt, cam, bg, dtype):
     """Full frame: the headline arithmetic against fp32x3 (exact fp32 products,
     test_gpu_x3.py) on the same frame, outside the timed region."""
     campos, camrot, rd = cam
-    a = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg)
+    ev_a, ev_b = [], []
+    a = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg, events=ev_a)
     prec = model.precision
     model.precision = "fp32x3"
     try:
-        b = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg)
+        b = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg, events=ev_b)
     finally:
         model.precision = prec
+    torch.cuda.synchronize()
     hit = (b[3] > 0).cpu().numpy()
     x, y = a[0].cpu().numpy(), b[0].cpu().numpy()
+
+    def agg_ms(ev):
+        return round(sum(e0.elapsed_time(e1) for name, e0, e1 in ev if name == "aggregate"), 3)
     return {f"psnr_{dtype}_vs_fp32x3_full_frame_db": psnr_db(x[hit], y[hit]),
             f"max_abs_err_{dtype}_vs_fp32x3_full_frame": float(np.abs(x - y).max()),
-            "full_frame_rays_hit": int(hit.sum())}
+            "full_frame_rays_hit": int(hit.sum()),
+            # the strict-fp32 arithmetic's cost on the same frame (one synchronous render each,
+            # P1 inline: not the timed steps' side-stream overlap)
+            f"aggregate_ms_{dtype}_same_frame": agg_ms(ev_a), "aggregate_ms_fp32x3_same_frame": agg_ms(ev_b)}
 
 
 def time_grid_build(model, opt, reps=5):
@@ -356,6 +366,16 @@ def stage_rooflines(args, opt, model, stage, per, launches, grid=None):
     return res
 
 
+# fp32-equivalent MFMA ceilings of the training arithmetic (3 f16 / 6 bf16 products per fp32 MAC)
+TRAIN_PEAK_TFLOPS = {"fp32h2": round(2500.0 / 3, 1), "fp32x3": round(2500.0 / 6, 1), "fp32": 157.3}
+TRAIN_ARITH = {
+    "fp32h2": "forward per-pair chain, colour branch, weight gradients and dX1 on the 2-way f16 split "
+              "(v_mfma_f32_32x32x16_f16, 3 products); the per-pair dX chain (k_pairs_bwd) on the exact 3-way bf16 "
+              "split (6 products); fp32 accumulation everywhere",
+    "fp32x3": "every GEMM on the exact 3-way bf16 split (v_mfma_f32_32x32x16_bf16, 6 products), fp32 accumulation",
+    "fp32": "native fp32 MFMA (v_mfma_f32_32x32x2_f32)"}
+
+
 def run_train(args, device):
     """Finetune step: random batch of pixels of one of
     8 cameras -> query -> aggregate (training forward) -> composite -> MSE on
@@ -440,11 +460,14 @@ def run_train(args, device):
     k = max(args.steps, 1)
     flops = 3.0 * (stats["pairs"] * FLOP_PER_PAIR + stats["valid"] * FLOP_PER_SAMPLE) / k  # fwd + 2x bwd GEMMs
     ms = t / k * 1e3
-    print(json.dumps({
+    tf = flops / (ms * 1e-3) / 1e12
+    peak = TRAIN_PEAK_TFLOPS[args.train_precision]
+    line = {
         "metric": "train steps/s (fwd+bwd+Adam, 3600-ray batches), 2M neural points",
         "value": round(1e3 / ms, 3), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32", "train_forward": args.train_precision, "h2_fallbacks": int(model.h2_fallbacks),
+        "dtype": args.train_precision, "arith": TRAIN_ARITH[args.train_precision],
+        "train_forward": args.train_precision, "h2_fallbacks": int(model.h2_fallbacks),
         "optimizer": "pnr_adam_step" if args.optimizer == "hip" else "torch.optim.Adam(fused=True)",
         "data": "synthetic (seeded lego-like point cloud, random target colours)",
         "config": {"workload": f"finetune step, {args.train_rays} random rays of {H}x{W} frames, {args.points} points",
@@ -452,10 +475,16 @@ def run_train(args, device):
         "ray_samples_per_s_M": round(world * args.train_rays * opt.SR / (ms * 1e-3) / 1e6, 3),
         "parallelism": (f"dp{world}: {args.train_rays} rays per rank per step, DDP-mean gradients "
                         f"(one flat MLP all_reduce + touched point rows all_gather)" if world > 1 else "single GPU"),
-        "gemm_tflops_per_s": round(flops / (ms * 1e-3) / 1e12, 3),
-        "counts_per_step": {k2: v // k for k2, v in stats.items()}}), flush=True)
+        "gemm_tflops_per_s": round(tf, 3),
+        "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(tf / peak, 4),
+                     "note": "whole step (fwd + bwd + Adam + query) against the MLP GEMM work only: 3 x (542 720 "
+                             "FLOP per valid pair + 137 216 per valid sample) per step (forward, data and weight "
+                             "gradients); peak = the fp32-equivalent ceiling of the split arithmetic"},
+        "counts_per_step": {k2: v // k for k2, v in stats.items()}}
     if world > 1:
         dist.destroy_process_group()
+    return line
 
 
 def main():
@@ -463,7 +492,10 @@ def main():
     if args.mode == "train":
         local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        return run_train(args, torch.device("cuda", local))
+        line = run_train(args, torch.device("cuda", local))
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -764,10 +796,31 @@ def main():
         if world == 1 and args.dtype in ("fp32h2", "bf16"):
             acc.update(accuracy_vs_x3(model, opt, dev_cams[0], bg, args.dtype))
         out["accuracy"] = acc
+        if world == 1 and args.config == "headline" and not args.no_train_line:
+            # SURVEY config c3's finetune step on the same box, outside the timed region
+            # (the line `bench.py --mode train` prints, with its own roofline)
+            del model, agg
+            torch.cuda.empty_cache()
+            try:
+                out["train"] = train_summary(args, device)
+            except Exception as e:  # the render line must never be lost to the training extra
+                out["train"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def train_summary(args, device):
+    """The finetune step (--mode train, default flags) measured after the render
+    line: 20 timed steps after 5 warm-up steps, same points and box."""
+    import copy
+    targs = copy.copy(args)
+    targs.mode, targs.steps, targs.warmup, targs.dtype = "train", 20, 5, "fp32"
+    line = run_train(targs, device)
+    keep = ("value", "unit", "ms_per_step", "dtype", "arith", "roofline", "h2_fallbacks", "optimizer", "config",
+            "counts_per_step", "gemm_tflops_per_s")
+    return {"train_ms_per_step": line["ms_per_step"], **{k: line[k] for k in keep}}
 
 
 if __name__ == "__main__":

@@ -72,22 +72,35 @@ class GridHP(dict):
     """get_hyperparameters' dict for a grid built on the device
     (pnr_grid_build_dev): the point-independent entries are host values, the
     bbox-derived ones (shift, dims, ranges) are read back from the device
-    geometry on first access (one wait for the build)."""
+    geometry on first access (one wait for the build).  The read is tied to the
+    build that made this dict: after a rebuild of the handle, or an in-place
+    edit of the points, an unread entry raises instead of returning the newer
+    geometry; and it is refused while the stream is being captured (the wait
+    is a host synchronisation)."""
 
-    def __init__(self, handle, base):
+    def __init__(self, handle, base, gen):
         super().__init__(base)
         self._handle = handle
+        self._gen = gen
+        self._xyz_version = handle._xyz._version
 
     def __missing__(self, key):
         if key not in ("shift", "dims", "ranges"):
             raise KeyError(key)
+        h = self._handle
+        if h.gen != self._gen or h._xyz._version != self._xyz_version:
+            raise L.PnrError(f"grid hyperparameter {key!r} read after the grid was rebuilt or its points "
+                             "changed: read it before the next build (or use the handle's current hp)")
+        if _capturing():
+            raise L.PnrError(f"grid hyperparameter {key!r} first read during stream capture: it waits for the "
+                             "build (read it once before capturing)")
         sh, vs, dm = (L.c_float * 3)(), (L.c_float * 3)(), (L.c_int32 * 3)()
-        L.check(L.lib().pnr_grid_geometry(self._handle.h, sh, vs, dm), "pnr_grid_geometry")
+        L.check(L.lib().pnr_grid_geometry(h.h, sh, vs, dm), "pnr_grid_geometry")
         shift = np.array(list(sh), np.float32)
         dims = np.array(list(dm), np.int32)
         # ranges_np = [min - pad, max + pad]: the min half is the shift; the max half is
         # the clipped bbox max + pad (bbox read once here, off the hot path)
-        mx = np.asarray(self._handle.bbox_max(), np.float32)
+        mx = np.asarray(h.bbox_max(), np.float32)
         ranges = np.asarray(self["opt_ranges"], np.float32)
         mx = (np.minimum(mx, ranges[3:]) + self["pad"]).astype(np.float32)
         self.update(shift=shift, dims=dims, ranges=np.concatenate([shift, mx]).astype(np.float32))
@@ -189,28 +202,66 @@ class CountsHandle:
         return self._d
 
 
+# Handles whose owner was garbage-collected.  A finaliser can run at any
+# allocation -- inside someone's HIP-graph capture too -- and pnr_destroy's
+# hipFree / hipHostFree / hipEventDestroy are illegal there (they invalidate a
+# global-mode capture: GPUTEST_r04's RenderGraph failure).  So __del__ never
+# calls HIP; the handles are destroyed at the next safe point
+# (release_deferred: a handle creation or build, finish(), RenderGraph after
+# its capture).
+_DEFERRED: list = []
+_CAPTURES = [0]   # RenderGraph captures in progress (any stream of this process)
+
+
+def _capturing() -> bool:
+    if _CAPTURES[0]:
+        return True
+    try:
+        return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+    except Exception:
+        return False
+
+
+def release_deferred() -> int:
+    """Destroy the handles dropped by the garbage collector; a no-op while this
+    thread's stream (or a RenderGraph) is capturing.  Returns the number freed."""
+    if not _DEFERRED or _capturing():
+        return 0
+    n = 0
+    while _DEFERRED:
+        L.lib().pnr_destroy(_DEFERRED.pop())
+        n += 1
+    return n
+
+
 class GridHandle:
     """pnr_handle + persistent grid for one point cloud version."""
 
     def __init__(self, device: torch.device):
         L.require_gpu()
+        release_deferred()
         self.device = device
         h = L.c_void_p()
         L.check(L.lib().pnr_create(device.index or 0, L.ctypes.byref(h)), "pnr_create")
         self.h = h
         self.key = None
         self.hp = None
+        self.gen = 0
 
     def close(self):
+        """Free the grid now (explicit; refused during stream capture)."""
         if self.h:
+            if _capturing():
+                raise L.PnrError("GridHandle.close() during stream capture: pnr_destroy frees device memory")
             L.lib().pnr_destroy(self.h)
             self.h = None
+        release_deferred()
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        h = getattr(self, "h", None)
+        if h:
+            _DEFERRED.append(h)   # no HIP call from a finaliser (see _DEFERRED)
+            self.h = None
 
     def bbox(self, xyz: torch.Tensor):
         out = torch.empty(6, dtype=torch.float32, device=xyz.device)
@@ -237,13 +288,15 @@ class GridHandle:
                int(getattr(opt, "slot0_drop", 1)), int(getattr(opt, "grid_seed", 0)), policy)
         if not force and key == self.key:
             return self.hp
+        release_deferred()
+        self.gen += 1
         sp, base = grid_spec(opt) if policy == "reservoir" else (None, None)
         if sp is not None and not getattr(opt, "grid_host_bbox", False):
             # no host sync: bbox -> get_hyperparameters -> build, all on the device
             L.check(L.lib().pnr_grid_build_dev(self.h, L.ptr(xyz), xyz.shape[0], L.ctypes.byref(sp),
                                                L.stream_ptr(xyz.device)), "pnr_grid_build_dev")
-            hp = GridHP(self, base)
             self._xyz = xyz
+            hp = GridHP(self, base, self.gen)
             self.key, self.hp = key, hp
             self._max_o, self._P = int(sp.max_o), int(opt.P)
             return hp

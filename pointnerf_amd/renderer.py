@@ -17,6 +17,8 @@ the feature buffer) and no ``raypos[R,400,3]`` / ``[R,SR,K,38]`` intermediates.
 """
 from __future__ import annotations
 
+import gc
+
 import torch
 import torch.nn as nn
 
@@ -417,6 +419,8 @@ class NeuralPointsRayMarching(nn.Module):
         the later ones' counts are kept for the next finish()).  Returns the
         per-call sample counts (the ``last_counts`` dict of each call, in issue
         order)."""
+        from .querier import release_deferred
+        release_deferred()
         done = getattr(self, "_done", [])
         n_all = len(done) + len(self._pending)
         k = n_all if upto is None else min(int(upto), n_all)
@@ -951,11 +955,30 @@ class RenderGraph:
                                None, False, self.state, capacity=cap, record=False)
         torch.cuda.current_stream(dev).wait_stream(stream)
         torch.cuda.synchronize(dev)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out, self.rec = model._render_rays(self.precision, self.campos, self.camrot, self.raydir, near, far,
-                                                    self.bg, False, None, False, self.state, capacity=cap,
-                                                    keep=self.keep, record=False)
+        # Nothing may issue a capture-illegal HIP call (hipFree, an event or stream
+        # sync) while the graph records -- from this thread, or from a finaliser
+        # the garbage collector runs at some allocation inside the capture (the
+        # GPUTEST_r04 failure).  Collect dead cycles now, keep the collector off
+        # during the capture, and have GridHandle finalisers defer their frees
+        # (querier._DEFERRED); other threads' calls cannot invalidate a
+        # thread-local capture.
+        from . import querier as Q
+        gc.collect()
+        Q.release_deferred()
+        gc_was_on = gc.isenabled()
+        gc.disable()
+        Q._CAPTURES[0] += 1
+        try:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                self.out, self.rec = model._render_rays(self.precision, self.campos, self.camrot, self.raydir, near,
+                                                        far, self.bg, False, None, False, self.state, capacity=cap,
+                                                        keep=self.keep, record=False)
+        finally:
+            Q._CAPTURES[0] -= 1
+            if gc_was_on:
+                gc.enable()
+        Q.release_deferred()
         self.capacity = cap
 
     def replay(self, campos=None, camrot=None, raydir=None):

@@ -2,6 +2,8 @@
 captured frame (RenderGraph): bitwise equal to the eager synchronous render
 (the reference syncs at qpiw.py:656, 716 and
 neural_points.py:786)."""
+import gc
+
 import pytest
 import torch
 
@@ -130,6 +132,81 @@ def test_render_graph_replay_bitwise(cuda, precision):
         assert _eq(want2, out)
     out = g.replay(cp, cr, rd)
     assert g.check() and _eq(want, out)
+
+
+def _grid_in_cycle(cuda, sc):
+    """A built GridHandle (device tables, pinned stats, an event) in a reference
+    cycle, held by the returned list: once the list is cleared, the garbage
+    collector, not the refcount, frees it."""
+    from pointnerf_amd.querier import GridHandle
+    h = GridHandle(cuda)
+    h.build(sc["opt"], torch.from_numpy(sc["xyz"]).to(cuda).contiguous())
+    torch.cuda.synchronize()
+    h.cycle = h
+    return [h]
+
+
+def test_finaliser_inside_user_capture_keeps_graph_valid(cuda):
+    """GPUTEST_r04's failure mode, forced: a dead GridHandle is collected inside
+    a global-mode capture (torch's default).  Its finaliser must not call HIP
+    (pnr_destroy's hipFree would invalidate the capture); the handle is freed
+    at the next safe point instead."""
+    from pointnerf_amd import querier as Q
+    sc, _ = _cams(cuda, thetas=(30.0,))
+    gc.collect()
+    Q.release_deferred()
+    gc_on = gc.isenabled()
+    gc.disable()
+    try:
+        _grid_in_cycle(cuda, sc).clear()
+        x = torch.zeros(16, device=cuda)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            assert gc.collect() > 0          # the finaliser runs here, mid-capture
+            x.add_(1.0)
+        assert len(Q._DEFERRED) == 1
+        g.replay()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(x, torch.full_like(x, 2.0))
+    finally:
+        if gc_on:
+            gc.enable()
+    assert Q.release_deferred() == 1 and not Q._DEFERRED
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32h2"])
+def test_render_graph_capture_survives_finaliser(cuda, precision):
+    """RenderGraph with a GridHandle finaliser forced inside its capture window
+    (an explicit collection at the captured call): the capture stays valid and
+    the replay equals the eager render bitwise."""
+    from pointnerf_amd import querier as Q
+    from pointnerf_amd.renderer import RenderGraph
+    sc, cams = _cams(cuda, thetas=(30.0,))
+    m = _renderer(sc, cuda, formula_params(salt=0.6))
+    m.precision = precision
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    cp, cr, rd = cams[0]
+    want = [t.clone() for t in m.render_rays(cp, cr, rd, 2.0, 6.0, bg)]
+    orig = m._render_rays
+    seen = []
+    holder = _grid_in_cycle(cuda, sc)
+
+    def render_with_finaliser(*a, **kw):
+        if kw.get("keep") is not None:        # the captured call
+            holder.clear()                    # the handle becomes cyclic garbage mid-capture
+            seen.append(gc.collect())
+            seen.append(len(Q._DEFERRED))
+        return orig(*a, **kw)
+
+    m._render_rays = render_with_finaliser
+    g = RenderGraph(m, cp, cr, rd, 2.0, 6.0, bg, margin=1.5)
+    del m._render_rays
+    assert seen and seen[0] > 0 and seen[1] >= 1
+    assert not Q._DEFERRED                   # released right after the capture
+    out = g.replay()
+    assert g.check()
+    assert _eq(want, out)
 
 
 def test_render_graph_flags_overflow(cuda):

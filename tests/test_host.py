@@ -135,3 +135,27 @@ def test_scene_points_cap_and_fixed_bbox():
         assert g["occ_numpnts"].max() <= o.P - 1
         assert np.all(p >= np.asarray(o.ranges[:3], np.float32)) and np.all(p <= np.asarray(o.ranges[3:], np.float32))
 
+
+
+def test_grid_handle_finaliser_defers_destroy():
+    """GridHandle.__del__ issues no HIP call (a finaliser may run inside someone's
+    graph capture, GPUTEST_r04): the handle lands on querier._DEFERRED and is
+    destroyed at the next safe point (release_deferred)."""
+    import ctypes
+    import gc
+    from pointnerf_amd import querier as Q
+    h = Q.GridHandle.__new__(Q.GridHandle)
+    h.h = ctypes.c_void_p(0x1234)      # never dereferenced: the test takes it back below
+    h.self_ref = h                     # a reference cycle: freed by the collector, not by refcount
+    n0 = len(Q._DEFERRED)
+    del h
+    gc.collect()
+    assert len(Q._DEFERRED) == n0 + 1
+    assert Q._DEFERRED.pop().value == 0x1234
+    Q._CAPTURES[0] += 1                # a capture in progress: nothing is released
+    try:
+        Q._DEFERRED.append(ctypes.c_void_p(0x5678))
+        assert Q.release_deferred() == 0 and len(Q._DEFERRED) == n0 + 1
+    finally:
+        Q._CAPTURES[0] -= 1
+        Q._DEFERRED.pop()
