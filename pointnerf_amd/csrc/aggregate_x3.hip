@@ -1036,432 +1036,6 @@ __global__ void __launch_bounds__(512, 1) k_pairs_x3_train(X3Args A) { pairs_bod
 __global__ void __launch_bounds__(512, 1) k_pairs_h2_train(X3Args A) { pairs_body<true, true>(A); }
 
 // ---------------------------------------------------------------------------
-// k_pairs_h2s: k_pairs_h2's per-pair chain -- same split packs, same f16-split
-// products, same outputs (hid planes for k_color_h2, alpha, vmask) -- with TWO
-// tiles in flight per CU.  k_pairs_h2 runs one 64-pair tile per CU: its four
-// MFMA waves (one per SIMD) stop the matrix pipe for every activation store
-// (~23 % of a tile) and the producer waves beside them issue no MFMA.  Here a
-// workgroup is four waves that do everything for their tile -- gather, PE,
-// the four layers, the tail -- and two workgroups share a CU (72 KB of LDS
-// each), so one workgroup's stores, gather latency and tail run beside the
-// other one's MFMA stream on the same SIMDs.  What made room in LDS:
-//   * the distance PE (block1.0's input) lives in rows 0..63 of the layer
-//     planes (free until act1 is stored over them), the block3.0 extras in row
-//     group 32 (only block3.0 reads rows 256..271), written by the gather;
-//   * P1 (block1.0's point half) is loaded straight into the accumulators
-//     (acc = P1 2^-(s-11), then the distance-PE products; the layer scale is
-//     a power of two, so the scaling is exact) instead of parked in LDS;
-//   * the tail (LeakyReLU, alpha partials, K sums) runs from the block3.2
-//     accumulators in registers (k_pairs_x3's DPP reduce-scatter) instead of
-//     a 66 KB park for producer waves.
-// The gather's dependent loads travel a layer apart: the sample row during
-// block1.2, pidx / sample positions during block3.0, the point rows after
-// block3.2, P1 after the tail.
-struct SL {
-  static constexpr int OffWt = 2 * kPlaneX;           // float [2][64] w_k clamp(conf_k) (tile parity)
-  static constexpr int OffSf = OffWt + 2 * kXT * 4;   // int   [2][8]  sample has a valid neighbour
-  static constexpr int OffAp = OffSf + 2 * kXTS * 4;  // float [4][64] alpha_branch.0 partials per wave
-  static constexpr int OffWa = OffAp + 4 * kXT * 4;   // float [256]   alpha_branch.0 weights
-  static constexpr int OffTq = OffWa + kHid * 4;      // int   [4]     tile of iteration i at i % 4
-  static constexpr int OffRw = OffTq + 16;            // float [9]     uniform Rw2c (pnr_mlp.rw2c or identity)
-  static constexpr int OffCam = OffRw + 48;           // float [12]    campos, camrot (one-camera launches)
-  static constexpr size_t Lds = (size_t)OffCam + 48;
-  static_assert(OffWt % 16 == 0 && OffAp % 16 == 0 && OffWa % 16 == 0, "16-B aligned LDS arrays");
-  static_assert(2 * Lds <= 160 * 1024, "two workgroups per CU");
-};
-
-// one tile's gather, lane = pair (sample lane >> 3, slot lane & 7).  Every load
-// is unconditional, from a valid address (sample-list entry 0 / point 0 for
-// empty lanes), and selected afterwards: a load under a divergent branch makes
-// the compiler drain vmcnt where the branch merges, and here that would also
-// wait for the weight ring and the P1 rows in flight.
-struct GS {
-  int64_t row, drow;
-  int pid;
-  bool active, slot;   // slot: active && k < K
-  float sw[3], sp[3], vd[3], pw3[3], col[3], pdir[3], cf, pp[3];
-};
-
-__device__ __forceinline__ void gs_row(const X3Args& A, int64_t n, int64_t tile, int lane, GS& g) {
-  const int64_t v = tile * kXTS + (lane >> 3);
-  g.active = v < n;
-  g.row = A.s.samp_list[g.active ? v : 0];
-}
-
-__device__ __forceinline__ void gs_sample(const X3Args& A, int lane, GS& g) {
-  const int k = lane & 7, K = A.s.K;
-  g.slot = g.active && k < K;
-  const int p = A.s.pidx[g.row * K + (k < K ? k : K - 1)];
-  g.pid = g.slot ? p : -1;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const float w = A.s.sample_w[g.row * 3 + a], q = A.s.sample_p[g.row * 3 + a];
-    g.sw[a] = g.active ? w : 0.f;
-    g.sp[a] = g.active ? q : 0.f;
-  }
-  g.drow = (int64_t)A.s.dir_map[g.row] / A.s.dir_div;
-}
-
-__device__ __forceinline__ void gs_points(const X3Args& A, GS& g) {
-  const bool valid = g.pid >= 0;
-  const int64_t pr = valid ? g.pid : 0;   // torch.clamp(sample_pidx, min=0)
-  const float* conf = A.pts.conf ? A.pts.conf : A.pts.xyz;
-  const float* pers = A.pts.pers ? A.pts.pers : A.pts.xyz;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const float d = A.s.dirs[g.drow * 3 + a], x = A.pts.xyz[pr * 3 + a], cl = A.pts.color[pr * 3 + a],
-                pd = A.pts.dir[pr * 3 + a], q = pers[pr * 3 + a];
-    g.vd[a] = g.active ? d : 0.f;
-    g.pw3[a] = valid ? x : 0.f;
-    g.col[a] = valid ? cl : 0.f;
-    g.pdir[a] = valid ? pd : 0.f;
-    g.pp[a] = valid ? q : 0.f;
-  }
-  g.cf = conf[pr];   // raw: gs_compute applies the table's presence (a select here sinks the load into a branch)
-}
-
-// k_pairs_h2's gather() arithmetic on a GS: the rotated 6-d distance (every
-// wave), and (wave 0) the block3.0 extras -> row group 32 of the planes, the
-// blend weights / sample flags of slot `par`, out_weight / out_conf.  The
-// uniform Rw2c and the one camera are in LDS (cam = [campos, camrot]).
-__device__ __forceinline__ void gs_compute(const X3Args& A, const GS& g, int lane, int wid, char* lds, int par,
-                                           float (&dr6)[6]) {
-  const float* Rw = reinterpret_cast<const float*>(lds + SL::OffRw);
-  const int j = lane >> 3, k = lane & 7;
-  const int K = A.s.K;
-  const bool valid = g.pid >= 0;
-  const int64_t prow = valid ? g.pid : (g.slot ? 0 : -1);
-  float pp[3] = {g.pp[0], g.pp[1], g.pp[2]};
-  if (!A.pts.pers) {
-    float c[3], R[9];
-    if (A.s.ray_cam) {   // multi-camera batch: the ray's camera tables
-      const int64_t cam = A.s.ray_cam[g.drow];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) c[i] = A.pts.campos[cam * 3 + i];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) R[i] = A.pts.camrot[cam * 9 + i];
-    } else {
-      const float* cam = reinterpret_cast<const float*>(lds + SL::OffCam);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) c[i] = cam[i];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) R[i] = cam[3 + i];
-    }
-    float q[3];
-    world_to_pers(g.pw3, c, R, q);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) pp[a] = valid ? q[a] : 0.f;
-  }
-  float d6[6];
-  d6[0] = g.pw3[0] - g.sw[0];
-  d6[1] = g.pw3[1] - g.sw[1];
-  d6[2] = g.pw3[2] - g.sw[2];
-  d6[3] = pp[0] * pp[2] - g.sp[0] * g.sp[2];
-  d6[4] = pp[1] * pp[2] - g.sp[1] * g.sp[2];
-  d6[5] = pp[2] - g.sp[2];
-  mat3(Rw, d6, dr6);
-  dr6[3] = d6[3];
-  dr6[4] = d6[4];
-  dr6[5] = d6[5];
-  if (A.pts.rw2c) rot_point(A.pts.rw2c, prow, d6, dr6);
-  if (wid != 0) return;
-  const float nrm = sqrtf(d6[0] * d6[0] + d6[1] * d6[1] + d6[2] * d6[2]);
-  const float wl = valid ? 1.f / fmaxf(nrm, 1e-6f) : 0.f;
-  const float wsum = xor8_sum(wl);
-  const float wn = wl / fmaxf(wsum, 1e-8f);
-  const float confc = fminf(fmaxf(A.pts.conf && g.slot ? g.cf : 1.f, 1e-4f), 1.f);
-  const bool samp_valid = xor8_sum(valid ? 1.f : 0.f) > 0.f;
-  float vrot[3], drot[3];
-  mat3(Rw, g.vd, vrot);
-  mat3(Rw, g.pdir, drot);
-  if (A.pts.rw2c) {
-    rot_point(A.pts.rw2c, prow, g.pdir, drot);
-    rot_point(A.pts.rw2c, g.active ? slot0_point(A.s, g.row) : 0, g.vd, vrot);
-  }
-  const float dot = drot[0] * vrot[0] + drot[1] * vrot[1] + drot[2] * vrot[2];
-  const float ex[8] = {g.col[0], g.col[1], g.col[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2], dot,
-                       1.f};
-  store_group<true>(lds, kPlaneX, 32, lane, ex);   // block3.0 inputs 256..263 (263: the bias column)
-  reinterpret_cast<float*>(lds + SL::OffWt)[par * kXT + lane] = wn * confc;
-  if (k == 0) reinterpret_cast<int*>(lds + SL::OffSf)[par * kXTS + j] = g.active && samp_valid;
-  if (g.slot) {
-    if (A.out_weight) A.out_weight[g.row * K + k] = wn;
-    if (A.out_conf) A.out_conf[g.row * K + k] = confc;
-  }
-}
-
-// PE_5 rows 2e (sin), 2e + 1 (cos) of item e = 5 ch + f, f16-split into the
-// layer planes (rows 0..59; 60..63 zero): wave w computes items e = w mod 4
-__device__ __forceinline__ void pe_rows(char* XP, int wid, int lane, const float (&dr6)[6]) {
-#pragma unroll
-  for (int e = 0; e < 30; ++e) {
-    if ((e & 3) != wid) continue;   // wave-uniform
-    float sn, cs;
-    sincosf(dr6[e / 5] * (float)(1 << (e % 5)), &sn, &cs);
-    unsigned x0, x1;
-    splith(sn, cs, x0, x1);
-    const int r = 2 * e;
-    char* d = XP + ((r >> 3) * kXT + lane) * 16 + 2 * (r & 7);
-    *reinterpret_cast<unsigned*>(d) = x0;
-    *reinterpret_cast<unsigned*>(d + kPlaneX) = x1;
-  }
-  if (wid == 3) {
-    char* pz = XP + (7 * kXT + lane) * 16 + 8;
-    *reinterpret_cast<uint2*>(pz) = make_uint2(0u, 0u);
-    *reinterpret_cast<uint2*>(pz + kPlaneX) = make_uint2(0u, 0u);
-  }
-}
-
-#ifdef PNR_H2S_TRACE
-// diagnostic build only (tools/h2s_trace.py): s_memtime per phase, waves' first 8 tiles
-__device__ unsigned long long g_h2s_trace[512 * 4 * 8 * 16];
-#define H2S_STAMP(i)                                                                           \
-  do {                                                                                         \
-    if (it < 8 && lane == 0 && blockIdx.x < 512)                                               \
-      g_h2s_trace[((blockIdx.x * 4 + wid) * 8 + it) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define H2S_STAMP(i) \
-  do {               \
-  } while (0)
-#endif
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_pairs_h2s(X3Args A) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = lane & 31, h = lane >> 5;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, kXTS);
-  const float neg = A.w.neg_slope;
-  char* const XP = lds;
-  const float* const waL = reinterpret_cast<const float*>(lds + SL::OffWa);
-  float* const apart = reinterpret_cast<float*>(lds + SL::OffAp);
-  int* const TQ = reinterpret_cast<int*>(lds + SL::OffTq);
-  const int T0 = 2 * wid;
-  const int voff = (T0 * 2 * 64 + lane) * 16;
-  const __amdgpu_buffer_rsrc_t r1 = rsrc(A.wx.pack[0]), r2 = rsrc(A.wx.pack[1]), r3 = rsrc(A.wx.pack[2]),
-                               r4 = rsrc(A.wx.pack[3]);
-  const float sc1 = A.wx.scale[0], sc2 = A.wx.scale[1], sc3 = A.wx.scale[2], sc4 = A.wx.scale[3];
-  const float inv1 = 1.f / sc1;   // exact: a power of two
-  const float ba = A.w.ba[0];
-  reinterpret_cast<float*>(lds + SL::OffWa)[threadIdx.x] = A.w.wa[threadIdx.x];
-  if (threadIdx.x < 9)
-    reinterpret_cast<float*>(lds + SL::OffRw)[threadIdx.x] =
-        A.w.rw2c ? A.w.rw2c[threadIdx.x] : (threadIdx.x % 4 == 0 ? 1.f : 0.f);
-  if (threadIdx.x >= 64 && threadIdx.x < 76 && !A.pts.pers && !A.s.ray_cam)
-    reinterpret_cast<float*>(lds + SL::OffCam)[threadIdx.x - 64] =
-        threadIdx.x < 67 ? A.pts.campos[threadIdx.x - 64] : A.pts.camrot[threadIdx.x - 67];
-  if (wid == 1) {   // rows 264..271: block3.0's 17th k-step reads them, nothing writes them
-    *reinterpret_cast<uint4*>(XP + (33 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(XP + kPlaneX + (33 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
-  }
-#ifdef PNR_H2S_TRACE
-  if (lane == 0 && blockIdx.x < 512) {
-    unsigned hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_h2s_trace[((blockIdx.x * 4 + wid) * 8 + 0) * 16 + 14] = hw;
-    g_h2s_trace[((blockIdx.x * 4 + wid) * 8 + 0) * 16 + 15] = xcc;
-  }
-#endif
-  int64_t tile = first_tile(ntiles);
-  if (threadIdx.x == 0) {
-    TQ[0] = (int)tile;
-    TQ[1] = tile < ntiles ? (int)take_tile(A, ntiles) : (int)ntiles;
-  }
-  GS g = {};
-  if (tile < ntiles) {
-    gs_row(A, n, tile, lane, g);
-    gs_sample(A, lane, g);
-    gs_points(A, g);
-  }
-  float chk = 0.f;   // 0 * outputs: NaN once one is not finite (f16 range, see k_pairs_h2)
-  WRing<true> wr;
-  f32x16 acc[4];
-  prime<true>(wr, r1, voff);
-  int it = 0;
-  bool pz[2] = {true, true};   // P1 row absent for pair column 32 pt + c
-  {
-    // the first tile's P1 rows -> acc (later tiles: issued right after the previous tail)
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const int pr = __shfl(g.pid, 32 * pt + c);
-      const int64_t row = pr;   // (launched without used_map: P1 rows = point rows)
-      pz[pt] = row < 0;
-      const f32x4n* src = reinterpret_cast<const f32x4n*>(A.p1 + (row < 0 ? 0 : row) * kHid + 32 * T0 + 4 * h);
-#pragma unroll
-      for (int T = 0; T < 2; ++T)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4n v = __builtin_nontemporal_load(src + (32 * T + 8 * q) / 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[2 * pt + T][4 * q + i] = v[i];
-        }
-    }
-  }
-  while (tile < ntiles) {   // uniform over the workgroup (TQ)
-    const int par = it & 1;
-    H2S_STAMP(0);
-    if (threadIdx.x == 0) {   // the tile after next (taken only while this workgroup goes on)
-      const int nx = TQ[(it + 1) & 3];
-      TQ[(it + 2) & 3] = nx < ntiles ? (int)take_tile(A, ntiles) : (int)ntiles;
-    }
-    // ------------------------------------------------------------ gather, PE, extras (planes free)
-    float dr6[6];
-    gs_compute(A, g, lane, wid, lds, par, dr6);
-    pe_rows(XP, wid, lane, dr6);
-    // acc = P1 / sc1 (0 for empty pairs): block1.0 = sc1 (acc + W1b . PE_5)
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-      for (int T = 0; T < 2; ++T) acc[2 * pt + T] = pz[pt] ? (f32x16){0.f} : acc[2 * pt + T] * inv1;
-    H2S_STAMP(1);
-    __syncthreads();   // B0: PE rows, extras, weights, TQ[it + 1]
-    H2S_STAMP(2);
-    const int64_t next = TQ[(it + 1) & 3];
-    // ------------------------------------------------------------ block1.0
-    layer<true>(acc, wr, r1, voff, XP, kPlaneX, 4, lane);
-    prime<true>(wr, r2, voff);
-    H2S_STAMP(3);
-    __syncthreads();   // B1: PE rows consumed
-    store_act<true>(acc, XP, neg, sc1, lane, T0);
-    acc_init<true>(acc, A.w.b2, 1.f / sc2, lane, T0);
-    __syncthreads();   // B2
-    H2S_STAMP(4);
-    // the next tile's gather, one dependent load per layer; unconditional (a tile past
-    // the end re-reads this one)
-    const int64_t nextc = next < ntiles ? next : tile;
-    GS gn;
-    gs_row(A, n, nextc, lane, gn);
-    // ------------------------------------------------------------ block1.2
-    layer<true>(acc, wr, r2, voff, XP, kPlaneX, kBiasSteps(true), lane);
-    prime<true>(wr, r3, voff);
-    H2S_STAMP(5);
-    __syncthreads();   // B3
-    store_act<true>(acc, XP, neg, sc2, lane, T0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
-    __syncthreads();   // B4
-    H2S_STAMP(6);
-    gs_sample(A, lane, gn);
-    // ------------------------------------------------------------ block3.0 (extras rows 256..263)
-    layer<true>(acc, wr, r3, voff, XP, kPlaneX, 17, lane);
-    prime<true>(wr, r4, voff);
-    H2S_STAMP(7);
-    __syncthreads();   // B5
-    store_act<true>(acc, XP, neg, sc3, lane, T0);
-    acc_init<true>(acc, A.w.b4, 1.f / sc4, lane, T0);
-    __syncthreads();   // B6
-    H2S_STAMP(8);
-    // ------------------------------------------------------------ block3.2
-    layer<true>(acc, wr, r4, voff, XP, kPlaneX, kBiasSteps(true), lane);
-    H2S_STAMP(9);
-    // ------------------------------------------------------------ tail: lrelu, alpha partials, K sums
-    {
-      const float* wtL = reinterpret_cast<const float*>(lds + SL::OffWt) + par * kXT;
-      const int* sflag = reinterpret_cast<const int*>(lds + SL::OffSf) + par * kXTS;
-      const int i8 = c & 7;
-      const bool b2 = (i8 & 4) != 0, b1 = (i8 & 2) != 0, b0 = (i8 & 1) != 0;
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt) {
-        float pa_part = 0.f;
-        const float wtp = wtL[32 * pt + c];
-        const int sj = (32 * pt + c) >> 3;
-        const int64_t vo = tile * kXTS + sj;
-        const bool wrt = vo < n && sflag[sj];
-        char* hrow = reinterpret_cast<char*>(A.hid) + (vo / kXT) * kHidTile + (vo % kXT) * 16 + 4 * (i8 & 1) + 8 * h;
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-          float v[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float hv = lrelu(acc[2 * pt + T][r] * sc4, neg);
-            pa_part += waL[32 * (T0 + T) + acc_row(r, h)] * hv;
-            v[r] = wtp * hv;
-          }
-          // K sums (point_aggregators.py:622-628): DPP reduce-scatter over the 8 lanes of a sample
-          float w8[8], w4[4], w2[2];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const float send = b2 ? v[q] : v[q + 8];
-            const float recv = __builtin_bit_cast(
-                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x141, 0xf, 0xf, false));
-            w8[q] = (b2 ? v[q + 8] : v[q]) + recv;
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float send = b1 ? w8[q] : w8[q + 4];
-            const float recv = __builtin_bit_cast(
-                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E, 0xf, 0xf, false));
-            w4[q] = (b1 ? w8[q + 4] : w8[q]) + recv;
-          }
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const float send = b0 ? w4[q] : w4[q + 2];
-            const float recv = __builtin_bit_cast(
-                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xf, 0xf, false));
-            w2[q] = (b0 ? w4[q + 2] : w4[q]) + recv;
-          }
-          chk = fmaf(0.f, w2[0] + w2[1], chk);
-          if (wrt) {   // neurons n0, n0 + 1 (n0 = 32 (T0 + T) + 8 (i8 >> 1) + 2 (i8 & 1) + 4 h) -> hid planes
-            unsigned hi, lo;
-            splith(w2[0], w2[1], hi, lo);
-            char* d = hrow + (4 * (T0 + T) + (i8 >> 1)) * kXT * 16;
-            *reinterpret_cast<unsigned*>(d) = hi;
-            *reinterpret_cast<unsigned*>(d + kHidPlane) = lo;
-          }
-        }
-        pa_part += __shfl_xor(pa_part, 32);
-        if (h == 0) apart[wid * kXT + 32 * pt + c] = pa_part;
-      }
-    }
-    H2S_STAMP(10);
-    // the next tile's point rows and P1 rows -> registers / acc (in flight during the
-    // alpha and the next tile's PE)
-    gs_points(A, gn);
-    {
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt) {
-        const int pr = __shfl(gn.pid, 32 * pt + c);
-        const int64_t row = pr;   // (launched without used_map: P1 rows = point rows)
-        pz[pt] = row < 0;
-        const f32x4n* src = reinterpret_cast<const f32x4n*>(A.p1 + (row < 0 ? 0 : row) * kHid + 32 * T0 + 4 * h);
-#pragma unroll
-        for (int T = 0; T < 2; ++T)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4n v = __builtin_nontemporal_load(src + (32 * T + 8 * q) / 4);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[2 * pt + T][4 * q + i] = v[i];
-          }
-      }
-    }
-    H2S_STAMP(11);
-    __syncthreads();   // B7: alpha partials ready, the planes free for the next gather
-    H2S_STAMP(12);
-    if (wid == 0) {   // alpha of this tile's samples (point_aggregators.py:608-614)
-      const float* wtL = reinterpret_cast<const float*>(lds + SL::OffWt) + par * kXT;
-      const int* sflag = reinterpret_cast<const int*>(lds + SL::OffSf) + par * kXTS;
-      const int j = lane >> 3, k = lane & 7;
-      const float pa = apart[lane] + apart[kXT + lane] + apart[2 * kXT + lane] + apart[3 * kXT + lane] + ba;
-      const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
-      const float alpha_s = xor8_sum(wtL[lane] * alpha_k);
-      chk = fmaf(0.f, alpha_s, chk);
-      const int64_t vo = tile * kXTS + j;
-      if (k == 0 && vo < n) {
-        A.vmask[vo] = sflag[j];
-        if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
-      }
-    }
-    prime<true>(wr, r1, voff);   // the next tile's block1.0 (after the tail: its registers are free)
-    g = gn;
-    tile = next;
-    ++it;
-  }
-  if (A.wx.range_flag && chk != 0.f) atomicOr(A.wx.range_flag, 1);
-}
-
-// ---------------------------------------------------------------------------
 // k_color_h2: the colour branch 280 -> 128 -> 128 -> 128 (LeakyReLU each,
 // point_aggregators.py:630-638) on the input [hid (K-summed features),
 // PE_4(R.viewdir) sin block, cos block] (:506-512), as fp32-accurate f16-split
@@ -1721,12 +1295,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 }  // namespace
 
-#ifdef PNR_H2S_TRACE
-extern "C" __attribute__((visibility("default"))) int pnr_dev_h2s_trace(void* host, size_t bytes) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h2s_trace), bytes) == hipSuccess ? 0 : 3;
-}
-#endif
-
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
                         hipStream_t st) {
   static bool attr = false;
@@ -1799,20 +1367,6 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
   else memset(&a.sv, 0, sizeof(a.sv));
   PNR_HIP(hipMemsetAsync(tile_ctr, 0, 8 * sizeof(int32_t), st));
   const int64_t tiles = cdiv(s.n_max, kXTS);
-  static const bool h2s = getenv("PNR_PAIRS_H2S") && atoi(getenv("PNR_PAIRS_H2S")) != 0;
-  // k_pairs_h2s' branch-free gather needs the sample list, the dir map, colour
-  // and dir tables, and P1 rows indexed by point row
-  if (H && !sv && h2s && s.samp_list && s.dir_map && pts.color && pts.dir && !pts.used_map) {
-    static bool attr_s = false;
-    if (!attr_s) {
-      PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_h2s),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL::Lds));
-      attr_s = true;
-    }
-    hipLaunchKernelGGL(k_pairs_h2s, dim3(grid_for(tiles, 1, 2 * 256)), dim3(256), SL::Lds, st, a);
-    PNR_LAUNCH_CHECK();
-    return PNR_OK;
-  }
   if (H && sv)
     hipLaunchKernelGGL(k_pairs_h2_train, dim3(grid_for(tiles, 1, 256)), dim3(512), XL<H>::Lds, st, a);
   else if (H)

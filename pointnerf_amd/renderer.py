@@ -223,6 +223,12 @@ class _ZeroOneConfLoss(torch.autograd.Function):
         return d, None, None, None, None
 
 
+# device bytes a training batch reserves per sample slot: the forward's kept activations
+# (train.Saved: 8 pairs x (h1..h4, PE_5, extras, masks, weights) + the sample's colour
+# rows) and the backward's dz1..dz4 rows (train.AggregateFn.backward)
+TRAIN_BYTES_PER_SAMPLE = 8 * (4 * 1024 + 256 + 128 + 128 + 16) + 2660 + 8 * (4 * 1024 + 4) + 1024
+
+
 class _TrainAux(dict):
     """render_rays_train's last_train_aux: keys whose values need the batch's
     host counts are computed when first read (so that the forward itself never
@@ -271,6 +277,11 @@ class NeuralPointsRayMarching(nn.Module):
         self.p1_side_stream = True        # fp32h2 sync-free calls: P1 beside the query (see _render_rays)
         self.p1_side_max_points_per_ray = 4.0
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
+        # render_rays_train sizes its per-sample buffers for every slot of the batch while
+        # R * SR * TRAIN_BYTES_PER_SAMPLE fits this many bytes (None: a quarter of the
+        # device memory), else it reads the batch's valid-sample count (train_count_reads)
+        self.train_memory_budget = None
+        self.train_count_reads = 0
         self._h2_blocked_key = None   # weights whose activations left the f16 range (render_rays)
         self.h2_fallbacks = 0
         self.opt = opt
@@ -737,7 +748,13 @@ class NeuralPointsRayMarching(nn.Module):
         used_buf, used_map = used_points_device(bufs, K, xyz.shape[0])
         counts = bufs.read_counts_async()
         self.last_counts = counts
+        # saved activations (train.Saved) and the backward's dz rows are sized by the
+        # sample capacity: every slot of the batch (R * SR, no host read) while that
+        # fits the memory budget, else this batch's valid-sample count (one host read)
         S_cap = R * SR
+        if S_cap * TRAIN_BYTES_PER_SAMPLE > self._train_budget(dev):
+            S_cap = max(int(bufs.read_counts()["S_valid"]), 1)
+            self.train_count_reads += 1
         s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, S_cap, bufs.pidx.data_ptr(),
                       bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                       bufs.fill_rs.data_ptr(), SR, K)
@@ -791,6 +808,15 @@ class NeuralPointsRayMarching(nn.Module):
                      lambda: self._march_aux(rays, qp, bufs, R, counts.get()["R_valid"], xyz, op))
         self.last_train_aux = aux
         return out
+
+    def _train_budget(self, dev) -> int:
+        """Bytes of per-sample training buffers a sync-free forward may reserve:
+        train_memory_budget, or (None) a quarter of the device's memory."""
+        if self.train_memory_budget is not None:
+            return int(self.train_memory_budget)
+        if getattr(self, "_budget_dev", None) is None:
+            self._budget_dev = torch.cuda.get_device_properties(dev).total_memory // 4
+        return self._budget_dev
 
     def wants_aux(self) -> bool:
         """The reference aggregator returns weight / conf_coefficient (and the

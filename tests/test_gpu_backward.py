@@ -531,6 +531,42 @@ def test_train_backward_repeatable(cuda, train_precision):
                 assert d <= 1e-6 * big, (k, d, big)
 
 
+@pytest.mark.parametrize("train_precision", ["fp32x3", "fp32h2"])
+def test_train_memory_budget_sizes_exactly(cuda, train_precision):
+    """a batch whose every-slot capacity (R * SR samples) exceeds
+    train_memory_budget reads its valid-sample count once and sizes the kept
+    activations exactly -- same render and gradients as the sync-free
+    every-slot sizing: the render bitwise, the gradients up to summation order
+    (the split-K GEMMs cut a different row count)."""
+    sc = scene(20000, H=32, W=32, theta=60.0, default_conf=None)
+    m = _train_model(sc, cuda, formula_params(salt=0.3))
+    m.train_precision = train_precision
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd, bg = torch.from_numpy(sc["raydir"]).to(cuda), torch.from_numpy(sc["bg"]).to(cuda)
+    outs = []
+    for budget in (None, 1):
+        m.train_memory_budget = budget
+        reads0 = m.train_count_reads
+        for p in list(m.parameters()) + list(m.neural_points.parameters()):
+            p.grad = None
+        color = m.render_rays_train(cp, cr, rd, 2.0, 6.0, bg)[0]
+        assert m.train_count_reads - reads0 == (0 if budget is None else 1)
+        G = torch.randn(color.shape, generator=torch.Generator().manual_seed(5)).to(cuda)
+        (color * G).sum().backward()
+        npt = m.neural_points
+        o = {"color": color.detach().clone()}
+        o.update({k: getattr(npt, k).grad.clone() for k in ("points_color", "points_dir", "points_embeding",
+                                                              "points_conf")})
+        o.update({"mlp " + k: p.grad.clone() for k, p in m.aggregator.named_parameters()})
+        outs.append(o)
+    for k, ref in outs[0].items():
+        got = outs[1][k]
+        if k == "color":
+            assert torch.equal(got, ref), k
+        else:
+            assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()), k
+
+
 def _w2pers_torch(p, campos, camrot):
     """qpiw.py:102-109 in torch (differentiable): (x/z, y/z, z) of R^T (p - c)."""
     s = p - campos
