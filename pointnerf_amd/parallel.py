@@ -194,11 +194,20 @@ class GradReducer:
     equal (up to summation order) to one process stepping the union batch
     with a loss averaged per rank."""
 
-    def __init__(self, dense_params, point_params, group=None):
+    def __init__(self, dense_params, point_params, group=None, host_group=None):
+        """Collective when the process group is not gloo: every rank of the default
+        group must construct its reducer (it creates the gloo group that carries
+        the host-side row counts, unless ``host_group`` -- a gloo group over the
+        same ranks as ``group`` -- is passed)."""
         self.dense = [p for p in dense_params if p.requires_grad]
         self.points = [p for p in point_params if p is not None and p.requires_grad]
         self.group = group
-        self._host_group = None   # gloo group for host-side integers (no device sync)
+        self._host_group = host_group   # gloo group for host-side integers (no device sync)
+        if self.points and host_group is None:
+            import torch.distributed as dist
+            if dist.is_initialized() and dist.get_backend(group) != "gloo":
+                ranks = None if group is None else dist.get_process_group_ranks(group)
+                self._host_group = dist.new_group(ranks=ranks, backend="gloo")
         # point tables as [rows, channels] (the reference keeps them [1, N, C])
         if self.points:
             n = self.points[0].numel() // self.points[0].shape[-1]
@@ -227,13 +236,11 @@ class GradReducer:
         """max of a host integer over the ranks, on the CPU (gloo): the padding
         size of the row all-gather without a device -> host copy."""
         import torch.distributed as dist
-        if dist.get_backend(self.group) == "gloo":
-            g = self.group
-        else:
-            if self._host_group is None:
-                ranks = None if self.group is None else dist.get_process_group_ranks(self.group)
-                self._host_group = dist.new_group(ranks=ranks, backend="gloo")
-            g = self._host_group
+        gloo = dist.get_backend(self.group) == "gloo"
+        g = self.group if gloo else self._host_group
+        if not gloo and g is None:
+            raise RuntimeError("GradReducer: no gloo group for the host counts (construct it after "
+                               "init_process_group, or pass host_group)")
         t = torch.tensor([int(v)], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
         return int(t.item())
@@ -279,10 +286,11 @@ class GradReducer:
         ids[:count] = rows
         vals = torch.zeros((mx, sum(widths)), dtype=self.points[0].dtype, device=dev)
         if count:
-            # -1 entries gather row 0 and are zeroed: padding adds exact zeros
+            # -1 entries gather row 0 and are zeroed (where, not a product: row 0 may hold
+            # inf / NaN, which a 0 * x would spread to every rank)
             src = rows.clamp(min=0)
-            vals[:count] = torch.cat([self._grad(p).reshape(n, -1)[src] for p in self.points], 1)
-            vals[:count] *= (rows >= 0).to(vals.dtype)[:, None]
+            g = torch.cat([self._grad(p).reshape(n, -1)[src] for p in self.points], 1)
+            vals[:count] = torch.where((rows >= 0)[:, None], g, torch.zeros((), dtype=g.dtype, device=dev))
         all_ids = self._all_gather(ids)      # [world, mx]
         all_vals = self._all_gather(vals)    # [world, mx, D]
         sel = all_ids.reshape(-1).clamp(min=0)

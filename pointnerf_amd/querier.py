@@ -107,6 +107,16 @@ class GridHP(dict):
         return dict.__getitem__(self, key)
 
 
+GRID_BYTES_PER_CELL = 13.5   # cell tables of one build: coor_2_occ, cell_start / cell_end, dilated bytes, bitmaps
+
+
+def grid_dev_max_cells(opt) -> int:
+    """Largest ranges-box grid (cells) the sync-free device build sizes its tables
+    for (opt.grid_dev_max_cells, default 2^28 ~ 3.6 GB of tables); bigger boxes
+    build on the host-read bbox."""
+    return int(getattr(opt, "grid_dev_max_cells", 1 << 28))
+
+
 def grid_spec(opt):
     """The point-independent half of get_hyperparameters (qpiw.py:48-81) as
     pnr_grid_spec, plus the host dict entries; None when opt.ranges is unset
@@ -291,6 +301,11 @@ class GridHandle:
         release_deferred()
         self.gen += 1
         sp, base = grid_spec(opt) if policy == "reservoir" else (None, None)
+        if sp is not None and int(np.prod(np.asarray(list(sp.dims_max), np.int64))) > grid_dev_max_cells(opt):
+            # the device path sizes its tables for the whole ranges box (it does not know the
+            # bbox before the build): a room-scale box at a fine voxel size (ScanNet: +-10 m,
+            # 0.016 m cells ~ 2G cells ~ 27 GB) takes the host bbox path instead
+            sp = None
         if sp is not None and not getattr(opt, "grid_host_bbox", False):
             # no host sync: bbox -> get_hyperparameters -> build, all on the device
             L.check(L.lib().pnr_grid_build_dev(self.h, L.ptr(xyz), xyz.shape[0], L.ctypes.byref(sp),
@@ -331,9 +346,12 @@ class GridHandle:
 
     def stats(self):
         s = self._stats_raw()
+        cells = int(np.prod(np.asarray(list(s.dims), np.int64)))
         return dict(n_points_in_grid=s.n_points_in_grid, n_voxels=s.n_voxels,
                     n_voxels_kept=s.n_voxels_kept, n_points_dropped=s.n_points_dropped,
-                    max_points_per_voxel=s.max_points_per_voxel, dims=list(s.dims))
+                    max_points_per_voxel=s.max_points_per_voxel, dims=list(s.dims),
+                    table_cells=cells, table_bytes_est=int(cells * GRID_BYTES_PER_CELL),
+                    device_geometry=isinstance(self.hp, GridHP))
 
     def export(self):
         """Grid tables as torch tensors (parity tests / inspection)."""

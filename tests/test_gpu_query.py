@@ -229,3 +229,30 @@ def test_device_geometry_equals_host(cuda, case):
     _, oh = _run(sc, cuda, q_host)
     for a, b in zip(od[:5], oh[:5]):
         assert torch.equal(a, b)
+
+
+def test_device_grid_cell_budget_takes_host_path(cuda):
+    """the sync-free device build sizes its tables for the whole
+    opt.ranges box; a box over opt.grid_dev_max_cells builds on the host-read
+    bbox instead (tables of the cloud's extent) with the same tables and
+    query, and stats() reports the table size of each build."""
+    from types import SimpleNamespace
+    from pointnerf_amd.querier import lighting_fast_querier
+    sc = scene(20000, H=24, W=24, theta=70.0)
+    t = torch.from_numpy(sc["xyz"]).to(cuda)
+    q_dev = _engine(sc, cuda)
+    hp_d = q_dev.grid.build(sc["opt"], t)
+    st_d = q_dev.grid.stats()
+    assert type(hp_d).__name__ == "GridHP" and st_d["device_geometry"]
+    small = SimpleNamespace(**{**vars(sc["opt"]), "grid_dev_max_cells": 1000})
+    q_b = lighting_fast_querier(cuda, small)
+    hp_b = q_b.grid.build(small, t)
+    st_b = q_b.grid.stats()
+    assert isinstance(hp_b, dict) and type(hp_b).__name__ == "dict" and not st_b["device_geometry"]
+    assert st_b["table_cells"] == int(np.prod(hp_b["dims"].astype(np.int64))) <= st_d["table_cells"]
+    assert st_b["table_bytes_est"] > 0
+    for k in ("shift", "dims", "ranges"):
+        assert np.array_equal(np.asarray(hp_d[k]), np.asarray(hp_b[k])), k
+    td, tb = q_dev.grid.export(), q_b.grid.export()
+    for k in td:
+        assert torch.equal(td[k], tb[k]), k

@@ -56,6 +56,44 @@ def _worker(rank, world, port, q, mode="dup"):
         dist.destroy_process_group()
 
 
+def _worker_inf(rank, world, port, q):
+    """Row 0 of a rank's point gradient is inf but untouched; the -1 placeholders
+    gather it and must add exact zeros (not 0 * inf = NaN) on every rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pointnerf_amd.parallel import GradReducer
+        p = torch.nn.Parameter(torch.zeros(N, 4))
+        g = torch.zeros(N, 4)
+        g[0] = float("inf")
+        rows = torch.tensor([5 + rank, 9, -1])
+        g[rows[:2]] = torch.tensor([[1.0, 2.0, 3.0, 4.0]]) * (rank + 1)
+        p.grad = g
+        GradReducer([], [p]).reduce(rows, rows.numel())
+        assert torch.isfinite(p.grad).all(), "NaN / inf spread by the padding"
+        assert torch.equal(p.grad[0], torch.zeros(4))
+        assert torch.allclose(p.grad[9], torch.tensor([1.0, 2.0, 3.0, 4.0]) * sum(r + 1 for r in range(world)) / world)
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_reducer_padding_does_not_spread_inf():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_inf, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    assert all(v == "ok" for v in res.values()), res
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -17,20 +17,25 @@ def main():
     ap.add_argument("--hw", type=int, default=800)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--config", default="headline", choices=("headline", "c4", "c5"))
     a = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
-    ns = argparse.Namespace(points=a.points, config="headline", dtype=a.precision)
+    cfg = bench.CONFIGS[a.config]
+    pts_n = a.points if a.config == "headline" else cfg["points"]
+    H, W = (a.hw, a.hw) if a.config == "headline" else (cfg["H"], cfg["W"])
+    ns = argparse.Namespace(points=pts_n, config=a.config, dtype=a.precision)
     opt, pts, feats, agg, model = bench.build_scene(ns, dev)
     model.precision = a.precision
-    campos, camrot, rd = bench.cameras(1, a.hw, a.hw)[0]
+    campos, camrot, rd = bench.cameras(1, H, W, cfg["flags"])[0]
     cp, cr, rd = [torch.from_numpy(x).to(dev) for x in (campos, camrot, rd)]
     bg = torch.rand(128, device=dev)
-    model.render_rays(cp, cr, rd, 2.0, 6.0, bg)
+    near, far = opt.near_plane, opt.far_plane
+    model.render_rays(cp, cr, rd, near, far, bg)
     per = {}
     for _ in range(a.reps):
         ev = []
-        out = model.render_rays(cp, cr, rd, 2.0, 6.0, bg, events=ev)
+        out = model.render_rays(cp, cr, rd, near, far, bg, events=ev)
         torch.cuda.synchronize()
         for n, s, e in ev:
             per.setdefault(n, []).append(s.elapsed_time(e))
