@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check); "
                          "default 12000 (headline), 3000 (c4, c5)")
+    ap.add_argument("--no-query-stream", action="store_true",
+                    help="run every frame's query on the launch stream (default: on a second stream, where it "
+                         "overlaps the previous frame's aggregate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-line", action="store_true",
                     help="headline run: skip the finetune-step measurement appended to the line ('train')")
@@ -549,6 +552,9 @@ def main():
         return ci, rd, sh
 
     stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0, "cand": 0, "rays": 0}
+    # frame s + 1's query on its own stream, beside frame s's aggregate (render_rays(query_stream=));
+    # --grid-rebuild keeps everything on the launch stream
+    qstream = None if (args.no_query_stream or args.grid_rebuild) else torch.cuda.Stream(device)
 
     steps = {}
     # shader clock under load: one probe wave per timed step on a side stream,
@@ -578,14 +584,15 @@ def main():
 
     def issue(s, timed):
         # every render call of the step is issued without a host sync
-        # (render_rays(sync=False)); complete() holds the step's one sync
+        # (render_rays(sync=False)); complete() holds the step's one sync; the
+        # queries run on qstream (inputs were made before the timed region)
         parts = []
         ev_step = [] if timed else None
         if shard_world > 1 and not args.per_frame_calls:
             st, rd, cp, cr = step_batch(s)
             color = model.render_rays(cp, cr, rd, opt.near_plane, opt.far_plane, bg,
                                       force_grid=args.grid_rebuild, events=ev_step, sync=False,
-                                      ray_cam=st.ray_cam)[0]
+                                      ray_cam=st.ray_cam, query_stream=qstream)[0]
             parts.append((st, color, rd.shape[0]))
         else:
             for f in range(shard_world):
@@ -596,7 +603,7 @@ def main():
                 campos, camrot, _ = dev_cams[ci]
                 color = model.render_rays(campos, camrot, rd, opt.near_plane, opt.far_plane, bg,
                                           force_grid=(f == 0 and args.grid_rebuild),
-                                          events=ev_step, reuse_p1=f > 0, sync=False)[0]
+                                          events=ev_step, reuse_p1=f > 0, sync=False, query_stream=qstream)[0]
                 parts.append((sh, color, rd.shape[0]))
         if timed:
             clock_probe()
@@ -718,6 +725,7 @@ def main():
                                    + ("" if args.config == "headline" else f" (BASELINE config {args.config})"),
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "max_o": int(opt.max_o), "grid_rebuild_per_step": bool(args.grid_rebuild),
+                       "query_stream": qstream is not None,
                        "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else

@@ -255,7 +255,9 @@ typedef struct {
                            for these rows only -- the training-batch case            */
   int64_t n_used;
   const int32_t* used_map; /* [n] row -> index into used (-1 = unreferenced); required
-                              with used                                              */
+                              with used, except by pnr_aggregate_fwd_bf16: there used
+                              without used_map computes P1 for the used rows only but
+                              keeps the table indexed by point row ([n,256])         */
   int32_t p1_ready;     /* aggregate forward only: 1 = the scratch's first n_p1*256
                            values already hold block1.0's point half for these same
                            rows and weights (an earlier call on the same scratch with

@@ -190,12 +190,15 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
     for (int pt = 0; pt < kBPT; ++pt) {
       const int64_t row = tile * kBT + 32 * pt + c;
       if (row >= np) continue;
+      // used rows without used_map: the table stays indexed by point row (only the
+      // rows the frame references are computed; k_pairs_b reads P1[pid] directly)
+      const int64_t orow = A.pts.used && !A.pts.used_map ? (int64_t)A.pts.used[row] : row;
       // P1 rows in accumulator order: neuron tile T, lane half h -> 16 contiguous
       // bf16 (the tile's 16 registers), so k_pairs_b reloads them with 2 x 16-B loads
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
         const f32x16& v = acc[pt * 2 + T];
-        uint4* d = reinterpret_cast<uint4*>(A.p1 + row * kHid + 32 * (2 * wid + T) + 16 * h);
+        uint4* d = reinterpret_cast<uint4*>(A.p1 + orow * kHid + 32 * (2 * wid + T) + 16 * h);
         d[0] = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                           pack_bf16x2(v[6], v[7]));
         d[1] = make_uint4(pack_bf16x2(v[8], v[9]), pack_bf16x2(v[10], v[11]), pack_bf16x2(v[12], v[13]),
@@ -746,8 +749,11 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
                     ((uintptr_t)scratch & 15) == 0,
                 "aggregate_bf16: emb (16 B), emb_bf16 (8 B) and scratch (16 B) must be aligned");
   PNR_CHECK_ARG(pts->pers || (pts->campos && pts->camrot), "aggregate_bf16: need pers or camera");
-  PNR_CHECK_ARG(!pts->used || pts->used_map, "aggregate_bf16: used list needs used_map");
-  const int64_t n_p1 = pts->used ? pts->n_used : pts->n;
+  PNR_CHECK_ARG(!pts->used || (pts->n_used >= 0 && pts->n_used <= pts->n), "aggregate_bf16: bad n_used");
+  // P1 table rows: the used rows (compact, indexed through used_map) or every point
+  // row (also when used is given without used_map: only those rows are computed)
+  const int64_t n_p1 = pts->used && pts->used_map ? pts->n_used : pts->n;
+  const int64_t n_pre = pts->used ? pts->n_used : pts->n;   // rows k_point_pre_b computes (capacity)
   PNR_CHECK_ARG(scratch_bytes >= scratch_need_b(s->n_max, n_p1), "aggregate_bf16: scratch too small");
   if (s->n_max <= 0) return PNR_OK;
   hipStream_t st = as_stream(stream);
@@ -781,7 +787,7 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   if (!pts->p1_ready) {
-    hipLaunchKernelGGL(k_point_pre_b, dim3(grid_for(cdiv(n_p1, kBT), 1, 256 * 2)), dim3(64 * kBWaves),
+    hipLaunchKernelGGL(k_point_pre_b, dim3(grid_for(cdiv(n_pre, kBT), 1, 256 * 2)), dim3(64 * kBWaves),
                        kBT * kPB * 2, st, a);
     PNR_LAUNCH_CHECK();
   }

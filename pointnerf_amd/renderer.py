@@ -275,6 +275,7 @@ class NeuralPointsRayMarching(nn.Module):
         # MFMA, the measured default) / fp32x3 (split-bf16 MFMA) / fp32
         self.train_precision = "fp32h2"
         self.p1_side_stream = True        # fp32h2 sync-free calls: P1 beside the query (see _render_rays)
+        self.p1_used_only = True          # bf16: P1 for the referenced points only (see _render_rays)
         self.p1_side_max_points_per_ray = 4.0
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         # render_rays_train sizes its per-sample buffers for every slot of the batch while
@@ -320,7 +321,7 @@ class NeuralPointsRayMarching(nn.Module):
 
     @torch.no_grad()
     def render_rays(self, campos, camrot, raydir, near, far, bg_color, force_grid=False, events=None,
-                    reuse_p1=False, sync=True, ray_cam=None):
+                    reuse_p1=False, sync=True, ray_cam=None, query_stream=None):
         """Fused query -> aggregate -> composite for one ray batch [R,3].
         Returns ray_color [R,C], opacity [R,SR], is_bg [R], ray_mask [R] (int8).
         ``events``: optional list that receives (stage, start, end) HIP events
@@ -343,6 +344,14 @@ class NeuralPointsRayMarching(nn.Module):
         valid once ``finish()`` returned.  The first call (no estimate yet)
         runs synchronously.
 
+        ``query_stream`` (sync-free calls): run the call's query on this HIP
+        stream instead of the launch stream, so it overlaps the previous call's
+        aggregate (the query is memory-latency bound, the aggregate MFMA bound,
+        and one query workgroup fits beside a k_pairs_h2 workgroup on a CU).  The
+        aggregate waits for it; the query waits only for the launch-stream work
+        that last read its buffers (two sets, alternating).  The caller
+        guarantees the call's inputs (rays, cameras) are ready on that stream.
+
         fp32h2: the f16 split holds activations below 65504 only.  Each call
         reads the launches' range flag once (a 4-byte read after the last
         chunk); if an activation left the f16 range, the call is rendered again
@@ -358,7 +367,8 @@ class NeuralPointsRayMarching(nn.Module):
         prec = self._precision_now()
         if not sync and self._sv_per_ray is not None:
             out, rec = self._render_rays(prec, campos, camrot, raydir, near, far, bg_color, force_grid, events,
-                                         reuse_p1, self._state, capacity=self._capacity_per_ray(), ray_cam=ray_cam)
+                                         reuse_p1, self._state, capacity=self._capacity_per_ray(), ray_cam=ray_cam,
+                                         query_stream=query_stream)
             rec["args"] = (campos, camrot, raydir, near, far, bg_color, force_grid, reuse_p1, ray_cam)
             rec["out"] = out
             # what a re-render in finish() must find unchanged (weights, grid)
@@ -502,7 +512,7 @@ class NeuralPointsRayMarching(nn.Module):
         return counts
 
     def _render_rays(self, precision, campos, camrot, raydir, near, far, bg_color, force_grid, events, reuse_p1,
-                     state, capacity=None, keep=None, record=True, ray_cam=None):
+                     state, capacity=None, keep=None, record=True, ray_cam=None, query_stream=None):
         """One render call.  capacity None: size the feature buffer from this
         batch's counts (one host sync per chunk); else capacity = valid samples
         per ray the feature buffer is sized for (no sync; the per-chunk counts
@@ -598,10 +608,30 @@ class NeuralPointsRayMarching(nn.Module):
             r1 = min(R, r0 + chunk)
             rd = raydir[r0:r1].contiguous()
             rc = None if ray_cam is None else ray_cam[r0:r1]
-            e0 = mark()
-            bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=state.bufs, ray_cam=rc)
-            e1 = mark()
-            state.bufs = bufs
+            slot = None
+            if query_stream is not None and capacity is not None:
+                # the query on its own stream, two buffer sets in turn; each set is
+                # reused after the launch-stream work that read it (its event)
+                if getattr(state, "qring", None) is None:
+                    state.qring, state.qfree, state.qslot = [None, None], [None, None], 1
+                slot = state.qslot = state.qslot ^ 1
+                if state.qfree[slot] is not None:
+                    query_stream.wait_event(state.qfree[slot])
+                with torch.cuda.stream(query_stream):
+                    e0 = mark()
+                    bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far,
+                                               bufs=state.qring[slot], ray_cam=rc)
+                    e1 = mark()
+                    ev_q = torch.cuda.Event()
+                    ev_q.record(query_stream)
+                state.qring[slot] = bufs
+                torch.cuda.current_stream(dev).wait_event(ev_q)
+            else:
+                e0 = mark()
+                bufs, hp, rays, qp = q.run(np_.xyz.detach(), rd, campos, camrot, near, far, bufs=state.bufs,
+                                           ray_cam=rc)
+                e1 = mark()
+                state.bufs = bufs
             if capacity is None:
                 cnt = bufs.read_counts()
                 for k in totals:
@@ -616,7 +646,18 @@ class NeuralPointsRayMarching(nn.Module):
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K, L.ptr(rc))
             e2 = mark()
+            # bf16 (config c5: 20 M points, a frame references a fraction of them): block1.0's
+            # point half only for the points this batch's neighbour lists reference
+            # (pnr_used_points, device list and count), written at their own rows of the P1
+            # table (pnr_points.used without used_map) -- no indirection in the pairs kernel
+            used_only = (bf16 and self.p1_used_only and n_chunks == 1 and keep is None and not reuse_p1)
+            if used_only:
+                pts.used = L.ptr(self._used_points(state, bufs, K, pts.n))
+                pts.n_used, pts.used_map = pts.n, None
+                pts.n_used_dev = bufs.counts.data_ptr() + 5 * 4
             scratch, ready = self._agg_scratch(state, max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
+            if used_only:
+                ready, state.scratch_key = False, None   # the table holds this batch's rows only
             if p1_side is not None:   # P1 written into this same scratch by the side stream
                 torch.cuda.current_stream(dev).wait_event(p1_side)
                 ready = True
@@ -655,6 +696,10 @@ class NeuralPointsRayMarching(nn.Module):
                     rec["host"][ci].copy_(bufs.counts, non_blocking=True)
                 else:
                     rec["dcounts"][ci].copy_(bufs.counts)
+            if slot is not None:   # the launch stream's last reader of this query-buffer set
+                ev_free = torch.cuda.Event()
+                ev_free.record(torch.cuda.current_stream(dev))
+                state.qfree[slot] = ev_free
             if events is not None:
                 e4 = mark()
                 events += [("query", e0, e1), ("aggregate", e2, e3), ("composite", e3, e4)]
@@ -671,6 +716,26 @@ class NeuralPointsRayMarching(nn.Module):
         else:
             self.last_counts = totals
         return (ray_color, opacity, is_bg, ray_mask), rec
+
+    @staticmethod
+    def _used_points(state, bufs, K, n_points):
+        """pnr_used_points of a query (count into bufs.counts[5]) on buffers kept in
+        the render state: the device list of referenced point rows."""
+        dev = bufs.pidx.device
+        if getattr(state, "used_n", None) != n_points:
+            i32 = dict(dtype=torch.int32, device=dev)
+            nb = L.c_size_t(0)
+            L.check(L.lib().pnr_used_points_scratch_bytes(n_points, L.ctypes.byref(nb)),
+                    "pnr_used_points_scratch_bytes")
+            state.used_bufs = tuple(torch.empty(n_points, **i32) for _ in range(3)) + (
+                torch.empty(max(int(nb.value), 16), dtype=torch.uint8, device=dev),)
+            state.used_n = n_points
+        flags, used_map, used, scr = state.used_bufs
+        cap = bufs.pidx.numel() // K
+        L.check(L.lib().pnr_used_points(L.ptr(bufs.pidx), L.ptr(bufs.counts), K, cap, n_points, L.ptr(flags),
+                                        L.ptr(used_map), L.ptr(used), L.c_void_p(bufs.counts.data_ptr() + 20),
+                                        L.ptr(scr), scr.numel(), L.stream_ptr(dev)), "pnr_used_points")
+        return used
 
     def _agg_scratch(self, state, n_max, n_points, dev, bf16, reuse, precision="fp32"):
         """Persistent aggregate scratch (P1 lives at its start, see

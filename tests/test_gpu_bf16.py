@@ -138,3 +138,29 @@ def test_bf16_pair_buckets_equal_unbucketed(cuda, flags):
     need = ((pidx >= 0) * torch.arange(1, K + 1, device=cuda)).amax(1)
     if flags == "truck":
         assert int((need <= 1).sum()) > 100 and int(((need > 2) & (need <= 4)).sum()) > 100
+
+
+@pytest.mark.parametrize("flags", ["truck", "lego"])
+def test_bf16_p1_used_only_equals_all_points(cuda, flags):
+    """P1 (block1.0's point half) computed only for the points the batch
+    references (pnr_used_points; pnr_points.used without used_map: the table stays
+    indexed by point row) renders bitwise like P1 for every point; repeated
+    calls with other cameras never reuse the partial table."""
+    from pointnerf_amd.renderer import NeuralPointsRayMarching
+    from scenes import flag_scene
+    sc = flag_scene(flags, n_points=60000 if flags == "truck" else 30000, H=64, view=0)
+    sc2 = flag_scene(flags, n_points=60000 if flags == "truck" else 30000, H=64, view=1)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.6))
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="bf16")
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    outs = {}
+    for used_only in (False, True):
+        m.p1_used_only = used_only
+        for tag, s in (("a", sc), ("b", sc2), ("a2", sc)):
+            o = m.render_rays(torch.from_numpy(s["campos"]).to(cuda), torch.from_numpy(s["camrot"]).to(cuda),
+                              torch.from_numpy(s["raydir"]).to(cuda), s["near"], s["far"], bg)
+            outs[(used_only, tag)] = [t.clone() for t in o]
+    assert int(outs[(True, "a")][3].sum()) > 100
+    for tag in ("a", "b", "a2"):
+        for x, y in zip(outs[(False, tag)], outs[(True, tag)]):
+            assert torch.equal(x, y), tag

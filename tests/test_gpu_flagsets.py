@@ -213,15 +213,24 @@ def test_c2_lego_500k_800_properties_and_oracle_sample(cuda, precision):
 
 
 # ------------------------------------------------------------------------- c3
-def test_c3_ship_finetune_batch_grads_vs_oracle(cuda):
+@pytest.mark.parametrize("train_precision", ["fp32x3", "fp32h2"])
+def test_c3_ship_finetune_batch_grads_vs_oracle(cuda, train_precision):
     """c3: ship flags, ~2 M points, one finetune batch of 3 600 random rays of an
     800x800 frame (random_sample_size 60): forward + backward through the HIP
     kernels; ray colours and every point-table / MLP gradient vs torch autograd
-    of the CPU oracle (tolerances of test_gpu_backward.py)."""
+    of the CPU oracle (tolerances of test_gpu_backward.py).
+
+    fp32h2 (the training default) is held to a stated contract instead of the
+    strict bound: its per-layer error (~10x fp32 rounding) puts a few more
+    LeakyReLU pre-activations on the other side of 0 than fp32 does, and each
+    such kink flip changes one (pair, neuron) term by a factor 0.2 / 1.  Per
+    tensor: at most 0.1 % of the entries (>= 16) outside the strict fp32 bound,
+    none of them more than 2 % of the tensor's largest entry away from fp64."""
     from test_gpu_backward import close
     sc = flag_scene("ship", 2_000_000, H=800, view=3, default_conf=None)
     params = formula_params(salt=0.15)
     m = _model(sc, cuda, params, train=True)
+    m.train_precision = train_precision
     rng = np.random.default_rng(5)
     sel = np.sort(rng.choice(800 * 800, size=3600, replace=False))
     rdn = np.ascontiguousarray(sc["raydir"][sel])
@@ -283,17 +292,26 @@ def test_c3_ship_finetune_batch_grads_vs_oracle(cuda):
     # max|ref|-scaled term for LeakyReLU kinks (a pre-activation within fp32 noise of
     # 0 takes the other slope; 5e-5 point tables, 3e-4 MLP weights as in
     # test_gpu_backward.py).
-    errs = []
+    errs, contract = [], []
     for k, ref in g64.items():
         a = got[k].detach().cpu().double().numpy()
         r = ref.numpy()
         e32 = float(np.abs(g32[k].double().numpy() - r).max())
         kink = (5e-5 if k.startswith("points_") else 3e-4) * float(np.abs(r).max())
         bad = np.abs(a - r) > 4 * e32 + 1e-4 * np.abs(r) + kink
-        if bad.any():
+        if train_precision == "fp32h2":
+            ok = bad.sum() <= max(16, 1e-3 * bad.size) and np.abs(a - r).max() <= 2e-2 * np.abs(r).max()
+            contract.append((k, int(bad.sum()), bad.size, float(np.abs(a - r).max() / np.abs(r).max())))
+            if not ok:
+                errs.append(f"d {k}: {bad.sum()} / {bad.size} outside the fp32 bound, max |d| / max |ref| "
+                            f"{np.abs(a - r).max() / np.abs(r).max():.3e}")
+        elif bad.any():
             errs.append(f"d {k}: {bad.sum()} / {bad.size} outside, max |d| {np.abs(a - r).max():.3e} vs fp32-oracle "
                         f"error {e32:.3e}, max |ref| {np.abs(r).max():.3e}")
     untouched = torch.ones(npts.points_embeding.shape[1], dtype=torch.bool, device=cuda)
     untouched[u] = False
     assert float(npts.points_embeding.grad.reshape(-1, 32)[untouched].abs().max()) == 0.0
+    if contract:
+        print("fp32h2 gradient contract (tensor, entries outside the fp32 bound, size, max |d| / max |ref|):",
+              contract)
     assert not errs, errs

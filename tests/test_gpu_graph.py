@@ -73,6 +73,31 @@ def test_partial_finish_keeps_later_calls_queued(cuda, precision):
         assert _eq(w, g)
 
 
+@pytest.mark.parametrize("precision", ["fp32h2", "bf16"])
+def test_query_stream_equals_sync(cuda, precision):
+    """render_rays(sync=False, query_stream=s): each call's query on a second
+    stream (two buffer sets in turn, each reused after the launch-stream work
+    that read it) -- five queued calls over three cameras give the synchronous
+    renders bitwise, and an overflowing call is still re-rendered in place."""
+    sc, cams = _cams(cuda, thetas=(30.0, 200.0, 120.0))
+    m = _renderer(sc, cuda, formula_params(salt=0.4))
+    m.precision = precision
+    bg = torch.from_numpy(sc["bg"]).to(cuda)
+    want = [[t.clone() for t in m.render_rays(cp, cr, rd, 2.0, 6.0, bg)] for cp, cr, rd in cams]
+    qs = torch.cuda.Stream(cuda)
+    torch.cuda.synchronize()
+    order = [0, 1, 2, 0, 1]
+    got = [m.render_rays(*cams[i], 2.0, 6.0, bg, sync=False, query_stream=qs) for i in order]
+    m.finish()
+    for i, g in zip(order, got):
+        assert _eq(want[i], g)
+    m._sv_per_ray = 0.01   # the next call overflows its feature buffer
+    r0 = m.overflow_rerenders
+    g = m.render_rays(*cams[2], 2.0, 6.0, bg, sync=False, query_stream=qs)
+    m.finish()
+    assert m.overflow_rerenders == r0 + 1 and _eq(want[2], g)
+
+
 def test_side_stream_p1_equals_sync(cuda):
     """fp32h2 sync-free calls run P1 (pnr_point_pre_h2) on a side stream beside
     the query and the aggregate waits on it: renders bitwise equal to the

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--config", default="headline", choices=("headline", "c4", "c5"))
+    ap.add_argument("--p1-all", action="store_true", help="bf16: P1 for every point (not only the referenced)")
     a = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
@@ -27,6 +28,7 @@ def main():
     ns = argparse.Namespace(points=pts_n, config=a.config, dtype=a.precision)
     opt, pts, feats, agg, model = bench.build_scene(ns, dev)
     model.precision = a.precision
+    model.p1_used_only = not a.p1_all
     campos, camrot, rd = bench.cameras(1, H, W, cfg["flags"])[0]
     cp, cr, rd = [torch.from_numpy(x).to(dev) for x in (campos, camrot, rd)]
     bg = torch.rand(128, device=dev)
