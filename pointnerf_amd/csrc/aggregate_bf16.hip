@@ -31,8 +31,7 @@ constexpr int kBPT = kBT / 32;           // 32-column quarters per tile
 constexpr int kBWaves = 4;
 constexpr int kPB = 280;                 // Xb pitch (bf16) for <= 272 input rows (k_pairs_b, k_point_pre_b)
 constexpr int kPBc = 296;                // Xb pitch for the colour branch (288 input rows)
-constexpr int kBPad = 2;                 // zero k-steps padded onto bf16 weight packs (prefetch)
-static_assert(kBPad >= 2, "mlp_layer_b loads weights two k-steps ahead");
+constexpr int kBPad = 4;                 // zero k-steps padded onto bf16 weight packs (the ring's lead)
 
 struct AggArgsB {
   pnr_points pts;
@@ -41,6 +40,7 @@ struct AggArgsB {
   uint16_t* p1;      // [n_p1, 256] bf16 per-point block1.0 partial, accumulator order
   uint16_t* hid;     // [n_max, 256] bf16 K-summed features
   int32_t* vmask;    // [n_max]
+  float4* vdir;      // [n_max] rotated view direction of each sample (k_pairs_b -> k_color_b's PE)
   float* out_feat;
   float* out_weight;
   float* out_conf;
@@ -55,41 +55,101 @@ __device__ __forceinline__ float bf16_hi(unsigned u) { return __builtin_bit_cast
 __device__ __forceinline__ uint16_t to_bf16(float a) { return __builtin_bit_cast(uint16_t, (__bf16)a); }
 
 // Y^T += W . X^T on bf16 MFMA: NT output tiles x PT 32-column quarters over
-// nsteps k-steps of 16.  Weight fragments 2 steps ahead, B fragments 1 step.
-template <int NT, int PT, int NTOT, int PITCH>
-__device__ __forceinline__ void mlp_layer_b(f32x16 (&acc)[PT * NT], const uint4* __restrict__ wf,
+// nsteps k-steps of 16.  Weight fragments WD steps ahead in a register ring
+// (raw buffer loads; the packs carry kBPad >= WD zero steps), B fragments one
+// step ahead from LDS.  sched_barrier(0) pins the order: without it hipcc sank
+// each weight load next to its MFMAs and waited vmcnt(0) on it every k-step
+// (k_color_b then ran at 0.14 MFMA busy).
+template <int NT, int PT, int NTOT, int PITCH, int WD>
+__device__ __forceinline__ void mlp_layer_ring(f32x16 (&acc)[PT * NT], const uint4* __restrict__ wf,
                                             const uint16_t* Xb, int nsteps, int lane) {
+  static_assert(WD <= kBPad, "the packs' zero steps cover the ring's lead");
   const int c = lane & 31, h = lane >> 5;
-  const uint4* p = wf + lane;
-  uint4 a0[NT], a1[NT];
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wf), 0, 0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  uint4 w[WD][NT];
+  auto ldw = [&](uint4 (&a)[NT], int t) {
 #pragma unroll
-  for (int T = 0; T < NT; ++T) {
-    a0[T] = p[(0 * NTOT + T) * 64];
-    a1[T] = p[(1 * NTOT + T) * 64];
-  }
+    for (int T = 0; T < NT; ++T)
+      a[T] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (t * NTOT + T) * 1024, 0));
+  };
+#pragma unroll
+  for (int d = 0; d < WD; ++d) ldw(w[d], d);
   const uint16_t* xr = Xb + c * PITCH + 8 * h;
-  uint4 x[PT];
+  uint4 x[2][PT];
 #pragma unroll
-  for (int pt = 0; pt < PT; ++pt) x[pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH);
-#pragma unroll 1
-  for (int t = 0; t < nsteps; ++t) {
-    uint4 y[PT];
+  for (int pt = 0; pt < PT; ++pt) x[0][pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH);
+  auto step = [&](int t, int d, int xs) {
     const int tn = t + 1 < nsteps ? t + 1 : t;
 #pragma unroll
-    for (int pt = 0; pt < PT; ++pt) y[pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH + 16 * tn);
+    for (int pt = 0; pt < PT; ++pt) x[xs ^ 1][pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH + 16 * tn);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
       for (int T = 0; T < NT; ++T)
         acc[pt * NT + T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            __builtin_bit_cast(bf16x8, a0[T]), __builtin_bit_cast(bf16x8, x[pt]), acc[pt * NT + T], 0, 0, 0);
+            __builtin_bit_cast(bf16x8, w[d][T]), __builtin_bit_cast(bf16x8, x[xs][pt]), acc[pt * NT + T], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    ldw(w[d], t + WD);   // zero padding past the last step
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // unrolled by U = lcm(WD, 2): ring slot and B slot compile-time
+  constexpr int U = WD % 2 ? 2 * WD : WD;
+  int t = 0;
+#pragma unroll 1
+  for (; t + U <= nsteps; t += U) {
+#pragma unroll
+    for (int d = 0; d < U; ++d) step(t + d, d % WD, d & 1);
+  }
+#pragma unroll
+  for (int d = 0; d < U - 1; ++d)
+    if (t + d < nsteps) step(t + d, d % WD, d & 1);
+}
+
+// WD = 0: compiler-scheduled (it loads each step's weights where they are used):
+// the k_pairs_b tiles whose registers have no room for a ring (measured faster)
+template <int NT, int PT, int NTOT, int PITCH, int WD = 2>
+__device__ __forceinline__ void mlp_layer_b(f32x16 (&acc)[PT * NT], const uint4* __restrict__ wf,
+                                            const uint16_t* Xb, int nsteps, int lane) {
+  if constexpr (WD > 0) {
+    mlp_layer_ring<NT, PT, NTOT, PITCH, WD>(acc, wf, Xb, nsteps, lane);
+  } else {
+    // the round-4 loop (a0 / a1 and x / y one step ahead as written; hipcc
+    // schedules the loads itself)
+    const int c = lane & 31, h = lane >> 5;
+    const uint4* p = wf + lane;
+    uint4 a0[NT], a1[NT];
 #pragma unroll
     for (int T = 0; T < NT; ++T) {
-      a0[T] = a1[T];
-      a1[T] = p[((t + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
+      a0[T] = p[(0 * NTOT + T) * 64];
+      a1[T] = p[(1 * NTOT + T) * 64];
     }
+    const uint16_t* xr = Xb + c * PITCH + 8 * h;
+    uint4 x[PT];
 #pragma unroll
-    for (int pt = 0; pt < PT; ++pt) x[pt] = y[pt];
+    for (int pt = 0; pt < PT; ++pt) x[pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH);
+#pragma unroll 1
+    for (int t = 0; t < nsteps; ++t) {
+      uint4 y[PT];
+      const int tn = t + 1 < nsteps ? t + 1 : t;
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) y[pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH + 16 * tn);
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+        for (int T = 0; T < NT; ++T)
+          acc[pt * NT + T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              __builtin_bit_cast(bf16x8, a0[T]), __builtin_bit_cast(bf16x8, x[pt]), acc[pt * NT + T], 0, 0, 0);
+#pragma unroll
+      for (int T = 0; T < NT; ++T) {
+        a0[T] = a1[T];
+        a1[T] = p[((t + 2) * NTOT + T) * 64];   // packs carry kBPad zero steps
+      }
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) x[pt] = y[pt];
+    }
   }
 }
 
@@ -222,6 +282,11 @@ constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
 constexpr int kHP = kHid + 8;  // bf16 pitch of the staged hid rows (16-B aligned rows)
 static_assert(kBTSmax * kHP <= kBT * kPB, "staged hid rows must fit Xb");
 constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT + kBTSmax) * 4;
+
+// weight-ring depth of k_pairs_b's layers per tile shape (measured at c5: the
+// one-slot tiles gain from a one-step lead, the others spill with it)
+template <int KT>
+constexpr int kPairsWD = KT == 1 ? 1 : 0;
 
 template <int KT>
 __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const int32_t* bk_list, const int32_t* bk_info,
@@ -356,6 +421,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         if (k == 0) {
           sflag[j] = active && samp_valid;
           vL[j] = (int)v;   // the list entry, read once here (not per store below)
+          // the colour branch's view PE input (k_color_b reads it with the hid row
+          // instead of walking sample row -> dir map -> ray dir again)
+          if (active) A.vdir[v] = make_float4(vrot[0], vrot[1], vrot[2], 0.f);
         }
         if (active && k < K) {
           // the bucket's dropped slots (KT..K-1) are empty: weight 0, their gathered conf
@@ -421,7 +489,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     }
     nx_v = pf_v(tile + gridDim.x);   // the next tile's chain, link 1
     // -------------------------------------------- block1: + W1[:, 224:284] . PE_5 (4 steps), block1.2
-    mlp_layer_b<2, kBPT, 8, kPB>(acc, w1b, Xb, 4, lane);
+    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w1b, Xb, 4, lane);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {
@@ -433,7 +501,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     nx_row = pf_row(nx_v);   // link 2
-    mlp_layer_b<2, kBPT, 8, kPB>(acc, w2, Xb, 17, lane);
+    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w2, Xb, 17, lane);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263 (+ zeros to 271)
@@ -451,7 +519,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     nx_pid = pf_pid(nx_row);   // link 3
-    mlp_layer_b<2, kBPT, 8, kPB>(acc, w3, Xb, 17, lane);
+    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w3, Xb, 17, lane);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {
@@ -462,7 +530,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_b<2, kBPT, 8, kPB>(acc, w4, Xb, 17, lane);
+    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w4, Xb, 17, lane);
     __syncthreads();   // Xb is free: the K-sums are staged there (hid rows, kHP pitch)
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
     {
@@ -605,9 +673,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
   const int64_t n = eff_n(A.s);
   const int64_t ntiles = cdiv(n, kBT);
   const float neg = A.w.neg_slope;
-  float Rw[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rw[i] = A.w.rw2c ? A.w.rw2c[i] : (i % 4 == 0 ? 1.f : 0.f);
   const uint4* w1 = reinterpret_cast<const uint4*>(A.w.wc1f) + wid * 64;
   const uint4* w2 = reinterpret_cast<const uint4*>(A.w.wc2f) + wid * 64;
   const uint4* w3 = reinterpret_cast<const uint4*>(A.w.wc3f) + wid * 64;
@@ -616,19 +681,29 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
   // during this tile's three layers (a chain of 16 dependent load rounds per tile
   // otherwise: the kernel waited on HBM latency, not on HBM bandwidth)
   constexpr int kHidChunks = kBT * (kHid / 8) / (64 * kBWaves);
-  uint4 hu[kHidChunks];
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  u32x4v hu[kHidChunks];
+  float4 vdn = make_float4(0.f, 0.f, 0.f, 0.f);   // the loaded tile's view direction (threads < kBT)
   uint64_t vm0 = 0, vm1 = 0;   // the loaded tile's vmask bits
+  // Every load unconditional, from a clamped (valid) row: a load under a branch
+  // made hipcc drain vmcnt(0) after it, which serialised the whole prefetch.
+  // Masked samples' hid rows are loaded as they are (stale); only their own
+  // columns see them and their outputs are never stored.
   auto load_hid = [&](int64_t t) {
     const int64_t b = t * kBT;
-    vm0 = __ballot(t < ntiles && b + lane < n && A.vmask[b + lane] != 0);
-    vm1 = __ballot(t < ntiles && b + 64 + lane < n && A.vmask[b + 64 + lane] != 0);
+    const int64_t r0 = b + lane < n ? b + lane : 0, r1 = b + 64 + lane < n ? b + 64 + lane : 0;
+    const int64_t rv = b + (threadIdx.x & (kBT - 1)) < n ? b + (threadIdx.x & (kBT - 1)) : 0;
+    const int32_t m0 = A.vmask[r0], m1 = A.vmask[r1];
+    vdn = A.vdir[rv];
 #pragma unroll
     for (int k = 0; k < kHidChunks; ++k) {
       const int i = threadIdx.x + 64 * kBWaves * k;
       const int col = i >> 5, q = i & 31;
-      const bool ok = ((col < 64 ? vm0 : vm1) >> (col & 63)) & 1;
-      hu[k] = ok ? reinterpret_cast<const uint4*>(A.hid + (b + col) * kHid)[q] : make_uint4(0, 0, 0, 0);
+      const int64_t r = b + col < n ? b + col : 0;
+      hu[k] = reinterpret_cast<const u32x4v*>(A.hid + r * kHid)[q];
     }
+    vm0 = __ballot(b + lane < n && m0 != 0);
+    vm1 = __ballot(b + 64 + lane < n && m1 != 0);
   };
   load_hid(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -636,37 +711,27 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
 #pragma unroll
     for (int k = 0; k < kHidChunks; ++k) {
       const int i = threadIdx.x + 64 * kBWaves * k;
-      *reinterpret_cast<uint4*>(Xb + (i >> 5) * kPBc + 8 * (i & 31)) = hu[k];
+      *reinterpret_cast<u32x4v*>(Xb + (i >> 5) * kPBc + 8 * (i & 31)) = hu[k];
     }
     const uint64_t tm0 = vm0, tm1 = vm1;
+    const float4 vdc = vdn;
     load_hid(tile + gridDim.x);
     // view PE (ori dropped): rows 256 + 4ch + f = sin, 268 + 4ch + f = cos, bias 280, zeros to 287
     if (threadIdx.x < kBT) {
       const int col = threadIdx.x;
-      const int64_t v = v0 + col;
-      float vrot[3] = {0.f, 0.f, 0.f};
-      if (v < n) {
-        const int64_t row = sample_row(A.s, v);
-        const int64_t drow = dir_row(A.s, row);
-        const float vd[3] = {A.s.dirs[drow * 3], A.s.dirs[drow * 3 + 1], A.s.dirs[drow * 3 + 2]};
-        mat3(Rw, vd, vrot);
-        if (A.pts.rw2c) rot_point(A.pts.rw2c, slot0_point(A.s, row), vd, vrot);
+      // the rotated view direction k_pairs_b wrote for the sample (masked samples: 0)
+      const bool valid = ((col < 64 ? tm0 : tm1) >> (col & 63)) & 1;
+      const float vrot[3] = {valid ? vdc.x : 0.f, valid ? vdc.y : 0.f, valid ? vdc.z : 0.f};
+      uint16_t* xc = Xb + col * kPBc;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {   // rows 256 + 4 ch + f (sin), 268 + 4 ch + f (cos)
+        float sn[4], cs[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) sincosf(vrot[ch] * (float)(1 << f), &sn[f], &cs[f]);
+        *reinterpret_cast<uint2*>(xc + 256 + 4 * ch) = make_uint2(pack_bf16x2(sn[0], sn[1]), pack_bf16x2(sn[2], sn[3]));
+        *reinterpret_cast<uint2*>(xc + 268 + 4 * ch) = make_uint2(pack_bf16x2(cs[0], cs[1]), pack_bf16x2(cs[2], cs[3]));
       }
-      float pe[32];
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch)
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          float sn, cs;
-          sincosf(vrot[ch] * (float)(1 << f), &sn, &cs);
-          pe[4 * ch + f] = sn;
-          pe[12 + 4 * ch + f] = cs;
-        }
-      pe[24] = 1.f;
-#pragma unroll
-      for (int i = 25; i < 32; ++i) pe[i] = 0.f;
-      tail_rows_b(Xb, kPBc, col, 256, pe, 16);
-      tail_rows_b(Xb, kPBc, col, 272, pe + 16, 16);
+      *reinterpret_cast<uint4*>(xc + 280) = make_uint4(pack_bf16x2(1.f, 0.f), 0u, 0u, 0u);   // bias row, zeros to 287
     }
     __syncthreads();
     f32x16 acc[kBPT];
@@ -708,11 +773,17 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
         for (int i = 0; i < 4; ++i)
           Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
     __syncthreads();
-    for (int r = wid; r < kBT; r += kBWaves) {
+    // two rows per store instruction (lane half = row, 16 B per lane; the rows
+    // are 516 B apart, so the stores are only 4-B aligned): 16 store instructions
+    // per wave and tile instead of 64, so the next tile's wait for its prefetched
+    // hid rows (older in vmcnt order) need not wait for these stores' completion
+    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+    for (int r2 = wid; r2 < kBT / 2; r2 += kBWaves) {
+      const int r = 2 * r2 + (lane >> 5), l = lane & 31;
       if (!(((r < 64 ? tm0 : tm1) >> (r & 63)) & 1)) continue;
-      float* o = A.out_feat + (v0 + r) * (kC + 1) + 1;
-      o[lane] = Ob[r * kOPitch + lane];
-      o[64 + lane] = Ob[r * kOPitch + 64 + lane];
+      const float* src = Ob + r * kOPitch + 4 * l;
+      const f4u v = {src[0], src[1], src[2], src[3]};
+      *reinterpret_cast<f4u*>(A.out_feat + (v0 + r) * (kC + 1) + 1 + 4 * l) = v;
     }
     __syncthreads();
   }
@@ -721,8 +792,8 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
 static size_t scratch_need_b(int64_t n_max, int64_t n_p1) {
   const int64_t nm = n_max > 0 ? n_max : 1;
   const int64_t np = n_p1 > 0 ? n_p1 : 1;
-  // P1 | hid | vmask | pair buckets (buckets.hip)
-  return (size_t)nm * kHid * 2 + (size_t)cdiv(nm, 4) * 16 + (size_t)np * kHid * 2 +
+  // P1 | hid | vmask | vdir | pair buckets (buckets.hip)
+  return (size_t)nm * kHid * 2 + (size_t)cdiv(nm, 4) * 16 + (size_t)nm * 16 + (size_t)np * kHid * 2 +
          (size_t)bucket_scratch_ints(nm) * 4;
 }
 
@@ -782,7 +853,8 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   a.p1 = static_cast<uint16_t*>(scratch);
   a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
   a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
-  int32_t* bk_scratch = a.vmask + cdiv(nm, 4) * 4;
+  a.vdir = reinterpret_cast<float4*>(a.vmask + cdiv(nm, 4) * 4);
+  int32_t* bk_scratch = reinterpret_cast<int32_t*>(a.vdir + nm);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
