@@ -20,6 +20,7 @@ shading-slot) entry of the dense H*W*SR grid the reference materialises
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -79,6 +80,9 @@ def parse():
     ap.add_argument("--no-query-stream", action="store_true",
                     help="run every frame's query on the launch stream (default: on a second stream, where it "
                          "overlaps the previous frame's aggregate)")
+    ap.add_argument("--launch-priority", choices=("default", "high"), default="default",
+                    help="high: the frames' launch stream (aggregate, composite) is a high-priority stream, so "
+                         "the workgroup dispatcher prefers it over the query stream beside it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-line", action="store_true",
                     help="headline run: skip the finetune-step measurement appended to the line ('train')")
@@ -555,6 +559,10 @@ def main():
     # frame s + 1's query on its own stream, beside frame s's aggregate (render_rays(query_stream=));
     # --grid-rebuild keeps everything on the launch stream
     qstream = None if (args.no_query_stream or args.grid_rebuild) else torch.cuda.Stream(device)
+    lstream = None
+    if args.launch_priority == "high":
+        lstream = torch.cuda.Stream(device, priority=torch.cuda.Stream.priority_range()[1])
+        lstream.wait_stream(torch.cuda.current_stream(device))
 
     steps = {}
     # shader clock under load: one probe wave per timed step on a side stream,
@@ -647,24 +655,25 @@ def main():
     def step(s, timed):
         return complete(issue(s, timed))
 
-    for s in range(args.warmup):
-        finish(step(s, False))
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    rerenders0 = model.overflow_rerenders
-    t0 = time.perf_counter()
-    prev = []
-    pend = issue(args.warmup, True)
-    for s in range(1, args.steps + 1):
-        nxt = issue(args.warmup + s, True) if s < args.steps else None   # queued before step s-1's sync
-        cur = complete(pend)
-        finish(prev)   # step s-2's all-gather travelled over xGMI while steps s-1 and s rendered
-        prev, pend = cur, nxt
-    finish(prev)       # the last step's frames are gathered inside the timed region
-    torch.cuda.synchronize()
-    t_local = time.perf_counter() - t0
+    with (torch.cuda.stream(lstream) if lstream is not None else contextlib.nullcontext()):
+        for s in range(args.warmup):
+            finish(step(s, False))
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        rerenders0 = model.overflow_rerenders
+        t0 = time.perf_counter()
+        prev = []
+        pend = issue(args.warmup, True)
+        for s in range(1, args.steps + 1):
+            nxt = issue(args.warmup + s, True) if s < args.steps else None   # queued before step s-1's sync
+            cur = complete(pend)
+            finish(prev)   # step s-2's all-gather travelled over xGMI while steps s-1 and s rendered
+            prev, pend = cur, nxt
+        finish(prev)       # the last step's frames are gathered inside the timed region
+        torch.cuda.synchronize()
+        t_local = time.perf_counter() - t0
     if dist:
         dist.barrier()
         tt = torch.tensor([t_local], device=device, dtype=torch.float64)
@@ -726,6 +735,7 @@ def main():
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "max_o": int(opt.max_o), "grid_rebuild_per_step": bool(args.grid_rebuild),
                        "query_stream": qstream is not None,
+                       "launch_priority": args.launch_priority,
                        "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else
