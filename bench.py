@@ -20,7 +20,6 @@ shading-slot) entry of the dense H*W*SR grid the reference materialises
 from __future__ import annotations
 
 import argparse
-import contextlib
 import json
 import os
 import sys
@@ -77,12 +76,12 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="rays in the CPU-baseline sample (also the rays of the PSNR-vs-oracle check); "
                          "default 12000 (headline), 3000 (c4, c5)")
-    ap.add_argument("--no-query-stream", action="store_true",
-                    help="run every frame's query on the launch stream (default: on a second stream, where it "
-                         "overlaps the previous frame's aggregate)")
-    ap.add_argument("--launch-priority", choices=("default", "high"), default="default",
-                    help="high: the frames' launch stream (aggregate, composite) is a high-priority stream, so "
-                         "the workgroup dispatcher prefers it over the query stream beside it")
+    ap.add_argument("--query-stream", choices=("auto", "on", "off"), default="auto",
+                    help="on: every frame's query on a second stream, where it overlaps the previous frame's "
+                         "aggregate; off: on the launch stream; auto (default): on for the headline, off for c4/c5, "
+                         "where the 15-ms KNN beside the bucketed aggregate holds CU slots its small kernels wait "
+                         "for (DESIGN.md section 14: c5 879 vs 960 Mray-samples/s)")
+    ap.add_argument("--no-query-stream", action="store_true", help="same as --query-stream off")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-line", action="store_true",
                     help="headline run: skip the finetune-step measurement appended to the line ('train')")
@@ -558,11 +557,8 @@ def main():
     stage = {"flops": 0.0, "pairs": 0, "valid": 0, "filled": 0, "cand": 0, "rays": 0}
     # frame s + 1's query on its own stream, beside frame s's aggregate (render_rays(query_stream=));
     # --grid-rebuild keeps everything on the launch stream
-    qstream = None if (args.no_query_stream or args.grid_rebuild) else torch.cuda.Stream(device)
-    lstream = None
-    if args.launch_priority == "high":
-        lstream = torch.cuda.Stream(device, priority=torch.cuda.Stream.priority_range()[1])
-        lstream.wait_stream(torch.cuda.current_stream(device))
+    use_qs = {"on": True, "off": False, "auto": args.config == "headline"}[args.query_stream]
+    qstream = None if (args.no_query_stream or args.grid_rebuild or not use_qs) else torch.cuda.Stream(device)
 
     steps = {}
     # shader clock under load: one probe wave per timed step on a side stream,
@@ -655,25 +651,24 @@ def main():
     def step(s, timed):
         return complete(issue(s, timed))
 
-    with (torch.cuda.stream(lstream) if lstream is not None else contextlib.nullcontext()):
-        for s in range(args.warmup):
-            finish(step(s, False))
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        rerenders0 = model.overflow_rerenders
-        t0 = time.perf_counter()
-        prev = []
-        pend = issue(args.warmup, True)
-        for s in range(1, args.steps + 1):
-            nxt = issue(args.warmup + s, True) if s < args.steps else None   # queued before step s-1's sync
-            cur = complete(pend)
-            finish(prev)   # step s-2's all-gather travelled over xGMI while steps s-1 and s rendered
-            prev, pend = cur, nxt
-        finish(prev)       # the last step's frames are gathered inside the timed region
-        torch.cuda.synchronize()
-        t_local = time.perf_counter() - t0
+    for s in range(args.warmup):
+        finish(step(s, False))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    rerenders0 = model.overflow_rerenders
+    t0 = time.perf_counter()
+    prev = []
+    pend = issue(args.warmup, True)
+    for s in range(1, args.steps + 1):
+        nxt = issue(args.warmup + s, True) if s < args.steps else None   # queued before step s-1's sync
+        cur = complete(pend)
+        finish(prev)   # step s-2's all-gather travelled over xGMI while steps s-1 and s rendered
+        prev, pend = cur, nxt
+    finish(prev)       # the last step's frames are gathered inside the timed region
+    torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0
     if dist:
         dist.barrier()
         tt = torch.tensor([t_local], device=device, dtype=torch.float64)
@@ -735,7 +730,6 @@ def main():
                        "points": args.points, "H": H, "W": W, "K": opt.K, "SR": SR, "P": opt.P,
                        "max_o": int(opt.max_o), "grid_rebuild_per_step": bool(args.grid_rebuild),
                        "query_stream": qstream is not None,
-                       "launch_priority": args.launch_priority,
                        "point_table_bytes_per_point": model.neural_points.bytes_per_point(),
                        "parallelism": (f"dp{world} (whole-frame ray batches, async RCCL all_gather of the "
                                        f"step's frames)" if args.shard == "frames" else

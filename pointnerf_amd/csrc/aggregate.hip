@@ -858,7 +858,10 @@ struct BwdArgs {
 };
 
 constexpr int kBwdLdsFloats = 66 * kQP + 4 * kTP /*dot parts*/ + 4 * 7 * kTP /*extras parts*/;
-constexpr size_t kBwdLdsBytes = (size_t)kBwdLdsFloats * sizeof(float);
+#ifndef PNR_BWD_LDS_PAD   // experiment builds (tools/extras_variant.sh): extra LDS per workgroup
+#define PNR_BWD_LDS_PAD 0
+#endif
+constexpr size_t kBwdLdsBytes = (size_t)kBwdLdsFloats * sizeof(float) + PNR_BWD_LDS_PAD;
 
 // max |v| over a wave's lanes into an LDS slot (float bits compared as unsigned:
 // a NaN's bits exceed every finite and infinite value, so it propagates).
@@ -1058,6 +1061,17 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_
     if (t + d < nsteps) step(w.a[d], t + d);
 }
 
+// PNR_X3_EXTRAS_IN_KERNEL (experiment builds only, tools/extras_variant.sh): the
+// x3 variant computes the block3.0 extras from the LDS dz3 rows as the fp32 one
+// does (co-residency defect), instead of k_extras_bwd
+#ifndef PNR_X3_EXTRAS_IN_KERNEL
+#define PNR_X3_EXTRAS_IN_KERNEL 0
+#endif
+constexpr bool kX3ExIn = PNR_X3_EXTRAS_IN_KERNEL != 0;
+#if defined(PNR_EXP_CHECK)
+__device__ unsigned g_exp_check = 0;
+#endif
+
 template <bool X3>
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
@@ -1167,7 +1181,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
     // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
     wave_sync();
-    if constexpr (!X3) {
+    if constexpr (!X3 || kX3ExIn) {
       float ex[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
@@ -1187,16 +1201,33 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // colour / dir gradients of the pair (wave 0, lane = pair), before the
     // block3.0^T GEMM: its registers stay free for the GEMM.  The pair's
     // indices are recomputed here rather than kept live across the GEMMs.
-    if (!X3 && wid == 0 && tile * kTS + (lane >> 3) < n) {
+    if ((!X3 || kX3ExIn) && wid == 0 && tile * kTS + (lane >> 3) < n) {
       const int64_t pair = tile * kTP + lane;
       const int64_t v = tile * kTS + (lane >> 3);
       const int32_t pr = A.sv.prow[pair];
       if (pr >= 0) {
         float g[7];
+#if defined(PNR_EXP_OPAQUE) || defined(PNR_EXP_CHECK)
+        // experiment: the partials' LDS addresses recomputed here from an opaque
+        // lane id (not hoisted to the prologue, so never spilled)
+        int ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+#else
+        const int ln = lane;
+#endif
+#if defined(PNR_EXP_CHECK)
+        // experiment: count the reloaded (hoisted, spilled) addresses that differ
+        // from the recomputed ones
 #pragma unroll
         for (int e = 0; e < 7; ++e)
-          g[e] = exP[(0 * 7 + e) * kTP + lane] + exP[(1 * 7 + e) * kTP + lane] + exP[(2 * 7 + e) * kTP + lane] +
-                 exP[(3 * 7 + e) * kTP + lane];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (&exP[(i * 7 + e) * kTP + lane] != &exP[(i * 7 + e) * kTP + ln]) atomicAdd(&g_exp_check, 1u);
+#endif
+#pragma unroll
+        for (int e = 0; e < 7; ++e)
+          g[e] = exP[(0 * 7 + e) * kTP + ln] + exP[(1 * 7 + e) * kTP + ln] + exP[(2 * 7 + e) * kTP + ln] +
+                 exP[(3 * 7 + e) * kTP + ln];
         if (A.d_color) {
 #pragma unroll
           for (int a = 0; a < 3; ++a) atomicAdd(A.d_color + (int64_t)pr * 3 + a, g[a]);
@@ -2088,7 +2119,7 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
     PNR_LAUNCH_CHECK();
     // wb->w3e == NULL: the caller runs the extras per point inside
     // pnr_pairs_to_points_ex (no float atomics, coalesced dz3 rows)
-    if ((d_color || d_dir) && wb->w3e)
+    if ((d_color || d_dir) && wb->w3e && !kX3ExIn)
       hipLaunchKernelGGL(k_extras_bwd, dim3(grid_for(cdiv(s->n_max * kKN, 64), 4, 2048)), dim3(256), 0, st, a);
   } else
     hipLaunchKernelGGL(k_pairs_bwd<false>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
@@ -2249,6 +2280,13 @@ extern "C" int pnr_aggregate_bwd_xyz(const pnr_points* pts, const pnr_samples* s
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
+
+#if defined(PNR_EXP_CHECK)
+extern "C" __attribute__((visibility("default"))) int pnr_exp_check_count(unsigned* out) {
+  PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_check), sizeof(unsigned)));
+  return PNR_OK;
+}
+#endif
 
 extern "C" int pnr_used_points_scratch_bytes(int64_t n_points, size_t* out) {
   PNR_CHECK_ARG(out && n_points >= 0, "used_points_scratch_bytes: bad args");

@@ -36,6 +36,12 @@ import torch
 from . import _lib as L
 from .aggregator import frag_pack, frag_pack_x3
 
+# x3 backward: the block3.0 extras' colour / dir gradients per point inside
+# pnr_pairs_to_points_ex (True, the product).  False hands them to
+# pnr_aggregate_bwd_pairs_x3 (k_extras_bwd, or the in-kernel experiment build of
+# tools/extras_variant.sh) -- DESIGN.md section 10.
+X3_POINT_EXTRAS = True
+
 _PARAM_NAMES = ("block1.0.weight", "block1.0.bias", "block1.2.weight", "block1.2.bias",
                 "block3.0.weight", "block3.0.bias", "block3.2.weight", "block3.2.bias",
                 "alpha_branch.0.weight", "alpha_branch.0.bias",
@@ -287,7 +293,7 @@ class AggregateFn(torch.autograd.Function):
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
         d_conf = torch.zeros(N, **f32) if has_f else None
         wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3)
-        point_extras = wbx is not None and (has_c or has_d)
+        point_extras = wbx is not None and (has_c or has_d) and X3_POINT_EXTRAS
         if point_extras:
             # the block3.0 extras' colour / dir gradients: per point inside
             # pnr_pairs_to_points_ex below (no float atomics), not in the pairs pass
