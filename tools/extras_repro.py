@@ -52,9 +52,17 @@ def main():
         d = max(float((o[k] - ref).abs().max()) for o in outs[1:])
         res[k] = d / big if big else d
     worst = max(res, key=res.get)
-    print(json.dumps({"lib": os.environ.get("PNR_LIB", "libpnr.so"), "kernel_extras": args.kernel_extras,
-                      "worst": worst, "worst_rel": res[worst],
-                      "rel": {k: v for k, v in res.items() if v > 0}}))
+    out = {"lib": os.environ.get("PNR_LIB", "libpnr.so"), "kernel_extras": args.kernel_extras,
+           "worst": worst, "worst_rel": res[worst], "rel": {k: v for k, v in res.items() if v > 0}}
+    lib = TR.L.lib()
+    if hasattr(lib, "pnr_exp_check_count"):   # experiment builds (PNR_EXP_CHECK2)
+        import ctypes
+        buf = (ctypes.c_uint * 9)()
+        lib.pnr_exp_check_count(buf)
+        out["lds_vs_global_mismatches"] = buf[0]
+        out["first_mismatch"] = dict(zip(("set", "tile", "block", "wave", "lane", "neuron", "lds_bits", "global_bits"),
+                                         list(buf)[1:]))
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
