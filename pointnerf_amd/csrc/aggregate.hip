@@ -1068,10 +1068,6 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_
 #define PNR_X3_EXTRAS_IN_KERNEL 0
 #endif
 constexpr bool kX3ExIn = PNR_X3_EXTRAS_IN_KERNEL != 0;
-#if defined(PNR_EXP_CHECK) || defined(PNR_EXP_CHECK2)
-__device__ unsigned g_exp_check = 0;
-__device__ unsigned g_exp_info[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
 
 template <bool X3>
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
@@ -1188,28 +1184,6 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
         const float4 x4 = *reinterpret_cast<const float4*>(X + u * kQP + 4 * lane);
         const float xv[4] = {x4.x, x4.z, x4.y, x4.w};   // neurons 4u + 0..3 (quad perm)
-#if defined(PNR_EXP_CHECK2)
-        // experiment: the LDS row read back vs the same dz3 row in global memory
-        // (written by this wave's lrelu_bwd_m above); first mismatch recorded
-        if (tile * kTS + (lane >> 3) < n) {
-          const float4 g4 = *reinterpret_cast<const float4*>(A.dz[2] + (tile * kTP + lane) * kHid + 4 * u);
-          const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (__float_as_uint(gv[i]) != __float_as_uint(xv[i])) {
-              atomicAdd(&g_exp_check, 1u);
-              if (atomicCAS(&g_exp_info[0], 0u, 1u) == 0u) {
-                g_exp_info[1] = (unsigned)tile;
-                g_exp_info[2] = blockIdx.x;
-                g_exp_info[3] = wid;
-                g_exp_info[4] = lane;
-                g_exp_info[5] = 4 * u + i;
-                g_exp_info[6] = __float_as_uint(xv[i]);
-                g_exp_info[7] = __float_as_uint(gv[i]);
-              }
-            }
-        }
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float* we = A.wb.w3e + (4 * u + i) * 7;
@@ -1230,27 +1204,10 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
       const int32_t pr = A.sv.prow[pair];
       if (pr >= 0) {
         float g[7];
-#if defined(PNR_EXP_OPAQUE) || defined(PNR_EXP_CHECK)
-        // experiment: the partials' LDS addresses recomputed here from an opaque
-        // lane id (not hoisted to the prologue, so never spilled)
-        int ln;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-#else
-        const int ln = lane;
-#endif
-#if defined(PNR_EXP_CHECK)
-        // experiment: count the reloaded (hoisted, spilled) addresses that differ
-        // from the recomputed ones
 #pragma unroll
         for (int e = 0; e < 7; ++e)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (&exP[(i * 7 + e) * kTP + lane] != &exP[(i * 7 + e) * kTP + ln]) atomicAdd(&g_exp_check, 1u);
-#endif
-#pragma unroll
-        for (int e = 0; e < 7; ++e)
-          g[e] = exP[(0 * 7 + e) * kTP + ln] + exP[(1 * 7 + e) * kTP + ln] + exP[(2 * 7 + e) * kTP + ln] +
-                 exP[(3 * 7 + e) * kTP + ln];
+          g[e] = exP[(0 * 7 + e) * kTP + lane] + exP[(1 * 7 + e) * kTP + lane] + exP[(2 * 7 + e) * kTP + lane] +
+                 exP[(3 * 7 + e) * kTP + lane];
         if (A.d_color) {
 #pragma unroll
           for (int a = 0; a < 3; ++a) atomicAdd(A.d_color + (int64_t)pr * 3 + a, g[a]);
@@ -2303,15 +2260,6 @@ extern "C" int pnr_aggregate_bwd_xyz(const pnr_points* pts, const pnr_samples* s
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
-
-#if defined(PNR_EXP_CHECK) || defined(PNR_EXP_CHECK2)
-// experiment builds: out[0] = mismatch count, out[1..8] = first mismatch record
-extern "C" __attribute__((visibility("default"))) int pnr_exp_check_count(unsigned* out) {
-  PNR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_check), sizeof(unsigned)));
-  PNR_HIP(hipMemcpyFromSymbol(out + 1, HIP_SYMBOL(g_exp_info), 8 * sizeof(unsigned)));
-  return PNR_OK;
-}
-#endif
 
 extern "C" int pnr_used_points_scratch_bytes(int64_t n_points, size_t* out) {
   PNR_CHECK_ARG(out && n_points >= 0, "used_points_scratch_bytes: bad args");

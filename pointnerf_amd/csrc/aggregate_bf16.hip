@@ -14,7 +14,8 @@
 // load per lane per (k-step, tile).
 //
 // Tiles.  A 4-wave workgroup owns 128 (sample, neighbour) pairs = 16 samples
-// x K 8 (k_pairs_b) or 128 samples (k_color_b) or 128 points (k_point_pre_b);
+// x K 8 (k_pairs_b; its colour branch runs on the tile's samples) or 128
+// points (k_point_pre_b);
 // wave w owns output tiles {2w, 2w+1} (256-wide layers) or {w} (128-wide)
 // for all four 32-column quarters, so each 1-KB weight fragment feeds 4
 // MFMAs.  ~78 KB of LDS per workgroup -> 2 per CU (2 waves per SIMD).
@@ -38,9 +39,6 @@ struct AggArgsB {
   pnr_samples s;
   pnr_mlp_bf16 w;
   uint16_t* p1;      // [n_p1, 256] bf16 per-point block1.0 partial, accumulator order
-  uint16_t* hid;     // [n_max, 256] bf16 K-summed features
-  int32_t* vmask;    // [n_max]
-  float4* vdir;      // [n_max] rotated view direction of each sample (k_pairs_b -> k_color_b's PE)
   float* out_feat;
   float* out_weight;
   float* out_conf;
@@ -59,8 +57,11 @@ __device__ __forceinline__ uint16_t to_bf16(float a) { return __builtin_bit_cast
 // (raw buffer loads; the packs carry kBPad >= WD zero steps), B fragments one
 // step ahead from LDS.  sched_barrier(0) pins the order: without it hipcc sank
 // each weight load next to its MFMAs and waited vmcnt(0) on it every k-step
-// (k_color_b then ran at 0.14 MFMA busy).
-template <int NT, int PT, int NTOT, int PITCH, int WD>
+// (the colour kernel of round 4 then ran at 0.14 MFMA busy).
+// BROW: the B rows of the last k-step's upper half (16 (nsteps - 1) + 8 .. + 15)
+// are the bias row (1) and zeros, whatever Xb holds there (the fused colour
+// branch keeps its 280 input rows at pitch kPB: no room for the bias row).
+template <int NT, int PT, int NTOT, int PITCH, int WD, bool BROW = false>
 __device__ __forceinline__ void mlp_layer_ring(f32x16 (&acc)[PT * NT], const uint4* __restrict__ wf,
                                             const uint16_t* Xb, int nsteps, int lane) {
   static_assert(WD <= kBPad, "the packs' zero steps cover the ring's lead");
@@ -84,6 +85,11 @@ __device__ __forceinline__ void mlp_layer_ring(f32x16 (&acc)[PT * NT], const uin
     const int tn = t + 1 < nsteps ? t + 1 : t;
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) x[xs ^ 1][pt] = *reinterpret_cast<const uint4*>(xr + 32 * pt * PITCH + 16 * tn);
+    if constexpr (BROW) {
+      const bool bias = h && tn == nsteps - 1;
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) x[xs ^ 1][pt] = bias ? make_uint4(0x3f80u, 0u, 0u, 0u) : x[xs ^ 1][pt];
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt)
@@ -110,12 +116,13 @@ __device__ __forceinline__ void mlp_layer_ring(f32x16 (&acc)[PT * NT], const uin
 
 // WD = 0: compiler-scheduled (it loads each step's weights where they are used):
 // the k_pairs_b tiles whose registers have no room for a ring (measured faster)
-template <int NT, int PT, int NTOT, int PITCH, int WD = 2>
+template <int NT, int PT, int NTOT, int PITCH, int WD = 2, bool BROW = false>
 __device__ __forceinline__ void mlp_layer_b(f32x16 (&acc)[PT * NT], const uint4* __restrict__ wf,
                                             const uint16_t* Xb, int nsteps, int lane) {
   if constexpr (WD > 0) {
-    mlp_layer_ring<NT, PT, NTOT, PITCH, WD>(acc, wf, Xb, nsteps, lane);
+    mlp_layer_ring<NT, PT, NTOT, PITCH, WD, BROW>(acc, wf, Xb, nsteps, lane);
   } else {
+    static_assert(!BROW, "bias-row override: ring layers only");
     // the round-4 loop (a0 / a1 and x / y one step ahead as written; hipcc
     // schedules the loads itself)
     const int c = lane & 31, h = lane >> 5;
@@ -279,9 +286,11 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 // zero weights; the xor-tree and DPP reduce-scatter sums below pair the
 // remaining lanes exactly as the 8-lane trees do).
 constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
-constexpr int kHP = kHid + 8;  // bf16 pitch of the staged hid rows (16-B aligned rows)
-static_assert(kBTSmax * kHP <= kBT * kPB, "staged hid rows must fit Xb");
-constexpr size_t kPairsBLds = (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT + kBTSmax) * 4;
+constexpr size_t kPairsBLds =
+    (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT + kBTSmax + 3 * kBTSmax) * 4;
+constexpr int kOPitch = kC + 1;   // fp32 output staging pitch (odd: conflict-free column writes)
+static_assert((size_t)kBT * kOPitch * 4 <= (size_t)kBT * kPB * 2, "output staging must fit the Xb tile");
+static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit the Xb pitch");
 
 // weight-ring depth of k_pairs_b's layers per tile shape (measured at c5: the
 // one-slot tiles gain from a one-step lead, the others spill with it)
@@ -300,7 +309,8 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   float* exL = reinterpret_cast<float*>(sflag + kBTSmax);  // [8][128]
   int* prowL = reinterpret_cast<int*>(exL + 8 * kBT);      // [128]
   int* vL = prowL + kBT;                                   // [SPT] sample index of each tile row
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* vrL = reinterpret_cast<float*>(vL + kBTSmax);     // [3][SPT] rotated view dir of each sample
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar addressing
   const int c = lane & 31, h = lane >> 5;
   const int K = A.s.K;
   // bucket samples list[0 .. n) (buckets.hip), or every sample in order
@@ -421,9 +431,10 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         if (k == 0) {
           sflag[j] = active && samp_valid;
           vL[j] = (int)v;   // the list entry, read once here (not per store below)
-          // the colour branch's view PE input (k_color_b reads it with the hid row
-          // instead of walking sample row -> dir map -> ray dir again)
-          if (active) A.vdir[v] = make_float4(vrot[0], vrot[1], vrot[2], 0.f);
+          // the colour branch's view-PE input (kept from the gather: no second walk
+          // sample row -> dir map -> ray dir)
+#pragma unroll
+          for (int a = 0; a < 3; ++a) vrL[a * kBTSmax + j] = vrot[a];
         }
         if (active && k < K) {
           // the bucket's dropped slots (KT..K-1) are empty: weight 0, their gathered conf
@@ -555,7 +566,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
         // K-sum of the sample's KT lanes as a DPP reduce-scatter: each lane keeps
         // 16 / KT of the 16 accumulator rows (the 8-lane tree's pairing)
-        uint16_t* hrow = Xb + sj * kHP + 32 * (T0 + T) + 4 * h;   // staged row of sample sj
+        uint16_t* hrow = Xb + sj * kPB + 32 * (T0 + T) + 4 * h;   // staged row of sample sj
         if constexpr (KT == 8) {
           const bool b2 = (ik & 4) != 0, b1 = (ik & 2) != 0, b0 = (ik & 1) != 0;
           float w8[8], w4v[4], w2[2];
@@ -632,15 +643,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       for (int pt = 0; pt < kBPT; ++pt) apart[wid * kBT + 32 * pt + c] = pa_part[pt];
     }
     __syncthreads();
-    // staged hid rows -> global, 16 B per thread (a wave writes two whole rows)
-    for (int i = threadIdx.x; i < SPT * (kHid / 8); i += 64 * kBWaves) {
-      const int r = i / (kHid / 8), q = i % (kHid / 8);
-      const int64_t jv = tile * SPT + r;
-      if (jv < n && sflag[r]) {
-        const int64_t vo = vL[r];
-        reinterpret_cast<uint4*>(A.hid + vo * kHid)[q] = *reinterpret_cast<const uint4*>(Xb + r * kHP + 8 * q);
-      }
-    }
     if (wid < 2) {
       const int col = 64 * wid + lane;
       const int j = col / KT, k = col % KT;
@@ -648,142 +650,82 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
       const float alpha_s = xork_sum_nc<KT>(wtL[col] * alpha_k);
       const int64_t jv = tile * SPT + j;
-      if (k == 0 && jv < n) {
-        const int64_t vo = vL[j];
-        A.vmask[vo] = sflag[j];
-        if (sflag[j]) A.out_feat[vo * (kC + 1)] = alpha_s;
-      }
-    }
-    }
-    __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_color_b: [hid, PE_4(view dir)] -> 128 -> 128 -> 128 for 128 samples.
-constexpr size_t kColorBLds = (size_t)kBT * kPBc * 2;
-constexpr int kOPitch = kC + 1;   // fp32 output staging pitch (odd: conflict-free column writes)
-static_assert((size_t)kBT * kOPitch * 4 <= kColorBLds, "output staging must fit the Xb tile");
-
-__global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t xb_dyn[];
-  uint16_t* Xb = xb_dyn;   // [128][kPBc]
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = lane & 31, h = lane >> 5;
-  const int64_t n = eff_n(A.s);
-  const int64_t ntiles = cdiv(n, kBT);
-  const float neg = A.w.neg_slope;
-  const uint4* w1 = reinterpret_cast<const uint4*>(A.w.wc1f) + wid * 64;
-  const uint4* w2 = reinterpret_cast<const uint4*>(A.w.wc2f) + wid * 64;
-  const uint4* w3 = reinterpret_cast<const uint4*>(A.w.wc3f) + wid * 64;
-  // hid rows of a tile (512 B each; zeros for masked samples) in 16 x 16-B
-  // chunks per thread, loaded one tile ahead: the next tile's loads are in flight
-  // during this tile's three layers (a chain of 16 dependent load rounds per tile
-  // otherwise: the kernel waited on HBM latency, not on HBM bandwidth)
-  constexpr int kHidChunks = kBT * (kHid / 8) / (64 * kBWaves);
-  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-  u32x4v hu[kHidChunks];
-  float4 vdn = make_float4(0.f, 0.f, 0.f, 0.f);   // the loaded tile's view direction (threads < kBT)
-  uint64_t vm0 = 0, vm1 = 0;   // the loaded tile's vmask bits
-  // Every load unconditional, from a clamped (valid) row: a load under a branch
-  // made hipcc drain vmcnt(0) after it, which serialised the whole prefetch.
-  // Masked samples' hid rows are loaded as they are (stale); only their own
-  // columns see them and their outputs are never stored.
-  auto load_hid = [&](int64_t t) {
-    const int64_t b = t * kBT;
-    const int64_t r0 = b + lane < n ? b + lane : 0, r1 = b + 64 + lane < n ? b + 64 + lane : 0;
-    const int64_t rv = b + (threadIdx.x & (kBT - 1)) < n ? b + (threadIdx.x & (kBT - 1)) : 0;
-    const int32_t m0 = A.vmask[r0], m1 = A.vmask[r1];
-    vdn = A.vdir[rv];
+      if (k == 0 && jv < n && sflag[j]) A.out_feat[(int64_t)vL[j] * (kC + 1)] = alpha_s;
+    } else if (threadIdx.x - 128 < SPT) {
+      // colour-branch inputs 256 .. 279 of sample j: PE_4 of the rotated view dir
+      // (ori dropped; masked samples: 0) -- rows 256 + 4 ch + f sin, 268 + 4 ch + f cos
+      const int j = threadIdx.x - 128;
+      const bool valid = sflag[j] != 0;
+      uint16_t* xc = Xb + j * kPB;
 #pragma unroll
-    for (int k = 0; k < kHidChunks; ++k) {
-      const int i = threadIdx.x + 64 * kBWaves * k;
-      const int col = i >> 5, q = i & 31;
-      const int64_t r = b + col < n ? b + col : 0;
-      hu[k] = reinterpret_cast<const u32x4v*>(A.hid + r * kHid)[q];
-    }
-    vm0 = __ballot(b + lane < n && m0 != 0);
-    vm1 = __ballot(b + 64 + lane < n && m1 != 0);
-  };
-  load_hid(blockIdx.x);
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t v0 = tile * kBT;
-#pragma unroll
-    for (int k = 0; k < kHidChunks; ++k) {
-      const int i = threadIdx.x + 64 * kBWaves * k;
-      *reinterpret_cast<u32x4v*>(Xb + (i >> 5) * kPBc + 8 * (i & 31)) = hu[k];
-    }
-    const uint64_t tm0 = vm0, tm1 = vm1;
-    const float4 vdc = vdn;
-    load_hid(tile + gridDim.x);
-    // view PE (ori dropped): rows 256 + 4ch + f = sin, 268 + 4ch + f = cos, bias 280, zeros to 287
-    if (threadIdx.x < kBT) {
-      const int col = threadIdx.x;
-      // the rotated view direction k_pairs_b wrote for the sample (masked samples: 0)
-      const bool valid = ((col < 64 ? tm0 : tm1) >> (col & 63)) & 1;
-      const float vrot[3] = {valid ? vdc.x : 0.f, valid ? vdc.y : 0.f, valid ? vdc.z : 0.f};
-      uint16_t* xc = Xb + col * kPBc;
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {   // rows 256 + 4 ch + f (sin), 268 + 4 ch + f (cos)
+      for (int ch = 0; ch < 3; ++ch) {
+        const float vr = valid ? vrL[ch * kBTSmax + j] : 0.f;
         float sn[4], cs[4];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) sincosf(vrot[ch] * (float)(1 << f), &sn[f], &cs[f]);
+        for (int f = 0; f < 4; ++f) sincosf(vr * (float)(1 << f), &sn[f], &cs[f]);
         *reinterpret_cast<uint2*>(xc + 256 + 4 * ch) = make_uint2(pack_bf16x2(sn[0], sn[1]), pack_bf16x2(sn[2], sn[3]));
         *reinterpret_cast<uint2*>(xc + 268 + 4 * ch) = make_uint2(pack_bf16x2(cs[0], cs[1]), pack_bf16x2(cs[2], cs[3]));
       }
-      *reinterpret_cast<uint4*>(xc + 280) = make_uint4(pack_bf16x2(1.f, 0.f), 0u, 0u, 0u);   // bias row, zeros to 287
+    }
     }
     __syncthreads();
-    f32x16 acc[kBPT];
+    // -------------------------------------------- colour branch on the tile's samples
+    // [hid (K-summed, staged above), PE_4(view)] -> 128 -> 128 -> 128 (the
+    // reference's color_branch, point_aggregators.py:640-646), columns = samples:
+    // the K-summed rows never leave the CU.  Bias of the first layer: the ring's
+    // last-step override (row 280 = 1), the 280 real rows fill the pitch.
+    {
+      constexpr int PTc = SPT >= 32 ? SPT / 32 : 1;   // 32-column quarters holding the SPT samples
+      constexpr int NCc = 32 * PTc;
+      const uint4* wc1 = reinterpret_cast<const uint4*>(A.w.wc1f) + wid * 64;
+      const uint4* wc2 = reinterpret_cast<const uint4*>(A.w.wc2f) + wid * 64;
+      const uint4* wc3 = reinterpret_cast<const uint4*>(A.w.wc3f) + wid * 64;
+      f32x16 cacc[PTc];
 #pragma unroll
-    for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_b<1, kBPT, 4, kPBc>(acc, w1, Xb, 18, lane);
-    __syncthreads();
-    store_act_b<1, kBPT, kPBc>(acc, Xb, neg, lane, wid);
-    if (wid == 0) {
-      const float one = 1.f;
-      tail_rows_b(Xb, kPBc, lane, kC, &one, 1);
-      tail_rows_b(Xb, kPBc, lane + 64, kC, &one, 1);
-    }
-    __syncthreads();
+      for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
+      mlp_layer_b<1, PTc, 4, kPB, 2, true>(cacc, wc1, Xb, 18, lane);
+      __syncthreads();
+      store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
+      if (wid == 0) {
+        const float one = 1.f;
 #pragma unroll
-    for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_b<1, kBPT, 4, kPBc>(acc, w2, Xb, 9, lane);
-    __syncthreads();
-    store_act_b<1, kBPT, kPBc>(acc, Xb, neg, lane, wid);
-    if (wid == 0) {
-      const float one = 1.f;
-      tail_rows_b(Xb, kPBc, lane, kC, &one, 1);
-      tail_rows_b(Xb, kPBc, lane + 64, kC, &one, 1);
-    }
-    __syncthreads();
+        for (int cc = lane; cc < NCc; cc += 64) tail_rows_b(Xb, kPB, cc, kC, &one, 1);
+      }
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kBPT; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_b<1, kBPT, 4, kPBc>(acc, w3, Xb, 9, lane);
-    // out_feat rows (valid samples only) through LDS: a lane holds 16 neurons of
-    // one sample, so direct stores would touch 32 rows (516 B apart) per
-    // instruction; staged, each store writes 64 consecutive channels of a row.
-    __syncthreads();   // every wave's layer-3 reads of Xb are done
-    float* Ob = reinterpret_cast<float*>(xb_dyn);   // [128][kOPitch] fp32
+      for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
+      mlp_layer_b<1, PTc, 4, kPB, 2>(cacc, wc2, Xb, 9, lane);
+      __syncthreads();
+      store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
+      if (wid == 0) {
+        const float one = 1.f;
 #pragma unroll
-    for (int pt = 0; pt < kBPT; ++pt)
+        for (int cc = lane; cc < NCc; cc += 64) tail_rows_b(Xb, kPB, cc, kC, &one, 1);
+      }
+      __syncthreads();
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
+      mlp_layer_b<1, PTc, 4, kPB, 2>(cacc, wc3, Xb, 9, lane);
+      __syncthreads();   // every wave's layer-3 reads of Xb are done
+      // out_feat rows (valid samples only) through LDS, two rows per store
+      // instruction (lane half = row, 16 B per lane, rows 516 B apart: 4-B aligned)
+      float* Ob = reinterpret_cast<float*>(Xb);   // [NCc][kOPitch] fp32
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(acc[pt][4 * q + i], neg);
-    __syncthreads();
-    // two rows per store instruction (lane half = row, 16 B per lane; the rows
-    // are 516 B apart, so the stores are only 4-B aligned): 16 store instructions
-    // per wave and tile instead of 64, so the next tile's wait for its prefetched
-    // hid rows (older in vmcnt order) need not wait for these stores' completion
-    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-    for (int r2 = wid; r2 < kBT / 2; r2 += kBWaves) {
-      const int r = 2 * r2 + (lane >> 5), l = lane & 31;
-      if (!(((r < 64 ? tm0 : tm1) >> (r & 63)) & 1)) continue;
-      const float* src = Ob + r * kOPitch + 4 * l;
-      const f4u v = {src[0], src[1], src[2], src[3]};
-      *reinterpret_cast<f4u*>(A.out_feat + (v0 + r) * (kC + 1) + 1 + 4 * l) = v;
+      for (int pt = 0; pt < PTc; ++pt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(cacc[pt][4 * q + i], neg);
+      __syncthreads();
+      typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+      for (int r2 = wid; r2 < SPT / 2; r2 += kBWaves) {
+        const int r = 2 * r2 + (lane >> 5), l = lane & 31;
+        if (tile * SPT + r >= n || !sflag[r]) continue;
+        const float* src = Ob + r * kOPitch + 4 * l;
+        const f4u v = {src[0], src[1], src[2], src[3]};
+        *reinterpret_cast<f4u*>(A.out_feat + (int64_t)vL[r] * (kC + 1) + 1 + 4 * l) = v;
+      }
     }
     __syncthreads();
   }
@@ -792,9 +734,8 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_color_b(AggArgsB A) {
 static size_t scratch_need_b(int64_t n_max, int64_t n_p1) {
   const int64_t nm = n_max > 0 ? n_max : 1;
   const int64_t np = n_p1 > 0 ? n_p1 : 1;
-  // P1 | hid | vmask | vdir | pair buckets (buckets.hip)
-  return (size_t)nm * kHid * 2 + (size_t)cdiv(nm, 4) * 16 + (size_t)nm * 16 + (size_t)np * kHid * 2 +
-         (size_t)bucket_scratch_ints(nm) * 4;
+  // P1 | pair buckets (buckets.hip)
+  return (size_t)np * kHid * 2 + (size_t)bucket_scratch_ints(nm) * 4;
 }
 
 }  // namespace pnr
@@ -840,8 +781,6 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<8>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_b), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kColorBLds));
     attr = true;
   }
   const int64_t nm = s->n_max;
@@ -849,12 +788,9 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   a.pts = *pts;
   a.s = *s;
   a.w = *w;
-  // P1 [n_p1, 256] first (fixed place, reusable via p1_ready) | hid | vmask
+  // P1 [n_p1, 256] first (fixed place, reusable via p1_ready) | pair buckets
   a.p1 = static_cast<uint16_t*>(scratch);
-  a.hid = a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid;
-  a.vmask = reinterpret_cast<int32_t*>(a.hid + nm * kHid);
-  a.vdir = reinterpret_cast<float4*>(a.vmask + cdiv(nm, 4) * 4);
-  int32_t* bk_scratch = reinterpret_cast<int32_t*>(a.vdir + nm);
+  int32_t* bk_scratch = reinterpret_cast<int32_t*>(a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid);
   a.out_feat = out_feat;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
@@ -883,7 +819,5 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
                        st, a, nullptr, nullptr, 3);
     PNR_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_color_b, dim3(grid_for(cdiv(nm, kBT), 1, 256 * 2)), dim3(64 * kBWaves), kColorBLds, st, a);
-  PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
