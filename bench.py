@@ -743,8 +743,9 @@ def main():
                              "fp32h2": "pnr_aggregate_fwd_h2 = k_point_pre_h2 + k_pairs_h2 + k_color_h2 (f16x2 split, "
                                        "v_mfma_f32_32x32x16_f16; k_point_pre_h2 runs on a side stream beside "
                                        "the query, its duration added to the span)",
-                             "bf16": "pnr_aggregate_fwd_bf16 = k_point_pre_b + k_pairs_b + k_color_b "
-                                     "(v_mfma_f32_32x32x16_bf16)"}[args.dtype],
+                             "bf16": "pnr_used_points (k_mark_used, scan, k_used_list) + pnr_aggregate_fwd_bf16 = "
+                                     "k_point_pre_b + sample buckets + k_pairs_b<1/2/4/8> with the colour branch "
+                                     "fused (v_mfma_f32_32x32x16_bf16)"}[args.dtype],
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                          "peak_note": {"fp32": "fp32 MFMA dense peak",
                                        "fp32x3": "fp32-equivalent: bf16 MFMA dense peak / 6 products per fp32 MAC",

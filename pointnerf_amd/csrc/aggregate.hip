@@ -1359,7 +1359,9 @@ __global__ void k_mark_used(const int32_t* __restrict__ pidx, const int32_t* __r
   const int64_t n = (n_dev ? (int64_t)*n_dev : cap) * K;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t p = pidx[i];
-    if (p >= 0) flags[p] = 1;
+    // read before write: neighbouring samples share most points, so nearly every
+    // flag is already set and stays a cached read instead of a partial-line write
+    if (p >= 0 && flags[p] == 0) flags[p] = 1;
   }
 }
 

@@ -26,6 +26,7 @@ namespace pnr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));   // (HIP's uint4 arrays can land in scratch)
 
 constexpr int kBT = 128;                 // columns (pairs / samples / points) per tile
 constexpr int kBPT = kBT / 32;           // 32-column quarters per tile
@@ -292,10 +293,11 @@ constexpr int kOPitch = kC + 1;   // fp32 output staging pitch (odd: conflict-fr
 static_assert((size_t)kBT * kOPitch * 4 <= (size_t)kBT * kPB * 2, "output staging must fit the Xb tile");
 static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit the Xb pitch");
 
-// weight-ring depth of k_pairs_b's layers per tile shape (measured at c5: the
-// one-slot tiles gain from a one-step lead, the others spill with it)
+// weight-ring depth of k_pairs_b's layers per tile shape (measured at c5, with
+// the colour branch fused: two steps ahead for the one-slot tiles, one for the
+// others -- 59.6 ms against 61.1 for one / compiler-scheduled)
 template <int KT>
-constexpr int kPairsWD = KT == 1 ? 1 : 0;
+constexpr int kPairsWD = KT == 1 ? 2 : 1;
 
 template <int KT>
 __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const int32_t* bk_list, const int32_t* bk_info,
@@ -350,6 +352,29 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   int nx_row = pf_row(nx_v);
   int nx_pid = pf_pid(nx_row);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // -------------------------------------------- P1 rows in flight during the gather
+    // The pair ids come from the prefetched chain; one barrier hands them to the
+    // MFMA lanes, whose raw bf16 P1 loads (2 x 16 B per quarter and tile) then
+    // travel while the gather computes (the accumulators are not live yet).
+    // Every load from a clamped row, the empty pairs zeroed at the unpack.
+    if (threadIdx.x < kBT) prowL[threadIdx.x] = nx_pid;
+    __syncthreads();
+    u32x4v p1raw[kBPT][2][2];
+    unsigned p1m = 0;
+#pragma unroll
+    for (int pt = 0; pt < kBPT; ++pt) {
+      const int pr = prowL[32 * pt + c];
+      p1m |= (pr >= 0 ? 1u : 0u) << pt;
+      const int prc = pr >= 0 ? pr : 0;
+      // (the clamped row's used_map entry may be -1: clamp again)
+      const int64_t p1r = A.pts.used_map ? (int64_t)max(A.pts.used_map[prc], 0) : (int64_t)prc;
+#pragma unroll
+      for (int T = 0; T < 2; ++T) {
+        const u32x4v* src = reinterpret_cast<const u32x4v*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 16 * h);
+        p1raw[pt][T][0] = src[0];
+        p1raw[pt][T][1] = src[1];
+      }
+    }
     // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
     {
       const int col = threadIdx.x & (kBT - 1), role = threadIdx.x >> 7;
@@ -427,7 +452,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 #pragma unroll
         for (int e = 0; e < 8; ++e) exL[e * kBT + col] = ex[e];
         wtL[col] = wn * confc;
-        prowL[col] = valid ? (int)prow : -1;
         if (k == 0) {
           sflag[j] = active && samp_valid;
           vL[j] = (int)v;   // the list entry, read once here (not per store below)
@@ -476,25 +500,19 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       }
     }
     __syncthreads();
-    // -------------------------------------------- P1 gather into the accumulators
+    // -------------------------------------------- P1 rows into the accumulators
     f32x16 acc[kBPT * 2];
 #pragma unroll
     for (int pt = 0; pt < kBPT; ++pt) {
-      const int pr = prowL[32 * pt + c];
-      const int64_t p1r = pr < 0 ? -1 : (A.pts.used_map ? (int64_t)A.pts.used_map[pr] : (int64_t)pr);
+      const bool has = (p1m >> pt) & 1;
 #pragma unroll
       for (int T = 0; T < 2; ++T) {
-        if (p1r >= 0) {
-          const uint4* src = reinterpret_cast<const uint4*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 16 * h);
-          const uint4 u0 = src[0], u1 = src[1];
-          const unsigned w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+        const u32x4v u0 = p1raw[pt][T][0], u1 = p1raw[pt][T][1];
+        const unsigned w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            acc[pt * 2 + T][2 * q] = bf16_lo(w[q]);
-            acc[pt * 2 + T][2 * q + 1] = bf16_hi(w[q]);
-          }
-        } else {
-          acc[pt * 2 + T] = (f32x16){0.f};
+        for (int q = 0; q < 8; ++q) {
+          acc[pt * 2 + T][2 * q] = has ? bf16_lo(w[q]) : 0.f;
+          acc[pt * 2 + T][2 * q + 1] = has ? bf16_hi(w[q]) : 0.f;
         }
       }
     }

@@ -17,8 +17,9 @@ import sys
 AGG_BY_DTYPE = {"fp32": ("k_point_pre", "k_pairs", "k_color"),
                 "fp32x3": ("k_point_pre", "k_pairs_x3", "k_color"),
                 "fp32h2": ("k_point_pre_h2", "k_pairs_h2", "k_color_h2"),
-                "bf16": ("k_point_pre_b", "k_bucket_hist", "k_bucket_scan", "k_bucket_scatter", "k_pairs_b",
-                         "k_color_b")}
+                # (the last name runs once per aggregate launch: the per-launch divisor)
+                "bf16": ("k_mark_used", "k_used_list", "k_point_pre_b", "k_bucket_hist", "k_bucket_scan",
+                         "k_pairs_b", "k_bucket_scatter")}
 MOPS = {"fp32": "SQ_INSTS_VALU_MFMA_MOPS_F32", "fp32x3": "SQ_INSTS_VALU_MFMA_MOPS_BF16",
         "fp32h2": "SQ_INSTS_VALU_MFMA_MOPS_F16",
         "bf16": "SQ_INSTS_VALU_MFMA_MOPS_BF16"}
@@ -33,7 +34,7 @@ def short(name):
 def per_kernel(path, counters):
     """Counter values per aggregate launch: summed over a kernel's dispatches
     (the bf16 pairs stage is one dispatch per neighbour bucket), divided by the
-    number of launches (dispatches of the colour kernel, once per launch)."""
+    number of launches (dispatches of the list's last kernel, once per launch)."""
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
