@@ -192,6 +192,16 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
 // f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
                         hipStream_t st);
+// Workgroup barrier for an LDS hand-off only: lgkmcnt(0) + s_barrier between
+// LDS-scoped fences, so the compiler keeps LDS accesses on their side while
+// global loads stay in flight across it (__syncthreads' fence drains them with
+// vmcnt(0)).  Only where no global-memory hand-off between waves crosses.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Sample buckets by filled neighbour slots (buckets.hip): list = the sample
 // indices partitioned by bucket b (KT = 1 << b slots), bucket b at
 // [info[b], info[b] + info[4 + b]), in sample order within a bucket.

@@ -299,7 +299,25 @@ static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit
 template <int KT>
 constexpr int kPairsWD = KT == 1 ? 2 : 1;
 
-template <int KT>
+#ifdef PNR_PB_TRACE
+// diagnostic build only (tools/pb_trace.py): s_memtime per phase of the first 8
+// tiles of every wave of workgroups < 512, for the KT = PNR_PB_TRACE launch
+__device__ unsigned long long g_pb_trace[512 * 4 * 8 * 20];
+#define PB_STAMP(i)                                                                            \
+  do {                                                                                         \
+    if (KT == PNR_PB_TRACE && it_tr < 8 && lane == 0 && blockIdx.x < 512)                      \
+      g_pb_trace[((blockIdx.x * 4 + wid) * 8 + it_tr) * 20 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PB_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
+// GEN = false: no per-point Rw2c, no used_map, no multi-camera batch, no
+// out_weight / out_conf (the render path) -- the general-path branches are compiled out, so no branch
+// merge makes the gather wait (vmcnt(0)) for the P1 rows in flight.
+template <int KT, bool GEN>
 __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const int32_t* bk_list, const int32_t* bk_info,
                                                               int bucket) {
   constexpr int SPT = kBT / KT;                            // samples per tile
@@ -348,34 +366,28 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   };
   auto pf_row = [&](int v) -> int { return v >= 0 ? (int)sample_row(A.s, v) : -1; };
   auto pf_pid = [&](int row) -> int { return (row >= 0 && pf_k < K) ? A.s.pidx[(int64_t)row * K + pf_k] : -1; };
+  auto pf_drow = [&](int row) -> int { return row >= 0 ? (int)dir_row(A.s, row) : 0; };   // ray-dir row
   int nx_v = pf_v(blockIdx.x);
   int nx_row = pf_row(nx_v);
   int nx_pid = pf_pid(nx_row);
+  int nx_drow = pf_drow(nx_row);
+#ifdef PNR_PB_TRACE
+  int it_tr = -1;
+#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    // -------------------------------------------- P1 rows in flight during the gather
-    // The pair ids come from the prefetched chain; one barrier hands them to the
-    // MFMA lanes, whose raw bf16 P1 loads (2 x 16 B per quarter and tile) then
-    // travel while the gather computes (the accumulators are not live yet).
-    // Every load from a clamped row, the empty pairs zeroed at the unpack.
+#ifdef PNR_PB_TRACE
+    ++it_tr;
+#endif
+    PB_STAMP(0);
+    // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
+    // Order: the gather's own loads, an LDS-only barrier that hands the pair ids
+    // (prefetched chain) to the MFMA lanes, their raw P1 row loads, then the
+    // gather's math -- so the math waits for its loads only (vmcnt counts in
+    // issue order) and the P1 rows travel meanwhile.  Every load unconditional
+    // (clamped rows, zeroed at the unpack).
     if (threadIdx.x < kBT) prowL[threadIdx.x] = nx_pid;
-    __syncthreads();
     u32x4v p1raw[kBPT][2][2];
     unsigned p1m = 0;
-#pragma unroll
-    for (int pt = 0; pt < kBPT; ++pt) {
-      const int pr = prowL[32 * pt + c];
-      p1m |= (pr >= 0 ? 1u : 0u) << pt;
-      const int prc = pr >= 0 ? pr : 0;
-      // (the clamped row's used_map entry may be -1: clamp again)
-      const int64_t p1r = A.pts.used_map ? (int64_t)max(A.pts.used_map[prc], 0) : (int64_t)prc;
-#pragma unroll
-      for (int T = 0; T < 2; ++T) {
-        const u32x4v* src = reinterpret_cast<const u32x4v*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 16 * h);
-        p1raw[pt][T][0] = src[0];
-        p1raw[pt][T][1] = src[1];
-      }
-    }
-    // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
     {
       const int col = threadIdx.x & (kBT - 1), role = threadIdx.x >> 7;
       const int j = col / KT, k = col % KT;
@@ -383,42 +395,71 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const bool active = jv < n;
       const int64_t v = active ? (int64_t)nx_v : 0;
       const int64_t row = active ? (int64_t)nx_row : 0;
-      int64_t prow = -1;
-      bool valid = false;
-      if (active && k < K) {
-        const int pid = nx_pid;
-        valid = pid >= 0;
-        prow = valid ? pid : 0;
-      }
-      float sw[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, vd[3] = {0.f, 0.f, 0.f};
-      int64_t drow = 0;
-      if (active) {
-        drow = dir_row(A.s, row);
+      const bool slot = active && k < K;
+      const bool valid = slot && nx_pid >= 0;
+      const int64_t prow = valid ? nx_pid : 0;
+      const int64_t drow = active ? (int64_t)nx_drow : 0;
+      // Every load unconditional -- clamped rows, absent arrays read through a
+      // present one -- and masked afterwards: a load under a branch made hipcc
+      // drain vmcnt(0) after it (one HBM round trip per load group: the gather was
+      // 15.5 k of a 100 k-cycle tile at c5), and these now travel together.
+      const float* colp = A.pts.color ? A.pts.color : A.pts.xyz;
+      const float* dirp = A.pts.dir ? A.pts.dir : A.pts.xyz;
+      const float* persp = A.pts.pers ? A.pts.pers : A.pts.xyz;
+      const float* confp = A.pts.conf ? A.pts.conf : A.pts.xyz;
+      float sw[3], sp[3], vd[3], pw[3], pp[3], colr[3], pdir[3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          sw[a] = A.s.sample_w[row * 3 + a];
-          sp[a] = A.s.sample_p[row * 3 + a];
-          vd[a] = A.s.dirs[drow * 3 + a];
+      for (int a = 0; a < 3; ++a) {
+        sw[a] = A.s.sample_w[row * 3 + a];
+        sp[a] = A.s.sample_p[row * 3 + a];
+        vd[a] = A.s.dirs[drow * 3 + a];
+        pw[a] = A.pts.xyz[prow * 3 + a];
+        colr[a] = colp[prow * 3 + a];
+        pdir[a] = dirp[prow * 3 + a];
+        pp[a] = persp[prow * 3 + a];
+      }
+      const float cfl = confp[slot ? prow : 0];
+      __builtin_amdgcn_sched_barrier(0);
+      lds_barrier();   // prowL: LDS only, the loads above stay in flight
+      PB_STAMP(1);
+#pragma unroll
+      for (int pt = 0; pt < kBPT; ++pt) {
+        const int pr = prowL[32 * pt + c];
+        p1m |= (pr >= 0 ? 1u : 0u) << pt;
+        const int prc = pr >= 0 ? pr : 0;
+        // (the clamped row's used_map entry may be -1: clamp again)
+        const int64_t p1r = GEN && A.pts.used_map ? (int64_t)max(A.pts.used_map[prc], 0) : (int64_t)prc;
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+          const u32x4v* src = reinterpret_cast<const u32x4v*>(A.p1 + p1r * kHid + 32 * (T0 + T) + 16 * h);
+          // streamed (non-temporal): the P1 rows must not push the weights out of L2
+          p1raw[pt][T][0] = __builtin_nontemporal_load(src);
+          p1raw[pt][T][1] = __builtin_nontemporal_load(src + 1);
         }
       }
-      float pw[3] = {0.f, 0.f, 0.f}, pp[3] = {0.f, 0.f, 0.f}, colr[3] = {0.f, 0.f, 0.f},
-            pdir[3] = {0.f, 0.f, 0.f};
-      float cf = 1.f;
-      if (valid) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          pw[a] = A.pts.xyz[prow * 3 + a];
-          colr[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
-          pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
-        }
-        if (A.pts.pers) {
-#pragma unroll
-          for (int a = 0; a < 3; ++a) pp[a] = A.pts.pers[prow * 3 + a];
-        } else {
-          pair_pers(A.pts, A.s, drow, pw, cam_c, cam_R, pp);
-        }
+      for (int a = 0; a < 3; ++a) {
+        sw[a] = active ? sw[a] : 0.f;
+        sp[a] = active ? sp[a] : 0.f;
+        vd[a] = active ? vd[a] : 0.f;
+        pw[a] = valid ? pw[a] : 0.f;
+        colr[a] = valid && A.pts.color ? colr[a] : 0.f;
+        pdir[a] = valid && A.pts.dir ? pdir[a] : 0.f;
+        pp[a] = valid && A.pts.pers ? pp[a] : 0.f;
       }
-      if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
+      if (!A.pts.pers) {
+        // w2pers under the camera of the pair's ray: the launch's one camera
+        // (registers) or, GEN only, the ray's entry of the camera tables (loads)
+        float ppc[3];
+        if (GEN)
+          pair_pers(A.pts, A.s, drow, pw, cam_c, cam_R, ppc);
+        else
+          world_to_pers(pw, cam_c, cam_R, ppc);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) pp[a] = valid ? ppc[a] : 0.f;
+      }
+      const float cf = A.pts.conf && slot ? cfl : 1.f;
       float d6[6];
       d6[0] = pw[0] - sw[0];
       d6[1] = pw[1] - sw[1];
@@ -437,12 +478,12 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       dr6[3] = d6[3];
       dr6[4] = d6[4];
       dr6[5] = d6[5];
-      if (A.pts.rw2c) rot_point(A.pts.rw2c, prow, d6, dr6);   // per-point Rw2c (agg_common.h)
+      if (GEN && A.pts.rw2c) rot_point(A.pts.rw2c, prow, d6, dr6);   // per-point Rw2c (agg_common.h)
       if (role == 0) {
         float vrot[3], drot[3];
         mat3(Rw, vd, vrot);
         mat3(Rw, pdir, drot);
-        if (A.pts.rw2c) {
+        if (GEN && A.pts.rw2c) {
           rot_point(A.pts.rw2c, prow, pdir, drot);
           rot_point(A.pts.rw2c, active ? slot0_point(A.s, row) : 0, vd, vrot);
         }
@@ -462,12 +503,12 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
         if (active && k < K) {
           // the bucket's dropped slots (KT..K-1) are empty: weight 0, their gathered conf
-          if (A.out_weight) {
+          if (GEN && A.out_weight) {
             A.out_weight[row * K + k] = wn;
             if (k == 0)
               for (int kk = KT; kk < K; ++kk) A.out_weight[row * K + kk] = 0.f;
           }
-          if (A.out_conf) {
+          if (GEN && A.out_conf) {
             A.out_conf[row * K + k] = confc;
             if (k == 0)
               for (int kk = KT; kk < K; ++kk) {
@@ -499,7 +540,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
       }
     }
+    PB_STAMP(2);
     __syncthreads();
+    PB_STAMP(3);
     // -------------------------------------------- P1 rows into the accumulators
     f32x16 acc[kBPT * 2];
 #pragma unroll
@@ -518,7 +561,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     }
     nx_v = pf_v(tile + gridDim.x);   // the next tile's chain, link 1
     // -------------------------------------------- block1: + W1[:, 224:284] . PE_5 (4 steps), block1.2
+    PB_STAMP(4);
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w1b, Xb, 4, lane);
+    PB_STAMP(5);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {
@@ -527,10 +572,12 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       tail_rows_b(Xb, kPB, lane + 64, 256, &one, 1);
     }
     __syncthreads();
+    PB_STAMP(6);
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     nx_row = pf_row(nx_v);   // link 2
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w2, Xb, 17, lane);
+    PB_STAMP(7);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263 (+ zeros to 271)
@@ -544,11 +591,14 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       }
     }
     __syncthreads();
+    PB_STAMP(8);
     // -------------------------------------------- block3
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     nx_pid = pf_pid(nx_row);   // link 3
+    nx_drow = pf_drow(nx_row);
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w3, Xb, 17, lane);
+    PB_STAMP(9);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {
@@ -557,9 +607,11 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       tail_rows_b(Xb, kPB, lane + 64, 256, &one, 1);
     }
     __syncthreads();
+    PB_STAMP(10);
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w4, Xb, 17, lane);
+    PB_STAMP(11);
     __syncthreads();   // Xb is free: the K-sums are staged there (hid rows, kHP pitch)
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
     {
@@ -660,6 +712,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 #pragma unroll
       for (int pt = 0; pt < kBPT; ++pt) apart[wid * kBT + 32 * pt + c] = pa_part[pt];
     }
+    PB_STAMP(12);
     __syncthreads();
     if (wid < 2) {
       const int col = 64 * wid + lane;
@@ -687,6 +740,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     }
     }
     __syncthreads();
+    PB_STAMP(13);
     // -------------------------------------------- colour branch on the tile's samples
     // [hid (K-summed, staged above), PE_4(view)] -> 128 -> 128 -> 128 (the
     // reference's color_branch, point_aggregators.py:640-646), columns = samples:
@@ -710,6 +764,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         for (int cc = lane; cc < NCc; cc += 64) tail_rows_b(Xb, kPB, cc, kC, &one, 1);
       }
       __syncthreads();
+      PB_STAMP(14);
 #pragma unroll
       for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
       mlp_layer_b<1, PTc, 4, kPB, 2>(cacc, wc2, Xb, 9, lane);
@@ -721,6 +776,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         for (int cc = lane; cc < NCc; cc += 64) tail_rows_b(Xb, kPB, cc, kC, &one, 1);
       }
       __syncthreads();
+      PB_STAMP(15);
 #pragma unroll
       for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
       mlp_layer_b<1, PTc, 4, kPB, 2>(cacc, wc3, Xb, 9, lane);
@@ -736,17 +792,34 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
           for (int i = 0; i < 4; ++i)
             Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(cacc[pt][4 * q + i], neg);
       __syncthreads();
+      PB_STAMP(16);
       typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
       for (int r2 = wid; r2 < SPT / 2; r2 += kBWaves) {
         const int r = 2 * r2 + (lane >> 5), l = lane & 31;
         if (tile * SPT + r >= n || !sflag[r]) continue;
         const float* src = Ob + r * kOPitch + 4 * l;
         const f4u v = {src[0], src[1], src[2], src[3]};
-        *reinterpret_cast<f4u*>(A.out_feat + (int64_t)vL[r] * (kC + 1) + 1 + 4 * l) = v;
+        __builtin_nontemporal_store(v, reinterpret_cast<f4u*>(A.out_feat + (int64_t)vL[r] * (kC + 1) + 1 + 4 * l));
       }
     }
     __syncthreads();
+    PB_STAMP(17);
   }
+}
+
+#ifdef PNR_PB_TRACE
+extern "C" __attribute__((visibility("default"))) int pnr_dev_pb_trace(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pb_trace), bytes) == hipSuccess ? 0 : 3;
+}
+#endif
+
+template <int KT>
+static void launch_pairs_b(bool gen, unsigned grid, hipStream_t st, const AggArgsB& a, const int32_t* list,
+                           const int32_t* info, int bucket) {
+  if (gen)
+    hipLaunchKernelGGL((k_pairs_b<KT, true>), dim3(grid), dim3(64 * kBWaves), kPairsBLds, st, a, list, info, bucket);
+  else
+    hipLaunchKernelGGL((k_pairs_b<KT, false>), dim3(grid), dim3(64 * kBWaves), kPairsBLds, st, a, list, info, bucket);
 }
 
 static size_t scratch_need_b(int64_t n_max, int64_t n_p1) {
@@ -791,13 +864,21 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre_b),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kBT * kPB * 2)));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<1>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<1, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<2>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<1, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<4>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<2, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<8>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<2, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<4, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<4, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<8, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_b<8, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairsBLds));
     attr = true;
   }
@@ -817,6 +898,8 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
                        kBT * kPB * 2, st, a);
     PNR_LAUNCH_CHECK();
   }
+  // the general path's branches only when a caller needs them
+  const bool gen = pts->rw2c || pts->used_map || out_weight || out_conf || s->ray_cam;
   if (w->pair_buckets) {
     // samples partitioned by filled slots, one launch per bucket (the heaviest first)
     PairBuckets bk;
@@ -824,17 +907,16 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
     if ((rc = launch_buckets(a.s, bk_scratch, &bk, st))) return rc;
     const unsigned g8 = grid_for(cdiv(nm, kBT / 8), 1, 256 * 2), g4 = grid_for(cdiv(nm, kBT / 4), 1, 256 * 2),
                    g2 = grid_for(cdiv(nm, kBT / 2), 1, 256 * 2), g1 = grid_for(cdiv(nm, kBT), 1, 256 * 2);
-    hipLaunchKernelGGL(k_pairs_b<8>, dim3(g8), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 3);
+    launch_pairs_b<8>(gen, g8, st, a, bk.list, bk.info, 3);
     PNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pairs_b<4>, dim3(g4), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 2);
+    launch_pairs_b<4>(gen, g4, st, a, bk.list, bk.info, 2);
     PNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pairs_b<2>, dim3(g2), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 1);
+    launch_pairs_b<2>(gen, g2, st, a, bk.list, bk.info, 1);
     PNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pairs_b<1>, dim3(g1), dim3(64 * kBWaves), kPairsBLds, st, a, bk.list, bk.info, 0);
+    launch_pairs_b<1>(gen, g1, st, a, bk.list, bk.info, 0);
     PNR_LAUNCH_CHECK();
   } else {
-    hipLaunchKernelGGL(k_pairs_b<8>, dim3(grid_for(cdiv(nm, kBT / 8), 1, 256 * 2)), dim3(64 * kBWaves), kPairsBLds,
-                       st, a, nullptr, nullptr, 3);
+    launch_pairs_b<8>(gen, grid_for(cdiv(nm, kBT / 8), 1, 256 * 2), st, a, nullptr, nullptr, 3);
     PNR_LAUNCH_CHECK();
   }
   return PNR_OK;
