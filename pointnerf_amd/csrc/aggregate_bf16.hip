@@ -293,11 +293,11 @@ constexpr int kOPitch = kC + 1;   // fp32 output staging pitch (odd: conflict-fr
 static_assert((size_t)kBT * kOPitch * 4 <= (size_t)kBT * kPB * 2, "output staging must fit the Xb tile");
 static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit the Xb pitch");
 
-// weight-ring depth of k_pairs_b's layers per tile shape (measured at c5, with
-// the colour branch fused: two steps ahead for the one-slot tiles, one for the
-// others -- 59.6 ms against 61.1 for one / compiler-scheduled)
+// weight-ring depth of k_pairs_b's layers (measured at c5 with the colour branch
+// fused and the render variant's branch-free gather: two steps ahead for every
+// tile shape, 58.9 ms against 60.1 with one step for KT > 1, alternating on one box)
 template <int KT>
-constexpr int kPairsWD = KT == 1 ? 2 : 1;
+constexpr int kPairsWD = 2;
 
 #ifdef PNR_PB_TRACE
 // diagnostic build only (tools/pb_trace.py): s_memtime per phase of the first 8
