@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
 constexpr size_t kPairsBLds =
     (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT + kBTSmax + 3 * kBTSmax) * 4;
-constexpr int kOPitch = kC + 1;   // fp32 output staging pitch (odd: conflict-free column writes)
+constexpr int kOPitch = kC + 4;   // fp32 output staging pitch: 16-B rows, an accumulator quad is one b128 write
 static_assert((size_t)kBT * kOPitch * 4 <= (size_t)kBT * kPB * 2, "output staging must fit the Xb tile");
 static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit the Xb pitch");
 
@@ -789,17 +789,17 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       for (int pt = 0; pt < PTc; ++pt)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            Ob[(32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q + i] = lrelu(cacc[pt][4 * q + i], neg);
+          *reinterpret_cast<float4*>(Ob + (32 * pt + c) * kOPitch + 32 * wid + 4 * h + 8 * q) =
+              make_float4(lrelu(cacc[pt][4 * q], neg), lrelu(cacc[pt][4 * q + 1], neg), lrelu(cacc[pt][4 * q + 2], neg),
+                          lrelu(cacc[pt][4 * q + 3], neg));
       __syncthreads();
       PB_STAMP(16);
       typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
       for (int r2 = wid; r2 < SPT / 2; r2 += kBWaves) {
         const int r = 2 * r2 + (lane >> 5), l = lane & 31;
         if (tile * SPT + r >= n || !sflag[r]) continue;
-        const float* src = Ob + r * kOPitch + 4 * l;
-        const f4u v = {src[0], src[1], src[2], src[3]};
+        const float4 s4 = *reinterpret_cast<const float4*>(Ob + r * kOPitch + 4 * l);
+        const f4u v = {s4.x, s4.y, s4.z, s4.w};
         __builtin_nontemporal_store(v, reinterpret_cast<f4u*>(A.out_feat + (int64_t)vL[r] * (kC + 1) + 1 + 4 * l));
       }
     }

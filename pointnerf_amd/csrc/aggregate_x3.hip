@@ -1050,7 +1050,7 @@ __global__ void __launch_bounds__(512, 1) k_pairs_h2_train(X3Args A) { pairs_bod
 constexpr int kCG = 18;                       // 8-row groups per half (144 rows)
 constexpr int kCPlane = kCG * kXT * 16;       // bytes per f16 plane
 constexpr size_t kColH2Lds = 2 * (size_t)kCPlane;
-constexpr int kOPitch = kC + 1;   // fp32 output staging pitch
+constexpr int kOPitch = kC + 4;   // fp32 output staging pitch: 16-B rows, an accumulator quad is one b128 write
 static_assert((size_t)kXT * kOPitch * 4 <= kColH2Lds, "output staging must fit the planes");
 
 struct ColH2Args {
@@ -1185,8 +1185,12 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int T = 0; T < 2; ++T)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          Ob[(32 * pt + c) * kOPitch + 32 * (T0 + T) + acc_row(r, h)] = lrelu(acc[2 * pt + T][r] * sc3, neg);
+        for (int q = 0; q < 4; ++q) {   // rows acc_row(4q .. 4q + 3, h): 4 consecutive neurons
+          const f32x16& a = acc[2 * pt + T];
+          *reinterpret_cast<float4*>(Ob + (32 * pt + c) * kOPitch + 32 * (T0 + T) + 8 * q + 4 * h) =
+              make_float4(lrelu(a[4 * q] * sc3, neg), lrelu(a[4 * q + 1] * sc3, neg), lrelu(a[4 * q + 2] * sc3, neg),
+                          lrelu(a[4 * q + 3] * sc3, neg));
+        }
     __syncthreads();
     for (int r = wid; r < kXT; r += 2) {
       if (!((vm >> r) & 1)) continue;
