@@ -135,6 +135,66 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_final(const int32_t* __rest
   }
 }
 
+// Two-launch variant for up to kScanDirect tiles (every query compaction and
+// grid-build scan at the bench sizes): each block sums the tile totals before it
+// itself (<= kScanDirect / 256 loads per thread) instead of a one-block scan of
+// the sums between the passes -- one dependent launch fewer per scan.  The
+// block holding the last element writes the grand total.
+constexpr int64_t kScanDirect = 2048;
+__global__ void __launch_bounds__(kScanBlock) k_scan_final_direct(const int32_t* __restrict__ in, int64_t n,
+                                                                  const int32_t* n_dev, int as_flag,
+                                                                  const int32_t* __restrict__ sums,
+                                                                  int32_t* __restrict__ out, int32_t* total_dev,
+                                                                  const int32_t* run_if) {
+  __shared__ int tile[kScanTile];
+  __shared__ int lds4[4];
+  if (run_if && *run_if == 0) return;
+  const int64_t ne = eff_len(n, n_dev);
+  const int64_t start = (int64_t)blockIdx.x * kScanTile;
+  if (ne == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      out[0] = 0;
+      if (total_dev) *total_dev = 0;
+    }
+    return;
+  }
+  if (start >= ne) return;
+  int pre = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += kScanBlock) pre += sums[i];
+  int pre_tot;
+  block_excl_scan(pre, lds4, &pre_tot);   // (block_excl_scan's barriers also order the tile loads below)
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = start + j * kScanBlock + threadIdx.x;
+    tile[j * kScanBlock + threadIdx.x] = load_item(in, i, ne, as_flag);
+  }
+  __syncthreads();
+  int v[kScanItems];
+  int acc = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    v[j] = tile[threadIdx.x * kScanItems + j];
+    acc += v[j];
+  }
+  int tot;
+  int base = block_excl_scan(acc, lds4, &tot) + pre_tot;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    tile[threadIdx.x * kScanItems + j] = base;
+    base += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    int64_t i = start + j * kScanBlock + threadIdx.x;
+    if (i < ne) out[i] = tile[j * kScanBlock + threadIdx.x];
+  }
+  if (start + kScanTile >= ne && threadIdx.x == 0) {   // the tile of the last element
+    out[ne] = pre_tot + tot;
+    if (total_dev) *total_dev = pre_tot + tot;
+  }
+}
+
 int64_t scan_blocks(int64_t n) { return cdiv(n > 0 ? n : 1, kScanTile); }
 
 size_t scan_scratch_bytes(int64_t n) { return (size_t)(scan_blocks(n) + 1) * sizeof(int32_t); }
@@ -151,6 +211,12 @@ int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* 
   int32_t* sums = static_cast<int32_t*>(scratch);
   hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, run_if);
   PNR_LAUNCH_CHECK();
+  if (nb <= kScanDirect) {
+    hipLaunchKernelGGL(k_scan_final_direct, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums,
+                       out, total_dev, run_if);
+    PNR_LAUNCH_CHECK();
+    return PNR_OK;
+  }
   hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanBlock), 0, st, sums, nb, n, n_dev, out, total_dev, run_if);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, out, run_if);
