@@ -310,21 +310,44 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
     }
     return kid < K ? kid : K;
   }
+  // Any layer count (truck: 3 layers, 125 cells).  Layer L visits x -> y -> z
+  // (qpiw.py:481-527) the cells of Chebyshev radius L: in a ring column
+  // (max(|x|, |y|) = L) the whole z-run [fz - L, fz + L], in an inner column its
+  // two end cells.  A run of consecutive cells is one record range in rank order
+  // (grid.hip "query index"), so a ring column costs one or two word loads and,
+  // only when it holds a point, one rec_off pair -- not a word load per cell.
   for (int layer = 0; layer < layers; ++layer) {
-    const int x0 = max(-fx, -layer), x1 = min(g.dims[0] - fx, layer + 1);
-    const int y0 = max(-fy, -layer), y1 = min(g.dims[1] - fy, layer + 1);
-    const int z0 = max(-fz, -layer), z1 = min(g.dims[2] - fz, layer + 1);
+    const int L = layer;
+    const int x0 = max(-fx, -L), x1 = min(g.dims[0] - fx, L + 1);
+    const int y0 = max(-fy, -L), y1 = min(g.dims[1] - fy, L + 1);
+    const int zr0 = max(fz - L, 0), zr1 = min(fz + L, g.dims[2] - 1);   // a ring column's run
     for (int x = x0; x < x1; ++x) {
       for (int y = y0; y < y1; ++y) {
-        for (int z = z0; z < z1; ++z) {
-          if (max(abs(z), max(abs(x), abs(y))) != layer) continue;
-          const int64_t cell = ((int64_t)(fx + x) * g.dims[1] + (fy + y)) * g.dims[2] + (fz + z);
-          const int r = held_rank(qi.words[cell >> 5], (int)(cell & 31));
-          if (r < 0) continue;
-          const int o = qi.rec_off[r];
-          const int cn = qi.rec_off[r + 1] - o;
+        const int64_t base = ((int64_t)(fx + x) * g.dims[1] + (fy + y)) * g.dims[2];
+        if (x == -L || x == L || y == -L || y == L) {
+          const int64_t ca = base + zr0, cb = base + zr1;
+          const uint2 wa = qi.words[ca >> 5];
+          const uint2 wb = (cb >> 5) == (ca >> 5) ? wa : qi.words[cb >> 5];
+          const int lo = (int)wa.y + __popc(wa.x & ((1u << (ca & 31)) - 1u));
+          const int hi = (int)wb.y + __popc(wb.x & ((1u << (cb & 31)) - 1u)) + (int)((wb.x >> (cb & 31)) & 1u);
+          if (hi == lo) continue;   // no held cell in the run
+          const int o = qi.rec_off[lo];
+          const int cn = qi.rec_off[hi] - o;
           n_cand += cn;
           knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {   // z = fz - L, then fz + L (inside the grid only)
+            const int z = e ? fz + L : fz - L;
+            if (z < 0 || z >= g.dims[2]) continue;
+            const int64_t cell = base + z;
+            const int r = held_rank(qi.words[cell >> 5], (int)(cell & 31));
+            if (r < 0) continue;
+            const int o = qi.rec_off[r];
+            const int cn = qi.rec_off[r + 1] - o;
+            n_cand += cn;
+            knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
+          }
         }
       }
     }
