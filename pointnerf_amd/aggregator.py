@@ -143,7 +143,7 @@ def frag_pack(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor
     return Wp.view(NT, 32, tot, 2).permute(2, 0, 3, 1).contiguous().view(-1)
 
 
-BF16_PAD = 4   # kBPad in aggregate_bf16.hip (mlp_layer_b loads up to 4 k-steps ahead)
+BF16_PAD = 6   # kBPad in aggregate_bf16.hip (mlp_layer_b loads up to 6 k-steps ahead)
 
 
 def frag_pack_bf16(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:

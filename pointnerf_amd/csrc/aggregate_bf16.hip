@@ -33,7 +33,7 @@ constexpr int kBPT = kBT / 32;           // 32-column quarters per tile
 constexpr int kBWaves = 4;
 constexpr int kPB = 280;                 // Xb pitch (bf16) for <= 272 input rows (k_pairs_b, k_point_pre_b)
 constexpr int kPBc = 296;                // Xb pitch for the colour branch (288 input rows)
-constexpr int kBPad = 4;                 // zero k-steps padded onto bf16 weight packs (the ring's lead)
+constexpr int kBPad = 6;                 // zero k-steps padded onto bf16 weight packs (the ring's lead)
 
 struct AggArgsB {
   pnr_points pts;
@@ -298,6 +298,9 @@ static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit
 // tile shape, 58.9 ms against 60.1 with one step for KT > 1, alternating on one box)
 template <int KT>
 constexpr int kPairsWD = 2;
+// colour layers' ring depth: one fragment per k-step (4 VGPRs a slot), so the
+// lead can be long (c5: 2 steps 55.0 ms, 4 steps 53.9, 6 steps 53.7)
+constexpr int kColWD = 6;
 
 #ifdef PNR_PB_TRACE
 // diagnostic build only (tools/pb_trace.py): s_memtime per phase of the first 8
@@ -756,7 +759,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       f32x16 cacc[PTc];
 #pragma unroll
       for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
-      mlp_layer_b<1, PTc, 4, kPB, 2, true>(cacc, wc1, Xb, 18, lane);
+      mlp_layer_b<1, PTc, 4, kPB, kColWD, true>(cacc, wc1, Xb, 18, lane);
       __syncthreads();
       store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
       if (wid == 0) {
@@ -768,7 +771,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       PB_STAMP(14);
 #pragma unroll
       for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
-      mlp_layer_b<1, PTc, 4, kPB, 2>(cacc, wc2, Xb, 9, lane);
+      mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc2, Xb, 9, lane);
       __syncthreads();
       store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
       if (wid == 0) {
@@ -780,7 +783,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       PB_STAMP(15);
 #pragma unroll
       for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
-      mlp_layer_b<1, PTc, 4, kPB, 2>(cacc, wc3, Xb, 9, lane);
+      mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc3, Xb, 9, lane);
       __syncthreads();   // every wave's layer-3 reads of Xb are done
       // out_feat rows (valid samples only) through LDS, two rows per store
       // instruction (lane half = row, 16 B per lane, rows 516 B apart: 4-B aligned)
