@@ -287,8 +287,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 // zero weights; the xor-tree and DPP reduce-scatter sums below pair the
 // remaining lanes exactly as the 8-lane trees do).
 constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
+// Xb | wtL | apart | sflag | exB (bf16) | prowL | vL | vrL | waL
 constexpr size_t kPairsBLds =
-    (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 8 * kBT + kBT + kBTSmax + 3 * kBTSmax) * 4;
+    (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 4 * kBT + kBT + kBTSmax + 3 * kBTSmax + kHid) * 4;
 constexpr int kOPitch = kC + 4;   // fp32 output staging pitch: 16-B rows, an accumulator quad is one b128 write
 static_assert((size_t)kBT * kOPitch * 4 <= (size_t)kBT * kPB * 2, "output staging must fit the Xb tile");
 static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit the Xb pitch");
@@ -329,10 +330,13 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   float* wtL = reinterpret_cast<float*>(Xb + kBT * kPB);   // [128]
   float* apart = wtL + kBT;                                // [4][128]
   int* sflag = reinterpret_cast<int*>(apart + 4 * kBT);    // [SPT]
-  float* exL = reinterpret_cast<float*>(sflag + kBTSmax);  // [8][128]
-  int* prowL = reinterpret_cast<int*>(exL + 8 * kBT);      // [128]
+  // block3.0's extra inputs, bf16 as they enter the GEMM (tail_rows_b rounds them
+  // the same way): half the LDS of fp32 rows, which leaves room for waL
+  uint16_t* exB = reinterpret_cast<uint16_t*>(sflag + kBTSmax);   // [8][128]
+  int* prowL = reinterpret_cast<int*>(exB + 8 * kBT);      // [128]
   int* vL = prowL + kBT;                                   // [SPT] sample index of each tile row
   float* vrL = reinterpret_cast<float*>(vL + kBTSmax);     // [3][SPT] rotated view dir of each sample
+  float* waL = vrL + 3 * kBTSmax;                          // [256] alpha_branch weights (loaded once)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar addressing
   const int c = lane & 31, h = lane >> 5;
   const int K = A.s.K;
@@ -374,6 +378,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   int nx_row = pf_row(nx_v);
   int nx_pid = pf_pid(nx_row);
   int nx_drow = pf_drow(nx_row);
+  waL[threadIdx.x] = A.w.wa[threadIdx.x];   // 256 threads, 256 weights (ordered by the tile's first barrier)
 #ifdef PNR_PB_TRACE
   int it_tr = -1;
 #endif
@@ -495,7 +500,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         const float ex[8] = {colr[0], colr[1], colr[2], drot[0] - vrot[0], drot[1] - vrot[1], drot[2] - vrot[2],
                              dot, 1.f};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) exL[e * kBT + col] = ex[e];
+        for (int e = 0; e < 8; ++e) exB[e * kBT + col] = to_bf16(ex[e]);
         wtL[col] = wn * confc;
         if (k == 0) {
           sflag[j] = active && samp_valid;
@@ -590,7 +595,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         const int col = lane + 64 * half;
         float ex[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ex[e] = exL[e * kBT + col];
+        for (int e = 0; e < 8; ++e) ex[e] = __uint_as_float((unsigned)exB[e * kBT + col] << 16);
         tail_rows_b(Xb, kPB, col, 256, ex, 8);
       }
     }
@@ -625,7 +630,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     for (int T = 0; T < 2; ++T) {
       float wa[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) wa[r] = A.w.wa[32 * (T0 + T) + acc_row(r, h)];
+      for (int r = 0; r < 16; ++r) wa[r] = waL[32 * (T0 + T) + acc_row(r, h)];
 #pragma unroll
       for (int pt = 0; pt < kBPT; ++pt) {
         const int col = 32 * pt + c;
