@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 19
+#define PNR_ABI_VERSION 20
 
 enum {
   PNR_OK = 0,
@@ -338,6 +338,17 @@ int pnr_aggregate_scratch_bytes_bf16(int64_t n_max, int64_t n_points, size_t* ou
 int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
                            float* out_feat, float* out_weight, float* out_conf, void* scratch,
                            size_t scratch_bytes, void* stream);
+
+/* Same (v20), with the aggregated features themselves in bf16 -- config c5's
+ * bf16 path end to end, half the feature bytes written here and read by the
+ * composite.  out_feat_h: rows of PNR_FEAT_H_PITCH uint16 (272 B, 16-B aligned)
+ * = [alpha as one fp32 in slots 0-1 | slots 2-7 unused | 128 bf16 features in
+ * slots 8..135, each the round-to-nearest-even of pnr_aggregate_fwd_bf16's
+ * fp32 value].  Read by pnr_composite_fwd_hf. */
+#define PNR_FEAT_H_PITCH 136
+int pnr_aggregate_fwd_bf16_hf(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
+                              uint16_t* out_feat_h, float* out_weight, float* out_conf, void* scratch,
+                              size_t scratch_bytes, void* stream);
 
 /* fp32-accurate aggregation on bf16 MFMA (same contract and scratch as
  * pnr_aggregate_fwd).  Each fp32 GEMM operand is split exactly into three bf16
@@ -679,6 +690,13 @@ int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q,
                       const pnr_query_bufs* b, const pnr_composite_params* c,
                       const float* feat, float* ray_color, float* opacity,
                       float* is_bg, int8_t* ray_mask, void* stream);
+
+/* pnr_composite_fwd on pnr_aggregate_fwd_bf16_hf's rows (v20; c->C even, <= 128):
+ * the same blend in fp32 from bf16 features and the fp32 alpha. */
+int pnr_composite_fwd_hf(const pnr_rays* rays, const pnr_query_params* q,
+                         const pnr_query_bufs* b, const pnr_composite_params* c,
+                         const uint16_t* feat_h, float* ray_color, float* opacity,
+                         float* is_bg, int8_t* ray_mask, void* stream);
 
 /* ray_march on dense inputs (diff_ray_marching.py:509-555, radiance_render,
  * alpha_blend): ray_dist[NR,SR], ray_valid[NR,SR] (uint8), feat[NR,SR,C+1],

@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 19
+ABI_VERSION = 20
+FEAT_H_PITCH = 136   # PNR_FEAT_H_PITCH: uint16 per bf16 feature row (pnr_aggregate_fwd_bf16_hf)
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
 
@@ -172,6 +173,8 @@ SIGNATURES = {
     "pnr_aggregate_scratch_bytes_bf16": (c_int, [c_int64, c_int64, P(c_size_t)]),
     "pnr_aggregate_fwd_bf16": (c_int, [P(Points), P(Samples), P(MlpBf16), c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_size_t, c_void_p]),
+    "pnr_aggregate_fwd_bf16_hf": (c_int, [P(Points), P(Samples), P(MlpBf16), c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train": (c_int, [P(Points), P(Samples), P(Mlp), P(AggSaved), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
     "pnr_aggregate_fwd_train_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpX3), P(AggSaved), c_void_p,
@@ -239,6 +242,8 @@ SIGNATURES = {
                               c_void_p, c_void_p]),
     "pnr_composite_fwd": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams),
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_composite_fwd_hf": (c_int, [P(Rays), P(QueryParams), P(QueryBufs), P(CompositeParams),
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_ray_march_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_neural_render_scratch_bytes": (c_int, [c_int32, c_int32, P(c_size_t)]),

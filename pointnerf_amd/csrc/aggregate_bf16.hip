@@ -40,7 +40,8 @@ struct AggArgsB {
   pnr_samples s;
   pnr_mlp_bf16 w;
   uint16_t* p1;      // [n_p1, 256] bf16 per-point block1.0 partial, accumulator order
-  float* out_feat;
+  float* out_feat;     // [n, C + 1] fp32 rows, or
+  uint16_t* out_feat_h;   // [n, PNR_FEAT_H_PITCH]: alpha fp32 (slots 0-1), C bf16 from slot 8
   float* out_weight;
   float* out_conf;
 };
@@ -730,7 +731,12 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const float alpha_k = A.w.act_super ? softplus(pa - 1.f) : fmaxf(pa, 0.f);
       const float alpha_s = xork_sum_nc<KT>(wtL[col] * alpha_k);
       const int64_t jv = tile * SPT + j;
-      if (k == 0 && jv < n && sflag[j]) A.out_feat[(int64_t)vL[j] * (kC + 1)] = alpha_s;
+      if (k == 0 && jv < n && sflag[j]) {
+        if (A.out_feat_h)
+          *reinterpret_cast<float*>(A.out_feat_h + (int64_t)vL[j] * PNR_FEAT_H_PITCH) = alpha_s;
+        else
+          A.out_feat[(int64_t)vL[j] * (kC + 1)] = alpha_s;
+      }
     } else if (threadIdx.x - 128 < SPT) {
       // colour-branch inputs 256 .. 279 of sample j: PE_4 of the rotated view dir
       // (ori dropped; masked samples: 0) -- rows 256 + 4 ch + f sin, 268 + 4 ch + f cos
@@ -807,8 +813,15 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         const int r = 2 * r2 + (lane >> 5), l = lane & 31;
         if (tile * SPT + r >= n || !sflag[r]) continue;
         const float4 s4 = *reinterpret_cast<const float4*>(Ob + r * kOPitch + 4 * l);
-        const f4u v = {s4.x, s4.y, s4.z, s4.w};
-        __builtin_nontemporal_store(v, reinterpret_cast<f4u*>(A.out_feat + (int64_t)vL[r] * (kC + 1) + 1 + 4 * l));
+        if (A.out_feat_h) {   // bf16 rows: 8 B per lane, a 272-B row per lane half
+          typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+          const u32x2v hv = {pack_bf16x2(s4.x, s4.y), pack_bf16x2(s4.z, s4.w)};
+          __builtin_nontemporal_store(hv, reinterpret_cast<u32x2v*>(A.out_feat_h + (int64_t)vL[r] * PNR_FEAT_H_PITCH +
+                                                                    8 + 4 * l));
+        } else {
+          const f4u v = {s4.x, s4.y, s4.z, s4.w};
+          __builtin_nontemporal_store(v, reinterpret_cast<f4u*>(A.out_feat + (int64_t)vL[r] * (kC + 1) + 1 + 4 * l));
+        }
       }
     }
     __syncthreads();
@@ -848,10 +861,11 @@ extern "C" int pnr_aggregate_scratch_bytes_bf16(int64_t n_max, int64_t n_points,
   return PNR_OK;
 }
 
-extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
-                                      float* out_feat, float* out_weight, float* out_conf, void* scratch,
-                                      size_t scratch_bytes, void* stream) {
-  PNR_CHECK_ARG(pts && s && w && out_feat, "aggregate_bf16: null pointer");
+static int aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w, float* out_feat,
+                              uint16_t* out_feat_h, float* out_weight, float* out_conf, void* scratch,
+                              size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(pts && s && w && (out_feat || out_feat_h), "aggregate_bf16: null pointer");
+  PNR_CHECK_ARG(((uintptr_t)out_feat_h & 15) == 0, "aggregate_bf16_hf: out_feat_h must be 16-B aligned");
   PNR_CHECK_ARG(pts->xyz && (pts->emb || pts->emb_bf16) && s->pidx, "aggregate_bf16: point xyz/emb and pidx required");
   PNR_CHECK_ARG(s->sample_w && s->sample_p && s->dirs && s->dir_div >= 1, "aggregate_bf16: sample arrays required");
   PNR_CHECK_ARG(s->K >= 1 && s->K <= kKN, "aggregate_bf16: K=%d unsupported (1..8)", s->K);
@@ -900,6 +914,7 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
   a.p1 = static_cast<uint16_t*>(scratch);
   int32_t* bk_scratch = reinterpret_cast<int32_t*>(a.p1 + (n_p1 > 0 ? n_p1 : 1) * kHid);
   a.out_feat = out_feat;
+  a.out_feat_h = out_feat_h;
   a.out_weight = out_weight;
   a.out_conf = out_conf;
   if (!pts->p1_ready) {
@@ -929,4 +944,18 @@ extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* 
     PNR_LAUNCH_CHECK();
   }
   return PNR_OK;
+}
+
+extern "C" int pnr_aggregate_fwd_bf16(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
+                                      float* out_feat, float* out_weight, float* out_conf, void* scratch,
+                                      size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(out_feat, "aggregate_bf16: null out_feat");
+  return aggregate_fwd_bf16(pts, s, w, out_feat, nullptr, out_weight, out_conf, scratch, scratch_bytes, stream);
+}
+
+extern "C" int pnr_aggregate_fwd_bf16_hf(const pnr_points* pts, const pnr_samples* s, const pnr_mlp_bf16* w,
+                                         uint16_t* out_feat_h, float* out_weight, float* out_conf, void* scratch,
+                                         size_t scratch_bytes, void* stream) {
+  PNR_CHECK_ARG(out_feat_h, "aggregate_bf16_hf: null out_feat_h");
+  return aggregate_fwd_bf16(pts, s, w, nullptr, out_feat_h, out_weight, out_conf, scratch, scratch_bytes, stream);
 }

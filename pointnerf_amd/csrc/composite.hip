@@ -19,6 +19,9 @@ constexpr int kCBlock = 256;
 // feature rows in flight per ray (a ray has ~8 valid samples; A/B: 4 rows 0.94 ms,
 // 8 rows 0.93, 16 rows 1.12 on the bench frame, identical checksums)
 constexpr int kCRows = 8;
+#ifndef PNR_HF_ROWS
+#define PNR_HF_ROWS 8
+#endif
 
 __device__ __forceinline__ float wave_max_scan_incl(float v) {
   const int lane = threadIdx.x & 63;
@@ -87,6 +90,7 @@ struct CompArgs {
   const int32_t* valid_off;
   const float* sample_p;
   const float* feat;
+  const uint16_t* feat_h;   // pnr_composite_fwd_hf: bf16 rows (PNR_FEAT_H_PITCH) instead of feat
   int64_t feat_rows;   // rows of feat: valid samples at or past it are not read (capacity overflow)
   float vsize_z;
   int unit;
@@ -112,7 +116,11 @@ __device__ float origin_depth(const CompArgs& a, int64_t cam) {
   return pc[2];
 }
 
+// HF: features from pnr_aggregate_fwd_bf16_hf's bf16 rows -- lane l holds
+// channels 2l and 2l + 1 (one 4-B load per row), alpha the row's fp32 head.
+template <bool HF>
 __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
+  constexpr int NRW = HF ? PNR_HF_ROWS : kCRows;   // feature rows in flight (bf16 rows: 4 B per lane each)
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -144,7 +152,10 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
       const bool val = filled && a.vflag[i];
       vrow[q] = val ? a.valid_off[i] : -1;
       if (vrow[q] >= a.feat_rows) vrow[q] = -1;   // capacity overflow: the caller re-renders
-      sig[q] = vrow[q] >= 0 ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
+      if constexpr (HF)
+        sig[q] = vrow[q] >= 0 ? *reinterpret_cast<const float*>(a.feat_h + (int64_t)vrow[q] * PNR_FEAT_H_PITCH) : 0.f;
+      else
+        sig[q] = vrow[q] >= 0 ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
     }
     // cummax over slots (neural_points_volumetric_model.py:293)
     float cm0 = wave_max_scan_incl(z[0]);
@@ -168,15 +179,15 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
     if (lane + 64 < SR) a.opacity[r * SR + lane + 64] = so.op1;
     const float w0 = so.op0 * so.T0, w1 = so.op1 * so.T1;
     // colour = sum_s w_s * features[s, 1:] + bg * T_bg  (lane = channel)
-    // valid slots in slot order, kCRows feature rows in flight per iteration
+    // valid slots in slot order, NRW feature rows in flight per iteration
     // (same accumulation order as a plain slot loop)
     float col0 = 0.f, col1 = 0.f;
     unsigned long long m0 = __ballot(vrow[0] >= 0), m1 = __ballot(vrow[1] >= 0);
     while (m0 | m1) {
-      int vr[kCRows];
-      float w[kCRows];
+      int vr[NRW];
+      float w[NRW];
 #pragma unroll
-      for (int u = 0; u < kCRows; ++u) {
+      for (int u = 0; u < NRW; ++u) {
         vr[u] = -1;
         w[u] = 0.f;
         if (m0) {
@@ -191,24 +202,44 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
           w[u] = __shfl(w1, src);
         }
       }
-      float f0[kCRows], f1[kCRows];
+      float f0[NRW], f1[NRW];
 #pragma unroll
-      for (int u = 0; u < kCRows; ++u) {
-        const float* f = a.feat + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * CF + 1;
-        f0[u] = (vr[u] >= 0 && lane < C) ? f[lane] : 0.f;
-        f1[u] = (vr[u] >= 0 && lane + 64 < C) ? f[lane + 64] : 0.f;
+      for (int u = 0; u < NRW; ++u) {
+        if constexpr (HF) {
+          const uint32_t* f = reinterpret_cast<const uint32_t*>(
+              a.feat_h + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * PNR_FEAT_H_PITCH + 8);
+          const uint32_t v = (vr[u] >= 0 && 2 * lane < C) ? f[lane] : 0u;
+          f0[u] = __uint_as_float(v << 16);            // channel 2 lane
+          f1[u] = __uint_as_float(v & 0xffff0000u);    // channel 2 lane + 1
+        } else {
+          const float* f = a.feat + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * CF + 1;
+          f0[u] = (vr[u] >= 0 && lane < C) ? f[lane] : 0.f;
+          f1[u] = (vr[u] >= 0 && lane + 64 < C) ? f[lane + 64] : 0.f;
+        }
       }
 #pragma unroll
-      for (int u = 0; u < kCRows; ++u) {
+      for (int u = 0; u < NRW; ++u) {
         if (vr[u] < 0) break;
         col0 += w[u] * f0[u];
         col1 += w[u] * f1[u];
       }
     }
-    for (int c = lane, q = 0; c < C; c += 64, ++q) {
-      float v = q == 0 ? col0 : (q == 1 ? col1 : 0.f);
-      if (a.bg) v += a.bg[c] * so.bgT;
-      a.ray_color[r * C + c] = v;
+    if constexpr (HF) {
+      if (2 * lane < C) {
+        float v0 = col0, v1 = col1;
+        if (a.bg) {
+          v0 += a.bg[2 * lane] * so.bgT;
+          v1 += a.bg[2 * lane + 1] * so.bgT;
+        }
+        a.ray_color[r * C + 2 * lane] = v0;
+        a.ray_color[r * C + 2 * lane + 1] = v1;
+      }
+    } else {
+      for (int c = lane, q = 0; c < C; c += 64, ++q) {
+        float v = q == 0 ? col0 : (q == 1 ? col1 : 0.f);
+        if (a.bg) v += a.bg[c] * so.bgT;
+        a.ray_color[r * C + c] = v;
+      }
     }
     if (lane == 0) {
       a.is_bg[r] = so.bgT;
@@ -620,10 +651,9 @@ __global__ void __launch_bounds__(kCBlock) k_march_aux(AuxArgs a) {
 
 using namespace pnr;
 
-extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q,
-                                 const pnr_query_bufs* b, const pnr_composite_params* c,
-                                 const float* feat, float* ray_color, float* opacity, float* is_bg,
-                                 int8_t* ray_mask, void* stream) {
+static int composite_fwd(const pnr_rays* rays, const pnr_query_params* q, const pnr_query_bufs* b,
+                         const pnr_composite_params* c, const float* feat, const uint16_t* feat_h, float* ray_color,
+                         float* opacity, float* is_bg, int8_t* ray_mask, void* stream) {
   PNR_CHECK_ARG(rays && q && b && c && ray_color && opacity && is_bg && ray_mask,
                 "composite: null pointer");
   PNR_CHECK_ARG(rays->campos_dev && rays->camrot_dev, "composite: camera required");
@@ -643,6 +673,7 @@ extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q
   a.valid_off = b->valid_off;
   a.sample_p = b->sample_p;
   a.feat = feat;
+  a.feat_h = feat_h;
   a.feat_rows = c->feat_rows > 0 ? c->feat_rows : INT64_MAX;
   a.vsize_z = c->vsize_z;
   a.unit = c->raydist_mode_unit;
@@ -653,9 +684,28 @@ extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q
   a.is_bg = is_bg;
   a.ray_mask = ray_mask;
   const unsigned grid = grid_for(rays->R * 64, kCBlock, 256 * 16);
-  hipLaunchKernelGGL(k_composite, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
+  if (feat_h)
+    hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(kCBlock), 0, as_stream(stream), a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
+}
+
+extern "C" int pnr_composite_fwd(const pnr_rays* rays, const pnr_query_params* q,
+                                 const pnr_query_bufs* b, const pnr_composite_params* c,
+                                 const float* feat, float* ray_color, float* opacity, float* is_bg,
+                                 int8_t* ray_mask, void* stream) {
+  return composite_fwd(rays, q, b, c, feat, nullptr, ray_color, opacity, is_bg, ray_mask, stream);
+}
+
+extern "C" int pnr_composite_fwd_hf(const pnr_rays* rays, const pnr_query_params* q,
+                                    const pnr_query_bufs* b, const pnr_composite_params* c,
+                                    const uint16_t* feat_h, float* ray_color, float* opacity, float* is_bg,
+                                    int8_t* ray_mask, void* stream) {
+  PNR_CHECK_ARG(feat_h && c && (c->C % 2) == 0, "composite_hf: feat_h required, C even");
+  PNR_CHECK_ARG(((uintptr_t)feat_h & 15) == 0, "composite_hf: feat_h must be 16-B aligned");
+  return composite_fwd(rays, q, b, c, nullptr, feat_h, ray_color, opacity, is_bg, ray_mask, stream);
 }
 
 extern "C" int pnr_ray_march_fwd(const float* ray_dist, const uint8_t* ray_valid, const float* feat,

@@ -157,6 +157,7 @@ class _RenderState:
         self.scratch_key = None
         self.side = None   # fp32h2: the side stream P1 runs on
         self.feat = None   # decoded features [rows, 129], reused by every call on this stream
+        self.feat_h = None   # bf16 precision: the same as bf16 rows [rows, L.FEAT_H_PITCH] (uint16)
 
     def feat_rows(self, rows: int, dev) -> torch.Tensor:
         """[rows, 129] view of the persistent feature buffer.  The calls of one
@@ -170,6 +171,15 @@ class _RenderState:
             self.feat = None
             self.feat = torch.empty((max(rows, int(1.5 * old)), 129), dtype=torch.float32, device=dev)
         return self.feat[:rows]
+
+    def feat_h_rows(self, rows: int, dev) -> torch.Tensor:
+        """feat_rows for pnr_aggregate_fwd_bf16_hf's bf16 feature rows."""
+        rows = max(int(rows), 1)
+        if self.feat_h is None or self.feat_h.shape[0] < rows or self.feat_h.device != dev:
+            old = 0 if self.feat_h is None else self.feat_h.shape[0]
+            self.feat_h = None
+            self.feat_h = torch.empty((max(rows, int(1.5 * old)), L.FEAT_H_PITCH), dtype=torch.int16, device=dev)
+        return self.feat_h[:rows]
 
 
 def _counts_dict(c):
@@ -276,6 +286,9 @@ class NeuralPointsRayMarching(nn.Module):
         self.train_precision = "fp32h2"
         self.p1_side_stream = True        # fp32h2 sync-free calls: P1 beside the query (see _render_rays)
         self.p1_used_only = True          # bf16: P1 for the referenced points only (see _render_rays)
+        # bf16: the aggregated features themselves in bf16 (pnr_aggregate_fwd_bf16_hf ->
+        # pnr_composite_fwd_hf: half the feature bytes written and read)
+        self.bf16_features = True
         self.p1_side_max_points_per_ray = 4.0
         self.keep_train_saved = False   # tests: last_train_aux["saved"] = the forward's kept activations
         # render_rays_train sizes its per-sample buffers for every slot of the batch while
@@ -641,7 +654,8 @@ class NeuralPointsRayMarching(nn.Module):
             else:
                 Sv = min(int((r1 - r0) * capacity) + 1024, (r1 - r0) * SR)
                 rec["caps"].append((Sv, r1 - r0))
-            feat = state.feat_rows(Sv, dev)
+            hf = bf16 and C == 128 and self.bf16_features
+            feat = state.feat_h_rows(Sv, dev) if hf else state.feat_rows(Sv, dev)
             s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
                           bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(),
                           bufs.fill_rs.data_ptr(), SR, K, L.ptr(rc))
@@ -663,9 +677,9 @@ class NeuralPointsRayMarching(nn.Module):
                 ready = True
             pts.p1_ready = int(ready)
             if bf16:
-                L.check(L.lib().pnr_aggregate_fwd_bf16(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
-                                                       L.ptr(feat), None, None, L.ptr(scratch), scratch.numel() * 4,
-                                                       L.stream_ptr(dev)),
+                fn = L.lib().pnr_aggregate_fwd_bf16_hf if hf else L.lib().pnr_aggregate_fwd_bf16
+                L.check(fn(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp), L.ptr(feat), None, None,
+                           L.ptr(scratch), scratch.numel() * 4, L.stream_ptr(dev)),
                         "pnr_aggregate_fwd_bf16")
             elif precision == "fp32x3":
                 L.check(L.lib().pnr_aggregate_fwd_x3(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp),
@@ -686,10 +700,10 @@ class NeuralPointsRayMarching(nn.Module):
                 feat = self.aggregator.apply_rgb_head(feat, n_dev=bufs.counts[1:2], n=Sv)
             e3 = mark()
             cp = L.CompositeParams(float(opt.vsize[2]), int(opt.raydist_mode_unit), C, L.ptr(bg), max(Sv, 1))
-            L.check(L.lib().pnr_composite_fwd(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c),
-                                              L.ctypes.byref(cp), L.ptr(feat), L.ptr(ray_color[r0:r1]),
-                                              L.ptr(opacity[r0:r1]), L.ptr(is_bg[r0:r1]),
-                                              L.ptr(ray_mask[r0:r1]), L.stream_ptr(dev)),
+            comp = L.lib().pnr_composite_fwd_hf if hf else L.lib().pnr_composite_fwd
+            L.check(comp(L.ctypes.byref(rays), L.ctypes.byref(qp), L.ctypes.byref(bufs.c), L.ctypes.byref(cp),
+                         L.ptr(feat), L.ptr(ray_color[r0:r1]), L.ptr(opacity[r0:r1]), L.ptr(is_bg[r0:r1]),
+                         L.ptr(ray_mask[r0:r1]), L.stream_ptr(dev)),
                     "pnr_composite_fwd")
             if rec is not None:
                 if record:

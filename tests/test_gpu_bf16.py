@@ -215,3 +215,61 @@ def test_bf16_render_variant_equals_general(cuda, flags):
         # the bf16 operands of the next GEMM can round either way
         assert rel <= 1e-5 and frac <= 0.01, (bk, frac, rel)   # measured: 1e-7, 4e-4
         assert int(torch.isfinite(outs[0][:, 0]).sum()) > 1000
+
+
+@pytest.mark.parametrize("flags", ["truck", "lego"])
+def test_bf16_feature_rows_are_rounded_fp32_rows(cuda, flags):
+    """pnr_aggregate_fwd_bf16_hf (ABI 20): the alpha of every written row equals
+    pnr_aggregate_fwd_bf16's bitwise, each feature is the round-to-nearest-even
+    bf16 of its fp32 feature, and the unwritten rows are the same."""
+    from pointnerf_amd import _lib as L
+    from scenes import flag_scene
+    sc = flag_scene(flags, n_points=60000 if flags == "truck" else 30000, H=64, view=0)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.6))
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda).contiguous()
+    bufs, hp, rays, qp = np_.querier.run(np_.xyz.detach(), rd, cp, cr, sc["near"], sc["far"])
+    cnt = bufs.read_counts()
+    Sv, K = cnt["S_valid"], sc["opt"].K
+    s = L.Samples(bufs.valid_list.data_ptr(), bufs.counts.data_ptr() + 4, Sv, bufs.pidx.data_ptr(),
+                  bufs.sample_w.data_ptr(), bufs.sample_p.data_ptr(), rd.data_ptr(), bufs.fill_rs.data_ptr(),
+                  sc["opt"].SR, K)
+    pts, keep = np_.tables(cp, cr)
+    mlp16, _k = agg.packed_bf16()
+    f = torch.full((Sv, 129), float("nan"), device=cuda)
+    fh = torch.full((Sv, L.FEAT_H_PITCH), -1, dtype=torch.int16, device=cuda)
+    for fn, out in ((L.lib().pnr_aggregate_fwd_bf16, f), (L.lib().pnr_aggregate_fwd_bf16_hf, fh)):
+        scr = L.aggregate_scratch_bf16(Sv, pts.n, cuda)
+        L.check(fn(L.ctypes.byref(pts), L.ctypes.byref(s), L.ctypes.byref(mlp16), L.ptr(out), None, None, L.ptr(scr),
+                   scr.numel() * 4, L.stream_ptr(cuda)), "bf16")
+    torch.cuda.synchronize()
+    written = ~torch.isnan(f[:, 0])
+    assert int(written.sum()) > 1000
+    assert torch.equal(~torch.isnan(f[:, 1:]).any(1), written)
+    alpha_h = fh[:, :2].contiguous().view(torch.float32)[:, 0]
+    assert torch.equal(alpha_h[written], f[written, 0])
+    assert bool((fh[~written, :2] == -1).all())   # rows the kernel skipped stay untouched
+    want = f[written, 1:].to(torch.bfloat16).view(torch.int16)
+    assert torch.equal(fh[written, 8:8 + 128], want)
+
+
+def test_bf16_render_with_bf16_features(cuda):
+    """The bf16 render path with bf16 feature rows (pnr_composite_fwd_hf) against
+    the same path with fp32 rows: one feature rounding apart (<= 2^-8 relative
+    per feature, blended in fp32)."""
+    from pointnerf_amd.renderer import NeuralPointsRayMarching
+    from scenes import flag_scene
+    sc = flag_scene("truck", n_points=60000, H=64, view=0)
+    agg, np_ = _setup(sc, cuda, formula_params(salt=0.6))
+    m = NeuralPointsRayMarching(sc["opt"], np_, agg, precision="bf16")
+    cp, cr = torch.from_numpy(sc["campos"]).to(cuda), torch.from_numpy(sc["camrot"]).to(cuda)
+    rd = torch.from_numpy(sc["raydir"]).to(cuda).contiguous()
+    bg = torch.rand(128, generator=torch.Generator().manual_seed(3)).to(cuda)
+    outs = []
+    for hf in (False, True):
+        m.bf16_features = hf
+        outs.append([t.clone() for t in m.render_rays(cp, cr, rd, sc["near"], sc["far"], bg)])
+    (c0, o0, b0, k0), (c1, o1, b1, k1) = outs
+    assert torch.equal(k0, k1) and torch.equal(o0, o1) and torch.equal(b0, b1)   # alpha path unchanged
+    d = (c0 - c1).abs()
+    assert float(d.max()) <= 2 ** -7 * float(c0.abs().max()), float(d.max())
