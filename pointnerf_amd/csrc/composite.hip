@@ -19,9 +19,6 @@ constexpr int kCBlock = 256;
 // feature rows in flight per ray (a ray has ~8 valid samples; A/B: 4 rows 0.94 ms,
 // 8 rows 0.93, 16 rows 1.12 on the bench frame, identical checksums)
 constexpr int kCRows = 8;
-#ifndef PNR_HF_ROWS
-#define PNR_HF_ROWS 8
-#endif
 
 __device__ __forceinline__ float wave_max_scan_incl(float v) {
   const int lane = threadIdx.x & 63;
@@ -120,7 +117,7 @@ __device__ float origin_depth(const CompArgs& a, int64_t cam) {
 // channels 2l and 2l + 1 (one 4-B load per row), alpha the row's fp32 head.
 template <bool HF>
 __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
-  constexpr int NRW = HF ? PNR_HF_ROWS : kCRows;   // feature rows in flight (bf16 rows: 4 B per lane each)
+  constexpr int NRW = kCRows;   // feature rows in flight (bf16 rows too: 12 / 16 measured slower at c5)
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
