@@ -511,7 +511,8 @@ int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples* s, const p
                             float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                             float* d_dir, float* d_conf, void* stream);
 /* The points referenced by a query's neighbour rows (pnr_points.used /
- * used_map for a training batch): flags[n_points] (scratch), used_map[p] = rank
+ * used_map for a training batch): flags[n_points] (scratch, 16-B aligned,
+ * as is scratch: a byte and a bit per point), used_map[p] = rank
  * of p among the referenced points or -1, used[0 .. *n_used_dev) = the referenced
  * points ascending; rows pidx[0 .. (*n_samples_dev) * K) (n_samples_dev NULL:
  * cap_samples).  No host synchronisation (the count stays on the device). */

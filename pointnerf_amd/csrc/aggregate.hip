@@ -1352,25 +1352,54 @@ __global__ void k_point_counts(const int32_t* __restrict__ pidx, const int32_t* 
   }
 }
 
-// pnr_used_points: flag the points referenced by the first (*n_dev) samples'
-// neighbour rows, rank them (scan), list them in ascending order.
+// pnr_used_points: a byte per point marked by plain stores (20 MB at c5's 20 M
+// points, where an int32 flag per point was 80 MB of randomly touched lines;
+// bit atomics measured slower: each drops its line from the XCD's L2), packed
+// to one bit per point with the words' popcounts, ranked by a scan of those.
+// The read comes before the store: neighbouring samples share most points, so
+// nearly every flag is already set and stays a cached read.
 __global__ void k_mark_used(const int32_t* __restrict__ pidx, const int32_t* __restrict__ n_dev, int K, int64_t cap,
-                            int32_t* __restrict__ flags) {
+                            uint8_t* __restrict__ flags) {
   const int64_t n = (n_dev ? (int64_t)*n_dev : cap) * K;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t p = pidx[i];
-    // read before write: neighbouring samples share most points, so nearly every
-    // flag is already set and stays a cached read instead of a partial-line write
     if (p >= 0 && flags[p] == 0) flags[p] = 1;
   }
 }
 
-__global__ void k_used_list(const int32_t* __restrict__ flags, int64_t n_points, int32_t* __restrict__ used_map,
-                            int32_t* __restrict__ used) {
+// word w of the bitset from flags[32w .. 32w+32) (two 16-B loads; the byte array
+// is padded to whole words), cnt[w] = its popcount
+__global__ void k_pack_used(const uint8_t* __restrict__ flags, int64_t nw, uint32_t* __restrict__ bits,
+                            int32_t* __restrict__ cnt) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const uint4* f = reinterpret_cast<const uint4*>(flags + w * 32);
+    const uint4 a = f[0], b = f[1];
+    const uint32_t q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= ((q[j] >> (8 * k)) & 1u) << (4 * j + k);
+    bits[w] = m;
+    cnt[w] = __popc(m);
+  }
+}
+
+// used_map[p] = rank of p (word prefix + set bits below p in its word) or -1;
+// used[rank] = p.
+__global__ void k_used_list(const uint32_t* __restrict__ bits, const int32_t* __restrict__ wpre, int64_t n_points,
+                            int32_t* __restrict__ used_map, int32_t* __restrict__ used) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n_points;
        p += (int64_t)gridDim.x * blockDim.x) {
-    if (flags[p]) used[used_map[p]] = (int32_t)p;
-    else used_map[p] = -1;
+    const uint32_t word = bits[p >> 5];
+    const int b = (int)(p & 31);
+    if ((word >> b) & 1u) {
+      const int32_t r = wpre[p >> 5] + __popc(word & ((1u << b) - 1u));
+      used_map[p] = r;
+      used[r] = (int32_t)p;
+    } else {
+      used_map[p] = -1;
+    }
   }
 }
 
@@ -2263,27 +2292,53 @@ extern "C" int pnr_aggregate_bwd_xyz(const pnr_points* pts, const pnr_samples* s
   return PNR_OK;
 }
 
+// flags: the bytes [32 * nw] | the bitset [nw] (fits the caller's int32 [n_points]
+// only from 64 points up: below, both live in scratch); scratch: the word prefix
+// [nw + 1] | (small n: bytes + bits) | the scan's scratch, each 16-B padded
+static size_t pad16(size_t b) { return (b + 15) & ~(size_t)15; }
+static bool used_small(int64_t n_points) { return cdiv(n_points, 32) * 36 > n_points * 4; }
+static size_t used_head_bytes(int64_t n_points) {
+  const int64_t nw = cdiv(n_points, 32);
+  return pad16((size_t)(nw + 1) * 4) + (used_small(n_points) ? pad16((size_t)nw * 36) : 0);
+}
+
 extern "C" int pnr_used_points_scratch_bytes(int64_t n_points, size_t* out) {
   PNR_CHECK_ARG(out && n_points >= 0, "used_points_scratch_bytes: bad args");
-  *out = scan_scratch_bytes(n_points);
+  *out = used_head_bytes(n_points) + scan_scratch_bytes(cdiv(n_points, 32));
   return PNR_OK;
 }
 
 extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev, int32_t K, int64_t cap_samples,
                                int64_t n_points, int32_t* flags, int32_t* used_map, int32_t* used, int32_t* n_used_dev,
                                void* scratch, size_t scratch_bytes, void* stream) {
-  PNR_CHECK_ARG(pidx && flags && used_map && used && n_used_dev && K > 0 && cap_samples >= 0 && n_points > 0,
-                "used_points: bad args");
+  PNR_CHECK_ARG(pidx && flags && used_map && used && n_used_dev && scratch && K > 0 && cap_samples >= 0 &&
+                    n_points > 0, "used_points: bad args");
+  const int64_t nw = cdiv(n_points, 32);
+  const size_t hb = used_head_bytes(n_points);
+  PNR_CHECK_ARG(scratch_bytes >= hb + scan_scratch_bytes(nw), "used_points: scratch too small (%zu < %zu)",
+                scratch_bytes, hb + scan_scratch_bytes(nw));
+  PNR_CHECK_ARG(((uintptr_t)flags & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+                "used_points: flags / scratch must be 16-B aligned");
   hipStream_t st = as_stream(stream);
-  PNR_HIP(hipMemsetAsync(flags, 0, (size_t)n_points * sizeof(int32_t), st));
+  int32_t* wpre = static_cast<int32_t*>(scratch);
+  uint8_t* bytes = used_small(n_points) ? static_cast<uint8_t*>(scratch) + pad16((size_t)(nw + 1) * 4)
+                                        : reinterpret_cast<uint8_t*>(flags);
+  uint32_t* bits = reinterpret_cast<uint32_t*>(bytes + nw * 32);
+  PNR_HIP(hipMemsetAsync(bytes, 0, (size_t)nw * 32, st));
   if (cap_samples > 0) {
     hipLaunchKernelGGL(k_mark_used, dim3(grid_for(cap_samples * K, 256)), dim3(256), 0, st, pidx, n_samples_dev, K,
-                       cap_samples, flags);
+                       cap_samples, bytes);
     PNR_LAUNCH_CHECK();
   }
+  // the words' popcounts go through `used` (n_points >= nw entries, written after)
+  hipLaunchKernelGGL(k_pack_used, dim3(grid_for(nw, 256)), dim3(256), 0, st, bytes, nw, bits, used);
+  PNR_LAUNCH_CHECK();
   int rc;
-  if ((rc = exclusive_scan(flags, n_points, nullptr, used_map, n_used_dev, scratch, scratch_bytes, st, 0))) return rc;
-  hipLaunchKernelGGL(k_used_list, dim3(grid_for(n_points, 256)), dim3(256), 0, st, flags, n_points, used_map, used);
+  if ((rc = exclusive_scan(used, nw, nullptr, wpre, n_used_dev, static_cast<char*>(scratch) + hb,
+                           scratch_bytes - hb, st, 0)))
+    return rc;
+  hipLaunchKernelGGL(k_used_list, dim3(grid_for(n_points, 256)), dim3(256), 0, st, bits, wpre, n_points, used_map,
+                     used);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

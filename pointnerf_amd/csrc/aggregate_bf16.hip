@@ -32,7 +32,6 @@ constexpr int kBT = 128;                 // columns (pairs / samples / points) p
 constexpr int kBPT = kBT / 32;           // 32-column quarters per tile
 constexpr int kBWaves = 4;
 constexpr int kPB = 280;                 // Xb pitch (bf16) for <= 272 input rows (k_pairs_b, k_point_pre_b)
-constexpr int kPBc = 296;                // Xb pitch for the colour branch (288 input rows)
 constexpr int kBPad = 6;                 // zero k-steps padded onto bf16 weight packs (the ring's lead)
 
 struct AggArgsB {

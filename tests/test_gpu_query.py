@@ -196,6 +196,38 @@ def test_used_points_device_equals_torch(cuda):
     assert torch.equal(used_map, m_ref)
 
 
+@pytest.mark.parametrize("n_points", [1, 33, 100_003])
+def test_used_points_ragged(cuda, n_points):
+    """pnr_used_points (byte marks packed to one bit per point, word popcount ranks) on synthetic rows:
+    point counts that are not a multiple of 32, empty (-1) slots, a device row
+    count below the capacity and none (cap rows), vs train.used_points."""
+    from pointnerf_amd import _lib as L
+    from pointnerf_amd.train import used_points
+    g = torch.Generator().manual_seed(n_points)
+    K, cap = 8, 4000
+    pidx = torch.randint(-1, n_points, (cap * K,), generator=g, dtype=torch.int32)
+    pidx[torch.rand(cap * K, generator=g) < 0.5] = -1
+    pidx = pidx.to(cuda)
+    i32 = dict(dtype=torch.int32, device=cuda)
+    nb = L.c_size_t(0)
+    L.check(L.lib().pnr_used_points_scratch_bytes(n_points, L.ctypes.byref(nb)), "scratch")
+    for n_rows in (None, 1234):
+        flags, used_map, used = (torch.full((n_points,), 7, **i32) for _ in range(3))
+        scratch = torch.empty(int(nb.value), dtype=torch.uint8, device=cuda)
+        cnt = torch.zeros(2, **i32)
+        if n_rows is not None:
+            cnt[0] = n_rows
+        L.check(L.lib().pnr_used_points(L.ptr(pidx), L.ptr(cnt) if n_rows is not None else None, K, cap, n_points,
+                                        L.ptr(flags), L.ptr(used_map), L.ptr(used),
+                                        L.c_void_p(cnt.data_ptr() + 4), L.ptr(scratch), scratch.numel(),
+                                        L.stream_ptr(cuda)), "pnr_used_points")
+        torch.cuda.synchronize()
+        u_ref, m_ref = used_points(pidx[: (n_rows or cap) * K], n_points)
+        assert int(cnt[1]) == u_ref.numel()
+        assert torch.equal(used[: u_ref.numel()], u_ref)
+        assert torch.equal(used_map, m_ref)
+
+
 @pytest.mark.parametrize("case", ["inside", "crossing", "shifted"])
 def test_device_geometry_equals_host(cuda, case):
     """pnr_grid_build_dev (get_hyperparameters on the device, no host read of the
