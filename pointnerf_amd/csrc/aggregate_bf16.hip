@@ -179,6 +179,28 @@ __device__ __forceinline__ void store_act_b(const f32x16 (&acc)[PT * NT], uint16
       }
 }
 
+// Accumulators of output rows 32(T0+T) + 8q + 4h + i start at the layer's bias
+// (bf16, the value its pack holds in the bias column): the layer then runs
+// without its bias k-step (bias rows of Xb neither written nor read).
+template <int NT, int PT>
+__device__ __forceinline__ void acc_bias_b(f32x16 (&acc)[PT * NT], const uint16_t* bias, int lane, int T0) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int T = 0; T < NT; ++T)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint2 u = *reinterpret_cast<const uint2*>(bias + 32 * (T0 + T) + 8 * q + 4 * h);
+      const float v0 = bf16_lo(u.x), v1 = bf16_hi(u.x), v2 = bf16_lo(u.y), v3 = bf16_hi(u.y);
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) {
+        acc[pt * NT + T][4 * q] = v0;
+        acc[pt * NT + T][4 * q + 1] = v1;
+        acc[pt * NT + T][4 * q + 2] = v2;
+        acc[pt * NT + T][4 * q + 3] = v3;
+      }
+    }
+}
+
 // Rows [r0, r0 + 16) of one column: first `nval` from vals, then 1 (bias) if
 // bias, then zeros -- the inputs past a layer's last real row.
 __device__ __forceinline__ void tail_rows_b(uint16_t* Xb, int pitch, int col, int r0, const float* vals, int nval) {
@@ -287,9 +309,11 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_point_pre_b(AggArgsB A) {
 // zero weights; the xor-tree and DPP reduce-scatter sums below pair the
 // remaining lanes exactly as the 8-lane trees do).
 constexpr int kBTSmax = kBT;   // samples per tile at KT = 1
-// Xb | wtL | apart | sflag | exB (bf16) | prowL | vL | vrL | waL
+// Xb | wtL | apart | sflag | exB (bf16) | prowL | vL | vrL | waL | bL (bf16 biases)
+constexpr int kBiasL = 2 * kHid + 2 * kC;   // block1.2, block3.2, color_branch.2, color_branch.4
 constexpr size_t kPairsBLds =
-    (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 4 * kBT + kBT + kBTSmax + 3 * kBTSmax + kHid) * 4;
+    (size_t)kBT * kPB * 2 + (kBT + 4 * kBT + kBTSmax + 4 * kBT + kBT + kBTSmax + 3 * kBTSmax + kHid) * 4 + kBiasL * 2;
+static_assert(2 * kPairsBLds <= 160 * 1024, "two k_pairs_b workgroups per CU");
 constexpr int kOPitch = kC + 4;   // fp32 output staging pitch: 16-B rows, an accumulator quad is one b128 write
 static_assert((size_t)kBT * kOPitch * 4 <= (size_t)kBT * kPB * 2, "output staging must fit the Xb tile");
 static_assert(kHid + 24 <= kPB, "the colour branch's hid + view-PE rows must fit the Xb pitch");
@@ -337,6 +361,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   int* vL = prowL + kBT;                                   // [SPT] sample index of each tile row
   float* vrL = reinterpret_cast<float*>(vL + kBTSmax);     // [3][SPT] rotated view dir of each sample
   float* waL = vrL + 3 * kBTSmax;                          // [256] alpha_branch weights (loaded once)
+  uint16_t* bL = reinterpret_cast<uint16_t*>(waL + kHid);  // [kBiasL] layer biases (loaded once)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar addressing
   const int c = lane & 31, h = lane >> 5;
   const int K = A.s.K;
@@ -379,6 +404,18 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
   int nx_pid = pf_pid(nx_row);
   int nx_drow = pf_drow(nx_row);
   waL[threadIdx.x] = A.w.wa[threadIdx.x];   // 256 threads, 256 weights (ordered by the tile's first barrier)
+  {
+    // bias of output n = 32 T + c: pack entry [last step][T][lane c][0] (frag_pack_bf16:
+    // W' = [W | bias | 0], bias column 256 -> step 16 (block1.2 / 3.2, 8 tiles), 128 ->
+    // step 8 (color_branch.2 / .4, 4 tiles))
+    const int T = threadIdx.x >> 5, cc = threadIdx.x & 31;
+    bL[threadIdx.x] = A.w.w2f[((size_t)(16 * 8 + T) * 64 + cc) * 8];
+    bL[kHid + threadIdx.x] = A.w.w4f[((size_t)(16 * 8 + T) * 64 + cc) * 8];
+    if (threadIdx.x < kC) {
+      bL[2 * kHid + threadIdx.x] = A.w.wc2f[((size_t)(8 * 4 + T) * 64 + cc) * 8];
+      bL[2 * kHid + kC + threadIdx.x] = A.w.wc3f[((size_t)(8 * 4 + T) * 64 + cc) * 8];
+    }
+  }
 #ifdef PNR_PB_TRACE
   int it_tr = -1;
 #endif
@@ -575,17 +612,11 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     PB_STAMP(5);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
-    if (wid == 0) {
-      const float one = 1.f;
-      tail_rows_b(Xb, kPB, lane, 256, &one, 1);
-      tail_rows_b(Xb, kPB, lane + 64, 256, &one, 1);
-    }
     __syncthreads();
     PB_STAMP(6);
-#pragma unroll
-    for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
+    acc_bias_b<2, kBPT>(acc, bL, lane, T0);
     nx_row = pf_row(nx_v);   // link 2
-    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w2, Xb, 17, lane);
+    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w2, Xb, 16, lane);
     PB_STAMP(7);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
@@ -610,16 +641,10 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     PB_STAMP(9);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
-    if (wid == 0) {
-      const float one = 1.f;
-      tail_rows_b(Xb, kPB, lane, 256, &one, 1);
-      tail_rows_b(Xb, kPB, lane + 64, 256, &one, 1);
-    }
     __syncthreads();
     PB_STAMP(10);
-#pragma unroll
-    for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
-    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w4, Xb, 17, lane);
+    acc_bias_b<2, kBPT>(acc, bL + kHid, lane, T0);
+    mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w4, Xb, 16, lane);
     PB_STAMP(11);
     __syncthreads();   // Xb is free: the K-sums are staged there (hid rows, kHP pitch)
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
@@ -762,7 +787,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     // last-step override (row 280 = 1), the 280 real rows fill the pitch.
     {
       constexpr int PTc = SPT >= 32 ? SPT / 32 : 1;   // 32-column quarters holding the SPT samples
-      constexpr int NCc = 32 * PTc;
       const uint4* wc1 = reinterpret_cast<const uint4*>(A.w.wc1f) + wid * 64;
       const uint4* wc2 = reinterpret_cast<const uint4*>(A.w.wc2f) + wid * 64;
       const uint4* wc3 = reinterpret_cast<const uint4*>(A.w.wc3f) + wid * 64;
@@ -772,32 +796,20 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       mlp_layer_b<1, PTc, 4, kPB, kColWD, true>(cacc, wc1, Xb, 18, lane);
       __syncthreads();
       store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
-      if (wid == 0) {
-        const float one = 1.f;
-#pragma unroll
-        for (int cc = lane; cc < NCc; cc += 64) tail_rows_b(Xb, kPB, cc, kC, &one, 1);
-      }
       __syncthreads();
       PB_STAMP(14);
-#pragma unroll
-      for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
-      mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc2, Xb, 9, lane);
+      acc_bias_b<1, PTc>(cacc, bL + 2 * kHid, lane, wid);
+      mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc2, Xb, 8, lane);
       __syncthreads();
       store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
-      if (wid == 0) {
-        const float one = 1.f;
-#pragma unroll
-        for (int cc = lane; cc < NCc; cc += 64) tail_rows_b(Xb, kPB, cc, kC, &one, 1);
-      }
       __syncthreads();
       PB_STAMP(15);
-#pragma unroll
-      for (int i = 0; i < PTc; ++i) cacc[i] = (f32x16){0.f};
-      mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc3, Xb, 9, lane);
+      acc_bias_b<1, PTc>(cacc, bL + 2 * kHid + kC, lane, wid);
+      mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc3, Xb, 8, lane);
       __syncthreads();   // every wave's layer-3 reads of Xb are done
       // out_feat rows (valid samples only) through LDS, two rows per store
       // instruction (lane half = row, 16 B per lane, rows 516 B apart: 4-B aligned)
-      float* Ob = reinterpret_cast<float*>(Xb);   // [NCc][kOPitch] fp32
+      float* Ob = reinterpret_cast<float*>(Xb);   // [32 PTc][kOPitch] fp32
 #pragma unroll
       for (int pt = 0; pt < PTc; ++pt)
 #pragma unroll

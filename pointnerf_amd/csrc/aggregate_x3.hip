@@ -1046,7 +1046,7 @@ __global__ void __launch_bounds__(512, 1) k_pairs_h2_train(X3Args A) { pairs_bod
 // (37 KB, four workgroups = two waves per SIMD per CU, so one workgroup's hid
 // loads hide behind another's MFMAs): colour layer 1 runs as two 144-row halves
 // (packs wc1a = columns 0..143, wc1b = columns 144..279 + bias), layers 2 and
-// 3 as 129-row GEMMs with the bias row.
+// 3 as 128-row GEMMs from bias-initialised accumulators.
 constexpr int kCG = 18;                       // 8-row groups per half (144 rows)
 constexpr int kCPlane = kCG * kXT * 16;       // bytes per f16 plane
 constexpr size_t kColH2Lds = 2 * (size_t)kCPlane;
@@ -1146,27 +1146,19 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r2, voff);
     __syncthreads();
     // ---------------------------------------------------- layer 2
+    // (layers 2 and 3: accumulators start at bias / scale, as block1.2 / 3.2 in
+    // k_pairs_h2: 8 k-steps, the packs' bias step and the bias input row unused)
     store_act<true>(acc, lds, neg, A.scale[0], lane, T0, kCPlane);
-    if (wid == 0) {   // row 128 = 1 (bias column), 129..143 = 0
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        *reinterpret_cast<uint4*>(lds + pl * kCPlane + (16 * kXT + lane) * 16) =
-            make_uint4(pl == 0 ? XL<true>::kOne : 0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(lds + pl * kCPlane + (17 * kXT + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    acc_init<true>(acc, A.w.bc2, 1.f / A.scale[1], lane, T0);
     __syncthreads();
-    layer<true, 4>(acc, wr, r2, voff, lds, kCPlane, 9, lane);
+    layer<true, 4>(acc, wr, r2, voff, lds, kCPlane, 8, lane);
     prime<true, 4>(wr, r3, voff);
     __syncthreads();
-    // ---------------------------------------------------- layer 3 (bias rows kept)
+    // ---------------------------------------------------- layer 3
     store_act<true>(acc, lds, neg, A.scale[1], lane, T0, kCPlane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
+    acc_init<true>(acc, A.w.bc3, 1.f / A.scale[2], lane, T0);
     __syncthreads();
-    layer<true, 4>(acc, wr, r3, voff, lds, kCPlane, 9, lane);
+    layer<true, 4>(acc, wr, r3, voff, lds, kCPlane, 8, lane);
     prime<true, 4>(wr, r1a, voff);   // the next tile
     // out_feat[v, 1 + 32 (T0 + T) + row] (valid samples only; the others keep their zeros)
     const float sc3 = A.scale[2];

@@ -173,7 +173,8 @@ def test_bf16_render_variant_equals_general(cuda, flags):
     computes the features of the general-path variant a call with out_weight /
     out_conf runs, bucketed and unbucketed: the same samples written, values
     equal up to the FMA contraction hipcc picks per instantiation (measured and
-    printed: ~4e-4 of the entries by ~1e-7 of the maximum)."""
+    printed: ~4e-4 of the entries differ, by up to ~1e-3 of the maximum when a
+    last-bit difference flips the bf16 rounding of a GEMM input)."""
     from pointnerf_amd import _lib as L
     from scenes import flag_scene
     sc = flag_scene(flags, n_points=60000 if flags == "truck" else 30000, H=64, view=0)
@@ -212,8 +213,9 @@ def test_bf16_render_variant_equals_general(cuda, flags):
         print(f"buckets={bk}: differing {frac:.2e} of the entries, max |d| / max |f| = {rel:.2e}")
         # the two instantiations may contract a different a * b + c into an FMA in
         # the gather's fp32 math (weights, distances): last-bit differences that
-        # the bf16 operands of the next GEMM can round either way
-        assert rel <= 1e-5 and frac <= 0.01, (bk, frac, rel)   # measured: 1e-7, 4e-4
+        # the bf16 operands of the next GEMM can round either way -- one bf16 step
+        # (2^-8 relative) of an input, carried to the outputs of its sample
+        assert rel <= 2.0 ** -7 and frac <= 0.01, (bk, frac, rel)   # measured: <= 1.3e-3, <= 4e-4
         assert int(torch.isfinite(outs[0][:, 0]).sum()) > 1000
 
 
