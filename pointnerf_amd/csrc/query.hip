@@ -138,9 +138,21 @@ __global__ void __launch_bounds__(kQBlock) k_fill_list(int64_t R, int SR, const 
 // One accepted-or-rejected candidate record of query_neigh_along_ray_layered
 // (qpiw.py:494-518): radius test, fill phase, then strict-closer replacement of
 // the first farthest entry.
+// The K neighbour ids of a lane's sample, in LDS: one column of the block's
+// [KMAX][kQBlock] array, so a dynamic index is one ds_write instead of a select
+// chain over KMAX registers, and KMAX VGPRs stay free in a kernel that spills at
+// 8 waves per SIMD (KMAX 8: 10 KB of LDS per block, 8 blocks per CU).
+// The distances stay in registers (the rescan reads all of them).
+template <int KMAX>
+struct KnnIds {
+  int32_t* p;   // this thread's column
+  __device__ __forceinline__ void set(int i, int32_t v) { p[i * kQBlock] = v; }
+  __device__ __forceinline__ int32_t get(int i) const { return p[i * kQBlock]; }
+};
+
 template <int KMAX>
 __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int K, float r2, float buf[KMAX],
-                                          int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
+                                          KnnIds<KMAX>& out, int& kid, int& far_ind, float& far2) {
   const float xv = __fsub_rn(v.x, p[0]);
   const float yv = __fsub_rn(v.y, p[1]);
   const float zv = __fsub_rn(v.z, p[2]);
@@ -149,13 +161,10 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
   const int pid = __float_as_int(v.w);
   if (kid < K) {
     // fill phase (qpiw.py:500-506)
+    out.set(kid, pid);
 #pragma unroll
-    for (int i = 0; i < KMAX; ++i) {
-      if (i == kid) {
-        out[i] = pid;
-        buf[i] = d2;
-      }
-    }
+    for (int i = 0; i < KMAX; ++i)
+      if (i == kid) buf[i] = d2;
     if (d2 > far2) {
       far2 = d2;
       far_ind = kid;
@@ -166,13 +175,10 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
     // replace phase (qpiw.py:507-518): strictly closer than the
     // current farthest, then rescan for the first maximum.
     if (d2 < far2) {
+      out.set(far_ind, pid);
 #pragma unroll
-      for (int i = 0; i < KMAX; ++i) {
-        if (i == far_ind) {
-          out[i] = pid;
-          buf[i] = d2;
-        }
-      }
+      for (int i = 0; i < KMAX; ++i)
+        if (i == far_ind) buf[i] = d2;
       far2 = d2;
 #pragma unroll
       for (int i = 0; i < KMAX; ++i) {
@@ -188,7 +194,7 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
 // All records of one record range, in order, KB loads in flight.
 template <int KMAX, int KB>
 __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
-                                         float buf[KMAX], int32_t out[KMAX], int& kid, int& far_ind, float& far2) {
+                                         float buf[KMAX], KnnIds<KMAX>& out, int& kid, int& far_ind, float& far2) {
   for (int g0 = 0; g0 < cnt; g0 += KB) {
     float4 vb[KB];
 #pragma unroll
@@ -221,7 +227,7 @@ __device__ __forceinline__ int held_rank(const uint2 wd, int bit) {
 // cells are looked up (bitmap + rank: no per-cell table of the whole grid).
 template <int KMAX, int LAYERS, int KB>
 __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, int layers, float r2,
-                                       const QIndex& qi, int32_t out[KMAX], int& n_cand) {
+                                       const QIndex& qi, KnnIds<KMAX>& out, int& n_cand) {
   const int fx = vox_coord(p[0], g.shift[0], g.vs[0]);
   const int fy = vox_coord(p[1], g.shift[1], g.vs[1]);
   const int fz = vox_coord(p[2], g.shift[2], g.vs[2]);
@@ -229,7 +235,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     buf[i] = 0.f;
-    out[i] = -1;
+    out.set(i, -1);
   }
   int kid = 0, far_ind = 0;
   float far2 = 0.f;
@@ -359,7 +365,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 // LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
 // layered loop inlined beside it costs registers); 0: any layer count.
 template <int KMAX, int LAYERS, int KB>
-__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
+__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KMAX <= 16 ? 8 : 3))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
@@ -378,6 +384,7 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8)
   // overlap, so their record loads share cache lines (the sample -> outputs
   // mapping is unchanged; only which lane computes which sample).
   __shared__ int hist[kQBlock], perm[kQBlock];
+  __shared__ int32_t ids_lds[KMAX * kQBlock];
   const bool by_slot = SR <= kQBlock;   // (A/B: lanes in fill order 3.45 ms query, by slot 2.94)
   const int tid = threadIdx.x, lane = tid & 63;
   // XCD-aware chunking (grid a multiple of 8; blocks b, b + 8, ... share an
@@ -459,17 +466,17 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(8)
       sample_w[i * 3 + a] = p[a];
       sample_p[i * 3 + a] = pp[a];
     }
-    int32_t out[KMAX];
+    KnnIds<KMAX> out{ids_lds + tid};
     const int nk = knn_one<KMAX, LAYERS, KB>(p, g, K, layers, r2, qi, out, n_cand);
     if (KMAX == 8 && K == 8 && vec_pidx) {   // two 16-B stores (pidx 16-B aligned)
       int4* o4 = reinterpret_cast<int4*>(pidx + i * 8);
-      o4[0] = make_int4(out[0], out[1], out[2], out[3]);
-      o4[1] = make_int4(out[4 % KMAX], out[5 % KMAX], out[6 % KMAX], out[7 % KMAX]);
+      o4[0] = make_int4(out.get(0), out.get(1), out.get(2), out.get(3));
+      o4[1] = make_int4(out.get(4 % KMAX), out.get(5 % KMAX), out.get(6 % KMAX), out.get(7 % KMAX));
     } else {
       for (int k = 0; k < K; ++k) {
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
-          if (j == k) pidx[i * K + k] = out[j];
+          if (j == k) pidx[i * K + k] = out.get(j);
       }
     }
     vflag[i] = nk > 0;
