@@ -457,10 +457,21 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KM
     const int64_t r = rs / SR;
     const int d = slot_d[rs];
     const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
-    if (q.ray_cam) load_cam(q, q.ray_cam[r], c, Rm);
+    // the sample's camera: the launch's (uniform, loaded once) or its ray's entry
+    // of a multi-camera batch -- read per sample into temporaries, so no camera
+    // is carried in VGPRs across the walk
+    float cs[3], Rs[9];
+    if (q.ray_cam) {
+      load_cam(q, q.ray_cam[r], cs, Rs);
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) cs[a] = c[a];
+#pragma unroll
+      for (int a = 0; a < 9; ++a) Rs[a] = Rm[a];
+    }
     float p[3], pp[3];
-    ray_point(c, dir, tval(q, r, d), p);
-    world_to_pers(p, c, Rm, pp);
+    ray_point(cs, dir, tval(q, r, d), p);
+    world_to_pers(p, cs, Rs, pp);
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       sample_w[i * 3 + a] = p[a];
