@@ -135,23 +135,26 @@ __global__ void __launch_bounds__(kQBlock) k_fill_list(int64_t R, int SR, const 
   if ((threadIdx.x & 63) == 0 && hit) atomicAdd(counts + 2, hit);
 }
 
+// The K neighbour ids and distances of a lane's sample, in LDS: one column of
+// the block's [KMAX][kQBlock] arrays, so a dynamic index is one ds_write instead
+// of a select chain over KMAX registers, and 2 KMAX VGPRs stay free in a kernel
+// that spilled at 8 waves per SIMD (KMAX 8: 18 KB of LDS per block, 8 blocks per
+// CU; A/B: headline query 2.04 -> 1.84 ms, c5 10.17 -> 8.94 ms).
+template <int KMAX>
+struct KnnIds {
+  int32_t* p;   // this thread's id column
+  float* q;     // this thread's distance column
+  __device__ __forceinline__ void set(int i, int32_t v) { p[i * kQBlock] = v; }
+  __device__ __forceinline__ int32_t get(int i) const { return p[i * kQBlock]; }
+  __device__ __forceinline__ void setd(int i, float v) { q[i * kQBlock] = v; }
+  __device__ __forceinline__ float getd(int i) const { return q[i * kQBlock]; }
+};
+
 // One accepted-or-rejected candidate record of query_neigh_along_ray_layered
 // (qpiw.py:494-518): radius test, fill phase, then strict-closer replacement of
 // the first farthest entry.
-// The K neighbour ids of a lane's sample, in LDS: one column of the block's
-// [KMAX][kQBlock] array, so a dynamic index is one ds_write instead of a select
-// chain over KMAX registers, and KMAX VGPRs stay free in a kernel that spills at
-// 8 waves per SIMD (KMAX 8: 10 KB of LDS per block, 8 blocks per CU).
-// The distances stay in registers (the rescan reads all of them).
 template <int KMAX>
-struct KnnIds {
-  int32_t* p;   // this thread's column
-  __device__ __forceinline__ void set(int i, int32_t v) { p[i * kQBlock] = v; }
-  __device__ __forceinline__ int32_t get(int i) const { return p[i * kQBlock]; }
-};
-
-template <int KMAX>
-__device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int K, float r2, float buf[KMAX],
+__device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int K, float r2,
                                           KnnIds<KMAX>& out, int& kid, int& far_ind, float& far2) {
   const float xv = __fsub_rn(v.x, p[0]);
   const float yv = __fsub_rn(v.y, p[1]);
@@ -162,9 +165,7 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
   if (kid < K) {
     // fill phase (qpiw.py:500-506)
     out.set(kid, pid);
-#pragma unroll
-    for (int i = 0; i < KMAX; ++i)
-      if (i == kid) buf[i] = d2;
+    out.setd(kid, d2);
     if (d2 > far2) {
       far2 = d2;
       far_ind = kid;
@@ -176,14 +177,15 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
     // current farthest, then rescan for the first maximum.
     if (d2 < far2) {
       out.set(far_ind, pid);
-#pragma unroll
-      for (int i = 0; i < KMAX; ++i)
-        if (i == far_ind) buf[i] = d2;
+      out.setd(far_ind, d2);
       far2 = d2;
+      float bv[KMAX];
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) bv[i] = out.getd(i);   // all reads issued, then the scan
 #pragma unroll
       for (int i = 0; i < KMAX; ++i) {
-        if (i < K && buf[i] > far2) {
-          far2 = buf[i];
+        if (i < K && bv[i] > far2) {
+          far2 = bv[i];
           far_ind = i;
         }
       }
@@ -194,7 +196,7 @@ __device__ __forceinline__ void knn_visit(const float4 v, const float p[3], int 
 // All records of one record range, in order, KB loads in flight.
 template <int KMAX, int KB>
 __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt, const float p[3], int K, float r2,
-                                         float buf[KMAX], KnnIds<KMAX>& out, int& kid, int& far_ind, float& far2) {
+                                         KnnIds<KMAX>& out, int& kid, int& far_ind, float& far2) {
   for (int g0 = 0; g0 < cnt; g0 += KB) {
     float4 vb[KB];
 #pragma unroll
@@ -202,7 +204,7 @@ __device__ __forceinline__ void knn_cell(const float4* __restrict__ rec, int cnt
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
       if (g0 + u >= cnt) break;
-      knn_visit<KMAX>(vb[u], p, K, r2, buf, out, kid, far_ind, far2);
+      knn_visit<KMAX>(vb[u], p, K, r2, out, kid, far_ind, far2);
     }
   }
 }
@@ -231,12 +233,8 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
   const int fx = vox_coord(p[0], g.shift[0], g.vs[0]);
   const int fy = vox_coord(p[1], g.shift[1], g.vs[1]);
   const int fz = vox_coord(p[2], g.shift[2], g.vs[2]);
-  float buf[KMAX];
 #pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    buf[i] = 0.f;
-    out.set(i, -1);
-  }
+  for (int i = 0; i < KMAX; ++i) out.set(i, -1);   // (distances: read only once all K are filled)
   int kid = 0, far_ind = 0;
   float far2 = 0.f;
   if (LAYERS == 2) {
@@ -253,7 +251,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
     const int zlo = fz > 0 ? fz - 1 : fz, zhi = fz + 1 < g.dims[2] ? fz + 1 : fz;
     auto range = [&](int o, int e) {
       n_cand += e - o;
-      knn_cell<KMAX, KB>(qi.recs + o, e - o, p, K, r2, buf, out, kid, far_ind, far2);
+      knn_cell<KMAX, KB>(qi.recs + o, e - o, p, K, r2, out, kid, far_ind, far2);
     };
     // Every index lookup of the 27 cells is issued up front: one round of 9-18
     // independent word loads (a column's 3-cell run spans <= 2 words; the
@@ -340,7 +338,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
           const int o = qi.rec_off[lo];
           const int cn = qi.rec_off[hi] - o;
           n_cand += cn;
-          knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
+          knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, out, kid, far_ind, far2);
         } else {
 #pragma unroll
           for (int e = 0; e < 2; ++e) {   // z = fz - L, then fz + L (inside the grid only)
@@ -352,7 +350,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
             const int o = qi.rec_off[r];
             const int cn = qi.rec_off[r + 1] - o;
             n_cand += cn;
-            knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, buf, out, kid, far_ind, far2);
+            knn_cell<KMAX, KB>(qi.recs + o, cn, p, K, r2, out, kid, far_ind, far2);
           }
         }
       }
@@ -365,7 +363,7 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 // LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
 // layered loop inlined beside it costs registers); 0: any layer count.
 template <int KMAX, int LAYERS, int KB>
-__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KMAX <= 16 ? 8 : 3))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
+__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? 8 : 64 / KMAX))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
@@ -385,6 +383,7 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KM
   // mapping is unchanged; only which lane computes which sample).
   __shared__ int hist[kQBlock], perm[kQBlock];
   __shared__ int32_t ids_lds[KMAX * kQBlock];
+  __shared__ float dist_lds[KMAX * kQBlock];
   const bool by_slot = SR <= kQBlock;   // (A/B: lanes in fill order 3.45 ms query, by slot 2.94)
   const int tid = threadIdx.x, lane = tid & 63;
   // XCD-aware chunking (grid a multiple of 8; blocks b, b + 8, ... share an
@@ -477,18 +476,14 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KM
       sample_w[i * 3 + a] = p[a];
       sample_p[i * 3 + a] = pp[a];
     }
-    KnnIds<KMAX> out{ids_lds + tid};
+    KnnIds<KMAX> out{ids_lds + tid, dist_lds + tid};
     const int nk = knn_one<KMAX, LAYERS, KB>(p, g, K, layers, r2, qi, out, n_cand);
     if (KMAX == 8 && K == 8 && vec_pidx) {   // two 16-B stores (pidx 16-B aligned)
       int4* o4 = reinterpret_cast<int4*>(pidx + i * 8);
       o4[0] = make_int4(out.get(0), out.get(1), out.get(2), out.get(3));
       o4[1] = make_int4(out.get(4 % KMAX), out.get(5 % KMAX), out.get(6 % KMAX), out.get(7 % KMAX));
     } else {
-      for (int k = 0; k < K; ++k) {
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-          if (j == k) pidx[i * K + k] = out.get(j);
-      }
+      for (int k = 0; k < K; ++k) pidx[i * K + k] = out.get(k);
     }
     vflag[i] = nk > 0;
     if (nk > 0) atomicAdd(ray_vcnt + r, 1);
