@@ -136,11 +136,11 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_final(const int32_t* __rest
 }
 
 // Two-launch variant for up to kScanDirect tiles (every query compaction and
-// grid-build scan at the bench sizes): each block sums the tile totals before it
+// grid-build scan at the headline's sizes): each block sums the tile totals before it
 // itself (<= kScanDirect / 256 loads per thread) instead of a one-block scan of
 // the sums between the passes -- one dependent launch fewer per scan.  The
 // block holding the last element writes the grand total.
-constexpr int64_t kScanDirect = 2048;
+constexpr int64_t kScanDirect = 4096;   // <= 16 tile totals per thread (the headline's 5.7 M-sample vflag scan: 2 768 tiles)
 __global__ void __launch_bounds__(kScanBlock) k_scan_final_direct(const int32_t* __restrict__ in, int64_t n,
                                                                   const int32_t* n_dev, int as_flag,
                                                                   const int32_t* __restrict__ sums,

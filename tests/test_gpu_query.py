@@ -141,7 +141,7 @@ def test_deterministic_and_repeatable(cuda):
 def test_scan_matches_cumsum(cuda):
     from pointnerf_amd import _lib as L
     rng = np.random.default_rng(0)
-    for n in (1, 7, 2048, 2049, 100000, 1 << 20, 5_000_000):   # <= 2048 tiles: two launches; beyond: three
+    for n in (1, 7, 2048, 2049, 100000, 1 << 20, 5_000_000, 9_000_000):   # <= 4096 tiles: two launches; beyond: three
         x = torch.from_numpy(rng.integers(0, 5, size=n).astype(np.int32)).to(cuda)
         out = torch.empty(n + 1, dtype=torch.int32, device=cuda)
         tot = torch.empty(1, dtype=torch.int32, device=cuda)
