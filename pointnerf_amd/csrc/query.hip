@@ -362,8 +362,12 @@ __device__ __forceinline__ int knn_one(const float p[3], const QGrid& g, int K, 
 
 // LAYERS = 2: the 3x3x3 query specialised (its own kernel: the generic
 // layered loop inlined beside it costs registers); 0: any layer count.
+// Waves per SIMD: 7 for the 3x3x3 walk (72 VGPRs, 21 spilled, against 64 and 29
+// at 8: headline query -0.7 %), 8 for the generic one (c5: 7 waves +6 %), fewer
+// for KMAX > 8 (the [KMAX][256] LDS columns bound the blocks per CU);
+// profiles/r05_knn_occupancy_lds_ab.json.
 template <int KMAX, int LAYERS, int KB>
-__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? 8 : 64 / KMAX))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
+__global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? (LAYERS == 2 ? 7 : 8) : 64 / KMAX))) k_knn(QRays q, const QGrid* __restrict__ gq, int SR, int K, int layers, float r2,
                                                  QIndex qi, const uint16_t* __restrict__ slot_d,
                                                  const int32_t* __restrict__ fill_rs,
                                                  int32_t* __restrict__ pidx, int32_t* __restrict__ vflag,
