@@ -452,18 +452,28 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       const float* dirp = A.pts.dir ? A.pts.dir : A.pts.xyz;
       const float* persp = A.pts.pers ? A.pts.pers : A.pts.xyz;
       const float* confp = A.pts.conf ? A.pts.conf : A.pts.xyz;
-      float sw[3], sp[3], vd[3], pw[3], pp[3], colr[3], pdir[3];
+      float sw[3] = {0.f, 0.f, 0.f}, sp[3], vd[3] = {0.f, 0.f, 0.f}, pw[3], pp[3], colr[3] = {0.f, 0.f, 0.f},
+            pdir[3] = {0.f, 0.f, 0.f};
+      float cfl = 1.f;
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        sw[a] = A.s.sample_w[row * 3 + a];
         sp[a] = A.s.sample_p[row * 3 + a];
-        vd[a] = A.s.dirs[drow * 3 + a];
         pw[a] = A.pts.xyz[prow * 3 + a];
-        colr[a] = colp[prow * 3 + a];
-        pdir[a] = dirp[prow * 3 + a];
         pp[a] = persp[prow * 3 + a];
       }
-      const float cfl = confp[slot ? prow : 0];
+      // role 1 (waves 2-3: PE channels 3-5 = the perspective half of the distance)
+      // needs only sample_p and the point's xyz / pers; the wave-uniform branch
+      // keeps the other 13 loads to role 0 (c5: aggregate -0.6 %)
+      if (role == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          sw[a] = A.s.sample_w[row * 3 + a];
+          vd[a] = A.s.dirs[drow * 3 + a];
+          colr[a] = colp[prow * 3 + a];
+          pdir[a] = dirp[prow * 3 + a];
+        }
+        cfl = confp[slot ? prow : 0];
+      }
       __builtin_amdgcn_sched_barrier(0);
       lds_barrier();   // prowL: LDS only, the loads above stay in flight
       PB_STAMP(1);
