@@ -452,7 +452,10 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
     sp[a] = g.sp[a];
   }
   const int64_t drow = active ? g.dmap / A.s.dir_div : 0;
-  if (active) {
+  // the view / point directions, colour and confidence feed the extras and the
+  // weights, which producer wave 0 alone writes: the others load only what their
+  // PE channels need (wave-uniform branch)
+  if (active && pw == 0) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) vd[a] = A.s.dirs[drow * 3 + a];
   }
@@ -460,10 +463,13 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
   float cf = 1.f;
   if (valid) {
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      pw3[a] = A.pts.xyz[prow * 3 + a];
-      col[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
-      pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
+    for (int a = 0; a < 3; ++a) pw3[a] = A.pts.xyz[prow * 3 + a];
+    if (pw == 0) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        col[a] = A.pts.color ? A.pts.color[prow * 3 + a] : 0.f;
+        pdir[a] = A.pts.dir ? A.pts.dir[prow * 3 + a] : 0.f;
+      }
     }
     if (A.pts.pers) {
 #pragma unroll
@@ -472,7 +478,7 @@ __device__ __forceinline__ void gather(const X3Args& A, const GatherState& g, in
       pair_pers(A.pts, A.s, drow, pw3, cam_c, cam_R, pp);
     }
   }
-  if (A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
+  if (pw == 0 && A.pts.conf && prow >= 0) cf = A.pts.conf[prow];
   float d6[6];
   d6[0] = pw3[0] - sw[0];
   d6[1] = pw3[1] - sw[1];
