@@ -83,6 +83,9 @@ def parse():
                          "for (DESIGN.md section 14: c5 879 vs 960 Mray-samples/s)")
     ap.add_argument("--no-query-stream", action="store_true", help="same as --query-stream off")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only, no libpnr: the N-rank launcher, sharding, all-gather and timing with a "
+                         "stand-in render (tests/test_bench_launch.py; PNR_DIST_BACKEND defaults to gloo)")
     ap.add_argument("--no-train-line", action="store_true",
                     help="headline run: skip the finetune-step measurement appended to the line ('train')")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
@@ -163,14 +166,23 @@ def cameras(n_frames, H, W, flags="lego"):
     return cams
 
 
+def cgroup_cpu_quota():
+    """CPUs the process's cgroup may use (cpu.max quota / period), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except Exception:
+        return None
+
+
 def cpu_threads():
-    """Host threads of the CPU baseline: the process's CPU share (OMP_NUM_THREADS
-    on the GPU box, else the affinity mask), never more than os.cpu_count()."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        n = min(n, int(env))
-    return max(1, n)
+    """Host threads of the CPU baseline: every core the process is allowed --
+    its affinity mask (len(os.sched_getaffinity(0))), bounded by the cgroup's
+    CPU quota when one is set (threads beyond it are only throttled).
+    OMP_NUM_THREADS is not a bound (the box sets it for builds)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    return max(1, min(aff, quota) if quota else aff), aff, quota
 
 
 def cpu_baseline(args, opt, pts, feats, agg, cam, H, W):
@@ -183,7 +195,7 @@ def cpu_baseline(args, opt, pts, feats, agg, cam, H, W):
     except Exception:  # pragma: no cover
         threadpool_limits = None
     from oracle import oracle as O
-    threads = cpu_threads()
+    threads, aff, quota = cpu_threads()
     ctx = threadpool_limits(limits=threads) if threadpool_limits else None
     torch.set_num_threads(threads)
     O.set_threads(threads)
@@ -207,7 +219,8 @@ def cpu_baseline(args, opt, pts, feats, agg, cam, H, W):
     out = {"value": round(R * opt.SR / t_frame / 1e6, 4), "unit": "Mray-samples/s", "cores": threads,
            "kind": "port",
            "sample": (f"oracle/ (C query: serial grid build + OpenMP ray/sample loops; NumPy fp32 "
-                      f"aggregate/composite, BLAS) with {threads} threads (os.cpu_count() = {os.cpu_count()}) on "
+                      f"aggregate/composite, BLAS) with {threads} threads (affinity mask {aff} CPUs, cgroup "
+                      f"quota {quota if quota else 'none'}, os.cpu_count() = {os.cpu_count()}) on "
                       f"{len(sel)} random rays of one {H}x{W} frame, {args.points} points: grid build "
                       f"{t1 - t0:.2f}s + sample {t2 - t1:.2f}s, extrapolated to the frame "
                       f"({t_frame:.1f}s/frame)")}
@@ -493,8 +506,125 @@ def run_train(args, device):
     return line
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without torchrun: start N rank processes with
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) BEFORE any GPU
+    call in this process (it only parsed its arguments), wait for them, and print
+    the ONE JSON line rank 0 wrote, with the launcher recorded in it.  A failing
+    rank makes this process exit non-zero with the ranks' output tail."""
+    import subprocess
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    env["PNR_BENCH_LAUNCHER"] = "self"
+    # the ranks' stderr passes through live (progress); their stdout is captured for the line
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env, cwd=ROOT)
+    out, _ = p.communicate()
+    lines = []
+    for ln in out.splitlines():
+        ln = ln.strip()
+        if ln.startswith("{"):
+            try:
+                rec = json.loads(ln)
+            except ValueError:
+                continue
+            if isinstance(rec, dict) and "metric" in rec:
+                lines.append(rec)
+    if p.returncode != 0 or len(lines) != 1:
+        sys.stderr.write(out[-4000:])
+        print(f"bench.py launcher: torch.distributed.run with {args.gpus} ranks exited {p.returncode} "
+              f"with {len(lines)} result lines", file=sys.stderr)
+        return p.returncode or 1
+    rec = lines[0]
+    rec["launcher"] = (f"bench.py --gpus {args.gpus}: {args.gpus} rank processes via torch.distributed.run "
+                       f"(--nnodes=1 --nproc-per-node={args.gpus}, 127.0.0.1), started before any GPU call")
+    print(json.dumps(rec), flush=True)
+    return 0
+
+
+def run_dry(args):
+    """--dry-run (CPU, no libpnr, no GPU): the N-rank step machinery alone -- the
+    launcher, init_process_group, the step's band shares as one batch
+    (StepShard), a stand-in 'render' of every ray (a closed-form function of its
+    direction), the all-gather that assembles the step's frames, the barrier +
+    max-over-ranks timing and rank 0's one line.  Every assembled frame is
+    checked against the stand-in render of the whole frame."""
+    import torch.distributed as dist
+    from pointnerf_amd.parallel import StepShard, TileShard
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(os.environ.get("PNR_DIST_BACKEND", "gloo"))
+    if os.environ.get("PNR_BENCH_FAIL_RANK") == str(rank):   # launcher test: a rank that dies
+        raise SystemExit(f"rank {rank}: failure injected by PNR_BENCH_FAIL_RANK")
+    H = W = min(args.H, 64)
+    cams = [torch.from_numpy(c[2]) for c in cameras(8, H, W)]
+
+    def shade(rd):   # [n, 3] -> [n, 4]
+        return torch.cat([rd, rd.square().sum(1, keepdim=True)], 1)
+
+    def one_step(s):
+        cis = [(s * world + i) % len(cams) for i in range(world)]
+        if world == 1:
+            return [shade(cams[cis[0]])], cis
+        st = StepShard([TileShard(H, W, rank, world, i, None) for i in range(world)], None)
+        return st.assemble_async(shade(st.select([cams[c] for c in cis]))).wait(), cis
+
+    ok = True
+    for s in range(args.warmup):
+        one_step(s)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        frames, cis = one_step(args.warmup + s)
+        ok &= all(torch.equal(f, shade(cams[c])) for f, c in zip(frames, cis))
+    if world > 1:
+        dist.barrier()
+    t_local = time.perf_counter() - t0
+    per_rank = [t_local]
+    if world > 1:
+        tl = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(tl, torch.tensor([t_local, float(ok)], dtype=torch.float64))
+        per_rank = [float(t[0]) for t in tl]
+        ok = all(float(t[1]) == 1.0 for t in tl)
+    t_max = max(per_rank)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "dry run (no GPU): assembled stand-in frames per second", "value": round(world * args.steps / t_max, 3),
+            "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_max / max(args.steps, 1) * 1e3, 3),
+            "ms_per_step_per_rank": [round(t / max(args.steps, 1) * 1e3, 3) for t in per_rank],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "dry_run": True, "frames_equal": bool(ok),
+            "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "dist_backend": dist.get_backend() if world > 1 else None,
+            "config": {"workload": f"stand-in shading of {H}x{W} frames, band shards, one all-gather per step"}}),
+            flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's `python bench.py --gpus N`: this process only launches the ranks
+        sys.exit(launch_ranks(args))
+    if args.dry_run:
+        run_dry(args)
+        return
     if args.mode == "train":
         local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
@@ -506,9 +636,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
-            sys.exit(2)
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; the line reports n_gpus={world}",
+              file=sys.stderr)
     ndev = torch.cuda.device_count()
     local_dev = local % max(ndev, 1)          # == local on a node with one GPU per rank
     torch.cuda.set_device(local_dev)
@@ -669,13 +798,14 @@ def main():
     finish(prev)       # the last step's frames are gathered inside the timed region
     torch.cuda.synchronize()
     t_local = time.perf_counter() - t0
+    per_rank_s = [t_local]
     if dist:
         dist.barrier()
-        tt = torch.tensor([t_local], device=device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-    else:
-        t_max = t_local
+        tdev = device if dist.get_backend() == "nccl" else "cpu"
+        tt = [torch.zeros(1, device=tdev, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(tt, torch.tensor([t_local], device=tdev, dtype=torch.float64))
+        per_rank_s = [float(x.item()) for x in tt]
+    t_max = max(per_rank_s)
     torch.cuda.synchronize()
     # per-stage times from HIP events recorded on the launch stream
     per = {}
@@ -714,6 +844,9 @@ def main():
             "value": round(value, 3), "unit": "Mray-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step_per_rank": [round(t / args.steps * 1e3, 3) for t in per_rank_s],
+            "rccl_world": dist.get_world_size() if dist else 1,
+            "dist_backend": dist.get_backend() if dist else None,
             "dtype": args.dtype,
             "arith": {"fp32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
                       "fp32x3": "fp32-accurate: exact 3-way bf16 split of each fp32 operand, 6 cross products on "

@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 20
+#define PNR_ABI_VERSION 21
 
 enum {
   PNR_OK = 0,
@@ -134,6 +134,10 @@ typedef struct {
 } pnr_grid_spec;
 int pnr_grid_build_dev(pnr_handle* h, const float* xyz_dev, int64_t n, const pnr_grid_spec* spec, void* stream);
 int pnr_grid_geometry(pnr_handle* h, float shift[3], float vsize[3], int32_t dims[3]);
+/* The point bbox {min xyz, max xyz} the last pnr_grid_build_dev derived its
+ * geometry from (waits for the build; ABI 21): what get_hyperparameters'
+ * ranges come from, unaffected by later in-place edits of the points. */
+int pnr_grid_bbox(pnr_handle* h, float out6[6]);
 
 typedef struct {
   int64_t n_points_in_grid;   /* points whose voxel is inside dims            */
@@ -897,9 +901,11 @@ int pnr_clock_probe(float* out_dev, int32_t spins, void* stream);
 
 /* Exclusive scan of n int32 values (n_dev: optional device-side length <= n,
  * entries past it are treated as 0 and out[] is written up to n_dev+1);
- * total written to *total_dev (may be NULL). */
+ * total written to *total_dev (may be NULL).  out_len: int32 entries at out,
+ * at least n + 1 (the total is also stored at out[n_eff]); PNR_EINVAL otherwise
+ * (ABI 21). */
 int pnr_scan_scratch_bytes(int64_t n, size_t* out);
-int pnr_exclusive_scan_i32(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
+int pnr_exclusive_scan_i32(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out, int64_t out_len,
                            int32_t* total_dev, void* scratch, size_t scratch_bytes,
                            void* stream);
 

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 20
+ABI_VERSION = 21
 FEAT_H_PITCH = 136   # PNR_FEAT_H_PITCH: uint16 per bf16 feature row (pnr_aggregate_fwd_bf16_hf)
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
@@ -155,6 +155,7 @@ SIGNATURES = {
     "pnr_grid_stats_get": (c_int, [c_void_p, P(GridStats)]),
     "pnr_grid_build_dev": (c_int, [c_void_p, c_void_p, c_int64, P(GridSpec), c_void_p]),
     "pnr_grid_geometry": (c_int, [c_void_p, P(c_float), P(c_float), P(c_int32)]),
+    "pnr_grid_bbox": (c_int, [c_void_p, P(c_float)]),
     "pnr_grid_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pnr_query_scratch_bytes": (c_int, [c_int64, c_int32, P(c_size_t)]),
     "pnr_query": (c_int, [c_void_p, P(Rays), P(QueryParams), P(QueryBufs), c_void_p]),
@@ -267,7 +268,7 @@ SIGNATURES = {
     "pnr_vox_closest": (c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_size_t, c_void_p]),
     "pnr_scan_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
-    "pnr_exclusive_scan_i32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+    "pnr_exclusive_scan_i32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),
 }
 

@@ -858,10 +858,7 @@ struct BwdArgs {
 };
 
 constexpr int kBwdLdsFloats = 66 * kQP + 4 * kTP /*dot parts*/ + 4 * 7 * kTP /*extras parts*/;
-#ifndef PNR_BWD_LDS_PAD   // experiment builds (tools/extras_variant.sh): extra LDS per workgroup
-#define PNR_BWD_LDS_PAD 0
-#endif
-constexpr size_t kBwdLdsBytes = (size_t)kBwdLdsFloats * sizeof(float) + PNR_BWD_LDS_PAD;
+constexpr size_t kBwdLdsBytes = (size_t)kBwdLdsFloats * sizeof(float);
 
 // max |v| over a wave's lanes into an LDS slot (float bits compared as unsigned:
 // a NaN's bits exceed every finite and infinite value, so it propagates).
@@ -1061,13 +1058,6 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_
     if (t + d < nsteps) step(w.a[d], t + d);
 }
 
-// PNR_X3_EXTRAS_IN_KERNEL (experiment builds only, tools/extras_variant.sh): the
-// x3 variant computes the block3.0 extras from the LDS dz3 rows as the fp32 one
-// does (co-residency defect), instead of k_extras_bwd
-#ifndef PNR_X3_EXTRAS_IN_KERNEL
-#define PNR_X3_EXTRAS_IN_KERNEL 0
-#endif
-constexpr bool kX3ExIn = PNR_X3_EXTRAS_IN_KERNEL != 0;
 
 template <bool X3>
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
@@ -1178,7 +1168,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
     // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
     wave_sync();
-    if constexpr (!X3 || kX3ExIn) {
+    if constexpr (!X3) {
       float ex[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
       for (int u = 16 * wid; u < 16 * wid + 16; ++u) {
@@ -1198,7 +1188,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     // colour / dir gradients of the pair (wave 0, lane = pair), before the
     // block3.0^T GEMM: its registers stay free for the GEMM.  The pair's
     // indices are recomputed here rather than kept live across the GEMMs.
-    if ((!X3 || kX3ExIn) && wid == 0 && tile * kTS + (lane >> 3) < n) {
+    if (!X3 && wid == 0 && tile * kTS + (lane >> 3) < n) {
       const int64_t pair = tile * kTP + lane;
       const int64_t v = tile * kTS + (lane >> 3);
       const int32_t pr = A.sv.prow[pair];
@@ -2130,7 +2120,7 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
     PNR_LAUNCH_CHECK();
     // wb->w3e == NULL: the caller runs the extras per point inside
     // pnr_pairs_to_points_ex (no float atomics, coalesced dz3 rows)
-    if ((d_color || d_dir) && wb->w3e && !kX3ExIn)
+    if ((d_color || d_dir) && wb->w3e)
       hipLaunchKernelGGL(k_extras_bwd, dim3(grid_for(cdiv(s->n_max * kKN, 64), 4, 2048)), dim3(256), 0, st, a);
   } else
     hipLaunchKernelGGL(k_pairs_bwd<false>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
@@ -2334,7 +2324,7 @@ extern "C" int pnr_used_points(const int32_t* pidx, const int32_t* n_samples_dev
   hipLaunchKernelGGL(k_pack_used, dim3(grid_for(nw, 256)), dim3(256), 0, st, bytes, nw, bits, used);
   PNR_LAUNCH_CHECK();
   int rc;
-  if ((rc = exclusive_scan(used, nw, nullptr, wpre, n_used_dev, static_cast<char*>(scratch) + hb,
+  if ((rc = exclusive_scan(used, nw, nullptr, wpre, nw + 1, n_used_dev, static_cast<char*>(scratch) + hb,
                            scratch_bytes - hb, st, 0)))
     return rc;
   hipLaunchKernelGGL(k_used_list, dim3(grid_for(n_points, 256)), dim3(256), 0, st, bits, wpre, n_points, used_map,

@@ -327,20 +327,6 @@ constexpr int kPairsWD = 2;
 // lead can be long (c5: 2 steps 55.0 ms, 4 steps 53.9, 6 steps 53.7)
 constexpr int kColWD = 6;
 
-#ifdef PNR_PB_TRACE
-// diagnostic build only (tools/pb_trace.py): s_memtime per phase of the first 8
-// tiles of every wave of workgroups < 512, for the KT = PNR_PB_TRACE launch
-__device__ unsigned long long g_pb_trace[512 * 4 * 8 * 20];
-#define PB_STAMP(i)                                                                            \
-  do {                                                                                         \
-    if (KT == PNR_PB_TRACE && it_tr < 8 && lane == 0 && blockIdx.x < 512)                      \
-      g_pb_trace[((blockIdx.x * 4 + wid) * 8 + it_tr) * 20 + (i)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define PB_STAMP(i) \
-  do {              \
-  } while (0)
-#endif
 
 // GEN = false: no per-point Rw2c, no used_map, no multi-camera batch, no
 // out_weight / out_conf (the render path) -- the general-path branches are compiled out, so no branch
@@ -416,14 +402,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       bL[2 * kHid + kC + threadIdx.x] = A.w.wc3f[((size_t)(8 * 4 + T) * 64 + cc) * 8];
     }
   }
-#ifdef PNR_PB_TRACE
-  int it_tr = -1;
-#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-#ifdef PNR_PB_TRACE
-    ++it_tr;
-#endif
-    PB_STAMP(0);
     // -------------------------------------------- gather (thread = pair col, role = tid >> 7)
     // Order: the gather's own loads, an LDS-only barrier that hands the pair ids
     // (prefetched chain) to the MFMA lanes, their raw P1 row loads, then the
@@ -476,7 +455,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       }
       __builtin_amdgcn_sched_barrier(0);
       lds_barrier();   // prowL: LDS only, the loads above stay in flight
-      PB_STAMP(1);
 #pragma unroll
       for (int pt = 0; pt < kBPT; ++pt) {
         const int pr = prowL[32 * pt + c];
@@ -596,9 +574,7 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
         }
       }
     }
-    PB_STAMP(2);
     __syncthreads();
-    PB_STAMP(3);
     // -------------------------------------------- P1 rows into the accumulators
     f32x16 acc[kBPT * 2];
 #pragma unroll
@@ -617,17 +593,13 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     }
     nx_v = pf_v(tile + gridDim.x);   // the next tile's chain, link 1
     // -------------------------------------------- block1: + W1[:, 224:284] . PE_5 (4 steps), block1.2
-    PB_STAMP(4);
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w1b, Xb, 4, lane);
-    PB_STAMP(5);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     __syncthreads();
-    PB_STAMP(6);
     acc_bias_b<2, kBPT>(acc, bL, lane, T0);
     nx_row = pf_row(nx_v);   // link 2
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w2, Xb, 16, lane);
-    PB_STAMP(7);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     if (wid == 0) {   // block3.0 inputs 256..263 (+ zeros to 271)
@@ -641,21 +613,17 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       }
     }
     __syncthreads();
-    PB_STAMP(8);
     // -------------------------------------------- block3
 #pragma unroll
     for (int i = 0; i < kBPT * 2; ++i) acc[i] = (f32x16){0.f};
     nx_pid = pf_pid(nx_row);   // link 3
     nx_drow = pf_drow(nx_row);
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w3, Xb, 17, lane);
-    PB_STAMP(9);
     __syncthreads();
     store_act_b<2, kBPT, kPB>(acc, Xb, neg, lane, T0);
     __syncthreads();
-    PB_STAMP(10);
     acc_bias_b<2, kBPT>(acc, bL + kHid, lane, T0);
     mlp_layer_b<2, kBPT, 8, kPB, kPairsWD<KT>>(acc, w4, Xb, 16, lane);
-    PB_STAMP(11);
     __syncthreads();   // Xb is free: the K-sums are staged there (hid rows, kHP pitch)
     // -------------------------------------------- alpha + K sums from the fp32 accumulators
     {
@@ -756,7 +724,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
 #pragma unroll
       for (int pt = 0; pt < kBPT; ++pt) apart[wid * kBT + 32 * pt + c] = pa_part[pt];
     }
-    PB_STAMP(12);
     __syncthreads();
     if (wid < 2) {
       const int col = 64 * wid + lane;
@@ -789,7 +756,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
     }
     }
     __syncthreads();
-    PB_STAMP(13);
     // -------------------------------------------- colour branch on the tile's samples
     // [hid (K-summed, staged above), PE_4(view)] -> 128 -> 128 -> 128 (the
     // reference's color_branch, point_aggregators.py:640-646), columns = samples:
@@ -807,13 +773,11 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       __syncthreads();
       store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
       __syncthreads();
-      PB_STAMP(14);
       acc_bias_b<1, PTc>(cacc, bL + 2 * kHid, lane, wid);
       mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc2, Xb, 8, lane);
       __syncthreads();
       store_act_b<1, PTc, kPB>(cacc, Xb, neg, lane, wid);
       __syncthreads();
-      PB_STAMP(15);
       acc_bias_b<1, PTc>(cacc, bL + 2 * kHid + kC, lane, wid);
       mlp_layer_b<1, PTc, 4, kPB, kColWD>(cacc, wc3, Xb, 8, lane);
       __syncthreads();   // every wave's layer-3 reads of Xb are done
@@ -828,7 +792,6 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
               make_float4(lrelu(cacc[pt][4 * q], neg), lrelu(cacc[pt][4 * q + 1], neg), lrelu(cacc[pt][4 * q + 2], neg),
                           lrelu(cacc[pt][4 * q + 3], neg));
       __syncthreads();
-      PB_STAMP(16);
       typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
       for (int r2 = wid; r2 < SPT / 2; r2 += kBWaves) {
         const int r = 2 * r2 + (lane >> 5), l = lane & 31;
@@ -846,15 +809,9 @@ __global__ void __launch_bounds__(64 * kBWaves, 2) k_pairs_b(AggArgsB A, const i
       }
     }
     __syncthreads();
-    PB_STAMP(17);
   }
 }
 
-#ifdef PNR_PB_TRACE
-extern "C" __attribute__((visibility("default"))) int pnr_dev_pb_trace(void* host, size_t bytes) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pb_trace), bytes) == hipSuccess ? 0 : 3;
-}
-#endif
 
 template <int KT>
 static void launch_pairs_b(bool gen, unsigned grid, hipStream_t st, const AggArgsB& a, const int32_t* list,

@@ -764,7 +764,7 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
                        h->sort_hist.as<int32_t>());
     PNR_LAUNCH_CHECK();
     if ((rc = exclusive_scan(h->sort_hist.as<int32_t>(), (int64_t)256 * tiles, nullptr, h->sort_offs.as<int32_t>(),
-                             nullptr, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+                             (int64_t)(h->sort_offs.bytes / 4), nullptr, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
     hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], pass ? vals[cur] : nullptr, n,
                        shift, tiles, h->sort_offs.as<int32_t>(), keys[cur ^ 1], vals[cur ^ 1]);
@@ -777,7 +777,7 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
                      cell_end, counters);
   PNR_LAUNCH_CHECK();
   // slot = rank of the claimer's point id (the serial claim order)
-  if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 0, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+  if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, (int64_t)(h->pt_slot.bytes / 4), counters + 0, h->scan_tmp.p, h->scan_tmp.bytes, st)))
     return rc;
   if (n > cap_o) {
     // more points than max_o: the occupied voxels may overflow it (counters[0]
@@ -793,7 +793,7 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
     }
     hipLaunchKernelGGL(k_sel_apply, dim3(gs), dim3(kBlock), 0, st, n, g.seed, (int)cap_o, ss, hist, pt_flag);
     PNR_LAUNCH_CHECK();
-    if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, counters + 6, h->scan_tmp.p, h->scan_tmp.bytes, st, 0,
+    if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, (int64_t)(h->pt_slot.bytes / 4), counters + 6, h->scan_tmp.p, h->scan_tmp.bytes, st, 0,
                              &ss->active)))
       return rc;
   }
@@ -890,7 +890,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
     PNR_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pack_held, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, qw, wcnt);
     PNR_LAUNCH_CHECK();
-    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, (int64_t)((h->cell_bytes.bytes - words * 32) / 4), counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
     hipLaunchKernelGGL(k_word_rank, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, words, wrank, qw);
     PNR_LAUNCH_CHECK();
@@ -898,7 +898,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
                        occ_numpnts, occ_2_coor, qw, h->q_rank_slot.as<int32_t>(), h->q_rank_cnt.as<int32_t>());
     PNR_LAUNCH_CHECK();
     if ((rc = exclusive_scan(h->q_rank_cnt.as<int32_t>(), cap_o, counters + 4, h->q_rec_off.as<int32_t>(),
-                             counters + 5, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+                             (int64_t)(h->q_rec_off.bytes / 4), counters + 5, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
     hipLaunchKernelGGL(k_fill_recs, dim3(grid_for(cap_o * 16, kBlock)), dim3(kBlock), 0, st, g, counters + 4,
                        h->q_rank_slot.as<int32_t>(), h->q_rec_off.as<int32_t>(), occ_pts, h->q_recs.as<float4>());
@@ -911,6 +911,10 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   if (h->stats_pending) PNR_HIP(hipEventSynchronize(h->stats_ev));   // the previous build's copy is done
   PNR_HIP(hipMemcpyAsync(h->host_cnt, counters, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   PNR_HIP(hipMemcpyAsync(h->host_geom, geo, sizeof(QGrid), hipMemcpyDeviceToHost, st));
+  if (h->geom_on_device) {   // the bbox this build's geometry came from (pnr_grid_bbox)
+    if (!h->host_bbox) PNR_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->host_bbox), 8 * sizeof(float)));
+    PNR_HIP(hipMemcpyAsync(h->host_bbox, h->bbox.p, 8 * sizeof(float), hipMemcpyDeviceToHost, st));
+  }
   PNR_HIP(hipEventRecord(h->stats_ev, st));
   h->stats_pending = true;
   h->gp = *p;
@@ -971,6 +975,14 @@ extern "C" int pnr_grid_build_dev(pnr_handle* h, const float* xyz_dev, int64_t n
   p.seed = sp->seed;
   h->geom_on_device = true;
   return grid_build_body(h, xyz_dev, n, &p, st);
+}
+
+extern "C" int pnr_grid_bbox(pnr_handle* h, float out6[6]) {
+  PNR_CHECK_ARG(h && out6, "grid_bbox: null pointer");
+  PNR_CHECK_ARG(h->built && h->geom_on_device && h->host_bbox, "grid_bbox: no device-geometry build");
+  PNR_HIP(hipEventSynchronize(h->stats_ev));
+  for (int a = 0; a < 6; ++a) out6[a] = h->host_bbox[a];
+  return PNR_OK;
 }
 
 extern "C" int pnr_grid_geometry(pnr_handle* h, float shift[3], float vsize[3], int32_t dims[3]) {

@@ -48,7 +48,9 @@ inline unsigned grid_for(int64_t items, int block, int max_blocks = 256 * 8) {
 // Device-wide exclusive scan (scan.hip).
 int64_t scan_blocks(int64_t n);
 size_t scan_scratch_bytes(int64_t n);
-int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
+// out_cap: int32 entries the caller allocated at out; the scan writes out[0 .. n]
+// (n + 1 entries: the grand total lands at out[n_eff]), checked here.
+int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out, int64_t out_cap,
                    int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
                    int as_flag = 0,   // as_flag: scan (in[i] != 0) instead of in[i]
                    const int32_t* run_if = nullptr);  // device flag: 0 = leave out untouched
@@ -201,6 +203,7 @@ struct pnr_handle {
   DevBuf geom;            // QGrid of the built grid (device)
   DevBuf bbox;            // float [8] point bbox of the last pnr_grid_build_dev
   QGrid* host_geom = nullptr;   // pinned copy of geom behind stats_ev
+  float* host_bbox = nullptr;   // pinned copy of bbox (device builds) behind stats_ev
   bool geom_on_device = false;  // gp.shift / dims are bounds, the exact geometry is geom (device)
   int64_t n_points = 0;
   pnr_grid_stats stats{};
@@ -214,6 +217,8 @@ struct pnr_handle {
     if (host_cnt) (void)hipHostFree(host_cnt);
     if (host_geom) (void)hipHostFree(host_geom);
     host_geom = nullptr;
+    if (host_bbox) (void)hipHostFree(host_bbox);
+    host_bbox = nullptr;
     if (stats_ev) (void)hipEventDestroy(stats_ev);
     host_cnt = nullptr;
     stats_ev = nullptr;

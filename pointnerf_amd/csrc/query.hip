@@ -624,7 +624,7 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
     hipLaunchKernelGGL((k_march_coop<kMarchLanes, kMarchUnroll>), dim3(grid_for(R * kMarchLanes, kQBlock, kMarchGridCap)),
                        dim3(kQBlock), 0, st, q, g_dev, qp->SR, h->occ_bits.as<uint32_t>(), b->n_filled, b->slot_d);
   PNR_LAUNCH_CHECK();
-  if ((rc = exclusive_scan(b->n_filled, R, nullptr, b->ray_off, b->counts + 0, b->scratch,
+  if ((rc = exclusive_scan(b->n_filled, R, nullptr, b->ray_off, R + 1, b->counts + 0, b->scratch,
                            b->scratch_bytes, st)))
     return rc;
   hipLaunchKernelGGL(k_fill_list, dim3(grid_for(R, kQBlock)), dim3(kQBlock), 0, st, R, qp->SR,
@@ -657,13 +657,13 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   else PNR_KNN(32);
 #undef PNR_KNN
   PNR_LAUNCH_CHECK();
-  if ((rc = exclusive_scan(b->vflag, RS, b->counts + 0, b->valid_off, b->counts + 1, b->scratch,
+  if ((rc = exclusive_scan(b->vflag, RS, b->counts + 0, b->valid_off, RS + 1, b->counts + 1, b->scratch,
                            b->scratch_bytes, st)))
     return rc;
   hipLaunchKernelGGL(k_valid_list, dim3(grid_for(RS, kQBlock)), dim3(kQBlock), 0, st, b->vflag,
                      b->valid_off, b->valid_list, b->counts);
   PNR_LAUNCH_CHECK();
-  if ((rc = exclusive_scan(b->ray_vcnt, R, nullptr, b->ray_row, b->counts + 3, b->scratch,
+  if ((rc = exclusive_scan(b->ray_vcnt, R, nullptr, b->ray_row, R + 1, b->counts + 3, b->scratch,
                            b->scratch_bytes, st, /*as_flag=*/1)))
     return rc;
   return PNR_OK;

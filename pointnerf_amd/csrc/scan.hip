@@ -199,11 +199,14 @@ int64_t scan_blocks(int64_t n) { return cdiv(n > 0 ? n : 1, kScanTile); }
 
 size_t scan_scratch_bytes(int64_t n) { return (size_t)(scan_blocks(n) + 1) * sizeof(int32_t); }
 
-int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out,
+int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out, int64_t out_cap,
                    int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
                    int as_flag, const int32_t* run_if) {
   PNR_CHECK_ARG(in && out && scratch, "scan: null pointer");
   PNR_CHECK_ARG(n >= 0, "scan: negative length");
+  // the grand total is stored at out[n_eff] (n_eff <= n): out needs n + 1 entries
+  PNR_CHECK_ARG(out_cap >= n + 1, "scan: out holds %lld entries, the scan of %lld writes %lld",
+                (long long)out_cap, (long long)n, (long long)n + 1);
   const int64_t nb = scan_blocks(n);
   PNR_CHECK_ARG(scratch_bytes >= scan_scratch_bytes(n), "scan: scratch too small (%zu < %zu)",
                 scratch_bytes, scan_scratch_bytes(n));
@@ -233,8 +236,8 @@ extern "C" int pnr_scan_scratch_bytes(int64_t n, size_t* out) {
 }
 
 extern "C" int pnr_exclusive_scan_i32(const int32_t* in, int64_t n, const int32_t* n_dev,
-                                      int32_t* out, int32_t* total_dev, void* scratch,
+                                      int32_t* out, int64_t out_len, int32_t* total_dev, void* scratch,
                                       size_t scratch_bytes, void* stream) {
-  return pnr::exclusive_scan(in, n, n_dev, out, total_dev, scratch, scratch_bytes,
+  return pnr::exclusive_scan(in, n, n_dev, out, out_len, total_dev, scratch, scratch_bytes,
                              pnr::as_stream(stream), 0);
 }

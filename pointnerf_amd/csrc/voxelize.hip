@@ -150,6 +150,7 @@ struct VoxScratch {
   int32_t* idx_out;
   int32_t* flag;
   int32_t* off;
+  int64_t off_cap;   // entries at off (m + 1: the scan's total lands at off[n])
   int32_t* start;
   float* box;
   VoxSpace* space;
@@ -185,6 +186,7 @@ size_t carve(void* base, int64_t n, VoxScratch* s) {
   t.idx_out = reinterpret_cast<int32_t*>(take(m * 4));
   t.flag = reinterpret_cast<int32_t*>(take(m * 4));
   t.off = reinterpret_cast<int32_t*>(take((m + 1) * 4));
+  t.off_cap = m + 1;
   t.start = reinterpret_cast<int32_t*>(take((m + 1) * 4));
   t.box = reinterpret_cast<float*>(take(8 * 4));
   t.space = reinterpret_cast<VoxSpace*>(take(sizeof(VoxSpace)));
@@ -231,7 +233,7 @@ extern "C" int pnr_vox_closest(const float* xyz, int64_t n, int32_t vox_res, flo
   PNR_HIP(rocprim::radix_sort_pairs(s.sort, sb, s.keys_in, s.keys_out, s.idx_in, s.idx_out, (size_t)n, 0, 63, st));
   hipLaunchKernelGGL(k_vox_flags, dim3(g), dim3(kVBlock), 0, st, s.keys_out, n, s.flag);
   PNR_LAUNCH_CHECK();
-  if ((rc = exclusive_scan(s.flag, n, nullptr, s.off, counts, s.scan, s.scan_bytes, st))) return rc;
+  if ((rc = exclusive_scan(s.flag, n, nullptr, s.off, s.off_cap, counts, s.scan, s.scan_bytes, st))) return rc;
   hipLaunchKernelGGL(k_vox_runs, dim3(g), dim3(kVBlock), 0, st, n, s.flag, s.off, s.idx_out, counts, s.start,
                      inv_idx);
   PNR_LAUNCH_CHECK();

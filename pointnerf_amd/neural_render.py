@@ -13,7 +13,7 @@ forward's activations and its backward runs ``pnr_neural_render_bwd`` (data
 gradients as flipped-weight convolutions on the same kernel, weight gradients
 as implicit-GEMM reductions over the pixels, deterministic), the gradients of
 the reference's torch autograd through neural_renderer.py:81-104.
-``forward_torch`` is the torch-convolution restatement the tests check against.
+(The torch-convolution restatement the tests check against is tests/nr_ref.py.)
 """
 from __future__ import annotations
 
@@ -21,7 +21,6 @@ import math
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import _lib as L
 from .aggregator import frag_pack, pack_h2_dev
@@ -142,16 +141,6 @@ class NeuralRenderer(nn.Module):
                                             t["ws"].data_ptr(), 0.2), t
         self._packed_t_key = key
         return self._packed_t
-
-    def forward_torch(self, x):
-        """neural_renderer.py:81-104 with torch convolutions (autograd path)."""
-        x = x.permute(0, 3, 1, 2)
-        rgb = self.conv_rgb[0](x)
-        net = x
-        for i, layer in enumerate(self.conv_layers):
-            net = F.leaky_relu(layer(net), 0.2)
-            rgb = rgb + self.conv_rgb[i + 1](net)
-        return torch.sigmoid(rgb).permute(0, 2, 3, 1)
 
     def _fwd(self, x):
         """pnr_neural_render_fwd -> (rgb [H*W, 3], x [H*W, 128], forward scratch)."""

@@ -195,15 +195,18 @@ class GradReducer:
     with a loss averaged per rank."""
 
     def __init__(self, dense_params, point_params, group=None, host_group=None):
-        """Collective when the process group is not gloo: every rank of the default
-        group must construct its reducer (it creates the gloo group that carries
-        the host-side row counts, unless ``host_group`` -- a gloo group over the
-        same ranks as ``group`` -- is passed)."""
+        """Collective when the process group is not gloo: EVERY rank of the default
+        group must construct its reducer, in the same order relative to other
+        group creations -- it creates the gloo group that carries the host-side
+        row counts (dist.new_group is a collective over the default group),
+        whether or not this rank's reducer has point parameters, unless
+        ``host_group`` (a gloo group over the same ranks as ``group``) is
+        passed."""
         self.dense = [p for p in dense_params if p.requires_grad]
         self.points = [p for p in point_params if p is not None and p.requires_grad]
         self.group = group
         self._host_group = host_group   # gloo group for host-side integers (no device sync)
-        if self.points and host_group is None:
+        if host_group is None:
             import torch.distributed as dist
             if dist.is_initialized() and dist.get_backend(group) != "gloo":
                 ranks = None if group is None else dist.get_process_group_ranks(group)

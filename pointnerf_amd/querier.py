@@ -73,24 +73,24 @@ class GridHP(dict):
     (pnr_grid_build_dev): the point-independent entries are host values, the
     bbox-derived ones (shift, dims, ranges) are read back from the device
     geometry on first access (one wait for the build).  The read is tied to the
-    build that made this dict: after a rebuild of the handle, or an in-place
-    edit of the points, an unread entry raises instead of returning the newer
-    geometry; and it is refused while the stream is being captured (the wait
-    is a host synchronisation)."""
+    build that made this dict (its generation): after a rebuild of the handle an
+    unread entry raises instead of returning the newer geometry.  An in-place
+    edit of the points without a rebuild leaves the device geometry the one of
+    this build, so the read still returns it.  It is refused while the stream
+    is being captured (the wait is a host synchronisation)."""
 
     def __init__(self, handle, base, gen):
         super().__init__(base)
         self._handle = handle
         self._gen = gen
-        self._xyz_version = handle._xyz._version
 
     def __missing__(self, key):
         if key not in ("shift", "dims", "ranges"):
             raise KeyError(key)
         h = self._handle
-        if h.gen != self._gen or h._xyz._version != self._xyz_version:
-            raise L.PnrError(f"grid hyperparameter {key!r} read after the grid was rebuilt or its points "
-                             "changed: read it before the next build (or use the handle's current hp)")
+        if h.gen != self._gen:
+            raise L.PnrError(f"grid hyperparameter {key!r} read after the grid was rebuilt: read it before "
+                             "the next build (or use the handle's current hp)")
         if _capturing():
             raise L.PnrError(f"grid hyperparameter {key!r} first read during stream capture: it waits for the "
                              "build (read it once before capturing)")
@@ -281,8 +281,11 @@ class GridHandle:
         return b[:3], b[3:]
 
     def bbox_max(self):
-        """Max corner of the last built cloud's bbox (host read; GridHP's ranges)."""
-        return self.bbox(self._xyz)[1]
+        """Max corner of the bbox the last device build derived its geometry from
+        (pnr_grid_bbox: waits for the build; GridHP's ranges)."""
+        out = (L.c_float * 6)()
+        L.check(L.lib().pnr_grid_bbox(self.h, out), "pnr_grid_bbox")
+        return np.array(list(out)[3:], np.float32)
 
     def build(self, opt, xyz: torch.Tensor, force: bool = False):
         """get_hyperparameters + build_occ_vox; skipped when the point tensor is

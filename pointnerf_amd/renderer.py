@@ -362,8 +362,12 @@ class NeuralPointsRayMarching(nn.Module):
         aggregate (the query is memory-latency bound, the aggregate MFMA bound,
         and one query workgroup fits beside a k_pairs_h2 workgroup on a CU).  The
         aggregate waits for it; the query waits only for the launch-stream work
-        that last read its buffers (two sets, alternating).  The caller
-        guarantees the call's inputs (rays, cameras) are ready on that stream.
+        that last read its buffers (two sets, alternating) and, when the points
+        changed since the last such call (new storage or version, or
+        ``force_grid``), for the whole launch stream.  The call's own copies of
+        its inputs (contiguous rays, camera tables) are made on the query
+        stream; the caller makes ``raydir`` / ``campos`` / ``camrot`` /
+        ``ray_cam`` themselves ready on that stream.
 
         fp32h2: the f16 split holds activations below 65504 only.  Each call
         reads the launches' range flag once (a 4-byte read after the last
@@ -552,9 +556,35 @@ class NeuralPointsRayMarching(nn.Module):
             if bg is None:
                 raise L.PnrError(f"bg_color must have 1 or {C} channels")
         from .querier import camera_tables
-        campos, camrot = camera_tables(campos, camrot, ray_cam)
-        if ray_cam is not None:
-            ray_cam = ray_cam.to(device=dev, dtype=torch.int32).contiguous()
+        use_qs = query_stream is not None and capacity is not None
+        launch = torch.cuda.current_stream(dev)
+        if use_qs:
+            # The query's inputs are made on query_stream itself (the caller makes
+            # campos / camrot / raydir / ray_cam ready on the launch stream, but the
+            # copies below are this call's own).  The points can change on the launch
+            # stream (an optimizer step on xyz, a forced rebuild): the query stream
+            # then waits for the launch stream before the grid build reads them.
+            xkey = (np_.xyz.data_ptr(), np_.xyz._version)
+            if force_grid or getattr(state, "q_xkey", None) != xkey:
+                query_stream.wait_stream(launch)
+            state.q_xkey = xkey
+            with torch.cuda.stream(query_stream):
+                campos, camrot = camera_tables(campos, camrot, ray_cam)
+                if ray_cam is not None:
+                    ray_cam = ray_cam.to(device=dev, dtype=torch.int32).contiguous()
+                ev_cam = torch.cuda.Event()
+                ev_cam.record(query_stream)
+            # np_.tables and the aggregate read the camera tables on the launch stream
+            # (the query stream's tail is the previous query, which the launch stream
+            # already waited for: no overlap is lost)
+            launch.wait_event(ev_cam)
+            for t in (campos, camrot, ray_cam):
+                if t is not None:
+                    t.record_stream(launch)
+        else:
+            campos, camrot = camera_tables(campos, camrot, ray_cam)
+            if ray_cam is not None:
+                ray_cam = ray_cam.to(device=dev, dtype=torch.int32).contiguous()
         bf16 = precision == "bf16"
         mlp, _keepw = self.aggregator.packed_bf16() if bf16 else self.aggregator.packed()
         mlpx = mlph = _keepx = _keeph = None
@@ -619,10 +649,15 @@ class NeuralPointsRayMarching(nn.Module):
 
         for ci, r0 in enumerate(range(0, R, chunk)):
             r1 = min(R, r0 + chunk)
-            rd = raydir[r0:r1].contiguous()
+            if use_qs:   # a non-contiguous raydir's copy belongs to the query stream too
+                with torch.cuda.stream(query_stream):
+                    rd = raydir[r0:r1].contiguous()
+                rd.record_stream(launch)
+            else:
+                rd = raydir[r0:r1].contiguous()
             rc = None if ray_cam is None else ray_cam[r0:r1]
             slot = None
-            if query_stream is not None and capacity is not None:
+            if use_qs:
                 # the query on its own stream, two buffer sets in turn; each set is
                 # reused after the launch-stream work that read it (its event)
                 if getattr(state, "qring", None) is None:
@@ -664,13 +699,14 @@ class NeuralPointsRayMarching(nn.Module):
             # point half only for the points this batch's neighbour lists reference
             # (pnr_used_points, device list and count), written at their own rows of the P1
             # table (pnr_points.used without used_map) -- no indirection in the pairs kernel
-            used_only = (bf16 and self.p1_used_only and n_chunks == 1 and keep is None and not reuse_p1)
+            scratch, ready = self._agg_scratch(state, max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
+            # (a reuse_p1 call after a used-only one finds the table partial (key
+            # cleared): it computes its own used rows, not the whole table)
+            used_only = (bf16 and self.p1_used_only and n_chunks == 1 and keep is None and not ready)
             if used_only:
                 pts.used = L.ptr(self._used_points(state, bufs, K, pts.n))
                 pts.n_used, pts.used_map = pts.n, None
                 pts.n_used_dev = bufs.counts.data_ptr() + 5 * 4
-            scratch, ready = self._agg_scratch(state, max(Sv, 1), pts.n, dev, bf16, reuse_p1 or r0 > 0, precision)
-            if used_only:
                 ready, state.scratch_key = False, None   # the table holds this batch's rows only
             if p1_side is not None:   # P1 written into this same scratch by the side stream
                 torch.cuda.current_stream(dev).wait_event(p1_side)

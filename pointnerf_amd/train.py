@@ -38,8 +38,7 @@ from .aggregator import frag_pack, frag_pack_x3
 
 # x3 backward: the block3.0 extras' colour / dir gradients per point inside
 # pnr_pairs_to_points_ex (True, the product).  False hands them to
-# pnr_aggregate_bwd_pairs_x3 (k_extras_bwd, or the in-kernel experiment build of
-# tools/extras_variant.sh) -- DESIGN.md section 10.
+# pnr_aggregate_bwd_pairs_x3 (k_extras_bwd) -- DESIGN.md section 10.
 X3_POINT_EXTRAS = True
 
 _PARAM_NAMES = ("block1.0.weight", "block1.0.bias", "block1.2.weight", "block1.2.bias",

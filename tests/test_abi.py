@@ -54,6 +54,21 @@ def test_ctypes_binding_covers_header_and_loads(built):
     assert lib.pnr_destroy(None) == L.PNR_OK
 
 
+def test_scan_refuses_an_output_without_room_for_the_total(built):
+    """exclusive_scan stores the grand total at out[n]: an `out` of n entries is
+    refused on the host before any launch (the r05 used_map overrun).
+    The pointers are never dereferenced: the check runs first."""
+    from pointnerf_amd import _lib as L
+    lib = L.lib()
+    fake = L.c_void_p(0x1000)
+    n = 1000
+    nb = L.c_size_t(0)
+    assert lib.pnr_scan_scratch_bytes(n, L.ctypes.byref(nb)) == L.PNR_OK
+    rc = lib.pnr_exclusive_scan_i32(fake, n, None, fake, n, None, fake, nb.value, None)
+    assert rc == L.PNR_EINVAL
+    assert b"out holds 1000 entries" in lib.pnr_last_error()
+
+
 def test_code_object_targets_gfx950(built):
     data = open(built, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data

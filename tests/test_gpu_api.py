@@ -15,6 +15,7 @@ import torch
 from formula import LEGO_SHAPES, UPSTREAM_SHAPES, formula_params
 from oracle import oracle as O
 from oracle import oracle_grad as OG
+from nr_ref import neural_render_torch
 from scenes import oracle_points, scene
 
 pytestmark = pytest.mark.gpu
@@ -247,6 +248,6 @@ def test_module_neural_render_cnn_trains(cuda):
     nr64.load_state_dict({k: v.detach().cpu() for k, v in nr.state_dict().items()})
     nr64 = nr64.double().to(cuda)
     x2 = coarse.double().requires_grad_(True)
-    (nr64.forward_torch(x2) * g.double().reshape(1, H, W, 3)).sum().backward()
+    (neural_render_torch(nr64, x2) * g.double().reshape(1, H, W, 3)).sum().backward()
     err = float((x1.grad.double() - x2.grad).abs().max())
     assert err <= 2e-5 * max(float(x2.grad.abs().max()), 1e-3), err

@@ -96,6 +96,24 @@ def test_query_stream_equals_sync(cuda, precision):
     g = m.render_rays(*cams[2], 2.0, 6.0, bg, sync=False, query_stream=qs)
     m.finish()
     assert m.overflow_rerenders == r0 + 1 and _eq(want[2], g)
+    # a non-contiguous raydir (its contiguous copy is the call's own, made on the
+    # query stream) and an in-place point update on the launch stream between
+    # queued calls (the query stream then waits for the launch stream)
+    cp, cr, rd = cams[1]
+    rd_nc = torch.cat([rd, rd], 1)[:, :3]
+    assert not rd_nc.is_contiguous()
+    g = m.render_rays(cp, cr, rd_nc, 2.0, 6.0, bg, sync=False, query_stream=qs)
+    m.finish()
+    assert _eq(want[1], g)
+    xyz = m.neural_points.xyz
+    with torch.no_grad():
+        g0 = m.render_rays(*cams[0], 2.0, 6.0, bg, sync=False, query_stream=qs)
+        xyz.add_(0.0625)                 # launch stream, after the queued call (bumps xyz._version)
+        g1 = m.render_rays(*cams[0], 2.0, 6.0, bg, sync=False, query_stream=qs)
+        m.finish()
+        moved = [t.clone() for t in m.render_rays(*cams[0], 2.0, 6.0, bg)]
+        xyz.sub_(0.0625)
+    assert _eq(want[0], g0) and _eq(moved, g1)
 
 
 def test_side_stream_p1_equals_sync(cuda):

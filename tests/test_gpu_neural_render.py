@@ -7,6 +7,8 @@ import numpy as np
 import pytest
 import torch
 
+from nr_ref import neural_render_torch
+
 pytestmark = pytest.mark.gpu
 
 
@@ -22,7 +24,7 @@ def test_neural_render_vs_torch(cuda, H, W, precision):
     m.precision = precision
     x = torch.randn((1, H, W, 128)) * 0.5
     with torch.no_grad():
-        ref = m.forward_torch(x.double().float())           # CPU fp32 convolutions
+        ref = neural_render_torch(m, x.double().float())           # CPU fp32 convolutions
         md = m.to(cuda)
         got = md(x.to(cuda)).cpu()
     assert got.shape == (1, H, W, 3)
@@ -62,7 +64,7 @@ def test_neural_render_backward_vs_autograd(cuda, H, W, xs, gs, precision):
     floor = 1e-3 * gs * min(xs, 1.0)
     md = m.double()
     xr = x.double().requires_grad_(True)
-    ref_out = md.forward_torch(xr)
+    ref_out = neural_render_torch(md, xr)
     (ref_out * g.double()).sum().backward()
     ref = {"x": xr.grad} | {n: p.grad for n, p in md.named_parameters()}
     mg = NeuralRenderer(input_dim=128)

@@ -70,9 +70,14 @@ def test_grid_tables_bit_exact_sizes_and_overflow(cuda, n, max_o, P):
         assert g["n_occ"] > max_o and st["n_points_dropped"] > 0   # both reservoirs ran
 
 
-@pytest.mark.parametrize("K,theta", [(8, 30.0), (4, 130.0)])
-def test_query_points_bit_exact(cuda, K, theta):
-    sc = scene(20000, H=48, W=40, theta=theta, K=K)
+# K 16 / 24 / 32 run the KMAX = 16 / 32 instantiations of k_knn (their
+# LDS neighbour columns and replace-phase rescans are otherwise untested); their
+# denser clouds and larger P fill all K slots of some samples, so candidates
+# beyond K replace farther ones
+@pytest.mark.parametrize("K,theta,n,P", [(8, 30.0, 20000, 9), (4, 130.0, 20000, 9), (16, 70.0, 200000, 26),
+                                         (24, 200.0, 300000, 32), (32, 300.0, 300000, 40)])
+def test_query_points_bit_exact(cuda, K, theta, n, P):
+    sc = scene(n, H=48, W=40, theta=theta, K=K, P=P)
     _, out = _run(sc, cuda)
     ref = O.query_points(sc["opt"], sc["xyz"], sc["campos"], sc["camrot"], sc["raydir"], near=2.0, far=6.0)
     pidx, loc, loc_w, dirs, ray_mask = [t.cpu().numpy() for t in out[:5]]
@@ -80,6 +85,8 @@ def test_query_points_bit_exact(cuda, K, theta):
     assert ref["ray_mask"].sum() > 100, "scene must exercise the query"
     assert pidx.shape == (1,) + ref["sample_pidx"].shape
     assert np.array_equal(pidx[0], ref["sample_pidx"])          # same neighbours, same order
+    if K >= 16:
+        assert (ref["sample_pidx"][..., K - 1] >= 0).sum() > 0, "some samples must fill all K slots"
     assert np.array_equal(loc_w[0], ref["sample_loc_w"])
     assert np.array_equal(loc[0], ref["sample_loc"])
     assert np.array_equal(dirs[0], ref["sample_ray_dirs"])
@@ -148,7 +155,7 @@ def test_scan_matches_cumsum(cuda):
         nb = L.c_size_t(0)
         L.lib().pnr_scan_scratch_bytes(n, L.ctypes.byref(nb))
         scratch = torch.empty(nb.value, dtype=torch.uint8, device=cuda)
-        L.check(L.lib().pnr_exclusive_scan_i32(L.ptr(x), n, None, L.ptr(out), L.ptr(tot), L.ptr(scratch),
+        L.check(L.lib().pnr_exclusive_scan_i32(L.ptr(x), n, None, L.ptr(out), n + 1, L.ptr(tot), L.ptr(scratch),
                                                nb.value, L.stream_ptr()), "scan")
         ref = np.concatenate([[0], np.cumsum(x.cpu().numpy())])
         assert np.array_equal(out.cpu().numpy(), ref)
@@ -261,6 +268,27 @@ def test_device_geometry_equals_host(cuda, case):
     _, oh = _run(sc, cuda, q_host)
     for a, b in zip(od[:5], oh[:5]):
         assert torch.equal(a, b)
+
+
+def test_grid_hp_tied_to_its_build_not_to_point_edits(cuda):
+    """GridHP's lazy geometry read after an in-place point edit
+    (no rebuild) returns the geometry of the grid that exists; after a rebuild
+    an unread entry of the old dict raises."""
+    from pointnerf_amd._lib import PnrError
+    sc = scene(20000, H=24, W=24, theta=70.0)
+    t = torch.from_numpy(sc["xyz"]).to(cuda)
+    q = _engine(sc, cuda)
+    hp = q.grid.build(sc["opt"], t)
+    want = O.grid_build(sc["opt"], sc["xyz"])["hp"]
+    with torch.no_grad():
+        t.mul_(1.01)                     # in place, no rebuild
+    for k in ("shift", "dims"):
+        assert np.array_equal(np.asarray(hp[k]), np.asarray(want[k])), k
+    hp2 = q.grid.build(sc["opt"], t)     # the version changed: a rebuild, hp2 unread
+    assert type(hp2).__name__ == "GridHP"
+    q.grid.build(sc["opt"], t, force=True)
+    with pytest.raises(PnrError):
+        hp2["shift"]
 
 
 def test_device_grid_cell_budget_takes_host_path(cuda):

@@ -4,6 +4,8 @@ import json, os, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pointnerf_amd.neural_render import NeuralRenderer
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+from nr_ref import neural_render_torch  # noqa: E402
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 m = NeuralRenderer(input_dim=128).to(dev)
@@ -38,7 +40,7 @@ def step():
 
 def step_torch():
     m.zero_grad(set_to_none=True)
-    (m.forward_torch(xg) * g).sum().backward()
+    (neural_render_torch(m, xg) * g).sum().backward()
 
 
 res = {}
