@@ -16,6 +16,10 @@ for s in $STEPS; do
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
       cut -c1-600 $O/bench.json ;;
+    launch)   # bench.py --gpus 2 self-launch rehearsal: two ranks on the box's one GPU over gloo
+      PNR_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 > $O/launch2.json \
+        2> $O/launch2.err || { tail -20 $O/launch2.err; exit 1; }
+      cut -c1-700 $O/launch2.json ;;
     c4|c5)
       timeout -k 10 600 python bench.py --config $s --steps 5 --warmup 2 > $O/bench_$s.json 2> $O/bench_$s.err \
         || { tail -20 $O/bench_$s.err; exit 1; }
