@@ -175,45 +175,62 @@ __device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int
 // voxel's point count, and its first P ids the serial fill_occ2pnts order.
 // Points outside the grid carry the key `sentinel` (> every cell) and sort last.
 template <typename K>
+__device__ __forceinline__ int rs_digit(K k, int shift) {
+  return (int)((k >> shift) & (K)255);
+}
+
+constexpr int kRsItems = 8;
+constexpr int kRsTile = kBlock * kRsItems;  // 2048 keys: ~4 tiles per CU at 2 M points
+
+// Block b: the keys of sort tile b (kRsTile points) and the radix sort's first
+// digit histogram of that tile (k_rs_hist's pass 0, without a launch and a
+// re-read of the keys), and the empty state of slots [b kRsTile, (b+1) kRsTile).
+template <typename K>
 __global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ xyz, int64_t n, GridDev g0,
                                                       const QGrid* __restrict__ geo, K sentinel,
                                                       K* __restrict__ keys, int64_t n_slots,
                                                       int32_t* __restrict__ pt_flag,
                                                       int32_t* __restrict__ occ_numpnts,
-                                                      int32_t* __restrict__ occ_2_coor, int32_t* __restrict__ counters) {
+                                                      int32_t* __restrict__ occ_2_coor, int32_t* __restrict__ counters,
+                                                      int tiles, int32_t* __restrict__ hist) {
+  __shared__ int32_t h[256];
   const GridDev g = with_geom(g0, geo);
   if (blockIdx.x == 0 && threadIdx.x < 8) counters[threadIdx.x] = 0;
-  const int64_t m = n > n_slots ? n : n_slots;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (i < n) {
-      float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
-      int c[3];
-      const int64_t cell = cell_of(p, g, c);
-      keys[i] = cell >= 0 ? (K)cell : sentinel;
-      pt_flag[i] = 0;
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRsTile;
+  if ((int)blockIdx.x < tiles) {
+#pragma unroll 4
+    for (int r = 0; r < kRsItems; ++r) {
+      const int64_t i = base + r * kBlock + threadIdx.x;
+      if (i < n) {
+        float p[3] = {xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2]};
+        int c[3];
+        const int64_t cell = cell_of(p, g, c);
+        const K k = cell >= 0 ? (K)cell : sentinel;
+        keys[i] = k;
+        pt_flag[i] = 0;
+        atomicAdd(&h[rs_digit(k, 0)], 1);
+      }
     }
-    if (i < n_slots) {   // the slot tables' empty state
+  }
+  for (int r = 0; r < kRsItems; ++r) {   // the slot tables' empty state
+    const int64_t i = base + r * kBlock + threadIdx.x;
+    if (i < n_slots) {
       occ_numpnts[i] = 0;
       occ_2_coor[i * 3 + 0] = -1;
       occ_2_coor[i * 3 + 1] = -1;
       occ_2_coor[i * 3 + 2] = -1;
     }
   }
+  __syncthreads();
+  if ((int)blockIdx.x < tiles) hist[(int64_t)threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];
 }
 
 // LSD radix sort, 8 key bits per pass over tiles of kRsTile keys: per-tile
 // digit counts (k_rs_hist), their exclusive scan in digit-major order (the
 // device scan), then a stable scatter (k_rs_scatter) that ranks the tile in
 // LDS and writes each digit's keys of the tile as one contiguous run.
-constexpr int kRsItems = 8;
-constexpr int kRsTile = kBlock * kRsItems;  // 2048 keys: ~4 tiles per CU at 2 M points
-
-template <typename K>
-__device__ __forceinline__ int rs_digit(K k, int shift) {
-  return (int)((k >> shift) & (K)255);
-}
-
 template <typename K>
 __global__ void __launch_bounds__(kBlock) k_rs_hist(const K* __restrict__ keys, int64_t n, int shift, int tiles,
                                                     int32_t* __restrict__ hist) {
@@ -395,9 +412,14 @@ __device__ void sel_derive(const uint32_t* __restrict__ hist, int npass, int max
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_sel_hist(int64_t n, const int32_t* __restrict__ flag, uint64_t seed,
-                                                     int pass, int max_o, const SelState* __restrict__ st,
-                                                     uint32_t* __restrict__ hist) {
+// Pass 0 walks every point's claim flag and lists the claimers by slot
+// (cids[pt_slot[i]] = i: the first scan's ranks); the later passes and
+// k_sel_apply walk that list (the occupied voxels, 2.7 M of c5's 20 M points).
+__global__ void __launch_bounds__(kBlock) k_sel_hist(int64_t n, const int32_t* __restrict__ flag,
+                                                     const int32_t* __restrict__ pt_slot,
+                                                     int32_t* __restrict__ cids, const int32_t* __restrict__ n_vox,
+                                                     uint64_t seed, int pass, int max_o,
+                                                     const SelState* __restrict__ st, uint32_t* __restrict__ hist) {
   if (!st->active) return;
   __shared__ uint32_t h[256];
   __shared__ unsigned long long s[2];
@@ -407,17 +429,27 @@ __global__ void __launch_bounds__(kBlock) k_sel_hist(int64_t n, const int32_t* _
   const unsigned long long prefix = s[0];
   const int shift = 56 - 8 * pass;
   const unsigned long long hi = shift >= 56 ? 0ull : (~0ull << (shift + 8));
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (!flag[i]) continue;
-    const unsigned long long key = res_vkey(seed, (uint32_t)i);
-    if (((key ^ prefix) & hi) == 0) atomicAdd(&h[(key >> shift) & 255u], 1u);
+  if (pass == 0) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+      if (!flag[i]) continue;
+      cids[pt_slot[i]] = (int32_t)i;
+      const unsigned long long key = res_vkey(seed, (uint32_t)i);
+      atomicAdd(&h[(key >> shift) & 255u], 1u);
+    }
+  } else {
+    const int64_t nv = *n_vox;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nv; r += (int64_t)gridDim.x * blockDim.x) {
+      const unsigned long long key = res_vkey(seed, (uint32_t)cids[r]);
+      if (((key ^ prefix) & hi) == 0) atomicAdd(&h[(key >> shift) & 255u], 1u);
+    }
   }
   __syncthreads();
   if (h[threadIdx.x]) atomicAdd(hist + pass * 256 + threadIdx.x, h[threadIdx.x]);
 }
 
 // keep the claimer of a voxel only when its voxel is among the max_o kept
-__global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, int max_o,
+__global__ void __launch_bounds__(kBlock) k_sel_apply(const int32_t* __restrict__ cids,
+                                                      const int32_t* __restrict__ n_vox, uint64_t seed, int max_o,
                                                       const SelState* __restrict__ st,
                                                       const uint32_t* __restrict__ hist, int32_t* __restrict__ flag) {
   if (!st->active) return;
@@ -425,8 +457,11 @@ __global__ void __launch_bounds__(kBlock) k_sel_apply(int64_t n, uint64_t seed, 
   __shared__ uint32_t wtot[kBlock / 64];
   sel_derive(hist, kSelPasses, max_o, s, wtot);
   const unsigned long long thr = s[0];
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    if (flag[i] && res_vkey(seed, (uint32_t)i) > thr) flag[i] = 0;
+  const int64_t nv = *n_vox;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nv; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t i = cids[r];
+    if (res_vkey(seed, (uint32_t)i) > thr) flag[i] = 0;
+  }
 }
 
 // map_coor2occ + fill_occ2pnts (qpiw.py:305-387), one thread per sorted
@@ -445,24 +480,84 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
                                                   const int32_t* __restrict__ cell_start,
                                                   const int32_t* __restrict__ cell_end,
                                                   int32_t* __restrict__ coor_2_occ, int32_t* __restrict__ occ_2_coor,
-                                                  uint8_t* __restrict__ occ_bytes, int32_t* __restrict__ occ_numpnts,
+                                                  uint8_t* __restrict__ occ_bytes, uint8_t* __restrict__ held_bytes,
+                                                  int32_t* __restrict__ occ_numpnts,
                                                   float4* __restrict__ occ_pts, int32_t* __restrict__ slot_run,
                                                   int32_t* counters) {
   const GridDev g = with_geom(g0, geo);
   int dropped = 0, mx = 0;
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    const K key = skey[j];
-    if (key == sentinel) continue;
+  const int lane = threadIdx.x & 63;
+  const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;   // lanes 0 .. lane
+  // A wave takes 64 consecutive sorted points: a run's head lane (the first
+  // point of its voxel) loads the run's claim flag, slot and length, and the
+  // run's other lanes in the wave take them by shuffle; only lanes whose head
+  // lies in an earlier wave look the run up through cell_start (c5: ~5 random
+  // loads per point -> ~3 per run).
+  for (int64_t j0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63ll; j0 < n;
+       j0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = j0 + lane;
+    const K key = j < n ? skey[j] : sentinel;
+    const bool in = key != sentinel;
+    const bool head = in && (j == 0 || skey[j - 1] != key);
     const int64_t cell = (int64_t)key;
-    const int h = cell_start[cell];
-    const int id0 = sid[h];
-    if (!flag[id0]) continue;          // voxel dropped by the max_o reservoir
-    const int slot = pt_slot[id0];
-    if (slot >= g.max_o) continue;     // never: the reservoir kept <= max_o voxels
-    const int cnt = cell_end[cell] - h;
+    int hd = (int)j, ok = 0, slot = 0, cnt = 0;
+    if (head) {
+      const int id0 = sid[j];
+      ok = flag[id0];
+      slot = pt_slot[id0];
+      cnt = cell_end[cell] - (int)j;
+    }
+    const uint64_t heads = __ballot(head) & upto;
+    const int hl = heads ? 63 - __builtin_clzll(heads) : -1;   // this lane's head lane, if in the wave
+    const int ok_s = __shfl(ok, hl < 0 ? 0 : hl), slot_s = __shfl(slot, hl < 0 ? 0 : hl),
+              cnt_s = __shfl(cnt, hl < 0 ? 0 : hl);
+    if (hl >= 0) {
+      hd = (int)j0 + hl;
+      ok = ok_s;
+      slot = slot_s;
+      cnt = cnt_s;
+    } else if (in) {   // the run began in an earlier wave
+      hd = cell_start[cell];
+      const int id0 = sid[hd];
+      ok = flag[id0];
+      slot = pt_slot[id0];
+      cnt = cell_end[cell] - hd;
+    }
+    // ok: the voxel survived the max_o reservoir (slot < max_o always then)
+    const bool live = in && ok && slot < g.max_o;
     const int cnt_kept = (g.slot0_drop && slot == 0) ? 0 : cnt;
-    if (j == h) {
+    const int v = in ? sid[j] : 0;
+    // fill_occ2pnts' reservoir for a run that lies inside this wave: each lane
+    // ranks its point's res_pkey among the run's (keys are distinct), the P
+    // smallest are kept and numbered in run (= id) order by a ballot.  Runs that
+    // cross the wave go to k_reservoir (slot_run = head position).
+    const bool rw = live && cnt_kept > g.P && hd >= j0 && hd + cnt <= j0 + 64;
+    bool keep_rec = live && cnt_kept > 0 && cnt_kept <= g.P;
+    int rec = (int)j - hd;
+    if (__ballot(rw)) {
+      // res_pkey = (hash << 32) | id and the run's ids ascend with the lane, so
+      // key order = (hash, run position): one 32-bit shuffle per step
+      const uint32_t myh = res_pkey_hash(g.seed, (uint32_t)v);
+      int span = rw ? cnt : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+      const int hl0 = rw ? hd - (int)j0 : 0;
+      const int me = lane - hl0;   // this lane's position in its run
+      int rank = 0;
+      for (int t = 0; t < span; ++t) {   // wave-uniform trip count
+        const int src = rw && t < cnt ? hl0 + t : lane;
+        const uint32_t ht = (uint32_t)__shfl((int)myh, src);
+        rank += (rw && t < cnt && (ht < myh || (ht == myh && t < me))) ? 1 : 0;
+      }
+      const bool sel = rw && rank < g.P;
+      const uint64_t selm = __ballot(sel);
+      const uint64_t run_lo = hl0 >= 64 ? 0ull : ~((1ull << hl0) - 1ull);   // lanes hd - j0 .. 63
+      const int rr = __popcll(selm & run_lo & ((1ull << lane) - 1ull));
+      if (sel) rec = rr;
+      keep_rec = keep_rec || sel;
+    }
+    if (!live) continue;
+    if (head) {
       int c[3];
       if (cell <= 0x7fffffff) {   // 32-bit division when the cell index fits
         const int r = (int)cell / g.dims[2];
@@ -479,17 +574,16 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
       occ_2_coor[slot * 3 + 1] = c[1];
       occ_2_coor[slot * 3 + 2] = c[2];
       occ_bytes[cell] = 1;
+      if (cnt_kept > 0) held_bytes[cell] = 1;   // the query index's held voxels (was k_mark_held)
       occ_numpnts[slot] = cnt_kept;
       const int keep = min(cnt_kept, g.P);
-      if (cnt_kept > g.P) slot_run[slot] = h;   // records by k_reservoir (one lane per voxel)
+      if (cnt_kept > g.P) slot_run[slot] = rw ? -1 : hd;   // -1: records written here, else by k_reservoir
       dropped += cnt_kept - keep;
       mx = max(mx, cnt_kept);
     }
-    if (cnt_kept > 0 && cnt_kept <= g.P) {
-      const int v = sid[j];
-      occ_pts[(int64_t)slot * g.P + ((int)j - h)] =
+    if (keep_rec)
+      occ_pts[(int64_t)slot * g.P + rec] =
           make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2], __int_as_float(v));
-    }
   }
   dropped = wave_sum_i32(dropped);
 #pragma unroll
@@ -513,37 +607,135 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
 }
 
 // fill_occ2pnts' reservoir (qpiw.py:377-384) for the voxels whose run exceeds
-// P, one lane per slot (every lane of a wave a candidate voxel, not one in a
-// run's length as inside k_claim): the P points of smallest res_pkey, written in
-// ascending id order.
+// P: the P points of smallest res_pkey (keys are distinct: the id is their low
+// half), written in ascending id order.  One wave per 64 slots; the wave takes
+// its overflowing slots one at a time (ballot) and works through each run with
+// all 64 lanes: P rounds of a wave-wide minimum above the previous round's key
+// find the P-th smallest key, then one ballot-ranked pass writes the points at
+// or below it in run (= id) order.  (One lane per voxel walking its run P
+// times serialised the long runs: c5, 1.76 ms.)
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+    const uint64_t w = ((uint64_t)hi << 32) | lo;
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+constexpr int kResChunks = 8;   // runs of <= 512 points: hashes held in registers (longer: recomputed)
+
 __global__ void __launch_bounds__(kBlock) k_reservoir(int n_slots, GridDev g, const float* __restrict__ xyz,
                                                       const int32_t* __restrict__ sid,
                                                       const int32_t* __restrict__ occ_numpnts,
                                                       const int32_t* __restrict__ slot_run,
                                                       float4* __restrict__ occ_pts) {
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
-    const int cnt = occ_numpnts[s];
-    if (cnt <= g.P) continue;
-    const int32_t* ids = sid + slot_run[s];
-    float4* dst = occ_pts + (int64_t)s * g.P;
-    // threshold = the P-th smallest key of the voxel's points
-    uint64_t thr = 0;
-    bool first = true;
-    for (int q = 0; q < g.P; ++q) {
-      uint64_t best = ~0ull;
-      for (int e = 0; e < cnt; ++e) {
-        const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
-        if ((first || k > thr) && k < best) best = k;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ll; s0 < n_slots;
+       s0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sl = s0 + lane;
+    const int mine = sl < n_slots ? occ_numpnts[sl] : 0;
+    // (slot_run -1: the run fitted one wave of k_claim, which wrote its records)
+    uint64_t todo = __ballot(mine > g.P && slot_run[sl < n_slots ? sl : 0] >= 0);
+    while (todo) {
+      const int b = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int s = (int)s0 + b;
+      const int cnt = __shfl(mine, b);
+      const int32_t* ids = sid + slot_run[s];
+      float4* dst = occ_pts + (int64_t)s * g.P;
+      if (cnt <= 64 * kResChunks) {
+        // key order = (hash, run position) (res_pkey's low half is the id, ascending
+        // along the run).  MSB-first radix select of the P-th smallest hash with
+        // ballots: per bit, the candidates whose bit is 0 are counted; the selection
+        // stops as soon as the remaining candidates are exactly the ones still needed.
+        uint32_t hs[kResChunks];
+        uint64_t cand[kResChunks], sel[kResChunks];
+#pragma unroll
+        for (int c = 0; c < kResChunks; ++c) {
+          const int e = 64 * c + lane;
+          hs[c] = e < cnt ? res_pkey_hash(g.seed, (uint32_t)ids[e]) : 0u;
+          cand[c] = __ballot(e < cnt);
+          sel[c] = 0ull;
+        }
+        int rem = g.P;
+        for (int bit = 31; bit >= 0 && rem > 0; --bit) {
+          uint64_t zero[kResChunks];
+          int n0 = 0, nc = 0;
+#pragma unroll
+          for (int c = 0; c < kResChunks; ++c) {
+            zero[c] = 0ull;
+            if (64 * c < cnt) {   // wave-uniform: only the run's chunks
+              zero[c] = cand[c] & __ballot(((hs[c] >> bit) & 1u) == 0u);
+              n0 += __popcll(zero[c]);
+            }
+          }
+          if (rem <= n0) {
+#pragma unroll
+            for (int c = 0; c < kResChunks; ++c) cand[c] = zero[c];
+          } else {
+            rem -= n0;
+#pragma unroll
+            for (int c = 0; c < kResChunks; ++c) {
+              sel[c] |= zero[c];
+              cand[c] &= ~zero[c];
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < kResChunks; ++c) nc += __popcll(cand[c]);
+          if (nc == rem) {   // every remaining candidate is in
+#pragma unroll
+            for (int c = 0; c < kResChunks; ++c) sel[c] |= cand[c];
+            rem = 0;
+          }
+        }
+        // equal hashes past bit 0: the first `rem` of them in run (= id) order
+#pragma unroll
+        for (int c = 0; c < kResChunks; ++c) {
+          while (rem > 0 && cand[c]) {
+            const uint64_t lo = cand[c] & (~cand[c] + 1ull);
+            sel[c] |= lo;
+            cand[c] &= ~lo;
+            --rem;
+          }
+        }
+        int base = 0;
+#pragma unroll
+        for (int c = 0; c < kResChunks; ++c) {
+          if ((sel[c] >> lane) & 1ull) {
+            const int v = ids[64 * c + lane];
+            dst[base + __popcll(sel[c] & below)] =
+                make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2], __int_as_float(v));
+          }
+          base += __popcll(sel[c]);
+        }
+        continue;
       }
-      thr = best;
-      first = false;
-    }
-    int q = 0;
-    for (int e = 0; e < cnt && q < g.P; ++e) {   // the run is in ascending id order
-      const int v = ids[e];
-      if (res_pkey(g.seed, (uint32_t)v) > thr) continue;
-      dst[q++] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
-                             __int_as_float(v));
+      // long runs: P rounds of a wave-wide minimum above the previous round's key
+      uint64_t thr = 0;
+      for (int q = 0; q < g.P; ++q) {
+        uint64_t best = ~0ull;
+        for (int e = lane; e < cnt; e += 64) {
+          const uint64_t k = res_pkey(g.seed, (uint32_t)ids[e]);
+          if ((q == 0 || k > thr) && k < best) best = k;
+        }
+        thr = wave_min_u64(best);
+      }
+      int written = 0;
+      for (int e0 = 0; e0 < cnt && written < g.P; e0 += 64) {
+        const int e = e0 + lane;
+        const int v = e < cnt ? ids[e] : 0;
+        const bool take = e < cnt && res_pkey(g.seed, (uint32_t)v) <= thr;
+        const uint64_t m = __ballot(take);
+        const int pos = written + __popcll(m & below);
+        if (take && pos < g.P)
+          dst[pos] = make_float4(xyz[(int64_t)v * 3], xyz[(int64_t)v * 3 + 1], xyz[(int64_t)v * 3 + 2],
+                                 __int_as_float(v));
+        written += __popcll(m);
+      }
     }
   }
 }
@@ -645,20 +837,10 @@ __global__ void __launch_bounds__(kBlock) k_pack_bits(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------- query index
-// Voxels that hold >= 1 kept point (coor_2_occ >= 0 and occ_numpnts > 0: the
-// slot-0 voxel under slot0_drop and the truncated ones are skipped exactly as
-// the reference's loop `g < min(P, occ_numpnts)` skips them), one byte per cell.
-__global__ void __launch_bounds__(kBlock) k_mark_held(int n_slots, GridDev g0, const QGrid* __restrict__ geo,
-                                                      const int32_t* __restrict__ occ_numpnts,
-                                                      const int32_t* __restrict__ occ_2_coor,
-                                                      uint8_t* __restrict__ bytes) {
-  const GridDev g = with_geom(g0, geo);
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
-    if (occ_numpnts[s] <= 0 || occ_2_coor[s * 3] < 0) continue;
-    bytes[((int64_t)occ_2_coor[s * 3] * g.dims[1] + occ_2_coor[s * 3 + 1]) * g.dims[2] + occ_2_coor[s * 3 + 2]] = 1;
-  }
-}
-
+// Held voxels (>= 1 kept point: the slot-0 voxel under slot0_drop and the
+// truncated ones are skipped exactly as the reference's loop `g < min(P,
+// occ_numpnts)` skips them) arrive as one byte per cell from k_claim; packed
+// to the query bitmap words with their popcounts.
 __global__ void __launch_bounds__(kBlock) k_pack_held(const uint8_t* __restrict__ bytes, int64_t words,
                                                       uint2* __restrict__ qw, int32_t* __restrict__ wcnt) {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words;
@@ -753,16 +935,20 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   // (cell, point id) sorted by cell, ids ascending inside a cell
   K* keys[2] = {h->sort_k[0].as<K>(), h->sort_k[1].as<K>()};
   int32_t* vals[2] = {h->sort_v[0].as<int32_t>(), h->sort_v[1].as<int32_t>()};
-  hipLaunchKernelGGL(k_cell_keys<K>, dim3(grid_for(n > cap_o ? n : cap_o, kBlock)), dim3(kBlock), 0, st, xyz_dev,
-                     n, g, geo, sentinel, keys[0], cap_o, pt_flag, h->occ_numpnts.as<int32_t>(),
-                     h->occ_2_coor.as<int32_t>(), counters);
+  const int64_t kblocks = cdiv(n > cap_o ? n : cap_o, kRsTile);
+  PNR_CHECK_ARG(kblocks < (int64_t)1 << 31, "grid_build: too many sort tiles");
+  hipLaunchKernelGGL(k_cell_keys<K>, dim3((unsigned)kblocks), dim3(kBlock), 0, st, xyz_dev, n, g, geo, sentinel,
+                     keys[0], cap_o, pt_flag, h->occ_numpnts.as<int32_t>(), h->occ_2_coor.as<int32_t>(), counters,
+                     tiles, h->sort_hist.as<int32_t>());
   PNR_LAUNCH_CHECK();
   int cur = 0;
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = 8 * pass;
-    hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], n, shift, tiles,
-                       h->sort_hist.as<int32_t>());
-    PNR_LAUNCH_CHECK();
+    if (pass > 0) {   // (pass 0's histogram: k_cell_keys)
+      hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], n, shift, tiles,
+                         h->sort_hist.as<int32_t>());
+      PNR_LAUNCH_CHECK();
+    }
     if ((rc = exclusive_scan(h->sort_hist.as<int32_t>(), (int64_t)256 * tiles, nullptr, h->sort_offs.as<int32_t>(),
                              (int64_t)(h->sort_offs.bytes / 4), nullptr, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
@@ -787,22 +973,29 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
     const unsigned gs = grid_for(n, kBlock, 1024);
     hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, counters, (int)cap_o, ss, hist);
     PNR_LAUNCH_CHECK();
+    // the claimers listed by slot (pass 0) in sort_v[cur ^ 1]: free after the sort
+    int32_t* cids = vals[cur ^ 1];
+    // passes 1.. and the apply walk the claimer list (<= the occupied voxels): fewer blocks
+    const unsigned gl = grid_for(cap_o, kBlock, 256);
     for (int pass = 0; pass < kSelPasses; ++pass) {
-      hipLaunchKernelGGL(k_sel_hist, dim3(gs), dim3(kBlock), 0, st, n, pt_flag, g.seed, pass, (int)cap_o, ss, hist);
+      hipLaunchKernelGGL(k_sel_hist, dim3(pass ? gl : gs), dim3(kBlock), 0, st, n, pt_flag, pt_slot, cids,
+                         counters + 0, g.seed, pass, (int)cap_o, ss, hist);
       PNR_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_sel_apply, dim3(gs), dim3(kBlock), 0, st, n, g.seed, (int)cap_o, ss, hist, pt_flag);
+    hipLaunchKernelGGL(k_sel_apply, dim3(gl), dim3(kBlock), 0, st, cids, counters + 0, g.seed, (int)cap_o, ss, hist,
+                       pt_flag);
     PNR_LAUNCH_CHECK();
     if ((rc = exclusive_scan(pt_flag, n, nullptr, pt_slot, (int64_t)(h->pt_slot.bytes / 4), counters + 6, h->scan_tmp.p, h->scan_tmp.bytes, st, 0,
                              &ss->active)))
       return rc;
   }
+  // cell_bytes = [occupancy bytes | held bytes | word ranks], both byte arrays cleared at once
   uint8_t* occ_bytes = h->cell_bytes.as<uint8_t>();
-  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
+  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 64, st));
   hipLaunchKernelGGL(k_claim<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, skey, sid, sentinel, pt_flag,
                      pt_slot, cell_start, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(),
-                     occ_bytes, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), h->q_rank_slot.as<int32_t>(),
-                     counters);
+                     occ_bytes, occ_bytes + words * 32, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(),
+                     h->q_rank_slot.as<int32_t>(), counters);
   PNR_LAUNCH_CHECK();
   // q_rank_slot is scratch until the query index below: slot -> run start
   hipLaunchKernelGGL(k_reservoir, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, xyz_dev, sid,
@@ -842,7 +1035,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   int64_t scan_n = n;
   for (int64_t m : {cap_o, words, hist_n}) scan_n = m > scan_n ? m : scan_n;
   if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->cell_end.ensure(gvol * 4)) ||
-      (rc = h->cell_bytes.ensure(words * 36 + 16)) || (rc = h->occ_bits.ensure(words * 4)) ||
+      (rc = h->cell_bytes.ensure(words * 68 + 16)) || (rc = h->occ_bits.ensure(words * 4)) ||
       (rc = h->occ_numpnts.ensure(cap_o * 4)) || (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
       (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->sort_k[0].ensure(n * kbytes)) ||
       (rc = h->sort_k[1].ensure(n * kbytes)) || (rc = h->sort_v[0].ensure(n * 4)) ||
@@ -883,14 +1076,11 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   {
     uint2* qw = h->q_words.as<uint2>();
     int32_t* wcnt = h->q_wcnt.as<int32_t>();
-    int32_t* wrank = reinterpret_cast<int32_t*>(occ_bytes + words * 32);   // after the cell bytes
-    PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 32, st));
-    hipLaunchKernelGGL(k_mark_held, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, geo,
-                       occ_numpnts, occ_2_coor, occ_bytes);
+    const uint8_t* held_bytes = occ_bytes + words * 32;                    // written by k_claim
+    int32_t* wrank = reinterpret_cast<int32_t*>(occ_bytes + words * 64);   // after the two byte arrays
+    hipLaunchKernelGGL(k_pack_held, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, held_bytes, words, qw, wcnt);
     PNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pack_held, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, occ_bytes, words, qw, wcnt);
-    PNR_LAUNCH_CHECK();
-    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, (int64_t)((h->cell_bytes.bytes - words * 32) / 4), counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, (int64_t)((h->cell_bytes.bytes - words * 64) / 4), counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
     hipLaunchKernelGGL(k_word_rank, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, words, wrank, qw);
     PNR_LAUNCH_CHECK();

@@ -124,6 +124,9 @@ __host__ __device__ inline uint64_t res_vkey(uint64_t seed, uint32_t id) {
 __host__ __device__ inline uint64_t res_pkey(uint64_t seed, uint32_t id) {
   return ((uint64_t)res_hash32(seed + kPtSalt, id) << 32) | id;
 }
+__host__ __device__ inline uint32_t res_pkey_hash(uint64_t seed, uint32_t id) {   // res_pkey's high half
+  return res_hash32(seed + kPtSalt, id);
+}
 
 // Sum over the 64 lanes of a wave.
 __device__ __forceinline__ int wave_sum_i32(int v) {
@@ -176,7 +179,7 @@ struct pnr_handle {
   DevBuf coor_2_occ;      // int32 [gvol]   cell -> slot, -1 = empty
   DevBuf occ_bits;        // uint32 [gvol/32] dilated occupancy bitmap
   DevBuf cell_end;        // int32 [gvol]   one past the last sorted position of the cell's run (occupied cells only)
-  DevBuf cell_bytes;      // uint8 [32*words] + int32 [words+1]: occupancy bytes before packing, word ranks
+  DevBuf cell_bytes;      // uint8 [32*words] x 2 + int32 [words+1]: occupancy bytes before packing, held bytes, word ranks
   DevBuf occ_numpnts;     // int32 [max_o]  points that fell in the voxel
   DevBuf occ_pts;         // float4 [max_o*P] {x, y, z, bitcast(point id)}
   DevBuf occ_2_coor;      // int32 [max_o*3]

@@ -16,6 +16,25 @@ for s in $STEPS; do
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
       cut -c1-600 $O/bench.json ;;
+    gridprof)   # grid build kernel split, headline and c5 (GCONFIGS)
+      for c in ${GCONFIGS:-headline c5}; do
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/grid_$c -o run -- \
+          python tools/grid_bench.py --config $c --no-oracle --reps 10 > $O/grid_$c.json 2> $O/grid_$c.err \
+          || { tail -20 $O/grid_$c.err; exit 1; }
+        cat $O/grid_$c.json
+      done ;;
+    query)   # query stage per config (QCONFIGS), plain timing then a kernel-stats pass
+      for c in ${QCONFIGS:-headline c5}; do
+        timeout -k 10 300 python tools/query_bench.py --config $c --reps 10 > $O/query_$c.json 2> $O/query_$c.err \
+          || { tail -20 $O/query_$c.err; exit 1; }
+        python -c "import json; d=json.load(open('$O/query_$c.json')); print('$c', [(x['query_ms'], x['frac_hbm'], x['pidx_checksum']) for x in d['cams']])"
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/qstats_$c -o run -- \
+          python tools/query_bench.py --config $c --reps 3 > /dev/null 2> $O/qstats_$c.err || { tail -20 $O/qstats_$c.err; exit 1; }
+      done ;;
+    knnstats)   # layer statistics of the generic KNN walk (tools/_var/libpnr_qstats.so)
+      PNR_LIB=$PWD/tools/_var/libpnr_qstats.so timeout -k 10 300 python tools/knn_stats.py --config ${KCONFIG:-c5} \
+        > $O/knnstats.json 2> $O/knnstats.err || { tail -20 $O/knnstats.err; exit 1; }
+      cat $O/knnstats.json ;;
     launch)   # bench.py --gpus 2 self-launch rehearsal: two ranks on the box's one GPU over gloo
       PNR_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 > $O/launch2.json \
         2> $O/launch2.err || { tail -20 $O/launch2.err; exit 1; }
