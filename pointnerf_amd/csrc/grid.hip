@@ -858,6 +858,44 @@ __global__ void __launch_bounds__(kBlock) k_pack_held(const uint8_t* __restrict_
   }
 }
 
+// Coarse held-occupancy map for the KNN's column filter: one wave per (z-block
+// bz of 8 cells, x, 64 consecutive y): lane y tests the held bits of its column's
+// cells [8 bz, 8 bz + 8) (one or two bitmap words), a ballot makes two y-words.
+__global__ void __launch_bounds__(kBlock) k_coarse_held(GridDev g0, const QGrid* __restrict__ geo,
+                                                        const uint2* __restrict__ qw, uint32_t* __restrict__ coarse) {
+  const GridDev g = with_geom(g0, geo);
+  const int dx = g.dims[0], dy = g.dims[1], dz = g.dims[2];
+  const int nbz = (dz + 7) >> 3, nyw = (dy + 31) >> 5, nyc = (dy + 63) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t nrows = (int64_t)nbz * dx * nyc;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < nrows;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int yc = (int)(r % nyc);
+    const int64_t t = r / nyc;
+    const int x = (int)(t % dx), bz = (int)(t / dx);
+    const int y = yc * 64 + lane;
+    bool any = false;
+    if (y < dy) {
+      const int z0 = bz * 8, z1 = min(z0 + 8, dz) - 1;   // cells z0 .. z1
+      const int64_t c0 = ((int64_t)x * dy + y) * dz + z0, c1 = c0 + (z1 - z0);
+      const uint32_t wa = qw[c0 >> 5].x;
+      const int a = (int)(c0 & 31), b = (int)(c1 & 31);
+      if ((c1 >> 5) == (c0 >> 5)) {
+        any = ((wa >> a) & ((2u << (b - a)) - 1u)) != 0u;
+      } else {
+        const uint32_t wb = qw[c1 >> 5].x;
+        any = (wa >> a) != 0u || (wb & ((2u << b) - 1u)) != 0u;
+      }
+    }
+    const uint64_t m = __ballot(any);
+    if (lane == 0) {
+      uint32_t* row = coarse + ((int64_t)bz * dx + x) * nyw;
+      row[2 * yc] = (uint32_t)m;
+      if (2 * yc + 1 < nyw) row[2 * yc + 1] = (uint32_t)(m >> 32);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_word_rank(int64_t words, const int32_t* __restrict__ wrank,
                                                       uint2* __restrict__ qw) {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words;
@@ -1045,6 +1083,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
       (rc = h->counters.ensure(8 * 4)) || (rc = h->sel.ensure(sizeof(SelState) + kSelPasses * 256 * 4)) ||
       (rc = h->scan_tmp.ensure(scan_scratch_bytes(scan_n))) ||
       (rc = h->q_words.ensure(words * 8)) || (rc = h->q_wcnt.ensure((words + 1) * 4)) ||
+      (rc = h->q_coarse.ensure((size_t)cdiv(p->dims[2], 8) * p->dims[0] * cdiv(p->dims[1], 32) * 4)) ||
       (rc = h->q_rank_slot.ensure(cap_o * 4)) || (rc = h->q_rank_cnt.ensure(cap_o * 4)) ||
       (rc = h->q_rec_off.ensure((cap_o + 1) * 4)) || (rc = h->q_recs.ensure(n * sizeof(float4))))
     return rc;
@@ -1084,6 +1123,12 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
       return rc;
     hipLaunchKernelGGL(k_word_rank, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, words, wrank, qw);
     PNR_LAUNCH_CHECK();
+    {
+      const int64_t nrows = cdiv(p->dims[2], 8) * p->dims[0] * cdiv(p->dims[1], 64);
+      hipLaunchKernelGGL(k_coarse_held, dim3(grid_for(nrows * 64, kBlock)), dim3(kBlock), 0, st, g, geo, qw,
+                         h->q_coarse.as<uint32_t>());
+      PNR_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(k_rank_slots, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, geo,
                        occ_numpnts, occ_2_coor, qw, h->q_rank_slot.as<int32_t>(), h->q_rank_cnt.as<int32_t>());
     PNR_LAUNCH_CHECK();

@@ -199,6 +199,8 @@ struct pnr_handle {
   // stays in L2 and its records sit near each other in HBM.
   DevBuf q_words;         // uint2 [gvol/32] {bits: cell holds >= 1 kept point, rank of the word's first cell}
   DevBuf q_wcnt;          // int32 [gvol/32] scratch: popcount per word
+  DevBuf q_coarse;        // uint32 [ceil(dz/8)][dx][ceil(dy/32)]: bit y of word (bz, x, y/32) = column (x, y)
+                          //   holds a kept point in z-block [8 bz, 8 bz + 8) (the KNN's column filter)
   DevBuf q_rank_slot;     // int32 [max_o]   slot of rank r (scratch)
   DevBuf q_rank_cnt;      // int32 [max_o]   min(P, points) of rank r (scratch)
   DevBuf q_rec_off;       // int32 [max_o+1] first record of rank r (exclusive scan of q_rank_cnt)
@@ -228,7 +230,7 @@ struct pnr_handle {
     stats_pending = false;
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &cell_end, &cell_bytes, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &sort_k[0], &sort_k[1], &sort_v[0], &sort_v[1], &sort_hist, &sort_offs,
-                     &cell_start, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
+                     &cell_start, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_coarse, &q_rank_slot, &q_rank_cnt,
                      &q_rec_off, &q_recs, &geom, &bbox};
     for (DevBuf* b : all) b->release();
   }

@@ -35,6 +35,9 @@ for s in $STEPS; do
       PNR_LIB=$PWD/tools/_var/libpnr_qstats.so timeout -k 10 300 python tools/knn_stats.py --config ${KCONFIG:-c5} \
         > $O/knnstats.json 2> $O/knnstats.err || { tail -20 $O/knnstats.err; exit 1; }
       cat $O/knnstats.json ;;
+    qpmc)   # query kernel stats + PMC passes (tools/prof_query.sh), QCONFIG
+      bash tools/prof_query.sh $(basename $O)/qpmc || exit 1
+      python tools/pmc_fold.py $O/qpmc k_knn k_march > $O/qpmc_fold.json; cat $O/qpmc_fold.json | head -60 ;;
     launch)   # bench.py --gpus 2 self-launch rehearsal: two ranks on the box's one GPU over gloo
       PNR_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 > $O/launch2.json \
         2> $O/launch2.err || { tail -20 $O/launch2.err; exit 1; }
