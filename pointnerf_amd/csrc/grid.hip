@@ -133,8 +133,7 @@ __device__ __forceinline__ GridDev with_geom(const GridDev& g0, const QGrid* __r
 // float64 (vsize is a Python float list), dims = ceil(vdim / vscale) -- so shift
 // and dims are the host formula's bits.  dims are clamped to [1, the bound
 // the host allocated for].
-__global__ void k_grid_geom(const float* __restrict__ bbox, pnr_grid_spec sp, QGrid* __restrict__ geo) {
-  if (threadIdx.x != 0) return;
+__device__ __forceinline__ void grid_geom_from(const float* bbox, const pnr_grid_spec& sp, QGrid* geo) {
   QGrid G;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -152,6 +151,32 @@ __global__ void k_grid_geom(const float* __restrict__ bbox, pnr_grid_spec sp, QG
   }
   G.P = sp.P;
   *geo = G;
+}
+
+// The device build's bbox + geometry in TWO launches (was four: k_bbox_init,
+// k_bbox, k_bbox_fin, k_grid_geom): k_bbox reduces into the order-key
+// accumulators, k_geom_acc converts them to the float bbox (out6), derives the
+// geometry and puts the accumulators back in their initial state for the next
+// build (the state k_bbox_acc_init gives them at allocation).  (One launch with
+// a last-block ticket needed a device-scope release fence per block: 111 us.)
+__global__ void k_bbox_acc_init(unsigned* acc) {
+  if (threadIdx.x < 3) acc[threadIdx.x] = 0xffffffffu;
+  else if (threadIdx.x < 8) acc[threadIdx.x] = 0u;
+}
+
+__device__ __forceinline__ void grid_geom_from(const float* bb, const pnr_grid_spec& sp, QGrid* geo);
+
+__global__ void k_geom_acc(unsigned* acc, float* __restrict__ out6, pnr_grid_spec sp, QGrid* __restrict__ geo) {
+  if (threadIdx.x != 0) return;
+  float bb[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    bb[c] = ord2f(acc[c]);
+    out6[c] = bb[c];
+  }
+  grid_geom_from(bb, sp, geo);
+  acc[0] = acc[1] = acc[2] = 0xffffffffu;
+  acc[3] = acc[4] = acc[5] = 0u;
 }
 
 __global__ void k_set_geom(QGrid G, QGrid* __restrict__ geo) {
@@ -174,9 +199,16 @@ __device__ __forceinline__ int64_t cell_of(const float* p, const GridDev& g, int
 // (the smallest point id: the serial claim_occ's winner), its length the
 // voxel's point count, and its first P ids the serial fill_occ2pnts order.
 // Points outside the grid carry the key `sentinel` (> every cell) and sort last.
-template <typename K>
+// RB: radix bits per pass (the build uses 8), D = 2^RB digits
+constexpr int kSelPasses = 8;
+struct SelState {
+  int32_t active;  // 1: more occupied voxels than max_o
+  int32_t pad;
+};
+
+template <int RB, typename K>
 __device__ __forceinline__ int rs_digit(K k, int shift) {
-  return (int)((k >> shift) & (K)255);
+  return (int)((k >> shift) & (K)((1 << RB) - 1));
 }
 
 constexpr int kRsItems = 8;
@@ -185,18 +217,22 @@ constexpr int kRsTile = kBlock * kRsItems;  // 2048 keys: ~4 tiles per CU at 2 M
 // Block b: the keys of sort tile b (kRsTile points) and the radix sort's first
 // digit histogram of that tile (k_rs_hist's pass 0, without a launch and a
 // re-read of the keys), and the empty state of slots [b kRsTile, (b+1) kRsTile).
-template <typename K>
+template <int RB, typename K>
 __global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ xyz, int64_t n, GridDev g0,
                                                       const QGrid* __restrict__ geo, K sentinel,
                                                       K* __restrict__ keys, int64_t n_slots,
                                                       int32_t* __restrict__ pt_flag,
                                                       int32_t* __restrict__ occ_numpnts,
                                                       int32_t* __restrict__ occ_2_coor, int32_t* __restrict__ counters,
-                                                      int tiles, int32_t* __restrict__ hist) {
-  __shared__ int32_t h[256];
+                                                      int tiles, int32_t* __restrict__ hist,
+                                                      uint32_t* __restrict__ sel_hist) {
+  constexpr int D = 1 << RB;
+  __shared__ int32_t h[D];
   const GridDev g = with_geom(g0, geo);
   if (blockIdx.x == 0 && threadIdx.x < 8) counters[threadIdx.x] = 0;
-  h[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && sel_hist)   // the voxel reservoir's histograms (was k_sel_init)
+    for (int i = threadIdx.x; i < kSelPasses * 256; i += kBlock) sel_hist[i] = 0u;
+  for (int d = threadIdx.x; d < D; d += kBlock) h[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kRsTile;
   if ((int)blockIdx.x < tiles) {
@@ -210,7 +246,7 @@ __global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ 
         const K k = cell >= 0 ? (K)cell : sentinel;
         keys[i] = k;
         pt_flag[i] = 0;
-        atomicAdd(&h[rs_digit(k, 0)], 1);
+        atomicAdd(&h[rs_digit<RB>(k, 0)], 1);
       }
     }
   }
@@ -224,48 +260,55 @@ __global__ void __launch_bounds__(kBlock) k_cell_keys(const float* __restrict__ 
     }
   }
   __syncthreads();
-  if ((int)blockIdx.x < tiles) hist[(int64_t)threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];
+  if ((int)blockIdx.x < tiles)
+    for (int d = threadIdx.x; d < D; d += kBlock) hist[(int64_t)d * tiles + blockIdx.x] = h[d];
 }
 
 // LSD radix sort, 8 key bits per pass over tiles of kRsTile keys: per-tile
 // digit counts (k_rs_hist), their exclusive scan in digit-major order (the
 // device scan), then a stable scatter (k_rs_scatter) that ranks the tile in
 // LDS and writes each digit's keys of the tile as one contiguous run.
-template <typename K>
+template <int RB, typename K>
 __global__ void __launch_bounds__(kBlock) k_rs_hist(const K* __restrict__ keys, int64_t n, int shift, int tiles,
                                                     int32_t* __restrict__ hist) {
-  __shared__ int32_t h[256];
-  h[threadIdx.x] = 0;
+  constexpr int D = 1 << RB;
+  __shared__ int32_t h[D];
+  for (int d = threadIdx.x; d < D; d += kBlock) h[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kRsTile;
 #pragma unroll 4
   for (int r = 0; r < kRsItems; ++r) {
     const int64_t i = base + r * kBlock + threadIdx.x;
-    if (i < n) atomicAdd(&h[rs_digit(keys[i], shift)], 1);
+    if (i < n) atomicAdd(&h[rs_digit<RB>(keys[i], shift)], 1);
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];
+  for (int d = threadIdx.x; d < D; d += kBlock) hist[(int64_t)d * tiles + blockIdx.x] = h[d];
 }
 
 // vin == nullptr: the values are the keys' positions (the point ids, pass 0)
-template <typename K>
+template <int RB, typename K>
 __global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin, const int32_t* __restrict__ vin,
                                                        int64_t n, int shift, int tiles,
                                                        const int32_t* __restrict__ offs, K* __restrict__ kout,
                                                        int32_t* __restrict__ vout) {
+  constexpr int D = 1 << RB;
+  constexpr int DPT = D / kBlock;             // digits per thread (1 or 2)
   __shared__ K sk[kRsTile];
   __shared__ int32_t sv[kRsTile];
-  __shared__ int32_t wcnt[kBlock / 64][256];  // this round's digit counts per wave
-  __shared__ int32_t run[256];                // digit counts of the earlier rounds, then digit starts
-  __shared__ int32_t gb[256];                 // output position of the tile's digit-d keys minus their LDS start
+  __shared__ int32_t wcnt[kBlock / 64][D];    // this round's digit counts per wave
+  __shared__ int32_t run[D];                  // digit counts of the earlier rounds, then digit starts
+  __shared__ int32_t gb[D];                   // output position of the tile's digit-d keys minus their LDS start
   __shared__ int32_t wsum[kBlock / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * kRsTile;
   const int in_tile = (int)(n - base < kRsTile ? n - base : kRsTile);
   const uint64_t below = (1ull << lane) - 1ull;
-  run[tid] = 0;
 #pragma unroll
-  for (int q = 0; q < kBlock / 64; ++q) wcnt[q][tid] = 0;
+  for (int i = 0; i < DPT; ++i) {
+    run[tid * DPT + i] = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; ++q) wcnt[q][tid * DPT + i] = 0;
+  }
   K key[kRsItems];
   int32_t val[kRsItems], loc[kRsItems];
 #pragma unroll
@@ -281,10 +324,10 @@ __global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin
 #pragma unroll
   for (int r = 0; r < kRsItems; ++r) {
     const bool ok = r * kBlock + tid < in_tile;
-    const int d = rs_digit(key[r], shift);
+    const int d = rs_digit<RB>(key[r], shift);
     uint64_t peers = __ballot(ok);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < RB; ++b) {
       const uint64_t m = __ballot((d >> b) & 1);
       peers &= ((d >> b) & 1) ? m : ~m;
     }
@@ -295,18 +338,28 @@ __global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin
     for (int q = 0; q < w; ++q) pre += wcnt[q][d];
     loc[r] = pre + rk;
     __syncthreads();
-    int add = 0;
 #pragma unroll
-    for (int q = 0; q < kBlock / 64; ++q) {
-      add += wcnt[q][tid];
-      wcnt[q][tid] = 0;
+    for (int i = 0; i < DPT; ++i) {
+      const int dd = tid * DPT + i;
+      int add = 0;
+#pragma unroll
+      for (int q = 0; q < kBlock / 64; ++q) {
+        add += wcnt[q][dd];
+        wcnt[q][dd] = 0;
+      }
+      run[dd] += add;
     }
-    run[tid] += add;
     __syncthreads();
   }
-  // digit starts inside the tile (exclusive scan of the 256 counts)
-  const int my = run[tid];
-  int inc = my;
+  // digit starts inside the tile (exclusive scan of the D counts; thread t owns
+  // digits t DPT .. t DPT + DPT - 1)
+  int my[DPT], mine = 0;
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    my[i] = run[tid * DPT + i];
+    mine += my[i];
+  }
+  int inc = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int t = __shfl_up(inc, o);
@@ -315,14 +368,19 @@ __global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
   for (int q = 0; q < w; ++q) inc += wsum[q];
-  const int start = inc - my;
-  gb[tid] = offs[(int64_t)tid * tiles + blockIdx.x] - start;
-  run[tid] = start;
+  int start = inc - mine;
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int dd = tid * DPT + i;
+    gb[dd] = offs[(int64_t)dd * tiles + blockIdx.x] - start;
+    run[dd] = start;
+    start += my[i];
+  }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRsItems; ++r) {
     if (r * kBlock + tid < in_tile) {
-      const int p = run[rs_digit(key[r], shift)] + loc[r];
+      const int p = run[rs_digit<RB>(key[r], shift)] + loc[r];
       sk[p] = key[r];
       sv[p] = val[r];
     }
@@ -333,7 +391,7 @@ __global__ void __launch_bounds__(kBlock) k_rs_scatter(const K* __restrict__ kin
     const int e = r * kBlock + tid;
     if (e < in_tile) {
       const K k = sk[e];
-      const int64_t pos = (int64_t)gb[rs_digit(k, shift)] + e;
+      const int64_t pos = (int64_t)gb[rs_digit<RB>(k, shift)] + e;
       kout[pos] = k;
       vout[pos] = sv[e];
     }
@@ -369,16 +427,7 @@ __global__ void __launch_bounds__(kBlock) k_runs(const K* __restrict__ skey, con
 // most significant first.  Pass q counts into its own 256-bin histogram; every
 // later kernel re-derives the digits fixed so far from those histograms, so
 // no launch is spent on the pick.  Nothing runs when the voxels fit max_o.
-constexpr int kSelPasses = 8;
-struct SelState {
-  int32_t active;  // 1: more occupied voxels than max_o
-  int32_t pad;
-};
 
-__global__ void k_sel_init(const int32_t* __restrict__ n_vox, int max_o, SelState* st, uint32_t* hist) {
-  for (int i = threadIdx.x; i < kSelPasses * 256; i += blockDim.x) hist[i] = 0;
-  if (threadIdx.x == 0) st->active = *n_vox > max_o ? 1 : 0;
-}
 
 // Block of 256: s[0] = the key bits fixed by passes 0..npass-1, s[1] = the
 // rank still to find below them (the digit of pass q: the first whose running
@@ -419,8 +468,12 @@ __global__ void __launch_bounds__(kBlock) k_sel_hist(int64_t n, const int32_t* _
                                                      const int32_t* __restrict__ pt_slot,
                                                      int32_t* __restrict__ cids, const int32_t* __restrict__ n_vox,
                                                      uint64_t seed, int pass, int max_o,
-                                                     const SelState* __restrict__ st, uint32_t* __restrict__ hist) {
-  if (!st->active) return;
+                                                     SelState* __restrict__ st, uint32_t* __restrict__ hist) {
+  // pass 0 decides from the voxel count (the first scan's total) and publishes the
+  // flag for the later passes, k_sel_apply and the rescan
+  const bool active = pass == 0 ? *n_vox > max_o : st->active != 0;
+  if (pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) st->active = active ? 1 : 0;
+  if (!active) return;
   __shared__ uint32_t h[256];
   __shared__ unsigned long long s[2];
   __shared__ uint32_t wtot[kBlock / 64];
@@ -481,7 +534,7 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
                                                   const int32_t* __restrict__ cell_end,
                                                   int32_t* __restrict__ coor_2_occ, int32_t* __restrict__ occ_2_coor,
                                                   uint8_t* __restrict__ occ_bytes, uint8_t* __restrict__ held_bytes,
-                                                  int32_t* __restrict__ occ_numpnts,
+                                                  uint32_t* __restrict__ coarse, int32_t* __restrict__ occ_numpnts,
                                                   float4* __restrict__ occ_pts, int32_t* __restrict__ slot_run,
                                                   int32_t* counters) {
   const GridDev g = with_geom(g0, geo);
@@ -574,7 +627,12 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
       occ_2_coor[slot * 3 + 1] = c[1];
       occ_2_coor[slot * 3 + 2] = c[2];
       occ_bytes[cell] = 1;
-      if (cnt_kept > 0) held_bytes[cell] = 1;   // the query index's held voxels (was k_mark_held)
+      if (cnt_kept > 0) {
+        held_bytes[cell] = 1;   // the query index's held voxels (was k_mark_held)
+        // the KNN's coarse column map: bit y of word (z / 8, x, y / 32)
+        atomicOr(coarse + ((int64_t)(c[2] >> 3) * g.dims[0] + c[0]) * ((g.dims[1] + 31) >> 5) + (c[1] >> 5),
+                 1u << (c[1] & 31));
+      }
       occ_numpnts[slot] = cnt_kept;
       const int keep = min(cnt_kept, g.P);
       if (cnt_kept > g.P) slot_run[slot] = rw ? -1 : hd;   // -1: records written here, else by k_reservoir
@@ -858,44 +916,6 @@ __global__ void __launch_bounds__(kBlock) k_pack_held(const uint8_t* __restrict_
   }
 }
 
-// Coarse held-occupancy map for the KNN's column filter: one wave per (z-block
-// bz of 8 cells, x, 64 consecutive y): lane y tests the held bits of its column's
-// cells [8 bz, 8 bz + 8) (one or two bitmap words), a ballot makes two y-words.
-__global__ void __launch_bounds__(kBlock) k_coarse_held(GridDev g0, const QGrid* __restrict__ geo,
-                                                        const uint2* __restrict__ qw, uint32_t* __restrict__ coarse) {
-  const GridDev g = with_geom(g0, geo);
-  const int dx = g.dims[0], dy = g.dims[1], dz = g.dims[2];
-  const int nbz = (dz + 7) >> 3, nyw = (dy + 31) >> 5, nyc = (dy + 63) >> 6;
-  const int lane = threadIdx.x & 63;
-  const int64_t nrows = (int64_t)nbz * dx * nyc;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < nrows;
-       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int yc = (int)(r % nyc);
-    const int64_t t = r / nyc;
-    const int x = (int)(t % dx), bz = (int)(t / dx);
-    const int y = yc * 64 + lane;
-    bool any = false;
-    if (y < dy) {
-      const int z0 = bz * 8, z1 = min(z0 + 8, dz) - 1;   // cells z0 .. z1
-      const int64_t c0 = ((int64_t)x * dy + y) * dz + z0, c1 = c0 + (z1 - z0);
-      const uint32_t wa = qw[c0 >> 5].x;
-      const int a = (int)(c0 & 31), b = (int)(c1 & 31);
-      if ((c1 >> 5) == (c0 >> 5)) {
-        any = ((wa >> a) & ((2u << (b - a)) - 1u)) != 0u;
-      } else {
-        const uint32_t wb = qw[c1 >> 5].x;
-        any = (wa >> a) != 0u || (wb & ((2u << b) - 1u)) != 0u;
-      }
-    }
-    const uint64_t m = __ballot(any);
-    if (lane == 0) {
-      uint32_t* row = coarse + ((int64_t)bz * dx + x) * nyw;
-      row[2 * yc] = (uint32_t)m;
-      if (2 * yc + 1 < nyw) row[2 * yc + 1] = (uint32_t)(m >> 32);
-    }
-  }
-}
-
 __global__ void __launch_bounds__(kBlock) k_word_rank(int64_t words, const int32_t* __restrict__ wrank,
                                                       uint2* __restrict__ qw) {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words;
@@ -952,6 +972,11 @@ extern "C" int pnr_points_bbox(const float* xyz_dev, int64_t n, float* out6_dev,
   return PNR_OK;
 }
 
+// bytes of the KNN's coarse column map for allocation bounds dims (16-B padded)
+static size_t coarse_bytes(const int dims[3]) {
+  return (((size_t)cdiv(dims[2], 8) * dims[0] * cdiv(dims[1], 32) * 4) + 15) & ~(size_t)15;
+}
+
 // Sort, claim, count and fill (K: the cell key type, uint32 unless the grid
 // has 2^32 - 1 cells or more).
 template <typename K>
@@ -966,7 +991,12 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   int32_t* cell_end = h->cell_end.as<int32_t>();
   const K sentinel = (K)gvol;
   const int bits = 64 - __builtin_clzll((unsigned long long)gvol);
-  const int passes = (bits + 7) / 8;
+  // 8-bit digits (kRB): 9-bit ones save c5's fourth pass (26-bit keys) but each
+  // scatter pass took 185 instead of 120 us (4 keys per digit run of a tile:
+  // partial lines) and the build 3.04 vs 2.79 ms (round 6)
+  constexpr int kRB = 8;
+  const int rbits = kRB;
+  const int passes = (bits + rbits - 1) / rbits;
   const int tiles = (int)cdiv(n, kRsTile);
   const unsigned gp = grid_for(n, kBlock);
 
@@ -975,23 +1005,26 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
   int32_t* vals[2] = {h->sort_v[0].as<int32_t>(), h->sort_v[1].as<int32_t>()};
   const int64_t kblocks = cdiv(n > cap_o ? n : cap_o, kRsTile);
   PNR_CHECK_ARG(kblocks < (int64_t)1 << 31, "grid_build: too many sort tiles");
-  hipLaunchKernelGGL(k_cell_keys<K>, dim3((unsigned)kblocks), dim3(kBlock), 0, st, xyz_dev, n, g, geo, sentinel,
-                     keys[0], cap_o, pt_flag, h->occ_numpnts.as<int32_t>(), h->occ_2_coor.as<int32_t>(), counters,
-                     tiles, h->sort_hist.as<int32_t>());
+  hipLaunchKernelGGL((k_cell_keys<kRB, K>), dim3((unsigned)kblocks), dim3(kBlock), 0, st,
+                     xyz_dev, n, g, geo, sentinel, keys[0], cap_o, pt_flag, h->occ_numpnts.as<int32_t>(),
+                     h->occ_2_coor.as<int32_t>(), counters, tiles, h->sort_hist.as<int32_t>(),
+                     n > cap_o ? reinterpret_cast<uint32_t*>(h->sel.as<SelState>() + 1) : nullptr);
   PNR_LAUNCH_CHECK();
   int cur = 0;
   for (int pass = 0; pass < passes; ++pass) {
-    const int shift = 8 * pass;
+    const int shift = rbits * pass;
     if (pass > 0) {   // (pass 0's histogram: k_cell_keys)
-      hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], n, shift, tiles,
-                         h->sort_hist.as<int32_t>());
+      hipLaunchKernelGGL((k_rs_hist<kRB, K>), dim3(tiles), dim3(kBlock), 0, st, keys[cur], n,
+                         shift, tiles, h->sort_hist.as<int32_t>());
       PNR_LAUNCH_CHECK();
     }
-    if ((rc = exclusive_scan(h->sort_hist.as<int32_t>(), (int64_t)256 * tiles, nullptr, h->sort_offs.as<int32_t>(),
-                             (int64_t)(h->sort_offs.bytes / 4), nullptr, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+    if ((rc = exclusive_scan(h->sort_hist.as<int32_t>(), ((int64_t)1 << rbits) * tiles, nullptr,
+                             h->sort_offs.as<int32_t>(), (int64_t)(h->sort_offs.bytes / 4), nullptr, h->scan_tmp.p,
+                             h->scan_tmp.bytes, st)))
       return rc;
-    hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(kBlock), 0, st, keys[cur], pass ? vals[cur] : nullptr, n,
-                       shift, tiles, h->sort_offs.as<int32_t>(), keys[cur ^ 1], vals[cur ^ 1]);
+    hipLaunchKernelGGL((k_rs_scatter<kRB, K>), dim3(tiles), dim3(kBlock), 0, st, keys[cur],
+                       pass ? vals[cur] : nullptr, n, shift, tiles, h->sort_offs.as<int32_t>(), keys[cur ^ 1],
+                       vals[cur ^ 1]);
     PNR_LAUNCH_CHECK();
     cur ^= 1;
   }
@@ -1009,8 +1042,6 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
     SelState* ss = h->sel.as<SelState>();
     uint32_t* hist = reinterpret_cast<uint32_t*>(ss + 1);
     const unsigned gs = grid_for(n, kBlock, 1024);
-    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, counters, (int)cap_o, ss, hist);
-    PNR_LAUNCH_CHECK();
     // the claimers listed by slot (pass 0) in sort_v[cur ^ 1]: free after the sort
     int32_t* cids = vals[cur ^ 1];
     // passes 1.. and the apply walk the claimer list (<= the occupied voxels): fewer blocks
@@ -1027,13 +1058,14 @@ static int build_tables(pnr_handle* h, const float* xyz_dev, int64_t n, const Gr
                              &ss->active)))
       return rc;
   }
-  // cell_bytes = [occupancy bytes | held bytes | word ranks], both byte arrays cleared at once
+  // cell_bytes = [occupancy bytes | held bytes | coarse column map | word ranks]: the
+  // first three cleared by one memset
   uint8_t* occ_bytes = h->cell_bytes.as<uint8_t>();
-  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 64, st));
+  PNR_HIP(hipMemsetAsync(occ_bytes, 0, (size_t)words * 64 + coarse_bytes(g.dims), st));
   hipLaunchKernelGGL(k_claim<K>, dim3(gp), dim3(kBlock), 0, st, xyz_dev, n, g, geo, skey, sid, sentinel, pt_flag,
                      pt_slot, cell_start, cell_end, h->coor_2_occ.as<int32_t>(), h->occ_2_coor.as<int32_t>(),
-                     occ_bytes, occ_bytes + words * 32, h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(),
-                     h->q_rank_slot.as<int32_t>(), counters);
+                     occ_bytes, occ_bytes + words * 32, reinterpret_cast<uint32_t*>(occ_bytes + words * 64),
+                     h->occ_numpnts.as<int32_t>(), h->occ_pts.as<float4>(), h->q_rank_slot.as<int32_t>(), counters);
   PNR_LAUNCH_CHECK();
   // q_rank_slot is scratch until the query index below: slot -> run start
   hipLaunchKernelGGL(k_reservoir, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, xyz_dev, sid,
@@ -1073,7 +1105,7 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
   int64_t scan_n = n;
   for (int64_t m : {cap_o, words, hist_n}) scan_n = m > scan_n ? m : scan_n;
   if ((rc = h->coor_2_occ.ensure(gvol * 4)) || (rc = h->cell_end.ensure(gvol * 4)) ||
-      (rc = h->cell_bytes.ensure(words * 68 + 16)) || (rc = h->occ_bits.ensure(words * 4)) ||
+      (rc = h->cell_bytes.ensure(words * 68 + 16 + coarse_bytes(p->dims))) || (rc = h->occ_bits.ensure(words * 4)) ||
       (rc = h->occ_numpnts.ensure(cap_o * 4)) || (rc = h->occ_pts.ensure(cap_o * p->P * sizeof(float4))) ||
       (rc = h->occ_2_coor.ensure(cap_o * 12)) || (rc = h->sort_k[0].ensure(n * kbytes)) ||
       (rc = h->sort_k[1].ensure(n * kbytes)) || (rc = h->sort_v[0].ensure(n * 4)) ||
@@ -1083,7 +1115,6 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
       (rc = h->counters.ensure(8 * 4)) || (rc = h->sel.ensure(sizeof(SelState) + kSelPasses * 256 * 4)) ||
       (rc = h->scan_tmp.ensure(scan_scratch_bytes(scan_n))) ||
       (rc = h->q_words.ensure(words * 8)) || (rc = h->q_wcnt.ensure((words + 1) * 4)) ||
-      (rc = h->q_coarse.ensure((size_t)cdiv(p->dims[2], 8) * p->dims[0] * cdiv(p->dims[1], 32) * 4)) ||
       (rc = h->q_rank_slot.ensure(cap_o * 4)) || (rc = h->q_rank_cnt.ensure(cap_o * 4)) ||
       (rc = h->q_rec_off.ensure((cap_o + 1) * 4)) || (rc = h->q_recs.ensure(n * sizeof(float4))))
     return rc;
@@ -1116,19 +1147,16 @@ static int grid_build_body(pnr_handle* h, const float* xyz_dev, int64_t n, const
     uint2* qw = h->q_words.as<uint2>();
     int32_t* wcnt = h->q_wcnt.as<int32_t>();
     const uint8_t* held_bytes = occ_bytes + words * 32;                    // written by k_claim
-    int32_t* wrank = reinterpret_cast<int32_t*>(occ_bytes + words * 64);   // after the two byte arrays
+    const size_t cb = coarse_bytes(p->dims);
+    h->coarse_off = (size_t)words * 64;   // the KNN reads the coarse map there (query.hip)
+    int32_t* wrank = reinterpret_cast<int32_t*>(occ_bytes + words * 64 + cb);   // after the maps
     hipLaunchKernelGGL(k_pack_held, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, held_bytes, words, qw, wcnt);
     PNR_LAUNCH_CHECK();
-    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, (int64_t)((h->cell_bytes.bytes - words * 64) / 4), counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
+    if ((rc = exclusive_scan(wcnt, words, nullptr, wrank, (int64_t)((h->cell_bytes.bytes - words * 64 - cb) / 4), counters + 4, h->scan_tmp.p, h->scan_tmp.bytes, st)))
       return rc;
     hipLaunchKernelGGL(k_word_rank, dim3(grid_for(words, kBlock)), dim3(kBlock), 0, st, words, wrank, qw);
     PNR_LAUNCH_CHECK();
-    {
-      const int64_t nrows = cdiv(p->dims[2], 8) * p->dims[0] * cdiv(p->dims[1], 64);
-      hipLaunchKernelGGL(k_coarse_held, dim3(grid_for(nrows * 64, kBlock)), dim3(kBlock), 0, st, g, geo, qw,
-                         h->q_coarse.as<uint32_t>());
-      PNR_LAUNCH_CHECK();
-    }
+
     hipLaunchKernelGGL(k_rank_slots, dim3(grid_for(cap_o, kBlock)), dim3(kBlock), 0, st, (int)cap_o, g, geo,
                        occ_numpnts, occ_2_coor, qw, h->q_rank_slot.as<int32_t>(), h->q_rank_cnt.as<int32_t>());
     PNR_LAUNCH_CHECK();
@@ -1192,10 +1220,20 @@ extern "C" int pnr_grid_build_dev(pnr_handle* h, const float* xyz_dev, int64_t n
   PNR_HIP(hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
   int rc;
-  if ((rc = h->geom.ensure(sizeof(QGrid))) || (rc = h->bbox.ensure(8 * sizeof(float)))) return rc;
-  // bbox -> geometry on the device (k_bbox's reduction, then get_hyperparameters)
-  if ((rc = pnr_points_bbox(xyz_dev, n, h->bbox.as<float>(), stream))) return rc;
-  hipLaunchKernelGGL(k_grid_geom, dim3(1), dim3(64), 0, st, h->bbox.as<float>(), *sp, h->geom.as<QGrid>());
+  const bool fresh = h->bbox_acc.p == nullptr;
+  if ((rc = h->geom.ensure(sizeof(QGrid))) || (rc = h->bbox.ensure(8 * sizeof(float))) ||
+      (rc = h->bbox_acc.ensure(8 * sizeof(unsigned))))
+    return rc;
+  if (fresh) {   // the accumulators' initial state (each build's last block restores it)
+    hipLaunchKernelGGL(k_bbox_acc_init, dim3(1), dim3(64), 0, st, h->bbox_acc.as<unsigned>());
+    PNR_LAUNCH_CHECK();
+  }
+  // bbox -> geometry on the device (get_hyperparameters)
+  hipLaunchKernelGGL(k_bbox, dim3(grid_for(cdiv(n, 4), kBlock, 512)), dim3(kBlock), 0, st, xyz_dev, n,
+                     h->bbox_acc.as<unsigned>());
+  PNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_geom_acc, dim3(1), dim3(64), 0, st, h->bbox_acc.as<unsigned>(), h->bbox.as<float>(), *sp,
+                     h->geom.as<QGrid>());
   PNR_LAUNCH_CHECK();
   pnr_grid_params p{};
   for (int a = 0; a < 3; ++a) {

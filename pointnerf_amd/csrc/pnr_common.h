@@ -179,7 +179,10 @@ struct pnr_handle {
   DevBuf coor_2_occ;      // int32 [gvol]   cell -> slot, -1 = empty
   DevBuf occ_bits;        // uint32 [gvol/32] dilated occupancy bitmap
   DevBuf cell_end;        // int32 [gvol]   one past the last sorted position of the cell's run (occupied cells only)
-  DevBuf cell_bytes;      // uint8 [32*words] x 2 + int32 [words+1]: occupancy bytes before packing, held bytes, word ranks
+  DevBuf cell_bytes;      // uint8 [32*words] x 2, the coarse column map, int32 [words+1]: occupancy bytes
+                          //   before packing, held bytes, the KNN's coarse map (uint32 [ceil(dz/8)][dx]
+                          //   [ceil(dy/32)]: bit y = column (x, y) holds a kept point in z-block bz), word ranks
+  size_t coarse_off = 0;  // byte offset of the coarse map in cell_bytes
   DevBuf occ_numpnts;     // int32 [max_o]  points that fell in the voxel
   DevBuf occ_pts;         // float4 [max_o*P] {x, y, z, bitcast(point id)}
   DevBuf occ_2_coor;      // int32 [max_o*3]
@@ -199,14 +202,13 @@ struct pnr_handle {
   // stays in L2 and its records sit near each other in HBM.
   DevBuf q_words;         // uint2 [gvol/32] {bits: cell holds >= 1 kept point, rank of the word's first cell}
   DevBuf q_wcnt;          // int32 [gvol/32] scratch: popcount per word
-  DevBuf q_coarse;        // uint32 [ceil(dz/8)][dx][ceil(dy/32)]: bit y of word (bz, x, y/32) = column (x, y)
-                          //   holds a kept point in z-block [8 bz, 8 bz + 8) (the KNN's column filter)
   DevBuf q_rank_slot;     // int32 [max_o]   slot of rank r (scratch)
   DevBuf q_rank_cnt;      // int32 [max_o]   min(P, points) of rank r (scratch)
   DevBuf q_rec_off;       // int32 [max_o+1] first record of rank r (exclusive scan of q_rank_cnt)
   DevBuf q_recs;          // float4 [N]      {x, y, z, bitcast(id)} in rank order, per voxel ascending id
   DevBuf geom;            // QGrid of the built grid (device)
   DevBuf bbox;            // float [8] point bbox of the last pnr_grid_build_dev
+  DevBuf bbox_acc;        // uint32 [8] k_bbox_geom's order-key accumulators + block ticket (kept reset)
   QGrid* host_geom = nullptr;   // pinned copy of geom behind stats_ev
   float* host_bbox = nullptr;   // pinned copy of bbox (device builds) behind stats_ev
   bool geom_on_device = false;  // gp.shift / dims are bounds, the exact geometry is geom (device)
@@ -230,8 +232,8 @@ struct pnr_handle {
     stats_pending = false;
     DevBuf* all[] = {&coor_2_occ, &occ_bits, &cell_end, &cell_bytes, &occ_numpnts, &occ_pts, &occ_2_coor,
                      &sort_k[0], &sort_k[1], &sort_v[0], &sort_v[1], &sort_hist, &sort_offs,
-                     &cell_start, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_coarse, &q_rank_slot, &q_rank_cnt,
-                     &q_rec_off, &q_recs, &geom, &bbox};
+                     &cell_start, &pt_flag, &pt_slot, &counters, &sel, &scan_tmp, &q_words, &q_wcnt, &q_rank_slot, &q_rank_cnt,
+                     &q_rec_off, &q_recs, &geom, &bbox, &bbox_acc};
     for (DevBuf* b : all) b->release();
   }
 };

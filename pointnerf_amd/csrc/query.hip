@@ -683,7 +683,7 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   const int vec = ((uintptr_t)b->pidx & 15) == 0;
   QIndex qi;
   qi.words = h->q_words.as<uint2>();
-  qi.coarse = h->q_coarse.as<uint32_t>();
+  qi.coarse = reinterpret_cast<const uint32_t*>(h->cell_bytes.as<uint8_t>() + h->coarse_off);
   qi.rec_off = h->q_rec_off.as<int32_t>();
   qi.recs = h->q_recs.as<float4>();
 #define PNR_KNN(KM)                                                                              \

@@ -11,16 +11,20 @@ out=$(mktemp /tmp/kregs.XXXXXX.co)
 import sys, re
 cur = {}
 rows = []
+# a kernel entry of amdhsa.kernels starts with "  - .<first key>" (keys in alphabetical
+# order, so .agpr_count / .group_segment_fixed_size come BEFORE .name)
 for line in sys.stdin:
-    m = re.match(r"\s+\.(name|vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size|group_segment_fixed_size):\s+(\S+)", line)
+    if re.match(r"\s+- \.", line):
+        cur = {}
+        rows.append(cur)
+    m = re.match(r"\s+-?\s*\.(name|vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size|group_segment_fixed_size):\s+(\S+)", line)
     if not m:
         continue
     k, v = m.groups()
-    if k == "name" and not v.endswith(".kd"):
-        cur = {"name": v}
-        rows.append(cur)
-    elif cur:
-        cur[k] = v
+    if k == "name" and v.endswith(".kd"):
+        continue
+    cur[k] = v
+rows = [r for r in rows if "name" in r]
 for r in rows:
     print("%-60s vgpr %4s agpr %4s vspill %4s sspill %4s scratch %6s lds %6s" % (
         r["name"][:60], r.get("vgpr_count"), r.get("agpr_count"), r.get("vgpr_spill_count"),
