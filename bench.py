@@ -435,20 +435,28 @@ def run_train(args, device):
         optim = torch.optim.Adam(params, lr=5e-4, fused=True)
     gen = torch.Generator(device=device).manual_seed(rank)
     stats = {"pairs": 0, "valid": 0, "filled": 0}
+    host_ms = {"forward": 0.0, "loss": 0.0, "backward": 0.0, "optimizer": 0.0}   # host time per phase (timed steps)
 
     def step(i, timed):
         campos, camrot, rd = dev_cams[i % len(dev_cams)]
+        t0 = time.perf_counter()
         sel = torch.randint(0, H * W, (args.train_rays,), generator=gen, device=device)
         optim.zero_grad(set_to_none=True)
         color, _, _, _ = model.render_rays_train(campos, camrot, rd[sel], opt.near_plane, opt.far_plane, bg)
+        t1 = time.perf_counter()
         loss = torch.mean((color[:, :3] - target[sel]) ** 2)
         if "conf_coefficient" in model.last_train_aux:   # ship.sh: zero_one_loss_weights 1e-4
             loss = loss + 1e-4 * model.zero_one_conf_loss()
+        t2 = time.perf_counter()
         loss.backward()
         if reducer is not None:
             reducer.reduce(model.last_train_aux["touched_rows"], model.last_train_aux["touched_count"])
+        t3 = time.perf_counter()
         optim.step()
         if timed:
+            t4 = time.perf_counter()
+            for k, d in zip(host_ms, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+                host_ms[k] += d * 1e3
             c = model.last_counts
             stats["pairs"] += c["n_pairs"]
             stats["valid"] += c["S_valid"]
@@ -462,6 +470,7 @@ def run_train(args, device):
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, True)
+    t_issue = time.perf_counter() - t0   # host time to issue the steps (the GPU may still be working)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -500,7 +509,11 @@ def run_train(args, device):
                      "note": "whole step (fwd + bwd + Adam + query) against the MLP GEMM work only: 3 x (542 720 "
                              "FLOP per valid pair + 137 216 per valid sample) per step (forward, data and weight "
                              "gradients); peak = the fp32-equivalent ceiling of the split arithmetic"},
-        "counts_per_step": {k2: v // k for k2, v in stats.items()}}
+        "counts_per_step": {k2: v // k for k2, v in stats.items()},
+        # host time per step spent issuing (no device sync inside a step but the query-count
+        # read): close to ms_per_step means the step is bound by its launches, not the GPU
+        "host_issue_ms_per_step": round(t_issue / k * 1e3, 3),
+        "host_phase_ms_per_step": {k2: round(v / k, 3) for k2, v in host_ms.items()}}
     if world > 1:
         dist.destroy_process_group()
     return line
@@ -965,7 +978,7 @@ def train_summary(args, device):
     targs.mode, targs.steps, targs.warmup, targs.dtype = "train", 20, 5, "fp32"
     line = run_train(targs, device)
     keep = ("value", "unit", "ms_per_step", "dtype", "arith", "roofline", "h2_fallbacks", "optimizer", "config",
-            "counts_per_step", "gemm_tflops_per_s")
+            "counts_per_step", "gemm_tflops_per_s", "host_issue_ms_per_step", "host_phase_ms_per_step")
     return {"train_ms_per_step": line["ms_per_step"], **{k: line[k] for k in keep}}
 
 

@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 21
+#define PNR_ABI_VERSION 22
 
 enum {
   PNR_OK = 0,
@@ -600,6 +600,81 @@ int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, cons
                                const float* d_feat, const float* d_hid, float* dz1, float* dz2, float* dz3,
                                float* dz4, float* dpa, float* d_p1, float* d_color, float* d_dir,
                                float* d_conf, void* stream);
+/* Several weight packs in one launch (a training step rebuilds every pack per
+ * step): job q is pnr_pack_weights(kind, ...) for kind 0 / 1 and
+ * pnr_pack_weights_h2(..., shift, range_flag, ...) for kind 2 (shift and
+ * range_flag ignored otherwise), same layouts, bitwise the same outputs;
+ * 1 <= n <= 16. */
+typedef struct {
+  int32_t kind;
+  const float* W; int64_t ld_row; int64_t ld_col;
+  int32_t out_f; int32_t kin;
+  const float* bias;
+  int32_t pad_steps; int32_t shift;
+  int32_t* range_flag;
+  void* out; size_t out_bytes;
+} pnr_pack_job;
+int pnr_pack_batch(const pnr_pack_job* jobs, int32_t n, void* stream);
+/* Same, with the three dX GEMMs on fp32h2 split-f16 MFMA (the fp32h2 training
+ * step): wbh = pnr_pack_bwd_h2's packs and scales; each 64-pair tile's layer
+ * input is scaled by a power of two picked from its max |value| inside the
+ * kernel (no range flag, no fallback).  wb supplies w3e as above. */
+typedef struct {
+  const void* w4th; const void* w3th; const void* w2th;
+  const float* scale;   /* device [3]: 2^(s - 11) of each pack */
+} pnr_mlp_bwd_h2;
+int pnr_aggregate_bwd_pairs_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                               const pnr_mlp_bwd* wb, const pnr_mlp_bwd_h2* wbh, const pnr_agg_saved* saved,
+                               const float* d_feat, const float* d_hid, float* dz1, float* dz2, float* dz3,
+                               float* dz4, float* dpa, float* d_p1, float* d_color, float* d_dir,
+                               float* d_conf, void* stream);
+/* The packs of pnr_aggregate_bwd_pairs_h2 in one launch: block3.2.weight^T
+ * (w4, [256,256] row-major), block3.0.weight[:, :256]^T (w3, row stride ld3 >=
+ * 256) and block1.2.weight^T (w2) as frag_pack_h2 packs of 16 + pad_steps
+ * k-steps each (pad steps zero; the kernel reads 3 ahead: pad_steps >= 3),
+ * back to back in out (3 x (16 + pad) x 2048 x 8 B); scale_dev[m] = 2^(s_m - 11)
+ * with s_m picked on the device as pnr_pack_weights_h2_dev's. */
+int pnr_pack_bwd_h2(const float* w4, const float* w3, int64_t ld3, const float* w2, int32_t pad_steps,
+                    float* scale_dev, void* out, size_t out_bytes, void* stream);
+/* The pairs grouped by point: the (prow_sorted, pair_of) of torch.sort(prow[0..m),
+ * stable=True) over the pairs with prow >= 0 -- each referenced point's pairs in
+ * pair order -- followed by the empty pairs (prow_sorted = -1, pair_of = 0) at
+ * the END (torch.sort puts them first; pnr_pairs_to_points(_ex) skip them either
+ * way).  Key of a pair = key_map[prow] (the used-point map, keys < n_keys) or
+ * prow itself (key_map NULL, n_keys > max prow).  A counting sort with a
+ * per-key sort back into pair order: deterministic, no host sync. */
+int pnr_group_pairs_scratch_bytes(int64_t m, int64_t n_keys, size_t* out);
+int pnr_group_pairs(const int32_t* prow, int64_t m, const int32_t* key_map, int64_t n_keys, int32_t* prow_sorted,
+                    int32_t* pair_of, void* scratch, size_t scratch_bytes, void* stream);
+/* alpha_branch.0's gradient: out_w[c] = sum_r dpa[r] h4[r][c] (c < 256, h4 rows of
+ * 256), out_b[0] = sum_r dpa[r], r < m; deterministic (fixed per-block partials
+ * summed in block order); partials: pnr_alpha_colsum_scratch_floats() floats. */
+int pnr_alpha_colsum_scratch_floats(int64_t* out);
+int pnr_alpha_colsum(const float* dpa, const float* h4, int64_t m, float* out_w, float* out_b, float* partials,
+                     void* stream);
+/* The fp32h2 finetune step's backward through the aggregator in one call
+ * (replaces train.py AggregateFn.backward's sequence, point_aggregators.py
+ * autograd as listed there): colour branch (pnr_color_dz, pnr_gemm_tn_h2 /
+ * pnr_gemm_nn_h2), pnr_pack_bwd_h2 + pnr_aggregate_bwd_pairs_h2,
+ * pnr_group_pairs + pnr_aggregate_bwd_extras_rows + pnr_pairs_to_points_ex,
+ * the weight gradients, pnr_alpha_colsum, block1.0's point half
+ * (pnr_point_pe3_rows, pnr_gemm_tn_h2 / pnr_gemm_nn_h2, pnr_point_pe3_bwd_rows).
+ * prm: the 16 aggregator parameters as nn.Linear stores them (row-major), in
+ * train.py _PARAM_NAMES order; out->g: their gradients (same shapes, written);
+ * d_emb [N,32] written (zero for unreferenced points); d_color / d_dir [N,3],
+ * d_conf [N] written when not NULL.  n = valid samples (d_feat [>= n, 129]),
+ * n_used = referenced points (pts->used / used_map required).  Scratch:
+ * pnr_aggregate_bwd_step_h2_scratch_bytes (256-B aligned).  No host sync. */
+typedef struct { const float* p[16]; } pnr_agg_params;
+typedef struct {
+  float* g[16];
+  float* d_emb; float* d_color; float* d_dir; float* d_conf;
+} pnr_agg_grads;
+int pnr_aggregate_bwd_step_h2_scratch_bytes(int64_t n, int64_t n_used, size_t* out);
+int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                              const pnr_agg_params* prm, const pnr_agg_saved* saved, const float* d_feat, int64_t n,
+                              int64_t n_used, const pnr_agg_grads* out, void* scratch, size_t scratch_bytes,
+                              void* stream);
 /* Point-position gradient (--xyz_grad 1, neural_points.py:270; replaces the
  * autograd of sampled_xyz / sampled_xyz_pers, neural_points.py:635, 788-799,
  * through point_aggregators.py:775-804 and the PE_5 input of block1.0):
@@ -656,6 +731,15 @@ int pnr_gemm_tn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int
 int pnr_gemm_nn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K, int32_t N,
                    const float* act, int64_t ld_act, float slope, float* C, int64_t ldc, const uint32_t* a_absmax,
                    int32_t* range_flag, void* stream);
+/* The colour branch's backward input in one pass (train.py: replaces the torch
+ * ops (d_feat[:, 1:] * (vmask != 0)) then where(hc > 0, x, x * slope)):
+ * dz[r][c] = that, r < n, c < C (C % 4 == 0; dz [n, C] row-major; d_feat rows of
+ * ld_feat >= C + 1 floats, column 0 the alpha; hc rows of ld_hc, a multiple of 4;
+ * hc and dz 16-B aligned); absmax (optional,
+ * pre-zeroed): max |dz| folded in as float bits (NaN above inf), the scale of
+ * the h2 GEMMs that consume dz. */
+int pnr_color_dz(const float* d_feat, int64_t ld_feat, const int32_t* vmask, const float* hc, int64_t ld_hc,
+                 int64_t n, int32_t C, float slope, float* dz, uint32_t* absmax, void* stream);
 /* *out_bits = float bits of max |x[0, n)| (NaN if any x is NaN); partials:
  * pnr_absmax_scratch_floats() device floats.  No host sync. */
 int pnr_absmax_scratch_floats(int64_t* out);

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 21
+ABI_VERSION = 22
 FEAT_H_PITCH = 136   # PNR_FEAT_H_PITCH: uint16 per bf16 feature row (pnr_aggregate_fwd_bf16_hf)
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
@@ -140,6 +140,25 @@ class MlpBwdX3(ctypes.Structure):
     _fields_ = [("w4tx", c_void_p), ("w3tx", c_void_p), ("w2tx", c_void_p)]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("W", c_void_p), ("ld_row", c_int64), ("ld_col", c_int64), ("out_f", c_int32),
+                ("kin", c_int32), ("bias", c_void_p), ("pad_steps", c_int32), ("shift", c_int32),
+                ("range_flag", c_void_p), ("out", c_void_p), ("out_bytes", c_size_t)]
+
+
+class AggParams(ctypes.Structure):
+    _fields_ = [("p", c_void_p * 16)]
+
+
+class AggGrads(ctypes.Structure):
+    _fields_ = [("g", c_void_p * 16), ("d_emb", c_void_p), ("d_color", c_void_p), ("d_dir", c_void_p),
+                ("d_conf", c_void_p)]
+
+
+class MlpBwdH2(ctypes.Structure):
+    _fields_ = [("w4th", c_void_p), ("w3th", c_void_p), ("w2th", c_void_p), ("scale", c_void_p)]
+
+
 P = ctypes.POINTER
 # name -> (restype, argtypes); exactly the functions include/pnr.h declares.
 SIGNATURES = {
@@ -192,6 +211,22 @@ SIGNATURES = {
     "pnr_aggregate_bwd_pairs_x3": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(MlpBwdX3), P(AggSaved),
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_aggregate_bwd_pairs_h2": (c_int, [P(Points), P(Samples), P(Mlp), P(MlpBwd), P(MlpBwdH2), P(AggSaved),
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_color_dz": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_float, c_void_p,
+                             c_void_p, c_void_p]),
+    "pnr_group_pairs_scratch_bytes": (c_int, [c_int64, c_int64, P(c_size_t)]),
+    "pnr_group_pairs": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t,
+                                c_void_p]),
+    "pnr_alpha_colsum_scratch_floats": (c_int, [P(c_int64)]),
+    "pnr_alpha_colsum": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pnr_aggregate_bwd_step_h2_scratch_bytes": (c_int, [c_int64, c_int64, P(c_size_t)]),
+    "pnr_aggregate_bwd_step_h2": (c_int, [P(Points), P(Samples), P(Mlp), P(AggParams), P(AggSaved), c_void_p,
+                                          c_int64, c_int64, P(AggGrads), c_void_p, c_size_t, c_void_p]),
+    "pnr_pack_batch": (c_int, [P(PackJob), c_int32, c_void_p]),
+    "pnr_pack_bwd_h2": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_size_t,
+                                c_void_p]),
     "pnr_aggregate_bwd_xyz": (c_int, [P(Points), P(Samples), P(Mlp), P(AggSaved), c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p]),
     "pnr_used_points_scratch_bytes": (c_int, [c_int64, P(c_size_t)]),
@@ -326,7 +361,9 @@ class H2Gemm:
     the pnr_absmax scratch."""
 
     def __init__(self, device):
-        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        # [0]: the range flag; [1:]: pre-zeroed absmax words for fused producers
+        self.words = torch.zeros(8, dtype=torch.int32, device=device)
+        self.flag = self.words[:1]
         n = ctypes.c_int64(0)
         check(lib().pnr_absmax_scratch_floats(ctypes.byref(n)), "pnr_absmax_scratch_floats")
         self.part = torch.empty(int(n.value), dtype=torch.float32, device=device)
@@ -364,6 +401,21 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, colsum: bool = False, x3: bool = T
     check(fn(ptr(A), A.stride(0), ptr(B), B.stride(0), K, M, N, ptr(C), ptr(cs), ptr(scratch),
              scratch.numel() * 4, stream_ptr(A.device)), "pnr_gemm_tn")
     return (C, cs) if colsum else C
+
+
+def group_pairs(prow: torch.Tensor, key_map: torch.Tensor | None, n_keys: int):
+    """(prow_sorted, pair_of) int32 [m]: the pairs grouped by point in pair order
+    (pnr_group_pairs -- torch.sort(prow, stable=True) with the empty pairs last)."""
+    m = prow.numel()
+    dev = prow.device
+    nb = c_size_t(0)
+    check(lib().pnr_group_pairs_scratch_bytes(m, max(int(n_keys), 1), ctypes.byref(nb)),
+          "pnr_group_pairs_scratch_bytes")
+    scratch = torch.empty(max(int(nb.value), 16), dtype=torch.uint8, device=dev)
+    ps, po = (torch.empty(max(m, 1), dtype=torch.int32, device=dev) for _ in range(2))
+    check(lib().pnr_group_pairs(ptr(prow), m, ptr(key_map), max(int(n_keys), 1), ptr(ps), ptr(po), ptr(scratch),
+                                scratch.numel(), stream_ptr(dev)), "pnr_group_pairs")
+    return ps[:m], po[:m]
 
 
 def gemm_nn(A: torch.Tensor, B: torch.Tensor, act: torch.Tensor | None = None, slope: float = 0.0,

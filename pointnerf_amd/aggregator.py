@@ -300,30 +300,25 @@ class PointAggregator(nn.Module):
         self.pair_buckets = True
 
     # ---------------------------------------------------------------- weights
-    def packed(self) -> tuple[L.Mlp, dict]:
-        """Fragment-packed weights on the module's device, rebuilt only when a
-        parameter changed (version counters)."""
-        ps = list(self.parameters())
-        key = tuple((p.data_ptr(), p._version) for p in ps) + ((self.rw2c.data_ptr(), self.rw2c._version),)
-        if self._packed is not None and key == self._packed_key:
-            return self._packed
-        with torch.no_grad():
-            b1, b3 = self.block1, self.block3
-            t = dict(
-                w1af=frag_pack(b1[0].weight[:, :224], b1[0].bias),
-                w1bf=frag_pack(b1[0].weight[:, 224:]),
-                w2f=frag_pack(b1[2].weight, b1[2].bias), b2=b1[2].bias.float().contiguous(),
-                w3f=frag_pack(b3[0].weight, b3[0].bias), b3=b3[0].bias.float().contiguous(),
-                w4f=frag_pack(b3[2].weight, b3[2].bias), b4=b3[2].bias.float().contiguous(),
-                wa=self.alpha_branch[0].weight.float().reshape(-1).contiguous(),
-                ba=self.alpha_branch[0].bias.float().contiguous(),
-                wc1f=frag_pack(self.color_branch[0].weight, self.color_branch[0].bias),
-                bc1=self.color_branch[0].bias.float().contiguous(),
-                wc2f=frag_pack(self.color_branch[2].weight, self.color_branch[2].bias),
-                bc2=self.color_branch[2].bias.float().contiguous(),
-                wc3f=frag_pack(self.color_branch[4].weight, self.color_branch[4].bias),
-                bc3=self.color_branch[4].bias.float().contiguous(),
-                rw2c=self.rw2c.float().contiguous())
+    def _fp32_key(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters()) + (
+            (self.rw2c.data_ptr(), self.rw2c._version),)
+
+    def _fp32_specs(self) -> list:
+        """(name, W, bias) of the native-fp32 packs of packed()."""
+        b1, b3, cb = self.block1, self.block3, self.color_branch
+        return [("w1af", b1[0].weight[:, :224], b1[0].bias), ("w1bf", b1[0].weight[:, 224:], None),
+                ("w2f", b1[2].weight, b1[2].bias), ("w3f", b3[0].weight, b3[0].bias),
+                ("w4f", b3[2].weight, b3[2].bias), ("wc1f", cb[0].weight, cb[0].bias),
+                ("wc2f", cb[2].weight, cb[2].bias), ("wc3f", cb[4].weight, cb[4].bias)]
+
+    def _set_packed(self, t: dict, key):
+        b1, b3, cb = self.block1, self.block3, self.color_branch
+        t.update(b2=b1[2].bias.float().contiguous(), b3=b3[0].bias.float().contiguous(),
+                 b4=b3[2].bias.float().contiguous(), wa=self.alpha_branch[0].weight.float().reshape(-1).contiguous(),
+                 ba=self.alpha_branch[0].bias.float().contiguous(), bc1=cb[0].bias.float().contiguous(),
+                 bc2=cb[2].bias.float().contiguous(), bc3=cb[4].bias.float().contiguous(),
+                 rw2c=self.rw2c.float().contiguous())
         m = L.Mlp()
         for k, v in t.items():
             setattr(m, k, v.data_ptr())
@@ -331,6 +326,60 @@ class PointAggregator(nn.Module):
         m.act_super = self.act_super
         self._packed, self._packed_key = (m, t), key
         return self._packed
+
+    def packed(self) -> tuple[L.Mlp, dict]:
+        """Fragment-packed weights on the module's device, rebuilt only when a
+        parameter changed (version counters)."""
+        key = self._fp32_key()
+        if self._packed is not None and key == self._packed_key:
+            return self._packed
+        with torch.no_grad():
+            t = {k: frag_pack(W, b) for k, W, b in self._fp32_specs()}
+            return self._set_packed(t, key)
+
+    def packed_train(self, h2: bool) -> None:
+        """The training forward's packs -- packed() and, for fp32h2,
+        packed_h2_train() -- rebuilt in ONE pnr_pack_batch launch when the weights
+        changed (every step: the optimizer moved them); bitwise the packs of the
+        per-matrix calls.  Afterwards packed() / packed_h2_train() return them
+        from their caches."""
+        dev = self.block1[0].weight.device
+        if dev.type != "cuda":
+            return
+        kf = self._fp32_key()
+        need_f = self._packed is None or kf != self._packed_key
+        kh = self.h2_key()
+        need_h = h2 and (getattr(self, "_packedh2t", None) is None or kh != self._packedh2t_key)
+        if not (need_f or need_h):
+            return
+        jobs, keep, outs_f, outs_h = [], [], {}, []
+        with torch.no_grad():
+            if need_f:
+                for name, W, b in self._fp32_specs():
+                    out_f, kin = W.shape
+                    n = ((kin + (b is not None) + 1) // 2 + PREFETCH_PAD) * (out_f // 32) * 64
+                    outs_f[name] = torch.empty(n, dtype=torch.float32, device=dev)
+                    jobs.append((0, W, b, PREFETCH_PAD, 0, None, outs_f[name]))
+            if need_h:
+                mats = self._h2t_mats()
+                flag = self._h2t_prepare(mats)
+                for (W, b), sft in zip(mats, self._h2t_shifts):
+                    out_f, kin = W.shape
+                    n = ((kin + (b is not None) + 15) // 16 + H2_PAD) * (out_f // 32) * 64 * 2 * 8
+                    outs_h.append(torch.empty(n, dtype=torch.float16, device=dev))
+                    jobs.append((2, W, b, H2_PAD, sft, flag, outs_h[-1]))
+            arr = (L.PackJob * len(jobs))()
+            for q, (kind, W, b, pad, sft, flag, out) in enumerate(jobs):
+                W = W.detach().float()
+                b = None if b is None else b.detach().float().contiguous()
+                keep += [W, b]
+                arr[q] = L.PackJob(kind, W.data_ptr(), W.stride(0), W.stride(1), W.shape[0], W.shape[1], L.ptr(b),
+                                   pad, sft, L.ptr(flag), out.data_ptr(), out.numel() * out.element_size())
+            L.check(L.lib().pnr_pack_batch(arr, len(jobs), L.stream_ptr(dev)), "pnr_pack_batch")
+            if need_f:
+                self._set_packed(outs_f, kf)
+            if need_h:
+                self._set_packedh2t(outs_h, kh)
 
     def packed_bf16(self) -> tuple[L.MlpBf16, dict]:
         """bf16 fragment packs for pnr_aggregate_fwd_bf16 (cached like packed())."""
@@ -416,15 +465,27 @@ class PointAggregator(nn.Module):
         key = self.h2_key()
         if getattr(self, "_packedh2t", None) is not None and key == self._packedh2t_key:
             return self._packedh2t
+        mats = self._h2t_mats()
+        flag = self._h2t_prepare(mats)
+        packs = [_pack_h2_device(W, b, s, flag) for (W, b), s in zip(mats, self._h2t_shifts)]
+        return self._set_packedh2t(packs, key)
+
+    def _h2t_mats(self) -> list:
         b1, b3 = self.block1, self.block3
-        mats = [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None),
+        return [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None),
                 (b1[0].weight[:, :224], b1[0].bias)]   # the last: block1.0's point half (k_point_pre_h2)
+
+    def _h2t_prepare(self, mats) -> torch.Tensor:
+        """The training packs' shifts (picked on the host once, kept until a raised
+        range flag) and their device flag."""
         if getattr(self, "_h2t_shifts", None) is None:
             with torch.no_grad():
                 self._h2t_shifts = [h2_shift(W, b) for W, b in mats]
-            self._h2t_flag = torch.zeros(1, dtype=torch.int32, device=b1[0].weight.device)
+            self._h2t_flag = torch.zeros(1, dtype=torch.int32, device=self.block1[0].weight.device)
+        return self._h2t_flag
+
+    def _set_packedh2t(self, packs: list, key):
         flag = self._h2t_flag
-        packs = [_pack_h2_device(W, b, s, flag) for (W, b), s in zip(mats, self._h2t_shifts)]
         t = dict(w1bh=packs[0], w2h=packs[1], w3h=packs[2], w4h=packs[3], w1ah=packs[4], range_flag=flag)
         sc = [2.0 ** (s - 11) for s in self._h2t_shifts]
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),

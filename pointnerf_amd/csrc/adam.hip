@@ -60,17 +60,23 @@ __global__ void __launch_bounds__(kAdamBlock) k_adam(AdamArgs a) {
   if (vec) {
     const int64_t q1 = e0 + ((e1 - e0) & ~int64_t(3));   // float4 quads [e0, q1), e0 % 4 == 0
     for (int64_t e = e0 + 4 * (int64_t)threadIdx.x; e < q1; e += 4 * kAdamBlock) {
-      float4 p = *reinterpret_cast<const float4*>(P + e);
-      const float4 g = *reinterpret_cast<const float4*>(G + e);
-      float4 m = *reinterpret_cast<const float4*>(M + e);
-      float4 v = *reinterpret_cast<const float4*>(V + e);
+      // streamed once: nontemporal loads / stores (0.394 vs 0.418 ms per step on
+      // 78 M elements, tools/adam_bench.py A/B, same results)
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      const f4 pv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(P + e));
+      const f4 gv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(G + e));
+      const f4 mv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(M + e));
+      const f4 vv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(V + e));
+      float4 p = make_float4(pv.x, pv.y, pv.z, pv.w), m = make_float4(mv.x, mv.y, mv.z, mv.w);
+      float4 v = make_float4(vv.x, vv.y, vv.z, vv.w);
+      const float4 g = make_float4(gv.x, gv.y, gv.z, gv.w);
       adam1(p.x, g.x, m.x, v.x, a);
       adam1(p.y, g.y, m.y, v.y, a);
       adam1(p.z, g.z, m.z, v.z, a);
       adam1(p.w, g.w, m.w, v.w, a);
-      *reinterpret_cast<float4*>(P + e) = p;
-      *reinterpret_cast<float4*>(M + e) = m;
-      *reinterpret_cast<float4*>(V + e) = v;
+      __builtin_nontemporal_store((f4){p.x, p.y, p.z, p.w}, reinterpret_cast<f4*>(P + e));
+      __builtin_nontemporal_store((f4){m.x, m.y, m.z, m.w}, reinterpret_cast<f4*>(M + e));
+      __builtin_nontemporal_store((f4){v.x, v.y, v.z, v.w}, reinterpret_cast<f4*>(V + e));
     }
     for (int64_t e = q1 + threadIdx.x; e < e1; e += kAdamBlock) adam1(P[e], G[e], M[e], V[e], a);
   } else {

@@ -174,6 +174,19 @@ __device__ __forceinline__ uint4 f16x8_scale2048(const uint4& a) {
   return __builtin_bit_cast(uint4, __builtin_bit_cast(h8, a) * (h8)((_Float16)2048.f));
 }
 
+// gemm.hip, for the native backward step (train_step.hip): C[:, :ncols] (rows of
+// ldc floats) = A^T B on mode 0 fp32 / 1 fp32x3 / 2 fp32h2 (pnr_gemm_tn*), and
+// the scratch that takes.
+size_t gemm_scratch(int64_t K, int M, int N);
+int gemm_tn_run(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
+                float* C, int64_t ldc, int32_t ncols, float* colsum_a, void* scratch, size_t scratch_bytes,
+                void* stream, const uint32_t* a_absmax, int32_t* range_flag);
+// C = A B (x LeakyReLU derivative) on fp32 / fp32h2 (pnr_gemm_nn*), max |C| folded
+// into c_absmax when given (pre-zeroed): the next h2 product's scale, no pnr_absmax pass.
+int gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K, int32_t N,
+                const float* act, int64_t ld_act, float slope, float* C, int64_t ldc, const uint32_t* a_absmax,
+                int32_t* range_flag, uint32_t* c_absmax, void* stream);
+
 // aggregate_x3.hip: the pairs stage of pnr_aggregate_fwd_x3 (H = false: 3-way
 // bf16 split, six products) and pnr_aggregate_fwd_h2 (H = true: 2-way f16
 // split, three products).  packs: block1.0[:, 224:], block1.2, block3.0,

@@ -854,7 +854,9 @@ struct BwdArgs {
   float* d_color;        // [N,3] (+=) or null
   float* d_dir;          // [N,3] (+=) or null
   float* d_conf;         // [N]   (+=) or null
-  const void* wx[3];     // k_pairs_bwd<true>: frag_pack_x3 of W4^T, W3[:, :256]^T, W2^T
+  const void* wx[3];     // k_pairs_bwd<1>: frag_pack_x3 of W4^T, W3[:, :256]^T, W2^T;
+                         // k_pairs_bwd<2>: the three pnr_pack_bwd_h2 packs
+  const float* wxs;      // k_pairs_bwd<2>: device [3], the packs' scales 2^(s - 11)
 };
 
 constexpr int kBwdLdsFloats = 66 * kQP + 4 * kTP /*dot parts*/ + 4 * 7 * kTP /*extras parts*/;
@@ -1058,13 +1060,127 @@ __device__ __forceinline__ void mlp_layer_x3q(f32x16 (&acc)[4], __amdgpu_buffer_
     if (t + d < nsteps) step(w.a[d], t + d);
 }
 
+// ---- fp32h2 dX GEMMs of k_pairs_bwd<2>: the transposed weights as f16 (hi,
+// 2^11 lo) pairs of 2^-s W (pnr_pack_bwd_h2: F[t][T][plane][lane][8], kX3D zero
+// steps), the B fragments split from the fp32 quad rows times the tile's power
+// of two xs (max |X| xs in [2^13, 2^14): every value of the tile keeps 22
+// significant bits down to 2^-14 of the maximum), three products per 16-k step
+// on v_mfma_f32_32x32x16_f16 -- 2^11 (2^-s W X xs) in the accumulators, which
+// the caller scales back.
+struct H2QRing {
+  uint4 a[kX3D][2][2];
+};
 
-template <bool X3>
+__device__ __forceinline__ void h2q_load(uint4 (&a)[2][2], __amdgpu_buffer_rsrc_t rs, int voff, int t) {
+#pragma unroll
+  for (int T = 0; T < 2; ++T)
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      a[T][pl] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + pl * 1024,
+                                                                                   (t * 8 + T) * 2 * 1024, 0));
+}
+
+__device__ __forceinline__ void h2q_b(const float* X, int t, int pt, int lane, float xs, uint4 (&b)[2]) {
+  const int c = lane & 31, h = lane >> 5;
+  const float* xb = X + (4 * t + 2 * h) * kQP + 4 * (32 * pt + c);
+  const float4 q0 = *reinterpret_cast<const float4*>(xb);
+  const float4 q1 = *reinterpret_cast<const float4*>(xb + kQP);
+  unsigned w0[4], w1[4];
+  splith(q0.x * xs, q0.z * xs, w0[0], w1[0]);
+  splith(q0.y * xs, q0.w * xs, w0[1], w1[1]);
+  splith(q1.x * xs, q1.z * xs, w0[2], w1[2]);
+  splith(q1.y * xs, q1.w * xs, w0[3], w1[3]);
+  b[0] = make_uint4(w0[0], w0[1], w0[2], w0[3]);
+  b[1] = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+}
+
+__device__ __forceinline__ void mlp_layer_h2q(f32x16 (&acc)[4], __amdgpu_buffer_rsrc_t rs, int voff,
+                                              const float* X, int nsteps, int lane, float xs) {
+  H2QRing w;
+#pragma unroll
+  for (int d = 0; d < kX3D; ++d) h2q_load(w.a[d], rs, voff, d);
+  uint4 b[2][2];
+  h2q_b(X, 0, 0, lane, xs, b[0]);
+  h2q_b(X, 0, 1, lane, xs, b[1]);
+  auto step = [&](uint4 (&a)[2][2], int t) {
+    if (t > 0) {
+      h2q_b(X, t, 0, lane, xs, b[0]);
+      h2q_b(X, t, 1, lane, xs, b[1]);
+    }
+    // smallest terms first: Wl.Xh, Wh.Xl, then 2^11 Wh.Xh; four independent chains
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_f16(a[T][1], b[pt][0], acc[2 * pt + T]);
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int T = 0; T < 2; ++T) acc[2 * pt + T] = mfma_f16(a[T][0], b[pt][1], acc[2 * pt + T]);
+    const uint4 as0 = f16x8_scale2048(a[0][0]), as1 = f16x8_scale2048(a[1][0]);
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      acc[2 * pt] = mfma_f16(as0, b[pt][0], acc[2 * pt]);
+      acc[2 * pt + 1] = mfma_f16(as1, b[pt][0], acc[2 * pt + 1]);
+    }
+    h2q_load(a, rs, voff, t + kX3D);   // packs carry kX3D zero steps
+  };
+  int t = 0;
+#pragma unroll 1
+  for (; t + kX3D <= nsteps; t += kX3D) {
+#pragma unroll
+    for (int d = 0; d < kX3D; ++d) step(w.a[d], t + d);
+  }
+#pragma unroll
+  for (int d = 0; d < kX3D - 1; ++d)
+    if (t + d < nsteps) step(w.a[d], t + d);
+}
+
+// max |v| over this wave's accumulators into slot (one float per wave; NaN as +inf)
+__device__ __forceinline__ void wave_tile_absmax(const f32x16 (&acc)[4], float* slot) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float a = fabsf(acc[i][r]);
+      m = a != a ? __builtin_inff() : fmaxf(m, a);
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) *slot = m;
+}
+
+// the tile's X factor xs = 2^e (max |X| xs in [2^13, 2^14), e <= 126) from the
+// four waves' maxima; 1 for an all-zero or non-finite tile
+__device__ __forceinline__ float tile_xscale(const float* slots) {
+  const float m = fmaxf(fmaxf(slots[0], slots[1]), fmaxf(slots[2], slots[3]));
+  if (!(m > 0.f) || !(m <= 3.0e38f)) return 1.f;
+  int E;
+  (void)frexpf(m, &E);   // m = f 2^E, f in [0.5, 1)
+  return ldexpf(1.f, min(14 - E, 126));
+}
+
+// acc = acc / xs * ws (two steps: each factor alone stays in the normal range)
+__device__ __forceinline__ void h2q_unscale(f32x16 (&acc)[4], float xs, float ws) {
+  const float xu = 1.f / xs;   // exact: xs is a power of two
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = (acc[i][r] * xu) * ws;
+}
+
+
+// V = 0: native fp32 dX GEMMs; 1: fp32x3 (split bf16); 2: fp32h2 (split f16,
+// per-tile power-of-two scaling of X).  V >= 1 leaves the block3.0 extras to a
+// separate pass.
+template <int V>
 __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
+  constexpr bool X3 = V != 0;
   extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
   float* X = lds_dyn;                   // quad rows [66][kQP]
   float* dotp = X + 66 * kQP;           // [4][64] partial <d_hid, h4> per wave
-  float* exP = dotp + 4 * kTP;          // [4][7][64] partial block3.0 extras gradients
+  float* exP = dotp + 4 * kTP;          // [4][7][64] partial block3.0 extras gradients (V == 0)
+  float* tmx = exP;                     // [4] per-wave max |X| of the layer input (V == 2)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int j = lane >> 3;
@@ -1076,8 +1192,9 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
   const float* w3t = X3 ? nullptr : A.wb.w3t + T0 * 64;
   const float* w2t = X3 ? nullptr : A.wb.w2t + T0 * 64;
   float ring[kQD][kNTW];
-  const int xvoff = (T0 * 3 * 64 + lane) * 16;
+  const int xvoff = (T0 * (V == 2 ? 2 : 3) * 64 + lane) * 16;
   const __amdgpu_buffer_rsrc_t x4 = x3q_rsrc(A.wx[0]), x3 = x3q_rsrc(A.wx[1]), x2 = x3q_rsrc(A.wx[2]);
+  const float ws4 = V == 2 ? A.wxs[0] : 1.f, ws3 = V == 2 ? A.wxs[1] : 1.f, ws2 = V == 2 ? A.wxs[2] : 1.f;
   if constexpr (!X3) prime_q<kNTW>(ring, w4t, lane);
   // max |dz1..dz4|, |dpa| of this workgroup (pnr_agg_saved.dz_absmax: pnr_gemm_tn_h2's scales)
   __shared__ unsigned amx[5];
@@ -1141,6 +1258,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     }
     lrelu_bwd_q<kNTW, kPTW>(acc, A.sv.h4, A.dz[3], tile, n, slope, lane, T0, am ? am + 3 : nullptr);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
+    if constexpr (V == 2) wave_tile_absmax(acc, tmx + wid);
     __syncthreads();
     // d wt_k = d alpha_s a_k + <d f_s, h4_k>  ->  d conf_k (straight-through clamp, :724-726)
     if (wid == 0 && active && A.d_conf) {
@@ -1156,7 +1274,11 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     unsigned mk[kPTW * kNTW];
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 2, tile, n, lane, T0);
-    if constexpr (X3) {
+    if constexpr (V == 2) {
+      const float xs = tile_xscale(tmx);
+      mlp_layer_h2q(acc, x4, xvoff, X, 16, lane, xs);
+      h2q_unscale(acc, xs, ws4);
+    } else if constexpr (X3) {
       mlp_layer_x3q(acc, x4, xvoff, X, 16, lane);
     } else {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w4t, X, 128, lane);
@@ -1165,6 +1287,7 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     __syncthreads();
     lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[2], tile, n, slope, lane, T0, am ? am + 2 : nullptr);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
+    if constexpr (V == 2) wave_tile_absmax(acc, tmx + wid);
     // block3.0 extras (inputs 256..262): d x3e_e = sum_n W3[n, 256 + e] dz3[n];
     // wave w reads back its own 64 dz3 rows (quad rows 16w..16w+15), lane = pair
     wave_sync();
@@ -1229,7 +1352,11 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 1, tile, n, lane, T0);
-    if constexpr (X3) {
+    if constexpr (V == 2) {
+      const float xs = tile_xscale(tmx);
+      mlp_layer_h2q(acc, x3, xvoff, X, 16, lane, xs);
+      h2q_unscale(acc, xs, ws3);
+    } else if constexpr (X3) {
       mlp_layer_x3q(acc, x3, xvoff, X, 16, lane);
     } else {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w3t, X, 128, lane);
@@ -1238,12 +1365,17 @@ __global__ void __launch_bounds__(64 * kPairWaves, 2) k_pairs_bwd(BwdArgs A) {
     __syncthreads();
     lrelu_bwd_m<kNTW, kPTW>(acc, mk, A.dz[1], tile, n, slope, lane, T0, am ? am + 1 : nullptr);
     store_q<kNTW, kPTW>(acc, X, lane, T0);
+    if constexpr (V == 2) wave_tile_absmax(acc, tmx + wid);
     __syncthreads();
     // ---------------------------------------------------------- block1.2^T: dh1 = W2^T dz2
 #pragma unroll
     for (int i = 0; i < kPTW * kNTW; ++i) acc[i] = (f32x16){0.f};
     load_masks<kNTW, kPTW>(mk, A.sv.mask, 0, tile, n, lane, T0);
-    if constexpr (X3) {
+    if constexpr (V == 2) {
+      const float xs = tile_xscale(tmx);
+      mlp_layer_h2q(acc, x2, xvoff, X, 16, lane, xs);
+      h2q_unscale(acc, xs, ws2);
+    } else if constexpr (X3) {
       mlp_layer_x3q(acc, x2, xvoff, X, 16, lane);
     } else {
       mlp_layer_q<kNTW, kPTW>(acc, ring, w2t, X, 128, lane);
@@ -2068,13 +2200,18 @@ extern "C" int pnr_aggregate_fwd_train_masked(const pnr_points* pts, const pnr_s
 }
 
 static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w, const pnr_mlp_bwd* wb,
-                     const pnr_mlp_bwd_x3* wbx, const pnr_agg_saved* saved, const float* d_feat,
+                     const pnr_mlp_bwd_x3* wbx, const pnr_mlp_bwd_h2* wbh, const pnr_agg_saved* saved,
+                     const float* d_feat,
                      const float* d_hid, float* dz1, float* dz2, float* dz3, float* dz4, float* dpa, float* d_p1,
                      float* d_color, float* d_dir, float* d_conf, void* stream) {
   int rc;
   PNR_CHECK_ARG(pts && s && w && wb, "aggregate_bwd: null pointer");
   if ((rc = check_saved(saved))) return rc;
-  PNR_CHECK_ARG((wb->w3e || wbx) && w->wa && (wbx || (wb->w4t && wb->w3t && wb->w2t)), "aggregate_bwd: null weight");
+  PNR_CHECK_ARG((wb->w3e || wbx || wbh) && w->wa && (wbx || wbh || (wb->w4t && wb->w3t && wb->w2t)),
+                "aggregate_bwd: null weight");
+  PNR_CHECK_ARG(!wbh || (wbh->w4th && wbh->w3th && wbh->w2th && wbh->scale &&
+                         (((uintptr_t)wbh->w4th | (uintptr_t)wbh->w3th | (uintptr_t)wbh->w2th) & 15) == 0),
+                "aggregate_bwd_h2: null or unaligned split weight pack");
   PNR_CHECK_ARG(!wbx || (wbx->w4tx && wbx->w3tx && wbx->w2tx &&
                          (((uintptr_t)wbx->w4tx | (uintptr_t)wbx->w3tx | (uintptr_t)wbx->w2tx) & 15) == 0),
                 "aggregate_bwd_x3: null or unaligned split weight pack");
@@ -2087,9 +2224,11 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
   hipStream_t st = as_stream(stream);
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<false>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<0>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBwdLdsBytes));
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<true>),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBwdLdsBytes));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pairs_bwd<2>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBwdLdsBytes));
     attr = true;
   }
@@ -2110,20 +2249,25 @@ static int bwd_pairs(const pnr_points* pts, const pnr_samples* s, const pnr_mlp*
   a.d_color = d_color;
   a.d_dir = d_dir;
   a.d_conf = d_conf;
-  a.wx[0] = wbx ? wbx->w4tx : nullptr;
-  a.wx[1] = wbx ? wbx->w3tx : nullptr;
-  a.wx[2] = wbx ? wbx->w2tx : nullptr;
+  a.wx[0] = wbx ? wbx->w4tx : (wbh ? wbh->w4th : nullptr);
+  a.wx[1] = wbx ? wbx->w3tx : (wbh ? wbh->w3th : nullptr);
+  a.wx[2] = wbx ? wbx->w2tx : (wbh ? wbh->w2th : nullptr);
+  a.wxs = wbh ? wbh->scale : nullptr;
   const int64_t tiles = cdiv(s->n_max, kTS);
-  if (wbx) {
-    hipLaunchKernelGGL(k_pairs_bwd<true>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
-                       st, a);
+  if (wbx || wbh) {
+    if (wbh)
+      hipLaunchKernelGGL(k_pairs_bwd<2>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
+                         st, a);
+    else
+      hipLaunchKernelGGL(k_pairs_bwd<1>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
+                         st, a);
     PNR_LAUNCH_CHECK();
     // wb->w3e == NULL: the caller runs the extras per point inside
     // pnr_pairs_to_points_ex (no float atomics, coalesced dz3 rows)
     if ((d_color || d_dir) && wb->w3e)
       hipLaunchKernelGGL(k_extras_bwd, dim3(grid_for(cdiv(s->n_max * kKN, 64), 4, 2048)), dim3(256), 0, st, a);
   } else
-    hipLaunchKernelGGL(k_pairs_bwd<false>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
+    hipLaunchKernelGGL(k_pairs_bwd<0>, dim3(grid_for(tiles, 1, 256 * 2)), dim3(64 * kPairWaves), kBwdLdsBytes,
                        st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
@@ -2134,8 +2278,8 @@ extern "C" int pnr_aggregate_bwd_pairs(const pnr_points* pts, const pnr_samples*
                                        const float* d_feat, const float* d_hid, float* dz1, float* dz2,
                                        float* dz3, float* dz4, float* dpa, float* d_p1, float* d_color,
                                        float* d_dir, float* d_conf, void* stream) {
-  return bwd_pairs(pts, s, w, wb, nullptr, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
-                   d_conf, stream);
+  return bwd_pairs(pts, s, w, wb, nullptr, nullptr, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color,
+                   d_dir, d_conf, stream);
 }
 
 extern "C" int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
@@ -2144,7 +2288,17 @@ extern "C" int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_sampl
                                           float* dz1, float* dz2, float* dz3, float* dz4, float* dpa, float* d_p1,
                                           float* d_color, float* d_dir, float* d_conf, void* stream) {
   PNR_CHECK_ARG(wbx, "aggregate_bwd_x3: null split weight packs");
-  return bwd_pairs(pts, s, w, wb, wbx, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
+  return bwd_pairs(pts, s, w, wb, wbx, nullptr, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
+                   d_conf, stream);
+}
+
+extern "C" int pnr_aggregate_bwd_pairs_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
+                                          const pnr_mlp_bwd* wb, const pnr_mlp_bwd_h2* wbh,
+                                          const pnr_agg_saved* saved, const float* d_feat, const float* d_hid,
+                                          float* dz1, float* dz2, float* dz3, float* dz4, float* dpa, float* d_p1,
+                                          float* d_color, float* d_dir, float* d_conf, void* stream) {
+  PNR_CHECK_ARG(wbh, "aggregate_bwd_h2: null split weight packs");
+  return bwd_pairs(pts, s, w, wb, nullptr, wbh, saved, d_feat, d_hid, dz1, dz2, dz3, dz4, dpa, d_p1, d_color, d_dir,
                    d_conf, stream);
 }
 

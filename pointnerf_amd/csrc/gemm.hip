@@ -37,7 +37,6 @@ struct GemmArgs {
   int colsum;
   const uint32_t* a_absmax;   // h2: bits of max |A| (pnr_absmax), picks A's power-of-two scale
   int32_t* range_flag;        // h2: set when a scaled operand leaves the f16 split's range
-  const int32_t* run_if;      // x3: run only when *run_if != 0 (the h2 call's guarded fallback)
 };
 
 template <int NT>
@@ -150,9 +149,12 @@ constexpr int kXPitch = 24;             // bf16 per LDS line (16 k + 8 pad)
 constexpr int kXPlane = 256 * kXPitch;  // bf16 per plane (256 rows)
 constexpr size_t kXLds = 2 * 2 * 3 * (size_t)kXPlane * 2;   // [buf][A|B][plane] = 144 KB
 
-__global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
-  if (g.run_if && *g.run_if == 0) return;   // guarded fallback of an h2 call whose operands fit
-  extern __shared__ __attribute__((aligned(16))) uint16_t glds[];
+// One K split of the x3 product; plane(buf, p) is the LDS address of split
+// plane p (0..2: A, 3..5: B) of staging buffer buf, red a 1-KB LDS scratch for
+// the column sums.  Shared by k_gemm_tn_x3_part and k_gemm_tn_h2_part's
+// in-place fallback (which lays the twelve planes over its own LDS).
+template <class Plane>
+__device__ __forceinline__ void tn_x3_split(const GemmArgs& g, Plane plane, float* red) {
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
   const int64_t k_begin = (int64_t)blockIdx.x * g.kchunk;
   const int64_t k_end = k_begin + g.kchunk < g.K ? k_begin + g.kchunk : g.K;
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
     }
   };
   auto put = [&](int buf, const float (&va)[8], const float (&vb)[8]) {
-    uint16_t* base = glds + (size_t)buf * 6 * kXPlane + col * kXPitch + 8 * kh;
+    const int off = col * kXPitch + 8 * kh;
     uint4 pa[3], pb[3];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -189,8 +191,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
     }
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      *reinterpret_cast<uint4*>(base + p * kXPlane) = pa[p];
-      *reinterpret_cast<uint4*>(base + (3 + p) * kXPlane) = pb[p];
+      *reinterpret_cast<uint4*>(plane(buf, p) + off) = pa[p];
+      *reinterpret_cast<uint4*>(plane(buf, 3 + p) + off) = pb[p];
     }
   };
   f32x16 acc[2][4];
@@ -200,13 +202,13 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x16){0.f};
   const int mt0 = 2 * (wid & 3), nt0 = 4 * (wid >> 2);
   auto compute = [&](int buf) {
-    const uint16_t* lb = glds + (size_t)buf * 6 * kXPlane + c * kXPitch + 8 * h;
+    const int off = c * kXPitch + 8 * h;
     uint4 a[2][3];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        a[mi][p] = *reinterpret_cast<const uint4*>(lb + p * kXPlane + 32 * (mt0 + mi) * kXPitch);
+        a[mi][p] = *reinterpret_cast<const uint4*>(plane(buf, p) + off + 32 * (mt0 + mi) * kXPitch);
     // per N tile: its B planes, then the six products of both M tiles, smallest
     // terms first (A2B0, A1B1, A0B2, A1B0, A0B1, A0B0)
     constexpr int kPa[6] = {2, 1, 0, 1, 0, 0}, kPb[6] = {0, 1, 2, 0, 1, 0};
@@ -216,7 +218,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
       uint4 b[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        b[p] = *reinterpret_cast<const uint4*>(lb + (3 + p) * kXPlane + 32 * (nt0 + ni) * kXPitch);
+        b[p] = *reinterpret_cast<const uint4*>(plane(buf, 3 + p) + off + 32 * (nt0 + ni) * kXPitch);
 #pragma unroll
       for (int e = 0; e < 6; ++e)
 #pragma unroll
@@ -256,12 +258,17 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
       for (int r = 0; r < 16; ++r) out[(int64_t)(m0 + (r & 3) + 8 * (r >> 2) + 4 * h) * g.N + n0 + c] = acc[mi][ni][r];
     }
   if (g.colsum) {   // column sums of A: the two k-halves of every column
-    float* red = reinterpret_cast<float*>(glds);
     __syncthreads();
     if (kh == 1) red[col] = csum;
     __syncthreads();
     if (kh == 0 && stA) out[(int64_t)g.M * g.N + col] = csum + red[col];
   }
+}
+
+__global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t glds[];
+  tn_x3_split(g, [&](int buf, int p) { return glds + (size_t)(buf * 6 + p) * kXPlane; },
+              reinterpret_cast<float*>(glds));
 }
 
 // ---------------------------------------------------------------- h2 variant
@@ -274,8 +281,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_x3_part(GemmArgs g) {
 // -- three v_mfma_f32_32x32x16_f16 per 16 k-rows instead of x3's six bf16
 // products.  2^11 Ah is exact in f16 (|Ah| < 8).  The dropped 2^-22 Al^T Bl and
 // the split residuals are <= ~2^-21 |a b| per product.  Operands outside the
-// split's range (|B| >= 2^15, a stale max, non-finite) raise range_flag: the
-// caller launches the x3 kernel behind this one with run_if = range_flag.
+// split's range (|B| >= 2^15, a stale max, non-finite) raise range_flag, and
+// the workgroups that saw them redo their split on the x3 path in place
+// (tn_x3_split over this kernel's LDS): no second launch.
 //
 // Staging: the raw fp32 rows of a 16-row chunk (A and B, one <= 1-KB row per
 // wave instruction) go global -> LDS by buffer_load ... lds (no VGPRs), three
@@ -290,6 +298,8 @@ constexpr int kHRawRow = 1024;                        // bytes per staged row (2
 constexpr int kHRawSlot = 2 * kXK * kHRawRow;         // A rows then B rows: 32 KB
 constexpr int kHSlots = 3;
 constexpr size_t kHPlanes = 4 * (size_t)kXPlane * 2;  // Ah, Al, Bh, Bl: 48 KB
+// the in-place x3 fallback's twelve planes: four over the h2 planes, eight over raw
+static_assert(kHSlots * kHRawSlot == 8 * kXPlane * 2 && kHPlanes == 4 * (size_t)kXPlane * 2, "x3 fallback LDS map");
 
 __device__ __forceinline__ void hw_barrier_lds() {
   asm volatile("" ::: "memory");
@@ -437,7 +447,6 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_h2_part(GemmArgs g) {
     hw_barrier_lds();   // every wave is done reading the planes
   }
   wait_vm<0>();
-  if (bad) atomicOr(g.range_flag, 1);   // outside the split's range, or NaN / inf
   const float unscale = ldexpf(1.f, -(e + 11));   // exact: a power of two
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -455,6 +464,21 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tn_h2_part(GemmArgs g) {
     if (kh == 1) red[col] = csum;
     __syncthreads();
     if (kh == 0 && stA) out[(int64_t)g.M * g.N + col] = csum + red[col];
+  }
+  // written first so that no accumulator is live below
+  if (__syncthreads_or(bad)) {
+    // an operand of this split outside the f16 split's range (or NaN / inf): the
+    // split again on the exact x3 path, in place -- its twelve planes laid over
+    // this kernel's LDS (buffer 0 in raw[0 .. 6 planes), buffer 1 in glds' four
+    // planes + raw's last two) -- overwriting this split's partial; the other
+    // splits keep their h2 partials
+    if (tid == 0) atomicOr(g.range_flag, 1);
+    uint16_t* r16 = reinterpret_cast<uint16_t*>(raw);
+    tn_x3_split(g,
+                [&](int buf, int p) {
+                  return buf == 0 ? r16 + p * kXPlane : (p < 4 ? glds + p * kXPlane : r16 + (p + 2) * kXPlane);
+                },
+                reinterpret_cast<float*>(glds));
   }
 }
 
@@ -540,8 +564,11 @@ __global__ void k_reduce_splits(const float* __restrict__ part, int64_t n4, int 
 
 // Last level: c[i] = sum_g part[g][i] (float4 lanes) straight into the caller's
 // C (first nc4 lanes) and column sums (the rest; skipped when cs == NULL).
+// C [M, N] as rows of ldc floats of which the first ncols are written (a slice
+// of a wider gradient: ldc != N or ncols < N -> scalar stores).
 __global__ void k_reduce_final(const float* __restrict__ part, int64_t n4, int nsplit, int64_t nc4,
-                               float* __restrict__ c, float* __restrict__ cs) {
+                               float* __restrict__ c, float* __restrict__ cs, int nq, int64_t ldc, int ncols) {
+  const bool dense = ldc == 4 * nq && ncols == 4 * nq;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     if (i >= nc4 && cs == nullptr) break;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -552,8 +579,19 @@ __global__ void k_reduce_final(const float* __restrict__ part, int64_t n4, int n
       acc.z += v.z;
       acc.w += v.w;
     }
-    if (i < nc4) reinterpret_cast<float4*>(c)[i] = acc;
-    else reinterpret_cast<float4*>(cs)[i - nc4] = acc;
+    if (i >= nc4) {
+      reinterpret_cast<float4*>(cs)[i - nc4] = acc;
+    } else if (dense) {
+      reinterpret_cast<float4*>(c)[i] = acc;
+    } else {
+      const int64_t row = i / nq;
+      const int c0 = 4 * (int)(i - row * nq);
+      float* o = c + row * ldc + c0;
+      if (c0 < ncols) o[0] = acc.x;
+      if (c0 + 1 < ncols) o[1] = acc.y;
+      if (c0 + 2 < ncols) o[2] = acc.z;
+      if (c0 + 3 < ncols) o[3] = acc.w;
+    }
   }
 }
 
@@ -567,7 +605,7 @@ static void gemm_plan(int64_t K, int* nsplit, int64_t* kchunk) {
   *nsplit = (int)(K > 0 ? cdiv(K, kc) : 1);
 }
 
-static size_t gemm_scratch(int64_t K, int M, int N) {
+size_t gemm_scratch(int64_t K, int M, int N) {
   int ns;
   int64_t kc;
   gemm_plan(K, &ns, &kc);
@@ -605,21 +643,38 @@ struct GemmNNArgs {
   float slope;
   const uint32_t* a_absmax;   // h2: bits of max |A|
   int32_t* range_flag;        // h2: operand outside the f16 split's range
+  uint32_t* c_absmax;         // optional: max |C| folded in (float bits, atomic; pre-zeroed)
   const int32_t* run_if;      // fp32: run only when *run_if != 0 (the h2 call's fallback)
 };
 
+// max |v| of this thread's values into *word, one atomic per workgroup (NaN above inf)
+__device__ __forceinline__ void block_absmax_to(uint32_t* word, unsigned mb, unsigned* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mb;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mb = max(mb, red[w]);
+    if (mb) atomicMax(word, mb);
+  }
+}
+
+__device__ __forceinline__ unsigned abs_bits(float v) {
+  const float a = fabsf(v);
+  return a != a ? 0x7fc00000u : __float_as_uint(a);
+}
+
+// The fp32 product of rows row0 .. row0 + 32 WM (k_gemm_nn's body): as / bs the
+// LDS staging (32 WM x kNPitch and kNBMax floats).
 template <int NT, int WM>
-__global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
-  if (g.run_if && *g.run_if == 0) return;   // guarded fallback of an h2 call whose operands fit
+__device__ __forceinline__ void nn_fp32_rows(const GemmNNArgs& g, int64_t row0, float* as, float* bs) {
   constexpr int WN = 8 / WM;               // waves along N
   constexpr int NW = (NT + WN - 1) / WN;   // column tiles per wave (at most)
   constexpr int ROWS = 32 * WM;
   constexpr int AV = ROWS * kNK / 512;     // staged A floats per thread
   constexpr int BV = kNK * 32 * NT / 512;  // staged B floats per thread
-  __shared__ float as[ROWS * kNPitch];
-  __shared__ float bs[kNBMax];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, c = lane & 31, h = lane >> 5;
-  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const int wm = wid % WM, wn = wid / WM;
   const int N = 32 * NT;
   const int bp = N % 64 == 0 ? N + 32 : N;   // B pitch in LDS
@@ -672,6 +727,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
     }
   }
   // C/D layout: row = (r&3) + 8(r>>2) + 4h, col = c
+  unsigned mb = 0u;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t m = row0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -684,8 +740,18 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
       float v = acc[u][r];
       if (g.act != nullptr && !(g.act[m * g.ld_act + n] > 0.f)) v *= g.slope;
       g.C[m * g.ldc + n] = v;
+      mb = max(mb, abs_bits(v));
     }
   }
+  if (g.c_absmax) block_absmax_to(g.c_absmax, mb, reinterpret_cast<unsigned*>(as));
+}
+
+template <int NT, int WM>
+__global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
+  if (g.run_if && *g.run_if == 0) return;   // guarded fallback of an h2 call whose operands fit
+  __shared__ float as[32 * WM * kNPitch];
+  __shared__ float bs[kNBMax];
+  nn_fp32_rows<NT, WM>(g, (int64_t)blockIdx.x * 32 * WM, as, bs);
 }
 
 // h2 variant (pnr_gemm_nn_h2): the same C = A B (x LeakyReLU derivative) on
@@ -697,7 +763,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn(GemmNNArgs g) {
 // ([row][k]) and B's columns ([n][k], the transpose staged on the fly) are split
 // into two f16 planes each, double-buffered in LDS (2 x 37 KB).  Out-of-range
 // operands (|B| >= 2^15, a stale max, NaN / inf) raise range_flag; the caller
-// launches the fp32 kernel behind it with run_if = range_flag.
+// launches the fp32 kernel behind it with run_if = range_flag.  (Redoing the
+// flagged rows in place, as k_gemm_tn_h2_part does, made these kernels ~10 %
+// slower: the fp32 body's registers and 4 spills at 128 VGPRs.)
 constexpr int kNHRows = 128;
 constexpr int kNHPlaneA = kNHRows * kXPitch;   // f16 per A plane
 constexpr int kNHPlaneB = 256 * kXPitch;       // f16 per B plane
@@ -799,8 +867,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
     if (more) put(buf ^ 1);
     __syncthreads();
   }
-  if (bad) atomicOr(g.range_flag, 1);
   const float unscale = ldexpf(1.f, -(e + 11));
+  unsigned mb = 0u;
   // C/D layout: row = (r&3) + 8(r>>2) + 4h (the A rows), col = c
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -814,8 +882,14 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
       float v = acc[u][r] * unscale;
       if (g.act != nullptr && !(g.act[m * g.ld_act + n] > 0.f)) v *= g.slope;
       g.C[m * g.ldc + n] = v;
+      mb = max(mb, abs_bits(v));
     }
   }
+  if (bad) atomicOr(g.range_flag, 1);
+  // (on a raised flag the fp32 kernel behind this one rewrites C and folds its
+  // own max in: the word may then hold the discarded values' max too -- only
+  // ever larger, a valid scale for its consumer)
+  if (g.c_absmax) block_absmax_to(g.c_absmax, mb, reinterpret_cast<unsigned*>(nlds));
 }
 
 template <int NT>
@@ -832,13 +906,51 @@ static void launch_gemm_nn(const GemmNNArgs& g, hipStream_t st) {
   }
 }
 
+// The colour branch's first backward product input in one pass
+// (pnr_color_dz): dz[r][c] = lrelu'(hc[r][c]) (d_feat[r][1 + c] * (vmask[r] != 0)),
+// the torch ops' arithmetic (where(h > 0, x, x * slope) of x = d_feat * vm),
+// and max |dz| folded into *absmax (float bits, NaN as 0x7fc00000 > inf).
+__global__ void __launch_bounds__(256) k_color_dz(const float* __restrict__ d_feat, int64_t ldf,
+                                                  const int32_t* __restrict__ vmask, const float* __restrict__ hc,
+                                                  int64_t ldh, int64_t n, int C, float slope, float* __restrict__ dz,
+                                                  uint32_t* __restrict__ absmax) {
+  __shared__ unsigned red[4];
+  unsigned mb = 0u;
+  const int c4n = C >> 2;   // float4 columns per row (C % 4 == 0, hc / dz rows 16-B aligned)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * c4n; i += stride) {
+    const int64_t r = i / c4n;
+    const int c = 4 * (int)(i - r * c4n);
+    const float vm = vmask[r] != 0 ? 1.f : 0.f;
+    const float* f = d_feat + r * ldf + 1 + c;
+    const float4 h = *reinterpret_cast<const float4*>(hc + r * ldh + c);
+    const float x0 = f[0] * vm, x1 = f[1] * vm, x2 = f[2] * vm, x3 = f[3] * vm;
+    const float4 d = make_float4(h.x > 0.f ? x0 : x0 * slope, h.y > 0.f ? x1 : x1 * slope,
+                                 h.z > 0.f ? x2 : x2 * slope, h.w > 0.f ? x3 : x3 * slope);
+    *reinterpret_cast<float4*>(dz + r * C + c) = d;
+    const float a[4] = {fabsf(d.x), fabsf(d.y), fabsf(d.z), fabsf(d.w)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mb = max(mb, a[q] != a[q] ? 0x7fc00000u : __float_as_uint(a[q]));
+  }
+  if (absmax) {   // one atomic per workgroup
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      mb = max(max(red[0], red[1]), max(red[2], red[3]));
+      if (mb) atomicMax(absmax, mb);
+    }
+  }
+}
+
 }  // namespace pnr
 
 using namespace pnr;
 
-static int gemm_nn_impl(bool h2, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
-                        int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
-                        const uint32_t* a_absmax, int32_t* range_flag, void* stream) {
+int pnr::gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
+                     int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
+                     const uint32_t* a_absmax, int32_t* range_flag, uint32_t* c_absmax, void* stream) {
   PNR_CHECK_ARG(M == 0 || (A && B && C), "gemm_nn: null pointer");
   PNR_CHECK_ARG(M >= 0 && K > 0 && N > 0 && N % 32 == 0 && N <= 32 * kGMaxNT, "gemm_nn: N must be a multiple of 32 "
                 "in [32, 256], K > 0");
@@ -859,6 +971,7 @@ static int gemm_nn_impl(bool h2, const float* A, int64_t lda, const float* B, in
   g.slope = slope;
   g.a_absmax = a_absmax;
   g.range_flag = range_flag;
+  g.c_absmax = c_absmax;
   g.run_if = nullptr;
   hipStream_t st = as_stream(stream);
   if (h2) {
@@ -903,14 +1016,15 @@ static int gemm_nn_impl(bool h2, const float* A, int64_t lda, const float* B, in
 extern "C" int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
                            int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
                            void* stream) {
-  return gemm_nn_impl(false, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, nullptr, nullptr, stream);
+  return gemm_nn_run(false, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, nullptr, nullptr, nullptr, stream);
 }
 
 extern "C" int pnr_gemm_nn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
                               int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
                               const uint32_t* a_absmax, int32_t* range_flag, void* stream) {
   PNR_CHECK_ARG(a_absmax && range_flag, "gemm_nn_h2: a_absmax and range_flag required");
-  return gemm_nn_impl(true, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, a_absmax, range_flag, stream);
+  return gemm_nn_run(true, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, a_absmax, range_flag, nullptr,
+                     stream);
 }
 
 
@@ -920,20 +1034,23 @@ extern "C" int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t
   return PNR_OK;
 }
 
-static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
-                        int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes, void* stream,
-                        const uint32_t* a_absmax = nullptr, int32_t* range_flag = nullptr) {
+int pnr::gemm_tn_run(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M, int32_t N,
+                float* C, int64_t ldc, int32_t ncols, float* colsum_a, void* scratch, size_t scratch_bytes,
+                void* stream, const uint32_t* a_absmax, int32_t* range_flag) {
   const bool x3 = mode == 1, h2 = mode == 2;
   PNR_CHECK_ARG(C && scratch && (K == 0 || (A && B)), "gemm_tn: null pointer");
+  PNR_CHECK_ARG(ncols >= 1 && ncols <= N && ldc >= ncols, "gemm_tn: bad output slice (ldc %lld, ncols %d)",
+                (long long)ldc, ncols);
   PNR_CHECK_ARG(M > 0 && N > 0 && M % 32 == 0 && N % 32 == 0 && M <= 32 * kGWaves && N <= 32 * kGMaxNT,
                 "gemm_tn: M, N must be multiples of 32 in [32, 256]");
   PNR_CHECK_ARG(lda >= M && ldb >= N && K >= 0, "gemm_tn: bad leading dimensions");
-  PNR_CHECK_ARG(((uintptr_t)scratch & 15) == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)colsum_a & 15) == 0,
+  PNR_CHECK_ARG(((uintptr_t)scratch & 15) == 0 && ((ldc == N && ncols == N) ? ((uintptr_t)C & 15) == 0 : true) &&
+                    ((uintptr_t)colsum_a & 15) == 0,
                 "gemm_tn: 16-B aligned scratch, C and colsum_a required");
   PNR_CHECK_ARG(scratch_bytes >= gemm_scratch(K, M, N), "gemm_tn: scratch too small");
   hipStream_t st = as_stream(stream);
   if (K == 0) {
-    PNR_HIP(hipMemsetAsync(C, 0, (size_t)M * N * sizeof(float), st));
+    PNR_HIP(hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)ncols * sizeof(float), (size_t)M, st));
     if (colsum_a) PNR_HIP(hipMemsetAsync(colsum_a, 0, (size_t)M * sizeof(float), st));
     return PNR_OK;
   }
@@ -953,7 +1070,6 @@ static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, i
   g.colsum = colsum_a != nullptr;
   g.a_absmax = a_absmax;
   g.range_flag = range_flag;
-  g.run_if = nullptr;
   static bool attr = false;
   if (!attr && (x3 || h2)) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_x3_part),
@@ -962,9 +1078,6 @@ static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, i
   }
   if (h2) {
     hipLaunchKernelGGL(k_gemm_tn_h2_part, dim3(ns), dim3(512), 0, st, g);
-    PNR_LAUNCH_CHECK();
-    g.run_if = range_flag;   // the x3 kernel redoes the partials only when the flag is up
-    hipLaunchKernelGGL(k_gemm_tn_x3_part, dim3(ns), dim3(512), kXLds, st, g);
   } else if (x3) {
     hipLaunchKernelGGL(k_gemm_tn_x3_part, dim3(ns), dim3(512), kXLds, st, g);
   } else {
@@ -980,7 +1093,7 @@ static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, i
                      lvl1);
   PNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_reduce_final, dim3(grid_for(n4, 256, 256)), dim3(256), 0, st, lvl1, n4, ngrp,
-                     (int64_t)M * N / 4, C, colsum_a);
+                     (int64_t)M * N / 4, C, colsum_a, N / 4, ldc, ncols);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
@@ -988,21 +1101,34 @@ static int gemm_tn_impl(int mode, const float* A, int64_t lda, const float* B, i
 extern "C" int pnr_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
                            int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
                            void* stream) {
-  return gemm_tn_impl(0, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
+  return gemm_tn_run(0, A, lda, B, ldb, K, M, N, C, N, N, colsum_a, scratch, scratch_bytes, stream, nullptr, nullptr);
 }
 
 extern "C" int pnr_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
                               int32_t N, float* C, float* colsum_a, void* scratch, size_t scratch_bytes,
                               void* stream) {
-  return gemm_tn_impl(1, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream);
+  return gemm_tn_run(1, A, lda, B, ldb, K, M, N, C, N, N, colsum_a, scratch, scratch_bytes, stream, nullptr, nullptr);
 }
 
 extern "C" int pnr_gemm_tn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K, int32_t M,
                               int32_t N, float* C, float* colsum_a, const uint32_t* a_absmax, int32_t* range_flag,
                               void* scratch, size_t scratch_bytes, void* stream) {
   PNR_CHECK_ARG(a_absmax && range_flag, "gemm_tn_h2: a_absmax and range_flag required");
-  return gemm_tn_impl(2, A, lda, B, ldb, K, M, N, C, colsum_a, scratch, scratch_bytes, stream, a_absmax,
-                      range_flag);
+  return gemm_tn_run(2, A, lda, B, ldb, K, M, N, C, N, N, colsum_a, scratch, scratch_bytes, stream, a_absmax,
+                     range_flag);
+}
+
+extern "C" int pnr_color_dz(const float* d_feat, int64_t ld_feat, const int32_t* vmask, const float* hc, int64_t ld_hc,
+                            int64_t n, int32_t C, float slope, float* dz, uint32_t* absmax, void* stream) {
+  PNR_CHECK_ARG(n >= 0 && C >= 4 && C % 4 == 0 && ld_feat >= C + 1 && ld_hc >= C && ld_hc % 4 == 0 &&
+                    (n == 0 || (d_feat && vmask && hc && dz)),
+                "color_dz: bad args (n %lld, C %d, ld_hc %lld)", (long long)n, C, (long long)ld_hc);
+  PNR_CHECK_ARG((((uintptr_t)hc | (uintptr_t)dz) & 15) == 0, "color_dz: hc and dz must be 16-B aligned");
+  if (n == 0) return PNR_OK;
+  hipLaunchKernelGGL(k_color_dz, dim3(grid_for(n * (C / 4), 256, 256)), dim3(256), 0, as_stream(stream), d_feat,
+                     ld_feat, vmask, hc, ld_hc, n, C, slope, dz, absmax);
+  PNR_LAUNCH_CHECK();
+  return PNR_OK;
 }
 
 extern "C" int pnr_absmax_scratch_floats(int64_t* out) {

@@ -40,6 +40,14 @@ from .aggregator import frag_pack, frag_pack_x3
 # pnr_pairs_to_points_ex (True, the product).  False hands them to
 # pnr_aggregate_bwd_pairs_x3 (k_extras_bwd) -- DESIGN.md section 10.
 X3_POINT_EXTRAS = True
+# fp32h2 training: the backward's three dX GEMMs (k_pairs_bwd) on split-f16 MFMA
+# as well (False: on fp32x3, the round-5 product) -- DESIGN.md section 10.
+BWD_H2 = True
+# fp32h2 training with a used-point list (the renderer's training forward): the
+# whole backward through the aggregator as one native call
+# (pnr_aggregate_bwd_step_h2) instead of the Python sequence below -- the same
+# kernels, ~60 fewer host-side calls per step.
+NATIVE_BWD = True
 
 _PARAM_NAMES = ("block1.0.weight", "block1.0.bias", "block1.2.weight", "block1.2.bias",
                 "block3.0.weight", "block3.0.bias", "block3.2.weight", "block3.2.bias",
@@ -53,14 +61,35 @@ def agg_params(agg) -> list:
     return [d[n] for n in _PARAM_NAMES]
 
 
-def packed_bwd(agg, x3: bool = False):
+BWD_H2_PAD = 3   # k_pairs_bwd<2> loads 3 k-steps ahead (kX3D)
+
+
+def packed_bwd(agg, x3: bool = False, h2: bool = False):
     """Transposed fragment packs for the backward GEMMs: (pnr_mlp_bwd, None, keep)
-    with native-fp32 packs, or (pnr_mlp_bwd with w3e only, pnr_mlp_bwd_x3, keep)
-    with split-bf16 packs (frag_pack_x3) for pnr_aggregate_bwd_pairs_x3."""
+    with native-fp32 packs, (pnr_mlp_bwd with w3e only, pnr_mlp_bwd_x3, keep)
+    with split-bf16 packs (frag_pack_x3) for pnr_aggregate_bwd_pairs_x3, or (same,
+    pnr_mlp_bwd_h2, keep) with the split-f16 packs of pnr_pack_bwd_h2 (one launch,
+    shifts picked on the device) for pnr_aggregate_bwd_pairs_h2."""
     with torch.no_grad():
         W3 = agg.block3[0].weight
-        mats = dict(w4t=agg.block3[2].weight.t(), w3t=W3[:, :256].t(), w2t=agg.block1[2].weight.t())
         t = dict(w3e=W3[:, 256:263].float().contiguous())
+        if h2:
+            dev = W3.device
+            w4, w2 = agg.block3[2].weight.float().contiguous(), agg.block1[2].weight.float().contiguous()
+            w3 = W3.float()
+            if w3.stride(1) != 1:
+                w3 = w3.contiguous()
+            per = (16 + BWD_H2_PAD) * 2048
+            t["packs"] = torch.empty(3 * per * 2, dtype=torch.int32, device=dev)   # 3 x per x 8 B
+            t["scale"] = torch.empty(4, dtype=torch.float32, device=dev)
+            L.check(L.lib().pnr_pack_bwd_h2(L.ptr(w4), L.ptr(w3), w3.stride(0), L.ptr(w2), BWD_H2_PAD,
+                                            L.ptr(t["scale"]), L.ptr(t["packs"]), t["packs"].numel() * 4,
+                                            L.stream_ptr(dev)), "pnr_pack_bwd_h2")
+            t.update(w4=w4, w3=w3, w2=w2)
+            base = t["packs"].data_ptr()
+            m = L.MlpBwd(None, None, None, t["w3e"].data_ptr())
+            return m, L.MlpBwdH2(base, base + per * 8, base + 2 * per * 8, t["scale"].data_ptr()), t
+        mats = dict(w4t=agg.block3[2].weight.t(), w3t=W3[:, :256].t(), w2t=agg.block1[2].weight.t())
         if x3:
             t.update({k + "x": frag_pack_x3(v) for k, v in mats.items()})
         else:
@@ -137,10 +166,6 @@ def used_points(pidx: torch.Tensor, n_points: int):
     return used, used_map
 
 
-def _lrelu_grad(dy, h, slope):
-    return torch.where(h > 0, dy, dy * slope)
-
-
 class AggSpec:
     """Non-tensor description of one aggregate call (structs + keep-alive)."""
 
@@ -186,15 +211,19 @@ class AggregateFn(torch.autograd.Function):
             if len(spec.used) > 2:   # device count: used.numel() is the capacity
                 pts.n_used_dev = spec.used[2].data_ptr()
             n_p1 = used.numel()
+        run_h2 = spec.pair_mask is None and spec.h2
+        if run_h2:
+            # an earlier step's raised flag (its fallback already ran): shifts re-picked now
+            spec.h2_fallback = agg.h2_train_poll()
+        # every pack of the step in one launch (the optimizer changed the weights)
+        agg.packed_train(h2=run_h2)
         mlp, keepw = agg.packed()
         sv = Saved(n_max, dev, n_dev=s.n_dev)
         feat = _rows_zeroed((max(n_max, 1), 129), s.n_dev, dev)
         scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
         keepx = None
         run_x3 = spec.pair_mask is None and spec.x3
-        if spec.pair_mask is None and spec.h2:
-            # an earlier step's raised flag (its fallback already ran): shifts re-picked now
-            spec.h2_fallback = agg.h2_train_poll()
+        if run_h2:
             wh, keepx = agg.packed_h2_train()
             L.check(L.lib().pnr_aggregate_fwd_train_h2_guarded(
                 ctypes.byref(pts), ctypes.byref(s), ctypes.byref(mlp), ctypes.byref(wh), ctypes.byref(sv.c),
@@ -245,11 +274,13 @@ class AggregateFn(torch.autograd.Function):
         N = ctx.tabs[0].shape[0]
         slope = float(agg.neg_slope)
         d_feat = d_feat.contiguous()
+        xyz_grad = ctx.xyz_shape is not None and ctx.needs_input_grad[5]
+        if (NATIVE_BWD and spec.h2 and BWD_H2 and X3_POINT_EXTRAS and used_list is not None and not xyz_grad
+                and spec.pair_mask is None):
+            return _native_bwd_h2(ctx, spec, d_feat, n, used_list.numel(), params)
         f32 = dict(dtype=torch.float32, device=dev)
         grads = {}
         # ---- colour branch (color_branch.{0,2,4}: 280 -> 128 -> 128 -> 128, LeakyReLU each)
-        vm = (sv["vmask"][:n] != 0).float()[:, None]
-        dc = d_feat[:n, 1:] * vm
         hc1, hc2, hc3 = sv["hc1"][:n], sv["hc2"][:n], sv["hc3"][:n]
         # weight gradients dW = dZ^T X on pnr_gemm_tn_x3 (bias = column sums); the
         # dX = dZ W products with the LeakyReLU derivative fused on pnr_gemm_nn.
@@ -260,8 +291,11 @@ class AggregateFn(torch.autograd.Function):
         def amax(t):
             return hg.absmax(t) if hg is not None and t.shape[0] > 0 else None
 
-        dz = _lrelu_grad(dc, hc3, slope).contiguous()
-        am = amax(dz)
+        # dz = lrelu'(hc3) (d_feat[:, 1:] * vmask) and its max |.| in one pass
+        dz = torch.empty((n, 128), **f32)
+        am = hg.words[1:2] if hg is not None and n > 0 else None
+        L.check(L.lib().pnr_color_dz(L.ptr(d_feat), d_feat.stride(0), L.ptr(sv["vmask"]), L.ptr(hc3), hc3.stride(0),
+                                     n, 128, slope, L.ptr(dz), L.ptr(am), L.stream_ptr(dev)), "pnr_color_dz")
         grads["color_branch.4.weight"], grads["color_branch.4.bias"] = L.gemm_tn(
             dz, hc2.contiguous(), colsum=True, h2=hg, a_absmax=am)
         dz = L.gemm_nn(dz, P["color_branch.4.weight"], act=hc2, slope=slope, h2=hg, a_absmax=am)
@@ -291,7 +325,9 @@ class AggregateFn(torch.autograd.Function):
         d_color = torch.zeros((N, 3), **f32) if has_c else None
         d_dir = torch.zeros((N, 3), **f32) if has_d else None
         d_conf = torch.zeros(N, **f32) if has_f else None
-        wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3)
+        # fp32h2: the dX chain on split-f16 MFMA too (pnr_aggregate_bwd_pairs_h2)
+        bwd_h2 = spec.h2 and BWD_H2
+        wb, wbx, _keepb = packed_bwd(agg, x3=spec.x3 and not bwd_h2, h2=bwd_h2)
         point_extras = wbx is not None and (has_c or has_d) and X3_POINT_EXTRAS
         if point_extras:
             # the block3.0 extras' colour / dir gradients: per point inside
@@ -302,7 +338,11 @@ class AggregateFn(torch.autograd.Function):
         # (pairs sorted by point: no atomics, deterministic) instead of the kernel's atomics
         bufs = (L.ptr(d_feat), L.ptr(d_hid), L.ptr(dz1), L.ptr(dz2), L.ptr(dz3), L.ptr(dz4), L.ptr(dpa),
                 None, L.ptr(d_color), L.ptr(d_dir), L.ptr(d_conf), L.stream_ptr(dev))
-        if wbx is not None:
+        if bwd_h2:
+            L.check(L.lib().pnr_aggregate_bwd_pairs_h2(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                                       ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(wbx),
+                                                       ctypes.byref(sv.c), *bufs), "pnr_aggregate_bwd_pairs_h2")
+        elif wbx is not None:
             L.check(L.lib().pnr_aggregate_bwd_pairs_x3(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
                                                        ctypes.byref(ctx.mlp), ctypes.byref(wb), ctypes.byref(wbx),
                                                        ctypes.byref(sv.c), *bufs), "pnr_aggregate_bwd_pairs_x3")
@@ -313,9 +353,9 @@ class AggregateFn(torch.autograd.Function):
         m = n * 8
         # weight gradients on f16 MFMA (pnr_gemm_tn_h2, hg above) with the fp32h2
         # forward; fp32x3 keeps the bf16x3 GEMMs
-        prow_sorted, pair_of = torch.sort(sv["prow"][:m], stable=True)
-        pair_of = pair_of.to(torch.int32)
         used_map = None if spec.used is None else spec.used[1]
+        # the pairs grouped by point in pair order (torch.sort(prow, stable=True) natively)
+        prow_sorted, pair_of = L.group_pairs(sv["prow"][:m], used_map, n_p1 if used_map is not None else N)
         if point_extras:
             g_pair = torch.empty((max(m, 1), 8), **f32)
             L.check(L.lib().pnr_aggregate_bwd_extras_rows(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
@@ -386,6 +426,40 @@ class AggregateFn(torch.autograd.Function):
         out = [None, d_emb.view(emb_shape), d_color, d_dir, None if d_conf is None else d_conf.view(conf_shape), d_xyz]
         out += [grads[k] for k in _PARAM_NAMES]
         return tuple(out)
+
+
+def _native_bwd_h2(ctx, spec, d_feat, n: int, n_used: int, params) -> tuple:
+    """AggregateFn.backward for fp32h2 through pnr_aggregate_bwd_step_h2: every
+    gradient in one host call (outputs allocated here, written by the step)."""
+    dev = d_feat.device
+    N = ctx.tabs[0].shape[0]
+    f32 = dict(dtype=torch.float32, device=dev)
+    prm, out = L.AggParams(), L.AggGrads()
+    grads = []
+    for i, p in enumerate(params):
+        if p.dtype != torch.float32 or not p.is_contiguous():
+            raise L.PnrError(f"native backward: parameter {_PARAM_NAMES[i]} must be contiguous fp32")
+        prm.p[i] = p.data_ptr()
+        grads.append(torch.empty(p.shape, **f32))
+        out.g[i] = grads[-1].data_ptr()
+    has_c, has_d, has_f = ctx.has
+    d_emb = torch.empty((N, 32), **f32)
+    d_color = torch.empty((N, 3), **f32) if has_c else None
+    d_dir = torch.empty((N, 3), **f32) if has_d else None
+    d_conf = torch.empty(N, **f32) if has_f else None
+    out.d_emb, out.d_color, out.d_dir, out.d_conf = (None if t is None else t.data_ptr()
+                                                     for t in (d_emb, d_color, d_dir, d_conf))
+    nb = L.c_size_t(0)
+    L.check(L.lib().pnr_aggregate_bwd_step_h2_scratch_bytes(n, n_used, ctypes.byref(nb)),
+            "pnr_aggregate_bwd_step_h2_scratch_bytes")
+    scratch = torch.empty(max(int(nb.value), 256), dtype=torch.uint8, device=dev)
+    L.check(L.lib().pnr_aggregate_bwd_step_h2(ctypes.byref(ctx.pts), ctypes.byref(spec.samples),
+                                              ctypes.byref(ctx.mlp), ctypes.byref(prm), ctypes.byref(ctx.sv.c),
+                                              L.ptr(d_feat), n, n_used, ctypes.byref(out), L.ptr(scratch),
+                                              scratch.numel(), L.stream_ptr(dev)), "pnr_aggregate_bwd_step_h2")
+    emb_shape, conf_shape = ctx.shapes
+    return (None, d_emb.view(emb_shape), d_color, d_dir, None if d_conf is None else d_conf.view(conf_shape),
+            None, *grads)
 
 
 class RgbHeadFn(torch.autograd.Function):

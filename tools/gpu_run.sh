@@ -38,6 +38,18 @@ for s in $STEPS; do
     qpmc)   # query kernel stats + PMC passes (tools/prof_query.sh), QCONFIG
       bash tools/prof_query.sh $(basename $O)/qpmc || exit 1
       python tools/pmc_fold.py $O/qpmc k_knn k_march > $O/qpmc_fold.json; cat $O/qpmc_fold.json | head -60 ;;
+    abvar)   # A/B: product libpnr vs tools/_var/libpnr_$VAR.so on tools/agg_bench.py (AB_ARGS), two rounds
+      for rnd in 1 2; do for L in pointnerf_amd/libpnr.so tools/_var/libpnr_${VAR}.so; do
+        PNR_LIB=$PWD/$L timeout -k 10 300 python tools/agg_bench.py $AB_ARGS >> $O/ab.jsonl 2>> $O/ab.err \
+          || { tail -20 $O/ab.err; exit 1; }
+      done; done
+      python -c "import json; [print(d['lib'][-28:], d['stages_ms'], d['checksum']) for d in map(json.loads, open('$O/ab.jsonl'))]" ;;
+    adamab)   # A/B of Adam variants: product libpnr vs tools/_var/libpnr_$VAR.so on tools/adam_bench.py, two rounds
+      for rnd in 1 2; do for L in pointnerf_amd/libpnr.so tools/_var/libpnr_${VAR}.so; do
+        PNR_LIB=$PWD/$L timeout -k 10 120 python tools/adam_bench.py >> $O/adam.jsonl 2>> $O/adam.err \
+          || { tail -20 $O/adam.err; exit 1; }
+      done; done
+      cat $O/adam.jsonl ;;
     launch)   # bench.py --gpus 2 self-launch rehearsal: two ranks on the box's one GPU over gloo
       PNR_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 > $O/launch2.json \
         2> $O/launch2.err || { tail -20 $O/launch2.err; exit 1; }
@@ -62,7 +74,13 @@ for s in $STEPS; do
         || { tail -20 $O/train.err; exit 1; }
       timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 --train-precision fp32x3 > $O/train_x3.json \
         2> $O/train_x3.err || { tail -20 $O/train_x3.err; exit 1; }
-      cut -c1-400 $O/train.json $O/train_x3.json ;;
+      cut -c1-400 $O/train.json $O/train_x3.json
+      python -c "import json; [print(f, {k: d.get(k) for k in ('ms_per_step', 'host_issue_ms_per_step', 'host_phase_ms_per_step')}) for f in ('$O/train.json', '$O/train_x3.json') for d in [json.loads(open(f).read().strip().splitlines()[-1])]]" ;;
+    trainhost)   # host-side profile of the training step (cProfile; the step is bound by its host issue)
+      timeout -k 10 300 python -m cProfile -o $O/train.prof bench.py --mode train --steps 30 --warmup 5 \
+        --train-precision ${TP:-fp32h2} > $O/trainhost.json 2> $O/trainhost.err || { tail -20 $O/trainhost.err; exit 1; }
+      python -c "import pstats; s = pstats.Stats('$O/train.prof'); s.sort_stats('tottime').print_stats(45); s.sort_stats('cumtime').print_stats(60)" > $O/trainhost.txt
+      head -70 $O/trainhost.txt ;;
     trainprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trstats -o run -- \
         python bench.py --mode train --steps 20 --warmup 3 --train-precision ${TP:-fp32h2} > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
