@@ -57,7 +57,7 @@ extern "C" {
 /* libpnr.so is built with -fvisibility=hidden: only the declarations below are exported. */
 #pragma GCC visibility push(default)
 
-#define PNR_ABI_VERSION 22
+#define PNR_ABI_VERSION 23
 
 enum {
   PNR_OK = 0,
@@ -452,6 +452,10 @@ typedef struct {
   uint32_t* dz_absmax; /* optional [5]: pnr_aggregate_bwd_pairs(_x3) max-es |dz1..dz4| and
                       |dpa| into it (float bits, atomic; the caller zeroes it): the scales
                       of pnr_gemm_tn_h2 without a pnr_absmax pass (ABI 19)               */
+  float* x1;       /* optional [>= n_used][224] (ABI 23): block1.0's point-half inputs
+                      [emb, PE_3(emb)] of the used points, written by the fp32h2 training
+                      forward's k_point_pre_h2 (its angle-doubled PE) and read by the
+                      backward's block1.0 weight gradient instead of a recomputation   */
 } pnr_agg_saved;
 
 /* Transposed weights for the backward GEMMs, fragment-packed like pnr_mlp
@@ -476,8 +480,9 @@ int pnr_aggregate_fwd_train_x3(const pnr_points* pts, const pnr_samples* s, cons
 /* pnr_aggregate_fwd_train with the per-pair chain on the fp32h2 kernel of
  * pnr_aggregate_fwd_h2 (k_pairs_h2 + the same saves; wh's w1bh / w2h / w3h / w4h
  * packs and scales, and w1ah / scale1a when set: P1 on k_point_pre_h2, else on
- * fp32 MFMA; the colour packs are unused: the colour branch runs the fp32
- * training kernel), the range flag as pnr_aggregate_fwd_h2: set when an
+ * fp32 MFMA; with wc1a..wc3h / cscale set (ABI 22) the colour branch runs on
+ * f16-split MFMA too, k_color_h2 with k_color<train>'s saves (vpe, hc1..hc3),
+ * else on the fp32 training kernel), the range flag as pnr_aggregate_fwd_h2: set when an
  * activation left the f16 range, the caller then re-runs the step on
  * pnr_aggregate_fwd_train_x3).  Saved layout and outputs as the fp32 call. */
 int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_mlp* w,
@@ -486,7 +491,8 @@ int pnr_aggregate_fwd_train_h2(const pnr_points* pts, const pnr_samples* s, cons
                                void* stream);
 /* pnr_aggregate_fwd_train_h2 with its fallback on the device (v17): after the h2
  * chain, k_point_pre (when P1 ran on fp32h2) and the native-fp32 k_pairs<train>
- * are launched over the same outputs and saves, and each workgroup returns at
+ * (and, with the colour packs, the fp32 colour branch) are launched over the
+ * same outputs and saves, and each workgroup returns at
  * once unless *wh->range_flag != 0 -- so a raised flag never needs a host read
  * inside the step (the caller reads it later, asynchronously, to re-pick the
  * shifts).  wh->range_flag is required.  Outputs: those of the h2 call when the
@@ -604,7 +610,7 @@ int pnr_aggregate_bwd_pairs_x3(const pnr_points* pts, const pnr_samples* s, cons
  * step): job q is pnr_pack_weights(kind, ...) for kind 0 / 1 and
  * pnr_pack_weights_h2(..., shift, range_flag, ...) for kind 2 (shift and
  * range_flag ignored otherwise), same layouts, bitwise the same outputs;
- * 1 <= n <= 16. */
+ * 1 <= n <= 24. */
 typedef struct {
   int32_t kind;
   const float* W; int64_t ld_row; int64_t ld_col;

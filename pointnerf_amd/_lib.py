@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PNR_LIB", os.path.join(_HERE, "libpnr.so"))
 c_int, c_int8, c_int32, c_int64 = ctypes.c_int, ctypes.c_int8, ctypes.c_int32, ctypes.c_int64
 c_float, c_size_t, c_void_p = ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 PNR_OK, PNR_EINVAL, PNR_EOVERFLOW, PNR_EHIP, PNR_ENOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 22
+ABI_VERSION = 23
 FEAT_H_PITCH = 136   # PNR_FEAT_H_PITCH: uint16 per bf16 feature row (pnr_aggregate_fwd_bf16_hf)
 HEAD_BWD_BLOCKS = 512   # PNR_HEAD_BWD_BLOCKS (include/pnr.h)
 
@@ -118,7 +118,7 @@ class CompositeParams(ctypes.Structure):
 
 class AggSaved(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("h1", "h2", "h3", "h4", "pe5", "x3e", "pa", "wt", "wn", "prow", "hid",
-                                        "vpe", "hc1", "hc2", "hc3", "vmask", "mask", "dz_absmax")]
+                                        "vpe", "hc1", "hc2", "hc3", "vmask", "mask", "dz_absmax", "x1")]
 
 
 class MlpX3(ctypes.Structure):

@@ -202,6 +202,9 @@ def frag_pack_x3(W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Ten
 
 
 H2_PAD = 8        # >= the weight ring depth of k_pairs_h2 / k_color_h2 (WRing::kWD)
+# fp32h2 training: the colour branch on k_color_h2<true> (f16-split MFMA, k_color<true>'s
+# saves) instead of the fp32 training kernel
+H2_TRAIN_COLOR = True
 H2_WMAX = 16.0    # |W 2^-s| < 16, so 2^11 Wh (made in registers) stays inside f16
 
 
@@ -471,16 +474,24 @@ class PointAggregator(nn.Module):
         return self._set_packedh2t(packs, key)
 
     def _h2t_mats(self) -> list:
-        b1, b3 = self.block1, self.block3
-        return [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None),
-                (b1[0].weight[:, :224], b1[0].bias)]   # the last: block1.0's point half (k_point_pre_h2)
+        b1, b3, cb = self.block1, self.block3, self.color_branch
+        mats = [(b1[0].weight[:, 224:], None), (b1[2].weight, None), (b3[0].weight, b3[0].bias), (b3[2].weight, None),
+                (b1[0].weight[:, :224], b1[0].bias)]   # then: block1.0's point half (k_point_pre_h2)
+        if H2_TRAIN_COLOR:   # the colour branch (k_color_h2<true>): layer 1 in two halves of one shift
+            mats += [(cb[0].weight[:, :144], None), (cb[0].weight[:, 144:], cb[0].bias), (cb[2].weight, cb[2].bias),
+                     (cb[4].weight, cb[4].bias)]
+        return mats
 
     def _h2t_prepare(self, mats) -> torch.Tensor:
         """The training packs' shifts (picked on the host once, kept until a raised
         range flag) and their device flag."""
-        if getattr(self, "_h2t_shifts", None) is None:
+        if getattr(self, "_h2t_shifts", None) is None or len(self._h2t_shifts) != len(mats):
             with torch.no_grad():
-                self._h2t_shifts = [h2_shift(W, b) for W, b in mats]
+                self._h2t_shifts = [h2_shift(W, b) for W, b in mats[:5]]
+                if len(mats) > 5:
+                    cb = self.color_branch
+                    s1 = h2_shift(cb[0].weight, cb[0].bias)   # one scale for both halves of layer 1
+                    self._h2t_shifts += [s1, s1] + [h2_shift(W, b) for W, b in mats[7:]]
             self._h2t_flag = torch.zeros(1, dtype=torch.int32, device=self.block1[0].weight.device)
         return self._h2t_flag
 
@@ -488,9 +499,13 @@ class PointAggregator(nn.Module):
         flag = self._h2t_flag
         t = dict(w1bh=packs[0], w2h=packs[1], w3h=packs[2], w4h=packs[3], w1ah=packs[4], range_flag=flag)
         sc = [2.0 ** (s - 11) for s in self._h2t_shifts]
+        if len(packs) > 5:
+            t.update(wc1a=packs[5], wc1b=packs[6], wc2h=packs[7], wc3h=packs[8])
+            cp, cs = [t[k].data_ptr() for k in ("wc1a", "wc1b", "wc2h", "wc3h")], (sc[6], sc[7], sc[8])
+        else:
+            cp, cs = [None] * 4, (0.0, 0.0, 0.0)
         m = L.MlpH2(*(t[k].data_ptr() for k in ("w1bh", "w2h", "w3h", "w4h")),
-                    (L.c_float * 4)(*sc[:4]), flag.data_ptr(),
-                    None, None, None, None, (L.c_float * 3)(0.0, 0.0, 0.0), t["w1ah"].data_ptr(), sc[4])
+                    (L.c_float * 4)(*sc[:4]), flag.data_ptr(), *cp, (L.c_float * 3)(*cs), t["w1ah"].data_ptr(), sc[4])
         self._packedh2t, self._packedh2t_key = (m, t), key
         return self._packedh2t
 

@@ -183,9 +183,14 @@ int gemm_tn_run(int mode, const float* A, int64_t lda, const float* B, int64_t l
                 void* stream, const uint32_t* a_absmax, int32_t* range_flag);
 // C = A B (x LeakyReLU derivative) on fp32 / fp32h2 (pnr_gemm_nn*), max |C| folded
 // into c_absmax when given (pre-zeroed): the next h2 product's scale, no pnr_absmax pass.
+// b_split (h2, optional): B pre-split by nn_b_split (the same weights for every
+// row block: split once per call instead of per workgroup and chunk).
 int gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K, int32_t N,
                 const float* act, int64_t ld_act, float slope, float* C, int64_t ldc, const uint32_t* a_absmax,
-                int32_t* range_flag, uint32_t* c_absmax, void* stream);
+                int32_t* range_flag, uint32_t* c_absmax, void* stream, const void* b_split = nullptr);
+size_t nn_b_split_bytes(int K, int N);
+int nn_b_split(int n, const float* const* B, const int64_t* ldb, const int* K, const int* N, void* const* out,
+               int32_t* flag, void* stream);
 
 // aggregate_x3.hip: the pairs stage of pnr_aggregate_fwd_x3 (H = false: 3-way
 // bf16 split, six products) and pnr_aggregate_fwd_h2 (H = true: 2-way f16
@@ -203,8 +208,9 @@ int launch_pairs_split(const pnr_points& pts, const pnr_samples& s, const pnr_ml
                        float* out_conf, int32_t* tile_ctr, hipStream_t st, const pnr_agg_saved* sv = nullptr);
 // k_point_pre_h2 (aggregate_x3.hip): P1 = W1[:, :224].[emb, PE_3(emb)] + b1 on
 // f16-split MFMA (pack: frag_pack_h2 of W1[:, :224] with b1).
+// x1 (training, optional): the input rows [emb, PE_3(emb)] are written there too
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
-                        hipStream_t st);
+                        hipStream_t st, float* x1 = nullptr);
 // Workgroup barrier for an LDS hand-off only: lgkmcnt(0) + s_barrier between
 // LDS-scoped fences, so the compiler keeps LDS accesses on their side while
 // global loads stay in flight across it (__syncthreads' fence drains them with
@@ -256,8 +262,10 @@ __device__ __forceinline__ float xork_sum_nc(float v) {
 
 // k_color_h2 (aggregate_x3.hip): the colour branch on f16-split MFMA; pack =
 // color_branch.0 columns 0..143 / 144..279 + bias, color_branch.2, .4 (+ bias).
+// train: the training forward (hid from its fp32 rows, saves vpe / hc1..hc3 as
+// k_color<true> does); NULL: inference (hid planes from k_pairs_h2).
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
                     int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st,
-                    const float* rw2c_pp);
+                    const float* rw2c_pp, const pnr_agg_saved* train = nullptr);
 
 }  // namespace pnr

@@ -1700,7 +1700,7 @@ __global__ void __launch_bounds__(256) k_extras_rows(BwdArgs A, float* __restric
     float g[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (pr >= 0) {
       const float4* z4 = reinterpret_cast<const float4*>(A.dz[2] + pair * kHid);
-#pragma unroll 4
+#pragma unroll   // all 16 row pieces in flight (4 at a time: 90 us for 242 MB of dz3)
       for (int j = 0; j < kHid / 16; ++j) {
         const int c4 = 4 * j + q;   // float4 column: neurons 4 c4 .. 4 c4 + 3
         const float4 z = z4[c4];
@@ -2139,7 +2139,8 @@ static int fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_m
   if (wh->w1ah) {
     PNR_CHECK_ARG(((uintptr_t)wh->w1ah & 15) == 0 && wh->scale1a > 0.f && wh->scale1a < 1e30f,
                   "aggregate_train_h2: bad block1.0 point-half pack");
-    if ((rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a, wh->range_flag, a.p1, st))) return rc;
+    PNR_CHECK_ARG(((uintptr_t)saved->x1 & 15) == 0, "aggregate_train_h2: saved x1 must be 16-B aligned");
+    if ((rc = launch_point_pre_h2(a.pts, wh->w1ah, wh->scale1a, wh->range_flag, a.p1, st, saved->x1))) return rc;
   } else if ((rc = launch_t<false>(a, st, kStagePre))) {
     return rc;
   }
@@ -2154,6 +2155,22 @@ static int fwd_train_h2(const pnr_points* pts, const pnr_samples* s, const pnr_m
     f.run_if = wh->range_flag;
     f.pts.p1_ready = wh->w1ah ? 0 : 1;   // P1 again on fp32 when k_point_pre_h2 made it
     if ((rc = launch_t<true>(f, st, kStagePre | kStagePairs))) return rc;
+  }
+  if (wh->wc1a && wh->wc1b && wh->wc2h && wh->wc3h) {
+    // the colour branch on f16-split MFMA too (k_color_h2<true>: the same saves as
+    // k_color<true>), its fp32 rerun behind it when the flag is up (guarded)
+    PNR_CHECK_ARG((((uintptr_t)wh->wc1a | (uintptr_t)wh->wc1b | (uintptr_t)wh->wc2h | (uintptr_t)wh->wc3h) & 15) == 0,
+                  "aggregate_train_h2: colour packs must be 16-B aligned");
+    for (int i = 0; i < 3; ++i)
+      PNR_CHECK_ARG(wh->cscale[i] > 0.f && wh->cscale[i] < 1e30f, "aggregate_train_h2: bad colour scale %d", i);
+    const void* cp[4] = {wh->wc1a, wh->wc1b, wh->wc2h, wh->wc3h};
+    if ((rc = launch_color_h2(a.s, a.w, cp, wh->cscale, wh->range_flag, saved->hid, a.vmask, out_feat, st,
+                              a.pts.rw2c, saved)))
+      return rc;
+    if (!guarded) return PNR_OK;
+    AggArgs f = a;
+    f.run_if = wh->range_flag;
+    return launch_t<true>(f, st, kStageColor);
   }
   return launch_t<true>(a, st, kStageColor);
 }

@@ -1069,6 +1069,11 @@ struct ColH2Args {
   const int32_t* vmask;
   float* out_feat;
   const float* rw2c_pp;   // pnr_points.rw2c (per-point Rw2c) or NULL
+  // training (k_color_h2<true>): hid as fp32 rows [n][256] (k_pairs_h2_train's),
+  // and the saves of k_color<true>: vpe [n][24], hc1..hc3 [n][128] post-activation
+  const float* hid_rows;
+  float* vpe;
+  float* hc[3];
 };
 
 // hid row groups [G0, G0 + NG) of the tile's 64 samples (both planes) ->
@@ -1086,6 +1091,48 @@ __device__ __forceinline__ void color_load_hid(const ColH2Args& A, char* lds, in
   }
 }
 
+// training: hid row groups [G0, G0 + NG) of the tile's 64 samples from fp32 rows,
+// split into the planes here (wave w: groups w, w + 2, ...; lane = sample;
+// samples past n read as zeros)
+template <int G0, int NG>
+__device__ __forceinline__ void color_split_hid(const ColH2Args& A, char* lds, int64_t tile, int64_t n) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t v = tile * kXT + lane;
+  const bool ok = v < n;
+  const float4* src = reinterpret_cast<const float4*>(A.hid_rows + (ok ? v : 0) * kHid);
+#pragma unroll
+  for (int gg = 0; gg < (NG + 1) / 2; ++gg) {
+    const int g = 2 * gg + wid;
+    if (g >= NG) break;
+    const float4 a = ok ? src[2 * (G0 + g)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b = ok ? src[2 * (G0 + g) + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float g8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    store_group<true>(lds, kCPlane, g, lane, g8);
+  }
+}
+
+// training saves: lrelu(scale acc) rows [v][128] of the tile's samples v < n
+// (acc[2 pt + T]: sample 32 pt + c, neurons 32 (T0 + T) + 8 q + 4 h + i)
+__device__ __forceinline__ void save_act_rows(const f32x16 (&acc)[4], float* dst, int64_t v0, int64_t n, float neg,
+                                              float scale, int lane, int T0) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) {
+    const int64_t v = v0 + 32 * pt + c;
+    if (v >= n) continue;
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16& a = acc[2 * pt + T];
+        *reinterpret_cast<float4*>(dst + v * kC + 32 * (T0 + T) + 8 * q + 4 * h) =
+            make_float4(lrelu(a[4 * q] * scale, neg), lrelu(a[4 * q + 1] * scale, neg),
+                        lrelu(a[4 * q + 2] * scale, neg), lrelu(a[4 * q + 3] * scale, neg));
+      }
+  }
+}
+
+template <bool TR>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) k_color_h2(ColH2Args A) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1108,7 +1155,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int64_t v0 = tile * kXT;
     const uint64_t vm = __ballot(v0 + lane < n && A.vmask[v0 + lane] != 0);   // sample validity, one load
     // ---------------------------------------------------- layer 1, input rows 0..143 (hid)
-    color_load_hid<0, kCG>(A, lds, tile);
+    if constexpr (TR) color_split_hid<0, kCG>(A, lds, tile, n);
+    else color_load_hid<0, kCG>(A, lds, tile);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = (f32x16){0.f};
@@ -1116,7 +1164,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r1b, voff);
     __syncthreads();
     // ---------------------------------------------------- rows 144..255 (hid), 256..279 (view PE), 280 (bias)
-    color_load_hid<kCG, 14>(A, lds, tile);
+    if constexpr (TR) color_split_hid<kCG, 14>(A, lds, tile, n);
+    else color_load_hid<kCG, 14>(A, lds, tile);
     if (wid == 0) {   // lane = sample: PE_4 of the rotated view direction (k_color's order)
       const int64_t v = v0 + lane;
       float vrot[3] = {0.f, 0.f, 0.f};
@@ -1137,6 +1186,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
           pe[4 * ch + f] = sn;
           pe[12 + 4 * ch + f] = cs;
         }
+      if (TR && v < n) {   // vpe[v] = rows 256..279 (k_color<true>'s order)
+#pragma unroll
+        for (int i = 0; i < 24; ++i) A.vpe[v * 24 + i] = pe[i];
+      }
       pe[24] = 1.f;
 #pragma unroll
       for (int i = 25; i < 32; ++i) pe[i] = 0.f;
@@ -1154,6 +1207,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     // ---------------------------------------------------- layer 2
     // (layers 2 and 3: accumulators start at bias / scale, as block1.2 / 3.2 in
     // k_pairs_h2: 8 k-steps, the packs' bias step and the bias input row unused)
+    if (TR) save_act_rows(acc, A.hc[0], v0, n, neg, A.scale[0], lane, T0);
     store_act<true>(acc, lds, neg, A.scale[0], lane, T0, kCPlane);
     acc_init<true>(acc, A.w.bc2, 1.f / A.scale[1], lane, T0);
     __syncthreads();
@@ -1161,6 +1215,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r3, voff);
     __syncthreads();
     // ---------------------------------------------------- layer 3
+    if (TR) save_act_rows(acc, A.hc[1], v0, n, neg, A.scale[1], lane, T0);
     store_act<true>(acc, lds, neg, A.scale[1], lane, T0, kCPlane);
     acc_init<true>(acc, A.w.bc3, 1.f / A.scale[2], lane, T0);
     __syncthreads();
@@ -1168,6 +1223,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
     prime<true, 4>(wr, r1a, voff);   // the next tile
     // out_feat[v, 1 + 32 (T0 + T) + row] (valid samples only; the others keep their zeros)
     const float sc3 = A.scale[2];
+    if (TR) save_act_rows(acc, A.hc[2], v0, n, neg, sc3, lane, T0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)   // valid columns only: the others hold stale plane data
       if ((vm >> (32 * (i >> 1) + c)) & 1)
@@ -1219,6 +1275,7 @@ struct P1H2Args {
   float scale;
   int32_t* range_flag;
   float* p1;
+  float* x1;            // training (optional): the input rows [emb, PE_3] [np][224] (pnr_agg_saved.x1)
 };
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_point_pre_h2(P1H2Args A) {
@@ -1247,6 +1304,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w; e[4] = b.x; e[5] = b.y; e[6] = b.z; e[7] = b.w;
       }
       store_group<true>(lds, kP1Plane, wid, lane, e);
+      if (A.x1 && act) {   // training: this wave's emb channels of the input row
+        float4* xr = reinterpret_cast<float4*>(A.x1 + pt * 224 + 8 * wid);
+        xr[0] = make_float4(e[0], e[1], e[2], e[3]);
+        xr[1] = make_float4(e[4], e[5], e[6], e[7]);
+      }
       float pe[48];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {   // networks.py:175-190 order: rows 32 + 6c + {s0, c0, s1, c1, s2, c2}
@@ -1262,6 +1324,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         const float g8[8] = {pe[8 * g], pe[8 * g + 1], pe[8 * g + 2], pe[8 * g + 3],
                              pe[8 * g + 4], pe[8 * g + 5], pe[8 * g + 6], pe[8 * g + 7]};
         store_group<true>(lds, kP1Plane, 4 + 6 * wid + g, lane, g8);
+      }
+      if (A.x1 && act) {   // ... and their PE rows 32 + 48 wid .. + 47
+        float4* xr = reinterpret_cast<float4*>(A.x1 + pt * 224 + 32 + 48 * wid);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) xr[q] = make_float4(pe[4 * q], pe[4 * q + 1], pe[4 * q + 2], pe[4 * q + 3]);
       }
       if (wid == 0) {   // row 224 = 1 (bias column), 225..239 = 0
         const float one[8] = {1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1298,7 +1365,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 }  // namespace
 
 int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, int32_t* range_flag, float* p1,
-                        hipStream_t st) {
+                        hipStream_t st, float* x1) {
   static bool attr = false;
   if (!attr) {
     PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_point_pre_h2),
@@ -1311,6 +1378,7 @@ int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, in
   a.scale = scale;
   a.range_flag = range_flag;
   a.p1 = p1;
+  a.x1 = x1;
   const int64_t np = pts.used ? pts.n_used : pts.n;
   hipLaunchKernelGGL(k_point_pre_h2, dim3(grid_for(cdiv(np, kXT), 1, 256 * 2)), dim3(256), kP1H2Lds, st, a);
   PNR_LAUNCH_CHECK();
@@ -1319,10 +1387,12 @@ int launch_point_pre_h2(const pnr_points& pts, const void* pack, float scale, in
 
 int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pack[4], const float scale[3],
                     int32_t* range_flag, const float* hid, const int32_t* vmask, float* out_feat, hipStream_t st,
-                    const float* rw2c_pp) {
+                    const float* rw2c_pp, const pnr_agg_saved* train) {
   static bool attr = false;
   if (!attr) {
-    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_h2),
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_h2<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kColH2Lds));
+    PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_color_h2<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kColH2Lds));
     attr = true;
   }
@@ -1336,7 +1406,14 @@ int launch_color_h2(const pnr_samples& s, const pnr_mlp& w, const void* const pa
   a.vmask = vmask;
   a.out_feat = out_feat;
   a.rw2c_pp = rw2c_pp;
-  hipLaunchKernelGGL(k_color_h2, dim3(grid_for(cdiv(s.n_max, kXT), 1, 256 * 4)), dim3(128), kColH2Lds, st, a);
+  a.hid_rows = train ? train->hid : nullptr;
+  a.vpe = train ? train->vpe : nullptr;
+  a.hc[0] = train ? train->hc1 : nullptr;
+  a.hc[1] = train ? train->hc2 : nullptr;
+  a.hc[2] = train ? train->hc3 : nullptr;
+  const dim3 grid(grid_for(cdiv(s.n_max, kXT), 1, 256 * 4));
+  if (train) hipLaunchKernelGGL(k_color_h2<true>, grid, dim3(128), kColH2Lds, st, a);
+  else hipLaunchKernelGGL(k_color_h2<false>, grid, dim3(128), kColH2Lds, st, a);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }

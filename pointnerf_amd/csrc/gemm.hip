@@ -645,6 +645,7 @@ struct GemmNNArgs {
   int32_t* range_flag;        // h2: operand outside the f16 split's range
   uint32_t* c_absmax;         // optional: max |C| folded in (float bits, atomic; pre-zeroed)
   const int32_t* run_if;      // fp32: run only when *run_if != 0 (the h2 call's fallback)
+  const uint4* b_split;       // h2, optional: B already split (nn_b_split: [K/8][N][hi, lo]), range checked
 };
 
 // max |v| of this thread's values into *word, one atomic per workgroup (NaN above inf)
@@ -771,7 +772,7 @@ constexpr int kNHPlaneA = kNHRows * kXPitch;   // f16 per A plane
 constexpr int kNHPlaneB = 256 * kXPitch;       // f16 per B plane
 constexpr size_t kNHLds = 2 * (2 * (size_t)kNHPlaneA + 2 * (size_t)kNHPlaneB) * 2;
 
-template <int NT>
+template <int NT, bool BS>   // BS: B pre-split (g.b_split)
 __global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t nlds[];
   constexpr int NW = (NT + 1) / 2;   // column tiles per wave (waves 0-3: even tiles, 4-7: odd)
@@ -794,7 +795,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
   const int bn = tid & 255, bk = 8 * (tid >> 8);
   const bool stB = bn < g.N;
   float4 va;
-  float vb[8];
+  float vb[BS ? 1 : 8];
+  uint4 bsh = make_uint4(0u, 0u, 0u, 0u), bsl = bsh;
   auto load = [&](int k0) {
     const int64_t gr = row0 + ar;
     const int kk = k0 + ak;
@@ -809,10 +811,17 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
       va.z = gr < g.M && kk + 2 < g.K ? src[kk + 2] : 0.f;
       va.w = gr < g.M && kk + 3 < g.K ? src[kk + 3] : 0.f;
     }
+    if constexpr (BS) {   // the f16 planes straight from the pre-split B (L2-resident)
+      // columns >= N (their LDS rows are never multiplied) read column N - 1
+      const uint4* q = g.b_split + ((int64_t)((k0 + bk) >> 3) * g.N + (stB ? bn : g.N - 1)) * 2;
+      bsh = q[0];
+      bsl = q[1];
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int r = k0 + bk + j;
-      vb[j] = stB && r < g.K ? g.B[(int64_t)r * g.ldb + bn] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int r = k0 + bk + j;
+        vb[j] = stB && r < g.K ? g.B[(int64_t)r * g.ldb + bn] : 0.f;
+      }
     }
   };
   auto put = [&](int buf) {
@@ -826,13 +835,18 @@ __global__ void __launch_bounds__(512, 1) k_gemm_nn_h2(GemmNNArgs g) {
     *reinterpret_cast<uint2*>(pa + ar * kXPitch + ak) = make_uint2(h0, h1);
     *reinterpret_cast<uint2*>(pa + kNHPlaneA + ar * kXPitch + ak) = make_uint2(l0, l1);
     uint4 bh, bl;
+    if constexpr (BS) {
+      bh = bsh;
+      bl = bsl;
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ok = ok && fabsf(vb[2 * q]) < 32768.f && fabsf(vb[2 * q + 1]) < 32768.f;
-      unsigned x0, x1;
-      splith(vb[2 * q], vb[2 * q + 1], x0, x1);
-      reinterpret_cast<unsigned*>(&bh)[q] = x0;
-      reinterpret_cast<unsigned*>(&bl)[q] = x1;
+      for (int q = 0; q < 4; ++q) {
+        ok = ok && fabsf(vb[2 * q]) < 32768.f && fabsf(vb[2 * q + 1]) < 32768.f;
+        unsigned x0, x1;
+        splith(vb[2 * q], vb[2 * q + 1], x0, x1);
+        reinterpret_cast<unsigned*>(&bh)[q] = x0;
+        reinterpret_cast<unsigned*>(&bl)[q] = x1;
+      }
     }
     *reinterpret_cast<uint4*>(pb + bn * kXPitch + bk) = bh;
     *reinterpret_cast<uint4*>(pb + kNHPlaneB + bn * kXPitch + bk) = bl;
@@ -906,6 +920,52 @@ static void launch_gemm_nn(const GemmNNArgs& g, hipStream_t st) {
   }
 }
 
+// B of a gemm_nn_h2 pre-split once (nn_b_split): out[k8][n] = (hi, lo) uint4 pairs
+// of rows 8 k8 .. 8 k8 + 7 of column n (rows >= K zero) -- the planes every
+// workgroup of k_gemm_nn_h2 would otherwise split from the same weights per
+// 16-k chunk; an out-of-range entry (|b| >= 2^15, NaN / inf) raises the flag
+// (the fp32 kernel behind the h2 call then recomputes C).  Up to 4 matrices.
+struct NNSplitJob {
+  const float* B;
+  int64_t ldb;
+  uint4* out;
+  int K, N, blk0;
+};
+struct NNSplitBatch {
+  NNSplitJob j[4];
+  int n;
+  int32_t* flag;
+};
+__global__ void __launch_bounds__(256) k_nn_b_split(NNSplitBatch B) {
+  NNSplitJob J = B.j[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (q < B.n && (int)blockIdx.x >= B.j[q].blk0) J = B.j[q];
+  const int i = (blockIdx.x - J.blk0) * 256 + threadIdx.x;
+  const int k8n = ((J.K + 15) / 16) * 2;   // 8-row groups (K padded to whole 16-k chunks)
+  if (i >= k8n * J.N) return;
+  const int k8 = i / J.N, n = i - k8 * J.N;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int r = 8 * k8 + j;
+    v[j] = r < J.K ? J.B[(int64_t)r * J.ldb + n] : 0.f;
+  }
+  bool ok = true;
+  uint4 bh, bl;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    ok = ok && fabsf(v[2 * q]) < 32768.f && fabsf(v[2 * q + 1]) < 32768.f;
+    unsigned x0, x1;
+    splith(v[2 * q], v[2 * q + 1], x0, x1);
+    reinterpret_cast<unsigned*>(&bh)[q] = x0;
+    reinterpret_cast<unsigned*>(&bl)[q] = x1;
+  }
+  J.out[(int64_t)i * 2] = bh;
+  J.out[(int64_t)i * 2 + 1] = bl;
+  if (!ok) atomicOr(B.flag, 1);
+}
+
 // The colour branch's first backward product input in one pass
 // (pnr_color_dz): dz[r][c] = lrelu'(hc[r][c]) (d_feat[r][1 + c] * (vmask[r] != 0)),
 // the torch ops' arithmetic (where(h > 0, x, x * slope) of x = d_feat * vm),
@@ -950,7 +1010,9 @@ using namespace pnr;
 
 int pnr::gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
                      int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
-                     const uint32_t* a_absmax, int32_t* range_flag, uint32_t* c_absmax, void* stream) {
+                     const uint32_t* a_absmax, int32_t* range_flag, uint32_t* c_absmax, void* stream,
+                     const void* b_split) {
+  PNR_CHECK_ARG(!b_split || (h2 && ((uintptr_t)b_split & 15) == 0), "gemm_nn: b_split needs h2 and 16-B alignment");
   PNR_CHECK_ARG(M == 0 || (A && B && C), "gemm_nn: null pointer");
   PNR_CHECK_ARG(M >= 0 && K > 0 && N > 0 && N % 32 == 0 && N <= 32 * kGMaxNT, "gemm_nn: N must be a multiple of 32 "
                 "in [32, 256], K > 0");
@@ -973,12 +1035,15 @@ int pnr::gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64
   g.range_flag = range_flag;
   g.c_absmax = c_absmax;
   g.run_if = nullptr;
+  g.b_split = static_cast<const uint4*>(b_split);
   hipStream_t st = as_stream(stream);
   if (h2) {
     static bool attr = false;
     if (!attr) {
 #define PNR_NNH2_ATTR(T)                                                                                  \
-  PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nn_h2<T>),                          \
+  PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nn_h2<T, false>),                   \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNHLds));             \
+  PNR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nn_h2<T, true>),                    \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNHLds));
       PNR_NNH2_ATTR(1) PNR_NNH2_ATTR(2) PNR_NNH2_ATTR(3) PNR_NNH2_ATTR(4)
       PNR_NNH2_ATTR(5) PNR_NNH2_ATTR(6) PNR_NNH2_ATTR(7) PNR_NNH2_ATTR(8)
@@ -986,16 +1051,20 @@ int pnr::gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64
       attr = true;
     }
     const dim3 grid((unsigned)cdiv(M, (int64_t)kNHRows));
+#define PNR_NNH2_GO(T)                                                                        \
+  if (g.b_split) hipLaunchKernelGGL((k_gemm_nn_h2<T, true>), grid, dim3(512), kNHLds, st, g); \
+  else hipLaunchKernelGGL((k_gemm_nn_h2<T, false>), grid, dim3(512), kNHLds, st, g);
     switch (N / 32) {
-      case 1: hipLaunchKernelGGL(k_gemm_nn_h2<1>, grid, dim3(512), kNHLds, st, g); break;
-      case 2: hipLaunchKernelGGL(k_gemm_nn_h2<2>, grid, dim3(512), kNHLds, st, g); break;
-      case 3: hipLaunchKernelGGL(k_gemm_nn_h2<3>, grid, dim3(512), kNHLds, st, g); break;
-      case 4: hipLaunchKernelGGL(k_gemm_nn_h2<4>, grid, dim3(512), kNHLds, st, g); break;
-      case 5: hipLaunchKernelGGL(k_gemm_nn_h2<5>, grid, dim3(512), kNHLds, st, g); break;
-      case 6: hipLaunchKernelGGL(k_gemm_nn_h2<6>, grid, dim3(512), kNHLds, st, g); break;
-      case 7: hipLaunchKernelGGL(k_gemm_nn_h2<7>, grid, dim3(512), kNHLds, st, g); break;
-      default: hipLaunchKernelGGL(k_gemm_nn_h2<8>, grid, dim3(512), kNHLds, st, g); break;
+      case 1: PNR_NNH2_GO(1) break;
+      case 2: PNR_NNH2_GO(2) break;
+      case 3: PNR_NNH2_GO(3) break;
+      case 4: PNR_NNH2_GO(4) break;
+      case 5: PNR_NNH2_GO(5) break;
+      case 6: PNR_NNH2_GO(6) break;
+      case 7: PNR_NNH2_GO(7) break;
+      default: PNR_NNH2_GO(8) break;
     }
+#undef PNR_NNH2_GO
     PNR_LAUNCH_CHECK();
     g.run_if = range_flag;   // the fp32 kernel below recomputes C only when the flag is up
   }
@@ -1016,7 +1085,8 @@ int pnr::gemm_nn_run(bool h2, const float* A, int64_t lda, const float* B, int64
 extern "C" int pnr_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
                            int32_t N, const float* act, int64_t ld_act, float slope, float* C, int64_t ldc,
                            void* stream) {
-  return gemm_nn_run(false, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, nullptr, nullptr, nullptr, stream);
+  return gemm_nn_run(false, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, nullptr, nullptr, nullptr, stream,
+                     nullptr);
 }
 
 extern "C" int pnr_gemm_nn_h2(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t K,
@@ -1024,13 +1094,33 @@ extern "C" int pnr_gemm_nn_h2(const float* A, int64_t lda, const float* B, int64
                               const uint32_t* a_absmax, int32_t* range_flag, void* stream) {
   PNR_CHECK_ARG(a_absmax && range_flag, "gemm_nn_h2: a_absmax and range_flag required");
   return gemm_nn_run(true, A, lda, B, ldb, M, K, N, act, ld_act, slope, C, ldc, a_absmax, range_flag, nullptr,
-                     stream);
+                     stream, nullptr);
 }
 
 
 extern "C" int pnr_gemm_tn_scratch_bytes(int64_t K, int32_t M, int32_t N, size_t* out) {
   PNR_CHECK_ARG(out && K >= 0 && M > 0 && N > 0, "gemm_tn_scratch_bytes: bad args");
   *out = gemm_scratch(K, M, N);
+  return PNR_OK;
+}
+
+size_t pnr::nn_b_split_bytes(int K, int N) { return (size_t)((K + 15) / 16) * 2 * N * 32; }
+
+int pnr::nn_b_split(int n, const float* const* B, const int64_t* ldb, const int* K, const int* N, void* const* out,
+                    int32_t* flag, void* stream) {
+  PNR_CHECK_ARG(n >= 1 && n <= 4 && flag, "nn_b_split: 1..4 matrices and a flag");
+  NNSplitBatch b = {};
+  b.n = n;
+  b.flag = flag;
+  int blocks = 0;
+  for (int q = 0; q < n; ++q) {
+    PNR_CHECK_ARG(B[q] && out[q] && K[q] > 0 && N[q] > 0 && ldb[q] >= N[q] && ((uintptr_t)out[q] & 15) == 0,
+                  "nn_b_split: bad matrix %d", q);
+    b.j[q] = {B[q], ldb[q], static_cast<uint4*>(out[q]), K[q], N[q], blocks};
+    blocks += (int)cdiv((int64_t)((K[q] + 15) / 16) * 2 * N[q], 256);
+  }
+  hipLaunchKernelGGL(k_nn_b_split, dim3(blocks), dim3(256), 0, as_stream(stream), b);
+  PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
 

@@ -91,7 +91,7 @@ __global__ void k_pack_h2(const float* __restrict__ W, int64_t lr, int64_t lc, i
 // Several packs in one launch (pnr_pack_batch): job q owns blocks [blk0_q,
 // blk0_{q+1}), one item per thread.  The job is picked with constant indices
 // only (uniform selects), so the argument block is never indexed dynamically.
-constexpr int kMaxPackJobs = 16;
+constexpr int kMaxPackJobs = 24;
 struct PackJob {
   const float* W;
   const float* bias;

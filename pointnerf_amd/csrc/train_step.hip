@@ -107,15 +107,22 @@ size_t group_scratch(int64_t m, int64_t nk) {
          a256((size_t)(m > 0 ? m : 1) * 4) /*tmp*/;
 }
 
+// cnt_zeroed: the caller already zeroed the scratch's first nk + 1 words (the counts)
 int group_pairs(const int32_t* prow, int64_t m, const int32_t* map, int64_t nk, int32_t* prow_sorted,
-                int32_t* pair_of, void* scratch, size_t bytes, hipStream_t st) {
+                int32_t* pair_of, void* scratch, size_t bytes, hipStream_t st, const int32_t** off_out = nullptr,
+                bool cnt_zeroed = false) {
   PNR_CHECK_ARG(prow_sorted && pair_of && scratch && (m == 0 || prow) && m >= 0 && nk >= 1 && m < (1ll << 31) &&
                     nk < (1ll << 31),
                 "group_pairs: bad args (m %lld, keys %lld)", (long long)m, (long long)nk);
   PNR_CHECK_ARG(bytes >= group_scratch(m, nk), "group_pairs: scratch too small (%zu < %zu)", bytes,
                 group_scratch(m, nk));
-  if (m == 0) return PNR_OK;
   char* sp = static_cast<char*>(scratch);
+  if (m == 0) {   // no pairs: every key empty
+    int32_t* off0 = reinterpret_cast<int32_t*>(sp + a256((size_t)(nk + 1) * 4));
+    PNR_HIP(hipMemsetAsync(off0, 0, (size_t)(nk + 1) * 4, st));
+    if (off_out) *off_out = off0;
+    return PNR_OK;
+  }
   int32_t* cnt = reinterpret_cast<int32_t*>(sp);   // [nk] counts, then n_big
   int32_t* n_big = cnt + nk;
   sp += a256((size_t)(nk + 1) * 4);
@@ -126,7 +133,8 @@ int group_pairs(const int32_t* prow, int64_t m, const int32_t* map, int64_t nk, 
   int32_t* big = reinterpret_cast<int32_t*>(sp);
   sp += a256((size_t)nk * 4);
   int32_t* tmp = reinterpret_cast<int32_t*>(sp);
-  PNR_HIP(hipMemsetAsync(cnt, 0, (size_t)(nk + 1) * 4, st));
+  if (off_out) *off_out = off;
+  if (!cnt_zeroed) PNR_HIP(hipMemsetAsync(cnt, 0, (size_t)(nk + 1) * 4, st));
   const unsigned gm = grid_for(m, 256, 2048), gk = grid_for(nk, 256, 2048);
   hipLaunchKernelGGL(k_grp_count, dim3(gm), dim3(256), 0, st, prow, m, map, cnt);
   PNR_LAUNCH_CHECK();
@@ -140,6 +148,87 @@ int group_pairs(const int32_t* prow, int64_t m, const int32_t* map, int64_t nk, 
   hipLaunchKernelGGL(k_grp_sort_big, dim3(256), dim3(256), 0, st, off, big, n_big, pair_of, tmp);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
+}
+
+// The per-point sums over the groups (the step's pnr_pairs_to_points_ex): 16
+// lanes per used point u (4 points per wave), lane l the floats 16 l .. 16 l + 15
+// of the 256-wide rows (four float4 loads in flight per pair): d_p1[u] = sum of
+// dz1 over u's pairs in pair order (zero for a point without pairs), lanes 0..5
+// the g_pair sums -> d_color / d_dir of point used[u] (Rw_p^T for d dir), max
+// |d_p1| folded into *absmax.  Same sums in the same order as
+// k_pairs_to_points_ex: the same bits.
+__global__ void __launch_bounds__(256) k_points_from_groups(const int32_t* __restrict__ off,
+                                                            const int32_t* __restrict__ pair_of, int64_t nk,
+                                                            const int32_t* __restrict__ used,
+                                                            const float* __restrict__ dz1, float* __restrict__ d_p1,
+                                                            uint32_t* __restrict__ absmax,
+                                                            const float* __restrict__ g_pair,
+                                                            const float* __restrict__ rw_uniform,
+                                                            const float* __restrict__ rw_pp,
+                                                            float* __restrict__ d_color, float* __restrict__ d_dir) {
+  __shared__ unsigned red[4];
+  constexpr int kLp = 16, kQ = 64 / kLp;   // lanes per point, float4 per lane (8: 133 us, 16: 115 us)
+  const int lane = threadIdx.x & 63, l = lane & (kLp - 1), grp = lane / kLp;
+  unsigned mb = 0u;
+  const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / kLp);
+  for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kLp; u < nk; u += gstride) {
+    const int32_t b = off[u], e = off[u + 1];
+    float4 s[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ge = 0.f;
+    for (int32_t j = b; j < e; ++j) {
+      const int64_t pq = pair_of[j];
+      const float4* row = reinterpret_cast<const float4*>(dz1 + pq * 256) + kQ * l;
+      float4 v[kQ];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) v[q] = row[q];
+      if (l < 6) ge += g_pair[pq * 8 + l];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        if (j == b) {
+          s[q] = v[q];
+        } else {
+          s[q].x += v[q].x;
+          s[q].y += v[q].y;
+          s[q].z += v[q].z;
+          s[q].w += v[q].w;
+        }
+      }
+    }
+    float4* o = reinterpret_cast<float4*>(d_p1 + u * 256) + kQ * l;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      o[q] = s[q];
+      mb = max(max(mb, max(__float_as_uint(fabsf(s[q].x)), __float_as_uint(fabsf(s[q].y)))),
+               max(__float_as_uint(fabsf(s[q].z)), __float_as_uint(fabsf(s[q].w))));
+    }
+    const int src = grp * kLp;
+    const float g3 = __shfl(ge, src + 3), g4 = __shfl(ge, src + 4), g5 = __shfl(ge, src + 5);
+    if (e > b) {
+      const int32_t pr = used[u];
+      if (l < 3) {
+        if (d_color) d_color[(int64_t)pr * 3 + l] = ge;
+        if (d_dir) {   // d dir_a = sum_j Rw[j][a] gd_j
+          const float* R = rw_pp ? rw_pp + (int64_t)pr * 9 : rw_uniform;
+          const float r0 = R ? R[l] : (l == 0 ? 1.f : 0.f);
+          const float r1 = R ? R[3 + l] : (l == 1 ? 1.f : 0.f);
+          const float r2 = R ? R[6 + l] : (l == 2 ? 1.f : 0.f);
+          d_dir[(int64_t)pr * 3 + l] = r0 * g3 + r1 * g4 + r2 * g5;
+        }
+      }
+    }
+  }
+  if (absmax) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+    if (lane == 0) red[threadIdx.x >> 6] = mb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      mb = max(max(red[0], red[1]), max(red[2], red[3]));
+      if (mb) atomicMax(absmax, mb);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- alpha gradient
@@ -194,6 +283,31 @@ __global__ void __launch_bounds__(256) k_alpha_colsum_final(const float* __restr
   }
 }
 
+// The step's preparation in one launch: zero up to six buffers (the point-table
+// gradients d emb, d colour, d dir, d conf -- rows the backward does not write
+// stay zero -- the step's absmax / flag words and the grouping's counts) and
+// gather block3.0's extras columns W3[:, 256:263] into a [256][7] table.
+constexpr int kPrepBufs = 6;
+struct StepPrep {
+  float* p[kPrepBufs];
+  int64_t n4[kPrepBufs];    // float4 count (16-B aligned buffers)
+  int64_t tail[kPrepBufs];  // 4-byte words past the last whole float4
+  float* w3e;
+  const float* w3;          // [256][263]
+};
+__global__ void __launch_bounds__(256) k_step_prep(StepPrep z) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t first = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < kPrepBufs; ++q) {
+    if (!z.p[q]) continue;
+    float4* d = reinterpret_cast<float4*>(z.p[q]);
+    for (int64_t i = first; i < z.n4[q]; i += stride) d[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = first; i < z.tail[q]; i += stride) z.p[q][4 * z.n4[q] + i] = 0.f;
+  }
+  for (int64_t i = first; i < 256 * 7; i += stride) z.w3e[i] = z.w3[(i / 7) * 263 + 256 + i % 7];
+}
+
 // [n, 24] -> [n, 32] rows (zero padding: pnr_gemm_tn's N multiple of 32)
 __global__ void __launch_bounds__(256) k_pad_rows32(const float* __restrict__ src, int64_t n, int cols,
                                                     float* __restrict__ dst) {
@@ -207,7 +321,7 @@ __global__ void __launch_bounds__(256) k_pad_rows32(const float* __restrict__ sr
 // ---------------------------------------------------------------- the step's scratch
 struct StepPlan {
   size_t words, dzc3, dzc2, dzc1, d_hid, vpe32, dz[4], dpa, d_p1, g_pair, prow_sorted, pair_of, grp, x1, dx1, packs,
-      pscale, w3e, gemm, absp, acp, total;
+      pscale, w3e, gemm, absp, acp, bsplit[4], total;
   size_t gemm_bytes, grp_bytes;
 };
 
@@ -252,6 +366,8 @@ static StepPlan plan_step(int64_t n, int64_t n_used) {
   (void)pnr_absmax_scratch_floats(&nabs);
   p.absp = take((size_t)nabs * 4);
   p.acp = take((size_t)kAcBlocks * 257 * 4);
+  const int kn[4][2] = {{128, 128}, {128, 128}, {128, 256}, {256, 224}};   // the four gemm_nn B operands
+  for (int i = 0; i < 4; ++i) p.bsplit[i] = take(nn_b_split_bytes(kn[i][0], kn[i][1]));
   p.total = o;
   return p;
 }
@@ -317,11 +433,9 @@ extern "C" int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_sample
   float* const* G = out->g;
   static const int64_t kParamNumel[16] = {256 * 284, 256, 256 * 256, 256, 256 * 263, 256, 256 * 256, 256,
                                           256,       1,   128 * 280, 128, 128 * 128, 128, 128 * 128, 128};
-  if (out->d_conf) PNR_HIP(hipMemsetAsync(out->d_conf, 0, (size_t)N * 4, st));
-  if (out->d_color) PNR_HIP(hipMemsetAsync(out->d_color, 0, (size_t)N * 12, st));
-  if (out->d_dir) PNR_HIP(hipMemsetAsync(out->d_dir, 0, (size_t)N * 12, st));
-  PNR_HIP(hipMemsetAsync(out->d_emb, 0, (size_t)N * 32 * 4, st));
   if (n == 0) {
+    for (float* p : {out->d_emb, out->d_color, out->d_dir, out->d_conf})
+      if (p) PNR_HIP(hipMemsetAsync(p, 0, (size_t)N * (p == out->d_emb ? 32 : p == out->d_conf ? 1 : 3) * 4, st));
     for (int i = 0; i < 16; ++i) PNR_HIP(hipMemsetAsync(G[i], 0, (size_t)kParamNumel[i] * 4, st));
     return PNR_OK;
   }
@@ -336,18 +450,44 @@ extern "C" int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_sample
   do {                      \
     if ((rc = (x))) return rc; \
   } while (0)
-  PNR_HIP(hipMemsetAsync(words, 0, 64, st));
+  const int64_t nk = n_used > 0 ? n_used : 1;
+  float* w3e = F(P.w3e);
+  {   // zero fills (gradients, words, the grouping's counts) + the W3 extras gather: one launch
+    StepPrep z = {};
+    float* ps[kPrepBufs] = {out->d_emb, out->d_color, out->d_dir, out->d_conf, reinterpret_cast<float*>(words),
+                            reinterpret_cast<float*>(b + P.grp)};
+    const int64_t ns[kPrepBufs] = {N * 32, N * 3, N * 3, N, 16, nk + 1};
+    for (int q = 0; q < kPrepBufs; ++q) {
+      z.p[q] = ps[q];
+      const bool al = ps[q] && ((uintptr_t)ps[q] & 15) == 0;
+      z.n4[q] = al ? ns[q] / 4 : 0;
+      z.tail[q] = ps[q] ? ns[q] - 4 * z.n4[q] : 0;
+    }
+    z.w3e = w3e;
+    z.w3 = W[4];
+    hipLaunchKernelGGL(k_step_prep, dim3(grid_for(N * 8, 256, 8192)), dim3(256), 0, st, z);
+    PNR_LAUNCH_CHECK();
+  }
+  // the four data-gradient products' B operands (colour_branch.4 / .2 / .0[:, :256],
+  // block1.0[:, :224]) split into f16 planes once, one launch
+  {
+    const float* bs[4] = {W[14], W[12], W[10], W[0]};
+    const int64_t lds[4] = {128, 128, 280, 284};
+    const int ks[4] = {128, 128, 128, 256}, ns[4] = {128, 128, 256, 224};
+    void* outs[4] = {b + P.bsplit[0], b + P.bsplit[1], b + P.bsplit[2], b + P.bsplit[3]};
+    PNR_TRY(nn_b_split(4, bs, lds, ks, ns, outs, flag, sv));
+  }
   // ---- colour branch (color_branch.{0,2,4}: 280 -> 128 -> 128 -> 128, LeakyReLU each)
   float *dzc3 = F(P.dzc3), *dzc2 = F(P.dzc2), *dzc1 = F(P.dzc1), *d_hid = F(P.d_hid);
   PNR_TRY(pnr_color_dz(d_feat, kC + 1, saved->vmask, saved->hc3, 128, n, 128, slope, dzc3, words + 1, sv));
   PNR_TRY(gemm_tn_run(2, dzc3, 128, saved->hc2, 128, n, 128, 128, G[14], 128, 128, G[15], F(P.gemm), P.gemm_bytes,
                       sv, words + 1, flag));
   PNR_TRY(gemm_nn_run(true, dzc3, 128, W[14], 128, n, 128, 128, saved->hc2, 128, slope, dzc2, 128, words + 1, flag,
-                      words + 2, sv));
+                      words + 2, sv, b + P.bsplit[0]));
   PNR_TRY(gemm_tn_run(2, dzc2, 128, saved->hc1, 128, n, 128, 128, G[12], 128, 128, G[13], F(P.gemm), P.gemm_bytes,
                       sv, words + 2, flag));
   PNR_TRY(gemm_nn_run(true, dzc2, 128, W[12], 128, n, 128, 128, saved->hc1, 128, slope, dzc1, 128, words + 2, flag,
-                      words + 3, sv));
+                      words + 3, sv, b + P.bsplit[1]));
   PNR_TRY(gemm_tn_run(2, dzc1, 128, saved->hid, 256, n, 128, 256, G[10], 280, 256, G[11], F(P.gemm), P.gemm_bytes,
                       sv, words + 3, flag));
   float* vpe32 = F(P.vpe32);
@@ -355,14 +495,13 @@ extern "C" int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_sample
   PNR_LAUNCH_CHECK();
   PNR_TRY(gemm_tn_run(2, dzc1, 128, vpe32, 32, n, 128, 32, G[10] + 256, 280, 24, nullptr, F(P.gemm), P.gemm_bytes,
                       sv, words + 3, flag));
-  PNR_TRY(pnr_gemm_nn_h2(dzc1, 128, W[10], 280, n, 128, 256, nullptr, 0, 0.f, d_hid, 256, words + 3, flag, sv));
+  PNR_TRY(gemm_nn_run(true, dzc1, 128, W[10], 280, n, 128, 256, nullptr, 0, 0.f, d_hid, 256, words + 3, flag, nullptr,
+                      sv, b + P.bsplit[2]));
   // ---- per-pair chain (k_pairs_bwd<2>), dX packs from the current weights
   float* pscale = F(P.pscale);
   char* packs = b + P.packs;
   const size_t per = (size_t)(16 + 3) * 2048 * 8;
   PNR_TRY(pnr_pack_bwd_h2(W[6], W[4], 263, W[2], 3, pscale, packs, 3 * per, sv));
-  float* w3e = F(P.w3e);
-  PNR_HIP(hipMemcpy2DAsync(w3e, 7 * 4, W[4] + 256, 263 * 4, 7 * 4, 256, hipMemcpyDeviceToDevice, st));
   pnr_mlp_bwd wb = {nullptr, nullptr, nullptr, nullptr};   // extras per point below
   pnr_mlp_bwd_h2 wbh = {packs, packs + per, packs + 2 * per, pscale};
   float* dz[4] = {F(P.dz[0]), F(P.dz[1]), F(P.dz[2]), F(P.dz[3])};
@@ -372,13 +511,17 @@ extern "C" int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_sample
   // ---- per-point sums of dz1 and of the block3.0 extras (pairs grouped by point, pair order)
   int32_t* prow_sorted = reinterpret_cast<int32_t*>(b + P.prow_sorted);
   int32_t* pair_of = reinterpret_cast<int32_t*>(b + P.pair_of);
-  PNR_TRY(group_pairs(saved->prow, m, pts->used_map, n_used > 0 ? n_used : 1, prow_sorted, pair_of, b + P.grp,
-                      P.grp_bytes, st));
+  const int32_t* off = nullptr;
+  PNR_TRY(group_pairs(saved->prow, m, pts->used_map, nk, prow_sorted, pair_of, b + P.grp, P.grp_bytes, st, &off,
+                      true));
   float* g_pair = F(P.g_pair);
   PNR_TRY(pnr_aggregate_bwd_extras_rows(pts, s, w, saved, w3e, dz[2], g_pair, sv));
   float* d_p1 = F(P.d_p1);
-  PNR_TRY(pnr_pairs_to_points_ex(prow_sorted, pair_of, m, dz[0], pts->used_map, d_p1, saved->dz_absmax + 5, g_pair,
-                                 w->rw2c, pts->rw2c, out->d_color, out->d_dir, sv));
+  // per used point over its group (= pnr_pairs_to_points_ex's sums, 16 lanes per point)
+  hipLaunchKernelGGL(k_points_from_groups, dim3(grid_for(nk * 16, 256, 4096)), dim3(256), 0, st, off, pair_of, nk,
+                     pts->used, dz[0], d_p1, saved->dz_absmax + 5, g_pair, w->rw2c, pts->rw2c, out->d_color,
+                     out->d_dir);
+  PNR_LAUNCH_CHECK();
   // ---- weight gradients dW = dZ^T X over the pairs (A scales from k_pairs_bwd's maxima)
   const uint32_t* am = saved->dz_absmax;
   PNR_TRY(gemm_tn_run(2, dz[3], 256, saved->h3, 256, m, 256, 256, G[6], 256, 256, G[7], F(P.gemm), P.gemm_bytes, sv,
@@ -391,8 +534,8 @@ extern "C" int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_sample
                       am + 1, flag));
   PNR_TRY(pnr_alpha_colsum(dpa, saved->h4, m, G[8], G[9], F(P.acp), sv));
   // ---- block1.0: the point half from dP1 / X1 (used rows), the pair half from dz1 / PE_5
-  float *x1 = F(P.x1), *dx1 = F(P.dx1);
-  PNR_TRY(pnr_point_pe3_rows(pts->emb, pts->used, n_used, x1, sv));
+  float *x1 = saved->x1 ? saved->x1 : F(P.x1), *dx1 = F(P.dx1);
+  if (!saved->x1) PNR_TRY(pnr_point_pe3_rows(pts->emb, pts->used, n_used, x1, sv));   // else the forward's rows
   PNR_TRY(gemm_tn_run(2, d_p1, 256, x1, 224, n_used, 256, 224, G[0], 284, 224, G[1], F(P.gemm), P.gemm_bytes, sv,
                       am + 5, flag));
   PNR_TRY(gemm_tn_run(2, dz[0], 256, saved->pe5, 64, m, 256, 64, G[0] + 224, 284, 60, nullptr, F(P.gemm),
@@ -400,7 +543,8 @@ extern "C" int pnr_aggregate_bwd_step_h2(const pnr_points* pts, const pnr_sample
   // (a d emb pass over every row, zeros for the unreferenced ones, measured 176 us
   // against 35 + 42-69 us for the fill and the used-row pass)
   if (n_used > 0) {
-    PNR_TRY(pnr_gemm_nn_h2(d_p1, 256, W[0], 284, n_used, 256, 224, nullptr, 0, 0.f, dx1, 224, am + 5, flag, sv));
+    PNR_TRY(gemm_nn_run(true, d_p1, 256, W[0], 284, n_used, 256, 224, nullptr, 0, 0.f, dx1, 224, am + 5, flag,
+                        nullptr, sv, b + P.bsplit[3]));
     PNR_TRY(pnr_point_pe3_bwd_rows(pts->emb, pts->used, dx1, n_used, out->d_emb, sv));
   }
 #undef PNR_TRY

@@ -103,7 +103,7 @@ def packed_bwd(agg, x3: bool = False, h2: bool = False):
 class Saved:
     """Device activations kept by pnr_aggregate_fwd_train (pnr_agg_saved)."""
 
-    def __init__(self, n_max: int, device, n_dev=None):
+    def __init__(self, n_max: int, device, n_dev=None, n_x1: int = 0):
         n = max(int(n_max), 1)
         f = dict(dtype=torch.float32, device=device)
         P = n * 8
@@ -116,8 +116,10 @@ class Saved:
                       hc1=torch.empty((n, 128), **f), hc2=torch.empty((n, 128), **f),
                       hc3=torch.empty((n, 128), **f), vmask=torch.empty(n, dtype=torch.int32, device=device),
                       mask=torch.empty((P, 64), dtype=torch.int16, device=device),
-                      dz_absmax=torch.zeros(6, dtype=torch.int32, device=device))   # |dz1..dz4|, |dpa|, |d_p1|
-        self.c = L.AggSaved(*(self.t[k].data_ptr() for k, _ in L.AggSaved._fields_))
+                      dz_absmax=torch.zeros(6, dtype=torch.int32, device=device),   # |dz1..dz4|, |dpa|, |d_p1|
+                      # [emb, PE_3(emb)] of the used points (fp32h2 forward's k_point_pre_h2; ABI 23)
+                      x1=torch.empty((int(n_x1), 224), **f) if n_x1 else None)
+        self.c = L.AggSaved(*(L.ptr(self.t[k]) for k, _ in L.AggSaved._fields_))
 
     def absmax(self, i: int):
         """[1] int32 view: float bits of max |dz_{i+1}| (i < 4), |dpa| (4), |d_p1| (5)."""
@@ -218,7 +220,8 @@ class AggregateFn(torch.autograd.Function):
         # every pack of the step in one launch (the optimizer changed the weights)
         agg.packed_train(h2=run_h2)
         mlp, keepw = agg.packed()
-        sv = Saved(n_max, dev, n_dev=s.n_dev)
+        # fp32h2 with a used-point list: the forward also keeps block1.0's point-half inputs
+        sv = Saved(n_max, dev, n_dev=s.n_dev, n_x1=n_p1 if (run_h2 and spec.used is not None) else 0)
         feat = _rows_zeroed((max(n_max, 1), 129), s.n_dev, dev)
         scratch = L.aggregate_scratch(max(n_max, 1), max(n_p1, 1), dev)
         keepx = None
@@ -392,7 +395,9 @@ class AggregateFn(torch.autograd.Function):
         emb = ctx.tabs[0]
         d_p1 = d_p1[:n_p1]
         x1 = torch.empty((max(n_p1, 1), 224), **f32)[:n_p1]
-        if used is None:
+        if sv["x1"] is not None and used is not None:
+            x1 = sv["x1"][:n_p1]   # the forward's rows (k_point_pre_h2)
+        elif used is None:
             L.check(L.lib().pnr_point_pe3(L.ptr(emb), n_p1, L.ptr(x1), L.stream_ptr(dev)), "pnr_point_pe3")
         else:   # PE_3 of the used rows, read through the list (no gathered copy)
             L.check(L.lib().pnr_point_pe3_rows(L.ptr(emb), L.ptr(used), n_p1, L.ptr(x1), L.stream_ptr(dev)),
