@@ -84,6 +84,15 @@ for s in $STEPS; do
     trainprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trstats -o run -- \
         python bench.py --mode train --steps 20 --warmup 3 --train-precision ${TP:-fp32h2} > $O/trstats.log 2>&1 || { tail -20 $O/trstats.log; exit 1; } ;;
+    trainab)   # training-step variants: product libpnr vs tools/_var/libpnr_t*.so (bench line + kernel stats each)
+      for L in pointnerf_amd/libpnr.so tools/_var/libpnr_t*.so; do
+        n=$(basename $L .so)
+        PNR_LIB=$PWD/$L timeout -k 10 300 python bench.py --mode train --steps 20 --warmup 5 > $O/tab_$n.json \
+          2> $O/tab_$n.err || { tail -20 $O/tab_$n.err; exit 1; }
+        PNR_LIB=$PWD/$L timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tabst_$n -o run -- \
+          python bench.py --mode train --steps 20 --warmup 3 > $O/tabst_$n.log 2>&1 || { tail -20 $O/tabst_$n.log; exit 1; }
+        echo $n $(python -c "import json; print(json.loads(open('$O/tab_$n.json').read().strip().splitlines()[-1])['ms_per_step'])")
+      done ;;
     nrab)   # the 2-D renderer tile-shape variants in tools/_var (built on the CPU side)
       for v in tools/_var/libpnr_*.so; do
         PNR_LIB=$PWD/$v timeout -k 10 200 python tools/nr_bench.py > $O/nrab_$(basename $v .so).json 2>> $O/nrab.err \
