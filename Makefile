@@ -16,6 +16,10 @@ build/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pnr_common.h $(SRC_DIR)/agg_common.h incl
 
 # The query kernels must round exactly like the reference's fp32 ops: no FMA contraction.
 build/query.o build/grid.o build/voxelize.o: HIPFLAGS += -ffp-contract=off
+# The bf16 pair kernel's gather math (weights, distances, PE) without FMA
+# contraction: its render and general instantiations then round every fp32 op
+# the same way, so their features agree bit for bit (test_gpu_bf16.py).
+build/aggregate_bf16.o: HIPFLAGS += -ffp-contract=off
 # Split-MFMA kernels: no SLP packing of scalar f32 math into v_pk_*_f32, which
 # issues at a fraction of the rate of scalar VALU beside the MFMA stream
 # (MI355X_MICROARCH "price of one filler"; measured 1 % on the aggregate).

@@ -171,10 +171,11 @@ def test_bf16_render_variant_equals_general(cuda, flags):
     """k_pairs_b's render variant (no per-point Rw2c / used_map / ray_cam /
     out_weight / out_conf: those branches compiled out, aggregate_bf16.hip GEN)
     computes the features of the general-path variant a call with out_weight /
-    out_conf runs, bucketed and unbucketed: the same samples written, values
-    equal up to the FMA contraction hipcc picks per instantiation (measured and
-    printed: ~4e-4 of the entries differ, by up to ~1e-3 of the maximum when a
-    last-bit difference flips the bf16 rounding of a GEMM input)."""
+    out_conf runs, bucketed and unbucketed: the same samples written, alpha
+    within 2^-20 of its maximum, at most 0.1 % of the features one bf16 input
+    step apart (round 5 allowed 1 %: hipcc contracted different products into
+    FMAs per instantiation; aggregate_bf16.hip is now compiled with
+    -ffp-contract=off)."""
     from pointnerf_amd import _lib as L
     from scenes import flag_scene
     sc = flag_scene(flags, n_points=60000 if flags == "truck" else 30000, H=64, view=0)
@@ -205,17 +206,21 @@ def test_bf16_render_variant_equals_general(cuda, flags):
                                                    L.stream_ptr(cuda)), "bf16")
             outs.append(f)
         torch.cuda.synchronize()
-        a, b = torch.nan_to_num(outs[0], nan=7.0), torch.nan_to_num(outs[1], nan=7.0)
         assert torch.equal(torch.isnan(outs[0]), torch.isnan(outs[1])), bk   # same samples written
+        a, b = torch.nan_to_num(outs[0], nan=7.0), torch.nan_to_num(outs[1], nan=7.0)
+        # aggregate_bf16.hip is compiled without FMA contraction (Makefile): the two
+        # instantiations no longer contract different products into FMAs (round 5:
+        # up to 1.3e-3 of the entries differed).  A last-bit difference of the fp32
+        # accumulators is left (alpha, fp32 from the block3.2 accumulators, shows it:
+        # <= 2^-22 of its maximum); it flips the bf16 rounding of a later GEMM input in
+        # a few entries (measured: truck none, lego 6.9e-5 of the entries, by one bf16
+        # step of the input carried to the outputs of its sample)
         d = (a - b).abs()
         frac = float((d > 0).float().mean())
         rel = float(d.max()) / float(a.abs().max())
         print(f"buckets={bk}: differing {frac:.2e} of the entries, max |d| / max |f| = {rel:.2e}")
-        # the two instantiations may contract a different a * b + c into an FMA in
-        # the gather's fp32 math (weights, distances): last-bit differences that
-        # the bf16 operands of the next GEMM can round either way -- one bf16 step
-        # (2^-8 relative) of an input, carried to the outputs of its sample
-        assert rel <= 2.0 ** -7 and frac <= 0.01, (bk, frac, rel)   # measured: <= 1.3e-3, <= 4e-4
+        assert float(d[:, 0].max()) <= 2.0 ** -20 * float(a[:, 0].abs().max()), (bk, float(d[:, 0].max()))
+        assert rel <= 2.0 ** -7 and frac <= 1e-3, (bk, frac, rel)
         assert int(torch.isfinite(outs[0][:, 0]).sum()) > 1000
 
 
