@@ -224,11 +224,13 @@ def test_c3_ship_finetune_batch_grads_vs_oracle(cuda, train_precision):
     strict bound: its per-layer error (~10x fp32 rounding) puts a few more
     LeakyReLU pre-activations on the other side of 0 than fp32 does, and each
     such kink flip changes one (pair, neuron) term by a factor 0.2 / 1.  Per
-    tensor: at most 0.1 % of the entries (>= 16) outside the strict fp32 bound,
-    the whole tensor within 1 % of fp64 in relative L2 norm, and no entry more
-    than 10 % of the tensor's largest entry away (measured on this batch: 6 of
-    4.8 M point-table entries outside, max 4.8 %, L2 <= 0.4 % -- DESIGN.md
-    section 10)."""
+    tensor: at most 1e-5 of the entries (>= 16) outside the strict fp32 bound,
+    the whole tensor within 0.5 % of fp64 in relative L2 norm, and no entry more
+    than 6 % of the tensor's largest entry away (measured on this batch, round 6:
+    6 of 4.8 M point-table entries outside, max 4.8 % (points_color), L2 <= 0.39 %,
+    every MLP weight gradient inside the strict bound; the kernels are
+    deterministic, so the numbers repeat -- round 5 allowed 0.1 %, 1 % and 10 %;
+    DESIGN.md section 10)."""
     from test_gpu_backward import close
     sc = flag_scene("ship", 2_000_000, H=800, view=3, default_conf=None)
     params = formula_params(salt=0.15)
@@ -305,7 +307,7 @@ def test_c3_ship_finetune_batch_grads_vs_oracle(cuda, train_precision):
         if train_precision == "fp32h2":
             rel_l2 = float(np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-300))
             rel_max = float(np.abs(a - r).max() / np.abs(r).max())
-            ok = bad.sum() <= max(16, 1e-3 * bad.size) and rel_l2 <= 1e-2 and rel_max <= 0.1
+            ok = bad.sum() <= max(16, 1e-5 * bad.size) and rel_l2 <= 5e-3 and rel_max <= 0.06
             contract.append((k, int(bad.sum()), bad.size, round(rel_max, 5), rel_l2))
             if not ok:
                 errs.append(f"d {k}: {bad.sum()} / {bad.size} outside the fp32 bound, max |d| / max |ref| "
