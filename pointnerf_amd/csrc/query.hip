@@ -121,18 +121,52 @@ __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __
   }
 }
 
+// fill_rs (the filled slots as r * SR + s, ray after ray): a wave takes 64 rays,
+// whose slots are one contiguous output range [off(r0), off(r0) + their counts);
+// lane j writes positions off(r0) + j, + 64, ... (coalesced), finding its ray by
+// a binary search over the 64 offsets (the last ray whose offset <= position:
+// rays without slots share the next ray's offset and come before it).  One
+// thread per ray writing its own slots touched 64 lines per store (headline:
+// 70 us for 24 MB).
 __global__ void __launch_bounds__(kQBlock) k_fill_list(int64_t R, int SR, const int32_t* __restrict__ n_filled,
                                                        const int32_t* __restrict__ ray_off,
                                                        int32_t* __restrict__ fill_rs, int32_t* counts) {
+  const int lane = threadIdx.x & 63;
   int hit = 0;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < R;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const int n = n_filled[r], off = ray_off[r];
-    for (int s = 0; s < n; ++s) fill_rs[off + s] = (int)(r * SR + s);
+  const int64_t nwav = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t r0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6) * 64; r0 < R; r0 += nwav * 64) {
+    const int64_t r = r0 + lane;
+    const int n = r < R ? n_filled[r] : 0;
+    const int off = r < R ? ray_off[r] : 0;
     hit += n > 0;
+    const int last = (int)(R - 1 - r0 < 63 ? R - 1 - r0 : 63);   // the wave's last ray
+    const int base = __shfl(off, 0), end = __shfl(off + n, last);
+    const int iters = (end - base + 63) >> 6;   // wave-uniform: every lane takes part in the shuffles
+    for (int it = 0; it < iters; ++it) {
+      const int p = base + 64 * it + lane;
+      int lo = 0;
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1) {
+        const int c = lo + step;
+        const int oc = __shfl(off, c <= last ? c : last);
+        if (c <= last && oc <= p) lo = c;
+      }
+      const int olo = __shfl(off, lo);
+      if (p < end) fill_rs[p] = (int)((r0 + lo) * SR + (p - olo));
+    }
   }
+  // R_hit: one atomic per block (per wave, 10 k same-address atomics serialised at
+  // the L2 took ~70 us of this kernel at the headline)
+  __shared__ int red[kQBlock / 64];
   hit = wave_sum_i32(hit);
-  if ((threadIdx.x & 63) == 0 && hit) atomicAdd(counts + 2, hit);
+  if (lane == 0) red[threadIdx.x >> 6] = hit;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < kQBlock / 64; ++w) t += red[w];
+    if (t) atomicAdd(counts + 2, t);
+  }
 }
 
 // The K neighbour ids and distances of a lane's sample, in LDS: one column of

@@ -80,6 +80,12 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_sums(int32_t* sums, int64_t
                                                           int32_t* total_dev, const int32_t* run_if) {
   __shared__ int lds4[4];
   if (run_if && *run_if == 0) return;
+  // only the tiles below the effective length hold sums (k_scan_reduce zeroed the
+  // rest and k_scan_final skips them): a device length far below n (the query's
+  // vflag scan over R * SR slots, ~11 % filled at the headline) then costs its own
+  // tiles, not n's (41.7 -> ~5 us)
+  const int64_t nbe = cdiv(eff_len(n, n_dev), kScanTile);
+  if (nbe < nb) nb = nbe;
   const int64_t per = cdiv(nb, kScanBlock);
   const int64_t b0 = threadIdx.x * per;
   int acc = 0;
