@@ -53,7 +53,8 @@ size_t scan_scratch_bytes(int64_t n);
 int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out, int64_t out_cap,
                    int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
                    int as_flag = 0,   // as_flag: scan (in[i] != 0) instead of in[i]
-                   const int32_t* run_if = nullptr);  // device flag: 0 = leave out untouched
+                   const int32_t* run_if = nullptr,   // device flag: 0 = leave out untouched
+                   int32_t* list = nullptr);          // optional stream compaction: list[out[i]] = i for in[i] != 0
 
 // --------------------------------------------------------- device helpers
 // floor((p - shift) / vs) exactly as the reference kernels compute it in fp32

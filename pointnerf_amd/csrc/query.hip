@@ -574,16 +574,6 @@ __global__ void __launch_bounds__(kQBlock) __attribute__((amdgpu_waves_per_eu(KM
     atomicAdd(reinterpret_cast<unsigned long long*>(counts + 6), (unsigned long long)n_cand);
 }
 
-__global__ void __launch_bounds__(kQBlock) k_valid_list(const int32_t* __restrict__ vflag,
-                                                        const int32_t* __restrict__ valid_off,
-                                                        int32_t* __restrict__ valid_list,
-                                                        const int32_t* counts) {
-  const int64_t S = counts[0];
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < S;
-       i += (int64_t)gridDim.x * blockDim.x)
-    if (vflag[i]) valid_list[valid_off[i]] = (int)i;
-}
-
 // Reference-shaped query_points outputs for the R'' rays (qpiw.py:97-99, 715-719).
 __global__ void __launch_bounds__(kQBlock) k_compact(QRays q, int SR, int K, int64_t rows_max,
                                                      const int32_t* __restrict__ n_filled,
@@ -731,12 +721,11 @@ extern "C" int pnr_query(pnr_handle* h, const pnr_rays* rays, const pnr_query_pa
   else PNR_KNN(32);
 #undef PNR_KNN
   PNR_LAUNCH_CHECK();
+  // valid_off and, in the same pass, valid_list[valid_off[i]] = i for vflag[i] (the
+  // separate compaction re-read both arrays: c5 117 us)
   if ((rc = exclusive_scan(b->vflag, RS, b->counts + 0, b->valid_off, RS + 1, b->counts + 1, b->scratch,
-                           b->scratch_bytes, st)))
+                           b->scratch_bytes, st, 0, nullptr, b->valid_list)))
     return rc;
-  hipLaunchKernelGGL(k_valid_list, dim3(grid_for(RS, kQBlock)), dim3(kQBlock), 0, st, b->vflag,
-                     b->valid_off, b->valid_list, b->counts);
-  PNR_LAUNCH_CHECK();
   if ((rc = exclusive_scan(b->ray_vcnt, R, nullptr, b->ray_row, R + 1, b->counts + 3, b->scratch,
                            b->scratch_bytes, st, /*as_flag=*/1)))
     return rc;

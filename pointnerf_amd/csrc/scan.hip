@@ -1,5 +1,6 @@
 // Device-wide exclusive scan of int32 (three-pass: tile reduce, scan of tile
-// sums, tile scan + offset).  Used for every data-dependent compaction of the
+// sums, tile scan + offset), optionally with the stream compaction it sizes
+// (list[out[i]] = i for every nonzero in[i], written by the last pass).  Used for every data-dependent compaction of the
 // query (R -> R' -> R'' and the SR pick of qpiw.py:655-719), so none of them
 // needs a host round trip.
 #include "pnr_common.h"
@@ -106,17 +107,20 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_sums(int32_t* sums, int64_t
 __global__ void __launch_bounds__(kScanBlock) k_scan_final(const int32_t* __restrict__ in, int64_t n,
                                                            const int32_t* n_dev, int as_flag,
                                                            const int32_t* __restrict__ sums,
-                                                           int32_t* __restrict__ out, const int32_t* run_if) {
+                                                           int32_t* __restrict__ out, const int32_t* run_if,
+                                                           int32_t* __restrict__ list) {
   __shared__ int tile[kScanTile];
   __shared__ int lds4[4];
   if (run_if && *run_if == 0) return;
   const int64_t ne = eff_len(n, n_dev);
   const int64_t start = (int64_t)blockIdx.x * kScanTile;
   if (start >= ne) return;
+  int lv[kScanItems];   // this thread's loaded items (the list's flags)
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
     int64_t i = start + j * kScanBlock + threadIdx.x;
-    tile[j * kScanBlock + threadIdx.x] = load_item(in, i, ne, as_flag);
+    lv[j] = load_item(in, i, ne, as_flag);
+    tile[j * kScanBlock + threadIdx.x] = lv[j];
   }
   __syncthreads();
   int v[kScanItems];
@@ -137,7 +141,11 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_final(const int32_t* __rest
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
     int64_t i = start + j * kScanBlock + threadIdx.x;
-    if (i < ne) out[i] = tile[j * kScanBlock + threadIdx.x];
+    if (i < ne) {
+      const int o = tile[j * kScanBlock + threadIdx.x];
+      out[i] = o;
+      if (list && lv[j]) list[o] = (int)i;
+    }
   }
 }
 
@@ -151,7 +159,7 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_final_direct(const int32_t*
                                                                   const int32_t* n_dev, int as_flag,
                                                                   const int32_t* __restrict__ sums,
                                                                   int32_t* __restrict__ out, int32_t* total_dev,
-                                                                  const int32_t* run_if) {
+                                                                  const int32_t* run_if, int32_t* __restrict__ list) {
   __shared__ int tile[kScanTile];
   __shared__ int lds4[4];
   if (run_if && *run_if == 0) return;
@@ -169,10 +177,12 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_final_direct(const int32_t*
   for (int i = threadIdx.x; i < (int)blockIdx.x; i += kScanBlock) pre += sums[i];
   int pre_tot;
   block_excl_scan(pre, lds4, &pre_tot);   // (block_excl_scan's barriers also order the tile loads below)
+  int lv[kScanItems];   // this thread's loaded items (the list's flags)
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
     int64_t i = start + j * kScanBlock + threadIdx.x;
-    tile[j * kScanBlock + threadIdx.x] = load_item(in, i, ne, as_flag);
+    lv[j] = load_item(in, i, ne, as_flag);
+    tile[j * kScanBlock + threadIdx.x] = lv[j];
   }
   __syncthreads();
   int v[kScanItems];
@@ -193,7 +203,11 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_final_direct(const int32_t*
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
     int64_t i = start + j * kScanBlock + threadIdx.x;
-    if (i < ne) out[i] = tile[j * kScanBlock + threadIdx.x];
+    if (i < ne) {
+      const int o = tile[j * kScanBlock + threadIdx.x];
+      out[i] = o;
+      if (list && lv[j]) list[o] = (int)i;
+    }
   }
   if (start + kScanTile >= ne && threadIdx.x == 0) {   // the tile of the last element
     out[ne] = pre_tot + tot;
@@ -207,7 +221,7 @@ size_t scan_scratch_bytes(int64_t n) { return (size_t)(scan_blocks(n) + 1) * siz
 
 int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* out, int64_t out_cap,
                    int32_t* total_dev, void* scratch, size_t scratch_bytes, hipStream_t st,
-                   int as_flag, const int32_t* run_if) {
+                   int as_flag, const int32_t* run_if, int32_t* list) {
   PNR_CHECK_ARG(in && out && scratch, "scan: null pointer");
   PNR_CHECK_ARG(n >= 0, "scan: negative length");
   // the grand total is stored at out[n_eff] (n_eff <= n): out needs n + 1 entries
@@ -222,13 +236,14 @@ int exclusive_scan(const int32_t* in, int64_t n, const int32_t* n_dev, int32_t* 
   PNR_LAUNCH_CHECK();
   if (nb <= kScanDirect) {
     hipLaunchKernelGGL(k_scan_final_direct, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums,
-                       out, total_dev, run_if);
+                       out, total_dev, run_if, list);
     PNR_LAUNCH_CHECK();
     return PNR_OK;
   }
   hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanBlock), 0, st, sums, nb, n, n_dev, out, total_dev, run_if);
   PNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, out, run_if);
+  hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, n_dev, as_flag, sums, out, run_if,
+                     list);
   PNR_LAUNCH_CHECK();
   return PNR_OK;
 }
