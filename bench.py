@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0
 # committed PMC passes (tools/prof_bench.sh -> tools/profile_summary.py) per (config, dtype)
 PMC_FILES = {("headline", "fp32"): "r01_fp32_pmc_aggregate.json",
              ("headline", "fp32x3"): "r01_pmc_aggregate_x3.json",
-             ("headline", "fp32h2"): "r06_end_pmc_aggregate_h2.json",
+             ("headline", "fp32h2"): "r06_final_pmc_aggregate_h2.json",
              ("c5", "bf16"): "r06_c5_pmc_aggregate_bf16.json",
              ("c4", "fp32h2"): "r06_c4_pmc_aggregate_h2.json"}
 
