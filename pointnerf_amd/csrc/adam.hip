@@ -24,6 +24,7 @@ namespace pnr {
 constexpr int kAdamMax = 32;
 constexpr int kAdamBlock = 256;
 constexpr int64_t kAdamChunk = 8192;   // elements per workgroup (32 per lane)
+constexpr int kAdamQ = 4;               // float4 quads per lane in flight (2: 0.394 ms, 4: 0.377, one: 0.385)
 
 struct AdamArgs {
   float* p[kAdamMax];
@@ -59,24 +60,36 @@ __global__ void __launch_bounds__(kAdamBlock) k_adam(AdamArgs a) {
                      reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(V)) & 15) == 0;
   if (vec) {
     const int64_t q1 = e0 + ((e1 - e0) & ~int64_t(3));   // float4 quads [e0, q1), e0 % 4 == 0
-    for (int64_t e = e0 + 4 * (int64_t)threadIdx.x; e < q1; e += 4 * kAdamBlock) {
-      // streamed once: nontemporal loads / stores (0.394 vs 0.418 ms per step on
-      // 78 M elements, tools/adam_bench.py A/B, same results)
-      typedef float f4 __attribute__((ext_vector_type(4)));
-      const f4 pv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(P + e));
-      const f4 gv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(G + e));
-      const f4 mv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(M + e));
-      const f4 vv = __builtin_nontemporal_load(reinterpret_cast<const f4*>(V + e));
-      float4 p = make_float4(pv.x, pv.y, pv.z, pv.w), m = make_float4(mv.x, mv.y, mv.z, mv.w);
-      float4 v = make_float4(vv.x, vv.y, vv.z, vv.w);
-      const float4 g = make_float4(gv.x, gv.y, gv.z, gv.w);
-      adam1(p.x, g.x, m.x, v.x, a);
-      adam1(p.y, g.y, m.y, v.y, a);
-      adam1(p.z, g.z, m.z, v.z, a);
-      adam1(p.w, g.w, m.w, v.w, a);
-      __builtin_nontemporal_store((f4){p.x, p.y, p.z, p.w}, reinterpret_cast<f4*>(P + e));
-      __builtin_nontemporal_store((f4){m.x, m.y, m.z, m.w}, reinterpret_cast<f4*>(M + e));
-      __builtin_nontemporal_store((f4){v.x, v.y, v.z, v.w}, reinterpret_cast<f4*>(V + e));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    // kAdamQ quads per lane per round, all 4 kAdamQ loads issued before any math
+    // (tools/adam_bench.py, the finetune set's 78 M elements: 0.385 -> 0.377 ms, 5.8 TB/s)
+    for (int64_t e = e0 + 4 * (int64_t)threadIdx.x; e < q1; e += 4 * kAdamQ * kAdamBlock) {
+      f4 pv[kAdamQ], gv[kAdamQ], mv[kAdamQ], vv[kAdamQ];
+#pragma unroll
+      for (int u = 0; u < kAdamQ; ++u) {
+        const int64_t eu = e + (int64_t)u * 4 * kAdamBlock;
+        const int64_t ec = eu < q1 ? eu : e;   // past the tensor: reload (never stored)
+        pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(P + ec));
+        gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(G + ec));
+        mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(M + ec));
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(V + ec));
+      }
+#pragma unroll
+      for (int u = 0; u < kAdamQ; ++u) {
+        const int64_t eu = e + (int64_t)u * 4 * kAdamBlock;
+        float4 p = make_float4(pv[u].x, pv[u].y, pv[u].z, pv[u].w), m = make_float4(mv[u].x, mv[u].y, mv[u].z, mv[u].w);
+        float4 v = make_float4(vv[u].x, vv[u].y, vv[u].z, vv[u].w);
+        const float4 g = make_float4(gv[u].x, gv[u].y, gv[u].z, gv[u].w);
+        adam1(p.x, g.x, m.x, v.x, a);
+        adam1(p.y, g.y, m.y, v.y, a);
+        adam1(p.z, g.z, m.z, v.z, a);
+        adam1(p.w, g.w, m.w, v.w, a);
+        if (eu < q1) {
+          __builtin_nontemporal_store((f4){p.x, p.y, p.z, p.w}, reinterpret_cast<f4*>(P + eu));
+          __builtin_nontemporal_store((f4){m.x, m.y, m.z, m.w}, reinterpret_cast<f4*>(M + eu));
+          __builtin_nontemporal_store((f4){v.x, v.y, v.z, v.w}, reinterpret_cast<f4*>(V + eu));
+        }
+      }
     }
     for (int64_t e = q1 + threadIdx.x; e < e1; e += kAdamBlock) adam1(P[e], G[e], M[e], V[e], a);
   } else {
