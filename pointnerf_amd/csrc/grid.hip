@@ -609,9 +609,8 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
       if (sel) rec = rr;
       keep_rec = keep_rec || sel;
     }
-    if (!live) continue;
-    if (head) {
-      int c[3];
+    int c[3] = {0, 0, 0};
+    if (live && head) {
       if (cell <= 0x7fffffff) {   // 32-bit division when the cell index fits
         const int r = (int)cell / g.dims[2];
         c[2] = (int)cell - r * g.dims[2];
@@ -622,17 +621,30 @@ __global__ void __launch_bounds__(kBlock) k_claim(const float* __restrict__ xyz,
         c[1] = (int)((cell / g.dims[2]) % g.dims[1]);
         c[0] = (int)(cell / ((int64_t)g.dims[2] * g.dims[1]));
       }
+    }
+    // the KNN's coarse column map: bit y of word (z / 8, x, y / 32) for every held
+    // voxel.  A column's held cells of one z-block are consecutive heads of the
+    // sorted keys with the same word and bit: only the first of such a run in the
+    // wave sets it (one same-address atomic per run instead of per voxel; they
+    // serialised at the L2: 27 us of this kernel at the headline and at c5)
+    {
+      const bool cset = live && head && cnt_kept > 0;
+      const int64_t cw = cset ? ((int64_t)(c[2] >> 3) * g.dims[0] + c[0]) * ((g.dims[1] + 31) >> 5) + (c[1] >> 5) : -1;
+      const int cb = c[1] & 31;
+      const uint64_t cm = __ballot(cset) & ((1ull << lane) - 1ull);   // setting lanes below this one
+      const int pl = cm ? 63 - __builtin_clzll(cm) : lane;
+      const int pw_lo = __shfl((int)(uint32_t)cw, pl), pw_hi = __shfl((int)(cw >> 32), pl), pb = __shfl(cb, pl);
+      const int64_t pw = (int64_t)(((uint64_t)(uint32_t)pw_hi << 32) | (uint32_t)pw_lo);
+      if (cset && (!cm || pw != cw || pb != cb)) atomicOr(coarse + cw, 1u << cb);
+    }
+    if (!live) continue;
+    if (head) {
       coor_2_occ[cell] = slot;
       occ_2_coor[slot * 3 + 0] = c[0];
       occ_2_coor[slot * 3 + 1] = c[1];
       occ_2_coor[slot * 3 + 2] = c[2];
       occ_bytes[cell] = 1;
-      if (cnt_kept > 0) {
-        held_bytes[cell] = 1;   // the query index's held voxels (was k_mark_held)
-        // the KNN's coarse column map: bit y of word (z / 8, x, y / 32)
-        atomicOr(coarse + ((int64_t)(c[2] >> 3) * g.dims[0] + c[0]) * ((g.dims[1] + 31) >> 5) + (c[1] >> 5),
-                 1u << (c[1] & 31));
-      }
+      if (cnt_kept > 0) held_bytes[cell] = 1;   // the query index's held voxels (was k_mark_held)
       occ_numpnts[slot] = cnt_kept;
       const int keep = min(cnt_kept, g.P);
       if (cnt_kept > g.P) slot_run[slot] = rw ? -1 : hd;   // -1: records written here, else by k_reservoir
