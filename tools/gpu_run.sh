@@ -110,7 +110,7 @@ for s in $STEPS; do
       python -c "import json; [print(d['lib'][-20:], d['stages_ms'], d['checksum']) for d in map(json.loads, open('$O/compab.jsonl'))]" ;;
     qab)   # query-stage variants (tools/_var/libpnr_q*.so), two rounds
       for rnd in 1 2; do for v in tools/_var/libpnr_q*.so; do
-        PNR_LIB=$PWD/$v timeout -k 10 200 python tools/query_bench.py >> $O/qab.jsonl 2>> $O/qab.err \
+        PNR_LIB=$PWD/$v timeout -k 10 200 python tools/query_bench.py $QAB_ARGS >> $O/qab.jsonl 2>> $O/qab.err \
           || { tail -20 $O/qab.err; exit 1; }
       done; done
       python -c "import json; [print(d['lib'][-12:], [c['query_ms'] for c in d['cams']], [c['pidx_checksum'] for c in d['cams']]) for d in map(json.loads, open('$O/qab.jsonl'))]" ;;
