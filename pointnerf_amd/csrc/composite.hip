@@ -154,6 +154,49 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
       else
         sig[q] = vrow[q] >= 0 ? a.feat[(int64_t)vrow[q] * CF] : 0.f;
     }
+    // the first NRW valid rows' channels are loaded now, beside sigma, before the
+    // slot scans below (their weights are applied after them): one round trip
+    // fewer on a ray's dependent chain (A/B, identical checksums: c5 4.00 -> 3.46
+    // ms, the headline unchanged at 0.89 ms -- profiles/r06_composite_prefetch_ab.jsonl)
+    unsigned long long m0 = __ballot(vrow[0] >= 0), m1 = __ballot(vrow[1] >= 0);
+    int vr[NRW], sl[NRW];   // row and source slot (wave-uniform) of each row in flight
+    float f0[NRW], f1[NRW];
+    auto pick = [&]() {
+#pragma unroll
+      for (int u = 0; u < NRW; ++u) {
+        vr[u] = -1;
+        sl[u] = -1;
+        if (m0) {
+          const int src = __builtin_ctzll(m0);
+          m0 &= m0 - 1;
+          vr[u] = __shfl(vrow[0], src);
+          sl[u] = src;
+        } else if (m1) {
+          const int src = __builtin_ctzll(m1);
+          m1 &= m1 - 1;
+          vr[u] = __shfl(vrow[1], src);
+          sl[u] = 64 + src;
+        }
+      }
+    };
+    auto load_rows = [&]() {
+#pragma unroll
+      for (int u = 0; u < NRW; ++u) {
+        if constexpr (HF) {
+          const uint32_t* f = reinterpret_cast<const uint32_t*>(
+              a.feat_h + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * PNR_FEAT_H_PITCH + 8);
+          const uint32_t v = (vr[u] >= 0 && 2 * lane < C) ? f[lane] : 0u;
+          f0[u] = __uint_as_float(v << 16);            // channel 2 lane
+          f1[u] = __uint_as_float(v & 0xffff0000u);    // channel 2 lane + 1
+        } else {
+          const float* f = a.feat + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * CF + 1;
+          f0[u] = (vr[u] >= 0 && lane < C) ? f[lane] : 0.f;
+          f1[u] = (vr[u] >= 0 && lane + 64 < C) ? f[lane + 64] : 0.f;
+        }
+      }
+    };
+    pick();
+    load_rows();
     // cummax over slots (neural_points_volumetric_model.py:293)
     float cm0 = wave_max_scan_incl(z[0]);
     float cm1 = fmaxf(wave_max_scan_incl(z[1]), __shfl(cm0, 63));
@@ -179,47 +222,17 @@ __global__ void __launch_bounds__(kCBlock) k_composite(CompArgs a) {
     // valid slots in slot order, NRW feature rows in flight per iteration
     // (same accumulation order as a plain slot loop)
     float col0 = 0.f, col1 = 0.f;
-    unsigned long long m0 = __ballot(vrow[0] >= 0), m1 = __ballot(vrow[1] >= 0);
-    while (m0 | m1) {
-      int vr[NRW];
-      float w[NRW];
-#pragma unroll
-      for (int u = 0; u < NRW; ++u) {
-        vr[u] = -1;
-        w[u] = 0.f;
-        if (m0) {
-          const int src = __builtin_ctzll(m0);
-          m0 &= m0 - 1;
-          vr[u] = __shfl(vrow[0], src);
-          w[u] = __shfl(w0, src);
-        } else if (m1) {
-          const int src = __builtin_ctzll(m1);
-          m1 &= m1 - 1;
-          vr[u] = __shfl(vrow[1], src);
-          w[u] = __shfl(w1, src);
-        }
-      }
-      float f0[NRW], f1[NRW];
-#pragma unroll
-      for (int u = 0; u < NRW; ++u) {
-        if constexpr (HF) {
-          const uint32_t* f = reinterpret_cast<const uint32_t*>(
-              a.feat_h + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * PNR_FEAT_H_PITCH + 8);
-          const uint32_t v = (vr[u] >= 0 && 2 * lane < C) ? f[lane] : 0u;
-          f0[u] = __uint_as_float(v << 16);            // channel 2 lane
-          f1[u] = __uint_as_float(v & 0xffff0000u);    // channel 2 lane + 1
-        } else {
-          const float* f = a.feat + (int64_t)(vr[u] < 0 ? 0 : vr[u]) * CF + 1;
-          f0[u] = (vr[u] >= 0 && lane < C) ? f[lane] : 0.f;
-          f1[u] = (vr[u] >= 0 && lane + 64 < C) ? f[lane + 64] : 0.f;
-        }
-      }
+    for (;;) {
 #pragma unroll
       for (int u = 0; u < NRW; ++u) {
         if (vr[u] < 0) break;
-        col0 += w[u] * f0[u];
-        col1 += w[u] * f1[u];
+        const float w = sl[u] < 64 ? __shfl(w0, sl[u]) : __shfl(w1, sl[u] - 64);
+        col0 += w * f0[u];
+        col1 += w * f1[u];
       }
+      if (!(m0 | m1)) break;
+      pick();
+      load_rows();
     }
     if constexpr (HF) {
       if (2 * lane < C) {
