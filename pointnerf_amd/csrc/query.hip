@@ -88,13 +88,50 @@ __global__ void __launch_bounds__(kQBlock) k_march_coop(QRays q, const QGrid* __
     const float c[3] = {q.campos[cam * 3], q.campos[cam * 3 + 1], q.campos[cam * 3 + 2]};
     const float dir[3] = {q.raydir[r * 3], q.raydir[r * 3 + 1], q.raydir[r * 3 + 2]};
     int n = 0;   // hits so far: the same in every lane of the group
-    for (int d0 = 0; d0 < q.D && n < SR; d0 += G * U) {
+    // Shared (ascending) tvals: candidates outside the grid box padded by one voxel
+    // cannot land in a cell (their coordinates fail the bounds test below), so the
+    // walk covers only [d_lo, d_hi): the slab-test t range of the padded box,
+    // widened for rounding, mapped to indices conservatively (every skipped
+    // candidate lies outside it).  The same hits in the same slots; rays that miss
+    // the box (most background rays of an object scene) test no candidate.
+    int d_lo = 0, d_hi = q.D;
+    if (!q.per_ray && q.D > 1) {
+      float tlo = -INFINITY, thi = INFINITY;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const float lo = g.shift[a] - g.vs[a], hi = g.shift[a] + (float)(g.dims[a] + 1) * g.vs[a];
+        if (fabsf(dir[a]) < 1e-30f) {
+          if (!(c[a] >= lo && c[a] <= hi)) tlo = INFINITY;
+        } else {
+          const float t0 = (lo - c[a]) / dir[a], t1 = (hi - c[a]) / dir[a];
+          tlo = fmaxf(tlo, fminf(t0, t1));
+          thi = fminf(thi, fmaxf(t0, t1));
+        }
+      }
+      tlo -= 1e-3f * fabsf(tlo) + 1e-3f * g.vs[0];
+      thi += 1e-3f * fabsf(thi) + 1e-3f * g.vs[0];
+      if (!(tlo <= thi)) {
+        d_hi = 0;   // no candidate can be inside (also: a NaN bound -- then no skip below)
+        if (tlo != tlo || thi != thi) d_hi = q.D;
+      } else {
+        const float ta = tval(q, r, 0), tb = tval(q, r, q.D - 1);
+        if (tb > ta) {   // index guesses from the end points, then moved until provably outside
+          int a0 = (int)fminf(fmaxf(floorf((tlo - ta) / (tb - ta) * (float)(q.D - 1)), 0.f), (float)q.D);
+          while (a0 > 0 && !(tval(q, r, a0 - 1) < tlo)) --a0;   // every d < a0: t(d) < tlo
+          int b0 = (int)fminf(fmaxf(ceilf((thi - ta) / (tb - ta) * (float)(q.D - 1)) + 1.f, 0.f), (float)q.D);
+          while (b0 < q.D && !(tval(q, r, b0) > thi)) ++b0;     // every d >= b0: t(d) > thi
+          d_lo = a0;
+          d_hi = b0 > a0 ? b0 : a0;
+        }
+      }
+    }
+    for (int d0 = d_lo; d0 < d_hi && n < SR; d0 += G * U) {
       bool hit[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int d = d0 + u * G + gl;
         hit[u] = false;
-        if (d < q.D) {
+        if (d < d_hi) {
           float p[3];
           ray_point(c, dir, tval(q, r, d), p);
           const int x = vox_coord_fast(p[0], g.shift[0], g.vs[0], inv[0]);
