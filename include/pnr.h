@@ -159,7 +159,9 @@ int pnr_grid_export(pnr_handle* h, int32_t* coor_2_occ, uint32_t* occ_bits, int3
  * Rays: raypos(r,d) = campos + raydir[r] * tvals[d]  (diff_ray_marching.py:387,
  * mul then add, fp32, no contraction).  tvals holds the D mid-point depths
  * middle_point_ts (diff_ray_marching.py:369-385), either one table shared by
- * every ray (tvals_per_ray = 0, jitter = 0) or one row per ray. */
+ * every ray (tvals_per_ray = 0, jitter = 0) or one row per ray.  Depths ascend
+ * along a ray (as middle_point_ts makes them): with a shared table the march
+ * tests only the depths inside the grid box, found from the table's order. */
 typedef struct {
   const float* campos_dev;    /* [3]  ([n_cams,3] with ray_cam)        */
   const float* camrot_dev;    /* [3,3] row-major camrotc2w ([n_cams,3,3] with ray_cam) */
