@@ -185,6 +185,40 @@ def test_coop_march_equals_serial_march(cuda):
     assert torch.equal(sd[keep], sd_big[keep])
 
 
+def test_march_box_clipping_edge_rays(cuda):
+    """The shared-table march tests only the depths inside the grid box padded by
+    one voxel (query.hip k_march_coop): rays from a camera inside the box in every
+    direction, axis-parallel rays (zero direction components, +-x, +-y, +-z), and
+    rays from outside that run along the box's faces -- the same filled slots and
+    neighbours as the oracle's serial walk."""
+    sc = scene(20000, H=16, W=16)
+    xyz = sc["xyz"]
+    lo, hi = xyz.min(0), xyz.max(0)
+    ctr = ((lo + hi) / 2).astype(np.float32)
+    rng = np.random.default_rng(7)
+    d = rng.normal(size=(250, 3))
+    d = np.concatenate([d, np.eye(3), -np.eye(3), [[1, 1, 0], [0, 1, -1], [1, 0, 1]]])
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    q = _engine(sc, cuda)
+    xt = torch.from_numpy(xyz).to(cuda)
+    cr = torch.from_numpy(sc["camrot"]).to(cuda)
+    cams = [ctr,                                                          # inside the box
+            np.array([lo[0] - 1.0, ctr[1], hi[2]], dtype=np.float32),     # on the top face's plane
+            np.array([ctr[0], lo[1] - 0.5, lo[2]], dtype=np.float32)]     # on the bottom face's plane
+    R, SR = d.shape[0], sc["opt"].SR
+    filled = 0
+    for cam in cams:
+        bufs, _, _, _ = q.run(xt, torch.from_numpy(d).to(cuda), torch.from_numpy(cam).to(cuda), cr, 0.05, 3.0)
+        ref = O.query_points(sc["opt"], xyz, cam, sc["camrot"], d, near=0.05, far=3.0)
+        nf = bufs.n_filled[:R].cpu().numpy()
+        assert np.array_equal(nf, ref["n_filled"])
+        sd = bufs.slot_d[: R * SR].cpu().numpy().astype(np.int32).reshape(R, SR)
+        for r in range(R):
+            assert np.array_equal(sd[r, : nf[r]], ref["slot_d"][r, : nf[r]]), r
+        filled += int(nf.sum())
+    assert filled > 1000
+
+
 def test_used_points_device_equals_torch(cuda):
     """pnr_used_points (device list + map, count in counts[5]) == the torch
     restatement train.used_points on the query's filled rows."""
